@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: sharded HBM web-cache serving step (one process per GPU).
+
+Contract (see task README): ``python bench.py --gpus N --steps K --warmup W``;
+for N>1 launched by torch.distributed.run (one rank per GPU, RCCL). Prints ONE
+JSON line on rank 0.
+
+Step = one serving tick of the distributed cache on every rank:
+  * a GET batch of ``--batch`` Zipf(0.99) requests over the whole key space,
+    routed to owner shards (RCCL all-to-all), probed + gathered on the owner's
+    HBM by the HIP kernels, values returned to the requesting rank's HBM;
+  * a SET batch of ``--sets`` requests (same popularity law) routed, shipped
+    (payload all-to-all) and committed (dedupe, scan-allocate, log write, CAS
+    index insert) on the owners.
+Per-GPU work is fixed as N grows (weak scaling): each rank issues the same
+number of requests and owns ``--keys-per-gpu`` objects of the key space.
+
+Metric: whole-job cache operations per second (GET+SET requests served).
+The reference (kmacrow/Shellac) publishes no numbers, so vs_baseline is null.
+Secondary (outside the timed region): the BASELINE.json platform smoke checks
+— the MFMA hello tile and an RCCL all-reduce of a 1 GiB bf16 tensor.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from shellac_amd.bench.workload import Workload  # noqa: E402
+from shellac_amd.models.sharded_cache import ShardedCache  # noqa: E402
+from shellac_amd.ops.cache import CacheShard  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=262144, help="GET requests per rank per step")
+    ap.add_argument("--sets", type=int, default=16384, help="SET requests per rank per step")
+    ap.add_argument("--keys-per-gpu", type=int, default=4 << 20)
+    ap.add_argument("--zipf", type=float, default=0.99)
+    ap.add_argument("--min-val", type=int, default=64)
+    ap.add_argument("--max-val", type=int, default=4096)
+    ap.add_argument("--log-gb", type=float, default=16.0, help="value-log GiB per shard")
+    ap.add_argument("--no-smoke", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def smoke(rank, world, dev):
+    out = {}
+    try:
+        from shellac_amd.ops.smoke import mfma_hello
+
+        g = torch.Generator(device=dev).manual_seed(7)
+        a = torch.randn(64, 32, 16, generator=g, device=dev).to(torch.bfloat16)
+        b = torch.randn(64, 16, 32, generator=g, device=dev).to(torch.bfloat16)
+        c = mfma_hello(a, b)
+        ref = torch.bmm(a.float(), b.float())
+        out["mfma_hello_max_abs_err"] = float((c - ref).abs().max())
+    except Exception as e:  # report, never hide
+        out["mfma_hello_error"] = repr(e)
+    if world > 1:
+        x = torch.ones(512 << 20, dtype=torch.bfloat16, device=dev)  # 1 GiB
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        iters = 5
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+        nbytes = x.numel() * 2
+        out["allreduce_1GiB_bf16_ms"] = round(dt * 1e3, 3)
+        out["allreduce_busbw_GBps"] = round(nbytes * 2 * (world - 1) / world / dt / 1e9, 1)
+        del x
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    total_keys = args.keys_per_gpu * world
+    t_setup = time.perf_counter()
+    wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
+    nb = 1
+    while nb * 2 < args.keys_per_gpu:  # ~50% slot load with 4-entry buckets
+        nb *= 2
+    log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
+    shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)
+    sc = ShardedCache(shard)
+
+    # populate: every rank SETs its slice of the key space through the routed path
+    chunk = 1 << 18
+    lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
+    for s in range(lo, hi, chunk):
+        ids = torch.arange(s, min(s + chunk, hi), device=dev)
+        sc.set(wl.set_batch(ids))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    log(rank, f"[bench] populated {total_keys} keys in {time.perf_counter() - t_setup:.1f}s")
+
+    # pre-generated request batches (the "data loader"); cycled through the steps
+    P = 4
+    gets = [wl.digests.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
+            for i in range(P)]
+    sets = [wl.set_batch(wl.sample_ids(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
+    shard.reserve(max(args.sets * 2, chunk))
+    before = shard.counters()
+
+    def step(i):
+        r = sc.get(gets[i % P])
+        sc.set(sets[i % P])
+        return r
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        res = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t)
+
+    after = shard.counters()
+    hits = after["get_hits"] - before["get_hits"]
+    gops = after["get_ops"] - before["get_ops"]
+    gbytes = after["get_bytes"] - before["get_bytes"]
+    agg = torch.tensor([hits, gops, gbytes], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(agg)
+    hits, gops, gbytes = (int(v) for v in agg.tolist())
+
+    if args.check:
+        # verify the last GET batch against the workload's ground truth
+        from shellac_amd.ops.cache import unpack_records
+
+        k = 200
+        ids = wl.sample_ids(args.batch, 1000 + 97 * rank + (args.steps - 1) % P)[:k]
+        recs = unpack_records(res.data, res.off[:k], res.size[:k])
+        bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
+        log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
+
+    sm = {} if args.no_smoke else smoke(rank, world, dev)
+
+    ops_per_step = (args.batch + args.sets) * world
+    ms = elapsed / args.steps * 1e3
+    value = ops_per_step * args.steps / elapsed
+    out = {
+        "metric": "cache_ops_per_s",
+        "value": round(value, 1),
+        "unit": "requests/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "uint8",
+        "data": "synthetic (device-generated Zipf web-object workload; random payloads)",
+        "config": {
+            "model": "shellac-hbm-cache: ketama-ring sharded, 1 shard/GPU, FIFO log + 2-choice index",
+            "global_batch": ops_per_step,
+            "seq_len": None,
+            "parallelism": f"shard{world} (all-to-all routed)",
+            "get_per_rank": args.batch,
+            "set_per_rank": args.sets,
+            "keys_total": total_keys,
+            "zipf_s": args.zipf,
+            "value_bytes": [args.min_val, args.max_val],
+            "log_gib_per_shard": args.log_gb,
+        },
+        "get_hit_ratio": round(hits / max(gops, 1), 4),
+        "get_value_GBps": round(gbytes / elapsed / 1e9, 2),
+        "smoke": sm,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

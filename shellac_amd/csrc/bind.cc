@@ -1,0 +1,226 @@
+// pybind11 bindings for the shellac_amd native core (_shellac_core).
+//
+// Device-side entry points take raw device pointers and a hipStream_t as Python
+// ints (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream) so the core
+// does not link against libtorch; the Python layer (shellac_amd/ops) owns
+// allocation through PyTorch's caching allocator.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "bind_parts.h"
+#include "hbm_cache.h"
+#include "host_cache.h"
+
+namespace py = pybind11;
+using namespace shellac;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict counters_dict(const CacheCounters& c) {
+  py::dict d;
+  d["get_ops"] = c.get_ops;
+  d["get_hits"] = c.get_hits;
+  d["get_bytes"] = c.get_bytes;
+  d["set_ops"] = c.set_ops;
+  d["set_bytes"] = c.set_bytes;
+  d["set_dropped"] = c.set_dropped;
+  d["set_evicted"] = c.set_evicted;
+  d["del_ops"] = c.del_ops;
+  d["del_hits"] = c.del_hits;
+  d["swept"] = c.swept;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_shellac_core, m) {
+  m.doc() = "shellac_amd native core: HBM/DRAM cache shards, HTTP codec, reactor, protocols";
+
+  m.attr("ENTRY_BYTES") = (int)sizeof(Entry);
+  m.attr("BUCKET_BYTES") = (int)kBucketBytes;
+  m.attr("ITEM_HEADER_BYTES") = (int)kItemHeaderBytes;
+  m.attr("ITEM_MAGIC") = kItemMagic;
+  m.attr("MISS_LOC") = py::int_(kMissLoc);
+
+  m.def("digest", [](py::bytes b) {
+    std::string s = b;
+    Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    return py::make_tuple(d.lo, d.hi);
+  }, "128-bit digest (lo, hi) of a byte string");
+  m.def("item_bytes", [](uint32_t vlen) { return item_bytes(vlen); });
+
+  // ---------------- device (HIP) ----------------
+  py::class_<HbmCache>(m, "HbmCache")
+      .def(py::init([](uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int device) {
+             ShardConfig c;
+             c.log_bytes = log_bytes;
+             c.nbuckets = nbuckets;
+             c.max_item = max_item;
+             c.device = device;
+             return new HbmCache(c);
+           }),
+           py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"))
+      .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
+                        uintptr_t off, uint32_t now, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
+                 now, S(s));
+      })
+      .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
+                        uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s));
+      })
+      .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
+                       uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
+                       uint64_t bytes_bound, uint32_t now, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
+                P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
+                bytes_bound, now, S(s));
+      })
+      .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
+                        uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.remove(P<const Digest>(keys), n, P<uint8_t>(found), now, S(s));
+      })
+      .def("sweep", [](HbmCache& c, uint32_t now, uintptr_t s) {
+        uint64_t live = 0, bytes = 0;
+        {
+          py::gil_scoped_release nogil;
+          c.sweep(now, S(s), &live, &bytes);
+        }
+        return py::make_tuple(live, bytes);
+      })
+      .def("flush", [](HbmCache& c, uintptr_t s) { c.flush(S(s)); })
+      .def("counters", [](HbmCache& c, uintptr_t s) { return counters_dict(c.counters(S(s))); })
+      .def("head", [](HbmCache& c, uintptr_t s) { return c.head(S(s)); })
+      .def("reserve", &HbmCache::reserve)
+      .def("hbm_bytes", &HbmCache::hbm_bytes)
+      .def_property_readonly("log_ptr", [](HbmCache& c) { return (uintptr_t)c.log_ptr(); })
+      .def_property_readonly("index_ptr", [](HbmCache& c) { return (uintptr_t)c.index_ptr(); })
+      .def_property_readonly("head_ptr", [](HbmCache& c) { return (uintptr_t)c.head_ptr(); });
+
+  m.def("scan_tmp_bytes", &device_scan_tmp_bytes);
+  m.def("exclusive_scan", [](uintptr_t in, uintptr_t out, int64_t n, uintptr_t tmp,
+                             size_t tmp_bytes, uintptr_t s) {
+    device_exclusive_scan(P<const uint64_t>(in), P<uint64_t>(out), n, P<void>(tmp), tmp_bytes,
+                          S(s));
+  });
+  m.def("segcopy", [](uintptr_t src, uintptr_t src_off, uintptr_t dst_off, int64_t n,
+                      uintptr_t dst, uintptr_t s) {
+    segcopy(P<const uint8_t>(src), P<const uint64_t>(src_off), P<const uint64_t>(dst_off), n,
+            P<uint8_t>(dst), S(s));
+  });
+  m.def("digest_keys", [](uintptr_t bytes, uintptr_t offs, int64_t n, uintptr_t out,
+                          uintptr_t s) {
+    digest_keys(P<const uint8_t>(bytes), P<const int64_t>(offs), n, P<Digest>(out), S(s));
+  });
+  m.def("route_keys", [](uintptr_t keys, int64_t n, uintptr_t pts, uintptr_t owner, int32_t npts,
+                         uintptr_t dest, uintptr_t counts, int32_t nranks, uintptr_t s) {
+    route_keys(P<const Digest>(keys), n, P<const uint32_t>(pts), P<const int32_t>(owner), npts,
+               P<int32_t>(dest), P<int64_t>(counts), nranks, S(s));
+  });
+  m.def("scatter_by_dest", [](uintptr_t dest, uintptr_t base, int64_t n, int32_t nranks,
+                              uintptr_t cursor, uintptr_t perm, uintptr_t s) {
+    scatter_by_dest(P<const int32_t>(dest), P<const int64_t>(base), n, nranks, P<int64_t>(cursor),
+                    P<int64_t>(perm), S(s));
+  });
+  m.def("permute_records", [](uintptr_t in, uintptr_t perm, int64_t n, int32_t rec_bytes,
+                              uintptr_t out, uintptr_t s) {
+    permute_records(P<const void>(in), P<const int64_t>(perm), n, rec_bytes, P<void>(out), S(s));
+  });
+  m.def("mfma_hello", [](uintptr_t a, uintptr_t b, uintptr_t c, int tiles, uintptr_t s) {
+    mfma_hello(P<const uint16_t>(a), P<const uint16_t>(b), P<float>(c), tiles, S(s));
+  });
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+
+  // ---------------- host (DRAM) ----------------
+  py::class_<HostCache>(m, "HostCache")
+      .def(py::init<uint64_t, uint64_t, uint32_t>(), py::arg("log_bytes"), py::arg("nbuckets"),
+           py::arg("max_item"))
+      .def("lookup", [](HostCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
+                        uintptr_t off, uint32_t now) {
+        py::gil_scoped_release nogil;
+        c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
+                 now);
+      })
+      .def("gather", [](HostCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out) {
+        py::gil_scoped_release nogil;
+        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out));
+      })
+      .def("store", [](HostCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
+                       uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
+                       uint32_t now) {
+        py::gil_scoped_release nogil;
+        c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
+                P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
+                now);
+      })
+      .def("remove", [](HostCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now) {
+        py::gil_scoped_release nogil;
+        c.remove(P<const Digest>(keys), n, P<uint8_t>(found), now);
+      })
+      .def("sweep", [](HostCache& c, uint32_t now) {
+        uint64_t live = 0, bytes = 0;
+        c.sweep(now, &live, &bytes);
+        return py::make_tuple(live, bytes);
+      })
+      .def("flush", &HostCache::flush)
+      .def("counters", [](HostCache& c) { return counters_dict(c.counters()); })
+      .def("head", &HostCache::head)
+      .def("get", [](HostCache& c, py::bytes key, uint32_t now) -> py::object {
+        std::string k = key;
+        Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        std::vector<uint8_t> v;
+        uint32_t flags = 0;
+        if (!c.get_one(d, &v, &flags, now)) return py::none();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("set", [](HostCache& c, py::bytes key, py::bytes value, uint32_t flags,
+                     uint32_t expire, uint32_t now) {
+        std::string k = key, v = value;
+        Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        c.set_one(d, reinterpret_cast<const uint8_t*>(v.data()), (uint32_t)v.size(), flags, expire,
+                  now);
+      });
+
+  m.def("host_exclusive_scan", [](uintptr_t in, uintptr_t out, int64_t n) {
+    host_exclusive_scan(P<const uint64_t>(in), P<uint64_t>(out), n);
+  });
+  m.def("host_segcopy", [](uintptr_t src, uintptr_t src_off, uintptr_t dst_off, int64_t n,
+                           uintptr_t dst) {
+    host_segcopy(P<const uint8_t>(src), P<const uint64_t>(src_off), P<const uint64_t>(dst_off), n,
+                 P<uint8_t>(dst));
+  });
+  m.def("host_digest_keys", [](uintptr_t bytes, uintptr_t offs, int64_t n, uintptr_t out) {
+    host_digest_keys(P<const uint8_t>(bytes), P<const int64_t>(offs), n, P<Digest>(out));
+  });
+  m.def("host_route_keys", [](uintptr_t keys, int64_t n, uintptr_t pts, uintptr_t owner,
+                              int32_t npts, uintptr_t dest, uintptr_t counts, int32_t nranks) {
+    host_route_keys(P<const Digest>(keys), n, P<const uint32_t>(pts), P<const int32_t>(owner),
+                    npts, P<int32_t>(dest), P<int64_t>(counts), nranks);
+  });
+  m.def("host_scatter_by_dest", [](uintptr_t dest, uintptr_t base, int64_t n, int32_t nranks,
+                                   uintptr_t cursor, uintptr_t perm) {
+    host_scatter_by_dest(P<const int32_t>(dest), P<const int64_t>(base), n, nranks,
+                         P<int64_t>(cursor), P<int64_t>(perm));
+  });
+  m.def("host_permute_records", [](uintptr_t in, uintptr_t perm, int64_t n, int32_t rec_bytes,
+                                   uintptr_t out) {
+    host_permute_records(P<const void>(in), P<const int64_t>(perm), n, rec_bytes, P<void>(out));
+  });
+
+  bind_http(m);
+  bind_net(m);
+}

@@ -1,0 +1,6 @@
+// Split pybind11 registration units (keeps each translation unit small).
+#pragma once
+#include <pybind11/pybind11.h>
+
+void bind_http(pybind11::module_& m);  // bind_http.cc: HttpParser, StreamBuf
+void bind_net(pybind11::module_& m);   // bind_net.cc: ketama ring, proxy, memcached protocol

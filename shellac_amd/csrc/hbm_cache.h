@@ -1,0 +1,128 @@
+// HBM-resident cache shard (one per MI355X GPU) and its batch operations.
+//
+// Capability parity: this is the "distributed key/value store" side of Shellac,
+// which the reference delegates to memcached through pylibmc
+// (src/python/shellac/server/Server.py:79-83 client, :335 get, :432 set with
+// time=ttl). The README's roadmap item "replacing Memcached with a
+// purpose-built cache" (README.md:79) is what this class is.
+//
+// Every operation is a *batch* of fixed 16-byte digests on a HIP stream; all
+// pointer arguments are device pointers unless stated otherwise. No operation
+// allocates or synchronises except where documented (lookup_total, sweep,
+// counters, reserve), so the batch pipeline can run back-to-back on a stream.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <mutex>
+
+#include "layout.h"
+
+namespace shellac {
+
+struct ShardConfig {
+  uint64_t log_bytes = 1ull << 30;  // value-log capacity (multiple of 16)
+  uint64_t nbuckets = 1ull << 20;   // power of two, 4 entries (128 B) each
+  uint32_t max_item = 1u << 20;     // max value bytes (memcached's 1 MB item limit)
+  int device = 0;
+};
+
+class HbmCache {
+ public:
+  explicit HbmCache(const ShardConfig& cfg);
+  ~HbmCache();
+  HbmCache(const HbmCache&) = delete;
+  HbmCache& operator=(const HbmCache&) = delete;
+
+  // GET phase 1: probe both candidate buckets of every key. Writes, per key,
+  // the physical log offset of the item (kMissLoc on miss) and the bytes the
+  // item occupies in a GET response (0 on miss); then an exclusive scan of the
+  // sizes into off[0..n] (off[n] = total response bytes).
+  void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
+              uint32_t now, hipStream_t s);
+  // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i].
+  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s);
+  // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
+  // the buffer readable 16 bytes past every value). Later duplicates of a key in
+  // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).
+  void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
+             uint64_t bytes_bound, uint32_t now, hipStream_t s);
+  // DELETE a batch; found[i] = 1 if a live entry was removed.
+  void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now, hipStream_t s);
+  // Reclaim index slots whose items expired or were overwritten. Synchronises;
+  // returns {live entries, live item bytes}.
+  void sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64_t* live_bytes);
+  // Drop everything (memcached FLUSH).
+  void flush(hipStream_t s);
+  CacheCounters counters(hipStream_t s);
+  uint64_t head(hipStream_t s);
+
+  const ShardConfig& config() const { return cfg_; }
+  uint8_t* log_ptr() const { return log_; }
+  Entry* index_ptr() const { return index_; }
+  uint64_t* head_ptr() const { return head_; }
+  // Pre-size the SET workspace for batches of n keys (allocates; call outside capture).
+  void reserve(int64_t n);
+  uint64_t hbm_bytes() const;
+
+ private:
+  void ensure_set_ws(int64_t n, hipStream_t s);
+  void ensure_scan_ws(int64_t n);
+
+  ShardConfig cfg_;
+  uint8_t* log_ = nullptr;
+  Entry* index_ = nullptr;
+  uint64_t* head_ = nullptr;         // device: logical write head
+  unsigned int* ticket_ = nullptr;   // device: last-block ticket for head advance
+  CacheCounters* ctr_ = nullptr;     // device counters
+  unsigned long long* scratch_ = nullptr;  // device scratch for reductions
+  uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
+  // SET workspace
+  int64_t set_cap_ = 0;
+  uint64_t* dd_keys_ = nullptr;
+  int* dd_win_ = nullptr;
+  uint32_t* dd_slot_ = nullptr;
+  uint64_t* set_size_ = nullptr;
+  uint64_t* set_off_ = nullptr;
+  uint32_t dd_mask_ = 0;
+  // scan workspace
+  void* scan_tmp_ = nullptr;
+  size_t scan_tmp_bytes_ = 0;
+  int64_t scan_cap_ = 0;
+  std::mutex mu_;
+};
+
+// ---- Generic device kernels used by the distributed serving path ----------------
+
+// Exclusive scan of in[0..n) into out[0..n] (out[n] = total), u64.
+void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* tmp,
+                           size_t tmp_bytes, hipStream_t s);
+size_t device_scan_tmp_bytes(int64_t n);
+
+// Load-balanced segmented copy: segment i copies (dst_off[i+1]-dst_off[i]) bytes
+// from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
+void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
+             uint8_t* dst, hipStream_t s);
+
+// Digest packed key bytes: key i = bytes[offs[i] .. offs[i+1]).
+void digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out,
+                 hipStream_t s);
+
+// Consistent-hash routing: dest[i] = owner of the first ring point >= ring_position(keys[i])
+// (wrapping), counts[r] += #keys routed to r. `counts` must be zeroed by the caller.
+void route_keys(const Digest* keys, int64_t n, const uint32_t* ring_pts, const int32_t* ring_owner,
+                int32_t npts, int32_t* dest, int64_t* counts, int32_t nranks, hipStream_t s);
+
+// Stable-within-wave scatter of records by destination: pos = base[dest[i]] + rank,
+// perm[i] = pos, out[pos] = in[i] for `rec_bytes`-byte records (16 or 32-multiple of 4).
+void scatter_by_dest(const int32_t* dest, const int64_t* base, int64_t n, int32_t nranks,
+                     int64_t* cursor, int64_t* perm, hipStream_t s);
+void permute_records(const void* in, const int64_t* perm, int64_t n, int32_t rec_bytes, void* out,
+                     hipStream_t s);
+
+// MFMA smoke kernel (BASELINE.json platform check): C[32x32] = A[32x16] * B[16x32],
+// bf16 inputs, fp32 accumulate, one v_mfma_f32_32x32x16_bf16 per wave.
+void mfma_hello(const uint16_t* a, const uint16_t* b, float* c, int tiles, hipStream_t s);
+
+}  // namespace shellac

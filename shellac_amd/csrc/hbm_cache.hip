@@ -1,0 +1,819 @@
+// HIP/CDNA4 kernels and host driver for the HBM cache shard (see hbm_cache.h).
+//
+// Kernel map (all wave64, 256-thread workgroups):
+//   k_probe        16 lanes per key: lanes 0-7 read bucket1, 8-15 bucket2 (two
+//                  coalesced 128-B lines), pair-lane shuffle joins the {digest}
+//                  and {loc,vlen,expire} halves of each entry, max-reduce picks
+//                  the newest live match. No dependent read of the value log.
+//   k_segcopy      load-balanced byte mover: each workgroup owns a 32 KiB tile
+//                  of the *output*, finds the segments covering it (binary search
+//                  of the offsets staged in LDS) and every lane moves 16 B per
+//                  step, so item-size skew never idles lanes. Used for GET
+//                  gathers and for packing SET payloads for the all-to-all.
+//   k_set_dedupe   batch-local open-addressing table: the last SET of a key in a
+//                  batch wins (request order = memcached/HTTP pipelining order).
+//   k_set_copy     load-balanced writer of [ItemHeader|value] into the log at
+//                  head + exclusive-scan(item sizes): batch allocation is a scan.
+//   k_set_index    16 lanes per key: two-choice insert with a 64-bit CAS on the
+//                  entry's loc word; replaces the key's own entry, else a dead
+//                  slot in the emptier bucket, else evicts the oldest item. The
+//                  last workgroup (ticket) advances the log head.
+//   k_delete, k_sweep, k_digest, k_route*, k_permute, k_mfma_hello.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "hbm_cache.h"
+
+namespace shellac {
+
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      throw Error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + #expr + \
+                  " [" + __FILE__ + ":" + std::to_string(__LINE__) + "]");             \
+  } while (0)
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kTileChunks = 2048;          // 16-B chunks per segcopy tile (32 KiB)
+constexpr int kChunksPerThread = kTileChunks / kBlock;
+constexpr int kTileSegCap = 2048;          // segments staged in LDS per tile
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+inline int grid_for(int64_t work_items, int per_block, int cap = 8192) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------------
+// GET: probe
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ keys, int64_t n,
+                                                  const Entry* __restrict__ index, uint64_t mask,
+                                                  const uint64_t* __restrict__ head_ptr,
+                                                  uint64_t cap, uint32_t now,
+                                                  uint64_t* __restrict__ out_loc,
+                                                  uint64_t* __restrict__ out_size,
+                                                  CacheCounters* __restrict__ ctr) {
+  const int l16 = threadIdx.x & 15;
+  const uint64_t head = *head_ptr;
+  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
+  unsigned long long hits = 0, bytes = 0, ops = 0;
+  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
+    const Digest d = keys[i];
+    const uint64_t b = (l16 < 8) ? bucket1(d, mask) : bucket2(d, mask);
+    const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l16 & 7];
+    const uint64_t a = pack2(v.x, v.y);   // even lane: d0   | odd lane: loc
+    const uint64_t c = pack2(v.z, v.w);   // even lane: d1   | odd lane: vlen | expire<<32
+    const uint64_t pa = __shfl_xor(a, 1);
+    const uint64_t pc = __shfl_xor(c, 1);
+    const bool even = (l16 & 1) == 0;
+    const bool hit = even && a == d.lo && c == d.hi &&
+                     entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
+    uint64_t hl = hit ? pa : 0;
+    uint32_t hv = hit ? (uint32_t)pc : 0;
+#pragma unroll
+    for (int s = 2; s < 16; s <<= 1) {
+      const uint64_t ol = __shfl_xor(hl, s);
+      const uint32_t ov = __shfl_xor(hv, s);
+      if (ol > hl) { hl = ol; hv = ov; }
+    }
+    if (l16 == 0) {
+      ++ops;
+      if (hl) {
+        out_loc[i] = (hl - 1) % cap;
+        out_size[i] = item_bytes(hv);
+        ++hits;
+        bytes += hv;
+      } else {
+        out_loc[i] = kMissLoc;
+        out_size[i] = 0;
+      }
+    }
+  }
+  ops = wave_sum(ops);
+  hits = wave_sum(hits);
+  bytes = wave_sum(bytes);
+  if ((threadIdx.x & 63) == 0 && ops) {
+    atomicAdd(&ctr->get_ops, ops);
+    atomicAdd(&ctr->get_hits, hits);
+    atomicAdd(&ctr->get_bytes, bytes);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Load-balanced segmented copy
+// ---------------------------------------------------------------------------------
+// Last index j in [lo, hi) with off[j] <= x (off non-decreasing).
+template <typename T>
+__device__ __forceinline__ int64_t seg_search(const T* off, int64_t lo, int64_t hi, uint64_t x) {
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)off[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int64_t seg_search_global(const uint64_t* off, int64_t n, uint64_t x) {
+  // last j in [0, n) with off[j] <= x
+  int64_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (off[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w.
+// Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
+// src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_segcopy(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint64_t* __restrict__ dst_off, int64_t n, uint8_t* __restrict__ dst,
+    // MODE 1 extras
+    const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
+    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
+    const uint64_t* __restrict__ head_ptr, uint64_t cap) {
+  __shared__ uint64_t s_off[kTileSegCap + 1];
+  __shared__ uint64_t s_src[kTileSegCap];
+  __shared__ int64_t s_j0, s_cnt;
+  const uint64_t total = dst_off[n];
+  const int64_t nchunks = (int64_t)(total >> 4);
+  const uint64_t base = MODE == 1 ? *head_ptr : 0;
+  for (int64_t tile = blockIdx.x; tile * kTileChunks < nchunks; tile += gridDim.x) {
+    const int64_t c0 = tile * kTileChunks;
+    const int64_t c1 = min(c0 + (int64_t)kTileChunks, nchunks);
+    if (threadIdx.x == 0) {
+      const int64_t j0 = seg_search_global(dst_off, n + 1, (uint64_t)c0 << 4);
+      const int64_t j1 = seg_search_global(dst_off, n + 1, ((uint64_t)c1 << 4) - 1);
+      s_j0 = j0;
+      s_cnt = j1 - j0 + 1;
+    }
+    __syncthreads();
+    const int64_t j0 = s_j0, cnt = s_cnt;
+    const bool staged = cnt <= kTileSegCap;
+    if (staged) {
+      for (int64_t k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
+      for (int64_t k = threadIdx.x; k < cnt; k += kBlock) {
+        const int64_t j = j0 + k;
+        s_src[k] = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
+      }
+    }
+    __syncthreads();
+    int64_t jl = 0;
+#pragma unroll 2
+    for (int u = 0; u < kChunksPerThread; ++u) {
+      const int64_t c = c0 + (int64_t)u * kBlock + threadIdx.x;
+      if (c >= c1) break;
+      const uint64_t x = (uint64_t)c << 4;
+      int64_t j;
+      uint64_t seg_start, seg_src;
+      if (staged) {
+        jl = seg_search(s_off, jl, cnt, x);
+        j = j0 + jl;
+        seg_start = s_off[jl];
+        seg_src = s_src[jl];
+      } else {
+        j = j0 + seg_search(dst_off + j0, 0, cnt, x);
+        seg_start = dst_off[j];
+        seg_src = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
+      }
+      const uint64_t w = x - seg_start;
+      if (MODE == 0) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + seg_src + w);
+        *reinterpret_cast<uint4*>(dst + x) = v;
+      } else {
+        uint4 v;
+        if (w == 0) {
+          const Digest d = keys[j];
+          v = make_uint4((uint32_t)d.lo, (uint32_t)(d.lo >> 32), (uint32_t)d.hi,
+                         (uint32_t)(d.hi >> 32));
+        } else if (w == 16) {
+          v = make_uint4(vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic);
+        } else {
+          v = *reinterpret_cast<const uint4*>(src + src_off[j] + (w - kItemHeaderBytes));
+        }
+        *reinterpret_cast<uint4*>(dst + seg_src + w) = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// SET
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys, int64_t n,
+                                                       unsigned long long* __restrict__ tk,
+                                                       int* __restrict__ tw, uint32_t tmask,
+                                                       uint32_t* __restrict__ slot_of) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const unsigned long long key = keys[i].lo ? keys[i].lo : 1ull;
+    uint32_t s = (uint32_t)fmix64(key) & tmask;
+    for (uint32_t probe = 0; probe <= tmask; ++probe) {
+      const unsigned long long prev = atomicCAS(&tk[s], 0ull, key);
+      if (prev == 0ull || prev == key) {
+        atomicMax(&tw[s], (int)i);
+        slot_of[i] = s;
+        break;
+      }
+      s = (s + 1) & tmask;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict__ vlen, int64_t n,
+                                                     const int* __restrict__ tw,
+                                                     const uint32_t* __restrict__ slot_of,
+                                                     uint32_t max_item,
+                                                     uint64_t* __restrict__ size,
+                                                     CacheCounters* __restrict__ ctr) {
+  unsigned long long dropped = 0, ops = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i <= n;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i == n) { size[n] = 0; continue; }
+    const bool win = tw[slot_of[i]] == (int)i && vlen[i] <= max_item;
+    size[i] = win ? item_bytes(vlen[i]) : 0;
+    ++ops;
+    dropped += win ? 0 : 1;
+  }
+  ops = wave_sum(ops);
+  dropped = wave_sum(dropped);
+  if ((threadIdx.x & 63) == 0 && ops) {
+    atomicAdd(&ctr->set_ops, ops);
+    atomicAdd(&ctr->set_dropped, dropped);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_set_index(
+    const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
+    const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
+    uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now, unsigned int* ticket,
+    CacheCounters* __restrict__ ctr) {
+  const int l16 = threadIdx.x & 15;
+  const uint64_t base = *head_ptr;
+  const uint64_t head_new = base + off[n];
+  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
+  unsigned long long evicted = 0, bytes = 0;
+  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
+    if (size[i] == 0) continue;  // uniform across the 16-lane group
+    const Digest d = keys[i];
+    const uint64_t myloc = base + off[i] + 1;
+    const uint32_t myvlen = vlen[i];
+    const uint32_t myexp = expire ? expire[i] : 0u;
+    const uint64_t b1 = bucket1(d, mask), b2 = bucket2(d, mask);
+    const uint64_t b = (l16 < 8) ? b1 : b2;
+    Entry* const bucket = index + b * kEntriesPerBucket;
+    for (int attempt = 0; attempt < 16; ++attempt) {
+      // agent-scope loads: a retry must see other workgroups' CAS results, not stale L1
+      const uint64_t* q = reinterpret_cast<const uint64_t*>(bucket) + 2 * (l16 & 7);
+      const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t c = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t pa = __shfl_xor(a, 1), pc = __shfl_xor(c, 1);
+      const bool even = (l16 & 1) == 0;
+      const bool match = even && a == d.lo && c == d.hi;
+      const bool live = even && entry_live(pa, (uint32_t)(pc >> 32), head_new, cap, now);
+      // group-local masks over the 8 entries (bit e = entry e; e<4 bucket1, e>=4 bucket2)
+      const int gbase = threadIdx.x & 48;
+      const unsigned long long bm = __ballot(match);
+      const unsigned long long bl = __ballot(live);
+      uint32_t mmask = 0, lmask = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mmask |= (uint32_t)((bm >> (gbase + 2 * e)) & 1ull) << e;
+        lmask |= (uint32_t)((bl >> (gbase + 2 * e)) & 1ull) << e;
+      }
+      int target;
+      bool evict = false;
+      if (mmask) {
+        target = __ffs(mmask) - 1;
+      } else {
+        const uint32_t dead = ~lmask & 0xffu;
+        const int live1 = __popc(lmask & 0xfu), live2 = __popc(lmask & 0xf0u);
+        if (dead) {
+          const uint32_t pref = live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu);
+          target = __ffs(pref ? pref : dead) - 1;
+        } else {
+          // both buckets full of live items: evict the oldest (smallest loc)
+          uint64_t oldest = ~0ull;
+          target = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint64_t le = __shfl(pa, gbase + 2 * e);
+            if (le < oldest) { oldest = le; target = e; }
+          }
+          evict = true;
+        }
+      }
+      const uint64_t expected = __shfl(pa, gbase + 2 * target);
+      Entry* const slot = index + (target < 4 ? b1 : b2) * kEntriesPerBucket + (target & 3);
+      int ok = 0;
+      if (l16 == 0) {
+        const unsigned long long prev = atomicCAS(
+            reinterpret_cast<unsigned long long*>(&slot->loc), (unsigned long long)expected,
+            (unsigned long long)myloc);
+        if (prev == expected) {
+          slot->d0 = d.lo;
+          slot->d1 = d.hi;
+          *reinterpret_cast<uint64_t*>(&slot->vlen) = pack2(myvlen, myexp);
+          ok = 1;
+          evicted += evict ? 1 : 0;
+          bytes += myvlen;
+        }
+      }
+      ok = __shfl(ok, gbase);
+      if (ok) break;
+    }
+  }
+  evicted = wave_sum(evicted);
+  bytes = wave_sum(bytes);
+  if ((threadIdx.x & 63) == 0 && (evicted | bytes)) {
+    atomicAdd(&ctr->set_evicted, evicted);
+    atomicAdd(&ctr->set_bytes, bytes);
+  }
+  // The last workgroup to finish publishes the new head (every workgroup has
+  // already read `base`; the next kernel on the stream observes the store).
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned int t = atomicAdd(ticket, 1u);
+    if (t == gridDim.x - 1) {
+      *head_ptr = head_new;
+      *ticket = 0u;
+      __threadfence();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// DELETE / SWEEP
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_delete(const Digest* __restrict__ keys, int64_t n,
+                                                   Entry* __restrict__ index, uint64_t mask,
+                                                   const uint64_t* __restrict__ head_ptr,
+                                                   uint64_t cap, uint32_t now,
+                                                   uint8_t* __restrict__ found,
+                                                   CacheCounters* __restrict__ ctr) {
+  const int l16 = threadIdx.x & 15;
+  const uint64_t head = *head_ptr;
+  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
+  unsigned long long ops = 0, hits = 0;
+  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
+    const Digest d = keys[i];
+    const uint64_t b = (l16 < 8) ? bucket1(d, mask) : bucket2(d, mask);
+    Entry* const bucket = index + b * kEntriesPerBucket;
+    const uint4 v = reinterpret_cast<const uint4*>(bucket)[l16 & 7];
+    const uint64_t a = pack2(v.x, v.y), c = pack2(v.z, v.w);
+    const uint64_t pa = __shfl_xor(a, 1), pc = __shfl_xor(c, 1);
+    const bool even = (l16 & 1) == 0;
+    int was_live = 0;
+    if (even && a == d.lo && c == d.hi && pa != 0) {
+      Entry* const slot = bucket + ((l16 & 7) >> 1);
+      const unsigned long long prev =
+          atomicCAS(reinterpret_cast<unsigned long long*>(&slot->loc), (unsigned long long)pa, 0ull);
+      if (prev == pa && entry_live(pa, (uint32_t)(pc >> 32), head, cap, now)) was_live = 1;
+    }
+    const unsigned long long any = __ballot(was_live);
+    const int gbase = threadIdx.x & 48;
+    const int f = ((any >> gbase) & 0xffffull) != 0;
+    if (l16 == 0) {
+      ++ops;
+      hits += f;
+      if (found) found[i] = (uint8_t)f;
+    }
+  }
+  ops = wave_sum(ops);
+  hits = wave_sum(hits);
+  if ((threadIdx.x & 63) == 0 && ops) {
+    atomicAdd(&ctr->del_ops, ops);
+    atomicAdd(&ctr->del_hits, hits);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sweep(Entry* __restrict__ index, uint64_t nslots,
+                                                  const uint64_t* __restrict__ head_ptr,
+                                                  uint64_t cap, uint32_t now,
+                                                  unsigned long long* __restrict__ out,
+                                                  CacheCounters* __restrict__ ctr) {
+  const uint64_t head = *head_ptr;
+  unsigned long long live = 0, bytes = 0, swept = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < nslots;
+       k += (uint64_t)gridDim.x * kBlock) {
+    Entry* const e = index + k;
+    const uint64_t loc = e->loc;
+    if (!loc) continue;
+    const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
+    if (entry_live(loc, (uint32_t)(ve >> 32), head, cap, now)) {
+      ++live;
+      bytes += item_bytes((uint32_t)ve);
+    } else if (atomicCAS(reinterpret_cast<unsigned long long*>(&e->loc), (unsigned long long)loc,
+                         0ull) == loc) {
+      ++swept;
+    }
+  }
+  live = wave_sum(live);
+  bytes = wave_sum(bytes);
+  swept = wave_sum(swept);
+  if ((threadIdx.x & 63) == 0) {
+    if (live) atomicAdd(&out[0], live);
+    if (bytes) atomicAdd(&out[1], bytes);
+    if (swept) atomicAdd(&ctr->swept, swept);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Digest / routing / permutation
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_digest(const uint8_t* __restrict__ bytes,
+                                                   const int64_t* __restrict__ offs, int64_t n,
+                                                   Digest* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t b = offs[i];
+    out[i] = digest_bytes(bytes + b, (uint64_t)(offs[i + 1] - b));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_route(const Digest* __restrict__ keys, int64_t n,
+                                                  const uint32_t* __restrict__ pts,
+                                                  const int32_t* __restrict__ owner, int32_t npts,
+                                                  int32_t* __restrict__ dest,
+                                                  int64_t* __restrict__ counts, int32_t nranks) {
+  extern __shared__ unsigned long long s_cnt[];
+  for (int r = threadIdx.x; r < nranks; r += kBlock) s_cnt[r] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t p = ring_position(keys[i]);
+    int lo = 0, hi = npts;  // first point >= p
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (pts[mid] < p) lo = mid + 1; else hi = mid;
+    }
+    const int r = owner[lo == npts ? 0 : lo];
+    dest[i] = r;
+    atomicAdd(&s_cnt[r], 1ull);
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nranks; r += kBlock)
+    if (s_cnt[r]) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[r]), s_cnt[r]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ dest,
+                                                    const int64_t* __restrict__ base, int64_t n,
+                                                    int64_t* __restrict__ cursor,
+                                                    int64_t* __restrict__ perm) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < n; i0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool act = i < n;
+    const int d = act ? dest[i] : -1;
+    // wave-aggregated slot reservation: one atomic per distinct destination per wave
+    unsigned long long todo = __ballot(act);
+    int64_t pos = 0;
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const int ld = __shfl(d, leader);
+      const unsigned long long same = __ballot(act && d == ld);
+      int64_t start = 0;
+      if (lane == leader)
+        start = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[ld]),
+                                   (unsigned long long)__popcll(same));
+      start = __shfl(start, leader);
+      if (d == ld && act) {
+        const unsigned long long below = same & ((1ull << lane) - 1ull);
+        pos = base[ld] + start + __popcll(below);
+      }
+      todo &= ~same;
+    }
+    if (act) perm[i] = pos;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_permute(const uint32_t* __restrict__ in,
+                                                    const int64_t* __restrict__ perm, int64_t n,
+                                                    int32_t words, uint32_t* __restrict__ out) {
+  const int64_t total = n * words;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = t / words, w = t - i * words;
+    out[perm[i] * words + w] = in[t];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// MFMA hello (platform smoke)
+// ---------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__global__ __launch_bounds__(64) void k_mfma_hello(const uint16_t* __restrict__ A,
+                                                   const uint16_t* __restrict__ B,
+                                                   float* __restrict__ C) {
+  // tile t: A_t [32 x 16] row-major, B_t [16 x 32] row-major, C_t [32 x 32] row-major
+  const int t = blockIdx.x, l = threadIdx.x, r = l & 31, h = l >> 5;
+  const uint16_t* a = A + (size_t)t * 32 * 16;
+  const uint16_t* b = B + (size_t)t * 16 * 32;
+  u16x8_t av, bv;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    av[j] = a[r * 16 + 8 * h + j];      // A[row r][k = 8h + j]
+    bv[j] = b[(8 * h + j) * 32 + r];    // B[k = 8h + j][col r]
+  }
+  f32x16_t acc = {};
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, av),
+                                                __builtin_bit_cast(bf16x8_t, bv), acc, 0, 0, 0);
+  float* c = C + (size_t)t * 32 * 32;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    c[row * 32 + r] = acc[i];
+  }
+}
+
+}  // namespace
+
+// =====================================================================================
+// Host side
+// =====================================================================================
+size_t device_scan_tmp_bytes(int64_t n) {
+  size_t bytes = 0;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr,
+                                          (uint64_t*)nullptr, (int)(n + 1)));
+  return bytes;
+}
+
+void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* tmp,
+                           size_t tmp_bytes, hipStream_t s) {
+  // in must be readable at [0, n]; the caller guarantees in[n] == 0.
+  SH_CHECK(n + 1 < (int64_t)INT32_MAX, "scan too large");
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, (int)(n + 1), s));
+}
+
+void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
+             uint8_t* dst, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_segcopy<0>, dim3(2048), dim3(kBlock), 0, s, src, src_off, dst_off, n, dst,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, (uint64_t)1);
+  HIP_OK(hipGetLastError());
+}
+
+void digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out,
+                 hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_digest, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, bytes, offs, n, out);
+  HIP_OK(hipGetLastError());
+}
+
+void route_keys(const Digest* keys, int64_t n, const uint32_t* ring_pts, const int32_t* ring_owner,
+                int32_t npts, int32_t* dest, int64_t* counts, int32_t nranks, hipStream_t s) {
+  if (n <= 0) return;
+  SH_CHECK(npts > 0 && nranks > 0 && nranks <= 4096, "bad ring");
+  hipLaunchKernelGGL(k_route, dim3(grid_for(n, kBlock * 8, 1024)), dim3(kBlock),
+                     nranks * sizeof(unsigned long long), s, keys, n, ring_pts, ring_owner, npts,
+                     dest, counts, nranks);
+  HIP_OK(hipGetLastError());
+}
+
+void scatter_by_dest(const int32_t* dest, const int64_t* base, int64_t n, int32_t nranks,
+                     int64_t* cursor, int64_t* perm, hipStream_t s) {
+  if (n <= 0) return;
+  (void)nranks;
+  hipLaunchKernelGGL(k_scatter, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, dest, base, n,
+                     cursor, perm);
+  HIP_OK(hipGetLastError());
+}
+
+void permute_records(const void* in, const int64_t* perm, int64_t n, int32_t rec_bytes, void* out,
+                     hipStream_t s) {
+  if (n <= 0) return;
+  SH_CHECK(rec_bytes % 4 == 0, "record size must be a multiple of 4");
+  const int32_t words = rec_bytes / 4;
+  hipLaunchKernelGGL(k_permute, dim3(grid_for(n * words, kBlock)), dim3(kBlock), 0, s,
+                     (const uint32_t*)in, perm, n, words, (uint32_t*)out);
+  HIP_OK(hipGetLastError());
+}
+
+void mfma_hello(const uint16_t* a, const uint16_t* b, float* c, int tiles, hipStream_t s) {
+  if (tiles <= 0) return;
+  hipLaunchKernelGGL(k_mfma_hello, dim3(tiles), dim3(64), 0, s, a, b, c);
+  HIP_OK(hipGetLastError());
+}
+
+HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
+  SH_CHECK(cfg_.nbuckets >= 2 && (cfg_.nbuckets & (cfg_.nbuckets - 1)) == 0,
+           "nbuckets must be a power of two >= 2");
+  SH_CHECK(cfg_.log_bytes >= 4096 && cfg_.log_bytes % 16 == 0, "log_bytes must be >=4096, %16");
+  SH_CHECK(cfg_.max_item > 0 && item_bytes(cfg_.max_item) * 2 <= cfg_.log_bytes,
+           "max_item too large for the log");
+  DeviceGuard g(cfg_.device);
+  const uint64_t slack = item_bytes(cfg_.max_item) + 64;
+  HIP_OK(hipMalloc(&log_, cfg_.log_bytes + slack));
+  HIP_OK(hipMalloc(&index_, cfg_.nbuckets * kBucketBytes));
+  HIP_OK(hipMalloc(&head_, 64));
+  HIP_OK(hipMalloc(&ticket_, 64));
+  HIP_OK(hipMalloc(&ctr_, sizeof(CacheCounters)));
+  HIP_OK(hipMalloc(&scratch_, 64));
+  HIP_OK(hipHostMalloc(&host_buf_, 64 * sizeof(uint64_t), hipHostMallocDefault));
+  HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
+  HIP_OK(hipMemset(head_, 0, 64));
+  HIP_OK(hipMemset(ticket_, 0, 64));
+  HIP_OK(hipMemset(ctr_, 0, sizeof(CacheCounters)));
+  HIP_OK(hipDeviceSynchronize());
+}
+
+HbmCache::~HbmCache() {
+  DeviceGuard g(cfg_.device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(log_);
+  (void)hipFree(index_);
+  (void)hipFree(head_);
+  (void)hipFree(ticket_);
+  (void)hipFree(ctr_);
+  (void)hipFree(scratch_);
+  (void)hipHostFree(host_buf_);
+  (void)hipFree(dd_keys_);
+  (void)hipFree(dd_win_);
+  (void)hipFree(dd_slot_);
+  (void)hipFree(set_size_);
+  (void)hipFree(set_off_);
+  (void)hipFree(scan_tmp_);
+}
+
+uint64_t HbmCache::hbm_bytes() const {
+  return cfg_.log_bytes + item_bytes(cfg_.max_item) + 64 + cfg_.nbuckets * kBucketBytes;
+}
+
+void HbmCache::ensure_scan_ws(int64_t n) {
+  if (n <= scan_cap_) return;
+  int64_t cap = scan_cap_ ? scan_cap_ : 1024;
+  while (cap < n) cap *= 2;
+  const size_t need = device_scan_tmp_bytes(cap);
+  if (need > scan_tmp_bytes_) {
+    HIP_OK(hipDeviceSynchronize());
+    (void)hipFree(scan_tmp_);
+    HIP_OK(hipMalloc(&scan_tmp_, need));
+    scan_tmp_bytes_ = need;
+  }
+  scan_cap_ = cap;
+}
+
+void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
+  (void)s;
+  if (n <= set_cap_) return;
+  int64_t cap = set_cap_ ? set_cap_ : 1024;
+  while (cap < n) cap *= 2;
+  HIP_OK(hipDeviceSynchronize());
+  (void)hipFree(dd_keys_); (void)hipFree(dd_win_); (void)hipFree(dd_slot_);
+  (void)hipFree(set_size_); (void)hipFree(set_off_);
+  const uint64_t tslots = (uint64_t)cap * 2;
+  HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
+  HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
+  HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
+  HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
+  HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
+  dd_mask_ = (uint32_t)(tslots - 1);
+  set_cap_ = cap;
+}
+
+void HbmCache::reserve(int64_t n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  ensure_set_ws(n, nullptr);
+  ensure_scan_ws(n);
+}
+
+void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
+                      uint32_t now, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  if (n <= 0) {
+    HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
+    return;
+  }
+  ensure_scan_ws(n);
+  HIP_OK(hipMemsetAsync(size + n, 0, sizeof(uint64_t), s));
+  hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, 16384)), dim3(kBlock), 0, s, keys, n,
+                     index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, loc, size, ctr_);
+  HIP_OK(hipGetLastError());
+  device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
+}
+
+void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
+                      hipStream_t s) {
+  DeviceGuard g(cfg_.device);
+  segcopy(log_, loc, off, n, out, s);
+}
+
+void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
+                     int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s) {
+  if (n <= 0) return;
+  SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
+           "SET batch larger than half the log; split the batch");
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  ensure_set_ws(n, s);
+  ensure_scan_ws(n);
+  const uint64_t tslots = (uint64_t)dd_mask_ + 1;
+  HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
+  HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
+  const int grid = grid_for(n, kBlock);
+  hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, n,
+                     (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
+  hipLaunchKernelGGL(k_set_size, dim3(grid_for(n + 1, kBlock)), dim3(kBlock), 0, s, vlen, n,
+                     dd_win_, dd_slot_, cfg_.max_item, set_size_, ctr_);
+  HIP_OK(hipGetLastError());
+  device_exclusive_scan(set_size_, set_off_, n, scan_tmp_, scan_tmp_bytes_, s);
+  hipLaunchKernelGGL(k_segcopy<1>, dim3(2048), dim3(kBlock), 0, s, values, val_off, set_off_, n,
+                     log_, keys, vlen, flags, expire, head_, cfg_.log_bytes);
+  HIP_OK(hipGetLastError());
+  const int igrid = grid_for(n * 16, kBlock, 16384);
+  hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
+                     vlen, expire, index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, ticket_,
+                     ctr_);
+  HIP_OK(hipGetLastError());
+}
+
+void HbmCache::remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now, hipStream_t s) {
+  if (n <= 0) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  hipLaunchKernelGGL(k_delete, dim3(grid_for(n * 16, kBlock, 16384)), dim3(kBlock), 0, s, keys, n,
+                     index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, found, ctr_);
+  HIP_OK(hipGetLastError());
+}
+
+void HbmCache::sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64_t* live_bytes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  unsigned long long* out = scratch_;
+  HIP_OK(hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s));
+  const uint64_t nslots = cfg_.nbuckets * kEntriesPerBucket;
+  hipLaunchKernelGGL(k_sweep, dim3(grid_for((int64_t)nslots, kBlock, 4096)), dim3(kBlock), 0, s,
+                     index_, nslots, head_, cfg_.log_bytes, now, out, ctr_);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(host_buf_, out, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (live_entries) *live_entries = host_buf_[0];
+  if (live_bytes) *live_bytes = host_buf_[1];
+}
+
+void HbmCache::flush(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  HIP_OK(hipMemsetAsync(index_, 0, cfg_.nbuckets * kBucketBytes, s));
+}
+
+CacheCounters HbmCache::counters(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  CacheCounters c;
+  HIP_OK(hipMemcpyAsync(host_buf_, ctr_, sizeof(CacheCounters), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  std::memcpy(&c, host_buf_, sizeof(CacheCounters));
+  return c;
+}
+
+uint64_t HbmCache::head(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  HIP_OK(hipMemcpyAsync(host_buf_, head_, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return host_buf_[0];
+}
+
+}  // namespace shellac

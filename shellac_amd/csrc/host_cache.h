@@ -1,0 +1,73 @@
+// Host-DRAM cache shard with exactly the HBM shard's layout and semantics.
+//
+// Uses: (a) the cache backend on machines/CI without a GPU, (b) the semantic
+// reference the HIP kernels are tested against, (c) the CPU implementation of the
+// batch ops when the distributed serving path runs over gloo. Thread-safe (one
+// mutex per shard; the proxy stripes keys over several shards for concurrency).
+#pragma once
+
+#include <mutex>
+#include <vector>
+
+#include "layout.h"
+
+namespace shellac {
+
+class HostCache {
+ public:
+  HostCache(uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item);
+  ~HostCache();
+  HostCache(const HostCache&) = delete;
+  HostCache& operator=(const HostCache&) = delete;
+
+  void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
+              uint32_t now);
+  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out) const;
+  void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
+             uint32_t now);
+  void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now);
+  void sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes);
+  void flush();
+  CacheCounters counters();
+  uint64_t head();
+
+  // Single-key conveniences used by the proxy / memcached server. get() copies
+  // the value (not the header) into `out` and returns false on miss.
+  bool get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* flags, uint32_t now);
+  void set_one(const Digest& key, const uint8_t* value, uint32_t vlen, uint32_t flags,
+               uint32_t expire, uint32_t now);
+
+  uint64_t log_bytes() const { return log_bytes_; }
+  uint64_t nbuckets() const { return nbuckets_; }
+  uint32_t max_item() const { return max_item_; }
+
+ private:
+  bool insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uint32_t expire, uint32_t now);
+  uint64_t probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) const;
+
+  uint64_t log_bytes_, nbuckets_, mask_;
+  uint32_t max_item_;
+  uint8_t* log_ = nullptr;
+  size_t log_alloc_ = 0;
+  Entry* index_ = nullptr;
+  size_t index_alloc_ = 0;
+  uint64_t head_ = 0;
+  CacheCounters ctr_{};
+  mutable std::mutex mu_;
+};
+
+// CPU versions of the device batch helpers (same contracts as hbm_cache.h).
+void host_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n);
+void host_segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
+                  uint8_t* dst);
+void host_digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out);
+void host_route_keys(const Digest* keys, int64_t n, const uint32_t* ring_pts,
+                     const int32_t* ring_owner, int32_t npts, int32_t* dest, int64_t* counts,
+                     int32_t nranks);
+void host_scatter_by_dest(const int32_t* dest, const int64_t* base, int64_t n, int32_t nranks,
+                          int64_t* cursor, int64_t* perm);
+void host_permute_records(const void* in, const int64_t* perm, int64_t n, int32_t rec_bytes,
+                          void* out);
+
+}  // namespace shellac

@@ -1,0 +1,82 @@
+// Memory layout of one cache shard, shared by the HBM (HIP) and DRAM (host) engines.
+//
+// A shard is two regions:
+//
+//   index : nbuckets x 128-byte buckets, 4 x 32-byte Entry each. Every object has
+//           two candidate buckets (two-choice hashing), so a probe is exactly two
+//           independent cache-line reads and never touches the value log.
+//   log   : a circular, append-only byte log of `capacity` bytes (+ one max item
+//           of slack so an item that starts near the end never wraps). Items are
+//           appended at a monotonically increasing *logical* head; physical offset
+//           = logical % capacity. Eviction is FIFO by construction: appending
+//           overwrites the oldest bytes. An entry is live iff its item has not
+//           been overwritten (head <= loc + capacity) and has not expired.
+//
+// This replaces the reference's external memcached slab store (Server.py:81-83,
+// :335 get, :432 set with time=ttl) with a structure that maps onto HBM: no
+// free lists, no per-class slabs, no fragmentation, batch allocation is one
+// prefix sum, and lookups are coalesced 128-byte reads.
+#pragma once
+
+#include "digest.h"
+
+namespace shellac {
+
+constexpr uint32_t kEntriesPerBucket = 4;
+constexpr uint32_t kBucketBytes = 128;
+constexpr uint32_t kItemHeaderBytes = 32;
+constexpr uint32_t kItemMagic = 0x5348a11cu;
+constexpr uint64_t kMissLoc = ~0ULL;
+
+struct alignas(32) Entry {
+  uint64_t d0;      // digest.lo
+  uint64_t d1;      // digest.hi
+  uint64_t loc;     // logical offset of the item header + 1 (0 = empty slot)
+  uint32_t vlen;    // value length in bytes
+  uint32_t expire;  // absolute expiry (seconds since cache epoch), 0 = never
+};
+static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
+
+// Header written in front of every value in the log; a GET returns header+value.
+struct alignas(16) ItemHeader {
+  uint64_t d0;
+  uint64_t d1;
+  uint32_t vlen;
+  uint32_t flags;   // opaque client flags (memcached protocol)
+  uint32_t expire;
+  uint32_t magic;
+};
+static_assert(sizeof(ItemHeader) == kItemHeaderBytes, "ItemHeader must be 32 bytes");
+
+SH_HD uint64_t item_bytes(uint32_t vlen) { return kItemHeaderBytes + align_up(vlen, 16); }
+
+SH_HD uint64_t bucket1(const Digest& d, uint64_t mask) { return d.lo & mask; }
+
+SH_HD uint64_t bucket2(const Digest& d, uint64_t mask) {
+  uint64_t b1 = d.lo & mask;
+  uint64_t b2 = fmix64(d.hi ^ rotl64(d.lo, 29)) & mask;
+  return b2 == b1 ? (b1 ^ 1) & mask : b2;
+}
+
+SH_HD bool entry_live(uint64_t loc, uint32_t expire, uint64_t head, uint64_t capacity,
+                      uint32_t now) {
+  return loc != 0 && head <= (loc - 1) + capacity && (expire == 0 || expire > now);
+}
+
+// Counters kept on the device (and mirrored by the host engine).
+struct CacheCounters {
+  unsigned long long get_ops;
+  unsigned long long get_hits;
+  unsigned long long get_bytes;
+  unsigned long long set_ops;
+  unsigned long long set_bytes;
+  unsigned long long set_dropped;   // rejected (too large) or lost a same-batch dedupe
+  unsigned long long set_evicted;   // a live entry displaced because both buckets were full
+  unsigned long long del_ops;
+  unsigned long long del_hits;
+  unsigned long long swept;         // dead entries reclaimed by sweep()
+  unsigned long long reserved[6];
+};
+static_assert(sizeof(CacheCounters) == 128, "CacheCounters layout");
+
+}  // namespace shellac

@@ -1,0 +1,274 @@
+"""Tensor-level batch operations on one cache shard (HBM on a GPU, DRAM on the CPU).
+
+This is the compute path of the cache. A ``CacheShard`` on a ``cuda`` device
+drives the hand-written HIP kernels in ``csrc/hbm_cache.hip`` (probe, load-
+balanced gather, dedupe + scan-allocated log write, two-choice CAS insert); on
+the CPU it drives ``csrc/host_cache.cc``, which implements the same layout and
+policies and is the semantic reference the kernels are tested against.
+
+Keys are 128-bit digests stored as ``int64`` tensors of shape ``[n, 2]`` (lo, hi)
+(see ``csrc/digest.h``). The reference addresses objects by URL string through
+pylibmc (src/python/shellac/server/Server.py:327, :335, :432); digests are what
+let the GPU path move fixed 16-byte records.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .._native import core
+
+ITEM_HEADER_BYTES = 32
+ITEM_MAGIC = 0x5348A11C
+MISS_LOC = (1 << 64) - 1
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def item_bytes(vlen: int) -> int:
+    return ITEM_HEADER_BYTES + ((vlen + 15) & ~15)
+
+
+# ----------------------------------------------------------------------------------
+# digests & packing helpers
+# ----------------------------------------------------------------------------------
+def pack_bytes(items: Sequence[bytes]) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate byte strings -> (uint8 buffer, int64 offsets[n+1])."""
+    offs = np.zeros(len(items) + 1, dtype=np.int64)
+    np.cumsum([len(x) for x in items], out=offs[1:])
+    buf = np.frombuffer(b"".join(items), dtype=np.uint8) if items else np.zeros(0, np.uint8)
+    return buf, offs
+
+
+def digest_strings(keys: Sequence[bytes], device: str | torch.device = "cpu") -> torch.Tensor:
+    """128-bit digests of ``keys`` as an int64 tensor [n, 2] (computed on the host)."""
+    c = core()
+    buf, offs = pack_bytes(list(keys))
+    buf = np.ascontiguousarray(buf)
+    if buf.size == 0:
+        buf = np.zeros(1, np.uint8)
+    out = np.zeros((len(keys), 2), dtype=np.int64)
+    c.host_digest_keys(buf.ctypes.data, offs.ctypes.data, len(keys), out.ctypes.data)
+    return torch.from_numpy(out).to(device)
+
+
+def digest_packed(buf: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """Digest packed key bytes on the tensors' device (HIP kernel on GPU)."""
+    c = core()
+    n = offs.numel() - 1
+    out = torch.empty((n, 2), dtype=torch.int64, device=buf.device)
+    if buf.is_cuda:
+        c.digest_keys(buf.data_ptr(), offs.data_ptr(), n, out.data_ptr(), _stream_handle(buf.device))
+    else:
+        c.host_digest_keys(buf.data_ptr(), offs.data_ptr(), n, out.data_ptr())
+    return out
+
+
+def pack_values(values: Sequence[bytes], device: str | torch.device = "cpu"):
+    """Pack values 16-byte aligned (+16 B readable slack) for ``CacheShard.store``.
+
+    Returns (values uint8 tensor, val_off int64 tensor, vlen int32 tensor).
+    """
+    n = len(values)
+    vlen = np.array([len(v) for v in values], dtype=np.int64)
+    padded = (vlen + 15) & ~15
+    val_off = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(padded[:-1], out=val_off[1:])
+    total = int(padded.sum()) + 16
+    buf = np.zeros(total, dtype=np.uint8)
+    for i, v in enumerate(values):
+        buf[val_off[i] : val_off[i] + len(v)] = np.frombuffer(v, dtype=np.uint8)
+    return (
+        torch.from_numpy(buf).to(device),
+        torch.from_numpy(val_off).to(device),
+        torch.from_numpy(vlen.astype(np.int32)).to(device),
+    )
+
+
+def unpack_records(out: torch.Tensor, off: torch.Tensor, size: torch.Tensor) -> list:
+    """Decode GET output ([ItemHeader | value | pad] per hit) -> list of (value, flags) or None."""
+    o = out.cpu().numpy()
+    offs = off.cpu().numpy()
+    sizes = size.cpu().numpy()
+    res = []
+    for i in range(len(sizes)):
+        if sizes[i] == 0:
+            res.append(None)
+            continue
+        base = int(offs[i])
+        hdr = o[base : base + ITEM_HEADER_BYTES].view(np.uint32)
+        vl, flags, magic = int(hdr[4]), int(hdr[5]), int(hdr[7])
+        if magic != ITEM_MAGIC:
+            raise RuntimeError(f"corrupt item header at {base}: magic {magic:#x}")
+        res.append((o[base + ITEM_HEADER_BYTES : base + ITEM_HEADER_BYTES + vl].tobytes(), flags))
+    return res
+
+
+@dataclass
+class Lookup:
+    loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
+    size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
+    off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
+
+    @property
+    def n(self) -> int:
+        return self.loc.numel()
+
+    def hits(self) -> torch.Tensor:
+        return self.size[: self.n] > 0
+
+
+class CacheShard:
+    """One cache shard: an HBM arena on ``cuda:i`` or a DRAM arena on ``cpu``.
+
+    Args:
+      log_bytes: capacity of the circular value log (FIFO eviction when full).
+      nbuckets: index buckets (power of two); 4 entries each, two-choice hashing.
+      max_item: largest storable value (memcached parity default 1 MiB).
+    """
+
+    def __init__(self, log_bytes: int, nbuckets: int, max_item: int = 1 << 20,
+                 device: str | torch.device = "cpu"):
+        self.device = torch.device(device)
+        self.log_bytes = int(log_bytes)
+        self.nbuckets = int(nbuckets)
+        self.max_item = int(max_item)
+        c = core()
+        if self.device.type == "cuda":
+            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self.device = torch.device("cuda", idx)
+            self._impl = c.HbmCache(self.log_bytes, self.nbuckets, self.max_item, idx)
+            self.is_gpu = True
+        elif self.device.type == "cpu":
+            self._impl = c.HostCache(self.log_bytes, self.nbuckets, self.max_item)
+            self.is_gpu = False
+        else:
+            raise ValueError(f"unsupported device {self.device}")
+        self.epoch = time.time()
+
+    # -- time ---------------------------------------------------------------------
+    def now(self) -> int:
+        """Seconds since this shard's epoch (the unit of ``expire``)."""
+        return int(time.time() - self.epoch) + 1
+
+    def expire_at(self, ttl_seconds: int) -> int:
+        return 0 if ttl_seconds <= 0 else self.now() + int(ttl_seconds)
+
+    def _s(self) -> int:
+        return _stream_handle(self.device)
+
+    def _check(self, t: torch.Tensor, name: str):
+        if t.device != self.device:
+            raise ValueError(f"{name} on {t.device}, shard on {self.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+    # -- GET ----------------------------------------------------------------------
+    def lookup(self, keys: torch.Tensor, now: Optional[int] = None) -> Lookup:
+        self._check(keys, "keys")
+        n = keys.shape[0]
+        loc = torch.empty(n, dtype=torch.int64, device=self.device)
+        size = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        now = self.now() if now is None else now
+        if self.is_gpu:
+            self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
+                              now, self._s())
+        else:
+            size[n] = 0
+            self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
+                              now)
+        return Lookup(loc, size, off)
+
+    def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
+               total: Optional[int] = None) -> torch.Tensor:
+        """Copy hits into ``out`` (allocated from off[n] if not given: one sync)."""
+        if out is None:
+            total = int(lk.off[lk.n].item()) if total is None else total
+            out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
+        self._check(out, "out")
+        if self.is_gpu:
+            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s())
+        else:
+            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
+        return out
+
+    def get(self, keys: torch.Tensor, now: Optional[int] = None):
+        """lookup + gather. Returns (out bytes, off[n], size[n]); record i = out[off[i]:+size[i]]."""
+        lk = self.lookup(keys, now)
+        out = self.gather(lk)
+        return out, lk.off[: lk.n], lk.size[: lk.n]
+
+    # -- SET ----------------------------------------------------------------------
+    def store(self, keys: torch.Tensor, values: torch.Tensor, val_off: torch.Tensor,
+              vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
+              expire: Optional[torch.Tensor] = None, now: Optional[int] = None) -> None:
+        for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
+            self._check(t, nm)
+        if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
+            raise TypeError("vlen must be int32 and val_off int64")
+        n = keys.shape[0]
+        if n == 0:
+            return
+        now = self.now() if now is None else now
+        fp = 0 if flags is None else flags.data_ptr()
+        ep = 0 if expire is None else expire.data_ptr()
+        if self.is_gpu:
+            bound = 48 * n + values.numel()
+            self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
+                             fp, ep, n, bound, now, self._s())
+        else:
+            self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
+                             fp, ep, n, now)
+
+    def set_many(self, keys: Sequence[bytes], values: Sequence[bytes], ttl: int = 0,
+                 flags: int = 0) -> None:
+        d = digest_strings(keys, self.device)
+        v, vo, vl = pack_values(values, self.device)
+        ex = torch.full((len(keys),), self.expire_at(ttl), dtype=torch.int32, device=self.device)
+        fl = torch.full((len(keys),), flags, dtype=torch.int32, device=self.device)
+        self.store(d, v, vo, vl, fl, ex)
+
+    def get_many(self, keys: Sequence[bytes]) -> list:
+        d = digest_strings(keys, self.device)
+        out, off, size = self.get(d)
+        return [None if r is None else r[0] for r in unpack_records(out, off, size)]
+
+    # -- DELETE / maintenance ------------------------------------------------------
+    def remove(self, keys: torch.Tensor, now: Optional[int] = None) -> torch.Tensor:
+        self._check(keys, "keys")
+        n = keys.shape[0]
+        found = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        now = self.now() if now is None else now
+        if self.is_gpu:
+            self._impl.remove(keys.data_ptr(), n, found.data_ptr(), now, self._s())
+        else:
+            self._impl.remove(keys.data_ptr(), n, found.data_ptr(), now)
+        return found.bool()
+
+    def sweep(self, now: Optional[int] = None) -> tuple[int, int]:
+        now = self.now() if now is None else now
+        return tuple(self._impl.sweep(now, self._s()) if self.is_gpu else self._impl.sweep(now))
+
+    def flush(self) -> None:
+        if self.is_gpu:
+            self._impl.flush(self._s())
+        else:
+            self._impl.flush()
+
+    def counters(self) -> dict:
+        return self._impl.counters(self._s()) if self.is_gpu else self._impl.counters()
+
+    def head(self) -> int:
+        return self._impl.head(self._s()) if self.is_gpu else self._impl.head()
+
+    def reserve(self, n: int) -> None:
+        if self.is_gpu:
+            self._impl.reserve(n)

@@ -1,0 +1,113 @@
+"""Semantics of a cache shard (DRAM engine on the CPU; the HBM kernels are checked
+against the same engine in tests/test_hbm_gpu.py)."""
+import numpy as np
+import pytest
+import torch
+
+from shellac_amd.ops.cache import (CacheShard, digest_strings, item_bytes, pack_values,
+                                   unpack_records)
+from shellac_amd.ops import routing as R
+
+
+def make(log=1 << 20, nb=1 << 10, max_item=8192):
+    return CacheShard(log, nb, max_item, "cpu")
+
+
+def test_set_get_roundtrip_and_flags():
+    s = make()
+    keys = [f"/p/{i}".encode() for i in range(200)]
+    vals = [bytes([i % 251]) * (i * 7 % 300) for i in range(200)]
+    d = digest_strings(keys)
+    v, vo, vl = pack_values(vals)
+    flags = torch.arange(200, dtype=torch.int32)
+    s.store(d, v, vo, vl, flags=flags)
+    out, off, size = s.get(d)
+    recs = unpack_records(out, off, size)
+    assert [r[0] for r in recs] == vals
+    assert [r[1] for r in recs] == list(range(200))
+    assert size.tolist() == [item_bytes(len(x)) for x in vals]
+
+
+def test_overwrite_last_writer_wins_within_batch():
+    s = make()
+    s.set_many([b"/a", b"/b", b"/a", b"/a"], [b"1", b"2", b"3", b"4"])
+    assert s.get_many([b"/a", b"/b"]) == [b"4", b"2"]
+    c = s.counters()
+    assert c["set_ops"] == 4 and c["set_dropped"] == 2
+    s.set_many([b"/a"], [b"5"])
+    assert s.get_many([b"/a"]) == [b"5"]
+
+
+def test_miss_and_delete():
+    s = make()
+    s.set_many([b"/x", b"/y"], [b"xx", b"yy"])
+    found = s.remove(digest_strings([b"/x", b"/nope"]))
+    assert found.tolist() == [True, False]
+    assert s.get_many([b"/x", b"/y"]) == [None, b"yy"]
+
+
+def test_ttl_expiry_and_sweep():
+    s = make()
+    d = digest_strings([b"/t1", b"/t2"])
+    v, vo, vl = pack_values([b"a", b"b"])
+    now = 100
+    s.store(d, v, vo, vl, expire=torch.tensor([105, 0], dtype=torch.int32), now=now)
+    recs = unpack_records(*s.get(d, now=104))
+    assert recs[0][0] == b"a" and recs[1][0] == b"b"
+    recs = unpack_records(*s.get(d, now=105))
+    assert recs[0] is None and recs[1][0] == b"b"
+    live, _ = s.sweep(now=105)
+    assert live == 1
+    assert s.counters()["swept"] == 1
+
+
+def test_fifo_log_eviction():
+    # 64 KiB log, 1 KiB values: only the newest ~64 survive
+    s = make(log=64 << 10, nb=1 << 8, max_item=4096)
+    keys = [f"/e/{i}".encode() for i in range(300)]
+    for i in range(0, 300, 10):
+        s.set_many(keys[i : i + 10], [bytes([i % 256]) * 1000] * 10)
+    got = s.get_many(keys)
+    alive = [i for i, g in enumerate(got) if g is not None]
+    assert alive, "nothing survived"
+    assert min(alive) > 200 and max(alive) == 299
+    assert all(got[i] == bytes([(i // 10 * 10) % 256]) * 1000 for i in alive)
+
+
+def test_too_large_rejected():
+    s = make(max_item=100)
+    s.set_many([b"/big", b"/ok"], [b"z" * 101, b"z" * 100])
+    assert s.get_many([b"/big", b"/ok"]) == [None, b"z" * 100]
+    assert s.counters()["set_dropped"] == 1
+
+
+def test_bucket_overflow_evicts_oldest():
+    # 2 buckets x 4 entries = 8 slots: the 9th..20th keys must displace older ones
+    s = make(log=1 << 20, nb=2, max_item=64)
+    keys = [f"/o/{i}".encode() for i in range(20)]
+    for k in keys:
+        s.set_many([k], [k])
+    got = s.get_many(keys)
+    assert sum(g is not None for g in got) == 8
+    assert got[-1] == keys[-1]
+    assert s.counters()["set_evicted"] == 12
+
+
+def test_flush():
+    s = make()
+    s.set_many([b"/f"], [b"v"])
+    s.flush()
+    assert s.get_many([b"/f"]) == [None]
+
+
+def test_scan_and_segcopy_host():
+    x = torch.tensor([16, 0, 32, 48], dtype=torch.int64)
+    off = R.exclusive_scan(x)
+    assert off.tolist() == [0, 16, 16, 48, 96]
+    src = torch.arange(256, dtype=torch.int64).to(torch.uint8)
+    src_off = torch.tensor([64, 0, 16, 128], dtype=torch.int64)
+    dst = torch.zeros(96, dtype=torch.uint8)
+    R.segcopy(src, src_off, off, dst)
+    assert dst[:16].tolist() == list(range(64, 80))
+    assert dst[16:48].tolist() == list(range(16, 48))
+    assert dst[48:96].tolist() == list(range(128, 176))

@@ -1,0 +1,81 @@
+"""Multi-process sharded cache over gloo (CPU shards, world_size 2 and 3)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+
+        shard = CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu")
+        sc = ShardedCache(shard)
+        # every rank writes its own keys (some colliding keys written by all ranks)
+        keys = [f"/r{rank}/{i}".encode() for i in range(300)] + [b"/shared"]
+        vals = [f"{rank}:{i}".encode() * (1 + i % 11) for i in range(300)] + [b"s"]
+        v, vo, vl = pack_values(vals)
+        sc.set(SetBatch(digest_strings(keys), v, vo, vl,
+                        flags=torch.full((301,), rank, dtype=torch.int32)))
+        dist.barrier()
+        # read everybody's keys
+        allkeys, expect = [], []
+        for r in range(world):
+            allkeys += [f"/r{r}/{i}".encode() for i in range(300)]
+            expect += [f"{r}:{i}".encode() * (1 + i % 11) for i in range(300)]
+        allkeys += [b"/nothing-here", b"/shared"]
+        res = sc.get(digest_strings(allkeys))
+        recs = unpack_records(res.data, res.off, res.size)
+        got = [r[0] if r else None for r in recs]
+        assert got[: len(expect)] == expect
+        assert got[-2] is None and got[-1] == b"s"
+        # flags travel with the payload
+        assert all(recs[r * 300][1] == r for r in range(world))
+        # keys live only on their owner shard
+        owned = shard.sweep()[0]
+        total = sc.counters()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, owned)
+        assert sum(gathered) == 300 * world + 1
+        # delete through the routed path
+        found = sc.delete(digest_strings([f"/r{(rank + 1) % world}/0".encode(), b"/zz"]))
+        assert found.tolist() == [True, False]
+        dist.barrier()
+        q.put((rank, "ok", total["get_ops"]))
+    except BaseException as e:  # surface the failure in the parent
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_cache_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    fails = [r for r in results if r[1] != "ok"]
+    assert not fails, fails[0][2]
+    assert all(r[2] == world * (300 * world + 2) for r in results)

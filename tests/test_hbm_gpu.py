@@ -1,0 +1,184 @@
+"""HIP kernels vs the host (DRAM) engine / plain PyTorch references. GPU only."""
+import numpy as np
+import pytest
+import torch
+
+from shellac_amd.ops.cache import (CacheShard, digest_packed, digest_strings, item_bytes,
+                                   pack_values, unpack_records)
+from shellac_amd.ops import routing as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(log=1 << 24, nb=1 << 12, max_item=1 << 16, dev=None):
+    return CacheShard(log, nb, max_item, dev), CacheShard(log, nb, max_item, "cpu")
+
+
+def _batch(keys, vals, dev):
+    d = digest_strings(keys)
+    v, vo, vl = pack_values(vals)
+    return d, v, vo, vl
+
+
+def _get_both(g, h, keys, now):
+    d = digest_strings(keys)
+    og, offg, sg = g.get(d.to(g.device), now=now)
+    oh, offh, sh = h.get(d, now=now)
+    return unpack_records(og, offg, sg), unpack_records(oh, offh, sh), sg.cpu(), sh
+
+
+def test_native_extension_is_loaded(core):
+    import shellac_amd
+
+    assert core.device_count() >= 1
+    assert core.__file__.startswith(shellac_amd.__path__[0])
+
+
+def test_roundtrip_matches_host_engine(cuda_dev):
+    g, h = _pair(dev=cuda_dev)
+    rng = np.random.default_rng(0)
+    keys = [f"/obj/{i}".encode() for i in range(3000)]
+    vals = [rng.integers(0, 256, size=int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+            for _ in keys]
+    d, v, vo, vl = _batch(keys, vals, cuda_dev)
+    fl = torch.arange(len(keys), dtype=torch.int32)
+    now = 10
+    g.store(d.to(cuda_dev), v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev), fl.to(cuda_dev), now=now)
+    h.store(d, v, vo, vl, fl, now=now)
+    probe = keys + [f"/miss/{i}".encode() for i in range(500)]
+    rg, rh, sg, sh = _get_both(g, h, probe, now)
+    assert torch.equal(sg, sh)
+    assert rg == rh
+    assert [r[0] for r in rg[:3000]] == vals
+    assert g.head() == h.head()
+    cg, ch = g.counters(), h.counters()
+    for k in ("get_ops", "get_hits", "get_bytes", "set_ops", "set_bytes", "set_dropped"):
+        assert cg[k] == ch[k], k
+
+
+def test_duplicate_keys_in_batch_last_wins(cuda_dev):
+    g, h = _pair(dev=cuda_dev)
+    keys = [b"/dup"] * 50 + [f"/u/{i}".encode() for i in range(50)] + [b"/dup", b"/u/3"]
+    vals = [f"v{i}".encode() * (i + 1) for i in range(len(keys))]
+    d, v, vo, vl = _batch(keys, vals, cuda_dev)
+    g.store(d.to(cuda_dev), v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev), now=1)
+    h.store(d, v, vo, vl, now=1)
+    rg, rh, _, _ = _get_both(g, h, [b"/dup", b"/u/3", b"/u/4"], 1)
+    assert rg == rh
+    assert rg[0][0] == vals[100] and rg[1][0] == vals[101]
+
+
+def test_many_batches_fifo_eviction_matches_host(cuda_dev):
+    g, h = _pair(log=1 << 20, nb=1 << 14, max_item=1 << 14, dev=cuda_dev)
+    rng = np.random.default_rng(1)
+    allkeys = [f"/f/{i}".encode() for i in range(6000)]
+    for b in range(12):
+        ks = [allkeys[j] for j in rng.integers(0, len(allkeys), size=400)]
+        vs = [rng.integers(0, 256, size=int(rng.integers(1, 3000)), dtype=np.uint8).tobytes()
+              for _ in ks]
+        d, v, vo, vl = _batch(ks, vs, cuda_dev)
+        g.store(d.to(cuda_dev), v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev), now=5)
+        h.store(d, v, vo, vl, now=5)
+    assert g.head() == h.head() and g.head() > (1 << 20)  # the log wrapped
+    rg, rh, sg, sh = _get_both(g, h, allkeys, 5)
+    assert rg == rh
+    assert sum(r is not None for r in rg) > 100
+
+
+def test_ttl_delete_sweep(cuda_dev):
+    g, h = _pair(dev=cuda_dev)
+    keys = [f"/t/{i}".encode() for i in range(1000)]
+    d, v, vo, vl = _batch(keys, [b"x" * 33] * 1000, cuda_dev)
+    ex = torch.tensor([0 if i % 3 == 0 else 50 + i % 7 for i in range(1000)], dtype=torch.int32)
+    for s, dv in ((g, cuda_dev), (h, "cpu")):
+        s.store(d.to(dv), v.to(dv), vo.to(dv), vl.to(dv), expire=ex.to(dv), now=40)
+    fg = g.remove(d[:100].to(cuda_dev), now=40).cpu()
+    fh = h.remove(d[:100], now=40)
+    assert torch.equal(fg, fh) and bool(fg.all())
+    for now in (40, 52, 54, 60):
+        rg, rh, _, _ = _get_both(g, h, keys, now)
+        assert rg == rh, now
+    assert g.sweep(now=54) == h.sweep(now=54)
+
+
+def test_bucket_overflow_eviction_invariants(cuda_dev):
+    g = CacheShard(1 << 20, 2, 64, cuda_dev)  # 8 slots total
+    keys = [f"/o/{i}".encode() for i in range(20)]
+    for k in keys:  # one key per batch: deterministic order
+        g.set_many([k], [k])
+    got = g.get_many(keys)
+    assert sum(x is not None for x in got) == 8
+    assert got[-1] == keys[-1]
+    assert g.counters()["set_evicted"] == 12
+
+
+def test_digest_kernel_matches_host(cuda_dev):
+    keys = [f"/digest/{i}/".encode() * (i % 9) for i in range(777)]
+    from shellac_amd.ops.cache import pack_bytes
+
+    buf, offs = pack_bytes(keys)
+    bt = torch.from_numpy(np.concatenate([buf, np.zeros(1, np.uint8)])).to(cuda_dev)
+    ot = torch.from_numpy(offs).to(cuda_dev)
+    assert torch.equal(digest_packed(bt, ot).cpu(), digest_strings(keys))
+
+
+def test_routing_kernels_match_host(cuda_dev):
+    from shellac_amd.parallel.ring import ShardRing
+
+    ring = ShardRing(list(range(8)))
+    keys = digest_strings([f"/route/{i}".encode() for i in range(20000)])
+    pts, own = ring.tensors("cpu")
+    dh, ch = R.route(keys, pts, own, 8)
+    pg, og = ring.tensors(cuda_dev)
+    dg, cgt = R.route(keys.to(cuda_dev), pg, og, 8)
+    assert torch.equal(dg.cpu(), dh) and torch.equal(cgt.cpu(), ch)
+    perm = R.scatter_positions(dg, cgt)
+    assert sorted(perm.cpu().tolist()) == list(range(20000))
+    grouped = R.permute(keys.to(cuda_dev), perm)
+    gd = R.permute(dg.view(-1, 1), perm).view(-1)
+    assert bool((gd[1:] >= gd[:-1]).all())
+    assert torch.equal(grouped.index_select(0, perm).cpu(), keys)
+
+
+def test_scan_and_segcopy_kernels(cuda_dev):
+    g = torch.Generator().manual_seed(3)
+    n = 50000
+    sizes = (torch.randint(0, 200, (n,), generator=g) * 16) * (torch.rand(n, generator=g) > 0.3)
+    off_h = R.exclusive_scan(sizes)
+    off_d = R.exclusive_scan(sizes.to(cuda_dev))
+    assert torch.equal(off_h, off_d.cpu())
+    src = torch.randint(0, 256, (1 << 22,), generator=g, dtype=torch.uint8)
+    src_off = (torch.randint(0, (1 << 22) - 4096, (n,), generator=g) // 16) * 16
+    total = int(off_h[-1])
+    dh = torch.zeros(total, dtype=torch.uint8)
+    R.segcopy(src, src_off, off_h, dh)
+    dd = torch.zeros(total, dtype=torch.uint8, device=cuda_dev)
+    R.segcopy(src.to(cuda_dev), src_off.to(cuda_dev), off_d, dd)
+    assert torch.equal(dh, dd.cpu())
+
+
+def test_mfma_hello_matches_fp32_reference(cuda_dev):
+    from shellac_amd.ops.smoke import mfma_hello
+
+    a = torch.randn(16, 32, 16, device=cuda_dev).to(torch.bfloat16)
+    # asymmetric B catches a transposed C write
+    b = (torch.arange(16 * 32, device=cuda_dev, dtype=torch.float32).view(16, 32) / 97.0)
+    b = (b.unsqueeze(0).repeat(16, 1, 1) + torch.randn(16, 16, 32, device=cuda_dev)).to(torch.bfloat16)
+    c = mfma_hello(a, b)
+    ref = torch.bmm(a.float(), b.float())
+    torch.testing.assert_close(c, ref, atol=1e-3, rtol=1e-4)
+
+
+def test_sharded_cache_single_rank_gpu(cuda_dev):
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(20000, cuda_dev, pool_bytes=1 << 20)
+    shard = CacheShard(1 << 26, 1 << 14, 1 << 16, cuda_dev)
+    sc = ShardedCache(shard)
+    sc.set(wl.set_batch(torch.arange(20000, device=cuda_dev)))
+    ids = wl.sample_ids(5000, 9)
+    res = sc.get(wl.digests.index_select(0, ids).contiguous())
+    recs = unpack_records(res.data, res.off, res.size)
+    for i, r in zip(ids.tolist()[:500], recs[:500]):
+        assert r is not None and r[0] == wl.expected_value(i)
