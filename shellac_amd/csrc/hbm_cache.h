@@ -74,8 +74,7 @@ class HbmCache {
   uint8_t* log_ = nullptr;
   Entry* index_ = nullptr;
   uint64_t* head_ = nullptr;         // device: logical write head
-  unsigned int* ticket_ = nullptr;   // device: last-block ticket for head advance
-  CacheCounters* ctr_ = nullptr;     // device counters
+  CacheCounters* ctr_ = nullptr;     // device counters (64 shards)
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
   // SET workspace

@@ -5,19 +5,23 @@
 //                  coalesced 128-B lines), pair-lane shuffle joins the {digest}
 //                  and {loc,vlen,expire} halves of each entry, max-reduce picks
 //                  the newest live match. No dependent read of the value log.
-//   k_segcopy      load-balanced byte mover: each workgroup owns a 32 KiB tile
-//                  of the *output*, finds the segments covering it (binary search
-//                  of the offsets staged in LDS) and every lane moves 16 B per
-//                  step, so item-size skew never idles lanes. Used for GET
-//                  gathers and for packing SET payloads for the all-to-all.
+//   k_segcopy      load-balanced byte mover: each workgroup owns a 64 KiB tile
+//                  of the *output*, finds the segments covering it (block-wide
+//                  128-ary search, then per-lane binary search of offsets staged
+//                  in LDS) and every lane moves 16 x 16 B, so item-size skew
+//                  never idles lanes. Used for GET gathers, SET log writes and
+//                  packing SET payloads for the all-to-all.
 //   k_set_dedupe   batch-local open-addressing table: the last SET of a key in a
 //                  batch wins (request order = memcached/HTTP pipelining order).
 //   k_set_copy     load-balanced writer of [ItemHeader|value] into the log at
 //                  head + exclusive-scan(item sizes): batch allocation is a scan.
 //   k_set_index    16 lanes per key: two-choice insert with a 64-bit CAS on the
 //                  entry's loc word; replaces the key's own entry, else a dead
-//                  slot in the emptier bucket, else evicts the oldest item. The
-//                  last workgroup (ticket) advances the log head.
+//                  slot in the emptier bucket, else evicts the oldest item;
+//                  k_advance_head then publishes the new log head.
+//   All per-op counters are block-reduced and added to one of 64 counter
+//   shards (one atomic per block per field; same-address fan-in measured at
+//   ~12 ns/atomic would otherwise serialise a 64K-wave probe into milliseconds).
 //   k_delete, k_sweep, k_digest, k_route*, k_permute, k_mfma_hello.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -41,9 +45,11 @@ namespace shellac {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTileChunks = 2048;          // 16-B chunks per segcopy tile (32 KiB)
+constexpr int kTileChunks = 4096;          // 16-B chunks per segcopy tile (64 KiB)
 constexpr int kChunksPerThread = kTileChunks / kBlock;
 constexpr int kTileSegCap = 2048;          // segments staged in LDS per tile
+constexpr int kMaxGrid = 2048;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));             // 8 x 256-thread blocks per CU x 256 CUs
 
 struct DeviceGuard {
   int prev = -1;
@@ -68,6 +74,42 @@ inline int grid_for(int64_t work_items, int per_block, int cap = 8192) {
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
   for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
   return v;
+}
+
+constexpr int kCtrShards = 64;  // counters spread over 64 cache lines (no same-address fan-in)
+
+// Block-wide sum of up to 3 per-thread counters, then ONE atomic per field per
+// block into this block's counter shard. Every thread of the block must call it.
+__device__ __forceinline__ void block_count(CacheCounters* shards, unsigned long long a,
+                                            unsigned long long CacheCounters::*fa,
+                                            unsigned long long b = 0,
+                                            unsigned long long CacheCounters::*fb = nullptr,
+                                            unsigned long long c = 0,
+                                            unsigned long long CacheCounters::*fc = nullptr) {
+  __shared__ unsigned long long s_red[3][kBlock / 64];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[0][w] = a;
+    s_red[1][w] = b;
+    s_red[2][w] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) {
+      t0 += s_red[0][k];
+      t1 += s_red[1][k];
+      t2 += s_red[2][k];
+    }
+    CacheCounters* c_ = shards + (blockIdx.x & (kCtrShards - 1));
+    if (t0) atomicAdd(&(c_->*fa), t0);
+    if (fb && t1) atomicAdd(&(c_->*fb), t1);
+    if (fc && t2) atomicAdd(&(c_->*fc), t2);
+  }
 }
 
 __device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
@@ -120,14 +162,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
       }
     }
   }
-  ops = wave_sum(ops);
-  hits = wave_sum(hits);
-  bytes = wave_sum(bytes);
-  if ((threadIdx.x & 63) == 0 && ops) {
-    atomicAdd(&ctr->get_ops, ops);
-    atomicAdd(&ctr->get_hits, hits);
-    atomicAdd(&ctr->get_bytes, bytes);
-  }
+  block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
+              &CacheCounters::get_bytes);
 }
 
 // ---------------------------------------------------------------------------------
@@ -153,9 +189,51 @@ __device__ __forceinline__ int64_t seg_search_global(const uint64_t* off, int64_
   return lo;
 }
 
+// Cooperative search: each half of the block (128 lanes) finds, for its own x,
+// the last j in [0, n1) with off[j] <= x by 128-ary narrowing (one load per lane
+// per round, ~3 rounds for 10^6 segments) instead of one lane's ~20 dependent
+// loads. Every thread of the block must call it; results land in s_res[0..1].
+__device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, int64_t n1,
+                                            uint64_t x0, uint64_t x1, int64_t* s_lo,
+                                            int64_t* s_hi, int* s_cnt) {
+  const int h = threadIdx.x >> 7, t = threadIdx.x & 127, w = threadIdx.x >> 6;
+  const uint64_t x = h ? x1 : x0;
+  if (threadIdx.x < 2) {
+    s_lo[threadIdx.x] = 0;
+    s_hi[threadIdx.x] = n1;
+  }
+  __syncthreads();
+  for (int round = 0; round < 16; ++round) {
+    const int64_t lo = s_lo[h], hi = s_hi[h];
+    const bool done = (s_hi[0] - s_lo[0] <= 1) && (s_hi[1] - s_lo[1] <= 1);
+    if (done) break;  // uniform: every thread read the same LDS words
+    const int64_t len = hi - lo;
+    // probe p_t = lo + ceil(len*(t+1)/128) for t < 127 (p_t in (lo, hi))
+    bool ok = false;
+    if (len > 1 && t < 127) {
+      const int64_t p = lo + (len * (t + 1) + 127) / 128;
+      ok = p < hi && off[p] <= x;
+    }
+    const unsigned long long b = __ballot(ok);
+    __syncthreads();  // all lanes have read s_lo/s_hi of this round
+    if ((threadIdx.x & 63) == 0) s_cnt[w] = __popcll(b);
+    __syncthreads();
+    if (t == 0 && len > 1) {
+      const int k = s_cnt[2 * h] + s_cnt[2 * h + 1];  // probes 0..k-1 passed (monotone)
+      const int64_t nlo = k > 0 ? lo + (len * k + 127) / 128 : lo;
+      const int64_t nhi = k < 127 ? lo + (len * (k + 1) + 127) / 128 : hi;
+      s_lo[h] = nlo;
+      s_hi[h] = nhi < hi ? nhi : hi;
+    }
+    __syncthreads();
+  }
+}
+
 // Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w.
 // Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
 // src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w.
+// Each workgroup owns 64 KiB tiles of the destination; each lane resolves its 16
+// chunks' segments first, then issues 8 independent 16-B loads before their stores.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_segcopy(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -166,21 +244,16 @@ __global__ __launch_bounds__(kBlock) void k_segcopy(
     const uint64_t* __restrict__ head_ptr, uint64_t cap) {
   __shared__ uint64_t s_off[kTileSegCap + 1];
   __shared__ uint64_t s_src[kTileSegCap];
-  __shared__ int64_t s_j0, s_cnt;
+  __shared__ int64_t s_lo[2], s_hi[2];
+  __shared__ int s_cnt[kBlock / 64];
   const uint64_t total = dst_off[n];
   const int64_t nchunks = (int64_t)(total >> 4);
   const uint64_t base = MODE == 1 ? *head_ptr : 0;
   for (int64_t tile = blockIdx.x; tile * kTileChunks < nchunks; tile += gridDim.x) {
     const int64_t c0 = tile * kTileChunks;
     const int64_t c1 = min(c0 + (int64_t)kTileChunks, nchunks);
-    if (threadIdx.x == 0) {
-      const int64_t j0 = seg_search_global(dst_off, n + 1, (uint64_t)c0 << 4);
-      const int64_t j1 = seg_search_global(dst_off, n + 1, ((uint64_t)c1 << 4) - 1);
-      s_j0 = j0;
-      s_cnt = j1 - j0 + 1;
-    }
-    __syncthreads();
-    const int64_t j0 = s_j0, cnt = s_cnt;
+    block_find2(dst_off, n + 1, (uint64_t)c0 << 4, ((uint64_t)c1 << 4) - 1, s_lo, s_hi, s_cnt);
+    const int64_t j0 = s_lo[0], cnt = s_lo[1] - s_lo[0] + 1;
     const bool staged = cnt <= kTileSegCap;
     if (staged) {
       for (int64_t k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
@@ -191,40 +264,54 @@ __global__ __launch_bounds__(kBlock) void k_segcopy(
     }
     __syncthreads();
     int64_t jl = 0;
-#pragma unroll 2
-    for (int u = 0; u < kChunksPerThread; ++u) {
-      const int64_t c = c0 + (int64_t)u * kBlock + threadIdx.x;
-      if (c >= c1) break;
-      const uint64_t x = (uint64_t)c << 4;
-      int64_t j;
-      uint64_t seg_start, seg_src;
-      if (staged) {
-        jl = seg_search(s_off, jl, cnt, x);
-        j = j0 + jl;
-        seg_start = s_off[jl];
-        seg_src = s_src[jl];
-      } else {
-        j = j0 + seg_search(dst_off + j0, 0, cnt, x);
-        seg_start = dst_off[j];
-        seg_src = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
-      }
-      const uint64_t w = x - seg_start;
-      if (MODE == 0) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + seg_src + w);
-        *reinterpret_cast<uint4*>(dst + x) = v;
-      } else {
-        uint4 v;
-        if (w == 0) {
-          const Digest d = keys[j];
-          v = make_uint4((uint32_t)d.lo, (uint32_t)(d.lo >> 32), (uint32_t)d.hi,
-                         (uint32_t)(d.hi >> 32));
-        } else if (w == 16) {
-          v = make_uint4(vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      constexpr int U = kChunksPerThread / 2;
+      const u32x4* sp[U];
+      u32x4 hv[U];
+      uint64_t dofs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t c = c0 + (int64_t)(half * U + u) * kBlock + threadIdx.x;
+        sp[u] = nullptr;
+        dofs[u] = ~0ull;
+        if (c >= c1) continue;
+        const uint64_t x = (uint64_t)c << 4;
+        int64_t j;
+        uint64_t seg_start, seg_src;
+        if (staged) {
+          jl = seg_search(s_off, jl, cnt, x);
+          j = j0 + jl;
+          seg_start = s_off[jl];
+          seg_src = s_src[jl];
         } else {
-          v = *reinterpret_cast<const uint4*>(src + src_off[j] + (w - kItemHeaderBytes));
+          j = j0 + seg_search(dst_off + j0, 0, cnt, x);
+          seg_start = dst_off[j];
+          seg_src = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
         }
-        *reinterpret_cast<uint4*>(dst + seg_src + w) = v;
+        const uint64_t w = x - seg_start;
+        if (MODE == 0) {
+          sp[u] = reinterpret_cast<const u32x4*>(src + seg_src + w);
+          dofs[u] = x;
+        } else {
+          dofs[u] = seg_src + w;
+          if (w == 0) {
+            const Digest d = keys[j];
+            hv[u] = u32x4{(uint32_t)d.lo, (uint32_t)(d.lo >> 32), (uint32_t)d.hi,
+                          (uint32_t)(d.hi >> 32)};
+          } else if (w == 16) {
+            hv[u] = u32x4{vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic};
+          } else {
+            sp[u] = reinterpret_cast<const u32x4*>(src + src_off[j] + (w - kItemHeaderBytes));
+          }
+        }
       }
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = sp[u] ? __builtin_nontemporal_load(sp[u]) : hv[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (dofs[u] != ~0ull) *reinterpret_cast<u32x4*>(dst + dofs[u]) = v[u];
     }
     __syncthreads();
   }
@@ -268,19 +355,14 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
     ++ops;
     dropped += win ? 0 : 1;
   }
-  ops = wave_sum(ops);
-  dropped = wave_sum(dropped);
-  if ((threadIdx.x & 63) == 0 && ops) {
-    atomicAdd(&ctr->set_ops, ops);
-    atomicAdd(&ctr->set_dropped, dropped);
-  }
+  block_count(ctr, ops, &CacheCounters::set_ops, dropped, &CacheCounters::set_dropped);
 }
 
 __global__ __launch_bounds__(kBlock) void k_set_index(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
-    uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now, unsigned int* ticket,
+    const uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now,
     CacheCounters* __restrict__ ctr) {
   const int l16 = threadIdx.x & 15;
   const uint64_t base = *head_ptr;
@@ -357,24 +439,14 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       if (ok) break;
     }
   }
-  evicted = wave_sum(evicted);
-  bytes = wave_sum(bytes);
-  if ((threadIdx.x & 63) == 0 && (evicted | bytes)) {
-    atomicAdd(&ctr->set_evicted, evicted);
-    atomicAdd(&ctr->set_bytes, bytes);
-  }
-  // The last workgroup to finish publishes the new head (every workgroup has
-  // already read `base`; the next kernel on the stream observes the store).
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned int t = atomicAdd(ticket, 1u);
-    if (t == gridDim.x - 1) {
-      *head_ptr = head_new;
-      *ticket = 0u;
-      __threadfence();
-    }
-  }
+  block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes);
+}
+
+// Publishes the new log head after k_set_index (a separate launch: stream order
+// guarantees every workgroup of k_set_index read the old head first).
+__global__ void k_advance_head(uint64_t* __restrict__ head_ptr, const uint64_t* __restrict__ off,
+                               int64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *head_ptr += off[n];
 }
 
 // ---------------------------------------------------------------------------------
@@ -414,12 +486,7 @@ __global__ __launch_bounds__(kBlock) void k_delete(const Digest* __restrict__ ke
       if (found) found[i] = (uint8_t)f;
     }
   }
-  ops = wave_sum(ops);
-  hits = wave_sum(hits);
-  if ((threadIdx.x & 63) == 0 && ops) {
-    atomicAdd(&ctr->del_ops, ops);
-    atomicAdd(&ctr->del_hits, hits);
-  }
+  block_count(ctr, ops, &CacheCounters::del_ops, hits, &CacheCounters::del_hits);
 }
 
 __global__ __launch_bounds__(kBlock) void k_sweep(Entry* __restrict__ index, uint64_t nslots,
@@ -443,13 +510,12 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Entry* __restrict__ index, uin
       ++swept;
     }
   }
+  block_count(ctr, swept, &CacheCounters::swept);
   live = wave_sum(live);
   bytes = wave_sum(bytes);
-  swept = wave_sum(swept);
   if ((threadIdx.x & 63) == 0) {
     if (live) atomicAdd(&out[0], live);
     if (bytes) atomicAdd(&out[1], bytes);
-    if (swept) atomicAdd(&ctr->swept, swept);
   }
 }
 
@@ -644,14 +710,12 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&log_, cfg_.log_bytes + slack));
   HIP_OK(hipMalloc(&index_, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMalloc(&head_, 64));
-  HIP_OK(hipMalloc(&ticket_, 64));
-  HIP_OK(hipMalloc(&ctr_, sizeof(CacheCounters)));
+  HIP_OK(hipMalloc(&ctr_, kCtrShards * sizeof(CacheCounters)));
   HIP_OK(hipMalloc(&scratch_, 64));
-  HIP_OK(hipHostMalloc(&host_buf_, 64 * sizeof(uint64_t), hipHostMallocDefault));
+  HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
-  HIP_OK(hipMemset(ticket_, 0, 64));
-  HIP_OK(hipMemset(ctr_, 0, sizeof(CacheCounters)));
+  HIP_OK(hipMemset(ctr_, 0, kCtrShards * sizeof(CacheCounters)));
   HIP_OK(hipDeviceSynchronize());
 }
 
@@ -661,7 +725,6 @@ HbmCache::~HbmCache() {
   (void)hipFree(log_);
   (void)hipFree(index_);
   (void)hipFree(head_);
-  (void)hipFree(ticket_);
   (void)hipFree(ctr_);
   (void)hipFree(scratch_);
   (void)hipHostFree(host_buf_);
@@ -726,7 +789,7 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   }
   ensure_scan_ws(n);
   HIP_OK(hipMemsetAsync(size + n, 0, sizeof(uint64_t), s));
-  hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, 16384)), dim3(kBlock), 0, s, keys, n,
+  hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, loc, size, ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
@@ -751,20 +814,20 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   const uint64_t tslots = (uint64_t)dd_mask_ + 1;
   HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
   HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
-  const int grid = grid_for(n, kBlock);
+  const int grid = grid_for(n, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
-  hipLaunchKernelGGL(k_set_size, dim3(grid_for(n + 1, kBlock)), dim3(kBlock), 0, s, vlen, n,
+  hipLaunchKernelGGL(k_set_size, dim3(grid_for(n + 1, kBlock, kMaxGrid)), dim3(kBlock), 0, s, vlen, n,
                      dd_win_, dd_slot_, cfg_.max_item, set_size_, ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(set_size_, set_off_, n, scan_tmp_, scan_tmp_bytes_, s);
   hipLaunchKernelGGL(k_segcopy<1>, dim3(2048), dim3(kBlock), 0, s, values, val_off, set_off_, n,
                      log_, keys, vlen, flags, expire, head_, cfg_.log_bytes);
   HIP_OK(hipGetLastError());
-  const int igrid = grid_for(n * 16, kBlock, 16384);
+  const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
-                     vlen, expire, index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, ticket_,
-                     ctr_);
+                     vlen, expire, index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, ctr_);
+  hipLaunchKernelGGL(k_advance_head, dim3(1), dim3(64), 0, s, head_, set_off_, n);
   HIP_OK(hipGetLastError());
 }
 
@@ -772,7 +835,7 @@ void HbmCache::remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t no
   if (n <= 0) return;
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
-  hipLaunchKernelGGL(k_delete, dim3(grid_for(n * 16, kBlock, 16384)), dim3(kBlock), 0, s, keys, n,
+  hipLaunchKernelGGL(k_delete, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, found, ctr_);
   HIP_OK(hipGetLastError());
 }
@@ -801,10 +864,15 @@ void HbmCache::flush(hipStream_t s) {
 CacheCounters HbmCache::counters(hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
-  CacheCounters c;
-  HIP_OK(hipMemcpyAsync(host_buf_, ctr_, sizeof(CacheCounters), hipMemcpyDeviceToHost, s));
+  CacheCounters c{};
+  HIP_OK(hipMemcpyAsync(host_buf_, ctr_, kCtrShards * sizeof(CacheCounters),
+                        hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
-  std::memcpy(&c, host_buf_, sizeof(CacheCounters));
+  const auto* sh = reinterpret_cast<const unsigned long long*>(host_buf_);
+  auto* dst = reinterpret_cast<unsigned long long*>(&c);
+  constexpr int kWords = sizeof(CacheCounters) / sizeof(unsigned long long);
+  for (int k = 0; k < kCtrShards; ++k)
+    for (int w = 0; w < kWords; ++w) dst[w] += sh[k * kWords + w];
   return c;
 }
 

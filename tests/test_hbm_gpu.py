@@ -72,8 +72,8 @@ def test_many_batches_fifo_eviction_matches_host(cuda_dev):
     g, h = _pair(log=1 << 20, nb=1 << 14, max_item=1 << 14, dev=cuda_dev)
     rng = np.random.default_rng(1)
     allkeys = [f"/f/{i}".encode() for i in range(6000)]
-    for b in range(12):
-        ks = [allkeys[j] for j in rng.integers(0, len(allkeys), size=400)]
+    for b in range(24):
+        ks = [allkeys[j] for j in rng.integers(0, len(allkeys), size=200)]
         vs = [rng.integers(0, 256, size=int(rng.integers(1, 3000)), dtype=np.uint8).tobytes()
               for _ in ks]
         d, v, vo, vl = _batch(ks, vs, cuda_dev)
