@@ -1,0 +1,198 @@
+// Cache backends behind the proxy and the memcached-protocol shard server.
+//
+// The reference has exactly one: a blocking pylibmc client doing one TCP round
+// trip per request inside the reactor (src/python/shellac/server/Server.py:335
+// get, :432 set). Here every backend is asynchronous (completions are posted to
+// the calling reactor's Executor), so a slow cache never stalls the event loop:
+//
+//   DramBackend       striped host-DRAM shards (csrc/host_cache.cc), synchronous
+//                     fast path, no GPU needed;
+//   HbmBackend        one HBM shard per local MI355X (csrc/hbm_cache.hip), fed by a
+//                     batcher thread that coalesces the GETs/SETs of all reactors
+//                     into one kernel pipeline per GPU per tick;
+//   MemcachedBackend  memcached binary protocol over TCP to remote nodes (real
+//                     memcached or `shellac-cached`), ketama-routed, pipelined on
+//                     persistent connections, with node ejection + retry.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "digest.h"
+#include "host_cache.h"
+#include "ketama.h"
+#include "net.h"
+#include "stream_buf.h"
+
+namespace shellac {
+
+class HbmCache;
+
+class Executor {
+ public:
+  virtual ~Executor() = default;
+  virtual void post(std::function<void()> fn) = 0;  // run fn on the executor's thread
+};
+
+struct CacheValue {
+  Bytes data;
+  uint32_t flags = 0;
+};
+using GetCallback = std::function<void(bool hit, CacheValue v)>;
+using DelCallback = std::function<void(bool found)>;
+using StatList = std::vector<std::pair<std::string, uint64_t>>;
+
+class CacheBackend {
+ public:
+  virtual ~CacheBackend() = default;
+  // `done` runs on `ex`'s thread (inline for synchronous backends).
+  virtual void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) = 0;
+  virtual void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+                   uint32_t ttl_s) = 0;
+  virtual void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) = 0;
+  virtual void flush() = 0;
+  virtual std::string name() const = 0;
+  virtual void stats(StatList* out) = 0;
+};
+
+// 32-bit-point ring over digests, identical to shellac_amd.parallel.ring.ShardRing.
+class DigestRing {
+ public:
+  explicit DigestRing(int nshards, int points_per_shard = 160);
+  int owner(const Digest& d) const;
+
+ private:
+  std::vector<std::pair<uint32_t, int>> pts_;
+};
+
+class DramBackend : public CacheBackend {
+ public:
+  DramBackend(uint64_t bytes, uint32_t max_item, int stripes = 16);
+  void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
+  void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+           uint32_t ttl_s) override;
+  void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
+  void flush() override;
+  std::string name() const override { return "dram"; }
+  void stats(StatList* out) override;
+  uint32_t now() const;
+
+ private:
+  HostCache& shard(const Digest& d) { return *shards_[(d.hi >> 17) % shards_.size()]; }
+  std::vector<std::unique_ptr<HostCache>> shards_;
+  double epoch_;
+};
+
+struct HbmBackendConfig {
+  std::vector<int> devices{0};
+  uint64_t log_bytes_per_gpu = 8ull << 30;
+  uint64_t nbuckets_per_gpu = 1ull << 22;
+  uint32_t max_item = 1u << 20;
+  int batch_us = 50;        // max time a request waits for batch-mates
+  int max_batch = 65536;    // flush early when this many requests are queued
+};
+
+class HbmBackend : public CacheBackend {
+ public:
+  explicit HbmBackend(const HbmBackendConfig& cfg);
+  ~HbmBackend() override;
+  void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
+  void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+           uint32_t ttl_s) override;
+  void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
+  void flush() override;
+  std::string name() const override { return "hbm"; }
+  void stats(StatList* out) override;
+
+ private:
+  struct Req {
+    int kind;  // 0 get, 1 set, 2 del
+    Digest d;
+    Bytes value;
+    uint32_t flags = 0, ttl = 0;
+    Executor* ex = nullptr;
+    GetCallback gcb;
+    DelCallback dcb;
+  };
+  struct Dev;
+  void loop();
+  void run_batch(std::vector<Req>& batch);
+  uint32_t now() const;
+
+  HbmBackendConfig cfg_;
+  DigestRing ring_;
+  std::vector<std::unique_ptr<Dev>> devs_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Req> q_;
+  bool stop_ = false;
+  bool flush_req_ = false;
+  std::thread th_;
+  double epoch_;
+  std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};
+  std::atomic<uint64_t> batch_ns_{0};
+};
+
+struct MemcachedConfig {
+  std::vector<Addr> servers;
+  int retry_timeout_s = 2;     // ejected node is retried after this long
+  int connect_timeout_ms = 500;
+  int op_timeout_ms = 1000;
+};
+
+class MemcachedBackend : public CacheBackend {
+ public:
+  explicit MemcachedBackend(const MemcachedConfig& cfg);
+  ~MemcachedBackend() override;
+  void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
+  void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+           uint32_t ttl_s) override;
+  void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
+  void flush() override;
+  std::string name() const override { return "memcached"; }
+  void stats(StatList* out) override;
+
+ private:
+  struct Pending {
+    uint8_t op;
+    Executor* ex;
+    GetCallback gcb;
+    DelCallback dcb;
+    double t0;
+  };
+  struct Node;
+  struct Cmd {
+    std::string key;
+    uint8_t op;
+    Bytes value;
+    uint32_t flags, ttl;
+    Executor* ex;
+    GetCallback gcb;
+    DelCallback dcb;
+  };
+  void loop();
+  void submit(Cmd c);
+  void node_fail(int idx);
+  void drain_commands();
+  static std::string wire_key(const std::string& key);
+
+  MemcachedConfig cfg_;
+  KetamaRing ring_;
+  std::vector<std::unique_ptr<Node>> nodes_;
+  int epfd_ = -1, evfd_ = -1;
+  std::mutex mu_;
+  std::vector<Cmd> inbox_;
+  std::atomic<bool> stop_{false};
+  std::thread th_;
+  std::atomic<uint64_t> gets_{0}, hits_{0}, sets_{0}, errors_{0}, ejections_{0};
+};
+
+}  // namespace shellac

@@ -1,2 +1,187 @@
+// pybind11 registration: ketama ring, cache backends, proxy server, memcached server.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <condition_variable>
+
+#include "backend.h"
 #include "bind_parts.h"
-void bind_net(pybind11::module_& m) { (void)m; }
+#include "ketama.h"
+#include "mcserver.h"
+#include "proxy.h"
+
+namespace py = pybind11;
+using namespace shellac;
+
+namespace {
+
+// Executes posted completions inline on whatever thread completes them.
+class InlineExecutor : public Executor {
+ public:
+  void post(std::function<void()> fn) override { fn(); }
+};
+InlineExecutor g_inline;
+
+struct BackendHandle {
+  std::shared_ptr<CacheBackend> be;
+};
+
+py::object blocking_get(CacheBackend* be, const std::string& key) {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false, hit = false;
+  CacheValue val;
+  {
+    py::gil_scoped_release nogil;
+    const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(key.data()), key.size());
+    be->get(key, d, &g_inline, [&](bool h, CacheValue v) {
+      std::lock_guard<std::mutex> lk(mu);
+      hit = h;
+      val = std::move(v);
+      done = true;
+      cv.notify_all();
+    });
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+  }
+  if (!hit || !val.data) return py::none();
+  return py::make_tuple(py::bytes(*val.data), val.flags);
+}
+
+bool blocking_del(CacheBackend* be, const std::string& key) {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false, found = false;
+  py::gil_scoped_release nogil;
+  const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(key.data()), key.size());
+  be->del(key, d, &g_inline, [&](bool f) {
+    std::lock_guard<std::mutex> lk(mu);
+    found = f;
+    done = true;
+    cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(mu);
+  cv.wait(lk, [&] { return done; });
+  return found;
+}
+
+}  // namespace
+
+void bind_net(py::module_& m) {
+  m.def("md5_hex", [](py::bytes b) { return md5_hex(std::string(b)); });
+
+  py::class_<KetamaRing>(m, "KetamaRing")
+      .def(py::init([](const std::vector<std::string>& names, uint32_t ppw) {
+             std::vector<KetamaRing::Node> nodes;
+             for (const auto& n : names) nodes.push_back(KetamaRing::Node{n, 1, true});
+             return new KetamaRing(nodes, ppw);
+           }),
+           py::arg("names"), py::arg("points_per_weight") = 160)
+      .def("pick", [](KetamaRing& r, py::bytes k) { return r.pick(std::string(k)); })
+      .def("set_alive", &KetamaRing::set_alive)
+      .def("points", &KetamaRing::points)
+      .def_static("key_hash", [](py::bytes k) {
+        std::string s = k;
+        return KetamaRing::key_hash(s.data(), s.size());
+      });
+
+  py::class_<BackendHandle>(m, "CacheBackend")
+      .def_property_readonly("name", [](BackendHandle& h) { return h.be->name(); })
+      .def("get", [](BackendHandle& h, py::bytes key) { return blocking_get(h.be.get(), key); })
+      .def("set", [](BackendHandle& h, py::bytes key, py::bytes value, uint32_t flags,
+                     uint32_t ttl) {
+        std::string k = key;
+        const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        h.be->set(k, d, std::make_shared<const std::string>(std::string(value)), flags, ttl);
+      }, py::arg("key"), py::arg("value"), py::arg("flags") = 0, py::arg("ttl") = 0)
+      .def("delete", [](BackendHandle& h, py::bytes key) { return blocking_del(h.be.get(), key); })
+      .def("flush", [](BackendHandle& h) { h.be->flush(); })
+      .def("stats", [](BackendHandle& h) {
+        StatList st;
+        h.be->stats(&st);
+        py::dict d;
+        for (auto& kv : st) d[py::str(kv.first)] = kv.second;
+        return d;
+      });
+
+  m.def("dram_backend", [](uint64_t bytes, uint32_t max_item, int stripes) {
+    return BackendHandle{std::make_shared<DramBackend>(bytes, max_item, stripes)};
+  }, py::arg("bytes"), py::arg("max_item") = 1u << 20, py::arg("stripes") = 16);
+  m.def("hbm_backend", [](std::vector<int> devices, uint64_t log_bytes_per_gpu,
+                          uint64_t nbuckets_per_gpu, uint32_t max_item, int batch_us,
+                          int max_batch) {
+    HbmBackendConfig c;
+    c.devices = std::move(devices);
+    c.log_bytes_per_gpu = log_bytes_per_gpu;
+    c.nbuckets_per_gpu = nbuckets_per_gpu;
+    c.max_item = max_item;
+    c.batch_us = batch_us;
+    c.max_batch = max_batch;
+    py::gil_scoped_release nogil;
+    return BackendHandle{std::make_shared<HbmBackend>(c)};
+  }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
+     py::arg("max_item") = 1u << 20, py::arg("batch_us") = 50, py::arg("max_batch") = 65536);
+  m.def("memcached_backend", [](const std::string& servers, int retry_s, int op_timeout_ms) {
+    MemcachedConfig c;
+    c.servers = resolve_list(servers, 11211);
+    c.retry_timeout_s = retry_s;
+    c.op_timeout_ms = op_timeout_ms;
+    return BackendHandle{std::make_shared<MemcachedBackend>(c)};
+  }, py::arg("servers"), py::arg("retry_s") = 2, py::arg("op_timeout_ms") = 1000);
+
+  py::class_<Proxy>(m, "Proxy")
+      .def(py::init([](const std::string& upstreams, py::object backend, uint16_t port,
+                       const std::string& bind, int threads, uint32_t ttl, bool compress,
+                       const std::string& policy, bool kill_switch, bool key_host,
+                       int client_timeout, int client_max_reqs, const std::string& balance,
+                       bool decode_gzip, int upstream_retry_s) {
+             ProxyConfig c;
+             c.upstreams = resolve_list(upstreams, 80);
+             c.port = port;
+             c.bind = bind;
+             c.threads = threads;
+             c.ttl = ttl;
+             c.compress = compress;
+             c.policy = policy;
+             c.kill_switch = kill_switch;
+             c.key_host = key_host;
+             c.client_timeout = client_timeout;
+             c.client_max_reqs = client_max_reqs;
+             c.balance = balance;
+             c.decode_gzip = decode_gzip;
+             c.upstream_retry_s = upstream_retry_s;
+             std::shared_ptr<CacheBackend> be;
+             if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
+             c.cache_enabled = be != nullptr;
+             return new Proxy(c, be);
+           }),
+           py::arg("upstreams"), py::arg("backend") = py::none(), py::arg("port") = 8080,
+           py::arg("bind") = "0.0.0.0", py::arg("threads") = 1, py::arg("ttl") = 170,
+           py::arg("compress") = false, py::arg("policy") = "rfc", py::arg("kill_switch") = true,
+           py::arg("key_host") = false, py::arg("client_timeout") = 30,
+           py::arg("client_max_reqs") = 1000, py::arg("balance") = "random",
+           py::arg("decode_gzip") = false, py::arg("upstream_retry_s") = 2)
+      .def("start", &Proxy::start)
+      .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Proxy::stop)
+      .def_property_readonly("port", &Proxy::port)
+      .def_property_readonly("running", &Proxy::running)
+      .def("stats_json", &Proxy::stats_json);
+
+  py::class_<CacheServer>(m, "CacheServer")
+      .def(py::init([](BackendHandle& be, uint16_t port, const std::string& bind, int threads) {
+             CacheServerConfig c;
+             c.port = port;
+             c.bind = bind;
+             c.threads = threads;
+             return new CacheServer(c, be.be);
+           }),
+           py::arg("backend"), py::arg("port") = 11211, py::arg("bind") = "0.0.0.0",
+           py::arg("threads") = 1)
+      .def("start", &CacheServer::start)
+      .def("stop", &CacheServer::stop)
+      .def("wait", &CacheServer::wait, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &CacheServer::port)
+      .def_property_readonly("running", &CacheServer::running)
+      .def("ops", &CacheServer::ops);
+}

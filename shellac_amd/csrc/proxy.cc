@@ -1,0 +1,930 @@
+// Native caching reverse proxy (see proxy.h for the reference map and fixes).
+#include "proxy.h"
+
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/timerfd.h>
+#include <sys/uio.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <deque>
+#include <random>
+#include <sstream>
+#include <unordered_map>
+
+#include "http.h"
+
+namespace shellac {
+
+namespace {
+
+constexpr uint64_t kListenId = 1, kEventId = 2, kTimerId = 3, kFirstConnId = 16;
+constexpr int kHistBuckets = 40;
+
+std::string simple_response(int code, const char* reason, const std::string& server,
+                            const std::string& body, const char* ctype = "text/plain",
+                            bool close = false) {
+  std::string s = "HTTP/1.1 " + std::to_string(code) + " " + reason + "\r\nServer: " + server +
+                  "\r\nContent-Type: " + ctype + "\r\nContent-Length: " +
+                  std::to_string(body.size()) + "\r\nConnection: " +
+                  (close ? "close" : "keep-alive") + "\r\n\r\n";
+  return s + body;
+}
+
+bool contains_ci(const std::string* h, const char* needle) {
+  if (!h) return false;
+  return to_lower(*h).find(needle) != std::string::npos;
+}
+
+// Cache-Control max-age / s-maxage (seconds), -1 if absent.
+long cc_max_age(const std::string* cc) {
+  if (!cc) return -1;
+  const std::string s = to_lower(*cc);
+  long best = -1;
+  for (const char* k : {"s-maxage=", "max-age="}) {
+    const size_t p = s.find(k);
+    if (p != std::string::npos) {
+      best = std::strtol(s.c_str() + p + std::strlen(k), nullptr, 10);
+      break;
+    }
+  }
+  return best;
+}
+
+}  // namespace
+
+struct Slot {
+  uint64_t seq = 0;
+  StreamBuf out;
+  bool ready = false;
+  bool close_after = false;
+  std::string fwd;  // serialized request for the miss path
+  std::string key;
+  Digest d{};
+  bool lookup = false, head = false, client_gzip = false;
+  int attempts = 0;
+  double t0 = 0;
+};
+
+struct Conn {
+  int fd = -1;
+  int kind = 0;  // 0 client, 1 upstream
+  uint64_t id = 0;
+  double ctime = 0, atime = 0;
+  bool dead = false;
+  bool out_armed = false;
+  virtual ~Conn() = default;
+};
+
+struct Upstream;
+
+struct Client : Conn {
+  HttpParser req{true};
+  std::deque<std::unique_ptr<Slot>> slots;
+  uint64_t next_seq = 1;
+  Upstream* up = nullptr;
+  int nreq = 0;
+  bool closing = false;  // stop parsing (bad request / EOF)
+  bool eof = false;      // peer finished sending: close after the last response
+  bool loopback = false;
+};
+
+struct Pend {
+  uint64_t client_id, seq;
+  std::string key;
+  Digest d;
+  bool lookup, head, client_gzip;
+};
+
+struct Upstream : Conn {
+  int server = 0;
+  bool connected = false;
+  StreamBuf out;
+  std::unique_ptr<HttpParser> resp;
+  std::deque<Pend> pend;
+  Client* owner = nullptr;
+  double ka_timeout = -1;
+  int ka_max = 1 << 30;
+  int count = 0;
+};
+
+class Reactor : public Executor {
+ public:
+  Reactor(Proxy* px, int id, int listen_fd);
+  ~Reactor() override;
+  void loop();
+  void post(std::function<void()> fn) override;
+  void wake() {
+    uint64_t one = 1;
+    (void)!write(evfd_, &one, 8);
+  }
+
+  // stats (read by Proxy::stats_json from another thread)
+  std::atomic<uint64_t> requests{0}, hits{0}, misses{0}, upstream_reqs{0}, responses{0},
+      bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
+      cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0};
+  std::atomic<uint64_t> hist[kHistBuckets] = {};
+
+ private:
+  void accept_all();
+  void on_client(Client* c, uint32_t ev);
+  void on_upstream(Upstream* u, uint32_t ev);
+  void on_request(Client* c);
+  void on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v);
+  void forward(Client* c, Slot* s);
+  void on_upstream_response(Upstream* u);
+  Upstream* pick_upstream(Client* c);
+  int choose_server();
+  void flush_client(Client* c);
+  void flush_upstream(Upstream* u);
+  void complete_slot(Client* c, Slot* s, Bytes data);
+  void fail_pend(Pend& p, int code, const char* reason);
+  void release_waiters(const std::string& key, Bytes obj);
+  void close_client(Client* c);
+  void close_upstream(Upstream* u);
+  void arm(Conn* c, bool out);
+  void gc();
+  Client* find_client(uint64_t id);
+  Slot* find_slot(Client* c, uint64_t seq);
+  void drain_posted();
+  bool cacheable_response(const HttpParser& r, uint32_t* ttl) const;
+
+  Proxy* px_;
+  const ProxyConfig& cfg_;
+  int id_;
+  int epfd_ = -1, listen_fd_ = -1, evfd_ = -1, timerfd_ = -1;
+  uint64_t next_id_ = kFirstConnId;
+  std::unordered_map<uint64_t, Conn*> conns_;
+  std::vector<Upstream*> pool_;
+  std::vector<Conn*> graveyard_;
+  std::mutex post_mu_;
+  std::vector<std::function<void()>> posted_;
+  std::mt19937 rng_;
+  std::vector<char> buf_;
+  // collapsed forwarding: key -> requests waiting on the in-flight miss of the
+  // same object (only the first one goes upstream)
+  std::unordered_map<std::string, std::vector<std::pair<uint64_t, uint64_t>>> inflight_;
+  // servers that answered "Connection: close": never pipeline onto them
+  std::vector<char> server_nka_;
+};
+
+// =====================================================================================
+Reactor::Reactor(Proxy* px, int id, int listen_fd)
+    : px_(px), cfg_(px->cfg_), id_(id), listen_fd_(listen_fd), rng_(1234 + id), buf_(1 << 16),
+      server_nka_(px->cfg_.upstreams.size(), 0) {
+  epfd_ = epoll_create1(EPOLL_CLOEXEC);
+  evfd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  timerfd_ = timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
+  itimerspec its{};
+  its.it_interval.tv_sec = 1;
+  its.it_value.tv_sec = 1;
+  timerfd_settime(timerfd_, 0, &its, nullptr);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.u64 = kListenId;
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, listen_fd_, &ev);
+  ev.data.u64 = kEventId;
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
+  ev.data.u64 = kTimerId;
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, timerfd_, &ev);
+}
+
+Reactor::~Reactor() {
+  for (auto& kv : conns_) {
+    close(kv.second->fd);
+    delete kv.second;
+  }
+  for (Conn* c : graveyard_) delete c;
+  close(listen_fd_);
+  close(evfd_);
+  close(timerfd_);
+  close(epfd_);
+}
+
+void Reactor::post(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    posted_.push_back(std::move(fn));
+  }
+  wake();
+}
+
+void Reactor::drain_posted() {
+  std::vector<std::function<void()>> fns;
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    fns.swap(posted_);
+  }
+  for (auto& f : fns) f();
+}
+
+void Reactor::arm(Conn* c, bool out) {
+  if (c->dead || c->out_armed == out) return;
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP | (out ? EPOLLOUT : 0);
+  ev.data.u64 = c->id;
+  epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+  c->out_armed = out;
+}
+
+void Reactor::loop() {
+  epoll_event evs[256];
+  while (px_->running_) {
+    const int n = epoll_wait(epfd_, evs, 256, 100);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t id = evs[i].data.u64;
+      if (id == kListenId) {
+        accept_all();
+      } else if (id == kEventId) {
+        uint64_t v;
+        (void)!read(evfd_, &v, 8);
+      } else if (id == kTimerId) {
+        uint64_t v;
+        (void)!read(timerfd_, &v, 8);
+        gc();
+      } else {
+        auto it = conns_.find(id);
+        if (it == conns_.end() || it->second->dead) continue;
+        Conn* c = it->second;
+        if (c->kind == 0) on_client(static_cast<Client*>(c), evs[i].events);
+        else on_upstream(static_cast<Upstream*>(c), evs[i].events);
+      }
+    }
+    drain_posted();
+    for (Conn* c : graveyard_) delete c;
+    graveyard_.clear();
+  }
+}
+
+void Reactor::accept_all() {
+  for (;;) {
+    sockaddr_in sa{};
+    socklen_t len = sizeof sa;
+    const int fd = accept4(listen_fd_, reinterpret_cast<sockaddr*>(&sa), &len,
+                           SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) return;
+    set_nodelay(fd);
+    auto* c = new Client();
+    c->fd = fd;
+    c->kind = 0;
+    c->id = next_id_++;
+    c->ctime = c->atime = now_s();
+    c->loopback = (ntohl(sa.sin_addr.s_addr) >> 24) == 127;
+    conns_[c->id] = c;
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP;
+    ev.data.u64 = c->id;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+    accepts++;
+    clients++;
+  }
+}
+
+Client* Reactor::find_client(uint64_t id) {
+  auto it = conns_.find(id);
+  if (it == conns_.end() || it->second->dead || it->second->kind != 0) return nullptr;
+  return static_cast<Client*>(it->second);
+}
+
+Slot* Reactor::find_slot(Client* c, uint64_t seq) {
+  for (auto& s : c->slots)
+    if (s->seq == seq) return s.get();
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------------
+// client side
+// ---------------------------------------------------------------------------------
+void Reactor::on_client(Client* c, uint32_t ev) {
+  if (ev & EPOLLOUT) flush_client(c);
+  if (c->dead) return;
+  if (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+    for (;;) {
+      const ssize_t r = recv(c->fd, buf_.data(), buf_.size(), 0);
+      if (r > 0) {
+        c->atime = now_s();
+        const char* p = buf_.data();
+        size_t n = (size_t)r;
+        while (n > 0 && !c->dead && !c->closing) {
+          const size_t used = c->req.parse(p, n);
+          p += used;
+          n -= used;
+          if (c->req.error()) {
+            bad_requests++;
+            auto s = std::make_unique<Slot>();
+            s->seq = c->next_seq++;
+            s->out.write(simple_response(400, "Bad Request", cfg_.server_name, "bad request\n",
+                                         "text/plain", true));
+            s->out.close();
+            s->ready = true;
+            s->close_after = true;
+            c->slots.push_back(std::move(s));
+            c->closing = true;
+            break;
+          }
+          if (c->req.message_complete()) {
+            on_request(c);
+            if (c->dead) return;
+            c->req.reset();
+          } else if (used == 0) {
+            break;
+          }
+        }
+        if (c->dead) return;
+        if ((size_t)r < buf_.size()) break;
+        continue;
+      }
+      if (r == 0) {  // client EOF: finish every queued response, then close
+        c->eof = true;
+        c->closing = true;
+        if (c->slots.empty()) close_client(c);
+        else flush_client(c);
+        return;
+      }
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      errors++;
+      close_client(c);
+      return;
+    }
+    flush_client(c);
+  }
+}
+
+void Reactor::on_request(Client* c) {
+  HttpParser& q = c->req;
+  c->nreq++;
+  requests++;
+  const std::string url = q.url();
+  if (cfg_.kill_switch && url == "/kill" && (!cfg_.kill_loopback_only || c->loopback)) {
+    // KILL SWITCH (Server.py:329-331: sys.exit(0))
+    std::fprintf(stderr, "[shellac] /kill received; shutting down\n");
+    px_->stop();
+    return;
+  }
+  auto s = std::make_unique<Slot>();
+  Slot* sp = s.get();
+  s->seq = c->next_seq++;
+  s->t0 = now_s();
+  s->close_after = !q.keep_alive() || c->nreq >= cfg_.client_max_reqs;
+  if (url == "/_shellac/stats") {
+    s->out.write(simple_response(200, "OK", cfg_.server_name, px_->stats_json(),
+                                 "application/json", s->close_after));
+    s->out.close();
+    s->ready = true;
+    c->slots.push_back(std::move(s));
+    flush_client(c);
+    return;
+  }
+  const std::string& method = q.method();
+  s->head = method == "HEAD";
+  s->client_gzip = contains_ci(q.header("accept-encoding"), "gzip");
+  const std::string* host = q.header("host");
+  s->key = cfg_.key_host && host ? *host + url : url;  // reference key: URL (Server.py:327)
+  s->d = digest_bytes(reinterpret_cast<const uint8_t*>(s->key.data()), s->key.size());
+  // upstream request: force gzip (Server.py:358), pool the connection
+  q.set_header("accept-encoding", "gzip");
+  q.remove_header("proxy-connection");
+  q.remove_header("keep-alive");
+  q.set_header("connection", "keep-alive");
+  s->fwd = q.serialize();
+  s->lookup = px_->cfg_.cache_enabled &&
+              (cfg_.policy == "reference" || method == "GET") && !q.header("authorization");
+  c->slots.push_back(std::move(s));
+  if (sp->lookup) {
+    const uint64_t cid = c->id, seq = sp->seq;
+    px_->backend_->get(sp->key, sp->d, this, [this, cid, seq](bool hit, CacheValue v) {
+      on_cache(cid, seq, hit, std::move(v));
+    });
+  } else {
+    forward(c, sp);
+  }
+}
+
+void Reactor::on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v) {
+  Client* c = find_client(cid);
+  if (!c) return;
+  Slot* s = find_slot(c, seq);
+  if (!s || s->ready) return;
+  if (hit && v.data) {
+    hits++;
+    complete_slot(c, s, v.data);
+    return;
+  }
+  misses++;
+  auto it = inflight_.find(s->key);
+  if (it != inflight_.end()) {  // same object already being fetched: wait for it
+    collapsed++;
+    it->second.emplace_back(cid, seq);
+    return;
+  }
+  inflight_[s->key];  // this request leads the fetch
+  forward(c, s);
+}
+
+void Reactor::complete_slot(Client* c, Slot* s, Bytes data) {
+  s->out.write_shared(std::move(data));
+  s->out.close();
+  s->ready = true;
+  const double us = (now_s() - s->t0) * 1e6;
+  const int b = us < 1 ? 0 : std::min(kHistBuckets - 1, 1 + (int)std::log2(us));
+  hist[b]++;
+  flush_client(c);
+}
+
+void Reactor::flush_client(Client* c) {
+  // Head-of-line ordered write of every *ready* response slot (Server.py:236-239),
+  // many pipelined responses per writev.
+  if (c->dead) return;
+  for (;;) {
+    iovec iov[64];
+    int cnt = 0;
+    size_t want = 0;
+    for (auto& s : c->slots) {
+      if (!s->ready || cnt >= 64) break;
+      const int k = s->out.iov(iov + cnt, 64 - cnt);
+      for (int j = 0; j < k; ++j) want += iov[cnt + j].iov_len;
+      cnt += k;
+    }
+    if (cnt == 0) break;
+    const ssize_t w = writev(c->fd, iov, cnt);
+    if (w < 0) {
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        arm(c, true);
+        return;
+      }
+      errors++;
+      close_client(c);
+      return;
+    }
+    bytes_out += (uint64_t)w;
+    c->atime = now_s();
+    size_t left = (size_t)w;
+    while (!c->slots.empty() && c->slots.front()->ready) {
+      Slot* s = c->slots.front().get();
+      const size_t take = std::min<size_t>(left, s->out.pending());
+      s->out.ack(take);
+      left -= take;
+      if (!s->out.complete()) break;
+      const bool last = s->close_after;
+      c->slots.pop_front();
+      if (last) {  // "Connection: close" / max requests reached / bad request
+        close_client(c);
+        return;
+      }
+    }
+    if ((size_t)w < want) {
+      arm(c, true);
+      return;
+    }
+  }
+  if (c->eof && c->slots.empty()) {
+    close_client(c);
+    return;
+  }
+  arm(c, false);
+}
+
+void Reactor::close_client(Client* c) {
+  if (c->dead) return;
+  c->dead = true;
+  epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+  close(c->fd);
+  conns_.erase(c->id);
+  clients--;
+  if (c->up) {
+    // release the pooled upstream (Server.py:189-192); its in-flight responses
+    // still complete and fill the cache
+    if (c->up->owner == c) c->up->owner = nullptr;
+    c->up = nullptr;
+  }
+  graveyard_.push_back(c);
+}
+
+// ---------------------------------------------------------------------------------
+// upstream side
+// ---------------------------------------------------------------------------------
+int Reactor::choose_server() {
+  const int n = (int)cfg_.upstreams.size();
+  if (n == 0) return -1;
+  const double t = now_s();
+  std::vector<int> up;
+  for (int i = 0; i < n; ++i)
+    if (px_->upstream_up(i, t)) up.push_back(i);
+  if (up.empty()) return -1;
+  if (cfg_.balance == "roundrobin") return up[(size_t)px_->next_rr() % up.size()];
+  if (cfg_.balance == "leastconn") {
+    std::vector<int> load(n, 0);
+    for (Upstream* u : pool_) load[u->server] += (int)u->pend.size() + (u->owner ? 1 : 0);
+    int best = up[0];
+    for (int i : up)
+      if (load[i] < load[best]) best = i;
+    return best;
+  }
+  return up[std::uniform_int_distribution<size_t>(0, up.size() - 1)(rng_)];  // Server.py:123
+}
+
+Upstream* Reactor::pick_upstream(Client* c) {
+  const double t = now_s();
+  auto valid = [&](Upstream* u) {
+    if (u->dead) return false;
+    if (u->count >= u->ka_max) return false;
+    return u->ka_timeout < 0 || t - u->atime < u->ka_timeout;
+  };
+  if (c->up && valid(c->up)) return c->up;  // affinity (Server.py:94-101)
+  if (c->up) {
+    if (c->up->owner == c) c->up->owner = nullptr;
+    c->up = nullptr;
+  }
+  for (Upstream* u : pool_) {  // reuse a free pooled connection (Server.py:103-116)
+    if (!u->owner && valid(u) && px_->upstream_up(u->server, t)) {
+      u->owner = c;
+      c->up = u;
+      return u;
+    }
+  }
+  for (int attempt = 0; attempt < (int)cfg_.upstreams.size() + 1; ++attempt) {
+    const int srv = choose_server();
+    if (srv < 0) return nullptr;
+    const int fd = connect_nonblock(cfg_.upstreams[srv]);  // non-blocking (ref blocks, :126)
+    if (fd < 0) {
+      px_->upstream_failed(srv, t);
+      upstream_failures++;
+      continue;
+    }
+    auto* u = new Upstream();
+    if (server_nka_[srv]) u->ka_max = 1;
+    u->fd = fd;
+    u->kind = 1;
+    u->id = next_id_++;
+    u->server = srv;
+    u->ctime = u->atime = t;
+    conns_[u->id] = u;
+    pool_.push_back(u);
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
+    ev.data.u64 = u->id;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+    u->out_armed = true;
+    upstreams++;
+    u->owner = c;
+    c->up = u;
+    return u;
+  }
+  return nullptr;
+}
+
+void Reactor::forward(Client* c, Slot* s) {
+  s->attempts++;
+  Upstream* u = pick_upstream(c);
+  if (!u) {
+    complete_slot(c, s, std::make_shared<const std::string>(simple_response(
+                            503, "Service Unavailable", cfg_.server_name, "no upstream available\n")));
+    return;
+  }
+  u->out.write(s->fwd);
+  u->pend.push_back(Pend{c->id, s->seq, s->key, s->d, s->lookup, s->head, s->client_gzip});
+  u->count++;
+  upstream_reqs++;
+  flush_upstream(u);
+}
+
+void Reactor::flush_upstream(Upstream* u) {
+  if (u->dead) return;
+  if (!u->connected) {
+    arm(u, true);
+    return;
+  }
+  while (u->out.pending()) {
+    iovec iov[64];
+    const int cnt = u->out.iov(iov, 64);
+    const ssize_t w = writev(u->fd, iov, cnt);
+    if (w < 0) {
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        arm(u, true);
+        return;
+      }
+      close_upstream(u);
+      return;
+    }
+    u->out.ack((uint64_t)w);
+    u->atime = now_s();
+  }
+  u->out.release_acked();
+  arm(u, false);
+}
+
+void Reactor::release_waiters(const std::string& key, Bytes obj) {
+  auto it = inflight_.find(key);
+  if (it == inflight_.end()) return;
+  std::vector<std::pair<uint64_t, uint64_t>> waiters;
+  waiters.swap(it->second);
+  inflight_.erase(it);
+  for (auto& w : waiters) {
+    Client* c = find_client(w.first);
+    if (!c) continue;
+    Slot* s = find_slot(c, w.second);
+    if (!s || s->ready) continue;
+    if (obj) {
+      hits++;
+      complete_slot(c, s, obj);
+    } else {
+      forward(c, s);  // uncacheable ("hit-for-pass"): each waiter fetches its own copy
+    }
+  }
+}
+
+void Reactor::fail_pend(Pend& p, int code, const char* reason) {
+  if (p.lookup && code != 502) release_waiters(p.key, nullptr);
+  Client* c = find_client(p.client_id);
+  if (!c) {
+    if (p.lookup) release_waiters(p.key, nullptr);
+    return;
+  }
+  Slot* s = find_slot(c, p.seq);
+  if (!s || s->ready) return;
+  if (s->attempts < 3 && code == 502) {  // idempotent retry on another connection
+    retries++;
+    if (c->up && c->up->dead) c->up = nullptr;
+    forward(c, s);
+    return;
+  }
+  if (p.lookup) release_waiters(p.key, nullptr);
+  complete_slot(c, s, std::make_shared<const std::string>(
+                          simple_response(code, reason, cfg_.server_name, "upstream failed\n")));
+}
+
+void Reactor::on_upstream(Upstream* u, uint32_t ev) {
+  if ((ev & EPOLLOUT) && !u->connected) {
+    int err = 0;
+    socklen_t el = sizeof err;
+    getsockopt(u->fd, SOL_SOCKET, SO_ERROR, &err, &el);
+    if (err) {
+      px_->upstream_failed(u->server, now_s());
+      upstream_failures++;
+      close_upstream(u);
+      return;
+    }
+    u->connected = true;
+  }
+  if (ev & EPOLLOUT) flush_upstream(u);
+  if (u->dead) return;
+  if (!(ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR))) return;
+  for (;;) {
+    const ssize_t r = recv(u->fd, buf_.data(), buf_.size(), 0);
+    if (r > 0) {
+      u->atime = now_s();
+      const char* p = buf_.data();
+      size_t n = (size_t)r;
+      while (n > 0 && !u->dead) {
+        if (u->pend.empty()) {  // unsolicited bytes: protocol error
+          close_upstream(u);
+          return;
+        }
+        if (!u->resp) {
+          u->resp = std::make_unique<HttpParser>(cfg_.decode_gzip);
+          u->resp->set_no_body(u->pend.front().head);
+          u->resp->set_eof_body(true);
+        }
+        const size_t used = u->resp->parse(p, n);
+        p += used;
+        n -= used;
+        if (u->resp->error()) {
+          close_upstream(u);
+          return;
+        }
+        if (u->resp->message_complete()) {
+          on_upstream_response(u);
+          if (u->dead) return;
+        } else if (used == 0) {
+          break;
+        }
+      }
+      if ((size_t)r < buf_.size()) return;
+      continue;
+    }
+    if (r == 0) {
+      if (u->resp && u->resp->finish() && !u->pend.empty()) on_upstream_response(u);
+      close_upstream(u);
+      return;
+    }
+    if (errno == EAGAIN || errno == EWOULDBLOCK) return;
+    close_upstream(u);
+    return;
+  }
+}
+
+bool Reactor::cacheable_response(const HttpParser& r, uint32_t* ttl) const {
+  *ttl = cfg_.ttl;
+  if (cfg_.policy == "reference") return true;  // Server.py:431-432 caches everything
+  switch (r.status()) {
+    case 200: case 203: case 204: case 300: case 301: case 404: case 405: case 410: case 414:
+    case 501:
+      break;
+    default:
+      return false;
+  }
+  const std::string* cc = r.header("cache-control");
+  if (contains_ci(cc, "no-store") || contains_ci(cc, "private") || contains_ci(cc, "no-cache"))
+    return false;
+  if (r.header("set-cookie")) return false;
+  const long ma = cc_max_age(cc);
+  if (ma == 0) return false;
+  if (ma > 0) *ttl = (uint32_t)ma;
+  return true;
+}
+
+void Reactor::on_upstream_response(Upstream* u) {
+  Pend p = std::move(u->pend.front());
+  u->pend.pop_front();
+  std::unique_ptr<HttpParser> rp = std::move(u->resp);
+  HttpParser& r = *rp;
+  const bool ka = r.keep_alive();
+  const auto kap = r.keep_alive_params();
+  responses++;
+  // header rewrite (Server.py:412-416)
+  r.set_header("server", cfg_.server_name);
+  r.set_header("keep-alive", "timeout=5, max=100");
+  r.set_header("connection", "keep-alive");
+  r.remove_header("accept-ranges");
+  const std::string* ce = r.header("content-encoding");
+  if (cfg_.compress && !ce && p.client_gzip && r.body().size() >= 256) {
+    const std::string* ct = r.header("content-type");
+    if (ct && (contains_ci(ct, "text/") || contains_ci(ct, "json") || contains_ci(ct, "javascript") ||
+               contains_ci(ct, "xml"))) {
+      r.mutable_body() = gzip_compress(r.body(), 6);
+      r.set_header("content-encoding", "gzip");
+      r.set_header("vary", "Accept-Encoding");
+    }
+  }
+  Bytes obj;
+  if (p.head) {
+    const std::string* cl = r.header("content-length");
+    const uint64_t len = cl ? std::strtoull(cl->c_str(), nullptr, 10) : 0;
+    obj = std::make_shared<const std::string>(r.serialize_head(len, cl != nullptr));
+  } else {
+    obj = std::make_shared<const std::string>(r.serialize());
+  }
+  uint32_t ttl = cfg_.ttl;
+  bool cached = false;
+  if (p.lookup && !p.head && cacheable_response(r, &ttl)) {
+    cached = true;
+    px_->backend_->set(p.key, p.d, obj, 0, ttl);  // Server.py:432 mc.set(key, obj, time=ttl)
+    cache_sets++;
+  }
+  if (Client* c = find_client(p.client_id)) {
+    if (Slot* s = find_slot(c, p.seq)) {
+      if (!s->ready) complete_slot(c, s, obj);
+    }
+  }
+  if (p.lookup) release_waiters(p.key, cached ? obj : nullptr);
+  if (!ka) {
+    server_nka_[u->server] = 1;
+    close_upstream(u);  // remaining pipelined requests are retried elsewhere
+    return;
+  }
+  server_nka_[u->server] = 0;
+  u->ka_timeout = kap.first;
+  u->ka_max = kap.second;
+}
+
+void Reactor::close_upstream(Upstream* u) {
+  if (u->dead) return;
+  u->dead = true;
+  epoll_ctl(epfd_, EPOLL_CTL_DEL, u->fd, nullptr);
+  close(u->fd);
+  conns_.erase(u->id);
+  upstreams--;
+  pool_.erase(std::remove(pool_.begin(), pool_.end(), u), pool_.end());
+  if (u->owner && u->owner->up == u) u->owner->up = nullptr;
+  u->owner = nullptr;
+  std::deque<Pend> pend;
+  pend.swap(u->pend);
+  graveyard_.push_back(u);
+  for (auto& p : pend) fail_pend(p, 502, "Bad Gateway");
+}
+
+void Reactor::gc() {
+  // Client keep-alive policy (Server.py:155-166): idle timeout / max requests.
+  const double t = now_s();
+  std::vector<Client*> idle;
+  std::vector<Upstream*> stale;
+  for (auto& kv : conns_) {
+    Conn* c = kv.second;
+    if (c->dead) continue;
+    if (c->kind == 0) {
+      auto* cl = static_cast<Client*>(c);
+      if (cl->slots.empty() &&
+          (t - cl->atime >= cfg_.client_timeout || cl->nreq >= cfg_.client_max_reqs))
+        idle.push_back(cl);
+    } else {
+      auto* u = static_cast<Upstream*>(c);
+      if (u->pend.empty() && !u->owner && u->ka_timeout >= 0 &&
+          (t - u->atime >= u->ka_timeout || u->count >= u->ka_max))
+        stale.push_back(u);
+    }
+  }
+  for (Client* c : idle) {
+    gc_closed++;
+    close_client(c);
+  }
+  for (Upstream* u : stale) close_upstream(u);
+}
+
+// =====================================================================================
+// Proxy
+// =====================================================================================
+Proxy::Proxy(const ProxyConfig& cfg, std::shared_ptr<CacheBackend> backend)
+    : cfg_(cfg), backend_(std::move(backend)) {
+  SH_CHECK(!cfg_.upstreams.empty(), "no upstream web servers specified");
+  SH_CHECK(cfg_.threads >= 1, "threads >= 1");
+  if (cfg_.cache_enabled) SH_CHECK(backend_ != nullptr, "cache enabled without a backend");
+  up_down_until_.reset(new std::atomic<double>[cfg_.upstreams.size()]);
+  for (size_t i = 0; i < cfg_.upstreams.size(); ++i) up_down_until_[i] = 0;
+}
+
+Proxy::~Proxy() {
+  stop();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+}
+
+bool Proxy::upstream_up(int idx, double now) const { return now >= up_down_until_[idx].load(); }
+
+void Proxy::upstream_failed(int idx, double now) {
+  up_down_until_[idx] = now + cfg_.upstream_retry_s;
+}
+
+void Proxy::start() {
+  SH_CHECK(!running_, "already running");
+  start_time_ = now_s();
+  const int first = listen_tcp(cfg_.bind, cfg_.port, cfg_.threads > 1, cfg_.backlog);
+  port_ = local_port(first);
+  running_ = true;
+  for (int i = 0; i < cfg_.threads; ++i) {
+    const int fd = i == 0 ? first : listen_tcp(cfg_.bind, port_, true, cfg_.backlog);
+    reactors_.emplace_back(new Reactor(this, i, fd));
+  }
+  for (auto& r : reactors_) {
+    Reactor* rp = r.get();
+    threads_.emplace_back([rp] { rp->loop(); });
+  }
+}
+
+void Proxy::wait() {
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+}
+
+void Proxy::stop() {
+  running_ = false;
+  for (auto& r : reactors_) r->wake();
+}
+
+std::string Proxy::stats_json() {
+  uint64_t req = 0, hit = 0, miss = 0, ur = 0, resp = 0, bo = 0, err = 0, cl = 0, up = 0, acc = 0,
+           gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0;
+  uint64_t h[kHistBuckets] = {};
+  for (auto& r : reactors_) {
+    req += r->requests; hit += r->hits; miss += r->misses; ur += r->upstream_reqs;
+    resp += r->responses; bo += r->bytes_out; err += r->errors; cl += r->clients;
+    up += r->upstreams; acc += r->accepts; gcc += r->gc_closed; sets += r->cache_sets;
+    bad += r->bad_requests; uf += r->upstream_failures; rt += r->retries; col += r->collapsed;
+    for (int b = 0; b < kHistBuckets; ++b) h[b] += r->hist[b];
+  }
+  uint64_t total = 0;
+  for (uint64_t v : h) total += v;
+  auto pct = [&](double q) -> double {
+    if (!total) return 0;
+    uint64_t acc2 = 0;
+    for (int b = 0; b < kHistBuckets; ++b) {
+      acc2 += h[b];
+      if (acc2 >= q * total) return b == 0 ? 1.0 : std::pow(2.0, b);  // bucket upper bound (us)
+    }
+    return std::pow(2.0, kHistBuckets);
+  };
+  std::ostringstream o;
+  o << "{\"server\":\"" << cfg_.server_name << "\",\"uptime_s\":" << (now_s() - start_time_)
+    << ",\"threads\":" << cfg_.threads << ",\"requests\":" << req << ",\"cache_hits\":" << hit
+    << ",\"cache_misses\":" << miss << ",\"upstream_requests\":" << ur
+    << ",\"upstream_responses\":" << resp << ",\"cache_fills\":" << sets
+    << ",\"bytes_out\":" << bo << ",\"errors\":" << err << ",\"bad_requests\":" << bad
+    << ",\"upstream_failures\":" << uf << ",\"retries\":" << rt << ",\"collapsed\":" << col
+    << ",\"clients\":" << cl
+    << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
+    << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
+    << total << "}";
+  if (backend_) {
+    StatList st;
+    backend_->stats(&st);
+    o << ",\"backend\":\"" << backend_->name() << "\",\"cache\":{";
+    for (size_t i = 0; i < st.size(); ++i)
+      o << (i ? "," : "") << "\"" << st[i].first << "\":" << st[i].second;
+    o << "}";
+  }
+  o << "}";
+  return o.str();
+}
+
+}  // namespace shellac

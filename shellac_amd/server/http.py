@@ -26,10 +26,12 @@ class HttpParser:
     """Incremental HTTP/1.1 request/response parser (see csrc/http.h for the list of
     deliberate fixes relative to the reference)."""
 
-    def __init__(self, decode_gzip: bool = True, eof_body: bool = False):
+    def __init__(self, decode_gzip: bool = True, eof_body: bool = False, no_body: bool = False):
         self._p = core().NativeHttpParser(decode_gzip)
         if eof_body:
             self._p.set_eof_body(True)
+        if no_body:  # parsing the response to a HEAD request
+            self._p.set_no_body(True)
         self._headers: Optional[dict] = None
         self._body: Optional[io.BytesIO] = None
 

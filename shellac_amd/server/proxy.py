@@ -1,0 +1,208 @@
+"""Python API and CLI of the caching reverse proxy.
+
+``Server`` keeps the reference constructor (src/python/shellac/server/Server.py:30,
+``Server(servers, caches, port=8080, ttl=170, compress=False, cache=False)``) and
+``run()`` (Server.py:442); the event loop itself is the native multi-threaded
+reactor in ``csrc/proxy.cc``. ``main()`` keeps the reference CLI
+(Server.py:490-547: ``-s/--servers``, ``-c/--caches``, ``-p/--port``, ``-t/--ttl``,
+``-z/--compress``) and adds flags for the promoted constants and the GPU cache.
+"""
+from __future__ import annotations
+
+import argparse
+import signal
+import socket
+import sys
+import threading
+from typing import Iterable, Optional, Sequence, Union
+
+from .._native import core
+
+ServerSpec = Union[str, tuple]
+
+
+def _csv(items: Iterable[ServerSpec], default_port: int) -> str:
+    out = []
+    for it in items:
+        if isinstance(it, tuple):
+            out.append(f"{it[0]}:{int(it[1])}")
+        elif ":" in str(it):
+            out.append(str(it))
+        else:
+            out.append(f"{it}:{default_port}")
+    return ",".join(out)
+
+
+def parse_server_list(slist: str, default_port: int) -> list:
+    """``"a:1,b"`` -> ``[(ip, 1), (ip, default_port)]`` with DNS resolution
+    (reference: parse_server_list, Server.py:493-505)."""
+    result = []
+    for srv in [s for s in (slist or "").split(",") if s]:
+        if ":" in srv:
+            host, port = srv.rsplit(":", 1)
+            result.append((socket.gethostbyname(host), int(port)))
+        else:
+            result.append((socket.gethostbyname(srv), default_port))
+    return result
+
+
+def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
+                 dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
+                 hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 50,
+                 retry_s: int = 2):
+    """Build a native cache backend.
+
+    kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
+    ``dram`` (local host memory), ``hbm`` (one HBM shard per GPU in ``gpus``) or
+    ``none``.
+    """
+    c = core()
+    if kind == "none":
+        return None
+    if kind == "memcached":
+        if not caches:
+            raise ValueError("memcached backend needs cache servers (-c host:port,...)")
+        return c.memcached_backend(_csv(caches, 11211), retry_s=retry_s)
+    if kind == "dram":
+        return c.dram_backend(int(dram_mb) << 20, max_item)
+    if kind == "hbm":
+        devs = list(gpus) if gpus is not None else list(range(max(1, c.device_count())))
+        log_bytes = int(hbm_gb * (1 << 30)) // 16 * 16
+        nb = 1
+        while nb * 4 * 1024 < log_bytes:  # ~2 KiB/object at <=50% slot load
+            nb *= 2
+        return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us)
+    raise ValueError(f"unknown cache backend {kind!r}")
+
+
+class Server:
+    """Shellac caching reverse proxy (reference-compatible constructor)."""
+
+    def __init__(self, servers: Sequence[ServerSpec], caches: Sequence[ServerSpec] = (),
+                 port: int = 8080, ttl: int = 170, compress: bool = False, cache: bool = False,
+                 *, backend=None, backend_kind: Optional[str] = None, threads: int = 1,
+                 policy: str = "rfc", kill_switch: bool = True, key_host: bool = False,
+                 client_timeout: int = 30, client_max_reqs: int = 1000,
+                 balance: str = "random", bind: str = "0.0.0.0", decode_gzip: bool = False,
+                 **backend_opts):
+        if not servers:
+            raise ValueError("No upstream web servers specified.")
+        self._backend = backend
+        if self._backend is None and (cache or backend_kind):
+            kind = backend_kind or ("memcached" if caches else "dram")
+            self._backend = make_backend(kind, caches=caches, **backend_opts)
+        self._proxy = core().Proxy(
+            _csv(servers, 80), self._backend, port=port, bind=bind, threads=threads, ttl=ttl,
+            compress=compress, policy=policy, kill_switch=kill_switch, key_host=key_host,
+            client_timeout=client_timeout, client_max_reqs=client_max_reqs, balance=balance,
+            decode_gzip=decode_gzip)
+        self._started = False
+
+    @property
+    def port(self) -> int:
+        return self._proxy.port
+
+    @property
+    def backend(self):
+        return self._backend
+
+    def start(self) -> "Server":
+        if not self._started:
+            self._proxy.start()
+            self._started = True
+        return self
+
+    def run(self) -> None:
+        """Serve until ``stop()`` / ``GET /kill`` / SIGTERM (blocking)."""
+        self.start()
+        self._proxy.wait()
+
+    def stop(self) -> None:
+        self._proxy.stop()
+        if self._started:
+            self._proxy.wait()
+
+    def running(self) -> bool:
+        return self._proxy.running
+
+    def stats(self) -> dict:
+        import json
+
+        return json.loads(self._proxy.stats_json())
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+
+def build_arg_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="shellac", description="Shellac Accelerator (MI355X-native)")
+    p.add_argument("-s", "--servers", help="Web servers to cache: host:port,host:port,... (port defaults to 80)")
+    p.add_argument("-c", "--caches", help="Cache servers to use: host:port,host:port,... (port defaults to 11211)")
+    p.add_argument("-p", "--port", type=int, default=8080, help="Port to listen for connections on.")
+    p.add_argument("-t", "--ttl", type=int, default=170, help="Lifetime of cached objects.")
+    p.add_argument("-z", "--compress", action="store_true", help="Compress cached objects.")
+    # beyond the reference
+    p.add_argument("--cache", choices=["memcached", "dram", "hbm", "none"], default=None,
+                   help="cache backend (default: memcached if -c is given, else dram)")
+    p.add_argument("--gpus", type=str, default=None, help="GPU ids for --cache hbm, e.g. 0,1,2,3")
+    p.add_argument("--hbm-gb", type=float, default=16.0, help="HBM value-log GiB per GPU")
+    p.add_argument("--dram-mb", type=int, default=1024, help="host cache MiB for --cache dram")
+    p.add_argument("--batch-us", type=int, default=50, help="HBM batching window (us)")
+    p.add_argument("--threads", type=int, default=1, help="reactor threads (SO_REUSEPORT)")
+    p.add_argument("--bind", default="0.0.0.0")
+    p.add_argument("--policy", choices=["rfc", "reference"], default="rfc",
+                   help="rfc: cache GET 200/301/404.. honouring Cache-Control; reference: cache everything")
+    p.add_argument("--balance", choices=["random", "roundrobin", "leastconn"], default="random")
+    p.add_argument("--client-timeout", type=int, default=30)
+    p.add_argument("--client-max-reqs", type=int, default=1000)
+    p.add_argument("--key-host", action="store_true", help="include Host in the cache key")
+    p.add_argument("--no-kill-switch", action="store_true", help="disable GET /kill")
+    p.add_argument("--decode-gzip", action="store_true",
+                   help="inflate + re-deflate every miss like the reference (default: passthrough)")
+    return p
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    args = build_arg_parser().parse_args(argv)
+    servers = parse_server_list(args.servers, 80) if args.servers else []
+    caches = parse_server_list(args.caches, 11211) if args.caches else []
+    if not servers:
+        print("No upstream web servers specified. See shellac -h for help.")
+        return 1
+    kind = args.cache or ("memcached" if caches else "dram")
+    if kind == "memcached" and not caches:
+        print("No cache servers specified. See shellac -h for help.")
+        return 1
+    gpus = [int(x) for x in args.gpus.split(",")] if args.gpus else None
+    srv = Server(servers, caches, port=args.port, ttl=args.ttl, compress=args.compress,
+                 backend_kind=kind, threads=args.threads, policy=args.policy,
+                 kill_switch=not args.no_kill_switch, key_host=args.key_host,
+                 client_timeout=args.client_timeout, client_max_reqs=args.client_max_reqs,
+                 balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
+                 **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
+                 **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}
+                    if kind == "hbm" else {}))
+    print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)
+    stop = threading.Event()
+
+    def _sig(signum, frame):  # SIGINT/SIGTERM: clean shutdown (ref installs a no-op SIGINT)
+        stop.set()
+        srv.stop()
+
+    signal.signal(signal.SIGINT, _sig)
+    signal.signal(signal.SIGTERM, _sig)
+    try:
+        srv.start()
+        while srv.running() and not stop.is_set():
+            stop.wait(0.2)
+    finally:
+        srv.stop()
+        print("\nShutting down...")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,101 @@
+"""A tiny HTTP/1.1 origin server for tests and benchmarks (stands in for the
+reference's Apache upstream, benchmarks/run-baseline.sh). Counts requests per
+path so tests can prove which requests the cache absorbed."""
+from __future__ import annotations
+
+import gzip
+import threading
+from collections import Counter
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+
+class Origin:
+    def __init__(self, port: int = 0, body_bytes: int = 1024, delay_s: float = 0.0,
+                 keep_alive: bool = True):
+        self.hits: Counter = Counter()
+        self.lock = threading.Lock()
+        outer = self
+
+        class H(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1" if keep_alive else "HTTP/1.0"
+
+            def log_message(self, *a):
+                pass
+
+            def _reply(self, head: bool):
+                with outer.lock:
+                    outer.hits[self.path] += 1
+                    n = outer.hits[self.path]
+                if delay_s:
+                    import time
+
+                    time.sleep(delay_s)
+                path = self.path
+                if path.startswith("/status/"):
+                    code = int(path.split("/")[2])
+                    body = f"status {code}\n".encode()
+                else:
+                    code = 200
+                    body = (f"<html>{path} #{n} ".encode() + b"x" * body_bytes + b"</html>\n")
+                headers = {"Content-Type": "text/html"}
+                if path.startswith("/nocache"):
+                    headers["Cache-Control"] = "no-store"
+                if path.startswith("/cookie"):
+                    headers["Set-Cookie"] = "a=1"
+                if path.startswith("/gz") and "gzip" in (self.headers.get("Accept-Encoding") or ""):
+                    body = gzip.compress(body)
+                    headers["Content-Encoding"] = "gzip"
+                if path.startswith("/chunked"):
+                    self.send_response(code)
+                    for k, v in headers.items():
+                        self.send_header(k, v)
+                    self.send_header("Transfer-Encoding", "chunked")
+                    self.end_headers()
+                    if not head:
+                        for i in range(0, len(body), 100):
+                            part = body[i : i + 100]
+                            self.wfile.write(b"%x\r\n" % len(part) + part + b"\r\n")
+                        self.wfile.write(b"0\r\n\r\n")
+                    return
+                self.send_response(code)
+                for k, v in headers.items():
+                    self.send_header(k, v)
+                self.send_header("Content-Length", str(len(body)))
+                if not keep_alive:
+                    self.send_header("Connection", "close")
+                self.end_headers()
+                if not head:
+                    self.wfile.write(body)
+
+            def do_GET(self):
+                self._reply(False)
+
+            def do_HEAD(self):
+                self._reply(True)
+
+            def do_POST(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                data = self.rfile.read(n)
+                with outer.lock:
+                    outer.hits["POST " + self.path] += 1
+                body = b"posted " + data
+                self.send_response(200)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        class S(ThreadingHTTPServer):
+            daemon_threads = True
+            allow_reuse_address = True
+
+        self._srv = S(("127.0.0.1", port), H)
+        self.port = self._srv.server_address[1]
+        self._th = threading.Thread(target=self._srv.serve_forever, daemon=True)
+
+    def start(self) -> "Origin":
+        self._th.start()
+        return self
+
+    def stop(self) -> None:
+        self._srv.shutdown()
+        self._srv.server_close()

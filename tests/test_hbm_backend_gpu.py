@@ -1,0 +1,67 @@
+"""The HBM cache behind the proxy and the memcached-protocol node (GPU only)."""
+import time
+
+import pytest
+
+from shellac_amd.server.cached import CacheNode
+from shellac_amd.server.proxy import Server, make_backend
+from shellac_amd.utils.fakemc import MemcacheClient
+from shellac_amd.utils.httpclient import HttpClient
+from shellac_amd.utils.origin import Origin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hbm():
+    return make_backend("hbm", gpus=[0], hbm_gb=1.0, batch_us=20)
+
+
+def _wait_get(be, key, timeout=3.0):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        r = be.get(key)
+        if r is not None:
+            return r
+        time.sleep(0.01)
+    return None
+
+
+def test_hbm_backend_roundtrip(hbm):
+    assert hbm.name == "hbm"
+    hbm.set(b"/gpu/a", b"A" * 5000, 3, 0)
+    hbm.set(b"/gpu/b", b"", 0, 0)
+    assert _wait_get(hbm, b"/gpu/a") == (b"A" * 5000, 3)
+    assert _wait_get(hbm, b"/gpu/b") == (b"", 0)
+    assert hbm.get(b"/gpu/none") is None
+    assert hbm.delete(b"/gpu/a") is True
+    assert hbm.get(b"/gpu/a") is None
+    st = hbm.stats()
+    assert st["hbm_gpus"] == 1 and st["hbm_batches"] >= 1
+
+
+def test_hbm_cache_node_over_memcached_protocol(hbm):
+    with CacheNode(backend=hbm, port=0, threads=2) as node:
+        c = MemcacheClient(port=node.port)
+        for i in range(200):
+            c.set(b"n%d" % i, b"v%d" % i * 10, flags=i)
+        got = c.get_multi([b"n%d" % i for i in range(200)])
+        assert len(got) == 200 and got[b"n7"] == b"v7" * 10
+        assert c.get(b"n9") == (b"v9" * 10, 9)
+
+
+def test_proxy_with_hbm_backend(hbm):
+    o = Origin(body_bytes=3000).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend=hbm, threads=2) as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/hbm/{i}" for i in range(50)]
+            first = [c.get(p).body().read() for p in paths]
+            time.sleep(0.2)
+            rs = c.pipeline(paths)
+            assert [r.body().read() for r in rs] == first
+            assert all(o.hits[p] == 1 for p in paths)
+            st = px.stats()
+            assert st["cache_hits"] >= 50 and st["backend"] == "hbm"
+    finally:
+        o.stop()

@@ -1,0 +1,276 @@
+"""End-to-end proxy tests (CPU): native reactor + upstream pool + cache backends.
+
+The reference has no integration tests at all; these cover the
+request/response paths (Server.py:302-440), pipelining order, keep-alive policy,
+teardown, /kill, the distributed cache over the memcached binary protocol, and
+cache-node failure."""
+import json
+import socket
+import threading
+import time
+
+import pytest
+
+from shellac_amd.server.cached import CacheNode
+from shellac_amd.server.proxy import Server, make_backend
+from shellac_amd.utils.fakemc import FakeMemcached, MemcacheClient
+from shellac_amd.utils.httpclient import HttpClient
+from shellac_amd.utils.origin import Origin
+
+
+@pytest.fixture
+def origin():
+    o = Origin(body_bytes=2000).start()
+    yield o
+    o.stop()
+
+
+def make_proxy(origin_ports, **kw):
+    kw.setdefault("backend_kind", "dram")
+    kw.setdefault("dram_mb", 64)
+    srv = Server([("127.0.0.1", p) for p in origin_ports], port=0, **kw).start()
+    return srv
+
+
+def test_miss_then_hit(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        r1 = c.get("/page.html")
+        assert r1.status() == 200 and b"/page.html #1" in r1.body().read()
+        assert r1.headers()["server"].startswith("Shellac")
+        assert r1.headers()["connection"] == "keep-alive"
+        assert r1.headers()["keep-alive"] == "timeout=5, max=100"
+        r2 = c.get("/page.html")
+        assert b"/page.html #1" in r2.body().read()  # served from cache
+        assert origin.hits["/page.html"] == 1
+        st = px.stats()
+        assert st["cache_hits"] == 1 and st["cache_misses"] == 1 and st["requests"] == 2
+
+
+def test_pipelined_order_mixed_hits_and_misses(origin):
+    with make_proxy([origin.port], threads=2) as px:
+        c = HttpClient(port=px.port)
+        c.get("/a")  # warm /a
+        paths = ["/a", "/b", "/a", "/c", "/b", "/d"]
+        rs = c.pipeline(paths)
+        bodies = [r.body().read() for r in rs]
+        for p, b in zip(paths, bodies):
+            assert f"<html>{p} #".encode() in b, (p, b[:40])
+        assert origin.hits["/a"] == 1 and origin.hits["/b"] == 1
+
+
+def test_gzip_passthrough_and_accept_encoding_forced(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        r = c.get("/gzpage")  # origin gzips because the proxy forces Accept-Encoding: gzip
+        assert r.headers().get("content-encoding") == "gzip"
+        assert b"/gzpage #1" in r.body().read()  # client parser inflates
+        r = c.get("/gzpage")
+        assert b"/gzpage #1" in r.body().read()
+
+
+def test_chunked_upstream_dechunked(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        r = c.get("/chunked/x")
+        assert "transfer-encoding" not in r.headers()
+        assert int(r.headers()["content-length"]) == len(r.body().read())
+        assert c.get("/chunked/x").body().read() == r.body().getvalue()
+        assert origin.hits["/chunked/x"] == 1
+
+
+def test_rfc_policy_does_not_cache_post_nostore_cookie_errors(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        for _ in range(2):
+            assert c.get("/echo", method="POST", body=b"hi").body().read() == b"posted hi"
+            c.get("/nocache/1")
+            c.get("/cookie/1")
+            c.get("/status/500")
+        assert origin.hits["POST /echo"] == 2
+        assert origin.hits["/nocache/1"] == 2
+        assert origin.hits["/cookie/1"] == 2
+        assert origin.hits["/status/500"] == 2
+        c.get("/status/404")
+        c.get("/status/404")
+        assert origin.hits["/status/404"] == 1  # negative caching of 404
+
+
+def test_reference_policy_caches_everything(origin):
+    with make_proxy([origin.port], policy="reference") as px:
+        c = HttpClient(port=px.port)
+        c.get("/status/500")
+        c.get("/status/500")
+        assert origin.hits["/status/500"] == 1
+
+
+def test_head_request(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        r = c.get("/h", method="HEAD")
+        assert r.status() == 200 and r.body().read() == b""
+        assert int(r.headers()["content-length"]) > 2000
+        r = c.get("/h")
+        assert len(r.body().read()) > 2000
+
+
+def test_connection_close_and_http10(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        r = c.get("/x", headers={"Connection": "close"})
+        assert r.status() == 200
+        assert c.closed_by_peer()
+        s = socket.create_connection(("127.0.0.1", px.port))
+        s.sendall(b"GET /x HTTP/1.0\r\n\r\n")
+        data = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        assert data.startswith(b"HTTP/1.1 200")
+
+
+def test_client_max_requests(origin):
+    with make_proxy([origin.port], client_max_reqs=3) as px:
+        c = HttpClient(port=px.port)
+        for _ in range(3):
+            assert c.get("/m").status() == 200
+        assert c.closed_by_peer()
+
+
+def test_idle_client_gc(origin):
+    with make_proxy([origin.port], client_timeout=1) as px:
+        c = HttpClient(port=px.port)
+        c.get("/g")
+        time.sleep(2.5)
+        assert c.closed_by_peer()
+        assert px.stats()["gc_closed"] >= 1
+
+
+def test_bad_request_gets_400(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        c.send(b"NONSENSE\r\n\r\n")
+        r = c.read_response()
+        assert r.status() == 400
+
+
+def test_stats_endpoint(origin):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        c.get("/s")
+        r = c.get("/_shellac/stats")
+        st = json.loads(r.body().read())
+        assert st["requests"] >= 1 and st["backend"] == "dram"
+        assert "p99" in st["latency_us"]
+
+
+def test_kill_switch(origin):
+    px = make_proxy([origin.port])
+    c = HttpClient(port=px.port)
+    c.send(HttpClient.request_bytes("/kill"))
+    deadline = time.time() + 5
+    while px.running() and time.time() < deadline:
+        time.sleep(0.05)
+    assert not px.running()
+    px.stop()
+
+
+def test_upstream_down_then_failover():
+    dead = socket.socket()
+    dead.bind(("127.0.0.1", 0))
+    dead_port = dead.getsockname()[1]
+    dead.close()  # nothing listens here
+    o = Origin().start()
+    try:
+        with make_proxy([dead_port, o.port], balance="roundrobin") as px:
+            c = HttpClient(port=px.port)
+            for i in range(6):
+                r = c.get(f"/f{i}")
+                assert r.status() == 200, r.status()
+    finally:
+        o.stop()
+
+
+def test_no_upstream_available_503():
+    dead = socket.socket()
+    dead.bind(("127.0.0.1", 0))
+    port = dead.getsockname()[1]
+    dead.close()
+    with make_proxy([port]) as px:
+        c = HttpClient(port=px.port)
+        assert c.get("/z").status() in (502, 503)
+
+
+def test_non_keepalive_upstream_does_not_kill_client():
+    o = Origin(keep_alive=False).start()
+    try:
+        with make_proxy([o.port]) as px:
+            c = HttpClient(port=px.port)
+            rs = c.pipeline(["/k1", "/k2", "/k3"])
+            assert [r.status() for r in rs] == [200, 200, 200]
+            assert b"/k3" in rs[2].body().read()
+    finally:
+        o.stop()
+
+
+def test_load_balancing_spreads_over_upstreams():
+    a, b = Origin().start(), Origin().start()
+    try:
+        with make_proxy([a.port, b.port], balance="roundrobin", backend_kind="none") as px:
+            clients = [HttpClient(port=px.port) for _ in range(8)]  # concurrent: 8 upstream conns
+            for i, c in enumerate(clients):
+                c.get(f"/lb{i}")
+            assert sum(a.hits.values()) == 4 and sum(b.hits.values()) == 4
+            for c in clients:
+                c.close()
+    finally:
+        a.stop()
+        b.stop()
+
+
+def test_distributed_cache_over_memcached_protocol(origin):
+    """Two proxies share one logical cache spread over two cache nodes (ketama)."""
+    n1 = CacheNode(port=0, kind="dram", dram_mb=64).start()
+    n2 = CacheNode(port=0, kind="dram", dram_mb=64).start()
+    try:
+        caches = [("127.0.0.1", n1.port), ("127.0.0.1", n2.port)]
+        with make_proxy([origin.port], backend_kind="memcached", caches=caches) as pa, \
+                make_proxy([origin.port], backend_kind="memcached", caches=caches) as pb:
+            ca, cb = HttpClient(port=pa.port), HttpClient(port=pb.port)
+            paths = [f"/shared/{i}" for i in range(20)]
+            for p in paths:
+                ca.get(p)
+            time.sleep(0.3)  # SETs are fire-and-forget
+            for p in paths:
+                assert f"<html>{p} #1".encode() in cb.get(p).body().read()
+            assert all(origin.hits[p] == 1 for p in paths)
+            # both nodes hold part of the key space
+            s1 = MemcacheClient(port=n1.port).stats()
+            s2 = MemcacheClient(port=n2.port).stats()
+            assert int(s1["cache_set_ops"]) > 0 and int(s2["cache_set_ops"]) > 0
+    finally:
+        n1.stop()
+        n2.stop()
+
+
+def test_memcached_client_against_fake_and_node_failure(origin):
+    f1, f2 = FakeMemcached().start(), FakeMemcached().start()
+    try:
+        with make_proxy([origin.port], backend_kind="memcached",
+                        caches=[("127.0.0.1", f1.port), ("127.0.0.1", f2.port)]) as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/mf/{i}" for i in range(10)]
+            for p in paths:
+                c.get(p)
+            time.sleep(0.3)
+            assert len(f1.data) + len(f2.data) == 10
+            for p in paths:
+                c.get(p)
+            assert all(origin.hits[p] == 1 for p in paths)
+            f1.stop()  # a cache node dies: requests still succeed (misses go upstream)
+            for p in paths:
+                assert c.get(p).status() == 200
+    finally:
+        f2.stop()
