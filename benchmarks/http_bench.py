@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""HTTP-level parity benchmark (BASELINE.md metrics 1, 2 and 4).
+
+Starts an origin, a shellac_amd proxy (in-process native reactors) with the
+chosen cache backend, warms the cache, then drives keep-alive gzip clients with
+the native ab-equivalent load generator:
+
+  * cache-hit RPS + p50/p99 latency at 10 and 1000 concurrent connections
+    (the reference's README graphs: `ab -k -n 10000 -c 1000 -H "Accept-Encoding: gzip"`);
+  * cache-miss RPS against the local origin (unique URLs);
+  * peak RSS of the process.
+
+Writes one JSON document (stdout or --out). Example:
+  python benchmarks/http_bench.py --backend hbm --threads 8 --out profiles/http_hbm.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import resource
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from shellac_amd.bench.ab import run  # noqa: E402
+from shellac_amd.server.proxy import Server, make_backend  # noqa: E402
+from shellac_amd.utils.origin import Origin  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", choices=["dram", "hbm", "none"], default="dram")
+    ap.add_argument("--threads", type=int, default=4, help="proxy reactor threads")
+    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--objects", type=int, default=1000)
+    ap.add_argument("--body", type=int, default=4096, help="origin body bytes (before gzip)")
+    ap.add_argument("--requests", type=int, default=200000)
+    ap.add_argument("--miss-requests", type=int, default=5000)
+    ap.add_argument("--depth", type=int, default=1)
+    ap.add_argument("--hbm-gb", type=float, default=4.0)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+
+    origin = Origin(body_bytes=a.body).start()
+    backend = None if a.backend == "none" else make_backend(
+        a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
+                                                                       "batch_us": 20}))
+    px = Server([("127.0.0.1", origin.port)], port=0, backend=backend, threads=a.threads,
+                client_max_reqs=1 << 30).start()
+    url = f"http://127.0.0.1:{px.port}"
+    hdr = ["Accept-Encoding: gzip"]
+    paths = [f"/gz/obj{i}.html" for i in range(a.objects)]
+    out = {"backend": a.backend, "proxy_threads": a.threads, "objects": a.objects,
+           "body_bytes": a.body, "cpu_count": os.cpu_count()}
+    # warm the cache (every object fetched once from the origin)
+    run(url, len(paths), 8, True, hdr, 1, 1, paths=paths)
+    time.sleep(0.5)
+    for conc in (10, 1000):
+        r = run(url, a.requests, conc, True, hdr, a.depth, a.client_threads, paths=paths)
+        out[f"hit_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
+        print(f"[http] hit c={conc}: {r['rps']:.0f} rps p50 {r['latency_ms']['p50']:.3f} ms "
+              f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
+    miss_paths = [f"/miss/{i}" for i in range(a.miss_requests)]
+    r = run(url, a.miss_requests, 10, True, hdr, 1, 1, paths=miss_paths)
+    out["miss_c10"] = {k: v for k, v in r.items() if not k.startswith("_")}
+    print(f"[http] miss c=10: {r['rps']:.0f} rps (origin-bound)", file=sys.stderr)
+    out["proxy_stats"] = px.stats()
+    out["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+    px.stop()
+    origin.stop()
+    js = json.dumps(out, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+"""``shellac-ab``: ApacheBench-style driver for the native load generator.
+
+Mirrors the reference's benchmark invocation (benchmarks/run-shellac.sh:
+``ab -k -n 400 -c 10 -g shellac.dat -H "Accept-Encoding: gzip" http://127.0.0.1:8080/``)
+and adds pipelining depth, worker threads and percentile output. ``-g`` writes an
+ab-compatible gnuplot TSV (column 9 = ttime in ms, as benchmarks/requests.p plots).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from typing import Optional, Sequence
+from urllib.parse import urlparse
+
+import numpy as np
+
+from .._native import core
+
+
+def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool = True,
+        headers: Sequence[str] = (), depth: int = 1, threads: int = 1,
+        paths: Optional[Sequence[str]] = None, method: str = "GET", timeout_s: float = 120.0) -> dict:
+    u = urlparse(url)
+    host = u.hostname or "127.0.0.1"
+    port = u.port or 80
+    path = u.path or "/"
+    if u.query:
+        path += "?" + u.query
+    res = core().run_load(host, port, list(paths) if paths else [path], int(requests),
+                          int(concurrency), int(depth), int(threads), bool(keepalive),
+                          list(headers), method, float(timeout_s))
+    lat = np.asarray(res["latency"]) * 1e3
+    done = int(res["completed"])
+    el = float(res["elapsed_s"])
+    out = {
+        "completed": done,
+        "elapsed_s": el,
+        "rps": done / el if el > 0 else 0.0,
+        "transfer_MBps": res["bytes"] / el / 1e6 if el > 0 else 0.0,
+        "errors": int(res["errors"]),
+        "non2xx": int(res["non2xx"]),
+        "reconnects": int(res["reconnects"]),
+        "latency_ms": {
+            "mean": float(lat.mean()) if done else 0.0,
+            "p50": float(np.percentile(lat, 50)) if done else 0.0,
+            "p90": float(np.percentile(lat, 90)) if done else 0.0,
+            "p99": float(np.percentile(lat, 99)) if done else 0.0,
+            "max": float(lat.max()) if done else 0.0,
+        },
+        "_start": res["start"],
+        "_latency": res["latency"],
+        "_status": res["status"],
+    }
+    return out
+
+
+def write_gnuplot(path: str, result: dict, t0: float) -> None:
+    """ab -g format: starttime seconds ctime dtime ttime wait (ttime in column 9 ms)."""
+    with open(path, "w") as f:
+        f.write("starttime\tseconds\tctime\tdtime\tttime\twait\n")
+        for s, l in zip(result["_start"], result["_latency"]):
+            ts = t0 + float(s)
+            ms = int(round(float(l) * 1e3))
+            f.write(f"{time.strftime('%a %b %d %H:%M:%S %Y', time.localtime(ts))}\t{int(ts)}\t0\t{ms}\t{ms}\t{ms}\n")
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    p = argparse.ArgumentParser(prog="shellac-ab", description="ab-style HTTP load generator (native)")
+    p.add_argument("-n", type=int, default=1000, help="number of requests")
+    p.add_argument("-c", type=int, default=10, help="concurrency (connections)")
+    p.add_argument("-k", action="store_true", help="HTTP keep-alive")
+    p.add_argument("-g", default=None, help="gnuplot TSV output")
+    p.add_argument("-H", action="append", default=[], help="extra header 'Name: value'")
+    p.add_argument("--depth", type=int, default=1, help="pipelined requests per connection")
+    p.add_argument("--threads", type=int, default=1)
+    p.add_argument("--json", action="store_true")
+    p.add_argument("url")
+    a = p.parse_args(argv)
+    t0 = time.time()
+    r = run(a.url, a.n, a.c, a.k, a.H, a.depth, a.threads)
+    if a.g:
+        write_gnuplot(a.g, r, t0)
+    pub = {k: v for k, v in r.items() if not k.startswith("_")}
+    if a.json:
+        print(json.dumps(pub))
+    else:
+        print(f"Complete requests:      {pub['completed']}")
+        print(f"Failed requests:        {pub['errors']} (non-2xx {pub['non2xx']})")
+        print(f"Time taken for tests:   {pub['elapsed_s']:.3f} seconds")
+        print(f"Requests per second:    {pub['rps']:.2f} [#/sec] (mean)")
+        print(f"Transfer rate:          {pub['transfer_MBps']:.2f} MB/s")
+        lm = pub["latency_ms"]
+        print(f"Latency (ms):           mean {lm['mean']:.3f}  p50 {lm['p50']:.3f}  "
+              f"p90 {lm['p90']:.3f}  p99 {lm['p99']:.3f}  max {lm['max']:.3f}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

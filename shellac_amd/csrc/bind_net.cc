@@ -7,6 +7,8 @@
 #include "backend.h"
 #include "bind_parts.h"
 #include "ketama.h"
+#include "loadgen.h"
+#include <pybind11/numpy.h>
 #include "mcserver.h"
 #include "proxy.h"
 
@@ -68,6 +70,54 @@ bool blocking_del(CacheBackend* be, const std::string& key) {
 }  // namespace
 
 void bind_net(py::module_& m) {
+  m.def("run_load", [](const std::string& host, uint16_t port, std::vector<std::string> paths,
+                       int64_t requests, int concurrency, int depth, int threads, bool keepalive,
+                       std::vector<std::string> headers, const std::string& method,
+                       double timeout_s) {
+    LoadConfig c;
+    c.host = host;
+    c.port = port;
+    c.paths = std::move(paths);
+    c.requests = requests;
+    c.concurrency = concurrency;
+    c.depth = depth;
+    c.threads = threads;
+    c.keepalive = keepalive;
+    c.headers = std::move(headers);
+    c.method = method;
+    c.timeout_s = timeout_s;
+    LoadResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = run_load(c);
+    }
+    const size_t n = r.samples.size();
+    py::array_t<double> start(n), lat(n);
+    py::array_t<int32_t> status(n);
+    auto ps = start.mutable_unchecked<1>();
+    auto pl = lat.mutable_unchecked<1>();
+    auto pst = status.mutable_unchecked<1>();
+    for (size_t i = 0; i < n; ++i) {
+      ps(i) = r.samples[i].start;
+      pl(i) = r.samples[i].latency;
+      pst(i) = r.samples[i].status;
+    }
+    py::dict d;
+    d["completed"] = r.completed;
+    d["elapsed_s"] = r.elapsed_s;
+    d["bytes"] = r.bytes;
+    d["errors"] = r.errors;
+    d["non2xx"] = r.non2xx;
+    d["reconnects"] = r.reconnects;
+    d["start"] = start;
+    d["latency"] = lat;
+    d["status"] = status;
+    return d;
+  }, py::arg("host"), py::arg("port"), py::arg("paths"), py::arg("requests"),
+     py::arg("concurrency"), py::arg("depth") = 1, py::arg("threads") = 1,
+     py::arg("keepalive") = true, py::arg("headers") = std::vector<std::string>{},
+     py::arg("method") = "GET", py::arg("timeout_s") = 60.0);
+
   m.def("md5_hex", [](py::bytes b) { return md5_hex(std::string(b)); });
 
   py::class_<KetamaRing>(m, "KetamaRing")

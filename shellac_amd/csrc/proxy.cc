@@ -423,7 +423,33 @@ void Reactor::on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v) {
   forward(c, s);
 }
 
+// The last response on a connection announces the close (cached objects carry
+// "Connection: keep-alive" from the fill, Server.py:414-415).
+static Bytes with_connection_close(const Bytes& obj) {
+  const size_t eoh = obj->find("\r\n\r\n");
+  if (eoh == std::string::npos) return obj;
+  std::string head = obj->substr(0, eoh + 2);
+  std::string out;
+  out.reserve(obj->size() + 8);
+  size_t pos = 0;
+  while (pos < head.size()) {
+    size_t e = head.find("\r\n", pos);
+    if (e == std::string::npos) e = head.size();
+    const std::string line = head.substr(pos, e - pos);
+    const std::string low = to_lower(line.substr(0, line.find(':')));
+    if (pos == 0 || (low != "connection" && low != "keep-alive")) {
+      out += line;
+      out += "\r\n";
+    }
+    pos = e + 2;
+  }
+  out += "Connection: close\r\n\r\n";
+  out.append(*obj, eoh + 4, std::string::npos);
+  return std::make_shared<const std::string>(std::move(out));
+}
+
 void Reactor::complete_slot(Client* c, Slot* s, Bytes data) {
+  if (s->close_after && data) data = with_connection_close(data);
   s->out.write_shared(std::move(data));
   s->out.close();
   s->ready = true;

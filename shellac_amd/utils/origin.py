@@ -18,6 +18,7 @@ class Origin:
 
         class H(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1" if keep_alive else "HTTP/1.0"
+            disable_nagle_algorithm = True
 
             def log_message(self, *a):
                 pass
