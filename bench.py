@@ -50,6 +50,11 @@ def parse():
     ap.add_argument("--min-val", type=int, default=64)
     ap.add_argument("--max-val", type=int, default=4096)
     ap.add_argument("--log-gb", type=float, default=16.0, help="value-log GiB per shard")
+    ap.add_argument("--set-dist", choices=["uniform", "zipf"], default="uniform",
+                    help="SET popularity: uniform (TTL refresh fills, default) or zipf")
+    ap.add_argument("--replicate", type=int, default=65536,
+                    help="hot objects replicated on every rank (N>1; 0 = off)")
+    ap.add_argument("--replica-gb", type=float, default=1.0)
     ap.add_argument("--no-smoke", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
@@ -115,7 +120,14 @@ def main():
         nb *= 2
     log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
     shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)
-    sc = ShardedCache(shard)
+    replica = None
+    if world > 1 and args.replicate > 0:
+        rnb = 1
+        while rnb * 2 < args.replicate:
+            rnb *= 2
+        replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
+                             max_item=1 << 20, device=dev)
+    sc = ShardedCache(shard, replica=replica)
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
@@ -132,7 +144,12 @@ def main():
     P = 4
     gets = [wl.digests.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
             for i in range(P)]
-    sets = [wl.set_batch(wl.sample_ids(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
+    pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
+    sets = [wl.set_batch(pick(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
+    if replica is not None:
+        # hot-object replica tier from the observed request stream (periodic in a server)
+        nrep = sc.refresh_replica(args.replicate, keys=torch.cat(gets))
+        log(rank, f"[bench] replicated {nrep} hot objects on every rank")
     shard.reserve(max(args.sets * 2, chunk))
     before = shard.counters()
 
@@ -208,8 +225,11 @@ def main():
             "zipf_s": args.zipf,
             "value_bytes": [args.min_val, args.max_val],
             "log_gib_per_shard": args.log_gb,
+            "set_dist": args.set_dist,
+            "replicated_hot_objects": args.replicate if world > 1 else 0,
         },
         "get_hit_ratio": round(hits / max(gops, 1), 4),
+        "replica_hit_fraction": round(sc.stats["replica_hits"] / max(sc.stats["get_requests"], 1), 4),
         "get_value_GBps": round(gbytes / elapsed / 1e9, 2),
         "smoke": sm,
     }

@@ -79,10 +79,17 @@ class Workload:
                         & ~15).to(dev)
 
     def sample_ids(self, n: int, seed: int) -> torch.Tensor:
+        """Zipf(s)-popular object ids (GET traffic)."""
         g = torch.Generator(device=self.device).manual_seed(seed)
         r = torch.rand(n, generator=g, dtype=torch.float64, device=self.device)
         idx = torch.searchsorted(self.cdf, r).clamp_(max=self.total_keys - 1)
         return self.rank_to_id.index_select(0, idx)
+
+    def uniform_ids(self, n: int, seed: int) -> torch.Tensor:
+        """Uniform object ids (cache-fill / refresh SET traffic: in a TTL cache every
+        requested object is refetched about once per TTL, independent of popularity)."""
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        return torch.randint(0, self.total_keys, (n,), generator=g, device=self.device)
 
     def set_batch(self, ids: torch.Tensor, ttl_expire: int = 0):
         from ..models.sharded_cache import SetBatch

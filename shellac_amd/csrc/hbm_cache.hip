@@ -320,12 +320,14 @@ __global__ __launch_bounds__(kBlock) void k_segcopy(
 // ---------------------------------------------------------------------------------
 // SET
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vlen, int64_t n,
                                                        unsigned long long* __restrict__ tk,
                                                        int* __restrict__ tw, uint32_t tmask,
                                                        uint32_t* __restrict__ slot_of) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
+    if (vlen[i] == kSkipVlen) { slot_of[i] = 0; continue; }
     const unsigned long long key = keys[i].lo ? keys[i].lo : 1ull;
     uint32_t s = (uint32_t)fmix64(key) & tmask;
     for (uint32_t probe = 0; probe <= tmask; ++probe) {
@@ -350,6 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i <= n;
        i += (int64_t)gridDim.x * kBlock) {
     if (i == n) { size[n] = 0; continue; }
+    if (vlen[i] == kSkipVlen) { size[i] = 0; continue; }  // row addressed to another tier
     const bool win = tw[slot_of[i]] == (int)i && vlen[i] <= max_item;
     size[i] = win ? item_bytes(vlen[i]) : 0;
     ++ops;
@@ -815,7 +818,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
   HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
   const int grid = grid_for(n, kBlock, kMaxGrid);
-  hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, n,
+  hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
   hipLaunchKernelGGL(k_set_size, dim3(grid_for(n + 1, kBlock, kMaxGrid)), dim3(kBlock), 0, s, vlen, n,
                      dd_win_, dd_slot_, cfg_.max_item, set_size_, ctr_);

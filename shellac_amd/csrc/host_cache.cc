@@ -129,10 +129,12 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
   // last write of a key in the batch wins (dedupe on digest.lo, as on the device)
   std::unordered_map<uint64_t, int64_t> last;
   last.reserve((size_t)n * 2);
-  for (int64_t i = 0; i < n; ++i) last[keys[i].lo ? keys[i].lo : 1] = i;
+  for (int64_t i = 0; i < n; ++i)
+    if (vlen[i] != kSkipVlen) last[keys[i].lo ? keys[i].lo : 1] = i;
   std::vector<uint64_t> sz((size_t)n);
   uint64_t total = 0;
   for (int64_t i = 0; i < n; ++i) {
+    if (vlen[i] == kSkipVlen) { sz[i] = 0; continue; }
     ctr_.set_ops++;
     const bool win = last[keys[i].lo ? keys[i].lo : 1] == i && vlen[i] <= max_item_;
     sz[i] = win ? item_bytes(vlen[i]) : 0;

@@ -27,6 +27,8 @@ constexpr uint32_t kBucketBytes = 128;
 constexpr uint32_t kItemHeaderBytes = 32;
 constexpr uint32_t kItemMagic = 0x5348a11cu;
 constexpr uint64_t kMissLoc = ~0ULL;
+// vlen sentinel: "this SET row is not for this tier" (skipped, not counted).
+constexpr uint32_t kSkipVlen = 0xFFFFFFFFu;
 
 struct alignas(32) Entry {
   uint64_t d0;      // digest.lo

@@ -6,12 +6,21 @@ entire cluster" (README.md:12, :30) built from ketama-sharded memcached nodes
 ``CacheShard`` (its GPU's HBM), a ``ShardRing`` assigns digests to ranks, and a
 serving step moves whole request batches with RCCL all-to-alls:
 
-  GET:  route (k_route) -> group by owner (k_scatter + k_permute) -> a2a digests
-        -> owner probe + scan (k_probe, hipcub) -> a2a sizes -> owner gather
-        (k_segcopy, straight into the a2a send buffer) -> a2a values.
-  SET:  route -> group -> pack payloads by owner (k_segcopy) -> a2a digests,
-        metadata, payloads -> owner store (dedupe, scan-allocate, log write,
-        CAS insert).
+  GET:  [replica probe] -> route (k_route) -> group by owner (k_scatter,
+        k_permute) -> a2a digests -> owner probe + scan (k_probe, hipcub) ->
+        a2a sizes -> owner gather (k_segcopy, straight into the a2a send
+        buffer) -> a2a values into the caller's response buffer.
+  SET:  route (+ fan-out of replicated keys to every rank) -> group -> pack
+        payloads (k_segcopy) -> a2a digests, metadata, payloads -> owner store
+        (dedupe, scan-allocate, log write, CAS insert) / replica store.
+
+Hot-object replication (SURVEY.md §5.8 "hot-key broadcast"): Zipf-popular
+objects are copied into a small per-rank *replica* shard so their GETs never
+leave the GPU. ``refresh_replica`` picks the global top-k keys from recent
+request samples (one all_gather of candidates + one routed GET). Consistency is
+write-through with no extra collective: a SET for a replicated key is fanned out
+by the same all-to-all to its owner (main shard) and to every other rank
+(replica shard), so a GET issued after a SET step never sees the old value.
 
 Two host syncs per phase (the split sizes all_to_all_single needs) and no
 per-request host work. With one rank every step is purely local.
@@ -19,14 +28,19 @@ per-request host work. With one rank every step is purely local.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional
 
 import torch
+import torch.distributed as dist
 
-from ..ops.cache import CacheShard, Lookup
 from ..ops import routing as R
-from ..parallel.exchange import all_to_all_rows, dist_info, exchange_counts, segment_sums
+from ..ops.cache import CacheShard
+from ..parallel.exchange import (all_to_all_rows, allreduce_stats, dist_info, exchange_counts,
+                                 segment_sums)
 from ..parallel.ring import ShardRing
+
+SKIP_VLEN = -1  # int32 view of the kSkipVlen sentinel (row not for this tier)
+HDR_WORDS = 8   # ItemHeader = 8 x u32: d0 lo/hi, d1 lo/hi, vlen, flags, expire, magic
 
 
 @dataclass
@@ -54,21 +68,57 @@ class SetBatch:
     expire: Optional[torch.Tensor] = None  # int32 [n]
 
 
+def records_to_set_batch(keys: torch.Tensor, res: GetResult) -> SetBatch:
+    """Turn GET records back into a SET batch (replica fill, shard migration).
+    Misses become skip rows."""
+    words = res.data[: res.data.numel() // 4 * 4].view(torch.int32)
+    hit = res.size > 0
+    base = torch.where(hit, torch.div(res.off, 4, rounding_mode="floor"), torch.zeros_like(res.off))
+    v = words.index_select(0, base + 4)
+    vlen = torch.where(hit, v, torch.full_like(v, SKIP_VLEN))
+    flags = words.index_select(0, base + 5)
+    expire = words.index_select(0, base + 6)
+    val_off = torch.where(hit, res.off + 32, torch.zeros_like(res.off))
+    return SetBatch(keys=keys.contiguous(), values=res.data, val_off=val_off.contiguous(),
+                    vlen=vlen.contiguous(), flags=flags.contiguous(), expire=expire.contiguous())
+
+
 class ShardedCache:
-    def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160):
+    def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
+                 replica: Optional[CacheShard] = None, sample_rows: int = 65536,
+                 sample_batches: int = 8):
         self.shard = shard
         self.group = group
         self.rank, self.world = dist_info(group)
         self.device = shard.device
         self.ring = ShardRing(list(range(self.world)), points_per_shard)
         self.ring_pts, self.ring_own = self.ring.tensors(self.device)
-        self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0}
+        self.replica = replica if self.world > 1 else None
+        self.sample_rows = sample_rows
+        self.sample_batches = sample_batches
+        self._samples: List[torch.Tensor] = []
+        self._hot: Optional[torch.Tensor] = None   # sorted hot digests [h, 2] (same on all ranks)
+        self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
+                      "replica_hits": 0, "replica_refreshes": 0}
 
     # ------------------------------------------------------------------------------
-    def _group_by_owner(self, keys: torch.Tensor):
-        dest, counts = R.route(keys, self.ring_pts, self.ring_own, self.world)
-        perm = R.scatter_positions(dest, counts)
-        return dest, counts, perm
+    def _route(self, keys: torch.Tensor):
+        return R.route(keys, self.ring_pts, self.ring_own, self.world)
+
+    def _sample(self, keys: torch.Tensor) -> None:
+        if self.replica is None:
+            return
+        self._samples.append(keys[: self.sample_rows])
+        if len(self._samples) > self.sample_batches:
+            self._samples.pop(0)
+
+    def _is_hot(self, keys: torch.Tensor) -> torch.Tensor:
+        """Membership of each digest in the replicated hot set (device op, no sync)."""
+        h = self._hot
+        idx = torch.searchsorted(h[:, 0].contiguous(), keys[:, 0].contiguous())
+        idx = torch.clamp(idx, max=h.shape[0] - 1)
+        cand = h.index_select(0, idx)
+        return (cand == keys).all(dim=1)
 
     def get(self, keys: torch.Tensor, now: Optional[int] = None) -> GetResult:
         n = keys.shape[0]
@@ -77,34 +127,63 @@ class ShardedCache:
             lk = self.shard.lookup(keys, now)
             data = self.shard.gather(lk)
             return GetResult(data, lk.off[:n], lk.size[:n])
-
-        _, counts, perm = self._group_by_owner(keys)
+        self._sample(keys)
+        w = self.world
+        dest, _ = self._route(keys)
+        rl = None
+        if self.replica is not None:
+            rl = self.replica.lookup(keys, now)           # local copies of hot objects
+            local = rl.size[:n] > 0
+            dest = torch.where(local, torch.full_like(dest, w), dest)
+        counts = torch.bincount(dest.long(), minlength=w + 1)
+        perm = R.scatter_positions(dest, counts)         # local hits sort to the tail
         send_keys = R.permute(keys, perm)
-        recv_counts = exchange_counts(counts, self.group)
-        both = torch.cat([counts, recv_counts]).cpu()          # sync 1
-        send_rows = both[: self.world].tolist()
-        recv_rows = both[self.world :].tolist()
-        req = all_to_all_rows(send_keys, send_rows, recv_rows, self.group)
+        recv_counts = exchange_counts(counts[:w].contiguous(), self.group)
+        local_total = rl.off[n:n + 1] if rl is not None else torch.zeros(1, dtype=torch.int64,
+                                                                           device=self.device)
+        host = torch.cat([counts, recv_counts, local_total]).cpu()       # sync 1
+        send_rows, n_local = host[:w].tolist(), int(host[w])
+        recv_rows = host[w + 1: 2 * w + 1].tolist()
+        local_bytes = int(host[2 * w + 1])
+        n_remote = n - n_local
+        req = all_to_all_rows(send_keys[:n_remote], send_rows, recv_rows, self.group)
 
         # owner side: probe my shard for everything I received
         lk = self.shard.lookup(req, now)
         m = req.shape[0]
         rc = torch.tensor(recv_rows, dtype=torch.int64, device=self.device)
-        reply_bytes = segment_sums(lk.off, rc)                  # bytes I send back per source
-        got_bytes = exchange_counts(reply_bytes, self.group)    # bytes I receive per owner
-        nbytes = torch.cat([reply_bytes, got_bytes]).cpu()      # sync 2
-        send_b = nbytes[: self.world].tolist()
-        recv_b = nbytes[self.world :].tolist()
-        out = torch.empty(max(int(sum(send_b)), 16), dtype=torch.uint8, device=self.device)
-        self.shard.gather(lk, out)
+        reply_bytes = segment_sums(lk.off, rc)                   # bytes I send back per source
+        got_bytes = exchange_counts(reply_bytes, self.group)     # bytes I receive per owner
+        nbytes = torch.cat([reply_bytes, got_bytes]).cpu()       # sync 2
+        send_b, recv_b = nbytes[:w].tolist(), nbytes[w:].tolist()
+        reply = torch.empty(max(int(sum(send_b)), 16), dtype=torch.uint8, device=self.device)
+        self.shard.gather(lk, reply)
         sizes_back = all_to_all_rows(lk.size[:m], recv_rows, send_rows, self.group)
-        data = all_to_all_rows(out[: int(sum(send_b))], send_b, recv_b, self.group)
-
-        # requester side: sizes_back/data are in grouped (perm) order
+        # response buffer: [local replica hits | remote values]
+        data = torch.empty(local_bytes + int(sum(recv_b)) + 16, dtype=torch.uint8,
+                           device=self.device)
+        if rl is not None and n_local:
+            self.replica.gather(rl, data)
+        dist.all_to_all_single(data[local_bytes: local_bytes + int(sum(recv_b))],
+                               reply[: int(sum(send_b))], output_split_sizes=recv_b,
+                               input_split_sizes=send_b, group=self.group)
+        # requester side: remote sizes arrive in grouped (perm) order
         goff = R.exclusive_scan(sizes_back)
-        size = sizes_back.index_select(0, perm)
-        off = goff.index_select(0, perm)
-        self.stats["remote_gets"] += n - int(send_rows[self.rank])
+        pos = torch.clamp(perm, max=max(n_remote - 1, 0))
+        if n_remote:
+            rsize = sizes_back.index_select(0, pos)
+            roff = goff.index_select(0, pos) + local_bytes
+        else:
+            rsize = torch.zeros(n, dtype=torch.int64, device=self.device)
+            roff = torch.zeros(n, dtype=torch.int64, device=self.device)
+        if rl is not None:
+            local = rl.size[:n] > 0
+            size = torch.where(local, rl.size[:n], rsize)
+            off = torch.where(local, rl.off[:n], roff)
+        else:
+            size, off = rsize, roff
+        self.stats["remote_gets"] += n_remote - int(send_rows[self.rank])
+        self.stats["replica_hits"] += n_local
         return GetResult(data, off, size)
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
@@ -114,57 +193,142 @@ class ShardedCache:
             self.shard.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                              batch.expire, now)
             return
-        dev = self.device
-        _, counts, perm = self._group_by_owner(batch.keys)
-        # metadata records [vlen, flags, expire, 0] as int32x4 (16 B)
+        dev, w = self.device, self.world
+        owner, _ = self._route(batch.keys)
+        # metadata records [vlen, flags, expire, tier] as int32x4 (16 B); tier 1 = replica copy
         meta = torch.zeros((n, 4), dtype=torch.int32, device=dev)
         meta[:, 0] = batch.vlen
         if batch.flags is not None:
             meta[:, 1] = batch.flags
         if batch.expire is not None:
             meta[:, 2] = batch.expire
-        send_keys = R.permute(batch.keys, perm)
+        if self.replica is not None and self._hot is not None:
+            # write-through: a replicated key goes to its owner AND to every other rank
+            hot = self._is_hot(batch.keys)
+            r = torch.arange(w, device=dev, dtype=torch.int32).view(1, w)
+            own = owner.view(n, 1)
+            valid = (r == own) | hot.view(n, 1)
+            dest = torch.where(valid, r.expand(n, w), torch.full((n, w), w, dtype=torch.int32,
+                                                                 device=dev)).reshape(-1)
+            keys = batch.keys.repeat_interleave(w, dim=0)
+            meta = meta.repeat_interleave(w, dim=0)
+            meta[:, 3] = (r != own).reshape(-1).to(torch.int32)
+            val_off = batch.val_off.repeat_interleave(w)
+        else:
+            dest, keys, val_off = owner, batch.keys, batch.val_off
+        counts = torch.bincount(dest.long(), minlength=w + 1)
+        perm = R.scatter_positions(dest, counts)
+        send_keys = R.permute(keys, perm)
         send_meta = R.permute(meta, perm)
-        # pack payloads contiguously in owner order
+        nvalid = keys.shape[0] - counts[w:w + 1]
         padded = (send_meta[:, 0].to(torch.int64) + 15) & ~15
+        padded = torch.where(torch.arange(keys.shape[0], device=dev) < nvalid, padded,
+                             torch.zeros_like(padded))
         dst_off = R.exclusive_scan(padded)
-        src_off = R.permute(batch.val_off.view(-1, 1), perm).view(-1)
-        seg_bytes = segment_sums(dst_off, counts)
-        recv_counts = exchange_counts(counts, self.group)
+        src_off = R.permute(val_off.view(-1, 1), perm).view(-1)
+        seg_bytes = segment_sums(dst_off, counts[:w].contiguous())
+        recv_counts = exchange_counts(counts[:w].contiguous(), self.group)
         recv_bytes = exchange_counts(seg_bytes, self.group)
-        host = torch.cat([counts, recv_counts, seg_bytes, recv_bytes]).cpu()  # sync 1
-        w = self.world
-        send_rows, recv_rows = host[:w].tolist(), host[w : 2 * w].tolist()
-        send_b, recv_b = host[2 * w : 3 * w].tolist(), host[3 * w :].tolist()
+        host = torch.cat([counts[:w], recv_counts, seg_bytes, recv_bytes]).cpu()  # sync 1
+        send_rows, recv_rows = host[:w].tolist(), host[w: 2 * w].tolist()
+        send_b, recv_b = host[2 * w: 3 * w].tolist(), host[3 * w:].tolist()
+        ns = int(sum(send_rows))
         payload = torch.empty(int(sum(send_b)) + 16, dtype=torch.uint8, device=dev)
-        R.segcopy(batch.values, src_off, dst_off, payload)
-        rkeys = all_to_all_rows(send_keys, send_rows, recv_rows, self.group)
-        rmeta = all_to_all_rows(send_meta, send_rows, recv_rows, self.group)
+        R.segcopy(batch.values, src_off[:ns].contiguous(), dst_off[: ns + 1].contiguous(), payload)
+        rkeys = all_to_all_rows(send_keys[:ns], send_rows, recv_rows, self.group)
+        rmeta = all_to_all_rows(send_meta[:ns], send_rows, recv_rows, self.group)
         rvals = torch.empty(int(sum(recv_b)) + 16, dtype=torch.uint8, device=dev)
-        dist_out = rvals[: int(sum(recv_b))]
-        torch.distributed.all_to_all_single(dist_out, payload[: int(sum(send_b))],
-                                            output_split_sizes=recv_b, input_split_sizes=send_b,
-                                            group=self.group)
+        dist.all_to_all_single(rvals[: int(sum(recv_b))], payload[: int(sum(send_b))],
+                               output_split_sizes=recv_b, input_split_sizes=send_b,
+                               group=self.group)
         rvlen = rmeta[:, 0].contiguous()
         roff = R.exclusive_scan((rvlen.to(torch.int64) + 15) & ~15)[:-1].contiguous()
-        self.shard.store(rkeys, rvals, roff, rvlen, rmeta[:, 1].contiguous(),
-                         rmeta[:, 2].contiguous(), now)
+        tier = rmeta[:, 3]
+        skip = torch.full_like(rvlen, SKIP_VLEN)
+        self.shard.store(rkeys, rvals, roff, torch.where(tier == 0, rvlen, skip).contiguous(),
+                         rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
+        if self.replica is not None:
+            self.replica.store(rkeys, rvals, roff, torch.where(tier == 1, rvlen, skip).contiguous(),
+                               rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
 
     def delete(self, keys: torch.Tensor, now: Optional[int] = None) -> torch.Tensor:
-        n = keys.shape[0]
         if self.world == 1:
             return self.shard.remove(keys, now)
-        _, counts, perm = self._group_by_owner(keys)
+        if self.replica is not None:  # replicas are dropped everywhere (collective)
+            cnt = torch.tensor([keys.shape[0]], dtype=torch.int64, device=self.device)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
+            pad = torch.zeros((int(cnt), 2), dtype=keys.dtype, device=self.device)
+            pad[: keys.shape[0]] = keys
+            allk = [torch.empty_like(pad) for _ in range(self.world)]
+            dist.all_gather(allk, pad, group=self.group)
+            self.replica.remove(torch.cat(allk).contiguous(), now)
+        dest, counts = self._route(keys)
+        perm = R.scatter_positions(dest, counts)
         send_keys = R.permute(keys, perm)
         recv_counts = exchange_counts(counts, self.group)
         both = torch.cat([counts, recv_counts]).cpu()
-        send_rows, recv_rows = both[: self.world].tolist(), both[self.world :].tolist()
+        send_rows, recv_rows = both[: self.world].tolist(), both[self.world:].tolist()
         req = all_to_all_rows(send_keys, send_rows, recv_rows, self.group)
         found = self.shard.remove(req, now).to(torch.int32)
         back = all_to_all_rows(found, recv_rows, send_rows, self.group)
         return back.index_select(0, perm).bool()
 
-    def counters(self) -> dict:
-        from ..parallel.exchange import allreduce_stats
+    # ------------------------------------------------------------------------------
+    def refresh_replica(self, top_k: int, keys: Optional[torch.Tensor] = None,
+                        now: Optional[int] = None) -> int:
+        """Collective. Replace the replica tier with the global top-k keys by request
+        frequency (from ``keys`` or the recent GET samples). Returns #objects cached."""
+        if self.replica is None:
+            return 0
+        dev, w = self.device, self.world
+        if keys is None:
+            keys = torch.cat(self._samples) if self._samples else torch.zeros((0, 2), dtype=torch.int64,
+                                                                             device=dev)
+        if keys.shape[0]:
+            uniq, cnt = torch.unique(keys, dim=0, return_counts=True)
+        else:
+            uniq = torch.zeros((0, 2), dtype=torch.int64, device=dev)
+            cnt = torch.zeros(0, dtype=torch.int64, device=dev)
+        k = min(top_k, uniq.shape[0])
+        top = torch.topk(cnt, k).indices if k else cnt[:0]
+        cand = torch.zeros((top_k, 2), dtype=torch.int64, device=dev)
+        ccnt = torch.zeros(top_k, dtype=torch.int64, device=dev)
+        cand[:k] = uniq.index_select(0, top)
+        ccnt[:k] = cnt.index_select(0, top)
+        all_c = [torch.empty_like(cand) for _ in range(w)]
+        all_n = [torch.empty_like(ccnt) for _ in range(w)]
+        dist.all_gather(all_c, cand, group=self.group)
+        dist.all_gather(all_n, ccnt, group=self.group)
+        allc = torch.cat(all_c)
+        alln = torch.cat(all_n)
+        u, inv = torch.unique(allc, dim=0, return_inverse=True)
+        tot = torch.zeros(u.shape[0], dtype=torch.int64, device=dev).scatter_add_(0, inv, alln)
+        valid = tot > 0
+        tot = torch.where(valid, tot, torch.full_like(tot, -1))
+        kk = min(top_k, u.shape[0])
+        hot = u.index_select(0, torch.topk(tot, kk).indices)
+        hot = hot[(hot != 0).any(dim=1)].contiguous()      # drop padding rows (identical everywhere)
+        if hot.shape[0] == 0:
+            self.replica.flush()
+            self._hot = None
+            return 0
+        order = torch.argsort(hot[:, 0])
+        self._hot = hot.index_select(0, order).contiguous()
+        saved = self.replica
+        self.replica = None                               # fetch through the owners only
+        try:
+            res = self.get(hot, now)
+        finally:
+            self.replica = saved
+        self.replica.flush()
+        sb = records_to_set_batch(hot, res)
+        # an owner serves its own keys from its main shard (write-through updates only
+        # non-owner replicas), so owned keys stay out of the local replica
+        owner, _ = self._route(hot)
+        sb.vlen = torch.where(owner == self.rank, torch.full_like(sb.vlen, SKIP_VLEN), sb.vlen)
+        self.replica.store(sb.keys, sb.values, sb.val_off, sb.vlen, sb.flags, sb.expire, now)
+        self.stats["replica_refreshes"] += 1
+        return int((sb.vlen != SKIP_VLEN).sum())
 
+    def counters(self) -> dict:
         return allreduce_stats(self.shard.counters(), self.device, self.group)

@@ -79,3 +79,76 @@ def test_sharded_cache_gloo(world):
     fails = [r for r in results if r[1] != "ok"]
     assert not fails, fails[0][2]
     assert all(r[2] == world * (300 * world + 2) for r in results)
+
+
+def _replica_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+
+        shard = CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu")
+        replica = CacheShard(1 << 20, 1 << 10, 1 << 14, "cpu")
+        sc = ShardedCache(shard, replica=replica)
+        keys = [f"/k{i}".encode() for i in range(400)]
+        if rank == 0:
+            v, vo, vl = pack_values([b"v1-" + k for k in keys])
+            batch = SetBatch(digest_strings(keys), v, vo, vl)
+        else:
+            v, vo, vl = pack_values([])
+            batch = SetBatch(digest_strings([]), v, vo, vl)
+        sc.set(batch)
+        dist.barrier()
+        hot = keys[:20]
+        reqs = digest_strings(hot * 10 + keys[100:120])   # hot keys dominate the sample
+        res = sc.get(reqs)
+        nrep = sc.refresh_replica(20)
+        owned = sum(sc.ring.owner_of_key(k) == rank for k in hot)
+        assert nrep == 20 - owned, (nrep, owned)
+        before = sc.stats["replica_hits"]
+        res = sc.get(digest_strings(keys))
+        got = [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+        assert got == [b"v1-" + k for k in keys]
+        assert sc.stats["replica_hits"] - before == 20 - owned  # hot keys served locally
+        # write-through: rank 1 overwrites hot keys; everybody must see the new values
+        if rank == 1:
+            v, vo, vl = pack_values([b"v2-" + k for k in hot])
+            batch = SetBatch(digest_strings(hot), v, vo, vl)
+        else:
+            v, vo, vl = pack_values([])
+            batch = SetBatch(digest_strings([]), v, vo, vl)
+        sc.set(batch)
+        dist.barrier()
+        res = sc.get(digest_strings(hot))
+        got = [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+        assert got == [b"v2-" + k for k in hot], got[:2]
+        # deletes drop replicas everywhere
+        found = sc.delete(digest_strings(hot[:5] if rank == 0 else []))
+        dist.barrier()
+        res = sc.get(digest_strings(hot[:6]))
+        got = [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+        assert got[:5] == [None] * 5 and got[5] == b"v2-" + hot[5]
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hot_object_replication_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    fails = [r for r in results if r[1] != "ok"]
+    assert not fails, fails[0][2]
