@@ -40,19 +40,21 @@ def main():
     ap.add_argument("--miss-requests", type=int, default=5000)
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--hbm-gb", type=float, default=4.0)
+    ap.add_argument("--l1-mb", type=int, default=0, help="DRAM L1 in front of hbm (0 = off)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
     origin = Origin(body_bytes=a.body).start()
     backend = None if a.backend == "none" else make_backend(
         a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
-                                                                       "batch_us": 20}))
+                                                                       "batch_us": 20,
+                                                                       "l1_mb": a.l1_mb}))
     px = Server([("127.0.0.1", origin.port)], port=0, backend=backend, threads=a.threads,
                 client_max_reqs=1 << 30).start()
     url = f"http://127.0.0.1:{px.port}"
     hdr = ["Accept-Encoding: gzip"]
     paths = [f"/gz/obj{i}.html" for i in range(a.objects)]
-    out = {"backend": a.backend, "proxy_threads": a.threads, "objects": a.objects,
+    out = {"backend": a.backend + (f"+l1:{a.l1_mb}MB" if a.backend == "hbm" and a.l1_mb else ""), "proxy_threads": a.threads, "objects": a.objects,
            "body_bytes": a.body, "cpu_count": os.cpu_count()}
     # warm the cache (every object fetched once from the origin)
     run(url, len(paths), 8, True, hdr, 1, 1, paths=paths)

@@ -62,9 +62,11 @@ uint32_t DramBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
 void DramBackend::get(const std::string&, const Digest& d, Executor*, GetCallback done) {
   std::vector<uint8_t> v;
-  uint32_t flags = 0;
-  if (shard(d).get_one(d, &v, &flags, now())) {
-    done(true, CacheValue{std::make_shared<const std::string>(v.begin(), v.end()), flags});
+  uint32_t flags = 0, expire = 0;
+  const uint32_t t = now();
+  if (shard(d).get_one(d, &v, &flags, t, &expire)) {
+    done(true, CacheValue{std::make_shared<const std::string>(v.begin(), v.end()), flags,
+                          expire ? (int64_t)expire - t : 0});
   } else {
     done(false, CacheValue{});
   }
@@ -368,6 +370,7 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
         if (h.magic == kItemMagic && h.d0 == r.d.lo && h.d1 == r.d.hi) {
           hit = true;
           v.flags = h.flags;
+          v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
           v.data = std::make_shared<const std::string>(
               reinterpret_cast<const char*>(dv.h_out + o + kItemHeaderBytes), h.vlen);
         }
@@ -452,6 +455,72 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_batched_requests", batched_reqs_.load());
   out->emplace_back("hbm_max_batch", max_batch_seen_.load());
   out->emplace_back("hbm_batch_ns_total", batch_ns_.load());
+}
+
+// =====================================================================================
+// Tiered (L1 DRAM + L2)
+// =====================================================================================
+TieredBackend::TieredBackend(std::shared_ptr<CacheBackend> l1, std::shared_ptr<CacheBackend> l2,
+                             uint32_t promote_ttl_s)
+    : l1_(std::move(l1)), l2_(std::move(l2)), promote_ttl_(promote_ttl_s) {
+  SH_CHECK(l1_ && l2_, "tiered backend needs two levels");
+}
+
+void TieredBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
+  auto l2 = l2_;
+  auto l1 = l1_;
+  const uint32_t pttl = promote_ttl_;
+  l1_->get(key, d, ex, [this, key, d, ex, done, l1, l2, pttl](bool hit, CacheValue v) {
+    if (hit) {
+      l1_hits_++;
+      done(true, std::move(v));
+      return;
+    }
+    l2->get(key, d, ex, [this, key, d, done, l1, pttl](bool hit2, CacheValue v2) {
+      if (hit2 && v2.data) {
+        l2_hits_++;
+        if (v2.ttl_left > 0 || v2.ttl_left == 0 || v2.ttl_left == -1) {
+          const uint32_t ttl = v2.ttl_left > 0 ? (uint32_t)v2.ttl_left
+                                               : (v2.ttl_left == 0 ? 0u : pttl);
+          l1->set(key, d, v2.data, v2.flags, ttl);  // promote
+        }
+      } else {
+        misses_++;
+      }
+      done(hit2, std::move(v2));
+    });
+  });
+}
+
+void TieredBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+                        uint32_t ttl_s) {
+  l2_->set(key, d, value, flags, ttl_s);
+  l1_->set(key, d, std::move(value), flags, ttl_s);
+}
+
+void TieredBackend::del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) {
+  auto l2 = l2_;
+  l1_->del(key, d, ex, [key, d, ex, done, l2](bool f1) {
+    l2->del(key, d, ex, [done, f1](bool f2) {
+      if (done) done(f1 || f2);
+    });
+  });
+}
+
+void TieredBackend::flush() {
+  l1_->flush();
+  l2_->flush();
+}
+
+void TieredBackend::stats(StatList* out) {
+  out->emplace_back("tier_l1_hits", l1_hits_.load());
+  out->emplace_back("tier_l2_hits", l2_hits_.load());
+  out->emplace_back("tier_misses", misses_.load());
+  StatList a, b;
+  l1_->stats(&a);
+  l2_->stats(&b);
+  for (auto& kv : a) out->emplace_back("l1_" + kv.first, kv.second);
+  for (auto& kv : b) out->emplace_back("l2_" + kv.first, kv.second);
 }
 
 // =====================================================================================

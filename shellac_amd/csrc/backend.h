@@ -45,6 +45,7 @@ class Executor {
 struct CacheValue {
   Bytes data;
   uint32_t flags = 0;
+  int64_t ttl_left = -1;  // seconds of life left: -1 unknown, 0 never expires
 };
 using GetCallback = std::function<void(bool hit, CacheValue v)>;
 using DelCallback = std::function<void(bool found)>;
@@ -139,6 +140,27 @@ class HbmBackend : public CacheBackend {
   double epoch_;
   std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};
   std::atomic<uint64_t> batch_ns_{0};
+};
+
+// Two-level cache: a small host-DRAM L1 in front of a big L2 (HBM shards or
+// remote nodes). L1 hits cost a hash probe on the reactor thread (~us); L1
+// misses go to L2 and promote on hit; writes go to both levels.
+class TieredBackend : public CacheBackend {
+ public:
+  TieredBackend(std::shared_ptr<CacheBackend> l1, std::shared_ptr<CacheBackend> l2,
+                uint32_t promote_ttl_s = 60);
+  void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
+  void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+           uint32_t ttl_s) override;
+  void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
+  void flush() override;
+  std::string name() const override { return l1_->name() + "+" + l2_->name(); }
+  void stats(StatList* out) override;
+
+ private:
+  std::shared_ptr<CacheBackend> l1_, l2_;
+  uint32_t promote_ttl_;
+  std::atomic<uint64_t> l1_hits_{0}, l2_hits_{0}, misses_{0};
 };
 
 struct MemcachedConfig {

@@ -171,6 +171,9 @@ void bind_net(py::module_& m) {
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
      py::arg("max_item") = 1u << 20, py::arg("batch_us") = 50, py::arg("max_batch") = 65536);
+  m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl) {
+    return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl)};
+  }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60);
   m.def("memcached_backend", [](const std::string& servers, int retry_s, int op_timeout_ms) {
     MemcachedConfig c;
     c.servers = resolve_list(servers, 11211);

@@ -222,7 +222,7 @@ uint64_t HostCache::head() {
 }
 
 bool HostCache::get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* flags,
-                        uint32_t now) {
+                        uint32_t now, uint32_t* expire) {
   std::lock_guard<std::mutex> lk(mu_);
   uint32_t vl = 0;
   const uint64_t l = probe_locked(key, now, &vl);
@@ -234,6 +234,7 @@ bool HostCache::get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* 
   ItemHeader h;
   std::memcpy(&h, p, sizeof h);
   if (flags) *flags = h.flags;
+  if (expire) *expire = h.expire;
   out->assign(p + kItemHeaderBytes, p + kItemHeaderBytes + vl);
   return true;
 }

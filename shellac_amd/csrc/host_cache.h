@@ -34,7 +34,8 @@ class HostCache {
 
   // Single-key conveniences used by the proxy / memcached server. get() copies
   // the value (not the header) into `out` and returns false on miss.
-  bool get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* flags, uint32_t now);
+  bool get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* flags, uint32_t now,
+               uint32_t* expire = nullptr);
   void set_one(const Digest& key, const uint8_t* value, uint32_t vlen, uint32_t flags,
                uint32_t expire, uint32_t now);
 

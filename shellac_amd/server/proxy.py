@@ -49,16 +49,22 @@ def parse_server_list(slist: str, default_port: int) -> list:
 def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
                  hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 50,
-                 retry_s: int = 2):
+                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
     ``dram`` (local host memory), ``hbm`` (one HBM shard per GPU in ``gpus``) or
-    ``none``.
+    ``none``. ``l1_mb > 0`` puts a host-DRAM L1 of that size in front of the
+    ``hbm`` / ``memcached`` tier (``TieredBackend``: L1 hits never wait for a GPU
+    batch or a network round trip).
     """
     c = core()
     if kind == "none":
         return None
+    if l1_mb and kind in ("hbm", "memcached"):
+        l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
+                          batch_us=batch_us, retry_s=retry_s)
+        return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
             raise ValueError("memcached backend needs cache servers (-c host:port,...)")
@@ -151,6 +157,8 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--hbm-gb", type=float, default=16.0, help="HBM value-log GiB per GPU")
     p.add_argument("--dram-mb", type=int, default=1024, help="host cache MiB for --cache dram")
     p.add_argument("--batch-us", type=int, default=50, help="HBM batching window (us)")
+    p.add_argument("--l1-mb", type=int, default=256,
+                   help="host-DRAM L1 in front of --cache hbm/memcached (0 = off)")
     p.add_argument("--threads", type=int, default=1, help="reactor threads (SO_REUSEPORT)")
     p.add_argument("--bind", default="0.0.0.0")
     p.add_argument("--policy", choices=["rfc", "reference"], default="rfc",
@@ -184,7 +192,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}
-                    if kind == "hbm" else {}))
+                    if kind == "hbm" else {}),
+                 **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))
     print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)
     stop = threading.Event()
 

@@ -65,3 +65,21 @@ def test_proxy_with_hbm_backend(hbm):
             assert st["cache_hits"] >= 50 and st["backend"] == "hbm"
     finally:
         o.stop()
+
+
+def test_proxy_with_tiered_dram_hbm():
+    be = make_backend("hbm", gpus=[0], hbm_gb=1.0, batch_us=20, l1_mb=16)
+    o = Origin(body_bytes=1000).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend=be) as px:
+            c = HttpClient(port=px.port)
+            for i in range(20):
+                c.get(f"/tier/{i}")
+            time.sleep(0.2)
+            for i in range(20):
+                c.get(f"/tier/{i}")
+            st = px.stats()["cache"]
+            assert st["tier_l1_hits"] == 20 and st["l2_hbm_gpus"] == 1
+            assert all(o.hits[f"/tier/{i}"] == 1 for i in range(20))
+    finally:
+        o.stop()

@@ -274,3 +274,28 @@ def test_memcached_client_against_fake_and_node_failure(origin):
                 assert c.get(p).status() == 200
     finally:
         f2.stop()
+
+
+def test_tiered_l1_dram_over_memcached(origin):
+    f = FakeMemcached().start()
+    try:
+        with make_proxy([origin.port], backend_kind="memcached",
+                        caches=[("127.0.0.1", f.port)], l1_mb=16) as px:
+            c = HttpClient(port=px.port)
+            c.get("/t1")
+            time.sleep(0.2)
+            assert len(f.data) == 1           # written through to L2
+            c.get("/t1")
+            st = px.stats()["cache"]
+            assert st["tier_l1_hits"] == 1 and st["tier_l2_hits"] == 0
+            # a second proxy with a cold L1 finds it in L2 and promotes it
+        with make_proxy([origin.port], backend_kind="memcached",
+                        caches=[("127.0.0.1", f.port)], l1_mb=16) as px2:
+            c = HttpClient(port=px2.port)
+            c.get("/t1")
+            c.get("/t1")
+            st = px2.stats()["cache"]
+            assert st["tier_l2_hits"] == 1 and st["tier_l1_hits"] == 1
+            assert origin.hits["/t1"] == 1
+    finally:
+        f.stop()
