@@ -61,7 +61,7 @@ class HbmCache {
   const ShardConfig& config() const { return cfg_; }
   uint8_t* log_ptr() const { return log_; }
   Entry* index_ptr() const { return index_; }
-  uint64_t* head_ptr() const { return head_; }
+  uint64_t* head_ptr() const { return head_ + hsel_; }
   // Pre-size the SET workspace for batches of n keys (allocates; call outside capture).
   void reserve(int64_t n);
   uint64_t hbm_bytes() const;
@@ -73,7 +73,10 @@ class HbmCache {
   ShardConfig cfg_;
   uint8_t* log_ = nullptr;
   Entry* index_ = nullptr;
-  uint64_t* head_ = nullptr;         // device: logical write head
+  uint64_t* head_ = nullptr;         // device: logical write head, 2 ping-pong slots
+  int hsel_ = 0;                     // slot holding the current head
+  uint64_t* cur_head() const { return head_ + hsel_; }
+  uint64_t* next_head() const { return head_ + (hsel_ ^ 1); }
   CacheCounters* ctr_ = nullptr;     // device counters (64 shards)
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads

@@ -18,7 +18,8 @@
 //   k_set_index    16 lanes per key: two-choice insert with a 64-bit CAS on the
 //                  entry's loc word; replaces the key's own entry, else a dead
 //                  slot in the emptier bucket, else evicts the oldest item;
-//                  k_advance_head then publishes the new log head.
+//                  workgroup 0 publishes the new log head into the other of two
+//                  ping-pong head slots, and every item resets its dedupe slot.
 //   All per-op counters are block-reduced and added to one of 64 counter
 //   shards (one atomic per block per field; same-address fan-in measured at
 //   ~12 ns/atomic would otherwise serialise a 64K-wave probe into milliseconds).
@@ -130,6 +131,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   const uint64_t head = *head_ptr;
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
   unsigned long long hits = 0, bytes = 0, ops = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;  // scan reads n+1 sizes
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
     const Digest d = keys[i];
     const uint64_t b = (l16 < 8) ? bucket1(d, mask) : bucket2(d, mask);
@@ -365,14 +367,23 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
-    const uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now,
-    CacheCounters* __restrict__ ctr) {
+    const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
+    uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
+    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr) {
   const int l16 = threadIdx.x & 15;
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
   unsigned long long evicted = 0, bytes = 0;
+  // publish the new head into the other ping-pong slot: every workgroup of this
+  // launch (and of k_segcopy<1> before it) reads the current slot
+  if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
+    if (l16 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
+      const uint32_t sl = slot_of[i];
+      dd_keys[sl] = 0ull;
+      dd_win[sl] = -1;
+    }
     if (size[i] == 0) continue;  // uniform across the 16-lane group
     const Digest d = keys[i];
     const uint64_t myloc = base + off[i] + 1;
@@ -445,12 +456,6 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
   block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes);
 }
 
-// Publishes the new log head after k_set_index (a separate launch: stream order
-// guarantees every workgroup of k_set_index read the old head first).
-__global__ void k_advance_head(uint64_t* __restrict__ head_ptr, const uint64_t* __restrict__ off,
-                               int64_t n) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *head_ptr += off[n];
-}
 
 // ---------------------------------------------------------------------------------
 // DELETE / SWEEP
@@ -768,6 +773,9 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   const uint64_t tslots = (uint64_t)cap * 2;
   HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
+  // the table is cleared once here; k_set_index resets every slot a batch used
+  HIP_OK(hipMemset(dd_keys_, 0, tslots * sizeof(uint64_t)));
+  HIP_OK(hipMemset(dd_win_, 0xff, tslots * sizeof(int)));
   HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
@@ -791,9 +799,8 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
     return;
   }
   ensure_scan_ws(n);
-  HIP_OK(hipMemsetAsync(size + n, 0, sizeof(uint64_t), s));
   hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, loc, size, ctr_);
+                     index_, cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, loc, size, ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
 }
@@ -814,9 +821,6 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, s);
   ensure_scan_ws(n);
-  const uint64_t tslots = (uint64_t)dd_mask_ + 1;
-  HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
-  HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
   const int grid = grid_for(n, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
@@ -825,12 +829,13 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   HIP_OK(hipGetLastError());
   device_exclusive_scan(set_size_, set_off_, n, scan_tmp_, scan_tmp_bytes_, s);
   hipLaunchKernelGGL(k_segcopy<1>, dim3(2048), dim3(kBlock), 0, s, values, val_off, set_off_, n,
-                     log_, keys, vlen, flags, expire, head_, cfg_.log_bytes);
+                     log_, keys, vlen, flags, expire, cur_head(), cfg_.log_bytes);
   HIP_OK(hipGetLastError());
   const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
-                     vlen, expire, index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, ctr_);
-  hipLaunchKernelGGL(k_advance_head, dim3(1), dim3(64), 0, s, head_, set_off_, n);
+                     vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
+                     cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_);
+  hsel_ ^= 1;  // later operations on the stream read the published slot
   HIP_OK(hipGetLastError());
 }
 
@@ -839,7 +844,7 @@ void HbmCache::remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t no
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   hipLaunchKernelGGL(k_delete, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     index_, cfg_.nbuckets - 1, head_, cfg_.log_bytes, now, found, ctr_);
+                     index_, cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, found, ctr_);
   HIP_OK(hipGetLastError());
 }
 
@@ -850,7 +855,7 @@ void HbmCache::sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64
   HIP_OK(hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s));
   const uint64_t nslots = cfg_.nbuckets * kEntriesPerBucket;
   hipLaunchKernelGGL(k_sweep, dim3(grid_for((int64_t)nslots, kBlock, 4096)), dim3(kBlock), 0, s,
-                     index_, nslots, head_, cfg_.log_bytes, now, out, ctr_);
+                     index_, nslots, cur_head(), cfg_.log_bytes, now, out, ctr_);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(host_buf_, out, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
@@ -882,7 +887,7 @@ CacheCounters HbmCache::counters(hipStream_t s) {
 uint64_t HbmCache::head(hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
-  HIP_OK(hipMemcpyAsync(host_buf_, head_, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(host_buf_, cur_head(), sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return host_buf_[0];
 }
