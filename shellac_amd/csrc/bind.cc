@@ -99,6 +99,23 @@ PYBIND11_MODULE(_shellac_core, m) {
         return py::make_tuple(live, bytes);
       })
       .def("flush", [](HbmCache& c, uintptr_t s) { c.flush(S(s)); })
+      .def("export_keys", [](HbmCache& c, uintptr_t out, uint64_t cap, uint32_t now, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        return c.export_keys(P<Digest>(out), cap, now, S(s));
+      })
+      .def("save", [](HbmCache& c, const std::string& path, std::vector<uint64_t> user, uintptr_t s) {
+        user.resize(4);
+        py::gil_scoped_release nogil;
+        c.save(path, user.data(), S(s));
+      })
+      .def("load", [](HbmCache& c, const std::string& path, uintptr_t s) {
+        std::vector<uint64_t> user(4);
+        {
+          py::gil_scoped_release nogil;
+          c.load(path, user.data(), S(s));
+        }
+        return user;
+      })
       .def("counters", [](HbmCache& c, uintptr_t s) { return counters_dict(c.counters(S(s))); })
       .def("head", [](HbmCache& c, uintptr_t s) { return c.head(S(s)); })
       .def("reserve", &HbmCache::reserve)
@@ -177,6 +194,18 @@ PYBIND11_MODULE(_shellac_core, m) {
         return py::make_tuple(live, bytes);
       })
       .def("flush", &HostCache::flush)
+      .def("export_keys", [](HostCache& c, uintptr_t out, uint64_t cap, uint32_t now) {
+        return c.export_keys(P<Digest>(out), cap, now);
+      })
+      .def("save", [](HostCache& c, const std::string& path, std::vector<uint64_t> user) {
+        user.resize(4);
+        c.save(path, user.data());
+      })
+      .def("load", [](HostCache& c, const std::string& path) {
+        std::vector<uint64_t> user(4);
+        c.load(path, user.data());
+        return user;
+      })
       .def("counters", [](HostCache& c) { return counters_dict(c.counters()); })
       .def("head", &HostCache::head)
       .def("get", [](HostCache& c, py::bytes key, uint32_t now) -> py::object {

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <mutex>
+#include <string>
 
 #include "layout.h"
 
@@ -53,6 +54,13 @@ class HbmCache {
   // Reclaim index slots whose items expired or were overwritten. Synchronises;
   // returns {live entries, live item bytes}.
   void sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64_t* live_bytes);
+  // Digests of every live entry -> out (device, up to out_cap); returns the live
+  // count (may exceed out_cap). Synchronises. Used for rebalancing / migration.
+  uint64_t export_keys(Digest* out, uint64_t out_cap, uint32_t now, hipStream_t s);
+  // Snapshot / warm restore of the whole shard (index + log + head) to a file;
+  // `user` carries 4 caller words (e.g. the epoch). load() needs equal geometry.
+  void save(const std::string& path, const uint64_t user[4], hipStream_t s);
+  void load(const std::string& path, uint64_t user[4], hipStream_t s);
   // Drop everything (memcached FLUSH).
   void flush(hipStream_t s);
   CacheCounters counters(hipStream_t s);

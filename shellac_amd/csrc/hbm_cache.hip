@@ -527,6 +527,46 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Entry* __restrict__ index, uin
   }
 }
 
+
+// Export the digests of all live entries (rebalancing / warm restore). One atomic
+// per workgroup per pass reserves the output range; lanes write in block order.
+__global__ __launch_bounds__(kBlock) void k_export(const Entry* __restrict__ index, uint64_t nslots,
+                                                   const uint64_t* __restrict__ head_ptr,
+                                                   uint64_t cap, uint32_t now,
+                                                   Digest* __restrict__ out, uint64_t out_cap,
+                                                   unsigned long long* __restrict__ counter) {
+  __shared__ unsigned int s_wcnt[kBlock / 64];
+  __shared__ unsigned long long s_base;
+  const uint64_t head = *head_ptr;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t k0 = (uint64_t)blockIdx.x * kBlock; k0 < nslots; k0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t k = k0 + threadIdx.x;
+    bool live = false;
+    Digest d{0, 0};
+    if (k < nslots) {
+      const Entry e = index[k];
+      live = entry_live(e.loc, e.expire, head, cap, now);
+      d = Digest{e.d0, e.d1};
+    }
+    const unsigned long long m = __ballot(live);
+    if (lane == 0) s_wcnt[w] = (unsigned int)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int tot = 0;
+      for (int i = 0; i < kBlock / 64; ++i) tot += s_wcnt[i];
+      s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    unsigned int before = 0;
+    for (int i = 0; i < w; ++i) before += s_wcnt[i];
+    if (live) {
+      const uint64_t pos = s_base + before + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (pos < out_cap) out[pos] = d;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Digest / routing / permutation
 // ---------------------------------------------------------------------------------
@@ -861,6 +901,97 @@ void HbmCache::sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64
   HIP_OK(hipStreamSynchronize(s));
   if (live_entries) *live_entries = host_buf_[0];
   if (live_bytes) *live_bytes = host_buf_[1];
+}
+
+uint64_t HbmCache::export_keys(Digest* out, uint64_t out_cap, uint32_t now, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  HIP_OK(hipMemsetAsync(scratch_, 0, sizeof(unsigned long long), s));
+  const uint64_t nslots = cfg_.nbuckets * kEntriesPerBucket;
+  hipLaunchKernelGGL(k_export, dim3(grid_for((int64_t)nslots, kBlock, 4096)), dim3(kBlock), 0, s,
+                     index_, nslots, cur_head(), cfg_.log_bytes, now, out, out_cap, scratch_);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(host_buf_, scratch_, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return host_buf_[0];
+}
+
+namespace {
+struct SnapHeader {
+  char magic[8];
+  uint64_t version, log_bytes, nbuckets, max_item, head, index_bytes, log_saved, user[4];
+};
+constexpr char kSnapMagic[8] = {'S', 'H', 'L', 'C', 'S', 'N', 'P', '1'};
+}  // namespace
+
+void HbmCache::save(const std::string& path, const uint64_t user[4], hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  HIP_OK(hipStreamSynchronize(s));
+  uint64_t head = 0;
+  HIP_OK(hipMemcpy(&head, cur_head(), 8, hipMemcpyDeviceToHost));
+  const uint64_t slack = item_bytes(cfg_.max_item) + 64;
+  SnapHeader h{};
+  std::memcpy(h.magic, kSnapMagic, 8);
+  h.version = 1;
+  h.log_bytes = cfg_.log_bytes;
+  h.nbuckets = cfg_.nbuckets;
+  h.max_item = cfg_.max_item;
+  h.head = head;
+  h.index_bytes = cfg_.nbuckets * kBucketBytes;
+  h.log_saved = head >= cfg_.log_bytes ? cfg_.log_bytes + slack : std::min(head + slack, cfg_.log_bytes + slack);
+  for (int i = 0; i < 4; ++i) h.user[i] = user ? user[i] : 0;
+  FILE* f = std::fopen(path.c_str(), "wb");
+  SH_CHECK(f, "cannot open snapshot for writing: " + path);
+  const size_t chunk = 64u << 20;
+  uint8_t* pin = nullptr;
+  HIP_OK(hipHostMalloc(&pin, chunk, hipHostMallocDefault));
+  bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
+  auto dump = [&](const uint8_t* dev, uint64_t bytes) {
+    for (uint64_t o = 0; ok && o < bytes; o += chunk) {
+      const size_t n = (size_t)std::min<uint64_t>(chunk, bytes - o);
+      HIP_OK(hipMemcpy(pin, dev + o, n, hipMemcpyDeviceToHost));
+      ok = std::fwrite(pin, 1, n, f) == n;
+    }
+  };
+  dump(reinterpret_cast<const uint8_t*>(index_), h.index_bytes);
+  dump(log_, h.log_saved);
+  (void)hipHostFree(pin);
+  ok = (std::fclose(f) == 0) && ok;
+  SH_CHECK(ok, "snapshot write failed: " + path);
+}
+
+void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  FILE* f = std::fopen(path.c_str(), "rb");
+  SH_CHECK(f, "cannot open snapshot: " + path);
+  SnapHeader h{};
+  bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kSnapMagic, 8) == 0;
+  if (!ok || h.log_bytes != cfg_.log_bytes || h.nbuckets != cfg_.nbuckets ||
+      h.max_item != cfg_.max_item) {
+    std::fclose(f);
+    throw Error("snapshot " + path + " does not match this shard's geometry");
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  const size_t chunk = 64u << 20;
+  uint8_t* pin = nullptr;
+  HIP_OK(hipHostMalloc(&pin, chunk, hipHostMallocDefault));
+  auto fill = [&](uint8_t* dev, uint64_t bytes) {
+    for (uint64_t o = 0; ok && o < bytes; o += chunk) {
+      const size_t n = (size_t)std::min<uint64_t>(chunk, bytes - o);
+      ok = std::fread(pin, 1, n, f) == n;
+      if (ok) HIP_OK(hipMemcpy(dev + o, pin, n, hipMemcpyHostToDevice));
+    }
+  };
+  fill(reinterpret_cast<uint8_t*>(index_), h.index_bytes);
+  fill(log_, h.log_saved);
+  (void)hipHostFree(pin);
+  std::fclose(f);
+  SH_CHECK(ok, "snapshot truncated: " + path);
+  HIP_OK(hipMemcpy(cur_head(), &h.head, 8, hipMemcpyHostToDevice));
+  if (user)
+    for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
 
 void HbmCache::flush(hipStream_t s) {

@@ -4,6 +4,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 
@@ -204,6 +205,68 @@ void HostCache::sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes
   }
   if (live_entries) *live_entries = live;
   if (live_bytes) *live_bytes = bytes;
+}
+
+uint64_t HostCache::export_keys(Digest* out, uint64_t out_cap, uint32_t now) {
+  std::lock_guard<std::mutex> lk(mu_);
+  uint64_t m = 0;
+  const uint64_t nslots = nbuckets_ * kEntriesPerBucket;
+  for (uint64_t k = 0; k < nslots; ++k) {
+    const Entry& e = index_[k];
+    if (!entry_live(e.loc, e.expire, head_, log_bytes_, now)) continue;
+    if (m < out_cap) out[m] = Digest{e.d0, e.d1};
+    ++m;
+  }
+  return m;
+}
+
+namespace {
+struct SnapHeader {
+  char magic[8];
+  uint64_t version, log_bytes, nbuckets, max_item, head, index_bytes, log_saved, user[4];
+};
+constexpr char kSnapMagic[8] = {'S', 'H', 'L', 'C', 'S', 'N', 'P', '1'};
+}  // namespace
+
+void HostCache::save(const std::string& path, const uint64_t user[4]) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const uint64_t slack = item_bytes(max_item_) + 64;
+  SnapHeader h{};
+  std::memcpy(h.magic, kSnapMagic, 8);
+  h.version = 1;
+  h.log_bytes = log_bytes_;
+  h.nbuckets = nbuckets_;
+  h.max_item = max_item_;
+  h.head = head_;
+  h.index_bytes = nbuckets_ * kBucketBytes;
+  h.log_saved = head_ >= log_bytes_ ? log_bytes_ + slack : std::min(head_ + slack, log_bytes_ + slack);
+  for (int i = 0; i < 4; ++i) h.user[i] = user ? user[i] : 0;
+  FILE* f = std::fopen(path.c_str(), "wb");
+  SH_CHECK(f, "cannot open snapshot for writing: " + path);
+  bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
+            std::fwrite(index_, 1, h.index_bytes, f) == h.index_bytes &&
+            std::fwrite(log_, 1, h.log_saved, f) == h.log_saved;
+  ok = (std::fclose(f) == 0) && ok;
+  SH_CHECK(ok, "snapshot write failed: " + path);
+}
+
+void HostCache::load(const std::string& path, uint64_t user[4]) {
+  std::lock_guard<std::mutex> lk(mu_);
+  FILE* f = std::fopen(path.c_str(), "rb");
+  SH_CHECK(f, "cannot open snapshot: " + path);
+  SnapHeader h{};
+  bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kSnapMagic, 8) == 0;
+  if (!ok || h.log_bytes != log_bytes_ || h.nbuckets != nbuckets_ || h.max_item != max_item_) {
+    std::fclose(f);
+    throw Error("snapshot " + path + " does not match this shard's geometry");
+  }
+  ok = std::fread(index_, 1, h.index_bytes, f) == h.index_bytes &&
+       std::fread(log_, 1, h.log_saved, f) == h.log_saved;
+  std::fclose(f);
+  SH_CHECK(ok, "snapshot truncated: " + path);
+  head_ = h.head;
+  if (user)
+    for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
 
 void HostCache::flush() {

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "layout.h"
@@ -29,6 +30,9 @@ class HostCache {
   void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now);
   void sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes);
   void flush();
+  uint64_t export_keys(Digest* out, uint64_t out_cap, uint32_t now);
+  void save(const std::string& path, const uint64_t user[4]);
+  void load(const std::string& path, uint64_t user[4]);
   CacheCounters counters();
   uint64_t head();
 

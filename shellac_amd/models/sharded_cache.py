@@ -330,5 +330,67 @@ class ShardedCache:
         self.stats["replica_refreshes"] += 1
         return int((sb.vlen != SKIP_VLEN).sum())
 
+    # ------------------------------------------------------------------------------
+    # membership changes: rebalancing, failure, warm recovery, snapshots
+    # ------------------------------------------------------------------------------
+    def set_ring(self, ring: ShardRing, migrate: bool = True, now: Optional[int] = None) -> int:
+        """Collective. Switch every rank to ``ring``. With ``migrate`` each rank ships
+        the live objects it holds that the new ring assigns elsewhere to their new
+        owners through the routed SET path (warm rebalancing: no refetch from the
+        origin). Returns the number of objects this rank migrated."""
+        moved = 0
+        batch = None
+        mkeys = None
+        if migrate and self.world > 1:
+            keys = self.shard.export_keys(now)
+            pts, own = ring.tensors(self.device)
+            dest, _ = R.route(keys, pts, own, self.world)
+            sel = dest != self.rank
+            mkeys = keys[sel].contiguous()
+            moved = int(mkeys.shape[0])
+            lk = self.shard.lookup(mkeys, now)
+            data = self.shard.gather(lk)
+            batch = records_to_set_batch(mkeys, GetResult(data, lk.off[:moved], lk.size[:moved]))
+        self.ring = ring
+        self.ring_pts, self.ring_own = ring.tensors(self.device)
+        if batch is not None:
+            self.set(batch, now)                  # lands on the new owners
+            if moved:
+                self.shard.remove(mkeys, now)     # this rank no longer owns them
+        return moved
+
+    def fail_shard(self, rank: int) -> None:
+        """Collective. Simulate (or react to) the loss of ``rank``'s shard: every rank
+        drops it from the ring (its keys remap, like ketama auto-eject) and the lost
+        shard's contents are discarded."""
+        if rank not in self.ring.shards:
+            return
+        self.set_ring(self.ring.without(rank), migrate=False)
+        if self.rank == rank:
+            self.shard.flush()
+        if self.replica is not None:
+            self.replica.flush()
+            self._hot = None
+
+    def restore_shard(self, rank: int, now: Optional[int] = None) -> int:
+        """Collective. Re-admit ``rank``; objects written while it was out migrate
+        back to it from their interim owners (warm restore from peer shards)."""
+        shards = sorted(set(self.ring.shards) | {rank})
+        return self.set_ring(ShardRing(shards, self.ring.points_per_shard), migrate=True, now=now)
+
+    def save(self, directory: str) -> str:
+        """Snapshot this rank's shard to ``directory/shard-<rank>.snap``."""
+        import os
+
+        os.makedirs(directory, exist_ok=True)
+        path = os.path.join(directory, f"shard-{self.rank}.snap")
+        self.shard.save(path)
+        return path
+
+    def load(self, directory: str) -> None:
+        import os
+
+        self.shard.load(os.path.join(directory, f"shard-{self.rank}.snap"))
+
     def counters(self) -> dict:
         return allreduce_stats(self.shard.counters(), self.device, self.group)

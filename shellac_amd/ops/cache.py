@@ -263,6 +263,38 @@ class CacheShard:
         else:
             self._impl.flush()
 
+    def export_keys(self, now: Optional[int] = None) -> torch.Tensor:
+        """Digests of every live object in this shard, int64 [m, 2] on the shard's device."""
+        now = self.now() if now is None else now
+        cap = 1 << 16
+        while True:
+            out = torch.empty((cap, 2), dtype=torch.int64, device=self.device)
+            if self.is_gpu:
+                m = self._impl.export_keys(out.data_ptr(), cap, now, self._s())
+            else:
+                m = self._impl.export_keys(out.data_ptr(), cap, now)
+            if m <= cap:
+                return out[:m]
+            cap = int(m * 1.25) + 1024
+
+    def save(self, path: str) -> None:
+        """Snapshot index + log + head to ``path`` (warm restart)."""
+        import struct
+
+        user = [struct.unpack("<Q", struct.pack("<d", self.epoch))[0], 0, 0, 0]
+        if self.is_gpu:
+            self._impl.save(path, user, self._s())
+        else:
+            self._impl.save(path, user)
+
+    def load(self, path: str) -> None:
+        """Restore a snapshot written by ``save`` (same geometry); expiry times
+        stay relative to the saved epoch."""
+        import struct
+
+        user = self._impl.load(path, self._s()) if self.is_gpu else self._impl.load(path)
+        self.epoch = struct.unpack("<d", struct.pack("<Q", int(user[0])))[0]
+
     def counters(self) -> dict:
         return self._impl.counters(self._s()) if self.is_gpu else self._impl.counters()
 

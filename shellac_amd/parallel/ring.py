@@ -60,9 +60,14 @@ class ShardRing:
         return self.owner_of_digest(lo, hi)
 
     def tensors(self, device) -> tuple[torch.Tensor, torch.Tensor]:
-        """(points int32-bit-pattern as int32 tensor, owners int32) for ``ops.routing.route``."""
+        """(points as an int32 bit pattern, owner ids int32) for ``ops.routing.route``.
+        Owner ids are the shard ids when shards are ints (ranks), else ring indices."""
         pts = torch.from_numpy(self.pts.view(np.int32).copy()).to(device)
-        own = torch.from_numpy(self.owner.copy()).to(device)
+        if all(isinstance(x, (int, np.integer)) for x in self.shards):
+            ids = np.asarray(self.shards, dtype=np.int32)[self.owner]
+        else:
+            ids = self.owner
+        own = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int32)).to(device)
         return pts, own
 
     def without(self, shard) -> "ShardRing":

@@ -152,3 +152,77 @@ def test_hot_object_replication_gloo(world):
         p.join(timeout=60)
     fails = [r for r in results if r[1] != "ok"]
     assert not fails, fails[0][2]
+
+
+def _membership_worker(rank, world, port, q, snapdir):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+
+        def mk():
+            return CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu")
+
+        sc = ShardedCache(mk())
+        def put(keys, tag):
+            mine = keys if rank == 0 else []
+            v, vo, vl = pack_values([tag + k for k in mine])
+            sc.set(SetBatch(digest_strings(mine), v, vo, vl))
+            dist.barrier()
+
+        def read(keys):
+            res = sc.get(digest_strings(keys))
+            return [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+
+        keys = [f"/m{i}".encode() for i in range(300)]
+        put(keys, b"a-")
+        owner = {k: sc.ring.owner_of_key(k) for k in keys}
+        # shard 1 fails: its keys miss, everything else still hits
+        sc.fail_shard(1)
+        got = read(keys)
+        for k, g in zip(keys, got):
+            assert (g is None) == (owner[k] == 1), (k, g)
+        # writes during the outage land on the interim owners
+        late = [f"/late{i}".encode() for i in range(100)]
+        put(late, b"b-")
+        assert read(late) == [b"b-" + k for k in late]
+        # warm restore: shard 1 rejoins and pulls back its keys from peers
+        sc.restore_shard(1)
+        assert read(late) == [b"b-" + k for k in late]
+        full = sc.ring
+        late_owned = sum(full.owner_of_key(k) == 1 for k in late)
+        assert late_owned > 0
+        if rank == 1:
+            assert sc.shard.sweep()[0] >= late_owned
+        # snapshot + warm restart of every shard
+        sc.save(snapdir)
+        dist.barrier()
+        sc2 = ShardedCache(mk())
+        sc2.load(snapdir)
+        sc = sc2
+        assert read(late) == [b"b-" + k for k in late]
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_shard_failure_rebalance_and_snapshot_gloo(tmp_path):
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_membership_worker, args=(r, world, port, q, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    fails = [r for r in results if r[1] != "ok"]
+    assert not fails, fails[0][2]

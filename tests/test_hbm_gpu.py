@@ -182,3 +182,23 @@ def test_sharded_cache_single_rank_gpu(cuda_dev):
     recs = unpack_records(res.data, res.off, res.size)
     for i, r in zip(ids.tolist()[:500], recs[:500]):
         assert r is not None and r[0] == wl.expected_value(i)
+
+
+def test_export_keys_and_snapshot_roundtrip(cuda_dev, tmp_path):
+    g, h = _pair(log=1 << 22, nb=1 << 12, dev=cuda_dev)
+    keys = [f"/snap/{i}".encode() for i in range(3000)]
+    vals = [bytes([i % 251]) * (i % 700) for i in range(3000)]
+    d, v, vo, vl = _batch(keys, vals, cuda_dev)
+    g.store(d.to(cuda_dev), v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev), now=3)
+    h.store(d, v, vo, vl, now=3)
+    g.remove(d[:100].to(cuda_dev), now=3)
+    h.remove(d[:100], now=3)
+    eg = {tuple(r) for r in g.export_keys(now=3).cpu().tolist()}
+    eh = {tuple(r) for r in h.export_keys(now=3).tolist()}
+    assert eg == eh and len(eg) == 2900
+    path = str(tmp_path / "gpu.snap")
+    g.save(path)
+    g2 = CacheShard(1 << 22, 1 << 12, 1 << 16, cuda_dev)
+    g2.load(path)
+    rg, _, _, _ = _get_both(g2, h, keys, 3)
+    assert [r[0] if r else None for r in rg] == [None] * 100 + vals[100:]
