@@ -73,12 +73,10 @@ PYBIND11_MODULE(_shellac_core, m) {
                  now, S(s));
       })
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
-                        uintptr_t s, uint64_t max_item_bytes) {
+                        uintptr_t s) {
         py::gil_scoped_release nogil;
-        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s),
-                 max_item_bytes);
-      }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
-         py::arg("max_item_bytes") = 0)
+        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s));
+      })
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s) {

@@ -42,10 +42,7 @@ class HbmCache {
   void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
               uint32_t now, hipStream_t s);
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i].
-  // lookup() leaves the batch's largest item size in size[n]; passing it as
-  // max_item_bytes selects the item-centric kernel when every item is small.
-  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s,
-              uint64_t max_item_bytes = 0);
+  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).

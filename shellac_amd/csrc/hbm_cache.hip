@@ -50,7 +50,6 @@ constexpr int kTileChunks = 4096;          // 16-B chunks per segcopy tile (64 K
 constexpr int kChunksPerThread = kTileChunks / kBlock;
 constexpr int kTileSegCap = 2048;          // segments staged in LDS per tile
 constexpr int kMaxGrid = 2048;
-constexpr uint64_t kItemGatherMax = 16384;  // item-centric gather up to this item size
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));             // 8 x 256-thread blocks per CU x 256 CUs
 
 struct DeviceGuard {
@@ -127,10 +126,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
                                                   uint64_t cap, uint32_t now,
                                                   uint64_t* __restrict__ out_loc,
                                                   uint64_t* __restrict__ out_size,
-                                                  CacheCounters* __restrict__ ctr,
-                                                  unsigned long long* __restrict__ max_size) {
+                                                  CacheCounters* __restrict__ ctr) {
   const int l16 = threadIdx.x & 15;
-  unsigned long long mx = 0;
   const uint64_t head = *head_ptr;
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
   unsigned long long hits = 0, bytes = 0, ops = 0;
@@ -158,9 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
       ++ops;
       if (hl) {
         out_loc[i] = (hl - 1) % cap;
-        const uint64_t ib = item_bytes(hv);
-        out_size[i] = ib;
-        mx = ib > mx ? ib : mx;
+        out_size[i] = item_bytes(hv);
         ++hits;
         bytes += hv;
       } else {
@@ -171,43 +166,6 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   }
   block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
               &CacheCounters::get_bytes);
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long t = __shfl_xor(mx, o);
-    mx = t > mx ? t : mx;
-  }
-  if ((threadIdx.x & 63) == 0 && mx) atomicMax(max_size, mx);
-}
-
-// Item-centric gather for batches of small objects: a 16-lane group copies one
-// object (no segment search, no LDS), four 16-B chunks per lane in flight per
-// step; 16 groups per block, grid-stride over objects. Chosen by the host when
-// the batch's largest object fits kItemGatherMax (k_probe publishes the max).
-__global__ __launch_bounds__(kBlock) void k_gather_items(const uint8_t* __restrict__ src,
-                                                         const uint64_t* __restrict__ src_off,
-                                                         const uint64_t* __restrict__ dst_off,
-                                                         int64_t n, uint8_t* __restrict__ dst) {
-  const int l16 = threadIdx.x & 15;
-  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
-  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
-    const uint64_t d0 = dst_off[i];
-    const uint64_t sz = dst_off[i + 1] - d0;
-    if (!sz) continue;
-    const uint8_t* s = src + src_off[i];
-    uint8_t* d = dst + d0;
-    for (uint64_t c = (uint64_t)l16 * 16; c < sz; c += 4 * 256) {
-      u32x4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t o = c + (uint64_t)u * 256;
-        if (o < sz) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + o));
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t o = c + (uint64_t)u * 256;
-        if (o < sz) *reinterpret_cast<u32x4*>(d + o) = v[u];
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -802,7 +760,6 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&head_, 64));
   HIP_OK(hipMalloc(&ctr_, kCtrShards * sizeof(CacheCounters)));
   HIP_OK(hipMalloc(&scratch_, 64));
-  HIP_OK(hipMemset(scratch_, 0, 64));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
@@ -883,26 +840,14 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   }
   ensure_scan_ws(n);
   hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     index_, cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, loc, size, ctr_,
-                     scratch_ + 2);
+                     index_, cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, loc, size, ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
-  // size[n] is not read by the exclusive scan's outputs: hand the batch's largest
-  // item to the host there (read together with off[n]) and re-arm the max word.
-  HIP_OK(hipMemcpyAsync(size + n, scratch_ + 2, 8, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemsetAsync(scratch_ + 2, 0, 8, s));
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
-                      hipStream_t s, uint64_t max_item_bytes) {
+                      hipStream_t s) {
   DeviceGuard g(cfg_.device);
-  if (max_item_bytes && max_item_bytes <= kItemGatherMax) {
-    if (n <= 0) return;
-    hipLaunchKernelGGL(k_gather_items, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0,
-                       s, log_, loc, off, n, out);
-    HIP_OK(hipGetLastError());
-    return;
-  }
   segcopy(log_, loc, off, n, out, s);
 }
 

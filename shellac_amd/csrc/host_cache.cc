@@ -57,7 +57,7 @@ uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) 
 void HostCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size,
                        uint64_t* off, uint32_t now) {
   std::lock_guard<std::mutex> lk(mu_);
-  uint64_t acc = 0, mx = 0;
+  uint64_t acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     uint32_t vl = 0;
     const uint64_t l = probe_locked(keys[i], now, &vl);
@@ -73,10 +73,8 @@ void HostCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* s
     }
     off[i] = acc;
     acc += size[i];
-    mx = size[i] > mx ? size[i] : mx;
   }
   off[n] = acc;
-  size[n] = mx;  // largest item in the batch (as the HBM engine reports it)
 }
 
 void HostCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out) const {

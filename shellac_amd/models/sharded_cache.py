@@ -139,12 +139,12 @@ class ShardedCache:
         perm = R.scatter_positions(dest, counts)         # local hits sort to the tail
         send_keys = R.permute(keys, perm)
         recv_counts = exchange_counts(counts[:w].contiguous(), self.group)
-        local_ext = torch.stack([rl.off[n], rl.size[n]]) if rl is not None else \
-            torch.zeros(2, dtype=torch.int64, device=self.device)
-        host = torch.cat([counts, recv_counts, local_ext]).cpu()         # sync 1
+        local_total = rl.off[n:n + 1] if rl is not None else torch.zeros(1, dtype=torch.int64,
+                                                                           device=self.device)
+        host = torch.cat([counts, recv_counts, local_total]).cpu()       # sync 1
         send_rows, n_local = host[:w].tolist(), int(host[w])
         recv_rows = host[w + 1: 2 * w + 1].tolist()
-        local_bytes, local_max = int(host[2 * w + 1]), int(host[2 * w + 2])
+        local_bytes = int(host[2 * w + 1])
         n_remote = n - n_local
         req = all_to_all_rows(send_keys[:n_remote], send_rows, recv_rows, self.group)
 
@@ -154,16 +154,16 @@ class ShardedCache:
         rc = torch.tensor(recv_rows, dtype=torch.int64, device=self.device)
         reply_bytes = segment_sums(lk.off, rc)                   # bytes I send back per source
         got_bytes = exchange_counts(reply_bytes, self.group)     # bytes I receive per owner
-        nbytes = torch.cat([reply_bytes, got_bytes, lk.size[m:m + 1]]).cpu()  # sync 2
-        send_b, recv_b = nbytes[:w].tolist(), nbytes[w:2 * w].tolist()
+        nbytes = torch.cat([reply_bytes, got_bytes]).cpu()       # sync 2
+        send_b, recv_b = nbytes[:w].tolist(), nbytes[w:].tolist()
         reply = torch.empty(max(int(sum(send_b)), 16), dtype=torch.uint8, device=self.device)
-        self.shard.gather(lk, reply, max_item=int(nbytes[2 * w]))
+        self.shard.gather(lk, reply)
         sizes_back = all_to_all_rows(lk.size[:m], recv_rows, send_rows, self.group)
         # response buffer: [local replica hits | remote values]
         data = torch.empty(local_bytes + int(sum(recv_b)) + 16, dtype=torch.uint8,
                            device=self.device)
         if rl is not None and n_local:
-            self.replica.gather(rl, data, max_item=local_max)
+            self.replica.gather(rl, data)
         dist.all_to_all_single(data[local_bytes: local_bytes + int(sum(recv_b))],
                                reply[: int(sum(send_b))], output_split_sizes=recv_b,
                                input_split_sizes=send_b, group=self.group)
@@ -349,7 +349,7 @@ class ShardedCache:
             mkeys = keys[sel].contiguous()
             moved = int(mkeys.shape[0])
             lk = self.shard.lookup(mkeys, now)
-            data = self.shard.gather(lk)  # (one sync for the extent)
+            data = self.shard.gather(lk)
             batch = records_to_set_batch(mkeys, GetResult(data, lk.off[:moved], lk.size[:moved]))
         self.ring = ring
         self.ring_pts, self.ring_own = ring.tensors(self.device)

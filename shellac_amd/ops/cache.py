@@ -114,7 +114,7 @@ def unpack_records(out: torch.Tensor, off: torch.Tensor, size: torch.Tensor) -> 
 @dataclass
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
-    size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = largest
+    size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
     off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
 
     @property
@@ -187,26 +187,15 @@ class CacheShard:
                               now)
         return Lookup(loc, size, off)
 
-    def batch_extent(self, lk: Lookup) -> tuple:
-        """(total response bytes, largest item bytes) of a lookup — one host sync."""
-        t, m = torch.stack([lk.off[lk.n], lk.size[lk.n]]).tolist()
-        return int(t), int(m)
-
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
-               total: Optional[int] = None, max_item: Optional[int] = None) -> torch.Tensor:
-        """Copy hits into ``out`` (allocated from off[n] if not given: one sync).
-        ``max_item`` (from ``batch_extent``) lets small-object batches use the
-        item-centric gather kernel."""
-        if out is None or max_item is None:
-            t, m = self.batch_extent(lk)
-            total = t if total is None else total
-            max_item = m if max_item is None else max_item
+               total: Optional[int] = None) -> torch.Tensor:
+        """Copy hits into ``out`` (allocated from off[n] if not given: one sync)."""
         if out is None:
+            total = int(lk.off[lk.n].item()) if total is None else total
             out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
         self._check(out, "out")
         if self.is_gpu:
-            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s(),
-                              int(max_item))
+            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s())
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
