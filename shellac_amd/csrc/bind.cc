@@ -67,11 +67,12 @@ PYBIND11_MODULE(_shellac_core, m) {
            }),
            py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"))
       .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
-                        uintptr_t off, uint32_t now, uintptr_t s) {
+                        uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve) {
         py::gil_scoped_release nogil;
         c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
-                 now, S(s));
-      })
+                 now, S(s), reserve);
+      }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
+         py::arg("now"), py::arg("stream"), py::arg("reserve") = 0)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
                         uintptr_t s) {
         py::gil_scoped_release nogil;
@@ -167,11 +168,12 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def(py::init<uint64_t, uint64_t, uint32_t>(), py::arg("log_bytes"), py::arg("nbuckets"),
            py::arg("max_item"))
       .def("lookup", [](HostCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
-                        uintptr_t off, uint32_t now) {
+                        uintptr_t off, uint32_t now, uint64_t reserve) {
         py::gil_scoped_release nogil;
         c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
-                 now);
-      })
+                 now, reserve);
+      }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
+         py::arg("now"), py::arg("reserve") = 0)
       .def("gather", [](HostCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out) {
         py::gil_scoped_release nogil;
         c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out));

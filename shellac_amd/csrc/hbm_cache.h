@@ -39,8 +39,10 @@ class HbmCache {
   // the physical log offset of the item (kMissLoc on miss) and the bytes the
   // item occupies in a GET response (0 on miss); then an exclusive scan of the
   // sizes into off[0..n] (off[n] = total response bytes).
+  // `reserve` > 0 treats objects that the next `reserve` appended bytes will
+  // overwrite as misses, so SETs may be queued between this lookup and its gather.
   void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-              uint32_t now, hipStream_t s);
+              uint32_t now, hipStream_t s, uint64_t reserve = 0);
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i].
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,

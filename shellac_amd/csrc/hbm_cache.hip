@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -47,10 +48,31 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kTileChunks = 4096;          // 16-B chunks per segcopy tile (64 KiB)
-constexpr int kChunksPerThread = kTileChunks / kBlock;
-constexpr int kTileSegCap = 2048;          // segments staged in LDS per tile
+constexpr int kTileSegCap = 1024;          // segments staged in LDS per tile
 constexpr int kMaxGrid = 2048;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));             // 8 x 256-thread blocks per CU x 256 CUs
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Smallest segcopy tile in 16-B chunks (16 KiB); SHELLAC_SEGCOPY_MIN_TILE overrides it
+// for tuning sweeps (benchmarks/kernel_bench.py).
+// Variant (loads in flight per lane, target waves/SIMD); SHELLAC_SEGCOPY_VARIANT selects
+// one for tuning (launch_segcopy lists them); 1 = 4 loads / 8 waves is the default.
+int segcopy_variant() {
+  static const int v = [] {
+    const char* e = getenv("SHELLAC_SEGCOPY_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+int min_tile_chunks() {
+  static const int v = [] {
+    const char* e = getenv("SHELLAC_SEGCOPY_MIN_TILE");
+    int t = e ? atoi(e) : 1024;
+    t = (t + kBlock - 1) / kBlock * kBlock;
+    return t < kBlock ? kBlock : (t > kTileChunks ? kTileChunks : t);
+  }();
+  return v;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -123,12 +145,14 @@ __device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
 __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ keys, int64_t n,
                                                   const Entry* __restrict__ index, uint64_t mask,
                                                   const uint64_t* __restrict__ head_ptr,
-                                                  uint64_t cap, uint32_t now,
+                                                  uint64_t reserve, uint64_t cap, uint32_t now,
                                                   uint64_t* __restrict__ out_loc,
                                                   uint64_t* __restrict__ out_size,
                                                   CacheCounters* __restrict__ ctr) {
   const int l16 = threadIdx.x & 15;
-  const uint64_t head = *head_ptr;
+  // `reserve`: bytes about to be appended before this lookup's gather runs; objects
+  // that those appends will overwrite are already treated as evicted
+  const uint64_t head = *head_ptr + reserve;
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
   unsigned long long hits = 0, bytes = 0, ops = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;  // scan reads n+1 sizes
@@ -233,89 +257,135 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
 
 // Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w.
 // Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
-// src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w.
-// Each workgroup owns 64 KiB tiles of the destination; each lane resolves its 16
-// chunks' segments first, then issues 8 independent 16-B loads before their stores.
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_segcopy(
+// src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w, where
+// the batch is at most cap/2 so the modulo is one compare against the wrap point.
+// The grid is exactly the number of co-resident workgroups; workgroup b owns the
+// contiguous destination range [b*span, (b+1)*span), so every workgroup moves the same
+// bytes in one pass (no tail round). One cooperative search finds the segments holding
+// the range's first and last byte; their offsets are then staged in LDS kTileSegCap at
+// a time, and every lane walks its chunks (256 x 16 B apart) with a galloping search
+// over the staged offsets, issuing U independent 16-B loads before their stores.
+template <int MODE, int U, int WAVES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_segcopy(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint64_t* __restrict__ dst_off, int64_t n, uint8_t* __restrict__ dst,
     // MODE 1 extras
     const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
-    const uint64_t* __restrict__ head_ptr, uint64_t cap) {
+    const uint64_t* __restrict__ head_ptr, uint64_t cap, int min_tile) {
   __shared__ uint64_t s_off[kTileSegCap + 1];
   __shared__ uint64_t s_src[kTileSegCap];
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
   const uint64_t total = dst_off[n];
   const int64_t nchunks = (int64_t)(total >> 4);
-  const uint64_t base = MODE == 1 ? *head_ptr : 0;
-  for (int64_t tile = blockIdx.x; tile * kTileChunks < nchunks; tile += gridDim.x) {
-    const int64_t c0 = tile * kTileChunks;
-    const int64_t c1 = min(c0 + (int64_t)kTileChunks, nchunks);
-    block_find2(dst_off, n + 1, (uint64_t)c0 << 4, ((uint64_t)c1 << 4) - 1, s_lo, s_hi, s_cnt);
-    const int64_t j0 = s_lo[0], cnt = s_lo[1] - s_lo[0] + 1;
-    const bool staged = cnt <= kTileSegCap;
-    if (staged) {
-      for (int64_t k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
-      for (int64_t k = threadIdx.x; k < cnt; k += kBlock) {
-        const int64_t j = j0 + k;
-        s_src[k] = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
-      }
-    }
+  const uint64_t base = MODE == 1 ? *head_ptr % cap : 0;
+  int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
+  span = (span + kBlock - 1) & ~(int64_t)(kBlock - 1);
+  if (span < min_tile) span = min_tile;
+  const int64_t r0 = (int64_t)blockIdx.x * span;
+  const int64_t r1 = min(r0 + span, nchunks);
+  if (r0 >= r1) return;
+  block_find2(dst_off, n + 1, (uint64_t)r0 << 4, ((uint64_t)r1 << 4) - 1, s_lo, s_hi, s_cnt);
+  const int64_t ja = s_lo[0], jb = s_lo[1];
+  for (int64_t j0 = ja; j0 <= jb; j0 += kTileSegCap) {
+    const int cnt = (int)min((int64_t)kTileSegCap, jb - j0 + 1);
+    __syncthreads();  // previous pass done with s_off / s_src (and s_lo read above)
+    for (int k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
+    for (int k = threadIdx.x; k < cnt; k += kBlock) s_src[k] = src_off[j0 + k];
     __syncthreads();
-    int64_t jl = 0;
+    const int64_t c0 = max(r0, (int64_t)(s_off[0] >> 4));
+    const int64_t c1 = min(r1, (int64_t)(s_off[cnt] >> 4));
+    int jl = 0;
+    const int64_t nu = (c1 - c0 + kBlock - 1) / kBlock;  // chunks per lane in this pass
 #pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-      constexpr int U = kChunksPerThread / 2;
+    for (int64_t u0 = 0; u0 < nu; u0 += U) {
       const u32x4* sp[U];
-      u32x4 hv[U];
-      uint64_t dofs[U];
+      u32x4 v[U];
+      uint64_t dofs[MODE == 1 ? U : 1];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t c = c0 + (int64_t)(half * U + u) * kBlock + threadIdx.x;
+        const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
         sp[u] = nullptr;
-        dofs[u] = ~0ull;
         if (c >= c1) continue;
         const uint64_t x = (uint64_t)c << 4;
-        int64_t j;
-        uint64_t seg_start, seg_src;
-        if (staged) {
-          jl = seg_search(s_off, jl, cnt, x);
-          j = j0 + jl;
-          seg_start = s_off[jl];
-          seg_src = s_src[jl];
-        } else {
-          j = j0 + seg_search(dst_off + j0, 0, cnt, x);
-          seg_start = dst_off[j];
-          seg_src = MODE == 1 ? (base + dst_off[j]) % cap : src_off[j];
+        // galloping search: last k >= jl with s_off[k] <= x (s_off[jl] <= x holds)
+        int step = 1, hi;
+        while (jl + step < cnt && s_off[jl + step] <= x) {
+          jl += step;
+          step <<= 1;
         }
+        hi = min(jl + step, cnt);
+        while (hi - jl > 1) {
+          const int mid = (jl + hi) >> 1;
+          if (s_off[mid] <= x) jl = mid; else hi = mid;
+        }
+        const uint64_t seg_start = s_off[jl];
+        const uint64_t seg_src = s_src[jl];
         const uint64_t w = x - seg_start;
         if (MODE == 0) {
           sp[u] = reinterpret_cast<const u32x4*>(src + seg_src + w);
-          dofs[u] = x;
         } else {
-          dofs[u] = seg_src + w;
+          const int64_t j = j0 + jl;
+          const uint64_t p = base + seg_start;
+          dofs[u] = (p >= cap ? p - cap : p) + w;
           if (w == 0) {
             const Digest d = keys[j];
-            hv[u] = u32x4{(uint32_t)d.lo, (uint32_t)(d.lo >> 32), (uint32_t)d.hi,
-                          (uint32_t)(d.hi >> 32)};
+            v[u] = u32x4{(uint32_t)d.lo, (uint32_t)(d.lo >> 32), (uint32_t)d.hi,
+                         (uint32_t)(d.hi >> 32)};
           } else if (w == 16) {
-            hv[u] = u32x4{vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic};
+            v[u] = u32x4{vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic};
           } else {
-            sp[u] = reinterpret_cast<const u32x4*>(src + src_off[j] + (w - kItemHeaderBytes));
+            sp[u] = reinterpret_cast<const u32x4*>(src + seg_src + (w - kItemHeaderBytes));
           }
         }
       }
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = sp[u] ? __builtin_nontemporal_load(sp[u]) : hv[u];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (dofs[u] != ~0ull) *reinterpret_cast<u32x4*>(dst + dofs[u]) = v[u];
+        if (sp[u]) v[u] = __builtin_nontemporal_load(sp[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
+        if (c >= c1) continue;
+        const uint64_t d = MODE == 1 ? dofs[MODE == 1 ? u : 0] : (uint64_t)c << 4;
+        *reinterpret_cast<u32x4*>(dst + d) = v[u];
+      }
     }
-    __syncthreads();
+  }
+}
+
+// Co-resident workgroups of a kernel on the current device (occupancy x CUs), cached.
+template <typename K>
+int resident_grid(K kernel, int* cache) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cache[dev] = per_cu > 0 && cus > 0 ? per_cu * cus : kMaxGrid;
+  }
+  return cache[dev];
+}
+
+template <int MODE, int U, int WAVES, typename... Args>
+void launch_segcopy_v(hipStream_t s, Args... args) {
+  static int grid[64];
+  const auto kern = k_segcopy<MODE, U, WAVES>;
+  hipLaunchKernelGGL(kern, dim3(resident_grid(kern, grid)), dim3(kBlock), 0, s, args...,
+                     min_tile_chunks());
+}
+
+template <int MODE, typename... Args>
+void launch_segcopy(hipStream_t s, Args... args) {
+  switch (segcopy_variant()) {
+    case 0: launch_segcopy_v<MODE, 8, 4>(s, args...); break;
+    case 2: launch_segcopy_v<MODE, 6, 6>(s, args...); break;
+    case 3: launch_segcopy_v<MODE, 2, 8>(s, args...); break;
+    case 4: launch_segcopy_v<MODE, 8, 6>(s, args...); break;
+    case 5: launch_segcopy_v<MODE, 16, 4>(s, args...); break;
+    default: launch_segcopy_v<MODE, 4, 8>(s, args...);
   }
 }
 
@@ -700,8 +770,8 @@ void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* t
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
              uint8_t* dst, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_segcopy<0>, dim3(2048), dim3(kBlock), 0, s, src, src_off, dst_off, n, dst,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, (uint64_t)1);
+  launch_segcopy<0>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr, nullptr,
+                    (uint64_t)1);
   HIP_OK(hipGetLastError());
 }
 
@@ -831,7 +901,7 @@ void HbmCache::reserve(int64_t n) {
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-                      uint32_t now, hipStream_t s) {
+                      uint32_t now, hipStream_t s, uint64_t reserve) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   if (n <= 0) {
@@ -840,7 +910,8 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   }
   ensure_scan_ws(n);
   hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     index_, cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, loc, size, ctr_);
+                     index_, cfg_.nbuckets - 1, cur_head(), reserve, cfg_.log_bytes, now, loc, size,
+                     ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
 }
@@ -868,8 +939,8 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                      dd_win_, dd_slot_, cfg_.max_item, set_size_, ctr_);
   HIP_OK(hipGetLastError());
   device_exclusive_scan(set_size_, set_off_, n, scan_tmp_, scan_tmp_bytes_, s);
-  hipLaunchKernelGGL(k_segcopy<1>, dim3(2048), dim3(kBlock), 0, s, values, val_off, set_off_, n,
-                     log_, keys, vlen, flags, expire, cur_head(), cfg_.log_bytes);
+  launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
+                    cfg_.log_bytes);
   HIP_OK(hipGetLastError());
   const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,

@@ -36,7 +36,8 @@ HostCache::~HostCache() {
   munmap(index_, index_alloc_);
 }
 
-uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) const {
+uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen,
+                                 uint64_t reserve) const {
   uint64_t best = 0;
   uint32_t bv = 0;
   const uint64_t bs[2] = {bucket1(d, mask_), bucket2(d, mask_)};
@@ -44,7 +45,7 @@ uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) 
     const Entry* e = index_ + b * kEntriesPerBucket;
     for (uint32_t k = 0; k < kEntriesPerBucket; ++k) {
       if (e[k].d0 == d.lo && e[k].d1 == d.hi &&
-          entry_live(e[k].loc, e[k].expire, head_, log_bytes_, now) && e[k].loc > best) {
+          entry_live(e[k].loc, e[k].expire, head_ + reserve, log_bytes_, now) && e[k].loc > best) {
         best = e[k].loc;
         bv = e[k].vlen;
       }
@@ -55,12 +56,12 @@ uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) 
 }
 
 void HostCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size,
-                       uint64_t* off, uint32_t now) {
+                       uint64_t* off, uint32_t now, uint64_t reserve) {
   std::lock_guard<std::mutex> lk(mu_);
   uint64_t acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     uint32_t vl = 0;
-    const uint64_t l = probe_locked(keys[i], now, &vl);
+    const uint64_t l = probe_locked(keys[i], now, &vl, reserve);
     ctr_.get_ops++;
     if (l) {
       loc[i] = (l - 1) % log_bytes_;

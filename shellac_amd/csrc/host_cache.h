@@ -22,7 +22,7 @@ class HostCache {
   HostCache& operator=(const HostCache&) = delete;
 
   void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-              uint32_t now);
+              uint32_t now, uint64_t reserve = 0);
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out) const;
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
@@ -49,7 +49,7 @@ class HostCache {
 
  private:
   bool insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uint32_t expire, uint32_t now);
-  uint64_t probe_locked(const Digest& d, uint32_t now, uint32_t* vlen) const;
+  uint64_t probe_locked(const Digest& d, uint32_t now, uint32_t* vlen, uint64_t reserve = 0) const;
 
   uint64_t log_bytes_, nbuckets_, mask_;
   uint32_t max_item_;

@@ -98,6 +98,7 @@ class ShardedCache:
         self.sample_batches = sample_batches
         self._samples: List[torch.Tensor] = []
         self._hot: Optional[torch.Tensor] = None   # sorted hot digests [h, 2] (same on all ranks)
+        self._pinned: Optional[torch.Tensor] = None  # host landing slot for a GET's total bytes
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -185,6 +186,37 @@ class ShardedCache:
         self.stats["remote_gets"] += n_remote - int(send_rows[self.rank])
         self.stats["replica_hits"] += n_local
         return GetResult(data, off, size)
+
+    def serve(self, keys: torch.Tensor, batch: SetBatch, now: Optional[int] = None) -> GetResult:
+        """One serving step: a GET batch and a SET batch, GETs ordered before SETs.
+
+        With one rank the GET's extent read (the only host sync) is hidden behind
+        the SET kernels: the lookup reserves the SET's log bytes (objects the SET may
+        overwrite count as misses), its total is copied to pinned memory, the SET is
+        queued, and only then does the host wait for the total to size the gather.
+        With several ranks the routed get() and set() run back to back."""
+        if self.world > 1:
+            res = self.get(keys, now)
+            self.set(batch, now)
+            return res
+        n = keys.shape[0]
+        self.stats["get_requests"] += n
+        self.stats["set_requests"] += batch.keys.shape[0]
+        sh = self.shard
+        lk = sh.lookup(keys, now, reserve_bytes=sh.set_bound(batch.keys.shape[0],
+                                                             batch.values.numel()))
+        if self._pinned is None:
+            self._pinned = torch.empty(1, dtype=torch.int64, pin_memory=sh.is_gpu)
+        self._pinned.copy_(lk.off[n:], non_blocking=sh.is_gpu)
+        ev = None
+        if sh.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags, batch.expire, now)
+        if ev is not None:
+            ev.synchronize()
+        data = sh.gather(lk, total=int(self._pinned[0]))
+        return GetResult(data, lk.off[:n], lk.size[:n])
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
         n = batch.keys.shape[0]

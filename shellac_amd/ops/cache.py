@@ -171,7 +171,11 @@ class CacheShard:
             raise ValueError(f"{name} must be contiguous")
 
     # -- GET ----------------------------------------------------------------------
-    def lookup(self, keys: torch.Tensor, now: Optional[int] = None) -> Lookup:
+    def lookup(self, keys: torch.Tensor, now: Optional[int] = None,
+               reserve_bytes: int = 0) -> Lookup:
+        """Probe the index. ``reserve_bytes`` > 0 also misses objects that the next
+        ``reserve_bytes`` of log appends would overwrite, so a SET of at most that many
+        bytes (``set_bound``) may run between this lookup and its gather."""
         self._check(keys, "keys")
         n = keys.shape[0]
         loc = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -180,11 +184,11 @@ class CacheShard:
         now = self.now() if now is None else now
         if self.is_gpu:
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
-                              now, self._s())
+                              now, self._s(), int(reserve_bytes))
         else:
             size[n] = 0
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
-                              now)
+                              now, int(reserve_bytes))
         return Lookup(loc, size, off)
 
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
@@ -207,6 +211,12 @@ class CacheShard:
         return out, lk.off[: lk.n], lk.size[: lk.n]
 
     # -- SET ----------------------------------------------------------------------
+    @staticmethod
+    def set_bound(n: int, payload_bytes: int) -> int:
+        """Upper bound of the log bytes a SET of ``n`` values from a ``payload_bytes``
+        buffer appends (32-B header + value, 16-B aligned, per item)."""
+        return 48 * int(n) + int(payload_bytes)
+
     def store(self, keys: torch.Tensor, values: torch.Tensor, val_off: torch.Tensor,
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None) -> None:
@@ -221,7 +231,7 @@ class CacheShard:
         fp = 0 if flags is None else flags.data_ptr()
         ep = 0 if expire is None else expire.data_ptr()
         if self.is_gpu:
-            bound = 48 * n + values.numel()
+            bound = self.set_bound(n, values.numel())
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s())
         else:

@@ -74,6 +74,39 @@ def test_fifo_log_eviction():
     assert all(got[i] == bytes([(i // 10 * 10) % 256]) * 1000 for i in alive)
 
 
+def check_reserve_lookup_survives_queued_set(dev):
+    """A lookup that reserves a SET's log bytes stays valid after that SET runs."""
+    s = CacheShard(64 << 10, 1 << 8, 4096, dev)
+    keys = [f"/r/{i}".encode() for i in range(60)]
+    vals = [bytes([i]) * 1000 for i in range(60)]
+    for i in range(0, 60, 10):
+        s.set_many(keys[i : i + 10], vals[i : i + 10])
+    d = digest_strings(keys, s.device)
+    plain = s.lookup(d).hits().cpu()
+    newk = [f"/n/{i}".encode() for i in range(12)]
+    v, vo, vl = pack_values([b"x" * 1000] * 12, s.device)
+    bound = CacheShard.set_bound(12, v.numel())
+    lk = s.lookup(d, reserve_bytes=bound)
+    res_hits = lk.hits().cpu()
+    # the reserved lookup drops exactly the oldest objects (a prefix of the FIFO)
+    assert res_hits.sum() < plain.sum()
+    first = int(res_hits.nonzero()[0])
+    assert not res_hits[:first].any() and res_hits[first:].all() and plain[first:].all()
+    s.store(digest_strings(newk, s.device), v, vo, vl)   # overwrites the oldest objects
+    out = s.gather(lk)
+    recs = unpack_records(out, lk.off[: lk.n], lk.size[: lk.n])
+    for i, r in enumerate(recs):
+        assert (r is None) == (not bool(res_hits[i]))
+        if r is not None:
+            assert r[0] == vals[i]
+    got = s.get_many(keys)
+    assert sum(g is not None for g in got) >= int(res_hits.sum())  # the bound is conservative
+
+
+def test_reserve_lookup_survives_queued_set():
+    check_reserve_lookup_survives_queued_set("cpu")
+
+
 def test_too_large_rejected():
     s = make(max_item=100)
     s.set_many([b"/big", b"/ok"], [b"z" * 101, b"z" * 100])

@@ -202,3 +202,43 @@ def test_export_keys_and_snapshot_roundtrip(cuda_dev, tmp_path):
     g2.load(path)
     rg, _, _, _ = _get_both(g2, h, keys, 3)
     assert [r[0] if r else None for r in rg] == [None] * 100 + vals[100:]
+
+
+def test_reserve_lookup_survives_queued_set_gpu(cuda_dev):
+    from test_cache_semantics import check_reserve_lookup_survives_queued_set
+
+    check_reserve_lookup_survives_queued_set(cuda_dev)
+
+
+def test_serve_overlapped_matches_get_then_set(cuda_dev):
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(20000, cuda_dev)
+    outs = []
+    for mode in ("serve", "seq"):
+        sc = ShardedCache(CacheShard(256 << 20, 1 << 14, 1 << 16, cuda_dev))
+        for s0 in range(0, 20000, 5000):
+            sc.set(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev)))
+        keys = wl.digests.index_select(0, wl.sample_ids(4096, 3)).contiguous()
+        sb = wl.set_batch(wl.uniform_ids(2048, 4))
+        if mode == "serve":
+            r = sc.serve(keys, sb)
+        else:
+            r = sc.get(keys)
+            sc.set(sb)
+        outs.append((r.size.cpu(), r.data[: int(r.off[-1] + r.size[-1])].cpu()))
+        after = sc.get(keys)
+        outs.append((after.size.cpu(),))
+    (s1, d1), (a1,), (s2, d2), (a2,) = outs
+    # the reserved lookup may miss objects the SET could evict, never hit more
+    hit1, hit2 = s1 > 0, s2 > 0
+    assert not (hit1 & ~hit2).any()
+    assert hit1.float().mean() > 0.5
+    assert torch.equal(a1, a2)
+    ids = wl.sample_ids(4096, 3).cpu()
+    o1 = torch.cumsum(torch.cat([torch.zeros(1, dtype=s1.dtype), s1[:-1]]), 0)
+    for i in range(0, 4096, 97):
+        if hit1[i]:
+            rec = d1[o1[i] + 32 : o1[i] + 32 + s1[i] - 32].numpy().tobytes()
+            assert rec.startswith(wl.expected_value(int(ids[i])))
