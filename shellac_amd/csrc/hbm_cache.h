@@ -78,7 +78,6 @@ class HbmCache {
 
  private:
   void ensure_set_ws(int64_t n, hipStream_t s);
-  void ensure_scan_ws(int64_t n);
 
   ShardConfig cfg_;
   uint8_t* log_ = nullptr;
@@ -89,6 +88,7 @@ class HbmCache {
   uint64_t* next_head() const { return head_ + (hsel_ ^ 1); }
   CacheCounters* ctr_ = nullptr;     // device counters (64 shards)
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
+  uint64_t* part_ = nullptr;         // per-workgroup size sums: [0,kMaxGrid) GET, then SET
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
   // SET workspace
   int64_t set_cap_ = 0;
@@ -98,10 +98,6 @@ class HbmCache {
   uint64_t* set_size_ = nullptr;
   uint64_t* set_off_ = nullptr;
   uint32_t dd_mask_ = 0;
-  // scan workspace
-  void* scan_tmp_ = nullptr;
-  size_t scan_tmp_bytes_ = 0;
-  int64_t scan_cap_ = 0;
   std::mutex mu_;
 };
 

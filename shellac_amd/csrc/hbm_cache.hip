@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -135,6 +136,76 @@ __device__ __forceinline__ void block_count(CacheCounters* shards, unsigned long
   }
 }
 
+// Block-wide sum of v written to part[blockIdx.x] (every thread must call it).
+__device__ __forceinline__ void block_partial(unsigned long long v, uint64_t* __restrict__ part) {
+  __shared__ unsigned long long s_p[kBlock / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_p[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += s_p[k];
+    part[blockIdx.x] = t;
+  }
+}
+
+// Items per workgroup when n items are split into contiguous ranges over `grid` groups.
+__host__ __device__ __forceinline__ int64_t part_len(int64_t n, int grid) {
+  return (n + grid - 1) / grid;
+}
+
+// Second half of a two-kernel exclusive scan whose first half is fused into the
+// producer (k_probe / k_set_size write one partial sum per workgroup over contiguous
+// ranges of `plen` items). Workgroup b covers producer groups [b*q, (b+1)*q): it sums
+// the partials before its range, then scans its items, `per` consecutive ones per lane.
+// off[n] = total. Replaces hipcub's init + scan pair (one launch, no lookback state).
+__global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__ size, int64_t n,
+                                                    const uint64_t* __restrict__ part, int nparts,
+                                                    int64_t plen, int q,
+                                                    uint64_t* __restrict__ off) {
+  __shared__ unsigned long long s_w[kBlock / 64];
+  __shared__ unsigned long long s_base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p0 = blockIdx.x * q;
+  unsigned long long pre = 0;
+  for (int k = threadIdx.x; k < p0 && k < nparts; k += kBlock) pre += part[k];
+  pre = wave_sum(pre);
+  if (lane == 0) s_w[w] = pre;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += s_w[k];
+    s_base = t;
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)p0 * plen;
+  const int64_t i1 = min(n, (int64_t)(p0 + q) * plen);
+  const int64_t per = (i1 - i0 + kBlock - 1) / kBlock;
+  const int64_t a = min(i1, i0 + per * threadIdx.x), b = min(i1, a + per);
+  unsigned long long mine = 0;
+  for (int64_t i = a; i < b; ++i) mine += size[i];
+  // inclusive wave scan of the lane sums, then the waves' totals
+  unsigned long long inc = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  unsigned long long run = s_base;
+  for (int k = 0; k < w; ++k) run += s_w[k];
+  run += inc - mine;
+  for (int64_t i = a; i < b; ++i) {
+    off[i] = run;
+    run += size[i];
+  }
+  if (i1 == n && b == n && a < b) off[n] = run;
+  if (i1 == n && i0 == n && threadIdx.x == 0) off[n] = s_base;
+}
+
 __device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
   return ((uint64_t)hi << 32) | lo;
 }
@@ -148,15 +219,18 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
                                                   uint64_t reserve, uint64_t cap, uint32_t now,
                                                   uint64_t* __restrict__ out_loc,
                                                   uint64_t* __restrict__ out_size,
-                                                  CacheCounters* __restrict__ ctr) {
+                                                  CacheCounters* __restrict__ ctr,
+                                                  uint64_t* __restrict__ part) {
   const int l16 = threadIdx.x & 15;
   // `reserve`: bytes about to be appended before this lookup's gather runs; objects
   // that those appends will overwrite are already treated as evicted
   const uint64_t head = *head_ptr + reserve;
-  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
-  unsigned long long hits = 0, bytes = 0, ops = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;  // scan reads n+1 sizes
-  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
+  unsigned long long hits = 0, bytes = 0, ops = 0, psum = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;
+  // contiguous key range per workgroup (k_offsets scans it from the partial sums)
+  const int64_t plen = part_len(n, gridDim.x);
+  const int64_t i1 = min(n, (int64_t)(blockIdx.x + 1) * plen);
+  for (int64_t i = (int64_t)blockIdx.x * plen + (threadIdx.x >> 4); i < i1; i += kBlock / 16) {
     const Digest d = keys[i];
     const uint64_t b = (l16 < 8) ? bucket1(d, mask) : bucket2(d, mask);
     const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l16 & 7];
@@ -182,6 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
         out_size[i] = item_bytes(hv);
         ++hits;
         bytes += hv;
+        psum += item_bytes(hv);
       } else {
         out_loc[i] = kMissLoc;
         out_size[i] = 0;
@@ -190,6 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   }
   block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
               &CacheCounters::get_bytes);
+  block_partial(psum, part);
 }
 
 // ---------------------------------------------------------------------------------
@@ -419,18 +495,23 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ slot_of,
                                                      uint32_t max_item,
                                                      uint64_t* __restrict__ size,
-                                                     CacheCounters* __restrict__ ctr) {
-  unsigned long long dropped = 0, ops = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i <= n;
-       i += (int64_t)gridDim.x * kBlock) {
-    if (i == n) { size[n] = 0; continue; }
+                                                     CacheCounters* __restrict__ ctr,
+                                                     uint64_t* __restrict__ part) {
+  unsigned long long dropped = 0, ops = 0, psum = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) size[n] = 0;
+  const int64_t plen = part_len(n, gridDim.x);
+  const int64_t i1 = min(n, (int64_t)(blockIdx.x + 1) * plen);
+  for (int64_t i = (int64_t)blockIdx.x * plen + threadIdx.x; i < i1; i += kBlock) {
     if (vlen[i] == kSkipVlen) { size[i] = 0; continue; }  // row addressed to another tier
     const bool win = tw[slot_of[i]] == (int)i && vlen[i] <= max_item;
-    size[i] = win ? item_bytes(vlen[i]) : 0;
+    const uint64_t sz = win ? item_bytes(vlen[i]) : 0;
+    size[i] = sz;
+    psum += sz;
     ++ops;
     dropped += win ? 0 : 1;
   }
   block_count(ctr, ops, &CacheCounters::set_ops, dropped, &CacheCounters::set_dropped);
+  block_partial(psum, part);
 }
 
 __global__ __launch_bounds__(kBlock) void k_set_index(
@@ -760,6 +841,16 @@ size_t device_scan_tmp_bytes(int64_t n) {
   return bytes;
 }
 
+// k_offsets launch for sizes produced by `grid` workgroups over contiguous ranges.
+void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
+                    uint64_t* off, hipStream_t s) {
+  const int64_t plen = part_len(n, grid);
+  const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
+  const int g2 = (grid + q - 1) / q;
+  hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off);
+  HIP_OK(hipGetLastError());
+}
+
 void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* tmp,
                            size_t tmp_bytes, hipStream_t s) {
   // in must be readable at [0, n]; the caller guarantees in[n] == 0.
@@ -830,6 +921,7 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&head_, 64));
   HIP_OK(hipMalloc(&ctr_, kCtrShards * sizeof(CacheCounters)));
   HIP_OK(hipMalloc(&scratch_, 64));
+  HIP_OK(hipMalloc(&part_, 2 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
@@ -845,31 +937,17 @@ HbmCache::~HbmCache() {
   (void)hipFree(head_);
   (void)hipFree(ctr_);
   (void)hipFree(scratch_);
+  (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipFree(dd_keys_);
   (void)hipFree(dd_win_);
   (void)hipFree(dd_slot_);
   (void)hipFree(set_size_);
   (void)hipFree(set_off_);
-  (void)hipFree(scan_tmp_);
 }
 
 uint64_t HbmCache::hbm_bytes() const {
   return cfg_.log_bytes + item_bytes(cfg_.max_item) + 64 + cfg_.nbuckets * kBucketBytes;
-}
-
-void HbmCache::ensure_scan_ws(int64_t n) {
-  if (n <= scan_cap_) return;
-  int64_t cap = scan_cap_ ? scan_cap_ : 1024;
-  while (cap < n) cap *= 2;
-  const size_t need = device_scan_tmp_bytes(cap);
-  if (need > scan_tmp_bytes_) {
-    HIP_OK(hipDeviceSynchronize());
-    (void)hipFree(scan_tmp_);
-    HIP_OK(hipMalloc(&scan_tmp_, need));
-    scan_tmp_bytes_ = need;
-  }
-  scan_cap_ = cap;
 }
 
 void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
@@ -897,7 +975,6 @@ void HbmCache::reserve(int64_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, nullptr);
-  ensure_scan_ws(n);
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
@@ -908,12 +985,11 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
     HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
     return;
   }
-  ensure_scan_ws(n);
-  hipLaunchKernelGGL(k_probe, dim3(grid_for(n * 16, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     index_, cfg_.nbuckets - 1, cur_head(), reserve, cfg_.log_bytes, now, loc, size,
-                     ctr_);
+  const int grid = grid_for(n * 16, kBlock, kMaxGrid);
+  hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
+                     cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_);
   HIP_OK(hipGetLastError());
-  device_exclusive_scan(size, off, n, scan_tmp_, scan_tmp_bytes_, s);
+  launch_offsets(size, n, part_, grid, off, s);
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
@@ -931,14 +1007,14 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, s);
-  ensure_scan_ws(n);
   const int grid = grid_for(n, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
-  hipLaunchKernelGGL(k_set_size, dim3(grid_for(n + 1, kBlock, kMaxGrid)), dim3(kBlock), 0, s, vlen, n,
-                     dd_win_, dd_slot_, cfg_.max_item, set_size_, ctr_);
+  const int sgrid = grid_for(n, kBlock, kMaxGrid);
+  hipLaunchKernelGGL(k_set_size, dim3(sgrid), dim3(kBlock), 0, s, vlen, n, dd_win_, dd_slot_,
+                     cfg_.max_item, set_size_, ctr_, part_ + kMaxGrid);
   HIP_OK(hipGetLastError());
-  device_exclusive_scan(set_size_, set_off_, n, scan_tmp_, scan_tmp_bytes_, s);
+  launch_offsets(set_size_, n, part_ + kMaxGrid, sgrid, set_off_, s);
   launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());

@@ -242,3 +242,24 @@ def test_serve_overlapped_matches_get_then_set(cuda_dev):
         if hit1[i]:
             rec = d1[o1[i] + 32 : o1[i] + 32 + s1[i] - 32].numpy().tobytes()
             assert rec.startswith(wl.expected_value(int(ids[i])))
+
+
+@pytest.mark.parametrize("n", [1, 5, 17, 255, 2049, 40001, 300007])
+def test_lookup_offsets_fused_scan(cuda_dev, n):
+    """k_probe's per-workgroup partials + k_offsets == exclusive cumsum of sizes."""
+    shard = CacheShard(64 << 20, 1 << 18, 1 << 12, cuda_dev)
+    g = torch.Generator().manual_seed(n)
+    keys = torch.randint(-2**62, 2**62, (n, 2), generator=g, dtype=torch.int64)
+    vl = torch.randint(0, 200, (n,), generator=g, dtype=torch.int32)
+    store = torch.rand(n, generator=g) < 0.6
+    ks = keys[store].contiguous().to(cuda_dev)
+    vls = vl[store].contiguous()
+    vo = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), vls.long()]), 0)[:-1]
+    pay = torch.zeros(int(vls.sum()) + 16, dtype=torch.uint8, device=cuda_dev)
+    if ks.shape[0]:
+        shard.store(ks, pay, vo.contiguous().to(cuda_dev), vls.to(cuda_dev))
+    lk = shard.lookup(keys.to(cuda_dev))
+    size = lk.size[:n].cpu()
+    assert torch.equal(size > 0, store)
+    ref = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), size]), 0)
+    assert torch.equal(lk.off.cpu(), ref)
