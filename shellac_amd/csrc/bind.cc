@@ -67,12 +67,17 @@ PYBIND11_MODULE(_shellac_core, m) {
            }),
            py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"))
       .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
-                        uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve) {
+                        uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve, int slot) {
         py::gil_scoped_release nogil;
         c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
-                 now, S(s), reserve);
+                 now, S(s), reserve, slot);
       }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
-         py::arg("now"), py::arg("stream"), py::arg("reserve") = 0)
+         py::arg("now"), py::arg("stream"), py::arg("reserve") = 0, py::arg("total_slot") = -1)
+      .def("host_slot", &HbmCache::host_slot)
+      .def("wait_host_slot", [](const HbmCache& c, int i, int64_t timeout_ms) {
+        py::gil_scoped_release nogil;
+        return c.wait_host_slot(i, timeout_ms);
+      }, py::arg("slot"), py::arg("timeout_ms") = 10000)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
                         uintptr_t s) {
         py::gil_scoped_release nogil;

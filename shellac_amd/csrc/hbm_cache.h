@@ -41,8 +41,18 @@ class HbmCache {
   // sizes into off[0..n] (off[n] = total response bytes).
   // `reserve` > 0 treats objects that the next `reserve` appended bytes will
   // overwrite as misses, so SETs may be queued between this lookup and its gather.
+  // `total_slot` >= 0 also writes off[n] straight into host slot `total_slot` (pinned,
+  // coherent), readable with host_slot() once the stream has passed the lookup: the
+  // response size without a D2H copy.
   void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-              uint32_t now, hipStream_t s, uint64_t reserve = 0);
+              uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1);
+  uint64_t host_slot(int i) const;
+  // Spin until the lookup that was given `total_slot` i has written it (no stream or
+  // event synchronisation: the kernel's system-scope store is the signal). Throws after
+  // timeout_ms. Each lookup that names a slot must be waited for before the slot is reused.
+  uint64_t wait_host_slot(int i, int64_t timeout_ms = 10000) const;
+  static constexpr int kHostSlots = 64;
+  static constexpr uint64_t kSlotPending = ~0ull;
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i].
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
@@ -90,6 +100,7 @@ class HbmCache {
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
   uint64_t* part_ = nullptr;         // per-workgroup size sums: [0,kMaxGrid) GET, then SET
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
+  uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;

@@ -163,7 +163,8 @@ __host__ __device__ __forceinline__ int64_t part_len(int64_t n, int grid) {
 __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__ size, int64_t n,
                                                     const uint64_t* __restrict__ part, int nparts,
                                                     int64_t plen, int q,
-                                                    uint64_t* __restrict__ off) {
+                                                    uint64_t* __restrict__ off,
+                                                    uint64_t* __restrict__ host_total) {
   __shared__ unsigned long long s_w[kBlock / 64];
   __shared__ unsigned long long s_base;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -202,8 +203,11 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
     off[i] = run;
     run += size[i];
   }
-  if (i1 == n && b == n && a < b) off[n] = run;
-  if (i1 == n && i0 == n && threadIdx.x == 0) off[n] = s_base;
+  if ((i1 == n && b == n && a < b) || (i1 == n && i0 == n && threadIdx.x == 0)) {
+    off[n] = run;  // the lane holding item n-1 (or lane 0 of an empty tail range)
+    if (host_total)
+      __hip_atomic_store(host_total, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 __device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
@@ -843,11 +847,12 @@ size_t device_scan_tmp_bytes(int64_t n) {
 
 // k_offsets launch for sizes produced by `grid` workgroups over contiguous ranges.
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
-                    uint64_t* off, hipStream_t s) {
+                    uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr) {
   const int64_t plen = part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
-  hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off);
+  hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
+                     host_total);
   HIP_OK(hipGetLastError());
 }
 
@@ -923,6 +928,9 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&scratch_, 64));
   HIP_OK(hipMalloc(&part_, 2 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
+  HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(host_slots_, 0, kHostSlots * sizeof(uint64_t));
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
   HIP_OK(hipMemset(ctr_, 0, kCtrShards * sizeof(CacheCounters)));
@@ -939,6 +947,7 @@ HbmCache::~HbmCache() {
   (void)hipFree(scratch_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
+  (void)hipHostFree(host_slots_);
   (void)hipFree(dd_keys_);
   (void)hipFree(dd_win_);
   (void)hipFree(dd_slot_);
@@ -978,18 +987,45 @@ void HbmCache::reserve(int64_t n) {
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-                      uint32_t now, hipStream_t s, uint64_t reserve) {
+                      uint32_t now, hipStream_t s, uint64_t reserve, int total_slot) {
+  SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
+  uint64_t* ht = total_slot >= 0 ? host_slots_ + total_slot : nullptr;
+  if (ht) __atomic_store_n(ht, kSlotPending, __ATOMIC_RELEASE);
   if (n <= 0) {
     HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
+    if (ht) *ht = 0;
     return;
   }
   const int grid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s);
+  launch_offsets(size, n, part_, grid, off, s, ht);
+}
+
+uint64_t HbmCache::host_slot(int i) const {
+  SH_CHECK(i >= 0 && i < kHostSlots, "host slot out of range");
+  return __atomic_load_n(host_slots_ + i, __ATOMIC_ACQUIRE);
+}
+
+uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
+  SH_CHECK(i >= 0 && i < kHostSlots, "host slot out of range");
+  const uint64_t* p = host_slots_ + i;
+  uint64_t v = __atomic_load_n(p, __ATOMIC_ACQUIRE);
+  if (v != kSlotPending) return v;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    v = __atomic_load_n(p, __ATOMIC_ACQUIRE);
+    if (v != kSlotPending) return v;
+    if ((spin & 1023) == 1023) {
+      const auto el = std::chrono::steady_clock::now() - t0;
+      SH_CHECK(std::chrono::duration_cast<std::chrono::milliseconds>(el).count() < timeout_ms,
+               "timed out waiting for a lookup total (GPU stalled?)");
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,

@@ -98,7 +98,6 @@ class ShardedCache:
         self.sample_batches = sample_batches
         self._samples: List[torch.Tensor] = []
         self._hot: Optional[torch.Tensor] = None   # sorted hot digests [h, 2] (same on all ranks)
-        self._pinned: Optional[torch.Tensor] = None  # host landing slot for a GET's total bytes
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -192,8 +191,9 @@ class ShardedCache:
 
         With one rank the GET's extent read (the only host sync) is hidden behind
         the SET kernels: the lookup reserves the SET's log bytes (objects the SET may
-        overwrite count as misses), its total is copied to pinned memory, the SET is
-        queued, and only then does the host wait for the total to size the gather.
+        overwrite count as misses) and its kernel writes the total into a pinned host
+        slot; the SET is queued, and only then does the host spin on that slot to size
+        the gather (no event, no copy).
         With several ranks the routed get() and set() run back to back."""
         if self.world > 1:
             res = self.get(keys, now)
@@ -203,19 +203,16 @@ class ShardedCache:
         self.stats["get_requests"] += n
         self.stats["set_requests"] += batch.keys.shape[0]
         sh = self.shard
-        lk = sh.lookup(keys, now, reserve_bytes=sh.set_bound(batch.keys.shape[0],
-                                                             batch.values.numel()))
-        if self._pinned is None:
-            self._pinned = torch.empty(1, dtype=torch.int64, pin_memory=sh.is_gpu)
-        self._pinned.copy_(lk.off[n:], non_blocking=sh.is_gpu)
-        ev = None
-        if sh.is_gpu:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
+        bound = sh.set_bound(batch.keys.shape[0], batch.values.numel())
+        if not sh.is_gpu:
+            lk = sh.lookup(keys, now, reserve_bytes=bound)
+            sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                     batch.expire, now)
+            data = sh.gather(lk)
+            return GetResult(data, lk.off[:n], lk.size[:n])
+        lk = sh.lookup(keys, now, reserve_bytes=bound, total_slot=0)
         sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags, batch.expire, now)
-        if ev is not None:
-            ev.synchronize()
-        data = sh.gather(lk, total=int(self._pinned[0]))
+        data = sh.gather(lk, total=sh.host_total(0))
         return GetResult(data, lk.off[:n], lk.size[:n])
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:

@@ -172,10 +172,12 @@ class CacheShard:
 
     # -- GET ----------------------------------------------------------------------
     def lookup(self, keys: torch.Tensor, now: Optional[int] = None,
-               reserve_bytes: int = 0) -> Lookup:
+               reserve_bytes: int = 0, total_slot: int = -1) -> Lookup:
         """Probe the index. ``reserve_bytes`` > 0 also misses objects that the next
         ``reserve_bytes`` of log appends would overwrite, so a SET of at most that many
-        bytes (``set_bound``) may run between this lookup and its gather."""
+        bytes (``set_bound``) may run between this lookup and its gather.
+        ``total_slot`` >= 0 (GPU) has the kernel write off[n] into that pinned host slot
+        (``host_total``), so the response size needs no device-to-host copy."""
         self._check(keys, "keys")
         n = keys.shape[0]
         loc = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -184,12 +186,17 @@ class CacheShard:
         now = self.now() if now is None else now
         if self.is_gpu:
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
-                              now, self._s(), int(reserve_bytes))
+                              now, self._s(), int(reserve_bytes), int(total_slot))
         else:
             size[n] = 0
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
                               now, int(reserve_bytes))
         return Lookup(loc, size, off)
+
+    def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
+        """Total bytes of the last lookup given ``total_slot=slot``: spins on the pinned
+        slot until the kernel has written it (no stream or event synchronisation)."""
+        return int(self._impl.wait_host_slot(slot, timeout_ms))
 
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
                total: Optional[int] = None) -> torch.Tensor:
@@ -206,8 +213,11 @@ class CacheShard:
 
     def get(self, keys: torch.Tensor, now: Optional[int] = None):
         """lookup + gather. Returns (out bytes, off[n], size[n]); record i = out[off[i]:+size[i]]."""
-        lk = self.lookup(keys, now)
-        out = self.gather(lk)
+        if not self.is_gpu:
+            lk = self.lookup(keys, now)
+            return self.gather(lk), lk.off[: lk.n], lk.size[: lk.n]
+        lk = self.lookup(keys, now, total_slot=1)
+        out = self.gather(lk, total=self.host_total(1))
         return out, lk.off[: lk.n], lk.size[: lk.n]
 
     # -- SET ----------------------------------------------------------------------

@@ -263,3 +263,6 @@ def test_lookup_offsets_fused_scan(cuda_dev, n):
     assert torch.equal(size > 0, store)
     ref = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), size]), 0)
     assert torch.equal(lk.off.cpu(), ref)
+    # the kernel-written host slot carries the same total without a D2H copy
+    shard.lookup(keys.to(cuda_dev), total_slot=3)
+    assert shard.host_total(3) == int(ref[-1])
