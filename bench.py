@@ -52,9 +52,15 @@ def parse():
     ap.add_argument("--log-gb", type=float, default=16.0, help="value-log GiB per shard")
     ap.add_argument("--set-dist", choices=["uniform", "zipf"], default="uniform",
                     help="SET popularity: uniform (TTL refresh fills, default) or zipf")
-    ap.add_argument("--replicate", type=int, default=65536,
+    ap.add_argument("--replicate", type=int, default=1 << 20,
                     help="hot objects replicated on every rank (N>1; 0 = off)")
-    ap.add_argument("--replica-gb", type=float, default=1.0)
+    ap.add_argument("--replica-gb", type=float, default=2.0)
+    ap.add_argument("--sample-batches", type=int, default=8,
+                    help="GET batches (independent of the timed ones) observed to pick the "
+                         "replicated hot set")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = functional rehearsal of the distributed path over gloo "
+                         "(DRAM shards); never a performance number")
     ap.add_argument("--no-smoke", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
@@ -107,10 +113,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if args.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    else:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
 
     total_keys = args.keys_per_gpu * world
     t_setup = time.perf_counter()
@@ -135,7 +150,7 @@ def main():
     for s in range(lo, hi, chunk):
         ids = torch.arange(s, min(s + chunk, hi), device=dev)
         sc.set(wl.set_batch(ids))
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     log(rank, f"[bench] populated {total_keys} keys in {time.perf_counter() - t_setup:.1f}s")
@@ -147,11 +162,14 @@ def main():
     pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
     sets = [wl.set_batch(pick(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
     if replica is not None:
-        # hot-object replica tier from the observed request stream (periodic in a server)
-        nrep = sc.refresh_replica(args.replicate, keys=torch.cat(gets))
+        # hot-object replica tier from an observed request stream (periodic in a server);
+        # the observed batches are independent samples, not the timed ones
+        seen = torch.cat([wl.digests.index_select(0, wl.sample_ids(args.batch, 9000 + 97 * rank + i))
+                          for i in range(args.sample_batches)])
+        nrep = sc.refresh_replica(args.replicate, keys=seen)
+        del seen
         log(rank, f"[bench] replicated {nrep} hot objects on every rank")
     shard.reserve(max(args.sets * 2, chunk))
-    before = shard.counters()
 
     def step(i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
@@ -159,17 +177,19 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    sync()
+    before = shard.counters()
+    st0 = dict(sc.stats)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         res = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -177,13 +197,16 @@ def main():
     elapsed = float(t)
 
     after = shard.counters()
-    hits = after["get_hits"] - before["get_hits"]
-    gops = after["get_ops"] - before["get_ops"]
-    gbytes = after["get_bytes"] - before["get_bytes"]
-    agg = torch.tensor([hits, gops, gbytes], dtype=torch.int64, device=dev)
+    # owner-shard counters cover the GETs that left the replica tier; replica hits
+    # are counted by the serving step
+    rep_hits = sc.stats["replica_hits"] - st0["replica_hits"]
+    agg = torch.tensor([after["get_hits"] - before["get_hits"], after["get_ops"] - before["get_ops"],
+                        after["get_bytes"] - before["get_bytes"], rep_hits,
+                        sc.stats["get_requests"] - st0["get_requests"]], dtype=torch.int64,
+                       device=dev)
     if world > 1:
         dist.all_reduce(agg)
-    hits, gops, gbytes = (int(v) for v in agg.tolist())
+    hits, gops, gbytes, rep_hits, greq = (int(v) for v in agg.tolist())
 
     if args.check:
         # verify the last GET batch against the workload's ground truth
@@ -195,7 +218,7 @@ def main():
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
 
-    sm = {} if args.no_smoke else smoke(rank, world, dev)
+    sm = {} if (args.no_smoke or dev.type != "cuda") else smoke(rank, world, dev)
 
     ops_per_step = (args.batch + args.sets) * world
     ms = elapsed / args.steps * 1e3
@@ -227,11 +250,13 @@ def main():
             "set_dist": args.set_dist,
             "replicated_hot_objects": args.replicate if world > 1 else 0,
         },
-        "get_hit_ratio": round(hits / max(gops, 1), 4),
-        "replica_hit_fraction": round(sc.stats["replica_hits"] / max(sc.stats["get_requests"], 1), 4),
-        "get_value_GBps": round(gbytes / elapsed / 1e9, 2),
+        "get_hit_ratio": round((hits + rep_hits) / max(gops + rep_hits, 1), 4),
+        "replica_hit_fraction": round(rep_hits / max(greq, 1), 4),
+        "get_value_GBps_owner_shards": round(gbytes / elapsed / 1e9, 2),
         "smoke": sm,
     }
+    if dev.type != "cuda":
+        out["data"] = "cpu rehearsal over gloo: functional only, not a performance number"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -404,7 +404,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const uint64_t seg_src = s_src[jl];
         const uint64_t w = x - seg_start;
         if (MODE == 0) {
-          sp[u] = reinterpret_cast<const u32x4*>(src + seg_src + w);
+          // integer address math: src may be null with absolute addresses in src_off
+          sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
         } else {
           const int64_t j = j0 + jl;
           const uint64_t p = base + seg_start;
@@ -416,7 +417,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
           } else if (w == 16) {
             v[u] = u32x4{vlen[j], flags ? flags[j] : 0u, expire ? expire[j] : 0u, kItemMagic};
           } else {
-            sp[u] = reinterpret_cast<const u32x4*>(src + seg_src + (w - kItemHeaderBytes));
+            sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src +
+                                                   (w - kItemHeaderBytes));
           }
         }
       }

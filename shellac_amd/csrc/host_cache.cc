@@ -325,7 +325,8 @@ void host_segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* d
                   uint8_t* dst) {
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t sz = dst_off[i + 1] - dst_off[i];
-    if (sz) std::memcpy(dst + dst_off[i], src + src_off[i], sz);
+    // integer address math: src may be null with absolute addresses in src_off
+    if (sz) std::memcpy(dst + dst_off[i], reinterpret_cast<const uint8_t*>((uintptr_t)src + src_off[i]), sz);
   }
 }
 

@@ -59,6 +59,19 @@ def segcopy(src: torch.Tensor, src_off: torch.Tensor, dst_off: torch.Tensor,
     return dst
 
 
+def gather_segments(addrs: torch.Tensor, dst_off: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """Like ``segcopy`` but segment i comes from the absolute address ``addrs[i]``
+    (e.g. ``t.data_ptr() + k``) so one launch can assemble a buffer out of several
+    tensors. All addresses must be on dst's device; offsets/lengths multiples of 16."""
+    n = addrs.numel()
+    assert dst_off.numel() == n + 1 and addrs.dtype == torch.int64
+    if dst.is_cuda:
+        core().segcopy(0, addrs.data_ptr(), dst_off.data_ptr(), n, dst.data_ptr(), _s(dst))
+    else:
+        core().host_segcopy(0, addrs.data_ptr(), dst_off.data_ptr(), n, dst.data_ptr())
+    return dst
+
+
 def route(keys: torch.Tensor, ring_pts: torch.Tensor, ring_owner: torch.Tensor,
           nranks: int) -> tuple[torch.Tensor, torch.Tensor]:
     """Owner rank of every digest on a consistent-hash ring -> (dest int32 [n], counts int64 [R])."""

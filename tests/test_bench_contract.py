@@ -1,0 +1,40 @@
+"""bench.py contract on the CPU: the distributed serving step rehearsed over gloo
+(world 2, DRAM shards) must print exactly one well-formed JSON line and return
+correct values (--check)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_cpu_rehearsal_world2():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--device", "cpu", "--batch", "4096", "--sets", "512", "--keys-per-gpu", "32768",
+           "--log-gb", "0.125", "--replicate", "4096", "--replica-gb", "0.03",
+           "--sample-batches", "2", "--check"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["config"]["global_batch"] == 2 * (4096 + 512)
+    assert out["get_hit_ratio"] == 1.0
+    assert "0 mismatches" in p.stderr

@@ -16,6 +16,36 @@ def _free_port():
     return p
 
 
+def _run_world(target, world, *args, timeout=240):
+    """Spawn `world` ranks of target(rank, world, port, q, *args); fail fast if one dies."""
+    import queue
+    import time
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    results, t0 = [], time.time()
+    try:
+        while len(results) < world:
+            try:
+                results.append(q.get(timeout=1))
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                assert not dead, f"rank exited with {dead} before reporting"
+                assert time.time() - t0 < timeout, "distributed test timed out"
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    fails = [r for r in results if r[1] != "ok"]
+    assert not fails, fails[0][2]
+    return results
+
+
 def _worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -67,17 +97,7 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_cache_gloo(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    fails = [r for r in results if r[1] != "ok"]
-    assert not fails, fails[0][2]
+    results = _run_world(_worker, world)
     assert all(r[2] == world * (300 * world + 2) for r in results)
 
 
@@ -141,17 +161,7 @@ def _replica_worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_hot_object_replication_gloo(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    fails = [r for r in results if r[1] != "ok"]
-    assert not fails, fails[0][2]
+    _run_world(_replica_worker, world)
 
 
 def _membership_worker(rank, world, port, q, snapdir):
@@ -213,16 +223,63 @@ def _membership_worker(rank, world, port, q, snapdir):
 
 
 def test_shard_failure_rebalance_and_snapshot_gloo(tmp_path):
-    world = 3
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_membership_worker, args=(r, world, port, q, str(tmp_path)))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    results = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    fails = [r for r in results if r[1] != "ok"]
-    assert not fails, fails[0][2]
+    _run_world(_membership_worker, 3, str(tmp_path))
+
+
+def _serve_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SKIP_VLEN, SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+
+        shard = CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu")
+        replica = CacheShard(1 << 20, 1 << 10, 1 << 14, "cpu")
+        sc = ShardedCache(shard, replica=replica)
+
+        def batch(keys, vals, skip_last=False):
+            v, vo, vl = pack_values(vals)
+            if skip_last and len(vals):
+                vl[-1] = SKIP_VLEN          # a row with no value (e.g. a refetch miss)
+            return SetBatch(digest_strings(keys), v, vo, vl,
+                            flags=torch.full((len(keys),), rank, dtype=torch.int32))
+
+        def values(res):
+            return [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+
+        keys = [f"/s{r}/{i}".encode() for r in range(world) for i in range(150)]
+        mine = [k for k in keys if k.startswith(f"/s{rank}/".encode())]
+        # step 1: GETs of everything (all misses) + every rank fills its own keys
+        res = sc.serve(digest_strings(keys), batch(mine, [b"v1" + k * (1 + len(k) % 5)
+                                                          for k in mine]))
+        assert values(res) == [None] * len(keys)
+        hot = keys[:10] + keys[-10:]
+        sc.get(digest_strings(hot * 8))
+        sc.refresh_replica(20)
+        # step 2: GETs see the state before this step's SETs (hot and cold overwrites)
+        upd = hot[:6] + keys[40:60] if rank == 1 else []
+        v1 = [b"v1" + k * (1 + len(k) % 5) for k in keys]
+        res = sc.serve(digest_strings(keys + [b"/none"]),
+                       batch(upd + [b"/skipped"], [b"v2" + k for k in upd] + [b"x"],
+                             skip_last=True))
+        assert values(res) == v1 + [None]
+        # step 3: the overwrites are visible everywhere (replicas written through)
+        res = sc.serve(digest_strings(keys + [b"/skipped"]), batch([], []))
+        expect = {k: b"v2" + k for k in hot[:6] + keys[40:60]}
+        assert values(res) == [expect.get(k, v) for k, v in zip(keys, v1)] + [None]
+        flags = [r[1] if r else None for r in unpack_records(res.data, res.off, res.size)]
+        assert flags[40] == 1 and flags[0] == 1
+        assert sc.stats["replica_hits"] > 0
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fused_serve_step_gloo(world):
+    _run_world(_serve_worker, world)
