@@ -22,6 +22,9 @@ namespace {
 
 constexpr uint64_t kListenId = 1, kEventId = 2, kTimerId = 3, kFirstConnId = 16;
 constexpr int kHistBuckets = 40;
+// Streamed responses: stop reading the upstream while this much waits for a slow
+// client, resume below the low-water mark.
+constexpr uint64_t kStreamHighWater = 8 << 20, kStreamLowWater = 2 << 20;
 
 std::string simple_response(int code, const char* reason, const std::string& server,
                             const std::string& body, const char* ctype = "text/plain",
@@ -59,6 +62,8 @@ struct Slot {
   uint64_t seq = 0;
   StreamBuf out;
   bool ready = false;
+  bool streaming = false;  // response bytes flow out before the response is complete
+  uint64_t stream_up = 0;  // id of the upstream feeding a streamed response
   bool close_after = false;
   std::string fwd;  // serialized request for the miss path
   std::string key;
@@ -75,6 +80,7 @@ struct Conn {
   double ctime = 0, atime = 0;
   bool dead = false;
   bool out_armed = false;
+  bool in_paused = false;  // EPOLLIN withheld (backpressure from a slow client)
   virtual ~Conn() = default;
 };
 
@@ -108,6 +114,8 @@ struct Upstream : Conn {
   double ka_timeout = -1;
   int ka_max = 1 << 30;
   int count = 0;
+  bool streaming = false;       // the front response is being streamed through
+  bool stream_chunked = false;  // ... re-framed as chunked (unknown length)
 };
 
 class Reactor : public Executor {
@@ -124,7 +132,8 @@ class Reactor : public Executor {
   // stats (read by Proxy::stats_json from another thread)
   std::atomic<uint64_t> requests{0}, hits{0}, misses{0}, upstream_reqs{0}, responses{0},
       bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
-      cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0};
+      cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0},
+      streamed{0}, stream_pauses{0};
   std::atomic<uint64_t> hist[kHistBuckets] = {};
 
  private:
@@ -135,6 +144,12 @@ class Reactor : public Executor {
   void on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v);
   void forward(Client* c, Slot* s);
   void on_upstream_response(Upstream* u);
+  void rewrite_response_headers(HttpParser& r);
+  void pause_input(Conn* c, bool paused);
+  void rearm(Conn* c);
+  bool maybe_stream(Upstream* u);
+  void resume_stream(uint64_t up_id);
+  void stream_out(Upstream* u, std::string data, bool last);
   Upstream* pick_upstream(Client* c);
   int choose_server();
   void flush_client(Client* c);
@@ -222,11 +237,22 @@ void Reactor::drain_posted() {
 
 void Reactor::arm(Conn* c, bool out) {
   if (c->dead || c->out_armed == out) return;
+  c->out_armed = out;
+  rearm(c);
+}
+
+void Reactor::pause_input(Conn* c, bool paused) {
+  if (c->dead || c->in_paused == paused) return;
+  c->in_paused = paused;
+  rearm(c);
+}
+
+void Reactor::rearm(Conn* c) {
   epoll_event ev{};
-  ev.events = EPOLLIN | EPOLLRDHUP | (out ? EPOLLOUT : 0);
+  ev.events = (c->in_paused ? 0u : (uint32_t)(EPOLLIN | EPOLLRDHUP)) |
+              (c->out_armed ? (uint32_t)EPOLLOUT : 0u);
   ev.data.u64 = c->id;
   epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
-  c->out_armed = out;
 }
 
 void Reactor::loop() {
@@ -468,10 +494,11 @@ void Reactor::flush_client(Client* c) {
     int cnt = 0;
     size_t want = 0;
     for (auto& s : c->slots) {
-      if (!s->ready || cnt >= 64) break;
+      if (!(s->ready || s->streaming) || cnt >= 64) break;
       const int k = s->out.iov(iov + cnt, 64 - cnt);
       for (int j = 0; j < k; ++j) want += iov[cnt + j].iov_len;
       cnt += k;
+      if (!s->ready) break;  // a response still streaming holds back its successors
     }
     if (cnt == 0) break;
     const ssize_t w = writev(c->fd, iov, cnt);
@@ -487,18 +514,24 @@ void Reactor::flush_client(Client* c) {
     bytes_out += (uint64_t)w;
     c->atime = now_s();
     size_t left = (size_t)w;
-    while (!c->slots.empty() && c->slots.front()->ready) {
+    while (!c->slots.empty() && (c->slots.front()->ready || c->slots.front()->streaming)) {
       Slot* s = c->slots.front().get();
       const size_t take = std::min<size_t>(left, s->out.pending());
       s->out.ack(take);
       left -= take;
       if (!s->out.complete()) break;
       const bool last = s->close_after;
+      if (s->stream_up) resume_stream(s->stream_up);
       c->slots.pop_front();
       if (last) {  // "Connection: close" / max requests reached / bad request
         close_client(c);
         return;
       }
+    }
+    if (!c->slots.empty()) {
+      Slot* f = c->slots.front().get();
+      if (f->streaming && f->stream_up && f->out.pending() < kStreamLowWater)
+        resume_stream(f->stream_up);
     }
     if ((size_t)w < want) {
       arm(c, true);
@@ -525,6 +558,8 @@ void Reactor::close_client(Client* c) {
     if (c->up->owner == c) c->up->owner = nullptr;
     c->up = nullptr;
   }
+  for (auto& s : c->slots)  // a stream paused for this client drains (and is dropped)
+    if (s->stream_up) resume_stream(s->stream_up);
   graveyard_.push_back(c);
 }
 
@@ -723,6 +758,10 @@ void Reactor::on_upstream(Upstream* u, uint32_t ev) {
         if (u->resp->message_complete()) {
           on_upstream_response(u);
           if (u->dead) return;
+        } else if (u->resp->headers_complete() && maybe_stream(u)) {
+          stream_out(u, std::move(u->resp->mutable_body()), false);
+          u->resp->mutable_body().clear();
+          if (used == 0) break;
         } else if (used == 0) {
           break;
         }
@@ -769,11 +808,24 @@ void Reactor::on_upstream_response(Upstream* u) {
   const bool ka = r.keep_alive();
   const auto kap = r.keep_alive_params();
   responses++;
-  // header rewrite (Server.py:412-416)
-  r.set_header("server", cfg_.server_name);
-  r.set_header("keep-alive", "timeout=5, max=100");
-  r.set_header("connection", "keep-alive");
-  r.remove_header("accept-ranges");
+  if (u->streaming) {  // tail of a streamed response: nothing is cached
+    u->pend.push_front(std::move(p));
+    stream_out(u, std::move(r.mutable_body()), true);
+    p = std::move(u->pend.front());
+    u->pend.pop_front();
+    u->streaming = false;
+    if (p.lookup) release_waiters(p.key, nullptr);
+    if (!ka) {
+      server_nka_[u->server] = 1;
+      close_upstream(u);
+      return;
+    }
+    server_nka_[u->server] = 0;
+    u->ka_timeout = kap.first;
+    u->ka_max = kap.second;
+    return;
+  }
+  rewrite_response_headers(r);
   const std::string* ce = r.header("content-encoding");
   if (cfg_.compress && !ce && p.client_gzip && r.body().size() >= 256) {
     const std::string* ct = r.header("content-type");
@@ -815,6 +867,85 @@ void Reactor::on_upstream_response(Upstream* u) {
   u->ka_max = kap.second;
 }
 
+void Reactor::rewrite_response_headers(HttpParser& r) {
+  // header rewrite (Server.py:412-416)
+  r.set_header("server", cfg_.server_name);
+  r.set_header("keep-alive", "timeout=5, max=100");
+  r.set_header("connection", "keep-alive");
+  r.remove_header("accept-ranges");
+}
+
+bool Reactor::maybe_stream(Upstream* u) {
+  if (u->streaming) return true;
+  HttpParser& r = *u->resp;
+  const Pend& p = u->pend.front();
+  if (p.head || r.body_decoded()) return false;
+  const int64_t cl = r.content_length();
+  const bool big = (!r.chunked() && cl >= 0 && (uint64_t)cl > cfg_.stream_bytes) ||
+                   r.body().size() > cfg_.stream_bytes;
+  if (!big) return false;
+  Client* c = find_client(p.client_id);
+  Slot* s = c ? find_slot(c, p.seq) : nullptr;
+  u->streaming = true;
+  u->stream_chunked = r.chunked() || cl < 0;
+  streamed++;
+  rewrite_response_headers(r);
+  if (s && s->close_after) r.set_header("connection", "close");
+  std::string head;
+  if (u->stream_chunked) {
+    head = r.serialize_head(0, false);
+    head.insert(head.size() - 2, "Transfer-Encoding: chunked\r\n");
+  } else {
+    head = r.serialize_head((uint64_t)cl, true);
+  }
+  stream_out(u, std::move(head), false);
+  return true;
+}
+
+// Append streamed bytes to the front request's client slot (`last` ends the response).
+// Body pieces are re-framed as chunks when the length is unknown.
+void Reactor::stream_out(Upstream* u, std::string data, bool last) {
+  const Pend& p = u->pend.front();
+  Client* c = find_client(p.client_id);
+  Slot* s = c ? find_slot(c, p.seq) : nullptr;
+  if (!s || s->ready) return;  // client gone: drain and drop
+  const bool is_head = !s->streaming;
+  std::string framed;
+  if (!is_head && u->stream_chunked) {
+    if (!data.empty()) {
+      char hx[24];
+      std::snprintf(hx, sizeof hx, "%zx\r\n", data.size());
+      framed = hx;
+      framed += data;
+      framed += "\r\n";
+    }
+    if (last) framed += "0\r\n\r\n";
+  } else {
+    framed = std::move(data);
+  }
+  s->streaming = true;
+  s->stream_up = u->id;
+  if (!framed.empty()) s->out.write_shared(std::make_shared<const std::string>(std::move(framed)));
+  if (last) {
+    s->out.close();
+    s->ready = true;
+    const double us = (now_s() - s->t0) * 1e6;
+    const int b = us < 1 ? 0 : std::min(kHistBuckets - 1, 1 + (int)std::log2(us));
+    hist[b]++;
+  }
+  flush_client(c);
+  if (!last && !c->dead && s->out.pending() > kStreamHighWater && !u->in_paused) {
+    stream_pauses++;
+    pause_input(u, true);
+  }
+}
+
+void Reactor::resume_stream(uint64_t up_id) {
+  auto it = conns_.find(up_id);
+  if (it != conns_.end() && !it->second->dead && it->second->in_paused)
+    pause_input(it->second, false);
+}
+
 void Reactor::close_upstream(Upstream* u) {
   if (u->dead) return;
   u->dead = true;
@@ -828,6 +959,13 @@ void Reactor::close_upstream(Upstream* u) {
   std::deque<Pend> pend;
   pend.swap(u->pend);
   graveyard_.push_back(u);
+  if (u->streaming && !pend.empty()) {  // bytes already left: the client cannot be answered
+    u->streaming = false;
+    Pend p = std::move(pend.front());
+    pend.pop_front();
+    if (p.lookup) release_waiters(p.key, nullptr);
+    if (Client* c = find_client(p.client_id)) close_client(c);
+  }
   for (auto& p : pend) fail_pend(p, 502, "Bad Gateway");
 }
 
@@ -910,13 +1048,14 @@ void Proxy::stop() {
 
 std::string Proxy::stats_json() {
   uint64_t req = 0, hit = 0, miss = 0, ur = 0, resp = 0, bo = 0, err = 0, cl = 0, up = 0, acc = 0,
-           gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0;
+           gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0, stm = 0, stp = 0;
   uint64_t h[kHistBuckets] = {};
   for (auto& r : reactors_) {
     req += r->requests; hit += r->hits; miss += r->misses; ur += r->upstream_reqs;
     resp += r->responses; bo += r->bytes_out; err += r->errors; cl += r->clients;
     up += r->upstreams; acc += r->accepts; gcc += r->gc_closed; sets += r->cache_sets;
     bad += r->bad_requests; uf += r->upstream_failures; rt += r->retries; col += r->collapsed;
+    stm += r->streamed; stp += r->stream_pauses;
     for (int b = 0; b < kHistBuckets; ++b) h[b] += r->hist[b];
   }
   uint64_t total = 0;
@@ -937,7 +1076,7 @@ std::string Proxy::stats_json() {
     << ",\"upstream_responses\":" << resp << ",\"cache_fills\":" << sets
     << ",\"bytes_out\":" << bo << ",\"errors\":" << err << ",\"bad_requests\":" << bad
     << ",\"upstream_failures\":" << uf << ",\"retries\":" << rt << ",\"collapsed\":" << col
-    << ",\"clients\":" << cl
+    << ",\"streamed\":" << stm << ",\"stream_pauses\":" << stp << ",\"clients\":" << cl
     << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
     << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
     << total << "}";

@@ -49,6 +49,9 @@ struct ProxyConfig {
   std::string balance = "random";     // random (ref :123) | roundrobin | leastconn
   int upstream_retry_s = 2;           // a failed upstream is skipped for this long
   bool decode_gzip = false;           // inflate + re-deflate every miss like the reference
+  // Responses whose body exceeds this are streamed to the client as they arrive and not
+  // cached (the reference buffers every object whole, Server.py:408-421).
+  uint64_t stream_bytes = 1 << 20;
   int backlog = 1024;
   std::string server_name = "Shellac/0.2.0";
 };

@@ -90,7 +90,7 @@ class Server:
                  policy: str = "rfc", kill_switch: bool = True, key_host: bool = False,
                  client_timeout: int = 30, client_max_reqs: int = 1000,
                  balance: str = "random", bind: str = "0.0.0.0", decode_gzip: bool = False,
-                 **backend_opts):
+                 stream_bytes: int = 1 << 20, **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
         self._backend = backend
@@ -101,7 +101,7 @@ class Server:
             _csv(servers, 80), self._backend, port=port, bind=bind, threads=threads, ttl=ttl,
             compress=compress, policy=policy, kill_switch=kill_switch, key_host=key_host,
             client_timeout=client_timeout, client_max_reqs=client_max_reqs, balance=balance,
-            decode_gzip=decode_gzip)
+            decode_gzip=decode_gzip, stream_bytes=stream_bytes)
         self._started = False
 
     @property
@@ -168,6 +168,8 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--client-max-reqs", type=int, default=1000)
     p.add_argument("--key-host", action="store_true", help="include Host in the cache key")
     p.add_argument("--no-kill-switch", action="store_true", help="disable GET /kill")
+    p.add_argument("--stream-bytes", type=int, default=1 << 20,
+                   help="stream responses larger than this to the client without caching them")
     p.add_argument("--decode-gzip", action="store_true",
                    help="inflate + re-deflate every miss like the reference (default: passthrough)")
     return p
@@ -190,6 +192,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  kill_switch=not args.no_kill_switch, key_host=args.key_host,
                  client_timeout=args.client_timeout, client_max_reqs=args.client_max_reqs,
                  balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
+                 stream_bytes=args.stream_bytes,
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}
                     if kind == "hbm" else {}),

@@ -37,7 +37,10 @@ class Origin:
                     body = f"status {code}\n".encode()
                 else:
                     code = 200
-                    body = (f"<html>{path} #{n} ".encode() + b"x" * body_bytes + b"</html>\n")
+                    nb = body_bytes
+                    if "/big/" in path:  # /big/<bytes>: a large object
+                        nb = int(path.rsplit("/", 1)[1])
+                    body = (f"<html>{path} #{n} ".encode() + b"x" * nb + b"</html>\n")
                 headers = {"Content-Type": "text/html"}
                 if path.startswith("/nocache"):
                     headers["Cache-Control"] = "no-store"
@@ -53,8 +56,9 @@ class Origin:
                     self.send_header("Transfer-Encoding", "chunked")
                     self.end_headers()
                     if not head:
-                        for i in range(0, len(body), 100):
-                            part = body[i : i + 100]
+                        step = 100 if len(body) < 100000 else 65536
+                        for i in range(0, len(body), step):
+                            part = body[i : i + step]
                             self.wfile.write(b"%x\r\n" % len(part) + part + b"\r\n")
                         self.wfile.write(b"0\r\n\r\n")
                     return

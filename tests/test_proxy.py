@@ -79,6 +79,53 @@ def test_chunked_upstream_dechunked(origin):
         assert origin.hits["/chunked/x"] == 1
 
 
+def test_large_objects_stream_through_uncached(origin):
+    with make_proxy([origin.port], stream_bytes=100000) as px:
+        c = HttpClient(port=px.port)
+        for path, chunked in (("/big/3000000", False), ("/chunked/big/700000", True)):
+            r = c.get(path)
+            body = r.body().read()
+            assert body.startswith(f"<html>{path} #1 ".encode()) and len(body) > 700000
+            assert ("transfer-encoding" in r.headers()) == chunked
+            r = c.get(path)   # too large to cache: fetched again
+            assert r.body().read().startswith(f"<html>{path} #2 ".encode())
+        # pipelined neighbours of a streamed response keep their order
+        c.get("/small")
+        paths = ["/small", "/big/500000", "/small2", "/chunked/big/300000", "/small"]
+        rs = c.pipeline(paths)
+        for p, r in zip(paths, rs):
+            assert f"<html>{p} #".encode() in r.body().read()[:64], p
+        assert origin.hits["/small"] == 1
+
+
+def test_streaming_backpressure_slow_client(origin):
+    """A 40 MB object to a client that reads slowly: the proxy pauses the upstream
+    instead of buffering everything, and the bytes arrive intact."""
+    with make_proxy([origin.port], stream_bytes=100000) as px:
+        s = socket.create_connection(("127.0.0.1", px.port))
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 16)
+        s.sendall(b"GET /big/40000000 HTTP/1.1\r\nHost: x\r\n\r\n")
+        time.sleep(0.5)   # let the proxy hit its high-water mark
+        got = bytearray()
+        while True:
+            d = s.recv(1 << 20)
+            if not d:
+                break
+            got += d
+            if b"\r\n\r\n" in got:
+                head, _, body = bytes(got).partition(b"\r\n\r\n")
+                n = int([ln.split(b":")[1] for ln in head.split(b"\r\n")
+                         if ln.lower().startswith(b"content-length")][0])
+                if len(body) >= n:
+                    break
+        head, _, body = bytes(got).partition(b"\r\n\r\n")
+        assert body.startswith(b"<html>/big/40000000 #1 ") and body.endswith(b"</html>\n")
+        assert len(body) == n
+        s.close()
+        st = px.stats()
+        assert st["streamed"] == 1 and st["stream_pauses"] >= 1
+
+
 def test_rfc_policy_does_not_cache_post_nostore_cookie_errors(origin):
     with make_proxy([origin.port]) as px:
         c = HttpClient(port=px.port)
