@@ -1,5 +1,6 @@
-// Cache backends: DRAM (striped host shards), HBM (batched HIP pipeline per GPU),
-// memcached binary protocol client (ketama, pipelined, ejection + retry).
+// Cache backends: DRAM (striped host shards), tiered L1/L2, memcached binary protocol
+// client (ketama, pipelined, ejection + retry). The HBM backend (HIP) is in
+// backend_hbm.cc so these host-only backends also build without ROCm (sanitizer presets).
 #include "backend.h"
 
 #include <sys/epoll.h>
@@ -9,7 +10,6 @@
 #include <chrono>
 #include <cstdio>
 
-#include "hbm_cache.h"
 #include "mcproto.h"
 
 namespace shellac {
@@ -103,358 +103,6 @@ void DramBackend::stats(StatList* out) {
   out->emplace_back("cache_set_bytes", t.set_bytes);
   out->emplace_back("cache_evicted", t.set_evicted);
   out->emplace_back("cache_shards", shards_.size());
-}
-
-// =====================================================================================
-// HBM
-// =====================================================================================
-#define HB_OK(expr)                                                                   \
-  do {                                                                                \
-    hipError_t _e = (expr);                                                           \
-    if (_e != hipSuccess) throw Error(std::string("HIP: ") + hipGetErrorString(_e) + \
-                                      " at " #expr);                                  \
-  } while (0)
-
-struct HbmBackend::Dev {
-  int device = 0;
-  std::unique_ptr<HbmCache> cache;
-  hipStream_t stream = nullptr;
-  size_t n_cap = 0, out_cap = 0, vals_cap = 0;
-  Digest *d_keys = nullptr, *h_keys = nullptr;
-  uint64_t *d_loc = nullptr, *d_size = nullptr, *d_off = nullptr, *h_off = nullptr;
-  uint8_t *d_out = nullptr, *h_out = nullptr;
-  uint8_t *d_vals = nullptr, *h_vals = nullptr;
-  uint64_t *d_voff = nullptr, *h_voff = nullptr;
-  uint32_t *d_meta = nullptr, *h_meta = nullptr;  // [vlen | flags | expire] x n
-  uint8_t *d_found = nullptr, *h_found = nullptr;
-
-  void set_device() { HB_OK(hipSetDevice(device)); }
-
-  void ensure_n(size_t n) {
-    if (n <= n_cap) return;
-    size_t cap = n_cap ? n_cap : 1024;
-    while (cap < n) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_keys); (void)hipHostFree(h_keys); (void)hipFree(d_loc); (void)hipFree(d_size);
-    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
-    (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
-    HB_OK(hipMalloc(&d_keys, cap * sizeof(Digest)));
-    HB_OK(hipHostMalloc(&h_keys, cap * sizeof(Digest), hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_loc, cap * 8));
-    HB_OK(hipMalloc(&d_size, (cap + 1) * 8));
-    HB_OK(hipMalloc(&d_off, (cap + 1) * 8));
-    HB_OK(hipHostMalloc(&h_off, (cap + 1) * 8, hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_voff, cap * 8));
-    HB_OK(hipHostMalloc(&h_voff, cap * 8, hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_meta, cap * 12));
-    HB_OK(hipHostMalloc(&h_meta, cap * 12, hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_found, cap));
-    HB_OK(hipHostMalloc(&h_found, cap, hipHostMallocDefault));
-    n_cap = cap;
-    cache->reserve((int64_t)cap);
-  }
-  void ensure_out(size_t bytes) {
-    if (bytes <= out_cap) return;
-    size_t cap = out_cap ? out_cap : (1u << 20);
-    while (cap < bytes) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_out); (void)hipHostFree(h_out);
-    HB_OK(hipMalloc(&d_out, cap));
-    HB_OK(hipHostMalloc(&h_out, cap, hipHostMallocDefault));
-    out_cap = cap;
-  }
-  void ensure_vals(size_t bytes) {
-    if (bytes <= vals_cap) return;
-    size_t cap = vals_cap ? vals_cap : (1u << 20);
-    while (cap < bytes) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_vals); (void)hipHostFree(h_vals);
-    HB_OK(hipMalloc(&d_vals, cap));
-    HB_OK(hipHostMalloc(&h_vals, cap, hipHostMallocDefault));
-    vals_cap = cap;
-  }
-  ~Dev() {
-    (void)hipSetDevice(device);
-    (void)hipStreamSynchronize(stream);
-    cache.reset();
-    (void)hipFree(d_keys); (void)hipHostFree(h_keys); (void)hipFree(d_loc); (void)hipFree(d_size);
-    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipFree(d_out); (void)hipHostFree(h_out);
-    (void)hipFree(d_vals); (void)hipHostFree(h_vals); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
-    (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-
-HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
-    : cfg_(cfg), ring_((int)cfg.devices.size()), epoch_(wall_s()) {
-  SH_CHECK(!cfg_.devices.empty(), "HbmBackend needs at least one device");
-  for (int dev : cfg_.devices) {
-    auto d = std::make_unique<Dev>();
-    d->device = dev;
-    d->set_device();
-    ShardConfig sc;
-    sc.log_bytes = cfg_.log_bytes_per_gpu / 16 * 16;
-    sc.nbuckets = cfg_.nbuckets_per_gpu;
-    sc.max_item = cfg_.max_item;
-    sc.device = dev;
-    d->cache = std::make_unique<HbmCache>(sc);
-    HB_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    d->ensure_n(4096);
-    d->ensure_out(4u << 20);
-    d->ensure_vals(4u << 20);
-    devs_.push_back(std::move(d));
-  }
-  th_ = std::thread([this] { loop(); });
-}
-
-HbmBackend::~HbmBackend() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
-  }
-  cv_.notify_all();
-  if (th_.joinable()) th_.join();
-}
-
-uint32_t HbmBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
-
-void HbmBackend::get(const std::string&, const Digest& d, Executor* ex, GetCallback done) {
-  Req r;
-  r.kind = 0;
-  r.d = d;
-  r.ex = ex;
-  r.gcb = std::move(done);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(std::move(r));
-  }
-  cv_.notify_one();
-}
-
-void HbmBackend::set(const std::string&, const Digest& d, Bytes value, uint32_t flags,
-                     uint32_t ttl_s) {
-  if (!value || value->size() > cfg_.max_item) return;
-  Req r;
-  r.kind = 1;
-  r.d = d;
-  r.value = std::move(value);
-  r.flags = flags;
-  r.ttl = ttl_s;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(std::move(r));
-  }
-  cv_.notify_one();
-}
-
-void HbmBackend::del(const std::string&, const Digest& d, Executor* ex, DelCallback done) {
-  Req r;
-  r.kind = 2;
-  r.d = d;
-  r.ex = ex;
-  r.dcb = std::move(done);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(std::move(r));
-  }
-  cv_.notify_one();
-}
-
-void HbmBackend::flush() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    flush_req_ = true;
-  }
-  cv_.notify_one();
-}
-
-void HbmBackend::loop() {
-  std::vector<Req> batch;
-  for (;;) {
-    bool do_flush = false;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_; });
-      if (stop_ && q_.empty()) return;
-      // give batch-mates up to batch_us to arrive (a lone request pays at most that)
-      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.batch_us);
-      while (!stop_ && (int)q_.size() < cfg_.max_batch &&
-             cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
-      }
-      batch.swap(q_);
-      do_flush = flush_req_;
-      flush_req_ = false;
-    }
-    const double t0 = wall_s();
-    try {
-      if (do_flush)
-        for (auto& d : devs_) {
-          d->set_device();
-          d->cache->flush(d->stream);
-          HB_OK(hipStreamSynchronize(d->stream));
-        }
-      if (!batch.empty()) run_batch(batch);
-    } catch (const std::exception& e) {
-      std::fprintf(stderr, "[shellac hbm] batch failed: %s\n", e.what());
-      for (auto& r : batch) {
-        if (r.kind == 0 && r.gcb) {
-          auto cb = std::move(r.gcb);
-          r.ex->post([cb]() { cb(false, CacheValue{}); });
-        } else if (r.kind == 2 && r.dcb) {
-          auto cb = std::move(r.dcb);
-          r.ex->post([cb]() { cb(false); });
-        }
-      }
-    }
-    const uint64_t n = batch.size();
-    if (n) {
-      batches_++;
-      batched_reqs_ += n;
-      uint64_t prev = max_batch_seen_.load();
-      while (n > prev && !max_batch_seen_.compare_exchange_weak(prev, n)) {
-      }
-      batch_ns_ += (uint64_t)((wall_s() - t0) * 1e9);
-    }
-    batch.clear();
-  }
-}
-
-void HbmBackend::run_batch(std::vector<Req>& batch) {
-  const size_t nd = devs_.size();
-  const uint32_t tnow = now();
-  std::vector<std::vector<size_t>> gets(nd), sets(nd), dels(nd);
-  for (size_t i = 0; i < batch.size(); ++i) {
-    const int o = nd == 1 ? 0 : ring_.owner(batch[i].d);
-    (batch[i].kind == 0 ? gets : batch[i].kind == 1 ? sets : dels)[o].push_back(i);
-  }
-  // ---- GET phase 1: H2D keys, probe + scan, D2H offsets (all devices in flight)
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
-    if (!n) continue;
-    dv.set_device();
-    dv.ensure_n(std::max(n, std::max(sets[k].size(), dels[k].size())));
-    for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[gets[k][j]].d;
-    HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-    dv.cache->lookup(dv.d_keys, (int64_t)n, dv.d_loc, dv.d_size, dv.d_off, tnow, dv.stream);
-    HB_OK(hipMemcpyAsync(dv.h_off, dv.d_off, (n + 1) * 8, hipMemcpyDeviceToHost, dv.stream));
-  }
-  // ---- GET phase 2: gather + D2H values
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
-    if (!n) continue;
-    dv.set_device();
-    HB_OK(hipStreamSynchronize(dv.stream));
-    const uint64_t total = dv.h_off[n];
-    if (total) {
-      dv.ensure_out(total);
-      dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.d_out, dv.stream);
-      HB_OK(hipMemcpyAsync(dv.h_out, dv.d_out, total, hipMemcpyDeviceToHost, dv.stream));
-    }
-  }
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
-    if (!n) continue;
-    dv.set_device();
-    HB_OK(hipStreamSynchronize(dv.stream));
-    for (size_t j = 0; j < n; ++j) {
-      Req& r = batch[gets[k][j]];
-      const uint64_t o = dv.h_off[j], sz = dv.h_off[j + 1] - o;
-      bool hit = false;
-      CacheValue v;
-      if (sz) {
-        ItemHeader h;
-        std::memcpy(&h, dv.h_out + o, sizeof h);
-        if (h.magic == kItemMagic && h.d0 == r.d.lo && h.d1 == r.d.hi) {
-          hit = true;
-          v.flags = h.flags;
-          v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
-          v.data = std::make_shared<const std::string>(
-              reinterpret_cast<const char*>(dv.h_out + o + kItemHeaderBytes), h.vlen);
-        }
-      }
-      auto cb = std::move(r.gcb);
-      r.ex->post([cb, hit, v]() { cb(hit, v); });
-    }
-  }
-  // ---- SET: pack 16-aligned payloads in pinned staging, H2D, store
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = sets[k].size();
-    if (!n) continue;
-    dv.set_device();
-    dv.ensure_n(n);
-    uint64_t bytes = 16;
-    for (size_t idx : sets[k]) bytes += align_up(batch[idx].value->size(), 16);
-    dv.ensure_vals(bytes);
-    uint64_t off = 0, bound = 0;
-    uint32_t* vl = dv.h_meta;
-    uint32_t* fl = dv.h_meta + n;
-    uint32_t* ex = dv.h_meta + 2 * n;
-    for (size_t j = 0; j < n; ++j) {
-      const Req& r = batch[sets[k][j]];
-      dv.h_keys[j] = r.d;
-      std::memcpy(dv.h_vals + off, r.value->data(), r.value->size());
-      dv.h_voff[j] = off;
-      vl[j] = (uint32_t)r.value->size();
-      fl[j] = r.flags;
-      ex[j] = r.ttl ? tnow + r.ttl : 0;
-      off += align_up(r.value->size(), 16);
-      bound += item_bytes(vl[j]);
-    }
-    HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_vals, dv.h_vals, off + 16, hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_voff, dv.h_voff, n * 8, hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_meta, dv.h_meta, n * 12, hipMemcpyHostToDevice, dv.stream));
-    dv.cache->store(dv.d_keys, dv.d_vals, dv.d_voff, dv.d_meta, dv.d_meta + n, dv.d_meta + 2 * n,
-                    (int64_t)n, bound, tnow, dv.stream);
-  }
-  // ---- DELETE
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = dels[k].size();
-    dv.set_device();
-    if (n) {
-      HB_OK(hipStreamSynchronize(dv.stream));  // staging reuse after SET
-      dv.ensure_n(n);
-      for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[dels[k][j]].d;
-      HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-      dv.cache->remove(dv.d_keys, (int64_t)n, dv.d_found, tnow, dv.stream);
-      HB_OK(hipMemcpyAsync(dv.h_found, dv.d_found, n, hipMemcpyDeviceToHost, dv.stream));
-    }
-    HB_OK(hipStreamSynchronize(dv.stream));
-    for (size_t j = 0; j < n; ++j) {
-      Req& r = batch[dels[k][j]];
-      const bool f = dv.h_found[j] != 0;
-      auto cb = std::move(r.dcb);
-      if (cb) r.ex->post([cb, f]() { cb(f); });
-    }
-  }
-}
-
-void HbmBackend::stats(StatList* out) {
-  CacheCounters t{};
-  uint64_t hbm = 0;
-  for (auto& d : devs_) {
-    d->set_device();
-    const CacheCounters c = d->cache->counters(nullptr);
-    t.get_ops += c.get_ops; t.get_hits += c.get_hits; t.set_ops += c.set_ops;
-    t.set_bytes += c.set_bytes; t.set_evicted += c.set_evicted; t.del_ops += c.del_ops;
-    hbm += d->cache->hbm_bytes();
-  }
-  out->emplace_back("cache_get_ops", t.get_ops);
-  out->emplace_back("cache_get_hits", t.get_hits);
-  out->emplace_back("cache_set_ops", t.set_ops);
-  out->emplace_back("cache_set_bytes", t.set_bytes);
-  out->emplace_back("cache_evicted", t.set_evicted);
-  out->emplace_back("hbm_gpus", devs_.size());
-  out->emplace_back("hbm_bytes", hbm);
-  out->emplace_back("hbm_batches", batches_.load());
-  out->emplace_back("hbm_batched_requests", batched_reqs_.load());
-  out->emplace_back("hbm_max_batch", max_batch_seen_.load());
-  out->emplace_back("hbm_batch_ns_total", batch_ns_.load());
 }
 
 // =====================================================================================
@@ -797,6 +445,175 @@ void MemcachedBackend::stats(StatList* out) {
   out->emplace_back("memcached_errors", errors_.load());
   out->emplace_back("memcached_ejections", ejections_.load());
   out->emplace_back("memcached_nodes", nodes_.size());
+}
+
+// =====================================================================================
+// Fault injection
+// =====================================================================================
+FaultSpec parse_fault_spec(const std::string& spec) {
+  FaultSpec f;
+  size_t i = 0;
+  while (i < spec.size()) {
+    size_t j = spec.find(',', i);
+    if (j == std::string::npos) j = spec.size();
+    const std::string kv = spec.substr(i, j - i);
+    i = j + 1;
+    if (kv.empty()) continue;
+    const size_t eq = kv.find('=');
+    const std::string k = kv.substr(0, eq);
+    const std::string v = eq == std::string::npos ? "" : kv.substr(eq + 1);
+    if (k == "get_miss") f.get_miss = std::stod(v);
+    else if (k == "set_drop") f.set_drop = std::stod(v);
+    else if (k == "delay_us") f.delay_us = (uint32_t)std::stoul(v);
+    else if (k == "down") f.down = v.empty() || v == "1" || v == "true";
+    else throw Error("unknown fault '" + k + "' (get_miss, set_drop, delay_us, down)");
+  }
+  return f;
+}
+
+FaultBackend::FaultBackend(std::shared_ptr<CacheBackend> inner, const FaultSpec& spec,
+                           uint64_t seed)
+    : inner_(std::move(inner)), spec_(spec), rng_(seed * 0x9E3779B97F4A7C15ull + 1) {
+  th_ = std::thread([this] { timer_loop(); });
+}
+
+FaultBackend::~FaultBackend() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  th_.join();
+}
+
+void FaultBackend::set_spec(const FaultSpec& spec) {
+  std::lock_guard<std::mutex> lk(mu_);
+  spec_ = spec;
+}
+
+FaultSpec FaultBackend::spec() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return spec_;
+}
+
+bool FaultBackend::roll(double p) {
+  if (p <= 0) return false;
+  if (p >= 1) return true;
+  std::lock_guard<std::mutex> lk(mu_);
+  rng_ ^= rng_ << 13;
+  rng_ ^= rng_ >> 7;
+  rng_ ^= rng_ << 17;
+  return (double)(rng_ >> 11) * (1.0 / 9007199254740992.0) < p;
+}
+
+void FaultBackend::later(std::function<void()> fn) {
+  const FaultSpec f = spec();
+  if (!f.delay_us) {
+    fn();
+    return;
+  }
+  injected_delay_++;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    timers_.emplace_back(wall_s() + f.delay_us * 1e-6, std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void FaultBackend::timer_loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    if (stop_) break;
+    if (timers_.empty()) {
+      cv_.wait(lk);
+      continue;
+    }
+    const double due = timers_.front().first, t = wall_s();
+    if (due > t) {
+      // system_clock deadline: libstdc++ maps steady-clock waits to pthread_cond_clockwait,
+      // which ThreadSanitizer does not intercept (false reports under the tsan preset)
+      cv_.wait_until(lk, std::chrono::system_clock::now() +
+                             std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                 std::chrono::duration<double>(due - t)));
+      continue;
+    }
+    auto fn = std::move(timers_.front().second);
+    timers_.pop_front();
+    lk.unlock();
+    fn();
+    lk.lock();
+  }
+  // run what is left so no caller waits forever
+  while (!timers_.empty()) {
+    auto fn = std::move(timers_.front().second);
+    timers_.pop_front();
+    lk.unlock();
+    fn();
+    lk.lock();
+  }
+}
+
+void FaultBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
+  const FaultSpec f = spec();
+  if (f.down || roll(f.get_miss)) {
+    injected_miss_++;
+    if (!f.delay_us) {
+      done(false, CacheValue{});
+      return;
+    }
+    later([ex, done] {
+      if (ex) ex->post([done] { done(false, CacheValue{}); });
+      else done(false, CacheValue{});
+    });
+    return;
+  }
+  if (!f.delay_us) {
+    inner_->get(key, d, ex, std::move(done));
+    return;
+  }
+  // the delayed lookup runs from the timer thread; a synchronous tier would answer
+  // right there, so the answer is always handed back to `ex`
+  later([this, key, d, ex, done] {
+    inner_->get(key, d, ex, [ex, done](bool hit, CacheValue v) {
+      if (ex) ex->post([done, hit, v] { done(hit, v); });
+      else done(hit, v);
+    });
+  });
+}
+
+void FaultBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+                       uint32_t ttl_s) {
+  const FaultSpec f = spec();
+  if (f.down || roll(f.set_drop)) {
+    injected_drop_++;
+    return;
+  }
+  inner_->set(key, d, std::move(value), flags, ttl_s);
+}
+
+void FaultBackend::del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) {
+  const FaultSpec f = spec();
+  if (f.down) {
+    done(false);
+    return;
+  }
+  if (!f.delay_us) {
+    inner_->del(key, d, ex, std::move(done));
+    return;
+  }
+  later([this, key, d, ex, done] {
+    inner_->del(key, d, ex, [ex, done](bool found) {
+      if (ex) ex->post([done, found] { done(found); });
+      else done(found);
+    });
+  });
+}
+
+void FaultBackend::stats(StatList* out) {
+  inner_->stats(out);
+  out->emplace_back("fault_injected_miss", injected_miss_.load());
+  out->emplace_back("fault_injected_drop", injected_drop_.load());
+  out->emplace_back("fault_injected_delay", injected_delay_.load());
 }
 
 }  // namespace shellac

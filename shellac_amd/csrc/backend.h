@@ -163,6 +163,49 @@ class TieredBackend : public CacheBackend {
   std::atomic<uint64_t> l1_hits_{0}, l2_hits_{0}, misses_{0};
 };
 
+// Fault injection: a decorator that makes the wrapped tier misbehave
+// on purpose — GETs answered as misses, SETs dropped, answers delayed, or the whole
+// tier "down" (every GET misses, every SET is lost) — with probabilities that can be
+// changed while the proxy runs. Used by the failure tests and for drills.
+struct FaultSpec {
+  double get_miss = 0;    // P(GET answered as a miss without asking the tier)
+  double set_drop = 0;    // P(SET silently dropped)
+  uint32_t delay_us = 0;  // extra latency before every GET/DEL is answered
+  bool down = false;      // tier unreachable
+};
+FaultSpec parse_fault_spec(const std::string& spec);  // "get_miss=0.1,set_drop=1,delay_us=500,down"
+
+class FaultBackend : public CacheBackend {
+ public:
+  FaultBackend(std::shared_ptr<CacheBackend> inner, const FaultSpec& spec, uint64_t seed = 1);
+  ~FaultBackend() override;
+  void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
+  void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
+           uint32_t ttl_s) override;
+  void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
+  void flush() override { inner_->flush(); }
+  std::string name() const override { return "fault(" + inner_->name() + ")"; }
+  void stats(StatList* out) override;
+  void set_spec(const FaultSpec& spec);
+  FaultSpec spec() const;
+
+ private:
+  bool roll(double p);
+  void later(std::function<void()> fn);  // run after delay_us on the timer thread
+  void timer_loop();
+
+  std::shared_ptr<CacheBackend> inner_;
+  mutable std::mutex mu_;
+  FaultSpec spec_;
+  uint64_t rng_;
+  std::atomic<uint64_t> injected_miss_{0}, injected_drop_{0}, injected_delay_{0};
+  // delay timer
+  std::condition_variable cv_;
+  std::deque<std::pair<double, std::function<void()>>> timers_;  // FIFO: one fixed delay
+  bool stop_ = false;
+  std::thread th_;
+};
+
 struct MemcachedConfig {
   std::vector<Addr> servers;
   int retry_timeout_s = 2;     // ejected node is retried after this long

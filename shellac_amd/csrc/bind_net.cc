@@ -154,6 +154,15 @@ void bind_net(py::module_& m) {
         return d;
       });
 
+  m.def("fault_backend", [](BackendHandle inner, const std::string& spec, uint64_t seed) {
+    auto fb = std::make_shared<FaultBackend>(inner.be, parse_fault_spec(spec), seed);
+    return BackendHandle{fb};
+  }, py::arg("inner"), py::arg("spec") = "", py::arg("seed") = 1);
+  m.def("set_fault", [](BackendHandle& h, const std::string& spec) {
+    auto* fb = dynamic_cast<FaultBackend*>(h.be.get());
+    if (!fb) throw Error("not a fault-injection backend");
+    fb->set_spec(parse_fault_spec(spec));
+  });
   m.def("dram_backend", [](uint64_t bytes, uint32_t max_item, int stripes) {
     return BackendHandle{std::make_shared<DramBackend>(bytes, max_item, stripes)};
   }, py::arg("bytes"), py::arg("max_item") = 1u << 20, py::arg("stripes") = 16);

@@ -49,18 +49,25 @@ def parse_server_list(slist: str, default_port: int) -> list:
 def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
                  hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 50,
-                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60):
+                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = ""):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
     ``dram`` (local host memory), ``hbm`` (one HBM shard per GPU in ``gpus``) or
     ``none``. ``l1_mb > 0`` puts a host-DRAM L1 of that size in front of the
     ``hbm`` / ``memcached`` tier (``TieredBackend``: L1 hits never wait for a GPU
-    batch or a network round trip).
+    batch or a network round trip). ``fault`` (e.g. ``"get_miss=0.1,delay_us=500"``,
+    ``"down"``) wraps the stack in a fault-injection backend; see ``set_fault``.
     """
     c = core()
     if kind == "none":
         return None
+    if fault:
+        # fault injection wraps the whole cache stack (set_fault() changes it live)
+        inner = make_backend(kind, caches=caches, dram_mb=dram_mb, gpus=gpus, hbm_gb=hbm_gb,
+                             max_item=max_item, batch_us=batch_us, retry_s=retry_s, l1_mb=l1_mb,
+                             promote_ttl=promote_ttl)
+        return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
                           batch_us=batch_us, retry_s=retry_s)
@@ -79,6 +86,12 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
             nb *= 2
         return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us)
     raise ValueError(f"unknown cache backend {kind!r}")
+
+
+def set_fault(backend, spec: str) -> None:
+    """Change the faults of a backend built with ``make_backend(..., fault=...)`` live:
+    ``get_miss=P``, ``set_drop=P``, ``delay_us=N``, ``down`` (``""`` = healthy)."""
+    core().set_fault(backend, spec)
 
 
 class Server:
@@ -107,6 +120,10 @@ class Server:
     @property
     def port(self) -> int:
         return self._proxy.port
+
+    def set_fault(self, spec: str) -> None:
+        """Live fault injection on the cache tier (requires ``fault=`` at construction)."""
+        set_fault(self._backend, spec)
 
     @property
     def backend(self):
@@ -168,6 +185,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--client-max-reqs", type=int, default=1000)
     p.add_argument("--key-host", action="store_true", help="include Host in the cache key")
     p.add_argument("--no-kill-switch", action="store_true", help="disable GET /kill")
+    p.add_argument("--fault", default="",
+                   help="fault injection on the cache tier, e.g. get_miss=0.1,set_drop=0.5,"
+                        "delay_us=500 or down (drills; default off)")
     p.add_argument("--stream-bytes", type=int, default=1 << 20,
                    help="stream responses larger than this to the client without caching them")
     p.add_argument("--decode-gzip", action="store_true",
@@ -193,6 +213,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  client_timeout=args.client_timeout, client_max_reqs=args.client_max_reqs,
                  balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
                  stream_bytes=args.stream_bytes,
+                 **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}
                     if kind == "hbm" else {}),

@@ -126,6 +126,32 @@ def test_streaming_backpressure_slow_client(origin):
         assert st["streamed"] == 1 and st["stream_pauses"] >= 1
 
 
+def test_fault_injection_cache_tier(origin):
+    """Cache-tier faults degrade to upstream fetches, never to client errors."""
+    with make_proxy([origin.port], fault="get_miss=1") as px:
+        c = HttpClient(port=px.port)
+        for i in range(3):
+            assert c.get("/f").body().read().startswith(f"<html>/f #{i + 1} ".encode())
+        px.set_fault("")                     # healthy again: the last fill is served
+        assert c.get("/f").body().read().startswith(b"<html>/f #3 ")
+        px.set_fault("down")                 # tier unreachable: pass-through, no caching
+        assert c.get("/g").body().read().startswith(b"<html>/g #1 ")
+        assert c.get("/g").body().read().startswith(b"<html>/g #2 ")
+        px.set_fault("set_drop=1")           # fills lost
+        c.get("/h")
+        assert c.get("/h").body().read().startswith(b"<html>/h #2 ")
+        px.set_fault("delay_us=30000")       # slow tier: answers still arrive, in order
+        t0 = time.time()
+        rs = c.pipeline(["/f", "/zz", "/f"])
+        assert time.time() - t0 >= 0.03
+        assert [r.body().read()[:9] for r in rs] == [b"<html>/f ", b"<html>/zz", b"<html>/f "]
+        st = px.stats()
+        assert st["errors"] == 0
+        assert st["cache"]["fault_injected_miss"] >= 5 and st["cache"]["fault_injected_delay"] >= 3
+    with pytest.raises(Exception):
+        make_backend("dram", fault="explode=1")
+
+
 def test_rfc_policy_does_not_cache_post_nostore_cookie_errors(origin):
     with make_proxy([origin.port]) as px:
         c = HttpClient(port=px.port)
