@@ -2,7 +2,7 @@
 
 HIP translation units (``*.hip``) are compiled by ``hipcc --offload-arch=gfx950``;
 host C++ units (``*.cc``) by ``g++`` against the HIP runtime headers; everything
-is linked by ``hipcc -shared`` against ``libamdhip64`` and ``libz``. Objects are
+is linked by ``hipcc -shared`` against ``libamdhip64``, ROCTX (timeline markers) and ``libz``. Objects are
 cached under ``build/obj`` and rebuilt when the source or any ``csrc`` header is
 newer. No JIT cache: the ``.so`` lands in the package directory so it travels
 to the GPU box with the repository snapshot.
@@ -99,7 +99,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
         cmd = [f"{ROCM}/bin/hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs,
-               "-o", TARGET + ".tmp", f"-L{ROCM}/lib", "-lamdhip64", "-lz", "-lpthread",
+               "-o", TARGET + ".tmp", f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-lz",
+               "-lpthread",
                f"-Wl,-rpath,{ROCM}/lib"]
         p = subprocess.run(cmd, capture_output=True, text=True)
         if p.returncode != 0:

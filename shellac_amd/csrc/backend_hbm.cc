@@ -5,6 +5,7 @@
 
 #include "backend.h"
 #include "hbm_cache.h"
+#include "trace.h"
 
 namespace shellac {
 
@@ -230,6 +231,7 @@ void HbmBackend::loop() {
 }
 
 void HbmBackend::run_batch(std::vector<Req>& batch) {
+  TraceRange tr("hbm_backend.batch");
   const size_t nd = devs_.size();
   const uint32_t tnow = now();
   std::vector<std::vector<size_t>> gets(nd), sets(nd), dels(nd);

@@ -12,6 +12,7 @@
 #include "bind_parts.h"
 #include "hbm_cache.h"
 #include "host_cache.h"
+#include "trace.h"
 
 namespace py = pybind11;
 using namespace shellac;
@@ -136,6 +137,11 @@ PYBIND11_MODULE(_shellac_core, m) {
     device_exclusive_scan(P<const uint64_t>(in), P<uint64_t>(out), n, P<void>(tmp), tmp_bytes,
                           S(s));
   });
+  m.def("trace_enable", [](bool on) { trace_enable(on); });
+  m.def("trace_on", []() { return trace_on(); });
+  m.def("trace_push", [](const std::string& name) { trace_push(name.c_str()); });
+  m.def("trace_pop", []() { trace_pop(); });
+  m.def("trace_mark", [](const std::string& name) { trace_mark(name.c_str()); });
   m.def("segcopy", [](uintptr_t src, uintptr_t src_off, uintptr_t dst_off, int64_t n,
                       uintptr_t dst, uintptr_t s) {
     segcopy(P<const uint8_t>(src), P<const uint64_t>(src_off), P<const uint64_t>(dst_off), n,

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "hbm_cache.h"
+#include "trace.h"
 
 namespace shellac {
 
@@ -990,6 +991,7 @@ void HbmCache::reserve(int64_t n) {
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
                       uint32_t now, hipStream_t s, uint64_t reserve, int total_slot) {
+  TraceRange tr("hbm.lookup");
   SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
@@ -1032,6 +1034,7 @@ uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
                       hipStream_t s) {
+  TraceRange tr("hbm.gather");
   DeviceGuard g(cfg_.device);
   segcopy(log_, loc, off, n, out, s);
 }
@@ -1039,6 +1042,7 @@ void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s) {
+  TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
            "SET batch larger than half the log; split the batch");
@@ -1065,6 +1069,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
 }
 
 void HbmCache::remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now, hipStream_t s) {
+  TraceRange tr("hbm.remove");
   if (n <= 0) return;
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);

@@ -38,6 +38,7 @@ from ..ops.cache import CacheShard
 from ..parallel.exchange import (all_to_all_rows, allreduce_stats, dist_info, exchange_counts,
                                  segment_sums)
 from ..parallel.ring import ShardRing
+from .._native import core as _core
 
 SKIP_VLEN = -1  # int32 view of the kSkipVlen sentinel (row not for this tier)
 HDR_WORDS = 8   # ItemHeader = 8 x u32: d0 lo/hi, d1 lo/hi, vlen, flags, expire, magic
@@ -81,6 +82,30 @@ def records_to_set_batch(keys: torch.Tensor, res: GetResult) -> SetBatch:
     val_off = torch.where(hit, res.off + 32, torch.zeros_like(res.off))
     return SetBatch(keys=keys.contiguous(), values=res.data, val_off=val_off.contiguous(),
                     vlen=vlen.contiguous(), flags=flags.contiguous(), expire=expire.contiguous())
+
+
+class _Phases:
+    """Consecutive ROCTX ranges for the phases of one serving step (no-op when
+    tracing is off; see shellac_amd.utils.trace)."""
+
+    def __init__(self, prefix: str):
+        self.c = _core()
+        self.on = self.c.trace_on()
+        self.prefix = prefix
+        self.open = False
+
+    def next(self, name: str) -> None:
+        if not self.on:
+            return
+        if self.open:
+            self.c.trace_pop()
+        self.c.trace_push(self.prefix + name)
+        self.open = True
+
+    def end(self) -> None:
+        if self.on and self.open:
+            self.c.trace_pop()
+            self.open = False
 
 
 class ShardedCache:
@@ -262,7 +287,9 @@ class ShardedCache:
         self.stats["set_requests"] += batch.keys.shape[0]
         self._sample(keys)
         i64 = torch.int64
+        ph = _Phases("serve.")
         # ---- 1. routing + count exchange
+        ph.next("route")
         dest_g, _ = self._route(keys)
         rl = None
         if self.replica is not None:
@@ -284,6 +311,7 @@ class ShardedCache:
         vscan = R.exclusive_scan(padded)
         vb = segment_sums(vscan, cnt_s[:w].contiguous())
         table = torch.stack([cnt_g[:w], cnt_s[:w], vb], dim=1).contiguous()
+        ph.next("count_exchange")
         rtable = torch.empty_like(table)
         dist.all_to_all_single(rtable, table, group=self.group)
         ltot = rl.off[n:n + 1] if rl is not None else torch.zeros(1, dtype=i64, device=dev)
@@ -300,6 +328,7 @@ class ShardedCache:
         ns = sum(s_rows)
 
         # ---- 2. request exchange: per peer [G | R | V]
+        ph.next("pack_requests")
         g_start = [0] * w
         s_start = [0] * w
         for p in range(1, w):
@@ -325,11 +354,13 @@ class ShardedCache:
         send = torch.empty(sum(send_b) + 16, dtype=torch.uint8, device=dev)
         R.gather_segments(seg_src, R.exclusive_scan(seg_len), send)
         recv = torch.empty(sum(recv_b) + 16, dtype=torch.uint8, device=dev)
+        ph.next("request_a2a")
         dist.all_to_all_single(recv[: sum(recv_b)], send[: sum(send_b)],
                                output_split_sizes=recv_b, input_split_sizes=send_b,
                                group=self.group)
 
         # ---- 3. owner: de-interleave digests and records, probe
+        ph.next("owner_lookup")
         mg, ms = sum(rg_rows), sum(rs_rows)
         body = torch.empty(16 * mg + 32 * ms + 16, dtype=torch.uint8, device=dev)
         src_l, len_l = [], []
@@ -353,10 +384,12 @@ class ShardedCache:
         n_remote = n - n_local
         gscan = R.exclusive_scan(sizes_back)
         got_bytes = segment_sums(gscan, torch.tensor(g_rows, dtype=i64).to(dev, non_blocking=True))
+        ph.next("reply_sizes")
         nb = torch.cat([reply_bytes, got_bytes]).cpu()                    # sync 2
         rep_b, got_b = nb[:w].tolist(), nb[w:].tolist()
 
         # ---- 4. replies (async) overlapped with SET stores and the replica gather
+        ph.next("reply_a2a+set_store")
         reply = torch.empty(max(sum(rep_b), 16), dtype=torch.uint8, device=dev)
         self.shard.gather(lk, reply)
         data = torch.empty(local_bytes + sum(got_b) + 16, dtype=torch.uint8, device=dev)
@@ -392,6 +425,7 @@ class ShardedCache:
         work.wait()
 
         # ---- requester: response offsets in request order
+        ph.next("assemble")
         if n_remote:
             pos = torch.clamp(perm_g, max=n_remote - 1)
             rsize = sizes_back.index_select(0, pos)
@@ -407,6 +441,7 @@ class ShardedCache:
             size, off = rsize, roff_g
         self.stats["remote_gets"] += n_remote - int(g_rows[me])
         self.stats["replica_hits"] += n_local
+        ph.end()
         return GetResult(data, off, size)
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
