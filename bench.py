@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--sample-batches", type=int, default=8,
                     help="GET batches (independent of the timed ones) observed to pick the "
                          "replicated hot set")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="profiling only: run rank 0 of an N-rank job on one GPU with mirrored "
+                         "all-to-alls (no interconnect); prints a *_simulated metric")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = functional rehearsal of the distributed path over gloo "
                          "(DRAM shards); never a performance number")
@@ -111,7 +114,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    sim = args.simulate_world
+    if sim and world != 1:
+        raise SystemExit("--simulate-world runs as a single process")
+    if world != args.gpus and not sim:
         log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if args.device == "cuda":
         torch.cuda.set_device(local)
@@ -127,11 +133,20 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize()
 
+    group = None
+    if sim:
+        from shellac_amd.parallel.exchange import MirrorComm
+
+        group = MirrorComm(sim)
+        world = sim
+    real_world = 1 if sim else world
+
     total_keys = args.keys_per_gpu * world
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
     nb = 1
-    while nb * 2 < args.keys_per_gpu:  # ~50% slot load with 4-entry buckets
+    shard_keys = total_keys if sim else args.keys_per_gpu
+    while nb * 2 < shard_keys:  # ~50% slot load with 4-entry buckets
         nb *= 2
     log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
     shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)
@@ -142,16 +157,18 @@ def main():
             rnb *= 2
         replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
                              max_item=1 << 20, device=dev)
-    sc = ShardedCache(shard, replica=replica)
+    sc = ShardedCache(shard, group=group, replica=replica)
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
     lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
+    if sim:  # the mirrored owners all live in this one shard
+        lo, hi = 0, total_keys
     for s in range(lo, hi, chunk):
         ids = torch.arange(s, min(s + chunk, hi), device=dev)
         sc.set(wl.set_batch(ids))
     sync()
-    if world > 1:
+    if real_world > 1:
         dist.barrier()
     log(rank, f"[bench] populated {total_keys} keys in {time.perf_counter() - t_setup:.1f}s")
 
@@ -180,19 +197,19 @@ def main():
     sync()
     before = shard.counters()
     st0 = dict(sc.stats)
-    if world > 1:
+    if real_world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         res = step(i)
     sync()
-    if world > 1:
+    if real_world > 1:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if real_world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t)
 
@@ -204,7 +221,7 @@ def main():
                         after["get_bytes"] - before["get_bytes"], rep_hits,
                         sc.stats["get_requests"] - st0["get_requests"]], dtype=torch.int64,
                        device=dev)
-    if world > 1:
+    if real_world > 1:
         dist.all_reduce(agg)
     hits, gops, gbytes, rep_hits, greq = (int(v) for v in agg.tolist())
 
@@ -218,7 +235,7 @@ def main():
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
 
-    sm = {} if (args.no_smoke or dev.type != "cuda") else smoke(rank, world, dev)
+    sm = {} if (args.no_smoke or dev.type != "cuda" or sim) else smoke(rank, world, dev)
 
     ops_per_step = (args.batch + args.sets) * world
     ms = elapsed / args.steps * 1e3
@@ -257,9 +274,15 @@ def main():
     }
     if dev.type != "cuda":
         out["data"] = "cpu rehearsal over gloo: functional only, not a performance number"
+    if sim:
+        out["metric"] = "cache_ops_per_s_simulated"
+        out["data"] = (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
+                       "locally (no interconnect); profiling only, not a scaling result")
+        out["n_gpus"] = 1
+        out["simulated_world"] = sim
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if real_world > 1:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -265,4 +265,5 @@ PYBIND11_MODULE(_shellac_core, m) {
 
   bind_http(m);
   bind_net(m);
+  bind_router(m);
 }

@@ -35,8 +35,8 @@ import torch.distributed as dist
 
 from ..ops import routing as R
 from ..ops.cache import CacheShard
-from ..parallel.exchange import (all_to_all_rows, allreduce_stats, dist_info, exchange_counts,
-                                 segment_sums)
+from ..parallel.exchange import (all_gather, all_reduce, all_to_all_rows, all_to_all_single,
+                                 allreduce_stats, dist_info, exchange_counts, segment_sums)
 from ..parallel.ring import ShardRing
 from .._native import core as _core
 
@@ -123,6 +123,11 @@ class ShardedCache:
         self.sample_batches = sample_batches
         self._samples: List[torch.Tensor] = []
         self._hot: Optional[torch.Tensor] = None   # sorted hot digests [h, 2] (same on all ranks)
+        # GPU shards run the routed step through the fused native ops (csrc/router.hip);
+        # the framework-op version (_serve_routed) is the CPU path and the test oracle
+        self.fused = True
+        self._engine = None
+        self._xtable = None
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -189,7 +194,7 @@ class ShardedCache:
                            device=self.device)
         if rl is not None and n_local:
             self.replica.gather(rl, data)
-        dist.all_to_all_single(data[local_bytes: local_bytes + int(sum(recv_b))],
+        all_to_all_single(data[local_bytes: local_bytes + int(sum(recv_b))],
                                reply[: int(sum(send_b))], output_split_sizes=recv_b,
                                input_split_sizes=send_b, group=self.group)
         # requester side: remote sizes arrive in grouped (perm) order
@@ -222,6 +227,8 @@ class ShardedCache:
         With several ranks see ``_serve_routed``: 4 collectives and 2 host syncs for
         the whole step instead of 10 and 3 for get() followed by set()."""
         if self.world > 1:
+            if self.fused and self.device.type == "cuda":
+                return self._serve_routed_fused(keys, batch, now)
             return self._serve_routed(keys, batch, now)
         n = keys.shape[0]
         self.stats["get_requests"] += n
@@ -238,6 +245,78 @@ class ShardedCache:
         sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags, batch.expire, now)
         data = sh.gather(lk, total=sh.host_total(0))
         return GetResult(data, lk.off[:n], lk.size[:n])
+
+    def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
+                            now: Optional[int] = None) -> GetResult:
+        """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep):
+        every step between the collectives is a fused kernel sequence over a grow-only
+        device arena; Python issues the four all-to-alls and nothing else. Same
+        protocol and results as the framework-op version (tests/test_hbm_gpu.py)."""
+        c = _core()
+        dev, w, me = self.device, self.world, self.rank
+        st = torch.cuda.current_stream(dev).cuda_stream
+        i64, u8 = torch.int64, torch.uint8
+        n = keys.shape[0]
+        ns_in = batch.keys.shape[0]
+        self.stats["get_requests"] += n
+        self.stats["set_requests"] += ns_in
+        self._sample(keys)
+        now = self.shard.now() if now is None else now
+        e = self._engine
+        if e is None:
+            e = self._engine = c.RoutedStep(w, me, dev.index)
+            self._xtable = torch.empty((2, w, 3), dtype=i64, device=dev)
+        e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
+        fanout = self.replica is not None and self._hot is not None
+        e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0)
+        rep = self.replica._impl if self.replica is not None else None
+        table, rtable = self._xtable[0], self._xtable[1]
+        ph = _Phases("serve.")
+        ph.next("plan")
+        e.plan(keys.data_ptr(), n, rep, now, batch.keys.data_ptr(), batch.vlen.data_ptr(),
+               batch.flags.data_ptr() if batch.flags is not None else 0,
+               batch.expire.data_ptr() if batch.expire is not None else 0,
+               batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
+               table.data_ptr(), st)
+        ph.next("count_exchange")
+        all_to_all_single(rtable, table, group=self.group)
+        h = e.read_counts(rtable.data_ptr(), st)                          # sync 1
+        g_rows = h[0: 3 * w: 3]
+        rg_rows = h[3 * w: 6 * w: 3]
+        send_b = [16 * h[3 * p] + 32 * h[3 * p + 1] + h[3 * p + 2] for p in range(w)]
+        recv_b = [16 * h[3 * w + 3 * p] + 32 * h[3 * w + 3 * p + 1] + h[3 * w + 3 * p + 2]
+                  for p in range(w)]
+        n_local, local_bytes = h[6 * w], h[6 * w + 1]
+        ph.next("pack_requests")
+        send = torch.empty(sum(send_b) + 16, dtype=u8, device=dev)
+        e.pack(send.data_ptr(), st)
+        recv = torch.empty(sum(recv_b) + 16, dtype=u8, device=dev)
+        ph.next("request_a2a")
+        all_to_all_single(recv[: sum(recv_b)], send[: sum(send_b)], output_split_sizes=recv_b,
+                          input_split_sizes=send_b, group=self.group)
+        ph.next("owner_lookup")
+        mg = e.mg
+        sizes_out = torch.empty(mg + 1, dtype=i64, device=dev)
+        e.owner(recv.data_ptr(), self.shard._impl, now, sizes_out.data_ptr(), st)
+        sizes_in = all_to_all_rows(sizes_out[:mg], rg_rows, g_rows, self.group)
+        ph.next("reply_sizes")
+        nb = e.reply_sizes(sizes_in.data_ptr(), st)                        # sync 2
+        rep_b, got_b = nb[:w], nb[w:]
+        ph.next("reply_a2a+set_store")
+        reply = torch.empty(max(sum(rep_b), 16), dtype=u8, device=dev)
+        e.gather_replies(self.shard._impl, reply.data_ptr(), st)
+        data = torch.empty(local_bytes + sum(got_b) + 16, dtype=u8, device=dev)
+        work = all_to_all_single(data[local_bytes: local_bytes + sum(got_b)], reply[: sum(rep_b)],
+                                 output_split_sizes=got_b, input_split_sizes=rep_b,
+                                 group=self.group, async_op=True)
+        out = torch.empty((2, n), dtype=i64, device=dev)
+        e.finish(data.data_ptr(), recv.data_ptr(), sum(recv_b), self.shard._impl, rep, now,
+                 out[0].data_ptr(), out[1].data_ptr(), st)
+        work.wait()
+        self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
+        self.stats["replica_hits"] += n_local
+        ph.end()
+        return GetResult(data, out[1], out[0])
 
     def _set_rows(self, batch: SetBatch):
         """Routing of a SET batch: (dest int32 [m], records int64 [m, 4], val_off [m]).
@@ -313,7 +392,7 @@ class ShardedCache:
         table = torch.stack([cnt_g[:w], cnt_s[:w], vb], dim=1).contiguous()
         ph.next("count_exchange")
         rtable = torch.empty_like(table)
-        dist.all_to_all_single(rtable, table, group=self.group)
+        all_to_all_single(rtable, table, group=self.group)
         ltot = rl.off[n:n + 1] if rl is not None else torch.zeros(1, dtype=i64, device=dev)
         host = torch.cat([table.view(-1), rtable.view(-1), cnt_g[w:w + 1], ltot]).cpu()  # sync 1
         t = host[: 3 * w].view(w, 3).tolist()
@@ -355,7 +434,7 @@ class ShardedCache:
         R.gather_segments(seg_src, R.exclusive_scan(seg_len), send)
         recv = torch.empty(sum(recv_b) + 16, dtype=torch.uint8, device=dev)
         ph.next("request_a2a")
-        dist.all_to_all_single(recv[: sum(recv_b)], send[: sum(send_b)],
+        all_to_all_single(recv[: sum(recv_b)], send[: sum(send_b)],
                                output_split_sizes=recv_b, input_split_sizes=send_b,
                                group=self.group)
 
@@ -393,7 +472,7 @@ class ShardedCache:
         reply = torch.empty(max(sum(rep_b), 16), dtype=torch.uint8, device=dev)
         self.shard.gather(lk, reply)
         data = torch.empty(local_bytes + sum(got_b) + 16, dtype=torch.uint8, device=dev)
-        work = dist.all_to_all_single(data[local_bytes: local_bytes + sum(got_b)],
+        work = all_to_all_single(data[local_bytes: local_bytes + sum(got_b)],
                                       reply[: sum(rep_b)], output_split_sizes=got_b,
                                       input_split_sizes=rep_b, group=self.group, async_op=True)
         if rl is not None and n_local:
@@ -496,7 +575,7 @@ class ShardedCache:
         rkeys = all_to_all_rows(send_keys[:ns], send_rows, recv_rows, self.group)
         rmeta = all_to_all_rows(send_meta[:ns], send_rows, recv_rows, self.group)
         rvals = torch.empty(int(sum(recv_b)) + 16, dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(rvals[: int(sum(recv_b))], payload[: int(sum(send_b))],
+        all_to_all_single(rvals[: int(sum(recv_b))], payload[: int(sum(send_b))],
                                output_split_sizes=recv_b, input_split_sizes=send_b,
                                group=self.group)
         rvlen = rmeta[:, 0].contiguous()
@@ -514,11 +593,11 @@ class ShardedCache:
             return self.shard.remove(keys, now)
         if self.replica is not None:  # replicas are dropped everywhere (collective)
             cnt = torch.tensor([keys.shape[0]], dtype=torch.int64, device=self.device)
-            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
+            all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
             pad = torch.zeros((int(cnt), 2), dtype=keys.dtype, device=self.device)
             pad[: keys.shape[0]] = keys
             allk = [torch.empty_like(pad) for _ in range(self.world)]
-            dist.all_gather(allk, pad, group=self.group)
+            all_gather(allk, pad, group=self.group)
             self.replica.remove(torch.cat(allk).contiguous(), now)
         dest, counts = self._route(keys)
         perm = R.scatter_positions(dest, counts)
@@ -555,8 +634,8 @@ class ShardedCache:
         ccnt[:k] = cnt.index_select(0, top)
         all_c = [torch.empty_like(cand) for _ in range(w)]
         all_n = [torch.empty_like(ccnt) for _ in range(w)]
-        dist.all_gather(all_c, cand, group=self.group)
-        dist.all_gather(all_n, ccnt, group=self.group)
+        all_gather(all_c, cand, group=self.group)
+        all_gather(all_n, ccnt, group=self.group)
         allc = torch.cat(all_c)
         alln = torch.cat(all_n)
         u, inv = torch.unique(allc, dim=0, return_inverse=True)

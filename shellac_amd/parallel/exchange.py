@@ -16,25 +16,80 @@ import torch
 import torch.distributed as dist
 
 
+class MirrorComm:
+    """Single-process stand-in for an N-rank group whose traffic is symmetric: every
+    peer sends me exactly what I send it, so an all-to-all returns its input.
+
+    Profiling tool only (``bench.py --simulate-world N``): it runs the complete routed
+    serving step of rank 0 of an N-rank job on one GPU — routing, packing, owner
+    lookups, gathers, stores, host syncs, Python overhead — with the interconnect
+    transfers replaced by local copies. It never produces a scaling number."""
+
+    def __init__(self, world: int, rank: int = 0):
+        self.world, self.rank = int(world), int(rank)
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
 def dist_info(group=None) -> tuple[int, int]:
+    if isinstance(group, MirrorComm):
+        return group.rank, group.world
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
+
+
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, output_split_sizes=None,
+                      input_split_sizes=None, group=None, async_op: bool = False):
+    """torch.distributed.all_to_all_single (RCCL on ROCm) or the mirror stand-in."""
+    if isinstance(group, MirrorComm):
+        if out.numel() != inp.numel():
+            raise ValueError("mirror all_to_all needs symmetric splits")
+        out.copy_(inp.view(out.shape) if out.shape != inp.shape else inp)
+        return _Done() if async_op else None
+    return dist.all_to_all_single(out, inp, output_split_sizes=output_split_sizes,
+                                  input_split_sizes=input_split_sizes, group=group,
+                                  async_op=async_op)
+
+
+def all_gather(tensors: list, t: torch.Tensor, group=None) -> None:
+    if isinstance(group, MirrorComm):
+        for x in tensors:
+            x.copy_(t)
+        return
+    dist.all_gather(tensors, t, group=group)
+
+
+def all_reduce(t: torch.Tensor, op=None, group=None) -> None:
+    op = dist.ReduceOp.SUM if op is None else op
+    if isinstance(group, MirrorComm):
+        if op == dist.ReduceOp.SUM:
+            t.mul_(group.world)
+        return
+    dist.all_reduce(t, op=op, group=group)
+
+
+def barrier(group=None) -> None:
+    if not isinstance(group, MirrorComm):
+        dist.barrier(group=group)
 
 
 def all_to_all_rows(x: torch.Tensor, send_rows: Sequence[int], recv_rows: Sequence[int],
                     group=None) -> torch.Tensor:
     """all_to_all_single over the first dim with explicit row splits."""
     out = torch.empty((int(sum(recv_rows)),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_to_all_single(out, x.contiguous(), output_split_sizes=list(map(int, recv_rows)),
-                           input_split_sizes=list(map(int, send_rows)), group=group)
+    all_to_all_single(out, x.contiguous(), output_split_sizes=list(map(int, recv_rows)),
+                      input_split_sizes=list(map(int, send_rows)), group=group)
     return out
 
 
 def exchange_counts(counts: torch.Tensor, group=None) -> torch.Tensor:
     """counts[r] = rows I send to r  ->  rows r sends to me (same device)."""
     out = torch.empty_like(counts)
-    dist.all_to_all_single(out, counts.contiguous(), group=group)
+    all_to_all_single(out, counts.contiguous(), group=group)
     return out
 
 
@@ -43,7 +98,7 @@ def allreduce_stats(stats: dict, device, group=None) -> dict:
     keys = sorted(stats)
     t = torch.tensor([int(stats[k]) for k in keys], dtype=torch.int64, device=device)
     if dist_info(group)[1] > 1:
-        dist.all_reduce(t, group=group)
+        all_reduce(t, group=group)
     return {k: int(v) for k, v in zip(keys, t.tolist())}
 
 

@@ -266,3 +266,34 @@ def test_lookup_offsets_fused_scan(cuda_dev, n):
     # the kernel-written host slot carries the same total without a D2H copy
     shard.lookup(keys.to(cuda_dev), total_slot=3)
     assert shard.host_total(3) == int(ref[-1])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
+    """The fused native routed step (csrc/router.hip) returns exactly what the
+    framework-op version returns, on one GPU with mirrored all-to-alls."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+    from shellac_amd.parallel.exchange import MirrorComm
+
+    wl = Workload(40000, cuda_dev)
+    outs = []
+    for fused in (False, True):
+        sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(world),
+                          replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev))
+        sc.fused = fused
+        for s0 in range(0, 40000, 10000):
+            sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
+        sc.refresh_replica(2000, keys=wl.digests.index_select(0, wl.sample_ids(50000, 1)))
+        keys = wl.digests.index_select(0, wl.sample_ids(8192, 2)).contiguous()
+        got = []
+        for step in range(3):
+            r = sc.serve(keys, wl.set_batch(wl.uniform_ids(1024, 10 + step)))
+            got.append([None if x is None else x[0]
+                        for x in unpack_records(r.data, r.off, r.size)])
+        outs.append((got, dict(sc.stats)))
+    (g0, s0), (g1, s1) = outs
+    assert g0 == g1
+    assert s0 == s1
+    assert sum(v is not None for v in g1[0]) == 8192     # every GET hits
+    assert s1["replica_hits"] > 0
