@@ -35,56 +35,10 @@ void route_gets(const Digest* keys, int64_t n, const uint64_t* replica_size,
                 const uint32_t* ring_pts, const int32_t* ring_owner, int32_t npts, int32_t w,
                 int32_t* dest, hipStream_t s);
 
-// SET side: route + hot-key fan-out + grouping. With `fanout` every input row j
-// becomes w virtual rows (j, r): r receives it if r owns the key (tier 0) or the
-// key is in the sorted hot set (tier 1, replica copy). Outputs in grouped order:
-// srec[m][4] = {digest lo, hi, vlen | flags << 32, expire | tier << 32},
-// sval[m] = values_base + val_off[j] (absolute address), spad[m] = 16-aligned value
-// bytes (0 for skip rows and bucket-w rows), counts[w + 1]. m = ns * (fanout ? w : 1).
-// Scratch: dest_ws[m] int32, owner_ws[ns] int32, ws = group_ws_words(m, w + 1).
-void plan_sets(const Digest* keys, const uint32_t* vlen, const uint32_t* flags,
-               const uint32_t* expire, const uint64_t* val_off, int64_t ns, uint64_t values_base,
-               const uint32_t* ring_pts, const int32_t* ring_owner, int32_t npts,
-               const Digest* hot, int64_t nhot, int32_t w, bool fanout, int32_t* dest_ws,
-               int32_t* owner_ws, uint64_t* ws, int64_t* srec, uint64_t* sval, uint64_t* spad,
-               int64_t* counts, hipStream_t s);
-
-// table[p] = {GET rows, SET rows, SET value bytes} I send to peer p (int64 [w][3]);
-// vscan = exclusive scan of spad (m + 1 entries).
-void plan_table(const int64_t* cnt_g, const int64_t* cnt_s, const uint64_t* vscan, int32_t w,
-                int64_t* table, hipStream_t s);
-
-// Segment list of the request buffer: per peer p [G_p | R_p | V rows of p], for
-// gather_segments. gk / srec are the grouped GET digests and SET records; ns = SET rows
-// that leave this rank (host value, sum of cnt_s[0..w)). seg_len / seg_src: 2w + ns.
-void send_segments(const int64_t* cnt_g, const int64_t* cnt_s, const uint64_t* spad,
-                   const uint64_t* sval, uint64_t gk_base, uint64_t srec_base, int32_t w,
-                   int64_t ns, uint64_t* seg_len, uint64_t* seg_src, hipStream_t s);
-
-// Segment list that de-interleaves the received buffer into [all G | all R]
-// (2w segments) from the received table rtable[w][3].
-void recv_segments(const int64_t* rtable, uint64_t recv_base, int32_t w, uint64_t* seg_len,
-                   uint64_t* seg_src, hipStream_t s);
-
-// Received SET rows: keys, per-tier vlen (skip sentinel for the other tier), flags,
-// expire and the offset of each value inside the received buffer. rpad_ws / rscan_ws
-// are [ms] / [ms + 1] scratch; scan_tmp is device_scan_tmp_bytes(ms) bytes.
-void recv_sets(const int64_t* rrec, int64_t ms, const int64_t* rtable, int32_t w,
-               uint64_t* rpad_ws, uint64_t* rscan_ws, void* scan_tmp, size_t scan_tmp_bytes,
-               Digest* keys, uint32_t* vlen0, uint32_t* vlen1, uint32_t* flags, uint32_t* expire,
-               uint64_t* roff, hipStream_t s);
-
-// bytes[0..w) = reply bytes per source q (owner side, from lk_off over rtable GET rows),
-// bytes[w..2w) = bytes expected from owner p (requester side, from gscan over table).
-void reply_bytes(const uint64_t* lk_off, const int64_t* rtable, const uint64_t* gscan,
-                 const int64_t* table, int32_t w, int64_t* bytes, hipStream_t s);
-
-// Response (size, off) in request order: replica hits from (rl_size, rl_off), the rest
-// from the grouped remote sizes (sizes_back, gscan) shifted by local_bytes.
-void assemble_response(const int64_t* perm_g, int64_t n, int64_t n_remote,
-                       const uint64_t* sizes_back, const uint64_t* gscan,
-                       const uint64_t* rl_size, const uint64_t* rl_off, uint64_t local_bytes,
-                       uint64_t* size, uint64_t* off, hipStream_t s);
+// Exclusive scan of n uint64 values into out[0..n] (out[n] = total) in two launches,
+// without hipcub's sentinel/temp requirements; parts = scan_parts_words(n) words.
+void scan_u64(const uint64_t* in, int64_t n, uint64_t* parts, uint64_t* out, hipStream_t s);
+int64_t scan_parts_words(int64_t n);
 
 class HbmCache;
 
@@ -141,7 +95,6 @@ class RoutedStep {
   };
   template <typename T>
   T* buf(int slot, size_t count);
-  uint64_t* scan(uint64_t* in, uint64_t* out, int64_t n, hipStream_t s);  // in[n] zeroed here
 
   int w_, rank_, device_;
   const uint32_t* pts_ = nullptr;
@@ -162,7 +115,7 @@ class RoutedStep {
   uint64_t *rl_loc_ = nullptr, *rl_size_ = nullptr, *rl_off_ = nullptr;
   Digest* gk_ = nullptr;
   int64_t *perm_g_ = nullptr, *cnt_g_ = nullptr, *cnt_s_ = nullptr, *srec_ = nullptr;
-  uint64_t *sval_ = nullptr, *spad_ = nullptr;
+  uint64_t *sval_ = nullptr, *svoff_ = nullptr;
   const int64_t* rrec_ = nullptr;
   uint64_t *lk_loc_ = nullptr, *lk_off_ = nullptr, *gscan_ = nullptr;
   const uint64_t* sizes_in_ = nullptr;

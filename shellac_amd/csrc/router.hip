@@ -155,17 +155,22 @@ __global__ __launch_bounds__(kB) void k_route_gets(const Digest* __restrict__ ke
     dest[i] = (rsize && rsize[i] > 0) ? w : ring_owner_of(keys[i], pts, own, npts);
 }
 
-__global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys, int64_t ns,
+// SET planning. Input row j becomes virtual row v = j * w + r (fan-out) or v = j.
+__global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
+                                                const uint32_t* __restrict__ vlen, int64_t ns,
                                                 const uint32_t* __restrict__ pts,
                                                 const int32_t* __restrict__ own, int npts,
                                                 const Digest* __restrict__ hot, int64_t nhot,
                                                 int32_t w, bool fanout,
                                                 int32_t* __restrict__ dest,
-                                                int32_t* __restrict__ owner) {
+                                                int32_t* __restrict__ owner,
+                                                uint32_t* __restrict__ vpad) {
   for (int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x; j < ns; j += (int64_t)gridDim.x * kB) {
     const Digest k = keys[j];
     const int o = ring_owner_of(k, pts, own, npts);
     owner[j] = o;
+    const uint32_t vl = vlen[j];
+    vpad[j] = vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
     if (!fanout) {
       dest[j] = o;
       continue;
@@ -175,123 +180,212 @@ __global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
   }
 }
 
-__global__ __launch_bounds__(kB) void k_ps_scatter(
-    const int32_t* __restrict__ dest, int64_t m, int32_t nb, int64_t plen,
-    const uint64_t* __restrict__ table, const Digest* __restrict__ keys,
-    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ expire, const uint64_t* __restrict__ val_off,
-    uint64_t values_base, const int32_t* __restrict__ owner, int32_t w, bool fanout,
-    int64_t* __restrict__ srec, uint64_t* __restrict__ sval, uint64_t* __restrict__ spad) {
-  extern __shared__ uint32_t s_cur[];
-  for (int d = threadIdx.x; d < nb; d += kB) s_cur[d] = 0;
+// Rows AND value bytes per (bucket, workgroup): one packed 64-bit LDS counter
+// (rows | bytes << 32) so the scatter below can hand out row slots and byte ranges in
+// the same order.
+__global__ __launch_bounds__(kB) void k_ps_hist(const int32_t* __restrict__ dest, int64_t m,
+                                                int32_t nb, int64_t plen, int32_t w, bool fanout,
+                                                const uint32_t* __restrict__ vpad,
+                                                uint64_t* __restrict__ tcnt,
+                                                uint64_t* __restrict__ tbytes) {
+  extern __shared__ unsigned long long s_cb[];
+  for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(m, i0 + plen);
   for (int64_t v = i0 + threadIdx.x; v < i1; v += kB) {
     const int d = dest[v];
-    const int64_t pos =
-        (int64_t)table[(int64_t)d * gridDim.x + blockIdx.x] + atomicAdd(&s_cur[d], 1u);
+    const uint64_t pad = d < w ? vpad[fanout ? v / w : v] : 0;
+    atomicAdd(&s_cb[d], 1ull | (pad << 32));
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nb; d += kB) {
+    const uint64_t c = s_cb[d];
+    tcnt[(int64_t)d * gridDim.x + blockIdx.x] = c & 0xFFFFFFFFull;
+    tbytes[(int64_t)d * gridDim.x + blockIdx.x] = c >> 32;
+  }
+}
+
+// One workgroup: block-wide exclusive scan of t[0..T) in place, returns the total.
+__device__ unsigned long long block_scan_inplace(uint64_t* __restrict__ t, int64_t T,
+                                                 unsigned long long* s_w) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t per = (T + 1023) / 1024;
+  const int64_t a = min(T, per * tid), b = min(T, a + per);
+  unsigned long long mine = 0;
+  for (int64_t i = a; i < b; ++i) mine += t[i];
+  unsigned long long inc = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  __syncthreads();
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long run = 0;
+    for (int k = 0; k < 16; ++k) {
+      const unsigned long long v = s_w[k];
+      s_w[k] = run;
+      run += v;
+    }
+    s_w[16] = run;
+  }
+  __syncthreads();
+  unsigned long long run = s_w[wv] + inc - mine;
+  for (int64_t i = a; i < b; ++i) {
+    const unsigned long long v = t[i];
+    t[i] = run;
+    run += v;
+  }
+  const unsigned long long total = s_w[16];
+  __syncthreads();
+  return total;
+}
+
+// Scans both SET tables, then writes the per-peer exchange table
+// table[p] = {GET rows, SET rows, SET value bytes} and extras = {local GET hits,
+// local replica response bytes}.
+__global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
+                                                  uint64_t* __restrict__ tbytes, int32_t nb,
+                                                  int32_t G, const int64_t* __restrict__ cnt_g,
+                                                  const uint64_t* __restrict__ rl_off_n,
+                                                  int64_t* __restrict__ cnt_s,
+                                                  int64_t* __restrict__ table,
+                                                  int64_t* __restrict__ extras) {
+  __shared__ unsigned long long s_w[17];
+  const int64_t T = (int64_t)nb * G;
+  const unsigned long long tc = block_scan_inplace(tcnt, T, s_w);
+  const unsigned long long tb = block_scan_inplace(tbytes, T, s_w);
+  __syncthreads();
+  const int w = nb - 1;
+  for (int d = threadIdx.x; d < nb; d += 1024) {
+    const uint64_t c1 = d + 1 < nb ? tcnt[(int64_t)(d + 1) * G] : tc;
+    const uint64_t b1 = d + 1 < nb ? tbytes[(int64_t)(d + 1) * G] : tb;
+    const int64_t c = (int64_t)(c1 - tcnt[(int64_t)d * G]);
+    cnt_s[d] = c;
+    if (d < w) {
+      table[d * 3 + 0] = cnt_g[d];
+      table[d * 3 + 1] = c;
+      table[d * 3 + 2] = (int64_t)(b1 - tbytes[(int64_t)d * G]);
+    }
+  }
+  if (threadIdx.x == 0) {
+    extras[0] = cnt_g[w];
+    extras[1] = rl_off_n ? (int64_t)*rl_off_n : 0;
+  }
+}
+
+// rec = {lo, hi, vlen | flags << 32, expire | (voff | tier << 31) << 32} where voff is
+// the value's offset inside the destination peer's value block.
+__global__ __launch_bounds__(kB) void k_ps_scatter(
+    const int32_t* __restrict__ dest, int64_t m, int32_t nb, int64_t plen,
+    const uint64_t* __restrict__ tcnt, const uint64_t* __restrict__ tbytes,
+    const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
+    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
+    const uint64_t* __restrict__ val_off, uint64_t values_base, const int32_t* __restrict__ owner,
+    const uint32_t* __restrict__ vpad, int32_t w, bool fanout, int64_t* __restrict__ srec,
+    uint64_t* __restrict__ sval, uint64_t* __restrict__ svoff) {
+  extern __shared__ unsigned long long s_cb[];
+  for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
+  __syncthreads();
+  const int G = gridDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(m, i0 + plen);
+  for (int64_t v = i0 + threadIdx.x; v < i1; v += kB) {
+    const int d = dest[v];
     const int64_t j = fanout ? v / w : v;
+    const uint64_t pad = d < w ? vpad[j] : 0;
+    const unsigned long long old = atomicAdd(&s_cb[d], 1ull | (pad << 32));
+    const int64_t pos = (int64_t)tcnt[(int64_t)d * G + blockIdx.x] + (int64_t)(old & 0xFFFFFFFFull);
+    const uint64_t vglob = tbytes[(int64_t)d * G + blockIdx.x] + (old >> 32);
+    const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
     const int r = fanout ? (int)(v - j * w) : owner[j];
-    const uint32_t tier = (fanout && r != owner[j]) ? 1u : 0u;
+    const uint64_t tier = (fanout && r != owner[j]) ? 1ull : 0ull;
     const Digest k = keys[j];
-    const uint32_t vl = vlen[j];
     int64_t* rec = srec + pos * 4;
     rec[0] = (int64_t)k.lo;
     rec[1] = (int64_t)k.hi;
-    rec[2] = (int64_t)((uint64_t)vl | ((uint64_t)(flags ? flags[j] : 0u) << 32));
-    rec[3] = (int64_t)((uint64_t)(expire ? expire[j] : 0u) | ((uint64_t)tier << 32));
+    rec[2] = (int64_t)((uint64_t)vlen[j] | ((uint64_t)(flags ? flags[j] : 0u) << 32));
+    rec[3] = (int64_t)((uint64_t)(expire ? expire[j] : 0u) | ((voff | (tier << 31)) << 32));
     sval[pos] = values_base + val_off[j];
-    spad[pos] = (d < w && vl != kSkipVlen) ? align16(vl) : 0;
+    svoff[pos] = vglob;
   }
 }
 
-__global__ void k_plan_table(const int64_t* __restrict__ cnt_g, const int64_t* __restrict__ cnt_s,
-                             const uint64_t* __restrict__ vscan, int32_t w,
-                             int64_t* __restrict__ table) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int64_t S = 0;
-  for (int p = 0; p < w; ++p) {
-    table[p * 3 + 0] = cnt_g[p];
-    table[p * 3 + 1] = cnt_s[p];
-    table[p * 3 + 2] = (int64_t)(vscan[S + cnt_s[p]] - vscan[S]);
-    S += cnt_s[p];
-  }
-}
-
-// Per-peer prefix sums staged in LDS by every workgroup (w is small).
-__global__ __launch_bounds__(kB) void k_send_segs(const int64_t* __restrict__ cnt_g,
-                                                  const int64_t* __restrict__ cnt_s,
-                                                  const uint64_t* __restrict__ spad,
+// Request buffer, per peer p: [G_p | R_p | V rows of p]; destination offsets follow
+// from the exchange table, so no scan: seg_off[2w + ns + 1] (last = total bytes).
+__global__ __launch_bounds__(kB) void k_send_segs(const int64_t* __restrict__ table,
+                                                  const uint64_t* __restrict__ svoff,
                                                   const uint64_t* __restrict__ sval,
                                                   uint64_t gk_base, uint64_t srec_base, int32_t w,
-                                                  int64_t ns, uint64_t* __restrict__ seg_len,
+                                                  int64_t ns, uint64_t* __restrict__ seg_off,
                                                   uint64_t* __restrict__ seg_src) {
-  extern __shared__ int64_t s_pre[];  // S[w+1], Gp[w+1]
+  extern __shared__ int64_t s_pre[];  // S[w+1] rows, Gp[w+1], P[w+1] peer starts, V[w+1]
   int64_t* S = s_pre;
-  int64_t* Gp = s_pre + (w + 1);
+  int64_t* Gp = S + (w + 1);
+  int64_t* P = Gp + (w + 1);
+  int64_t* V = P + (w + 1);
   if (threadIdx.x == 0) {
-    S[0] = Gp[0] = 0;
+    S[0] = Gp[0] = P[0] = V[0] = 0;
     for (int p = 0; p < w; ++p) {
-      S[p + 1] = S[p] + cnt_s[p];
-      Gp[p + 1] = Gp[p] + cnt_g[p];
+      const int64_t g = table[p * 3], sr = table[p * 3 + 1], vb = table[p * 3 + 2];
+      S[p + 1] = S[p] + sr;
+      Gp[p + 1] = Gp[p] + g;
+      V[p + 1] = V[p] + vb;
+      P[p + 1] = P[p] + 16 * g + 32 * sr + vb;
     }
   }
   __syncthreads();
   const int64_t total = ns + w;
-  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < total;
+  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i <= total;
        i += (int64_t)gridDim.x * kB) {
-    if (i < ns) {
-      int lo = 0, hi = w;  // last p with S[p] <= i
+    if (i == total) {
+      seg_off[2 * w + ns] = (uint64_t)P[w];
+    } else if (i < ns) {
+      int lo = 0, hi = w;  // peer p with S[p] <= i < S[p+1]
       while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
         if (S[mid] <= i) lo = mid; else hi = mid;
       }
       const int64_t seg = i + 2 * lo + 2;
-      seg_len[seg] = spad[i];
+      const int64_t sr = S[lo + 1] - S[lo], g = Gp[lo + 1] - Gp[lo];
+      seg_off[seg] = (uint64_t)(P[lo] + 16 * g + 32 * sr) + (svoff[i] - (uint64_t)V[lo]);
       seg_src[seg] = sval[i];
     } else {
       const int p = (int)(i - ns);
-      const int64_t g = 2 * p + S[p];
-      seg_len[g] = 16 * (uint64_t)cnt_g[p];
-      seg_src[g] = gk_base + 16 * (uint64_t)Gp[p];
-      seg_len[g + 1] = 32 * (uint64_t)cnt_s[p];
-      seg_src[g + 1] = srec_base + 32 * (uint64_t)S[p];
+      const int64_t gseg = 2 * p + S[p];
+      const int64_t g = Gp[p + 1] - Gp[p];
+      seg_off[gseg] = (uint64_t)P[p];
+      seg_src[gseg] = gk_base + 16 * (uint64_t)Gp[p];
+      seg_off[gseg + 1] = (uint64_t)(P[p] + 16 * g);
+      seg_src[gseg + 1] = srec_base + 32 * (uint64_t)S[p];
     }
   }
 }
 
+// De-interleave the received buffer into [all G | all R]: 2w segments + end offset.
 __global__ void k_recv_segs(const int64_t* __restrict__ rtable, uint64_t recv_base, int32_t w,
-                            uint64_t* __restrict__ seg_len, uint64_t* __restrict__ seg_src) {
+                            uint64_t* __restrict__ seg_off, uint64_t* __restrict__ seg_src) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t q0 = 0;
+  uint64_t q0 = 0, g0 = 0, r0 = 0, gtot = 0;
+  for (int q = 0; q < w; ++q) gtot += 16 * (uint64_t)rtable[q * 3];
   for (int q = 0; q < w; ++q) {
     const uint64_t a = (uint64_t)rtable[q * 3], b = (uint64_t)rtable[q * 3 + 1],
                    c = (uint64_t)rtable[q * 3 + 2];
-    seg_len[q] = 16 * a;
+    seg_off[q] = g0;
     seg_src[q] = recv_base + q0;
-    seg_len[w + q] = 32 * b;
+    seg_off[w + q] = gtot + r0;
     seg_src[w + q] = recv_base + q0 + 16 * a;
+    g0 += 16 * a;
+    r0 += 32 * b;
     q0 += 16 * a + 32 * b + c;
   }
-}
-
-__global__ __launch_bounds__(kB) void k_rs_pad(const int64_t* __restrict__ rrec, int64_t ms,
-                                               uint64_t* __restrict__ rpad) {
-  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r <= ms; r += (int64_t)gridDim.x * kB) {
-    if (r == ms) {
-      rpad[ms] = 0;
-      continue;
-    }
-    const uint32_t vl = (uint32_t)rrec[r * 4 + 2];
-    rpad[r] = vl == kSkipVlen ? 0 : align16(vl);
-  }
+  seg_off[2 * w] = gtot + r0;
 }
 
 __global__ __launch_bounds__(kB) void k_rs_fill(
     const int64_t* __restrict__ rrec, int64_t ms, const int64_t* __restrict__ rtable, int32_t w,
-    const uint64_t* __restrict__ rscan, Digest* __restrict__ keys, uint32_t* __restrict__ vlen0,
-    uint32_t* __restrict__ vlen1, uint32_t* __restrict__ flags, uint32_t* __restrict__ expire,
-    uint64_t* __restrict__ roff) {
+    Digest* __restrict__ keys, uint32_t* __restrict__ vlen0, uint32_t* __restrict__ vlen1,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ expire, uint64_t* __restrict__ roff) {
   extern __shared__ int64_t s_q[];  // first[w+1], vstart[w]
   int64_t* first = s_q;
   int64_t* vstart = s_q + (w + 1);
@@ -315,13 +409,73 @@ __global__ __launch_bounds__(kB) void k_rs_fill(
     const int64_t* rec = rrec + r * 4;
     keys[r] = Digest{(uint64_t)rec[0], (uint64_t)rec[1]};
     const uint32_t vl = (uint32_t)rec[2];
-    const uint32_t tier = (uint32_t)((uint64_t)rec[3] >> 32);
+    const uint64_t hi32 = (uint64_t)rec[3] >> 32;
+    const uint32_t tier = (uint32_t)(hi32 >> 31);
     vlen0[r] = tier == 0 ? vl : kSkipVlen;
     vlen1[r] = tier == 1 ? vl : kSkipVlen;
     flags[r] = (uint32_t)((uint64_t)rec[2] >> 32);
     expire[r] = (uint32_t)rec[3];
-    roff[r] = (uint64_t)vstart[lo] + (rscan[r] - rscan[first[lo]]);
+    roff[r] = (uint64_t)vstart[lo] + (hi32 & 0x7FFFFFFFull);
   }
+}
+
+// Two-launch exclusive scan of n values (out[n] = total) that needs no sentinel:
+// per-workgroup sums over contiguous ranges, then each workgroup adds the sums before it.
+constexpr int kScanItems = 4096;
+__global__ __launch_bounds__(kB) void k_scan_parts(const uint64_t* __restrict__ in, int64_t n,
+                                                   uint64_t* __restrict__ parts) {
+  __shared__ unsigned long long s_w[kB / 64];
+  const int64_t i0 = (int64_t)blockIdx.x * kScanItems, i1 = min(n, i0 + kScanItems);
+  unsigned long long v = 0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += kB) v += in[i];
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int k = 0; k < kB / 64; ++k) t += s_w[k];
+    parts[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_scan_apply(const uint64_t* __restrict__ in, int64_t n,
+                                                   const uint64_t* __restrict__ parts,
+                                                   uint64_t* __restrict__ out) {
+  __shared__ unsigned long long s_w[kB / 64];
+  __shared__ unsigned long long s_base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long pre = 0;
+  for (int k = threadIdx.x; k < (int)blockIdx.x; k += kB) pre += parts[k];
+  for (int d = 32; d > 0; d >>= 1) pre += __shfl_xor(pre, d);
+  if (lane == 0) s_w[wv] = pre;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int k = 0; k < kB / 64; ++k) t += s_w[k];
+    s_base = t;
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kScanItems, i1 = min(n, i0 + kScanItems);
+  constexpr int per = kScanItems / kB;
+  const int64_t a = min(i1, i0 + (int64_t)per * threadIdx.x), b = min(i1, a + per);
+  unsigned long long mine = 0;
+  for (int64_t i = a; i < b; ++i) mine += in[i];
+  unsigned long long inc = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  __syncthreads();
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  unsigned long long run = s_base + inc - mine;
+  for (int k = 0; k < wv; ++k) run += s_w[k];
+  for (int64_t i = a; i < b; ++i) {
+    out[i] = run;
+    run += in[i];
+  }
+  if (b == n && a < b) out[n] = run;
+  if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
 }
 
 __global__ void k_reply_bytes(const uint64_t* __restrict__ lk_off,
@@ -393,76 +547,15 @@ void route_gets(const Digest* keys, int64_t n, const uint64_t* replica_size,
   RT_OK(hipGetLastError());
 }
 
-void plan_sets(const Digest* keys, const uint32_t* vlen, const uint32_t* flags,
-               const uint32_t* expire, const uint64_t* val_off, int64_t ns, uint64_t values_base,
-               const uint32_t* ring_pts, const int32_t* ring_owner, int32_t npts,
-               const Digest* hot, int64_t nhot, int32_t w, bool fanout, int32_t* dest_ws,
-               int32_t* owner_ws, uint64_t* ws, int64_t* srec, uint64_t* sval, uint64_t* spad,
-               int64_t* counts, hipStream_t s) {
-  const int64_t m = fanout ? ns * w : ns;
-  if (m <= 0) {
-    RT_OK(hipMemsetAsync(counts, 0, (w + 1) * sizeof(int64_t), s));
-    return;
-  }
-  hipLaunchKernelGGL(k_ps_dest, dim3(grid1(ns)), dim3(kB), 0, s, keys, ns, ring_pts, ring_owner,
-                     npts, hot, nhot, w, fanout, dest_ws, owner_ws);
-  int G;
-  int64_t plen;
-  hist_and_scan(dest_ws, m, w + 1, ws, counts, &G, &plen, s);
-  hipLaunchKernelGGL(k_ps_scatter, dim3(G), dim3(kB), (w + 1) * sizeof(uint32_t), s, dest_ws, m,
-                     w + 1, plen, ws, keys, vlen, flags, expire, val_off, values_base, owner_ws, w,
-                     fanout, srec, sval, spad);
+// Exclusive scan with out[n] = total; parts needs ceil(n / kScanItems) words.
+void scan_u64(const uint64_t* in, int64_t n, uint64_t* parts, uint64_t* out, hipStream_t s) {
+  const int g = (int)std::max<int64_t>(1, (n + kScanItems - 1) / kScanItems);
+  hipLaunchKernelGGL(k_scan_parts, dim3(g), dim3(kB), 0, s, in, n, parts);
+  hipLaunchKernelGGL(k_scan_apply, dim3(g), dim3(kB), 0, s, in, n, parts, out);
   RT_OK(hipGetLastError());
 }
 
-void plan_table(const int64_t* cnt_g, const int64_t* cnt_s, const uint64_t* vscan, int32_t w,
-                int64_t* table, hipStream_t s) {
-  hipLaunchKernelGGL(k_plan_table, dim3(1), dim3(64), 0, s, cnt_g, cnt_s, vscan, w, table);
-  RT_OK(hipGetLastError());
-}
-
-void send_segments(const int64_t* cnt_g, const int64_t* cnt_s, const uint64_t* spad,
-                   const uint64_t* sval, uint64_t gk_base, uint64_t srec_base, int32_t w,
-                   int64_t ns, uint64_t* seg_len, uint64_t* seg_src, hipStream_t s) {
-  hipLaunchKernelGGL(k_send_segs, dim3(grid1(ns + w)), dim3(kB), 2 * (w + 1) * sizeof(int64_t), s,
-                     cnt_g, cnt_s, spad, sval, gk_base, srec_base, w, ns, seg_len, seg_src);
-  RT_OK(hipGetLastError());
-}
-
-void recv_segments(const int64_t* rtable, uint64_t recv_base, int32_t w, uint64_t* seg_len,
-                   uint64_t* seg_src, hipStream_t s) {
-  hipLaunchKernelGGL(k_recv_segs, dim3(1), dim3(64), 0, s, rtable, recv_base, w, seg_len, seg_src);
-  RT_OK(hipGetLastError());
-}
-
-void recv_sets(const int64_t* rrec, int64_t ms, const int64_t* rtable, int32_t w,
-               uint64_t* rpad_ws, uint64_t* rscan_ws, void* scan_tmp, size_t scan_tmp_bytes,
-               Digest* keys, uint32_t* vlen0, uint32_t* vlen1, uint32_t* flags, uint32_t* expire,
-               uint64_t* roff, hipStream_t s) {
-  if (ms <= 0) return;
-  hipLaunchKernelGGL(k_rs_pad, dim3(grid1(ms + 1)), dim3(kB), 0, s, rrec, ms, rpad_ws);
-  device_exclusive_scan(rpad_ws, rscan_ws, ms, scan_tmp, scan_tmp_bytes, s);
-  hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w + 1) * sizeof(int64_t), s, rrec,
-                     ms, rtable, w, rscan_ws, keys, vlen0, vlen1, flags, expire, roff);
-  RT_OK(hipGetLastError());
-}
-
-void reply_bytes(const uint64_t* lk_off, const int64_t* rtable, const uint64_t* gscan,
-                 const int64_t* table, int32_t w, int64_t* bytes, hipStream_t s) {
-  hipLaunchKernelGGL(k_reply_bytes, dim3(1), dim3(64), 0, s, lk_off, rtable, gscan, table, w,
-                     bytes);
-  RT_OK(hipGetLastError());
-}
-
-void assemble_response(const int64_t* perm_g, int64_t n, int64_t n_remote,
-                       const uint64_t* sizes_back, const uint64_t* gscan,
-                       const uint64_t* rl_size, const uint64_t* rl_off, uint64_t local_bytes,
-                       uint64_t* size, uint64_t* off, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_assemble, dim3(grid1(n)), dim3(kB), 0, s, perm_g, n, n_remote, sizes_back,
-                     gscan, rl_size, rl_off, local_bytes, size, off);
-  RT_OK(hipGetLastError());
-}
+int64_t scan_parts_words(int64_t n) { return (n + kScanItems - 1) / kScanItems + 1; }
 
 }  // namespace shellac
 
@@ -473,10 +566,9 @@ namespace shellac {
 
 namespace {
 enum Slot {
-  kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kDestS, kOwnerS, kSrec, kSval,
-  kSpad, kCntS, kWsS, kVscan, kExtras, kSegLen, kSegSrc, kSegOff, kBody, kRSegLen, kRSegSrc,
-  kRSegOff, kLkLoc, kLkOff, kGin, kGscan, kNbytes, kRpad, kRscan, kRkeys, kV0, kV1, kFl, kEx,
-  kRoff, kScanTmp, kNumSlots
+  kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kDestS, kOwnerS, kVpad, kTcnt,
+  kTbytes, kSrec, kSval, kSvoff, kCntS, kExtras, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
+  kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
 };
 }  // namespace
 
@@ -522,14 +614,6 @@ T* RoutedStep::buf(int slot, size_t count) {
   return static_cast<T*>(b.p);
 }
 
-uint64_t* RoutedStep::scan(uint64_t* in, uint64_t* out, int64_t n, hipStream_t s) {
-  RT_OK(hipMemsetAsync(in + n, 0, sizeof(uint64_t), s));
-  const size_t tb = device_scan_tmp_bytes(std::max<int64_t>(n, 1));
-  uint8_t* tmp = buf<uint8_t>(kScanTmp, tb);
-  device_exclusive_scan(in, out, n, tmp, bufs_[kScanTmp].cap, s);
-  return out;
-}
-
 void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
                       const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
                       const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues,
@@ -547,6 +631,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
     rl_off_ = buf<uint64_t>(kRlOff, n + 1);
     replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
   }
+  // GET rows: owner (or bucket W = local replica hit), counting sort by owner
   int32_t* dest_g = buf<int32_t>(kDestG, n);
   route_gets(keys, n, rl_size, pts_, own_, npts_, W, dest_g, s);
   gk_ = buf<Digest>(kGk, n);
@@ -554,24 +639,35 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   cnt_g_ = buf<int64_t>(kCntG, W + 1);
   group_rows(dest_g, n, W + 1, keys, 16, gk_, perm_g_, cnt_g_,
              buf<uint64_t>(kWsG, group_ws_words(std::max<int64_t>(n, 1), W + 1)), s);
+  // SET rows: owner + hot fan-out, counting sort by destination with value-byte ranges
   m_ = fanout ? ns * W : ns;
+  const int nb = W + 1;
+  const int G = group_grid(std::max<int64_t>(m_, 1));
+  const int64_t plen = (std::max<int64_t>(m_, 1) + G - 1) / G;
+  int32_t* dest_s = buf<int32_t>(kDestS, m_);
+  int32_t* owner_s = buf<int32_t>(kOwnerS, ns);
+  uint32_t* vpad = buf<uint32_t>(kVpad, ns);
+  uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * G);
+  uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * G);
   srec_ = buf<int64_t>(kSrec, 4 * (size_t)m_);
   sval_ = buf<uint64_t>(kSval, m_);
-  spad_ = buf<uint64_t>(kSpad, m_ + 1);
-  cnt_s_ = buf<int64_t>(kCntS, W + 1);
-  plan_sets(skeys, svlen, sflags, sexpire, sval_off, ns, (uint64_t)(uintptr_t)svalues, pts_, own_,
-            npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0, W, fanout,
-            buf<int32_t>(kDestS, m_), buf<int32_t>(kOwnerS, ns),
-            buf<uint64_t>(kWsS, group_ws_words(std::max<int64_t>(m_, 1), W + 1)), srec_, sval_,
-            spad_, cnt_s_, s);
-  uint64_t* vscan = scan(spad_, buf<uint64_t>(kVscan, m_ + 1), m_, s);
-  plan_table(cnt_g_, cnt_s_, vscan, W, table, s);
+  svoff_ = buf<uint64_t>(kSvoff, m_);
+  cnt_s_ = buf<int64_t>(kCntS, nb);
   int64_t* extras = buf<int64_t>(kExtras, 2);
-  RT_OK(hipMemcpyAsync(extras, cnt_g_ + W, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-  if (replica)
-    RT_OK(hipMemcpyAsync(extras + 1, rl_off_ + n, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-  else
-    RT_OK(hipMemsetAsync(extras + 1, 0, sizeof(int64_t), s));
+  if (ns > 0)
+    hipLaunchKernelGGL(k_ps_dest, dim3(grid1(ns)), dim3(kB), 0, s, skeys, svlen, ns, pts_, own_,
+                       npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0, W, fanout, dest_s,
+                       owner_s, vpad);
+  hipLaunchKernelGGL(k_ps_hist, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, dest_s, m_,
+                     nb, plen, W, fanout, vpad, tcnt, tbytes);
+  hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, s, tcnt, tbytes, nb, G, cnt_g_,
+                     replica ? rl_off_ + n : nullptr, cnt_s_, table, extras);
+  if (m_ > 0)
+    hipLaunchKernelGGL(k_ps_scatter, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, dest_s,
+                       m_, nb, plen, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
+                       (uint64_t)(uintptr_t)svalues, owner_s, vpad, W, fanout, srec_, sval_,
+                       svoff_);
+  RT_OK(hipGetLastError());
 }
 
 std::vector<int64_t> RoutedStep::read_counts(const int64_t* rtable, hipStream_t s) {
@@ -591,29 +687,35 @@ std::vector<int64_t> RoutedStep::read_counts(const int64_t* rtable, hipStream_t 
     ns_ += out[3 * p + 1];
     mg_ += out[3 * W + 3 * p];
     ms_ += out[3 * W + 3 * p + 1];
+    // value offsets travel as 31-bit fields in the SET records
+    SH_CHECK(out[3 * p + 2] < (1ll << 31) && out[3 * W + 3 * p + 2] < (1ll << 31),
+             "SET values for one peer exceed 2 GiB per step; split the batch");
   }
   return out;
 }
 
 void RoutedStep::pack(uint8_t* send, hipStream_t s) {
-  const int64_t nseg = 2 * (int64_t)w_ + ns_;
-  uint64_t* seg_len = buf<uint64_t>(kSegLen, nseg + 1);
+  const int W = w_;
+  const int64_t nseg = 2 * (int64_t)W + ns_;
+  uint64_t* seg_off = buf<uint64_t>(kSegOff, nseg + 1);
   uint64_t* seg_src = buf<uint64_t>(kSegSrc, nseg);
-  send_segments(cnt_g_, cnt_s_, spad_, sval_, (uint64_t)(uintptr_t)gk_,
-                (uint64_t)(uintptr_t)srec_, w_, ns_, seg_len, seg_src, s);
-  uint64_t* seg_off = scan(seg_len, buf<uint64_t>(kSegOff, nseg + 1), nseg, s);
+  hipLaunchKernelGGL(k_send_segs, dim3(grid1(ns_ + W + 1)), dim3(kB), 4 * (W + 1) * sizeof(int64_t),
+                     s, table_, svoff_, sval_, (uint64_t)(uintptr_t)gk_,
+                     (uint64_t)(uintptr_t)srec_, W, ns_, seg_off, seg_src);
+  RT_OK(hipGetLastError());
   segcopy(nullptr, seg_src, seg_off, nseg, send, s);
 }
 
 void RoutedStep::owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint64_t* sizes_out,
                        hipStream_t s) {
-  const int64_t W2 = 2 * (int64_t)w_;
+  const int W = w_;
   uint8_t* body = buf<uint8_t>(kBody, 16 * mg_ + 32 * ms_ + 16);
-  uint64_t* rlen = buf<uint64_t>(kRSegLen, W2 + 1);
-  uint64_t* rsrc = buf<uint64_t>(kRSegSrc, W2);
-  recv_segments(rtable_, (uint64_t)(uintptr_t)recv, w_, rlen, rsrc, s);
-  uint64_t* roff = scan(rlen, buf<uint64_t>(kRSegOff, W2 + 1), W2, s);
-  segcopy(nullptr, rsrc, roff, W2, body, s);
+  uint64_t* roff = buf<uint64_t>(kRSegOff, 2 * W + 1);
+  uint64_t* rsrc = buf<uint64_t>(kRSegSrc, 2 * W);
+  hipLaunchKernelGGL(k_recv_segs, dim3(1), dim3(64), 0, s, rtable_, (uint64_t)(uintptr_t)recv, W,
+                     roff, rsrc);
+  RT_OK(hipGetLastError());
+  segcopy(nullptr, rsrc, roff, 2 * W, body, s);
   rrec_ = reinterpret_cast<const int64_t*>(body + 16 * mg_);
   lk_loc_ = buf<uint64_t>(kLkLoc, mg_);
   lk_off_ = buf<uint64_t>(kLkOff, mg_ + 1);
@@ -623,12 +725,12 @@ void RoutedStep::owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint6
 std::vector<int64_t> RoutedStep::reply_sizes(const uint64_t* sizes_in, hipStream_t s) {
   const int W = w_;
   sizes_in_ = sizes_in;
-  uint64_t* gin = buf<uint64_t>(kGin, n_remote_ + 1);
-  if (n_remote_ > 0)
-    RT_OK(hipMemcpyAsync(gin, sizes_in, n_remote_ * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-  gscan_ = scan(gin, buf<uint64_t>(kGscan, n_remote_ + 1), n_remote_, s);
+  gscan_ = buf<uint64_t>(kGscan, n_remote_ + 1);
+  scan_u64(sizes_in, n_remote_, buf<uint64_t>(kParts, scan_parts_words(n_remote_)), gscan_, s);
   int64_t* nb = buf<int64_t>(kNbytes, 2 * W);
-  reply_bytes(lk_off_, rtable_, gscan_, table_, W, nb, s);
+  hipLaunchKernelGGL(k_reply_bytes, dim3(1), dim3(64), 0, s, lk_off_, rtable_, gscan_, table_, W,
+                     nb);
+  RT_OK(hipGetLastError());
   RT_OK(hipMemcpyAsync(host_ + 6 * W + 2, nb, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   RT_OK(hipStreamSynchronize(s));
   return std::vector<int64_t>(host_ + 6 * W + 2, host_ + 8 * W + 2);
@@ -644,23 +746,24 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
   if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
   if (ms_ > 0) {
     const int64_t ms = ms_;
-    uint64_t* rpad = buf<uint64_t>(kRpad, ms + 1);
-    uint64_t* rscan = buf<uint64_t>(kRscan, ms + 1);
     Digest* rkeys = buf<Digest>(kRkeys, ms);
     uint32_t* v0 = buf<uint32_t>(kV0, ms);
     uint32_t* v1 = buf<uint32_t>(kV1, ms);
     uint32_t* fl = buf<uint32_t>(kFl, ms);
     uint32_t* ex = buf<uint32_t>(kEx, ms);
     uint64_t* roff = buf<uint64_t>(kRoff, ms);
-    uint8_t* tmp = buf<uint8_t>(kScanTmp, device_scan_tmp_bytes(ms));
-    recv_sets(rrec_, ms, rtable_, w_, rpad, rscan, tmp, bufs_[kScanTmp].cap, rkeys, v0, v1, fl, ex,
-              roff, s);
+    hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t), s,
+                       rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
+    RT_OK(hipGetLastError());
     const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
     shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, s);
     if (replica) replica->store(rkeys, recv, roff, v1, fl, ex, ms, bound, now, s);
   }
-  assemble_response(perm_g_, n_, n_remote_, sizes_in_, gscan_, have_replica_ ? rl_size_ : nullptr,
-                    have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off, s);
+  if (n_ > 0)
+    hipLaunchKernelGGL(k_assemble, dim3(grid1(n_)), dim3(kB), 0, s, perm_g_, n_, n_remote_,
+                       sizes_in_, gscan_, have_replica_ ? rl_size_ : nullptr,
+                       have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off);
+  RT_OK(hipGetLastError());
 }
 
 }  // namespace shellac
