@@ -52,10 +52,10 @@ def parse():
     ap.add_argument("--log-gb", type=float, default=16.0, help="value-log GiB per shard")
     ap.add_argument("--set-dist", choices=["uniform", "zipf"], default="uniform",
                     help="SET popularity: uniform (TTL refresh fills, default) or zipf")
-    ap.add_argument("--replicate", type=int, default=1 << 20,
+    ap.add_argument("--replicate", type=int, default=2 << 20,
                     help="hot objects replicated on every rank (N>1; 0 = off)")
-    ap.add_argument("--replica-gb", type=float, default=2.0)
-    ap.add_argument("--sample-batches", type=int, default=8,
+    ap.add_argument("--replica-gb", type=float, default=4.0)
+    ap.add_argument("--sample-batches", type=int, default=32,
                     help="GET batches (independent of the timed ones) observed to pick the "
                          "replicated hot set")
     ap.add_argument("--simulate-world", type=int, default=0,

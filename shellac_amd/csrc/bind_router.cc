@@ -35,9 +35,9 @@ void bind_router(py::module_& m) {
       .def("set_ring", [](RoutedStep& r, uintptr_t pts, uintptr_t owner, int32_t npts) {
         r.set_ring(P<const uint32_t>(pts), P<const int32_t>(owner), npts);
       })
-      .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot) {
-        r.set_hot(P<const Digest>(hot), nhot);
-      })
+      .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot, uintptr_t dir) {
+        r.set_hot(P<const Digest>(hot), nhot, P<const int64_t>(dir));
+      }, py::arg("hot"), py::arg("nhot"), py::arg("dir") = 0)
       .def("plan", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
                       uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,

@@ -60,7 +60,8 @@ class RoutedStep {
   RoutedStep& operator=(const RoutedStep&) = delete;
 
   void set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts);
-  void set_hot(const Digest* hot, int64_t nhot);
+  // Sorted hot set (by signed lo) + optional 65537-entry directory (see is_hot).
+  void set_hot(const Digest* hot, int64_t nhot, const int64_t* dir = nullptr);
 
   // GET routing (replica probe first when `replica`), SET routing + hot fan-out,
   // per-peer table[w][3] = {GET rows, SET rows, SET value bytes} into `table`.
@@ -102,6 +103,7 @@ class RoutedStep {
   int32_t npts_ = 0;
   const Digest* hot_ = nullptr;
   int64_t nhot_ = 0;
+  const int64_t* hot_dir_ = nullptr;
   std::vector<Buf> bufs_;
   int64_t* host_ = nullptr;  // pinned
   // per-step state

@@ -42,10 +42,17 @@ __device__ __forceinline__ int ring_owner_of(const Digest& k, const uint32_t* __
 }
 
 // Membership in the hot set, sorted by the signed low word (torch's sort of column 0).
+// `dir` (optional, 65537 entries) narrows the search to the keys sharing the top 16
+// bits of the order-preserving unsigned image of lo, ~nhot/65536 of them.
 __device__ __forceinline__ bool is_hot(const Digest& k, const Digest* __restrict__ hot,
-                                       int64_t nhot) {
+                                       int64_t nhot, const int64_t* __restrict__ dir) {
   const int64_t x = (int64_t)k.lo;
   int64_t lo = 0, hi = nhot;
+  if (dir) {
+    const uint32_t b = (uint32_t)((k.lo ^ (1ull << 63)) >> 48);
+    lo = dir[b];
+    hi = dir[b + 1];
+  }
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if ((int64_t)hot[mid].lo < x) lo = mid + 1; else hi = mid;
@@ -161,6 +168,7 @@ __global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
                                                 const uint32_t* __restrict__ pts,
                                                 const int32_t* __restrict__ own, int npts,
                                                 const Digest* __restrict__ hot, int64_t nhot,
+                                                const int64_t* __restrict__ hot_dir,
                                                 int32_t w, bool fanout,
                                                 int32_t* __restrict__ dest,
                                                 int32_t* __restrict__ owner,
@@ -175,7 +183,7 @@ __global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
       dest[j] = o;
       continue;
     }
-    const bool h = nhot > 0 && is_hot(k, hot, nhot);
+    const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
     for (int r = 0; r < w; ++r) dest[j * w + r] = (r == o || h) ? r : w;
   }
 }
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(kB) void k_ps_scatter(
     const unsigned long long old = atomicAdd(&s_cb[d], 1ull | (pad << 32));
     const int64_t pos = (int64_t)tcnt[(int64_t)d * G + blockIdx.x] + (int64_t)(old & 0xFFFFFFFFull);
     const uint64_t vglob = tbytes[(int64_t)d * G + blockIdx.x] + (old >> 32);
+    if (d == w) continue;  // goes nowhere: never read
     const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
     const int r = fanout ? (int)(v - j * w) : owner[j];
     const uint64_t tier = (fanout && r != owner[j]) ? 1ull : 0ull;
@@ -592,9 +601,10 @@ void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npt
   npts_ = npts;
 }
 
-void RoutedStep::set_hot(const Digest* hot, int64_t nhot) {
+void RoutedStep::set_hot(const Digest* hot, int64_t nhot, const int64_t* dir) {
   hot_ = hot;
   nhot_ = hot ? nhot : 0;
+  hot_dir_ = hot ? dir : nullptr;
 }
 
 template <typename T>
@@ -656,8 +666,8 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   int64_t* extras = buf<int64_t>(kExtras, 2);
   if (ns > 0)
     hipLaunchKernelGGL(k_ps_dest, dim3(grid1(ns)), dim3(kB), 0, s, skeys, svlen, ns, pts_, own_,
-                       npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0, W, fanout, dest_s,
-                       owner_s, vpad);
+                       npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0,
+                       fanout ? hot_dir_ : nullptr, W, fanout, dest_s, owner_s, vpad);
   hipLaunchKernelGGL(k_ps_hist, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, dest_s, m_,
                      nb, plen, W, fanout, vpad, tcnt, tbytes);
   hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, s, tcnt, tbytes, nb, G, cnt_g_,

@@ -84,6 +84,18 @@ def records_to_set_batch(keys: torch.Tensor, res: GetResult) -> SetBatch:
                     vlen=vlen.contiguous(), flags=flags.contiguous(), expire=expire.contiguous())
 
 
+def _hot_directory(hot: torch.Tensor) -> torch.Tensor:
+    """dir[b] = first row of ``hot`` (sorted by signed lo) whose order-preserving unsigned
+    image of lo has top-16 bits >= b; b in [0, 65536]. Lets the device membership test
+    binary-search ~len(hot)/65536 rows instead of all of them."""
+    b = torch.arange(65537, dtype=torch.int64, device=hot.device)
+    bounds = (b - 32768) << 48            # signed value whose unsigned image is b << 48
+    bounds[-1] = torch.iinfo(torch.int64).max
+    d = torch.searchsorted(hot[:, 0].contiguous(), bounds, side="left")
+    d[-1] = hot.shape[0]
+    return d.contiguous()
+
+
 class _Phases:
     """Consecutive ROCTX ranges for the phases of one serving step (no-op when
     tracing is off; see shellac_amd.utils.trace)."""
@@ -128,6 +140,7 @@ class ShardedCache:
         self.fused = True
         self._engine = None
         self._xtable = None
+        self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -268,7 +281,10 @@ class ShardedCache:
             self._xtable = torch.empty((2, w, 3), dtype=i64, device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
-        e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0)
+        if fanout and self._hot_dir is None:
+            self._hot_dir = _hot_directory(self._hot)
+        e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0,
+                  self._hot_dir.data_ptr() if fanout else 0)
         rep = self.replica._impl if self.replica is not None else None
         table, rtable = self._xtable[0], self._xtable[1]
         ph = _Phases("serve.")
@@ -651,6 +667,7 @@ class ShardedCache:
             return 0
         order = torch.argsort(hot[:, 0])
         self._hot = hot.index_select(0, order).contiguous()
+        self._hot_dir = None
         saved = self.replica
         self.replica = None                               # fetch through the owners only
         try:
@@ -663,7 +680,18 @@ class ShardedCache:
         # non-owner replicas), so owned keys stay out of the local replica
         owner, _ = self._route(hot)
         sb.vlen = torch.where(owner == self.rank, torch.full_like(sb.vlen, SKIP_VLEN), sb.vlen)
-        self.replica.store(sb.keys, sb.values, sb.val_off, sb.vlen, sb.flags, sb.expire, now)
+        # store in chunks with exact byte bounds (the records buffer can be GBs)
+        k = hot.shape[0]
+        chunk = 1 << 17
+        cuts = list(range(0, k, chunk)) + [k]
+        # records of a chunk are scattered in the response buffer: bound by their sizes
+        sizes = torch.stack([res.size[cuts[i]:cuts[i + 1]].sum()
+                             for i in range(len(cuts) - 1)]).tolist()
+        for i in range(len(cuts) - 1):
+            a, b = cuts[i], cuts[i + 1]
+            self.replica.store(sb.keys[a:b], sb.values, sb.val_off[a:b], sb.vlen[a:b],
+                               sb.flags[a:b], sb.expire[a:b], now,
+                               bytes_bound=int(sizes[i]) + 48 * (b - a))
         self.stats["replica_refreshes"] += 1
         return int((sb.vlen != SKIP_VLEN).sum())
 

@@ -229,7 +229,10 @@ class CacheShard:
 
     def store(self, keys: torch.Tensor, values: torch.Tensor, val_off: torch.Tensor,
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
-              expire: Optional[torch.Tensor] = None, now: Optional[int] = None) -> None:
+              expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
+              bytes_bound: Optional[int] = None) -> None:
+        """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
+        batch appends; the default assumes every byte of ``values`` is stored."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -241,7 +244,7 @@ class CacheShard:
         fp = 0 if flags is None else flags.data_ptr()
         ep = 0 if expire is None else expire.data_ptr()
         if self.is_gpu:
-            bound = self.set_bound(n, values.numel())
+            bound = self.set_bound(n, values.numel()) if bytes_bound is None else int(bytes_bound)
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s())
         else:
