@@ -107,7 +107,7 @@ class RoutedStep {
   std::vector<Buf> bufs_;
   int64_t* host_ = nullptr;  // pinned
   // per-step state
-  int64_t n_ = 0, m_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
+  int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
   uint64_t local_bytes_ = 0;
   bool have_replica_ = false;
   const uint8_t* values_ = nullptr;

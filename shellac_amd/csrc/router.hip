@@ -23,8 +23,8 @@ constexpr int kB = 256;
 constexpr int64_t kGroupRows = 2048;  // rows per workgroup in the counting sort
 constexpr int kMaxBuckets = 4097;
 
-int group_grid(int64_t n) {
-  int64_t g = (n + kGroupRows - 1) / kGroupRows;
+int group_grid(int64_t n, int64_t rows_per_group = kGroupRows) {
+  int64_t g = (n + rows_per_group - 1) / rows_per_group;
   return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 1024);
 }
 
@@ -162,48 +162,46 @@ __global__ __launch_bounds__(kB) void k_route_gets(const Digest* __restrict__ ke
     dest[i] = (rsize && rsize[i] > 0) ? w : ring_owner_of(keys[i], pts, own, npts);
 }
 
-// SET planning. Input row j becomes virtual row v = j * w + r (fan-out) or v = j.
+// SET planning. Input row j goes to its owner, and (fan-out) to every rank when its
+// key is hot: tier 0 = owner copy, tier 1 = replica copy.
 __global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
                                                 const uint32_t* __restrict__ vlen, int64_t ns,
                                                 const uint32_t* __restrict__ pts,
                                                 const int32_t* __restrict__ own, int npts,
                                                 const Digest* __restrict__ hot, int64_t nhot,
                                                 const int64_t* __restrict__ hot_dir,
-                                                int32_t w, bool fanout,
-                                                int32_t* __restrict__ dest,
                                                 int32_t* __restrict__ owner,
                                                 uint32_t* __restrict__ vpad) {
   for (int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x; j < ns; j += (int64_t)gridDim.x * kB) {
     const Digest k = keys[j];
     const int o = ring_owner_of(k, pts, own, npts);
-    owner[j] = o;
+    const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
+    owner[j] = h ? (o | (1 << 30)) : o;  // bit 30: fan out to every rank
     const uint32_t vl = vlen[j];
     vpad[j] = vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
-    if (!fanout) {
-      dest[j] = o;
-      continue;
-    }
-    const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
-    for (int r = 0; r < w; ++r) dest[j * w + r] = (r == o || h) ? r : w;
   }
 }
 
-// Rows AND value bytes per (bucket, workgroup): one packed 64-bit LDS counter
+// Rows AND value bytes per (destination, workgroup): one packed 64-bit LDS counter
 // (rows | bytes << 32) so the scatter below can hand out row slots and byte ranges in
 // the same order.
-__global__ __launch_bounds__(kB) void k_ps_hist(const int32_t* __restrict__ dest, int64_t m,
-                                                int32_t nb, int64_t plen, int32_t w, bool fanout,
+__global__ __launch_bounds__(kB) void k_ps_hist(const int32_t* __restrict__ owner, int64_t ns,
+                                                int32_t nb, int64_t plen, int32_t w,
                                                 const uint32_t* __restrict__ vpad,
                                                 uint64_t* __restrict__ tcnt,
                                                 uint64_t* __restrict__ tbytes) {
   extern __shared__ unsigned long long s_cb[];
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(m, i0 + plen);
-  for (int64_t v = i0 + threadIdx.x; v < i1; v += kB) {
-    const int d = dest[v];
-    const uint64_t pad = d < w ? vpad[fanout ? v / w : v] : 0;
-    atomicAdd(&s_cb[d], 1ull | (pad << 32));
+  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
+  for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
+    const int o = owner[j];
+    const unsigned long long inc = 1ull | ((unsigned long long)vpad[j] << 32);
+    if (o >> 30) {
+      for (int r = 0; r < w; ++r) atomicAdd(&s_cb[r], inc);
+    } else {
+      atomicAdd(&s_cb[o], inc);
+    }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < nb; d += kB) {
@@ -286,37 +284,42 @@ __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
 // rec = {lo, hi, vlen | flags << 32, expire | (voff | tier << 31) << 32} where voff is
 // the value's offset inside the destination peer's value block.
 __global__ __launch_bounds__(kB) void k_ps_scatter(
-    const int32_t* __restrict__ dest, int64_t m, int32_t nb, int64_t plen,
-    const uint64_t* __restrict__ tcnt, const uint64_t* __restrict__ tbytes,
-    const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
-    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
-    const uint64_t* __restrict__ val_off, uint64_t values_base, const int32_t* __restrict__ owner,
-    const uint32_t* __restrict__ vpad, int32_t w, bool fanout, int64_t* __restrict__ srec,
-    uint64_t* __restrict__ sval, uint64_t* __restrict__ svoff) {
+    int64_t ns, int32_t nb, int64_t plen, const uint64_t* __restrict__ tcnt,
+    const uint64_t* __restrict__ tbytes, const Digest* __restrict__ keys,
+    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ expire, const uint64_t* __restrict__ val_off,
+    uint64_t values_base, const int32_t* __restrict__ owner, const uint32_t* __restrict__ vpad,
+    int32_t w, int64_t* __restrict__ srec, uint64_t* __restrict__ sval,
+    uint64_t* __restrict__ svoff) {
   extern __shared__ unsigned long long s_cb[];
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   __syncthreads();
   const int G = gridDim.x;
-  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(m, i0 + plen);
-  for (int64_t v = i0 + threadIdx.x; v < i1; v += kB) {
-    const int d = dest[v];
-    const int64_t j = fanout ? v / w : v;
-    const uint64_t pad = d < w ? vpad[j] : 0;
-    const unsigned long long old = atomicAdd(&s_cb[d], 1ull | (pad << 32));
-    const int64_t pos = (int64_t)tcnt[(int64_t)d * G + blockIdx.x] + (int64_t)(old & 0xFFFFFFFFull);
-    const uint64_t vglob = tbytes[(int64_t)d * G + blockIdx.x] + (old >> 32);
-    if (d == w) continue;  // goes nowhere: never read
-    const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
-    const int r = fanout ? (int)(v - j * w) : owner[j];
-    const uint64_t tier = (fanout && r != owner[j]) ? 1ull : 0ull;
+  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
+  for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
+    const int ow = owner[j];
+    const bool fan = (ow >> 30) != 0;
+    const int o = ow & ((1 << 30) - 1);
+    const uint64_t pad = vpad[j];
     const Digest k = keys[j];
-    int64_t* rec = srec + pos * 4;
-    rec[0] = (int64_t)k.lo;
-    rec[1] = (int64_t)k.hi;
-    rec[2] = (int64_t)((uint64_t)vlen[j] | ((uint64_t)(flags ? flags[j] : 0u) << 32));
-    rec[3] = (int64_t)((uint64_t)(expire ? expire[j] : 0u) | ((voff | (tier << 31)) << 32));
-    sval[pos] = values_base + val_off[j];
-    svoff[pos] = vglob;
+    const uint64_t r2 = (uint64_t)vlen[j] | ((uint64_t)(flags ? flags[j] : 0u) << 32);
+    const uint64_t ex = expire ? expire[j] : 0u;
+    const uint64_t src = values_base + val_off[j];
+    const int r0 = fan ? 0 : o, r1 = fan ? w : o + 1;
+    for (int d = r0; d < r1; ++d) {
+      const unsigned long long old = atomicAdd(&s_cb[d], 1ull | (pad << 32));
+      const int64_t pos = (int64_t)tcnt[(int64_t)d * G + blockIdx.x] + (int64_t)(old & 0xFFFFFFFFull);
+      const uint64_t vglob = tbytes[(int64_t)d * G + blockIdx.x] + (old >> 32);
+      const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
+      const uint64_t tier = d != o ? 1ull : 0ull;
+      int64_t* rec = srec + pos * 4;
+      rec[0] = (int64_t)k.lo;
+      rec[1] = (int64_t)k.hi;
+      rec[2] = (int64_t)r2;
+      rec[3] = (int64_t)(ex | ((voff | (tier << 31)) << 32));
+      sval[pos] = src;
+      svoff[pos] = vglob;
+    }
   }
 }
 
@@ -575,7 +578,7 @@ namespace shellac {
 
 namespace {
 enum Slot {
-  kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kDestS, kOwnerS, kVpad, kTcnt,
+  kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kOwnerS, kVpad, kTcnt,
   kTbytes, kSrec, kSval, kSvoff, kCntS, kExtras, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
   kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
 };
@@ -650,33 +653,32 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   group_rows(dest_g, n, W + 1, keys, 16, gk_, perm_g_, cnt_g_,
              buf<uint64_t>(kWsG, group_ws_words(std::max<int64_t>(n, 1), W + 1)), s);
   // SET rows: owner + hot fan-out, counting sort by destination with value-byte ranges
-  m_ = fanout ? ns * W : ns;
   const int nb = W + 1;
-  const int G = group_grid(std::max<int64_t>(m_, 1));
-  const int64_t plen = (std::max<int64_t>(m_, 1) + G - 1) / G;
-  int32_t* dest_s = buf<int32_t>(kDestS, m_);
+  // SET rows fan out up to W ways: smaller ranges per workgroup than the GET sort
+  const int G = group_grid(std::max<int64_t>(ns, 1), 256);
+  const int64_t plen = (std::max<int64_t>(ns, 1) + G - 1) / G;
+  const int64_t mcap = fanout ? ns * W : ns;  // upper bound of routed SET rows
   int32_t* owner_s = buf<int32_t>(kOwnerS, ns);
   uint32_t* vpad = buf<uint32_t>(kVpad, ns);
   uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * G);
   uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * G);
-  srec_ = buf<int64_t>(kSrec, 4 * (size_t)m_);
-  sval_ = buf<uint64_t>(kSval, m_);
-  svoff_ = buf<uint64_t>(kSvoff, m_);
+  srec_ = buf<int64_t>(kSrec, 4 * (size_t)mcap);
+  sval_ = buf<uint64_t>(kSval, mcap);
+  svoff_ = buf<uint64_t>(kSvoff, mcap);
   cnt_s_ = buf<int64_t>(kCntS, nb);
   int64_t* extras = buf<int64_t>(kExtras, 2);
   if (ns > 0)
     hipLaunchKernelGGL(k_ps_dest, dim3(grid1(ns)), dim3(kB), 0, s, skeys, svlen, ns, pts_, own_,
                        npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0,
-                       fanout ? hot_dir_ : nullptr, W, fanout, dest_s, owner_s, vpad);
-  hipLaunchKernelGGL(k_ps_hist, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, dest_s, m_,
-                     nb, plen, W, fanout, vpad, tcnt, tbytes);
+                       fanout ? hot_dir_ : nullptr, owner_s, vpad);
+  hipLaunchKernelGGL(k_ps_hist, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, owner_s, ns,
+                     nb, plen, W, vpad, tcnt, tbytes);
   hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, s, tcnt, tbytes, nb, G, cnt_g_,
                      replica ? rl_off_ + n : nullptr, cnt_s_, table, extras);
-  if (m_ > 0)
-    hipLaunchKernelGGL(k_ps_scatter, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, dest_s,
-                       m_, nb, plen, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
-                       (uint64_t)(uintptr_t)svalues, owner_s, vpad, W, fanout, srec_, sval_,
-                       svoff_);
+  if (ns > 0)
+    hipLaunchKernelGGL(k_ps_scatter, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, ns, nb,
+                       plen, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
+                       (uint64_t)(uintptr_t)svalues, owner_s, vpad, W, srec_, sval_, svoff_);
   RT_OK(hipGetLastError());
 }
 
