@@ -41,13 +41,14 @@ def main():
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--hbm-gb", type=float, default=4.0)
     ap.add_argument("--l1-mb", type=int, default=0, help="DRAM L1 in front of hbm (0 = off)")
+    ap.add_argument("--batch-us", type=int, default=0, help="HBM batch linger (0 = natural)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
     origin = Origin(body_bytes=a.body).start()
     backend = None if a.backend == "none" else make_backend(
         a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
-                                                                       "batch_us": 20,
+                                                                       "batch_us": a.batch_us,
                                                                        "l1_mb": a.l1_mb}))
     px = Server([("127.0.0.1", origin.port)], port=0, backend=backend, threads=a.threads,
                 client_max_reqs=1 << 30).start()

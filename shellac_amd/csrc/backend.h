@@ -97,7 +97,7 @@ struct HbmBackendConfig {
   uint64_t log_bytes_per_gpu = 8ull << 30;
   uint64_t nbuckets_per_gpu = 1ull << 22;
   uint32_t max_item = 1u << 20;
-  int batch_us = 50;        // max time a request waits for batch-mates
+  int batch_us = 0;         // optional linger for batch-mates (0: natural batching)
   int max_batch = 65536;    // flush early when this many requests are queued
 };
 

@@ -33,7 +33,8 @@ struct HbmBackend::Dev {
   size_t n_cap = 0, out_cap = 0, vals_cap = 0;
   Digest *d_keys = nullptr, *h_keys = nullptr;
   uint64_t *d_loc = nullptr, *d_size = nullptr, *d_off = nullptr, *h_off = nullptr;
-  uint8_t *d_out = nullptr, *h_out = nullptr;
+  uint8_t* h_out = nullptr;
+  uint8_t* h_out_dev = nullptr;  // device view of the pinned h_out (zero-copy gather target)
   uint8_t *d_vals = nullptr, *h_vals = nullptr;
   uint64_t *d_voff = nullptr, *h_voff = nullptr;
   uint32_t *d_meta = nullptr, *h_meta = nullptr;  // [vlen | flags | expire] x n
@@ -66,12 +67,12 @@ struct HbmBackend::Dev {
   }
   void ensure_out(size_t bytes) {
     if (bytes <= out_cap) return;
-    size_t cap = out_cap ? out_cap : (1u << 20);
+    size_t cap = out_cap ? out_cap : (16u << 20);
     while (cap < bytes) cap *= 2;
     HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_out); (void)hipHostFree(h_out);
-    HB_OK(hipMalloc(&d_out, cap));
-    HB_OK(hipHostMalloc(&h_out, cap, hipHostMallocDefault));
+    (void)hipHostFree(h_out);
+    HB_OK(hipHostMalloc(&h_out, cap, hipHostMallocMapped));
+    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_out_dev), h_out, 0));
     out_cap = cap;
   }
   void ensure_vals(size_t bytes) {
@@ -89,7 +90,7 @@ struct HbmBackend::Dev {
     (void)hipStreamSynchronize(stream);
     cache.reset();
     (void)hipFree(d_keys); (void)hipHostFree(h_keys); (void)hipFree(d_loc); (void)hipFree(d_size);
-    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipFree(d_out); (void)hipHostFree(h_out);
+    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipHostFree(h_out);
     (void)hipFree(d_vals); (void)hipHostFree(h_vals); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
     (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
     if (stream) (void)hipStreamDestroy(stream);
@@ -187,10 +188,14 @@ void HbmBackend::loop() {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_; });
       if (stop_ && q_.empty()) return;
-      // give batch-mates up to batch_us to arrive (a lone request pays at most that)
-      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.batch_us);
-      while (!stop_ && (int)q_.size() < cfg_.max_batch &&
-             cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
+      // Natural batching: whatever queued while the previous batch ran goes now. An
+      // optional linger (batch_us > 0) trades latency for bigger batches.
+      if (cfg_.batch_us > 0) {
+        const auto deadline =
+            std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.batch_us);
+        while (!stop_ && (int)q_.size() < cfg_.max_batch &&
+               cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
+        }
       }
       batch.swap(q_);
       do_flush = flush_req_;
@@ -239,19 +244,21 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     const int o = nd == 1 ? 0 : ring_.owner(batch[i].d);
     (batch[i].kind == 0 ? gets : batch[i].kind == 1 ? sets : dels)[o].push_back(i);
   }
-  // ---- GET phase 1: H2D keys, probe + scan, D2H offsets (all devices in flight)
+  // ---- GET: H2D keys, probe + scan, gather straight into pinned host memory (skipped
+  // by the kernel if the batch does not fit), D2H offsets; one sync per device
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
     const size_t n = gets[k].size();
     if (!n) continue;
     dv.set_device();
     dv.ensure_n(std::max(n, std::max(sets[k].size(), dels[k].size())));
+    dv.ensure_out(1);
     for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[gets[k][j]].d;
     HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
     dv.cache->lookup(dv.d_keys, (int64_t)n, dv.d_loc, dv.d_size, dv.d_off, tnow, dv.stream);
+    dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
     HB_OK(hipMemcpyAsync(dv.h_off, dv.d_off, (n + 1) * 8, hipMemcpyDeviceToHost, dv.stream));
   }
-  // ---- GET phase 2: gather + D2H values
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
     const size_t n = gets[k].size();
@@ -259,10 +266,10 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     dv.set_device();
     HB_OK(hipStreamSynchronize(dv.stream));
     const uint64_t total = dv.h_off[n];
-    if (total) {
+    if (total > dv.out_cap) {  // rare: grow the zero-copy buffer and gather again
       dv.ensure_out(total);
-      dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.d_out, dv.stream);
-      HB_OK(hipMemcpyAsync(dv.h_out, dv.d_out, total, hipMemcpyDeviceToHost, dv.stream));
+      dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
+      HB_OK(hipStreamSynchronize(dv.stream));
     }
   }
   for (size_t k = 0; k < nd; ++k) {

@@ -179,7 +179,7 @@ void bind_net(py::module_& m) {
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
-     py::arg("max_item") = 1u << 20, py::arg("batch_us") = 50, py::arg("max_batch") = 65536);
+     py::arg("max_item") = 1u << 20, py::arg("batch_us") = 0, py::arg("max_batch") = 65536);
   m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl) {
     return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl)};
   }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60);

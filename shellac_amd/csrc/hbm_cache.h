@@ -53,8 +53,11 @@ class HbmCache {
   uint64_t wait_host_slot(int i, int64_t timeout_ms = 10000) const;
   static constexpr int kHostSlots = 64;
   static constexpr uint64_t kSlotPending = ~0ull;
-  // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i].
-  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s);
+  // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
+  // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
+  // caller can queue the gather before it knows the total and retry if it did not fit.
+  void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s,
+              uint64_t out_cap = ~0ull);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).
@@ -122,7 +125,7 @@ size_t device_scan_tmp_bytes(int64_t n);
 // Load-balanced segmented copy: segment i copies (dst_off[i+1]-dst_off[i]) bytes
 // from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
-             uint8_t* dst, hipStream_t s);
+             uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
 
 // Digest packed key bytes: key i = bytes[offs[i] .. offs[i+1]).
 void digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out,

@@ -359,6 +359,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
   const uint64_t total = dst_off[n];
+  if (MODE == 0 && total > cap) return;  // MODE 0: `cap` = destination capacity
   const int64_t nchunks = (int64_t)(total >> 4);
   const uint64_t base = MODE == 1 ? *head_ptr % cap : 0;
   int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
@@ -867,10 +868,10 @@ void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* t
 }
 
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
-             uint8_t* dst, hipStream_t s) {
+             uint8_t* dst, hipStream_t s, uint64_t dst_cap) {
   if (n <= 0) return;
   launch_segcopy<0>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr, nullptr,
-                    (uint64_t)1);
+                    dst_cap);
   HIP_OK(hipGetLastError());
 }
 
@@ -1033,10 +1034,10 @@ uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
-                      hipStream_t s) {
+                      hipStream_t s, uint64_t out_cap) {
   TraceRange tr("hbm.gather");
   DeviceGuard g(cfg_.device);
-  segcopy(log_, loc, off, n, out, s);
+  segcopy(log_, loc, off, n, out, s, out_cap);
 }
 
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,

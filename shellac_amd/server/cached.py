@@ -53,7 +53,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--dram-mb", type=int, default=1024)
     p.add_argument("--gpus", type=str, default=None)
     p.add_argument("--hbm-gb", type=float, default=16.0)
-    p.add_argument("--batch-us", type=int, default=50)
+    p.add_argument("--batch-us", type=int, default=0)
     a = p.parse_args(argv)
     opts = ({"dram_mb": a.dram_mb} if a.cache == "dram" else
             {"gpus": [int(x) for x in a.gpus.split(",")] if a.gpus else None, "hbm_gb": a.hbm_gb,

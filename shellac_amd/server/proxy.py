@@ -48,7 +48,7 @@ def parse_server_list(slist: str, default_port: int) -> list:
 
 def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
-                 hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 50,
+                 hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 0,
                  retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = ""):
     """Build a native cache backend.
 
@@ -173,7 +173,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--gpus", type=str, default=None, help="GPU ids for --cache hbm, e.g. 0,1,2,3")
     p.add_argument("--hbm-gb", type=float, default=16.0, help="HBM value-log GiB per GPU")
     p.add_argument("--dram-mb", type=int, default=1024, help="host cache MiB for --cache dram")
-    p.add_argument("--batch-us", type=int, default=50, help="HBM batching window (us)")
+    p.add_argument("--batch-us", type=int, default=0,
+                   help="HBM batch linger (us); 0 = natural batching (what queued during the "
+                        "previous batch)")
     p.add_argument("--l1-mb", type=int, default=256,
                    help="host-DRAM L1 in front of --cache hbm/memcached (0 = off)")
     p.add_argument("--threads", type=int, default=1, help="reactor threads (SO_REUSEPORT)")
