@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=262144, help="GET requests per rank per step")
-    ap.add_argument("--sets", type=int, default=16384, help="SET requests per rank per step")
+    ap.add_argument("--batch", type=int, default=1 << 20, help="GET requests per rank per step")
+    ap.add_argument("--sets", type=int, default=1 << 16, help="SET requests per rank per step")
     ap.add_argument("--keys-per-gpu", type=int, default=4 << 20)
     ap.add_argument("--zipf", type=float, default=0.99)
     ap.add_argument("--min-val", type=int, default=64)
@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--replicate", type=int, default=2 << 20,
                     help="hot objects replicated on every rank (N>1; 0 = off)")
     ap.add_argument("--replica-gb", type=float, default=4.0)
-    ap.add_argument("--sample-batches", type=int, default=32,
+    ap.add_argument("--sample-batches", type=int, default=8,
                     help="GET batches (independent of the timed ones) observed to pick the "
                          "replicated hot set")
     ap.add_argument("--simulate-world", type=int, default=0,

@@ -57,7 +57,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // Smallest segcopy tile in 16-B chunks (16 KiB); SHELLAC_SEGCOPY_MIN_TILE overrides it
 // for tuning sweeps (benchmarks/kernel_bench.py).
 // Variant (loads in flight per lane, target waves/SIMD); SHELLAC_SEGCOPY_VARIANT selects
-// one for tuning (launch_segcopy lists them); 1 = 4 loads / 8 waves is the default.
+// one for tuning (launch_segcopy lists them); default 1 = 4 loads / 8 waves with
+// nontemporal stores (A/B in scripts/nt_ab.sh: -3.5% gather time vs 6 = plain stores).
 int segcopy_variant() {
   static const int v = [] {
     const char* e = getenv("SHELLAC_SEGCOPY_VARIANT");
@@ -346,7 +347,7 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
 // the range's first and last byte; their offsets are then staged in LDS kTileSegCap at
 // a time, and every lane walks its chunks (256 x 16 B apart) with a galloping search
 // over the staged offsets, issuing U independent 16-B loads before their stores.
-template <int MODE, int U, int WAVES>
+template <int MODE, int U, int WAVES, bool NTSTORE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_segcopy(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint64_t* __restrict__ dst_off, int64_t n, uint8_t* __restrict__ dst,
@@ -432,7 +433,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
         if (c >= c1) continue;
         const uint64_t d = MODE == 1 ? dofs[MODE == 1 ? u : 0] : (uint64_t)c << 4;
-        *reinterpret_cast<u32x4*>(dst + d) = v[u];
+        if (NTSTORE)
+          __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + d));
+        else
+          *reinterpret_cast<u32x4*>(dst + d) = v[u];
       }
     }
   }
@@ -453,10 +457,10 @@ int resident_grid(K kernel, int* cache) {
   return cache[dev];
 }
 
-template <int MODE, int U, int WAVES, typename... Args>
+template <int MODE, int U, int WAVES, bool NT = false, typename... Args>
 void launch_segcopy_v(hipStream_t s, Args... args) {
   static int grid[64];
-  const auto kern = k_segcopy<MODE, U, WAVES>;
+  const auto kern = k_segcopy<MODE, U, WAVES, NT>;
   hipLaunchKernelGGL(kern, dim3(resident_grid(kern, grid)), dim3(kBlock), 0, s, args...,
                      min_tile_chunks());
 }
@@ -469,7 +473,9 @@ void launch_segcopy(hipStream_t s, Args... args) {
     case 3: launch_segcopy_v<MODE, 2, 8>(s, args...); break;
     case 4: launch_segcopy_v<MODE, 8, 6>(s, args...); break;
     case 5: launch_segcopy_v<MODE, 16, 4>(s, args...); break;
-    default: launch_segcopy_v<MODE, 4, 8>(s, args...);
+    case 6: launch_segcopy_v<MODE, 4, 8, false>(s, args...); break;
+    case 7: launch_segcopy_v<MODE, 8, 5, true>(s, args...); break;
+    default: launch_segcopy_v<MODE, 4, 8, true>(s, args...);
   }
 }
 

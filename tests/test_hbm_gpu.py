@@ -297,3 +297,31 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
     assert s0 == s1
     assert sum(v is not None for v in g1[0]) == 8192     # every GET hits
     assert s1["replica_hits"] > 0
+
+
+@pytest.mark.parametrize("n,nb", [(1, 2), (777, 3), (100003, 9), (300000, 65)])
+def test_group_rows_counting_sort(cuda_dev, n, nb):
+    """csrc/router.hip counting sort: bucket counts, a permutation, rows moved with it,
+    every bucket contiguous and in bucket order."""
+    from shellac_amd._native import core
+
+    c = core()
+    g = torch.Generator(device=cuda_dev).manual_seed(n)
+    dest = torch.randint(0, nb, (n,), generator=g, device=cuda_dev, dtype=torch.int32)
+    rows = torch.randint(-2**62, 2**62, (n, 2), generator=g, device=cuda_dev)
+    out = torch.empty_like(rows)
+    perm = torch.empty(n, dtype=torch.int64, device=cuda_dev)
+    counts = torch.empty(nb, dtype=torch.int64, device=cuda_dev)
+    ws = torch.empty(c.group_ws_words(n, nb), dtype=torch.int64, device=cuda_dev)
+    st = torch.cuda.current_stream(cuda_dev).cuda_stream
+    c.group_rows(dest.data_ptr(), n, nb, rows.data_ptr(), 16, out.data_ptr(), perm.data_ptr(),
+                 counts.data_ptr(), ws.data_ptr(), st)
+    assert torch.equal(counts.cpu(), torch.bincount(dest.long().cpu(), minlength=nb))
+    assert torch.equal(torch.sort(perm).values.cpu(), torch.arange(n))
+    assert torch.equal(out[perm], rows)
+    starts = torch.cumsum(counts, 0) - counts
+    grouped = torch.empty_like(dest)
+    grouped[perm] = dest
+    expect = torch.repeat_interleave(torch.arange(nb, device=cuda_dev, dtype=torch.int32), counts)
+    assert torch.equal(grouped, expect)
+    assert int(starts[0]) == 0
