@@ -99,6 +99,7 @@ struct HbmBackendConfig {
   uint32_t max_item = 1u << 20;
   int batch_us = 0;         // optional linger for batch-mates (0: natural batching)
   int max_batch = 65536;    // flush early when this many requests are queued
+  int sweep_interval_s = 10;  // idle-time expiry sweep of every shard (0 = off)
 };
 
 class HbmBackend : public CacheBackend {
@@ -140,6 +141,8 @@ class HbmBackend : public CacheBackend {
   double epoch_;
   std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};
   std::atomic<uint64_t> batch_ns_{0};
+  std::atomic<uint64_t> sweeps_{0}, live_objects_{0}, live_bytes_{0};
+  void sweep_all();
 };
 
 // Two-level cache: a small host-DRAM L1 in front of a big L2 (HBM shards or

@@ -186,7 +186,23 @@ void HbmBackend::loop() {
     bool do_flush = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_; });
+      if (cfg_.sweep_interval_s > 0) {
+        // idle: expire TTL'd objects out of every shard's index now and then (the
+        // FIFO log reclaims bytes by itself; expired entries are otherwise only
+        // skipped lazily at lookup)
+        if (!cv_.wait_for(lk, std::chrono::seconds(cfg_.sweep_interval_s),
+                          [&] { return stop_ || !q_.empty() || flush_req_; })) {
+          lk.unlock();
+          try {
+            sweep_all();
+          } catch (const std::exception& e) {
+            std::fprintf(stderr, "[shellac hbm] sweep failed: %s\n", e.what());
+          }
+          continue;
+        }
+      } else {
+        cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_; });
+      }
       if (stop_ && q_.empty()) return;
       // Natural batching: whatever queued while the previous batch ran goes now. An
       // optional linger (batch_us > 0) trades latency for bigger batches.
@@ -353,6 +369,22 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
   }
 }
 
+void HbmBackend::sweep_all() {
+  TraceRange tr("hbm_backend.sweep");
+  const uint32_t t = now();
+  uint64_t objs = 0, bytes = 0;
+  for (auto& d : devs_) {
+    d->set_device();
+    uint64_t o = 0, b = 0;
+    d->cache->sweep(t, d->stream, &o, &b);
+    objs += o;
+    bytes += b;
+  }
+  live_objects_ = objs;
+  live_bytes_ = bytes;
+  sweeps_++;
+}
+
 void HbmBackend::stats(StatList* out) {
   CacheCounters t{};
   uint64_t hbm = 0;
@@ -374,6 +406,9 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_batched_requests", batched_reqs_.load());
   out->emplace_back("hbm_max_batch", max_batch_seen_.load());
   out->emplace_back("hbm_batch_ns_total", batch_ns_.load());
+  out->emplace_back("hbm_sweeps", sweeps_.load());
+  out->emplace_back("hbm_live_objects", live_objects_.load());
+  out->emplace_back("hbm_live_bytes", live_bytes_.load());
 }
 
 }  // namespace shellac

@@ -49,7 +49,8 @@ def parse_server_list(slist: str, default_port: int) -> list:
 def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
                  hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 0,
-                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = ""):
+                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = "",
+                 sweep_s: int = 10):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -66,11 +67,11 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
         # fault injection wraps the whole cache stack (set_fault() changes it live)
         inner = make_backend(kind, caches=caches, dram_mb=dram_mb, gpus=gpus, hbm_gb=hbm_gb,
                              max_item=max_item, batch_us=batch_us, retry_s=retry_s, l1_mb=l1_mb,
-                             promote_ttl=promote_ttl)
+                             promote_ttl=promote_ttl, sweep_s=sweep_s)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
-                          batch_us=batch_us, retry_s=retry_s)
+                          batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -84,7 +85,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
         nb = 1
         while nb * 4 * 1024 < log_bytes:  # ~2 KiB/object at <=50% slot load
             nb *= 2
-        return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us)
+        return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us, sweep_interval_s=sweep_s)
     raise ValueError(f"unknown cache backend {kind!r}")
 
 

@@ -83,3 +83,16 @@ def test_proxy_with_tiered_dram_hbm():
             assert all(o.hits[f"/tier/{i}"] == 1 for i in range(20))
     finally:
         o.stop()
+
+
+def test_hbm_backend_idle_sweep_expires_ttl():
+    be = make_backend("hbm", gpus=[0], hbm_gb=0.25, sweep_s=1)
+    be.set(b"/ttl/short", b"x" * 100, 0, 1)
+    be.set(b"/ttl/long", b"y" * 100, 0, 3600)
+    assert _wait_get(be, b"/ttl/long") == (b"y" * 100, 0)
+    time.sleep(3.2)
+    st = be.stats()
+    assert st["hbm_sweeps"] >= 1
+    assert be.get(b"/ttl/short") is None
+    assert be.get(b"/ttl/long") == (b"y" * 100, 0)
+    assert st["hbm_live_objects"] == 1
