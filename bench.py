@@ -146,7 +146,7 @@ def main():
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
     nb = 1
     shard_keys = total_keys if sim else args.keys_per_gpu
-    while nb * 2 < shard_keys:  # ~50% slot load with 4-entry buckets
+    while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
     log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
     shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)

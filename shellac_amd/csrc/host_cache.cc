@@ -103,9 +103,13 @@ bool HostCache::insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uin
     if (slots[e]->d0 == d.lo && slots[e]->d1 == d.hi) target = e;
   if (target < 0) {
     const uint32_t dead = ~lmask & 0xffu;
-    const int live1 = __builtin_popcount(lmask & 0xfu), live2 = __builtin_popcount(lmask & 0xf0u);
     if (dead) {
-      const uint32_t pref = live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu);
+      // first bucket while it keeps >= 2 free slots (lookups read it first), else the
+      // emptier bucket
+      const int live1 = __builtin_popcount(lmask & 0xfu), live2 = __builtin_popcount(lmask & 0xf0u);
+      const uint32_t pref = __builtin_popcount(dead & 0x0fu) >= 2
+                                ? (dead & 0x0fu)
+                                : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
       target = __builtin_ctz(pref ? pref : dead);
     } else {
       uint64_t oldest = ~0ull;
