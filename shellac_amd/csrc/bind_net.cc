@@ -198,7 +198,8 @@ void bind_net(py::module_& m) {
                        const std::string& bind, int threads, uint32_t ttl, bool compress,
                        const std::string& policy, bool kill_switch, bool key_host,
                        int client_timeout, int client_max_reqs, const std::string& balance,
-                       bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes) {
+                       bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
+                       uint64_t stream_high_water) {
              ProxyConfig c;
              c.upstreams = resolve_list(upstreams, 80);
              c.port = port;
@@ -215,6 +216,7 @@ void bind_net(py::module_& m) {
              c.decode_gzip = decode_gzip;
              c.upstream_retry_s = upstream_retry_s;
              c.stream_bytes = stream_bytes;
+             c.stream_high_water = stream_high_water;
              std::shared_ptr<CacheBackend> be;
              if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
              c.cache_enabled = be != nullptr;
@@ -226,7 +228,7 @@ void bind_net(py::module_& m) {
            py::arg("key_host") = false, py::arg("client_timeout") = 30,
            py::arg("client_max_reqs") = 1000, py::arg("balance") = "random",
            py::arg("decode_gzip") = false, py::arg("upstream_retry_s") = 2,
-           py::arg("stream_bytes") = 1 << 20)
+           py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20)
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

@@ -22,9 +22,6 @@ namespace {
 
 constexpr uint64_t kListenId = 1, kEventId = 2, kTimerId = 3, kFirstConnId = 16;
 constexpr int kHistBuckets = 40;
-// Streamed responses: stop reading the upstream while this much waits for a slow
-// client, resume below the low-water mark.
-constexpr uint64_t kStreamHighWater = 8 << 20, kStreamLowWater = 2 << 20;
 
 std::string simple_response(int code, const char* reason, const std::string& server,
                             const std::string& body, const char* ctype = "text/plain",
@@ -530,7 +527,7 @@ void Reactor::flush_client(Client* c) {
     }
     if (!c->slots.empty()) {
       Slot* f = c->slots.front().get();
-      if (f->streaming && f->stream_up && f->out.pending() < kStreamLowWater)
+      if (f->streaming && f->stream_up && f->out.pending() < cfg_.stream_high_water / 4)
         resume_stream(f->stream_up);
     }
     if ((size_t)w < want) {
@@ -934,7 +931,7 @@ void Reactor::stream_out(Upstream* u, std::string data, bool last) {
     hist[b]++;
   }
   flush_client(c);
-  if (!last && !c->dead && s->out.pending() > kStreamHighWater && !u->in_paused) {
+  if (!last && !c->dead && s->out.pending() > cfg_.stream_high_water && !u->in_paused) {
     stream_pauses++;
     pause_input(u, true);
   }

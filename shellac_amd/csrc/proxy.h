@@ -52,6 +52,9 @@ struct ProxyConfig {
   // Responses whose body exceeds this are streamed to the client as they arrive and not
   // cached (the reference buffers every object whole, Server.py:408-421).
   uint64_t stream_bytes = 1 << 20;
+  // A streamed response stops reading its upstream while this much waits for the
+  // client, and resumes below a quarter of it.
+  uint64_t stream_high_water = 8 << 20;
   int backlog = 1024;
   std::string server_name = "Shellac/0.2.0";
 };

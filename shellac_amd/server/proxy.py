@@ -104,7 +104,8 @@ class Server:
                  policy: str = "rfc", kill_switch: bool = True, key_host: bool = False,
                  client_timeout: int = 30, client_max_reqs: int = 1000,
                  balance: str = "random", bind: str = "0.0.0.0", decode_gzip: bool = False,
-                 stream_bytes: int = 1 << 20, **backend_opts):
+                 stream_bytes: int = 1 << 20, stream_high_water: int = 8 << 20,
+                 **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
         self._backend = backend
@@ -115,7 +116,8 @@ class Server:
             _csv(servers, 80), self._backend, port=port, bind=bind, threads=threads, ttl=ttl,
             compress=compress, policy=policy, kill_switch=kill_switch, key_host=key_host,
             client_timeout=client_timeout, client_max_reqs=client_max_reqs, balance=balance,
-            decode_gzip=decode_gzip, stream_bytes=stream_bytes)
+            decode_gzip=decode_gzip, stream_bytes=stream_bytes,
+            stream_high_water=stream_high_water)
         self._started = False
 
     @property

@@ -101,7 +101,7 @@ def test_large_objects_stream_through_uncached(origin):
 def test_streaming_backpressure_slow_client(origin):
     """A 40 MB object to a client that reads slowly: the proxy pauses the upstream
     instead of buffering everything, and the bytes arrive intact."""
-    with make_proxy([origin.port], stream_bytes=100000) as px:
+    with make_proxy([origin.port], stream_bytes=100000, stream_high_water=1 << 20) as px:
         s = socket.create_connection(("127.0.0.1", px.port))
         s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 16)
         s.sendall(b"GET /big/40000000 HTTP/1.1\r\nHost: x\r\n\r\n")
