@@ -157,7 +157,11 @@ def main():
             rnb *= 2
         replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
                              max_item=1 << 20, device=dev)
-    sc = ShardedCache(shard, group=group, replica=replica)
+    data_group = None
+    if real_world > 1:
+        # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
+        data_group = dist.new_group(ranks=list(range(real_world)))
+    sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group)
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
@@ -231,6 +235,7 @@ def main():
 
         k = 200
         ids = wl.sample_ids(args.batch, 1000 + 97 * rank + (args.steps - 1) % P)[:k]
+        res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")

@@ -54,6 +54,16 @@ class GetResult:
     data: torch.Tensor
     off: torch.Tensor
     size: torch.Tensor
+    _pending: Optional[object] = None  # value all-to-all still in flight (routed serve)
+
+    def wait(self) -> "GetResult":
+        """Order the current stream after the value transfer. A routed ``serve`` returns
+        while its value all-to-all is still running so the next step's routing overlaps
+        it; call this before reading ``data`` (``off`` / ``size`` are ready)."""
+        if self._pending is not None:
+            self._pending.wait()
+            self._pending = None
+        return self
 
     def hit_mask(self) -> torch.Tensor:
         return self.size > 0
@@ -123,9 +133,12 @@ class _Phases:
 class ShardedCache:
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
-                 sample_batches: int = 8):
+                 sample_batches: int = 8, data_group=None):
         self.shard = shard
         self.group = group
+        # Optional second communicator for the value all-to-all: its stream runs the
+        # previous step's value transfer while this step's small exchanges proceed.
+        self.data_group = data_group if data_group is not None else group
         self.rank, self.world = dist_info(group)
         self.device = shard.device
         self.ring = ShardRing(list(range(self.world)), points_per_shard)
@@ -324,15 +337,15 @@ class ShardedCache:
         data = torch.empty(local_bytes + sum(got_b) + 16, dtype=u8, device=dev)
         work = all_to_all_single(data[local_bytes: local_bytes + sum(got_b)], reply[: sum(rep_b)],
                                  output_split_sizes=got_b, input_split_sizes=rep_b,
-                                 group=self.group, async_op=True)
+                                 group=self.data_group, async_op=True)
         out = torch.empty((2, n), dtype=i64, device=dev)
         e.finish(data.data_ptr(), recv.data_ptr(), sum(recv_b), self.shard._impl, rep, now,
                  out[0].data_ptr(), out[1].data_ptr(), st)
-        work.wait()
         self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
         self.stats["replica_hits"] += n_local
         ph.end()
-        return GetResult(data, out[1], out[0])
+        # the value transfer completes in the background: GetResult.wait() before reading
+        return GetResult(data, out[1], out[0], _pending=work)
 
     def _set_rows(self, batch: SetBatch):
         """Routing of a SET batch: (dest int32 [m], records int64 [m, 4], val_off [m]).

@@ -288,7 +288,7 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
         keys = wl.digests.index_select(0, wl.sample_ids(8192, 2)).contiguous()
         got = []
         for step in range(3):
-            r = sc.serve(keys, wl.set_batch(wl.uniform_ids(1024, 10 + step)))
+            r = sc.serve(keys, wl.set_batch(wl.uniform_ids(1024, 10 + step))).wait()
             got.append([None if x is None else x[0]
                         for x in unpack_records(r.data, r.off, r.size)])
         outs.append((got, dict(sc.stats)))
