@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--replicate", type=int, default=2 << 20,
                     help="hot objects replicated on every rank (N>1; 0 = off)")
     ap.add_argument("--replica-gb", type=float, default=4.0)
-    ap.add_argument("--sample-batches", type=int, default=8,
+    ap.add_argument("--sample-batches", type=int, default=32,
                     help="GET batches (independent of the timed ones) observed to pick the "
                          "replicated hot set")
     ap.add_argument("--simulate-world", type=int, default=0,
