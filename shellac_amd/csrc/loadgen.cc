@@ -29,6 +29,7 @@ struct LgConn {
   std::deque<double> sent;  // send timestamps of in-flight requests
   std::unique_ptr<HttpParser> parser;
   size_t path_idx = 0;
+  bool out_armed = true;    // EPOLLOUT in the interest set
 };
 }  // namespace
 
@@ -41,14 +42,16 @@ LoadResult run_load(const LoadConfig& cfg) {
   std::atomic<uint64_t> bytes{0}, errors{0}, non2xx{0}, reconnects{0};
   const double t_start = now_s();
 
-  auto req_bytes = [&](size_t i) {
-    std::string r = cfg.method + " " + cfg.paths[i % cfg.paths.size()] + " HTTP/1.1\r\nHost: " +
-                    cfg.host + "\r\n";
+  // serialized requests, one per path (built once)
+  std::vector<std::string> reqs;
+  for (const auto& path : cfg.paths) {
+    std::string r = cfg.method + " " + path + " HTTP/1.1\r\nHost: " + cfg.host + "\r\n";
     if (cfg.keepalive) r += "Connection: keep-alive\r\n";
     for (const auto& h : cfg.headers) r += h + "\r\n";
     r += "\r\n";
-    return r;
-  };
+    reqs.push_back(std::move(r));
+  }
+  auto req_bytes = [&](size_t i) -> const std::string& { return reqs[i % reqs.size()]; };
 
   auto worker = [&](int tid) {
     const int nconn = cfg.concurrency / cfg.threads + (tid < cfg.concurrency % cfg.threads ? 1 : 0);
@@ -87,6 +90,32 @@ LoadResult run_load(const LoadConfig& cfg) {
         c.sent.push_back(0);  // timestamp set at send
       }
     };
+    // send what is queued right away; returns false on a socket error
+    auto flush = [&](LgConn& c) {
+      if (!c.connected || c.out_off >= c.out.size()) return true;
+      const double t = now_s();
+      for (auto& ts : c.sent)
+        if (ts == 0) ts = t;
+      const ssize_t w = send(c.fd, c.out.data() + c.out_off, c.out.size() - c.out_off, MSG_NOSIGNAL);
+      if (w > 0) c.out_off += (size_t)w;
+      if (c.out_off == c.out.size()) {
+        c.out.clear();
+        c.out_off = 0;
+      }
+      return w >= 0 || errno == EAGAIN || errno == EWOULDBLOCK;
+    };
+    // EPOLLOUT only while bytes wait (one epoll_ctl per change, not per event)
+    auto rearm = [&](int i) {
+      LgConn& c = conns[i];
+      if (c.fd < 0) return;
+      const bool want = !c.connected || c.out_off < c.out.size();
+      if (want == c.out_armed) return;
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLRDHUP | (want ? EPOLLOUT : 0);
+      ev.data.u32 = (uint32_t)i;
+      epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
+      c.out_armed = want;
+    };
     for (int i = 0; i < nconn; ++i) {
       if (open_conn(i)) top_up(conns[i]);
     }
@@ -112,17 +141,7 @@ LoadResult run_load(const LoadConfig& cfg) {
             c.connected = true;
           }
         }
-        if (c.connected && c.out_off < c.out.size()) {
-          const double t = now_s();
-          for (auto& ts : c.sent)
-            if (ts == 0) ts = t;
-          const ssize_t w = send(c.fd, c.out.data() + c.out_off, c.out.size() - c.out_off, MSG_NOSIGNAL);
-          if (w > 0) c.out_off += (size_t)w;
-          if (c.out_off == c.out.size()) {
-            c.out.clear();
-            c.out_off = 0;
-          }
-        }
+        flush(c);
         if (evs[e].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
           bool dead = false;
           for (;;) {
@@ -171,13 +190,9 @@ LoadResult run_load(const LoadConfig& cfg) {
             close_conn(i);
             continue;
           }
+          flush(c);  // the next request leaves in this iteration, not the next one
         }
-        if (c.fd >= 0) {
-          epoll_event ev{};
-          ev.events = EPOLLIN | EPOLLRDHUP | (c.out_off < c.out.size() || !c.connected ? EPOLLOUT : 0);
-          ev.data.u32 = (uint32_t)i;
-          epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
-        }
+        rearm(i);
       }
     }
     for (int i = 0; i < nconn; ++i) close_conn(i);
