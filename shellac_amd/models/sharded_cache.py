@@ -613,7 +613,7 @@ class ShardedCache:
         skip = torch.full_like(rvlen, SKIP_VLEN)
         self.shard.store(rkeys, rvals, roff, torch.where(tier == 0, rvlen, skip).contiguous(),
                          rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
-        if self.replica is not None:
+        if self.replica is not None and self._hot is not None:  # tier-1 rows only exist then
             self.replica.store(rkeys, rvals, roff, torch.where(tier == 1, rvlen, skip).contiguous(),
                                rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
 

@@ -325,3 +325,35 @@ def test_group_rows_counting_sort(cuda_dev, n, nb):
     expect = torch.repeat_interleave(torch.arange(nb, device=cuda_dev, dtype=torch.int32), counts)
     assert torch.equal(grouped, expect)
     assert int(starts[0]) == 0
+
+
+def test_fused_routed_step_edge_cases(cuda_dev):
+    """Empty GET / SET batches, SET skip rows and an all-replica GET batch take the same
+    path through the native executor and the framework-op version."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import SKIP_VLEN, SetBatch, ShardedCache
+    from shellac_amd.parallel.exchange import MirrorComm
+
+    wl = Workload(20000, cuda_dev)
+    empty_keys = torch.zeros((0, 2), dtype=torch.int64, device=cuda_dev)
+    results = []
+    for fused in (False, True):
+        sc = ShardedCache(CacheShard(512 << 20, 1 << 15, 1 << 16, cuda_dev), group=MirrorComm(3),
+                          replica=CacheShard(128 << 20, 1 << 12, 1 << 16, cuda_dev))
+        sc.fused = fused
+        sc.set(wl.set_batch(torch.arange(0, 20000, device=cuda_dev)))
+        hot = wl.digests[:500].contiguous()
+        sc.refresh_replica(500, keys=hot)
+        sb = wl.set_batch(wl.uniform_ids(300, 5))
+        sb.vlen[::7] = SKIP_VLEN
+        empty_sb = SetBatch(empty_keys, sb.values, sb.val_off[:0].contiguous(),
+                            sb.vlen[:0].contiguous())
+        got = []
+        for keys, batch in ((empty_keys, sb), (hot, empty_sb), (hot, sb),
+                            (wl.digests[:4000].contiguous(), empty_sb)):
+            r = sc.serve(keys, batch).wait()
+            got.append(([None if x is None else x[0]
+                          for x in unpack_records(r.data, r.off, r.size)]))
+        results.append((got, dict(sc.stats)))
+    assert results[0] == results[1]
+    assert all(v is not None for v in results[1][0][1])  # hot keys all served
