@@ -32,6 +32,8 @@ struct HbmBackend::Dev {
   hipStream_t stream = nullptr;
   size_t n_cap = 0, out_cap = 0, vals_cap = 0;
   Digest *d_keys = nullptr, *h_keys = nullptr;
+  Digest* h_keys_dev = nullptr;    // device view of the mapped h_keys
+  uint64_t* h_off_dev = nullptr;   // device view of the mapped h_off
   uint64_t *d_loc = nullptr, *d_size = nullptr, *d_off = nullptr, *h_off = nullptr;
   uint8_t* h_out = nullptr;
   uint8_t* h_out_dev = nullptr;  // device view of the pinned h_out (zero-copy gather target)
@@ -51,11 +53,13 @@ struct HbmBackend::Dev {
     (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
     (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
     HB_OK(hipMalloc(&d_keys, cap * sizeof(Digest)));
-    HB_OK(hipHostMalloc(&h_keys, cap * sizeof(Digest), hipHostMallocDefault));
+    HB_OK(hipHostMalloc(&h_keys, cap * sizeof(Digest), hipHostMallocMapped));
+    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_keys_dev), h_keys, 0));
     HB_OK(hipMalloc(&d_loc, cap * 8));
     HB_OK(hipMalloc(&d_size, (cap + 1) * 8));
     HB_OK(hipMalloc(&d_off, (cap + 1) * 8));
-    HB_OK(hipHostMalloc(&h_off, (cap + 1) * 8, hipHostMallocDefault));
+    HB_OK(hipHostMalloc(&h_off, (cap + 1) * 8, hipHostMallocMapped));
+    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_off_dev), h_off, 0));
     HB_OK(hipMalloc(&d_voff, cap * 8));
     HB_OK(hipHostMalloc(&h_voff, cap * 8, hipHostMallocDefault));
     HB_OK(hipMalloc(&d_meta, cap * 12));
@@ -270,6 +274,12 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     dv.ensure_n(std::max(n, std::max(sets[k].size(), dels[k].size())));
     dv.ensure_out(1);
     for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[gets[k][j]].d;
+    if ((int64_t)n <= HbmCache::kSmallGetMax) {
+      // one launch, no copies: keys, offsets and values all live in mapped host memory
+      dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
+                          tnow, dv.stream);
+      continue;
+    }
     HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
     dv.cache->lookup(dv.d_keys, (int64_t)n, dv.d_loc, dv.d_size, dv.d_off, tnow, dv.stream);
     dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
@@ -284,7 +294,11 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     const uint64_t total = dv.h_off[n];
     if (total > dv.out_cap) {  // rare: grow the zero-copy buffer and gather again
       dv.ensure_out(total);
-      dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
+      if ((int64_t)n <= HbmCache::kSmallGetMax)
+        dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
+                            tnow, dv.stream);
+      else
+        dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
       HB_OK(hipStreamSynchronize(dv.stream));
     }
   }

@@ -74,6 +74,12 @@ PYBIND11_MODULE(_shellac_core, m) {
                  now, S(s), reserve, slot);
       }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
          py::arg("now"), py::arg("stream"), py::arg("reserve") = 0, py::arg("total_slot") = -1)
+      .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
+                           uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.small_get(P<const Digest>(keys), n, P<uint8_t>(out), out_cap, P<uint64_t>(off), now,
+                    S(s));
+      })
       .def("host_slot", &HbmCache::host_slot)
       .def("wait_host_slot", [](const HbmCache& c, int i, int64_t timeout_ms) {
         py::gil_scoped_release nogil;

@@ -53,6 +53,12 @@ class HbmCache {
   uint64_t wait_host_slot(int i, int64_t timeout_ms = 10000) const;
   static constexpr int kHostSlots = 64;
   static constexpr uint64_t kSlotPending = ~0ull;
+  // Small batches (n <= 2048, the proxy's micro-batches): lookup + scan + gather in one
+  // launch. keys / out / off may be mapped host memory (no copies); off[0..n] is always
+  // written, the bytes only when off[n] <= out_cap.
+  void small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap, uint64_t* off,
+                 uint32_t now, hipStream_t s);
+  static constexpr int64_t kSmallGetMax = 2048;
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
   // caller can queue the gather before it knows the total and retry if it did not fit.

@@ -487,6 +487,105 @@ void launch_segcopy(hipStream_t s, Args... args) {
 }
 
 // ---------------------------------------------------------------------------------
+// Small GET batches (the HTTP proxy's micro-batches): probe + scan + gather in ONE
+// launch. Every workgroup probes all n keys (n <= kSmallGet, the index lines come from
+// L2 after the first workgroup) and scans the sizes in LDS; workgroup 0 publishes the
+// offsets and counters, and each workgroup copies its share of the response bytes.
+// keys / off_out / out may be mapped host memory: a batch then needs no copies at all.
+// ---------------------------------------------------------------------------------
+constexpr int kSmallGet = 2048;
+
+__global__ __launch_bounds__(kBlock) void k_small_get(
+    const Digest* __restrict__ keys, int64_t n, const Entry* __restrict__ index, uint64_t mask,
+    const uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now,
+    const uint8_t* __restrict__ log, uint8_t* __restrict__ out, uint64_t out_cap,
+    uint64_t* __restrict__ off_out, CacheCounters* __restrict__ ctr) {
+  __shared__ uint64_t s_off[kSmallGet + 1];
+  __shared__ uint64_t s_loc[kSmallGet];
+  __shared__ unsigned long long s_w[kBlock / 64];
+  const int l8 = threadIdx.x & 7, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t head = *head_ptr;
+  unsigned long long hits = 0, bytes = 0;
+  for (int64_t i = threadIdx.x >> 3; i < n; i += kBlock / 8) {
+    const Digest d = keys[i];
+    uint64_t hl = 0;
+    uint32_t hv = 0;
+#pragma unroll 1
+    for (int round = 0; round < 2 && hl == 0; ++round) {
+      const uint64_t b = round == 0 ? bucket1(d, mask) : bucket2(d, mask);
+      const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l8];
+      const uint64_t a = pack2(v.x, v.y), c = pack2(v.z, v.w);
+      const uint64_t pa = __shfl_xor(a, 1), pc = __shfl_xor(c, 1);
+      const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
+                       entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
+      hl = hit ? pa : 0;
+      hv = hit ? (uint32_t)pc : 0;
+#pragma unroll
+      for (int sh = 2; sh < 8; sh <<= 1) {
+        const uint64_t ol = __shfl_xor(hl, sh);
+        const uint32_t ov = __shfl_xor(hv, sh);
+        if (ol > hl) { hl = ol; hv = ov; }
+      }
+    }
+    if (l8 == 0) {
+      s_loc[i] = hl ? (hl - 1) % cap : 0;
+      s_off[i] = hl ? item_bytes(hv) : 0;  // sizes; scanned below
+      hits += hl ? 1 : 0;
+      bytes += hv;
+    }
+  }
+  __syncthreads();
+  // exclusive scan of s_off[0..n) in place, s_off[n] = total (n <= 2048: 8 per lane)
+  const int per = (int)((n + kBlock - 1) / kBlock);
+  const int a0 = min((int)n, per * (int)threadIdx.x), a1 = min((int)n, a0 + per);
+  unsigned long long mine = 0;
+  for (int k = a0; k < a1; ++k) mine += s_off[k];
+  unsigned long long inc = mine;
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const unsigned long long o = __shfl_up(inc, dd);
+    if (lane >= dd) inc += o;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  unsigned long long run = inc - mine;
+  for (int k = 0; k < wv; ++k) run += s_w[k];
+  for (int k = a0; k < a1; ++k) {
+    const unsigned long long v = s_off[k];
+    s_off[k] = run;
+    run += v;
+  }
+  if (a1 == n && a0 < a1) s_off[n] = run;
+  if (n == 0 && threadIdx.x == 0) s_off[0] = 0;
+  __syncthreads();
+  const uint64_t total = s_off[n];
+  if (blockIdx.x == 0) {
+    for (int64_t k = threadIdx.x; k <= n; k += kBlock) off_out[k] = s_off[k];
+  }
+  if (blockIdx.x == 0)
+    block_count(ctr, (unsigned long long)(threadIdx.x == 0 ? n : 0), &CacheCounters::get_ops, hits,
+                &CacheCounters::get_hits, bytes, &CacheCounters::get_bytes);
+  if (total > out_cap) return;  // the caller sees total in off_out and retries bigger
+  // copy: this workgroup's contiguous share of the response chunks
+  const int64_t nchunks = (int64_t)(total >> 4);
+  const int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = (int64_t)blockIdx.x * span, c1 = min(nchunks, c0 + span);
+  int jl = 0;
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += kBlock) {
+    const uint64_t x = (uint64_t)c << 4;
+    int lo = jl, hi = (int)n;  // last k with s_off[k] <= x (monotone per lane)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid] <= x) lo = mid; else hi = mid;
+    }
+    jl = lo;
+    const uint64_t w = x - s_off[lo];
+    const u32x4 v = __builtin_nontemporal_load(
+        reinterpret_cast<const u32x4*>(log + s_loc[lo] + w));
+    *reinterpret_cast<u32x4*>(out + x) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // SET
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys,
@@ -1049,6 +1148,20 @@ uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
     }
     __builtin_ia32_pause();
   }
+}
+
+void HbmCache::small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap,
+                         uint64_t* off, uint32_t now, hipStream_t s) {
+  SH_CHECK(n >= 0 && n <= kSmallGet, "small_get batch too large");
+  TraceRange tr("hbm.small_get");
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  // ~64 KiB of response per workgroup at 4 KiB values; >= 1
+  const int grid = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / 8));
+  hipLaunchKernelGGL(k_small_get, dim3(grid), dim3(kBlock), 0, s, keys, n, index_,
+                     cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, log_, out, out_cap, off,
+                     ctr_);
+  HIP_OK(hipGetLastError());
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,

@@ -198,6 +198,19 @@ class CacheShard:
         slot until the kernel has written it (no stream or event synchronisation)."""
         return int(self._impl.wait_host_slot(slot, timeout_ms))
 
+    def small_get(self, keys: torch.Tensor, out_cap: int = 16 << 20,
+                  now: Optional[int] = None):
+        """GPU, n <= 2048: lookup + scan + gather in one kernel (the proxy's micro-batch
+        path). Returns (out bytes, off[n+1]); off[n] > out_cap means nothing was copied."""
+        assert self.is_gpu and keys.shape[0] <= 2048
+        self._check(keys, "keys")
+        n = keys.shape[0]
+        out = torch.empty(max(int(out_cap), 16), dtype=torch.uint8, device=self.device)
+        off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        self._impl.small_get(keys.data_ptr(), n, out.data_ptr(), int(out_cap), off.data_ptr(),
+                             self.now() if now is None else now, self._s())
+        return out, off
+
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
                total: Optional[int] = None) -> torch.Tensor:
         """Copy hits into ``out`` (allocated from off[n] if not given: one sync)."""

@@ -357,3 +357,24 @@ def test_fused_routed_step_edge_cases(cuda_dev):
         results.append((got, dict(sc.stats)))
     assert results[0] == results[1]
     assert all(v is not None for v in results[1][0][1])  # hot keys all served
+
+
+@pytest.mark.parametrize("n", [0, 1, 100, 777, 2048])
+def test_small_get_matches_lookup_gather(cuda_dev, n):
+    """The one-launch micro-batch GET returns the same bytes and offsets as lookup +
+    gather, and copies nothing when the output capacity is too small."""
+    shard = CacheShard(64 << 20, 1 << 14, 1 << 14, cuda_dev)
+    keys = [f"/small/{i}".encode() for i in range(3000)]
+    vals = [bytes([i % 251]) * (i * 13 % 3000) for i in range(3000)]
+    shard.set_many(keys[:2000], vals[:2000])
+    req = digest_strings([keys[(i * 7) % 3000] for i in range(n)], cuda_dev)
+    lk = shard.lookup(req)
+    ref = shard.gather(lk)
+    out, off = shard.small_get(req)
+    assert torch.equal(off.cpu(), lk.off.cpu())
+    total = int(off[-1])
+    assert torch.equal(out[:total].cpu(), ref[:total].cpu())
+    if total > 64:
+        out2, off2 = shard.small_get(req, out_cap=total - 16)
+        assert int(off2[-1]) == total
+        assert not torch.equal(out2[:64].cpu(), ref[:64].cpu()) or total == 0
