@@ -148,7 +148,9 @@ def main():
     shard_keys = total_keys if sim else args.keys_per_gpu
     while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
-    log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
+    # the simulated rank's one shard stands in for all N owners: give it N logs' worth
+    # (8 x 16 GiB still fits one MI355X's 288 GB) so the key space does not wrap it
+    log_bytes = int(args.log_gb * (sim or 1) * (1 << 30)) // 16 * 16
     shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)
     replica = None
     if world > 1 and args.replicate > 0:

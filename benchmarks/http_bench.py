@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from shellac_amd.bench.ab import run  # noqa: E402
 from shellac_amd.server.proxy import Server, make_backend  # noqa: E402
-from shellac_amd.utils.origin import Origin  # noqa: E402
+from shellac_amd.utils.origin import NativeOrigin, Origin  # noqa: E402
 
 
 def main():
@@ -37,7 +37,10 @@ def main():
     ap.add_argument("--objects", type=int, default=1000)
     ap.add_argument("--body", type=int, default=4096, help="origin body bytes (before gzip)")
     ap.add_argument("--requests", type=int, default=200000)
-    ap.add_argument("--miss-requests", type=int, default=5000)
+    ap.add_argument("--miss-requests", type=int, default=50000)
+    ap.add_argument("--origin", choices=["native", "python"], default="native",
+                    help="native = C++ epoll origin (csrc/origin.cc); python = http.server")
+    ap.add_argument("--origin-threads", type=int, default=4)
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--hbm-gb", type=float, default=4.0)
     ap.add_argument("--l1-mb", type=int, default=0, help="DRAM L1 in front of hbm (0 = off)")
@@ -45,7 +48,10 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
-    origin = Origin(body_bytes=a.body).start()
+    if a.origin == "native":
+        origin = NativeOrigin(body_bytes=a.body, threads=a.origin_threads).start()
+    else:
+        origin = Origin(body_bytes=a.body).start()
     backend = None if a.backend == "none" else make_backend(
         a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
                                                                        "batch_us": a.batch_us,
@@ -56,7 +62,7 @@ def main():
     hdr = ["Accept-Encoding: gzip"]
     paths = [f"/gz/obj{i}.html" for i in range(a.objects)]
     out = {"backend": a.backend + (f"+l1:{a.l1_mb}MB" if a.backend == "hbm" and a.l1_mb else ""), "proxy_threads": a.threads, "objects": a.objects,
-           "body_bytes": a.body, "cpu_count": os.cpu_count()}
+           "body_bytes": a.body, "cpu_count": os.cpu_count(), "origin": a.origin}
     # warm the cache (every object fetched once from the origin)
     run(url, len(paths), 8, True, hdr, 1, 1, paths=paths)
     time.sleep(0.5)
@@ -65,10 +71,13 @@ def main():
         out[f"hit_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
         print(f"[http] hit c={conc}: {r['rps']:.0f} rps p50 {r['latency_ms']['p50']:.3f} ms "
               f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
-    miss_paths = [f"/miss/{i}" for i in range(a.miss_requests)]
-    r = run(url, a.miss_requests, 10, True, hdr, 1, 1, paths=miss_paths)
-    out["miss_c10"] = {k: v for k, v in r.items() if not k.startswith("_")}
-    print(f"[http] miss c=10: {r['rps']:.0f} rps (origin-bound)", file=sys.stderr)
+    # misses: unique gzip URLs, every one forwarded to the origin and filled into the cache
+    for conc in (10, 100):
+        miss_paths = [f"/gz/miss{conc}/{i}.html" for i in range(a.miss_requests)]
+        r = run(url, a.miss_requests, conc, True, hdr, 1, a.client_threads, paths=miss_paths)
+        out[f"miss_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
+        print(f"[http] miss c={conc}: {r['rps']:.0f} rps p50 {r['latency_ms']['p50']:.3f} ms "
+              f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
     out["proxy_stats"] = px.stats()
     out["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
     px.stop()

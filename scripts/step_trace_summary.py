@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Per-step summary of a rocprofv3 --marker-trace --kernel-trace run of the routed
+step (scripts/trace_bench.sh): kernels and ROCTX phases between consecutive
+`serve.plan` markers, plus the timeline of the last step.
+
+usage: step_trace_summary.py TRACE_DIR [STEPS]"""
+import csv,sys,re
+from collections import defaultdict
+d=sys.argv[1]; nsteps=int(sys.argv[2]) if len(sys.argv)>2 else 10
+m=list(csv.DictReader(open(d+'/bench_marker_api_trace.csv')))
+k=list(csv.DictReader(open(d+'/bench_kernel_trace.csv')))
+def short(n):
+    n=re.sub(r"\(anonymous namespace\)::","",n); n=re.sub(r"^void ","",n)
+    mm=re.match(r"([\w:]+(<[^()]*?>)?)",n); b=mm.group(1) if mm else n
+    if b.startswith("at::") or b.startswith("rocprim"): b=b.split("<")[0]
+    return b.replace("shellac::","")[:60]
+plans=sorted(int(r['Start_Timestamp']) for r in m if r['Function']=='serve.plan')
+print(len(plans),'plan markers')
+st=plans[-nsteps-1:]
+ks=sorted((int(r['Start_Timestamp']),int(r['End_Timestamp']),short(r['Kernel_Name'])) for r in k)
+tot=defaultdict(lambda:[0,0])
+t0,t1=st[0],st[-1]
+for s,e,n in ks:
+    if t0<=s<t1: tot[n][0]+=1; tot[n][1]+=e-s
+busy=sum(v[1] for v in tot.values())
+print(f"wall/step {(t1-t0)/1e3/nsteps:.1f} us, busy {busy/1e3/nsteps:.1f} us")
+for n,(c,dd) in sorted(tot.items(),key=lambda x:-x[1][1])[:40]:
+    print(f"{dd/1e3/nsteps:8.1f} us {c/nsteps:5.1f}x  {n}")
+# phases
+ph=defaultdict(int)
+for r in m:
+    s=int(r['Start_Timestamp']);e=int(r['End_Timestamp'])
+    if t0<=s<t1: ph[r['Function']]+=e-s
+for p,v in sorted(ph.items(),key=lambda x:-x[1]): print(f"{v/1e3/nsteps:8.1f} us host  {p}")
+# timeline of last step
+print("--- last step timeline")
+a,b=st[-2],st[-1]
+prev=a
+for s,e,n in ks:
+    if a<=s<b:
+        print(f"{(s-a)/1e3:8.1f} {(e-s)/1e3:7.1f} gap {(s-prev)/1e3:6.1f} {n}"); prev=max(prev,e)

@@ -10,6 +10,7 @@
 #include "loadgen.h"
 #include <pybind11/numpy.h>
 #include "mcserver.h"
+#include "origin.h"
 #include "proxy.h"
 
 namespace py = pybind11;
@@ -252,4 +253,22 @@ void bind_net(py::module_& m) {
       .def_property_readonly("port", &CacheServer::port)
       .def_property_readonly("running", &CacheServer::running)
       .def("ops", &CacheServer::ops);
+
+  py::class_<NativeOrigin>(m, "NativeOrigin")
+      .def(py::init([](uint16_t port, int threads, int body_bytes, int gzip_level,
+                       const std::string& host) {
+             OriginConfig c;
+             c.host = host;
+             c.port = port;
+             c.threads = threads;
+             c.body_bytes = body_bytes;
+             c.gzip_level = gzip_level;
+             return new NativeOrigin(c);
+           }),
+           py::arg("port") = 0, py::arg("threads") = 2, py::arg("body_bytes") = 1024,
+           py::arg("gzip_level") = 1, py::arg("host") = "127.0.0.1")
+      .def("start", &NativeOrigin::start)
+      .def("stop", &NativeOrigin::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &NativeOrigin::port)
+      .def_property_readonly("requests", &NativeOrigin::requests);
 }

@@ -104,3 +104,29 @@ class Origin:
     def stop(self) -> None:
         self._srv.shutdown()
         self._srv.server_close()
+
+
+class NativeOrigin:
+    """C++ epoll origin (csrc/origin.cc) with the same response shape as ``Origin``
+    for GET/HEAD: ``<html>{path} #1 xxx…</html>``, gzip-encoded for ``/gz*`` paths
+    when the request accepts gzip. Used by ``benchmarks/http_bench.py`` so the
+    miss-path RPS measures the proxy, not Python's ``http.server``."""
+
+    def __init__(self, port: int = 0, body_bytes: int = 1024, threads: int = 2,
+                 gzip_level: int = 1):
+        from .._native import core
+
+        self._o = core().NativeOrigin(port=port, threads=threads, body_bytes=body_bytes,
+                                      gzip_level=gzip_level)
+        self.port = self._o.port
+
+    @property
+    def requests(self) -> int:
+        return self._o.requests
+
+    def start(self) -> "NativeOrigin":
+        self._o.start()
+        return self
+
+    def stop(self) -> None:
+        self._o.stop()

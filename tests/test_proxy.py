@@ -372,3 +372,28 @@ def test_tiered_l1_dram_over_memcached(origin):
             assert origin.hits["/t1"] == 1
     finally:
         f.stop()
+
+
+def test_native_origin_behind_proxy():
+    """The C++ benchmark origin (csrc/origin.cc) answers like the Python fixture:
+    keep-alive, gzip for /gz* paths, pipelined requests in order."""
+    from shellac_amd.utils.origin import NativeOrigin
+
+    o = NativeOrigin(body_bytes=3000, threads=2).start()
+    try:
+        direct = HttpClient(port=o.port)
+        rs = direct.pipeline(["/x", "/y", "/x"])
+        assert [r.status() for r in rs] == [200, 200, 200]
+        assert b"<html>/y #1 " in rs[1].body().read()
+        with make_proxy([o.port]) as px:
+            c = HttpClient(port=px.port)
+            r = c.get("/gz/obj1.html")
+            assert r.headers().get("content-encoding") == "gzip"
+            assert b"/gz/obj1.html #1" in r.body().read()
+            before = o.requests
+            r = c.get("/gz/obj1.html")  # hit: the origin sees nothing
+            assert b"/gz/obj1.html #1" in r.body().read()
+            assert o.requests == before
+            assert px.stats()["cache_hits"] == 1
+    finally:
+        o.stop()
