@@ -5,7 +5,7 @@
 // The reference has no equivalent; its "routing" is one ketama pick and one TCP
 // round trip per request (src/python/shellac/server/Server.py:335, :432). Here a
 // whole batch is routed, grouped by owner, packed, unpacked and reassembled on
-// the GPU around four all-to-alls (see the phase list in sharded_cache.py).
+// the GPU around five all-to-alls (see the phase list in sharded_cache.py).
 //
 // Conventions: all pointers are device pointers; int64 counts; `w` = world size;
 // bucket `w` collects rows that go nowhere (local replica hits, SET rows of
@@ -43,15 +43,20 @@ int64_t scan_parts_words(int64_t n);
 class HbmCache;
 
 // The routed serving step of one rank as a native executor: ShardedCache keeps only
-// the four collectives (torch.distributed -> RCCL) and hands every buffer in between
+// the five collectives (torch.distributed -> RCCL) and hands every buffer in between
 // to this object, which keeps its scratch in a grow-only device arena (no allocator
 // traffic per step) and reads the two host-visible results (per-peer counts, reply
 // byte splits) through pinned memory with one stream sync each.
 //
 // Call order per step (stream-ordered on `s`):
-//   plan -> [a2a table -> rtable] -> read_counts -> pack(send) -> [a2a send -> recv]
+//   plan -> [a2a table -> rtable] -> read_counts -> pack(send)
+//   -> [a2a send request region -> recv request region]
+//   -> [async a2a send value region -> recv value region]   (SET payloads, off the
+//       critical path: only finish() reads them)
 //   -> owner(recv, sizes_out) -> [a2a sizes_out -> sizes_in] -> reply_sizes(sizes_in)
-//   -> gather_replies(reply) -> [async a2a reply -> data] -> finish(data, ...) -> [wait]
+//   -> gather_replies(reply) -> [async a2a reply -> data] -> [wait value region]
+//   -> finish(data, recv, ...) -> [wait reply a2a before reading data]
+// send / recv = [request region: per peer G_p | R_p][value region: per peer V_p].
 class RoutedStep {
  public:
   RoutedStep(int world, int rank, int device);
@@ -71,6 +76,7 @@ class RoutedStep {
             bool fanout, int64_t* table, hipStream_t s);
   // Host sync 1. Returns [table (3w) | rtable (3w) | n_local | local_bytes].
   std::vector<int64_t> read_counts(const int64_t* rtable, hipStream_t s);
+  // send: request region (sum 16 G_p + 32 R_p) then value region (sum V_p).
   void pack(uint8_t* send, hipStream_t s);
   // Owner side: de-interleave the received requests, probe `shard`; sizes_out[mg+1].
   void owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint64_t* sizes_out,

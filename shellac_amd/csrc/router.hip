@@ -323,73 +323,70 @@ __global__ __launch_bounds__(kB) void k_ps_scatter(
   }
 }
 
-// Request buffer, per peer p: [G_p | R_p | V rows of p]; destination offsets follow
-// from the exchange table, so no scan: seg_off[2w + ns + 1] (last = total bytes).
+// Request buffer: a request region [G_0 | R_0 | G_1 | R_1 | ...] (digests and SET
+// records, exchanged synchronously) followed by a value region [V_0 | V_1 | ...] (SET
+// payloads, exchanged asynchronously so they stay off the critical path to the owner
+// lookup). Destination offsets follow from the exchange table, so no scan:
+// segments G_p = 2p, R_p = 2p + 1, value row i = 2w + i; seg_off[2w + ns] = total bytes.
 __global__ __launch_bounds__(kB) void k_send_segs(const int64_t* __restrict__ table,
                                                   const uint64_t* __restrict__ svoff,
                                                   const uint64_t* __restrict__ sval,
                                                   uint64_t gk_base, uint64_t srec_base, int32_t w,
                                                   int64_t ns, uint64_t* __restrict__ seg_off,
                                                   uint64_t* __restrict__ seg_src) {
-  extern __shared__ int64_t s_pre[];  // S[w+1] rows, Gp[w+1], P[w+1] peer starts, V[w+1]
+  extern __shared__ int64_t s_pre[];  // S[w+1] SET rows, Gp[w+1] GET rows, P[w+1] request starts
   int64_t* S = s_pre;
   int64_t* Gp = S + (w + 1);
   int64_t* P = Gp + (w + 1);
-  int64_t* V = P + (w + 1);
+  __shared__ int64_t s_vtot;
   if (threadIdx.x == 0) {
-    S[0] = Gp[0] = P[0] = V[0] = 0;
+    S[0] = Gp[0] = P[0] = 0;
+    int64_t vt = 0;
     for (int p = 0; p < w; ++p) {
-      const int64_t g = table[p * 3], sr = table[p * 3 + 1], vb = table[p * 3 + 2];
+      const int64_t g = table[p * 3], sr = table[p * 3 + 1];
       S[p + 1] = S[p] + sr;
       Gp[p + 1] = Gp[p] + g;
-      V[p + 1] = V[p] + vb;
-      P[p + 1] = P[p] + 16 * g + 32 * sr + vb;
+      P[p + 1] = P[p] + 16 * g + 32 * sr;
+      vt += table[p * 3 + 2];
     }
+    s_vtot = vt;
   }
   __syncthreads();
+  const uint64_t req = (uint64_t)P[w];
   const int64_t total = ns + w;
   for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i <= total;
        i += (int64_t)gridDim.x * kB) {
     if (i == total) {
-      seg_off[2 * w + ns] = (uint64_t)P[w];
+      seg_off[2 * w + ns] = req + (uint64_t)s_vtot;
     } else if (i < ns) {
-      int lo = 0, hi = w;  // peer p with S[p] <= i < S[p+1]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (S[mid] <= i) lo = mid; else hi = mid;
-      }
-      const int64_t seg = i + 2 * lo + 2;
-      const int64_t sr = S[lo + 1] - S[lo], g = Gp[lo + 1] - Gp[lo];
-      seg_off[seg] = (uint64_t)(P[lo] + 16 * g + 32 * sr) + (svoff[i] - (uint64_t)V[lo]);
-      seg_src[seg] = sval[i];
+      seg_off[2 * w + i] = req + svoff[i];  // svoff: global byte offset in peer order
+      seg_src[2 * w + i] = sval[i];
     } else {
       const int p = (int)(i - ns);
-      const int64_t gseg = 2 * p + S[p];
       const int64_t g = Gp[p + 1] - Gp[p];
-      seg_off[gseg] = (uint64_t)P[p];
-      seg_src[gseg] = gk_base + 16 * (uint64_t)Gp[p];
-      seg_off[gseg + 1] = (uint64_t)(P[p] + 16 * g);
-      seg_src[gseg + 1] = srec_base + 32 * (uint64_t)S[p];
+      seg_off[2 * p] = (uint64_t)P[p];
+      seg_src[2 * p] = gk_base + 16 * (uint64_t)Gp[p];
+      seg_off[2 * p + 1] = (uint64_t)(P[p] + 16 * g);
+      seg_src[2 * p + 1] = srec_base + 32 * (uint64_t)S[p];
     }
   }
 }
 
-// De-interleave the received buffer into [all G | all R]: 2w segments + end offset.
+// De-interleave the received request region into [all G | all R]: 2w segments + end.
 __global__ void k_recv_segs(const int64_t* __restrict__ rtable, uint64_t recv_base, int32_t w,
                             uint64_t* __restrict__ seg_off, uint64_t* __restrict__ seg_src) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint64_t q0 = 0, g0 = 0, r0 = 0, gtot = 0;
   for (int q = 0; q < w; ++q) gtot += 16 * (uint64_t)rtable[q * 3];
   for (int q = 0; q < w; ++q) {
-    const uint64_t a = (uint64_t)rtable[q * 3], b = (uint64_t)rtable[q * 3 + 1],
-                   c = (uint64_t)rtable[q * 3 + 2];
+    const uint64_t a = (uint64_t)rtable[q * 3], b = (uint64_t)rtable[q * 3 + 1];
     seg_off[q] = g0;
     seg_src[q] = recv_base + q0;
     seg_off[w + q] = gtot + r0;
     seg_src[w + q] = recv_base + q0 + 16 * a;
     g0 += 16 * a;
     r0 += 32 * b;
-    q0 += 16 * a + 32 * b + c;
+    q0 += 16 * a + 32 * b;  // the value region follows all request chunks
   }
   seg_off[2 * w] = gtot + r0;
 }
@@ -402,13 +399,13 @@ __global__ __launch_bounds__(kB) void k_rs_fill(
   int64_t* first = s_q;
   int64_t* vstart = s_q + (w + 1);
   if (threadIdx.x == 0) {
-    int64_t q0 = 0;
+    int64_t v0 = 0;  // value region starts after every source's request chunk
+    for (int q = 0; q < w; ++q) v0 += 16 * rtable[q * 3] + 32 * rtable[q * 3 + 1];
     first[0] = 0;
     for (int q = 0; q < w; ++q) {
-      const int64_t a = rtable[q * 3], b = rtable[q * 3 + 1], c = rtable[q * 3 + 2];
-      vstart[q] = q0 + 16 * a + 32 * b;
-      first[q + 1] = first[q] + b;
-      q0 += 16 * a + 32 * b + c;
+      vstart[q] = v0;
+      first[q + 1] = first[q] + rtable[q * 3 + 1];
+      v0 += rtable[q * 3 + 2];
     }
   }
   __syncthreads();
@@ -711,7 +708,7 @@ void RoutedStep::pack(uint8_t* send, hipStream_t s) {
   const int64_t nseg = 2 * (int64_t)W + ns_;
   uint64_t* seg_off = buf<uint64_t>(kSegOff, nseg + 1);
   uint64_t* seg_src = buf<uint64_t>(kSegSrc, nseg);
-  hipLaunchKernelGGL(k_send_segs, dim3(grid1(ns_ + W + 1)), dim3(kB), 4 * (W + 1) * sizeof(int64_t),
+  hipLaunchKernelGGL(k_send_segs, dim3(grid1(ns_ + W + 1)), dim3(kB), 3 * (W + 1) * sizeof(int64_t),
                      s, table_, svoff_, sval_, (uint64_t)(uintptr_t)gk_,
                      (uint64_t)(uintptr_t)srec_, W, ns_, seg_off, seg_src);
   RT_OK(hipGetLastError());

@@ -250,7 +250,7 @@ class ShardedCache:
         overwrite count as misses) and its kernel writes the total into a pinned host
         slot; the SET is queued, and only then does the host spin on that slot to size
         the gather (no event, no copy).
-        With several ranks see ``_serve_routed``: 4 collectives and 2 host syncs for
+        With several ranks see ``_serve_routed``: 4-5 collectives and 2 host syncs for
         the whole step instead of 10 and 3 for get() followed by set()."""
         if self.world > 1:
             if self.fused and self.device.type == "cuda":
@@ -276,8 +276,12 @@ class ShardedCache:
                             now: Optional[int] = None) -> GetResult:
         """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep):
         every step between the collectives is a fused kernel sequence over a grow-only
-        device arena; Python issues the four all-to-alls and nothing else. Same
-        protocol and results as the framework-op version (tests/test_hbm_gpu.py)."""
+        device arena; Python issues the all-to-alls and nothing else. Same results as
+        the framework-op version (tests/test_hbm_gpu.py); the wire layout differs in
+        one respect: SET payloads leave the synchronous request exchange and travel in
+        their own asynchronous all-to-all on the data communicator, so the owner lookup
+        and the second host sync do not wait for them (xGMI is point-to-point: at N=2
+        one link carries every byte, so what sits on the critical path matters)."""
         c = _core()
         dev, w, me = self.device, self.world, self.rank
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -312,17 +316,24 @@ class ShardedCache:
         h = e.read_counts(rtable.data_ptr(), st)                          # sync 1
         g_rows = h[0: 3 * w: 3]
         rg_rows = h[3 * w: 6 * w: 3]
-        send_b = [16 * h[3 * p] + 32 * h[3 * p + 1] + h[3 * p + 2] for p in range(w)]
-        recv_b = [16 * h[3 * w + 3 * p] + 32 * h[3 * w + 3 * p + 1] + h[3 * w + 3 * p + 2]
-                  for p in range(w)]
+        # request region (GET digests + SET records) and value region (SET payloads)
+        send_q = [16 * h[3 * p] + 32 * h[3 * p + 1] for p in range(w)]
+        recv_q = [16 * h[3 * w + 3 * p] + 32 * h[3 * w + 3 * p + 1] for p in range(w)]
+        send_v = [h[3 * p + 2] for p in range(w)]
+        recv_v = [h[3 * w + 3 * p + 2] for p in range(w)]
+        sq, rq, sv, rv = sum(send_q), sum(recv_q), sum(send_v), sum(recv_v)
         n_local, local_bytes = h[6 * w], h[6 * w + 1]
         ph.next("pack_requests")
-        send = torch.empty(sum(send_b) + 16, dtype=u8, device=dev)
+        send = torch.empty(sq + sv + 16, dtype=u8, device=dev)
         e.pack(send.data_ptr(), st)
-        recv = torch.empty(sum(recv_b) + 16, dtype=u8, device=dev)
+        recv = torch.empty(rq + rv + 16, dtype=u8, device=dev)
         ph.next("request_a2a")
-        all_to_all_single(recv[: sum(recv_b)], send[: sum(send_b)], output_split_sizes=recv_b,
-                          input_split_sizes=send_b, group=self.group)
+        all_to_all_single(recv[:rq], send[:sq], output_split_sizes=recv_q,
+                          input_split_sizes=send_q, group=self.group)
+        # SET payloads travel on the data communicator while the owner probes and the
+        # reply sizes are exchanged; only the SET stores in finish() wait for them
+        vwork = all_to_all_single(recv[rq: rq + rv], send[sq: sq + sv], output_split_sizes=recv_v,
+                                  input_split_sizes=send_v, group=self.data_group, async_op=True)
         ph.next("owner_lookup")
         mg = e.mg
         sizes_out = torch.empty(mg + 1, dtype=i64, device=dev)
@@ -339,7 +350,8 @@ class ShardedCache:
                                  output_split_sizes=got_b, input_split_sizes=rep_b,
                                  group=self.data_group, async_op=True)
         out = torch.empty((2, n), dtype=i64, device=dev)
-        e.finish(data.data_ptr(), recv.data_ptr(), sum(recv_b), self.shard._impl, rep, now,
+        vwork.wait()  # stream-ordered: the SET stores below read the value region
+        e.finish(data.data_ptr(), recv.data_ptr(), rq + rv, self.shard._impl, rep, now,
                  out[0].data_ptr(), out[1].data_ptr(), st)
         self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
         self.stats["replica_hits"] += n_local
