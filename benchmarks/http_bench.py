@@ -32,8 +32,8 @@ from shellac_amd.utils.origin import NativeOrigin, Origin  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", choices=["dram", "hbm", "none"], default="dram")
-    ap.add_argument("--threads", type=int, default=4, help="proxy reactor threads")
-    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--threads", type=int, default=8, help="proxy reactor threads")
+    ap.add_argument("--client-threads", type=int, default=8)
     ap.add_argument("--objects", type=int, default=1000)
     ap.add_argument("--body", type=int, default=4096, help="origin body bytes (before gzip)")
     ap.add_argument("--requests", type=int, default=200000)

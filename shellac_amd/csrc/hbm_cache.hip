@@ -464,12 +464,26 @@ int resident_grid(K kernel, int* cache) {
   return cache[dev];
 }
 
+// Share of the co-resident slots a segcopy grid takes, in 1/64ths (64 = all of them).
+// Below 64 the byte mover leaves room for latency-bound kernels queued concurrently
+// on another stream (the SET chain during a GET gather); SHELLAC_SEGCOPY_OCC overrides.
+int segcopy_occ64() {
+  static const int v = [] {
+    const char* e = getenv("SHELLAC_SEGCOPY_OCC");
+    // 48/64: a gather at 3/4 of the slots is as fast as at all of them (memory-bound),
+    // and the rest lets a concurrent SET chain through (scripts/overlap_sweep.sh)
+    const int o = e ? atoi(e) : 48;
+    return o < 8 ? 8 : (o > 64 ? 64 : o);
+  }();
+  return v;
+}
+
 template <int MODE, int U, int WAVES, bool NT = false, typename... Args>
 void launch_segcopy_v(hipStream_t s, Args... args) {
   static int grid[64];
   const auto kern = k_segcopy<MODE, U, WAVES, NT>;
-  hipLaunchKernelGGL(kern, dim3(resident_grid(kern, grid)), dim3(kBlock), 0, s, args...,
-                     min_tile_chunks());
+  const int g = std::max(1, resident_grid(kern, grid) * segcopy_occ64() / 64);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., min_tile_chunks());
 }
 
 template <int MODE, typename... Args>

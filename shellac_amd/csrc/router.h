@@ -112,6 +112,10 @@ class RoutedStep {
   const int64_t* hot_dir_ = nullptr;
   std::vector<Buf> bufs_;
   int64_t* host_ = nullptr;  // pinned
+  // side stream: the main-shard SET chain runs there while the replica gather runs on
+  // the caller's stream (finish); events fork and join the two
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_fill_ = nullptr, ev_join_ = nullptr;
   // per-step state
   int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
   uint64_t local_bytes_ = 0;

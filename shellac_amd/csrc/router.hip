@@ -586,6 +586,10 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   SH_CHECK(world >= 1 && world < kMaxBuckets, "bad world size");
   RT_OK(hipSetDevice(device_));
   RT_OK(hipHostMalloc(&host_, (8 * (size_t)world + 8) * sizeof(int64_t), hipHostMallocDefault));
+  RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  RT_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+  RT_OK(hipEventCreateWithFlags(&ev_fill_, hipEventDisableTiming));
+  RT_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
 }
 
 RoutedStep::~RoutedStep() {
@@ -593,6 +597,10 @@ RoutedStep::~RoutedStep() {
   (void)hipDeviceSynchronize();
   for (auto& b : bufs_) (void)hipFree(b.p);
   (void)hipHostFree(host_);
+  (void)hipEventDestroy(ev_fork_);
+  (void)hipEventDestroy(ev_fill_);
+  (void)hipEventDestroy(ev_join_);
+  (void)hipStreamDestroy(side_);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
@@ -752,27 +760,44 @@ void RoutedStep::gather_replies(HbmCache* shard, uint8_t* reply, hipStream_t s) 
 void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
                         HbmCache* replica, uint32_t now, uint64_t* out_size, uint64_t* out_off,
                         hipStream_t s) {
-  if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
-  if (ms_ > 0) {
-    const int64_t ms = ms_;
-    Digest* rkeys = buf<Digest>(kRkeys, ms);
+  const int64_t ms = ms_;
+  uint32_t *v1 = nullptr, *fl = nullptr, *ex = nullptr;
+  Digest* rkeys = nullptr;
+  uint64_t* roff = nullptr;
+  const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
+  if (ms > 0) {
+    // fork: received-SET unpacking and the main-shard SET chain (latency-bound small
+    // grids) go to the side stream, concurrently with the bandwidth-bound replica
+    // gather below. They touch different shards; everything the caller queued before
+    // (reply gather from the main shard, the wait for the SET payloads) comes first.
+    rkeys = buf<Digest>(kRkeys, ms);
     uint32_t* v0 = buf<uint32_t>(kV0, ms);
-    uint32_t* v1 = buf<uint32_t>(kV1, ms);
-    uint32_t* fl = buf<uint32_t>(kFl, ms);
-    uint32_t* ex = buf<uint32_t>(kEx, ms);
-    uint64_t* roff = buf<uint64_t>(kRoff, ms);
-    hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t), s,
-                       rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
+    v1 = buf<uint32_t>(kV1, ms);
+    fl = buf<uint32_t>(kFl, ms);
+    ex = buf<uint32_t>(kEx, ms);
+    roff = buf<uint64_t>(kRoff, ms);
+    RT_OK(hipEventRecord(ev_fork_, s));
+    RT_OK(hipStreamWaitEvent(side_, ev_fork_, 0));
+    hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t),
+                       side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
     RT_OK(hipGetLastError());
-    const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
-    shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, s);
-    if (replica) replica->store(rkeys, recv, roff, v1, fl, ex, ms, bound, now, s);
+    RT_OK(hipEventRecord(ev_fill_, side_));
+    shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, side_);
+    RT_OK(hipEventRecord(ev_join_, side_));
+  }
+  if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
+  if (ms > 0 && replica) {
+    // the replica's own SET rows (tier 1) go after its gather: they may overwrite
+    // log bytes the gather reads
+    RT_OK(hipStreamWaitEvent(s, ev_fill_, 0));
+    replica->store(rkeys, recv, roff, v1, fl, ex, ms, bound, now, s);
   }
   if (n_ > 0)
     hipLaunchKernelGGL(k_assemble, dim3(grid1(n_)), dim3(kB), 0, s, perm_g_, n_, n_remote_,
                        sizes_in_, gscan_, have_replica_ ? rl_size_ : nullptr,
                        have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off);
   RT_OK(hipGetLastError());
+  if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_join_, 0));  // join: later work sees the SETs
 }
 
 }  // namespace shellac

@@ -27,6 +27,7 @@ per-request host work. With one rank every step is purely local.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -154,6 +155,9 @@ class ShardedCache:
         self._engine = None
         self._xtable = None
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
+        # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
+        self.overlap_store = os.environ.get("SHELLAC_OVERLAP_STORE", "1") != "0"
+        self._side = None
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -268,9 +272,31 @@ class ShardedCache:
             data = sh.gather(lk)
             return GetResult(data, lk.off[:n], lk.size[:n])
         lk = sh.lookup(keys, now, reserve_bytes=bound, total_slot=0)
-        sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags, batch.expire, now)
+        side = self._side_stream() if self.overlap_store else None
+        if side is None:
+            sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                     batch.expire, now)
+            data = sh.gather(lk, total=sh.host_total(0))
+            return GetResult(data, lk.off[:n], lk.size[:n])
+        # The SET chain (dedupe, size scan, log write, index CAS: mostly latency-bound
+        # small grids) runs on a side stream concurrently with the bandwidth-bound
+        # gather. Safe by construction: the lookup reserved the SET's log bytes, so the
+        # gather never reads a region the SET writes, and it does not read the index.
+        main = torch.cuda.current_stream(self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                     batch.expire, now)
         data = sh.gather(lk, total=sh.host_total(0))
+        main.wait_stream(side)  # the next step's lookup sees this step's SETs
         return GetResult(data, lk.off[:n], lk.size[:n])
+
+    def _side_stream(self):
+        if self.device.type != "cuda":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
                             now: Optional[int] = None) -> GetResult:
