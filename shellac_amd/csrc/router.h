@@ -68,13 +68,15 @@ class RoutedStep {
   // Sorted hot set (by signed lo) + optional 65537-entry directory (see is_hot).
   void set_hot(const Digest* hot, int64_t nhot, const int64_t* dir = nullptr);
 
-  // GET routing (replica probe first when `replica`), SET routing + hot fan-out,
-  // per-peer table[w][3] = {GET rows, SET rows, SET value bytes} into `table`.
+  // GET routing (replica probe first when `replica`), SET routing + hot fan-out (on a
+  // side stream, concurrently), per-peer table[w][3] = {GET rows, SET rows, SET value
+  // bytes} into `table`, which must hold 6w + 2 words: [table | rtable | extras].
   void plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
             const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
             const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues, int64_t ns,
             bool fanout, int64_t* table, hipStream_t s);
-  // Host sync 1. Returns [table (3w) | rtable (3w) | n_local | local_bytes].
+  // Host sync 1 (one D2H; rtable must be table + 3w). Returns
+  // [table (3w) | rtable (3w) | n_local | local_bytes].
   std::vector<int64_t> read_counts(const int64_t* rtable, hipStream_t s);
   // send: request region (sum 16 G_p + 32 R_p) then value region (sum V_p).
   void pack(uint8_t* send, hipStream_t s);
@@ -115,7 +117,7 @@ class RoutedStep {
   // side stream: the main-shard SET chain runs there while the replica gather runs on
   // the caller's stream (finish); events fork and join the two
   hipStream_t side_ = nullptr;
-  hipEvent_t ev_fork_ = nullptr, ev_fill_ = nullptr, ev_join_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_fill_ = nullptr, ev_join_ = nullptr, ev_pjoin_ = nullptr;
   // per-step state
   int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
   uint64_t local_bytes_ = 0;

@@ -79,9 +79,15 @@ __global__ __launch_bounds__(kB) void k_gr_hist(const int32_t* __restrict__ dest
 }
 
 // One workgroup: exclusive scan of table[0..T) in place; counts[d] = bucket totals.
+// Optionally (xtable != nullptr, routed GET plan) also writes the GET column of the
+// exchange table, xtable[d * 3] = counts[d] for d < nb - 1, and
+// extras = {counts[nb - 1] (local replica hits), *rl_off_n (their response bytes)}.
 __global__ __launch_bounds__(1024) void k_gr_scan(uint64_t* __restrict__ table, int64_t T,
                                                   int32_t nb, int32_t G,
-                                                  int64_t* __restrict__ counts) {
+                                                  int64_t* __restrict__ counts,
+                                                  int64_t* __restrict__ xtable = nullptr,
+                                                  const uint64_t* __restrict__ rl_off_n = nullptr,
+                                                  int64_t* __restrict__ extras = nullptr) {
   __shared__ unsigned long long s_w[16];
   __shared__ unsigned long long s_total;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -117,6 +123,13 @@ __global__ __launch_bounds__(1024) void k_gr_scan(uint64_t* __restrict__ table, 
     const uint64_t s0 = table[(int64_t)d * G];
     const uint64_t s1 = d + 1 < nb ? table[(int64_t)(d + 1) * G] : s_total;
     counts[d] = (int64_t)(s1 - s0);
+    if (xtable) {
+      if (d < nb - 1) xtable[(int64_t)d * 3] = (int64_t)(s1 - s0);
+      else {
+        extras[0] = (int64_t)(s1 - s0);
+        extras[1] = rl_off_n ? (int64_t)*rl_off_n : 0;
+      }
+    }
   }
 }
 
@@ -162,42 +175,55 @@ __global__ __launch_bounds__(kB) void k_route_gets(const Digest* __restrict__ ke
     dest[i] = (rsize && rsize[i] > 0) ? w : ring_owner_of(keys[i], pts, own, npts);
 }
 
-// SET planning. Input row j goes to its owner, and (fan-out) to every rank when its
-// key is hot: tier 0 = owner copy, tier 1 = replica copy.
-__global__ __launch_bounds__(kB) void k_ps_dest(const Digest* __restrict__ keys,
-                                                const uint32_t* __restrict__ vlen, int64_t ns,
-                                                const uint32_t* __restrict__ pts,
-                                                const int32_t* __restrict__ own, int npts,
-                                                const Digest* __restrict__ hot, int64_t nhot,
-                                                const int64_t* __restrict__ hot_dir,
-                                                int32_t* __restrict__ owner,
-                                                uint32_t* __restrict__ vpad) {
-  for (int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x; j < ns; j += (int64_t)gridDim.x * kB) {
-    const Digest k = keys[j];
-    const int o = ring_owner_of(k, pts, own, npts);
-    const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
-    owner[j] = h ? (o | (1 << 30)) : o;  // bit 30: fan out to every rank
-    const uint32_t vl = vlen[j];
-    vpad[j] = vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
+// Routed GET plan, fused: dest of every key of this workgroup's contiguous range
+// (owner, or `w` for a local replica hit) + its LDS histogram into table[d * G + b]
+// (the k_gr_hist layout, so k_gr_scan / k_gr_scatter follow unchanged).
+__global__ __launch_bounds__(kB) void k_route_hist(const Digest* __restrict__ keys, int64_t n,
+                                                   const uint64_t* __restrict__ rsize,
+                                                   const uint32_t* __restrict__ pts,
+                                                   const int32_t* __restrict__ own, int npts,
+                                                   int32_t w, int64_t plen,
+                                                   int32_t* __restrict__ dest,
+                                                   uint64_t* __restrict__ table) {
+  extern __shared__ uint32_t s_c[];
+  const int nb = w + 1;
+  for (int d = threadIdx.x; d < nb; d += kB) s_c[d] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(n, i0 + plen);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += kB) {
+    const int d = (rsize && rsize[i] > 0) ? w : ring_owner_of(keys[i], pts, own, npts);
+    dest[i] = d;
+    atomicAdd(&s_c[d], 1u);
   }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nb; d += kB) table[(int64_t)d * gridDim.x + blockIdx.x] = s_c[d];
 }
 
-// Rows AND value bytes per (destination, workgroup): one packed 64-bit LDS counter
-// (rows | bytes << 32) so the scatter below can hand out row slots and byte ranges in
-// the same order.
-__global__ __launch_bounds__(kB) void k_ps_hist(const int32_t* __restrict__ owner, int64_t ns,
-                                                int32_t nb, int64_t plen, int32_t w,
-                                                const uint32_t* __restrict__ vpad,
-                                                uint64_t* __restrict__ tcnt,
-                                                uint64_t* __restrict__ tbytes) {
+// SET planning, fused: input row j goes to its owner and (fan-out) to every rank when
+// its key is hot (tier 0 = owner copy, tier 1 = replica copy). Each workgroup handles
+// a contiguous range: owner / padded length per row, and the rows AND value bytes per
+// destination in one packed 64-bit LDS counter (rows | bytes << 32) so k_ps_scatter
+// can hand out row slots and byte ranges in the same order.
+__global__ __launch_bounds__(kB) void k_ps_dest_hist(
+    const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen, int64_t ns,
+    const uint32_t* __restrict__ pts, const int32_t* __restrict__ own, int npts,
+    const Digest* __restrict__ hot, int64_t nhot, const int64_t* __restrict__ hot_dir,
+    int32_t nb, int64_t plen, int32_t w, int32_t* __restrict__ owner,
+    uint32_t* __restrict__ vpad, uint64_t* __restrict__ tcnt, uint64_t* __restrict__ tbytes) {
   extern __shared__ unsigned long long s_cb[];
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
   for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
-    const int o = owner[j];
-    const unsigned long long inc = 1ull | ((unsigned long long)vpad[j] << 32);
-    if (o >> 30) {
+    const Digest k = keys[j];
+    const int o = ring_owner_of(k, pts, own, npts);
+    const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
+    owner[j] = h ? (o | (1 << 30)) : o;  // bit 30: fan out to every rank
+    const uint32_t vl = vlen[j];
+    const uint32_t vp = vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
+    vpad[j] = vp;
+    const unsigned long long inc = 1ull | ((unsigned long long)vp << 32);
+    if (h) {
       for (int r = 0; r < w; ++r) atomicAdd(&s_cb[r], inc);
     } else {
       atomicAdd(&s_cb[o], inc);
@@ -248,16 +274,13 @@ __device__ unsigned long long block_scan_inplace(uint64_t* __restrict__ t, int64
   return total;
 }
 
-// Scans both SET tables, then writes the per-peer exchange table
-// table[p] = {GET rows, SET rows, SET value bytes} and extras = {local GET hits,
-// local replica response bytes}.
+// Scans both SET tables, then writes the SET columns of the per-peer exchange table:
+// table[p * 3 + 1] = SET rows, table[p * 3 + 2] = SET value bytes (k_gr_scan writes
+// column 0 on the other stream).
 __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
                                                   uint64_t* __restrict__ tbytes, int32_t nb,
-                                                  int32_t G, const int64_t* __restrict__ cnt_g,
-                                                  const uint64_t* __restrict__ rl_off_n,
-                                                  int64_t* __restrict__ cnt_s,
-                                                  int64_t* __restrict__ table,
-                                                  int64_t* __restrict__ extras) {
+                                                  int32_t G, int64_t* __restrict__ cnt_s,
+                                                  int64_t* __restrict__ table) {
   __shared__ unsigned long long s_w[17];
   const int64_t T = (int64_t)nb * G;
   const unsigned long long tc = block_scan_inplace(tcnt, T, s_w);
@@ -270,14 +293,9 @@ __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
     const int64_t c = (int64_t)(c1 - tcnt[(int64_t)d * G]);
     cnt_s[d] = c;
     if (d < w) {
-      table[d * 3 + 0] = cnt_g[d];
       table[d * 3 + 1] = c;
       table[d * 3 + 2] = (int64_t)(b1 - tbytes[(int64_t)d * G]);
     }
-  }
-  if (threadIdx.x == 0) {
-    extras[0] = cnt_g[w];
-    extras[1] = rl_off_n ? (int64_t)*rl_off_n : 0;
   }
 }
 
@@ -576,7 +594,7 @@ namespace shellac {
 namespace {
 enum Slot {
   kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kOwnerS, kVpad, kTcnt,
-  kTbytes, kSrec, kSval, kSvoff, kCntS, kExtras, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
+  kTbytes, kSrec, kSval, kSvoff, kCntS, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
   kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
 };
 }  // namespace
@@ -590,6 +608,7 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   RT_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_fill_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  RT_OK(hipEventCreateWithFlags(&ev_pjoin_, hipEventDisableTiming));
 }
 
 RoutedStep::~RoutedStep() {
@@ -600,6 +619,7 @@ RoutedStep::~RoutedStep() {
   (void)hipEventDestroy(ev_fork_);
   (void)hipEventDestroy(ev_fill_);
   (void)hipEventDestroy(ev_join_);
+  (void)hipEventDestroy(ev_pjoin_);
   (void)hipStreamDestroy(side_);
 }
 
@@ -638,62 +658,76 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
                       int64_t ns, bool fanout, int64_t* table, hipStream_t s) {
   SH_CHECK(pts_ && own_ && npts_ > 0, "RoutedStep: ring not set");
   const int W = w_;
+  const int nb = W + 1;
   n_ = n;
   values_ = svalues;
   have_replica_ = replica != nullptr;
   table_ = table;
+  int64_t* extras = table + 6 * W;  // [table | rtable | extras]: one D2H in read_counts
+  // every buffer first (buf() may reallocate, which synchronises the device)
   uint64_t* rl_size = nullptr;
   if (replica) {
     rl_loc_ = buf<uint64_t>(kRlLoc, n);
     rl_size = rl_size_ = buf<uint64_t>(kRlSize, n + 1);
     rl_off_ = buf<uint64_t>(kRlOff, n + 1);
-    replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
   }
-  // GET rows: owner (or bucket W = local replica hit), counting sort by owner
   int32_t* dest_g = buf<int32_t>(kDestG, n);
-  route_gets(keys, n, rl_size, pts_, own_, npts_, W, dest_g, s);
   gk_ = buf<Digest>(kGk, n);
   perm_g_ = buf<int64_t>(kPermG, n);
-  cnt_g_ = buf<int64_t>(kCntG, W + 1);
-  group_rows(dest_g, n, W + 1, keys, 16, gk_, perm_g_, cnt_g_,
-             buf<uint64_t>(kWsG, group_ws_words(std::max<int64_t>(n, 1), W + 1)), s);
-  // SET rows: owner + hot fan-out, counting sort by destination with value-byte ranges
-  const int nb = W + 1;
+  cnt_g_ = buf<int64_t>(kCntG, nb);
+  const int64_t ng = std::max<int64_t>(n, 1);
+  const int Gg = group_grid(ng);
+  const int64_t plen_g = (ng + Gg - 1) / Gg;
+  uint64_t* ws_g = buf<uint64_t>(kWsG, group_ws_words(ng, nb));
   // SET rows fan out up to W ways: smaller ranges per workgroup than the GET sort
-  const int G = group_grid(std::max<int64_t>(ns, 1), 256);
-  const int64_t plen = (std::max<int64_t>(ns, 1) + G - 1) / G;
+  const int64_t nsx = std::max<int64_t>(ns, 1);
+  const int Gs = group_grid(nsx, 256);
+  const int64_t plen_s = (nsx + Gs - 1) / Gs;
   const int64_t mcap = fanout ? ns * W : ns;  // upper bound of routed SET rows
   int32_t* owner_s = buf<int32_t>(kOwnerS, ns);
   uint32_t* vpad = buf<uint32_t>(kVpad, ns);
-  uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * G);
-  uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * G);
+  uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * Gs);
+  uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * Gs);
   srec_ = buf<int64_t>(kSrec, 4 * (size_t)mcap);
   sval_ = buf<uint64_t>(kSval, mcap);
   svoff_ = buf<uint64_t>(kSvoff, mcap);
   cnt_s_ = buf<int64_t>(kCntS, nb);
-  int64_t* extras = buf<int64_t>(kExtras, 2);
+
+  // SET planning on the side stream (owner + hot fan-out, counting sort with value-byte
+  // ranges), concurrently with the replica probe and GET sort on `s`
+  RT_OK(hipEventRecord(ev_fork_, s));
+  RT_OK(hipStreamWaitEvent(side_, ev_fork_, 0));
+  hipLaunchKernelGGL(k_ps_dest_hist, dim3(Gs), dim3(kB), nb * sizeof(unsigned long long), side_,
+                     skeys, svlen, ns, pts_, own_, npts_, fanout ? hot_ : nullptr,
+                     fanout ? nhot_ : 0, fanout ? hot_dir_ : nullptr, nb, plen_s, W, owner_s,
+                     vpad, tcnt, tbytes);
+  hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, side_, tcnt, tbytes, nb, Gs, cnt_s_,
+                     table);
   if (ns > 0)
-    hipLaunchKernelGGL(k_ps_dest, dim3(grid1(ns)), dim3(kB), 0, s, skeys, svlen, ns, pts_, own_,
-                       npts_, fanout ? hot_ : nullptr, fanout ? nhot_ : 0,
-                       fanout ? hot_dir_ : nullptr, owner_s, vpad);
-  hipLaunchKernelGGL(k_ps_hist, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, owner_s, ns,
-                     nb, plen, W, vpad, tcnt, tbytes);
-  hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, s, tcnt, tbytes, nb, G, cnt_g_,
-                     replica ? rl_off_ + n : nullptr, cnt_s_, table, extras);
-  if (ns > 0)
-    hipLaunchKernelGGL(k_ps_scatter, dim3(G), dim3(kB), nb * sizeof(unsigned long long), s, ns, nb,
-                       plen, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
+    hipLaunchKernelGGL(k_ps_scatter, dim3(Gs), dim3(kB), nb * sizeof(unsigned long long), side_,
+                       ns, nb, plen_s, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
                        (uint64_t)(uintptr_t)svalues, owner_s, vpad, W, srec_, sval_, svoff_);
   RT_OK(hipGetLastError());
+  RT_OK(hipEventRecord(ev_pjoin_, side_));
+
+  // GET rows: owner (or bucket W = local replica hit), counting sort by owner
+  if (replica) replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
+  hipLaunchKernelGGL(k_route_hist, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, keys, n, rl_size,
+                     pts_, own_, npts_, W, plen_g, dest_g, ws_g);
+  hipLaunchKernelGGL(k_gr_scan, dim3(1), dim3(1024), 0, s, ws_g, (int64_t)nb * Gg, nb, Gg, cnt_g_,
+                     table, replica ? rl_off_ + n : nullptr, extras);
+  if (n > 0)
+    hipLaunchKernelGGL(k_gr_scatter, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, dest_g, n, nb,
+                       plen_g, ws_g, (const uint32_t*)keys, 4, (uint32_t*)gk_, perm_g_);
+  RT_OK(hipGetLastError());
+  RT_OK(hipStreamWaitEvent(s, ev_pjoin_, 0));  // join: the table is complete
 }
 
 std::vector<int64_t> RoutedStep::read_counts(const int64_t* rtable, hipStream_t s) {
   const int W = w_;
   rtable_ = rtable;
-  RT_OK(hipMemcpyAsync(host_, table_, 3 * W * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  RT_OK(hipMemcpyAsync(host_ + 3 * W, rtable, 3 * W * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  RT_OK(hipMemcpyAsync(host_ + 6 * W, bufs_[kExtras].p, 2 * sizeof(int64_t),
-                       hipMemcpyDeviceToHost, s));
+  SH_CHECK(rtable == table_ + 3 * W, "RoutedStep: rtable must follow table (one D2H)");
+  RT_OK(hipMemcpyAsync(host_, table_, (6 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   RT_OK(hipStreamSynchronize(s));
   std::vector<int64_t> out(host_, host_ + 6 * W + 2);
   n_local_ = out[6 * W];

@@ -321,7 +321,8 @@ class ShardedCache:
         e = self._engine
         if e is None:
             e = self._engine = c.RoutedStep(w, me, dev.index)
-            self._xtable = torch.empty((2, w, 3), dtype=i64, device=dev)
+            # [table (3w) | rtable (3w) | extras (2)]: read back with one copy
+            self._xtable = torch.empty(6 * w + 2, dtype=i64, device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
         if fanout and self._hot_dir is None:
@@ -329,7 +330,7 @@ class ShardedCache:
         e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0,
                   self._hot_dir.data_ptr() if fanout else 0)
         rep = self.replica._impl if self.replica is not None else None
-        table, rtable = self._xtable[0], self._xtable[1]
+        table, rtable = self._xtable[: 3 * w], self._xtable[3 * w: 6 * w]
         ph = _Phases("serve.")
         ph.next("plan")
         e.plan(keys.data_ptr(), n, rep, now, batch.keys.data_ptr(), batch.vlen.data_ptr(),

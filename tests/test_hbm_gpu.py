@@ -210,7 +210,10 @@ def test_reserve_lookup_survives_queued_set_gpu(cuda_dev):
     check_reserve_lookup_survives_queued_set(cuda_dev)
 
 
-def test_serve_overlapped_matches_get_then_set(cuda_dev):
+@pytest.mark.parametrize("side_stream", [True, False])
+def test_serve_overlapped_matches_get_then_set(cuda_dev, side_stream):
+    """serve() (reserved lookup; SET chain on a side stream concurrently with the
+    gather, or in stream order) returns what get() then set() returns."""
     from shellac_amd.bench.workload import Workload
     from shellac_amd.models.sharded_cache import ShardedCache
 
@@ -218,6 +221,7 @@ def test_serve_overlapped_matches_get_then_set(cuda_dev):
     outs = []
     for mode in ("serve", "seq"):
         sc = ShardedCache(CacheShard(256 << 20, 1 << 14, 1 << 16, cuda_dev))
+        sc.overlap_store = side_stream
         for s0 in range(0, 20000, 5000):
             sc.set(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev)))
         keys = wl.digests.index_select(0, wl.sample_ids(4096, 3)).contiguous()
