@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--client-threads", type=int, default=8)
     ap.add_argument("--objects", type=int, default=1000)
     ap.add_argument("--body", type=int, default=4096, help="origin body bytes (before gzip)")
-    ap.add_argument("--requests", type=int, default=200000)
+    ap.add_argument("--requests", type=int, default=500000)
     ap.add_argument("--miss-requests", type=int, default=50000)
     ap.add_argument("--origin", choices=["native", "python"], default="native",
                     help="native = C++ epoll origin (csrc/origin.cc); python = http.server")
@@ -69,14 +69,14 @@ def main():
     for conc in (10, 1000):
         r = run(url, a.requests, conc, True, hdr, a.depth, a.client_threads, paths=paths)
         out[f"hit_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
-        print(f"[http] hit c={conc}: {r['rps']:.0f} rps p50 {r['latency_ms']['p50']:.3f} ms "
+        print(f"[http] hit c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}) p50 {r['latency_ms']['p50']:.3f} ms "
               f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
     # misses: unique gzip URLs, every one forwarded to the origin and filled into the cache
     for conc in (10, 100):
         miss_paths = [f"/gz/miss{conc}/{i}.html" for i in range(a.miss_requests)]
         r = run(url, a.miss_requests, conc, True, hdr, 1, a.client_threads, paths=miss_paths)
         out[f"miss_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
-        print(f"[http] miss c={conc}: {r['rps']:.0f} rps p50 {r['latency_ms']['p50']:.3f} ms "
+        print(f"[http] miss c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}) p50 {r['latency_ms']['p50']:.3f} ms "
               f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
     out["proxy_stats"] = px.stats()
     out["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024

@@ -86,10 +86,12 @@ PYBIND11_MODULE(_shellac_core, m) {
         return c.wait_host_slot(i, timeout_ms);
       }, py::arg("slot"), py::arg("timeout_ms") = 10000)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
-                        uintptr_t s) {
+                        uintptr_t s, uint64_t out_cap) {
         py::gil_scoped_release nogil;
-        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s));
-      })
+        c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s),
+                 out_cap);
+      }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
+         py::arg("out_cap") = ~0ull)
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s) {
