@@ -52,9 +52,11 @@ def parse():
     ap.add_argument("--log-gb", type=float, default=16.0, help="value-log GiB per shard")
     ap.add_argument("--set-dist", choices=["uniform", "zipf"], default="uniform",
                     help="SET popularity: uniform (TTL refresh fills, default) or zipf")
-    ap.add_argument("--replicate", type=int, default=2 << 20,
-                    help="hot objects replicated on every rank (N>1; 0 = off)")
-    ap.add_argument("--replica-gb", type=float, default=4.0)
+    ap.add_argument("--replicate", type=int, default=None,
+                    help="hot objects replicated on every rank (N>1; 0 = off). Default: 4M "
+                         "up to 4 ranks, 2M at 8 (see docs/PERF.md, link model)")
+    ap.add_argument("--replica-gb", type=float, default=None,
+                    help="replica log GiB (default: 2 KiB per replicated object)")
     ap.add_argument("--sample-batches", type=int, default=32,
                     help="GET batches (independent of the timed ones) observed to pick the "
                          "replicated hot set")
@@ -141,6 +143,13 @@ def main():
         world = sim
     real_world = 1 if sim else world
 
+    if args.replicate is None:
+        # xGMI is point-to-point: N ranks talk over N-1 links each, so at small N the
+        # links bound the step and a bigger replica (fewer remote GETs, more SET fan-out)
+        # pays; at N=8 the step is compute-bound and the smaller replica is cheaper
+        args.replicate = (4 << 20) if world <= 4 else (2 << 20)
+    if args.replica_gb is None:
+        args.replica_gb = args.replicate * 2048 / (1 << 30)
     total_keys = args.keys_per_gpu * world
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
