@@ -38,6 +38,9 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
     # (excludes connection setup, which ab's total time includes: ~80 ms for 1000
     # connections here, 10 % of a 200K-request run)
     steady = 0.0
+    starts = np.sort(np.asarray(res["start"])) if done else np.zeros(1)
+    # ramp: when the c-th request left, i.e. every connection is up and busy
+    ramp_ms = float(starts[min(int(concurrency), len(starts)) - 1]) * 1e3
     if done >= 100:
         end = np.asarray(res["start"]) + np.asarray(res["latency"])
         a, b = np.percentile(end, [10, 90])
@@ -47,6 +50,8 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
         "elapsed_s": el,
         "rps": done / el if el > 0 else 0.0,
         "steady_rps": steady,
+        "ramp_ms": ramp_ms,
+        "connect_ms": float(res["connected_s"]) * 1e3,
         "transfer_MBps": res["bytes"] / el / 1e6 if el > 0 else 0.0,
         "errors": int(res["errors"]),
         "non2xx": int(res["non2xx"]),

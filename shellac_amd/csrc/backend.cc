@@ -115,25 +115,27 @@ TieredBackend::TieredBackend(std::shared_ptr<CacheBackend> l1, std::shared_ptr<C
 }
 
 void TieredBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
-  auto l2 = l2_;
-  auto l1 = l1_;
-  const uint32_t pttl = promote_ttl_;
-  l1_->get(key, d, ex, [this, key, d, ex, done, l1, l2, pttl](bool hit, CacheValue v) {
+  // Raw level pointers in the callbacks: the levels live as long as this object, which
+  // (like `this` below) must outlive its requests. Copying the shared_ptrs per request
+  // made every reactor thread bump the same two reference counts (c=10 hit path:
+  // 666K -> see docs/PERF.md).
+  CacheBackend* l2 = l2_.get();
+  l1_->get(key, d, ex, [this, key, d, ex, l2, done = std::move(done)](bool hit,
+                                                                      CacheValue v) mutable {
     if (hit) {
-      l1_hits_++;
+      l1_hits_.fetch_add(1, std::memory_order_relaxed);
       done(true, std::move(v));
       return;
     }
-    l2->get(key, d, ex, [this, key, d, done, l1, pttl](bool hit2, CacheValue v2) {
+    l2->get(key, d, ex, [this, key, d, done = std::move(done)](bool hit2, CacheValue v2) {
       if (hit2 && v2.data) {
-        l2_hits_++;
-        if (v2.ttl_left > 0 || v2.ttl_left == 0 || v2.ttl_left == -1) {
-          const uint32_t ttl = v2.ttl_left > 0 ? (uint32_t)v2.ttl_left
-                                               : (v2.ttl_left == 0 ? 0u : pttl);
-          l1->set(key, d, v2.data, v2.flags, ttl);  // promote
-        }
+        l2_hits_.fetch_add(1, std::memory_order_relaxed);
+        // promote with the L2 entry's remaining TTL (0 = no expiry, -1 = unknown)
+        const uint32_t ttl = v2.ttl_left > 0 ? (uint32_t)v2.ttl_left
+                                             : (v2.ttl_left == 0 ? 0u : promote_ttl_);
+        l1_->set(key, d, v2.data, v2.flags, ttl);
       } else {
-        misses_++;
+        misses_.fetch_add(1, std::memory_order_relaxed);
       }
       done(hit2, std::move(v2));
     });

@@ -106,6 +106,7 @@ void bind_net(py::module_& m) {
     py::dict d;
     d["completed"] = r.completed;
     d["elapsed_s"] = r.elapsed_s;
+    d["connected_s"] = r.connected_s;
     d["bytes"] = r.bytes;
     d["errors"] = r.errors;
     d["non2xx"] = r.non2xx;

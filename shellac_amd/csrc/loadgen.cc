@@ -40,6 +40,7 @@ LoadResult run_load(const LoadConfig& cfg) {
   std::atomic<int64_t> issued{0};
   std::vector<std::vector<LoadSample>> per_thread(cfg.threads);
   std::atomic<uint64_t> bytes{0}, errors{0}, non2xx{0}, reconnects{0};
+  std::vector<double> connected_at(cfg.threads, 0.0);  // last connection up, per thread
   const double t_start = now_s();
 
   // serialized requests, one per path (built once)
@@ -139,6 +140,7 @@ LoadResult run_load(const LoadConfig& cfg) {
               continue;
             }
             c.connected = true;
+            connected_at[tid] = std::max(connected_at[tid], now_s() - t_start);
           }
         }
         flush(c);
@@ -214,6 +216,7 @@ LoadResult run_load(const LoadConfig& cfg) {
   res.errors = errors;
   res.non2xx = non2xx;
   res.reconnects = reconnects;
+  res.connected_s = *std::max_element(connected_at.begin(), connected_at.end());
   return res;
 }
 

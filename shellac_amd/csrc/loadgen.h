@@ -32,6 +32,7 @@ struct LoadResult {
   std::vector<LoadSample> samples;
   uint64_t completed = 0, bytes = 0, errors = 0, non2xx = 0, reconnects = 0;
   double elapsed_s = 0;
+  double connected_s = 0;  // when the last connection completed its handshake
 };
 
 LoadResult run_load(const LoadConfig& cfg);
