@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Host-observed latency of one micro-batch GET (the proxy's HBM hit path) against the
+floor of a launch round trip: k_small_get with the completion slot, with a stream sync,
+and an empty-ish kernel (torch fill of one element) + sync, median of 2000 runs."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from shellac_amd.ops.cache import CacheShard, digest_strings  # noqa: E402
+
+
+def med(fn, iters=2000):
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return round(ts[len(ts) // 2] * 1e6, 1), round(ts[int(len(ts) * 0.99)] * 1e6, 1)
+
+
+dev = torch.device("cuda", 0)
+shard = CacheShard(1 << 30, 1 << 16, 1 << 16, dev)
+keys = [f"/lat/{i}".encode() for i in range(4096)]
+shard.set_many(keys, [b"x" * 4096] * 4096)
+torch.cuda.synchronize()
+s = torch.cuda.current_stream(dev).cuda_stream
+imp = shard._impl
+x = torch.zeros(1, device=dev)
+print("empty kernel + sync (p50, p99 us)", med(lambda: (x.fill_(1.0), torch.cuda.synchronize())))
+for n in (1, 10, 100, 1000):
+    req = digest_strings(keys[:n], "cpu")
+    pin_k = req.pin_memory()
+    out = torch.empty(n * 4200 + 4096, dtype=torch.uint8).pin_memory()
+    off = torch.empty(n + 1, dtype=torch.int64).pin_memory()
+    now = shard.now()
+
+    def sync_path():
+        imp.small_get(pin_k.data_ptr(), n, out.data_ptr(), out.numel(), off.data_ptr(), now, s, -1)
+        torch.cuda.synchronize()
+
+    def slot_path():
+        imp.small_get(pin_k.data_ptr(), n, out.data_ptr(), out.numel(), off.data_ptr(), now, s, 7)
+        imp.wait_host_slot(7, 10000)
+
+    print(f"n={n}: small_get+sync {med(sync_path)}  small_get+slot {med(slot_path)}", flush=True)

@@ -255,6 +255,10 @@ void HbmBackend::loop() {
   }
 }
 
+// Host slot the small-GET kernel signals completion through (this backend owns its
+// HbmCache instances, so no other user shares the slot).
+constexpr int kDoneSlot = HbmCache::kHostSlots - 1;
+
 void HbmBackend::run_batch(std::vector<Req>& batch) {
   TraceRange tr("hbm_backend.batch");
   const size_t nd = devs_.size();
@@ -275,9 +279,10 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     dv.ensure_out(1);
     for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[gets[k][j]].d;
     if ((int64_t)n <= HbmCache::kSmallGetMax) {
-      // one launch, no copies: keys, offsets and values all live in mapped host memory
+      // one launch, no copies: keys, offsets and values all live in mapped host memory;
+      // the kernel's last workgroup signals completion through a pinned host slot
       dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
-                          tnow, dv.stream);
+                          tnow, dv.stream, kDoneSlot);
       continue;
     }
     HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
@@ -290,11 +295,15 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     const size_t n = gets[k].size();
     if (!n) continue;
     dv.set_device();
-    HB_OK(hipStreamSynchronize(dv.stream));
+    const bool small = (int64_t)n <= HbmCache::kSmallGetMax;
+    if (small)
+      dv.cache->wait_host_slot(kDoneSlot, 10000);  // no stream sync on the hit path
+    else
+      HB_OK(hipStreamSynchronize(dv.stream));
     const uint64_t total = dv.h_off[n];
     if (total > dv.out_cap) {  // rare: grow the zero-copy buffer and gather again
       dv.ensure_out(total);
-      if ((int64_t)n <= HbmCache::kSmallGetMax)
+      if (small)
         dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
                             tnow, dv.stream);
       else
@@ -306,8 +315,6 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     Dev& dv = *devs_[k];
     const size_t n = gets[k].size();
     if (!n) continue;
-    dv.set_device();
-    HB_OK(hipStreamSynchronize(dv.stream));
     for (size_t j = 0; j < n; ++j) {
       Req& r = batch[gets[k][j]];
       const uint64_t o = dv.h_off[j], sz = dv.h_off[j + 1] - o;
@@ -364,6 +371,7 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
     const size_t n = dels[k].size();
+    if (!n && sets[k].empty()) continue;  // GET-only batch: nothing left on the stream
     dv.set_device();
     if (n) {
       HB_OK(hipStreamSynchronize(dv.stream));  // staging reuse after SET

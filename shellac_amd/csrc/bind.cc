@@ -75,11 +75,13 @@ PYBIND11_MODULE(_shellac_core, m) {
       }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
          py::arg("now"), py::arg("stream"), py::arg("reserve") = 0, py::arg("total_slot") = -1)
       .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
-                           uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s) {
+                           uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s,
+                           int done_slot) {
         py::gil_scoped_release nogil;
         c.small_get(P<const Digest>(keys), n, P<uint8_t>(out), out_cap, P<uint64_t>(off), now,
-                    S(s));
-      })
+                    S(s), done_slot);
+      }, py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
+         py::arg("now"), py::arg("stream"), py::arg("done_slot") = -1)
       .def("host_slot", &HbmCache::host_slot)
       .def("wait_host_slot", [](const HbmCache& c, int i, int64_t timeout_ms) {
         py::gil_scoped_release nogil;

@@ -56,8 +56,11 @@ class HbmCache {
   // Small batches (n <= 2048, the proxy's micro-batches): lookup + scan + gather in one
   // launch. keys / out / off may be mapped host memory (no copies); off[0..n] is always
   // written, the bytes only when off[n] <= out_cap.
+  // `done_slot` >= 0: the kernel's last workgroup writes off[n] into that host slot
+  // after every output byte is visible to the host, so wait_host_slot(done_slot)
+  // replaces a stream synchronisation (one batch in flight per slot).
   void small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap, uint64_t* off,
-                 uint32_t now, hipStream_t s);
+                 uint32_t now, hipStream_t s, int done_slot = -1);
   static constexpr int64_t kSmallGetMax = 2048;
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
@@ -110,6 +113,7 @@ class HbmCache {
   uint64_t* part_ = nullptr;         // per-workgroup size sums: [0,kMaxGrid) GET, then SET
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
   uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
+  unsigned int* done_ctr_ = nullptr; // device: small_get workgroups finished (self-resetting)
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;

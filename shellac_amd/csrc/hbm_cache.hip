@@ -513,7 +513,8 @@ __global__ __launch_bounds__(kBlock) void k_small_get(
     const Digest* __restrict__ keys, int64_t n, const Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now,
     const uint8_t* __restrict__ log, uint8_t* __restrict__ out, uint64_t out_cap,
-    uint64_t* __restrict__ off_out, CacheCounters* __restrict__ ctr) {
+    uint64_t* __restrict__ off_out, CacheCounters* __restrict__ ctr,
+    unsigned int* __restrict__ done_ctr, uint64_t* __restrict__ done_slot) {
   __shared__ uint64_t s_off[kSmallGet + 1];
   __shared__ uint64_t s_loc[kSmallGet];
   __shared__ unsigned long long s_w[kBlock / 64];
@@ -578,9 +579,9 @@ __global__ __launch_bounds__(kBlock) void k_small_get(
   if (blockIdx.x == 0)
     block_count(ctr, (unsigned long long)(threadIdx.x == 0 ? n : 0), &CacheCounters::get_ops, hits,
                 &CacheCounters::get_hits, bytes, &CacheCounters::get_bytes);
-  if (total > out_cap) return;  // the caller sees total in off_out and retries bigger
-  // copy: this workgroup's contiguous share of the response chunks
-  const int64_t nchunks = (int64_t)(total >> 4);
+  // copy (skipped when it does not fit: the caller sees total in off_out and retries
+  // bigger): this workgroup's contiguous share of the response chunks
+  const int64_t nchunks = total > out_cap ? 0 : (int64_t)(total >> 4);
   const int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * span, c1 = min(nchunks, c0 + span);
   int jl = 0;
@@ -596,6 +597,22 @@ __global__ __launch_bounds__(kBlock) void k_small_get(
     const u32x4 v = __builtin_nontemporal_load(
         reinterpret_cast<const u32x4*>(log + s_loc[lo] + w));
     *reinterpret_cast<u32x4*>(out + x) = v;
+  }
+  // Completion signal without a stream sync: every workgroup makes its offset / value
+  // stores (mapped host memory) visible system-wide, then counts itself done; the last
+  // one resets the counter for the next launch and publishes the total into a pinned
+  // host slot the batcher thread spins on.
+  if (done_slot) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int prev = atomicAdd(done_ctr, 1u);
+      if (prev == gridDim.x - 1) {
+        atomicExch(done_ctr, 0u);
+        __threadfence_system();
+        __hip_atomic_store(done_slot, total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -1061,6 +1078,8 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&head_, 64));
   HIP_OK(hipMalloc(&ctr_, kCtrShards * sizeof(CacheCounters)));
   HIP_OK(hipMalloc(&scratch_, 64));
+  HIP_OK(hipMalloc(&done_ctr_, 64));
+  HIP_OK(hipMemset(done_ctr_, 0, 64));
   HIP_OK(hipMalloc(&part_, 2 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
@@ -1080,6 +1099,7 @@ HbmCache::~HbmCache() {
   (void)hipFree(head_);
   (void)hipFree(ctr_);
   (void)hipFree(scratch_);
+  (void)hipFree(done_ctr_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -1165,16 +1185,19 @@ uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
 }
 
 void HbmCache::small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap,
-                         uint64_t* off, uint32_t now, hipStream_t s) {
+                         uint64_t* off, uint32_t now, hipStream_t s, int done_slot) {
   SH_CHECK(n >= 0 && n <= kSmallGet, "small_get batch too large");
+  SH_CHECK(done_slot < kHostSlots, "host slot out of range");
   TraceRange tr("hbm.small_get");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
+  uint64_t* ds = done_slot >= 0 ? host_slots_ + done_slot : nullptr;
+  if (ds) __atomic_store_n(ds, kSlotPending, __ATOMIC_RELEASE);
   // ~64 KiB of response per workgroup at 4 KiB values; >= 1
   const int grid = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / 8));
   hipLaunchKernelGGL(k_small_get, dim3(grid), dim3(kBlock), 0, s, keys, n, index_,
                      cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, log_, out, out_cap, off,
-                     ctr_);
+                     ctr_, ds ? done_ctr_ : nullptr, ds);
   HIP_OK(hipGetLastError());
 }
 

@@ -199,16 +199,19 @@ class CacheShard:
         return int(self._impl.wait_host_slot(slot, timeout_ms))
 
     def small_get(self, keys: torch.Tensor, out_cap: int = 16 << 20,
-                  now: Optional[int] = None):
+                  now: Optional[int] = None, done_slot: int = -1):
         """GPU, n <= 2048: lookup + scan + gather in one kernel (the proxy's micro-batch
-        path). Returns (out bytes, off[n+1]); off[n] > out_cap means nothing was copied."""
+        path). Returns (out bytes, off[n+1]); off[n] > out_cap means nothing was copied.
+        ``done_slot`` >= 0: the kernel's last workgroup publishes off[n] into that host
+        slot once every output byte is visible; ``host_total(done_slot)`` then replaces
+        a stream synchronisation."""
         assert self.is_gpu and keys.shape[0] <= 2048
         self._check(keys, "keys")
         n = keys.shape[0]
         out = torch.empty(max(int(out_cap), 16), dtype=torch.uint8, device=self.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         self._impl.small_get(keys.data_ptr(), n, out.data_ptr(), int(out_cap), off.data_ptr(),
-                             self.now() if now is None else now, self._s())
+                             self.now() if now is None else now, self._s(), int(done_slot))
         return out, off
 
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,

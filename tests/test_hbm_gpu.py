@@ -382,3 +382,27 @@ def test_small_get_matches_lookup_gather(cuda_dev, n):
         out2, off2 = shard.small_get(req, out_cap=total - 16)
         assert int(off2[-1]) == total
         assert not torch.equal(out2[:64].cpu(), ref[:64].cpu()) or total == 0
+
+
+@pytest.mark.parametrize("n", [1, 64, 2048])
+def test_small_get_completion_slot(cuda_dev, n):
+    """With a done slot, the host learns the batch finished from the pinned slot (the
+    last workgroup's system-scope store) and may read the output without a stream
+    sync; repeated launches reuse the self-resetting workgroup counter."""
+    shard = CacheShard(64 << 20, 1 << 14, 1 << 14, cuda_dev)
+    keys = [f"/done/{i}".encode() for i in range(3000)]
+    vals = [bytes([i % 251]) * (16 + i * 13 % 3000) for i in range(3000)]
+    shard.set_many(keys[:2500], vals[:2500])
+    torch.cuda.synchronize()
+    for rep in range(3):
+        idx = [(i * 7 + rep) % 3000 for i in range(n)]
+        req = digest_strings([keys[i] for i in idx], cuda_dev)
+        torch.cuda.synchronize()
+        out, off = shard.small_get(req, done_slot=5)
+        total = shard.host_total(5)  # spins on the slot; no torch.cuda.synchronize()
+        assert total == int(off[-1])
+        got = unpack_records(out, off[:-1], off[1:] - off[:-1])
+        for i, g in zip(idx, got):
+            assert (g is None) == (i >= 2500)
+            if g is not None:
+                assert g[0] == vals[i]
