@@ -47,3 +47,36 @@ for n in (1, 10, 100, 1000):
         imp.wait_host_slot(7, 10000)
 
     print(f"n={n}: small_get+sync {med(sync_path)}  small_get+slot {med(slot_path)}", flush=True)
+
+# SET micro-batches: the launched chain (5 kernels) vs one replayed graph, both reading
+# zero-copy staging in mapped pinned memory, + stream sync
+from shellac_amd._native import core  # noqa: E402
+
+cls = 64
+hk = torch.zeros((cls, 2), dtype=torch.int64).pin_memory()
+hv = torch.zeros(cls * 4096 + 16, dtype=torch.uint8).pin_memory()
+ho = (torch.arange(cls, dtype=torch.int64) * 4096).pin_memory()
+hm = torch.zeros(3 * cls, dtype=torch.int32).pin_memory()
+hk[:] = digest_strings([f"/set/{i}".encode() for i in range(cls)], "cpu")
+hm[:cls] = 4000
+g = core().StoreGraph()
+now = shard.now()
+side = torch.cuda.Stream(device=dev)  # capturable (not the legacy default stream)
+s = side.cuda_stream
+p = [t.data_ptr() for t in (hk, hv, ho)] + [hm.data_ptr(), hm.data_ptr() + 4 * cls,
+                                            hm.data_ptr() + 8 * cls]
+
+
+def set_launch():
+    imp.store(p[0], p[1], p[2], p[3], p[4], p[5], cls, 1 << 20, now, s)
+    torch.cuda.synchronize()
+
+
+def set_graph():
+    imp.store_graph(g, p[0], p[1], p[2], p[3], p[4], p[5], cls, 1 << 20, now, s)
+    torch.cuda.synchronize()
+
+
+print(f"SET n={cls}: launched chain + sync {med(set_launch, 1000)}  graph + sync "
+      f"{med(set_graph, 1000)} (captures {g.captures})", flush=True)
+g.destroy()

@@ -15,6 +15,8 @@
 //                     persistent connections, with node ejection + retry.
 #pragma once
 
+#include <cstdlib>
+
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -115,6 +117,10 @@ class HbmBackend : public CacheBackend {
   void stats(StatList* out) override;
 
  private:
+  const bool set_graphs_ = [] {
+    const char* e = std::getenv("SHELLAC_SET_GRAPH");
+    return e && e[0] == '1';
+  }();
   struct Req {
     int kind;  // 0 get, 1 set, 2 del
     Digest d;

@@ -57,6 +57,12 @@ PYBIND11_MODULE(_shellac_core, m) {
   m.def("item_bytes", [](uint32_t vlen) { return item_bytes(vlen); });
 
   // ---------------- device (HIP) ----------------
+  py::class_<HbmCache::StoreGraph>(m, "StoreGraph")
+      .def(py::init<>())
+      .def_readonly("captures", &HbmCache::StoreGraph::captures)
+      .def_readonly("launches", &HbmCache::StoreGraph::launches)
+      .def("destroy", [](HbmCache::StoreGraph& g) { HbmCache::destroy_graph(&g); });
+
   py::class_<HbmCache>(m, "HbmCache")
       .def(py::init([](uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int device) {
              ShardConfig c;
@@ -94,6 +100,16 @@ PYBIND11_MODULE(_shellac_core, m) {
                  out_cap);
       }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
          py::arg("out_cap") = ~0ull)
+      .def("store_graph", [](HbmCache& c, HbmCache::StoreGraph& g, uintptr_t keys,
+                             uintptr_t values, uintptr_t val_off, uintptr_t vlen, uintptr_t flags,
+                             uintptr_t expire, int64_t n, uint64_t bytes_bound, uint32_t now,
+                             uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.store_graph(&g, P<const Digest>(keys), P<const uint8_t>(values),
+                      P<const uint64_t>(val_off), P<const uint32_t>(vlen),
+                      P<const uint32_t>(flags), P<const uint32_t>(expire), n, bytes_bound, now,
+                      S(s));
+      })
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s) {

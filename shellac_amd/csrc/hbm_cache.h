@@ -73,6 +73,26 @@ class HbmCache {
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
              uint64_t bytes_bound, uint32_t now, hipStream_t s);
+  // SET through captured hipGraphs, for callers with fixed batch sizes and fixed
+  // staging buffers (the proxy's micro-batches, padded to a size class with
+  // vlen = kSkipVlen rows). The five SET kernels become one graph launch. A graph bakes
+  // in its pointers, `n`, `bytes_bound` and `now` and the head slot it reads, so `g`
+  // keeps one executable per head-slot parity and is re-captured whenever any of those
+  // (or the SET workspace) changes; `now` changes once a second.
+  struct StoreGraph {
+    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    const void* ptrs[6] = {};
+    int64_t n = -1;
+    uint64_t bound = 0;
+    uint32_t now = 0;
+    uint64_t ws_gen = 0;
+    uint64_t captures = 0, launches = 0;
+  };
+  void store_graph(StoreGraph* g, const Digest* keys, const uint8_t* values,
+                   const uint64_t* val_off, const uint32_t* vlen, const uint32_t* flags,
+                   const uint32_t* expire, int64_t n, uint64_t bytes_bound, uint32_t now,
+                   hipStream_t s);
+  static void destroy_graph(StoreGraph* g);
   // DELETE a batch; found[i] = 1 if a live entry was removed.
   void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now, hipStream_t s);
   // Reclaim index slots whose items expired or were overwritten. Synchronises;
@@ -122,7 +142,11 @@ class HbmCache {
   uint64_t* set_size_ = nullptr;
   uint64_t* set_off_ = nullptr;
   uint32_t dd_mask_ = 0;
+  uint64_t ws_gen_ = 0;  // bumped when the SET workspace moves (invalidates graphs)
   std::mutex mu_;
+  void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+                    const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
+                    int64_t n, uint32_t now, hipStream_t s);
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------

@@ -1133,6 +1133,7 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
   dd_mask_ = (uint32_t)(tslots - 1);
   set_cap_ = cap;
+  ++ws_gen_;
 }
 
 void HbmCache::reserve(int64_t n) {
@@ -1218,6 +1219,16 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, s);
+  store_locked(keys, values, val_off, vlen, flags, expire, n, now, s);
+  hsel_ ^= 1;  // later operations on the stream read the published slot
+}
+
+// The SET kernel chain (caller holds mu_, workspace sized): dedupe (last writer wins),
+// sizes + fused scan, log append (k_segcopy<1>), two-choice CAS index insert that also
+// publishes the new head into the other head slot.
+void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+                            const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
+                            int64_t n, uint32_t now, hipStream_t s) {
   const int grid = grid_for(n, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
@@ -1233,8 +1244,66 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                      cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_);
-  hsel_ ^= 1;  // later operations on the stream read the published slot
   HIP_OK(hipGetLastError());
+}
+
+void HbmCache::destroy_graph(StoreGraph* g) {
+  for (auto& e : g->exec)
+    if (e) {
+      (void)hipGraphExecDestroy(e);
+      e = nullptr;
+    }
+  g->n = -1;
+}
+
+void HbmCache::store_graph(StoreGraph* g, const Digest* keys, const uint8_t* values,
+                           const uint64_t* val_off, const uint32_t* vlen, const uint32_t* flags,
+                           const uint32_t* expire, int64_t n, uint64_t bytes_bound,
+                           uint32_t now, hipStream_t s) {
+  TraceRange tr("hbm.store_graph");
+  if (n <= 0) return;
+  SH_CHECK(s != nullptr, "store_graph needs a created stream (the legacy default stream "
+                         "cannot be captured)");
+  SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
+           "SET batch larger than half the log; split the batch");
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard dg(cfg_.device);
+  ensure_set_ws(n, s);  // before any capture: allocation is not capturable
+  const void* ptrs[6] = {keys, values, val_off, vlen, flags, expire};
+  bool same = g->n == n && g->bound == bytes_bound && g->now == now && g->ws_gen == ws_gen_ &&
+              g->exec[0] && g->exec[1];
+  for (int i = 0; same && i < 6; ++i) same = g->ptrs[i] == ptrs[i];
+  if (!same) {
+    destroy_graph(g);
+    const int keep = hsel_;
+    for (int p = 0; p < 2; ++p) {
+      hsel_ = p;  // the graph for parity p reads head slot p and publishes into 1 - p
+      hipGraph_t graph = nullptr;
+      HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+      try {
+        store_locked(keys, values, val_off, vlen, flags, expire, n, now, s);
+      } catch (...) {
+        (void)hipStreamEndCapture(s, &graph);
+        if (graph) (void)hipGraphDestroy(graph);
+        hsel_ = keep;
+        throw;
+      }
+      HIP_OK(hipStreamEndCapture(s, &graph));
+      const hipError_t e = hipGraphInstantiate(&g->exec[p], graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      HIP_OK(e);
+    }
+    hsel_ = keep;
+    for (int i = 0; i < 6; ++i) g->ptrs[i] = ptrs[i];
+    g->n = n;
+    g->bound = bytes_bound;
+    g->now = now;
+    g->ws_gen = ws_gen_;
+    g->captures++;
+  }
+  HIP_OK(hipGraphLaunch(g->exec[hsel_], s));
+  g->launches++;
+  hsel_ ^= 1;
 }
 
 void HbmCache::remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now, hipStream_t s) {

@@ -406,3 +406,51 @@ def test_small_get_completion_slot(cuda_dev, n):
             assert (g is None) == (i >= 2500)
             if g is not None:
                 assert g[0] == vals[i]
+
+
+def test_store_graph_matches_store(cuda_dev):
+    """A SET replayed from a captured hipGraph (fixed size class, skip-row padding, one
+    executable per head-slot parity) leaves the shard exactly as the launched SET
+    chain does; the graph is captured once per (pointers, n, now) and then replayed."""
+    from shellac_amd._native import core
+
+    cls = 64
+    a = CacheShard(8 << 20, 1 << 10, 1 << 12, cuda_dev)
+    b = CacheShard(8 << 20, 1 << 10, 1 << 12, cuda_dev)
+    g = core().StoreGraph()
+    now = a.now()
+    keys = torch.zeros((cls, 2), dtype=torch.int64, device=cuda_dev)
+    vals = torch.zeros(cls * 1024 + 16, dtype=torch.uint8, device=cuda_dev)
+    voff = torch.arange(cls, dtype=torch.int64, device=cuda_dev) * 1024
+    vlen = torch.empty(cls, dtype=torch.int32, device=cuda_dev)
+    flags = torch.zeros(cls, dtype=torch.int32, device=cuda_dev)
+    expire = torch.zeros(cls, dtype=torch.int32, device=cuda_dev)
+    side = torch.cuda.Stream(device=cuda_dev)  # the null stream cannot be captured
+    side.wait_stream(torch.cuda.current_stream(cuda_dev))
+    s = side.cuda_stream
+    rng = np.random.default_rng(3)
+    all_keys = []
+    torch.cuda.set_stream(side)
+    for step in range(40):  # several log wraps of the 8 MiB log
+        n = int(rng.integers(1, cls + 1))
+        ks = digest_strings([f"/g/{step}/{i % 23}".encode() for i in range(n)], cuda_dev)
+        all_keys.append(ks)
+        keys[:n] = ks
+        vals.copy_(torch.from_numpy(rng.integers(0, 256, vals.numel(), dtype=np.uint8)))
+        vlen.fill_(-1)  # skip rows
+        vlen[:n] = torch.from_numpy(rng.integers(1, 1000, n).astype(np.int32))
+        flags[:n] = step
+        a.store(keys[:n].contiguous(), vals, voff[:n].contiguous(), vlen[:n].contiguous(),
+                flags[:n].contiguous(), expire[:n].contiguous(), now)
+        b._impl.store_graph(g, keys.data_ptr(), vals.data_ptr(), voff.data_ptr(), vlen.data_ptr(),
+                            flags.data_ptr(), expire.data_ptr(), cls, 4 << 20, now, s)
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(torch.cuda.default_stream(cuda_dev))
+    assert g.launches == 40 and g.captures == 1
+    assert a.head() == b.head()
+    q = torch.cat(all_keys)
+    la, lb = a.lookup(q, now), b.lookup(q, now)
+    assert torch.equal(la.size, lb.size) and torch.equal(la.off, lb.off)
+    assert torch.equal(a.gather(la), b.gather(lb))
+    assert int((la.size > 0).sum()) > 0
+    g.destroy()
