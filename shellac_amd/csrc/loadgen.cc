@@ -85,7 +85,13 @@ LoadResult run_load(const LoadConfig& cfg) {
     };
     auto top_up = [&](LgConn& c) {  // keep `depth` requests in flight
       while ((int)c.sent.size() < cfg.depth) {
-        const int64_t k = issued.fetch_add(1);
+        // claim request k only while k < requests: a blind fetch_add past the end would
+        // inflate `issued`, and a thread whose connection died with requests in flight
+        // would then wrongly see nothing left to re-issue (lost requests)
+        int64_t k = issued.load();
+        do {
+          if (k >= cfg.requests) break;
+        } while (!issued.compare_exchange_weak(k, k + 1));
         if (k >= cfg.requests) break;
         c.out += req_bytes((size_t)k);
         c.sent.push_back(0);  // timestamp set at send
