@@ -201,7 +201,8 @@ void bind_net(py::module_& m) {
                        const std::string& policy, bool kill_switch, bool key_host,
                        int client_timeout, int client_max_reqs, const std::string& balance,
                        bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
-                       uint64_t stream_high_water) {
+                       uint64_t stream_high_water, const std::string& health_path,
+                       int health_interval_ms, int health_timeout_ms, int health_fails) {
              ProxyConfig c;
              c.upstreams = resolve_list(upstreams, 80);
              c.port = port;
@@ -219,6 +220,10 @@ void bind_net(py::module_& m) {
              c.upstream_retry_s = upstream_retry_s;
              c.stream_bytes = stream_bytes;
              c.stream_high_water = stream_high_water;
+             c.health_path = health_path;
+             c.health_interval_ms = health_interval_ms;
+             c.health_timeout_ms = health_timeout_ms;
+             c.health_fails = health_fails;
              std::shared_ptr<CacheBackend> be;
              if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
              c.cache_enabled = be != nullptr;
@@ -230,7 +235,9 @@ void bind_net(py::module_& m) {
            py::arg("key_host") = false, py::arg("client_timeout") = 30,
            py::arg("client_max_reqs") = 1000, py::arg("balance") = "random",
            py::arg("decode_gzip") = false, py::arg("upstream_retry_s") = 2,
-           py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20)
+           py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20,
+           py::arg("health_path") = "", py::arg("health_interval_ms") = 1000,
+           py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2)
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

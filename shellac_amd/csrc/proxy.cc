@@ -1,12 +1,15 @@
 // Native caching reverse proxy (see proxy.h for the reference map and fixes).
 #include "proxy.h"
 
+#include <poll.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/timerfd.h>
 #include <sys/uio.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <deque>
@@ -586,7 +589,7 @@ int Reactor::choose_server() {
 Upstream* Reactor::pick_upstream(Client* c) {
   const double t = now_s();
   auto valid = [&](Upstream* u) {
-    if (u->dead) return false;
+    if (u->dead || !px_->upstream_healthy(u->server)) return false;
     if (u->count >= u->ka_max) return false;
     return u->ka_timeout < 0 || t - u->atime < u->ka_timeout;
   };
@@ -1002,16 +1005,88 @@ Proxy::Proxy(const ProxyConfig& cfg, std::shared_ptr<CacheBackend> backend)
   SH_CHECK(cfg_.threads >= 1, "threads >= 1");
   if (cfg_.cache_enabled) SH_CHECK(backend_ != nullptr, "cache enabled without a backend");
   up_down_until_.reset(new std::atomic<double>[cfg_.upstreams.size()]);
-  for (size_t i = 0; i < cfg_.upstreams.size(); ++i) up_down_until_[i] = 0;
+  health_down_.reset(new std::atomic<bool>[cfg_.upstreams.size()]);
+  for (size_t i = 0; i < cfg_.upstreams.size(); ++i) {
+    up_down_until_[i] = 0;
+    health_down_[i] = false;
+  }
 }
 
 Proxy::~Proxy() {
   stop();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
+  if (health_th_.joinable()) health_th_.join();
 }
 
-bool Proxy::upstream_up(int idx, double now) const { return now >= up_down_until_[idx].load(); }
+bool Proxy::upstream_up(int idx, double now) const {
+  return !health_down_[idx].load(std::memory_order_relaxed) && now >= up_down_until_[idx].load();
+}
+
+// One health probe: connect, `GET path`, read the status line; true for a status < 400
+// within the timeout. Blocking I/O with poll() deadlines on the checker thread only.
+static bool probe_upstream(const Addr& a, const std::string& path, int timeout_ms) {
+  const double deadline = now_s() + timeout_ms * 1e-3;
+  auto left_ms = [&] { return std::max(0, (int)((deadline - now_s()) * 1e3)); };
+  const int fd = connect_nonblock(a);
+  if (fd < 0) return false;
+  bool ok = false;
+  pollfd pfd{fd, POLLOUT, 0};
+  if (poll(&pfd, 1, left_ms()) == 1 && (pfd.revents & POLLOUT)) {
+    int err = 0;
+    socklen_t el = sizeof err;
+    getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el);
+    const std::string req = "GET " + path + " HTTP/1.1\r\nHost: " + a.host +
+                            "\r\nUser-Agent: shellac-health\r\nConnection: close\r\n\r\n";
+    if (!err && send(fd, req.data(), req.size(), MSG_NOSIGNAL) == (ssize_t)req.size()) {
+      std::string head;
+      char buf[512];
+      while (head.find("\r\n") == std::string::npos && left_ms() > 0) {
+        pfd = pollfd{fd, POLLIN, 0};
+        if (poll(&pfd, 1, left_ms()) != 1) break;
+        const ssize_t k = recv(fd, buf, sizeof buf, 0);
+        if (k <= 0) break;
+        head.append(buf, (size_t)k);
+      }
+      // "HTTP/1.x SSS ..."
+      if (head.size() >= 12 && head.compare(0, 5, "HTTP/") == 0) {
+        const int status = std::atoi(head.c_str() + 9);
+        ok = status >= 100 && status < 400;
+      }
+    }
+  }
+  close(fd);
+  return ok;
+}
+
+void Proxy::health_loop() {
+  const size_t n = cfg_.upstreams.size();
+  std::vector<int> fails(n, 0), passes(n, 0);
+  while (running_) {
+    for (size_t i = 0; i < n && running_; ++i) {
+      const bool ok = probe_upstream(cfg_.upstreams[i], cfg_.health_path, cfg_.health_timeout_ms);
+      health_checks_++;
+      if (ok) {
+        fails[i] = 0;
+        if (health_down_[i] && ++passes[i] >= cfg_.health_passes) {
+          health_down_[i] = false;
+          health_transitions_++;
+        }
+      } else {
+        passes[i] = 0;
+        if (!health_down_[i] && ++fails[i] >= cfg_.health_fails) {
+          health_down_[i] = true;
+          health_transitions_++;
+        }
+      }
+    }
+    // sleep in small slices so stop() is prompt
+    const double until = now_s() + cfg_.health_interval_ms * 1e-3;
+    while (running_ && now_s() < until)
+      std::this_thread::sleep_for(std::chrono::milliseconds(
+          std::min(20, std::max(1, (int)((until - now_s()) * 1e3)))));
+  }
+}
 
 void Proxy::upstream_failed(int idx, double now) {
   up_down_until_[idx] = now + cfg_.upstream_retry_s;
@@ -1031,6 +1106,7 @@ void Proxy::start() {
     Reactor* rp = r.get();
     threads_.emplace_back([rp] { rp->loop(); });
   }
+  if (!cfg_.health_path.empty()) health_th_ = std::thread([this] { health_loop(); });
 }
 
 void Proxy::wait() {
@@ -1077,6 +1153,11 @@ std::string Proxy::stats_json() {
     << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
     << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
     << total << "}";
+  o << ",\"health_checks\":" << health_checks_.load()
+    << ",\"health_transitions\":" << health_transitions_.load() << ",\"upstreams_up\":[";
+  const double tn = now_s();
+  for (size_t i = 0; i < cfg_.upstreams.size(); ++i) o << (i ? "," : "") << (upstream_up((int)i, tn) ? 1 : 0);
+  o << "]";
   if (backend_) {
     StatList st;
     backend_->stats(&st);

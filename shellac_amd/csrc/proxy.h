@@ -48,6 +48,16 @@ struct ProxyConfig {
   int client_max_reqs = 1000;         // CLIENT_MAX_REQS (Server.py:24)
   std::string balance = "random";     // random (ref :123) | roundrobin | leastconn
   int upstream_retry_s = 2;           // a failed upstream is skipped for this long
+  // Active health checks (the reference's "todo: check that servers are responsive",
+  // Server.py:532): when `health_path` is set, a checker thread sends
+  // `GET <health_path>` to every upstream each `health_interval_ms`; `health_fails`
+  // consecutive failures (connect error, timeout, or a status >= 400) take it out of
+  // rotation, `health_passes` consecutive successes bring it back.
+  std::string health_path;
+  int health_interval_ms = 1000;
+  int health_timeout_ms = 500;
+  int health_fails = 2;
+  int health_passes = 1;
   bool decode_gzip = false;           // inflate + re-deflate every miss like the reference
   // Responses whose body exceeds this are streamed to the client as they arrive and not
   // cached (the reference buffers every object whole, Server.py:408-421).
@@ -74,8 +84,9 @@ class Proxy {
   const ProxyConfig& config() const { return cfg_; }
   CacheBackend* backend() { return backend_.get(); }
 
-  // upstream health (shared by all reactors)
+  // upstream health (shared by all reactors): passive (failed connects) and active
   bool upstream_up(int idx, double now) const;
+  bool upstream_healthy(int idx) const { return !health_down_[idx].load(); }
   void upstream_failed(int idx, double now);
   int next_rr() { return rr_++; }
 
@@ -88,6 +99,10 @@ class Proxy {
   std::atomic<bool> running_{false};
   uint16_t port_ = 0;
   std::unique_ptr<std::atomic<double>[]> up_down_until_;
+  std::unique_ptr<std::atomic<bool>[]> health_down_;
+  std::atomic<uint64_t> health_checks_{0}, health_transitions_{0};
+  std::thread health_th_;
+  void health_loop();
   std::atomic<int> rr_{0};
   std::mutex wait_mu_;
   double start_time_ = 0;

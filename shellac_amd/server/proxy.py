@@ -105,6 +105,8 @@ class Server:
                  client_timeout: int = 30, client_max_reqs: int = 1000,
                  balance: str = "random", bind: str = "0.0.0.0", decode_gzip: bool = False,
                  stream_bytes: int = 1 << 20, stream_high_water: int = 8 << 20,
+                 health_path: str = "", health_interval_ms: int = 1000,
+                 health_timeout_ms: int = 500, health_fails: int = 2,
                  **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
@@ -117,7 +119,9 @@ class Server:
             compress=compress, policy=policy, kill_switch=kill_switch, key_host=key_host,
             client_timeout=client_timeout, client_max_reqs=client_max_reqs, balance=balance,
             decode_gzip=decode_gzip, stream_bytes=stream_bytes,
-            stream_high_water=stream_high_water)
+            stream_high_water=stream_high_water, health_path=health_path,
+            health_interval_ms=health_interval_ms, health_timeout_ms=health_timeout_ms,
+            health_fails=health_fails)
         self._started = False
 
     @property
@@ -189,6 +193,12 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--client-timeout", type=int, default=30)
     p.add_argument("--client-max-reqs", type=int, default=1000)
     p.add_argument("--key-host", action="store_true", help="include Host in the cache key")
+    p.add_argument("--health-check", default="", metavar="PATH",
+                   help="actively probe every upstream with GET PATH (the reference's TODO "
+                        "'check that servers are responsive', Server.py:532)")
+    p.add_argument("--health-interval-ms", type=int, default=1000)
+    p.add_argument("--health-fails", type=int, default=2,
+                   help="consecutive failed probes that take an upstream out of rotation")
     p.add_argument("--no-kill-switch", action="store_true", help="disable GET /kill")
     p.add_argument("--fault", default="",
                    help="fault injection on the cache tier, e.g. get_miss=0.1,set_drop=0.5,"
@@ -217,7 +227,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  kill_switch=not args.no_kill_switch, key_host=args.key_host,
                  client_timeout=args.client_timeout, client_max_reqs=args.client_max_reqs,
                  balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
-                 stream_bytes=args.stream_bytes,
+                 stream_bytes=args.stream_bytes, health_path=args.health_check,
+                 health_interval_ms=args.health_interval_ms, health_fails=args.health_fails,
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}

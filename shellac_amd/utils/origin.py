@@ -14,6 +14,7 @@ class Origin:
                  keep_alive: bool = True):
         self.hits: Counter = Counter()
         self.lock = threading.Lock()
+        self.healthy = True  # GET /health answers 200, or 503 when False
         outer = self
 
         class H(BaseHTTPRequestHandler):
@@ -32,6 +33,15 @@ class Origin:
 
                     time.sleep(delay_s)
                 path = self.path
+                if path == "/health":
+                    code = 200 if outer.healthy else 503
+                    body = b"ok\n" if outer.healthy else b"sick\n"
+                    self.send_response(code)
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    if not head:
+                        self.wfile.write(body)
+                    return
                 if path.startswith("/status/"):
                     code = int(path.split("/")[2])
                     body = f"status {code}\n".encode()

@@ -397,3 +397,38 @@ def test_native_origin_behind_proxy():
             assert px.stats()["cache_hits"] == 1
     finally:
         o.stop()
+
+
+def test_active_health_checks_take_sick_upstream_out_of_rotation():
+    """--health-check: a checker thread probes every upstream; two failed probes take
+    a sick upstream out of rotation before any client request fails on it, and a
+    passing probe brings it back (the reference's TODO at Server.py:532)."""
+    a, b = Origin(body_bytes=100).start(), Origin(body_bytes=100).start()
+    try:
+        with make_proxy([a.port, b.port], balance="roundrobin", health_path="/health",
+                        health_interval_ms=40, health_fails=2) as px:
+            c = HttpClient(port=px.port)
+
+            def wait_for(up):
+                for _ in range(100):
+                    st = px.stats()
+                    if st["upstreams_up"] == up:
+                        return st
+                    time.sleep(0.02)
+                raise AssertionError(f"upstreams_up {px.stats()['upstreams_up']} != {up}")
+
+            wait_for([1, 1])
+            b.healthy = False
+            st = wait_for([1, 0])
+            assert st["health_transitions"] >= 1
+            for i in range(20):
+                assert c.get(f"/hc/sick/{i}").status() == 200
+            assert sum(n for p, n in b.hits.items() if p.startswith("/hc/sick/")) == 0
+            b.healthy = True
+            wait_for([1, 1])
+            for i in range(20):  # new connections: a client keeps its upstream (affinity)
+                assert HttpClient(port=px.port).get(f"/hc/back/{i}").status() == 200
+            assert sum(n for p, n in b.hits.items() if p.startswith("/hc/back/")) > 0
+    finally:
+        a.stop()
+        b.stop()
