@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--hbm-gb", type=float, default=4.0)
     ap.add_argument("--l1-mb", type=int, default=0, help="DRAM L1 in front of hbm (0 = off)")
     ap.add_argument("--batch-us", type=int, default=0, help="HBM batch linger (0 = natural)")
+    ap.add_argument("--no-filter", action="store_true", help="HBM: no host presence filter")
+    ap.add_argument("--spin-us", type=int, default=50, help="HBM batcher poll before blocking")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -55,7 +57,9 @@ def main():
     backend = None if a.backend == "none" else make_backend(
         a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
                                                                        "batch_us": a.batch_us,
-                                                                       "l1_mb": a.l1_mb}))
+                                                                       "l1_mb": a.l1_mb,
+                                                                       "hbm_filter": not a.no_filter,
+                                                                       "spin_us": a.spin_us}))
     px = Server([("127.0.0.1", origin.port)], port=0, backend=backend, threads=a.threads,
                 client_max_reqs=1 << 30).start()
     url = f"http://127.0.0.1:{px.port}"

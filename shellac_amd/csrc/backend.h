@@ -32,6 +32,7 @@
 #include "host_cache.h"
 #include "ketama.h"
 #include "net.h"
+#include "presence_filter.h"
 #include "stream_buf.h"
 
 namespace shellac {
@@ -102,6 +103,8 @@ struct HbmBackendConfig {
   int batch_us = 0;         // optional linger for batch-mates (0: natural batching)
   int max_batch = 65536;    // flush early when this many requests are queued
   int sweep_interval_s = 10;  // idle-time expiry sweep of every shard (0 = off)
+  int spin_us = 50;           // batcher polls the queue this long before blocking
+  bool presence_filter = true;  // answer GETs of never-stored digests on the host
 };
 
 class HbmBackend : public CacheBackend {
@@ -141,8 +144,21 @@ class HbmBackend : public CacheBackend {
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<Req> q_;
+  // q_.size() mirror the batcher polls (without the mutex) for a short while after each
+  // batch before it blocks on cv_: a request arriving then skips a futex wake-up
+  std::atomic<size_t> qn_{0};
+  std::atomic<bool> spinning_{false};
   bool stop_ = false;
   bool flush_req_ = false;
+  // Presence filter (presence_filter.h). SETs add their digest under mu_ to filt_ and,
+  // while a rebuild is in progress, to filt_next_; the batcher installs filt_next_ in the
+  // same critical section that takes a batch, commits that batch, then fills filt_next_
+  // from every shard's live keys and swaps it in (so no stored digest is ever missing).
+  std::shared_ptr<PresenceFilter> filt_, filt_next_;
+  uint64_t filt_bits_ = 0, filt_rebuild_at_ = 0;
+  bool filt_want_rebuild_ = false;
+  std::atomic<uint64_t> filt_skips_{0}, filt_rebuilds_{0};
+  void finish_filter_rebuild();
   std::thread th_;
   double epoch_;
   std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};

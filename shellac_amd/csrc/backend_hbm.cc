@@ -156,6 +156,14 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     d->ensure_vals(4u << 20);
     devs_.push_back(std::move(d));
   }
+  if (cfg_.presence_filter) {
+    // 16 bits per index slot of every shard (capped at 256 MiB): ~2 % false positives
+    // when a full index's worth of digests has been added since the last rebuild
+    const uint64_t slots = cfg_.nbuckets_per_gpu * kEntriesPerBucket * devs_.size();
+    filt_bits_ = std::min<uint64_t>(slots * 16, 1ull << 31);
+    filt_rebuild_at_ = slots;
+    filt_ = std::make_shared<PresenceFilter>(filt_bits_);
+  }
   th_ = std::thread([this] { loop(); });
 }
 
@@ -171,6 +179,12 @@ HbmBackend::~HbmBackend() {
 uint32_t HbmBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
 void HbmBackend::get(const std::string&, const Digest& d, Executor* ex, GetCallback done) {
+  if (cfg_.presence_filter && !std::atomic_load(&filt_)->maybe(d)) {
+    // never stored: a miss without a GPU batch
+    filt_skips_.fetch_add(1, std::memory_order_relaxed);
+    done(false, CacheValue{});
+    return;
+  }
   Req r;
   r.kind = 0;
   r.d = d;
@@ -179,8 +193,9 @@ void HbmBackend::get(const std::string&, const Digest& d, Executor* ex, GetCallb
   {
     std::lock_guard<std::mutex> lk(mu_);
     q_.push_back(std::move(r));
+    qn_.store(q_.size(), std::memory_order_release);
   }
-  cv_.notify_one();
+  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
 }
 
 void HbmBackend::set(const std::string&, const Digest& d, Bytes value, uint32_t flags,
@@ -194,9 +209,14 @@ void HbmBackend::set(const std::string&, const Digest& d, Bytes value, uint32_t 
   r.ttl = ttl_s;
   {
     std::lock_guard<std::mutex> lk(mu_);
+    if (cfg_.presence_filter) {
+      filt_->add(d);
+      if (filt_next_) filt_next_->add(d);
+    }
     q_.push_back(std::move(r));
+    qn_.store(q_.size(), std::memory_order_release);
   }
-  cv_.notify_one();
+  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
 }
 
 void HbmBackend::del(const std::string&, const Digest& d, Executor* ex, DelCallback done) {
@@ -208,8 +228,9 @@ void HbmBackend::del(const std::string&, const Digest& d, Executor* ex, DelCallb
   {
     std::lock_guard<std::mutex> lk(mu_);
     q_.push_back(std::move(r));
+    qn_.store(q_.size(), std::memory_order_release);
   }
-  cv_.notify_one();
+  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
 }
 
 void HbmBackend::flush() {
@@ -223,7 +244,17 @@ void HbmBackend::flush() {
 void HbmBackend::loop() {
   std::vector<Req> batch;
   for (;;) {
-    bool do_flush = false;
+    bool do_flush = false, rebuilding = false;
+    // After a batch, poll the queue for up to spin_us before blocking: under steady
+    // traffic the next request usually arrives within that window, and catching it here
+    // saves the futex wake-up (the producer skips notify while we spin).
+    if (cfg_.spin_us > 0 && qn_.load(std::memory_order_acquire) == 0) {
+      spinning_.store(true, std::memory_order_release);
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.spin_us);
+      while (qn_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+        __builtin_ia32_pause();
+      spinning_.store(false, std::memory_order_release);
+    }
     {
       std::unique_lock<std::mutex> lk(mu_);
       if (cfg_.sweep_interval_s > 0) {
@@ -231,7 +262,7 @@ void HbmBackend::loop() {
         // FIFO log reclaims bytes by itself; expired entries are otherwise only
         // skipped lazily at lookup)
         if (!cv_.wait_for(lk, std::chrono::seconds(cfg_.sweep_interval_s),
-                          [&] { return stop_ || !q_.empty() || flush_req_; })) {
+                          [&] { return stop_ || !q_.empty() || flush_req_ || filt_want_rebuild_; })) {
           lk.unlock();
           try {
             sweep_all();
@@ -241,7 +272,7 @@ void HbmBackend::loop() {
           continue;
         }
       } else {
-        cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_; });
+        cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_ || filt_want_rebuild_; });
       }
       if (stop_ && q_.empty()) return;
       // Natural batching: whatever queued while the previous batch ran goes now. An
@@ -253,7 +284,15 @@ void HbmBackend::loop() {
                cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
         }
       }
+      if (filt_want_rebuild_) {
+        // SETs queued from here on add to filt_next_; the ones already queued are in
+        // `batch` and committed before finish_filter_rebuild() exports the shards' keys
+        filt_next_ = std::make_shared<PresenceFilter>(filt_bits_);
+        filt_want_rebuild_ = false;
+        rebuilding = true;
+      }
       batch.swap(q_);
+      qn_.store(0, std::memory_order_release);
       do_flush = flush_req_;
       flush_req_ = false;
     }
@@ -277,6 +316,17 @@ void HbmBackend::loop() {
           r.ex->post([cb]() { cb(false); });
         }
       }
+    }
+    if (rebuilding) {
+      try {
+        finish_filter_rebuild();
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "[shellac hbm] presence filter rebuild failed: %s\n", e.what());
+        std::lock_guard<std::mutex> lk(mu_);
+        filt_next_.reset();
+      }
+    } else if (cfg_.presence_filter && filt_->adds() >= filt_rebuild_at_) {
+      filt_want_rebuild_ = true;  // read under mu_ by the wait predicate next iteration
     }
     const uint64_t n = batch.size();
     if (n) {
@@ -487,6 +537,33 @@ void HbmBackend::sweep_all() {
   sweeps_++;
 }
 
+void HbmBackend::finish_filter_rebuild() {
+  TraceRange tr("hbm_backend.filter_rebuild");
+  const uint32_t t = now();
+  for (auto& d : devs_) {
+    d->set_device();
+    const uint64_t live = d->cache->export_keys(nullptr, 0, t, d->stream);
+    if (!live) continue;
+    // the kernel writes the digests straight into mapped host memory (no device buffer)
+    Digest *h = nullptr, *hdev = nullptr;
+    Dev::map_alloc(&h, &hdev, live * sizeof(Digest));
+    uint64_t got = 0;
+    try {
+      got = std::min(live, d->cache->export_keys(hdev, live, t, d->stream));
+    } catch (...) {
+      (void)hipHostFree(h);
+      throw;
+    }
+    for (uint64_t i = 0; i < got; ++i) filt_next_->add(h[i]);
+    (void)hipHostFree(h);
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  std::atomic_store(&filt_, filt_next_);
+  filt_next_.reset();
+  filt_rebuild_at_ = filt_->adds() + cfg_.nbuckets_per_gpu * kEntriesPerBucket * devs_.size();
+  filt_rebuilds_++;
+}
+
 void HbmBackend::stats(StatList* out) {
   CacheCounters t{};
   uint64_t hbm = 0;
@@ -519,6 +596,13 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_set_graph_captures", gc);
   out->emplace_back("hbm_live_objects", live_objects_.load());
   out->emplace_back("hbm_live_bytes", live_bytes_.load());
+  if (cfg_.presence_filter) {
+    const auto f = std::atomic_load(&filt_);
+    out->emplace_back("hbm_filter_skips", filt_skips_.load());
+    out->emplace_back("hbm_filter_rebuilds", filt_rebuilds_.load());
+    out->emplace_back("hbm_filter_adds", f->adds());
+    out->emplace_back("hbm_filter_fill_ppm", (uint64_t)(f->fill() * 1e6));
+  }
 }
 
 }  // namespace shellac

@@ -170,7 +170,8 @@ void bind_net(py::module_& m) {
   }, py::arg("bytes"), py::arg("max_item") = 1u << 20, py::arg("stripes") = 16);
   m.def("hbm_backend", [](std::vector<int> devices, uint64_t log_bytes_per_gpu,
                           uint64_t nbuckets_per_gpu, uint32_t max_item, int batch_us,
-                          int max_batch, int sweep_interval_s) {
+                          int max_batch, int sweep_interval_s, int spin_us,
+                          bool presence_filter) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -179,11 +180,14 @@ void bind_net(py::module_& m) {
     c.batch_us = batch_us;
     c.max_batch = max_batch;
     c.sweep_interval_s = sweep_interval_s;
+    c.spin_us = spin_us;
+    c.presence_filter = presence_filter;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
      py::arg("max_item") = 1u << 20, py::arg("batch_us") = 0, py::arg("max_batch") = 65536,
-     py::arg("sweep_interval_s") = 10);
+     py::arg("sweep_interval_s") = 10, py::arg("spin_us") = 50,
+     py::arg("presence_filter") = true);
   m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl) {
     return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl)};
   }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60);

@@ -50,7 +50,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
                  hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 0,
                  retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = "",
-                 sweep_s: int = 10):
+                 sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -59,6 +59,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
     ``hbm`` / ``memcached`` tier (``TieredBackend``: L1 hits never wait for a GPU
     batch or a network round trip). ``fault`` (e.g. ``"get_miss=0.1,delay_us=500"``,
     ``"down"``) wraps the stack in a fault-injection backend; see ``set_fault``.
+    ``hbm_filter`` keeps a host presence filter of stored digests so cold-key GETs miss
+    without a GPU batch; ``spin_us`` is how long the HBM batcher polls before blocking.
     """
     c = core()
     if kind == "none":
@@ -67,11 +69,13 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
         # fault injection wraps the whole cache stack (set_fault() changes it live)
         inner = make_backend(kind, caches=caches, dram_mb=dram_mb, gpus=gpus, hbm_gb=hbm_gb,
                              max_item=max_item, batch_us=batch_us, retry_s=retry_s, l1_mb=l1_mb,
-                             promote_ttl=promote_ttl, sweep_s=sweep_s)
+                             promote_ttl=promote_ttl, sweep_s=sweep_s, hbm_filter=hbm_filter,
+                             spin_us=spin_us)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
-                          batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s)
+                          batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s,
+                          hbm_filter=hbm_filter, spin_us=spin_us)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -85,7 +89,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
         nb = 1
         while nb * 4 * 1024 < log_bytes:  # ~2 KiB/object at <=50% slot load
             nb *= 2
-        return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us, sweep_interval_s=sweep_s)
+        return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us, sweep_interval_s=sweep_s,
+                             spin_us=spin_us, presence_filter=hbm_filter)
     raise ValueError(f"unknown cache backend {kind!r}")
 
 

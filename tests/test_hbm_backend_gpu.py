@@ -96,3 +96,43 @@ def test_hbm_backend_idle_sweep_expires_ttl():
     assert be.get(b"/ttl/short") is None
     assert be.get(b"/ttl/long") == (b"y" * 100, 0)
     assert st["hbm_live_objects"] == 1
+
+
+def test_hbm_presence_filter_skips_cold_misses_and_survives_rebuild():
+    """GETs of never-stored digests are answered on the host (no GPU batch); once a
+    full index worth of digests was added the filter is rebuilt from the shard's live
+    keys, and every live object must still hit (no false negatives)."""
+    from shellac_amd import core
+
+    be = core().hbm_backend([0], 64 << 20, 256, 1 << 16, 0, sweep_interval_s=1)
+    st0 = be.stats()
+    assert be.get(b"/never/stored") is None
+    assert be.stats()["hbm_filter_skips"] == st0["hbm_filter_skips"] + 1
+    assert be.stats()["hbm_batches"] == st0["hbm_batches"]  # no GPU round trip
+    keys = [b"/pf/%d" % i for i in range(3000)]  # > 1024 index slots: rebuilds + evictions
+    for i, k in enumerate(keys):
+        be.set(k, b"v%d" % i, 0, 0)
+        if i % 500 == 499:
+            assert _wait_get(be, k) == (b"v%d" % i, 0)
+    assert _wait_get(be, keys[-1]) == (b"v2999", 0)
+    for k in keys[:8]:  # trigger the rebuild check after the last SET batch
+        be.get(k)
+    time.sleep(2.5)  # idle sweep refreshes hbm_live_objects
+    st = be.stats()
+    assert st["hbm_filter_rebuilds"] >= 1
+    hits = sum(1 for i, k in enumerate(keys) if be.get(k) == (b"v%d" % i, 0))
+    assert hits == be.stats()["hbm_live_objects"] > 0
+    skips = be.stats()["hbm_filter_skips"]
+    cold = sum(be.get(b"/cold/%d" % i) is None for i in range(1000))
+    assert cold == 1000
+    assert be.stats()["hbm_filter_skips"] - skips > 900  # few false positives
+
+
+def test_hbm_presence_filter_off_sends_every_get_to_the_gpu():
+    from shellac_amd import core
+
+    be = core().hbm_backend([0], 16 << 20, 256, 1 << 16, 0, presence_filter=False)
+    b0 = be.stats()["hbm_batches"]
+    assert be.get(b"/never/stored") is None
+    st = be.stats()
+    assert st["hbm_batches"] == b0 + 1 and "hbm_filter_skips" not in st
