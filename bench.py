@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = functional rehearsal of the distributed path over gloo "
                          "(DRAM shards); never a performance number")
+    ap.add_argument("--no-coalesce", action="store_true",
+                    help="probe and copy every GET request (no in-batch request collapsing)")
     ap.add_argument("--no-smoke", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
@@ -173,6 +175,7 @@ def main():
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
     sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group)
+    sc.coalesce = not args.no_coalesce
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
@@ -283,6 +286,10 @@ def main():
             "set_dist": args.set_dist,
             "replicated_hot_objects": args.replicate if world > 1 else 0,
         },
+        "get_coalescing": sc.coalesce,
+        # owner-shard probes (+ replica hits) per GET request: < 1 when duplicate
+        # requests of a batch share one probe and one response record
+        "get_probes_per_request": round((gops + rep_hits) / max(greq, 1), 4),
         "get_hit_ratio": round((hits + rep_hits) / max(gops + rep_hits, 1), 4),
         "replica_hit_fraction": round(rep_hits / max(greq, 1), 4),
         "get_value_GBps_owner_shards": round(gbytes / elapsed / 1e9, 2),

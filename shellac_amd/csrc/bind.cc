@@ -74,12 +74,26 @@ PYBIND11_MODULE(_shellac_core, m) {
            }),
            py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"))
       .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
-                        uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve, int slot) {
+                        uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve, int slot,
+                        uintptr_t first) {
         py::gil_scoped_release nogil;
         c.lookup(P<const Digest>(keys), n, P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off),
-                 now, S(s), reserve, slot);
+                 now, S(s), reserve, slot, P<const uint32_t>(first));
       }, py::arg("keys"), py::arg("n"), py::arg("loc"), py::arg("size"), py::arg("off"),
-         py::arg("now"), py::arg("stream"), py::arg("reserve") = 0, py::arg("total_slot") = -1)
+         py::arg("now"), py::arg("stream"), py::arg("reserve") = 0, py::arg("total_slot") = -1,
+         py::arg("first") = 0)
+      .def("lookup_coalesced", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t table,
+                                  int64_t slots, uintptr_t first, uintptr_t loc, uintptr_t size,
+                                  uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve,
+                                  int slot, uintptr_t cslot, bool table_clean) {
+        py::gil_scoped_release nogil;
+        c.lookup_coalesced(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first),
+                           P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off), now, S(s),
+                           reserve, slot, P<uint32_t>(cslot), table_clean);
+      }, py::arg("keys"), py::arg("n"), py::arg("table"), py::arg("slots"), py::arg("first"),
+         py::arg("loc"), py::arg("size"), py::arg("off"), py::arg("now"), py::arg("stream"),
+         py::arg("reserve") = 0, py::arg("total_slot") = -1, py::arg("cslot") = 0,
+         py::arg("table_clean") = false)
       .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
                            uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s,
                            int done_slot) {
@@ -112,12 +126,14 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
-                       uint64_t bytes_bound, uint32_t now, uintptr_t s) {
+                       uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
-                bytes_bound, now, S(s));
-      })
+                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after));
+      }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
+         py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
+         py::arg("stream"), py::arg("index_after") = 0)
       .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
                         uintptr_t s) {
         py::gil_scoped_release nogil;
@@ -172,6 +188,22 @@ PYBIND11_MODULE(_shellac_core, m) {
                       uintptr_t dst, uintptr_t s) {
     segcopy(P<const uint8_t>(src), P<const uint64_t>(src_off), P<const uint64_t>(dst_off), n,
             P<uint8_t>(dst), S(s));
+  });
+  m.def("coalesce_table_slots", &coalesce_table_slots);
+  m.def("coalesce_keys", [](uintptr_t keys, int64_t n, uintptr_t table, int64_t slots,
+                            uintptr_t first, uintptr_t s) {
+    coalesce_keys(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first), S(s));
+  });
+  m.def("expand_coalesced", [](uintptr_t first, int64_t n, uintptr_t size, uintptr_t off,
+                               uintptr_t s) {
+    expand_coalesced(P<const uint32_t>(first), n, P<uint64_t>(size), P<uint64_t>(off), S(s));
+  });
+  m.def("expand_coalesced_out", [](uintptr_t first, int64_t n, uintptr_t size, uintptr_t off,
+                                   uintptr_t out_size, uintptr_t out_off, uintptr_t table,
+                                   uintptr_t cslot, uintptr_t s) {
+    expand_coalesced_out(P<const uint32_t>(first), n, P<const uint64_t>(size),
+                         P<const uint64_t>(off), P<uint64_t>(out_size), P<uint64_t>(out_off),
+                         P<uint32_t>(table), P<const uint32_t>(cslot), S(s));
   });
   m.def("digest_keys", [](uintptr_t bytes, uintptr_t offs, int64_t n, uintptr_t out,
                           uintptr_t s) {

@@ -44,8 +44,22 @@ class HbmCache {
   // `total_slot` >= 0 also writes off[n] straight into host slot `total_slot` (pinned,
   // coherent), readable with host_slot() once the stream has passed the lookup: the
   // response size without a D2H copy.
+  // `first` (coalesce_keys output, may be null): rows with first[i] != i are duplicates
+  // and are answered as misses without touching the index (expand_coalesced fills them
+  // in after the gather).
   void lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-              uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1);
+              uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
+              const uint32_t* first = nullptr);
+  // Coalescing lookup: coalesce_keys and lookup(first=...) in one pass — the row that
+  // claims a digest probes the index for it; duplicate rows get size 0 (fill them in
+  // with expand_coalesced after the gather). `table`: coalesce_table_slots(n) words.
+  // `cslot` (optional, u32 [n]): each claiming row's table slot, for
+  // expand_coalesced_out to clear; `table_clean`: the caller guarantees a zeroed table
+  // (skips the memset).
+  void lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
+                        uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
+                        uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
+                        uint32_t* cslot = nullptr, bool table_clean = false);
   uint64_t host_slot(int i) const;
   // Spin until the lookup that was given `total_slot` i has written it (no stream or
   // event synchronisation: the kernel's system-scope store is the signal). Throws after
@@ -70,9 +84,15 @@ class HbmCache {
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).
+  // `index_after`: the chain up to the log write runs at once, the index insert waits
+  // for this event. A lookup enqueued (on another stream) before this store and
+  // followed by the event therefore runs concurrently with the SET's dedupe, sizing
+  // and log append: it reads the index and the current head slot, which only the index
+  // insert changes, and a `reserve` covering this SET keeps its gather off the bytes
+  // the append overwrites.
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
-             uint64_t bytes_bound, uint32_t now, hipStream_t s);
+             uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
   // SET through captured hipGraphs, for callers with fixed batch sizes and fixed
   // staging buffers (the proxy's micro-batches, padded to a size class with
   // vlen = kSkipVlen rows). The five SET kernels become one graph launch. A graph bakes
@@ -146,7 +166,7 @@ class HbmCache {
   std::mutex mu_;
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                    int64_t n, uint32_t now, hipStream_t s);
+                    int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------
@@ -160,6 +180,23 @@ size_t device_scan_tmp_bytes(int64_t n);
 // from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
              uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
+
+// GET coalescing: first[i] = the row that serves row i (one row per distinct digest
+// serves all its duplicates). `table` is scratch of coalesce_table_slots(n) u32 words.
+int64_t coalesce_table_slots(int64_t n);
+void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
+                   uint32_t* first, hipStream_t s);
+// After the gather of a coalesced lookup: size[i], off[i] of every duplicate row i :=
+// those of first[i] (in place), so each request addresses its claimer's record.
+void expand_coalesced(const uint32_t* first, int64_t n, uint64_t* size, uint64_t* off,
+                      hipStream_t s);
+
+// Out-of-place variant (may overlap the gather): out_size/out_off[i] := size/off of
+// first[i] for every row; claimers clear their table slot (cslot from lookup_coalesced)
+// so the table is clean for the next batch.
+void expand_coalesced_out(const uint32_t* first, int64_t n, const uint64_t* size,
+                          const uint64_t* off, uint64_t* out_size, uint64_t* out_off,
+                          uint32_t* table, const uint32_t* cslot, hipStream_t s);
 
 // Digest packed key bytes: key i = bytes[offs[i] .. offs[i+1]).
 void digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out,

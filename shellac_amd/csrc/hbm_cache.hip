@@ -229,7 +229,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
                                                   uint64_t* __restrict__ out_loc,
                                                   uint64_t* __restrict__ out_size,
                                                   CacheCounters* __restrict__ ctr,
-                                                  uint64_t* __restrict__ part) {
+                                                  uint64_t* __restrict__ part,
+                                                  const uint32_t* __restrict__ first) {
   const int l8 = threadIdx.x & 7;
   // `reserve`: bytes about to be appended before this lookup's gather runs; objects
   // that those appends will overwrite are already treated as evicted
@@ -240,6 +241,13 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   const int64_t plen = part_len(n, gridDim.x);
   const int64_t i1 = min(n, (int64_t)(blockIdx.x + 1) * plen);
   for (int64_t i = (int64_t)blockIdx.x * plen + (threadIdx.x >> 3); i < i1; i += kBlock / 8) {
+    if (first && first[i] != (uint32_t)i) {  // coalesced duplicate: served from its first row
+      if (l8 == 0) {
+        out_loc[i] = kMissLoc;
+        out_size[i] = 0;
+      }
+      continue;  // uniform in the 8-lane group
+    }
     const Digest d = keys[i];
     uint64_t hl = 0;
     uint32_t hv = 0;
@@ -279,6 +287,218 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
               &CacheCounters::get_bytes);
   block_partial(psum, part);
+}
+
+// ---------------------------------------------------------------------------------
+// GET coalescing (request collapsing inside a batch)
+// ---------------------------------------------------------------------------------
+// A Zipf request batch repeats its hot keys many times (1M Zipf(0.99) requests over 4M
+// objects hold ~1/3 distinct keys). first[i] = the row that serves row i: one row per
+// distinct digest claims a slot of an open-addressing table (u32 row+1, linear probing,
+// <= 50 % load) with one CAS; every other row of that digest finds the claim and points
+// at it. The probe and the gather then touch only claiming rows, and k_expand gives
+// each duplicate its claimer's (off, size) afterwards: duplicates share one record in
+// the response buffer, as a proxy hands one cached object to many clients.
+// Contention: a hot key repeats ~60K times in a 1M batch, and a same-address atomic
+// costs ~12 ns serialised, so one global CAS per request spent ~0.3 ms on the hottest
+// key alone (measured: 330 us per 1M-key batch). Each workgroup therefore first
+// collapses its own chunk of 1024 keys in an LDS table, and only its local claimers go
+// to the global table: a key's global atomics are bounded by the number of chunks.
+// A local claimer that saw local duplicates (likely hot) reads the global slot before
+// it CASes; a local single goes straight to the CAS (one round trip).
+// PROBE: the global claimer of a digest also probes the shard's index for it (one lane
+// reads the 128-B bucket), so coalescing and lookup are one pass over the batch, and
+// the workgroup's contiguous row range yields the partial sums k_offsets scans.
+constexpr int kCoPer = 4;                   // keys per thread per chunk
+constexpr int kCoKeys = kBlock * kCoPer;    // keys per chunk
+constexpr int kCoSlots = 2 * kCoKeys;       // LDS table slots (<= 50 % load)
+
+template <bool PROBE>
+__global__ __launch_bounds__(kBlock) void k_coalesce(
+    const Digest* __restrict__ keys, int64_t n, int64_t plen, uint32_t* __restrict__ tab,
+    uint32_t tmask, uint32_t* __restrict__ first, uint32_t* __restrict__ cslot,
+    const Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
+    uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
+    uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
+    uint64_t* __restrict__ part) {
+  __shared__ uint32_t s_tab[kCoSlots];  // local row + 1
+  __shared__ uint32_t s_rep[kCoKeys];   // global claimer of each local claimer
+  __shared__ uint32_t s_dup[kCoKeys];   // local duplicates of each local claimer
+  __shared__ uint32_t s_q[PROBE ? kCoKeys : 1];   // rows this chunk probes
+  __shared__ uint64_t s_loc[PROBE ? kCoKeys : 1]; // their log offsets
+  __shared__ uint32_t s_vl[PROBE ? kCoKeys : 1];  // their vlen (kSkipVlen = miss)
+  __shared__ int s_qn;
+  const uint64_t head = PROBE ? *head_ptr + reserve : 0;
+  const int l8 = threadIdx.x & 7;
+  unsigned long long ops = 0, hits = 0, bytes = 0, psum = 0;
+  const int64_t r0 = (int64_t)blockIdx.x * plen, r1 = min(n, r0 + plen);
+  for (int64_t base = r0; base < r1; base += kCoKeys) {
+    const int cnt = (int)min((int64_t)kCoKeys, r1 - base);
+    for (int k = threadIdx.x; k < kCoSlots; k += kBlock) s_tab[k] = 0;
+    for (int k = threadIdx.x; k < kCoKeys; k += kBlock) s_dup[k] = 0;
+    if (threadIdx.x == 0) s_qn = 0;
+    __syncthreads();
+    const Digest* kb = keys + base;
+    Digest dk[kCoPer];
+    uint32_t lrep[kCoPer];
+    // 1. local claims (rows strided by kBlock: coalesced 16-B loads)
+#pragma unroll
+    for (int u = 0; u < kCoPer; ++u) {
+      const int j = u * kBlock + threadIdx.x;
+      lrep[u] = (uint32_t)j;
+      if (j < cnt) dk[u] = kb[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kCoPer; ++u) {
+      const int j = u * kBlock + threadIdx.x;
+      if (j >= cnt) continue;
+      const Digest d = dk[u];
+      uint32_t h = (uint32_t)d.lo & (kCoSlots - 1);
+      for (int step = 0; step < kCoSlots; ++step) {
+        const uint32_t v = atomicCAS(&s_tab[h], 0u, (uint32_t)j + 1u);
+        if (v == 0) break;
+        const Digest o = kb[v - 1];  // keys are immutable: the claimer's digest is readable
+        if (o.lo == d.lo && o.hi == d.hi) {
+          lrep[u] = v - 1;
+          atomicAdd(&s_dup[v - 1], 1u);
+          break;
+        }
+        h = (h + 1) & (kCoSlots - 1);
+      }
+    }
+    __syncthreads();
+    // 2. local claimers claim globally; global claimers queue for the probe
+#pragma unroll
+    for (int u = 0; u < kCoPer; ++u) {
+      const int j = u * kBlock + threadIdx.x;
+      if (j >= cnt || lrep[u] != (uint32_t)j) continue;
+      const Digest d = dk[u];
+      const uint32_t i = (uint32_t)(base + j);
+      uint32_t h = (uint32_t)(d.hi ^ (d.hi >> 29)) & tmask;
+      uint32_t rep = i;
+      bool look = s_dup[j] > 0;  // likely hot: read before CAS
+      for (uint32_t step = 0; step <= tmask; ++step) {
+        uint32_t v = look ? __hip_atomic_load(tab + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0u;
+        if (v == 0) {
+          v = atomicCAS(tab + h, 0u, i + 1u);
+          if (v == 0) break;  // claimed: this row serves the digest
+        }
+        const Digest o = keys[v - 1];
+        if (o.lo == d.lo && o.hi == d.hi) {
+          rep = v - 1;
+          break;
+        }
+        h = (h + 1) & tmask;
+        look = true;  // a probed chain: read first from here on
+      }
+      s_rep[j] = rep;
+      if (rep == i) {
+        if (cslot) cslot[i] = h;  // k_expand_out clears it after the step
+        if (PROBE) s_q[atomicAdd(&s_qn, 1)] = (uint32_t)j;
+      }
+    }
+    __syncthreads();
+    if (PROBE) {
+      // 2b. probe the queued digests, one 8-lane group per digest (each lane one 16-B
+      //     quarter-entry of the 128-B bucket, as k_probe)
+      const int qn = s_qn;
+      for (int q = threadIdx.x >> 3; q < qn; q += kBlock / 8) {
+        const int j = (int)s_q[q];
+        const Digest d = kb[j];
+        uint64_t hl = 0;
+        uint32_t hv = 0;
+#pragma unroll 1
+        for (int round = 0; round < 2 && hl == 0; ++round) {  // hl is uniform in the group
+          const uint64_t b = round == 0 ? bucket1(d, mask) : bucket2(d, mask);
+          const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l8];
+          const uint64_t a = pack2(v.x, v.y);
+          const uint64_t c = pack2(v.z, v.w);
+          const uint64_t pa = __shfl_xor(a, 1);
+          const uint64_t pc = __shfl_xor(c, 1);
+          const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
+                           entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
+          hl = hit ? pa : 0;
+          hv = hit ? (uint32_t)pc : 0;
+#pragma unroll
+          for (int sh = 2; sh < 8; sh <<= 1) {
+            const uint64_t ol = __shfl_xor(hl, sh);
+            const uint32_t ov = __shfl_xor(hv, sh);
+            if (ol > hl) { hl = ol; hv = ov; }
+          }
+        }
+        if (l8 == 0) {
+          ++ops;
+          if (hl) {
+            s_loc[j] = (hl - 1) % cap;
+            s_vl[j] = hv;
+            ++hits;
+            bytes += hv;
+            psum += item_bytes(hv);
+          } else {
+            s_vl[j] = kSkipVlen;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // 3. every row takes its local claimer's global claimer
+#pragma unroll
+    for (int u = 0; u < kCoPer; ++u) {
+      const int j = u * kBlock + threadIdx.x;
+      if (j >= cnt) continue;
+      const uint32_t f = s_rep[lrep[u]];
+      first[base + j] = f;
+      if (PROBE) {
+        const bool hit = f == (uint32_t)(base + j) && s_vl[j] != kSkipVlen;
+        out_loc[base + j] = hit ? s_loc[j] : kMissLoc;
+        out_size[base + j] = hit ? item_bytes(s_vl[j]) : 0;
+      }
+    }
+    __syncthreads();  // LDS is reused by the next chunk
+  }
+  if (PROBE) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;
+    block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
+                &CacheCounters::get_bytes);
+    block_partial(psum, part);
+  }
+}
+
+// In place: every duplicate row takes its claiming row's (size, off). Only claiming rows
+// are read and only duplicate rows are written, so rows never race. Runs after the
+// gather (which needs the scan in `off` intact).
+__global__ __launch_bounds__(kBlock) void k_expand(const uint32_t* __restrict__ first, int64_t n,
+                                                   uint64_t* __restrict__ size,
+                                                   uint64_t* __restrict__ off) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t f = first[i];
+    if (f != (uint32_t)i) {
+      size[i] = size[f];
+      off[i] = off[f];
+    }
+  }
+}
+
+// Out of place (may run concurrently with the gather, which reads size/off): every row
+// takes its claimer's (size, off) into out_size/out_off, and every claimer clears its
+// slot of the coalescing table, so the next batch needs no table memset.
+__global__ __launch_bounds__(kBlock) void k_expand_out(const uint32_t* __restrict__ first,
+                                                       int64_t n,
+                                                       const uint64_t* __restrict__ size,
+                                                       const uint64_t* __restrict__ off,
+                                                       uint64_t* __restrict__ out_size,
+                                                       uint64_t* __restrict__ out_off,
+                                                       uint32_t* __restrict__ tab,
+                                                       const uint32_t* __restrict__ cslot) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t f = first[i];
+    out_size[i] = size[f];
+    out_off[i] = off[f];
+    if (f == (uint32_t)i && tab) tab[cslot[i]] = 0u;
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -999,8 +1219,9 @@ size_t device_scan_tmp_bytes(int64_t n) {
 
 // k_offsets launch for sizes produced by `grid` workgroups over contiguous ranges.
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
-                    uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr) {
-  const int64_t plen = part_len(n, grid);
+                    uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr,
+                    int64_t plen_override = 0) {
+  const int64_t plen = plen_override > 0 ? plen_override : part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
   hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
@@ -1020,6 +1241,43 @@ void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_of
   if (n <= 0) return;
   launch_segcopy<0>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr, nullptr,
                     dst_cap);
+  HIP_OK(hipGetLastError());
+}
+
+int64_t coalesce_table_slots(int64_t n) {
+  int64_t t = 1024;
+  while (t < 2 * n) t <<= 1;
+  return t;
+}
+
+void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
+                   uint32_t* first, hipStream_t s) {
+  if (n <= 0) return;
+  SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
+  SH_CHECK(table_slots >= 2 * n && (table_slots & (table_slots - 1)) == 0,
+           "coalesce: table needs a power of two >= 2n slots");
+  HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
+  const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
+  hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
+                     (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, nullptr,
+                     nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr);
+  HIP_OK(hipGetLastError());
+}
+
+void expand_coalesced(const uint32_t* first, int64_t n, uint64_t* size, uint64_t* off,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_expand, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, first, n, size,
+                     off);
+  HIP_OK(hipGetLastError());
+}
+
+void expand_coalesced_out(const uint32_t* first, int64_t n, const uint64_t* size,
+                          const uint64_t* off, uint64_t* out_size, uint64_t* out_off,
+                          uint32_t* table, const uint32_t* cslot, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_expand_out, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, first, n,
+                     size, off, out_size, out_off, table, cslot);
   HIP_OK(hipGetLastError());
 }
 
@@ -1143,7 +1401,8 @@ void HbmCache::reserve(int64_t n) {
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
-                      uint32_t now, hipStream_t s, uint64_t reserve, int total_slot) {
+                      uint32_t now, hipStream_t s, uint64_t reserve, int total_slot,
+                      const uint32_t* first) {
   TraceRange tr("hbm.lookup");
   SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   std::lock_guard<std::mutex> lk(mu_);
@@ -1157,9 +1416,42 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   }
   const int grid = grid_for(n * 8, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
-                     cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_);
+                     cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first);
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht);
+}
+
+void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
+                                int64_t table_slots, uint32_t* first, uint64_t* loc,
+                                uint64_t* size, uint64_t* off, uint32_t now, hipStream_t s,
+                                uint64_t reserve, int total_slot, uint32_t* cslot,
+                                bool table_clean) {
+  TraceRange tr("hbm.lookup_coalesced");
+  SH_CHECK(total_slot < kHostSlots, "host slot out of range");
+  SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
+  SH_CHECK(table_slots >= 2 * n && (table_slots & (table_slots - 1)) == 0,
+           "coalesce: table needs a power of two >= 2n slots");
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  uint64_t* ht = total_slot >= 0 ? host_slots_ + total_slot : nullptr;
+  if (ht) __atomic_store_n(ht, kSlotPending, __ATOMIC_RELEASE);
+  if (n <= 0) {
+    HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
+    if (ht) *ht = 0;
+    return;
+  }
+  if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
+  // contiguous whole chunks per workgroup, at most kMaxGrid partial sums
+  const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
+  const int64_t per = (chunks + kMaxGrid - 1) / kMaxGrid;
+  const int grid = (int)((chunks + per - 1) / per);
+  const int64_t plen = per * kCoKeys;
+  hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
+                     (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
+                     cur_head(),
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_);
+  HIP_OK(hipGetLastError());
+  launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }
 
 uint64_t HbmCache::host_slot(int i) const {
@@ -1211,7 +1503,8 @@ void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8
 
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                     int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s) {
+                     int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
+                     hipEvent_t index_after) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
@@ -1219,7 +1512,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, s);
-  store_locked(keys, values, val_off, vlen, flags, expire, n, now, s);
+  store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
 
@@ -1228,7 +1521,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
 // publishes the new head into the other head slot.
 void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                            int64_t n, uint32_t now, hipStream_t s) {
+                            int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after) {
   const int grid = grid_for(n, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
@@ -1240,6 +1533,8 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());
+  // the index insert is the only SET kernel a concurrent lookup can observe
+  if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
   const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),

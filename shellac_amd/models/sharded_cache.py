@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import routing as R
-from ..ops.cache import CacheShard
+from ..ops.cache import CacheShard, coalesce, expand, expand_out
 from ..parallel.exchange import (all_gather, all_reduce, all_to_all_rows, all_to_all_single,
                                  allreduce_stats, dist_info, exchange_counts, segment_sums)
 from ..parallel.ring import ShardRing
@@ -157,7 +157,13 @@ class ShardedCache:
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
         # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
         self.overlap_store = os.environ.get("SHELLAC_OVERLAP_STORE", "1") != "0"
+        # GET coalescing: the duplicate keys of a batch share one probe and one record
+        # (ops.cache.coalesce); SHELLAC_COALESCE=0 probes and copies every request
+        self.coalesce = os.environ.get("SHELLAC_COALESCE", "1") != "0"
         self._side = None
+        self._probe_done = None  # event: this step's probe is done (SET index may run)
+        self._gather_cap = 0     # response buffer bytes for the unsynced gather
+        self._co_table = None    # persistent GET-coalescing table (serve, side stream)
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0}
 
@@ -184,8 +190,12 @@ class ShardedCache:
         n = keys.shape[0]
         self.stats["get_requests"] += n
         if self.world == 1:
-            lk = self.shard.lookup(keys, now)
+            if self.coalesce:
+                lk, first, _ = self.shard.lookup_coalesced(keys, now)
+            else:
+                lk, first = self.shard.lookup(keys, now), None
             data = self.shard.gather(lk)
+            expand(first, lk.size, lk.off)
             return GetResult(data, lk.off[:n], lk.size[:n])
         self._sample(keys)
         w = self.world
@@ -271,25 +281,72 @@ class ShardedCache:
                      batch.expire, now)
             data = sh.gather(lk)
             return GetResult(data, lk.off[:n], lk.size[:n])
-        lk = sh.lookup(keys, now, reserve_bytes=bound, total_slot=0)
         side = self._side_stream() if self.overlap_store else None
+        if side is not None:
+            # The SET chain runs on a side stream from the start of the step: its dedupe,
+            # sizing and log append (bytes the lookup reserves, so the gather never reads
+            # them) overlap the coalescing and the probe; only its index insert waits for
+            # the probe (event), then runs under the bandwidth-bound gather.
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)  # the previous step's gather is done with the log
+            now = sh.now() if now is None else now
+        table = self._coalesce_table(n) if (self.coalesce and side is not None) else None
+        if self.coalesce:
+            lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
+                                                   table=table)
+        else:
+            lk, first, cslot = sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None
         if side is None:
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now)
-            data = sh.gather(lk, total=sh.host_total(0))
+            data = self._gather_unsynced(lk)
+            expand(first, lk.size, lk.off)
             return GetResult(data, lk.off[:n], lk.size[:n])
-        # The SET chain (dedupe, size scan, log write, index CAS: mostly latency-bound
-        # small grids) runs on a side stream concurrently with the bandwidth-bound
-        # gather. Safe by construction: the lookup reserved the SET's log bytes, so the
-        # gather never reads a region the SET writes, and it does not read the index.
-        main = torch.cuda.current_stream(self.device)
-        side.wait_stream(main)
+        # Safe by construction: the lookup reserved the SET's log bytes, so the gather
+        # never reads a region the SET writes, and the gather does not read the index.
+        ev = self._probe_done
+        if ev is None:
+            ev = self._probe_done = torch.cuda.Event()
+        ev.record(main)
+        if first is not None:
+            out_size = torch.empty(n, dtype=torch.int64, device=self.device)
+            out_off = torch.empty(n, dtype=torch.int64, device=self.device)
         with torch.cuda.stream(side):
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                     batch.expire, now)
-        data = sh.gather(lk, total=sh.host_total(0))
+                     batch.expire, now, index_after=ev)
+            if first is not None:
+                # per-request (size, off) and the table clean-up, under the gather
+                expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)
+        data = self._gather_unsynced(lk)
         main.wait_stream(side)  # the next step's lookup sees this step's SETs
+        if first is not None:
+            return GetResult(data, out_off, out_size)
         return GetResult(data, lk.off[:n], lk.size[:n])
+
+    def _coalesce_table(self, n: int) -> torch.Tensor:
+        """Persistent, zeroed GET-coalescing table (every serve step leaves it zeroed:
+        expand_out clears the slots its batch claimed)."""
+        slots = int(_core().coalesce_table_slots(n))
+        t = self._co_table
+        if t is None or t.numel() < slots:
+            t = self._co_table = torch.zeros(slots, dtype=torch.int32, device=self.device)
+        return t
+
+    def _gather_unsynced(self, lk) -> torch.Tensor:
+        """Gather a lookup given ``total_slot=0`` without stalling the GPU: the gather
+        is queued at once into a buffer sized from earlier steps (the kernel writes
+        nothing if the total exceeds it) and the host reads the kernel-written total
+        while the gather runs; only an outgrown buffer costs a second gather."""
+        sh = self.shard
+        cap = self._gather_cap
+        if cap:
+            data = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            sh.gather(lk, data, out_cap=cap)
+        total = sh.host_total(0)
+        if cap and total <= cap:
+            return data
+        self._gather_cap = max(int(total * 1.25), 1 << 20) // 16 * 16
+        return sh.gather(lk, total=total)
 
     def _side_stream(self):
         if self.device.type != "cuda":

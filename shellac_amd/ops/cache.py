@@ -111,6 +111,51 @@ def unpack_records(out: torch.Tensor, off: torch.Tensor, size: torch.Tensor) -> 
     return res
 
 
+def coalesce(keys: torch.Tensor) -> Optional[torch.Tensor]:
+    """GET coalescing (request collapsing inside a batch). Returns ``first`` (int32
+    [n]): the row that serves row i — one row per distinct digest claims it with a CAS
+    in an open-addressing table (``k_coalesce``), its duplicates point at that row.
+    Pass it to ``CacheShard.lookup(first=...)`` (duplicates skip the index probe and
+    the gather) and call ``expand(first, lookup)`` after the gather, so every request
+    addresses its claimer's record. CPU shards: ``None`` (the host engine probes every
+    row; results are the same values)."""
+    if not keys.is_cuda or keys.shape[0] == 0:
+        return None
+    c = core()
+    n = keys.shape[0]
+    slots = int(c.coalesce_table_slots(n))
+    table = torch.empty(slots, dtype=torch.int32, device=keys.device)
+    first = torch.empty(n, dtype=torch.int32, device=keys.device)
+    c.coalesce_keys(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
+                    _stream_handle(keys.device))
+    return first
+
+
+def expand(first: Optional[torch.Tensor], size: torch.Tensor, off: torch.Tensor) -> None:
+    """After the gather of a coalesced lookup: duplicate rows take their claimer's
+    (size, off), in place (``k_expand``). No-op when ``first`` is None."""
+    if first is None:
+        return
+    n = first.numel()
+    core().expand_coalesced(first.data_ptr(), n, size.data_ptr(), off.data_ptr(),
+                            _stream_handle(first.device))
+
+
+def expand_out(first: torch.Tensor, size: torch.Tensor, off: torch.Tensor,
+               out_size: torch.Tensor, out_off: torch.Tensor,
+               table: Optional[torch.Tensor] = None, cslot: Optional[torch.Tensor] = None) -> None:
+    """Out-of-place ``expand`` (``k_expand_out``): out_size/out_off[i] := size/off of
+    first[i]. It does not modify size/off, so it may run on another stream while the
+    gather reads them. With ``table``/``cslot`` from ``lookup_coalesced(table=...)`` it
+    also clears the claimed slots, leaving the table zeroed for the next batch."""
+    n = first.numel()
+    core().expand_coalesced_out(first.data_ptr(), n, size.data_ptr(), off.data_ptr(),
+                                out_size.data_ptr(), out_off.data_ptr(),
+                                table.data_ptr() if table is not None else 0,
+                                cslot.data_ptr() if cslot is not None else 0,
+                                _stream_handle(first.device))
+
+
 @dataclass
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
@@ -172,12 +217,15 @@ class CacheShard:
 
     # -- GET ----------------------------------------------------------------------
     def lookup(self, keys: torch.Tensor, now: Optional[int] = None,
-               reserve_bytes: int = 0, total_slot: int = -1) -> Lookup:
+               reserve_bytes: int = 0, total_slot: int = -1,
+               first: Optional[torch.Tensor] = None) -> Lookup:
         """Probe the index. ``reserve_bytes`` > 0 also misses objects that the next
         ``reserve_bytes`` of log appends would overwrite, so a SET of at most that many
         bytes (``set_bound``) may run between this lookup and its gather.
         ``total_slot`` >= 0 (GPU) has the kernel write off[n] into that pinned host slot
-        (``host_total``), so the response size needs no device-to-host copy."""
+        (``host_total``), so the response size needs no device-to-host copy.
+        ``first`` (GPU, from ``coalesce``): duplicate rows are answered as empty without
+        a probe; ``expand`` fills them in after the gather."""
         self._check(keys, "keys")
         n = keys.shape[0]
         loc = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -185,13 +233,55 @@ class CacheShard:
         off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         now = self.now() if now is None else now
         if self.is_gpu:
+            if first is not None:
+                self._check(first, "first")
+                if first.numel() != n or first.dtype != torch.int32:
+                    raise ValueError("first must be int32 [n] from coalesce()")
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
-                              now, self._s(), int(reserve_bytes), int(total_slot))
+                              now, self._s(), int(reserve_bytes), int(total_slot),
+                              first.data_ptr() if first is not None else 0)
         else:
             size[n] = 0
             self._impl.lookup(keys.data_ptr(), n, loc.data_ptr(), size.data_ptr(), off.data_ptr(),
                               now, int(reserve_bytes))
         return Lookup(loc, size, off)
+
+    def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
+                         reserve_bytes: int = 0, total_slot: int = -1,
+                         table: Optional[torch.Tensor] = None):
+        """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
+        row that claims a digest probes the index for it). Returns (Lookup, first,
+        cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
+        after the gather. ``table``: a caller-owned, zeroed coalescing table (int32,
+        >= ``coalesce_table_slots(n)`` power-of-two slots) — then ``cslot`` holds each
+        claimer's slot and ``expand_out`` must run to clean the table again; otherwise
+        a temporary table is zeroed here and ``cslot`` is None. CPU shards: a plain
+        lookup, ``first = cslot = None``."""
+        if not self.is_gpu or keys.shape[0] == 0:
+            return self.lookup(keys, now, reserve_bytes, total_slot), None, None
+        self._check(keys, "keys")
+        c = core()
+        n = keys.shape[0]
+        cslot = None
+        if table is None:
+            slots = int(c.coalesce_table_slots(n))
+            table = torch.empty(slots, dtype=torch.int32, device=self.device)
+        else:
+            slots = table.numel()
+            if slots < int(c.coalesce_table_slots(n)) or slots & (slots - 1):
+                raise ValueError("coalescing table too small or not a power of two")
+            cslot = torch.empty(n, dtype=torch.int32, device=self.device)
+        first = torch.empty(n, dtype=torch.int32, device=self.device)
+        loc = torch.empty(n, dtype=torch.int64, device=self.device)
+        size = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        now = self.now() if now is None else now
+        self._impl.lookup_coalesced(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
+                                    loc.data_ptr(), size.data_ptr(), off.data_ptr(), now,
+                                    self._s(), int(reserve_bytes), int(total_slot),
+                                    cslot.data_ptr() if cslot is not None else 0,
+                                    cslot is not None)
+        return Lookup(loc, size, off), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
         """Total bytes of the last lookup given ``total_slot=slot``: spins on the pinned
@@ -215,14 +305,18 @@ class CacheShard:
         return out, off
 
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
-               total: Optional[int] = None) -> torch.Tensor:
-        """Copy hits into ``out`` (allocated from off[n] if not given: one sync)."""
+               total: Optional[int] = None, out_cap: Optional[int] = None) -> torch.Tensor:
+        """Copy hits into ``out`` (allocated from off[n] if not given: one sync).
+        ``out_cap`` (GPU): the kernel writes nothing when off[n] exceeds it, so a gather
+        can be queued before the total is known."""
         if out is None:
             total = int(lk.off[lk.n].item()) if total is None else total
             out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
         self._check(out, "out")
         if self.is_gpu:
-            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s())
+            cap = out.numel() if out_cap is None else min(int(out_cap), out.numel())
+            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s(),
+                              cap)
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
@@ -246,9 +340,13 @@ class CacheShard:
     def store(self, keys: torch.Tensor, values: torch.Tensor, val_off: torch.Tensor,
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
-              bytes_bound: Optional[int] = None) -> None:
+              bytes_bound: Optional[int] = None,
+              index_after: Optional["torch.cuda.Event"] = None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
-        batch appends; the default assumes every byte of ``values`` is stored."""
+        batch appends; the default assumes every byte of ``values`` is stored.
+        ``index_after`` (GPU, a recorded event): dedupe, sizing and the log append run at
+        once, the index insert waits for the event — so a lookup followed by that event
+        on another stream overlaps the SET's log write (see ``HbmCache::store``)."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -262,7 +360,8 @@ class CacheShard:
         if self.is_gpu:
             bound = self.set_bound(n, values.numel()) if bytes_bound is None else int(bytes_bound)
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
-                             fp, ep, n, bound, now, self._s())
+                             fp, ep, n, bound, now, self._s(),
+                             index_after.cuda_event if index_after is not None else 0)
         else:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now)

@@ -231,7 +231,7 @@ def test_serve_overlapped_matches_get_then_set(cuda_dev, side_stream):
         else:
             r = sc.get(keys)
             sc.set(sb)
-        outs.append((r.size.cpu(), r.data[: int(r.off[-1] + r.size[-1])].cpu()))
+        outs.append((r.size.cpu(), unpack_records(r.data, r.off, r.size)))
         after = sc.get(keys)
         outs.append((after.size.cpu(),))
     (s1, d1), (a1,), (s2, d2), (a2,) = outs
@@ -241,11 +241,9 @@ def test_serve_overlapped_matches_get_then_set(cuda_dev, side_stream):
     assert hit1.float().mean() > 0.5
     assert torch.equal(a1, a2)
     ids = wl.sample_ids(4096, 3).cpu()
-    o1 = torch.cumsum(torch.cat([torch.zeros(1, dtype=s1.dtype), s1[:-1]]), 0)
     for i in range(0, 4096, 97):
         if hit1[i]:
-            rec = d1[o1[i] + 32 : o1[i] + 32 + s1[i] - 32].numpy().tobytes()
-            assert rec.startswith(wl.expected_value(int(ids[i])))
+            assert d1[i][0] == wl.expected_value(int(ids[i]))
 
 
 @pytest.mark.parametrize("n", [1, 5, 17, 255, 2049, 40001, 300007])
@@ -454,3 +452,63 @@ def test_store_graph_matches_store(cuda_dev):
     assert torch.equal(a.gather(la), b.gather(lb))
     assert int((la.size > 0).sum()) > 0
     g.destroy()
+
+
+@pytest.mark.parametrize("n", [1, 2, 1000, 65537, 1 << 20])
+def test_coalesce_kernel_first_rows(cuda_dev, n):
+    """k_coalesce: first[i] holds the same digest as row i, claimers point at
+    themselves, and there is exactly one claimer per distinct digest."""
+    from shellac_amd.ops.cache import coalesce
+
+    g = torch.Generator().manual_seed(n)
+    pool = torch.randint(-2**62, 2**62, (max(n // 3, 1), 2), generator=g, dtype=torch.int64)
+    # Zipf-like skew: low pool ids repeat a lot
+    ids = (torch.rand(n, generator=g) ** 3 * pool.shape[0]).long().clamp(max=pool.shape[0] - 1)
+    keys = pool.index_select(0, ids).contiguous().to(cuda_dev)
+    shard = CacheShard(16 << 20, 1 << 12, 1 << 12, cuda_dev)
+    ar = torch.arange(n, device=cuda_dev)
+    nuniq = torch.unique(keys, dim=0).shape[0]
+    lk, f2, _ = shard.lookup_coalesced(keys)  # fused coalesce + probe (empty shard: misses)
+    for first in (coalesce(keys).long(), f2.long()):
+        assert torch.equal(keys.index_select(0, first), keys)
+        assert torch.equal(first.index_select(0, first), first)
+        assert int((first == ar).sum()) == nuniq
+    assert int(lk.off[n]) == 0 and shard.counters()["get_ops"] == nuniq
+
+
+def test_coalesced_get_and_serve_match_uncoalesced(cuda_dev):
+    """A Zipf batch (many duplicates) coalesced: the same value for every request as
+    the uncoalesced path, one probe per distinct key, and a smaller response buffer."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(50000, cuda_dev)
+    ids = wl.sample_ids(200000, 5)
+    keys = wl.digests.index_select(0, ids).contiguous()
+    res = {}
+    for co in (False, True):
+        shard = CacheShard(512 << 20, 1 << 16, 1 << 16, cuda_dev)
+        sc = ShardedCache(shard)
+        sc.coalesce = co
+        for s0 in range(0, 50000, 10000):
+            sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
+        c0 = shard.counters()["get_ops"]
+        r = sc.get(keys)
+        probes = shard.counters()["get_ops"] - c0
+        s = sc.serve(keys, wl.set_batch(wl.uniform_ids(4096, 6)))
+        torch.cuda.synchronize()
+        if co:  # the persistent coalescing table is left zeroed by every step
+            assert sc._co_table is not None and int(sc._co_table.abs().sum()) == 0
+            s2 = sc.serve(keys, wl.set_batch(wl.uniform_ids(4096, 7)))
+            assert int(sc._co_table.abs().sum()) == 0
+            assert torch.equal(s2.size.cpu() > 0, s.size.cpu() > 0)
+        res[co] = (unpack_records(r.data, r.off, r.size), r.size.cpu(), probes,
+                   unpack_records(s.data, s.off, s.size), int(r.data.numel()))
+    a, b = res[False], res[True]
+    assert a[0] == b[0] and torch.equal(a[1], b[1])
+    assert a[3] == b[3]
+    assert a[2] == keys.shape[0]
+    assert b[2] == torch.unique(keys, dim=0).shape[0] < keys.shape[0] // 2
+    assert b[4] < a[4] // 2
+    for i in range(0, 200000, 997):
+        assert b[0][i] is not None and b[0][i][0] == wl.expected_value(int(ids[i]))
