@@ -291,7 +291,8 @@ def main():
         # requests of a batch share one probe and one response record
         "get_probes_per_request": round((gops + rep_hits) / max(greq, 1), 4),
         "get_hit_ratio": round((hits + rep_hits) / max(gops + rep_hits, 1), 4),
-        "replica_hit_fraction": round(rep_hits / max(greq, 1), 4),
+        # share of the distinct-key lookups (after coalescing) a local replica answered
+        "replica_hit_fraction": round(rep_hits / max(gops + rep_hits, 1), 4),
         "get_value_GBps_owner_shards": round(gbytes / elapsed / 1e9, 2),
         "smoke": sm,
     }

@@ -41,16 +41,16 @@ void bind_router(py::module_& m) {
       .def("plan", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
                       uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,
-                      uintptr_t table, uintptr_t s) {
+                      uintptr_t table, uintptr_t s, bool coalesce) {
         py::gil_scoped_release nogil;
         r.plan(P<const Digest>(keys), n, replica, now, P<const Digest>(skeys),
                P<const uint32_t>(svlen), P<const uint32_t>(sflags), P<const uint32_t>(sexpire),
                P<const uint64_t>(sval_off), P<const uint8_t>(svalues), ns, fanout,
-               P<int64_t>(table), S(s));
+               P<int64_t>(table), S(s), coalesce);
       }, py::arg("keys"), py::arg("n"), py::arg("replica").none(true), py::arg("now"),
          py::arg("skeys"), py::arg("svlen"), py::arg("sflags"), py::arg("sexpire"),
          py::arg("sval_off"), py::arg("svalues"), py::arg("ns"), py::arg("fanout"),
-         py::arg("table"), py::arg("stream"))
+         py::arg("table"), py::arg("stream"), py::arg("coalesce") = false)
       .def("read_counts", [](RoutedStep& r, uintptr_t rtable, uintptr_t s) {
         py::gil_scoped_release nogil;
         return r.read_counts(P<const int64_t>(rtable), S(s));

@@ -70,13 +70,16 @@ class RoutedStep {
 
   // GET routing (replica probe first when `replica`), SET routing + hot fan-out (on a
   // side stream, concurrently), per-peer table[w][3] = {GET rows, SET rows, SET value
-  // bytes} into `table`, which must hold 6w + 2 words: [table | rtable | extras].
+  // bytes} into `table`, which must hold 6w + 3 words: [table | rtable | extras].
+  // `coalesce`: duplicate GET digests of the batch are not routed; each is answered
+  // from the row that claimed its digest (coalesce_keys / expand_coalesced).
   void plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
             const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
             const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues, int64_t ns,
-            bool fanout, int64_t* table, hipStream_t s);
+            bool fanout, int64_t* table, hipStream_t s, bool coalesce = false);
   // Host sync 1 (one D2H; rtable must be table + 3w). Returns
-  // [table (3w) | rtable (3w) | n_local | local_bytes].
+  // [table (3w) | rtable (3w) | n_local | local_bytes | coalesced duplicates] (n_local
+  // includes the duplicates).
   std::vector<int64_t> read_counts(const int64_t* rtable, hipStream_t s);
   // send: request region (sum 16 G_p + 32 R_p) then value region (sum V_p).
   void pack(uint8_t* send, hipStream_t s);
@@ -130,6 +133,7 @@ class RoutedStep {
   Digest* gk_ = nullptr;
   int64_t *perm_g_ = nullptr, *cnt_g_ = nullptr, *cnt_s_ = nullptr, *srec_ = nullptr;
   uint64_t *sval_ = nullptr, *svoff_ = nullptr;
+  uint32_t* first_ = nullptr;  // coalescing: claiming row of each GET row (null = off)
   const int64_t* rrec_ = nullptr;
   uint64_t *lk_loc_ = nullptr, *lk_off_ = nullptr, *gscan_ = nullptr;
   const uint64_t* sizes_in_ = nullptr;

@@ -178,25 +178,35 @@ __global__ __launch_bounds__(kB) void k_route_gets(const Digest* __restrict__ ke
 // Routed GET plan, fused: dest of every key of this workgroup's contiguous range
 // (owner, or `w` for a local replica hit) + its LDS histogram into table[d * G + b]
 // (the k_gr_hist layout, so k_gr_scan / k_gr_scatter follow unchanged).
+// With GET coalescing (`first`), a duplicate row (first[i] != i) stays local too: it
+// is answered from its claiming row after the step (expand_coalesced), so it is never
+// sent; `ndup` counts them (one atomic per workgroup).
 __global__ __launch_bounds__(kB) void k_route_hist(const Digest* __restrict__ keys, int64_t n,
                                                    const uint64_t* __restrict__ rsize,
                                                    const uint32_t* __restrict__ pts,
                                                    const int32_t* __restrict__ own, int npts,
                                                    int32_t w, int64_t plen,
                                                    int32_t* __restrict__ dest,
-                                                   uint64_t* __restrict__ table) {
+                                                   uint64_t* __restrict__ table,
+                                                   const uint32_t* __restrict__ first,
+                                                   unsigned long long* __restrict__ ndup) {
   extern __shared__ uint32_t s_c[];
+  __shared__ unsigned int s_dup;
   const int nb = w + 1;
   for (int d = threadIdx.x; d < nb; d += kB) s_c[d] = 0;
+  if (threadIdx.x == 0) s_dup = 0;
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(n, i0 + plen);
   for (int64_t i = i0 + threadIdx.x; i < i1; i += kB) {
-    const int d = (rsize && rsize[i] > 0) ? w : ring_owner_of(keys[i], pts, own, npts);
+    const bool dup = first && first[i] != (uint32_t)i;
+    const int d = (dup || (rsize && rsize[i] > 0)) ? w : ring_owner_of(keys[i], pts, own, npts);
     dest[i] = d;
     atomicAdd(&s_c[d], 1u);
+    if (dup) atomicAdd(&s_dup, 1u);
   }
   __syncthreads();
   for (int d = threadIdx.x; d < nb; d += kB) table[(int64_t)d * gridDim.x + blockIdx.x] = s_c[d];
+  if (threadIdx.x == 0 && ndup && s_dup) atomicAdd(ndup, (unsigned long long)s_dup);
 }
 
 // SET planning, fused: input row j goes to its owner and (fan-out) to every rank when
@@ -595,7 +605,8 @@ namespace {
 enum Slot {
   kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kOwnerS, kVpad, kTcnt,
   kTbytes, kSrec, kSval, kSvoff, kCntS, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
-  kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
+  kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kCoTab, kFirst,
+  kNumSlots
 };
 }  // namespace
 
@@ -655,7 +666,7 @@ T* RoutedStep::buf(int slot, size_t count) {
 void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
                       const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
                       const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues,
-                      int64_t ns, bool fanout, int64_t* table, hipStream_t s) {
+                      int64_t ns, bool fanout, int64_t* table, hipStream_t s, bool coalesce) {
   SH_CHECK(pts_ && own_ && npts_ > 0, "RoutedStep: ring not set");
   const int W = w_;
   const int nb = W + 1;
@@ -664,6 +675,14 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   have_replica_ = replica != nullptr;
   table_ = table;
   int64_t* extras = table + 6 * W;  // [table | rtable | extras]: one D2H in read_counts
+  first_ = nullptr;
+  uint32_t* co_tab = nullptr;
+  int64_t co_slots = 0;
+  if (coalesce && n > 0) {
+    co_slots = coalesce_table_slots(n);
+    co_tab = buf<uint32_t>(kCoTab, co_slots);
+    first_ = buf<uint32_t>(kFirst, n);
+  }
   // every buffer first (buf() may reallocate, which synchronises the device)
   uint64_t* rl_size = nullptr;
   if (replica) {
@@ -710,10 +729,14 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   RT_OK(hipGetLastError());
   RT_OK(hipEventRecord(ev_pjoin_, side_));
 
-  // GET rows: owner (or bucket W = local replica hit), counting sort by owner
-  if (replica) replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
+  // GET rows: coalesce duplicates (they stay local and are filled in by finish), owner
+  // (or bucket W = local replica hit / duplicate), counting sort by owner
+  RT_OK(hipMemsetAsync(extras + 2, 0, sizeof(int64_t), s));
+  if (first_) coalesce_keys(keys, n, co_tab, co_slots, first_, s);
+  if (replica) replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s, 0, -1, first_);
   hipLaunchKernelGGL(k_route_hist, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, keys, n, rl_size,
-                     pts_, own_, npts_, W, plen_g, dest_g, ws_g);
+                     pts_, own_, npts_, W, plen_g, dest_g, ws_g, first_,
+                     reinterpret_cast<unsigned long long*>(extras + 2));
   hipLaunchKernelGGL(k_gr_scan, dim3(1), dim3(1024), 0, s, ws_g, (int64_t)nb * Gg, nb, Gg, cnt_g_,
                      table, replica ? rl_off_ + n : nullptr, extras);
   if (n > 0)
@@ -727,9 +750,9 @@ std::vector<int64_t> RoutedStep::read_counts(const int64_t* rtable, hipStream_t 
   const int W = w_;
   rtable_ = rtable;
   SH_CHECK(rtable == table_ + 3 * W, "RoutedStep: rtable must follow table (one D2H)");
-  RT_OK(hipMemcpyAsync(host_, table_, (6 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  RT_OK(hipMemcpyAsync(host_, table_, (6 * W + 3) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   RT_OK(hipStreamSynchronize(s));
-  std::vector<int64_t> out(host_, host_ + 6 * W + 2);
+  std::vector<int64_t> out(host_, host_ + 6 * W + 3);
   n_local_ = out[6 * W];
   local_bytes_ = (uint64_t)out[6 * W + 1];
   n_remote_ = n_ - n_local_;
@@ -831,6 +854,7 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
                        sizes_in_, gscan_, have_replica_ ? rl_size_ : nullptr,
                        have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off);
   RT_OK(hipGetLastError());
+  if (first_) expand_coalesced(first_, n_, out_size, out_off, s);  // duplicates: claimer's record
   if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_join_, 0));  // join: later work sees the SETs
 }
 

@@ -165,7 +165,7 @@ class ShardedCache:
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
         self._co_table = None    # persistent GET-coalescing table (serve, side stream)
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
-                      "replica_hits": 0, "replica_refreshes": 0}
+                      "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0}
 
     # ------------------------------------------------------------------------------
     def _route(self, keys: torch.Tensor):
@@ -378,8 +378,8 @@ class ShardedCache:
         e = self._engine
         if e is None:
             e = self._engine = c.RoutedStep(w, me, dev.index)
-            # [table (3w) | rtable (3w) | extras (2)]: read back with one copy
-            self._xtable = torch.empty(6 * w + 2, dtype=i64, device=dev)
+            # [table (3w) | rtable (3w) | extras (3)]: read back with one copy
+            self._xtable = torch.empty(6 * w + 3, dtype=i64, device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
         if fanout and self._hot_dir is None:
@@ -394,7 +394,7 @@ class ShardedCache:
                batch.flags.data_ptr() if batch.flags is not None else 0,
                batch.expire.data_ptr() if batch.expire is not None else 0,
                batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
-               table.data_ptr(), st)
+               table.data_ptr(), st, self.coalesce)
         ph.next("count_exchange")
         all_to_all_single(rtable, table, group=self.group)
         h = e.read_counts(rtable.data_ptr(), st)                          # sync 1
@@ -406,7 +406,8 @@ class ShardedCache:
         send_v = [h[3 * p + 2] for p in range(w)]
         recv_v = [h[3 * w + 3 * p + 2] for p in range(w)]
         sq, rq, sv, rv = sum(send_q), sum(recv_q), sum(send_v), sum(recv_v)
-        n_local, local_bytes = h[6 * w], h[6 * w + 1]
+        # n_local counts replica hits and coalesced duplicates (neither leaves the GPU)
+        n_local, local_bytes, n_dup = h[6 * w], h[6 * w + 1], h[6 * w + 2]
         ph.next("pack_requests")
         send = torch.empty(sq + sv + 16, dtype=u8, device=dev)
         e.pack(send.data_ptr(), st)
@@ -438,7 +439,8 @@ class ShardedCache:
         e.finish(data.data_ptr(), recv.data_ptr(), rq + rv, self.shard._impl, rep, now,
                  out[0].data_ptr(), out[1].data_ptr(), st)
         self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
-        self.stats["replica_hits"] += n_local
+        self.stats["replica_hits"] += n_local - n_dup
+        self.stats["coalesced_gets"] += n_dup
         ph.end()
         # the value transfer completes in the background: GetResult.wait() before reading
         return GetResult(data, out[1], out[0], _pending=work)

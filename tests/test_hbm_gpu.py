@@ -280,10 +280,11 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
 
     wl = Workload(40000, cuda_dev)
     outs = []
-    for fused in (False, True):
+    for fused, co in ((False, False), (True, False), (True, True)):
         sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(world),
                           replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev))
         sc.fused = fused
+        sc.coalesce = co
         for s0 in range(0, 40000, 10000):
             sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
         sc.refresh_replica(2000, keys=wl.digests.index_select(0, wl.sample_ids(50000, 1)))
@@ -294,11 +295,15 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
             got.append([None if x is None else x[0]
                         for x in unpack_records(r.data, r.off, r.size)])
         outs.append((got, dict(sc.stats)))
-    (g0, s0), (g1, s1) = outs
+    (g0, s0), (g1, s1), (g2, s2) = outs
     assert g0 == g1
     assert s0 == s1
     assert sum(v is not None for v in g1[0]) == 8192     # every GET hits
     assert s1["replica_hits"] > 0
+    # coalesced: the same values; duplicates neither probed nor sent
+    assert g2 == g1
+    assert s2["coalesced_gets"] > 0 and s2["remote_gets"] < s1["remote_gets"]
+    assert 0 < s2["replica_hits"] < s1["replica_hits"]
 
 
 @pytest.mark.parametrize("n,nb", [(1, 2), (777, 3), (100003, 9), (300000, 65)])
