@@ -54,6 +54,31 @@ constexpr int kTileSegCap = 1024;          // segments staged in LDS per tile
 constexpr int kMaxGrid = 2048;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// SHELLAC_COALESCE_LOCAL=1: the coalescing lookup collapses duplicates inside each
+// 1024-key chunk only (no global table atomics); an A/B knob, see docs/PERF.md.
+int coalesce_local_only() {
+  static const int v = [] {
+    const char* e = getenv("SHELLAC_COALESCE_LOCAL");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
+
+// Grid caps for k_probe / k_coalesce (tuning knobs: SHELLAC_PROBE_GRID,
+// SHELLAC_COALESCE_GRID; 0 = the defaults below).
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+int probe_grid_cap() {
+  static const int v = env_int("SHELLAC_PROBE_GRID", 0);
+  return v > 0 ? v : kMaxGrid;
+}
+int coalesce_grid_cap() {
+  static const int v = env_int("SHELLAC_COALESCE_GRID", 0);
+  return v > 0 ? std::min(v, kMaxGrid) : kMaxGrid;
+}
+
 // Smallest segcopy tile in 16-B chunks (16 KiB); SHELLAC_SEGCOPY_MIN_TILE overrides it
 // for tuning sweeps (benchmarks/kernel_bench.py).
 // Variant (loads in flight per lane, target waves/SIMD); SHELLAC_SEGCOPY_VARIANT selects
@@ -216,13 +241,40 @@ __device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+constexpr int kCoProbe = 3;   // keys an 8-lane group of k_probe probes concurrently (loads in flight)
+constexpr int kProbeTile = 512;  // digests k_probe stages in LDS at a time
+
+// One 8-lane group's match of digest `d` against the bucket quarter-entry `v` its lane
+// l8 loaded: pair-lane shuffles join entry halves, max-reduce keeps the newest live
+// match. hl = stored loc (0: none), hv = its vlen; uniform in the group.
+__device__ __forceinline__ void group_match(const uint4 v, const Digest& d, int l8,
+                                            uint64_t head, uint64_t cap, uint32_t now,
+                                            uint64_t* hl_out, uint32_t* hv_out) {
+  const uint64_t a = pack2(v.x, v.y);   // even lane: d0   | odd lane: loc
+  const uint64_t c = pack2(v.z, v.w);   // even lane: d1   | odd lane: vlen | expire<<32
+  const uint64_t pa = __shfl_xor(a, 1);
+  const uint64_t pc = __shfl_xor(c, 1);
+  const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
+                   entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
+  uint64_t hl = hit ? pa : 0;
+  uint32_t hv = hit ? (uint32_t)pc : 0;
+#pragma unroll
+  for (int sh = 2; sh < 8; sh <<= 1) {
+    const uint64_t ol = __shfl_xor(hl, sh);
+    const uint32_t ov = __shfl_xor(hv, sh);
+    if (ol > hl) { hl = ol; hv = ov; }
+  }
+  *hl_out = hl;
+  *hv_out = hv;
+}
+
 // ---------------------------------------------------------------------------------
 // GET: probe
 // ---------------------------------------------------------------------------------
 // One 8-lane group per key: the group reads the key's first bucket (128 B, 16 B per
 // lane; even lanes hold digests, odd lanes loc/vlen/expire) and only on a miss its
 // second bucket. SETs fill the first bucket first, so a hit usually costs one line.
-__global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ keys, int64_t n,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_probe(const Digest* __restrict__ keys, int64_t n,
                                                   const Entry* __restrict__ index, uint64_t mask,
                                                   const uint64_t* __restrict__ head_ptr,
                                                   uint64_t reserve, uint64_t cap, uint32_t now,
@@ -240,49 +292,66 @@ __global__ __launch_bounds__(kBlock) void k_probe(const Digest* __restrict__ key
   // contiguous key range per workgroup (k_offsets scans it from the partial sums)
   const int64_t plen = part_len(n, gridDim.x);
   const int64_t i1 = min(n, (int64_t)(blockIdx.x + 1) * plen);
-  for (int64_t i = (int64_t)blockIdx.x * plen + (threadIdx.x >> 3); i < i1; i += kBlock / 8) {
-    if (first && first[i] != (uint32_t)i) {  // coalesced duplicate: served from its first row
-      if (l8 == 0) {
-        out_loc[i] = kMissLoc;
-        out_size[i] = 0;
-      }
-      continue;  // uniform in the 8-lane group
+  // The range is probed in tiles staged through LDS: one coalesced pass loads the
+  // tile's digests (and coalescing flags), so the only dependent global access per key
+  // is its bucket line. Each 8-lane group keeps kCoProbe bucket loads in flight (a probe
+  // is latency-bound: measured 65 us per 1M keys whether 1M or 300K of them probed,
+  // when every key also waited for its own digest load).
+  __shared__ Digest s_k[kProbeTile];
+  __shared__ uint8_t s_go[kProbeTile];
+  constexpr int kG = kBlock / 8;
+  for (int64_t t0 = (int64_t)blockIdx.x * plen; t0 < i1; t0 += kProbeTile) {
+    const int cnt = (int)min((int64_t)kProbeTile, i1 - t0);
+    for (int k = threadIdx.x; k < cnt; k += kBlock) {
+      s_k[k] = keys[t0 + k];
+      s_go[k] = !first || first[t0 + k] == (uint32_t)(t0 + k);  // duplicates skip
     }
-    const Digest d = keys[i];
-    uint64_t hl = 0;
-    uint32_t hv = 0;
-#pragma unroll 1
-    for (int round = 0; round < 2 && hl == 0; ++round) {  // hl is uniform in the group
-      const uint64_t b = round == 0 ? bucket1(d, mask) : bucket2(d, mask);
-      const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l8];
-      const uint64_t a = pack2(v.x, v.y);   // even lane: d0   | odd lane: loc
-      const uint64_t c = pack2(v.z, v.w);   // even lane: d1   | odd lane: vlen | expire<<32
-      const uint64_t pa = __shfl_xor(a, 1);
-      const uint64_t pc = __shfl_xor(c, 1);
-      const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
-                       entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
-      hl = hit ? pa : 0;
-      hv = hit ? (uint32_t)pc : 0;
+    __syncthreads();
+    for (int q0 = threadIdx.x >> 3; q0 < cnt; q0 += kG * kCoProbe) {
+      uint4 vb[kCoProbe];
 #pragma unroll
-      for (int s = 2; s < 8; s <<= 1) {
-        const uint64_t ol = __shfl_xor(hl, s);
-        const uint32_t ov = __shfl_xor(hv, s);
-        if (ol > hl) { hl = ol; hv = ov; }
+      for (int p = 0; p < kCoProbe; ++p) {
+        const int q = q0 + p * kG;  // uniform in the 8-lane group
+        if (q < cnt && s_go[q])
+          vb[p] = reinterpret_cast<const uint4*>(index + bucket1(s_k[q], mask) * kEntriesPerBucket)[l8];
+      }
+#pragma unroll
+      for (int p = 0; p < kCoProbe; ++p) {
+        const int q = q0 + p * kG;
+        if (q >= cnt) continue;
+        const int64_t i = t0 + q;
+        if (!s_go[q]) {  // coalesced duplicate: served from its first row
+          if (l8 == 0) {
+            out_loc[i] = kMissLoc;
+            out_size[i] = 0;
+          }
+          continue;
+        }
+        const Digest d = s_k[q];
+        uint64_t hl;
+        uint32_t hv;
+        group_match(vb[p], d, l8, head, cap, now, &hl, &hv);
+        if (hl == 0) {  // second bucket only on a miss in the first (uniform in the group)
+          const uint4 v2 =
+              reinterpret_cast<const uint4*>(index + bucket2(d, mask) * kEntriesPerBucket)[l8];
+          group_match(v2, d, l8, head, cap, now, &hl, &hv);
+        }
+        if (l8 == 0) {
+          ++ops;
+          if (hl) {
+            out_loc[i] = (hl - 1) % cap;
+            out_size[i] = item_bytes(hv);
+            ++hits;
+            bytes += hv;
+            psum += item_bytes(hv);
+          } else {
+            out_loc[i] = kMissLoc;
+            out_size[i] = 0;
+          }
+        }
       }
     }
-    if (l8 == 0) {
-      ++ops;
-      if (hl) {
-        out_loc[i] = (hl - 1) % cap;
-        out_size[i] = item_bytes(hv);
-        ++hits;
-        bytes += hv;
-        psum += item_bytes(hv);
-      } else {
-        out_loc[i] = kMissLoc;
-        out_size[i] = 0;
-      }
-    }
+    __syncthreads();  // the tile's LDS is reused
   }
   block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
               &CacheCounters::get_bytes);
@@ -313,20 +382,22 @@ constexpr int kCoPer = 4;                   // keys per thread per chunk
 constexpr int kCoKeys = kBlock * kCoPer;    // keys per chunk
 constexpr int kCoSlots = 2 * kCoKeys;       // LDS table slots (<= 50 % load)
 
+// 4 waves per SIMD (<= 128 VGPRs): the 1024-key chunks of a 1M batch (1024 workgroups)
+// are all resident at once (4 per CU, 33 KB LDS each) — at 130 VGPRs (3 waves) a
+// quarter of them ran as a second round (151 vs 95 us)
 template <bool PROBE>
-__global__ __launch_bounds__(kBlock) void k_coalesce(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_coalesce(
     const Digest* __restrict__ keys, int64_t n, int64_t plen, uint32_t* __restrict__ tab,
     uint32_t tmask, uint32_t* __restrict__ first, uint32_t* __restrict__ cslot,
     const Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ part) {
+    uint64_t* __restrict__ part, int local_only) {
+  __shared__ Digest s_k[kCoKeys];       // the chunk's digests (LDS compares, probe input)
   __shared__ uint32_t s_tab[kCoSlots];  // local row + 1
   __shared__ uint32_t s_rep[kCoKeys];   // global claimer of each local claimer
   __shared__ uint32_t s_dup[kCoKeys];   // local duplicates of each local claimer
   __shared__ uint32_t s_q[PROBE ? kCoKeys : 1];   // rows this chunk probes
-  __shared__ uint64_t s_loc[PROBE ? kCoKeys : 1]; // their log offsets
-  __shared__ uint32_t s_vl[PROBE ? kCoKeys : 1];  // their vlen (kSkipVlen = miss)
   __shared__ int s_qn;
   const uint64_t head = PROBE ? *head_ptr + reserve : 0;
   const int l8 = threadIdx.x & 7;
@@ -337,17 +408,20 @@ __global__ __launch_bounds__(kBlock) void k_coalesce(
     for (int k = threadIdx.x; k < kCoSlots; k += kBlock) s_tab[k] = 0;
     for (int k = threadIdx.x; k < kCoKeys; k += kBlock) s_dup[k] = 0;
     if (threadIdx.x == 0) s_qn = 0;
-    __syncthreads();
-    const Digest* kb = keys + base;
     Digest dk[kCoPer];
     uint32_t lrep[kCoPer];
-    // 1. local claims (rows strided by kBlock: coalesced 16-B loads)
+    // 0. stage the chunk (rows strided by kBlock: coalesced 16-B loads)
 #pragma unroll
     for (int u = 0; u < kCoPer; ++u) {
       const int j = u * kBlock + threadIdx.x;
       lrep[u] = (uint32_t)j;
-      if (j < cnt) dk[u] = kb[j];
+      if (j < cnt) {
+        dk[u] = keys[base + j];
+        s_k[j] = dk[u];
+      }
     }
+    __syncthreads();
+    // 1. local claims in LDS
 #pragma unroll
     for (int u = 0; u < kCoPer; ++u) {
       const int j = u * kBlock + threadIdx.x;
@@ -357,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void k_coalesce(
       for (int step = 0; step < kCoSlots; ++step) {
         const uint32_t v = atomicCAS(&s_tab[h], 0u, (uint32_t)j + 1u);
         if (v == 0) break;
-        const Digest o = kb[v - 1];  // keys are immutable: the claimer's digest is readable
+        const Digest o = s_k[v - 1];
         if (o.lo == d.lo && o.hi == d.hi) {
           lrep[u] = v - 1;
           atomicAdd(&s_dup[v - 1], 1u);
@@ -367,92 +441,119 @@ __global__ __launch_bounds__(kBlock) void k_coalesce(
       }
     }
     __syncthreads();
-    // 2. local claimers claim globally; global claimers queue for the probe
+    // 2. local claimers claim globally; global claimers queue for the probe. The first
+    //    attempt of all kCoPer rows is issued back to back (independent loads / CASes in
+    //    flight together), then each row resolves; a probed chain (slot held by another
+    //    digest) continues one row at a time. local_only: chunk-local collapsing only
+    //    (no global atomics; a digest repeated across chunks is probed and copied once
+    //    per chunk — still exact results).
+    {
+      bool act[kCoPer];
+      uint32_t hh[kCoPer], vv[kCoPer];
 #pragma unroll
-    for (int u = 0; u < kCoPer; ++u) {
-      const int j = u * kBlock + threadIdx.x;
-      if (j >= cnt || lrep[u] != (uint32_t)j) continue;
-      const Digest d = dk[u];
-      const uint32_t i = (uint32_t)(base + j);
-      uint32_t h = (uint32_t)(d.hi ^ (d.hi >> 29)) & tmask;
-      uint32_t rep = i;
-      bool look = s_dup[j] > 0;  // likely hot: read before CAS
-      for (uint32_t step = 0; step <= tmask; ++step) {
-        uint32_t v = look ? __hip_atomic_load(tab + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          : 0u;
-        if (v == 0) {
-          v = atomicCAS(tab + h, 0u, i + 1u);
-          if (v == 0) break;  // claimed: this row serves the digest
-        }
-        const Digest o = keys[v - 1];
-        if (o.lo == d.lo && o.hi == d.hi) {
-          rep = v - 1;
-          break;
-        }
-        h = (h + 1) & tmask;
-        look = true;  // a probed chain: read first from here on
+      for (int u = 0; u < kCoPer; ++u) {
+        const int j = u * kBlock + threadIdx.x;
+        act[u] = !local_only && j < cnt && lrep[u] == (uint32_t)j;
+        hh[u] = (uint32_t)(dk[u].hi ^ (dk[u].hi >> 29)) & tmask;
+        // likely hot (seen again in this chunk): read before the CAS
+        vv[u] = act[u] && s_dup[j] > 0
+                    ? __hip_atomic_load(tab + hh[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
       }
-      s_rep[j] = rep;
-      if (rep == i) {
-        if (cslot) cslot[i] = h;  // k_expand_out clears it after the step
-        if (PROBE) s_q[atomicAdd(&s_qn, 1)] = (uint32_t)j;
+#pragma unroll
+      for (int u = 0; u < kCoPer; ++u)
+        if (act[u] && vv[u] == 0)
+          vv[u] = atomicCAS(tab + hh[u], 0u, (uint32_t)(base + u * kBlock + threadIdx.x) + 1u);
+      Digest oo[kCoPer];
+#pragma unroll
+      for (int u = 0; u < kCoPer; ++u)
+        if (act[u] && vv[u] != 0) oo[u] = keys[vv[u] - 1];
+#pragma unroll
+      for (int u = 0; u < kCoPer; ++u) {
+        const int j = u * kBlock + threadIdx.x;
+        if (j >= cnt || lrep[u] != (uint32_t)j) continue;
+        const Digest d = dk[u];
+        const uint32_t i = (uint32_t)(base + j);
+        uint32_t rep = i, h = hh[u];
+        if (act[u] && vv[u] != 0) {
+          if (oo[u].lo == d.lo && oo[u].hi == d.hi) {
+            rep = vv[u] - 1;
+          } else {  // collision with another digest: linear probing, one row at a time
+            for (uint32_t step = 0; step < tmask; ++step) {
+              h = (h + 1) & tmask;
+              uint32_t v = __hip_atomic_load(tab + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v == 0) {
+                v = atomicCAS(tab + h, 0u, i + 1u);
+                if (v == 0) break;  // claimed
+              }
+              const Digest o = keys[v - 1];
+              if (o.lo == d.lo && o.hi == d.hi) {
+                rep = v - 1;
+                break;
+              }
+            }
+          }
+        }
+        s_rep[j] = rep;
+        if (rep == i) {
+          if (cslot) cslot[i] = local_only ? 0u : h;  // k_expand_out clears it
+          if (PROBE) s_q[atomicAdd(&s_qn, 1)] = (uint32_t)j;
+        }
       }
     }
     __syncthreads();
     if (PROBE) {
       // 2b. probe the queued digests, one 8-lane group per digest (each lane one 16-B
-      //     quarter-entry of the 128-B bucket, as k_probe)
+      //     quarter-entry of the 128-B bucket, as k_probe), kCoProbe digests per group
+      //     in flight; results go straight to out_loc / out_size
       const int qn = s_qn;
-      for (int q = threadIdx.x >> 3; q < qn; q += kBlock / 8) {
-        const int j = (int)s_q[q];
-        const Digest d = kb[j];
-        uint64_t hl = 0;
-        uint32_t hv = 0;
-#pragma unroll 1
-        for (int round = 0; round < 2 && hl == 0; ++round) {  // hl is uniform in the group
-          const uint64_t b = round == 0 ? bucket1(d, mask) : bucket2(d, mask);
-          const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l8];
-          const uint64_t a = pack2(v.x, v.y);
-          const uint64_t c = pack2(v.z, v.w);
-          const uint64_t pa = __shfl_xor(a, 1);
-          const uint64_t pc = __shfl_xor(c, 1);
-          const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
-                           entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
-          hl = hit ? pa : 0;
-          hv = hit ? (uint32_t)pc : 0;
+      constexpr int kG = kBlock / 8;
+      for (int q0 = threadIdx.x >> 3; q0 < qn; q0 += kG * kCoProbe) {
+        uint4 vb[kCoProbe];
 #pragma unroll
-          for (int sh = 2; sh < 8; sh <<= 1) {
-            const uint64_t ol = __shfl_xor(hl, sh);
-            const uint32_t ov = __shfl_xor(hv, sh);
-            if (ol > hl) { hl = ol; hv = ov; }
-          }
+        for (int p = 0; p < kCoProbe; ++p) {
+          const int q = q0 + p * kG;  // uniform in the 8-lane group
+          if (q < qn)
+            vb[p] = reinterpret_cast<const uint4*>(
+                index + bucket1(s_k[s_q[q]], mask) * kEntriesPerBucket)[l8];
         }
-        if (l8 == 0) {
-          ++ops;
-          if (hl) {
-            s_loc[j] = (hl - 1) % cap;
-            s_vl[j] = hv;
-            ++hits;
-            bytes += hv;
-            psum += item_bytes(hv);
-          } else {
-            s_vl[j] = kSkipVlen;
+#pragma unroll
+        for (int p = 0; p < kCoProbe; ++p) {
+          const int q = q0 + p * kG;
+          if (q >= qn) continue;
+          const int j = (int)s_q[q];
+          const Digest d = s_k[j];
+          uint64_t hl;
+          uint32_t hv;
+          group_match(vb[p], d, l8, head, cap, now, &hl, &hv);
+          if (hl == 0) {  // second bucket only on a miss in the first (uniform in the group)
+            const uint4 v2 =
+                reinterpret_cast<const uint4*>(index + bucket2(d, mask) * kEntriesPerBucket)[l8];
+            group_match(v2, d, l8, head, cap, now, &hl, &hv);
+          }
+          if (l8 == 0) {
+            ++ops;
+            out_loc[base + j] = hl ? (hl - 1) % cap : kMissLoc;
+            out_size[base + j] = hl ? item_bytes(hv) : 0;
+            if (hl) {
+              ++hits;
+              bytes += hv;
+              psum += item_bytes(hv);
+            }
           }
         }
       }
-      __syncthreads();
     }
-    // 3. every row takes its local claimer's global claimer
+    // 3. every row takes its local claimer's global claimer; non-claimers are empty
 #pragma unroll
     for (int u = 0; u < kCoPer; ++u) {
       const int j = u * kBlock + threadIdx.x;
       if (j >= cnt) continue;
       const uint32_t f = s_rep[lrep[u]];
       first[base + j] = f;
-      if (PROBE) {
-        const bool hit = f == (uint32_t)(base + j) && s_vl[j] != kSkipVlen;
-        out_loc[base + j] = hit ? s_loc[j] : kMissLoc;
-        out_size[base + j] = hit ? item_bytes(s_vl[j]) : 0;
+      if (PROBE && f != (uint32_t)(base + j)) {
+        out_loc[base + j] = kMissLoc;
+        out_size[base + j] = 0;
       }
     }
     __syncthreads();  // LDS is reused by the next chunk
@@ -1260,7 +1361,8 @@ void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table
   const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
                      (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, nullptr,
-                     nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr);
+                     nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
+                     0);
   HIP_OK(hipGetLastError());
 }
 
@@ -1414,7 +1516,7 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
     if (ht) *ht = 0;
     return;
   }
-  const int grid = grid_for(n * 8, kBlock, kMaxGrid);
+  const int grid = grid_for(n * 8, kBlock, std::min(kMaxGrid, probe_grid_cap()));
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first);
   HIP_OK(hipGetLastError());
@@ -1443,13 +1545,13 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
   // contiguous whole chunks per workgroup, at most kMaxGrid partial sums
   const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
-  const int64_t per = (chunks + kMaxGrid - 1) / kMaxGrid;
+  const int64_t per = (chunks + coalesce_grid_cap() - 1) / coalesce_grid_cap();
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
-                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_);
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only());
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }

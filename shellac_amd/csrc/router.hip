@@ -732,8 +732,13 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   // GET rows: coalesce duplicates (they stay local and are filled in by finish), owner
   // (or bucket W = local replica hit / duplicate), counting sort by owner
   RT_OK(hipMemsetAsync(extras + 2, 0, sizeof(int64_t), s));
-  if (first_) coalesce_keys(keys, n, co_tab, co_slots, first_, s);
-  if (replica) replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s, 0, -1, first_);
+  if (first_ && replica)  // one pass: each digest's claiming row probes the replica
+    replica->lookup_coalesced(keys, n, co_tab, co_slots, first_, rl_loc_, rl_size_, rl_off_, now,
+                              s);
+  else if (first_)
+    coalesce_keys(keys, n, co_tab, co_slots, first_, s);
+  else if (replica)
+    replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
   hipLaunchKernelGGL(k_route_hist, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, keys, n, rl_size,
                      pts_, own_, npts_, W, plen_g, dest_g, ws_g, first_,
                      reinterpret_cast<unsigned long long*>(extras + 2));

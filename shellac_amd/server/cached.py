@@ -54,10 +54,14 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--gpus", type=str, default=None)
     p.add_argument("--hbm-gb", type=float, default=16.0)
     p.add_argument("--batch-us", type=int, default=0)
+    p.add_argument("--no-hbm-filter", action="store_true",
+                   help="send every GET to the GPUs (no host presence filter)")
+    p.add_argument("--hbm-spin-us", type=int, default=50)
     a = p.parse_args(argv)
     opts = ({"dram_mb": a.dram_mb} if a.cache == "dram" else
             {"gpus": [int(x) for x in a.gpus.split(",")] if a.gpus else None, "hbm_gb": a.hbm_gb,
-             "batch_us": a.batch_us})
+             "batch_us": a.batch_us, "hbm_filter": not a.no_hbm_filter,
+             "spin_us": a.hbm_spin_us})
     node = CacheNode(port=a.port, bind=a.bind, threads=a.threads, kind=a.cache, **opts).start()
     print(f"shellac-cached on port {node.port} ({a.cache})", flush=True)
     stop = threading.Event()

@@ -185,6 +185,11 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--gpus", type=str, default=None, help="GPU ids for --cache hbm, e.g. 0,1,2,3")
     p.add_argument("--hbm-gb", type=float, default=16.0, help="HBM value-log GiB per GPU")
     p.add_argument("--dram-mb", type=int, default=1024, help="host cache MiB for --cache dram")
+    p.add_argument("--no-hbm-filter", action="store_true",
+                   help="send every GET to the GPUs (default: a host presence filter answers "
+                        "GETs of never-stored keys without a GPU batch)")
+    p.add_argument("--hbm-spin-us", type=int, default=50,
+                   help="HBM batcher polls for new requests this long before sleeping")
     p.add_argument("--batch-us", type=int, default=0,
                    help="HBM batch linger (us); 0 = natural batching (what queued during the "
                         "previous batch)")
@@ -236,7 +241,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  health_interval_ms=args.health_interval_ms, health_fails=args.health_fails,
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
-                 **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us}
+                 **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,
+                     "hbm_filter": not args.no_hbm_filter, "spin_us": args.hbm_spin_us}
                     if kind == "hbm" else {}),
                  **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))
     print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)
