@@ -191,9 +191,11 @@ PYBIND11_MODULE(_shellac_core, m) {
   });
   m.def("coalesce_table_slots", &coalesce_table_slots);
   m.def("coalesce_keys", [](uintptr_t keys, int64_t n, uintptr_t table, int64_t slots,
-                            uintptr_t first, uintptr_t s) {
-    coalesce_keys(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first), S(s));
-  });
+                            uintptr_t first, uintptr_t s, uintptr_t cslot, bool table_clean) {
+    coalesce_keys(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first), S(s),
+                  P<uint32_t>(cslot), table_clean);
+  }, py::arg("keys"), py::arg("n"), py::arg("table"), py::arg("slots"), py::arg("first"),
+     py::arg("stream"), py::arg("cslot") = 0, py::arg("table_clean") = false);
   m.def("expand_coalesced", [](uintptr_t first, int64_t n, uintptr_t size, uintptr_t off,
                                uintptr_t s) {
     expand_coalesced(P<const uint32_t>(first), n, P<uint64_t>(size), P<uint64_t>(off), S(s));

@@ -161,6 +161,7 @@ class HbmCache {
   uint32_t* dd_slot_ = nullptr;
   uint64_t* set_size_ = nullptr;
   uint64_t* set_off_ = nullptr;
+  uint32_t* set_claim_ = nullptr;  // entry each SET row claimed (k_set_fixup)
   uint32_t dd_mask_ = 0;
   uint64_t ws_gen_ = 0;  // bumped when the SET workspace moves (invalidates graphs)
   std::mutex mu_;
@@ -185,7 +186,8 @@ void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_of
 // serves all its duplicates). `table` is scratch of coalesce_table_slots(n) u32 words.
 int64_t coalesce_table_slots(int64_t n);
 void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
-                   uint32_t* first, hipStream_t s);
+                   uint32_t* first, hipStream_t s, uint32_t* cslot = nullptr,
+                   bool table_clean = false);
 // After the gather of a coalesced lookup: size[i], off[i] of every duplicate row i :=
 // those of first[i] (in place), so each request addresses its claimer's record.
 void expand_coalesced(const uint32_t* first, int64_t n, uint64_t* size, uint64_t* off,

@@ -923,14 +923,20 @@ __global__ __launch_bounds__(kBlock) void k_small_get(
   // stores (mapped host memory) visible system-wide, then counts itself done; the last
   // one resets the counter for the next launch and publishes the total into a pinned
   // host slot the batcher thread spins on.
+  // Every wave drains its own stores (vmcnt) around the system-scope release fence:
+  // ROCm 7.2 can drop the fence's own wait, and a drain by lane 0 alone left a rare
+  // stale record behind the published total (1 of ~3000 one-key GETs missed).
   if (done_slot) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned int prev = atomicAdd(done_ctr, 1u);
       if (prev == gridDim.x - 1) {
         atomicExch(done_ctr, 0u);
         __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(done_slot, total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
@@ -992,7 +998,7 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
-    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr) {
+    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim) {
   const int l16 = threadIdx.x & 15;
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
@@ -1007,6 +1013,7 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       dd_keys[sl] = 0ull;
       dd_win[sl] = -1;
     }
+    if (l16 == 0) claim[i] = ~0u;  // no entry (yet)
     if (size[i] == 0) continue;  // uniform across the 16-lane group
     const Digest d = keys[i];
     const uint64_t myloc = base + off[i] + 1;
@@ -1064,6 +1071,11 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       const uint64_t expected = __shfl(pa, gbase + 2 * target);
       Entry* const slot = index + (target < 4 ? b1 : b2) * kEntriesPerBucket + (target & 3);
       int ok = 0;
+      // The CAS on loc arbitrates the entry; the digest / vlen words written after it can
+      // land late (another insert of this batch may re-claim the entry in between, and
+      // a late digest write would pair its key with the other key's loc), so the winner
+      // records the entry and k_set_fixup rewrites the words of every entry whose loc
+      // is still its own once this kernel is done.
       if (l16 == 0) {
         const unsigned long long prev = atomicCAS(
             reinterpret_cast<unsigned long long*>(&slot->loc), (unsigned long long)expected,
@@ -1072,6 +1084,7 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
           slot->d0 = d.lo;
           slot->d1 = d.hi;
           *reinterpret_cast<uint64_t*>(&slot->vlen) = pack2(myvlen, myexp);
+          claim[i] = (uint32_t)(slot - index);
           ok = 1;
           evicted += evict ? 1 : 0;
           bytes += myvlen;
@@ -1088,6 +1101,28 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
 // ---------------------------------------------------------------------------------
 // DELETE / SWEEP
 // ---------------------------------------------------------------------------------
+// After k_set_index (kernel boundary: every CAS and word write is visible): each entry
+// whose loc is still the one a row of this batch claimed gets that row's digest and
+// vlen|expire words again, so no entry pairs one key's digest with another key's loc.
+__global__ __launch_bounds__(kBlock) void k_set_fixup(
+    const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ expire,
+    const uint64_t* __restrict__ head_ptr, const uint32_t* __restrict__ claim,
+    Entry* __restrict__ index) {
+  const uint64_t base = *head_ptr;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t c = claim[i];
+    if (c == ~0u) continue;
+    Entry* const e = index + c;
+    if (e->loc != base + off[i] + 1) continue;  // evicted again within the batch
+    const Digest d = keys[i];
+    e->d0 = d.lo;
+    e->d1 = d.hi;
+    *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vlen[i], expire ? expire[i] : 0u);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_delete(const Digest* __restrict__ keys, int64_t n,
                                                    Entry* __restrict__ index, uint64_t mask,
                                                    const uint64_t* __restrict__ head_ptr,
@@ -1352,15 +1387,15 @@ int64_t coalesce_table_slots(int64_t n) {
 }
 
 void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
-                   uint32_t* first, hipStream_t s) {
+                   uint32_t* first, hipStream_t s, uint32_t* cslot, bool table_clean) {
   if (n <= 0) return;
   SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
   SH_CHECK(table_slots >= 2 * n && (table_slots & (table_slots - 1)) == 0,
            "coalesce: table needs a power of two >= 2n slots");
-  HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
+  if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
   const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
-                     (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, nullptr,
+                     (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, cslot,
                      nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
                      0);
   HIP_OK(hipGetLastError());
@@ -1467,7 +1502,7 @@ HbmCache::~HbmCache() {
   (void)hipFree(dd_win_);
   (void)hipFree(dd_slot_);
   (void)hipFree(set_size_);
-  (void)hipFree(set_off_);
+  (void)hipFree(set_off_); (void)hipFree(set_claim_);
 }
 
 uint64_t HbmCache::hbm_bytes() const {
@@ -1481,7 +1516,7 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   while (cap < n) cap *= 2;
   HIP_OK(hipDeviceSynchronize());
   (void)hipFree(dd_keys_); (void)hipFree(dd_win_); (void)hipFree(dd_slot_);
-  (void)hipFree(set_size_); (void)hipFree(set_off_);
+  (void)hipFree(set_size_); (void)hipFree(set_off_); (void)hipFree(set_claim_);
   const uint64_t tslots = (uint64_t)cap * 2;
   HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
@@ -1491,6 +1526,7 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
+  HIP_OK(hipMalloc(&set_claim_, cap * sizeof(uint32_t)));
   dd_mask_ = (uint32_t)(tslots - 1);
   set_cap_ = cap;
   ++ws_gen_;
@@ -1640,7 +1676,10 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
-                     cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_);
+                     cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
+                     set_claim_);
+  hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
+                     set_off_, vlen, expire, cur_head(), set_claim_, index_);
   HIP_OK(hipGetLastError());
 }
 

@@ -290,12 +290,13 @@ class ShardedCache:
             main = torch.cuda.current_stream(self.device)
             side.wait_stream(main)  # the previous step's gather is done with the log
             now = sh.now() if now is None else now
-        table = self._coalesce_table(n) if (self.coalesce and side is not None) else None
         if self.coalesce:
+            table = self._coalesce_table(n) if side is not None else None
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
                                                    table=table)
         else:
-            lk, first, cslot = sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None
+            lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound, total_slot=0),
+                                       None, None, None)
         if side is None:
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now)
@@ -325,7 +326,9 @@ class ShardedCache:
 
     def _coalesce_table(self, n: int) -> torch.Tensor:
         """Persistent, zeroed GET-coalescing table (every serve step leaves it zeroed:
-        expand_out clears the slots its batch claimed)."""
+        expand_out clears the slots its batch claimed). Coalescing the next batch
+        under this step's gather on a third stream (two tables, ping-pong) was measured
+        slower, 0.35 vs 0.30 ms/step: both passes compete for the same memory system."""
         slots = int(_core().coalesce_table_slots(n))
         t = self._co_table
         if t is None or t.numel() < slots:

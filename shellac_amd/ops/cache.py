@@ -111,24 +111,34 @@ def unpack_records(out: torch.Tensor, off: torch.Tensor, size: torch.Tensor) -> 
     return res
 
 
-def coalesce(keys: torch.Tensor) -> Optional[torch.Tensor]:
+def coalesce(keys: torch.Tensor, table: Optional[torch.Tensor] = None):
     """GET coalescing (request collapsing inside a batch). Returns ``first`` (int32
     [n]): the row that serves row i — one row per distinct digest claims it with a CAS
     in an open-addressing table (``k_coalesce``), its duplicates point at that row.
     Pass it to ``CacheShard.lookup(first=...)`` (duplicates skip the index probe and
     the gather) and call ``expand(first, lookup)`` after the gather, so every request
     addresses its claimer's record. CPU shards: ``None`` (the host engine probes every
-    row; results are the same values)."""
+    row; results are the same values).
+    ``table`` (a caller-owned, zeroed table, see ``CacheShard.lookup_coalesced``):
+    returns ``(first, cslot)`` and ``expand_out(..., table, cslot)`` must clean it."""
     if not keys.is_cuda or keys.shape[0] == 0:
-        return None
+        return None if table is None else (None, None)
     c = core()
     n = keys.shape[0]
-    slots = int(c.coalesce_table_slots(n))
-    table = torch.empty(slots, dtype=torch.int32, device=keys.device)
+    cslot = None
+    if table is None:
+        slots = int(c.coalesce_table_slots(n))
+        table = torch.empty(slots, dtype=torch.int32, device=keys.device)
+    else:
+        slots = table.numel()
+        if slots < int(c.coalesce_table_slots(n)) or slots & (slots - 1):
+            raise ValueError("coalescing table too small or not a power of two")
+        cslot = torch.empty(n, dtype=torch.int32, device=keys.device)
     first = torch.empty(n, dtype=torch.int32, device=keys.device)
     c.coalesce_keys(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
-                    _stream_handle(keys.device))
-    return first
+                    _stream_handle(keys.device), cslot.data_ptr() if cslot is not None else 0,
+                    cslot is not None)
+    return first if cslot is None else (first, cslot)
 
 
 def expand(first: Optional[torch.Tensor], size: torch.Tensor, off: torch.Tensor) -> None:

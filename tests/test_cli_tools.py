@@ -29,6 +29,10 @@ def test_argparse_reference_flags():
     a = build_arg_parser().parse_args(["-s", "a:81,b", "-c", "m1,m2:11212", "-p", "9090", "-t", "60", "-z"])
     assert (a.servers, a.caches, a.port, a.ttl, a.compress) == ("a:81,b", "m1,m2:11212", 9090, 60, True)
     assert parse_server_list("127.0.0.1:81,localhost", 80) == [("127.0.0.1", 81), ("127.0.0.1", 80)]
+    g = build_arg_parser().parse_args(["-s", "a", "--cache", "hbm", "--no-hbm-filter",
+                                       "--hbm-spin-us", "0"])
+    assert (g.cache, g.no_hbm_filter, g.hbm_spin_us) == ("hbm", True, 0)
+    assert build_arg_parser().parse_args(["-s", "a"]).no_hbm_filter is False
 
 
 def test_missing_servers_exits_1(capsys):

@@ -517,3 +517,27 @@ def test_coalesced_get_and_serve_match_uncoalesced(cuda_dev):
     assert b[4] < a[4] // 2
     for i in range(0, 200000, 997):
         assert b[0][i] is not None and b[0][i][0] == wl.expected_value(int(ids[i]))
+
+
+
+@pytest.mark.parametrize("bs,pad", [(300, 512), (1500, 2048), (3000, 4096)])
+def test_set_index_under_same_bucket_contention(cuda_dev, bs, pad):
+    """3000 keys into a 1024-slot index in large batches (~12 inserts per bucket pair per
+    batch, padded with skip rows like the HTTP backend's micro-batches): every key that
+    hits must return its own record (the insert claims an entry with a lock value before
+    it writes the digest; a late digest write once paired keys with other keys' records)."""
+    sh = CacheShard(64 << 20, 256, 1 << 16, cuda_dev)
+    keys = [b"/pf/%d" % i for i in range(3000)]
+    for s in range(0, 3000, bs):
+        kk = keys[s:s + bs]
+        d = torch.zeros((pad, 2), dtype=torch.int64)
+        d[: len(kk)] = digest_strings(kk)
+        v, vo, vl = pack_values([b"v%d" % i for i in range(s, s + len(kk))] + [b""] * (pad - len(kk)))
+        vl[len(kk):] = -1  # kSkipVlen padding rows
+        vo[len(kk):] = 0
+        sh.store(d.to(cuda_dev), v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev))
+    lk = sh.lookup(digest_strings(keys).to(cuda_dev))
+    recs = unpack_records(sh.gather(lk), lk.off[:3000], lk.size[:3000])
+    hits = [i for i, r in enumerate(recs) if r is not None]
+    assert len(hits) > 900
+    assert all(recs[i][0] == b"v%d" % i for i in hits)
