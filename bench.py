@@ -253,6 +253,15 @@ def main():
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
+        # every hit of the whole last batch: its record's header names the requested digest
+        keys_last = gets[(args.steps - 1) % P]
+        hit = res.size > 0
+        words = res.data[: res.data.numel() // 8 * 8].view(torch.int64)
+        at = torch.where(hit, torch.div(res.off, 8, rounding_mode="floor"), torch.zeros_like(res.off))
+        wrong = hit & ((words.index_select(0, at) != keys_last[:, 0]) |
+                       (words.index_select(0, at + 1) != keys_last[:, 1]))
+        log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
+                  f"another key")
 
     sm = {} if (args.no_smoke or dev.type != "cuda" or sim) else smoke(rank, world, dev)
 

@@ -38,3 +38,4 @@ def test_bench_cpu_rehearsal_world2():
     assert out["config"]["global_batch"] == 2 * (4096 + 512)
     assert out["get_hit_ratio"] == 1.0
     assert "0 mismatches" in p.stderr
+    assert "check: 0 of 4096 hit records name another key" in p.stderr
