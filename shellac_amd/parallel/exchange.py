@@ -29,13 +29,26 @@ class MirrorComm:
         self.world, self.rank = int(world), int(rank)
 
 
+class BounceComm:
+    """Device tensors exchanged through a host (gloo) process group: every collective
+    copies to the CPU, runs over gloo, and copies back (synchronously).
+
+    Test tool: it runs the real multi-process routed step — asymmetric traffic, every
+    rank its own shard — when the ranks share one GPU and RCCL cannot be used (RCCL
+    refuses two ranks on one device). Never a performance path."""
+
+    def __init__(self, pg=None):
+        self.pg = pg
+        self.rank, self.world = dist.get_rank(pg), dist.get_world_size(pg)
+
+
 class _Done:
     def wait(self):
         return True
 
 
 def dist_info(group=None) -> tuple[int, int]:
-    if isinstance(group, MirrorComm):
+    if isinstance(group, (MirrorComm, BounceComm)):
         return group.rank, group.world
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(group), dist.get_world_size(group)
@@ -50,6 +63,12 @@ def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, output_split_sizes=N
             raise ValueError("mirror all_to_all needs symmetric splits")
         out.copy_(inp.view(out.shape) if out.shape != inp.shape else inp)
         return _Done() if async_op else None
+    if isinstance(group, BounceComm):
+        host_out = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(host_out, inp.cpu(), output_split_sizes=output_split_sizes,
+                               input_split_sizes=input_split_sizes, group=group.pg)
+        out.copy_(host_out)
+        return _Done() if async_op else None
     return dist.all_to_all_single(out, inp, output_split_sizes=output_split_sizes,
                                   input_split_sizes=input_split_sizes, group=group,
                                   async_op=async_op)
@@ -60,6 +79,12 @@ def all_gather(tensors: list, t: torch.Tensor, group=None) -> None:
         for x in tensors:
             x.copy_(t)
         return
+    if isinstance(group, BounceComm):
+        host = [torch.empty(x.shape, dtype=x.dtype) for x in tensors]
+        dist.all_gather(host, t.cpu(), group=group.pg)
+        for x, h in zip(tensors, host):
+            x.copy_(h)
+        return
     dist.all_gather(tensors, t, group=group)
 
 
@@ -69,11 +94,18 @@ def all_reduce(t: torch.Tensor, op=None, group=None) -> None:
         if op == dist.ReduceOp.SUM:
             t.mul_(group.world)
         return
+    if isinstance(group, BounceComm):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group.pg)
+        t.copy_(h)
+        return
     dist.all_reduce(t, op=op, group=group)
 
 
 def barrier(group=None) -> None:
-    if not isinstance(group, MirrorComm):
+    if isinstance(group, BounceComm):
+        dist.barrier(group=group.pg)
+    elif not isinstance(group, MirrorComm):
         dist.barrier(group=group)
 
 

@@ -270,7 +270,7 @@ def test_lookup_offsets_fused_scan(cuda_dev, n):
     assert shard.host_total(3) == int(ref[-1])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
     """The fused native routed step (csrc/router.hip) returns exactly what the
     framework-op version returns, on one GPU with mirrored all-to-alls."""

@@ -1,0 +1,75 @@
+"""The fused routed serving step across real processes (GPU): 2 and 3 ranks, each with
+its own shard and replica on the box's one GPU, collectives bounced through gloo
+(BounceComm: RCCL refuses two ranks on one device). Unlike the single-process mirror
+(MirrorComm), traffic here is asymmetric and every owner is a different process —
+the path the 8-GPU scaling run takes, minus RCCL itself."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from test_distributed_cpu import _run_world
+
+pytestmark = pytest.mark.gpu
+
+
+def _routed_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+        from shellac_amd.parallel.exchange import BounceComm
+
+        dev = torch.device("cuda", 0)
+        comm = BounceComm()
+        shard = CacheShard(64 << 20, 1 << 12, 1 << 14, dev)
+        replica = CacheShard(16 << 20, 1 << 10, 1 << 14, dev)
+        sc = ShardedCache(shard, group=comm, replica=replica)
+        assert sc.fused and sc.coalesce
+
+        def batch(keys, vals):
+            v, vo, vl = pack_values(vals, dev)
+            return SetBatch(digest_strings(keys, dev), v, vo, vl,
+                            flags=torch.full((len(keys),), rank, dtype=torch.int32, device=dev))
+
+        def values(res):
+            res.wait()
+            return [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+
+        keys = [f"/m{r}/{i}".encode() for r in range(world) for i in range(200)]
+        mine = [k for k in keys if k.startswith(f"/m{rank}/".encode())]
+        v1 = {k: b"v1" + k * (1 + len(k) % 7) for k in keys}
+        # step 1: every rank fills its own keys; GETs (with duplicates) all miss
+        dup = keys[:50] * 3
+        res = sc.serve(digest_strings(keys + dup, dev), batch(mine, [v1[k] for k in mine]))
+        assert values(res) == [None] * (len(keys) + len(dup))
+        # hot set from a skewed sample, replicated on every rank
+        sc.get(digest_strings(keys[:20] * 10, dev))
+        sc.refresh_replica(20)
+        # step 2: duplicate-heavy GET batch, every key owned somewhere else or here;
+        # rank 1 overwrites some hot and cold keys (GETs see the state before the SETs)
+        upd = keys[:5] + keys[100:110] if rank == 1 else []
+        req = keys[:30] * 5 + keys + [b"/none"] * 3
+        res = sc.serve(digest_strings(req, dev), batch(upd, [b"v2" + k for k in upd]))
+        assert values(res) == [v1[k] for k in req[:-3]] + [None] * 3
+        # step 3: the overwrites are visible on every rank (replicas written through)
+        res = sc.serve(digest_strings(req, dev), batch([], []))
+        new = {k: b"v2" + k for k in keys[:5] + keys[100:110]}
+        assert values(res) == [new.get(k, v1[k]) for k in req[:-3]] + [None] * 3
+        st = sc.stats
+        assert st["coalesced_gets"] > 0 and st["replica_hits"] > 0 and st["remote_gets"] > 0
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fused_routed_step_multiprocess(world):
+    _run_world(_routed_worker, world, timeout=180)
