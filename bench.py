@@ -68,6 +68,10 @@ def parse():
                          "(DRAM shards); never a performance number")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="probe and copy every GET request (no in-batch request collapsing)")
+    ap.add_argument("--bounce", action="store_true",
+                    help="functional rehearsal of the N-rank GPU step on ONE GPU: every rank on "
+                         "cuda:0, collectives bounced through gloo (RCCL refuses two ranks on "
+                         "one device); never a performance number")
     ap.add_argument("--no-smoke", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
@@ -123,7 +127,12 @@ def main():
         raise SystemExit("--simulate-world runs as a single process")
     if world != args.gpus and not sim:
         log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    if args.device == "cuda":
+    bounce = args.bounce and args.device == "cuda" and world > 1
+    if bounce:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo")
+    elif args.device == "cuda":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
@@ -144,6 +153,10 @@ def main():
         group = MirrorComm(sim)
         world = sim
     real_world = 1 if sim else world
+    if bounce:
+        from shellac_amd.parallel.exchange import BounceComm
+
+        group = BounceComm()
 
     if args.replicate is None:
         # xGMI is point-to-point: N ranks talk over N-1 links each, so at small N the
@@ -171,7 +184,7 @@ def main():
         replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
                              max_item=1 << 20, device=dev)
     data_group = None
-    if real_world > 1:
+    if real_world > 1 and not bounce:
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
     sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group)
@@ -226,7 +239,8 @@ def main():
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
+    t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
     if real_world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t)
@@ -238,7 +252,7 @@ def main():
     agg = torch.tensor([after["get_hits"] - before["get_hits"], after["get_ops"] - before["get_ops"],
                         after["get_bytes"] - before["get_bytes"], rep_hits,
                         sc.stats["get_requests"] - st0["get_requests"]], dtype=torch.int64,
-                       device=dev)
+                       device=rdev)
     if real_world > 1:
         dist.all_reduce(agg)
     hits, gops, gbytes, rep_hits, greq = (int(v) for v in agg.tolist())
@@ -263,7 +277,7 @@ def main():
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
                   f"another key")
 
-    sm = {} if (args.no_smoke or dev.type != "cuda" or sim) else smoke(rank, world, dev)
+    sm = {} if (args.no_smoke or dev.type != "cuda" or sim or bounce) else smoke(rank, world, dev)
 
     ops_per_step = (args.batch + args.sets) * world
     ms = elapsed / args.steps * 1e3
@@ -307,6 +321,10 @@ def main():
     }
     if dev.type != "cuda":
         out["data"] = "cpu rehearsal over gloo: functional only, not a performance number"
+    if bounce:
+        out["metric"] = "cache_ops_per_s_rehearsal"
+        out["data"] = (f"functional rehearsal: {world} ranks on one GPU, collectives bounced "
+                       "through gloo; not a performance number")
     if sim:
         out["metric"] = "cache_ops_per_s_simulated"
         out["data"] = (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
