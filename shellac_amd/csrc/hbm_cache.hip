@@ -1463,6 +1463,7 @@ void mfma_hello(const uint16_t* a, const uint16_t* b, float* c, int tiles, hipSt
 HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   SH_CHECK(cfg_.nbuckets >= 2 && (cfg_.nbuckets & (cfg_.nbuckets - 1)) == 0,
            "nbuckets must be a power of two >= 2");
+  SH_CHECK(cfg_.nbuckets * kEntriesPerBucket < (1ull << 32), "index too large (u32 entry ids)");
   SH_CHECK(cfg_.log_bytes >= 4096 && cfg_.log_bytes % 16 == 0, "log_bytes must be >=4096, %16");
   SH_CHECK(cfg_.max_item > 0 && item_bytes(cfg_.max_item) * 2 <= cfg_.log_bytes,
            "max_item too large for the log");
