@@ -164,6 +164,7 @@ class HbmBackend : public CacheBackend {
   std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};
   std::atomic<uint64_t> batch_ns_{0};
   std::atomic<uint64_t> sweeps_{0}, live_objects_{0}, live_bytes_{0};
+  std::atomic<uint64_t> coalesced_gets_{0};  // GETs that shared a batch-mate's GPU row
   void sweep_all();
 };
 

@@ -51,6 +51,11 @@ struct HbmBackend::Dev {
   uint64_t *hs_voff = nullptr, *hs_voff_dev = nullptr;
   uint32_t *hs_meta = nullptr, *hs_meta_dev = nullptr;
   HbmCache::StoreGraph set_graph[kSetClasses];
+  // host-side GET coalescing scratch (batcher thread only)
+  std::vector<int32_t> co_tab;
+  std::vector<uint32_t> urow;
+  std::vector<CacheValue> uval;
+  std::vector<uint8_t> uhit;
 
   void set_device() { HB_OK(hipSetDevice(device)); }
 
@@ -355,15 +360,41 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
     (batch[i].kind == 0 ? gets : batch[i].kind == 1 ? sets : dels)[o].push_back(i);
   }
   // ---- GET: H2D keys, probe + scan, gather straight into pinned host memory (skipped
-  // by the kernel if the batch does not fit), D2H offsets; one sync per device
+  // by the kernel if the batch does not fit), D2H offsets; one sync per device.
+  // Coalesced on the host first: requests for the same digest in one batch (a hot
+  // object under concurrent clients) share one GPU row, one copy over PCIe and one
+  // CacheValue (the bytes are shared, as the DRAM tier shares them).
+  std::vector<size_t> nuniq(nd, 0);
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
-    if (!n) continue;
+    const size_t n0 = gets[k].size();
+    if (!n0) continue;
     dv.set_device();
-    dv.ensure_n(std::max(n, std::max(sets[k].size(), dels[k].size())));
+    dv.ensure_n(std::max(n0, std::max(sets[k].size(), dels[k].size())));
     dv.ensure_out(1);
-    for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[gets[k][j]].d;
+    size_t tsz = 16;
+    while (tsz < 2 * n0) tsz <<= 1;
+    dv.co_tab.assign(tsz, -1);
+    dv.urow.resize(n0);
+    size_t n = 0;
+    for (size_t j = 0; j < n0; ++j) {
+      const Digest& d = batch[gets[k][j]].d;
+      for (size_t h = (size_t)(d.hi ^ (d.hi >> 31)) & (tsz - 1);; h = (h + 1) & (tsz - 1)) {
+        const int32_t u = dv.co_tab[h];
+        if (u < 0) {  // first request for this digest: it gets a GPU row
+          dv.co_tab[h] = (int32_t)n;
+          dv.h_keys[n] = d;
+          dv.urow[j] = (uint32_t)n++;
+          break;
+        }
+        if (dv.h_keys[u].lo == d.lo && dv.h_keys[u].hi == d.hi) {
+          dv.urow[j] = (uint32_t)u;
+          break;
+        }
+      }
+    }
+    nuniq[k] = n;
+    coalesced_gets_ += n0 - n;
     if ((int64_t)n <= HbmCache::kSmallGetMax) {
       // one launch, no copies: keys, offsets and values all live in mapped host memory;
       // the kernel's last workgroup signals completion through a pinned host slot
@@ -378,7 +409,7 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
   }
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
+    const size_t n = nuniq[k];
     if (!n) continue;
     dv.set_device();
     const bool small = (int64_t)n <= HbmCache::kSmallGetMax;
@@ -399,24 +430,30 @@ void HbmBackend::run_batch(std::vector<Req>& batch) {
   }
   for (size_t k = 0; k < nd; ++k) {
     Dev& dv = *devs_[k];
-    const size_t n = gets[k].size();
+    const size_t n = nuniq[k];
     if (!n) continue;
-    for (size_t j = 0; j < n; ++j) {
-      Req& r = batch[gets[k][j]];
-      const uint64_t o = dv.h_off[j], sz = dv.h_off[j + 1] - o;
-      bool hit = false;
-      CacheValue v;
-      if (sz) {
-        ItemHeader h;
-        std::memcpy(&h, dv.h_out + o, sizeof h);
-        if (h.magic == kItemMagic && h.d0 == r.d.lo && h.d1 == r.d.hi) {
-          hit = true;
-          v.flags = h.flags;
-          v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
-          v.data = std::make_shared<const std::string>(
-              reinterpret_cast<const char*>(dv.h_out + o + kItemHeaderBytes), h.vlen);
-        }
+    // one CacheValue per GPU row, shared by that row's requests
+    dv.uval.assign(n, CacheValue{});
+    dv.uhit.assign(n, 0);
+    for (size_t u = 0; u < n; ++u) {
+      const uint64_t o = dv.h_off[u], sz = dv.h_off[u + 1] - o;
+      if (!sz) continue;
+      ItemHeader h;
+      std::memcpy(&h, dv.h_out + o, sizeof h);
+      if (h.magic == kItemMagic && h.d0 == dv.h_keys[u].lo && h.d1 == dv.h_keys[u].hi) {
+        dv.uhit[u] = 1;
+        CacheValue& v = dv.uval[u];
+        v.flags = h.flags;
+        v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
+        v.data = std::make_shared<const std::string>(
+            reinterpret_cast<const char*>(dv.h_out + o + kItemHeaderBytes), h.vlen);
       }
+    }
+    for (size_t j = 0; j < gets[k].size(); ++j) {
+      Req& r = batch[gets[k][j]];
+      const uint32_t u = dv.urow[j];
+      const bool hit = dv.uhit[u] != 0;
+      CacheValue v = dv.uval[u];
       auto cb = std::move(r.gcb);
       r.ex->post([cb, hit, v]() { cb(hit, v); });
     }
@@ -596,6 +633,7 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_set_graph_captures", gc);
   out->emplace_back("hbm_live_objects", live_objects_.load());
   out->emplace_back("hbm_live_bytes", live_bytes_.load());
+  out->emplace_back("hbm_coalesced_gets", coalesced_gets_.load());
   if (cfg_.presence_filter) {
     const auto f = std::atomic_load(&filt_);
     out->emplace_back("hbm_filter_skips", filt_skips_.load());

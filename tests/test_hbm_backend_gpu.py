@@ -61,6 +61,10 @@ def test_proxy_with_hbm_backend(hbm):
             rs = c.pipeline(paths)
             assert [r.body().read() for r in rs] == first
             assert all(o.hits[p] == 1 for p in paths)
+            # repeated paths in one pipeline: batch-mates share a GPU row (host coalescing)
+            rs = c.pipeline(paths[:10] * 8)
+            assert [r.body().read() for r in rs] == first[:10] * 8
+            assert all(o.hits[p] == 1 for p in paths)
             st = px.stats()
             assert st["cache_hits"] >= 50 and st["backend"] == "hbm"
     finally:
