@@ -1,10 +1,15 @@
 // HIP/CDNA4 kernels and host driver for the HBM cache shard (see hbm_cache.h).
 //
 // Kernel map (all wave64, 256-thread workgroups):
-//   k_probe        16 lanes per key: lanes 0-7 read bucket1, 8-15 bucket2 (two
-//                  coalesced 128-B lines), pair-lane shuffle joins the {digest}
-//                  and {loc,vlen,expire} halves of each entry, max-reduce picks
-//                  the newest live match. No dependent read of the value log.
+//   k_coalesce     GET request collapsing: each workgroup collapses a 1024-key chunk
+//                  in an LDS table, its local claimers claim a global open-addressing
+//                  table (one CAS; a plain load first for keys repeated in the chunk),
+//                  and (PROBE) the global claimers are probed by 8-lane groups.
+//   k_probe        8 lanes per key, digests staged in LDS, 3 keys in flight per
+//                  group: the group reads the first bucket (one 128-B line) and only
+//                  on a miss the second; pair-lane shuffles join the {digest} and
+//                  {loc,vlen,expire} halves of each entry, max-reduce picks the
+//                  newest live match. No dependent read of the value log.
 //   k_segcopy      load-balanced byte mover: each workgroup owns a 64 KiB tile
 //                  of the *output*, finds the segments covering it (block-wide
 //                  128-ary search, then per-lane binary search of offsets staged
@@ -15,15 +20,18 @@
 //                  batch wins (request order = memcached/HTTP pipelining order).
 //   k_set_copy     load-balanced writer of [ItemHeader|value] into the log at
 //                  head + exclusive-scan(item sizes): batch allocation is a scan.
-//   k_set_index    16 lanes per key: two-choice insert with a 64-bit CAS on the
+//   k_set_index    4 lanes per key: two-choice insert with a 64-bit CAS on the
 //                  entry's loc word; replaces the key's own entry, else a dead
 //                  slot in the emptier bucket, else evicts the oldest item;
 //                  workgroup 0 publishes the new log head into the other of two
 //                  ping-pong head slots, and every item resets its dedupe slot.
+//   k_set_fixup    rewrites the digest words of entries a later insert of the same
+//                  batch re-claimed (the CAS arbitrates loc only).
 //   All per-op counters are block-reduced and added to one of 64 counter
 //   shards (one atomic per block per field; same-address fan-in measured at
 //   ~12 ns/atomic would otherwise serialise a 64K-wave probe into milliseconds).
-//   k_delete, k_sweep, k_digest, k_route*, k_permute, k_mfma_hello.
+//   k_expand(_out), k_small_get, k_delete, k_sweep, k_export, k_digest, k_route*,
+//   k_permute, k_mfma_hello.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -992,6 +1000,15 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
   block_partial(psum, part);
 }
 
+// SET index insert, 4 lanes per key: lane q reads entry q of both candidate buckets
+// (4 x 8-B agent-scope loads each), so a wave keeps 16 keys' bucket reads in flight — the
+// insert is latency-bound, and beside the bandwidth-bound gather it only gets the slots
+// the gather leaves (a 16-lanes-per-key version took 130-140 us there, this one 39 us).
+// Policy: replace the key's own entry, else a dead slot (first bucket while it keeps
+// >= 2 free, else the emptier bucket), else evict the oldest; the entry is claimed by a
+// CAS on its loc word, the digest / vlen words follow and k_set_fixup repairs entries
+// a later insert of the same batch re-claimed. Workgroup 0 publishes the new log head
+// into the other ping-pong head slot; every row resets its dedupe-table slot.
 __global__ __launch_bounds__(kBlock) void k_set_index(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
@@ -999,48 +1016,45 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
     int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim) {
-  const int l16 = threadIdx.x & 15;
+  const int l4 = threadIdx.x & 3;
+  const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
-  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 4;
+  const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
   unsigned long long evicted = 0, bytes = 0;
-  // publish the new head into the other ping-pong slot: every workgroup of this
-  // launch (and of k_segcopy<1> before it) reads the current slot
   if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
-  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4; i < n; i += ngroups) {
-    if (l16 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
+  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
+    if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
       const uint32_t sl = slot_of[i];
       dd_keys[sl] = 0ull;
       dd_win[sl] = -1;
     }
-    if (l16 == 0) claim[i] = ~0u;  // no entry (yet)
-    if (size[i] == 0) continue;  // uniform across the 16-lane group
+    if (l4 == 0) claim[i] = ~0u;  // no entry (yet)
+    if (size[i] == 0) continue;   // uniform across the 4-lane group
     const Digest d = keys[i];
     const uint64_t myloc = base + off[i] + 1;
     const uint32_t myvlen = vlen[i];
     const uint32_t myexp = expire ? expire[i] : 0u;
     const uint64_t b1 = bucket1(d, mask), b2 = bucket2(d, mask);
-    const uint64_t b = (l16 < 8) ? b1 : b2;
-    Entry* const bucket = index + b * kEntriesPerBucket;
+    const uint64_t* q1 = reinterpret_cast<const uint64_t*>(index + b1 * kEntriesPerBucket + l4);
+    const uint64_t* q2 = reinterpret_cast<const uint64_t*>(index + b2 * kEntriesPerBucket + l4);
     for (int attempt = 0; attempt < 16; ++attempt) {
       // agent-scope loads: a retry must see other workgroups' CAS results, not stale L1
-      const uint64_t* q = reinterpret_cast<const uint64_t*>(bucket) + 2 * (l16 & 7);
-      const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t c = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t pa = __shfl_xor(a, 1), pc = __shfl_xor(c, 1);
-      const bool even = (l16 & 1) == 0;
-      const bool match = even && a == d.lo && c == d.hi;
-      const bool live = even && entry_live(pa, (uint32_t)(pc >> 32), head_new, cap, now);
-      // group-local masks over the 8 entries (bit e = entry e; e<4 bucket1, e>=4 bucket2)
-      const int gbase = threadIdx.x & 48;
-      const unsigned long long bm = __ballot(match);
-      const unsigned long long bl = __ballot(live);
-      uint32_t mmask = 0, lmask = 0;
+      uint64_t w1[4], w2[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        mmask |= (uint32_t)((bm >> (gbase + 2 * e)) & 1ull) << e;
-        lmask |= (uint32_t)((bl >> (gbase + 2 * e)) & 1ull) << e;
+      for (int k = 0; k < 4; ++k) {
+        w1[k] = __hip_atomic_load(q1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w2[k] = __hip_atomic_load(q2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      // words: d0, d1, loc, vlen | expire << 32
+      const bool m1 = w1[0] == d.lo && w1[1] == d.hi;
+      const bool m2 = w2[0] == d.lo && w2[1] == d.hi;
+      const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
+      const bool v2 = entry_live(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
+      const uint32_t mmask = (uint32_t)((__ballot(m1) >> gbase) & 0xfull) |
+                             ((uint32_t)((__ballot(m2) >> gbase) & 0xfull) << 4);
+      const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
+                             ((uint32_t)((__ballot(v2) >> gbase) & 0xfull) << 4);
       int target;
       bool evict = false;
       if (mmask) {
@@ -1048,35 +1062,28 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       } else {
         const uint32_t dead = ~lmask & 0xffu;
         if (dead) {
-          // first bucket while it keeps >= 2 free slots (k_probe reads the second bucket
-          // only on a miss: ~1.1 lines per hit at 50% load), else the emptier bucket
-          // (keeps the two-choice occupancy: 0.03% vs 0.37% evictions for always-first)
           const int live1 = __popc(lmask & 0xfu), live2 = __popc(lmask & 0xf0u);
           const uint32_t pref = __popc(dead & 0x0fu) >= 2
                                     ? (dead & 0x0fu)
                                     : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
           target = __ffs(pref ? pref : dead) - 1;
         } else {
-          // both buckets full of live items: evict the oldest (smallest loc)
           uint64_t oldest = ~0ull;
           target = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const uint64_t le = __shfl(pa, gbase + 2 * e);
+            const uint64_t le = e < 4 ? __shfl(w1[2], gbase + e) : __shfl(w2[2], gbase + e - 4);
             if (le < oldest) { oldest = le; target = e; }
           }
           evict = true;
         }
       }
-      const uint64_t expected = __shfl(pa, gbase + 2 * target);
+      const uint64_t e1 = __shfl(w1[2], gbase + (target & 3));
+      const uint64_t e2 = __shfl(w2[2], gbase + (target & 3));
+      const uint64_t expected = target < 4 ? e1 : e2;
       Entry* const slot = index + (target < 4 ? b1 : b2) * kEntriesPerBucket + (target & 3);
       int ok = 0;
-      // The CAS on loc arbitrates the entry; the digest / vlen words written after it can
-      // land late (another insert of this batch may re-claim the entry in between, and
-      // a late digest write would pair its key with the other key's loc), so the winner
-      // records the entry and k_set_fixup rewrites the words of every entry whose loc
-      // is still its own once this kernel is done.
-      if (l16 == 0) {
+      if (l4 == 0) {
         const unsigned long long prev = atomicCAS(
             reinterpret_cast<unsigned long long*>(&slot->loc), (unsigned long long)expected,
             (unsigned long long)myloc);
@@ -1097,10 +1104,6 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
   block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes);
 }
 
-
-// ---------------------------------------------------------------------------------
-// DELETE / SWEEP
-// ---------------------------------------------------------------------------------
 // After k_set_index (kernel boundary: every CAS and word write is visible): each entry
 // whose loc is still the one a row of this batch claimed gets that row's digest and
 // vlen|expire words again, so no entry pairs one key's digest with another key's loc.
@@ -1123,6 +1126,9 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// DELETE / SWEEP
+// ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_delete(const Digest* __restrict__ keys, int64_t n,
                                                    Entry* __restrict__ index, uint64_t mask,
                                                    const uint64_t* __restrict__ head_ptr,
@@ -1674,7 +1680,7 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   HIP_OK(hipGetLastError());
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
-  const int igrid = grid_for(n * 16, kBlock, kMaxGrid);
+  const int igrid = grid_for(n * 4, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                      cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
