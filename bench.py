@@ -23,8 +23,11 @@ Secondary (outside the timed region): the BASELINE.json platform smoke checks
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,9 +75,46 @@ def parse():
                     help="functional rehearsal of the N-rank GPU step on ONE GPU: every rank on "
                          "cuda:0, collectives bounced through gloo (RCCL refuses two ranks on "
                          "one device); never a performance number")
+    ap.add_argument("--batches", type=int, default=16,
+                    help="distinct pre-generated GET/SET batch pairs cycled through the steps "
+                         "(16 x 16 MiB of digests + 16 SET payload sets: more than the 256 MB MALL)")
+    ap.add_argument("--pg-timeout", type=float, default=300.0,
+                    help="process-group timeout in seconds: a stuck collective exits non-zero")
     ap.add_argument("--no-smoke", action="store_true")
+    ap.add_argument("--no-uncoalesced", action="store_true",
+                    help="skip the secondary uncoalesced-GET measurement")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def maybe_launch(args) -> None:
+    """``--gpus N`` (N > 1) without a torch.distributed launcher: run the N ranks as a
+    CHILD ``torch.distributed.run`` job and exit with its status. This happens before
+    anything touches the GPU (no exec from a process with a live HIP context). With a
+    launcher, the rank count must equal --gpus: a job that would silently report a
+    1-rank number as an N-GPU run exits non-zero instead."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus <= 1 or args.simulate_world:
+            return
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+        print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+        raise SystemExit(subprocess.run(cmd).returncode)
+    if int(world_env) != args.gpus and not args.simulate_world:
+        print(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} "
+              "ranks; refusing to report a number for the wrong GPU count", file=sys.stderr,
+              flush=True)
+        raise SystemExit(2)
 
 
 def log(rank, *a):
@@ -99,6 +139,11 @@ def smoke(rank, world, dev):
         x = torch.ones(512 << 20, dtype=torch.bfloat16, device=dev)  # 1 GiB
         dist.all_reduce(x)
         torch.cuda.synchronize()
+        # every element must equal the rank count (exact in bf16 for world <= 256)
+        lo, hi = float(x.min()), float(x.max())
+        if lo != world or hi != world:
+            raise RuntimeError(f"RCCL all-reduce smoke wrong: min {lo} max {hi}, want {world}")
+        out["allreduce_check"] = "ok"
         iters = 5
         dist.barrier()
         t0 = time.perf_counter()
@@ -119,28 +164,30 @@ def smoke(rank, world, dev):
 
 def main():
     args = parse()
+    maybe_launch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sim = args.simulate_world
     if sim and world != 1:
         raise SystemExit("--simulate-world runs as a single process")
-    if world != args.gpus and not sim:
-        log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     bounce = args.bounce and args.device == "cuda" and world > 1
+    pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
+    # a collective that outlives the timeout aborts the rank (non-zero exit), not a hang
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if bounce:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=pg_timeout)
     elif args.device == "cuda":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
     else:
         dev = torch.device("cpu")
         if world > 1:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
 
     def sync():
         if dev.type == "cuda":
@@ -203,8 +250,10 @@ def main():
         dist.barrier()
     log(rank, f"[bench] populated {total_keys} keys in {time.perf_counter() - t_setup:.1f}s")
 
-    # pre-generated request batches (the "data loader"); cycled through the steps
-    P = 4
+    # pre-generated request batches (the "data loader"), cycled through the steps: 16
+    # distinct pairs by default, so the GET digests alone (16 x 16 MiB) outgrow the 256 MB
+    # MALL and each step reads its batch from HBM rather than from the last-level cache
+    P = max(1, args.batches)
     gets = [wl.digests.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
             for i in range(P)]
     pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
@@ -223,28 +272,42 @@ def main():
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
         return sc.serve(gets[i % P], sets[i % P])
 
+    use_events = dev.type == "cuda"
+    rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
+
+    def timed(steps, first):
+        """Run `steps` steps bracketed by barrier + device sync; returns (max-over-ranks
+        wall seconds, per-step GPU-event intervals in ms, last result)."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if use_events else []
+        if real_world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        res = None
+        for i in range(steps):
+            if use_events:
+                evs[i].record()
+            res = step(first + i)
+        if use_events:
+            evs[steps].record()
+        sync()
+        if real_world > 1:
+            dist.barrier()
+        sync()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device=rdev)
+        if real_world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if use_events else []
+        return float(t), iv, res
+
     for i in range(args.warmup):
         step(i)
     sync()
     before = shard.counters()
     st0 = dict(sc.stats)
-    if real_world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        res = step(i)
-    sync()
-    if real_world > 1:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
-    t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-    if real_world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t)
-
+    elapsed, intervals, res = timed(args.steps, args.warmup)
+    last_batch = (args.warmup + args.steps - 1) % P
     after = shard.counters()
     # owner-shard counters cover the GETs that left the replica tier; replica hits
     # are counted by the serving step
@@ -262,13 +325,13 @@ def main():
         from shellac_amd.ops.cache import unpack_records
 
         k = 200
-        ids = wl.sample_ids(args.batch, 1000 + 97 * rank + (args.steps - 1) % P)[:k]
+        ids = wl.sample_ids(args.batch, 1000 + 97 * rank + last_batch)[:k]
         res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
         # every hit of the whole last batch: its record's header names the requested digest
-        keys_last = gets[(args.steps - 1) % P]
+        keys_last = gets[last_batch]
         hit = res.size > 0
         words = res.data[: res.data.numel() // 8 * 8].view(torch.int64)
         at = torch.where(hit, torch.div(res.off, 8, rounding_mode="floor"), torch.zeros_like(res.off))
@@ -277,7 +340,21 @@ def main():
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
                   f"another key")
 
+    # secondary (outside the headline timed region): the same steps with every GET probed
+    # and copied (no in-batch request collapsing)
+    unco = None
+    if sc.coalesce and not args.no_uncoalesced:
+        sc.coalesce = False
+        step(0)
+        unco_el, _, _ = timed(args.steps, args.warmup)
+        sc.coalesce = True
+        unco = (args.batch + args.sets) * world * args.steps / unco_el
+
+    t_sm = time.perf_counter()
     sm = {} if (args.no_smoke or dev.type != "cuda" or sim or bounce) else smoke(rank, world, dev)
+    if sm:
+        # BASELINE.json's headline: wall clock of the platform smoke checks
+        sm["smoke_wallclock_s"] = round(time.perf_counter() - t_sm, 3)
 
     ops_per_step = (args.batch + args.sets) * world
     ms = elapsed / args.steps * 1e3
@@ -317,8 +394,16 @@ def main():
         # share of the distinct-key lookups (after coalescing) a local replica answered
         "replica_hit_fraction": round(rep_hits / max(gops + rep_hits, 1), 4),
         "get_value_GBps_owner_shards": round(gbytes / elapsed / 1e9, 2),
+        # distinct keys looked up per second (owner probes + replica hits), i.e. requests
+        # that were not answered from a batch-mate's record
+        "get_unique_per_s": round((gops + rep_hits) / elapsed, 1),
+        "uncoalesced_ops_per_s": round(unco, 1) if unco else None,
+        "batches_cycled": P,
         "smoke": sm,
     }
+    if intervals:
+        srt = sorted(intervals)
+        out["ms_per_step_median_gpu_events"] = round(srt[len(srt) // 2], 4)
     if dev.type != "cuda":
         out["data"] = "cpu rehearsal over gloo: functional only, not a performance number"
     if bounce:

@@ -39,3 +39,34 @@ def test_bench_cpu_rehearsal_world2():
     assert out["get_hit_ratio"] == 1.0
     assert "0 mismatches" in p.stderr
     assert "check: 0 of 4096 hit records name another key" in p.stderr
+
+
+SMALL = ["--steps", "2", "--warmup", "1", "--device", "cpu", "--batch", "2048", "--sets", "256",
+         "--keys-per-gpu", "8192", "--log-gb", "0.0625", "--replicate", "1024",
+         "--replica-gb", "0.01", "--sample-batches", "1", "--batches", "2", "--no-uncoalesced"]
+
+
+def test_bench_self_launches_ranks_without_torchrun():
+    """--gpus 4 with no launcher: bench.py starts its own 4-rank child job (no exec) and
+    the JSON reports 4 GPUs' worth of work."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *SMALL],
+                       capture_output=True, text=True, timeout=600, cwd="/tmp", env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4
+    assert out["config"]["global_batch"] == 4 * (2048 + 256)
+    assert "launching 4 ranks" in p.stderr
+
+
+def test_bench_rank_count_mismatch_exits_nonzero():
+    """A launcher that started fewer ranks than --gpus must not yield a number."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *SMALL],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "refusing" in p.stderr
