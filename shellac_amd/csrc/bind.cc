@@ -35,6 +35,9 @@ py::dict counters_dict(const CacheCounters& c) {
   d["del_ops"] = c.del_ops;
   d["del_hits"] = c.del_hits;
   d["swept"] = c.swept;
+  d["get_coalesced"] = c.get_coalesced;
+  d["reinserted"] = c.reinserted;
+  d["reinsert_bytes"] = c.reinsert_bytes;
   return d;
 }
 

@@ -169,6 +169,7 @@ __device__ __forceinline__ void block_count(CacheCounters* shards, unsigned long
     if (fb && t1) atomicAdd(&(c_->*fb), t1);
     if (fc && t2) atomicAdd(&(c_->*fc), t2);
   }
+  __syncthreads();  // s_red may be reused by a following call
 }
 
 // Block-wide sum of v written to part[blockIdx.x] (every thread must call it).
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   __shared__ int s_qn;
   const uint64_t head = PROBE ? *head_ptr + reserve : 0;
   const int l8 = threadIdx.x & 7;
-  unsigned long long ops = 0, hits = 0, bytes = 0, psum = 0;
+  unsigned long long ops = 0, hits = 0, bytes = 0, psum = 0, dups = 0;
   const int64_t r0 = (int64_t)blockIdx.x * plen, r1 = min(n, r0 + plen);
   for (int64_t base = r0; base < r1; base += kCoKeys) {
     const int cnt = (int)min((int64_t)kCoKeys, r1 - base);
@@ -562,6 +563,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (PROBE && f != (uint32_t)(base + j)) {
         out_loc[base + j] = kMissLoc;
         out_size[base + j] = 0;
+        ++dups;
       }
     }
     __syncthreads();  // LDS is reused by the next chunk
@@ -570,6 +572,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;
     block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
                 &CacheCounters::get_bytes);
+    block_count(ctr, dups, &CacheCounters::get_coalesced);
     block_partial(psum, part);
   }
 }
@@ -1021,7 +1024,7 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
-  unsigned long long evicted = 0, bytes = 0;
+  unsigned long long evicted = 0, bytes = 0, lost = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
     if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
@@ -1046,9 +1049,14 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
         w1[k] = __hip_atomic_load(q1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         w2[k] = __hip_atomic_load(q2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      // words: d0, d1, loc, vlen | expire << 32
-      const bool m1 = w1[0] == d.lo && w1[1] == d.hi;
-      const bool m2 = w2[0] == d.lo && w2[1] == d.hi;
+      // words: d0, d1, loc, vlen | expire << 32. A digest match whose loc belongs to
+      // this batch, (base, head_new], is another row's claim whose digest words have not
+      // landed yet (dedupe leaves one row per key, so it is never this key's entry):
+      // taking it as our own would CAS that row's claim away and lose its SET.
+      const bool in1 = w1[2] > base && w1[2] <= head_new;
+      const bool in2 = w2[2] > base && w2[2] <= head_new;
+      const bool m1 = w1[0] == d.lo && w1[1] == d.hi && !in1;
+      const bool m2 = w2[0] == d.lo && w2[1] == d.hi && !in2;
       const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
       const bool v2 = entry_live(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
       const uint32_t mmask = (uint32_t)((__ballot(m1) >> gbase) & 0xfull) |
@@ -1099,9 +1107,11 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       }
       ok = __shfl(ok, gbase);
       if (ok) break;
+      if (attempt == 15 && l4 == 0) ++lost;  // bucket pair contended past the retry budget
     }
   }
-  block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes);
+  block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes, lost,
+              &CacheCounters::set_dropped);
 }
 
 // After k_set_index (kernel boundary: every CAS and word write is visible): each entry

@@ -65,7 +65,9 @@ SH_HD bool entry_live(uint64_t loc, uint32_t expire, uint64_t head, uint64_t cap
   return loc != 0 && head <= (loc - 1) + capacity && (expire == 0 || expire > now);
 }
 
-// Counters kept on the device (and mirrored by the host engine).
+// Counters kept on the device (and mirrored by the host engine). Under GET coalescing
+// get_ops / get_hits / get_bytes count distinct keys probed; the duplicate rows a
+// batch-mate's record answered are get_coalesced (requests = get_ops + get_coalesced).
 struct CacheCounters {
   unsigned long long get_ops;
   unsigned long long get_hits;
@@ -77,7 +79,10 @@ struct CacheCounters {
   unsigned long long del_ops;
   unsigned long long del_hits;
   unsigned long long swept;         // dead entries reclaimed by sweep()
-  unsigned long long reserved[6];
+  unsigned long long get_coalesced; // duplicate GET rows served by a batch-mate's probe
+  unsigned long long reinserted;    // referenced items the CLOCK hand gave a second life
+  unsigned long long reinsert_bytes;
+  unsigned long long reserved[3];
 };
 static_assert(sizeof(CacheCounters) == 128, "CacheCounters layout");
 

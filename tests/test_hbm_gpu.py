@@ -541,3 +541,30 @@ def test_set_index_under_same_bucket_contention(cuda_dev, bs, pad):
     hits = [i for i, r in enumerate(recs) if r is not None]
     assert len(hits) > 900
     assert all(recs[i][0] == b"v%d" % i for i in hits)
+
+
+def test_set_index_resets_over_dead_entries_lose_nothing(cuda_dev):
+    """Re-SET keys whose old entries are dead but still hold their digests (deleted), all
+    in one batch under same-bucket contention: a row must never take another row's fresh
+    claim (whose digest words have not landed) for its own entry. Every row of the batch
+    either hits with its own new value or is accounted for as evicted / dropped."""
+    sh = CacheShard(64 << 20, 256, 1 << 16, cuda_dev)
+    keys = [b"/rz/%d" % i for i in range(3000)]
+    d = digest_strings(keys).to(cuda_dev)
+    for s in range(0, 3000, 500):
+        v, vo, vl = pack_values([b"old%d" % i for i in range(s, s + 500)])
+        sh.store(d[s:s + 500], v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev))
+    sh.remove(d)
+    torch.cuda.synchronize()
+    c0 = sh.counters()
+    v, vo, vl = pack_values([b"new%d" % i for i in range(3000)])
+    sh.store(d, v.to(cuda_dev), vo.to(cuda_dev), vl.to(cuda_dev))
+    torch.cuda.synchronize()
+    c1 = sh.counters()
+    lk = sh.lookup(d)
+    recs = unpack_records(sh.gather(lk), lk.off[:3000], lk.size[:3000])
+    hits = [i for i, r in enumerate(recs) if r is not None]
+    assert all(recs[i][0] == b"new%d" % i for i in hits)
+    lost = (c1["set_evicted"] - c0["set_evicted"]) + (c1["set_dropped"] - c0["set_dropped"])
+    assert len(hits) + lost == 3000, (len(hits), lost)
+    assert len(hits) > 900
