@@ -49,6 +49,7 @@ PYBIND11_MODULE(_shellac_core, m) {
   m.attr("ENTRY_BYTES") = (int)sizeof(Entry);
   m.attr("BUCKET_BYTES") = (int)kBucketBytes;
   m.attr("ITEM_HEADER_BYTES") = (int)kItemHeaderBytes;
+  m.attr("SMALL_GET_MAX") = (int64_t)HbmCache::kSmallGetMax;
   m.attr("ITEM_MAGIC") = kItemMagic;
   m.attr("MISS_LOC") = py::int_(kMissLoc);
 
@@ -67,15 +68,20 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("destroy", [](HbmCache::StoreGraph& g) { HbmCache::destroy_graph(&g); });
 
   py::class_<HbmCache>(m, "HbmCache")
-      .def(py::init([](uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int device) {
+      .def(py::init([](uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int device,
+                       int evict, uint64_t reinsert_max) {
              ShardConfig c;
              c.log_bytes = log_bytes;
              c.nbuckets = nbuckets;
              c.max_item = max_item;
              c.device = device;
+             c.evict = evict;
+             c.reinsert_max = reinsert_max;
              return new HbmCache(c);
            }),
-           py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"))
+           py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"),
+           py::arg("evict") = (int)kEvictClock, py::arg("reinsert_max") = 0)
+      .def_property_readonly("reinsert_max", &HbmCache::reinsert_max)
       .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
                         uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve, int slot,
                         uintptr_t first) {
@@ -239,8 +245,10 @@ PYBIND11_MODULE(_shellac_core, m) {
 
   // ---------------- host (DRAM) ----------------
   py::class_<HostCache>(m, "HostCache")
-      .def(py::init<uint64_t, uint64_t, uint32_t>(), py::arg("log_bytes"), py::arg("nbuckets"),
-           py::arg("max_item"))
+      .def(py::init<uint64_t, uint64_t, uint32_t, int, uint64_t>(), py::arg("log_bytes"),
+           py::arg("nbuckets"), py::arg("max_item"), py::arg("evict") = 1,
+           py::arg("reinsert_max") = 0)
+      .def_property_readonly("reinsert_max", &HostCache::reinsert_max)
       .def("lookup", [](HostCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
                         uintptr_t off, uint32_t now, uint64_t reserve) {
         py::gil_scoped_release nogil;

@@ -48,7 +48,7 @@ py::object blocking_get(CacheBackend* be, const std::string& key) {
     cv.wait(lk, [&] { return done; });
   }
   if (!hit || !val.data) return py::none();
-  return py::make_tuple(py::bytes(*val.data), val.flags);
+  return py::make_tuple(py::bytes(val.data->data(), val.data->size()), val.flags);
 }
 
 bool blocking_del(CacheBackend* be, const std::string& key) {

@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 
@@ -21,11 +22,19 @@
 
 namespace shellac {
 
+// Eviction policies of the value log (ShardConfig::evict).
+enum : int { kEvictFifo = 0, kEvictClock = 1 };
+
 struct ShardConfig {
   uint64_t log_bytes = 1ull << 30;  // value-log capacity (multiple of 16)
   uint64_t nbuckets = 1ull << 20;   // power of two, 4 entries (128 B) each
   uint32_t max_item = 1u << 20;     // max value bytes (memcached's 1 MB item limit)
   int device = 0;
+  // kEvictClock: items read since the hand last passed get re-appended instead of being
+  // overwritten (CLOCK / FIFO-reinsertion, memcached-LRU-like hit ratios under
+  // capacity pressure). kEvictFifo: plain circular log.
+  int evict = kEvictClock;
+  uint64_t reinsert_max = 0;  // reinsertion budget per SET batch (bytes); 0 = auto
 };
 
 class HbmCache {
@@ -66,16 +75,22 @@ class HbmCache {
   // timeout_ms. Each lookup that names a slot must be waited for before the slot is reused.
   uint64_t wait_host_slot(int i, int64_t timeout_ms = 10000) const;
   static constexpr int kHostSlots = 64;
+  static constexpr int kHeadSlot = kHostSlots - 2;  // the SET chain publishes the head here
   static constexpr uint64_t kSlotPending = ~0ull;
-  // Small batches (n <= 2048, the proxy's micro-batches): lookup + scan + gather in one
-  // launch. keys / out / off may be mapped host memory (no copies); off[0..n] is always
-  // written, the bytes only when off[n] <= out_cap.
-  // `done_slot` >= 0: the kernel's last workgroup writes off[n] into that host slot
-  // after every output byte is visible to the host, so wait_host_slot(done_slot)
-  // replaces a stream synchronisation (one batch in flight per slot).
+  static constexpr uint64_t kSlotFailed = ~0ull - 1;  // the edge GET could not complete
+  // Edge GET (the proxy's micro-batches, n <= kSmallGetMax): probe + scan + gather in
+  // one launch, every key probed once (decoupled look-back scan across workgroups).
+  // keys / out / off may be mapped host memory (no copies); off[0..n] is always written;
+  // off[n] > out_cap means the output is incomplete (nothing is written past out_cap) and
+  // the batch must be repeated into a bigger buffer.
+  // `done_slot` >= 0: the kernel's last workgroup writes off[n] (or kSlotFailed) into
+  // that host slot after every output byte is visible to the host, so
+  // wait_host_slot(done_slot) replaces a stream synchronisation. Launches are ordered on
+  // their stream (the look-back state is shared), several may be queued at once with
+  // distinct slots.
   void small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap, uint64_t* off,
                  uint32_t now, hipStream_t s, int done_slot = -1);
-  static constexpr int64_t kSmallGetMax = 2048;
+  static constexpr int64_t kSmallGetMax = 1 << 17;
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
   // caller can queue the gather before it knows the total and retry if it did not fit.
@@ -137,9 +152,29 @@ class HbmCache {
   // Pre-size the SET workspace for batches of n keys (allocates; call outside capture).
   void reserve(int64_t n);
   uint64_t hbm_bytes() const;
+  uint64_t reinsert_max() const { return cfg_.evict == kEvictClock ? rmax_ : 0; }
 
  private:
   void ensure_set_ws(int64_t n, hipStream_t s);
+  void ensure_rc_ws(int64_t w);
+  bool should_reclaim(uint64_t bytes_bound) const;
+  void reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
+                      int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s);
+  uint64_t* cur_ring_tail() const { return head_ + 2 + hsel_; }
+  uint64_t* next_ring_tail() const { return head_ + 2 + (hsel_ ^ 1); }
+  // CLOCK state
+  uint64_t* ring_ = nullptr;           // item-start ring (logical locs, kRingSkip holes)
+  uint64_t ring_cap_ = 0;
+  unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, consumed
+  uint8_t* rc_scratch_ = nullptr;      // staged reinsertions (rmax_ + 64 bytes)
+  uint64_t rmax_ = 0;
+  int64_t rc_cap_ = 0;
+  uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_hx_ = nullptr, *rc_part_ = nullptr;
+  uint64_t *rc_src_ = nullptr, *rc_len_ = nullptr, *cb_voff_ = nullptr;
+  Digest* cb_keys_ = nullptr;
+  uint32_t *cb_vlen_ = nullptr, *cb_flags_ = nullptr, *cb_expire_ = nullptr;
+  int64_t cb_cap_ = 0;
 
   ShardConfig cfg_;
   uint8_t* log_ = nullptr;
@@ -150,10 +185,11 @@ class HbmCache {
   uint64_t* next_head() const { return head_ + (hsel_ ^ 1); }
   CacheCounters* ctr_ = nullptr;     // device counters (64 shards)
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
-  uint64_t* part_ = nullptr;         // per-workgroup size sums: [0,kMaxGrid) GET, then SET
+  uint64_t* part_ = nullptr;         // per-workgroup sums: GET sizes, SET sizes, SET counts
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
   uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
-  unsigned int* done_ctr_ = nullptr; // device: small_get workgroups finished (self-resetting)
+  unsigned int* done_ctr_ = nullptr; // device: edge-GET workgroups finished + fail flag (self-resetting)
+  unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;
@@ -162,6 +198,7 @@ class HbmCache {
   uint64_t* set_size_ = nullptr;
   uint64_t* set_off_ = nullptr;
   uint32_t* set_claim_ = nullptr;  // entry each SET row claimed (k_set_fixup)
+  uint64_t* set_cnt_ = nullptr;    // ring ordinal of each stored SET row (CLOCK)
   uint32_t dd_mask_ = 0;
   uint64_t ws_gen_ = 0;  // bumped when the SET workspace moves (invalidates graphs)
   std::mutex mu_;

@@ -184,6 +184,7 @@ __device__ __forceinline__ void block_partial(unsigned long long v, uint64_t* __
     for (int k = 0; k < kBlock / 64; ++k) t += s_p[k];
     part[blockIdx.x] = t;
   }
+  __syncthreads();  // s_p may be reused by a following call
 }
 
 // Items per workgroup when n items are split into contiguous ranges over `grid` groups.
@@ -196,51 +197,84 @@ __host__ __device__ __forceinline__ int64_t part_len(int64_t n, int grid) {
 // ranges of `plen` items). Workgroup b covers producer groups [b*q, (b+1)*q): it sums
 // the partials before its range, then scans its items, `per` consecutive ones per lane.
 // off[n] = total. Replaces hipcub's init + scan pair (one launch, no lookback state).
+// `part_cnt` / `cnt` (optional): the same scan over (size[i] != 0), i.e. each item's
+// ordinal among the non-empty ones (the CLOCK ring's entry per stored SET row).
 __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__ size, int64_t n,
                                                     const uint64_t* __restrict__ part, int nparts,
                                                     int64_t plen, int q,
                                                     uint64_t* __restrict__ off,
-                                                    uint64_t* __restrict__ host_total) {
-  __shared__ unsigned long long s_w[kBlock / 64];
-  __shared__ unsigned long long s_base;
+                                                    uint64_t* __restrict__ host_total,
+                                                    const uint64_t* __restrict__ part_cnt,
+                                                    uint64_t* __restrict__ cnt) {
+  __shared__ unsigned long long s_w[2][kBlock / 64];
+  __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int p0 = blockIdx.x * q;
-  unsigned long long pre = 0;
-  for (int k = threadIdx.x; k < p0 && k < nparts; k += kBlock) pre += part[k];
+  unsigned long long pre = 0, prec = 0;
+  for (int k = threadIdx.x; k < p0 && k < nparts; k += kBlock) {
+    pre += part[k];
+    if (cnt) prec += part_cnt[k];
+  }
   pre = wave_sum(pre);
-  if (lane == 0) s_w[w] = pre;
+  prec = wave_sum(prec);
+  if (lane == 0) {
+    s_w[0][w] = pre;
+    s_w[1][w] = prec;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 2) {
     unsigned long long t = 0;
 #pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) t += s_w[k];
-    s_base = t;
+    for (int k = 0; k < kBlock / 64; ++k) t += s_w[threadIdx.x][k];
+    s_base[threadIdx.x] = t;
   }
   __syncthreads();
   const int64_t i0 = (int64_t)p0 * plen;
   const int64_t i1 = min(n, (int64_t)(p0 + q) * plen);
   const int64_t per = (i1 - i0 + kBlock - 1) / kBlock;
   const int64_t a = min(i1, i0 + per * threadIdx.x), b = min(i1, a + per);
-  unsigned long long mine = 0;
-  for (int64_t i = a; i < b; ++i) mine += size[i];
+  unsigned long long mine = 0, minec = 0;
+  for (int64_t i = a; i < b; ++i) {
+    const uint64_t v = size[i];
+    mine += v;
+    minec += v ? 1 : 0;
+  }
   // inclusive wave scan of the lane sums, then the waves' totals
-  unsigned long long inc = mine;
+  unsigned long long inc = mine, incc = minec;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const unsigned long long o = __shfl_up(inc, d);
-    if (lane >= d) inc += o;
+    const unsigned long long oc = __shfl_up(incc, d);
+    if (lane >= d) {
+      inc += o;
+      incc += oc;
+    }
   }
-  if (lane == 63) s_w[w] = inc;
+  __syncthreads();  // s_w is reused
+  if (lane == 63) {
+    s_w[0][w] = inc;
+    s_w[1][w] = incc;
+  }
   __syncthreads();
-  unsigned long long run = s_base;
-  for (int k = 0; k < w; ++k) run += s_w[k];
+  unsigned long long run = s_base[0], runc = s_base[1];
+  for (int k = 0; k < w; ++k) {
+    run += s_w[0][k];
+    runc += s_w[1][k];
+  }
   run += inc - mine;
+  runc += incc - minec;
   for (int64_t i = a; i < b; ++i) {
+    const uint64_t v = size[i];
     off[i] = run;
-    run += size[i];
+    run += v;
+    if (cnt) {
+      cnt[i] = runc;
+      runc += v ? 1 : 0;
+    }
   }
   if ((i1 == n && b == n && a < b) || (i1 == n && i0 == n && threadIdx.x == 0)) {
     off[n] = run;  // the lane holding item n-1 (or lane 0 of an empty tail range)
+    if (cnt) cnt[n] = runc;
     if (host_total)
       __hip_atomic_store(host_total, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -255,10 +289,12 @@ constexpr int kProbeTile = 512;  // digests k_probe stages in LDS at a time
 
 // One 8-lane group's match of digest `d` against the bucket quarter-entry `v` its lane
 // l8 loaded: pair-lane shuffles join entry halves, max-reduce keeps the newest live
-// match. hl = stored loc (0: none), hv = its vlen; uniform in the group.
+// match. hl = stored loc (0: none), hv = its raw vlen word (kRefBit included), he = its
+// entry within the bucket; uniform in the group.
 __device__ __forceinline__ void group_match(const uint4 v, const Digest& d, int l8,
                                             uint64_t head, uint64_t cap, uint32_t now,
-                                            uint64_t* hl_out, uint32_t* hv_out) {
+                                            uint64_t* hl_out, uint32_t* hv_out,
+                                            int* he_out = nullptr) {
   const uint64_t a = pack2(v.x, v.y);   // even lane: d0   | odd lane: loc
   const uint64_t c = pack2(v.z, v.w);   // even lane: d1   | odd lane: vlen | expire<<32
   const uint64_t pa = __shfl_xor(a, 1);
@@ -267,14 +303,24 @@ __device__ __forceinline__ void group_match(const uint4 v, const Digest& d, int 
                    entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
   uint64_t hl = hit ? pa : 0;
   uint32_t hv = hit ? (uint32_t)pc : 0;
+  int he = l8 >> 1;
 #pragma unroll
   for (int sh = 2; sh < 8; sh <<= 1) {
     const uint64_t ol = __shfl_xor(hl, sh);
     const uint32_t ov = __shfl_xor(hv, sh);
-    if (ol > hl) { hl = ol; hv = ov; }
+    const int oe = __shfl_xor(he, sh);
+    if (ol > hl) { hl = ol; hv = ov; he = oe; }
   }
   *hl_out = hl;
   *hv_out = hv;
+  if (he_out) *he_out = he;
+}
+
+// CLOCK reference: a hit on an entry whose bit is clear sets it (one atomic the first
+// time an object is read per hand lap; hot objects already carry the bit, so a Zipf
+// probe stream almost never writes).
+__device__ __forceinline__ void mark_ref(Entry* index, uint64_t bucket, int e, uint32_t hv) {
+  if (!(hv & kRefBit)) atomicOr(&index[bucket * kEntriesPerBucket + e].vlen, kRefBit);
 }
 
 // ---------------------------------------------------------------------------------
@@ -284,7 +330,7 @@ __device__ __forceinline__ void group_match(const uint4 v, const Digest& d, int 
 // lane; even lanes hold digests, odd lanes loc/vlen/expire) and only on a miss its
 // second bucket. SETs fill the first bucket first, so a hit usually costs one line.
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_probe(const Digest* __restrict__ keys, int64_t n,
-                                                  const Entry* __restrict__ index, uint64_t mask,
+                                                  Entry* __restrict__ index, uint64_t mask,
                                                   const uint64_t* __restrict__ head_ptr,
                                                   uint64_t reserve, uint64_t cap, uint32_t now,
                                                   uint64_t* __restrict__ out_loc,
@@ -339,15 +385,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         const Digest d = s_k[q];
         uint64_t hl;
         uint32_t hv;
-        group_match(vb[p], d, l8, head, cap, now, &hl, &hv);
+        int he;
+        uint64_t hb = bucket1(d, mask);
+        group_match(vb[p], d, l8, head, cap, now, &hl, &hv, &he);
         if (hl == 0) {  // second bucket only on a miss in the first (uniform in the group)
-          const uint4 v2 =
-              reinterpret_cast<const uint4*>(index + bucket2(d, mask) * kEntriesPerBucket)[l8];
-          group_match(v2, d, l8, head, cap, now, &hl, &hv);
+          hb = bucket2(d, mask);
+          const uint4 v2 = reinterpret_cast<const uint4*>(index + hb * kEntriesPerBucket)[l8];
+          group_match(v2, d, l8, head, cap, now, &hl, &hv, &he);
         }
         if (l8 == 0) {
           ++ops;
           if (hl) {
+            mark_ref(index, hb, he, hv);
+            hv = entry_vlen(hv);
             out_loc[i] = (hl - 1) % cap;
             out_size[i] = item_bytes(hv);
             ++hits;
@@ -398,7 +448,7 @@ template <bool PROBE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_coalesce(
     const Digest* __restrict__ keys, int64_t n, int64_t plen, uint32_t* __restrict__ tab,
     uint32_t tmask, uint32_t* __restrict__ first, uint32_t* __restrict__ cslot,
-    const Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
+    Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
     uint64_t* __restrict__ part, int local_only) {
@@ -534,13 +584,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           const Digest d = s_k[j];
           uint64_t hl;
           uint32_t hv;
-          group_match(vb[p], d, l8, head, cap, now, &hl, &hv);
+          int he;
+          uint64_t hb = bucket1(d, mask);
+          group_match(vb[p], d, l8, head, cap, now, &hl, &hv, &he);
           if (hl == 0) {  // second bucket only on a miss in the first (uniform in the group)
-            const uint4 v2 =
-                reinterpret_cast<const uint4*>(index + bucket2(d, mask) * kEntriesPerBucket)[l8];
-            group_match(v2, d, l8, head, cap, now, &hl, &hv);
+            hb = bucket2(d, mask);
+            const uint4 v2 = reinterpret_cast<const uint4*>(index + hb * kEntriesPerBucket)[l8];
+            group_match(v2, d, l8, head, cap, now, &hl, &hv, &he);
           }
           if (l8 == 0) {
+            if (hl) mark_ref(index, hb, he, hv);
+            hv = entry_vlen(hv);
             ++ops;
             out_loc[base + j] = hl ? (hl - 1) % cap : kMissLoc;
             out_size[base + j] = hl ? item_bytes(hv) : 0;
@@ -833,121 +887,152 @@ void launch_segcopy(hipStream_t s, Args... args) {
 }
 
 // ---------------------------------------------------------------------------------
-// Small GET batches (the HTTP proxy's micro-batches): probe + scan + gather in ONE
-// launch. Every workgroup probes all n keys (n <= kSmallGet, the index lines come from
-// L2 after the first workgroup) and scans the sizes in LDS; workgroup 0 publishes the
-// offsets and counters, and each workgroup copies its share of the response bytes.
-// keys / off_out / out may be mapped host memory: a batch then needs no copies at all.
+// Edge GET (the HTTP proxy's micro-batches): probe + scan + gather in ONE launch, each
+// key probed once. Workgroup b owns keys [32b, 32b+32) (one 8-lane group per key): it
+// probes them, scans their sizes in LDS, learns the byte offset of its range by a
+// decoupled look-back over its predecessors' published aggregates (workgroups are
+// dispatched in order, so every predecessor is resident or done), then copies its own
+// records. keys / off_out / out may be mapped host memory, so a batch needs no copies:
+// the response lands in pinned host memory ready for writev.
 // ---------------------------------------------------------------------------------
-constexpr int kSmallGet = 2048;
+constexpr int kEdgeKeys = kBlock / 8;   // keys per workgroup
+constexpr unsigned long long kLbAgg = 1ull << 62;    // look-back state: aggregate ready
+constexpr unsigned long long kLbIncl = 2ull << 62;   // inclusive prefix ready
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 22;          // a predecessor that never publishes
 
-__global__ __launch_bounds__(kBlock) void k_small_get(
-    const Digest* __restrict__ keys, int64_t n, const Entry* __restrict__ index, uint64_t mask,
+__global__ __launch_bounds__(kBlock) void k_edge_get(
+    const Digest* __restrict__ keys, int64_t n, Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t cap, uint32_t now,
     const uint8_t* __restrict__ log, uint8_t* __restrict__ out, uint64_t out_cap,
     uint64_t* __restrict__ off_out, CacheCounters* __restrict__ ctr,
-    unsigned int* __restrict__ done_ctr, uint64_t* __restrict__ done_slot) {
-  __shared__ uint64_t s_off[kSmallGet + 1];
-  __shared__ uint64_t s_loc[kSmallGet];
-  __shared__ unsigned long long s_w[kBlock / 64];
-  const int l8 = threadIdx.x & 7, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long* __restrict__ state, unsigned int* __restrict__ done_ctr,
+    uint64_t* __restrict__ done_slot) {
+  __shared__ uint64_t s_off[kEdgeKeys + 1];
+  __shared__ uint64_t s_loc[kEdgeKeys];
+  __shared__ unsigned long long s_base;
+  __shared__ int s_fail;
+  const int g = threadIdx.x >> 3, l8 = threadIdx.x & 7, lane = threadIdx.x & 63;
+  const int64_t i0 = (int64_t)blockIdx.x * kEdgeKeys;
+  const int cnt = (int)min((int64_t)kEdgeKeys, n - i0);
   const uint64_t head = *head_ptr;
-  unsigned long long hits = 0, bytes = 0;
-  for (int64_t i = threadIdx.x >> 3; i < n; i += kBlock / 8) {
-    const Digest d = keys[i];
-    uint64_t hl = 0;
-    uint32_t hv = 0;
-#pragma unroll 1
-    for (int round = 0; round < 2 && hl == 0; ++round) {
-      const uint64_t b = round == 0 ? bucket1(d, mask) : bucket2(d, mask);
-      const uint4 v = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket)[l8];
-      const uint64_t a = pack2(v.x, v.y), c = pack2(v.z, v.w);
-      const uint64_t pa = __shfl_xor(a, 1), pc = __shfl_xor(c, 1);
-      const bool hit = (l8 & 1) == 0 && a == d.lo && c == d.hi &&
-                       entry_live(pa, (uint32_t)(pc >> 32), head, cap, now);
-      hl = hit ? pa : 0;
-      hv = hit ? (uint32_t)pc : 0;
+  uint64_t hl = 0;
+  uint32_t hv = 0;
+  if (g < cnt) {
+    const Digest d = keys[i0 + g];
+    int he = 0;
+    uint64_t hb = bucket1(d, mask);
+    group_match(reinterpret_cast<const uint4*>(index + hb * kEntriesPerBucket)[l8], d, l8, head,
+                cap, now, &hl, &hv, &he);
+    if (hl == 0) {
+      hb = bucket2(d, mask);
+      group_match(reinterpret_cast<const uint4*>(index + hb * kEntriesPerBucket)[l8], d, l8,
+                  head, cap, now, &hl, &hv, &he);
+    }
+    if (hl && l8 == 0) mark_ref(index, hb, he, hv);
+    hv = entry_vlen(hv);
+  }
+  if (l8 == 0) {
+    s_loc[g] = hl ? (hl - 1) % cap : 0;
+    s_off[g] = hl ? item_bytes(hv) : 0;
+  }
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
+  // wave 0: exclusive scan of the 32 sizes, publish the aggregate, look back
+  if (threadIdx.x < 64) {
+    const uint64_t v = lane < kEdgeKeys ? s_off[lane] : 0;
+    uint64_t inc = v;
 #pragma unroll
-      for (int sh = 2; sh < 8; sh <<= 1) {
-        const uint64_t ol = __shfl_xor(hl, sh);
-        const uint32_t ov = __shfl_xor(hv, sh);
-        if (ol > hl) { hl = ol; hv = ov; }
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint64_t o = __shfl_up(inc, dd);
+      if (lane >= dd) inc += o;
+    }
+    const uint64_t agg = __shfl(inc, 63);
+    unsigned long long base = 0;
+    if (lane == 0) {
+      if (blockIdx.x == 0) {
+        __hip_atomic_store(state, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_store(state + blockIdx.x, kLbAgg | agg, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        for (int64_t p = (int64_t)blockIdx.x - 1; p >= 0;) {
+          const unsigned long long st =
+              __hip_atomic_load(state + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if (st == 0) {
+            if (++spins > kLbSpinLimit) {  // never hang: report the batch as failed
+              s_fail = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          base += st & kLbVal;
+          if (st & kLbIncl) break;
+          --p;
+        }
+        __hip_atomic_store(state + blockIdx.x, kLbIncl | (base + agg), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
+      s_base = base;
     }
-    if (l8 == 0) {
-      s_loc[i] = hl ? (hl - 1) % cap : 0;
-      s_off[i] = hl ? item_bytes(hv) : 0;  // sizes; scanned below
-      hits += hl ? 1 : 0;
-      bytes += hv;
-    }
+    if (lane <= kEdgeKeys) s_off[lane] = inc - v;  // exclusive; s_off[32] = agg
   }
   __syncthreads();
-  // exclusive scan of s_off[0..n) in place, s_off[n] = total (n <= 2048: 8 per lane)
-  const int per = (int)((n + kBlock - 1) / kBlock);
-  const int a0 = min((int)n, per * (int)threadIdx.x), a1 = min((int)n, a0 + per);
-  unsigned long long mine = 0;
-  for (int k = a0; k < a1; ++k) mine += s_off[k];
-  unsigned long long inc = mine;
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const unsigned long long o = __shfl_up(inc, dd);
-    if (lane >= dd) inc += o;
-  }
-  if (lane == 63) s_w[wv] = inc;
-  __syncthreads();
-  unsigned long long run = inc - mine;
-  for (int k = 0; k < wv; ++k) run += s_w[k];
-  for (int k = a0; k < a1; ++k) {
-    const unsigned long long v = s_off[k];
-    s_off[k] = run;
-    run += v;
-  }
-  if (a1 == n && a0 < a1) s_off[n] = run;
-  if (n == 0 && threadIdx.x == 0) s_off[0] = 0;
-  __syncthreads();
-  const uint64_t total = s_off[n];
-  if (blockIdx.x == 0) {
-    for (int64_t k = threadIdx.x; k <= n; k += kBlock) off_out[k] = s_off[k];
-  }
-  if (blockIdx.x == 0)
-    block_count(ctr, (unsigned long long)(threadIdx.x == 0 ? n : 0), &CacheCounters::get_ops, hits,
-                &CacheCounters::get_hits, bytes, &CacheCounters::get_bytes);
-  // copy (skipped when it does not fit: the caller sees total in off_out and retries
-  // bigger): this workgroup's contiguous share of the response chunks
-  const int64_t nchunks = total > out_cap ? 0 : (int64_t)(total >> 4);
-  const int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
-  const int64_t c0 = (int64_t)blockIdx.x * span, c1 = min(nchunks, c0 + span);
-  int jl = 0;
-  for (int64_t c = c0 + threadIdx.x; c < c1; c += kBlock) {
-    const uint64_t x = (uint64_t)c << 4;
-    int lo = jl, hi = (int)n;  // last k with s_off[k] <= x (monotone per lane)
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_off[mid] <= x) lo = mid; else hi = mid;
+  const uint64_t base = s_base;
+  const uint64_t agg = s_off[kEdgeKeys];
+  const bool fail = s_fail != 0;
+  for (int k = threadIdx.x; k < cnt; k += kBlock) off_out[i0 + k] = base + s_off[k];
+  const bool last_wg = i0 + kEdgeKeys >= n;
+  if (last_wg && threadIdx.x == 0) off_out[n] = base + agg;
+  block_count(ctr, (unsigned long long)(threadIdx.x == 0 ? cnt : 0), &CacheCounters::get_ops,
+              (unsigned long long)(l8 == 0 && hl ? 1 : 0), &CacheCounters::get_hits,
+              (unsigned long long)(l8 == 0 && hl ? hv : 0), &CacheCounters::get_bytes);
+  // copy this workgroup's records (skipped if the batch outgrew the buffer: the caller
+  // sees off_out[n] > out_cap and repeats the batch into a bigger one)
+  if (!fail && base + agg <= out_cap) {
+    const int64_t nchunks = (int64_t)(agg >> 4);
+    int jl = 0;
+    for (int64_t c = threadIdx.x; c < nchunks; c += kBlock) {
+      const uint64_t x = (uint64_t)c << 4;
+      while (jl + 1 < cnt && s_off[jl + 1] <= x) ++jl;  // monotone per lane
+      const u32x4 v = __builtin_nontemporal_load(
+          reinterpret_cast<const u32x4*>(log + s_loc[jl] + (x - s_off[jl])));
+      *reinterpret_cast<u32x4*>(out + base + x) = v;
     }
-    jl = lo;
-    const uint64_t w = x - s_off[lo];
-    const u32x4 v = __builtin_nontemporal_load(
-        reinterpret_cast<const u32x4*>(log + s_loc[lo] + w));
-    *reinterpret_cast<u32x4*>(out + x) = v;
   }
-  // Completion signal without a stream sync: every workgroup makes its offset / value
-  // stores (mapped host memory) visible system-wide, then counts itself done; the last
-  // one resets the counter for the next launch and publishes the total into a pinned
-  // host slot the batcher thread spins on.
-  // Every wave drains its own stores (vmcnt) around the system-scope release fence:
-  // ROCm 7.2 can drop the fence's own wait, and a drain by lane 0 alone left a rare
-  // stale record behind the published total (1 of ~3000 one-key GETs missed).
+  // Completion signal without a stream sync: every wave drains its own stores (vmcnt)
+  // around a system-scope release fence (ROCm 7.2 can drop the fence's own wait), the
+  // workgroup counts itself done, and the last one resets the counter and the look-back
+  // state for the next launch, then publishes the total (or kSlotFailed) into the pinned
+  // host slot the batcher thread polls.
   if (done_slot) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __threadfence_system();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    if (fail) atomicOr(done_ctr + 1, 1u);
+    s_last = atomicAdd(done_ctr, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last) {
+    __shared__ unsigned long long s_total;
+    if (threadIdx.x == 0)  // the last range's inclusive prefix = the batch total
+      s_total = __hip_atomic_load(state + gridDim.x - 1, __ATOMIC_ACQUIRE,
+                                  __HIP_MEMORY_SCOPE_AGENT) & kLbVal;
+    __syncthreads();
+    for (unsigned k = threadIdx.x; k < gridDim.x; k += kBlock) state[k] = 0ull;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned int prev = atomicAdd(done_ctr, 1u);
-      if (prev == gridDim.x - 1) {
-        atomicExch(done_ctr, 0u);
-        __threadfence_system();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned int failed = atomicExch(done_ctr + 1, 0u);
+      atomicExch(done_ctr, 0u);
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (done_slot) {
+        const uint64_t total = failed ? HbmCache::kSlotFailed : (uint64_t)s_total;
         __hip_atomic_store(done_slot, total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
@@ -985,8 +1070,9 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
                                                      uint32_t max_item,
                                                      uint64_t* __restrict__ size,
                                                      CacheCounters* __restrict__ ctr,
-                                                     uint64_t* __restrict__ part) {
-  unsigned long long dropped = 0, ops = 0, psum = 0;
+                                                     uint64_t* __restrict__ part,
+                                                     uint64_t* __restrict__ part_cnt) {
+  unsigned long long dropped = 0, ops = 0, psum = 0, stored = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) size[n] = 0;
   const int64_t plen = part_len(n, gridDim.x);
   const int64_t i1 = min(n, (int64_t)(blockIdx.x + 1) * plen);
@@ -998,9 +1084,11 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
     psum += sz;
     ++ops;
     dropped += win ? 0 : 1;
+    stored += win ? 1 : 0;
   }
   block_count(ctr, ops, &CacheCounters::set_ops, dropped, &CacheCounters::set_dropped);
   block_partial(psum, part);
+  if (part_cnt) block_partial(stored, part_cnt);  // ring ordinals (CLOCK)
 }
 
 // SET index insert, 4 lanes per key: lane q reads entry q of both candidate buckets
@@ -1018,20 +1106,31 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
-    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim) {
+    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim,
+    uint64_t* __restrict__ ring, uint64_t rmask, const uint64_t* __restrict__ ring_tail,
+    uint64_t* __restrict__ ring_tail_next, const uint64_t* __restrict__ cnt_off,
+    uint64_t* __restrict__ head_host) {
   const int l4 = threadIdx.x & 3;
   const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
+  // item-start ring (CLOCK hand input): every stored row takes the next ring entry in
+  // row order = log order (cnt_off: exclusive count of stored rows)
+  const uint64_t rtail = ring ? *ring_tail : 0;
   unsigned long long evicted = 0, bytes = 0, lost = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *head_next = head_new;
+    if (ring) *ring_tail_next = rtail + cnt_off[n];
+    if (head_host) __hip_atomic_store(head_host, head_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
     if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
       const uint32_t sl = slot_of[i];
       dd_keys[sl] = 0ull;
       dd_win[sl] = -1;
     }
+    if (ring && l4 == 0 && size[i]) ring[(rtail + cnt_off[i]) & rmask] = base + off[i];
     if (l4 == 0) claim[i] = ~0u;  // no entry (yet)
     if (size[i] == 0) continue;   // uniform across the 4-lane group
     const Digest d = keys[i];
@@ -1137,6 +1236,217 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
 }
 
 // ---------------------------------------------------------------------------------
+// CLOCK eviction: second chances for referenced items before the log overwrites them
+// ---------------------------------------------------------------------------------
+// The log is a FIFO: a SET batch of B bytes overwrites the oldest B bytes. Before it
+// runs, the hand walks the item-start ring (one entry per stored item, in log order)
+// from the oldest item: an item whose index entry still points at it, is unexpired and
+// was read since the hand last passed it (kRefBit) is re-appended at the head in front
+// of the batch (a reinsertion, which also clears the bit); the rest are left to the
+// overwrite. The hand stops at the first entry c whose item the overwrite — now
+// B + R bytes, R = reinserted bytes of entries [0, c) — does not reach:
+//     loc_c >= head - cap + R_c + B        (entries [0, c) consumed)
+// R is capped by the reinsertion budget `rmax` (hot items past it just age out).
+// Kernels: k_rc_scan (per-entry loc/hot size + block partials), k_rc_cut (exclusive scan
+// of hot bytes, first entry meeting the bound), k_rc_pick (reinsert rows + the batch's
+// own rows into one combined SET batch), k_rc_copy (stage the reinserted records in a
+// scratch buffer: their old bytes lie in the region the combined batch overwrites).
+// The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
+// win over a reinsertion of the same key). Host twin: HostCache::reclaim.
+struct RcArgs {
+  const uint64_t* ring;
+  uint64_t rmask;
+  const uint64_t* ring_tail;
+  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first unconsumed, [3] consumed
+  int64_t W;
+  const uint64_t* head_ptr;
+  uint64_t cap;
+  uint32_t now;
+  uint64_t rmax;
+};
+
+__global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __restrict__ log,
+                                                    const Entry* __restrict__ index, uint64_t mask,
+                                                    const uint32_t* __restrict__ vlen_new,
+                                                    int64_t n_new, uint32_t max_item,
+                                                    uint64_t* __restrict__ rc_loc,
+                                                    uint64_t* __restrict__ rc_h,
+                                                    uint64_t* __restrict__ part_h) {
+  const uint64_t hand = a.ctl[0], rtail = *a.ring_tail, head = *a.head_ptr;
+  // the batch's bytes (upper bound: dedupe losers included)
+  unsigned long long best = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_new;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t v = vlen_new[i];
+    if (v != kSkipVlen && v <= max_item) best += item_bytes(v);
+  }
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t avail = rtail - hand;
+  uint64_t loc = kRingSkip, h = 0;
+  if (j < a.W && (uint64_t)j < avail) {
+    const uint64_t idx = hand + (uint64_t)j;
+    const uint64_t l = rtail - idx <= a.rmask + 1 ? a.ring[idx & a.rmask] : kRingSkip;
+    if (l != kRingSkip && head <= l + a.cap) {  // intact (not overwritten yet)
+      const uint4* hp = reinterpret_cast<const uint4*>(log + l % a.cap);
+      const uint4 w0 = hp[0], w1 = hp[1];
+      if (w1.w == kItemMagic) {
+        loc = l;
+        const uint64_t d0 = pack2(w0.x, w0.y), d1 = pack2(w0.z, w0.w);
+        const uint32_t vlen = w1.x;
+        const Digest d{d0, d1};
+        const uint64_t bs[2] = {bucket1(d, mask), bucket2(d, mask)};
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int k = 0; k < (int)kEntriesPerBucket; ++k) {
+            const Entry* e = index + bs[q] * kEntriesPerBucket + k;
+            const uint64_t el = __hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (el == l + 1) {
+              const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
+              const uint32_t ex = (uint32_t)(ve >> 32);
+              if (((uint32_t)ve & kRefBit) && (ex == 0 || ex > a.now)) h = item_bytes(vlen);
+            }
+          }
+      }
+    }
+  }
+  if (j < a.W) {
+    rc_loc[j] = loc;
+    rc_h[j] = h;
+  }
+  block_partial(h, part_h);
+  // batch bytes: one atomic per block
+  __shared__ unsigned long long s_b[kBlock / 64];
+  best = wave_sum(best);
+  if ((threadIdx.x & 63) == 0) s_b[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += s_b[k];
+    if (t) atomicAdd(&a.ctl[1], t);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rc_cut(RcArgs a, const uint64_t* __restrict__ rc_loc,
+                                                   const uint64_t* __restrict__ rc_h,
+                                                   const uint64_t* __restrict__ part_h,
+                                                   uint64_t* __restrict__ rc_hx) {
+  __shared__ unsigned long long s_w[kBlock / 64];
+  __shared__ unsigned long long s_pre;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long pre = 0;
+  for (unsigned b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += part_h[b];
+  pre = wave_sum(pre);
+  if (lane == 0) s_w[w] = pre;
+  __syncthreads();
+  if (threadIdx.x == 0) s_pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t h = j < a.W ? rc_h[j] : 0;
+  unsigned long long inc = h;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  __syncthreads();  // s_w reuse
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  unsigned long long hx = s_pre + inc - h;
+  for (int k = 0; k < w; ++k) hx += s_w[k];
+  if (j < a.W) {
+    rc_hx[j] = hx;
+    const uint64_t loc = rc_loc[j];
+    const uint64_t r = hx < a.rmax ? hx : a.rmax;
+    if (loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r)
+      atomicMin(&a.ctl[2], (unsigned long long)j);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rc_pick(
+    RcArgs a, const uint8_t* __restrict__ log, const uint64_t* __restrict__ rc_loc,
+    const uint64_t* __restrict__ rc_h, const uint64_t* __restrict__ rc_hx,
+    const uint8_t* __restrict__ scratch, const Digest* __restrict__ keys,
+    const uint8_t* __restrict__ values, const uint64_t* __restrict__ val_off,
+    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ expire, int64_t n_new, Digest* __restrict__ cb_keys,
+    uint64_t* __restrict__ cb_voff, uint32_t* __restrict__ cb_vlen,
+    uint32_t* __restrict__ cb_flags, uint32_t* __restrict__ cb_expire,
+    uint64_t* __restrict__ rc_src, uint64_t* __restrict__ rc_len, CacheCounters* __restrict__ ctr) {
+  const uint64_t avail = *a.ring_tail - a.ctl[0];
+  const uint64_t weff = (uint64_t)a.W < avail ? (uint64_t)a.W : avail;
+  const unsigned long long cut = a.ctl[2];
+  const uint64_t consumed = cut != ~0ull ? cut : weff;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl[3] = consumed;
+  unsigned long long nre = 0, bre = 0;
+  const int64_t rows = a.W + n_new;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * kBlock) {
+    if (r < a.W) {
+      const uint64_t h = rc_h[r], hx = rc_hx[r];
+      if ((uint64_t)r < consumed && h && hx + h <= a.rmax) {
+        const uint64_t phys = rc_loc[r] % a.cap;
+        const uint4* hp = reinterpret_cast<const uint4*>(log + phys);
+        const uint4 w0 = hp[0], w1 = hp[1];
+        cb_keys[r] = Digest{pack2(w0.x, w0.y), pack2(w0.z, w0.w)};
+        cb_voff[r] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
+        cb_vlen[r] = w1.x;
+        cb_flags[r] = w1.y;
+        cb_expire[r] = w1.z;
+        rc_src[r] = phys;
+        rc_len[r] = h;
+        ++nre;
+        bre += w1.x;
+      } else {
+        cb_keys[r] = Digest{0, 0};
+        cb_voff[r] = 0;
+        cb_vlen[r] = kSkipVlen;
+        cb_flags[r] = 0;
+        cb_expire[r] = 0;
+        rc_len[r] = 0;
+      }
+    } else {
+      const int64_t i = r - a.W;
+      cb_keys[r] = keys[i];
+      cb_voff[r] = (uint64_t)(uintptr_t)values + val_off[i];
+      cb_vlen[r] = vlen[i];
+      cb_flags[r] = flags ? flags[i] : 0u;
+      cb_expire[r] = expire ? expire[i] : 0u;
+    }
+  }
+  block_count(ctr, nre, &CacheCounters::reinserted, bre, &CacheCounters::reinsert_bytes);
+}
+
+// One wave per reinserted record: copy [header | value | pad] into the scratch buffer at
+// the record's hot-byte prefix. The last kernel of the hand step: advances the hand and
+// resets the per-step control words.
+__global__ __launch_bounds__(kBlock) void k_rc_copy(RcArgs a, const uint8_t* __restrict__ log,
+                                                    const uint64_t* __restrict__ rc_src,
+                                                    const uint64_t* __restrict__ rc_len,
+                                                    const uint64_t* __restrict__ rc_hx,
+                                                    uint8_t* __restrict__ scratch) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t hand = a.ctl[0] + a.ctl[3];
+    const uint64_t rtail = *a.ring_tail;
+    if (rtail - hand > a.rmask + 1) hand = rtail - (a.rmask + 1);  // ring lapped the hand
+    a.ctl[0] = hand;
+    a.ctl[1] = 0;
+    a.ctl[2] = ~0ull;
+    a.ctl[3] = 0;
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; r < a.W; r += nwaves) {
+    const uint64_t len = rc_len[r];
+    if (!len) continue;
+    const u32x4* src = reinterpret_cast<const u32x4*>(log + rc_src[r]);
+    u32x4* dst = reinterpret_cast<u32x4*>(scratch + rc_hx[r]);
+    for (uint64_t c = lane; c < (len >> 4); c += 64) dst[c] = __builtin_nontemporal_load(src + c);
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // DELETE / SWEEP
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_delete(const Digest* __restrict__ keys, int64_t n,
@@ -1191,7 +1501,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Entry* __restrict__ index, uin
     const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
     if (entry_live(loc, (uint32_t)(ve >> 32), head, cap, now)) {
       ++live;
-      bytes += item_bytes((uint32_t)ve);
+      bytes += item_bytes(entry_vlen((uint32_t)ve));
     } else if (atomicCAS(reinterpret_cast<unsigned long long*>(&e->loc), (unsigned long long)loc,
                          0ull) == loc) {
       ++swept;
@@ -1372,12 +1682,13 @@ size_t device_scan_tmp_bytes(int64_t n) {
 // k_offsets launch for sizes produced by `grid` workgroups over contiguous ranges.
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
                     uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr,
-                    int64_t plen_override = 0) {
+                    int64_t plen_override = 0, const uint64_t* part_cnt = nullptr,
+                    uint64_t* cnt = nullptr) {
   const int64_t plen = plen_override > 0 ? plen_override : part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
   hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
-                     host_total);
+                     host_total, part_cnt, cnt);
   HIP_OK(hipGetLastError());
 }
 
@@ -1492,7 +1803,10 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&scratch_, 64));
   HIP_OK(hipMalloc(&done_ctr_, 64));
   HIP_OK(hipMemset(done_ctr_, 0, 64));
-  HIP_OK(hipMalloc(&part_, 2 * kMaxGrid * sizeof(uint64_t)));
+  const size_t lb_words = (size_t)(kSmallGetMax / kEdgeKeys + 1);
+  HIP_OK(hipMalloc(&lb_state_, lb_words * sizeof(unsigned long long)));
+  HIP_OK(hipMemset(lb_state_, 0, lb_words * sizeof(unsigned long long)));
+  HIP_OK(hipMalloc(&part_, 3 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
                        hipHostMallocMapped | hipHostMallocCoherent));
@@ -1500,6 +1814,17 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
   HIP_OK(hipMemset(ctr_, 0, kCtrShards * sizeof(CacheCounters)));
+  SH_CHECK(cfg_.evict == kEvictFifo || cfg_.evict == kEvictClock, "unknown eviction policy");
+  SH_CHECK(cfg_.max_item <= kVlenMask, "max_item must be < 2 GiB (CLOCK bit in vlen)");
+  if (cfg_.evict == kEvictClock) {
+    rmax_ = reinsert_budget(cfg_.log_bytes, cfg_.reinsert_max);
+    ring_cap_ = ring_entries(cfg_.nbuckets);
+    HIP_OK(hipMalloc(&ring_, ring_cap_ * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&rc_ctl_, 8 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(rc_ctl_, 0, 8 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(rc_ctl_ + 2, 0xff, sizeof(unsigned long long)));  // no cut yet
+    HIP_OK(hipMalloc(&rc_scratch_, rmax_ + 64));
+  }
   HIP_OK(hipDeviceSynchronize());
 }
 
@@ -1512,6 +1837,7 @@ HbmCache::~HbmCache() {
   (void)hipFree(ctr_);
   (void)hipFree(scratch_);
   (void)hipFree(done_ctr_);
+  (void)hipFree(lb_state_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -1519,11 +1845,63 @@ HbmCache::~HbmCache() {
   (void)hipFree(dd_win_);
   (void)hipFree(dd_slot_);
   (void)hipFree(set_size_);
-  (void)hipFree(set_off_); (void)hipFree(set_claim_);
+  (void)hipFree(set_off_); (void)hipFree(set_claim_); (void)hipFree(set_cnt_);
+  (void)hipFree(ring_); (void)hipFree(rc_ctl_); (void)hipFree(rc_scratch_);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_hx_, (void*)rc_part_, (void*)rc_src_,
+                  (void*)rc_len_, (void*)cb_voff_, (void*)cb_keys_, (void*)cb_vlen_,
+                  (void*)cb_flags_, (void*)cb_expire_})
+    (void)hipFree(p);
 }
 
 uint64_t HbmCache::hbm_bytes() const {
-  return cfg_.log_bytes + item_bytes(cfg_.max_item) + 64 + cfg_.nbuckets * kBucketBytes;
+  return cfg_.log_bytes + item_bytes(cfg_.max_item) + 64 + cfg_.nbuckets * kBucketBytes +
+         ring_cap_ * sizeof(uint64_t) + (rc_scratch_ ? rmax_ + 64 : 0);
+}
+
+// Hand-step workspace for windows of w ring entries, and the combined SET batch (w
+// reinsertion rows + the batch's own rows).
+void HbmCache::ensure_rc_ws(int64_t w) {
+  if (w <= rc_cap_) return;
+  int64_t cap = rc_cap_ ? rc_cap_ : 4096;
+  while (cap < w) cap *= 2;
+  HIP_OK(hipDeviceSynchronize());
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_hx_, (void*)rc_part_, (void*)rc_src_,
+                  (void*)rc_len_})
+    (void)hipFree(p);
+  HIP_OK(hipMalloc(&rc_loc_, cap * 8));
+  HIP_OK(hipMalloc(&rc_h_, cap * 8));
+  HIP_OK(hipMalloc(&rc_hx_, cap * 8));
+  HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
+  HIP_OK(hipMalloc(&rc_src_, cap * 8));
+  HIP_OK(hipMalloc(&rc_len_, cap * 8));
+  rc_cap_ = cap;
+}
+
+bool HbmCache::should_reclaim(uint64_t bytes_bound) const {
+  if (cfg_.evict != kEvictClock) return false;
+  // head as of the last SET chain that completed (published by k_set_index); up to a
+  // few stores may be queued behind it, so reclaim once the log is within 4 batches of
+  // wrapping (the hand step decides exactly on the device; skipping is only an
+  // optimisation for a log that has not filled yet)
+  const uint64_t h = __atomic_load_n(host_slots_ + kHeadSlot, __ATOMIC_ACQUIRE);
+  return h + 4 * (bytes_bound + rmax_) > cfg_.log_bytes;
+}
+
+void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
+                              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
+                              int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s) {
+  RcArgs a{ring_, ring_cap_ - 1, cur_ring_tail(), rc_ctl_, w, cur_head(), cfg_.log_bytes, now, rmax};
+  const int g = (int)((w + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, log_, index_, cfg_.nbuckets - 1,
+                     vlen, n, cfg_.max_item, rc_loc_, rc_h_, rc_part_);
+  hipLaunchKernelGGL(k_rc_cut, dim3(g), dim3(kBlock), 0, s, a, rc_loc_, rc_h_, rc_part_, rc_hx_);
+  hipLaunchKernelGGL(k_rc_pick, dim3(grid_for(w + n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, a,
+                     log_, rc_loc_, rc_h_, rc_hx_, rc_scratch_, keys, values, val_off, vlen, flags,
+                     expire, n, cb_keys_, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, rc_src_,
+                     rc_len_, ctr_);
+  hipLaunchKernelGGL(k_rc_copy, dim3(grid_for(w * 64, kBlock, kMaxGrid)), dim3(kBlock), 0, s, a,
+                     log_, rc_src_, rc_len_, rc_hx_, rc_scratch_);
+  HIP_OK(hipGetLastError());
 }
 
 void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
@@ -1534,6 +1912,7 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   HIP_OK(hipDeviceSynchronize());
   (void)hipFree(dd_keys_); (void)hipFree(dd_win_); (void)hipFree(dd_slot_);
   (void)hipFree(set_size_); (void)hipFree(set_off_); (void)hipFree(set_claim_);
+  (void)hipFree(set_cnt_);
   const uint64_t tslots = (uint64_t)cap * 2;
   HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
@@ -1544,6 +1923,7 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_claim_, cap * sizeof(uint32_t)));
+  HIP_OK(hipMalloc(&set_cnt_, (cap + 1) * sizeof(uint64_t)));
   dd_mask_ = (uint32_t)(tslots - 1);
   set_cap_ = cap;
   ++ws_gen_;
@@ -1634,18 +2014,17 @@ uint64_t HbmCache::wait_host_slot(int i, int64_t timeout_ms) const {
 
 void HbmCache::small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap,
                          uint64_t* off, uint32_t now, hipStream_t s, int done_slot) {
-  SH_CHECK(n >= 0 && n <= kSmallGet, "small_get batch too large");
+  SH_CHECK(n >= 0 && n <= kSmallGetMax, "edge GET batch too large");
   SH_CHECK(done_slot < kHostSlots, "host slot out of range");
-  TraceRange tr("hbm.small_get");
+  TraceRange tr("hbm.edge_get");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   uint64_t* ds = done_slot >= 0 ? host_slots_ + done_slot : nullptr;
   if (ds) __atomic_store_n(ds, kSlotPending, __ATOMIC_RELEASE);
-  // ~64 KiB of response per workgroup at 4 KiB values; >= 1
-  const int grid = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / 8));
-  hipLaunchKernelGGL(k_small_get, dim3(grid), dim3(kBlock), 0, s, keys, n, index_,
+  const int grid = (int)std::max<int64_t>(1, (n + kEdgeKeys - 1) / kEdgeKeys);
+  hipLaunchKernelGGL(k_edge_get, dim3(grid), dim3(kBlock), 0, s, keys, n, index_,
                      cfg_.nbuckets - 1, cur_head(), cfg_.log_bytes, now, log_, out, out_cap, off,
-                     ctr_, ds ? done_ctr_ : nullptr, ds);
+                     ctr_, lb_state_, done_ctr_, ds);
   HIP_OK(hipGetLastError());
 }
 
@@ -1666,8 +2045,34 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
            "SET batch larger than half the log; split the batch");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
-  ensure_set_ws(n, s);
-  store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
+  // the CLOCK hand's reinsertions share the half-log bound with the batch
+  const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
+  if (rmax && should_reclaim(bytes_bound)) {
+    const int64_t w = hand_window(n);
+    ensure_rc_ws(w);
+    if (w + n > cb_cap_) {
+      int64_t cap = cb_cap_ ? cb_cap_ : 4096;
+      while (cap < w + n) cap *= 2;
+      HIP_OK(hipDeviceSynchronize());
+      for (void* p : {(void*)cb_voff_, (void*)cb_keys_, (void*)cb_vlen_, (void*)cb_flags_,
+                      (void*)cb_expire_})
+        (void)hipFree(p);
+      HIP_OK(hipMalloc(&cb_keys_, cap * sizeof(Digest)));
+      HIP_OK(hipMalloc(&cb_voff_, cap * 8));
+      HIP_OK(hipMalloc(&cb_vlen_, cap * 4));
+      HIP_OK(hipMalloc(&cb_flags_, cap * 4));
+      HIP_OK(hipMalloc(&cb_expire_, cap * 4));
+      cb_cap_ = cap;
+    }
+    ensure_set_ws(w + n, s);
+    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
+    // combined batch: reinsertions first (log order), then the batch (its SETs win)
+    store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
+                 index_after);
+  } else {
+    ensure_set_ws(n, s);
+    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
+  }
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
 
@@ -1681,10 +2086,12 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
                      (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
   const int sgrid = grid_for(n, kBlock, kMaxGrid);
+  uint64_t* part_cnt = ring_ ? part_ + 2 * kMaxGrid : nullptr;
   hipLaunchKernelGGL(k_set_size, dim3(sgrid), dim3(kBlock), 0, s, vlen, n, dd_win_, dd_slot_,
-                     cfg_.max_item, set_size_, ctr_, part_ + kMaxGrid);
+                     cfg_.max_item, set_size_, ctr_, part_ + kMaxGrid, part_cnt);
   HIP_OK(hipGetLastError());
-  launch_offsets(set_size_, n, part_ + kMaxGrid, sgrid, set_off_, s);
+  launch_offsets(set_size_, n, part_ + kMaxGrid, sgrid, set_off_, s, nullptr, 0, part_cnt,
+                 ring_ ? set_cnt_ : nullptr);
   launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());
@@ -1694,7 +2101,8 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                      cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
-                     set_claim_);
+                     set_claim_, ring_, ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(),
+                     next_ring_tail(), set_cnt_, host_slots_ + kHeadSlot);
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      set_off_, vlen, expire, cur_head(), set_claim_, index_);
   HIP_OK(hipGetLastError());
@@ -1871,6 +2279,13 @@ void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
   std::fclose(f);
   SH_CHECK(ok, "snapshot truncated: " + path);
   HIP_OK(hipMemcpy(cur_head(), &h.head, 8, hipMemcpyHostToDevice));
+  // the CLOCK ring is not part of a snapshot: the first lap after a restore is FIFO
+  HIP_OK(hipMemset(head_ + 2, 0, 2 * sizeof(uint64_t)));
+  if (rc_ctl_) {
+    HIP_OK(hipMemset(rc_ctl_, 0, 8 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(rc_ctl_ + 2, 0xff, sizeof(unsigned long long)));
+  }
+  __atomic_store_n(host_slots_ + kHeadSlot, h.head, __ATOMIC_RELEASE);
   if (user)
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }

@@ -20,11 +20,19 @@ void* map_zeroed(size_t bytes) {
 
 }  // namespace
 
-HostCache::HostCache(uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item)
-    : log_bytes_(log_bytes), nbuckets_(nbuckets), mask_(nbuckets - 1), max_item_(max_item) {
+HostCache::HostCache(uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int evict,
+                     uint64_t reinsert_max)
+    : log_bytes_(log_bytes), nbuckets_(nbuckets), mask_(nbuckets - 1), max_item_(max_item),
+      evict_(evict) {
   SH_CHECK(nbuckets >= 2 && (nbuckets & (nbuckets - 1)) == 0, "nbuckets must be a power of two");
   SH_CHECK(log_bytes >= 4096 && log_bytes % 16 == 0, "log_bytes must be >=4096 and %16");
   SH_CHECK(max_item > 0 && item_bytes(max_item) * 2 <= log_bytes, "max_item too large");
+  SH_CHECK(max_item <= kVlenMask, "max_item must be < 2 GiB (CLOCK bit in vlen)");
+  SH_CHECK(evict == 0 || evict == 1, "unknown eviction policy");
+  if (evict_) {
+    rmax_ = reinsert_budget(log_bytes, reinsert_max);
+    ring_.assign(ring_entries(nbuckets), kRingSkip);
+  }
   log_alloc_ = log_bytes + item_bytes(max_item) + 64;
   log_ = static_cast<uint8_t*>(map_zeroed(log_alloc_));
   index_alloc_ = nbuckets * kBucketBytes;
@@ -37,20 +45,23 @@ HostCache::~HostCache() {
 }
 
 uint64_t HostCache::probe_locked(const Digest& d, uint32_t now, uint32_t* vlen,
-                                 uint64_t reserve) const {
+                                 uint64_t reserve, bool mark) {
   uint64_t best = 0;
   uint32_t bv = 0;
+  Entry* be = nullptr;
   const uint64_t bs[2] = {bucket1(d, mask_), bucket2(d, mask_)};
   for (uint64_t b : bs) {
-    const Entry* e = index_ + b * kEntriesPerBucket;
+    Entry* e = index_ + b * kEntriesPerBucket;
     for (uint32_t k = 0; k < kEntriesPerBucket; ++k) {
       if (e[k].d0 == d.lo && e[k].d1 == d.hi &&
           entry_live(e[k].loc, e[k].expire, head_ + reserve, log_bytes_, now) && e[k].loc > best) {
         best = e[k].loc;
-        bv = e[k].vlen;
+        bv = entry_vlen(e[k].vlen);
+        be = &e[k];
       }
     }
   }
+  if (mark && be) be->vlen |= kRefBit;
   if (vlen) *vlen = bv;
   return best;  // 0 = miss, else logical+1
 }
@@ -61,7 +72,7 @@ void HostCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* s
   uint64_t acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     uint32_t vl = 0;
-    const uint64_t l = probe_locked(keys[i], now, &vl, reserve);
+    const uint64_t l = probe_locked(keys[i], now, &vl, reserve, true);
     ctr_.get_ops++;
     if (l) {
       loc[i] = (l - 1) % log_bytes_;
@@ -132,18 +143,93 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
                       const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                       int64_t n, uint32_t now) {
   std::lock_guard<std::mutex> lk(mu_);
+  std::vector<Row> rows;
+  std::vector<uint8_t> stage;
+  if (evict_ && rmax_) {
+    uint64_t bytes = 0;  // the batch's bytes (dedupe losers included), as the device
+    for (int64_t i = 0; i < n; ++i)
+      if (vlen[i] != kSkipVlen && vlen[i] <= max_item_) bytes += item_bytes(vlen[i]);
+    const int64_t w = hand_window(n);
+    reclaim_locked(n, bytes, now, &rows, &stage);
+    rows.resize((size_t)w);  // the device's combined batch: w reinsertion rows, then n
+    for (size_t r = 0; r < rows.size(); ++r)
+      if (!rows[r].val) rows[r] = Row{Digest{0, 0}, nullptr, kSkipVlen, 0, 0};
+  }
+  rows.reserve(rows.size() + (size_t)n);
+  for (int64_t i = 0; i < n; ++i)
+    rows.push_back(Row{keys[i], values + (vlen[i] == kSkipVlen ? 0 : val_off[i]), vlen[i],
+                       flags ? flags[i] : 0u, expire ? expire[i] : 0u});
+  store_rows_locked(rows, now);
+}
+
+void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vector<Row>* out,
+                               std::vector<uint8_t>* stage) {
+  const int64_t w = hand_window(n);
+  const uint64_t rcap = ring_.size(), rmask = rcap - 1;
+  const uint64_t avail = ring_tail_ - hand_;
+  const uint64_t weff = std::min<uint64_t>((uint64_t)w, avail);
+  struct Hot { int64_t j; uint64_t loc, h, hx; };
+  std::vector<Hot> hot;
+  uint64_t hx = 0, consumed = weff;
+  for (uint64_t j = 0; j < weff; ++j) {
+    const uint64_t idx = hand_ + j;
+    const uint64_t l = ring_tail_ - idx <= rcap ? ring_[idx & rmask] : kRingSkip;
+    if (l == kRingSkip || head_ > l + log_bytes_) continue;  // hole or overwritten
+    ItemHeader h;
+    std::memcpy(&h, log_ + l % log_bytes_, sizeof h);
+    if (h.magic != kItemMagic) continue;
+    // stop at the first item the overwrite (batch + reinsertions so far) does not reach
+    if (l + log_bytes_ >= head_ + bytes + std::min(hx, rmax_)) {
+      consumed = j;
+      break;
+    }
+    const Digest d{h.d0, h.d1};
+    const uint64_t bs[2] = {bucket1(d, mask_), bucket2(d, mask_)};
+    uint64_t hb = 0;
+    for (uint64_t b : bs)
+      for (uint32_t k = 0; k < kEntriesPerBucket; ++k) {
+        const Entry& e = index_[b * kEntriesPerBucket + k];
+        if (e.loc == l + 1 && (e.vlen & kRefBit) && (e.expire == 0 || e.expire > now))
+          hb = item_bytes(h.vlen);
+      }
+    if (hb) hot.push_back(Hot{(int64_t)j, l, hb, hx});
+    hx += hb;
+  }
+  out->assign((size_t)w, Row{Digest{0, 0}, nullptr, kSkipVlen, 0, 0});
+  uint64_t staged = 0;
+  for (const Hot& t : hot)
+    if ((uint64_t)t.j < consumed && t.hx + t.h <= rmax_) staged = t.hx + t.h;
+  stage->assign(staged + 16, 0);
+  for (const Hot& t : hot) {
+    if ((uint64_t)t.j >= consumed || t.hx + t.h > rmax_) continue;
+    const uint8_t* rec = log_ + t.loc % log_bytes_;
+    std::memcpy(stage->data() + t.hx, rec, t.h);
+    ItemHeader h;
+    std::memcpy(&h, rec, sizeof h);
+    (*out)[(size_t)t.j] = Row{Digest{h.d0, h.d1}, stage->data() + t.hx + kItemHeaderBytes, h.vlen,
+                              h.flags, h.expire};
+    ctr_.reinserted++;
+    ctr_.reinsert_bytes += h.vlen;
+  }
+  hand_ += consumed;
+  if (ring_tail_ - hand_ > rcap) hand_ = ring_tail_ - rcap;
+}
+
+void HostCache::store_rows_locked(const std::vector<Row>& rows, uint32_t now) {
+  const int64_t n = (int64_t)rows.size();
   // last write of a key in the batch wins (dedupe on digest.lo, as on the device)
   std::unordered_map<uint64_t, int64_t> last;
   last.reserve((size_t)n * 2);
   for (int64_t i = 0; i < n; ++i)
-    if (vlen[i] != kSkipVlen) last[keys[i].lo ? keys[i].lo : 1] = i;
+    if (rows[i].vlen != kSkipVlen) last[rows[i].key.lo ? rows[i].key.lo : 1] = i;
   std::vector<uint64_t> sz((size_t)n);
   uint64_t total = 0;
   for (int64_t i = 0; i < n; ++i) {
-    if (vlen[i] == kSkipVlen) { sz[i] = 0; continue; }
+    const Row& r = rows[i];
+    if (r.vlen == kSkipVlen) { sz[i] = 0; continue; }
     ctr_.set_ops++;
-    const bool win = last[keys[i].lo ? keys[i].lo : 1] == i && vlen[i] <= max_item_;
-    sz[i] = win ? item_bytes(vlen[i]) : 0;
+    const bool win = last[r.key.lo ? r.key.lo : 1] == i && r.vlen <= max_item_;
+    sz[i] = win ? item_bytes(r.vlen) : 0;
     if (!win) ctr_.set_dropped++;
     total += sz[i];
   }
@@ -152,22 +238,31 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
   uint64_t acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     if (!sz[i]) continue;
+    const Row& r = rows[i];
     const uint64_t L = base + acc;
     uint8_t* p = log_ + L % log_bytes_;
-    ItemHeader h{keys[i].lo, keys[i].hi, vlen[i], flags ? flags[i] : 0u, expire ? expire[i] : 0u,
-                 kItemMagic};
+    ItemHeader h{r.key.lo, r.key.hi, r.vlen, r.flags, r.expire, kItemMagic};
     std::memcpy(p, &h, sizeof h);
-    std::memcpy(p + kItemHeaderBytes, values + val_off[i], vlen[i]);
-    const uint64_t pad = sz[i] - kItemHeaderBytes - vlen[i];
-    if (pad) std::memset(p + kItemHeaderBytes + vlen[i], 0, pad);
+    std::memcpy(p + kItemHeaderBytes, r.val, r.vlen);
+    const uint64_t pad = sz[i] - kItemHeaderBytes - r.vlen;
+    if (pad) std::memset(p + kItemHeaderBytes + r.vlen, 0, pad);
     acc += sz[i];
   }
   head_ = base + total;
+  if (evict_) {  // item starts in log order, one ring entry per stored row
+    const uint64_t rmask = ring_.size() - 1;
+    uint64_t o = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (!sz[i]) continue;
+      ring_[ring_tail_++ & rmask] = base + o;
+      o += sz[i];
+    }
+  }
   acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     if (!sz[i]) continue;
-    insert_locked(keys[i], base + acc + 1, vlen[i], expire ? expire[i] : 0u, now);
-    ctr_.set_bytes += vlen[i];
+    insert_locked(rows[i].key, base + acc + 1, rows[i].vlen, rows[i].expire, now);
+    ctr_.set_bytes += rows[i].vlen;
     acc += sz[i];
   }
 }
@@ -202,7 +297,7 @@ void HostCache::sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes
     if (!e.loc) continue;
     if (entry_live(e.loc, e.expire, head_, log_bytes_, now)) {
       ++live;
-      bytes += item_bytes(e.vlen);
+      bytes += item_bytes(entry_vlen(e.vlen));
     } else {
       e.loc = 0;
       ctr_.swept++;
@@ -270,6 +365,7 @@ void HostCache::load(const std::string& path, uint64_t user[4]) {
   std::fclose(f);
   SH_CHECK(ok, "snapshot truncated: " + path);
   head_ = h.head;
+  ring_tail_ = hand_ = 0;  // the CLOCK ring is not part of a snapshot (first lap FIFO)
   if (user)
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
@@ -293,7 +389,7 @@ bool HostCache::get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* 
                         uint32_t now, uint32_t* expire) {
   std::lock_guard<std::mutex> lk(mu_);
   uint32_t vl = 0;
-  const uint64_t l = probe_locked(key, now, &vl);
+  const uint64_t l = probe_locked(key, now, &vl, 0, true);
   ctr_.get_ops++;
   if (!l) return false;
   ctr_.get_hits++;

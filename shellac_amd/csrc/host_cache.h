@@ -16,7 +16,9 @@ namespace shellac {
 
 class HostCache {
  public:
-  HostCache(uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item);
+  // evict: 0 FIFO, 1 CLOCK (as ShardConfig::evict); reinsert_max 0 = auto budget.
+  HostCache(uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int evict = 1,
+            uint64_t reinsert_max = 0);
   ~HostCache();
   HostCache(const HostCache&) = delete;
   HostCache& operator=(const HostCache&) = delete;
@@ -46,10 +48,24 @@ class HostCache {
   uint64_t log_bytes() const { return log_bytes_; }
   uint64_t nbuckets() const { return nbuckets_; }
   uint32_t max_item() const { return max_item_; }
+  uint64_t reinsert_max() const { return evict_ ? rmax_ : 0; }
 
  private:
+  struct Row {  // one SET row of a (possibly combined) batch
+    Digest key;
+    const uint8_t* val;
+    uint32_t vlen, flags, expire;
+  };
   bool insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uint32_t expire, uint32_t now);
-  uint64_t probe_locked(const Digest& d, uint32_t now, uint32_t* vlen, uint64_t reserve = 0) const;
+  // mark: a GET (sets the CLOCK reference bit of the entry it finds)
+  uint64_t probe_locked(const Digest& d, uint32_t now, uint32_t* vlen, uint64_t reserve = 0,
+                        bool mark = false);
+  void store_rows_locked(const std::vector<Row>& rows, uint32_t now);
+  // CLOCK hand step ahead of a batch of `bytes` log bytes over `n` rows (the device
+  // algorithm, sequentially): appends the reinsertion rows to `out`, their records
+  // staged in `stage`.
+  void reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vector<Row>* out,
+                      std::vector<uint8_t>* stage);
 
   uint64_t log_bytes_, nbuckets_, mask_;
   uint32_t max_item_;
@@ -60,6 +76,10 @@ class HostCache {
   uint64_t head_ = 0;
   CacheCounters ctr_{};
   mutable std::mutex mu_;
+  int evict_ = 1;
+  uint64_t rmax_ = 0;
+  std::vector<uint64_t> ring_;  // item starts in log order (kRingSkip holes)
+  uint64_t ring_tail_ = 0, hand_ = 0;
 };
 
 // CPU versions of the device batch helpers (same contracts as hbm_cache.h).

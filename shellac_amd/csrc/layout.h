@@ -34,10 +34,17 @@ struct alignas(32) Entry {
   uint64_t d0;      // digest.lo
   uint64_t d1;      // digest.hi
   uint64_t loc;     // logical offset of the item header + 1 (0 = empty slot)
-  uint32_t vlen;    // value length in bytes
+  uint32_t vlen;    // value length in bytes | kRefBit (read since the CLOCK hand last passed)
   uint32_t expire;  // absolute expiry (seconds since cache epoch), 0 = never
 };
 static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
+
+// CLOCK reference bit, kept in the top bit of Entry::vlen: set by a GET hit, cleared
+// when the eviction hand re-appends the item (a second chance) — see reclaim in
+// hbm_cache.h. Values are therefore < 2 GiB (max_item is checked against it).
+constexpr uint32_t kRefBit = 0x80000000u;
+constexpr uint32_t kVlenMask = 0x7fffffffu;
+SH_HD uint32_t entry_vlen(uint32_t v) { return v & kVlenMask; }
 
 // Header written in front of every value in the log; a GET returns header+value.
 struct alignas(16) ItemHeader {
@@ -64,6 +71,27 @@ SH_HD bool entry_live(uint64_t loc, uint32_t expire, uint64_t head, uint64_t cap
                       uint32_t now) {
   return loc != 0 && head <= (loc - 1) + capacity && (expire == 0 || expire > now);
 }
+
+// CLOCK eviction geometry shared by the HBM and host engines, so both make identical
+// decisions: the reinsertion budget per SET batch (`req` bytes, 0 = auto: 1/32 of the
+// log clamped to [1 MiB, 1 GiB] and at most 1/4 of it), the hand's window (ring entries
+// examined per SET batch of n rows) and the item-start ring size (power of two).
+inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
+  if (req) return req / 16 * 16;
+  uint64_t r = log_bytes / 32;
+  r = r < (1ull << 20) ? (1ull << 20) : (r > (1ull << 30) ? (1ull << 30) : r);
+  return (r < log_bytes / 4 ? r : log_bytes / 4) / 16 * 16;
+}
+inline int64_t hand_window(int64_t n) {
+  const int64_t w = 4 * n + 256;
+  return w < (1 << 20) ? w : (1 << 20);
+}
+inline uint64_t ring_entries(uint64_t nbuckets) {
+  uint64_t r = 4096;
+  while (r < 2 * nbuckets * kEntriesPerBucket) r <<= 1;
+  return r;
+}
+constexpr uint64_t kRingSkip = ~0ull;  // item-start ring: a SET row that stored nothing
 
 // Counters kept on the device (and mirrored by the host engine). Under GET coalescing
 // get_ops / get_hits / get_bytes count distinct keys probed; the duplicate rows a

@@ -205,7 +205,7 @@ void McReactor::handle(McClient* c, const mc::Frame& f) {
           if (hit && v.data) {
             std::string ex;
             mc::put32(ex, v.flags);
-            reply(sl, mc::OK, withkey ? key : std::string(), ex, *v.data);
+            reply(sl, mc::OK, withkey ? key : std::string(), ex, v.data.str());
           } else if (!quiet) {
             reply(sl, mc::KEY_ENOENT, withkey ? key : std::string(), "", "Not found");
           }
@@ -254,7 +254,8 @@ void McReactor::handle(McClient* c, const mc::Frame& f) {
             reply(sl, mc::NOT_STORED, "", "", "Not stored.");
             return;
           }
-          auto nv = std::make_shared<const std::string>(app ? *v.data + *val : *val + *v.data);
+          auto nv = std::make_shared<const std::string>(app ? v.data.str() + *val
+                                                            : *val + v.data.str());
           be->set(key, d, nv, v.flags, 0);
           reply(sl, mc::OK, "", "", "");
         });
@@ -282,7 +283,8 @@ void McReactor::handle(McClient* c, const mc::Frame& f) {
             nv = initial;
           } else {
             char* endp = nullptr;
-            const unsigned long long cur = std::strtoull(v.data->c_str(), &endp, 10);
+            const std::string cs = v.data.str();
+            const unsigned long long cur = std::strtoull(cs.c_str(), &endp, 10);
             if (v.data->empty() || (endp && *endp)) {
               reply(sl, mc::DELTA_BADVAL, "", "", "Non-numeric server-side value for incr or decr");
               return;

@@ -452,9 +452,10 @@ void Reactor::on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v) {
 // The last response on a connection announces the close (cached objects carry
 // "Connection: keep-alive" from the fill, Server.py:414-415).
 static Bytes with_connection_close(const Bytes& obj) {
-  const size_t eoh = obj->find("\r\n\r\n");
+  const std::string_view ov = obj.view();
+  const size_t eoh = ov.find("\r\n\r\n");
   if (eoh == std::string::npos) return obj;
-  std::string head = obj->substr(0, eoh + 2);
+  std::string head(ov.substr(0, eoh + 2));
   std::string out;
   out.reserve(obj->size() + 8);
   size_t pos = 0;
@@ -470,7 +471,7 @@ static Bytes with_connection_close(const Bytes& obj) {
     pos = e + 2;
   }
   out += "Connection: close\r\n\r\n";
-  out.append(*obj, eoh + 4, std::string::npos);
+  out.append(ov.substr(eoh + 4));
   return std::make_shared<const std::string>(std::move(out));
 }
 

@@ -10,14 +10,49 @@
 
 #include <sys/uio.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace shellac {
 
-using Bytes = std::shared_ptr<const std::string>;
+// An immutable, reference-counted byte range. It either owns a std::string (responses
+// built on the host) or views a slice of a larger buffer whose owner it keeps alive —
+// the HBM tier hands out hits this way as slices of the pinned buffer the GPU gathered
+// them into, so a cached object reaches writev() without a host copy. Pointer-like
+// (`if (b)`, `b->data()`, `b->size()`) so it stands in for shared_ptr<const string>.
+class ByteRef {
+ public:
+  ByteRef() = default;
+  ByteRef(std::nullptr_t) {}  // NOLINT: implicit, like a null shared_ptr
+  ByteRef(std::shared_ptr<const std::string> s)  // NOLINT: implicit on purpose
+      : p_(s ? s->data() : nullptr), n_(s ? s->size() : 0), hold_(std::move(s)) {}
+  ByteRef(std::shared_ptr<std::string> s)  // NOLINT
+      : ByteRef(std::shared_ptr<const std::string>(std::move(s))) {}
+  ByteRef(std::shared_ptr<const void> owner, const char* p, size_t n)
+      : p_(p), n_(n), hold_(std::move(owner)) {}
+
+  explicit operator bool() const { return hold_ != nullptr; }
+  const ByteRef* operator->() const { return this; }
+  const char* data() const { return p_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  std::string_view view() const { return std::string_view(p_, n_); }
+  std::string str() const { return std::string(p_, n_); }
+  // [off, off + n) of this range, sharing its owner
+  ByteRef sub(size_t off, size_t n) const { return ByteRef(hold_, p_ + off, n); }
+  const std::shared_ptr<const void>& owner() const { return hold_; }
+
+ private:
+  const char* p_ = nullptr;
+  size_t n_ = 0;
+  std::shared_ptr<const void> hold_;
+};
+
+using Bytes = ByteRef;
 
 class StreamBuf {
  public:

@@ -184,25 +184,36 @@ class CacheShard:
     """One cache shard: an HBM arena on ``cuda:i`` or a DRAM arena on ``cpu``.
 
     Args:
-      log_bytes: capacity of the circular value log (FIFO eviction when full).
+      log_bytes: capacity of the circular value log.
       nbuckets: index buckets (power of two); 4 entries each, two-choice hashing.
       max_item: largest storable value (memcached parity default 1 MiB).
+      evict: "clock" (default: objects read since the eviction hand last passed are
+        re-appended instead of overwritten — memcached-LRU-like hit ratios) or "fifo"
+        (plain circular log).
+      reinsert_max: CLOCK reinsertion budget per SET batch in bytes (0 = auto).
     """
 
+    EVICT = {"fifo": 0, "clock": 1}
+
     def __init__(self, log_bytes: int, nbuckets: int, max_item: int = 1 << 20,
-                 device: str | torch.device = "cpu"):
+                 device: str | torch.device = "cpu", evict: str = "clock",
+                 reinsert_max: int = 0):
         self.device = torch.device(device)
         self.log_bytes = int(log_bytes)
         self.nbuckets = int(nbuckets)
         self.max_item = int(max_item)
+        self.evict = evict
+        ev = self.EVICT[evict]
         c = core()
         if self.device.type == "cuda":
             idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
             self.device = torch.device("cuda", idx)
-            self._impl = c.HbmCache(self.log_bytes, self.nbuckets, self.max_item, idx)
+            self._impl = c.HbmCache(self.log_bytes, self.nbuckets, self.max_item, idx, ev,
+                                    int(reinsert_max))
             self.is_gpu = True
         elif self.device.type == "cpu":
-            self._impl = c.HostCache(self.log_bytes, self.nbuckets, self.max_item)
+            self._impl = c.HostCache(self.log_bytes, self.nbuckets, self.max_item, ev,
+                                     int(reinsert_max))
             self.is_gpu = False
         else:
             raise ValueError(f"unsupported device {self.device}")
@@ -300,12 +311,12 @@ class CacheShard:
 
     def small_get(self, keys: torch.Tensor, out_cap: int = 16 << 20,
                   now: Optional[int] = None, done_slot: int = -1):
-        """GPU, n <= 2048: lookup + scan + gather in one kernel (the proxy's micro-batch
-        path). Returns (out bytes, off[n+1]); off[n] > out_cap means nothing was copied.
-        ``done_slot`` >= 0: the kernel's last workgroup publishes off[n] into that host
-        slot once every output byte is visible; ``host_total(done_slot)`` then replaces
-        a stream synchronisation."""
-        assert self.is_gpu and keys.shape[0] <= 2048
+        """GPU edge GET (the proxy's micro-batch path): probe + scan + gather in one
+        kernel, each key probed once. Returns (out bytes, off[n+1]); off[n] > out_cap
+        means nothing was copied. ``done_slot`` >= 0: the kernel's last workgroup
+        publishes off[n] into that host slot once every output byte is visible;
+        ``host_total(done_slot)`` then replaces a stream synchronisation."""
+        assert self.is_gpu and keys.shape[0] <= int(core().SMALL_GET_MAX)
         self._check(keys, "keys")
         n = keys.shape[0]
         out = torch.empty(max(int(out_cap), 16), dtype=torch.uint8, device=self.device)
@@ -342,10 +353,17 @@ class CacheShard:
 
     # -- SET ----------------------------------------------------------------------
     @staticmethod
-    def set_bound(n: int, payload_bytes: int) -> int:
-        """Upper bound of the log bytes a SET of ``n`` values from a ``payload_bytes``
-        buffer appends (32-B header + value, 16-B aligned, per item)."""
+    def payload_bound(n: int, payload_bytes: int) -> int:
+        """Upper bound of the log bytes ``n`` values from a ``payload_bytes`` buffer
+        occupy (32-B header + value, 16-B aligned, per item)."""
         return 48 * int(n) + int(payload_bytes)
+
+    def set_bound(self, n: int, payload_bytes: int) -> int:
+        """Upper bound of the log bytes a SET of ``n`` values from a ``payload_bytes``
+        buffer appends — its own records plus, under CLOCK, the reinsertions of
+        referenced objects it triggers (the ``reserve_bytes`` a lookup that a SET may
+        overtake needs)."""
+        return self.payload_bound(n, payload_bytes) + int(self._impl.reinsert_max)
 
     def store(self, keys: torch.Tensor, values: torch.Tensor, val_off: torch.Tensor,
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
@@ -368,7 +386,8 @@ class CacheShard:
         fp = 0 if flags is None else flags.data_ptr()
         ep = 0 if expire is None else expire.data_ptr()
         if self.is_gpu:
-            bound = self.set_bound(n, values.numel()) if bytes_bound is None else int(bytes_bound)
+            bound = (self.payload_bound(n, values.numel()) if bytes_bound is None
+                     else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(),
                              index_after.cuda_event if index_after is not None else 0)

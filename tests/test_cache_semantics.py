@@ -85,7 +85,7 @@ def check_reserve_lookup_survives_queued_set(dev):
     plain = s.lookup(d).hits().cpu()
     newk = [f"/n/{i}".encode() for i in range(12)]
     v, vo, vl = pack_values([b"x" * 1000] * 12, s.device)
-    bound = CacheShard.set_bound(12, v.numel())
+    bound = s.set_bound(12, v.numel())
     lk = s.lookup(d, reserve_bytes=bound)
     res_hits = lk.hits().cpu()
     # the reserved lookup drops exactly the oldest objects (a prefix of the FIFO)
