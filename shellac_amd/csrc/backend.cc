@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 
+#include "keyed.h"
 #include "mcproto.h"
 
 namespace shellac {
@@ -45,6 +46,20 @@ int DigestRing::owner(const Digest& d) const {
   return it == pts_.end() ? pts_.front().second : it->second;
 }
 
+int DigestRing::owner(const Digest& d, uint64_t alive) const {
+  if (pts_.empty() || !alive) return -1;
+  const uint32_t p = ring_position(d);
+  size_t i = std::lower_bound(pts_.begin(), pts_.end(), p,
+                              [](const std::pair<uint32_t, int>& a, uint32_t v) {
+                                return a.first < v;
+                              }) - pts_.begin();
+  for (size_t k = 0; k < pts_.size(); ++k) {  // next point of a live shard (wrapping)
+    const int o = pts_[(i + k) % pts_.size()].second;
+    if ((alive >> o) & 1) return o;
+  }
+  return -1;
+}
+
 // =====================================================================================
 // DRAM
 // =====================================================================================
@@ -54,30 +69,39 @@ DramBackend::DramBackend(uint64_t bytes, uint32_t max_item, int stripes) : epoch
   // ~1 KiB average objects at <= 50% slot load
   uint64_t nb = 2;
   while (nb * 4 * 512 < per) nb *= 2;
-  const uint32_t mi = (uint32_t)std::min<uint64_t>(max_item, per / 4);
+  // values carry their key (keyed.h): room for a URL on top of max_item
+  const uint32_t mi = (uint32_t)std::min<uint64_t>((uint64_t)max_item + 4096, per / 4);
   for (int i = 0; i < stripes; ++i) shards_.emplace_back(new HostCache(per, nb, mi));
 }
 
 uint32_t DramBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
-void DramBackend::get(const std::string&, const Digest& d, Executor*, GetCallback done) {
-  std::vector<uint8_t> v;
+// Values are stored keyed ([klen | key | payload], keyed.h): a hit whose stored key is
+// not the requested one (a digest collision) is a miss.
+void DramBackend::get(const std::string& key, const Digest& d, Executor*, GetCallback done) {
+  auto v = std::make_shared<std::string>();
   uint32_t flags = 0, expire = 0;
   const uint32_t t = now();
-  if (shard(d).get_one(d, &v, &flags, t, &expire)) {
-    done(true, CacheValue{std::make_shared<const std::string>(v.begin(), v.end()), flags,
-                          expire ? (int64_t)expire - t : 0});
-  } else {
-    done(false, CacheValue{});
+  size_t po = 0;
+  if (shard(d).get_one(d, v.get(), &flags, t, &expire)) {
+    if (keyed_match(v->data(), v->size(), key, &po)) {
+      Bytes b(std::shared_ptr<const std::string>(std::move(v)));
+      done(true, CacheValue{b.sub(po, b.size() - po), flags, expire ? (int64_t)expire - t : 0});
+      return;
+    }
+    key_mismatch_.fetch_add(1, std::memory_order_relaxed);
   }
+  done(false, CacheValue{});
 }
 
-void DramBackend::set(const std::string&, const Digest& d, Bytes value, uint32_t flags,
+void DramBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
                       uint32_t ttl_s) {
-  if (!value) return;
+  if (!value || key.size() > kMaxKeyedKey) return;
   const uint32_t n = now();
-  shard(d).set_one(d, reinterpret_cast<const uint8_t*>(value->data()), (uint32_t)value->size(),
-                   flags, ttl_s ? n + ttl_s : 0, n);
+  std::string kv(keyed_size(key.size(), value->size()), '\0');
+  write_keyed(reinterpret_cast<uint8_t*>(&kv[0]), key, value->data(), value->size());
+  shard(d).set_one(d, reinterpret_cast<const uint8_t*>(kv.data()), (uint32_t)kv.size(), flags,
+                   ttl_s ? n + ttl_s : 0, n);
 }
 
 void DramBackend::del(const std::string&, const Digest& d, Executor*, DelCallback done) {
@@ -96,13 +120,16 @@ void DramBackend::stats(StatList* out) {
     const CacheCounters c = s->counters();
     t.get_ops += c.get_ops; t.get_hits += c.get_hits; t.set_ops += c.set_ops;
     t.set_bytes += c.set_bytes; t.set_evicted += c.set_evicted; t.del_ops += c.del_ops;
+    t.reinserted += c.reinserted;
   }
   out->emplace_back("cache_get_ops", t.get_ops);
   out->emplace_back("cache_get_hits", t.get_hits);
   out->emplace_back("cache_set_ops", t.set_ops);
   out->emplace_back("cache_set_bytes", t.set_bytes);
   out->emplace_back("cache_evicted", t.set_evicted);
+  out->emplace_back("cache_reinserted", t.reinserted);
   out->emplace_back("cache_shards", shards_.size());
+  out->emplace_back("cache_key_mismatch", key_mismatch_.load());
 }
 
 // =====================================================================================
@@ -468,15 +495,17 @@ FaultSpec parse_fault_spec(const std::string& spec) {
     else if (k == "set_drop") f.set_drop = std::stod(v);
     else if (k == "delay_us") f.delay_us = (uint32_t)std::stoul(v);
     else if (k == "down") f.down = v.empty() || v == "1" || v == "true";
-    else throw Error("unknown fault '" + k + "' (get_miss, set_drop, delay_us, down)");
+    else if (k == "gpu_down") f.gpu_down = std::stoi(v);
+    else throw Error("unknown fault '" + k + "' (get_miss, set_drop, delay_us, down, gpu_down)");
   }
   return f;
 }
 
 FaultBackend::FaultBackend(std::shared_ptr<CacheBackend> inner, const FaultSpec& spec,
                            uint64_t seed)
-    : inner_(std::move(inner)), spec_(spec), rng_(seed * 0x9E3779B97F4A7C15ull + 1) {
+    : inner_(std::move(inner)), spec_(FaultSpec{}), rng_(seed * 0x9E3779B97F4A7C15ull + 1) {
   th_ = std::thread([this] { timer_loop(); });
+  set_spec(spec);
 }
 
 FaultBackend::~FaultBackend() {
@@ -489,8 +518,27 @@ FaultBackend::~FaultBackend() {
 }
 
 void FaultBackend::set_spec(const FaultSpec& spec) {
-  std::lock_guard<std::mutex> lk(mu_);
-  spec_ = spec;
+  int old_gpu;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    old_gpu = spec_.gpu_down;
+    spec_ = spec;
+  }
+  // gpu_down=K: the GPU tier's shard K is ejected as if it had failed (and restored,
+  // flushed, when the drill is lifted)
+  if (old_gpu != spec.gpu_down) {
+    if (old_gpu >= 0) inner_->inject_shard_down(old_gpu, false);
+    if (spec.gpu_down >= 0 && !inner_->inject_shard_down(spec.gpu_down, true))
+      throw Error("gpu_down: the cache tier has no GPU shard " + std::to_string(spec.gpu_down));
+  }
+}
+
+bool FaultBackend::inject_shard_down(int shard, bool down) {
+  return inner_->inject_shard_down(shard, down);
+}
+
+bool TieredBackend::inject_shard_down(int shard, bool down) {
+  return l2_->inject_shard_down(shard, down);
 }
 
 FaultSpec FaultBackend::spec() const {

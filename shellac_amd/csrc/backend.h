@@ -43,6 +43,11 @@ class Executor {
  public:
   virtual ~Executor() = default;
   virtual void post(std::function<void()> fn) = 0;  // run fn on the executor's thread
+  // Several completions at once (one lock and one wake-up for a whole GPU batch).
+  virtual void post_batch(std::vector<std::function<void()>>& fns) {
+    for (auto& f : fns) post(std::move(f));
+    fns.clear();
+  }
 };
 
 struct CacheValue {
@@ -65,6 +70,13 @@ class CacheBackend {
   virtual void flush() = 0;
   virtual std::string name() const = 0;
   virtual void stats(StatList* out) = 0;
+  // Fault injection / drills: take GPU shard `shard` of this tier out of service (or
+  // bring it back). Returns false if the tier has no such shard.
+  virtual bool inject_shard_down(int shard, bool down) {
+    (void)shard;
+    (void)down;
+    return false;
+  }
 };
 
 // 32-bit-point ring over digests, identical to shellac_amd.parallel.ring.ShardRing.
@@ -72,6 +84,9 @@ class DigestRing {
  public:
   explicit DigestRing(int nshards, int points_per_shard = 160);
   int owner(const Digest& d) const;
+  // Owner among the shards whose bit is set in `alive` (ketama ejection: a dead shard's
+  // keys move to the next live point); -1 if none is alive.
+  int owner(const Digest& d, uint64_t alive) const;
 
  private:
   std::vector<std::pair<uint32_t, int>> pts_;
@@ -93,6 +108,7 @@ class DramBackend : public CacheBackend {
   HostCache& shard(const Digest& d) { return *shards_[(d.hi >> 17) % shards_.size()]; }
   std::vector<std::unique_ptr<HostCache>> shards_;
   double epoch_;
+  std::atomic<uint64_t> key_mismatch_{0};
 };
 
 struct HbmBackendConfig {
@@ -100,13 +116,25 @@ struct HbmBackendConfig {
   uint64_t log_bytes_per_gpu = 8ull << 30;
   uint64_t nbuckets_per_gpu = 1ull << 22;
   uint32_t max_item = 1u << 20;
-  int batch_us = 0;         // optional linger for batch-mates (0: natural batching)
-  int max_batch = 65536;    // flush early when this many requests are queued
+  int batch_us = 0;           // optional linger for batch-mates (0: natural batching)
+  int max_batch = 65536;      // requests per batch at most
   int sweep_interval_s = 10;  // idle-time expiry sweep of every shard (0 = off)
-  int spin_us = 50;           // batcher polls the queue this long before blocking
+  int spin_us = 50;           // a batcher polls its queue this long before blocking
   bool presence_filter = true;  // answer GETs of never-stored digests on the host
+  int depth = 3;              // batches in flight per GPU (pinned staging per batch)
+  int evict = 1;              // 0 FIFO, 1 CLOCK (ShardConfig::evict)
+  int retry_s = 2;            // an ejected GPU shard is retried after this long
+  int batch_timeout_ms = 2000;  // a batch unfinished this long ejects its GPU
+  bool flush_on_restore = true;  // a shard back from ejection may hold stale objects
 };
 
+// One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are
+// routed to their shard's queue by the digest ring, and the batcher keeps up to `depth`
+// batches in flight on its stream — GETs as one edge-GET launch that writes hits
+// straight into a pinned arena (handed to the reactors as zero-copy ByteRef slices),
+// SETs/DELETEs from pinned staging — reaping them in order as their completion slots /
+// events fire. A batch that errors or stalls ejects its GPU from the ring (its keys
+// fall through to the origin) until retry_s passes and the GPU proves healthy.
 class HbmBackend : public CacheBackend {
  public:
   explicit HbmBackend(const HbmBackendConfig& cfg);
@@ -118,15 +146,12 @@ class HbmBackend : public CacheBackend {
   void flush() override;
   std::string name() const override { return "hbm"; }
   void stats(StatList* out) override;
+  bool inject_shard_down(int shard, bool down) override;
 
- private:
-  const bool set_graphs_ = [] {
-    const char* e = std::getenv("SHELLAC_SET_GRAPH");
-    return e && e[0] == '1';
-  }();
   struct Req {
     int kind;  // 0 get, 1 set, 2 del
     Digest d;
+    std::string key;
     Bytes value;
     uint32_t flags = 0, ttl = 0;
     Executor* ex = nullptr;
@@ -134,38 +159,18 @@ class HbmBackend : public CacheBackend {
     DelCallback dcb;
   };
   struct Dev;
-  void loop();
-  void run_batch(std::vector<Req>& batch);
+
+ private:
+  int route(const Digest& d) const;
+  void enqueue(int dev, Req r);
   uint32_t now() const;
 
   HbmBackendConfig cfg_;
   DigestRing ring_;
   std::vector<std::unique_ptr<Dev>> devs_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::vector<Req> q_;
-  // q_.size() mirror the batcher polls (without the mutex) for a short while after each
-  // batch before it blocks on cv_: a request arriving then skips a futex wake-up
-  std::atomic<size_t> qn_{0};
-  std::atomic<bool> spinning_{false};
-  bool stop_ = false;
-  bool flush_req_ = false;
-  // Presence filter (presence_filter.h). SETs add their digest under mu_ to filt_ and,
-  // while a rebuild is in progress, to filt_next_; the batcher installs filt_next_ in the
-  // same critical section that takes a batch, commits that batch, then fills filt_next_
-  // from every shard's live keys and swaps it in (so no stored digest is ever missing).
-  std::shared_ptr<PresenceFilter> filt_, filt_next_;
-  uint64_t filt_bits_ = 0, filt_rebuild_at_ = 0;
-  bool filt_want_rebuild_ = false;
-  std::atomic<uint64_t> filt_skips_{0}, filt_rebuilds_{0};
-  void finish_filter_rebuild();
-  std::thread th_;
+  std::atomic<uint64_t> up_mask_{0};  // bit i: shard i serves requests
   double epoch_;
-  std::atomic<uint64_t> batches_{0}, batched_reqs_{0}, max_batch_seen_{0};
-  std::atomic<uint64_t> batch_ns_{0};
-  std::atomic<uint64_t> sweeps_{0}, live_objects_{0}, live_bytes_{0};
-  std::atomic<uint64_t> coalesced_gets_{0};  // GETs that shared a batch-mate's GPU row
-  void sweep_all();
+  std::atomic<uint64_t> no_shard_misses_{0};
 };
 
 // Two-level cache: a small host-DRAM L1 in front of a big L2 (HBM shards or
@@ -182,6 +187,7 @@ class TieredBackend : public CacheBackend {
   void flush() override;
   std::string name() const override { return l1_->name() + "+" + l2_->name(); }
   void stats(StatList* out) override;
+  bool inject_shard_down(int shard, bool down) override;
 
  private:
   std::shared_ptr<CacheBackend> l1_, l2_;
@@ -198,6 +204,7 @@ struct FaultSpec {
   double set_drop = 0;    // P(SET silently dropped)
   uint32_t delay_us = 0;  // extra latency before every GET/DEL is answered
   bool down = false;      // tier unreachable
+  int gpu_down = -1;      // GPU shard K of the tier ejected (HbmBackend ring ejection)
 };
 FaultSpec parse_fault_spec(const std::string& spec);  // "get_miss=0.1,set_drop=1,delay_us=500,down"
 
@@ -212,6 +219,7 @@ class FaultBackend : public CacheBackend {
   void flush() override { inner_->flush(); }
   std::string name() const override { return "fault(" + inner_->name() + ")"; }
   void stats(StatList* out) override;
+  bool inject_shard_down(int shard, bool down) override;
   void set_spec(const FaultSpec& spec);
   FaultSpec spec() const;
 

@@ -1,10 +1,27 @@
-// HbmBackend: the HTTP proxy's batched HIP pipeline over one HBM shard per local GPU
-// (split from backend.cc so the host-only backends build without ROCm).
+// HbmBackend: the HTTP proxy's (and the memcached node's) cache tier over one HBM shard
+// per local MI355X (split from backend.cc so the host-only backends build without ROCm).
+//
+// Replaces the reference's blocking memcached round trip inside the reactor
+// (src/python/shellac/server/Server.py:335 get, :432 set). Per GPU:
+//
+//   reactors ──get/set/del──▶ queue ──▶ batcher thread ──▶ HIP stream
+//                                          │  flight k:   edge GET (keys + offsets in
+//                                          │              mapped memory, values into a
+//                                          │              pinned arena), SET store,
+//                                          │              DELETE, event
+//                                          │  up to `depth` flights in flight
+//                                          ◀─ reap in order: completion slot / event
+//   reactors ◀──post_batch(callbacks)──────┘  hits = ByteRef slices of the arena
+//
+// A hit never touches a host copy: the GPU writes [ItemHeader | u16 klen | key | payload]
+// into pinned memory, the batcher checks the key bytes and hands out a slice of the
+// payload that keeps the arena alive until the last client write completes.
 #include <chrono>
 #include <cstdio>
 
 #include "backend.h"
 #include "hbm_cache.h"
+#include "keyed.h"
 #include "trace.h"
 
 namespace shellac {
@@ -16,9 +33,6 @@ double wall_s() {
 }
 }  // namespace
 
-// =====================================================================================
-// HBM
-// =====================================================================================
 #define HB_OK(expr)                                                                   \
   do {                                                                                \
     hipError_t _e = (expr);                                                           \
@@ -26,589 +40,818 @@ double wall_s() {
                                       " at " #expr);                                  \
   } while (0)
 
+namespace {
+
+// Mapped pinned buffer (host pointer + its device view) that grows on demand.
+struct Mapped {
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;
+  size_t cap = 0;
+  void ensure(size_t bytes) {
+    if (bytes <= cap) return;
+    size_t c = cap ? cap : 4096;
+    while (c < bytes) c *= 2;
+    release();
+    HB_OK(hipHostMalloc(reinterpret_cast<void**>(&h), c, hipHostMallocMapped));
+    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
+    cap = c;
+  }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    h = d = nullptr;
+    cap = 0;
+  }
+  template <typename T>
+  T* host() const { return reinterpret_cast<T*>(h); }
+  template <typename T>
+  T* dev() const { return reinterpret_cast<T*>(d); }
+};
+
+// Pinned response arenas. A GET batch gathers into one; its hits are ByteRef slices that
+// own a reference, so the arena returns to the pool (not to the allocator) when the last
+// response built from it has been written to its client.
+class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
+ public:
+  struct Arena {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+  };
+  explicit ArenaPool(int device) : device_(device) {}
+  ~ArenaPool() {
+    for (auto& a : free_) (void)hipHostFree(a.h);
+  }
+  std::shared_ptr<Arena> take(size_t min_cap) {
+    Arena a{};
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].cap >= min_cap) {
+          a = free_[i];
+          free_.erase(free_.begin() + (long)i);
+          break;
+        }
+    }
+    if (!a.h) {
+      size_t c = 1u << 20;
+      while (c < min_cap) c *= 2;
+      HB_OK(hipSetDevice(device_));
+      HB_OK(hipHostMalloc(reinterpret_cast<void**>(&a.h), c, hipHostMallocMapped));
+      HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.d), a.h, 0));
+      a.cap = c;
+      allocated_.fetch_add(c, std::memory_order_relaxed);
+    }
+    auto pool = shared_from_this();
+    return std::shared_ptr<Arena>(new Arena(a), [pool](Arena* p) {
+      pool->give_back(*p);
+      delete p;
+    });
+  }
+  uint64_t allocated() const { return allocated_.load(std::memory_order_relaxed); }
+
+ private:
+  void give_back(const Arena& a) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (free_.size() < 16) {
+      free_.push_back(a);
+      return;
+    }
+    (void)hipHostFree(a.h);
+    allocated_.fetch_sub(a.cap, std::memory_order_relaxed);
+  }
+  int device_;
+  std::mutex mu_;
+  std::vector<Arena> free_;
+  std::atomic<uint64_t> allocated_{0};
+};
+
+}  // namespace
+
+// One batch in flight on a GPU.
+struct Flight {
+  std::vector<HbmBackend::Req> reqs;
+  std::vector<uint32_t> gets, sets, dels;  // request indices by kind
+  std::vector<uint32_t> urow;              // GET request -> GPU row (host coalescing)
+  size_t rows = 0;                         // distinct GET digests
+  Mapped keys, offs, set_keys, set_vals, set_voff, set_meta, del_keys, del_found;
+  std::shared_ptr<ArenaPool::Arena> arena;
+  hipEvent_t ev = nullptr;
+  int slot = -1;
+  bool active = false, got = false;
+  uint32_t tnow = 0;
+  double t0 = 0;
+};
+
 struct HbmBackend::Dev {
-  int device = 0;
+  HbmBackend* be = nullptr;
+  int index = 0, device = 0;
   std::unique_ptr<HbmCache> cache;
   hipStream_t stream = nullptr;
-  size_t n_cap = 0, out_cap = 0, vals_cap = 0;
-  Digest *d_keys = nullptr, *h_keys = nullptr;
-  Digest* h_keys_dev = nullptr;    // device view of the mapped h_keys
-  uint64_t* h_off_dev = nullptr;   // device view of the mapped h_off
-  uint64_t *d_loc = nullptr, *d_size = nullptr, *d_off = nullptr, *h_off = nullptr;
-  uint8_t* h_out = nullptr;
-  uint8_t* h_out_dev = nullptr;  // device view of the pinned h_out (zero-copy gather target)
-  uint8_t *d_vals = nullptr, *h_vals = nullptr;
-  uint64_t *d_voff = nullptr, *h_voff = nullptr;
-  uint32_t *d_meta = nullptr, *h_meta = nullptr;  // [vlen | flags | expire] x n
-  uint8_t *d_found = nullptr, *h_found = nullptr;
-  // zero-copy SET staging for graph-replayed micro-batches (mapped pinned memory the
-  // kernels read directly): keys, value bytes, value offsets, [vlen | flags | expire]
-  static constexpr int kSetClasses = 3;
-  static constexpr int64_t kSetClass[kSetClasses] = {64, 512, 4096};
-  Digest *hs_keys = nullptr, *hs_keys_dev = nullptr;
-  uint8_t *hs_vals = nullptr, *hs_vals_dev = nullptr;
-  size_t hs_vals_cap = 0;
-  uint64_t *hs_voff = nullptr, *hs_voff_dev = nullptr;
-  uint32_t *hs_meta = nullptr, *hs_meta_dev = nullptr;
-  HbmCache::StoreGraph set_graph[kSetClasses];
-  // host-side GET coalescing scratch (batcher thread only)
+  std::shared_ptr<ArenaPool> pool;
+  std::vector<std::unique_ptr<Flight>> flights;
+  size_t head = 0, inflight = 0;  // oldest flight, flights launched and not yet freed
+  // queue (reactor threads -> batcher)
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Req> q;
+  std::atomic<size_t> qn{0};
+  std::atomic<bool> spinning{false};
+  bool stop = false, flush_req = false;
+  std::atomic<bool> ctl_pending{false};  // flush / filter rebuild requested (no requests needed)
+  std::thread th;
+  // health
+  std::atomic<bool> forced_down{false};
+  bool failed = false;
+  double retry_at = 0;
+  // presence filter (this shard's digests)
+  std::shared_ptr<PresenceFilter> filt, filt_next;
+  uint64_t filt_bits = 0, filt_rebuild_at = 0;
+  bool filt_want_rebuild = false;
+  // co-table for host GET coalescing (batcher thread only)
   std::vector<int32_t> co_tab;
-  std::vector<uint32_t> urow;
-  std::vector<CacheValue> uval;
-  std::vector<uint8_t> uhit;
+  double avg_row_bytes = 4096;
+  // stats
+  std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
+      filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
+      key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, dropped{0};
 
-  void set_device() { HB_OK(hipSetDevice(device)); }
-
-  template <typename T>
-  static void map_alloc(T** host, T** dev, size_t bytes) {
-    HB_OK(hipHostMalloc(reinterpret_cast<void**>(host), bytes, hipHostMallocMapped));
-    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0));
-  }
-  void ensure_set_staging(size_t val_bytes) {
-    const int64_t cmax = kSetClass[kSetClasses - 1];
-    if (!hs_keys) {
-      map_alloc(&hs_keys, &hs_keys_dev, cmax * sizeof(Digest));
-      map_alloc(&hs_voff, &hs_voff_dev, cmax * sizeof(uint64_t));
-      map_alloc(&hs_meta, &hs_meta_dev, 3 * cmax * sizeof(uint32_t));
-      cache->reserve(cmax);
-    }
-    if (val_bytes > hs_vals_cap) {  // graphs holding the old pointer re-capture
-      size_t cap = hs_vals_cap ? hs_vals_cap : (4u << 20);
-      while (cap < val_bytes) cap *= 2;
-      HB_OK(hipStreamSynchronize(stream));
-      (void)hipHostFree(hs_vals);
-      map_alloc(&hs_vals, &hs_vals_dev, cap);
-      hs_vals_cap = cap;
-    }
-  }
-
-  void ensure_n(size_t n) {
-    if (n <= n_cap) return;
-    size_t cap = n_cap ? n_cap : 1024;
-    while (cap < n) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_keys); (void)hipHostFree(h_keys); (void)hipFree(d_loc); (void)hipFree(d_size);
-    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
-    (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
-    HB_OK(hipMalloc(&d_keys, cap * sizeof(Digest)));
-    HB_OK(hipHostMalloc(&h_keys, cap * sizeof(Digest), hipHostMallocMapped));
-    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_keys_dev), h_keys, 0));
-    HB_OK(hipMalloc(&d_loc, cap * 8));
-    HB_OK(hipMalloc(&d_size, (cap + 1) * 8));
-    HB_OK(hipMalloc(&d_off, (cap + 1) * 8));
-    HB_OK(hipHostMalloc(&h_off, (cap + 1) * 8, hipHostMallocMapped));
-    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_off_dev), h_off, 0));
-    HB_OK(hipMalloc(&d_voff, cap * 8));
-    HB_OK(hipHostMalloc(&h_voff, cap * 8, hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_meta, cap * 12));
-    HB_OK(hipHostMalloc(&h_meta, cap * 12, hipHostMallocDefault));
-    HB_OK(hipMalloc(&d_found, cap));
-    HB_OK(hipHostMalloc(&h_found, cap, hipHostMallocDefault));
-    n_cap = cap;
-    cache->reserve((int64_t)cap);
-  }
-  void ensure_out(size_t bytes) {
-    if (bytes <= out_cap) return;
-    size_t cap = out_cap ? out_cap : (16u << 20);
-    while (cap < bytes) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipHostFree(h_out);
-    HB_OK(hipHostMalloc(&h_out, cap, hipHostMallocMapped));
-    HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_out_dev), h_out, 0));
-    out_cap = cap;
-  }
-  void ensure_vals(size_t bytes) {
-    if (bytes <= vals_cap) return;
-    size_t cap = vals_cap ? vals_cap : (1u << 20);
-    while (cap < bytes) cap *= 2;
-    HB_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d_vals); (void)hipHostFree(h_vals);
-    HB_OK(hipMalloc(&d_vals, cap));
-    HB_OK(hipHostMalloc(&h_vals, cap, hipHostMallocDefault));
-    vals_cap = cap;
+  void loop();
+  bool take_batch(std::vector<Req>* out, bool* do_flush, bool* rebuilding);
+  void launch(Flight& f);
+  bool try_reap(Flight& f, bool block);
+  void deliver_gets(Flight& f);
+  void deliver_dels(Flight& f);
+  void fail_flight(Flight& f);
+  void fail_requests(std::vector<Req>& reqs);
+  void eject(const char* why);
+  void maybe_restore();
+  void sweep();
+  void finish_filter_rebuild();
+  bool up() const { return (be->up_mask_.load(std::memory_order_acquire) >> index) & 1; }
+  void set_up(bool on) {
+    if (on) be->up_mask_.fetch_or(1ull << index);
+    else be->up_mask_.fetch_and(~(1ull << index));
   }
   ~Dev() {
     (void)hipSetDevice(device);
-    (void)hipStreamSynchronize(stream);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& f : flights) {
+      for (Mapped* m : {&f->keys, &f->offs, &f->set_keys, &f->set_vals, &f->set_voff,
+                        &f->set_meta, &f->del_keys, &f->del_found})
+        m->release();
+      f->arena.reset();
+      if (f->ev) (void)hipEventDestroy(f->ev);
+    }
     cache.reset();
-    (void)hipFree(d_keys); (void)hipHostFree(h_keys); (void)hipFree(d_loc); (void)hipFree(d_size);
-    (void)hipFree(d_off); (void)hipHostFree(h_off); (void)hipHostFree(h_out);
-    (void)hipFree(d_vals); (void)hipHostFree(h_vals); (void)hipFree(d_voff); (void)hipHostFree(h_voff);
-    (void)hipFree(d_meta); (void)hipHostFree(h_meta); (void)hipFree(d_found); (void)hipHostFree(h_found);
-    for (auto& g : set_graph) HbmCache::destroy_graph(&g);
-    (void)hipHostFree(hs_keys); (void)hipHostFree(hs_vals); (void)hipHostFree(hs_voff);
-    (void)hipHostFree(hs_meta);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
+// Host slots the edge GET signals completion through: one per flight.
+constexpr int kFlightSlot0 = 8;
+
 HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     : cfg_(cfg), ring_((int)cfg.devices.size()), epoch_(wall_s()) {
-  SH_CHECK(!cfg_.devices.empty(), "HbmBackend needs at least one device");
-  for (int dev : cfg_.devices) {
+  SH_CHECK(!cfg_.devices.empty() && cfg_.devices.size() <= 64, "HbmBackend needs 1..64 devices");
+  SH_CHECK(cfg_.depth >= 1 && kFlightSlot0 + cfg_.depth <= HbmCache::kHeadSlot,
+           "pipeline depth out of range");
+  for (size_t i = 0; i < cfg_.devices.size(); ++i) {
     auto d = std::make_unique<Dev>();
-    d->device = dev;
-    d->set_device();
+    d->be = this;
+    d->index = (int)i;
+    d->device = cfg_.devices[i];
+    HB_OK(hipSetDevice(d->device));
     ShardConfig sc;
     sc.log_bytes = cfg_.log_bytes_per_gpu / 16 * 16;
     sc.nbuckets = cfg_.nbuckets_per_gpu;
-    sc.max_item = cfg_.max_item;
-    sc.device = dev;
+    sc.max_item = cfg_.max_item + (uint32_t)keyed_size(kMaxKeyedKey, 0);
+    sc.device = d->device;
+    sc.evict = cfg_.evict;
     d->cache = std::make_unique<HbmCache>(sc);
     HB_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    d->ensure_n(4096);
-    d->ensure_out(4u << 20);
-    d->ensure_vals(4u << 20);
+    d->pool = std::make_shared<ArenaPool>(d->device);
+    for (int k = 0; k < cfg_.depth; ++k) {
+      auto f = std::make_unique<Flight>();
+      HB_OK(hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
+      f->slot = kFlightSlot0 + k;
+      f->keys.ensure(4096 * sizeof(Digest));
+      f->offs.ensure(4097 * 8);
+      d->flights.push_back(std::move(f));
+    }
+    d->cache->reserve(4096);
+    if (cfg_.presence_filter) {
+      // 16 bits per index slot (capped at 256 MiB): ~2 % false positives when a full
+      // index's worth of digests has been added since the last rebuild
+      const uint64_t slots = cfg_.nbuckets_per_gpu * kEntriesPerBucket;
+      d->filt_bits = std::min<uint64_t>(slots * 16, 1ull << 31);
+      d->filt_rebuild_at = slots;
+      d->filt = std::make_shared<PresenceFilter>(d->filt_bits);
+    }
+    up_mask_.fetch_or(1ull << i);
     devs_.push_back(std::move(d));
   }
-  if (cfg_.presence_filter) {
-    // 16 bits per index slot of every shard (capped at 256 MiB): ~2 % false positives
-    // when a full index's worth of digests has been added since the last rebuild
-    const uint64_t slots = cfg_.nbuckets_per_gpu * kEntriesPerBucket * devs_.size();
-    filt_bits_ = std::min<uint64_t>(slots * 16, 1ull << 31);
-    filt_rebuild_at_ = slots;
-    filt_ = std::make_shared<PresenceFilter>(filt_bits_);
+  for (auto& d : devs_) {
+    Dev* dp = d.get();
+    dp->th = std::thread([dp] { dp->loop(); });
   }
-  th_ = std::thread([this] { loop(); });
 }
 
 HbmBackend::~HbmBackend() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
+  for (auto& d : devs_) {
+    {
+      std::lock_guard<std::mutex> lk(d->mu);
+      d->stop = true;
+    }
+    d->cv.notify_all();
   }
-  cv_.notify_all();
-  if (th_.joinable()) th_.join();
+  for (auto& d : devs_)
+    if (d->th.joinable()) d->th.join();
 }
 
 uint32_t HbmBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
-void HbmBackend::get(const std::string&, const Digest& d, Executor* ex, GetCallback done) {
-  if (cfg_.presence_filter && !std::atomic_load(&filt_)->maybe(d)) {
-    // never stored: a miss without a GPU batch
-    filt_skips_.fetch_add(1, std::memory_order_relaxed);
+int HbmBackend::route(const Digest& d) const {
+  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+  if (devs_.size() == 1) return up & 1 ? 0 : -1;
+  return ring_.owner(d, up);
+}
+
+void HbmBackend::enqueue(int k, Req r) {
+  Dev& dv = *devs_[k];
+  {
+    std::lock_guard<std::mutex> lk(dv.mu);
+    if (r.kind == 1 && cfg_.presence_filter) {
+      dv.filt->add(r.d);
+      if (dv.filt_next) dv.filt_next->add(r.d);
+    }
+    dv.q.push_back(std::move(r));
+    dv.qn.store(dv.q.size(), std::memory_order_release);
+  }
+  if (!dv.spinning.load(std::memory_order_acquire)) dv.cv.notify_one();
+}
+
+void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
+  const int k = route(d);
+  if (k < 0) {  // every shard ejected: the request falls through to the origin
+    no_shard_misses_.fetch_add(1, std::memory_order_relaxed);
+    done(false, CacheValue{});
+    return;
+  }
+  Dev& dv = *devs_[k];
+  if (cfg_.presence_filter && !std::atomic_load(&dv.filt)->maybe(d)) {
+    dv.filt_skips.fetch_add(1, std::memory_order_relaxed);  // never stored: no GPU batch
     done(false, CacheValue{});
     return;
   }
   Req r;
   r.kind = 0;
   r.d = d;
+  r.key = key;
   r.ex = ex;
   r.gcb = std::move(done);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(std::move(r));
-    qn_.store(q_.size(), std::memory_order_release);
-  }
-  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
+  enqueue(k, std::move(r));
 }
 
-void HbmBackend::set(const std::string&, const Digest& d, Bytes value, uint32_t flags,
+void HbmBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
                      uint32_t ttl_s) {
-  if (!value || value->size() > cfg_.max_item) return;
+  if (!value || value->size() > cfg_.max_item || key.size() > kMaxKeyedKey) return;
+  const int k = route(d);
+  if (k < 0) return;
   Req r;
   r.kind = 1;
   r.d = d;
+  r.key = key;
   r.value = std::move(value);
   r.flags = flags;
   r.ttl = ttl_s;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (cfg_.presence_filter) {
-      filt_->add(d);
-      if (filt_next_) filt_next_->add(d);
-    }
-    q_.push_back(std::move(r));
-    qn_.store(q_.size(), std::memory_order_release);
-  }
-  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
+  enqueue(k, std::move(r));
 }
 
-void HbmBackend::del(const std::string&, const Digest& d, Executor* ex, DelCallback done) {
+void HbmBackend::del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) {
+  const int k = route(d);
+  if (k < 0) {
+    if (done) done(false);
+    return;
+  }
   Req r;
   r.kind = 2;
   r.d = d;
+  r.key = key;
   r.ex = ex;
   r.dcb = std::move(done);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(std::move(r));
-    qn_.store(q_.size(), std::memory_order_release);
-  }
-  if (!spinning_.load(std::memory_order_acquire)) cv_.notify_one();
+  enqueue(k, std::move(r));
 }
 
 void HbmBackend::flush() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    flush_req_ = true;
+  for (auto& d : devs_) {
+    {
+      std::lock_guard<std::mutex> lk(d->mu);
+      d->flush_req = true;
+      d->ctl_pending.store(true, std::memory_order_release);
+    }
+    d->cv.notify_one();
   }
-  cv_.notify_one();
 }
 
-void HbmBackend::loop() {
+bool HbmBackend::inject_shard_down(int shard, bool down) {
+  if (shard < 0 || shard >= (int)devs_.size()) return false;
+  Dev& dv = *devs_[shard];
+  dv.forced_down.store(down, std::memory_order_release);
+  if (down) {
+    dv.set_up(false);
+    dv.ejections++;
+  }
+  dv.cv.notify_one();  // the batcher restores the shard (flushing it) when forced_down clears
+  return true;
+}
+
+// ---------------------------------------------------------------------------------
+// batcher
+// ---------------------------------------------------------------------------------
+bool HbmBackend::Dev::take_batch(std::vector<Req>* out, bool* do_flush, bool* rebuilding) {
+  std::unique_lock<std::mutex> lk(mu);
+  ctl_pending.store(false, std::memory_order_relaxed);
+  if (q.empty() && !flush_req && !filt_want_rebuild) return false;
+  const HbmBackendConfig& cfg = be->cfg_;
+  if (cfg.batch_us > 0 && (int)q.size() < cfg.max_batch) {
+    // optional linger: trade latency for bigger batches
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg.batch_us);
+    while (!stop && (int)q.size() < cfg.max_batch &&
+           cv.wait_until(lk, deadline) != std::cv_status::timeout) {
+    }
+  }
+  if (filt_want_rebuild) {
+    // SETs queued from here on add to filt_next; the ones already queued are in this
+    // batch and committed before finish_filter_rebuild() exports the shard's keys
+    filt_next = std::make_shared<PresenceFilter>(filt_bits);
+    filt_want_rebuild = false;
+    *rebuilding = true;
+  }
+  if ((int)q.size() <= cfg.max_batch) {
+    out->swap(q);
+  } else {
+    out->assign(std::make_move_iterator(q.begin()),
+                std::make_move_iterator(q.begin() + cfg.max_batch));
+    q.erase(q.begin(), q.begin() + cfg.max_batch);
+  }
+  qn.store(q.size(), std::memory_order_release);
+  *do_flush = flush_req;
+  flush_req = false;
+  return true;
+}
+
+void HbmBackend::Dev::loop() {
+  const HbmBackendConfig& cfg = be->cfg_;
+  (void)hipSetDevice(device);
   std::vector<Req> batch;
   for (;;) {
-    bool do_flush = false, rebuilding = false;
-    // After a batch, poll the queue for up to spin_us before blocking: under steady
-    // traffic the next request usually arrives within that window, and catching it here
-    // saves the futex wake-up (the producer skips notify while we spin).
-    if (cfg_.spin_us > 0 && qn_.load(std::memory_order_acquire) == 0) {
-      spinning_.store(true, std::memory_order_release);
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.spin_us);
-      while (qn_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
-        __builtin_ia32_pause();
-      spinning_.store(false, std::memory_order_release);
-    }
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      if (cfg_.sweep_interval_s > 0) {
-        // idle: expire TTL'd objects out of every shard's index now and then (the
-        // FIFO log reclaims bytes by itself; expired entries are otherwise only
-        // skipped lazily at lookup)
-        if (!cv_.wait_for(lk, std::chrono::seconds(cfg_.sweep_interval_s),
-                          [&] { return stop_ || !q_.empty() || flush_req_ || filt_want_rebuild_; })) {
-          lk.unlock();
-          try {
-            sweep_all();
-          } catch (const std::exception& e) {
-            std::fprintf(stderr, "[shellac hbm] sweep failed: %s\n", e.what());
-          }
-          continue;
-        }
-      } else {
-        cv_.wait(lk, [&] { return stop_ || !q_.empty() || flush_req_ || filt_want_rebuild_; });
-      }
-      if (stop_ && q_.empty()) return;
-      // Natural batching: whatever queued while the previous batch ran goes now. An
-      // optional linger (batch_us > 0) trades latency for bigger batches.
-      if (cfg_.batch_us > 0) {
-        const auto deadline =
-            std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.batch_us);
-        while (!stop_ && (int)q_.size() < cfg_.max_batch &&
-               cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
-        }
-      }
-      if (filt_want_rebuild_) {
-        // SETs queued from here on add to filt_next_; the ones already queued are in
-        // `batch` and committed before finish_filter_rebuild() exports the shards' keys
-        filt_next_ = std::make_shared<PresenceFilter>(filt_bits_);
-        filt_want_rebuild_ = false;
-        rebuilding = true;
-      }
-      batch.swap(q_);
-      qn_.store(0, std::memory_order_release);
-      do_flush = flush_req_;
-      flush_req_ = false;
-    }
-    const double t0 = wall_s();
-    try {
-      if (do_flush)
-        for (auto& d : devs_) {
-          d->set_device();
-          d->cache->flush(d->stream);
-          HB_OK(hipStreamSynchronize(d->stream));
-        }
-      if (!batch.empty()) run_batch(batch);
-    } catch (const std::exception& e) {
-      std::fprintf(stderr, "[shellac hbm] batch failed: %s\n", e.what());
-      for (auto& r : batch) {
-        if (r.kind == 0 && r.gcb) {
-          auto cb = std::move(r.gcb);
-          r.ex->post([cb]() { cb(false, CacheValue{}); });
-        } else if (r.kind == 2 && r.dcb) {
-          auto cb = std::move(r.dcb);
-          r.ex->post([cb]() { cb(false); });
-        }
-      }
-    }
-    if (rebuilding) {
+    bool worked = false;
+    // 1. reap the oldest flight (in launch order) once its completion signal fired
+    if (inflight) {
+      Flight& f = *flights[head];
+      bool freed = false;
       try {
-        finish_filter_rebuild();
+        freed = try_reap(f, false);
       } catch (const std::exception& e) {
-        std::fprintf(stderr, "[shellac hbm] presence filter rebuild failed: %s\n", e.what());
-        std::lock_guard<std::mutex> lk(mu_);
-        filt_next_.reset();
+        std::fprintf(stderr, "[shellac hbm] gpu %d batch failed: %s\n", device, e.what());
+        fail_flight(f);
+        eject("batch error");
+        freed = true;
       }
-    } else if (cfg_.presence_filter && filt_->adds() >= filt_rebuild_at_) {
-      filt_want_rebuild_ = true;  // read under mu_ by the wait predicate next iteration
-    }
-    const uint64_t n = batch.size();
-    if (n) {
-      batches_++;
-      batched_reqs_ += n;
-      uint64_t prev = max_batch_seen_.load();
-      while (n > prev && !max_batch_seen_.compare_exchange_weak(prev, n)) {
+      if (!freed && f.active && (wall_s() - f.t0) * 1e3 > cfg.batch_timeout_ms) {
+        std::fprintf(stderr, "[shellac hbm] gpu %d batch stalled for %d ms\n", device,
+                     cfg.batch_timeout_ms);
+        fail_flight(f);  // answered as misses; the flight stays busy until the GPU finishes
+        eject("stall");
       }
-      batch_ns_ += (uint64_t)((wall_s() - t0) * 1e9);
+      if (freed) {
+        head = (head + 1) % flights.size();
+        --inflight;
+        worked = true;
+      }
     }
-    batch.clear();
+    // 2. launch the queued requests as a new flight
+    if (inflight < flights.size() &&
+        (qn.load(std::memory_order_acquire) || ctl_pending.load(std::memory_order_acquire))) {
+      bool do_flush = false, rebuilding = false;
+      batch.clear();
+      if (take_batch(&batch, &do_flush, &rebuilding)) {
+        worked = true;
+        if (!up() || failed) {
+          fail_requests(batch);
+        } else if (batch.empty()) {
+          try {
+            if (do_flush) cache->flush(stream);
+          } catch (const std::exception& e) {
+            std::fprintf(stderr, "[shellac hbm] gpu %d flush failed: %s\n", device, e.what());
+          }
+        } else {
+          Flight& f = *flights[(head + inflight) % flights.size()];
+          f.reqs.swap(batch);
+          try {
+            if (do_flush) cache->flush(stream);
+            launch(f);
+            ++inflight;
+          } catch (const std::exception& e) {
+            std::fprintf(stderr, "[shellac hbm] gpu %d launch failed: %s\n", device, e.what());
+            fail_requests(f.reqs);
+            f.reqs.clear();
+            f.active = false;
+            eject("launch error");
+          }
+        }
+        if (rebuilding) {
+          try {
+            finish_filter_rebuild();  // export_keys runs after the batch on the stream
+          } catch (const std::exception& e) {
+            std::fprintf(stderr, "[shellac hbm] presence filter rebuild failed: %s\n", e.what());
+            std::lock_guard<std::mutex> lk(mu);
+            filt_next.reset();
+          }
+        } else if (cfg.presence_filter && filt->adds() >= filt_rebuild_at) {
+          std::lock_guard<std::mutex> lk(mu);
+          filt_want_rebuild = true;
+          ctl_pending.store(true, std::memory_order_release);
+        }
+      }
+    }
+    if (worked) continue;
+    if (inflight) {  // waiting on the GPU: poll (the edge GET signals through host memory)
+      if (up()) __builtin_ia32_pause();
+      else std::this_thread::sleep_for(std::chrono::microseconds(200));  // ejected, draining
+      continue;
+    }
+    // 3. idle
+    if (!up()) maybe_restore();
+    if (cfg.spin_us > 0 && qn.load(std::memory_order_acquire) == 0) {
+      // poll for up to spin_us before blocking: under steady traffic the next request
+      // usually arrives within that window, and catching it saves a futex wake-up
+      spinning.store(true, std::memory_order_release);
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg.spin_us);
+      while (qn.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+        __builtin_ia32_pause();
+      spinning.store(false, std::memory_order_release);
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    if (stop && q.empty()) return;
+    if (!q.empty() || flush_req || filt_want_rebuild) continue;
+    const auto wake = [&] { return stop || !q.empty() || flush_req || filt_want_rebuild; };
+    const int wait_s = !up() ? 1 : cfg.sweep_interval_s;
+    if (wait_s > 0) {
+      if (!cv.wait_for(lk, std::chrono::seconds(wait_s), wake) && up() && cfg.sweep_interval_s > 0) {
+        // idle: expire TTL'd objects out of the index now and then
+        lk.unlock();
+        try {
+          sweep();
+        } catch (const std::exception& e) {
+          std::fprintf(stderr, "[shellac hbm] sweep failed: %s\n", e.what());
+        }
+      }
+    } else {
+      cv.wait(lk, wake);
+    }
   }
 }
 
-// Host slot the small-GET kernel signals completion through (this backend owns its
-// HbmCache instances, so no other user shares the slot).
-constexpr int kDoneSlot = HbmCache::kHostSlots - 1;
-
-void HbmBackend::run_batch(std::vector<Req>& batch) {
-  TraceRange tr("hbm_backend.batch");
-  const size_t nd = devs_.size();
-  const uint32_t tnow = now();
-  std::vector<std::vector<size_t>> gets(nd), sets(nd), dels(nd);
-  for (size_t i = 0; i < batch.size(); ++i) {
-    const int o = nd == 1 ? 0 : ring_.owner(batch[i].d);
-    (batch[i].kind == 0 ? gets : batch[i].kind == 1 ? sets : dels)[o].push_back(i);
-  }
-  // ---- GET: H2D keys, probe + scan, gather straight into pinned host memory (skipped
-  // by the kernel if the batch does not fit), D2H offsets; one sync per device.
-  // Coalesced on the host first: requests for the same digest in one batch (a hot
-  // object under concurrent clients) share one GPU row, one copy over PCIe and one
-  // CacheValue (the bytes are shared, as the DRAM tier shares them).
-  std::vector<size_t> nuniq(nd, 0);
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n0 = gets[k].size();
-    if (!n0) continue;
-    dv.set_device();
-    dv.ensure_n(std::max(n0, std::max(sets[k].size(), dels[k].size())));
-    dv.ensure_out(1);
+void HbmBackend::Dev::launch(Flight& f) {
+  TraceRange tr("hbm_backend.launch");
+  const HbmBackendConfig& cfg = be->cfg_;
+  f.gets.clear();
+  f.sets.clear();
+  f.dels.clear();
+  for (uint32_t i = 0; i < f.reqs.size(); ++i)
+    (f.reqs[i].kind == 0 ? f.gets : f.reqs[i].kind == 1 ? f.sets : f.dels).push_back(i);
+  f.tnow = be->now();
+  f.t0 = wall_s();
+  f.got = f.gets.empty();
+  f.active = true;
+  // ---- GET: coalesce equal digests on the host (a hot object under concurrent clients
+  // is one GPU row and one arena record, shared by its requests), then one edge-GET
+  // launch: keys and offsets in mapped memory, records straight into a pinned arena
+  const size_t n0 = f.gets.size();
+  f.rows = 0;
+  if (n0) {
     size_t tsz = 16;
     while (tsz < 2 * n0) tsz <<= 1;
-    dv.co_tab.assign(tsz, -1);
-    dv.urow.resize(n0);
-    size_t n = 0;
+    co_tab.assign(tsz, -1);
+    f.urow.resize(n0);
+    f.keys.ensure(n0 * sizeof(Digest));
+    Digest* hk = f.keys.host<Digest>();
     for (size_t j = 0; j < n0; ++j) {
-      const Digest& d = batch[gets[k][j]].d;
+      const Digest& d = f.reqs[f.gets[j]].d;
       for (size_t h = (size_t)(d.hi ^ (d.hi >> 31)) & (tsz - 1);; h = (h + 1) & (tsz - 1)) {
-        const int32_t u = dv.co_tab[h];
-        if (u < 0) {  // first request for this digest: it gets a GPU row
-          dv.co_tab[h] = (int32_t)n;
-          dv.h_keys[n] = d;
-          dv.urow[j] = (uint32_t)n++;
+        const int32_t u = co_tab[h];
+        if (u < 0) {
+          co_tab[h] = (int32_t)f.rows;
+          hk[f.rows] = d;
+          f.urow[j] = (uint32_t)f.rows++;
           break;
         }
-        if (dv.h_keys[u].lo == d.lo && dv.h_keys[u].hi == d.hi) {
-          dv.urow[j] = (uint32_t)u;
+        if (hk[u].lo == d.lo && hk[u].hi == d.hi) {
+          f.urow[j] = (uint32_t)u;
           break;
         }
       }
     }
-    nuniq[k] = n;
-    coalesced_gets_ += n0 - n;
-    if ((int64_t)n <= HbmCache::kSmallGetMax) {
-      // one launch, no copies: keys, offsets and values all live in mapped host memory;
-      // the kernel's last workgroup signals completion through a pinned host slot
-      dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
-                          tnow, dv.stream, kDoneSlot);
-      continue;
-    }
-    HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-    dv.cache->lookup(dv.d_keys, (int64_t)n, dv.d_loc, dv.d_size, dv.d_off, tnow, dv.stream);
-    dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
-    HB_OK(hipMemcpyAsync(dv.h_off, dv.d_off, (n + 1) * 8, hipMemcpyDeviceToHost, dv.stream));
+    coalesced += n0 - f.rows;
+    f.offs.ensure((f.rows + 1) * 8);
+    // arena sized from the running average record size (regathered if it falls short)
+    const size_t want = (size_t)(avg_row_bytes * 1.5 * (double)f.rows) + (64u << 10);
+    f.arena = pool->take(want);
+    cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
+                     f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
   }
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = nuniq[k];
-    if (!n) continue;
-    dv.set_device();
-    const bool small = (int64_t)n <= HbmCache::kSmallGetMax;
-    if (small)
-      dv.cache->wait_host_slot(kDoneSlot, 10000);  // no stream sync on the hit path
-    else
-      HB_OK(hipStreamSynchronize(dv.stream));
-    const uint64_t total = dv.h_off[n];
-    if (total > dv.out_cap) {  // rare: grow the zero-copy buffer and gather again
-      dv.ensure_out(total);
-      if (small)
-        dv.cache->small_get(dv.h_keys_dev, (int64_t)n, dv.h_out_dev, dv.out_cap, dv.h_off_dev,
-                            tnow, dv.stream);
-      else
-        dv.cache->gather(dv.d_loc, dv.d_off, (int64_t)n, dv.h_out_dev, dv.stream, dv.out_cap);
-      HB_OK(hipStreamSynchronize(dv.stream));
-    }
-  }
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = nuniq[k];
-    if (!n) continue;
-    // one CacheValue per GPU row, shared by that row's requests
-    dv.uval.assign(n, CacheValue{});
-    dv.uhit.assign(n, 0);
-    for (size_t u = 0; u < n; ++u) {
-      const uint64_t o = dv.h_off[u], sz = dv.h_off[u + 1] - o;
-      if (!sz) continue;
-      ItemHeader h;
-      std::memcpy(&h, dv.h_out + o, sizeof h);
-      if (h.magic == kItemMagic && h.d0 == dv.h_keys[u].lo && h.d1 == dv.h_keys[u].hi) {
-        dv.uhit[u] = 1;
-        CacheValue& v = dv.uval[u];
-        v.flags = h.flags;
-        v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
-        v.data = std::make_shared<const std::string>(
-            reinterpret_cast<const char*>(dv.h_out + o + kItemHeaderBytes), h.vlen);
-      }
-    }
-    for (size_t j = 0; j < gets[k].size(); ++j) {
-      Req& r = batch[gets[k][j]];
-      const uint32_t u = dv.urow[j];
-      const bool hit = dv.uhit[u] != 0;
-      CacheValue v = dv.uval[u];
-      auto cb = std::move(r.gcb);
-      r.ex->post([cb, hit, v]() { cb(hit, v); });
-    }
-  }
-  // ---- SET. Micro-batches: pack into mapped staging padded to a size class (skip
-  // rows); the SET kernels read it directly (no copies). SHELLAC_SET_GRAPH=1 replays a
-  // captured hipGraph per class instead of launching the chain: measured slower on
-  // ROCm 7 (52.8 vs 46.6 us per 64-row batch incl. sync, profiles/r1_small_get_latency.log),
-  // so off by default. Larger batches: pinned staging, H2D, store.
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = sets[k].size();
-    if (!n) continue;
-    dv.set_device();
-    int cls = 0;
-    while (cls < Dev::kSetClasses && Dev::kSetClass[cls] < (int64_t)n) ++cls;
-    if (cls < Dev::kSetClasses) {
-      const int64_t cn = Dev::kSetClass[cls];
-      uint64_t bytes = 16;
-      for (size_t idx : sets[k]) bytes += align_up(batch[idx].value->size(), 16);
-      dv.ensure_set_staging(bytes);
-      uint32_t* vl = dv.hs_meta;
-      uint32_t* fl = dv.hs_meta + cn;
-      uint32_t* ex = dv.hs_meta + 2 * cn;
-      uint64_t off = 0;
-      for (size_t j = 0; j < n; ++j) {
-        const Req& r = batch[sets[k][j]];
-        dv.hs_keys[j] = r.d;
-        std::memcpy(dv.hs_vals + off, r.value->data(), r.value->size());
-        dv.hs_voff[j] = off;
-        vl[j] = (uint32_t)r.value->size();
-        fl[j] = r.flags;
-        ex[j] = r.ttl ? tnow + r.ttl : 0;
-        off += align_up(r.value->size(), 16);
-      }
-      for (int64_t j = (int64_t)n; j < cn; ++j) {  // padding: rows the SET skips
-        dv.hs_keys[j] = Digest{0, 0};
-        dv.hs_voff[j] = 0;
-        vl[j] = kSkipVlen;
-        fl[j] = 0;
-        ex[j] = 0;
-      }
-      // the bound only guards against batches over half the log: a class constant
-      if (set_graphs_)
-        dv.cache->store_graph(&dv.set_graph[cls], dv.hs_keys_dev, dv.hs_vals_dev,
-                              dv.hs_voff_dev, dv.hs_meta_dev, dv.hs_meta_dev + cn,
-                              dv.hs_meta_dev + 2 * cn, cn, dv.cache->config().log_bytes / 2,
-                              tnow, dv.stream);
-      else
-        dv.cache->store(dv.hs_keys_dev, dv.hs_vals_dev, dv.hs_voff_dev, dv.hs_meta_dev,
-                        dv.hs_meta_dev + cn, dv.hs_meta_dev + 2 * cn, cn,
-                        dv.cache->config().log_bytes / 2, tnow, dv.stream);
-      continue;
-    }
-    dv.ensure_n(n);
-    uint64_t bytes = 16;
-    for (size_t idx : sets[k]) bytes += align_up(batch[idx].value->size(), 16);
-    dv.ensure_vals(bytes);
+  // ---- SET: [klen | key | payload] values packed into mapped staging the SET kernels
+  // read directly (no copies), exact log-bytes bound
+  const size_t ns = f.sets.size();
+  if (ns) {
+    f.set_keys.ensure(ns * sizeof(Digest));
+    f.set_voff.ensure(ns * 8);
+    f.set_meta.ensure(ns * 12);
+    size_t bytes = 16;
+    for (uint32_t i : f.sets)
+      bytes += align_up(keyed_size(f.reqs[i].key.size(), f.reqs[i].value->size()), 16);
+    f.set_vals.ensure(bytes);
+    Digest* kk = f.set_keys.host<Digest>();
+    uint64_t* vo = f.set_voff.host<uint64_t>();
+    uint32_t* vl = f.set_meta.host<uint32_t>();
+    uint32_t* fl = vl + ns;
+    uint32_t* ex = vl + 2 * ns;
     uint64_t off = 0, bound = 0;
-    uint32_t* vl = dv.h_meta;
-    uint32_t* fl = dv.h_meta + n;
-    uint32_t* ex = dv.h_meta + 2 * n;
-    for (size_t j = 0; j < n; ++j) {
-      const Req& r = batch[sets[k][j]];
-      dv.h_keys[j] = r.d;
-      std::memcpy(dv.h_vals + off, r.value->data(), r.value->size());
-      dv.h_voff[j] = off;
-      vl[j] = (uint32_t)r.value->size();
+    for (size_t j = 0; j < ns; ++j) {
+      const Req& r = f.reqs[f.sets[j]];
+      const size_t sz = keyed_size(r.key.size(), r.value->size());
+      write_keyed(f.set_vals.host<uint8_t>() + off, r.key, r.value->data(), r.value->size());
+      kk[j] = r.d;
+      vo[j] = off;
+      vl[j] = (uint32_t)sz;
       fl[j] = r.flags;
-      ex[j] = r.ttl ? tnow + r.ttl : 0;
-      off += align_up(r.value->size(), 16);
-      bound += item_bytes(vl[j]);
+      ex[j] = r.ttl ? f.tnow + r.ttl : 0;
+      off += align_up(sz, 16);
+      bound += item_bytes((uint32_t)sz);
     }
-    HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_vals, dv.h_vals, off + 16, hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_voff, dv.h_voff, n * 8, hipMemcpyHostToDevice, dv.stream));
-    HB_OK(hipMemcpyAsync(dv.d_meta, dv.h_meta, n * 12, hipMemcpyHostToDevice, dv.stream));
-    dv.cache->store(dv.d_keys, dv.d_vals, dv.d_voff, dv.d_meta, dv.d_meta + n, dv.d_meta + 2 * n,
-                    (int64_t)n, bound, tnow, dv.stream);
+    cache->store(f.set_keys.dev<Digest>(), f.set_vals.dev<uint8_t>(),
+                 f.set_voff.dev<uint64_t>(), f.set_meta.dev<uint32_t>(),
+                 f.set_meta.dev<uint32_t>() + ns, f.set_meta.dev<uint32_t>() + 2 * ns,
+                 (int64_t)ns, bound, f.tnow, stream);
+    for (uint32_t i : f.sets) f.reqs[i].value = Bytes();  // staged: drop the reference
   }
-  // ---- DELETE
-  for (size_t k = 0; k < nd; ++k) {
-    Dev& dv = *devs_[k];
-    const size_t n = dels[k].size();
-    if (!n && sets[k].empty()) continue;  // GET-only batch: nothing left on the stream
-    dv.set_device();
-    if (n) {
-      HB_OK(hipStreamSynchronize(dv.stream));  // staging reuse after SET
-      dv.ensure_n(n);
-      for (size_t j = 0; j < n; ++j) dv.h_keys[j] = batch[dels[k][j]].d;
-      HB_OK(hipMemcpyAsync(dv.d_keys, dv.h_keys, n * sizeof(Digest), hipMemcpyHostToDevice, dv.stream));
-      dv.cache->remove(dv.d_keys, (int64_t)n, dv.d_found, tnow, dv.stream);
-      HB_OK(hipMemcpyAsync(dv.h_found, dv.d_found, n, hipMemcpyDeviceToHost, dv.stream));
+  // ---- DELETE: keys and found flags in mapped memory
+  const size_t nd = f.dels.size();
+  if (nd) {
+    f.del_keys.ensure(nd * sizeof(Digest));
+    f.del_found.ensure(nd);
+    for (size_t j = 0; j < nd; ++j) f.del_keys.host<Digest>()[j] = f.reqs[f.dels[j]].d;
+    cache->remove(f.del_keys.dev<Digest>(), (int64_t)nd, f.del_found.dev<uint8_t>(), f.tnow,
+                  stream);
+  }
+  HB_OK(hipEventRecord(f.ev, stream));
+  batches++;
+  batched_reqs += f.reqs.size();
+  uint64_t prev = max_batch.load();
+  while (f.reqs.size() > prev && !max_batch.compare_exchange_weak(prev, f.reqs.size())) {
+  }
+}
+
+// Completion of flight f (non-blocking unless `block`): GET results as soon as the edge
+// GET's slot fires, DELETE results and the flight's buffers once its event completes.
+bool HbmBackend::Dev::try_reap(Flight& f, bool block) {
+  if (!f.got && f.active) {
+    const uint64_t total = block ? cache->wait_host_slot(f.slot, be->cfg_.batch_timeout_ms)
+                                 : cache->host_slot(f.slot);
+    if (total == HbmCache::kSlotPending) return false;
+    if (total == HbmCache::kSlotFailed) throw Error("edge GET reported a failed look-back");
+    if (total > f.arena->cap) {  // rare: the records outgrew the arena; gather again
+      regathers++;
+      HB_OK(hipEventSynchronize(f.ev));
+      f.arena = pool->take(total + (64u << 10));
+      cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
+                       f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
+      HB_OK(hipEventRecord(f.ev, stream));
+      const uint64_t t2 = cache->wait_host_slot(f.slot, be->cfg_.batch_timeout_ms);
+      SH_CHECK(t2 == total, "regather size changed");
     }
-    HB_OK(hipStreamSynchronize(dv.stream));
-    for (size_t j = 0; j < n; ++j) {
-      Req& r = batch[dels[k][j]];
-      const bool f = dv.h_found[j] != 0;
+    if (f.rows) avg_row_bytes = 0.9 * avg_row_bytes + 0.1 * ((double)total / (double)f.rows);
+    deliver_gets(f);
+    f.got = true;
+  }
+  if (block) {
+    HB_OK(hipEventSynchronize(f.ev));
+  } else {
+    const hipError_t e = hipEventQuery(f.ev);
+    if (e == hipErrorNotReady) return false;
+    HB_OK(e);
+  }
+  if (f.active) {
+    deliver_dels(f);
+    batch_ns += (uint64_t)((wall_s() - f.t0) * 1e9);
+  }
+  f.active = false;
+  f.reqs.clear();
+  f.arena.reset();  // hits hold their own references
+  return true;
+}
+
+// Group completions per executor: one post_batch (one lock, one wake-up) per reactor.
+namespace {
+struct PostGroups {
+  std::vector<std::pair<Executor*, std::vector<std::function<void()>>>> g;
+  std::vector<std::function<void()>>& at(Executor* ex) {
+    for (auto& p : g)
+      if (p.first == ex) return p.second;
+    g.emplace_back(ex, std::vector<std::function<void()>>{});
+    return g.back().second;
+  }
+  void flush() {
+    for (auto& p : g) p.first->post_batch(p.second);
+    g.clear();
+  }
+};
+}  // namespace
+
+void HbmBackend::Dev::deliver_gets(Flight& f) {
+  if (f.gets.empty()) return;
+  const uint64_t* off = f.offs.host<uint64_t>();
+  const Digest* hk = f.keys.host<Digest>();
+  const uint8_t* base = f.arena->h;
+  // the arena stays alive while any response built from it does
+  std::shared_ptr<const void> owner = f.arena;
+  PostGroups pg;
+  for (size_t j = 0; j < f.gets.size(); ++j) {
+    Req& r = f.reqs[f.gets[j]];
+    const uint32_t u = f.urow[j];
+    const uint64_t o = off[u], sz = off[u + 1] - o;
+    CacheValue v;
+    bool hit = false;
+    if (sz) {
+      ItemHeader h;
+      std::memcpy(&h, base + o, sizeof h);
+      size_t po = 0;
+      const char* val = reinterpret_cast<const char*>(base + o + kItemHeaderBytes);
+      if (h.magic == kItemMagic && h.d0 == hk[u].lo && h.d1 == hk[u].hi) {
+        if (keyed_match(val, h.vlen, r.key, &po)) {
+          hit = true;
+          v.flags = h.flags;
+          v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)f.tnow : 0;
+          v.data = ByteRef(owner, val + po, h.vlen - po);
+        } else {
+          key_mismatch.fetch_add(1, std::memory_order_relaxed);  // digest collision
+        }
+      }
+    }
+    auto cb = std::move(r.gcb);
+    if (r.ex)
+      pg.at(r.ex).push_back([cb = std::move(cb), hit, v = std::move(v)]() { cb(hit, v); });
+    else
+      cb(hit, std::move(v));
+  }
+  pg.flush();
+}
+
+void HbmBackend::Dev::deliver_dels(Flight& f) {
+  if (f.dels.empty()) return;
+  PostGroups pg;
+  for (size_t j = 0; j < f.dels.size(); ++j) {
+    Req& r = f.reqs[f.dels[j]];
+    const bool found = f.del_found.host<uint8_t>()[j] != 0;
+    auto cb = std::move(r.dcb);
+    if (!cb) continue;
+    if (r.ex)
+      pg.at(r.ex).push_back([cb = std::move(cb), found]() { cb(found); });
+    else
+      cb(found);
+  }
+  pg.flush();
+}
+
+void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs) {
+  PostGroups pg;
+  for (auto& r : reqs) {
+    if (r.kind == 0 && r.gcb) {
+      auto cb = std::move(r.gcb);
+      if (r.ex) pg.at(r.ex).push_back([cb = std::move(cb)]() { cb(false, CacheValue{}); });
+      else cb(false, CacheValue{});
+    } else if (r.kind == 2 && r.dcb) {
       auto cb = std::move(r.dcb);
-      if (cb) r.ex->post([cb, f]() { cb(f); });
+      if (r.ex) pg.at(r.ex).push_back([cb = std::move(cb)]() { cb(false); });
+      else cb(false);
+    } else if (r.kind == 1) {
+      dropped++;
     }
   }
+  pg.flush();
 }
 
-void HbmBackend::sweep_all() {
-  TraceRange tr("hbm_backend.sweep");
-  const uint32_t t = now();
-  uint64_t objs = 0, bytes = 0;
-  for (auto& d : devs_) {
-    d->set_device();
-    uint64_t o = 0, b = 0;
-    d->cache->sweep(t, d->stream, &o, &b);
-    objs += o;
-    bytes += b;
+// A failed or stalled flight: its requests are answered (GET miss, DEL not found), the
+// flight itself stays reserved until the GPU finishes with its buffers.
+void HbmBackend::Dev::fail_flight(Flight& f) {
+  failures++;
+  if (!f.got) fail_requests(f.reqs);
+  else {
+    std::vector<Req> rest;
+    for (uint32_t i : f.dels) rest.push_back(std::move(f.reqs[i]));
+    fail_requests(rest);
   }
-  live_objects_ = objs;
-  live_bytes_ = bytes;
-  sweeps_++;
+  f.got = true;
+  f.gets.clear();
+  f.dels.clear();
+  f.active = false;
 }
 
-void HbmBackend::finish_filter_rebuild() {
+void HbmBackend::Dev::eject(const char* why) {
+  if (up()) {
+    std::fprintf(stderr, "[shellac hbm] ejecting gpu %d (%s); retry in %d s\n", device, why,
+                 be->cfg_.retry_s);
+    ejections++;
+  }
+  failed = true;
+  retry_at = wall_s() + be->cfg_.retry_s;
+  set_up(false);
+  std::vector<Req> pending;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    pending.swap(q);
+    qn.store(0, std::memory_order_release);
+  }
+  fail_requests(pending);
+}
+
+// Bring an ejected shard back: the fault drill was lifted, or retry_s passed and every
+// flight has completed (the GPU answers again). Its contents may be stale (SETs routed
+// elsewhere while it was out), so it is flushed unless configured otherwise.
+void HbmBackend::Dev::maybe_restore() {
+  if (forced_down.load(std::memory_order_acquire)) return;
+  if (failed && wall_s() < retry_at) return;
+  try {
+    for (auto& f : flights) HB_OK(hipEventSynchronize(f->ev));
+    if (be->cfg_.flush_on_restore) cache->flush(stream);
+    HB_OK(hipStreamSynchronize(stream));
+  } catch (const std::exception&) {
+    retry_at = wall_s() + be->cfg_.retry_s;
+    return;
+  }
+  failed = false;
+  inflight = 0;
+  head = 0;
+  for (auto& f : flights) {
+    f->active = false;
+    f->reqs.clear();
+    f->arena.reset();
+  }
+  restores++;
+  set_up(true);
+  std::fprintf(stderr, "[shellac hbm] gpu %d back in service\n", device);
+}
+
+void HbmBackend::Dev::sweep() {
+  TraceRange tr("hbm_backend.sweep");
+  uint64_t o = 0, b = 0;
+  cache->sweep(be->now(), stream, &o, &b);
+  live_objects = o;
+  live_bytes = b;
+  sweeps++;
+}
+
+void HbmBackend::Dev::finish_filter_rebuild() {
   TraceRange tr("hbm_backend.filter_rebuild");
-  const uint32_t t = now();
-  for (auto& d : devs_) {
-    d->set_device();
-    const uint64_t live = d->cache->export_keys(nullptr, 0, t, d->stream);
-    if (!live) continue;
+  const uint32_t t = be->now();
+  const uint64_t live = cache->export_keys(nullptr, 0, t, stream);
+  if (live) {
     // the kernel writes the digests straight into mapped host memory (no device buffer)
-    Digest *h = nullptr, *hdev = nullptr;
-    Dev::map_alloc(&h, &hdev, live * sizeof(Digest));
+    Mapped m;
+    m.ensure(live * sizeof(Digest));
     uint64_t got = 0;
     try {
-      got = std::min(live, d->cache->export_keys(hdev, live, t, d->stream));
+      got = std::min(live, cache->export_keys(m.dev<Digest>(), live, t, stream));
     } catch (...) {
-      (void)hipHostFree(h);
+      m.release();
       throw;
     }
-    for (uint64_t i = 0; i < got; ++i) filt_next_->add(h[i]);
-    (void)hipHostFree(h);
+    for (uint64_t i = 0; i < got; ++i) filt_next->add(m.host<Digest>()[i]);
+    m.release();
   }
-  std::lock_guard<std::mutex> lk(mu_);
-  std::atomic_store(&filt_, filt_next_);
-  filt_next_.reset();
-  filt_rebuild_at_ = filt_->adds() + cfg_.nbuckets_per_gpu * kEntriesPerBucket * devs_.size();
-  filt_rebuilds_++;
+  std::lock_guard<std::mutex> lk(mu);
+  std::atomic_store(&filt, filt_next);
+  filt_next.reset();
+  filt_rebuild_at = filt->adds() + be->cfg_.nbuckets_per_gpu * kEntriesPerBucket;
+  filt_rebuilds++;
 }
 
 void HbmBackend::stats(StatList* out) {
   CacheCounters t{};
   uint64_t hbm = 0;
+  auto sum = [&](std::atomic<uint64_t> Dev::*m) {
+    uint64_t s = 0;
+    for (auto& d : devs_) s += ((*d).*m).load();
+    return s;
+  };
   for (auto& d : devs_) {
-    d->set_device();
+    (void)hipSetDevice(d->device);
+    // a separate stream: the batcher's may be busy; counters are advisory
     const CacheCounters c = d->cache->counters(nullptr);
     t.get_ops += c.get_ops; t.get_hits += c.get_hits; t.set_ops += c.set_ops;
     t.set_bytes += c.set_bytes; t.set_evicted += c.set_evicted; t.del_ops += c.del_ops;
+    t.reinserted += c.reinserted; t.reinsert_bytes += c.reinsert_bytes;
     hbm += d->cache->hbm_bytes();
   }
   out->emplace_back("cache_get_ops", t.get_ops);
@@ -616,30 +859,40 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("cache_set_ops", t.set_ops);
   out->emplace_back("cache_set_bytes", t.set_bytes);
   out->emplace_back("cache_evicted", t.set_evicted);
+  out->emplace_back("cache_reinserted", t.reinserted);
+  out->emplace_back("cache_reinsert_bytes", t.reinsert_bytes);
   out->emplace_back("hbm_gpus", devs_.size());
+  out->emplace_back("hbm_gpus_up", (uint64_t)__builtin_popcountll(up_mask_.load()));
   out->emplace_back("hbm_bytes", hbm);
-  out->emplace_back("hbm_batches", batches_.load());
-  out->emplace_back("hbm_batched_requests", batched_reqs_.load());
-  out->emplace_back("hbm_max_batch", max_batch_seen_.load());
-  out->emplace_back("hbm_batch_ns_total", batch_ns_.load());
-  out->emplace_back("hbm_sweeps", sweeps_.load());
-  uint64_t gl = 0, gc = 0;
-  for (auto& d : devs_)
-    for (auto& g : d->set_graph) {
-      gl += g.launches;
-      gc += g.captures;
-    }
-  out->emplace_back("hbm_set_graph_launches", gl);
-  out->emplace_back("hbm_set_graph_captures", gc);
-  out->emplace_back("hbm_live_objects", live_objects_.load());
-  out->emplace_back("hbm_live_bytes", live_bytes_.load());
-  out->emplace_back("hbm_coalesced_gets", coalesced_gets_.load());
+  out->emplace_back("hbm_pipeline_depth", (uint64_t)cfg_.depth);
+  out->emplace_back("hbm_batches", sum(&Dev::batches));
+  out->emplace_back("hbm_batched_requests", sum(&Dev::batched_reqs));
+  uint64_t mb = 0;
+  for (auto& d : devs_) mb = std::max<uint64_t>(mb, d->max_batch.load());
+  out->emplace_back("hbm_max_batch", mb);
+  out->emplace_back("hbm_batch_ns_total", sum(&Dev::batch_ns));
+  out->emplace_back("hbm_sweeps", sum(&Dev::sweeps));
+  out->emplace_back("hbm_live_objects", sum(&Dev::live_objects));
+  out->emplace_back("hbm_live_bytes", sum(&Dev::live_bytes));
+  out->emplace_back("hbm_coalesced_gets", sum(&Dev::coalesced));
+  out->emplace_back("hbm_key_mismatch", sum(&Dev::key_mismatch));
+  out->emplace_back("hbm_failures", sum(&Dev::failures));
+  out->emplace_back("hbm_ejections", sum(&Dev::ejections));
+  out->emplace_back("hbm_restores", sum(&Dev::restores));
+  out->emplace_back("hbm_regathers", sum(&Dev::regathers));
+  out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));
+  out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
+  uint64_t arena = 0;
+  for (auto& d : devs_) arena += d->pool->allocated();
+  out->emplace_back("hbm_arena_bytes", arena);
   if (cfg_.presence_filter) {
-    const auto f = std::atomic_load(&filt_);
-    out->emplace_back("hbm_filter_skips", filt_skips_.load());
-    out->emplace_back("hbm_filter_rebuilds", filt_rebuilds_.load());
-    out->emplace_back("hbm_filter_adds", f->adds());
-    out->emplace_back("hbm_filter_fill_ppm", (uint64_t)(f->fill() * 1e6));
+    uint64_t adds = 0;
+    for (auto& d : devs_) adds += std::atomic_load(&d->filt)->adds();
+    out->emplace_back("hbm_filter_skips", sum(&Dev::filt_skips));
+    out->emplace_back("hbm_filter_rebuilds", sum(&Dev::filt_rebuilds));
+    out->emplace_back("hbm_filter_adds", adds);
+    out->emplace_back("hbm_filter_fill_ppm",
+                      (uint64_t)(std::atomic_load(&devs_[0]->filt)->fill() * 1e6));
   }
 }
 

@@ -29,14 +29,15 @@ struct BackendHandle {
   std::shared_ptr<CacheBackend> be;
 };
 
-py::object blocking_get(CacheBackend* be, const std::string& key) {
+py::object blocking_get(CacheBackend* be, const std::string& key, const Digest* forced = nullptr) {
   std::mutex mu;
   std::condition_variable cv;
   bool done = false, hit = false;
   CacheValue val;
   {
     py::gil_scoped_release nogil;
-    const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(key.data()), key.size());
+    const Digest d = forced ? *forced
+                            : digest_bytes(reinterpret_cast<const uint8_t*>(key.data()), key.size());
     be->get(key, d, &g_inline, [&](bool h, CacheValue v) {
       std::lock_guard<std::mutex> lk(mu);
       hit = h;
@@ -140,6 +141,12 @@ void bind_net(py::module_& m) {
   py::class_<BackendHandle>(m, "CacheBackend")
       .def_property_readonly("name", [](BackendHandle& h) { return h.be->name(); })
       .def("get", [](BackendHandle& h, py::bytes key) { return blocking_get(h.be.get(), key); })
+      .def("get_with_digest", [](BackendHandle& h, py::bytes key, py::bytes digest_of) {
+        // GET `key` but look it up under the digest of `digest_of`: a forged collision
+        const std::string o = digest_of;
+        const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(o.data()), o.size());
+        return blocking_get(h.be.get(), key, &d);
+      })
       .def("set", [](BackendHandle& h, py::bytes key, py::bytes value, uint32_t flags,
                      uint32_t ttl) {
         std::string k = key;
@@ -171,7 +178,8 @@ void bind_net(py::module_& m) {
   m.def("hbm_backend", [](std::vector<int> devices, uint64_t log_bytes_per_gpu,
                           uint64_t nbuckets_per_gpu, uint32_t max_item, int batch_us,
                           int max_batch, int sweep_interval_s, int spin_us,
-                          bool presence_filter) {
+                          bool presence_filter, int depth, const std::string& evict,
+                          int retry_s, int batch_timeout_ms, bool flush_on_restore) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -182,12 +190,23 @@ void bind_net(py::module_& m) {
     c.sweep_interval_s = sweep_interval_s;
     c.spin_us = spin_us;
     c.presence_filter = presence_filter;
+    c.depth = depth;
+    SH_CHECK(evict == "clock" || evict == "fifo", "evict must be clock or fifo");
+    c.evict = evict == "clock" ? 1 : 0;
+    c.retry_s = retry_s;
+    c.batch_timeout_ms = batch_timeout_ms;
+    c.flush_on_restore = flush_on_restore;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
      py::arg("max_item") = 1u << 20, py::arg("batch_us") = 0, py::arg("max_batch") = 65536,
      py::arg("sweep_interval_s") = 10, py::arg("spin_us") = 50,
-     py::arg("presence_filter") = true);
+     py::arg("presence_filter") = true, py::arg("depth") = 3, py::arg("evict") = "clock",
+     py::arg("retry_s") = 2, py::arg("batch_timeout_ms") = 2000,
+     py::arg("flush_on_restore") = true);
+  m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
+    return h.be->inject_shard_down(shard, down);
+  }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);
   m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl) {
     return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl)};
   }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60);

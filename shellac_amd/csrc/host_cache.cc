@@ -149,11 +149,8 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
     uint64_t bytes = 0;  // the batch's bytes (dedupe losers included), as the device
     for (int64_t i = 0; i < n; ++i)
       if (vlen[i] != kSkipVlen && vlen[i] <= max_item_) bytes += item_bytes(vlen[i]);
-    const int64_t w = hand_window(n);
+    // the device's combined batch: reinsertions (in log order) ahead of the batch
     reclaim_locked(n, bytes, now, &rows, &stage);
-    rows.resize((size_t)w);  // the device's combined batch: w reinsertion rows, then n
-    for (size_t r = 0; r < rows.size(); ++r)
-      if (!rows[r].val) rows[r] = Row{Digest{0, 0}, nullptr, kSkipVlen, 0, 0};
   }
   rows.reserve(rows.size() + (size_t)n);
   for (int64_t i = 0; i < n; ++i)
@@ -195,7 +192,7 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vec
     if (hb) hot.push_back(Hot{(int64_t)j, l, hb, hx});
     hx += hb;
   }
-  out->assign((size_t)w, Row{Digest{0, 0}, nullptr, kSkipVlen, 0, 0});
+  out->clear();
   uint64_t staged = 0;
   for (const Hot& t : hot)
     if ((uint64_t)t.j < consumed && t.hx + t.h <= rmax_) staged = t.hx + t.h;
@@ -206,8 +203,8 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vec
     std::memcpy(stage->data() + t.hx, rec, t.h);
     ItemHeader h;
     std::memcpy(&h, rec, sizeof h);
-    (*out)[(size_t)t.j] = Row{Digest{h.d0, h.d1}, stage->data() + t.hx + kItemHeaderBytes, h.vlen,
-                              h.flags, h.expire};
+    out->push_back(Row{Digest{h.d0, h.d1}, stage->data() + t.hx + kItemHeaderBytes, h.vlen,
+                       h.flags, h.expire});
     ctr_.reinserted++;
     ctr_.reinsert_bytes += h.vlen;
   }
@@ -400,6 +397,24 @@ bool HostCache::get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* 
   if (flags) *flags = h.flags;
   if (expire) *expire = h.expire;
   out->assign(p + kItemHeaderBytes, p + kItemHeaderBytes + vl);
+  return true;
+}
+
+bool HostCache::get_one(const Digest& key, std::string* out, uint32_t* flags, uint32_t now,
+                        uint32_t* expire) {
+  std::lock_guard<std::mutex> lk(mu_);
+  uint32_t vl = 0;
+  const uint64_t l = probe_locked(key, now, &vl, 0, true);
+  ctr_.get_ops++;
+  if (!l) return false;
+  ctr_.get_hits++;
+  ctr_.get_bytes += vl;
+  const uint8_t* p = log_ + (l - 1) % log_bytes_;
+  ItemHeader h;
+  std::memcpy(&h, p, sizeof h);
+  if (flags) *flags = h.flags;
+  if (expire) *expire = h.expire;
+  out->assign(reinterpret_cast<const char*>(p + kItemHeaderBytes), vl);
   return true;
 }
 

@@ -42,6 +42,8 @@ class HostCache {
   // the value (not the header) into `out` and returns false on miss.
   bool get_one(const Digest& key, std::vector<uint8_t>* out, uint32_t* flags, uint32_t now,
                uint32_t* expire = nullptr);
+  bool get_one(const Digest& key, std::string* out, uint32_t* flags, uint32_t now,
+               uint32_t* expire = nullptr);
   void set_one(const Digest& key, const uint8_t* value, uint32_t vlen, uint32_t flags,
                uint32_t expire, uint32_t now);
 

@@ -60,11 +60,24 @@ class McReactor : public Executor {
     close(ep_);
   }
   void post(std::function<void()> fn) override {
+    bool was_empty;
     {
       std::lock_guard<std::mutex> lk(mu_);
+      was_empty = posted_.empty();
       posted_.push_back(std::move(fn));
     }
-    wake();
+    if (was_empty) wake();  // a non-empty queue already has a wake-up pending
+  }
+  void post_batch(std::vector<std::function<void()>>& fns) override {
+    if (fns.empty()) return;
+    bool was_empty;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      was_empty = posted_.empty();
+      for (auto& f : fns) posted_.push_back(std::move(f));
+    }
+    fns.clear();
+    if (was_empty) wake();
   }
   void wake() {
     uint64_t one = 1;

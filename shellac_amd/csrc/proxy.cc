@@ -124,6 +124,7 @@ class Reactor : public Executor {
   ~Reactor() override;
   void loop();
   void post(std::function<void()> fn) override;
+  void post_batch(std::vector<std::function<void()>>& fns) override;
   void wake() {
     uint64_t one = 1;
     (void)!write(evfd_, &one, 8);
@@ -219,11 +220,29 @@ Reactor::~Reactor() {
 }
 
 void Reactor::post(std::function<void()> fn) {
+  bool was_empty;
   {
     std::lock_guard<std::mutex> lk(post_mu_);
+    was_empty = posted_.empty();
     posted_.push_back(std::move(fn));
   }
-  wake();
+  if (was_empty) wake();  // a non-empty queue already has a wake-up pending
+}
+
+void Reactor::post_batch(std::vector<std::function<void()>>& fns) {
+  if (fns.empty()) return;
+  bool was_empty;
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    was_empty = posted_.empty();
+    if (was_empty) {
+      posted_.swap(fns);
+    } else {
+      for (auto& f : fns) posted_.push_back(std::move(f));
+    }
+  }
+  fns.clear();
+  if (was_empty) wake();
 }
 
 void Reactor::drain_posted() {

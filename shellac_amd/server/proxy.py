@@ -49,8 +49,10 @@ def parse_server_list(slist: str, default_port: int) -> list:
 def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  dram_mb: int = 1024, gpus: Optional[Sequence[int]] = None,
                  hbm_gb: float = 16.0, max_item: int = 1 << 20, batch_us: int = 0,
-                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60, fault: str = "",
-                 sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50):
+                 retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60,
+                 fault: Optional[str] = None,
+                 sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
+                 depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -60,22 +62,29 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
     batch or a network round trip). ``fault`` (e.g. ``"get_miss=0.1,delay_us=500"``,
     ``"down"``) wraps the stack in a fault-injection backend; see ``set_fault``.
     ``hbm_filter`` keeps a host presence filter of stored digests so cold-key GETs miss
-    without a GPU batch; ``spin_us`` is how long the HBM batcher polls before blocking.
+    without a GPU batch; ``spin_us`` is how long the HBM batcher polls before blocking;
+    ``depth`` is how many batches each GPU keeps in flight; ``evict`` is the log policy
+    (``clock``: read objects get a second chance, memcached-LRU-like; ``fifo``); a GPU
+    whose batch fails or stalls past ``batch_timeout_ms`` is ejected for ``retry_s``.
+    ``fault="gpu_down=K"`` ejects GPU shard K as a drill.
     """
     c = core()
     if kind == "none":
         return None
-    if fault:
-        # fault injection wraps the whole cache stack (set_fault() changes it live)
+    if fault is not None:
+        # fault injection wraps the whole cache stack (set_fault() changes it live; ""
+        # starts healthy)
         inner = make_backend(kind, caches=caches, dram_mb=dram_mb, gpus=gpus, hbm_gb=hbm_gb,
                              max_item=max_item, batch_us=batch_us, retry_s=retry_s, l1_mb=l1_mb,
                              promote_ttl=promote_ttl, sweep_s=sweep_s, hbm_filter=hbm_filter,
-                             spin_us=spin_us)
+                             spin_us=spin_us, depth=depth, evict=evict,
+                             batch_timeout_ms=batch_timeout_ms)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
                           batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s,
-                          hbm_filter=hbm_filter, spin_us=spin_us)
+                          hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
+                          batch_timeout_ms=batch_timeout_ms)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -90,7 +99,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
         while nb * 4 * 1024 < log_bytes:  # ~2 KiB/object at <=50% slot load
             nb *= 2
         return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us, sweep_interval_s=sweep_s,
-                             spin_us=spin_us, presence_filter=hbm_filter)
+                             spin_us=spin_us, presence_filter=hbm_filter, depth=depth,
+                             evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms)
     raise ValueError(f"unknown cache backend {kind!r}")
 
 
@@ -212,7 +222,13 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-kill-switch", action="store_true", help="disable GET /kill")
     p.add_argument("--fault", default="",
                    help="fault injection on the cache tier, e.g. get_miss=0.1,set_drop=0.5,"
-                        "delay_us=500 or down (drills; default off)")
+                        "delay_us=500, down, or gpu_down=K (eject GPU shard K; drills; "
+                        "default off)")
+    p.add_argument("--hbm-depth", type=int, default=3,
+                   help="GET/SET batches each GPU keeps in flight (--cache hbm)")
+    p.add_argument("--evict", choices=["clock", "fifo"], default="clock",
+                   help="HBM log eviction: clock (read objects get a second chance, "
+                        "memcached-LRU-like; default) or fifo")
     p.add_argument("--stream-bytes", type=int, default=1 << 20,
                    help="stream responses larger than this to the client without caching them")
     p.add_argument("--decode-gzip", action="store_true",
@@ -242,7 +258,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,
-                     "hbm_filter": not args.no_hbm_filter, "spin_us": args.hbm_spin_us}
+                     "hbm_filter": not args.no_hbm_filter, "spin_us": args.hbm_spin_us,
+                     "depth": args.hbm_depth, "evict": args.evict}
                     if kind == "hbm" else {}),
                  **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))
     print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)

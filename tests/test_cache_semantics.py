@@ -144,3 +144,16 @@ def test_scan_and_segcopy_host():
     assert dst[:16].tolist() == list(range(64, 80))
     assert dst[16:48].tolist() == list(range(16, 48))
     assert dst[48:96].tolist() == list(range(128, 176))
+
+
+def test_dram_backend_full_key_identity():
+    """The DRAM tier stores each value with its key: a GET under another key's digest
+    (a forged collision) misses instead of returning that object."""
+    from shellac_amd import core
+
+    be = core().dram_backend(16 << 20, 1 << 16, 4)
+    be.set(b"/victim", b"private", 7, 0)
+    assert be.get(b"/victim") == (b"private", 7)
+    assert be.get_with_digest(b"/attacker", b"/victim") is None
+    assert be.get_with_digest(b"/victim", b"/victim") == (b"private", 7)
+    assert be.stats()["cache_key_mismatch"] == 1

@@ -62,11 +62,14 @@ def test_proxy_with_hbm_backend(hbm):
             assert [r.body().read() for r in rs] == first
             assert all(o.hits[p] == 1 for p in paths)
             # repeated paths in one pipeline: batch-mates share a GPU row (host coalescing)
+            c0 = hbm.stats()["hbm_coalesced_gets"]
             rs = c.pipeline(paths[:10] * 8)
             assert [r.body().read() for r in rs] == first[:10] * 8
             assert all(o.hits[p] == 1 for p in paths)
             st = px.stats()
             assert st["cache_hits"] >= 50 and st["backend"] == "hbm"
+            # the batch-mates did share rows (not just correct bodies)
+            assert hbm.stats()["hbm_coalesced_gets"] > c0
     finally:
         o.stop()
 
@@ -140,3 +143,88 @@ def test_hbm_presence_filter_off_sends_every_get_to_the_gpu():
     assert be.get(b"/never/stored") is None
     st = be.stats()
     assert st["hbm_batches"] == b0 + 1 and "hbm_filter_skips" not in st
+
+
+def test_hbm_forged_digest_collision_is_a_miss(hbm):
+    """Objects are identified by their full key, not the digest: a GET for another key
+    that arrives with this object's digest (a forged collision) misses."""
+    hbm.set(b"/victim/page", b"secret" * 100, 5, 0)
+    assert _wait_get(hbm, b"/victim/page") == (b"secret" * 100, 5)
+    assert hbm.get_with_digest(b"/attacker/url", b"/victim/page") is None
+    assert hbm.get_with_digest(b"/victim/page", b"/victim/page") == (b"secret" * 100, 5)
+    assert hbm.stats()["hbm_key_mismatch"] >= 1
+
+
+def test_hbm_concurrent_clients_pipelined_batches():
+    """Many client threads against one GPU: batches overlap (depth 3), every GET gets
+    its own key's value, SETs interleave."""
+    import threading
+
+    be = make_backend("hbm", gpus=[0], hbm_gb=0.5, depth=3)
+    keys = [b"/cc/%d" % i for i in range(2000)]
+    for i, k in enumerate(keys):
+        be.set(k, b"%d:" % i + bytes([i % 251]) * (i % 3000), 0, 0)
+    assert _wait_get(be, keys[-1]) is not None
+    errors = []
+
+    def worker(t):
+        try:
+            for j in range(400):
+                i = (t * 7919 + j * 104729) % 2000
+                r = be.get(keys[i])
+                want = b"%d:" % i + bytes([i % 251]) * (i % 3000)
+                if r is None or r[0] != want:
+                    errors.append((i, r is None))
+                if j % 50 == 0:
+                    be.set(b"/cc/new/%d/%d" % (t, j), b"n" * 100, 0, 0)
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    st = be.stats()
+    assert st["hbm_batches"] > 0 and st["hbm_failures"] == 0 and st["hbm_regathers"] >= 0
+
+
+def test_gpu_shard_ejection_drill_and_restore():
+    """gpu_down=0: the shard leaves the ring, the proxy keeps answering (misses go to
+    the origin), SETs to it are dropped; lifting the drill restores (and flushes) the
+    shard, and hits resume once objects are cached again."""
+    from shellac_amd.server.proxy import set_fault
+
+    be = make_backend("hbm", gpus=[0], hbm_gb=0.5, fault="")
+    o = Origin(body_bytes=2000).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend=be, threads=2) as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/ej/{i}" for i in range(30)]
+            for p in paths:
+                assert c.get(p).status() == 200
+            time.sleep(0.2)
+            for p in paths:
+                c.get(p)
+            assert all(o.hits[p] == 1 for p in paths)  # cached
+            set_fault(be, "gpu_down=0")
+            for p in paths:
+                assert c.get(p).status() == 200     # still served: misses -> origin
+            assert all(o.hits[p] == 2 for p in paths)
+            st = px.stats()["cache"]
+            assert st["hbm_gpus_up"] == 0 and st["hbm_ejections"] >= 1
+            set_fault(be, "")
+            deadline = time.time() + 5
+            while px.stats()["cache"]["hbm_gpus_up"] == 0 and time.time() < deadline:
+                time.sleep(0.05)
+            assert px.stats()["cache"]["hbm_gpus_up"] == 1
+            for p in paths:
+                c.get(p)                             # flushed on restore: refill
+            time.sleep(0.3)
+            for p in paths:
+                assert c.get(p).status() == 200
+            assert all(o.hits[p] == 3 for p in paths)  # hits resumed
+            assert px.stats()["cache"]["hbm_restores"] >= 1
+    finally:
+        o.stop()

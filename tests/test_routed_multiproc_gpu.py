@@ -53,11 +53,19 @@ def _routed_worker(rank, world, port, q):
         upd = keys[:5] + keys[100:110] if rank == 1 else []
         req = keys[:30] * 5 + keys + [b"/none"] * 3
         res = sc.serve(digest_strings(req, dev), batch(upd, [b"v2" + k for k in upd]))
-        assert values(res) == [v1[k] for k in req[:-3]] + [None] * 3
+        got = values(res)
+        want = [v1[k] for k in req[:-3]] + [None] * 3
+        bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
+               enumerate(zip(got, want)) if g != w]
+        assert not bad, f"rank {rank}: {len(bad)} wrong GETs, first {bad[:6]}"
         # step 3: the overwrites are visible on every rank (replicas written through)
         res = sc.serve(digest_strings(req, dev), batch([], []))
         new = {k: b"v2" + k for k in keys[:5] + keys[100:110]}
-        assert values(res) == [new.get(k, v1[k]) for k in req[:-3]] + [None] * 3
+        got = values(res)
+        want = [new.get(k, v1[k]) for k in req[:-3]] + [None] * 3
+        bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
+               enumerate(zip(got, want)) if g != w]
+        assert not bad, f"rank {rank} step 3: {len(bad)} wrong GETs, first {bad[:6]}"
         st = sc.stats
         assert st["coalesced_gets"] > 0 and st["replica_hits"] > 0 and st["remote_gets"] > 0
         q.put((rank, "ok", 0))
