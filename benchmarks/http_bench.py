@@ -1,95 +1,186 @@
 #!/usr/bin/env python3
 """HTTP-level parity benchmark (BASELINE.md metrics 1, 2 and 4).
 
-Starts an origin, a shellac_amd proxy (in-process native reactors) with the
-chosen cache backend, warms the cache, then drives keep-alive gzip clients with
-the native ab-equivalent load generator:
+The reference's benchmark is ApacheBench against the proxy with a warm memcached
+cluster (README.md:47-65; benchmarks/run-shellac.sh: ``ab -k -n N -c C -H
+"Accept-Encoding: gzip"``). This runs the same shape with three processes:
 
-  * cache-hit RPS + p50/p99 latency at 10 and 1000 concurrent connections
-    (the reference's README graphs: `ab -k -n 10000 -c 1000 -H "Accept-Encoding: gzip"`);
-  * cache-miss RPS against the local origin (unique URLs);
-  * peak RSS of the process.
+  * the origin — native epoll server in its own process (``utils/origin.py``), serving
+    *incompressible* per-URL bodies of ``--body`` bytes (random bytes seeded by the
+    path), so a cached object is ``--body`` bytes on the wire;
+  * the proxy — shellac_amd's native reactors in THIS process, with the cache backend
+    under test (its peak RSS is reported alone);
+  * the load generator — ``shellac-ab`` in its own process, keep-alive clients issuing
+    Zipf(``--zipf``) requests over ``--objects`` URLs (paths generated natively).
 
-Writes one JSON document (stdout or --out). Example:
-  python benchmarks/http_bench.py --backend hbm --threads 8 --out profiles/http_hbm.json
+Flow: fill pass (every object fetched once through the proxy, so it is cached), then
+for each concurrency a short warm pass and a measured run: hit RPS, p50/p99/p99.9
+latency, the proxy's hit ratio over the run (cache hits / requests — with a working
+set larger than the cache some requests miss and go to the origin), bytes on the wire.
+
+Backends: ``dram`` (host-DRAM cache of ``--dram-mb``), ``hbm`` (HBM shards only),
+``tiered`` (``--l1-mb`` host L1 in front of the HBM shards).
+Example: python benchmarks/http_bench.py --backend tiered --objects 4000000 --l1-mb 256
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import resource
+import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
-from shellac_amd.bench.ab import run  # noqa: E402
 from shellac_amd.server.proxy import Server, make_backend  # noqa: E402
-from shellac_amd.utils.origin import NativeOrigin, Origin  # noqa: E402
+
+# the origin and the load generator never touch the GPU: no torch / HIP runtime in them
+HOST_ONLY = dict(os.environ, SHELLAC_NO_TORCH="1")
+
+
+def rss_mb() -> tuple[float, float]:
+    """(current, peak) resident MiB of this process (the proxy)."""
+    cur = peak = 0.0
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                cur = int(line.split()[1]) / 1024
+            elif line.startswith("VmHWM:"):
+                peak = int(line.split()[1]) / 1024
+    return cur, peak
+
+
+def thread_cpu() -> dict:
+    """CPU seconds of this process's threads grouped by name (reactors, GPU batchers,
+    the rest)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out: dict = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+        except OSError:
+            continue
+        cpu = (int(fields[11]) + int(fields[12])) / tick
+        grp = ("reactors" if name.startswith("shellac-rx") else
+               "gpu_batcher" if name.startswith("shellac-hbm") else "other")
+        out[grp] = out.get(grp, 0.0) + cpu
+    return out
+
+
+def start_origin(body: int, threads: int) -> tuple[subprocess.Popen, int]:
+    p = subprocess.Popen([sys.executable, "-m", "shellac_amd.utils.origin", "--body", str(body),
+                          "--threads", str(threads), "--random-body"],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT,
+                         env=HOST_ONLY)
+    line = p.stdout.readline().split()
+    if len(line) != 2 or line[0] != "port":
+        p.kill()
+        raise RuntimeError(f"origin failed to start: {line}")
+    return p, int(line[1])
+
+
+def load(port: int, n: int, conc: int, threads: int, objects: int, zipf: float, prefix: str,
+         seed: int, timeout: float) -> dict:
+    """One shellac-ab run in its own process; returns its JSON summary."""
+    cmd = [sys.executable, "-m", "shellac_amd.bench.ab", "-n", str(n), "-c", str(conc), "-k",
+           "--threads", str(threads), "--objects", str(objects), "--zipf", str(zipf),
+           "--prefix", prefix, "--suffix", "", "--seed", str(seed), "--timeout", str(timeout),
+           "-H", "Accept-Encoding: gzip", "--json", f"http://127.0.0.1:{port}/"]
+    p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=timeout + 120,
+                       env=HOST_ONLY)
+    if p.returncode != 0:
+        raise RuntimeError(f"load generator failed: {p.stderr[-2000:]}")
+    return json.loads(p.stdout.strip().splitlines()[-1])
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--backend", choices=["dram", "hbm", "none"], default="dram")
+    ap.add_argument("--backend", choices=["dram", "hbm", "tiered", "none"], default="tiered")
     ap.add_argument("--threads", type=int, default=8, help="proxy reactor threads")
-    ap.add_argument("--client-threads", type=int, default=8)
-    ap.add_argument("--objects", type=int, default=1000)
-    ap.add_argument("--body", type=int, default=4096, help="origin body bytes (before gzip)")
-    ap.add_argument("--requests", type=int, default=500000)
-    ap.add_argument("--miss-requests", type=int, default=50000)
-    ap.add_argument("--origin", choices=["native", "python"], default="native",
-                    help="native = C++ epoll origin (csrc/origin.cc); python = http.server")
-    ap.add_argument("--origin-threads", type=int, default=4)
-    ap.add_argument("--depth", type=int, default=1)
-    ap.add_argument("--hbm-gb", type=float, default=4.0)
-    ap.add_argument("--l1-mb", type=int, default=0, help="DRAM L1 in front of hbm (0 = off)")
-    ap.add_argument("--batch-us", type=int, default=0, help="HBM batch linger (0 = natural)")
-    ap.add_argument("--no-filter", action="store_true", help="HBM: no host presence filter")
-    ap.add_argument("--spin-us", type=int, default=50, help="HBM batcher poll before blocking")
+    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--origin-threads", type=int, default=2)
+    ap.add_argument("--objects", type=int, default=1000000)
+    ap.add_argument("--body", type=int, default=4096, help="origin body bytes (incompressible)")
+    ap.add_argument("--zipf", type=float, default=0.99)
+    ap.add_argument("--requests", type=int, default=1000000)
+    ap.add_argument("--conc", type=int, nargs="+", default=[10, 1000])
+    ap.add_argument("--fill-conc", type=int, default=256)
+    ap.add_argument("--dram-mb", type=int, default=256, help="--backend dram: cache MiB")
+    ap.add_argument("--l1-mb", type=int, default=256, help="--backend tiered: host L1 MiB")
+    ap.add_argument("--hbm-gb", type=float, default=0.0,
+                    help="HBM log GiB per GPU (default: 1.25x the working set, >= 4)")
+    ap.add_argument("--hbm-depth", type=int, default=3)
+    ap.add_argument("--evict", choices=["clock", "fifo"], default="clock")
+    ap.add_argument("--batch-us", type=int, default=0)
+    ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
-    if a.origin == "native":
-        origin = NativeOrigin(body_bytes=a.body, threads=a.origin_threads).start()
+    item = a.body + 400  # record + key + response headers, roughly
+    hbm_gb = a.hbm_gb or max(4.0, 1.25 * a.objects * item / (1 << 30))
+    origin, oport = start_origin(a.body, a.origin_threads)
+    rss0, _ = rss_mb()
+    if a.backend == "none":
+        backend = None
+    elif a.backend == "dram":
+        backend = make_backend("dram", dram_mb=a.dram_mb)
     else:
-        origin = Origin(body_bytes=a.body).start()
-    backend = None if a.backend == "none" else make_backend(
-        a.backend, **({"dram_mb": 1024} if a.backend == "dram" else {"gpus": [0], "hbm_gb": a.hbm_gb,
-                                                                       "batch_us": a.batch_us,
-                                                                       "l1_mb": a.l1_mb,
-                                                                       "hbm_filter": not a.no_filter,
-                                                                       "spin_us": a.spin_us}))
-    px = Server([("127.0.0.1", origin.port)], port=0, backend=backend, threads=a.threads,
+        backend = make_backend("hbm", gpus=[0], hbm_gb=hbm_gb, batch_us=a.batch_us,
+                               l1_mb=a.l1_mb if a.backend == "tiered" else 0,
+                               depth=a.hbm_depth, evict=a.evict)
+    px = Server([("127.0.0.1", oport)], port=0, backend=backend, threads=a.threads,
                 client_max_reqs=1 << 30).start()
-    url = f"http://127.0.0.1:{px.port}"
-    hdr = ["Accept-Encoding: gzip"]
-    paths = [f"/gz/obj{i}.html" for i in range(a.objects)]
-    out = {"backend": a.backend + (f"+l1:{a.l1_mb}MB" if a.backend == "hbm" and a.l1_mb else ""), "proxy_threads": a.threads, "objects": a.objects,
-           "body_bytes": a.body, "cpu_count": os.cpu_count(), "origin": a.origin}
-    # warm the cache (every object fetched once from the origin)
-    run(url, len(paths), 8, True, hdr, 1, 1, paths=paths)
-    time.sleep(0.5)
-    for conc in (10, 1000):
-        # a short pass first: the box's first burst of 1000 handshakes takes ~150 ms
-        # (kernel-side, not repeatable); the measured run then reports total and
-        # steady-state (10th-90th percentile completions) throughput
-        run(url, 20000, conc, True, hdr, a.depth, a.client_threads, paths=paths)
-        r = run(url, a.requests, conc, True, hdr, a.depth, a.client_threads, paths=paths)
-        out[f"hit_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
-        print(f"[http] hit c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}, ramp {r['ramp_ms']:.0f} ms) p50 {r['latency_ms']['p50']:.3f} ms "
-              f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
-    # misses: unique gzip URLs, every one forwarded to the origin and filled into the cache
-    for conc in (10, 100):
-        miss_paths = [f"/gz/miss{conc}/{i}.html" for i in range(a.miss_requests)]
-        r = run(url, a.miss_requests, conc, True, hdr, 1, a.client_threads, paths=miss_paths)
-        out[f"miss_c{conc}"] = {k: v for k, v in r.items() if not k.startswith("_")}
-        print(f"[http] miss c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}, ramp {r['ramp_ms']:.0f} ms) p50 {r['latency_ms']['p50']:.3f} ms "
-              f"p99 {r['latency_ms']['p99']:.3f} ms errors {r['errors']}", file=sys.stderr)
-    out["proxy_stats"] = px.stats()
-    out["peak_rss_MB"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
-    px.stop()
-    origin.stop()
+    prefix = "/o/"  # no /gz prefix: the origin sends the incompressible body as is
+    out = {"backend": a.backend, "proxy_threads": a.threads, "objects": a.objects,
+           "body_bytes": a.body, "zipf": a.zipf, "working_set_MB": a.objects * item / 1e6,
+           "dram_mb": a.dram_mb if a.backend == "dram" else None,
+           "l1_mb": a.l1_mb if a.backend == "tiered" else None,
+           "hbm_gb": hbm_gb if a.backend in ("hbm", "tiered") else None,
+           "cpu_count": os.cpu_count(), "processes": "origin | proxy | load generator"}
+    try:
+        t0 = time.time()
+        fill = load(px.port, a.objects, a.fill_conc, a.client_threads, a.objects, 0.0, prefix, 1,
+                    a.timeout)
+        out["fill"] = {"s": time.time() - t0, "rps": fill["rps"], "errors": fill["errors"]}
+        print(f"[http] fill {a.objects} objects: {fill['rps']:.0f} rps", file=sys.stderr)
+        time.sleep(1.0)
+        for conc in a.conc:
+            load(px.port, min(50000, a.requests), conc, a.client_threads, a.objects, a.zipf,
+                 prefix, 100 + conc, a.timeout)
+            s0 = px.stats()
+            c0, l0 = thread_cpu(), os.times()
+            r = load(px.port, a.requests, conc, a.client_threads, a.objects, a.zipf, prefix,
+                     200 + conc, a.timeout)
+            c1, l1 = thread_cpu(), os.times()
+            s1 = px.stats()
+            # where the CPU went during the run: proxy threads and the load generator
+            r["cpu_s"] = {k: round(c1.get(k, 0) - c0.get(k, 0), 2) for k in c1}
+            r["cpu_s"]["load_generator"] = round((l1.children_user + l1.children_system) -
+                                                 (l0.children_user + l0.children_system), 2)
+            reqs = s1["requests"] - s0["requests"]
+            hits = s1["cache_hits"] - s0["cache_hits"]
+            r["hit_ratio"] = hits / max(reqs, 1)
+            r["origin_requests"] = s1["upstream_requests"] - s0["upstream_requests"]
+            out[f"c{conc}"] = r
+            lm = r["latency_ms"]
+            print(f"[http] {a.backend} c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}) "
+                  f"hit ratio {r['hit_ratio']:.4f} p50 {lm['p50']:.3f} ms p99 {lm['p99']:.3f} ms "
+                  f"{r['transfer_MBps']:.0f} MB/s errors {r['errors']} cpu {r['cpu_s']} "
+                  f"elapsed {r['elapsed_s']:.2f}s", file=sys.stderr)
+        st = px.stats()
+        out["proxy_stats"] = st
+        cur, peak = rss_mb()
+        out["proxy_rss_MB"] = {"before_proxy": rss0, "end": cur, "peak": peak,
+                               "peak_minus_baseline": peak - rss0}
+    finally:
+        px.stop()
+        origin.stdin.close()
+        origin.wait(timeout=30)
     js = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as f:

@@ -22,10 +22,11 @@ def core():
     global _core
     if _core is not None:
         return _core
-    try:
-        import torch  # noqa: F401  (one HIP runtime per process; see module doc)
-    except ImportError:
-        pass
+    if not os.environ.get("SHELLAC_NO_TORCH"):  # host-only helpers (load generator, origin)
+        try:
+            import torch  # noqa: F401  (one HIP runtime per process; see module doc)
+        except ImportError:
+            pass
     try:
         _core = _try_import()
     except ImportError as first:

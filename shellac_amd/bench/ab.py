@@ -21,7 +21,12 @@ from .._native import core
 
 def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool = True,
         headers: Sequence[str] = (), depth: int = 1, threads: int = 1,
-        paths: Optional[Sequence[str]] = None, method: str = "GET", timeout_s: float = 120.0) -> dict:
+        paths: Optional[Sequence[str]] = None, method: str = "GET", timeout_s: float = 120.0,
+        objects: int = 0, zipf_s: float = 0.99, path_prefix: str = "/obj/",
+        path_suffix: str = ".html", seed: int = 1) -> dict:
+    """``objects`` > 0: request paths are generated natively — ``path_prefix + id +
+    path_suffix`` with ids drawn Zipf(``zipf_s``) over ``objects`` objects, or in order
+    (a cache-fill pass) when ``zipf_s`` is 0."""
     u = urlparse(url)
     host = u.hostname or "127.0.0.1"
     port = u.port or 80
@@ -30,7 +35,8 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
         path += "?" + u.query
     res = core().run_load(host, port, list(paths) if paths else [path], int(requests),
                           int(concurrency), int(depth), int(threads), bool(keepalive),
-                          list(headers), method, float(timeout_s))
+                          list(headers), method, float(timeout_s), int(objects), float(zipf_s),
+                          path_prefix, path_suffix, int(seed))
     lat = np.asarray(res["latency"]) * 1e3
     done = int(res["completed"])
     el = float(res["elapsed_s"])
@@ -61,6 +67,7 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
             "p50": float(np.percentile(lat, 50)) if done else 0.0,
             "p90": float(np.percentile(lat, 90)) if done else 0.0,
             "p99": float(np.percentile(lat, 99)) if done else 0.0,
+            "p999": float(np.percentile(lat, 99.9)) if done else 0.0,
             "max": float(lat.max()) if done else 0.0,
         },
         "_start": res["start"],
@@ -90,10 +97,19 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--depth", type=int, default=1, help="pipelined requests per connection")
     p.add_argument("--threads", type=int, default=1)
     p.add_argument("--json", action="store_true")
+    p.add_argument("--objects", type=int, default=0,
+                   help="generate paths over this many objects (prefix + id + suffix)")
+    p.add_argument("--zipf", type=float, default=0.99, help="popularity skew (0 = in order)")
+    p.add_argument("--prefix", default="/obj/")
+    p.add_argument("--suffix", default=".html")
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--timeout", type=float, default=120.0)
     p.add_argument("url")
     a = p.parse_args(argv)
     t0 = time.time()
-    r = run(a.url, a.n, a.c, a.k, a.H, a.depth, a.threads)
+    r = run(a.url, a.n, a.c, a.k, a.H, a.depth, a.threads, timeout_s=a.timeout,
+            objects=a.objects, zipf_s=a.zipf, path_prefix=a.prefix, path_suffix=a.suffix,
+            seed=a.seed)
     if a.g:
         write_gnuplot(a.g, r, t0)
     pub = {k: v for k, v in r.items() if not k.startswith("_")}

@@ -63,73 +63,47 @@ int DigestRing::owner(const Digest& d, uint64_t alive) const {
 // =====================================================================================
 // DRAM
 // =====================================================================================
-DramBackend::DramBackend(uint64_t bytes, uint32_t max_item, int stripes) : epoch_(wall_s()) {
-  SH_CHECK(stripes > 0, "stripes");
-  const uint64_t per = std::max<uint64_t>(bytes / stripes / 16 * 16, 1ull << 20);
-  // ~1 KiB average objects at <= 50% slot load
-  uint64_t nb = 2;
-  while (nb * 4 * 512 < per) nb *= 2;
-  // values carry their key (keyed.h): room for a URL on top of max_item
-  const uint32_t mi = (uint32_t)std::min<uint64_t>((uint64_t)max_item + 4096, per / 4);
-  for (int i = 0; i < stripes; ++i) shards_.emplace_back(new HostCache(per, nb, mi));
-}
+DramBackend::DramBackend(uint64_t bytes, uint32_t max_item, int stripes)
+    : cache_(bytes, max_item, stripes), epoch_(wall_s()) {}
 
 uint32_t DramBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
-// Values are stored keyed ([klen | key | payload], keyed.h): a hit whose stored key is
-// not the requested one (a digest collision) is a miss.
 void DramBackend::get(const std::string& key, const Digest& d, Executor*, GetCallback done) {
-  auto v = std::make_shared<std::string>();
-  uint32_t flags = 0, expire = 0;
   const uint32_t t = now();
-  size_t po = 0;
-  if (shard(d).get_one(d, v.get(), &flags, t, &expire)) {
-    if (keyed_match(v->data(), v->size(), key, &po)) {
-      Bytes b(std::shared_ptr<const std::string>(std::move(v)));
-      done(true, CacheValue{b.sub(po, b.size() - po), flags, expire ? (int64_t)expire - t : 0});
-      return;
-    }
-    key_mismatch_.fetch_add(1, std::memory_order_relaxed);
+  CacheValue v;
+  uint32_t expire = 0;
+  if (cache_.get(key, d, t, &v.data, &v.flags, &expire)) {
+    v.ttl_left = expire ? (int64_t)expire - t : 0;
+    done(true, std::move(v));
+  } else {
+    done(false, CacheValue{});
   }
-  done(false, CacheValue{});
 }
 
 void DramBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
                       uint32_t ttl_s) {
-  if (!value || key.size() > kMaxKeyedKey) return;
+  if (!value) return;
   const uint32_t n = now();
-  std::string kv(keyed_size(key.size(), value->size()), '\0');
-  write_keyed(reinterpret_cast<uint8_t*>(&kv[0]), key, value->data(), value->size());
-  shard(d).set_one(d, reinterpret_cast<const uint8_t*>(kv.data()), (uint32_t)kv.size(), flags,
-                   ttl_s ? n + ttl_s : 0, n);
+  cache_.set(key, d, value->data(), value->size(), flags, ttl_s ? n + ttl_s : 0, n);
 }
 
-void DramBackend::del(const std::string&, const Digest& d, Executor*, DelCallback done) {
-  uint8_t found = 0;
-  shard(d).remove(&d, 1, &found, now());
-  if (done) done(found != 0);
+void DramBackend::del(const std::string& key, const Digest& d, Executor*, DelCallback done) {
+  const bool found = cache_.del(key, d, now());
+  if (done) done(found);
 }
 
-void DramBackend::flush() {
-  for (auto& s : shards_) s->flush();
-}
+void DramBackend::flush() { cache_.clear(); }
 
 void DramBackend::stats(StatList* out) {
-  CacheCounters t{};
-  for (auto& s : shards_) {
-    const CacheCounters c = s->counters();
-    t.get_ops += c.get_ops; t.get_hits += c.get_hits; t.set_ops += c.set_ops;
-    t.set_bytes += c.set_bytes; t.set_evicted += c.set_evicted; t.del_ops += c.del_ops;
-    t.reinserted += c.reinserted;
-  }
-  out->emplace_back("cache_get_ops", t.get_ops);
-  out->emplace_back("cache_get_hits", t.get_hits);
-  out->emplace_back("cache_set_ops", t.set_ops);
-  out->emplace_back("cache_set_bytes", t.set_bytes);
-  out->emplace_back("cache_evicted", t.set_evicted);
-  out->emplace_back("cache_reinserted", t.reinserted);
-  out->emplace_back("cache_shards", shards_.size());
-  out->emplace_back("cache_key_mismatch", key_mismatch_.load());
+  const ObjectCacheStats t = cache_.stats();
+  out->emplace_back("cache_get_ops", t.gets);
+  out->emplace_back("cache_get_hits", t.hits);
+  out->emplace_back("cache_set_ops", t.sets);
+  out->emplace_back("cache_evicted", t.evictions);
+  out->emplace_back("cache_expired", t.expired);
+  out->emplace_back("cache_objects", t.objects);
+  out->emplace_back("cache_bytes", t.bytes);
+  out->emplace_back("cache_key_mismatch", t.key_mismatch);
 }
 
 // =====================================================================================

@@ -32,6 +32,7 @@
 #include "host_cache.h"
 #include "ketama.h"
 #include "net.h"
+#include "object_cache.h"
 #include "presence_filter.h"
 #include "stream_buf.h"
 
@@ -92,9 +93,11 @@ class DigestRing {
   std::vector<std::pair<uint32_t, int>> pts_;
 };
 
+// Host-DRAM tier: refcounted immutable objects (object_cache.h) — a hit is shared, not
+// copied, and the full key is checked; CLOCK eviction by bytes.
 class DramBackend : public CacheBackend {
  public:
-  DramBackend(uint64_t bytes, uint32_t max_item, int stripes = 16);
+  DramBackend(uint64_t bytes, uint32_t max_item, int stripes = 64);
   void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
   void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
            uint32_t ttl_s) override;
@@ -105,10 +108,8 @@ class DramBackend : public CacheBackend {
   uint32_t now() const;
 
  private:
-  HostCache& shard(const Digest& d) { return *shards_[(d.hi >> 17) % shards_.size()]; }
-  std::vector<std::unique_ptr<HostCache>> shards_;
+  ObjectCache cache_;
   double epoch_;
-  std::atomic<uint64_t> key_mismatch_{0};
 };
 
 struct HbmBackendConfig {

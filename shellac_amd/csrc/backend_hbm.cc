@@ -16,6 +16,8 @@
 // A hit never touches a host copy: the GPU writes [ItemHeader | u16 klen | key | payload]
 // into pinned memory, the batcher checks the key bytes and hands out a slice of the
 // payload that keeps the arena alive until the last client write completes.
+#include <pthread.h>
+
 #include <chrono>
 #include <cstdio>
 
@@ -403,6 +405,8 @@ bool HbmBackend::Dev::take_batch(std::vector<Req>* out, bool* do_flush, bool* re
 void HbmBackend::Dev::loop() {
   const HbmBackendConfig& cfg = be->cfg_;
   (void)hipSetDevice(device);
+  const std::string nm = "shellac-hbm" + std::to_string(device);
+  pthread_setname_np(pthread_self(), nm.c_str());
   std::vector<Req> batch;
   for (;;) {
     bool worked = false;

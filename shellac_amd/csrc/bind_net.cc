@@ -75,8 +75,15 @@ void bind_net(py::module_& m) {
   m.def("run_load", [](const std::string& host, uint16_t port, std::vector<std::string> paths,
                        int64_t requests, int concurrency, int depth, int threads, bool keepalive,
                        std::vector<std::string> headers, const std::string& method,
-                       double timeout_s) {
+                       double timeout_s, int64_t objects, double zipf_s,
+                       const std::string& path_prefix, const std::string& path_suffix,
+                       uint64_t seed) {
     LoadConfig c;
+    c.objects = objects;
+    c.zipf_s = zipf_s;
+    c.path_prefix = path_prefix;
+    c.path_suffix = path_suffix;
+    c.seed = seed;
     c.host = host;
     c.port = port;
     c.paths = std::move(paths);
@@ -119,7 +126,9 @@ void bind_net(py::module_& m) {
   }, py::arg("host"), py::arg("port"), py::arg("paths"), py::arg("requests"),
      py::arg("concurrency"), py::arg("depth") = 1, py::arg("threads") = 1,
      py::arg("keepalive") = true, py::arg("headers") = std::vector<std::string>{},
-     py::arg("method") = "GET", py::arg("timeout_s") = 60.0);
+     py::arg("method") = "GET", py::arg("timeout_s") = 60.0, py::arg("objects") = 0,
+     py::arg("zipf_s") = 0.99, py::arg("path_prefix") = "/obj/",
+     py::arg("path_suffix") = ".html", py::arg("seed") = 1);
 
   m.def("md5_hex", [](py::bytes b) { return md5_hex(std::string(b)); });
 
@@ -287,17 +296,19 @@ void bind_net(py::module_& m) {
 
   py::class_<NativeOrigin>(m, "NativeOrigin")
       .def(py::init([](uint16_t port, int threads, int body_bytes, int gzip_level,
-                       const std::string& host) {
+                       const std::string& host, bool random_body) {
              OriginConfig c;
              c.host = host;
              c.port = port;
              c.threads = threads;
              c.body_bytes = body_bytes;
              c.gzip_level = gzip_level;
+             c.random_body = random_body;
              return new NativeOrigin(c);
            }),
            py::arg("port") = 0, py::arg("threads") = 2, py::arg("body_bytes") = 1024,
-           py::arg("gzip_level") = 1, py::arg("host") = "127.0.0.1")
+           py::arg("gzip_level") = 1, py::arg("host") = "127.0.0.1",
+           py::arg("random_body") = false)
       .def("start", &NativeOrigin::start)
       .def("stop", &NativeOrigin::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &NativeOrigin::port)

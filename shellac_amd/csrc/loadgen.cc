@@ -8,10 +8,14 @@
 // ab-style "-g" per-request TSV.
 #include "loadgen.h"
 
+#include <strings.h>
 #include <sys/epoll.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <deque>
 #include <thread>
@@ -21,13 +25,90 @@
 namespace shellac {
 
 namespace {
+// Response framing without copying bodies: the head is collected and scanned for the
+// status, Content-Length and Connection; the body is skipped by count. A response the
+// fast path cannot frame (chunked, or no length) switches the connection to the full
+// HttpParser. The load generator then costs a fraction of the proxy it measures.
+struct FastFramer {
+  std::string head;      // bytes of the current head (until CRLFCRLF)
+  uint64_t body_left = 0;
+  bool in_body = false;
+  int status = 0;
+  bool keep_alive = true;
+
+  // Consume from [p, p+n); returns bytes used, sets *done when a response completed,
+  // *fallback when the response needs the full parser (nothing consumed then).
+  size_t feed(const char* p, size_t n, bool* done, bool* fallback) {
+    *done = *fallback = false;
+    size_t used = 0;
+    if (!in_body) {
+      // append up to the end of the head
+      const size_t start = head.size() >= 3 ? head.size() - 3 : 0;
+      head.append(p, n);
+      const size_t e = head.find("\r\n\r\n", start);
+      if (e == std::string::npos) return n;
+      used = n - (head.size() - (e + 4));
+      head.resize(e + 4);
+      if (!parse_head()) {
+        *fallback = true;
+        return 0;
+      }
+      in_body = true;
+    }
+    const size_t take = (size_t)std::min<uint64_t>(body_left, n - used);
+    body_left -= take;
+    used += take;
+    if (body_left == 0) {
+      *done = true;
+      in_body = false;
+      head.clear();
+    }
+    return used;
+  }
+
+  bool parse_head() {
+    // "HTTP/1.1 200 ..."
+    if (head.size() < 12 || head.compare(0, 5, "HTTP/") != 0) return false;
+    status = std::atoi(head.c_str() + 9);
+    bool have_len = false;
+    keep_alive = head.compare(5, 3, "1.0") != 0;
+    size_t pos = head.find("\r\n") + 2;
+    while (pos + 2 < head.size()) {
+      const size_t eol = head.find("\r\n", pos);
+      const size_t colon = head.find(':', pos);
+      if (colon != std::string::npos && colon < eol) {
+        const size_t nl = colon - pos;
+        const char* v = head.c_str() + colon + 1;
+        if (nl == 14 && strncasecmp(head.c_str() + pos, "content-length", 14) == 0) {
+          body_left = std::strtoull(v, nullptr, 10);
+          have_len = true;
+        } else if (nl == 17 && strncasecmp(head.c_str() + pos, "transfer-encoding", 17) == 0) {
+          return false;  // chunked: the full parser frames it
+        } else if (nl == 10 && strncasecmp(head.c_str() + pos, "connection", 10) == 0) {
+          const std::string val(v, eol - colon - 1);
+          if (strcasestr(val.c_str(), "close")) keep_alive = false;
+          else if (strcasestr(val.c_str(), "keep-alive")) keep_alive = true;
+        }
+      }
+      pos = eol + 2;
+    }
+    if (!have_len) {
+      if (status == 204 || status == 304 || status / 100 == 1) body_left = 0;
+      else return false;
+    }
+    return true;
+  }
+};
+
 struct LgConn {
   int fd = -1;
   bool connected = false;
   std::string out;
   size_t out_off = 0;
   std::deque<double> sent;  // send timestamps of in-flight requests
-  std::unique_ptr<HttpParser> parser;
+  std::unique_ptr<HttpParser> parser;  // full parser (fallback framing)
+  FastFramer fast;
+  bool use_parser = false;
   size_t path_idx = 0;
   bool out_armed = true;    // EPOLLOUT in the interest set
 };
@@ -35,7 +116,7 @@ struct LgConn {
 
 LoadResult run_load(const LoadConfig& cfg) {
   SH_CHECK(cfg.concurrency > 0 && cfg.threads > 0 && cfg.requests > 0, "bad load config");
-  SH_CHECK(!cfg.paths.empty(), "no paths");
+  SH_CHECK(!cfg.paths.empty() || cfg.objects > 0, "no paths");
   const Addr addr = resolve(cfg.host + ":" + std::to_string(cfg.port), cfg.port);
   std::atomic<int64_t> issued{0};
   std::vector<std::vector<LoadSample>> per_thread(cfg.threads);
@@ -44,18 +125,52 @@ LoadResult run_load(const LoadConfig& cfg) {
   const double t_start = now_s();
 
   // serialized requests, one per path (built once)
+  std::string tail = " HTTP/1.1\r\nHost: " + cfg.host + "\r\n";
+  if (cfg.keepalive) tail += "Connection: keep-alive\r\n";
+  for (const auto& h : cfg.headers) tail += h + "\r\n";
+  tail += "\r\n";
   std::vector<std::string> reqs;
-  for (const auto& path : cfg.paths) {
-    std::string r = cfg.method + " " + path + " HTTP/1.1\r\nHost: " + cfg.host + "\r\n";
-    if (cfg.keepalive) r += "Connection: keep-alive\r\n";
-    for (const auto& h : cfg.headers) r += h + "\r\n";
-    r += "\r\n";
-    reqs.push_back(std::move(r));
+  for (const auto& path : cfg.paths) reqs.push_back(cfg.method + " " + path + tail);
+  // generated paths: Zipf inverse-CDF table over popularity ranks, ranks -> ids by
+  // rank * P mod N (P prime and not a divisor of N: a bijection)
+  const int64_t nobj = cfg.objects;
+  std::vector<double> cdf;
+  uint64_t mult = 1;
+  if (nobj > 0 && cfg.zipf_s > 0) {
+    cdf.resize((size_t)nobj);
+    double acc = 0;
+    for (int64_t r = 0; r < nobj; ++r) {
+      acc += std::pow((double)(r + 1), -cfg.zipf_s);
+      cdf[(size_t)r] = acc;
+    }
+    for (auto& v : cdf) v /= acc;
+    mult = 2654435761ull;
+    while ((uint64_t)nobj % mult == 0) mult += 2;
   }
-  auto req_bytes = [&](size_t i) -> const std::string& { return reqs[i % reqs.size()]; };
+  auto gen_req = [&](int64_t k, uint64_t* rng, std::string* out) {
+    int64_t id;
+    if (cdf.empty()) {
+      id = k % nobj;
+    } else {
+      uint64_t& x = *rng;
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      const double u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
+      const int64_t r = std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin();
+      id = (int64_t)(((unsigned __int128)std::min<int64_t>(r, nobj - 1) * mult) % (uint64_t)nobj);
+    }
+    *out += cfg.method;
+    *out += ' ';
+    *out += cfg.path_prefix;
+    *out += std::to_string(id);
+    *out += cfg.path_suffix;
+    *out += tail;
+  };
 
   auto worker = [&](int tid) {
     const int nconn = cfg.concurrency / cfg.threads + (tid < cfg.concurrency % cfg.threads ? 1 : 0);
+    uint64_t rng = (cfg.seed + 1) * 0x9E3779B97F4A7C15ull ^ (uint64_t)(tid + 1) * 0xD1B54A32D192ED03ull;
     const int ep = epoll_create1(EPOLL_CLOEXEC);
     std::vector<LgConn> conns(nconn);
     auto& samples = per_thread[tid];
@@ -93,7 +208,8 @@ LoadResult run_load(const LoadConfig& cfg) {
           if (k >= cfg.requests) break;
         } while (!issued.compare_exchange_weak(k, k + 1));
         if (k >= cfg.requests) break;
-        c.out += req_bytes((size_t)k);
+        if (nobj > 0) gen_req(k, &rng, &c.out);
+        else c.out += reqs[(size_t)k % reqs.size()];
         c.sent.push_back(0);  // timestamp set at send
       }
     };
@@ -159,19 +275,42 @@ LoadResult run_load(const LoadConfig& cfg) {
               const char* p = buf;
               size_t left = (size_t)r;
               while (left > 0 && !c.sent.empty()) {
-                const size_t used = c.parser->parse(p, left);
+                bool complete = false;
+                int st = 0;
+                bool ka = true;
+                size_t used = 0;
+                if (!c.use_parser) {
+                  bool fallback = false;
+                  // the framer keeps the partial head; on fallback replay it to the parser
+                  const std::string pending = c.fast.head;
+                  used = c.fast.feed(p, left, &complete, &fallback);
+                  if (fallback) {
+                    c.use_parser = true;
+                    const size_t hp = c.parser->parse(pending.data(), pending.size());
+                    (void)hp;
+                    c.fast = FastFramer();
+                    continue;
+                  }
+                  st = c.fast.status;
+                  ka = c.fast.keep_alive;
+                } else {
+                  used = c.parser->parse(p, left);
+                  if (c.parser->error()) { dead = true; break; }
+                  complete = c.parser->message_complete();
+                  if (complete) {
+                    st = c.parser->status();
+                    ka = c.parser->keep_alive();
+                    c.parser->reset();
+                  }
+                }
                 p += used;
                 left -= used;
-                if (c.parser->error()) { dead = true; break; }
-                if (c.parser->message_complete()) {
+                if (complete) {
                   const double t = now_s();
-                  const int st = c.parser->status();
                   samples.push_back(LoadSample{c.sent.front() - t_start, t - c.sent.front(), st});
                   if (st < 200 || st >= 300) non2xx++;
                   c.sent.pop_front();
-                  const bool ka = c.parser->keep_alive() && cfg.keepalive;
-                  c.parser->reset();
-                  if (!ka) { dead = true; break; }
+                  if (!(ka && cfg.keepalive)) { dead = true; break; }
                 } else if (used == 0) {
                   break;
                 }

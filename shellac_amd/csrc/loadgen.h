@@ -20,6 +20,15 @@ struct LoadConfig {
   int threads = 1;
   bool keepalive = true;             // ab -k
   double timeout_s = 60;
+  // Generated request paths instead of `paths`: object ids 0..objects-1 as
+  // path_prefix + id + path_suffix, drawn Zipf(zipf_s) (popularity ranks scattered over
+  // ids by a fixed bijection) or, with zipf_s == 0, sequentially (request k -> id k mod
+  // objects: a cache-fill pass).
+  int64_t objects = 0;
+  double zipf_s = 0.99;
+  std::string path_prefix = "/obj/";
+  std::string path_suffix = ".html";
+  uint64_t seed = 1;
 };
 
 struct LoadSample {

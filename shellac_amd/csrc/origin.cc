@@ -6,6 +6,8 @@
 #include <sys/eventfd.h>
 #include <zlib.h>
 
+#include <algorithm>
+#include <cstring>
 #include <unordered_map>
 
 #include "common.h"
@@ -154,7 +156,20 @@ void NativeOrigin::loop(int lfd) {
       const bool http10 = c.in.compare(sp2 + 1, 8, "HTTP/1.0") == 0;
       const bool close_req = header_has(head, hlen, "connection", "close") ||
                              (http10 && !header_has(head, hlen, "connection", "keep-alive"));
-      std::string body = "<html>" + path + " #1 " + filler + "</html>\n";
+      std::string body;
+      if (cfg_.random_body) {
+        body.resize((size_t)cfg_.body_bytes);
+        uint64_t x = 0xcbf29ce484222325ull;  // FNV-1a of the path seeds a xorshift stream
+        for (unsigned char ch : path) x = (x ^ ch) * 0x100000001b3ull;
+        for (size_t k = 0; k < body.size(); k += 8) {
+          x ^= x << 13;
+          x ^= x >> 7;
+          x ^= x << 17;
+          std::memcpy(&body[k], &x, std::min<size_t>(8, body.size() - k));
+        }
+      } else {
+        body = "<html>" + path + " #1 " + filler + "</html>\n";
+      }
       std::string extra;
       if (path.compare(0, 3, "/gz") == 0 && header_has(head, hlen, "accept-encoding", "gzip")) {
         body = gzip_bytes(body, cfg_.gzip_level);

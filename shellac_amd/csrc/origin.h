@@ -18,6 +18,9 @@ struct OriginConfig {
   int threads = 2;       // one epoll loop + SO_REUSEPORT listener each
   int body_bytes = 1024; // filler bytes per body, like utils/origin.py
   int gzip_level = 1;    // /gz* paths are gzip-encoded when the client accepts it
+  // incompressible bodies: body_bytes of pseudo-random bytes seeded by the path (the same
+  // object always has the same body), so cached objects are body_bytes on the wire
+  bool random_body = false;
 };
 
 class NativeOrigin {

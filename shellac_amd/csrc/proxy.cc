@@ -3,6 +3,7 @@
 
 #include <poll.h>
 #include <sys/epoll.h>
+#include <pthread.h>
 #include <sys/eventfd.h>
 #include <sys/timerfd.h>
 #include <sys/uio.h>
@@ -65,7 +66,10 @@ struct Slot {
   bool streaming = false;  // response bytes flow out before the response is complete
   uint64_t stream_up = 0;  // id of the upstream feeding a streamed response
   bool close_after = false;
-  std::string fwd;  // serialized request for the miss path
+  std::string fwd;  // serialized request for the miss path (built on the first forward)
+  // The parsed request, kept (not serialized) while the cache answers: a hit never pays
+  // for re-serializing a request it does not forward. Returned to the reactor's pool.
+  std::unique_ptr<HttpParser> req;
   std::string key;
   Digest d{};
   bool lookup = false, head = false, client_gzip = false;
@@ -87,7 +91,7 @@ struct Conn {
 struct Upstream;
 
 struct Client : Conn {
-  HttpParser req{true};
+  std::unique_ptr<HttpParser> req = std::make_unique<HttpParser>(true);
   std::deque<std::unique_ptr<Slot>> slots;
   uint64_t next_seq = 1;
   Upstream* up = nullptr;
@@ -144,6 +148,10 @@ class Reactor : public Executor {
   void on_request(Client* c);
   void on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v);
   void forward(Client* c, Slot* s);
+  static std::string upstream_request(HttpParser& q);
+  std::unique_ptr<HttpParser> take_parser();
+  void give_parser(std::unique_ptr<HttpParser> p);
+  std::vector<std::unique_ptr<HttpParser>> parser_pool_;
   void on_upstream_response(Upstream* u);
   void rewrite_response_headers(HttpParser& r);
   void pause_input(Conn* c, bool paused);
@@ -353,10 +361,10 @@ void Reactor::on_client(Client* c, uint32_t ev) {
         const char* p = buf_.data();
         size_t n = (size_t)r;
         while (n > 0 && !c->dead && !c->closing) {
-          const size_t used = c->req.parse(p, n);
+          const size_t used = c->req->parse(p, n);
           p += used;
           n -= used;
-          if (c->req.error()) {
+          if (c->req->error()) {
             bad_requests++;
             auto s = std::make_unique<Slot>();
             s->seq = c->next_seq++;
@@ -369,10 +377,11 @@ void Reactor::on_client(Client* c, uint32_t ev) {
             c->closing = true;
             break;
           }
-          if (c->req.message_complete()) {
+          if (c->req->message_complete()) {
             on_request(c);
             if (c->dead) return;
-            c->req.reset();
+            if (c->req) c->req->reset();
+            else c->req = take_parser();  // the request moved into its slot
           } else if (used == 0) {
             break;
           }
@@ -398,7 +407,7 @@ void Reactor::on_client(Client* c, uint32_t ev) {
 }
 
 void Reactor::on_request(Client* c) {
-  HttpParser& q = c->req;
+  HttpParser& q = *c->req;
   c->nreq++;
   requests++;
   const std::string url = q.url();
@@ -428,14 +437,10 @@ void Reactor::on_request(Client* c) {
   const std::string* host = q.header("host");
   s->key = cfg_.key_host && host ? *host + url : url;  // reference key: URL (Server.py:327)
   s->d = digest_bytes(reinterpret_cast<const uint8_t*>(s->key.data()), s->key.size());
-  // upstream request: force gzip (Server.py:358), pool the connection
-  q.set_header("accept-encoding", "gzip");
-  q.remove_header("proxy-connection");
-  q.remove_header("keep-alive");
-  q.set_header("connection", "keep-alive");
-  s->fwd = q.serialize();
   s->lookup = px_->cfg_.cache_enabled &&
               (cfg_.policy == "reference" || method == "GET") && !q.header("authorization");
+  if (s->lookup) s->req = std::move(c->req);  // serialized only if the cache misses
+  else s->fwd = upstream_request(q);
   c->slots.push_back(std::move(s));
   if (sp->lookup) {
     const uint64_t cid = c->id, seq = sp->seq;
@@ -495,6 +500,7 @@ static Bytes with_connection_close(const Bytes& obj) {
 }
 
 void Reactor::complete_slot(Client* c, Slot* s, Bytes data) {
+  if (s->req) give_parser(std::move(s->req));
   if (s->close_after && data) data = with_connection_close(data);
   s->out.write_shared(std::move(data));
   s->out.close();
@@ -656,8 +662,35 @@ Upstream* Reactor::pick_upstream(Client* c) {
   return nullptr;
 }
 
+// The request as forwarded upstream: gzip forced (Server.py:358), hop-by-hop headers
+// dropped, the upstream connection kept alive for the pool.
+std::string Reactor::upstream_request(HttpParser& q) {
+  q.set_header("accept-encoding", "gzip");
+  q.remove_header("proxy-connection");
+  q.remove_header("keep-alive");
+  q.set_header("connection", "keep-alive");
+  return q.serialize();
+}
+
+std::unique_ptr<HttpParser> Reactor::take_parser() {
+  if (parser_pool_.empty()) return std::make_unique<HttpParser>(true);
+  auto p = std::move(parser_pool_.back());
+  parser_pool_.pop_back();
+  return p;
+}
+
+void Reactor::give_parser(std::unique_ptr<HttpParser> p) {
+  if (!p || parser_pool_.size() >= 4096) return;
+  p->reset();
+  parser_pool_.push_back(std::move(p));
+}
+
 void Reactor::forward(Client* c, Slot* s) {
   s->attempts++;
+  if (s->fwd.empty() && s->req) {
+    s->fwd = upstream_request(*s->req);
+    give_parser(std::move(s->req));
+  }
   Upstream* u = pick_upstream(c);
   if (!u) {
     complete_slot(c, s, std::make_shared<const std::string>(simple_response(
@@ -1122,9 +1155,13 @@ void Proxy::start() {
     const int fd = i == 0 ? first : listen_tcp(cfg_.bind, port_, true, cfg_.backlog);
     reactors_.emplace_back(new Reactor(this, i, fd));
   }
-  for (auto& r : reactors_) {
-    Reactor* rp = r.get();
-    threads_.emplace_back([rp] { rp->loop(); });
+  for (size_t i = 0; i < reactors_.size(); ++i) {
+    Reactor* rp = reactors_[i].get();
+    threads_.emplace_back([rp, i] {
+      const std::string nm = "shellac-rx" + std::to_string(i);  // per-thread CPU accounting
+      pthread_setname_np(pthread_self(), nm.c_str());
+      rp->loop();
+    });
   }
   if (!cfg_.health_path.empty()) health_th_ = std::thread([this] { health_loop(); });
 }

@@ -123,11 +123,12 @@ class NativeOrigin:
     miss-path RPS measures the proxy, not Python's ``http.server``."""
 
     def __init__(self, port: int = 0, body_bytes: int = 1024, threads: int = 2,
-                 gzip_level: int = 1):
+                 gzip_level: int = 1, random_body: bool = False):
         from .._native import core
 
+        # random_body: incompressible per-path bodies of exactly body_bytes
         self._o = core().NativeOrigin(port=port, threads=threads, body_bytes=body_bytes,
-                                      gzip_level=gzip_level)
+                                      gzip_level=gzip_level, random_body=random_body)
         self.port = self._o.port
 
     @property
@@ -140,3 +141,31 @@ class NativeOrigin:
 
     def stop(self) -> None:
         self._o.stop()
+
+
+def serve_native_origin(argv=None) -> int:
+    """Run a NativeOrigin in its own process (benchmarks: the origin's CPU and memory stay
+    out of the proxy process). Prints ``port <n>`` and serves until stdin closes."""
+    import argparse
+    import sys
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--body", type=int, default=4096)
+    ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--random-body", action="store_true")
+    ap.add_argument("--gzip-level", type=int, default=1)
+    a = ap.parse_args(argv)
+    o = NativeOrigin(body_bytes=a.body, threads=a.threads, gzip_level=a.gzip_level,
+                     random_body=a.random_body).start()
+    print(f"port {o.port}", flush=True)
+    try:
+        sys.stdin.read()
+    finally:
+        o.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(serve_native_origin())
