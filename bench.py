@@ -75,6 +75,12 @@ def parse():
                     help="functional rehearsal of the N-rank GPU step on ONE GPU: every rank on "
                          "cuda:0, collectives bounced through gloo (RCCL refuses two ranks on "
                          "one device); never a performance number")
+    ap.add_argument("--edge", choices=["device", "host"], default="device",
+                    help="host: the product edge — GET digests and SET payloads in pinned host "
+                         "memory, responses gathered into pinned host memory over PCIe "
+                         "(as the proxy's HBM tier); one rank")
+    ap.add_argument("--evict", choices=["clock", "fifo"], default="clock",
+                    help="value-log eviction policy of the shards")
     ap.add_argument("--batches", type=int, default=16,
                     help="distinct pre-generated GET/SET batch pairs cycled through the steps "
                          "(16 x 16 MiB of digests + 16 SET payload sets: more than the 256 MB MALL)")
@@ -222,7 +228,7 @@ def main():
     # the simulated rank's one shard stands in for all N owners: give it N logs' worth
     # (8 x 16 GiB still fits one MI355X's 288 GB) so the key space does not wrap it
     log_bytes = int(args.log_gb * (sim or 1) * (1 << 30)) // 16 * 16
-    shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev)
+    shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev, evict=args.evict)
     replica = None
     if world > 1 and args.replicate > 0:
         rnb = 1
@@ -267,6 +273,20 @@ def main():
         del seen
         log(rank, f"[bench] replicated {nrep} hot objects on every rank")
     shard.reserve(max(args.sets * 2, chunk))
+    host_edge = args.edge == "host"
+    if host_edge:
+        if real_world > 1 or sim or dev.type != "cuda":
+            raise SystemExit("--edge host runs one GPU rank")
+        from shellac_amd.models.sharded_cache import SetBatch
+
+        def pin(t):
+            return None if t is None else t.cpu().pin_memory()
+
+        pool_h = pin(wl.pool)
+        gets = [pin(g) for g in gets]
+        sets = [SetBatch(pin(b.keys), pool_h, pin(b.val_off), pin(b.vlen), pin(b.flags),
+                         pin(b.expire)) for b in sets]
+        sc.host_edge = True
 
     def step(i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
@@ -306,7 +326,9 @@ def main():
     sync()
     before = shard.counters()
     st0 = dict(sc.stats)
+    gb0 = sc.gathered_bytes
     elapsed, intervals, res = timed(args.steps, args.warmup)
+    gathered = sc.gathered_bytes - gb0
     last_batch = (args.warmup + args.steps - 1) % P
     after = shard.counters()
     # owner-shard counters cover the GETs that left the replica tier; replica hits
@@ -331,10 +353,12 @@ def main():
         bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
         log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
         # every hit of the whole last batch: its record's header names the requested digest
-        keys_last = gets[last_batch]
-        hit = res.size > 0
         words = res.data[: res.data.numel() // 8 * 8].view(torch.int64)
-        at = torch.where(hit, torch.div(res.off, 8, rounding_mode="floor"), torch.zeros_like(res.off))
+        wd = words.device  # pinned host memory under --edge host
+        keys_last = gets[last_batch].to(wd)
+        hit = (res.size > 0).to(wd)
+        at = torch.where(hit, torch.div(res.off.to(wd), 8, rounding_mode="floor"),
+                         torch.zeros_like(res.off, device=wd))
         wrong = hit & ((words.index_select(0, at) != keys_last[:, 0]) |
                        (words.index_select(0, at + 1) != keys_last[:, 1]))
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
@@ -373,7 +397,8 @@ def main():
         "dtype": "uint8",
         "data": "synthetic (device-generated Zipf web-object workload; random payloads)",
         "config": {
-            "model": "shellac-hbm-cache: ketama-ring sharded, 1 shard/GPU, FIFO log + 2-choice index",
+            "model": f"shellac-hbm-cache: ketama-ring sharded, 1 shard/GPU, {args.evict.upper()} log "
+                     "+ 2-choice index",
             "global_batch": ops_per_step,
             "seq_len": None,
             "parallelism": f"shard{world} (all-to-all routed)",
@@ -399,8 +424,18 @@ def main():
         "get_unique_per_s": round((gops + rep_hits) / elapsed, 1),
         "uncoalesced_ops_per_s": round(unco, 1) if unco else None,
         "batches_cycled": P,
+        "edge": args.edge,
         "smoke": sm,
     }
+    if host_edge:
+        # responses delivered into pinned host memory (GPU -> host over PCIe) against the
+        # PCIe 5.0 x16 roofline (~63 GB/s per direction); the keys and SET payloads
+        # travel the other way (host -> GPU)
+        out["host_delivered_GBps"] = round(gathered / elapsed / 1e9, 2)
+        out["pcie_roofline_GBps"] = 63.0
+        out["host_read_GBps"] = round(
+            (args.batch * 16 + args.sets * (16 + 8 + 12) + int(wl.vlen.float().mean()) * args.sets)
+            * args.steps / elapsed / 1e9, 2)
     if intervals:
         srt = sorted(intervals)
         out["ms_per_step_median_gpu_events"] = round(srt[len(srt) // 2], 4)

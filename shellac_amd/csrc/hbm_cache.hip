@@ -1100,37 +1100,29 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
 // CAS on its loc word, the digest / vlen words follow and k_set_fixup repairs entries
 // a later insert of the same batch re-claimed. Workgroup 0 publishes the new log head
 // into the other ping-pong head slot; every row resets its dedupe-table slot.
-__global__ __launch_bounds__(kBlock) void k_set_index(
+// Keep this kernel at <= 64 VGPRs (8 waves/SIMD): beside the gather, which holds 3/4 of
+// every SIMD's slots, a 72-VGPR build fits one wave per SIMD instead of two and ran 4x
+// slower (126 vs 31 us per 64K-row batch).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_set_index(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
-    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim,
-    uint64_t* __restrict__ ring, uint64_t rmask, const uint64_t* __restrict__ ring_tail,
-    uint64_t* __restrict__ ring_tail_next, const uint64_t* __restrict__ cnt_off,
-    uint64_t* __restrict__ head_host) {
+    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim) {
   const int l4 = threadIdx.x & 3;
   const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
-  // item-start ring (CLOCK hand input): every stored row takes the next ring entry in
-  // row order = log order (cnt_off: exclusive count of stored rows)
-  const uint64_t rtail = ring ? *ring_tail : 0;
   unsigned long long evicted = 0, bytes = 0, lost = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *head_next = head_new;
-    if (ring) *ring_tail_next = rtail + cnt_off[n];
-    if (head_host) __hip_atomic_store(head_host, head_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
     if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
       const uint32_t sl = slot_of[i];
       dd_keys[sl] = 0ull;
       dd_win[sl] = -1;
     }
-    if (ring && l4 == 0 && size[i]) ring[(rtail + cnt_off[i]) & rmask] = base + off[i];
     if (l4 == 0) claim[i] = ~0u;  // no entry (yet)
     if (size[i] == 0) continue;   // uniform across the 4-lane group
     const Digest d = keys[i];
@@ -1152,8 +1144,9 @@ __global__ __launch_bounds__(kBlock) void k_set_index(
       // this batch, (base, head_new], is another row's claim whose digest words have not
       // landed yet (dedupe leaves one row per key, so it is never this key's entry):
       // taking it as our own would CAS that row's claim away and lose its SET.
-      const bool in1 = w1[2] > base && w1[2] <= head_new;
-      const bool in2 = w2[2] > base && w2[2] <= head_new;
+      const uint64_t span = head_new - base;  // locs of this batch: (base, head_new]
+      const bool in1 = w1[2] - base - 1 < span;
+      const bool in2 = w2[2] - base - 1 < span;
       const bool m1 = w1[0] == d.lo && w1[1] == d.hi && !in1;
       const bool m2 = w2[0] == d.lo && w2[1] == d.hi && !in2;
       const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
@@ -1220,8 +1213,23 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ expire,
     const uint64_t* __restrict__ head_ptr, const uint32_t* __restrict__ claim,
-    Entry* __restrict__ index) {
+    Entry* __restrict__ index, const uint64_t* __restrict__ size, uint64_t* __restrict__ ring,
+    uint64_t rmask, const uint64_t* __restrict__ ring_tail, uint64_t* __restrict__ ring_tail_next,
+    const uint64_t* __restrict__ cnt_off, uint64_t* __restrict__ head_host) {
   const uint64_t base = *head_ptr;
+  // item-start ring (CLOCK hand input): every stored row takes the next ring entry in row
+  // order = log order (cnt_off: exclusive count of stored rows); the new head goes to the
+  // pinned host slot the host's reclaim decision reads
+  const uint64_t rtail = ring ? *ring_tail : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (ring) *ring_tail_next = rtail + cnt_off[n];
+    if (head_host)
+      __hip_atomic_store(head_host, base + off[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (ring)
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock)
+      if (size[i]) ring[(rtail + cnt_off[i]) & rmask] = base + off[i] + 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
     const uint32_t c = claim[i];
@@ -2101,10 +2109,11 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                      cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
-                     set_claim_, ring_, ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(),
-                     next_ring_tail(), set_cnt_, host_slots_ + kHeadSlot);
+                     set_claim_);
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
-                     set_off_, vlen, expire, cur_head(), set_claim_, index_);
+                     set_off_, vlen, expire, cur_head(), set_claim_, index_, set_size_, ring_,
+                     ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(), next_ring_tail(), set_cnt_,
+                     host_slots_ + kHeadSlot);
   HIP_OK(hipGetLastError());
 }
 

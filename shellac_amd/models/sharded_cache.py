@@ -164,6 +164,11 @@ class ShardedCache:
         self._probe_done = None  # event: this step's probe is done (SET index may run)
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
         self._co_table = None    # persistent GET-coalescing table (serve, side stream)
+        # host edge (one rank): GET digests / SET payloads may be pinned host tensors and
+        # responses are gathered straight into pinned host memory, as the proxy's HBM
+        # tier does (bench.py --edge host)
+        self.host_edge = False
+        self.gathered_bytes = 0  # response bytes the serving steps produced
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0}
 
@@ -343,13 +348,26 @@ class ShardedCache:
         sh = self.shard
         cap = self._gather_cap
         if cap:
-            data = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            data = self._out_buffer(cap)
             sh.gather(lk, data, out_cap=cap)
         total = sh.host_total(0)
+        self.gathered_bytes += total
         if cap and total <= cap:
             return data
         self._gather_cap = max(int(total * 1.25), 1 << 20) // 16 * 16
-        return sh.gather(lk, total=total)
+        return sh.gather(lk, self._out_buffer(max(total, 16)))
+
+    def _out_buffer(self, nbytes: int) -> torch.Tensor:
+        if self.host_edge:
+            # pinned host memory the gather kernel writes over PCIe; two buffers taken in
+            # turn, so a step's response stays valid while the next step runs
+            bufs = getattr(self, "_host_out", None) or [None, None]
+            self._host_out = bufs
+            k = self._host_turn = 1 - getattr(self, "_host_turn", 1)
+            if bufs[k] is None or bufs[k].numel() < nbytes:
+                bufs[k] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            return bufs[k][:nbytes]
+        return torch.empty(nbytes, dtype=torch.uint8, device=self.device)
 
     def _side_stream(self):
         if self.device.type != "cuda":

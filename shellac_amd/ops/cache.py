@@ -231,7 +231,11 @@ class CacheShard:
         return _stream_handle(self.device)
 
     def _check(self, t: torch.Tensor, name: str):
-        if t.device != self.device:
+        # a GPU shard also takes pinned host tensors: its kernels read and write them in
+        # place over PCIe (the proxy's edge: keys, SET payloads and responses stay in host
+        # memory, no staging copies)
+        host_ok = self.is_gpu and t.device.type == "cpu" and t.is_pinned()
+        if t.device != self.device and not host_ok:
             raise ValueError(f"{name} on {t.device}, shard on {self.device}")
         if not t.is_contiguous():
             raise ValueError(f"{name} must be contiguous")
