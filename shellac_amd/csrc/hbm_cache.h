@@ -190,6 +190,8 @@ class HbmCache {
   uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
   unsigned int* done_ctr_ = nullptr; // device: edge-GET workgroups finished + fail flag (self-resetting)
   unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
+  unsigned long long* lbc_state_ = nullptr; // device: coalescing lookup's look-back words
+  unsigned int* lbc_done_ = nullptr;
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;

@@ -187,6 +187,59 @@ __device__ __forceinline__ void block_partial(unsigned long long v, uint64_t* __
   __syncthreads();  // s_p may be reused by a following call
 }
 
+// ---- decoupled look-back (single-pass scans across workgroups) -------------------------
+// Workgroups are dispatched in blockIdx order, so when workgroup b waits for b-1's word,
+// b-1 is resident or done: the chain always completes. The state words are reset by the
+// launch's last workgroup (self-cleaning, no memset between launches).
+constexpr unsigned long long kLbAgg = 1ull << 62;    // look-back state: aggregate ready
+constexpr unsigned long long kLbIncl = 2ull << 62;   // inclusive prefix ready
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 22;          // a predecessor that never publishes
+
+// Thread 0 only: publish this workgroup's aggregate, return the sum of every earlier
+// workgroup's (exclusive prefix). *fail on a predecessor that never published.
+__device__ __forceinline__ unsigned long long lookback_exclusive(unsigned long long* state,
+                                                                unsigned long long agg,
+                                                                int* fail) {
+  if (blockIdx.x == 0) {
+    __hip_atomic_store(state, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __hip_atomic_store(state + blockIdx.x, kLbAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long base = 0;
+  uint32_t spins = 0;
+  for (int64_t p = (int64_t)blockIdx.x - 1; p >= 0;) {
+    const unsigned long long st =
+        __hip_atomic_load(state + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == 0) {
+      if (++spins > kLbSpinLimit) {
+        *fail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    base += st & kLbVal;
+    if (st & kLbIncl) break;
+    --p;
+  }
+  __hip_atomic_store(state + blockIdx.x, kLbIncl | (base + agg), __ATOMIC_RELEASE,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  return base;
+}
+
+// Every thread: the launch's last workgroup to get here clears the look-back words.
+__device__ __forceinline__ void lookback_done(unsigned long long* state, unsigned int* done) {
+  __shared__ int s_last_lb;
+  __syncthreads();
+  if (threadIdx.x == 0) s_last_lb = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (s_last_lb) {
+    for (unsigned k = threadIdx.x; k < gridDim.x; k += kBlock) state[k] = 0ull;
+    if (threadIdx.x == 0) atomicExch(done, 0u);
+  }
+}
+
 // Items per workgroup when n items are split into contiguous ranges over `grid` groups.
 __host__ __device__ __forceinline__ int64_t part_len(int64_t n, int grid) {
   return (n + grid - 1) / grid;
@@ -451,7 +504,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ part, int local_only) {
+    uint64_t* __restrict__ part, int local_only, uint64_t* __restrict__ off,
+    unsigned long long* __restrict__ lb_state, unsigned int* __restrict__ lb_done,
+    uint64_t* __restrict__ host_total) {
   __shared__ Digest s_k[kCoKeys];       // the chunk's digests (LDS compares, probe input)
   __shared__ uint32_t s_tab[kCoSlots];  // local row + 1
   __shared__ uint32_t s_rep[kCoKeys];   // global claimer of each local claimer
@@ -627,7 +682,54 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
                 &CacheCounters::get_bytes);
     block_count(ctr, dups, &CacheCounters::get_coalesced);
-    block_partial(psum, part);
+    if (!off) {
+      block_partial(psum, part);  // k_offsets scans the partials
+      return;
+    }
+    // Fused offsets: the range's byte offsets from a decoupled look-back over the earlier
+    // ranges' sums, then a block scan of the range's sizes (no separate scan kernel
+    // between the probe and the gather).
+    __shared__ unsigned long long s_w[kBlock / 64];
+    __shared__ unsigned long long s_base;
+    __shared__ int s_fail;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long t = wave_sum(psum);
+    if (lane == 0) s_w[w] = t;
+    if (threadIdx.x == 0) s_fail = 0;
+    __syncthreads();  // also orders this block's out_size stores before the reads below
+    if (threadIdx.x == 0) {
+      unsigned long long agg = 0;
+#pragma unroll
+      for (int k = 0; k < kBlock / 64; ++k) agg += s_w[k];
+      s_base = lookback_exclusive(lb_state, agg, &s_fail);
+    }
+    __syncthreads();
+    const int64_t len = r1 - r0;
+    const int64_t per = (len + kBlock - 1) / kBlock;
+    const int64_t a = min(r1, r0 + per * threadIdx.x), b = min(r1, a + per);
+    unsigned long long mine = 0;
+    for (int64_t i = a; i < b; ++i) mine += out_size[i];
+    unsigned long long inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long o = __shfl_up(inc, d);
+      if (lane >= d) inc += o;
+    }
+    __syncthreads();  // s_w reuse
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned long long run = s_base + inc - mine;
+    for (int k = 0; k < w; ++k) run += s_w[k];
+    for (int64_t i = a; i < b; ++i) {
+      off[i] = run;
+      run += out_size[i];
+    }
+    if (r1 == n && b == n && a < b) {  // the thread holding row n-1
+      off[n] = run;
+      if (host_total)
+        __hip_atomic_store(host_total, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    lookback_done(lb_state, lb_done);
   }
 }
 
@@ -896,10 +998,6 @@ void launch_segcopy(hipStream_t s, Args... args) {
 // the response lands in pinned host memory ready for writev.
 // ---------------------------------------------------------------------------------
 constexpr int kEdgeKeys = kBlock / 8;   // keys per workgroup
-constexpr unsigned long long kLbAgg = 1ull << 62;    // look-back state: aggregate ready
-constexpr unsigned long long kLbIncl = 2ull << 62;   // inclusive prefix ready
-constexpr unsigned long long kLbVal = (1ull << 62) - 1;
-constexpr uint32_t kLbSpinLimit = 1u << 22;          // a predecessor that never publishes
 
 __global__ __launch_bounds__(kBlock) void k_edge_get(
     const Digest* __restrict__ keys, int64_t n, Entry* __restrict__ index, uint64_t mask,
@@ -1732,7 +1830,7 @@ void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
                      (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, cslot,
                      nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
-                     0);
+                     0, nullptr, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
 }
 
@@ -1814,6 +1912,10 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   const size_t lb_words = (size_t)(kSmallGetMax / kEdgeKeys + 1);
   HIP_OK(hipMalloc(&lb_state_, lb_words * sizeof(unsigned long long)));
   HIP_OK(hipMemset(lb_state_, 0, lb_words * sizeof(unsigned long long)));
+  HIP_OK(hipMalloc(&lbc_state_, (kMaxGrid + 1) * sizeof(unsigned long long)));
+  HIP_OK(hipMemset(lbc_state_, 0, (kMaxGrid + 1) * sizeof(unsigned long long)));
+  HIP_OK(hipMalloc(&lbc_done_, 64));
+  HIP_OK(hipMemset(lbc_done_, 0, 64));
   HIP_OK(hipMalloc(&part_, 3 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
@@ -1846,6 +1948,8 @@ HbmCache::~HbmCache() {
   (void)hipFree(scratch_);
   (void)hipFree(done_ctr_);
   (void)hipFree(lb_state_);
+  (void)hipFree(lbc_state_);
+  (void)hipFree(lbc_done_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -1989,12 +2093,13 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   const int64_t per = (chunks + coalesce_grid_cap() - 1) / coalesce_grid_cap();
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
+  // the probe scans its own sizes (decoupled look-back): no k_offsets launch
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
-                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only());
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only(),
+                     off, lbc_state_, lbc_done_, ht);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }
 
 uint64_t HbmCache::host_slot(int i) const {

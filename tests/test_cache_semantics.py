@@ -157,3 +157,41 @@ def test_dram_backend_full_key_identity():
     assert be.get_with_digest(b"/attacker", b"/victim") is None
     assert be.get_with_digest(b"/victim", b"/victim") == (b"private", 7)
     assert be.stats()["cache_key_mismatch"] == 1
+
+
+def test_dram_object_cache_clock_keeps_read_objects():
+    """The host tier evicts by bytes with CLOCK: an object read between fills survives
+    a fill larger than the cache, unread ones of the same age do not."""
+    import time as _t
+
+    from shellac_amd import core
+
+    be = core().dram_backend(1 << 20, 1 << 16, 1)  # 1 MiB, one stripe: exact CLOCK order
+    be.set(b"/hot", b"h" * 2000, 0, 0)
+    be.set(b"/cold", b"c" * 2000, 0, 0)
+    for lap in range(4):
+        assert be.get(b"/hot") is not None
+        for i in range(200):
+            be.set(b"/fill/%d/%d" % (lap, i), b"f" * 2000, 0, 0)
+    assert be.get(b"/hot") == (b"h" * 2000, 0)
+    assert be.get(b"/cold") is None
+    st = be.stats()
+    assert st["cache_evicted"] > 0 and st["cache_bytes"] <= (1 << 20)
+    # TTL: expired objects read as misses
+    be.set(b"/ttl", b"t", 0, 1)
+    assert be.get(b"/ttl") == (b"t", 0)
+    _t.sleep(2.1)
+    assert be.get(b"/ttl") is None
+
+
+def test_dram_hit_is_shared_not_copied():
+    """Two hits of the same object return the same bytes (the tier hands out references
+    to one immutable object) and a later SET replaces it without touching them."""
+    from shellac_amd import core
+
+    be = core().dram_backend(16 << 20, 1 << 16, 4)
+    be.set(b"/obj", b"v1" * 100, 0, 0)
+    a = be.get(b"/obj")
+    be.set(b"/obj", b"v2" * 100, 0, 0)
+    assert a == (b"v1" * 100, 0) and be.get(b"/obj") == (b"v2" * 100, 0)
+    assert be.delete(b"/obj") is True and be.get(b"/obj") is None
