@@ -1,21 +1,12 @@
-#!/usr/bin/env bash
-# HBM traffic of the hot cache kernels (kernel_bench.py workload): FETCH_SIZE and
-# WRITE_SIZE (KiB to/from HBM) per dispatch -- one counter per run, the pair exceeds
-# what the hardware collects in one pass -- joined with the kernel durations of a plain
-# kernel-trace run by scripts/pmc_summary.py. PMC runs use --kernel-trace only.
-set -eu
-cd /tmp && export TMPDIR=/tmp
-ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
-OUT="$ROOT/gpurun_out/pmc"
-mkdir -p "$OUT"
-cd "$ROOT"
-run() {  # name, then rocprofv3 options
-  local name=$1
-  shift
-  timeout -k 10 150 rocprofv3 --kernel-trace "$@" --output-format csv -d "$OUT" -o "$name" -- \
-    python3 benchmarks/kernel_bench.py --iters 3
-}
-run fetch --pmc FETCH_SIZE --kernel-include-regex "segcopy|probe|set_index|set_dedupe"
-run write --pmc WRITE_SIZE --kernel-include-regex "segcopy|probe|set_index|set_dedupe"
-run occ --pmc SQ_WAVES SQ_BUSY_CYCLES --kernel-include-regex "segcopy|probe"
-run time
+# PMC roofline of the N=1 bench step: per-kernel HBM bytes (FETCH_SIZE, WRITE_SIZE: one
+# pass each, they cannot share the 4 TCC counters) plus a plain kernel-trace pass for
+# the durations. Summarised by scripts/pmc_roofline.py into profiles/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+mkdir -p gpurun_out/pmc
+ARGS="--steps 6 --warmup 2 --no-uncoalesced --no-smoke $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/trace -o run -- python3 bench.py $ARGS > gpurun_out/pmc/trace.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc/fetch -o run -- python3 bench.py $ARGS > gpurun_out/pmc/fetch.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc/write -o run -- python3 bench.py $ARGS > gpurun_out/pmc/write.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc/sq -o run -- python3 bench.py $ARGS > gpurun_out/pmc/sq.log 2>&1 || exit 1
+python3 scripts/pmc_roofline.py gpurun_out/pmc > gpurun_out/pmc/roofline.md && cat gpurun_out/pmc/roofline.md

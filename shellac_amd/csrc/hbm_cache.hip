@@ -196,35 +196,52 @@ constexpr unsigned long long kLbIncl = 2ull << 62;   // inclusive prefix ready
 constexpr unsigned long long kLbVal = (1ull << 62) - 1;
 constexpr uint32_t kLbSpinLimit = 1u << 22;          // a predecessor that never publishes
 
-// Thread 0 only: publish this workgroup's aggregate, return the sum of every earlier
-// workgroup's (exclusive prefix). *fail on a predecessor that never published.
+// Wave 0 (all 64 lanes): publish this workgroup's aggregate, return the sum of every
+// earlier workgroup's (exclusive prefix). The wave reads 64 predecessors' words per step
+// (lane l -> workgroup b-1-l) and stops at the nearest inclusive prefix: a walk over
+// thousands of aggregate-only predecessors is then a few dependent loads, not one per
+// predecessor (one lane at a time made a 1024-group coalescing probe 2x slower).
+// *fail on a predecessor that never published.
 __device__ __forceinline__ unsigned long long lookback_exclusive(unsigned long long* state,
                                                                 unsigned long long agg,
                                                                 int* fail) {
+  const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0) {
-    __hip_atomic_store(state, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+      __hip_atomic_store(state, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  __hip_atomic_store(state + blockIdx.x, kLbAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0)
+    __hip_atomic_store(state + blockIdx.x, kLbAgg | agg, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long base = 0;
+  int64_t end = (int64_t)blockIdx.x;  // window: workgroups [end-64, end)
   uint32_t spins = 0;
-  for (int64_t p = (int64_t)blockIdx.x - 1; p >= 0;) {
+  for (;;) {
+    const int64_t p = end - 1 - lane;
     const unsigned long long st =
-        __hip_atomic_load(state + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (st == 0) {
+        p >= 0 ? __hip_atomic_load(state + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+               : kLbIncl;  // before workgroup 0: an inclusive zero
+    const unsigned long long incl = __ballot((st & kLbIncl) != 0);
+    const int stop = incl ? __ffsll((long long)incl) - 1 : 63;  // last lane that counts
+    const unsigned long long notready = __ballot(st == 0);
+    const unsigned long long need = stop == 63 ? ~0ull : ((2ull << stop) - 1ull);
+    if (notready & need) {
       if (++spins > kLbSpinLimit) {
-        *fail = 1;
+        if (lane == 0) *fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    base += st & kLbVal;
-    if (st & kLbIncl) break;
-    --p;
+    unsigned long long v = lane <= stop ? (st & kLbVal) : 0ull;
+    base += wave_sum(v);
+    if (incl) break;
+    end -= 64;
   }
-  __hip_atomic_store(state + blockIdx.x, kLbIncl | (base + agg), __ATOMIC_RELEASE,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0)
+    __hip_atomic_store(state + blockIdx.x, kLbIncl | (base + agg), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
   return base;
 }
 
@@ -697,11 +714,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (lane == 0) s_w[w] = t;
     if (threadIdx.x == 0) s_fail = 0;
     __syncthreads();  // also orders this block's out_size stores before the reads below
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // wave 0 walks the predecessors
       unsigned long long agg = 0;
 #pragma unroll
       for (int k = 0; k < kBlock / 64; ++k) agg += s_w[k];
-      s_base = lookback_exclusive(lb_state, agg, &s_fail);
+      const unsigned long long b0 = lookback_exclusive(lb_state, agg, &s_fail);
+      if (threadIdx.x == 0) s_base = b0;
     }
     __syncthreads();
     const int64_t len = r1 - r0;
@@ -1046,34 +1064,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_get(
       if (lane >= dd) inc += o;
     }
     const uint64_t agg = __shfl(inc, 63);
-    unsigned long long base = 0;
-    if (lane == 0) {
-      if (blockIdx.x == 0) {
-        __hip_atomic_store(state, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __hip_atomic_store(state + blockIdx.x, kLbAgg | agg, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t spins = 0;
-        for (int64_t p = (int64_t)blockIdx.x - 1; p >= 0;) {
-          const unsigned long long st =
-              __hip_atomic_load(state + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          if (st == 0) {
-            if (++spins > kLbSpinLimit) {  // never hang: report the batch as failed
-              s_fail = 1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-          }
-          base += st & kLbVal;
-          if (st & kLbIncl) break;
-          --p;
-        }
-        __hip_atomic_store(state + blockIdx.x, kLbIncl | (base + agg), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_base = base;
-    }
+    // never hangs: a predecessor that never publishes marks the batch failed
+    const unsigned long long base = lookback_exclusive(state, agg, &s_fail);
+    if (lane == 0) s_base = base;
     if (lane <= kEdgeKeys) s_off[lane] = inc - v;  // exclusive; s_off[32] = agg
   }
   __syncthreads();
@@ -2093,13 +2086,16 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   const int64_t per = (chunks + coalesce_grid_cap() - 1) / coalesce_grid_cap();
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
-  // the probe scans its own sizes (decoupled look-back): no k_offsets launch
+  // (fusing the offsets scan into this kernel by decoupled look-back was measured slower:
+  // 0.45 vs 0.32 ms per step — a workgroup then holds its slot until every earlier one has
+  // published, and the SET chain on the side stream needs those slots)
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
                      reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only(),
-                     off, lbc_state_, lbc_done_, ht);
+                     nullptr, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
+  launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }
 
 uint64_t HbmCache::host_slot(int i) const {
