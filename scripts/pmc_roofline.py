@@ -27,7 +27,9 @@ def rows(pattern):
     return out
 
 
-def main(d):
+def main(d, last=6):
+    """last: dispatches per kernel kept (the timed steps run last; earlier ones are the
+    populate and warm-up launches)."""
     dur = {}
     for r in rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
         k = short(r["Kernel_Name"])
@@ -37,7 +39,9 @@ def main(d):
         for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
             k = short(r["Kernel_Name"])
             ctr.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    print("| kernel | calls | median us | fetch MiB | write MiB | GB/s | % of 6.29 TB/s | VALU/wave | VMEM rd+wr/wave | wait % |")
+    dur = {k: v[-last:] for k, v in dur.items()}
+    ctr = {k: {c: vals[-last:] for c, vals in cs.items()} for k, cs in ctr.items()}
+    print("| kernel | calls/step | median us | fetch MiB | write MiB | GB/s | % of 6.29 TB/s | VALU instr/wave | VMEM instr/wave | wait cycles/wave |")
     print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     items = sorted(dur.items(), key=lambda kv: -statistics.median(kv[1]) * len(kv[1]))
     for k, v in items:
@@ -52,12 +56,10 @@ def main(d):
         valu = statistics.median(c["SQ_INSTS_VALU"]) / waves if waves else float("nan")
         vmem = ((statistics.median(c.get("SQ_INSTS_VMEM_RD", [0])) +
                  statistics.median(c.get("SQ_INSTS_VMEM_WR", [0]))) / waves) if waves else float("nan")
-        busy = statistics.median(c.get("SQ_BUSY_CYCLES", [0]))
-        wait = statistics.median(c.get("SQ_WAIT_INST_ANY", [0]))
-        wpct = 100 * wait / busy if busy else float("nan")
-        print(f"| `{k}` | {len(v)} | {med:.1f} | {fe / 1024:.1f} | {wr / 1024:.1f} | {gbps:.0f} | "
-              f"{100 * gbps / PEAK:.0f}% | {valu:.0f} | {vmem:.0f} | {wpct:.0f} |")
+        wait = statistics.median(c.get("SQ_WAIT_INST_ANY", [0])) / waves if waves else float("nan")
+        print(f"| `{k}` | {len(v) / last:.0f} | {med:.1f} | {fe / 1024:.1f} | {wr / 1024:.1f} | {gbps:.0f} | "
+              f"{100 * gbps / PEAK:.0f}% | {valu:.0f} | {vmem:.0f} | {wait:.0f} |")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 6)
