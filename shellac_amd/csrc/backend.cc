@@ -110,8 +110,9 @@ void DramBackend::stats(StatList* out) {
 // Tiered (L1 DRAM + L2)
 // =====================================================================================
 TieredBackend::TieredBackend(std::shared_ptr<CacheBackend> l1, std::shared_ptr<CacheBackend> l2,
-                             uint32_t promote_ttl_s)
-    : l1_(std::move(l1)), l2_(std::move(l2)), promote_ttl_(promote_ttl_s) {
+                             uint32_t promote_ttl_s, uint64_t promote_max)
+    : l1_(std::move(l1)), l2_(std::move(l2)), promote_ttl_(promote_ttl_s),
+      promote_max_(promote_max) {
   SH_CHECK(l1_ && l2_, "tiered backend needs two levels");
 }
 
@@ -131,10 +132,15 @@ void TieredBackend::get(const std::string& key, const Digest& d, Executor* ex, G
     l2->get(key, d, ex, [this, key, d, done = std::move(done)](bool hit2, CacheValue v2) {
       if (hit2 && v2.data) {
         l2_hits_.fetch_add(1, std::memory_order_relaxed);
-        // promote with the L2 entry's remaining TTL (0 = no expiry, -1 = unknown)
-        const uint32_t ttl = v2.ttl_left > 0 ? (uint32_t)v2.ttl_left
-                                             : (v2.ttl_left == 0 ? 0u : promote_ttl_);
-        l1_->set(key, d, v2.data, v2.flags, ttl);
+        if (v2.data->size() <= promote_max_) {
+          // promote with the L2 entry's remaining TTL (0 = no expiry, -1 = unknown)
+          const uint32_t ttl = v2.ttl_left > 0 ? (uint32_t)v2.ttl_left
+                                               : (v2.ttl_left == 0 ? 0u : promote_ttl_);
+          l1_->set(key, d, v2.data, v2.flags, ttl);
+          promoted_.fetch_add(1, std::memory_order_relaxed);
+        } else {
+          not_promoted_.fetch_add(1, std::memory_order_relaxed);
+        }
       } else {
         misses_.fetch_add(1, std::memory_order_relaxed);
       }
@@ -167,6 +173,8 @@ void TieredBackend::stats(StatList* out) {
   out->emplace_back("tier_l1_hits", l1_hits_.load());
   out->emplace_back("tier_l2_hits", l2_hits_.load());
   out->emplace_back("tier_misses", misses_.load());
+  out->emplace_back("tier_promoted", promoted_.load());
+  out->emplace_back("tier_not_promoted_large", not_promoted_.load());
   StatList a, b;
   l1_->stats(&a);
   l2_->stats(&b);

@@ -179,8 +179,10 @@ class HbmBackend : public CacheBackend {
 // misses go to L2 and promote on hit; writes go to both levels.
 class TieredBackend : public CacheBackend {
  public:
+  // promote_max: L2 hits larger than this stay in L2 only (served from there every time,
+  // zero-copy for the HBM tier) instead of being copied into — and churning — the L1.
   TieredBackend(std::shared_ptr<CacheBackend> l1, std::shared_ptr<CacheBackend> l2,
-                uint32_t promote_ttl_s = 60);
+                uint32_t promote_ttl_s = 60, uint64_t promote_max = 32 << 10);
   void get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) override;
   void set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
            uint32_t ttl_s) override;
@@ -193,6 +195,8 @@ class TieredBackend : public CacheBackend {
  private:
   std::shared_ptr<CacheBackend> l1_, l2_;
   uint32_t promote_ttl_;
+  uint64_t promote_max_;
+  std::atomic<uint64_t> promoted_{0}, not_promoted_{0};
   std::atomic<uint64_t> l1_hits_{0}, l2_hits_{0}, misses_{0};
 };
 

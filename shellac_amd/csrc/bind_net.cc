@@ -216,9 +216,11 @@ void bind_net(py::module_& m) {
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);
-  m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl) {
-    return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl)};
-  }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60);
+  m.def("tiered_backend", [](BackendHandle& l1, BackendHandle& l2, uint32_t promote_ttl,
+                             uint64_t promote_max) {
+    return BackendHandle{std::make_shared<TieredBackend>(l1.be, l2.be, promote_ttl, promote_max)};
+  }, py::arg("l1"), py::arg("l2"), py::arg("promote_ttl") = 60,
+     py::arg("promote_max") = 32u << 10);
   m.def("memcached_backend", [](const std::string& servers, int retry_s, int op_timeout_ms) {
     MemcachedConfig c;
     c.servers = resolve_list(servers, 11211);

@@ -195,3 +195,21 @@ def test_dram_hit_is_shared_not_copied():
     be.set(b"/obj", b"v2" * 100, 0, 0)
     assert a == (b"v1" * 100, 0) and be.get(b"/obj") == (b"v2" * 100, 0)
     assert be.delete(b"/obj") is True and be.get(b"/obj") is None
+
+
+def test_tiered_promotes_small_objects_only():
+    """L2 hits are copied into the L1 up to promote_max bytes; larger objects keep being
+    served by the L2 (no L1 churn, no copy)."""
+    from shellac_amd import core
+
+    c = core()
+    l1 = c.dram_backend(16 << 20, 1 << 20, 4)
+    l2 = c.dram_backend(64 << 20, 1 << 20, 4)
+    t = c.tiered_backend(l1, l2, 60, 1024)
+    l2.set(b"/small", b"s" * 100, 0, 0)
+    l2.set(b"/big", b"b" * 5000, 0, 0)
+    assert t.get(b"/small") == (b"s" * 100, 0)
+    assert t.get(b"/big") == (b"b" * 5000, 0)
+    assert l1.get(b"/small") == (b"s" * 100, 0) and l1.get(b"/big") is None
+    st = t.stats()
+    assert st["tier_promoted"] == 1 and st["tier_not_promoted_large"] == 1
