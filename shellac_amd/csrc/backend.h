@@ -88,6 +88,7 @@ class DigestRing {
   // Owner among the shards whose bit is set in `alive` (ketama ejection: a dead shard's
   // keys move to the next live point); -1 if none is alive.
   int owner(const Digest& d, uint64_t alive) const;
+  const std::vector<std::pair<uint32_t, int>>& points() const { return pts_; }
 
  private:
   std::vector<std::pair<uint32_t, int>> pts_;
@@ -127,6 +128,9 @@ struct HbmBackendConfig {
   int retry_s = 2;            // an ejected GPU shard is retried after this long
   int batch_timeout_ms = 2000;  // a batch unfinished this long ejects its GPU
   bool flush_on_restore = true;  // a shard back from ejection may hold stale objects
+  // ...and is then warmed from its peers over xGMI: the objects of its key range that
+  // other shards took while it was out are peer-copied back (hipMemcpyPeerAsync)
+  bool warm_restore = true;
 };
 
 // One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are

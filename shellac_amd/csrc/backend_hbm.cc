@@ -169,13 +169,20 @@ struct HbmBackend::Dev {
   std::shared_ptr<PresenceFilter> filt, filt_next;
   uint64_t filt_bits = 0, filt_rebuild_at = 0;
   bool filt_want_rebuild = false;
+  // warm restore over xGMI: a stream for peer work on this GPU and the digest ring on
+  // the device (route_keys)
+  hipStream_t mstream = nullptr;
+  uint32_t* d_pts = nullptr;
+  int32_t* d_own = nullptr;
+  int npts = 0;
   // co-table for host GET coalescing (batcher thread only)
   std::vector<int32_t> co_tab;
   double avg_row_bytes = 4096;
   // stats
   std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
       filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
-      key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, dropped{0};
+      key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, dropped{0},
+      migrated{0}, migrate_ns{0};
 
   void loop();
   bool take_batch(std::vector<Req>* out, bool* do_flush, bool* rebuilding);
@@ -187,6 +194,7 @@ struct HbmBackend::Dev {
   void fail_requests(std::vector<Req>& reqs);
   void eject(const char* why);
   void maybe_restore();
+  uint64_t migrate_from(Dev& src);
   void sweep();
   void finish_filter_rebuild();
   bool up() const { return (be->up_mask_.load(std::memory_order_acquire) >> index) & 1; }
@@ -206,6 +214,9 @@ struct HbmBackend::Dev {
     }
     cache.reset();
     if (stream) (void)hipStreamDestroy(stream);
+    if (mstream) (void)hipStreamDestroy(mstream);
+    (void)hipFree(d_pts);
+    (void)hipFree(d_own);
   }
 };
 
@@ -231,6 +242,21 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     sc.evict = cfg_.evict;
     d->cache = std::make_unique<HbmCache>(sc);
     HB_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HB_OK(hipStreamCreateWithFlags(&d->mstream, hipStreamNonBlocking));
+    {
+      const auto& pts = ring_.points();
+      std::vector<uint32_t> hp(pts.size());
+      std::vector<int32_t> ho(pts.size());
+      for (size_t k = 0; k < pts.size(); ++k) {
+        hp[k] = pts[k].first;
+        ho[k] = pts[k].second;
+      }
+      d->npts = (int)pts.size();
+      HB_OK(hipMalloc(&d->d_pts, std::max<size_t>(1, hp.size()) * sizeof(uint32_t)));
+      HB_OK(hipMalloc(&d->d_own, std::max<size_t>(1, ho.size()) * sizeof(int32_t)));
+      HB_OK(hipMemcpy(d->d_pts, hp.data(), hp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      HB_OK(hipMemcpy(d->d_own, ho.data(), ho.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
     d->pool = std::make_shared<ArenaPool>(d->device);
     for (int k = 0; k < cfg_.depth; ++k) {
       auto f = std::make_unique<Flight>();
@@ -803,8 +829,164 @@ void HbmBackend::Dev::maybe_restore() {
     f->arena.reset();
   }
   restores++;
+  // Back in the ring first, then warm: objects of this shard's key range that its peers
+  // took while it was out are copied back GPU-to-GPU, inserted only where this shard has
+  // nothing yet — so a SET that reaches it from now on is never overwritten by an older
+  // migrated copy (requests queued meanwhile run after the migration, on this thread).
   set_up(true);
-  std::fprintf(stderr, "[shellac hbm] gpu %d back in service\n", device);
+  uint64_t moved = 0;
+  if (be->cfg_.warm_restore && be->cfg_.flush_on_restore) {
+    for (auto& other : be->devs_) {
+      if (other.get() == this || !other->up()) continue;
+      try {
+        moved += migrate_from(*other);
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "[shellac hbm] warm restore from gpu %d failed: %s\n",
+                     other->device, e.what());
+      }
+    }
+  }
+  std::fprintf(stderr, "[shellac hbm] gpu %d back in service (%llu objects warmed from peers)\n",
+               device, (unsigned long long)moved);
+}
+
+// Peer migration src -> this (both GPUs' HbmCache APIs are thread-safe; src's work goes
+// on src's migration stream, beside src's own batcher): export src's live digests, route
+// them on src's GPU, take the ones this shard owns, look them up and gather their records
+// on src, hipMemcpyPeerAsync the records to this GPU, turn them into a SET batch
+// (insert-if-absent against this shard's own lookup) and store them; finally delete them
+// from src, where nothing routes any more. Chunked so a store stays within half a log.
+uint64_t HbmBackend::Dev::migrate_from(Dev& src) {
+  TraceRange tr("hbm_backend.migrate");
+  const double t0 = wall_s();
+  const uint32_t t = be->now();
+  const int W = (int)be->devs_.size();
+  // ---- on src: live digests and their owners under the full ring
+  HB_OK(hipSetDevice(src.device));
+  const uint64_t live = src.cache->export_keys(nullptr, 0, t, src.mstream);
+  if (!live) {
+    HB_OK(hipSetDevice(device));
+    return 0;
+  }
+  Digest* s_keys = nullptr;
+  int32_t* s_dest = nullptr;
+  int64_t* s_cnt = nullptr;
+  HB_OK(hipMalloc(&s_keys, live * sizeof(Digest)));
+  HB_OK(hipMalloc(&s_dest, live * sizeof(int32_t)));
+  HB_OK(hipMalloc(&s_cnt, W * sizeof(int64_t)));
+  std::vector<int32_t> dest;
+  std::vector<Digest> keys;
+  uint64_t got = 0;
+  try {
+    got = std::min(live, src.cache->export_keys(s_keys, live, t, src.mstream));
+    HB_OK(hipMemsetAsync(s_cnt, 0, W * sizeof(int64_t), src.mstream));
+    route_keys(s_keys, (int64_t)got, src.d_pts, src.d_own, src.npts, s_dest, s_cnt, W,
+               src.mstream);
+    dest.resize(got);
+    keys.resize(got);
+    HB_OK(hipMemcpyAsync(dest.data(), s_dest, got * sizeof(int32_t), hipMemcpyDeviceToHost,
+                         src.mstream));
+    HB_OK(hipMemcpyAsync(keys.data(), s_keys, got * sizeof(Digest), hipMemcpyDeviceToHost,
+                         src.mstream));
+    HB_OK(hipStreamSynchronize(src.mstream));
+  } catch (...) {
+    (void)hipFree(s_keys); (void)hipFree(s_dest); (void)hipFree(s_cnt);
+    throw;
+  }
+  (void)hipFree(s_dest);
+  (void)hipFree(s_cnt);
+  std::vector<Digest> mine;
+  for (uint64_t i = 0; i < got; ++i)
+    if (dest[i] == index) mine.push_back(keys[i]);
+  (void)hipFree(s_keys);
+  if (be->cfg_.presence_filter && !mine.empty()) {  // GETs routed here must not skip them
+    std::lock_guard<std::mutex> lk(mu);
+    for (const Digest& d : mine) {
+      filt->add(d);
+      if (filt_next) filt_next->add(d);
+    }
+  }
+  uint64_t moved = 0;
+  const uint64_t rec_cap = std::max<uint64_t>(cache->config().log_bytes / 8, 1u << 20);
+  const size_t chunk = 65536;
+  for (size_t c0 = 0; c0 < mine.size(); c0 += chunk) {
+    const int64_t m = (int64_t)std::min(chunk, mine.size() - c0);
+    // ---- on src: look the chunk up (misses the tail the next appends will overwrite)
+    HB_OK(hipSetDevice(src.device));
+    Digest* sk = nullptr;
+    uint64_t *sloc = nullptr, *ssize = nullptr, *soff = nullptr;
+    uint8_t* srec = nullptr;
+    HB_OK(hipMalloc(&sk, m * sizeof(Digest)));
+    HB_OK(hipMalloc(&sloc, m * 8));
+    HB_OK(hipMalloc(&ssize, (m + 1) * 8));
+    HB_OK(hipMalloc(&soff, (m + 1) * 8));
+    uint64_t total = 0;
+    HB_OK(hipMemcpyAsync(sk, mine.data() + c0, m * sizeof(Digest), hipMemcpyHostToDevice,
+                         src.mstream));
+    src.cache->lookup(sk, m, sloc, ssize, soff, t, src.mstream, src.cache->config().log_bytes / 8);
+    HB_OK(hipMemcpyAsync(&total, soff + m, 8, hipMemcpyDeviceToHost, src.mstream));
+    HB_OK(hipStreamSynchronize(src.mstream));
+    if (total > rec_cap) total = 0;  // pathological chunk: skip it (objects just miss)
+    if (total) {
+      HB_OK(hipMalloc(&srec, total + 16));
+      src.cache->gather(sloc, soff, m, srec, src.mstream);
+      HB_OK(hipStreamSynchronize(src.mstream));
+    }
+    // ---- to this GPU over xGMI, insert-if-absent, store
+    HB_OK(hipSetDevice(device));
+    Digest* kk = nullptr;
+    uint64_t *koff = nullptr, *ksize = nullptr, *kloc = nullptr, *khave = nullptr,
+             *khoff = nullptr, *kvoff = nullptr;
+    uint8_t* krec = nullptr;
+    uint32_t* kmeta = nullptr;
+    Digest* skeys2 = nullptr;
+    bool ok = true;
+    try {
+      if (total) {
+        HB_OK(hipMalloc(&kk, m * sizeof(Digest)));
+        HB_OK(hipMalloc(&koff, (m + 1) * 8));
+        HB_OK(hipMalloc(&ksize, (m + 1) * 8));
+        HB_OK(hipMalloc(&kloc, m * 8));
+        HB_OK(hipMalloc(&khave, (m + 1) * 8));
+        HB_OK(hipMalloc(&khoff, (m + 1) * 8));
+        HB_OK(hipMalloc(&kvoff, m * 8));
+        HB_OK(hipMalloc(&kmeta, 3 * m * 4));
+        HB_OK(hipMalloc(&skeys2, m * sizeof(Digest)));
+        HB_OK(hipMalloc(&krec, total + 16));
+        HB_OK(hipMemcpyPeerAsync(krec, device, srec, src.device, total, stream));
+        HB_OK(hipMemcpyPeerAsync(koff, device, soff, src.device, (m + 1) * 8, stream));
+        HB_OK(hipMemcpyPeerAsync(ksize, device, ssize, src.device, (m + 1) * 8, stream));
+        HB_OK(hipMemcpyPeerAsync(kk, device, sk, src.device, m * sizeof(Digest), stream));
+        cache->lookup(kk, m, kloc, khave, khoff, t, stream);
+        records_to_set(krec, koff, ksize, khave, m, skeys2, kvoff, kmeta, kmeta + m, kmeta + 2 * m,
+                       stream);
+        cache->store(skeys2, krec, kvoff, kmeta, kmeta + m, kmeta + 2 * m, m, total + 48 * m, t,
+                     stream);
+        HB_OK(hipStreamSynchronize(stream));
+        std::vector<uint64_t> sz(m);
+        HB_OK(hipMemcpy(sz.data(), ksize, m * 8, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < m; ++i) moved += sz[i] ? 1 : 0;
+      }
+    } catch (...) {
+      ok = false;
+    }
+    for (void* p : {(void*)kk, (void*)koff, (void*)ksize, (void*)kloc, (void*)khave,
+                    (void*)khoff, (void*)kvoff, (void*)krec, (void*)kmeta, (void*)skeys2})
+      (void)hipFree(p);
+    // ---- src no longer serves these digests
+    HB_OK(hipSetDevice(src.device));
+    if (ok && total) {
+      src.cache->remove(sk, m, nullptr, t, src.mstream);
+      HB_OK(hipStreamSynchronize(src.mstream));
+    }
+    for (void* p : {(void*)sk, (void*)sloc, (void*)ssize, (void*)soff, (void*)srec})
+      (void)hipFree(p);
+    HB_OK(hipSetDevice(device));
+    if (!ok) throw Error("peer migration chunk failed");
+  }
+  migrated += moved;
+  migrate_ns += (uint64_t)((wall_s() - t0) * 1e9);
+  return moved;
 }
 
 void HbmBackend::Dev::sweep() {
@@ -884,6 +1066,8 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_ejections", sum(&Dev::ejections));
   out->emplace_back("hbm_restores", sum(&Dev::restores));
   out->emplace_back("hbm_regathers", sum(&Dev::regathers));
+  out->emplace_back("hbm_migrated", sum(&Dev::migrated));
+  out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));
   out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
   uint64_t arena = 0;

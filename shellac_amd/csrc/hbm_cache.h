@@ -239,6 +239,15 @@ void expand_coalesced_out(const uint32_t* first, int64_t n, const uint64_t* size
                           const uint64_t* off, uint64_t* out_size, uint64_t* out_off,
                           uint32_t* table, const uint32_t* cslot, hipStream_t s);
 
+// GET records -> a SET batch (shard migration over xGMI: records gathered on one GPU,
+// peer-copied to another, stored there). Row i's record is rec[off[i] .. +size[i]]
+// (size 0 = miss); a row whose `have_size[i]` (the destination's own lookup, may be null)
+// is non-zero is skipped — insert-if-absent, so a migration never overwrites an object
+// the destination has stored since. Outputs: vlen = kSkipVlen for skipped rows.
+void records_to_set(const uint8_t* rec, const uint64_t* off, const uint64_t* size,
+                    const uint64_t* have_size, int64_t n, Digest* keys, uint64_t* val_off,
+                    uint32_t* vlen, uint32_t* flags, uint32_t* expire, hipStream_t s);
+
 // Digest packed key bytes: key i = bytes[offs[i] .. offs[i+1]).
 void digest_keys(const uint8_t* bytes, const int64_t* offs, int64_t n, Digest* out,
                  hipStream_t s);

@@ -1735,6 +1735,33 @@ __global__ __launch_bounds__(kBlock) void k_permute(const uint32_t* __restrict__
   }
 }
 
+// Records -> SET rows (see records_to_set in hbm_cache.h).
+__global__ __launch_bounds__(kBlock) void k_records_to_set(
+    const uint8_t* __restrict__ rec, const uint64_t* __restrict__ off,
+    const uint64_t* __restrict__ size, const uint64_t* __restrict__ have, int64_t n,
+    Digest* __restrict__ keys, uint64_t* __restrict__ val_off, uint32_t* __restrict__ vlen,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ expire) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const bool skip = size[i] == 0 || (have && have[i] != 0);
+    if (skip) {
+      keys[i] = Digest{0, 0};
+      val_off[i] = 0;
+      vlen[i] = kSkipVlen;
+      flags[i] = 0;
+      expire[i] = 0;
+      continue;
+    }
+    const uint4* hp = reinterpret_cast<const uint4*>(rec + off[i]);
+    const uint4 w0 = hp[0], w1 = hp[1];
+    keys[i] = Digest{pack2(w0.x, w0.y), pack2(w0.z, w0.w)};
+    val_off[i] = off[i] + kItemHeaderBytes;
+    vlen[i] = w1.x;
+    flags[i] = w1.y;
+    expire[i] = w1.z;
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // MFMA hello (platform smoke)
 // ---------------------------------------------------------------------------------
@@ -1877,6 +1904,15 @@ void permute_records(const void* in, const int64_t* perm, int64_t n, int32_t rec
   const int32_t words = rec_bytes / 4;
   hipLaunchKernelGGL(k_permute, dim3(grid_for(n * words, kBlock)), dim3(kBlock), 0, s,
                      (const uint32_t*)in, perm, n, words, (uint32_t*)out);
+  HIP_OK(hipGetLastError());
+}
+
+void records_to_set(const uint8_t* rec, const uint64_t* off, const uint64_t* size,
+                    const uint64_t* have_size, int64_t n, Digest* keys, uint64_t* val_off,
+                    uint32_t* vlen, uint32_t* flags, uint32_t* expire, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_records_to_set, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, rec, off,
+                     size, have_size, n, keys, val_off, vlen, flags, expire);
   HIP_OK(hipGetLastError());
 }
 

@@ -228,3 +228,39 @@ def test_gpu_shard_ejection_drill_and_restore():
             assert px.stats()["cache"]["hbm_restores"] >= 1
     finally:
         o.stop()
+
+
+def test_gpu_shard_warm_restore_pulls_its_keys_back_from_peers():
+    """Two shards (both on GPU 0 here; on a node they are two GPUs and the copy goes
+    over xGMI). While shard 0 is ejected its key range is served by shard 1; when it
+    returns it flushes, then pulls those objects back peer-to-peer, so they keep hitting
+    (shard 1 drops them). Objects shard 1 owned all along are untouched."""
+    from shellac_amd import core
+
+    be = core().hbm_backend([0, 0], 64 << 20, 1 << 14, 1 << 16, 0)
+    before = [b"/wr/before/%d" % i for i in range(300)]
+    for i, k in enumerate(before):
+        be.set(k, b"b%d" % i * 20, 1, 0)
+    assert _wait_get(be, before[-1]) is not None
+    core().inject_shard_down(be, 0, True)
+    assert be.stats()["hbm_gpus_up"] == 1
+    during = [b"/wr/during/%d" % i for i in range(400)]
+    for i, k in enumerate(during):
+        be.set(k, b"d%d" % i * 30, 2, 0)
+    assert _wait_get(be, during[-1]) is not None
+    assert all(be.get(k) == (b"d%d" % i * 30, 2) for i, k in enumerate(during))
+    core().inject_shard_down(be, 0, False)
+    deadline = time.time() + 10
+    while be.stats()["hbm_gpus_up"] < 2 and time.time() < deadline:
+        time.sleep(0.05)
+    st = be.stats()
+    assert st["hbm_gpus_up"] == 2 and st["hbm_restores"] >= 1
+    # every object SET during the drill still hits (about half now live on shard 0)
+    got = [be.get(k) for k in during]
+    assert all(g == (b"d%d" % i * 30, 2) for i, g in enumerate(got)), \
+        sum(g is None for g in got)
+    st = be.stats()
+    assert 100 < st["hbm_migrated"] < 300, st["hbm_migrated"]
+    # before the drill: shard 1's objects hit, shard 0's were flushed on restore
+    hits = sum(be.get(k) == (b"b%d" % i * 20, 1) for i, k in enumerate(before))
+    assert 80 < hits < 220, hits
