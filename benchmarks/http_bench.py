@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from shellac_amd.server.proxy import Server, make_backend  # noqa: E402
+from shellac_amd.utils import cpus as cpu_plan  # noqa: E402
 
 # the origin and the load generator never touch the GPU: no torch / HIP runtime in them
 HOST_ONLY = dict(os.environ, SHELLAC_NO_TORCH="1")
@@ -72,9 +73,20 @@ def thread_cpu() -> dict:
     return out
 
 
-def start_origin(body: int, threads: int) -> tuple[subprocess.Popen, int]:
+def cgroup_cpus() -> int:
+    """CPUs the cgroup's CPU quota grants (0 when unlimited or unknown)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return 0 if q == "max" else max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        return 0
+
+
+def start_origin(body: int, threads: int, cpus=()) -> tuple[subprocess.Popen, int]:
     p = subprocess.Popen([sys.executable, "-m", "shellac_amd.utils.origin", "--body", str(body),
-                          "--threads", str(threads), "--random-body"],
+                          "--threads", str(threads), "--random-body",
+                          "--cpus", cpu_plan.format_cpus(cpus)],
                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT,
                          env=HOST_ONLY)
     line = p.stdout.readline().split()
@@ -85,12 +97,13 @@ def start_origin(body: int, threads: int) -> tuple[subprocess.Popen, int]:
 
 
 def load(port: int, n: int, conc: int, threads: int, objects: int, zipf: float, prefix: str,
-         seed: int, timeout: float) -> dict:
+         seed: int, timeout: float, cpus=()) -> dict:
     """One shellac-ab run in its own process; returns its JSON summary."""
     cmd = [sys.executable, "-m", "shellac_amd.bench.ab", "-n", str(n), "-c", str(conc), "-k",
            "--threads", str(threads), "--objects", str(objects), "--zipf", str(zipf),
            "--prefix", prefix, "--suffix", "", "--seed", str(seed), "--timeout", str(timeout),
-           "-H", "Accept-Encoding: gzip", "--json", f"http://127.0.0.1:{port}/"]
+           "-H", "Accept-Encoding: gzip", "--json", "--cpus", cpu_plan.format_cpus(cpus),
+           f"http://127.0.0.1:{port}/"]
     p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=timeout + 120,
                        env=HOST_ONLY)
     if p.returncode != 0:
@@ -101,8 +114,8 @@ def load(port: int, n: int, conc: int, threads: int, objects: int, zipf: float, 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", choices=["dram", "hbm", "tiered", "none"], default="tiered")
-    ap.add_argument("--threads", type=int, default=8, help="proxy reactor threads")
-    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--threads", type=int, default=9, help="proxy reactor threads")
+    ap.add_argument("--client-threads", type=int, default=5)
     ap.add_argument("--origin-threads", type=int, default=2)
     ap.add_argument("--objects", type=int, default=1000000)
     ap.add_argument("--body", type=int, default=4096, help="origin body bytes (incompressible)")
@@ -118,12 +131,45 @@ def main():
     ap.add_argument("--evict", choices=["clock", "fifo"], default="clock")
     ap.add_argument("--batch-us", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--pin", choices=["auto", "off"], default="auto",
+                    help="auto: each reactor and load-generator worker on its own core of "
+                         "the lowest allowed CPUs (one socket); the GPU batcher and the origin "
+                         "on the last cores of the CPU budget")
+    ap.add_argument("--cpu-budget", type=int, default=0,
+                    help="CPUs to lay the processes over (default: the cgroup CPU quota)")
+    ap.add_argument("--misc-cpus", type=int, default=0,
+                    help="cores for the GPU batcher, the proxy's other threads and the origin "
+                         "(default 1: the origin idles once the cache is filled)")
+    ap.add_argument("--layouts", nargs="+", default=None,
+                    help="RxC pairs (reactor threads x load-generator threads), each measured "
+                         "with its own proxy over the same filled cache (default: "
+                         "--threads x --client-threads)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
     item = a.body + 400  # record + key + response headers, roughly
     hbm_gb = a.hbm_gb or max(4.0, 1.25 * a.objects * item / (1 << 30))
-    origin, oport = start_origin(a.body, a.origin_threads)
+    gpu = a.backend in ("hbm", "tiered")
+    layouts = [tuple(int(x) for x in l.split("x")) for l in
+               (a.layouts or [f"{a.threads}x{a.client_threads}"])]
+    budget = a.cpu_budget or cgroup_cpus() or len(cpu_plan.allowed_cpus())
+    allowed = cpu_plan.allowed_cpus()[:budget]
+    pin = a.pin == "auto" and len(allowed) >= 4
+    nmisc = a.misc_cpus or 1
+    misc_cpus = allowed[-nmisc:] if pin else []
+    or_cpus = allowed[-1:] if pin else []  # the origin idles once the cache is filled
+
+    def layout_cpus(r, c):
+        if not pin:
+            return [], []
+        if r + c > len(allowed) - nmisc:
+            raise SystemExit(f"layout {r}x{c} does not fit {len(allowed)} CPUs")
+        return allowed[:r], allowed[r:r + c]
+
+    origin, oport = start_origin(a.body, a.origin_threads, or_cpus)
+    # threads created from here on (GPU batchers, HIP runtime) stay on the last cores;
+    # each reactor pins itself to its own core
+    cpu_plan.pin_process(misc_cpus)
     rss0, _ = rss_mb()
     if a.backend == "none":
         backend = None
@@ -133,52 +179,66 @@ def main():
         backend = make_backend("hbm", gpus=[0], hbm_gb=hbm_gb, batch_us=a.batch_us,
                                l1_mb=a.l1_mb if a.backend == "tiered" else 0,
                                depth=a.hbm_depth, evict=a.evict)
-    px = Server([("127.0.0.1", oport)], port=0, backend=backend, threads=a.threads,
-                client_max_reqs=1 << 30).start()
     prefix = "/o/"  # no /gz prefix: the origin sends the incompressible body as is
-    out = {"backend": a.backend, "proxy_threads": a.threads, "objects": a.objects,
+    out = {"backend": a.backend, "proxy_threads": layouts[0][0], "objects": a.objects,
            "body_bytes": a.body, "zipf": a.zipf, "working_set_MB": a.objects * item / 1e6,
            "dram_mb": a.dram_mb if a.backend == "dram" else None,
            "l1_mb": a.l1_mb if a.backend == "tiered" else None,
            "hbm_gb": hbm_gb if a.backend in ("hbm", "tiered") else None,
-           "cpu_count": os.cpu_count(), "processes": "origin | proxy | load generator"}
+           "cpu_count": os.cpu_count(), "cpu_budget": budget,
+           "processes": "origin | proxy | load generator",
+           "cpus": {"proxy_other": misc_cpus, "origin": or_cpus}}
+    px = None
     try:
-        t0 = time.time()
-        fill = load(px.port, a.objects, a.fill_conc, a.client_threads, a.objects, 0.0, prefix, 1,
-                    a.timeout)
-        out["fill"] = {"s": time.time() - t0, "rps": fill["rps"], "errors": fill["errors"]}
-        print(f"[http] fill {a.objects} objects: {fill['rps']:.0f} rps", file=sys.stderr)
-        time.sleep(1.0)
-        for conc in a.conc:
-            load(px.port, min(50000, a.requests), conc, a.client_threads, a.objects, a.zipf,
-                 prefix, 100 + conc, a.timeout)
-            s0 = px.stats()
-            c0, l0 = thread_cpu(), os.times()
-            r = load(px.port, a.requests, conc, a.client_threads, a.objects, a.zipf, prefix,
-                     200 + conc, a.timeout)
-            c1, l1 = thread_cpu(), os.times()
-            s1 = px.stats()
-            # where the CPU went during the run: proxy threads and the load generator
-            r["cpu_s"] = {k: round(c1.get(k, 0) - c0.get(k, 0), 2) for k in c1}
-            r["cpu_s"]["load_generator"] = round((l1.children_user + l1.children_system) -
-                                                 (l0.children_user + l0.children_system), 2)
-            reqs = s1["requests"] - s0["requests"]
-            hits = s1["cache_hits"] - s0["cache_hits"]
-            r["hit_ratio"] = hits / max(reqs, 1)
-            r["origin_requests"] = s1["upstream_requests"] - s0["upstream_requests"]
-            out[f"c{conc}"] = r
-            lm = r["latency_ms"]
-            print(f"[http] {a.backend} c={conc}: {r['rps']:.0f} rps (steady {r['steady_rps']:.0f}) "
-                  f"hit ratio {r['hit_ratio']:.4f} p50 {lm['p50']:.3f} ms p99 {lm['p99']:.3f} ms "
-                  f"{r['transfer_MBps']:.0f} MB/s errors {r['errors']} cpu {r['cpu_s']} "
-                  f"elapsed {r['elapsed_s']:.2f}s", file=sys.stderr)
-        st = px.stats()
+        for li, (nrx, ncl) in enumerate(layouts):
+            rx_cpus, lg_cpus = layout_cpus(nrx, ncl)
+            px = Server([("127.0.0.1", oport)], port=0, backend=backend, threads=nrx,
+                        client_max_reqs=1 << 30, cpus=rx_cpus).start()
+            tag = "" if li == 0 else f"{nrx}x{ncl}_"
+            out[f"{tag}layout"] = {"reactors": rx_cpus, "load_generator": lg_cpus}
+            if li == 0:
+                t0 = time.time()
+                fill = load(px.port, a.objects, a.fill_conc, ncl, a.objects, 0.0, prefix, 1,
+                            a.timeout, lg_cpus)
+                out["fill"] = {"s": time.time() - t0, "rps": fill["rps"], "errors": fill["errors"]}
+                print(f"[http] fill {a.objects} objects: {fill['rps']:.0f} rps", file=sys.stderr)
+                time.sleep(1.0)
+            for conc in a.conc:
+                load(px.port, min(50000, a.requests), conc, ncl, a.objects, a.zipf,
+                     prefix, 100 + conc, a.timeout, lg_cpus)
+                s0 = px.stats()
+                c0, l0 = thread_cpu(), os.times()
+                r = load(px.port, a.requests, conc, ncl, a.objects, a.zipf, prefix,
+                         200 + conc, a.timeout, lg_cpus)
+                c1, l1 = thread_cpu(), os.times()
+                s1 = px.stats()
+                # where the CPU went during the run: proxy threads and the load generator
+                r["cpu_s"] = {k: round(c1.get(k, 0) - c0.get(k, 0), 2) for k in c1}
+                r["cpu_s"]["load_generator"] = round((l1.children_user + l1.children_system) -
+                                                     (l0.children_user + l0.children_system), 2)
+                reqs = s1["requests"] - s0["requests"]
+                hits = s1["cache_hits"] - s0["cache_hits"]
+                r["hit_ratio"] = hits / max(reqs, 1)
+                r["origin_requests"] = s1["upstream_requests"] - s0["upstream_requests"]
+                r["layout"] = f"{nrx}x{ncl}"
+                out[f"{tag}c{conc}"] = r
+                lm = r["latency_ms"]
+                print(f"[http] {a.backend} {nrx}x{ncl} c={conc}: {r['rps']:.0f} rps "
+                      f"(steady {r['steady_rps']:.0f}) hit ratio {r['hit_ratio']:.4f} "
+                      f"p50 {lm['p50']:.3f} ms p99 {lm['p99']:.3f} ms "
+                      f"{r['transfer_MBps']:.0f} MB/s errors {r['errors']} cpu {r['cpu_s']} "
+                      f"elapsed {r['elapsed_s']:.2f}s", file=sys.stderr)
+            st = px.stats()
+            if li + 1 < len(layouts):
+                px.stop()
+                px = None
         out["proxy_stats"] = st
         cur, peak = rss_mb()
         out["proxy_rss_MB"] = {"before_proxy": rss0, "end": cur, "peak": peak,
                                "peak_minus_baseline": peak - rss0}
     finally:
-        px.stop()
+        if px is not None:
+            px.stop()
         origin.stdin.close()
         origin.wait(timeout=30)
     js = json.dumps(out, indent=1)

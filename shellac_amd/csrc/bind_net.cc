@@ -77,8 +77,9 @@ void bind_net(py::module_& m) {
                        std::vector<std::string> headers, const std::string& method,
                        double timeout_s, int64_t objects, double zipf_s,
                        const std::string& path_prefix, const std::string& path_suffix,
-                       uint64_t seed) {
+                       uint64_t seed, std::vector<int> cpus) {
     LoadConfig c;
+    c.cpus = std::move(cpus);
     c.objects = objects;
     c.zipf_s = zipf_s;
     c.path_prefix = path_prefix;
@@ -128,7 +129,8 @@ void bind_net(py::module_& m) {
      py::arg("keepalive") = true, py::arg("headers") = std::vector<std::string>{},
      py::arg("method") = "GET", py::arg("timeout_s") = 60.0, py::arg("objects") = 0,
      py::arg("zipf_s") = 0.99, py::arg("path_prefix") = "/obj/",
-     py::arg("path_suffix") = ".html", py::arg("seed") = 1);
+     py::arg("path_suffix") = ".html", py::arg("seed") = 1,
+     py::arg("cpus") = std::vector<int>{});
 
   m.def("md5_hex", [](py::bytes b) { return md5_hex(std::string(b)); });
 
@@ -238,7 +240,8 @@ void bind_net(py::module_& m) {
                        int client_timeout, int client_max_reqs, const std::string& balance,
                        bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
                        uint64_t stream_high_water, const std::string& health_path,
-                       int health_interval_ms, int health_timeout_ms, int health_fails) {
+                       int health_interval_ms, int health_timeout_ms, int health_fails,
+                       std::vector<int> cpus) {
              ProxyConfig c;
              c.upstreams = resolve_list(upstreams, 80);
              c.port = port;
@@ -260,6 +263,7 @@ void bind_net(py::module_& m) {
              c.health_interval_ms = health_interval_ms;
              c.health_timeout_ms = health_timeout_ms;
              c.health_fails = health_fails;
+             c.cpus = std::move(cpus);
              std::shared_ptr<CacheBackend> be;
              if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
              c.cache_enabled = be != nullptr;
@@ -273,7 +277,8 @@ void bind_net(py::module_& m) {
            py::arg("decode_gzip") = false, py::arg("upstream_retry_s") = 2,
            py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20,
            py::arg("health_path") = "", py::arg("health_interval_ms") = 1000,
-           py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2)
+           py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2,
+           py::arg("cpus") = std::vector<int>{})
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

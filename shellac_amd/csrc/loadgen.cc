@@ -169,6 +169,7 @@ LoadResult run_load(const LoadConfig& cfg) {
   };
 
   auto worker = [&](int tid) {
+    pin_thread(cfg.cpus, (size_t)tid);
     const int nconn = cfg.concurrency / cfg.threads + (tid < cfg.concurrency % cfg.threads ? 1 : 0);
     uint64_t rng = (cfg.seed + 1) * 0x9E3779B97F4A7C15ull ^ (uint64_t)(tid + 1) * 0xD1B54A32D192ED03ull;
     const int ep = epoll_create1(EPOLL_CLOEXEC);
@@ -193,6 +194,10 @@ LoadResult run_load(const LoadConfig& cfg) {
     auto close_conn = [&](int i) {
       LgConn& c = conns[i];
       if (c.fd < 0) return;
+      // abortive close (RST): a run leaves no TIME_WAIT sockets behind, so the next
+      // run's connect() does not crawl through thousands of them for a free port
+      const linger lg{1, 0};
+      setsockopt(c.fd, SOL_SOCKET, SO_LINGER, &lg, sizeof lg);
       epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
       close(c.fd);
       c.fd = -1;

@@ -18,6 +18,7 @@ struct LoadConfig {
   int concurrency = 10;              // ab -c
   int depth = 1;                     // pipelined requests per connection
   int threads = 1;
+  std::vector<int> cpus;  // worker t runs on cpus[t % size] (empty: unpinned)
   bool keepalive = true;             // ab -k
   double timeout_s = 60;
   // Generated request paths instead of `paths`: object ids 0..objects-1 as

@@ -6,6 +6,8 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -58,6 +60,17 @@ inline std::vector<Addr> resolve_list(const std::string& csv, uint16_t default_p
 inline void set_nonblock(int fd) {
   const int fl = fcntl(fd, F_GETFL, 0);
   fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+}
+
+// Pins the calling thread to cpus[i % size] (no-op for an empty list). Event-loop threads
+// pinned to distinct cores of one socket keep a request's loopback/NIC, socket-buffer
+// and reactor state in one L3 instead of migrating across a two-socket host.
+inline void pin_thread(const std::vector<int>& cpus, size_t i) {
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpus[i % cpus.size()], &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
 }
 
 inline void set_nodelay(int fd) {

@@ -1157,7 +1157,8 @@ void Proxy::start() {
   }
   for (size_t i = 0; i < reactors_.size(); ++i) {
     Reactor* rp = reactors_[i].get();
-    threads_.emplace_back([rp, i] {
+    threads_.emplace_back([this, rp, i] {
+      pin_thread(cfg_.cpus, i);
       const std::string nm = "shellac-rx" + std::to_string(i);  // per-thread CPU accounting
       pthread_setname_np(pthread_self(), nm.c_str());
       rp->loop();

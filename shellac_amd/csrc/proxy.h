@@ -37,6 +37,7 @@ struct ProxyConfig {
   uint16_t port = 8080;               // -p (Server.py:512)
   std::vector<Addr> upstreams;        // -s
   int threads = 1;
+  std::vector<int> cpus;  // reactor i runs on cpus[i % size] (empty: unpinned)
   uint32_t ttl = 170;                 // -t (Server.py:514)
   bool compress = false;              // -z: gzip uncompressed text before caching
   bool cache_enabled = true;

@@ -154,7 +154,10 @@ def serve_native_origin(argv=None) -> int:
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--random-body", action="store_true")
     ap.add_argument("--gzip-level", type=int, default=1)
+    ap.add_argument("--cpus", default="", help="run on these CPUs only ('0-3,8')")
     a = ap.parse_args(argv)
+    from .cpus import parse_cpus, pin_process
+    pin_process(parse_cpus(a.cpus))
     o = NativeOrigin(body_bytes=a.body, threads=a.threads, gzip_level=a.gzip_level,
                      random_body=a.random_body).start()
     print(f"port {o.port}", flush=True)
