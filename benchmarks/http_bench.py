@@ -97,12 +97,13 @@ def start_origin(body: int, threads: int, cpus=()) -> tuple[subprocess.Popen, in
 
 
 def load(port: int, n: int, conc: int, threads: int, objects: int, zipf: float, prefix: str,
-         seed: int, timeout: float, cpus=()) -> dict:
+         seed: int, timeout: float, cpus=(), spin_us: int = 0) -> dict:
     """One shellac-ab run in its own process; returns its JSON summary."""
     cmd = [sys.executable, "-m", "shellac_amd.bench.ab", "-n", str(n), "-c", str(conc), "-k",
            "--threads", str(threads), "--objects", str(objects), "--zipf", str(zipf),
            "--prefix", prefix, "--suffix", "", "--seed", str(seed), "--timeout", str(timeout),
            "-H", "Accept-Encoding: gzip", "--json", "--cpus", cpu_plan.format_cpus(cpus),
+           "--spin-us", str(spin_us),
            f"http://127.0.0.1:{port}/"]
     p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=timeout + 120,
                        env=HOST_ONLY)
@@ -135,6 +136,12 @@ def main():
                     help="auto: each reactor and load-generator worker on its own core of "
                          "the lowest allowed CPUs (one socket); the GPU batcher and the origin "
                          "on the last cores of the CPU budget")
+    ap.add_argument("--rx-spin-us", type=int, default=None,
+                    help="reactor busy-poll window (proxy --spin-us; default 200 when pinned, "
+                         "else 0)")
+    ap.add_argument("--lg-spin-us", type=int, default=None,
+                    help="load-generator busy-poll window (shellac-ab --spin-us; default 200 "
+                         "when pinned, else 0)")
     ap.add_argument("--cpu-budget", type=int, default=0,
                     help="CPUs to lay the processes over (default: the cgroup CPU quota)")
     ap.add_argument("--misc-cpus", type=int, default=0,
@@ -157,6 +164,11 @@ def main():
     pin = a.pin == "auto" and len(allowed) >= 4
     nmisc = a.misc_cpus or 1
     misc_cpus = allowed[-nmisc:] if pin else []
+    # busy-polling only on dedicated (pinned) cores
+    if a.rx_spin_us is None:
+        a.rx_spin_us = 200 if pin else 0
+    if a.lg_spin_us is None:
+        a.lg_spin_us = 200 if pin else 0
     or_cpus = allowed[-1:] if pin else []  # the origin idles once the cache is filled
 
     def layout_cpus(r, c):
@@ -187,13 +199,15 @@ def main():
            "hbm_gb": hbm_gb if a.backend in ("hbm", "tiered") else None,
            "cpu_count": os.cpu_count(), "cpu_budget": budget,
            "processes": "origin | proxy | load generator",
-           "cpus": {"proxy_other": misc_cpus, "origin": or_cpus}}
+           "cpus": {"proxy_other": misc_cpus, "origin": or_cpus},
+           "spin_us": {"reactors": a.rx_spin_us, "load_generator": a.lg_spin_us}}
     px = None
     try:
         for li, (nrx, ncl) in enumerate(layouts):
             rx_cpus, lg_cpus = layout_cpus(nrx, ncl)
             px = Server([("127.0.0.1", oport)], port=0, backend=backend, threads=nrx,
-                        client_max_reqs=1 << 30, cpus=rx_cpus).start()
+                        client_max_reqs=1 << 30, cpus=rx_cpus,
+                        spin_us=a.rx_spin_us).start()
             tag = "" if li == 0 else f"{nrx}x{ncl}_"
             out[f"{tag}layout"] = {"reactors": rx_cpus, "load_generator": lg_cpus}
             if li == 0:
@@ -205,11 +219,11 @@ def main():
                 time.sleep(1.0)
             for conc in a.conc:
                 load(px.port, min(50000, a.requests), conc, ncl, a.objects, a.zipf,
-                     prefix, 100 + conc, a.timeout, lg_cpus)
+                     prefix, 100 + conc, a.timeout, lg_cpus, a.lg_spin_us)
                 s0 = px.stats()
                 c0, l0 = thread_cpu(), os.times()
                 r = load(px.port, a.requests, conc, ncl, a.objects, a.zipf, prefix,
-                         200 + conc, a.timeout, lg_cpus)
+                         200 + conc, a.timeout, lg_cpus, a.lg_spin_us)
                 c1, l1 = thread_cpu(), os.times()
                 s1 = px.stats()
                 # where the CPU went during the run: proxy threads and the load generator

@@ -24,7 +24,8 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
         headers: Sequence[str] = (), depth: int = 1, threads: int = 1,
         paths: Optional[Sequence[str]] = None, method: str = "GET", timeout_s: float = 120.0,
         objects: int = 0, zipf_s: float = 0.99, path_prefix: str = "/obj/",
-        path_suffix: str = ".html", seed: int = 1, cpus: Sequence[int] = ()) -> dict:
+        path_suffix: str = ".html", seed: int = 1, cpus: Sequence[int] = (),
+        spin_us: int = 0) -> dict:
     """``objects`` > 0: request paths are generated natively — ``path_prefix + id +
     path_suffix`` with ids drawn Zipf(``zipf_s``) over ``objects`` objects, or in order
     (a cache-fill pass) when ``zipf_s`` is 0."""
@@ -37,7 +38,8 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
     res = core().run_load(host, port, list(paths) if paths else [path], int(requests),
                           int(concurrency), int(depth), int(threads), bool(keepalive),
                           list(headers), method, float(timeout_s), int(objects), float(zipf_s),
-                          path_prefix, path_suffix, int(seed), [int(c) for c in cpus])
+                          path_prefix, path_suffix, int(seed), [int(c) for c in cpus],
+                          int(spin_us))
     lat = np.asarray(res["latency"]) * 1e3
     done = int(res["completed"])
     el = float(res["elapsed_s"])
@@ -106,12 +108,14 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--timeout", type=float, default=120.0)
     p.add_argument("--cpus", default="", help="pin worker threads to these CPUs ('0-3,8')")
+    p.add_argument("--spin-us", type=int, default=0,
+                   help="workers busy-poll this long after their last event (pinned cores)")
     p.add_argument("url")
     a = p.parse_args(argv)
     t0 = time.time()
     r = run(a.url, a.n, a.c, a.k, a.H, a.depth, a.threads, timeout_s=a.timeout,
             objects=a.objects, zipf_s=a.zipf, path_prefix=a.prefix, path_suffix=a.suffix,
-            seed=a.seed, cpus=parse_cpus(a.cpus))
+            seed=a.seed, cpus=parse_cpus(a.cpus), spin_us=a.spin_us)
     if a.g:
         write_gnuplot(a.g, r, t0)
     pub = {k: v for k, v in r.items() if not k.startswith("_")}

@@ -102,6 +102,7 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
       HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.d), a.h, 0));
       a.cap = c;
       allocated_.fetch_add(c, std::memory_order_relaxed);
+      allocs_.fetch_add(1, std::memory_order_relaxed);
     }
     auto pool = shared_from_this();
     return std::shared_ptr<Arena>(new Arena(a), [pool](Arena* p) {
@@ -110,6 +111,8 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
     });
   }
   uint64_t allocated() const { return allocated_.load(std::memory_order_relaxed); }
+  uint64_t allocs() const { return allocs_.load(std::memory_order_relaxed); }
+  uint64_t frees() const { return frees_.load(std::memory_order_relaxed); }
 
  private:
   void give_back(const Arena& a) {
@@ -120,11 +123,12 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
     }
     (void)hipHostFree(a.h);
     allocated_.fetch_sub(a.cap, std::memory_order_relaxed);
+    frees_.fetch_add(1, std::memory_order_relaxed);
   }
   int device_;
   std::mutex mu_;
   std::vector<Arena> free_;
-  std::atomic<uint64_t> allocated_{0};
+  std::atomic<uint64_t> allocated_{0}, allocs_{0}, frees_{0};
 };
 
 }  // namespace
@@ -1070,9 +1074,15 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));
   out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
-  uint64_t arena = 0;
-  for (auto& d : devs_) arena += d->pool->allocated();
+  uint64_t arena = 0, aallocs = 0, afrees = 0;
+  for (auto& d : devs_) {
+    arena += d->pool->allocated();
+    aallocs += d->pool->allocs();
+    afrees += d->pool->frees();
+  }
   out->emplace_back("hbm_arena_bytes", arena);
+  out->emplace_back("hbm_arena_allocs", aallocs);
+  out->emplace_back("hbm_arena_frees", afrees);
   if (cfg_.presence_filter) {
     uint64_t adds = 0;
     for (auto& d : devs_) adds += std::atomic_load(&d->filt)->adds();

@@ -77,8 +77,9 @@ void bind_net(py::module_& m) {
                        std::vector<std::string> headers, const std::string& method,
                        double timeout_s, int64_t objects, double zipf_s,
                        const std::string& path_prefix, const std::string& path_suffix,
-                       uint64_t seed, std::vector<int> cpus) {
+                       uint64_t seed, std::vector<int> cpus, int spin_us) {
     LoadConfig c;
+    c.spin_us = spin_us;
     c.cpus = std::move(cpus);
     c.objects = objects;
     c.zipf_s = zipf_s;
@@ -130,7 +131,7 @@ void bind_net(py::module_& m) {
      py::arg("method") = "GET", py::arg("timeout_s") = 60.0, py::arg("objects") = 0,
      py::arg("zipf_s") = 0.99, py::arg("path_prefix") = "/obj/",
      py::arg("path_suffix") = ".html", py::arg("seed") = 1,
-     py::arg("cpus") = std::vector<int>{});
+     py::arg("cpus") = std::vector<int>{}, py::arg("spin_us") = 0);
 
   m.def("md5_hex", [](py::bytes b) { return md5_hex(std::string(b)); });
 
@@ -241,8 +242,9 @@ void bind_net(py::module_& m) {
                        bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
                        uint64_t stream_high_water, const std::string& health_path,
                        int health_interval_ms, int health_timeout_ms, int health_fails,
-                       std::vector<int> cpus) {
+                       std::vector<int> cpus, int spin_us) {
              ProxyConfig c;
+             c.spin_us = spin_us;
              c.upstreams = resolve_list(upstreams, 80);
              c.port = port;
              c.bind = bind;
@@ -278,7 +280,7 @@ void bind_net(py::module_& m) {
            py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20,
            py::arg("health_path") = "", py::arg("health_interval_ms") = 1000,
            py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2,
-           py::arg("cpus") = std::vector<int>{})
+           py::arg("cpus") = std::vector<int>{}, py::arg("spin_us") = 0)
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

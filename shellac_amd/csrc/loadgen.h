@@ -19,6 +19,7 @@ struct LoadConfig {
   int depth = 1;                     // pipelined requests per connection
   int threads = 1;
   std::vector<int> cpus;  // worker t runs on cpus[t % size] (empty: unpinned)
+  int spin_us = 0;        // > 0: poll epoll without sleeping for this long after an event
   bool keepalive = true;             // ab -k
   double timeout_s = 60;
   // Generated request paths instead of `paths`: object ids 0..objects-1 as

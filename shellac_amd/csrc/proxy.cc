@@ -139,6 +139,16 @@ class Reactor : public Executor {
       bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
       cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0},
       streamed{0}, stream_pauses{0};
+  // event-loop health: the longest iteration (events handled between two epoll_waits)
+  // and how many took over 10 ms — a reactor that stalls stops accepting connections
+  std::atomic<uint64_t> loop_max_us{0}, loop_slow{0};
+  // longest single step per kind: accept, client event, upstream event, posted
+  // completions, timer (gc)
+  std::atomic<uint64_t> phase_max_us[5] = {};
+  void phase_done(int k, double t0) {
+    const uint64_t us = (uint64_t)((now_s() - t0) * 1e6);
+    if (us > phase_max_us[k].load(std::memory_order_relaxed)) phase_max_us[k].store(us);
+  }
   std::atomic<uint64_t> hist[kHistBuckets] = {};
 
  private:
@@ -284,12 +294,19 @@ void Reactor::rearm(Conn* c) {
 
 void Reactor::loop() {
   epoll_event evs[256];
+  const double spin_s = cfg_.spin_us * 1e-6;
+  double last_work = now_s();
   while (px_->running_) {
-    const int n = epoll_wait(epfd_, evs, 256, 100);
+    const bool spin = spin_s > 0 && now_s() - last_work < spin_s;
+    const int n = epoll_wait(epfd_, evs, 256, spin ? 0 : 100);
+    const double t_it = n > 0 ? now_s() : 0;
+    if (n > 0 && spin_s > 0) last_work = t_it;
     for (int i = 0; i < n; ++i) {
       const uint64_t id = evs[i].data.u64;
+      const double t0 = now_s();
       if (id == kListenId) {
         accept_all();
+        phase_done(0, t0);
       } else if (id == kEventId) {
         uint64_t v;
         (void)!read(evfd_, &v, 8);
@@ -297,17 +314,32 @@ void Reactor::loop() {
         uint64_t v;
         (void)!read(timerfd_, &v, 8);
         gc();
+        phase_done(4, t0);
       } else {
         auto it = conns_.find(id);
         if (it == conns_.end() || it->second->dead) continue;
         Conn* c = it->second;
-        if (c->kind == 0) on_client(static_cast<Client*>(c), evs[i].events);
-        else on_upstream(static_cast<Upstream*>(c), evs[i].events);
+        if (c->kind == 0) {
+          on_client(static_cast<Client*>(c), evs[i].events);
+          phase_done(1, t0);
+        } else {
+          on_upstream(static_cast<Upstream*>(c), evs[i].events);
+          phase_done(2, t0);
+        }
       }
     }
-    drain_posted();
+    {
+      const double t0 = now_s();
+      drain_posted();
+      phase_done(3, t0);
+    }
     for (Conn* c : graveyard_) delete c;
     graveyard_.clear();
+    if (n > 0) {
+      const uint64_t us = (uint64_t)((now_s() - t_it) * 1e6);
+      if (us > loop_max_us.load(std::memory_order_relaxed)) loop_max_us.store(us);
+      if (us > 10000) loop_slow.fetch_add(1, std::memory_order_relaxed);
+    }
   }
 }
 
@@ -1179,7 +1211,9 @@ void Proxy::stop() {
 
 std::string Proxy::stats_json() {
   uint64_t req = 0, hit = 0, miss = 0, ur = 0, resp = 0, bo = 0, err = 0, cl = 0, up = 0, acc = 0,
-           gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0, stm = 0, stp = 0;
+           gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0, stm = 0, stp = 0, lmax = 0,
+           lslow = 0;
+  uint64_t pmax[5] = {};
   uint64_t h[kHistBuckets] = {};
   for (auto& r : reactors_) {
     req += r->requests; hit += r->hits; miss += r->misses; ur += r->upstream_reqs;
@@ -1187,6 +1221,9 @@ std::string Proxy::stats_json() {
     up += r->upstreams; acc += r->accepts; gcc += r->gc_closed; sets += r->cache_sets;
     bad += r->bad_requests; uf += r->upstream_failures; rt += r->retries; col += r->collapsed;
     stm += r->streamed; stp += r->stream_pauses;
+    lmax = std::max<uint64_t>(lmax, r->loop_max_us);
+    lslow += r->loop_slow;
+    for (int k = 0; k < 5; ++k) pmax[k] = std::max<uint64_t>(pmax[k], r->phase_max_us[k]);
     for (int b = 0; b < kHistBuckets; ++b) h[b] += r->hist[b];
   }
   uint64_t total = 0;
@@ -1209,6 +1246,10 @@ std::string Proxy::stats_json() {
     << ",\"upstream_failures\":" << uf << ",\"retries\":" << rt << ",\"collapsed\":" << col
     << ",\"streamed\":" << stm << ",\"stream_pauses\":" << stp << ",\"clients\":" << cl
     << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
+    << ",\"loop_max_us\":" << lmax << ",\"loop_slow\":" << lslow
+    << ",\"loop_phase_max_us\":{\"accept\":" << pmax[0] << ",\"client\":" << pmax[1]
+    << ",\"upstream\":" << pmax[2] << ",\"posted\":" << pmax[3] << ",\"timer\":" << pmax[4]
+    << "}"
     << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
     << total << "}";
   o << ",\"health_checks\":" << health_checks_.load()

@@ -38,6 +38,9 @@ struct ProxyConfig {
   std::vector<Addr> upstreams;        // -s
   int threads = 1;
   std::vector<int> cpus;  // reactor i runs on cpus[i % size] (empty: unpinned)
+  // > 0: a reactor that had work within the last spin_us polls epoll without sleeping
+  // (a dedicated core: no wake-up IPI or idle-state exit per request under load)
+  int spin_us = 0;
   uint32_t ttl = 170;                 // -t (Server.py:514)
   bool compress = false;              // -z: gzip uncompressed text before caching
   bool cache_enabled = true;

@@ -123,7 +123,7 @@ class Server:
                  stream_bytes: int = 1 << 20, stream_high_water: int = 8 << 20,
                  health_path: str = "", health_interval_ms: int = 1000,
                  health_timeout_ms: int = 500, health_fails: int = 2,
-                 cpus: Sequence[int] = (), **backend_opts):
+                 cpus: Sequence[int] = (), spin_us: int = 0, **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
         self._backend = backend
@@ -137,7 +137,7 @@ class Server:
             decode_gzip=decode_gzip, stream_bytes=stream_bytes,
             stream_high_water=stream_high_water, health_path=health_path,
             health_interval_ms=health_interval_ms, health_timeout_ms=health_timeout_ms,
-            health_fails=health_fails, cpus=[int(c) for c in cpus])
+            health_fails=health_fails, cpus=[int(c) for c in cpus], spin_us=int(spin_us))
         self._started = False
 
     @property
@@ -210,6 +210,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--bind", default="0.0.0.0")
     p.add_argument("--cpus", default="",
                    help="pin reactor i to the i-th of these CPUs, e.g. 0-7 (default: unpinned)")
+    p.add_argument("--spin-us", type=int, default=0,
+                   help="reactors busy-poll this long after their last event before sleeping "
+                        "(with --cpus: dedicated cores)")
     p.add_argument("--policy", choices=["rfc", "reference"], default="rfc",
                    help="rfc: cache GET 200/301/404.. honouring Cache-Control; reference: cache everything")
     p.add_argument("--balance", choices=["random", "roundrobin", "leastconn"], default="random")
@@ -258,7 +261,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  balance=args.balance, bind=args.bind, decode_gzip=args.decode_gzip,
                  stream_bytes=args.stream_bytes, health_path=args.health_check,
                  health_interval_ms=args.health_interval_ms, health_fails=args.health_fails,
-                 cpus=parse_cpus(args.cpus),
+                 cpus=parse_cpus(args.cpus), spin_us=args.spin_us,
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,
