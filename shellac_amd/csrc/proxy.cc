@@ -141,7 +141,7 @@ class Reactor : public Executor {
       streamed{0}, stream_pauses{0};
   // event-loop health: the longest iteration (events handled between two epoll_waits)
   // and how many took over 10 ms — a reactor that stalls stops accepting connections
-  std::atomic<uint64_t> loop_max_us{0}, loop_slow{0};
+  std::atomic<uint64_t> loop_max_us{0}, loop_slow{0}, client_resets{0};
   // longest single step per kind: accept, client event, upstream event, posted
   // completions, timer (gc)
   std::atomic<uint64_t> phase_max_us[5] = {};
@@ -430,7 +430,9 @@ void Reactor::on_client(Client* c, uint32_t ev) {
         return;
       }
       if (errno == EAGAIN || errno == EWOULDBLOCK) break;
-      errors++;
+      // a client that resets its connection has just gone away; not a proxy error
+      if (errno == ECONNRESET) client_resets++;
+      else errors++;
       close_client(c);
       return;
     }
@@ -565,7 +567,8 @@ void Reactor::flush_client(Client* c) {
         arm(c, true);
         return;
       }
-      errors++;
+      if (errno == ECONNRESET || errno == EPIPE) client_resets++;
+      else errors++;
       close_client(c);
       return;
     }
@@ -1213,7 +1216,7 @@ std::string Proxy::stats_json() {
   uint64_t req = 0, hit = 0, miss = 0, ur = 0, resp = 0, bo = 0, err = 0, cl = 0, up = 0, acc = 0,
            gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0, stm = 0, stp = 0, lmax = 0,
            lslow = 0;
-  uint64_t pmax[5] = {};
+  uint64_t pmax[5] = {}, crst = 0;
   uint64_t h[kHistBuckets] = {};
   for (auto& r : reactors_) {
     req += r->requests; hit += r->hits; miss += r->misses; ur += r->upstream_reqs;
@@ -1223,6 +1226,7 @@ std::string Proxy::stats_json() {
     stm += r->streamed; stp += r->stream_pauses;
     lmax = std::max<uint64_t>(lmax, r->loop_max_us);
     lslow += r->loop_slow;
+    crst += r->client_resets;
     for (int k = 0; k < 5; ++k) pmax[k] = std::max<uint64_t>(pmax[k], r->phase_max_us[k]);
     for (int b = 0; b < kHistBuckets; ++b) h[b] += r->hist[b];
   }
@@ -1246,6 +1250,7 @@ std::string Proxy::stats_json() {
     << ",\"upstream_failures\":" << uf << ",\"retries\":" << rt << ",\"collapsed\":" << col
     << ",\"streamed\":" << stm << ",\"stream_pauses\":" << stp << ",\"clients\":" << cl
     << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
+    << ",\"client_resets\":" << crst
     << ",\"loop_max_us\":" << lmax << ",\"loop_slow\":" << lslow
     << ",\"loop_phase_max_us\":{\"accept\":" << pmax[0] << ",\"client\":" << pmax[1]
     << ",\"upstream\":" << pmax[2] << ",\"posted\":" << pmax[3] << ",\"timer\":" << pmax[4]
