@@ -83,6 +83,32 @@ def cgroup_cpus() -> int:
         return 0
 
 
+def cgroup_throttle() -> dict:
+    """nr_throttled / throttled_usec of this cgroup (CPU quota enforcement)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            st = dict(l.split() for l in f if l.strip())
+        return {k: int(st[k]) for k in ("nr_throttled", "throttled_usec") if k in st}
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_ticks(cpus) -> dict:
+    """/proc/stat jiffies per CPU: {cpu: (user, system, irq, softirq, idle)}."""
+    out = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = line.split()
+                    c = int(v[0][3:])
+                    if c in cpus:
+                        out[c] = (int(v[1]) + int(v[2]), int(v[3]), int(v[6]), int(v[7]), int(v[4]))
+    except OSError:
+        pass
+    return out
+
+
 def start_origin(body: int, threads: int, cpus=()) -> tuple[subprocess.Popen, int]:
     p = subprocess.Popen([sys.executable, "-m", "shellac_amd.utils.origin", "--body", str(body),
                           "--threads", str(threads), "--random-body",
@@ -221,10 +247,15 @@ def main():
                 load(px.port, min(50000, a.requests), conc, ncl, a.objects, a.zipf,
                      prefix, 100 + conc, a.timeout, lg_cpus, a.lg_spin_us)
                 s0 = px.stats()
-                c0, l0 = thread_cpu(), os.times()
+                c0, l0, g0 = thread_cpu(), os.times(), cgroup_throttle()
+                k0 = cpu_ticks(set(allowed))
                 r = load(px.port, a.requests, conc, ncl, a.objects, a.zipf, prefix,
                          200 + conc, a.timeout, lg_cpus, a.lg_spin_us)
-                c1, l1 = thread_cpu(), os.times()
+                c1, l1, g1 = thread_cpu(), os.times(), cgroup_throttle()
+                r["cgroup_throttled"] = {k: g1[k] - g0.get(k, 0) for k in g1}
+                k1 = cpu_ticks(set(allowed))
+                # per core: (user, system, irq, softirq, idle) jiffies during the run
+                r["core_ticks"] = {c: [b - a for a, b in zip(k0[c], k1[c])] for c in k1 if c in k0}
                 s1 = px.stats()
                 # where the CPU went during the run: proxy threads and the load generator
                 r["cpu_s"] = {k: round(c1.get(k, 0) - c0.get(k, 0), 2) for k in c1}
@@ -241,7 +272,9 @@ def main():
                       f"(steady {r['steady_rps']:.0f}) hit ratio {r['hit_ratio']:.4f} "
                       f"p50 {lm['p50']:.3f} ms p99 {lm['p99']:.3f} ms "
                       f"{r['transfer_MBps']:.0f} MB/s errors {r['errors']} cpu {r['cpu_s']} "
-                      f"elapsed {r['elapsed_s']:.2f}s", file=sys.stderr)
+                      f"elapsed {r['elapsed_s']:.2f}s connect {r.get('connect_lat_ms')} "
+                      f"connect() {r.get('connect_call_ms')} open {r.get('open_loop_ms')} "
+                      f"throttled {r['cgroup_throttled']}", file=sys.stderr)
             st = px.stats()
             if li + 1 < len(layouts):
                 px.stop()

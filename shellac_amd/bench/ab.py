@@ -61,6 +61,16 @@ def run(url: str, requests: int = 1000, concurrency: int = 10, keepalive: bool =
         "steady_rps": steady,
         "ramp_ms": ramp_ms,
         "connect_ms": float(res["connected_s"]) * 1e3,
+        # per connection, connect() -> writable: a handshake the server's accept queue
+        # dropped shows here as a SYN retransmission (>= 1 s)
+        "connect_lat_ms": ({"p50": float(np.percentile(res["connect_lat"], 50)) * 1e3,
+                            "p99": float(np.percentile(res["connect_lat"], 99)) * 1e3,
+                            "max": float(np.max(res["connect_lat"])) * 1e3}
+                           if len(res["connect_lat"]) else None),
+        "connect_call_ms": ({"p50": float(np.percentile(res["connect_call"], 50)) * 1e3,
+                             "max": float(np.max(res["connect_call"])) * 1e3}
+                            if len(res["connect_call"]) else None),
+        "open_loop_ms": float(res["open_loop_s"]) * 1e3,
         "transfer_MBps": res["bytes"] / el / 1e6 if el > 0 else 0.0,
         "errors": int(res["errors"]),
         "non2xx": int(res["non2xx"]),

@@ -131,6 +131,9 @@ struct HbmBackendConfig {
   // ...and is then warmed from its peers over xGMI: the objects of its key range that
   // other shards took while it was out are peer-copied back (hipMemcpyPeerAsync)
   bool warm_restore = true;
+  // Pinned response arenas allocated up front per GPU (depth + 2 of this size): pinning
+  // host memory mid-run stalled every socket call on the box for up to ~0.5 s
+  uint64_t arena_bytes = 16u << 20;
 };
 
 // One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are

@@ -71,7 +71,10 @@ struct Mapped {
 
 // Pinned response arenas. A GET batch gathers into one; its hits are ByteRef slices that
 // own a reference, so the arena returns to the pool (not to the allocator) when the last
-// response built from it has been written to its client.
+// response built from it has been written to its client. Pinned allocations and frees
+// are slow and hipHostFree waits for the device, so neither happens on a reactor thread:
+// give_back() only files the arena; take() (the batcher) picks the smallest one that
+// fits and trims the pool beyond kKeepBytes of idle arenas.
 class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
  public:
   struct Arena {
@@ -79,27 +82,48 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
     uint8_t* d = nullptr;
     size_t cap = 0;
   };
+  static constexpr size_t kKeepBytes = size_t(1) << 30;  // idle arenas kept (per GPU)
   explicit ArenaPool(int device) : device_(device) {}
   ~ArenaPool() {
     for (auto& a : free_) (void)hipHostFree(a.h);
   }
   std::shared_ptr<Arena> take(size_t min_cap) {
     Arena a{};
+    std::vector<Arena> trim;
     {
       std::lock_guard<std::mutex> lk(mu_);
+      int best = -1;
       for (size_t i = 0; i < free_.size(); ++i)
-        if (free_[i].cap >= min_cap) {
-          a = free_[i];
-          free_.erase(free_.begin() + (long)i);
-          break;
-        }
+        if (free_[i].cap >= min_cap && (best < 0 || free_[i].cap < free_[(size_t)best].cap))
+          best = (int)i;
+      if (best >= 0) {
+        a = free_[(size_t)best];
+        free_.erase(free_.begin() + best);
+        free_bytes_ -= a.cap;
+      }
+      while (free_bytes_ > kKeepBytes && !free_.empty()) {  // the smallest idle arenas go
+        size_t k = 0;
+        for (size_t i = 1; i < free_.size(); ++i)
+          if (free_[i].cap < free_[k].cap) k = i;
+        free_bytes_ -= free_[k].cap;
+        trim.push_back(free_[k]);
+        free_.erase(free_.begin() + (long)k);
+      }
+    }
+    for (const Arena& t : trim) {
+      (void)hipHostFree(t.h);
+      allocated_.fetch_sub(t.cap, std::memory_order_relaxed);
+      frees_.fetch_add(1, std::memory_order_relaxed);
     }
     if (!a.h) {
       size_t c = 1u << 20;
       while (c < min_cap) c *= 2;
       HB_OK(hipSetDevice(device_));
+      const double t0 = wall_s();
       HB_OK(hipHostMalloc(reinterpret_cast<void**>(&a.h), c, hipHostMallocMapped));
       HB_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.d), a.h, 0));
+      const uint64_t us = (uint64_t)((wall_s() - t0) * 1e6);
+      if (us > alloc_max_us_.load(std::memory_order_relaxed)) alloc_max_us_.store(us);
       a.cap = c;
       allocated_.fetch_add(c, std::memory_order_relaxed);
       allocs_.fetch_add(1, std::memory_order_relaxed);
@@ -110,25 +134,27 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
       delete p;
     });
   }
+  // n arenas of cap bytes into the free list (at start-up, before any traffic)
+  void reserve(size_t n, size_t cap) {
+    std::vector<std::shared_ptr<Arena>> held;
+    for (size_t i = 0; i < n; ++i) held.push_back(take(cap));
+  }  // returned to the pool here
   uint64_t allocated() const { return allocated_.load(std::memory_order_relaxed); }
   uint64_t allocs() const { return allocs_.load(std::memory_order_relaxed); }
   uint64_t frees() const { return frees_.load(std::memory_order_relaxed); }
+  uint64_t alloc_max_us() const { return alloc_max_us_.load(std::memory_order_relaxed); }
 
  private:
-  void give_back(const Arena& a) {
+  void give_back(const Arena& a) {  // any thread (often a reactor): no HIP call here
     std::lock_guard<std::mutex> lk(mu_);
-    if (free_.size() < 16) {
-      free_.push_back(a);
-      return;
-    }
-    (void)hipHostFree(a.h);
-    allocated_.fetch_sub(a.cap, std::memory_order_relaxed);
-    frees_.fetch_add(1, std::memory_order_relaxed);
+    free_.push_back(a);
+    free_bytes_ += a.cap;
   }
   int device_;
   std::mutex mu_;
   std::vector<Arena> free_;
-  std::atomic<uint64_t> allocated_{0}, allocs_{0}, frees_{0};
+  size_t free_bytes_ = 0;
+  std::atomic<uint64_t> allocated_{0}, allocs_{0}, frees_{0}, alloc_max_us_{0};
 };
 
 }  // namespace
@@ -262,6 +288,7 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
       HB_OK(hipMemcpy(d->d_own, ho.data(), ho.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     d->pool = std::make_shared<ArenaPool>(d->device);
+    if (cfg_.arena_bytes) d->pool->reserve((size_t)cfg_.depth + 2, (size_t)cfg_.arena_bytes);
     for (int k = 0; k < cfg_.depth; ++k) {
       auto f = std::make_unique<Flight>();
       HB_OK(hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
@@ -1074,8 +1101,9 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));
   out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
-  uint64_t arena = 0, aallocs = 0, afrees = 0;
+  uint64_t arena = 0, aallocs = 0, afrees = 0, amax = 0;
   for (auto& d : devs_) {
+    amax = std::max<uint64_t>(amax, d->pool->alloc_max_us());
     arena += d->pool->allocated();
     aallocs += d->pool->allocs();
     afrees += d->pool->frees();
@@ -1083,6 +1111,7 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_arena_bytes", arena);
   out->emplace_back("hbm_arena_allocs", aallocs);
   out->emplace_back("hbm_arena_frees", afrees);
+  out->emplace_back("hbm_arena_alloc_max_us", amax);
   if (cfg_.presence_filter) {
     uint64_t adds = 0;
     for (auto& d : devs_) adds += std::atomic_load(&d->filt)->adds();

@@ -117,6 +117,9 @@ void bind_net(py::module_& m) {
     d["completed"] = r.completed;
     d["elapsed_s"] = r.elapsed_s;
     d["connected_s"] = r.connected_s;
+    d["connect_lat"] = r.connect_lat;
+    d["connect_call"] = r.connect_call;
+    d["open_loop_s"] = r.open_loop_s;
     d["bytes"] = r.bytes;
     d["errors"] = r.errors;
     d["non2xx"] = r.non2xx;

@@ -124,6 +124,7 @@ struct LgConn {
   bool use_parser = false;
   size_t path_idx = 0;
   bool out_armed = true;    // EPOLLOUT in the interest set
+  double t_connect = 0;     // when connect() was called
 };
 }  // namespace
 
@@ -133,6 +134,8 @@ LoadResult run_load(const LoadConfig& cfg) {
   const Addr addr = resolve(cfg.host + ":" + std::to_string(cfg.port), cfg.port);
   std::atomic<int64_t> issued{0};
   std::vector<std::vector<LoadSample>> per_thread(cfg.threads);
+  std::vector<std::vector<double>> conn_lat(cfg.threads), conn_call(cfg.threads);
+  std::vector<double> open_loop(cfg.threads, 0.0);
   std::atomic<uint64_t> bytes{0}, errors{0}, non2xx{0}, reconnects{0};
   std::vector<double> connected_at(cfg.threads, 0.0);  // last connection up, per thread
 
@@ -195,6 +198,7 @@ LoadResult run_load(const LoadConfig& cfg) {
     *out += tail;
   };
 
+  reserve_fd_table(cfg.concurrency + 256);
   // the clock starts at the first connection, after the path tables are built (the
   // Zipf CDF of 8M objects alone takes ~0.1 s)
   const double t_start = now_s();
@@ -238,7 +242,9 @@ LoadResult run_load(const LoadConfig& cfg) {
     auto open_conn = [&](int i) {
       LgConn& c = conns[i];
       c = LgConn();
+      c.t_connect = now_s();
       c.fd = connect_nonblock(addr);
+      conn_call[tid].push_back(now_s() - c.t_connect);
       if (c.fd < 0) return false;
       c.parser = std::make_unique<HttpParser>(false);
       c.parser->set_eof_body(true);
@@ -296,6 +302,7 @@ LoadResult run_load(const LoadConfig& cfg) {
       epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
       c.out_armed = want;
     };
+    const double t_open = now_s();
     for (int i = 0; i < nconn; ++i) {
       if (!work_left()) break;  // fewer requests than connections: open only what is used
       if (open_conn(i)) {
@@ -305,6 +312,7 @@ LoadResult run_load(const LoadConfig& cfg) {
         if (conns[i].sent.empty()) close_conn(i);
       }
     }
+    open_loop[tid] = now_s() - t_open;
     char buf[1 << 16];
     epoll_event evs[256];
     const double spin_s = cfg.spin_us * 1e-6;
@@ -329,7 +337,9 @@ LoadResult run_load(const LoadConfig& cfg) {
               continue;
             }
             c.connected = true;
-            connected_at[tid] = std::max(connected_at[tid], now_s() - t_start);
+            const double tc = now_s();
+            connected_at[tid] = std::max(connected_at[tid], tc - t_start);
+            conn_lat[tid].push_back(tc - c.t_connect);
           }
         }
         flush(c);
@@ -431,6 +441,9 @@ LoadResult run_load(const LoadConfig& cfg) {
   res.non2xx = non2xx;
   res.reconnects = reconnects;
   res.connected_s = *std::max_element(connected_at.begin(), connected_at.end());
+  for (auto& v : conn_lat) res.connect_lat.insert(res.connect_lat.end(), v.begin(), v.end());
+  for (auto& v : conn_call) res.connect_call.insert(res.connect_call.end(), v.begin(), v.end());
+  res.open_loop_s = *std::max_element(open_loop.begin(), open_loop.end());
   return res;
 }
 

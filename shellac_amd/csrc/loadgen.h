@@ -44,6 +44,9 @@ struct LoadResult {
   uint64_t completed = 0, bytes = 0, errors = 0, non2xx = 0, reconnects = 0;
   double elapsed_s = 0;
   double connected_s = 0;  // when the last connection completed its handshake
+  std::vector<double> connect_lat;  // per connection: connect() call -> writable (s)
+  std::vector<double> connect_call;  // per connection: the connect() syscall itself (s)
+  double open_loop_s = 0;            // longest per-thread loop opening its connections
 };
 
 LoadResult run_load(const LoadConfig& cfg);

@@ -1182,6 +1182,7 @@ void Proxy::upstream_failed(int idx, double now) {
 
 void Proxy::start() {
   SH_CHECK(!running_, "already running");
+  reserve_fd_table(cfg_.max_fds);
   start_time_ = now_s();
   const int first = listen_tcp(cfg_.bind, cfg_.port, cfg_.threads > 1, cfg_.backlog);
   port_ = local_port(first);

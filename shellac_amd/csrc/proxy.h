@@ -70,6 +70,7 @@ struct ProxyConfig {
   // client, and resumes below a quarter of it.
   uint64_t stream_high_water = 8 << 20;
   int backlog = 1024;
+  int max_fds = 1 << 16;  // fd table reserved at start (capped by RLIMIT_NOFILE)
   std::string server_name = "Shellac/0.2.0";
 };
 
