@@ -160,6 +160,19 @@ class ShardedCache:
         # GET coalescing: the duplicate keys of a batch share one probe and one record
         # (ops.cache.coalesce); SHELLAC_COALESCE=0 probes and copies every request
         self.coalesce = os.environ.get("SHELLAC_COALESCE", "1") != "0"
+        # Two measured, opt-in schedules (profiles/r2_step_schedule_ab.md; both slower on
+        # the 1M-GET bench step, so off by default):
+        # SHELLAC_COMPACT=1: compacting coalesced lookups — response offsets by bump
+        #   allocation, the gather copies a compacted hit list, no scan launch between
+        #   probe and gather (0.354 vs 0.322 ms: the gather then starts under the SET's
+        #   log append and both bandwidth-bound copies share the memory system)
+        self.compact = os.environ.get("SHELLAC_COMPACT", "0") == "1"
+        # SHELLAC_PLAN_FIRST=1: the SET's planning kernels (dedupe, sizes, scan) run
+        #   before the GET lookup instead of beside it (dedupe 10 us alone vs 48-92 us
+        #   beside k_coalesce, but k_coalesce then takes 139 us beside the log append and
+        #   the extra cross-stream wait costs ~14 us: 0.36 ms)
+        self.plan_first = os.environ.get("SHELLAC_PLAN_FIRST", "0") == "1"
+        self._plan_done = None
         self._side = None
         self._probe_done = None  # event: this step's probe is done (SET index may run)
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
@@ -196,7 +209,7 @@ class ShardedCache:
         self.stats["get_requests"] += n
         if self.world == 1:
             if self.coalesce:
-                lk, first, _ = self.shard.lookup_coalesced(keys, now)
+                lk, first, _ = self.shard.lookup_coalesced(keys, now, compact=self.compact)
             else:
                 lk, first = self.shard.lookup(keys, now), None
             data = self.shard.gather(lk)
@@ -295,10 +308,19 @@ class ShardedCache:
             main = torch.cuda.current_stream(self.device)
             side.wait_stream(main)  # the previous step's gather is done with the log
             now = sh.now() if now is None else now
+            if self.plan_first:
+                with torch.cuda.stream(side):
+                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                             batch.expire, now, begin_only=True)
+                pe = self._plan_done
+                if pe is None:
+                    pe = self._plan_done = torch.cuda.Event()
+                pe.record(side)
+                main.wait_event(pe)
         if self.coalesce:
             table = self._coalesce_table(n) if side is not None else None
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
-                                                   table=table)
+                                                   table=table, compact=self.compact)
         else:
             lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound, total_slot=0),
                                        None, None, None)
@@ -318,8 +340,11 @@ class ShardedCache:
             out_size = torch.empty(n, dtype=torch.int64, device=self.device)
             out_off = torch.empty(n, dtype=torch.int64, device=self.device)
         with torch.cuda.stream(side):
-            sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                     batch.expire, now, index_after=ev)
+            if self.plan_first:
+                sh.store_finish(index_after=ev)
+            else:
+                sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                         batch.expire, now, index_after=ev)
             if first is not None:
                 # per-request (size, off) and the table clean-up, under the gather
                 expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)

@@ -170,7 +170,12 @@ def expand_out(first: torch.Tensor, size: torch.Tensor, off: torch.Tensor,
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
     size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
-    off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
+    off: torch.Tensor   # int64 [n+1] response offset per key; off[n] = total bytes
+    # compacting lookups (``lookup_coalesced(compact=True)``): the hits as a segment list
+    # sorted by response offset — log loc, response offset, and the count on the device
+    seg_src: Optional[torch.Tensor] = None  # int64 [n+1]
+    seg_dst: Optional[torch.Tensor] = None  # int64 [n+1]; seg_dst[nseg] = total
+    nseg: Optional[torch.Tensor] = None     # int64 [1]
 
     @property
     def n(self) -> int:
@@ -273,7 +278,7 @@ class CacheShard:
 
     def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
                          reserve_bytes: int = 0, total_slot: int = -1,
-                         table: Optional[torch.Tensor] = None):
+                         table: Optional[torch.Tensor] = None, compact: bool = False):
         """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
         row that claims a digest probes the index for it). Returns (Lookup, first,
         cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
@@ -281,7 +286,12 @@ class CacheShard:
         >= ``coalesce_table_slots(n)`` power-of-two slots) — then ``cslot`` holds each
         claimer's slot and ``expand_out`` must run to clean the table again; otherwise
         a temporary table is zeroed here and ``cslot`` is None. CPU shards: a plain
-        lookup, ``first = cslot = None``."""
+        lookup, ``first = cslot = None``.
+        ``compact`` (GPU): no scan pass — hits take response offsets from one bump
+        allocation per 1024-key chunk (records in claim order, not row order) and form a
+        compacted segment list the gather copies; ``off`` is valid for claiming rows
+        (duplicates: after ``expand``/``expand_out``) and off[n] is the total. Compacting
+        lookups of one shard must be issued on one stream."""
         if not self.is_gpu or keys.shape[0] == 0:
             return self.lookup(keys, now, reserve_bytes, total_slot), None, None
         self._check(keys, "keys")
@@ -301,11 +311,18 @@ class CacheShard:
         size = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         now = self.now() if now is None else now
+        seg = (torch.empty(2, n + 1, dtype=torch.int64, device=self.device) if compact else None)
+        nseg = torch.empty(1, dtype=torch.int64, device=self.device) if compact else None
         self._impl.lookup_coalesced(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
                                     loc.data_ptr(), size.data_ptr(), off.data_ptr(), now,
                                     self._s(), int(reserve_bytes), int(total_slot),
                                     cslot.data_ptr() if cslot is not None else 0,
-                                    cslot is not None)
+                                    cslot is not None,
+                                    seg[0].data_ptr() if compact else 0,
+                                    seg[1].data_ptr() if compact else 0,
+                                    nseg.data_ptr() if compact else 0)
+        if compact:
+            return Lookup(loc, size, off, seg[0], seg[1], nseg), first, cslot
         return Lookup(loc, size, off), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
@@ -340,8 +357,12 @@ class CacheShard:
         self._check(out, "out")
         if self.is_gpu:
             cap = out.numel() if out_cap is None else min(int(out_cap), out.numel())
-            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(), self._s(),
-                              cap)
+            if lk.seg_src is not None:  # compacting lookup: copy the hit list only
+                self._impl.gather(lk.seg_src.data_ptr(), lk.seg_dst.data_ptr(), lk.n,
+                                  out.data_ptr(), self._s(), cap, lk.nseg.data_ptr())
+            else:
+                self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
+                                  self._s(), cap)
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
@@ -373,12 +394,15 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after: Optional["torch.cuda.Event"] = None) -> None:
+              index_after: Optional["torch.cuda.Event"] = None,
+              begin_only: bool = False) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded event): dedupe, sizing and the log append run at
         once, the index insert waits for the event — so a lookup followed by that event
-        on another stream overlaps the SET's log write (see ``HbmCache::store``)."""
+        on another stream overlaps the SET's log write (see ``HbmCache::store``).
+        ``begin_only`` (GPU): queue the planning kernels only (dedupe, sizes, scan);
+        ``store_finish(index_after)`` queues the log append and the index insert."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -394,10 +418,19 @@ class CacheShard:
                      else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(),
-                             index_after.cuda_event if index_after is not None else 0)
+                             index_after.cuda_event if index_after is not None else 0,
+                             bool(begin_only))
         else:
+            if begin_only:
+                raise ValueError("begin_only is a GPU-shard option")
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now)
+
+    def store_finish(self, index_after: Optional["torch.cuda.Event"] = None) -> None:
+        """Second half of ``store(begin_only=True)``: the log append and the index insert
+        (which waits for ``index_after``), on the current stream."""
+        self._impl.store_finish(self._s(),
+                                index_after.cuda_event if index_after is not None else 0)
 
     def set_many(self, keys: Sequence[bytes], values: Sequence[bytes], ttl: int = 0,
                  flags: int = 0) -> None:
