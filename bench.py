@@ -79,6 +79,11 @@ def parse():
                     help="host: the product edge — GET digests and SET payloads in pinned host "
                          "memory, responses gathered into pinned host memory over PCIe "
                          "(as the proxy's HBM tier); one rank")
+    ap.add_argument("--routed", action="store_true",
+                    help="one rank: run the routed multi-GPU step anyway, over a real one-rank "
+                         "RCCL communicator (every collective call of the N-GPU step; all keys "
+                         "are local, so no interconnect traffic) — a rehearsal, not a scaling "
+                         "number")
     ap.add_argument("--evict", choices=["clock", "fifo"], default="clock",
                     help="value-log eviction policy of the shards")
     ap.add_argument("--batches", type=int, default=16,
@@ -178,6 +183,9 @@ def main():
     if sim and world != 1:
         raise SystemExit("--simulate-world runs as a single process")
     bounce = args.bounce and args.device == "cuda" and world > 1
+    routed1 = args.routed and world == 1 and not sim
+    if routed1 and args.device != "cuda":
+        raise SystemExit("--routed is the one-GPU RCCL rehearsal")
     pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
     # a collective that outlives the timeout aborts the rank (non-zero exit), not a hang
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
@@ -190,6 +198,11 @@ def main():
         dev = torch.device("cuda", local)
         if world > 1:
             dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
+        elif routed1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout, rank=0,
+                                    world_size=1)
     else:
         dev = torch.device("cpu")
         if world > 1:
@@ -206,6 +219,8 @@ def main():
         group = MirrorComm(sim)
         world = sim
     real_world = 1 if sim else world
+    if routed1:
+        args.replicate = 0  # one rank owns every key: the replica tier is never consulted
     if bounce:
         from shellac_amd.parallel.exchange import BounceComm
 
@@ -237,10 +252,11 @@ def main():
         replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
                              max_item=1 << 20, device=dev)
     data_group = None
-    if real_world > 1 and not bounce:
+    if (real_world > 1 or routed1) and not bounce:
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
-    sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group)
+    sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group,
+                      routed=True if routed1 else None)
     sc.coalesce = not args.no_coalesce
 
     # populate: every rank SETs its slice of the key space through the routed path
@@ -445,6 +461,10 @@ def main():
         out["metric"] = "cache_ops_per_s_rehearsal"
         out["data"] = (f"functional rehearsal: {world} ranks on one GPU, collectives bounced "
                        "through gloo; not a performance number")
+    if routed1:
+        out["metric"] = "cache_ops_per_s_routed_rehearsal"
+        out["config"]["parallelism"] = "shard1, routed step over a one-rank RCCL communicator"
+        out["data"] += "; routed one-rank rehearsal: not the N=1 headline"
     if sim:
         out["metric"] = "cache_ops_per_s_simulated"
         out["data"] = (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
@@ -455,6 +475,7 @@ def main():
         print(json.dumps(out), flush=True)
     if real_world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

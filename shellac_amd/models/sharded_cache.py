@@ -134,17 +134,22 @@ class _Phases:
 class ShardedCache:
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
-                 sample_batches: int = 8, data_group=None):
+                 sample_batches: int = 8, data_group=None, routed: Optional[bool] = None):
         self.shard = shard
         self.group = group
         # Optional second communicator for the value all-to-all: its stream runs the
         # previous step's value transfer while this step's small exchanges proceed.
         self.data_group = data_group if data_group is not None else group
         self.rank, self.world = dist_info(group)
+        # routed: batches go through the collectives (routing, all-to-alls, replica tier).
+        # Default: with more than one rank. routed=True at world 1 runs the same path over
+        # a one-rank group — a real RCCL communicator on one GPU (the test and rehearsal of
+        # the multi-GPU step's collective calls that a one-GPU box can run)
+        self.routed = self.world > 1 if routed is None else bool(routed)
         self.device = shard.device
         self.ring = ShardRing(list(range(self.world)), points_per_shard)
         self.ring_pts, self.ring_own = self.ring.tensors(self.device)
-        self.replica = replica if self.world > 1 else None
+        self.replica = replica if self.routed else None
         self.sample_rows = sample_rows
         self.sample_batches = sample_batches
         self._samples: List[torch.Tensor] = []
@@ -207,7 +212,7 @@ class ShardedCache:
     def get(self, keys: torch.Tensor, now: Optional[int] = None) -> GetResult:
         n = keys.shape[0]
         self.stats["get_requests"] += n
-        if self.world == 1:
+        if not self.routed:
             if self.coalesce:
                 lk, first, _ = self.shard.lookup_coalesced(keys, now, compact=self.compact)
             else:
@@ -284,7 +289,7 @@ class ShardedCache:
         the gather (no event, no copy).
         With several ranks see ``_serve_routed``: 4-5 collectives and 2 host syncs for
         the whole step instead of 10 and 3 for get() followed by set()."""
-        if self.world > 1:
+        if self.routed:
             if self.fused and self.device.type == "cuda":
                 return self._serve_routed_fused(keys, batch, now)
             return self._serve_routed(keys, batch, now)
@@ -700,7 +705,7 @@ class ShardedCache:
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
         n = batch.keys.shape[0]
         self.stats["set_requests"] += n
-        if self.world == 1:
+        if not self.routed:
             self.shard.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                              batch.expire, now)
             return
@@ -763,7 +768,7 @@ class ShardedCache:
                                rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
 
     def delete(self, keys: torch.Tensor, now: Optional[int] = None) -> torch.Tensor:
-        if self.world == 1:
+        if not self.routed:
             return self.shard.remove(keys, now)
         if self.replica is not None:  # replicas are dropped everywhere (collective)
             cnt = torch.tensor([keys.shape[0]], dtype=torch.int64, device=self.device)
