@@ -142,7 +142,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", choices=["dram", "hbm", "tiered", "none"], default="tiered")
     ap.add_argument("--threads", type=int, default=9, help="proxy reactor threads")
-    ap.add_argument("--client-threads", type=int, default=5)
+    ap.add_argument("--client-threads", type=int, default=6)
     ap.add_argument("--origin-threads", type=int, default=2)
     ap.add_argument("--objects", type=int, default=1000000)
     ap.add_argument("--body", type=int, default=4096, help="origin body bytes (incompressible)")

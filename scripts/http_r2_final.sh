@@ -1,4 +1,4 @@
-# Round-2 HTTP matrix with the final bench defaults: 9 reactors + 5 load-generator
+# Round-2 HTTP matrix with the final bench defaults: 9 reactors + 6 load-generator
 # workers on their own cores of socket 0 (busy-polling 200 us), the GPU batcher, the
 # proxy's other threads and the origin on a 16th core (the box's cgroup quota is 16 CPUs).
 # Objects: 4 KiB incompressible bodies, 1K / 8M objects; 64 KiB bodies, 256K objects.
