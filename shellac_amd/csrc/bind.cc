@@ -245,6 +245,26 @@ PYBIND11_MODULE(_shellac_core, m) {
   m.def("mfma_hello", [](uintptr_t a, uintptr_t b, uintptr_t c, int tiles, uintptr_t s) {
     mfma_hello(P<const uint16_t>(a), P<const uint16_t>(b), P<float>(c), tiles, S(s));
   });
+  // Cross-stream ordering with events whose fence scope the caller picks (torch's events
+  // use the default: a system-scope release/acquire, i.e. an L2 write-back and invalidate at
+  // every record). Two streams of one GPU only need device scope.
+  m.attr("EVENT_DISABLE_TIMING") = (unsigned)hipEventDisableTiming;
+  m.attr("EVENT_DISABLE_SYSTEM_FENCE") = (unsigned)hipEventDisableSystemFence;
+  m.attr("EVENT_RELEASE_TO_DEVICE") = (unsigned)hipEventReleaseToDevice;
+  m.def("event_create", [](unsigned flags) {
+    hipEvent_t e = nullptr;
+    SH_CHECK(hipEventCreateWithFlags(&e, flags) == hipSuccess, "hipEventCreateWithFlags failed");
+    return reinterpret_cast<uintptr_t>(e);
+  });
+  m.def("event_destroy", [](uintptr_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
+  m.def("event_record", [](uintptr_t e, uintptr_t s) {
+    SH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(s)) == hipSuccess,
+             "hipEventRecord failed");
+  });
+  m.def("stream_wait_event", [](uintptr_t s, uintptr_t e) {
+    SH_CHECK(hipStreamWaitEvent(S(s), reinterpret_cast<hipEvent_t>(e), 0) == hipSuccess,
+             "hipStreamWaitEvent failed");
+  });
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

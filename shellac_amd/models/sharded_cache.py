@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import routing as R
-from ..ops.cache import CacheShard, coalesce, expand, expand_out
+from ..ops.cache import CacheShard, StreamEvent, coalesce, expand, expand_out
 from ..parallel.exchange import (all_gather, all_reduce, all_to_all_rows, all_to_all_single,
                                  allreduce_stats, dist_info, exchange_counts, segment_sums)
 from ..parallel.ring import ShardRing
@@ -177,9 +177,15 @@ class ShardedCache:
         #   beside k_coalesce, but k_coalesce then takes 139 us beside the log append and
         #   the extra cross-stream wait costs ~14 us: 0.36 ms)
         self.plan_first = os.environ.get("SHELLAC_PLAN_FIRST", "0") == "1"
-        self._plan_done = None
+        # fence scope of the events that order the main and side streams of a step:
+        # "system" = torch's events (a system-scope release: L2 write-back + invalidate
+        # at every record); "device" (default) / "none" = StreamEvent with a device-scope
+        # release / no system fence (both streams are on one GPU; nothing on the host reads
+        # what these events order). One box, two rounds: 0.309 / 0.308 ms per step with
+        # "device" vs 0.315 / 0.311 with "system" (profiles/r2_event_fence_ab.log)
+        self.event_fence = os.environ.get("SHELLAC_EVENT_FENCE", "device")
+        self._events = {}
         self._side = None
-        self._probe_done = None  # event: this step's probe is done (SET index may run)
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
         self._co_table = None    # persistent GET-coalescing table (serve, side stream)
         # host edge (one rank): GET digests / SET payloads may be pinned host tensors and
@@ -311,17 +317,13 @@ class ShardedCache:
             # them) overlap the coalescing and the probe; only its index insert waits for
             # the probe (event), then runs under the bandwidth-bound gather.
             main = torch.cuda.current_stream(self.device)
-            side.wait_stream(main)  # the previous step's gather is done with the log
+            self._xwait(side, main, "start")  # the previous step's gather is done with the log
             now = sh.now() if now is None else now
             if self.plan_first:
                 with torch.cuda.stream(side):
                     sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                              batch.expire, now, begin_only=True)
-                pe = self._plan_done
-                if pe is None:
-                    pe = self._plan_done = torch.cuda.Event()
-                pe.record(side)
-                main.wait_event(pe)
+                self._xwait(main, side, "plan")
         if self.coalesce:
             table = self._coalesce_table(n) if side is not None else None
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
@@ -337,9 +339,7 @@ class ShardedCache:
             return GetResult(data, lk.off[:n], lk.size[:n])
         # Safe by construction: the lookup reserved the SET's log bytes, so the gather
         # never reads a region the SET writes, and the gather does not read the index.
-        ev = self._probe_done
-        if ev is None:
-            ev = self._probe_done = torch.cuda.Event()
+        ev = self._event("probe")
         ev.record(main)
         if first is not None:
             out_size = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -354,10 +354,26 @@ class ShardedCache:
                 # per-request (size, off) and the table clean-up, under the gather
                 expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)
         data = self._gather_unsynced(lk)
-        main.wait_stream(side)  # the next step's lookup sees this step's SETs
+        self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
         if first is not None:
             return GetResult(data, out_off, out_size)
         return GetResult(data, lk.off[:n], lk.size[:n])
+
+    def _event(self, name: str):
+        e = self._events.get(name)
+        if e is None:
+            e = self._events[name] = (torch.cuda.Event() if self.event_fence == "system"
+                                      else StreamEvent(self.event_fence))
+        return e
+
+    def _xwait(self, waiter, signaler, name: str) -> None:
+        """``waiter`` stream waits for the work queued so far on ``signaler``."""
+        e = self._event(name)
+        e.record(signaler)
+        if isinstance(e, StreamEvent):
+            e.wait(waiter)
+        else:
+            waiter.wait_event(e)
 
     def _coalesce_table(self, n: int) -> torch.Tensor:
         """Persistent, zeroed GET-coalescing table (every serve step leaves it zeroed:

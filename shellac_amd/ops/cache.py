@@ -166,6 +166,51 @@ def expand_out(first: torch.Tensor, size: torch.Tensor, off: torch.Tensor,
                                 _stream_handle(first.device))
 
 
+class StreamEvent:
+    """A HIP event with a chosen fence scope, for ordering two streams of one GPU.
+
+    ``torch.cuda.Event`` records with the default system-scope release (an L2 write-back
+    and invalidate every time); ``fence="device"`` releases to device scope only
+    (``hipEventReleaseToDevice``), ``"none"`` disables the system fence
+    (``hipEventDisableSystemFence``), ``"system"`` is the default. Both streams must be on
+    the same GPU and nothing on the host may read what the event orders."""
+
+    def __init__(self, fence: str = "device"):
+        c = core()
+        flags = int(c.EVENT_DISABLE_TIMING)
+        if fence == "device":
+            flags |= int(c.EVENT_RELEASE_TO_DEVICE)
+        elif fence == "none":
+            flags |= int(c.EVENT_DISABLE_SYSTEM_FENCE)
+        elif fence != "system":
+            raise ValueError(f"unknown fence {fence!r}")
+        self.fence = fence
+        self.handle = int(c.event_create(flags))
+
+    def record(self, stream: "torch.cuda.Stream") -> None:
+        core().event_record(self.handle, stream.cuda_stream)
+
+    def wait(self, stream: "torch.cuda.Stream") -> None:
+        """``stream`` waits for the work this event recorded."""
+        core().stream_wait_event(stream.cuda_stream, self.handle)
+
+    def __del__(self):
+        h = getattr(self, "handle", 0)
+        if h:
+            try:
+                core().event_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
+
+def _event_handle(ev) -> int:
+    if ev is None:
+        return 0
+    if isinstance(ev, StreamEvent):
+        return ev.handle
+    return ev.cuda_event
+
+
 @dataclass
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
@@ -394,13 +439,13 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after: Optional["torch.cuda.Event"] = None,
-              begin_only: bool = False) -> None:
+              index_after=None, begin_only: bool = False) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
-        ``index_after`` (GPU, a recorded event): dedupe, sizing and the log append run at
-        once, the index insert waits for the event — so a lookup followed by that event
-        on another stream overlaps the SET's log write (see ``HbmCache::store``).
+        ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
+        dedupe, sizing and the log append run at once, the index insert waits for the
+        event — so a lookup followed by that event on another stream overlaps the SET's log
+        write (see ``HbmCache::store``).
         ``begin_only`` (GPU): queue the planning kernels only (dedupe, sizes, scan);
         ``store_finish(index_after)`` queues the log append and the index insert."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
@@ -417,8 +462,7 @@ class CacheShard:
             bound = (self.payload_bound(n, values.numel()) if bytes_bound is None
                      else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
-                             fp, ep, n, bound, now, self._s(),
-                             index_after.cuda_event if index_after is not None else 0,
+                             fp, ep, n, bound, now, self._s(), _event_handle(index_after),
                              bool(begin_only))
         else:
             if begin_only:
@@ -426,11 +470,10 @@ class CacheShard:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now)
 
-    def store_finish(self, index_after: Optional["torch.cuda.Event"] = None) -> None:
+    def store_finish(self, index_after=None) -> None:
         """Second half of ``store(begin_only=True)``: the log append and the index insert
         (which waits for ``index_after``), on the current stream."""
-        self._impl.store_finish(self._s(),
-                                index_after.cuda_event if index_after is not None else 0)
+        self._impl.store_finish(self._s(), _event_handle(index_after))
 
     def set_many(self, keys: Sequence[bytes], values: Sequence[bytes], ttl: int = 0,
                  flags: int = 0) -> None:

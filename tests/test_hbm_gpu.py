@@ -637,3 +637,29 @@ def test_serve_schedules_return_the_same_records(cuda_dev, compact, plan_first):
         got[mode] = recs
     assert got["default"] == got["alt"]
     assert sum(x is not None for x in got["alt"][-1]) > 90000
+
+
+@pytest.mark.parametrize("fence", ["system", "device", "none"])
+def test_serve_event_fences_return_the_same_records(cuda_dev, fence):
+    """The events ordering the serving step's two streams, at every fence scope: each
+    step's GETs see the previous step's SETs (index insert on the side stream) and the
+    coalescing table is clean again."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(20000, cuda_dev)
+    shard = CacheShard(128 << 20, 1 << 14, 1 << 16, cuda_dev)
+    sc = ShardedCache(shard)
+    sc.event_fence = fence
+    sc.set(wl.set_batch(torch.arange(0, 10000, device=cuda_dev)))
+    keys = wl.digests.index_select(0, wl.sample_ids(50000, 3)).contiguous()
+    ids_new = torch.arange(10000, 20000, device=cuda_dev)
+    r1 = sc.serve(keys, wl.set_batch(ids_new))  # ids >= 10000 miss now ...
+    r2 = sc.serve(keys, wl.set_batch(ids_new[:16]))  # ... and hit one step later
+    torch.cuda.synchronize()
+    ids = wl.sample_ids(50000, 3).cpu()
+    v1 = unpack_records(r1.data, r1.off, r1.size)
+    v2 = unpack_records(r2.data, r2.off, r2.size)
+    assert all((v is None) == (int(i) >= 10000) for v, i in zip(v1, ids))
+    assert all(v is not None and v[0] == wl.expected_value(int(i)) for v, i in zip(v2, ids))
+    assert int(sc._co_table.abs().sum()) == 0
