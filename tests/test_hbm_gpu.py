@@ -648,7 +648,7 @@ def test_serve_event_fences_return_the_same_records(cuda_dev, fence):
     from shellac_amd.models.sharded_cache import ShardedCache
 
     wl = Workload(20000, cuda_dev)
-    shard = CacheShard(128 << 20, 1 << 14, 1 << 16, cuda_dev)
+    shard = CacheShard(512 << 20, 1 << 14, 1 << 16, cuda_dev)
     sc = ShardedCache(shard)
     sc.event_fence = fence
     sc.set(wl.set_batch(torch.arange(0, 10000, device=cuda_dev)))
