@@ -173,9 +173,20 @@ def smoke(rank, world, dev):
     return out
 
 
+def _claim_stdout():
+    """The contract is ONE JSON line on rank 0's stdout, but RCCL prints a version banner
+    to fd 1 when a communicator comes up. Keep a private handle on the real stdout for the
+    JSON line and point fd 1 (C libraries, stray prints) at stderr."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     maybe_launch(args)
+    json_out = _claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -472,7 +483,7 @@ def main():
         out["n_gpus"] = 1
         out["simulated_world"] = sim
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if real_world > 1:
         dist.barrier()
     if dist.is_initialized():

@@ -107,6 +107,8 @@ class RoutedStep {
   };
   template <typename T>
   T* buf(int slot, size_t count);
+  void fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* shard, uint32_t now,
+                  hipStream_t s);
 
   int w_, rank_, device_;
   const uint32_t* pts_ = nullptr;

@@ -819,6 +819,31 @@ void RoutedStep::gather_replies(HbmCache* shard, uint8_t* reply, hipStream_t s) 
   if (mg_ > 0) shard->gather(lk_loc_, lk_off_, mg_, reply, s);
 }
 
+// Received-SET unpacking and the main-shard SET chain on the side stream, after the work
+// queued on `s` so far (the reply gather). Queuing it before host sync 2 instead (with the
+// owner lookup reserving its log bytes), to fill the GPU's idle time there, was measured
+// slower: simulated 8 ranks 0.83 / 0.82 vs 0.83 / 0.79 ms per step, 2 ranks 0.80 / 0.84 vs
+// 0.77 / 0.79 — the SET chain then competes with the owner probe and reply gather.
+void RoutedStep::fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
+                            uint32_t now, hipStream_t s) {
+  const int64_t ms = ms_;
+  const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
+  Digest* rkeys = buf<Digest>(kRkeys, ms);
+  uint32_t* v0 = buf<uint32_t>(kV0, ms);
+  uint32_t* v1 = buf<uint32_t>(kV1, ms);
+  uint32_t* fl = buf<uint32_t>(kFl, ms);
+  uint32_t* ex = buf<uint32_t>(kEx, ms);
+  uint64_t* roff = buf<uint64_t>(kRoff, ms);
+  RT_OK(hipEventRecord(ev_fork_, s));
+  RT_OK(hipStreamWaitEvent(side_, ev_fork_, 0));
+  hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t),
+                     side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
+  RT_OK(hipGetLastError());
+  RT_OK(hipEventRecord(ev_fill_, side_));
+  shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, side_);
+  RT_OK(hipEventRecord(ev_join_, side_));
+}
+
 void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
                         HbmCache* replica, uint32_t now, uint64_t* out_size, uint64_t* out_off,
                         hipStream_t s) {
@@ -832,20 +857,12 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
     // grids) go to the side stream, concurrently with the bandwidth-bound replica
     // gather below. They touch different shards; everything the caller queued before
     // (reply gather from the main shard, the wait for the SET payloads) comes first.
-    rkeys = buf<Digest>(kRkeys, ms);
-    uint32_t* v0 = buf<uint32_t>(kV0, ms);
+    fork_store(recv, recv_bytes, shard, now, s);
+    rkeys = buf<Digest>(kRkeys, ms);  // filled by k_rs_fill on the side stream (ev_fill_)
     v1 = buf<uint32_t>(kV1, ms);
     fl = buf<uint32_t>(kFl, ms);
     ex = buf<uint32_t>(kEx, ms);
     roff = buf<uint64_t>(kRoff, ms);
-    RT_OK(hipEventRecord(ev_fork_, s));
-    RT_OK(hipStreamWaitEvent(side_, ev_fork_, 0));
-    hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t),
-                       side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
-    RT_OK(hipGetLastError());
-    RT_OK(hipEventRecord(ev_fill_, side_));
-    shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, side_);
-    RT_OK(hipEventRecord(ev_join_, side_));
   }
   if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
   if (ms > 0 && replica) {
