@@ -319,24 +319,28 @@ def main():
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
         return sc.serve(gets[i % P], sets[i % P])
 
+    # Per-step GPU timing events are recorded in a separate pass after the timed one: an
+    # event record is a marker packet on the stream, and one between every two steps cost
+    # ~6 us of a 0.32 ms step (profiles/r2_bench_events_ab.log)
     use_events = dev.type == "cuda"
     rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
 
-    def timed(steps, first):
+    def timed(steps, first, events=False):
         """Run `steps` steps bracketed by barrier + device sync; returns (max-over-ranks
-        wall seconds, per-step GPU-event intervals in ms, last result)."""
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if use_events else []
+        wall seconds, per-step GPU-event intervals in ms if `events`, last result)."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if events else []
+        cur = torch.cuda.current_stream(dev) if events else None
         if real_world > 1:
             dist.barrier()
         sync()
         t0 = time.perf_counter()
         res = None
         for i in range(steps):
-            if use_events:
-                evs[i].record()
+            if events:
+                evs[i].record(cur)
             res = step(first + i)
-        if use_events:
-            evs[steps].record()
+        if events:
+            evs[steps].record(cur)
         sync()
         if real_world > 1:
             dist.barrier()
@@ -345,7 +349,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=rdev)
         if real_world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if use_events else []
+        iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if events else []
         return float(t), iv, res
 
     for i in range(args.warmup):
@@ -354,7 +358,7 @@ def main():
     before = shard.counters()
     st0 = dict(sc.stats)
     gb0 = sc.gathered_bytes
-    elapsed, intervals, res = timed(args.steps, args.warmup)
+    elapsed, _, res = timed(args.steps, args.warmup)
     gathered = sc.gathered_bytes - gb0
     last_batch = (args.warmup + args.steps - 1) % P
     after = shard.counters()
@@ -391,8 +395,13 @@ def main():
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
                   f"another key")
 
-    # secondary (outside the headline timed region): the same steps with every GET probed
-    # and copied (no in-batch request collapsing)
+    # secondary (outside the headline timed region): the same steps again with a GPU timing
+    # event between every two (per-step GPU time, median over the batches)
+    intervals = []
+    if use_events:
+        intervals = timed(args.steps, args.warmup + args.steps, events=True)[1]
+    # secondary: the same steps with every GET probed and copied (no in-batch request
+    # collapsing)
     unco = None
     if sc.coalesce and not args.no_uncoalesced:
         sc.coalesce = False

@@ -257,6 +257,14 @@ PYBIND11_MODULE(_shellac_core, m) {
     return reinterpret_cast<uintptr_t>(e);
   });
   m.def("event_destroy", [](uintptr_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
+  m.def("event_elapsed_ms", [](uintptr_t a, uintptr_t b) {
+    float ms = 0.f;
+    SH_CHECK(hipEventSynchronize(reinterpret_cast<hipEvent_t>(b)) == hipSuccess &&
+                 hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(a),
+                                     reinterpret_cast<hipEvent_t>(b)) == hipSuccess,
+             "hipEventElapsedTime failed");
+    return ms;
+  });
   m.def("event_record", [](uintptr_t e, uintptr_t s) {
     SH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(s)) == hipSuccess,
              "hipEventRecord failed");

@@ -175,9 +175,9 @@ class StreamEvent:
     (``hipEventDisableSystemFence``), ``"system"`` is the default. Both streams must be on
     the same GPU and nothing on the host may read what the event orders."""
 
-    def __init__(self, fence: str = "device"):
+    def __init__(self, fence: str = "device", timing: bool = False):
         c = core()
-        flags = int(c.EVENT_DISABLE_TIMING)
+        flags = 0 if timing else int(c.EVENT_DISABLE_TIMING)
         if fence == "device":
             flags |= int(c.EVENT_RELEASE_TO_DEVICE)
         elif fence == "none":
@@ -193,6 +193,11 @@ class StreamEvent:
     def wait(self, stream: "torch.cuda.Stream") -> None:
         """``stream`` waits for the work this event recorded."""
         core().stream_wait_event(stream.cuda_stream, self.handle)
+
+    def elapsed_time(self, end: "StreamEvent") -> float:
+        """Milliseconds from this event to ``end`` (both created with timing=True);
+        waits for ``end``."""
+        return float(core().event_elapsed_ms(self.handle, end.handle))
 
     def __del__(self):
         h = getattr(self, "handle", 0)
