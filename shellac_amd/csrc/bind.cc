@@ -139,14 +139,14 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after,
-                       bool begin_only) {
+                       int begin) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
-                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), begin_only);
+                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), begin);
       }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
          py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
-         py::arg("stream"), py::arg("index_after") = 0, py::arg("begin_only") = false)
+         py::arg("stream"), py::arg("index_after") = 0, py::arg("begin") = 0)
       .def("store_finish", [](HbmCache& c, uintptr_t s, uintptr_t index_after) {
         py::gil_scoped_release nogil;
         c.store_finish(S(s), reinterpret_cast<hipEvent_t>(index_after));

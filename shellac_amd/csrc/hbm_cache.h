@@ -52,7 +52,9 @@ class HbmCache {
   // overwrite as misses, so SETs may be queued between this lookup and its gather.
   // `total_slot` >= 0 also writes off[n] straight into host slot `total_slot` (pinned,
   // coherent), readable with host_slot() once the stream has passed the lookup: the
-  // response size without a D2H copy.
+  // response size without a D2H copy. The slot is written last, after every kernel of the
+  // lookup has finished and released its outputs: once the host has read it, work queued
+  // on any stream of this GPU may read loc/size/off (and `first`) without an event.
   // `first` (coalesce_keys output, may be null): rows with first[i] != i are duplicates
   // and are answered as misses without touching the index (expand_coalesced fills them
   // in after the gather).
@@ -115,15 +117,19 @@ class HbmCache {
   // and log append: it reads the index and the current head slot, which only the index
   // insert changes, and a `reserve` covering this SET keeps its gather off the bytes
   // the append overwrites.
-  // `begin_only`: queue only the SET's planning kernels (CLOCK reclaim, dedupe, sizes,
-  // scan — none touches the log, the index or the head, so a lookup may run beside or
-  // after them) and return; store_finish() queues the rest (log append, index insert).
-  // The caller records an event after the plan to start its lookup on it, then passes
-  // the lookup's event as store_finish's `index_after`. No other store may come between.
+  // `begin` != 0: queue only the first stages and return; store_finish() queues the rest.
+  //   kStorePlanOnly: the planning kernels (CLOCK reclaim, dedupe, sizes, scan — none
+  //     touches the log, the index or the head, so a lookup may run beside or after them);
+  //   kStoreThroughAppend: planning + the log append (a lookup reserving the SET's bytes
+  //     treats them as gone, so it may run beside these too).
+  // store_finish(index_after) then queues the index insert (after `index_after`), which a
+  // lookup can observe; calling it once the lookup is known to be done (e.g. after its
+  // host slot was read) needs no event. No other store may come in between.
+  static constexpr int kStorePlanOnly = 1, kStoreThroughAppend = 2;
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
              uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-             bool begin_only = false);
+             int begin = 0);
   void store_finish(hipStream_t s, hipEvent_t index_after = nullptr);
   // SET through captured hipGraphs, for callers with fixed batch sizes and fixed
   // staging buffers (the proxy's micro-batches, padded to a size class with
@@ -209,6 +215,9 @@ class HbmCache {
   unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
   unsigned long long* lbc_state_ = nullptr; // device: compacting lookup's bump word
   unsigned int* lbc_done_ = nullptr;        // device: its finished-workgroup counter
+  // device: finished-workgroup counter of a lookup's offsets scan (the last one publishes
+  // the host slot; self-resetting; lookups naming a host slot are ordered on one stream)
+  unsigned int* off_done_ = nullptr;
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;
@@ -221,14 +230,14 @@ class HbmCache {
   uint32_t dd_mask_ = 0;
   uint64_t ws_gen_ = 0;  // bumped when the SET workspace moves (invalidates graphs)
   std::mutex mu_;
+  static constexpr int kStagePlan = 1, kStageAppend = 2, kStageIndex = 4, kStagesAll = 7;
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                     int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-                    int phase = 0);
+                    int stages = kStagesAll);
   void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
-  void store_commit_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
-                           const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after);
+  void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
+                          int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after);
   // a store begun with begin_only, waiting for store_finish
   struct PendingStore {
     bool on = false;
@@ -238,6 +247,7 @@ class HbmCache {
     const uint32_t *vlen = nullptr, *flags = nullptr, *expire = nullptr;
     int64_t n = 0;
     uint32_t now = 0;
+    int stages = 0;  // what store_finish still queues
   } pend_;
 };
 

@@ -276,7 +276,8 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ off,
                                                     uint64_t* __restrict__ host_total,
                                                     const uint64_t* __restrict__ part_cnt,
-                                                    uint64_t* __restrict__ cnt) {
+                                                    uint64_t* __restrict__ cnt,
+                                                    unsigned int* __restrict__ done) {
   __shared__ unsigned long long s_w[2][kBlock / 64];
   __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -361,8 +362,35 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
     }
     off[n] = tot;
     if (cnt) cnt[n] = totc;
-    if (host_total)
+    if (host_total && !done)
       __hip_atomic_store(host_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (done) {
+    // `done` given: the host slot is written by the LAST workgroup to finish, after every
+    // workgroup released its offsets (device scope), so a host that read the slot may
+    // queue work on another stream that reads off[] without a GPU-side event. The total
+    // is the sum of the producer's partials (visible: they come from an earlier kernel).
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      unsigned long long t = 0;
+      for (int k = threadIdx.x; k < nparts; k += kBlock) t += part[k];
+      t = wave_sum(t);
+      if (lane == 0) s_w[0][w] = t;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+#pragma unroll
+        for (int k = 0; k < kBlock / 64; ++k) tot += s_w[0][k];
+        atomicExch(done, 0u);
+        __hip_atomic_store(host_total, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -793,7 +821,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // returned before its done-increment) and leaves both words zeroed
     __shared__ int s_last;
     __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) {
+      __threadfence();  // release this workgroup's outputs before it counts as done
+      s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
     __syncthreads();
     if (s_last && threadIdx.x == 0) {
       const unsigned long long t = atomicExch(bump, 0ull);
@@ -802,9 +833,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       *nseg = k;
       seg_dst[k] = total;
       off[n] = total;
-      if (host_total)
-        __hip_atomic_store(host_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       atomicExch(done, 0u);
+      if (host_total)
+        __hip_atomic_store(host_total, total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1871,12 +1902,12 @@ size_t device_scan_tmp_bytes(int64_t n) {
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
                     uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr,
                     int64_t plen_override = 0, const uint64_t* part_cnt = nullptr,
-                    uint64_t* cnt = nullptr) {
+                    uint64_t* cnt = nullptr, unsigned int* done = nullptr) {
   const int64_t plen = plen_override > 0 ? plen_override : part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
   hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
-                     host_total, part_cnt, cnt);
+                     host_total, part_cnt, cnt, host_total ? done : nullptr);
   HIP_OK(hipGetLastError());
 }
 
@@ -2007,6 +2038,8 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMemset(lbc_state_, 0, (kMaxGrid + 1) * sizeof(unsigned long long)));
   HIP_OK(hipMalloc(&lbc_done_, 64));
   HIP_OK(hipMemset(lbc_done_, 0, 64));
+  HIP_OK(hipMalloc(&off_done_, 64));
+  HIP_OK(hipMemset(off_done_, 0, 64));
   HIP_OK(hipMalloc(&part_, 3 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
@@ -2041,6 +2074,7 @@ HbmCache::~HbmCache() {
   (void)hipFree(lb_state_);
   (void)hipFree(lbc_state_);
   (void)hipFree(lbc_done_);
+  (void)hipFree(off_done_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -2156,7 +2190,7 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht);
+  launch_offsets(size, n, part_, grid, off, s, ht, 0, nullptr, nullptr, off_done_);
 }
 
 void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
@@ -2205,7 +2239,7 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
                      reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only(),
                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht, plen);
+  launch_offsets(size, n, part_, grid, off, s, ht, plen, nullptr, nullptr, off_done_);
 }
 
 uint64_t HbmCache::host_slot(int i) const {
@@ -2257,7 +2291,7 @@ void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
-                     hipEvent_t index_after, bool begin_only) {
+                     hipEvent_t index_after, int begin) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
@@ -2265,7 +2299,12 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   SH_CHECK(!pend_.on, "store: a split store is still waiting for store_finish");
-  const int phase = begin_only ? 1 : 0;
+  SH_CHECK(begin >= 0 && begin <= kStoreThroughAppend, "store: bad begin stage");
+  const bool begin_only = begin != 0;
+  // stages this call queues: all, the planning kernels, or planning + log append
+  const int stages = begin == 0 ? kStagesAll
+                     : begin == kStorePlanOnly ? kStagePlan
+                                               : (kStagePlan | kStageAppend);
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
   if (rmax && should_reclaim(bytes_bound)) {
@@ -2289,14 +2328,16 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
-                 index_after, phase);
+                 index_after, stages);
     if (begin_only)
       pend_ = PendingStore{true, cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_,
-                           w + n, now};
+                           w + n, now, kStagesAll & ~stages};
   } else {
     ensure_set_ws(n, s);
-    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, phase);
-    if (begin_only) pend_ = PendingStore{true, keys, values, val_off, vlen, flags, expire, n, now};
+    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, stages);
+    if (begin_only)
+      pend_ = PendingStore{true, keys, values, val_off, vlen, flags, expire, n, now,
+                           kStagesAll & ~stages};
   }
   if (!begin_only) hsel_ ^= 1;  // later operations on the stream read the published slot
 }
@@ -2309,22 +2350,27 @@ void HbmCache::store_finish(hipStream_t s, hipEvent_t index_after) {
   const PendingStore p = pend_;
   pend_.on = false;
   store_locked(p.keys, p.values, p.val_off, p.vlen, p.flags, p.expire, p.n, p.now, s,
-               index_after, 2);
+               index_after, p.stages);
   hsel_ ^= 1;
 }
 
 // The SET kernel chain (caller holds mu_, workspace sized): dedupe (last writer wins),
 // sizes + fused scan, log append (k_segcopy<1>), two-choice CAS index insert that also
-// publishes the new head into the other head slot. phase 1: the planning kernels only
-// (dedupe, sizes, scan: they touch neither the log, the index nor the head); phase 2: the
-// rest; 0: both.
+// publishes the new head into the other head slot. `stages` selects the parts queued:
+// kStagePlan (dedupe, sizes, scan: they touch neither the log, the index nor the head),
+// kStageAppend (the log write: only bytes a reserving lookup treats as gone), kStageIndex
+// (index insert + fix-up, after `index_after`: the only part a lookup can observe).
 void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                             int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
-                            int phase) {
-  if (phase != 2) store_plan_locked(keys, vlen, n, s);
-  if (phase == 1) return;
-  store_commit_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
+                            int stages) {
+  if (stages & kStagePlan) store_plan_locked(keys, vlen, n, s);
+  if (stages & kStageAppend) {
+    launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire,
+                      cur_head(), cfg_.log_bytes, (const int64_t*)nullptr);
+    HIP_OK(hipGetLastError());
+  }
+  if (stages & kStageIndex) store_index_locked(keys, vlen, expire, n, now, s, index_after);
 }
 
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,
@@ -2341,13 +2387,9 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
                  ring_ ? set_cnt_ : nullptr);
 }
 
-void HbmCache::store_commit_locked(const Digest* keys, const uint8_t* values,
-                                   const uint64_t* val_off, const uint32_t* vlen,
-                                   const uint32_t* flags, const uint32_t* expire, int64_t n,
-                                   uint32_t now, hipStream_t s, hipEvent_t index_after) {
-  launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
-                    cfg_.log_bytes, (const int64_t*)nullptr);
-  HIP_OK(hipGetLastError());
+void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
+                                  const uint32_t* expire, int64_t n, uint32_t now, hipStream_t s,
+                                  hipEvent_t index_after) {
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
   const int igrid = grid_for(n * 4, kBlock, kMaxGrid);

@@ -249,6 +249,7 @@ class CacheShard:
     """
 
     EVICT = {"fifo": 0, "clock": 1}
+    _BEGIN = {None: 0, "plan": 1, "append": 2}  # HbmCache::kStorePlanOnly / kStoreThroughAppend
 
     def __init__(self, log_bytes: int, nbuckets: int, max_item: int = 1 << 20,
                  device: str | torch.device = "cpu", evict: str = "clock",
@@ -444,15 +445,16 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after=None, begin_only: bool = False) -> None:
+              index_after=None, begin: Optional[str] = None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
         dedupe, sizing and the log append run at once, the index insert waits for the
         event — so a lookup followed by that event on another stream overlaps the SET's log
         write (see ``HbmCache::store``).
-        ``begin_only`` (GPU): queue the planning kernels only (dedupe, sizes, scan);
-        ``store_finish(index_after)`` queues the log append and the index insert."""
+        ``begin`` (GPU): queue the first stages only — ``"plan"`` (dedupe, sizes, scan)
+        or ``"append"`` (those plus the log write) — and let ``store_finish`` queue the
+        rest (the index insert, after ``index_after``)."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -468,10 +470,10 @@ class CacheShard:
                      else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(), _event_handle(index_after),
-                             bool(begin_only))
+                             self._BEGIN[begin])
         else:
-            if begin_only:
-                raise ValueError("begin_only is a GPU-shard option")
+            if begin is not None:
+                raise ValueError("begin is a GPU-shard option")
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now)
 

@@ -663,3 +663,30 @@ def test_serve_event_fences_return_the_same_records(cuda_dev, fence):
     assert all((v is None) == (int(i) >= 10000) for v, i in zip(v1, ids))
     assert all(v is not None and v[0] == wl.expected_value(int(i)) for v, i in zip(v2, ids))
     assert int(sc._co_table.abs().sum()) == 0
+
+
+def test_serve_host_ordered_index_returns_the_same_records(cuda_dev):
+    """SHELLAC_HOST_ORDER: the SET index insert and the per-request expansion are queued
+    after the host read the lookup total (no event between lookup and gather). Same records
+    as the event-ordered step, and each step sees the previous step's SETs."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(30000, cuda_dev)
+    got = {}
+    for mode in (False, True):
+        shard = CacheShard(512 << 20, 1 << 15, 1 << 16, cuda_dev)
+        sc = ShardedCache(shard)
+        sc.host_order = mode
+        sc.set(wl.set_batch(torch.arange(0, 15000, device=cuda_dev)))
+        recs = []
+        for step in range(4):
+            keys = wl.digests.index_select(0, wl.sample_ids(80000, 40 + step)).contiguous()
+            ids = torch.arange(15000 + 3000 * step, 18000 + 3000 * step, device=cuda_dev)
+            r = sc.serve(keys, wl.set_batch(ids))
+            torch.cuda.synchronize()
+            recs.append(unpack_records(r.data, r.off, r.size))
+        got[mode] = recs
+        assert int(sc._co_table.abs().sum()) == 0
+    assert got[False] == got[True]
+    assert sum(x is not None for x in got[True][-1]) > sum(x is not None for x in got[True][0])
