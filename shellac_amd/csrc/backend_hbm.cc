@@ -286,6 +286,9 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
       HB_OK(hipMalloc(&d->d_own, std::max<size_t>(1, ho.size()) * sizeof(int32_t)));
       HB_OK(hipMemcpy(d->d_pts, hp.data(), hp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       HB_OK(hipMemcpy(d->d_own, ho.data(), ho.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      // a pageable-memory hipMemcpy may return before its DMA lands; the batcher's
+      // non-blocking streams do not wait for the null stream
+      HB_OK(hipDeviceSynchronize());
     }
     d->pool = std::make_shared<ArenaPool>(d->device);
     if (cfg_.arena_bytes) d->pool->reserve((size_t)cfg_.depth + 2, (size_t)cfg_.arena_bytes);

@@ -2156,6 +2156,11 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   // the table is cleared once here; k_set_index resets every slot a batch used
   HIP_OK(hipMemset(dd_keys_, 0, tslots * sizeof(uint64_t)));
   HIP_OK(hipMemset(dd_win_, 0xff, tslots * sizeof(int)));
+  // hipMemset is asynchronous for device memory and runs on the null stream, which a
+  // non-blocking stream (the routed step's side stream) does not wait for: without this
+  // sync the first SET batch's dedupe could read the table before it is cleared and drop
+  // its rows (seen as set_dropped on one rank of a 3-process test, ~1 run in 6)
+  HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
@@ -2581,6 +2586,7 @@ void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
     HIP_OK(hipMemset(rc_ctl_, 0, 8 * sizeof(unsigned long long)));
     HIP_OK(hipMemset(rc_ctl_ + 2, 0xff, sizeof(unsigned long long)));
   }
+  HIP_OK(hipDeviceSynchronize());  // the null-stream memsets before any other stream's work
   __atomic_store_n(host_slots_ + kHeadSlot, h.head, __ATOMIC_RELEASE);
   if (user)
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];

@@ -42,7 +42,7 @@ def _run_world(target, world, *args, timeout=240):
             if p.is_alive():
                 p.kill()
     fails = [r for r in results if r[1] != "ok"]
-    assert not fails, fails[0][2]
+    assert not fails, "\n".join(f"rank {r[0]}: {r[2]}" for r in fails)
     return results
 
 

@@ -64,7 +64,13 @@ def _routed_worker(rank, world, port, q, backend="bounce"):
         want = [v1[k] for k in req[:-3]] + [None] * 3
         bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
                enumerate(zip(got, want)) if g != w]
-        assert not bad, f"rank {rank}: {len(bad)} wrong GETs, first {bad[:6]}"
+        if bad:  # diagnostics: which owners, hot or not, and this rank's step counters
+            owners, _ = sc._route(digest_strings([b[1] for b in bad], dev))
+            hot = sc._is_hot(digest_strings([b[1] for b in bad], dev))
+            by_owner = torch.bincount(owners.long(), minlength=world).tolist()
+            info = (f"by owner {by_owner}, hot {int(hot.sum())}, stats {sc.stats}, "
+                    f"counters {shard.counters()}")
+        assert not bad, f"rank {rank}: {len(bad)} wrong GETs, first {bad[:6]}; {info}"
         # step 3: the overwrites are visible on every rank (replicas written through)
         res = sc.serve(digest_strings(req, dev), batch([], []))
         new = {k: b"v2" + k for k in keys[:5] + keys[100:110]}
