@@ -52,9 +52,7 @@ class HbmCache {
   // overwrite as misses, so SETs may be queued between this lookup and its gather.
   // `total_slot` >= 0 also writes off[n] straight into host slot `total_slot` (pinned,
   // coherent), readable with host_slot() once the stream has passed the lookup: the
-  // response size without a D2H copy. The slot is written last, after every kernel of the
-  // lookup has finished and released its outputs: once the host has read it, work queued
-  // on any stream of this GPU may read loc/size/off (and `first`) without an event.
+  // response size without a D2H copy.
   // `first` (coalesce_keys output, may be null): rows with first[i] != i are duplicates
   // and are answered as misses without touching the index (expand_coalesced fills them
   // in after the gather).
@@ -215,9 +213,6 @@ class HbmCache {
   unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
   unsigned long long* lbc_state_ = nullptr; // device: compacting lookup's bump word
   unsigned int* lbc_done_ = nullptr;        // device: its finished-workgroup counter
-  // device: finished-workgroup counter of a lookup's offsets scan (the last one publishes
-  // the host slot; self-resetting; lookups naming a host slot are ordered on one stream)
-  unsigned int* off_done_ = nullptr;
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;

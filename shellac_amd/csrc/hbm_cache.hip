@@ -276,8 +276,7 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ off,
                                                     uint64_t* __restrict__ host_total,
                                                     const uint64_t* __restrict__ part_cnt,
-                                                    uint64_t* __restrict__ cnt,
-                                                    unsigned int* __restrict__ done) {
+                                                    uint64_t* __restrict__ cnt) {
   __shared__ unsigned long long s_w[2][kBlock / 64];
   __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -362,35 +361,8 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
     }
     off[n] = tot;
     if (cnt) cnt[n] = totc;
-    if (host_total && !done)
+    if (host_total)
       __hip_atomic_store(host_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (done) {
-    // `done` given: the host slot is written by the LAST workgroup to finish, after every
-    // workgroup released its offsets (device scope), so a host that read the slot may
-    // queue work on another stream that reads off[] without a GPU-side event. The total
-    // is the sum of the producer's partials (visible: they come from an earlier kernel).
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (s_last) {
-      unsigned long long t = 0;
-      for (int k = threadIdx.x; k < nparts; k += kBlock) t += part[k];
-      t = wave_sum(t);
-      if (lane == 0) s_w[0][w] = t;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned long long tot = 0;
-#pragma unroll
-        for (int k = 0; k < kBlock / 64; ++k) tot += s_w[0][k];
-        atomicExch(done, 0u);
-        __hip_atomic_store(host_total, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
   }
 }
 
@@ -821,10 +793,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // returned before its done-increment) and leaves both words zeroed
     __shared__ int s_last;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();  // release this workgroup's outputs before it counts as done
-      s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-    }
+    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
     __syncthreads();
     if (s_last && threadIdx.x == 0) {
       const unsigned long long t = atomicExch(bump, 0ull);
@@ -1902,12 +1871,12 @@ size_t device_scan_tmp_bytes(int64_t n) {
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
                     uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr,
                     int64_t plen_override = 0, const uint64_t* part_cnt = nullptr,
-                    uint64_t* cnt = nullptr, unsigned int* done = nullptr) {
+                    uint64_t* cnt = nullptr) {
   const int64_t plen = plen_override > 0 ? plen_override : part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
   hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
-                     host_total, part_cnt, cnt, host_total ? done : nullptr);
+                     host_total, part_cnt, cnt);
   HIP_OK(hipGetLastError());
 }
 
@@ -2038,8 +2007,6 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMemset(lbc_state_, 0, (kMaxGrid + 1) * sizeof(unsigned long long)));
   HIP_OK(hipMalloc(&lbc_done_, 64));
   HIP_OK(hipMemset(lbc_done_, 0, 64));
-  HIP_OK(hipMalloc(&off_done_, 64));
-  HIP_OK(hipMemset(off_done_, 0, 64));
   HIP_OK(hipMalloc(&part_, 3 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
@@ -2074,7 +2041,6 @@ HbmCache::~HbmCache() {
   (void)hipFree(lb_state_);
   (void)hipFree(lbc_state_);
   (void)hipFree(lbc_done_);
-  (void)hipFree(off_done_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -2195,7 +2161,7 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht, 0, nullptr, nullptr, off_done_);
+  launch_offsets(size, n, part_, grid, off, s, ht);
 }
 
 void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
@@ -2244,7 +2210,7 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
                      reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only(),
                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht, plen, nullptr, nullptr, off_done_);
+  launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }
 
 uint64_t HbmCache::host_slot(int i) const {

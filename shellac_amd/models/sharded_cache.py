@@ -177,13 +177,10 @@ class ShardedCache:
         #   beside k_coalesce, but k_coalesce then takes 139 us beside the log append and
         #   the extra cross-stream wait costs ~14 us: 0.36 ms)
         self.plan_first = os.environ.get("SHELLAC_PLAN_FIRST", "0") == "1"
-        # SHELLAC_HOST_ORDER=1: the SET's index insert and the per-request expansion are
-        # queued on the side stream only after the host has read the lookup's total (its
-        # host slot is written last, once every lookup kernel is done), instead of behind
-        # an event recorded on the main stream between the lookup and the gather. Measured
-        # within noise of the default (0.339-0.341 vs 0.339-0.343 ms, one box,
-        # profiles/r2_host_order_ab.log), so opt-in
-        self.host_order = os.environ.get("SHELLAC_HOST_ORDER", "0") == "1"
+        # (Queuing the SET index insert after the host read the lookup total, with no
+        # event between lookup and gather, needs the total published only once every
+        # lookup workgroup has released its outputs: a device-scope fence per workgroup,
+        # which cost ~30 us per step in k_offsets. Not adopted.)
         # fence scope of the events that order the main and side streams of a step:
         # "system" = torch's events (a system-scope release: L2 write-back + invalidate
         # at every record); "device" (default) / "none" = StreamEvent with a device-scope
@@ -349,19 +346,6 @@ class ShardedCache:
         if first is not None:
             out_size = torch.empty(n, dtype=torch.int64, device=self.device)
             out_off = torch.empty(n, dtype=torch.int64, device=self.device)
-        if self.host_order and not self.plan_first:
-            with torch.cuda.stream(side):  # dedupe, sizes, scan, log append
-                sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                         batch.expire, now, begin="append")
-            data = self._gather_unsynced(lk)  # returns once the host read the lookup total
-            with torch.cuda.stream(side):  # the lookup is done: no event needed
-                sh.store_finish()
-                if first is not None:
-                    expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)
-            self._xwait(main, side, "end")
-            if first is not None:
-                return GetResult(data, out_off, out_size)
-            return GetResult(data, lk.off[:n], lk.size[:n])
         ev = self._event("probe")
         ev.record(main)
         with torch.cuda.stream(side):

@@ -681,21 +681,3 @@ def test_serve_event_fences_return_the_same_records(cuda_dev, fence):
     assert all(v is not None and v[0] == pool[voff[i]: voff[i] + vlen[i]].tobytes()
                for v, i in zip(v2, ids))
     assert int(sc._co_table.abs().sum()) == 0
-
-
-def test_serve_host_ordered_index_returns_the_same_records(cuda_dev):
-    """SHELLAC_HOST_ORDER: the SET index insert and the per-request expansion are queued
-    after the host read the lookup total (no event between lookup and gather): every
-    request still gets its ground-truth record."""
-    from shellac_amd.bench.workload import Workload
-    from shellac_amd.models.sharded_cache import ShardedCache
-
-    wl = Workload(40000, cuda_dev)
-    shard = CacheShard(256 << 20, 1 << 15, 1 << 16, cuda_dev)
-    sc = ShardedCache(shard)
-    sc.host_order = True
-    for s0 in range(0, 40000, 10000):
-        sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
-    res = _serve_steps_vs_truth(sc, wl, cuda_dev)
-    assert all(w == 0 and m == 0 for w, m, _, _ in res), res
-    assert int(sc._co_table.abs().sum()) == 0
