@@ -94,18 +94,15 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("lookup_coalesced", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t table,
                                   int64_t slots, uintptr_t first, uintptr_t loc, uintptr_t size,
                                   uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve,
-                                  int slot, uintptr_t cslot, bool table_clean, uintptr_t seg_src,
-                                  uintptr_t seg_dst, uintptr_t nseg) {
+                                  int slot, uintptr_t cslot, bool table_clean) {
         py::gil_scoped_release nogil;
         c.lookup_coalesced(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first),
                            P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off), now, S(s),
-                           reserve, slot, P<uint32_t>(cslot), table_clean, P<uint64_t>(seg_src),
-                           P<uint64_t>(seg_dst), P<int64_t>(nseg));
+                           reserve, slot, P<uint32_t>(cslot), table_clean);
       }, py::arg("keys"), py::arg("n"), py::arg("table"), py::arg("slots"), py::arg("first"),
          py::arg("loc"), py::arg("size"), py::arg("off"), py::arg("now"), py::arg("stream"),
          py::arg("reserve") = 0, py::arg("total_slot") = -1, py::arg("cslot") = 0,
-         py::arg("table_clean") = false, py::arg("seg_src") = 0, py::arg("seg_dst") = 0,
-         py::arg("nseg") = 0)
+         py::arg("table_clean") = false)
       .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
                            uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s,
                            int done_slot) {
@@ -120,12 +117,12 @@ PYBIND11_MODULE(_shellac_core, m) {
         return c.wait_host_slot(i, timeout_ms);
       }, py::arg("slot"), py::arg("timeout_ms") = 10000)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
-                        uintptr_t s, uint64_t out_cap, uintptr_t n_dev) {
+                        uintptr_t s, uint64_t out_cap) {
         py::gil_scoped_release nogil;
         c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s),
-                 out_cap, P<const int64_t>(n_dev));
+                 out_cap);
       }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
-         py::arg("out_cap") = ~0ull, py::arg("n_dev") = 0)
+         py::arg("out_cap") = ~0ull)
       .def("store_graph", [](HbmCache& c, HbmCache::StoreGraph& g, uintptr_t keys,
                              uintptr_t values, uintptr_t val_off, uintptr_t vlen, uintptr_t flags,
                              uintptr_t expire, int64_t n, uint64_t bytes_bound, uint32_t now,
@@ -138,19 +135,14 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
-                       uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after,
-                       int begin) {
+                       uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
-                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), begin);
+                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after));
       }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
          py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
-         py::arg("stream"), py::arg("index_after") = 0, py::arg("begin") = 0)
-      .def("store_finish", [](HbmCache& c, uintptr_t s, uintptr_t index_after) {
-        py::gil_scoped_release nogil;
-        c.store_finish(S(s), reinterpret_cast<hipEvent_t>(index_after));
-      }, py::arg("stream"), py::arg("index_after") = 0)
+         py::arg("stream"), py::arg("index_after") = 0)
       .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
                         uintptr_t s) {
         py::gil_scoped_release nogil;

@@ -65,19 +65,10 @@ class HbmCache {
   // `cslot` (optional, u32 [n]): each claiming row's table slot, for
   // expand_coalesced_out to clear; `table_clean`: the caller guarantees a zeroed table
   // (skips the memset).
-  // `seg_src`/`seg_dst` (u64 [n+1]) and `nseg` (i64 [1]) given: the compacting form. No
-  // scan runs; each hit takes its response offset from a bump allocation (records in
-  // claim order, not row order), off[] holds the claimers' offsets (duplicates: set by
-  // expand_coalesced*), off[n] = total, and the hits form a compacted segment list
-  // (log loc, response offset) of *nseg entries with seg_dst[*nseg] = total for
-  // gather(seg_src, seg_dst, n, ..., n_dev = nseg). n < 2^24. Compacting lookups of one
-  // shard must be ordered (one stream): they share the bump word.
   void lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
                         uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
                         uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
-                        uint32_t* cslot = nullptr, bool table_clean = false,
-                        uint64_t* seg_src = nullptr, uint64_t* seg_dst = nullptr,
-                        int64_t* nseg = nullptr);
+                        uint32_t* cslot = nullptr, bool table_clean = false);
   uint64_t host_slot(int i) const;
   // Spin until the lookup that was given `total_slot` i has written it (no stream or
   // event synchronisation: the kernel's system-scope store is the signal). Throws after
@@ -103,9 +94,8 @@ class HbmCache {
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
   // caller can queue the gather before it knows the total and retry if it did not fit.
-  // `n_dev`: the segment count is read on the device (a compacting lookup's nseg).
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s,
-              uint64_t out_cap = ~0ull, const int64_t* n_dev = nullptr);
+              uint64_t out_cap = ~0ull);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).
@@ -115,20 +105,9 @@ class HbmCache {
   // and log append: it reads the index and the current head slot, which only the index
   // insert changes, and a `reserve` covering this SET keeps its gather off the bytes
   // the append overwrites.
-  // `begin` != 0: queue only the first stages and return; store_finish() queues the rest.
-  //   kStorePlanOnly: the planning kernels (CLOCK reclaim, dedupe, sizes, scan — none
-  //     touches the log, the index or the head, so a lookup may run beside or after them);
-  //   kStoreThroughAppend: planning + the log append (a lookup reserving the SET's bytes
-  //     treats them as gone, so it may run beside these too).
-  // store_finish(index_after) then queues the index insert (after `index_after`), which a
-  // lookup can observe; calling it once the lookup is known to be done (e.g. after its
-  // host slot was read) needs no event. No other store may come in between.
-  static constexpr int kStorePlanOnly = 1, kStoreThroughAppend = 2;
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
-             uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-             int begin = 0);
-  void store_finish(hipStream_t s, hipEvent_t index_after = nullptr);
+             uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
   // SET through captured hipGraphs, for callers with fixed batch sizes and fixed
   // staging buffers (the proxy's micro-batches, padded to a size class with
   // vlen = kSkipVlen rows). The five SET kernels become one graph launch. A graph bakes
@@ -211,8 +190,6 @@ class HbmCache {
   uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
   unsigned int* done_ctr_ = nullptr; // device: edge-GET workgroups finished + fail flag (self-resetting)
   unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
-  unsigned long long* lbc_state_ = nullptr; // device: compacting lookup's bump word
-  unsigned int* lbc_done_ = nullptr;        // device: its finished-workgroup counter
   // SET workspace
   int64_t set_cap_ = 0;
   uint64_t* dd_keys_ = nullptr;
@@ -225,25 +202,12 @@ class HbmCache {
   uint32_t dd_mask_ = 0;
   uint64_t ws_gen_ = 0;  // bumped when the SET workspace moves (invalidates graphs)
   std::mutex mu_;
-  static constexpr int kStagePlan = 1, kStageAppend = 2, kStageIndex = 4, kStagesAll = 7;
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                    int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-                    int stages = kStagesAll);
+                    int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
   void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after);
-  // a store begun with begin_only, waiting for store_finish
-  struct PendingStore {
-    bool on = false;
-    const Digest* keys = nullptr;
-    const uint8_t* values = nullptr;
-    const uint64_t* val_off = nullptr;
-    const uint32_t *vlen = nullptr, *flags = nullptr, *expire = nullptr;
-    int64_t n = 0;
-    uint32_t now = 0;
-    int stages = 0;  // what store_finish still queues
-  } pend_;
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------
@@ -255,10 +219,8 @@ size_t device_scan_tmp_bytes(int64_t n);
 
 // Load-balanced segmented copy: segment i copies (dst_off[i+1]-dst_off[i]) bytes
 // from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
-// `n_dev` (optional): read the segment count from device memory instead (at most n).
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
-             uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull,
-             const int64_t* n_dev = nullptr);
+             uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
 
 // GET coalescing: first[i] = the row that serves row i (one row per distinct digest
 // serves all its duplicates). `table` is scratch of coalesce_table_slots(n) u32 words.

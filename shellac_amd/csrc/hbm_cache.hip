@@ -530,36 +530,18 @@ constexpr int kCoSlots = 2 * kCoKeys;       // LDS table slots (<= 50 % load)
 // 4 waves per SIMD (<= 128 VGPRs): the 1024-key chunks of a 1M batch (1024 workgroups)
 // are all resident at once (4 per CU, 33 KB LDS each) — at 130 VGPRs (3 waves) a
 // quarter of them ran as a second round (151 vs 95 us)
-// COMPACT (with PROBE): no scan pass between the lookup and its gather. Each chunk sums
-// its hits' bytes and count, takes a contiguous range of the response buffer AND of a
-// compacted segment list with ONE 64-bit atomicAdd of (count << 40 | bytes) on a bump
-// word (count and bytes come from the same atomic, so segment order = byte order and the
-// list is sorted by destination), then writes each hit's (log loc, response offset) into
-// the list and its offset into off[row]. The launch's last workgroup publishes the
-// segment count (nseg), the total (seg_dst[nseg], off[n], the host slot) and resets the
-// bump and done words. The gather then copies the compacted hits only (k_segcopy with a
-// device-side count): ~317K segments instead of 1M rows for a Zipf batch. Records land in
-// chunk-claim order, not row order; every request still addresses its own record by off.
-constexpr int kPackShift = 40;  // bump word: count << 40 | bytes (bytes < 1 TiB, count < 16M)
-constexpr unsigned long long kPackBytes = (1ull << kPackShift) - 1;
-
-template <bool PROBE, bool COMPACT = false>
+template <bool PROBE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_coalesce(
     const Digest* __restrict__ keys, int64_t n, int64_t plen, uint32_t* __restrict__ tab,
     uint32_t tmask, uint32_t* __restrict__ first, uint32_t* __restrict__ cslot,
     Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ part, int local_only, uint64_t* __restrict__ off,
-    unsigned long long* __restrict__ bump, unsigned int* __restrict__ done,
-    uint64_t* __restrict__ host_total, uint64_t* __restrict__ seg_src,
-    uint64_t* __restrict__ seg_dst, int64_t* __restrict__ nseg) {
+    uint64_t* __restrict__ part, int local_only) {
   __shared__ Digest s_k[kCoKeys];       // the chunk's digests (LDS compares, probe input)
-  // local row + 1; COMPACT reuses it as the queued claimers' log locs after phase 2
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCoSlots];
+  __shared__ uint32_t s_tab[kCoSlots];  // local row + 1
   __shared__ uint32_t s_rep[kCoKeys];   // global claimer of each local claimer
-  // local duplicates of each local claimer; COMPACT reuses it as the queued sizes
-  __shared__ uint32_t s_dup[kCoKeys];
+  __shared__ uint32_t s_dup[kCoKeys];   // local duplicates of each local claimer
   __shared__ uint32_t s_q[PROBE ? kCoKeys : 1];   // rows this chunk probes
   __shared__ int s_qn;
   const uint64_t head = PROBE ? *head_ptr + reserve : 0;
@@ -700,68 +682,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             if (hl) mark_ref(index, hb, he, hv);
             hv = entry_vlen(hv);
             ++ops;
-            const uint64_t lc = hl ? (hl - 1) % cap : kMissLoc;
-            const uint32_t sz = hl ? item_bytes(hv) : 0u;
-            out_loc[base + j] = lc;
-            out_size[base + j] = sz;
-            if (COMPACT) {
-              reinterpret_cast<uint64_t*>(s_tab)[q] = lc;
-              s_dup[q] = sz;
-            }
+            out_loc[base + j] = hl ? (hl - 1) % cap : kMissLoc;
+            out_size[base + j] = hl ? item_bytes(hv) : 0;
             if (hl) {
               ++hits;
               bytes += hv;
               psum += item_bytes(hv);
             }
           }
-        }
-      }
-    }
-    if (COMPACT) {
-      // 2c. the chunk's hits take a contiguous range of the response and of the segment
-      //     list (queue order); thread t owns queue entries [t*kCoPer, t*kCoPer+kCoPer)
-      __shared__ unsigned long long s_cw[kBlock / 64];
-      __shared__ unsigned long long s_cbase;
-      __syncthreads();  // s_tab / s_dup hold every queued claimer's (loc, size)
-      const int qn = s_qn;
-      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-      const int q0 = threadIdx.x * kCoPer;
-      unsigned long long mine = 0;
-#pragma unroll
-      for (int u = 0; u < kCoPer; ++u) {
-        const int q = q0 + u;
-        const uint32_t sz = q < qn ? s_dup[q] : 0u;
-        mine += sz ? ((1ull << kPackShift) | sz) : 0ull;
-      }
-      unsigned long long inc = mine;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long o = __shfl_up(inc, d);
-        if (lane >= d) inc += o;
-      }
-      if (lane == 63) s_cw[w] = inc;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-#pragma unroll
-        for (int k = 0; k < kBlock / 64; ++k) t += s_cw[k];
-        s_cbase = t ? atomicAdd(bump, t) : 0ull;
-      }
-      __syncthreads();
-      unsigned long long run = s_cbase + inc - mine;
-      for (int k = 0; k < w; ++k) run += s_cw[k];
-#pragma unroll
-      for (int u = 0; u < kCoPer; ++u) {
-        const int q = q0 + u;
-        if (q >= qn) break;
-        const uint32_t sz = s_dup[q];
-        const uint64_t boff = run & kPackBytes;
-        off[base + s_q[q]] = boff;
-        if (sz) {
-          const uint64_t k = run >> kPackShift;
-          seg_src[k] = reinterpret_cast<const uint64_t*>(s_tab)[q];
-          seg_dst[k] = boff;
-          run += (1ull << kPackShift) | sz;
         }
       }
     }
@@ -785,27 +713,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     block_count(ctr, ops, &CacheCounters::get_ops, hits, &CacheCounters::get_hits, bytes,
                 &CacheCounters::get_bytes);
     block_count(ctr, dups, &CacheCounters::get_coalesced);
-    if (!COMPACT) {
-      block_partial(psum, part);  // k_offsets scans the partials
-      return;
-    }
-    // the last workgroup publishes the totals (every other workgroup's bump atomics
-    // returned before its done-increment) and leaves both words zeroed
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (s_last && threadIdx.x == 0) {
-      const unsigned long long t = atomicExch(bump, 0ull);
-      const int64_t k = (int64_t)(t >> kPackShift);
-      const uint64_t total = t & kPackBytes;
-      *nseg = k;
-      seg_dst[k] = total;
-      off[n] = total;
-      atomicExch(done, 0u);
-      if (host_total)
-        __hip_atomic_store(host_total, total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    block_partial(psum, part);  // k_offsets scans the partials
   }
 }
 
@@ -925,12 +833,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // MODE 1 extras
     const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
-    const uint64_t* __restrict__ head_ptr, uint64_t cap, const int64_t* __restrict__ n_dev,
-    int min_tile) {
+    const uint64_t* __restrict__ head_ptr, uint64_t cap, int min_tile) {
   __shared__ uint64_t s_off[kTileSegCap + 1];
-  // n_dev: the segment count lives on the device (a compacting producer wrote it; the
-  // launch did not wait for the host to learn it)
-  if (n_dev) n = *n_dev;
   __shared__ uint64_t s_src[kTileSegCap];
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
@@ -1888,10 +1792,10 @@ void device_exclusive_scan(const uint64_t* in, uint64_t* out, int64_t n, void* t
 }
 
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
-             uint8_t* dst, hipStream_t s, uint64_t dst_cap, const int64_t* n_dev) {
+             uint8_t* dst, hipStream_t s, uint64_t dst_cap) {
   if (n <= 0) return;
   launch_segcopy<0>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr, nullptr,
-                    dst_cap, n_dev);
+                    dst_cap);
   HIP_OK(hipGetLastError());
 }
 
@@ -1912,7 +1816,7 @@ void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
                      (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, cslot,
                      nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
-                     0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                     0);
   HIP_OK(hipGetLastError());
 }
 
@@ -2003,10 +1907,6 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   const size_t lb_words = (size_t)(kSmallGetMax / kEdgeKeys + 1);
   HIP_OK(hipMalloc(&lb_state_, lb_words * sizeof(unsigned long long)));
   HIP_OK(hipMemset(lb_state_, 0, lb_words * sizeof(unsigned long long)));
-  HIP_OK(hipMalloc(&lbc_state_, (kMaxGrid + 1) * sizeof(unsigned long long)));
-  HIP_OK(hipMemset(lbc_state_, 0, (kMaxGrid + 1) * sizeof(unsigned long long)));
-  HIP_OK(hipMalloc(&lbc_done_, 64));
-  HIP_OK(hipMemset(lbc_done_, 0, 64));
   HIP_OK(hipMalloc(&part_, 3 * kMaxGrid * sizeof(uint64_t)));
   HIP_OK(hipHostMalloc(&host_buf_, kCtrShards * sizeof(CacheCounters), hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
@@ -2039,8 +1939,6 @@ HbmCache::~HbmCache() {
   (void)hipFree(scratch_);
   (void)hipFree(done_ctr_);
   (void)hipFree(lb_state_);
-  (void)hipFree(lbc_state_);
-  (void)hipFree(lbc_done_);
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
@@ -2168,8 +2066,7 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
                                 int64_t table_slots, uint32_t* first, uint64_t* loc,
                                 uint64_t* size, uint64_t* off, uint32_t now, hipStream_t s,
                                 uint64_t reserve, int total_slot, uint32_t* cslot,
-                                bool table_clean, uint64_t* seg_src, uint64_t* seg_dst,
-                                int64_t* nseg) {
+                                bool table_clean) {
   TraceRange tr("hbm.lookup_coalesced");
   SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
@@ -2190,25 +2087,13 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   const int64_t per = (chunks + coalesce_grid_cap() - 1) / coalesce_grid_cap();
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
-  if (seg_src) {
-    // compacting lookup: offsets by one bump atomic per chunk, no scan launch (fusing the
-    // scan by decoupled look-back was measured slower, 0.45 vs 0.32 ms per step: a
-    // workgroup then holds its slot until every earlier one has published, and the SET
-    // chain on the side stream needs those slots; the bump never waits)
-    SH_CHECK(seg_dst && nseg && n < (1ll << 24), "compacting lookup: bad workspace or batch");
-    hipLaunchKernelGGL((k_coalesce<true, true>), dim3(grid), dim3(kBlock), 0, s, keys, n, plen,
-                       table, (uint32_t)(table_slots - 1), first, cslot, index_,
-                       cfg_.nbuckets - 1, cur_head(), reserve, cfg_.log_bytes, now, loc, size,
-                       ctr_, part_, coalesce_local_only(), off, lbc_state_, lbc_done_, ht,
-                       seg_src, seg_dst, nseg);
-    HIP_OK(hipGetLastError());
-    return;
-  }
+  // (fusing the offsets scan into this kernel — by decoupled look-back, or by one bump
+  // allocation per chunk with a compacted hit list — was measured slower: 0.45 and 0.35 vs
+  // 0.32 ms per step; see docs/PERF.md)
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
-                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only(),
-                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only());
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }
@@ -2253,29 +2138,22 @@ void HbmCache::small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t o
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
-                      hipStream_t s, uint64_t out_cap, const int64_t* n_dev) {
+                      hipStream_t s, uint64_t out_cap) {
   TraceRange tr("hbm.gather");
   DeviceGuard g(cfg_.device);
-  segcopy(log_, loc, off, n, out, s, out_cap, n_dev);
+  segcopy(log_, loc, off, n, out, s, out_cap);
 }
 
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
-                     hipEvent_t index_after, int begin) {
+                     hipEvent_t index_after) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
            "SET batch larger than half the log; split the batch");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
-  SH_CHECK(!pend_.on, "store: a split store is still waiting for store_finish");
-  SH_CHECK(begin >= 0 && begin <= kStoreThroughAppend, "store: bad begin stage");
-  const bool begin_only = begin != 0;
-  // stages this call queues: all, the planning kernels, or planning + log append
-  const int stages = begin == 0 ? kStagesAll
-                     : begin == kStorePlanOnly ? kStagePlan
-                                               : (kStagePlan | kStageAppend);
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
   if (rmax && should_reclaim(bytes_bound)) {
@@ -2299,49 +2177,28 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
-                 index_after, stages);
-    if (begin_only)
-      pend_ = PendingStore{true, cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_,
-                           w + n, now, kStagesAll & ~stages};
+                 index_after);
   } else {
     ensure_set_ws(n, s);
-    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, stages);
-    if (begin_only)
-      pend_ = PendingStore{true, keys, values, val_off, vlen, flags, expire, n, now,
-                           kStagesAll & ~stages};
+    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
   }
-  if (!begin_only) hsel_ ^= 1;  // later operations on the stream read the published slot
-}
-
-void HbmCache::store_finish(hipStream_t s, hipEvent_t index_after) {
-  TraceRange tr("hbm.store_finish");
-  std::lock_guard<std::mutex> lk(mu_);
-  DeviceGuard g(cfg_.device);
-  if (!pend_.on) return;  // the begun store had no rows
-  const PendingStore p = pend_;
-  pend_.on = false;
-  store_locked(p.keys, p.values, p.val_off, p.vlen, p.flags, p.expire, p.n, p.now, s,
-               index_after, p.stages);
-  hsel_ ^= 1;
+  hsel_ ^= 1;  // later operations on the stream read the published slot
 }
 
 // The SET kernel chain (caller holds mu_, workspace sized): dedupe (last writer wins),
 // sizes + fused scan, log append (k_segcopy<1>), two-choice CAS index insert that also
-// publishes the new head into the other head slot. `stages` selects the parts queued:
-// kStagePlan (dedupe, sizes, scan: they touch neither the log, the index nor the head),
-// kStageAppend (the log write: only bytes a reserving lookup treats as gone), kStageIndex
-// (index insert + fix-up, after `index_after`: the only part a lookup can observe).
+// publishes the new head into the other head slot. The planning kernels (dedupe, sizes,
+// scan) touch neither the log, the index nor the head; the log write touches only bytes a
+// reserving lookup treats as gone; the index insert (+ fix-up), queued after
+// `index_after`, is the only part a concurrent lookup can observe.
 void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                            int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
-                            int stages) {
-  if (stages & kStagePlan) store_plan_locked(keys, vlen, n, s);
-  if (stages & kStageAppend) {
-    launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire,
-                      cur_head(), cfg_.log_bytes, (const int64_t*)nullptr);
-    HIP_OK(hipGetLastError());
-  }
-  if (stages & kStageIndex) store_index_locked(keys, vlen, expire, n, now, s, index_after);
+                            int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after) {
+  store_plan_locked(keys, vlen, n, s);
+  launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
+                    cfg_.log_bytes);
+  HIP_OK(hipGetLastError());
+  store_index_locked(keys, vlen, expire, n, now, s, index_after);
 }
 
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,

@@ -165,18 +165,9 @@ class ShardedCache:
         # GET coalescing: the duplicate keys of a batch share one probe and one record
         # (ops.cache.coalesce); SHELLAC_COALESCE=0 probes and copies every request
         self.coalesce = os.environ.get("SHELLAC_COALESCE", "1") != "0"
-        # Two measured, opt-in schedules (profiles/r2_step_schedule_ab.md; both slower on
-        # the 1M-GET bench step, so off by default):
-        # SHELLAC_COMPACT=1: compacting coalesced lookups — response offsets by bump
-        #   allocation, the gather copies a compacted hit list, no scan launch between
-        #   probe and gather (0.354 vs 0.322 ms: the gather then starts under the SET's
-        #   log append and both bandwidth-bound copies share the memory system)
-        self.compact = os.environ.get("SHELLAC_COMPACT", "0") == "1"
-        # SHELLAC_PLAN_FIRST=1: the SET's planning kernels (dedupe, sizes, scan) run
-        #   before the GET lookup instead of beside it (dedupe 10 us alone vs 48-92 us
-        #   beside k_coalesce, but k_coalesce then takes 139 us beside the log append and
-        #   the extra cross-stream wait costs ~14 us: 0.36 ms)
-        self.plan_first = os.environ.get("SHELLAC_PLAN_FIRST", "0") == "1"
+        # (Two other N=1 schedules were measured slower and removed: a compacting lookup
+        # with bump-allocated response offsets, and the SET planning kernels ahead of the
+        # lookup; profiles/r2_step_schedule_ab.md.)
         # (Queuing the SET index insert after the host read the lookup total, with no
         # event between lookup and gather, needs the total published only once every
         # lookup workgroup has released its outputs: a device-scope fence per workgroup,
@@ -224,7 +215,7 @@ class ShardedCache:
         self.stats["get_requests"] += n
         if not self.routed:
             if self.coalesce:
-                lk, first, _ = self.shard.lookup_coalesced(keys, now, compact=self.compact)
+                lk, first, _ = self.shard.lookup_coalesced(keys, now)
             else:
                 lk, first = self.shard.lookup(keys, now), None
             data = self.shard.gather(lk)
@@ -323,15 +314,10 @@ class ShardedCache:
             main = torch.cuda.current_stream(self.device)
             self._xwait(side, main, "start")  # the previous step's gather is done with the log
             now = sh.now() if now is None else now
-            if self.plan_first:
-                with torch.cuda.stream(side):
-                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                             batch.expire, now, begin="plan")
-                self._xwait(main, side, "plan")
         if self.coalesce:
             table = self._coalesce_table(n) if side is not None else None
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
-                                                   table=table, compact=self.compact)
+                                                   table=table)
         else:
             lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound, total_slot=0),
                                        None, None, None)
@@ -349,11 +335,8 @@ class ShardedCache:
         ev = self._event("probe")
         ev.record(main)
         with torch.cuda.stream(side):
-            if self.plan_first:
-                sh.store_finish(index_after=ev)
-            else:
-                sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                         batch.expire, now, index_after=ev)
+            sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                     batch.expire, now, index_after=ev)
             if first is not None:
                 # per-request (size, off) and the table clean-up, under the gather
                 expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)

@@ -220,12 +220,7 @@ def _event_handle(ev) -> int:
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
     size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
-    off: torch.Tensor   # int64 [n+1] response offset per key; off[n] = total bytes
-    # compacting lookups (``lookup_coalesced(compact=True)``): the hits as a segment list
-    # sorted by response offset — log loc, response offset, and the count on the device
-    seg_src: Optional[torch.Tensor] = None  # int64 [n+1]
-    seg_dst: Optional[torch.Tensor] = None  # int64 [n+1]; seg_dst[nseg] = total
-    nseg: Optional[torch.Tensor] = None     # int64 [1]
+    off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
 
     @property
     def n(self) -> int:
@@ -249,7 +244,6 @@ class CacheShard:
     """
 
     EVICT = {"fifo": 0, "clock": 1}
-    _BEGIN = {None: 0, "plan": 1, "append": 2}  # HbmCache::kStorePlanOnly / kStoreThroughAppend
 
     def __init__(self, log_bytes: int, nbuckets: int, max_item: int = 1 << 20,
                  device: str | torch.device = "cpu", evict: str = "clock",
@@ -329,7 +323,7 @@ class CacheShard:
 
     def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
                          reserve_bytes: int = 0, total_slot: int = -1,
-                         table: Optional[torch.Tensor] = None, compact: bool = False):
+                         table: Optional[torch.Tensor] = None):
         """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
         row that claims a digest probes the index for it). Returns (Lookup, first,
         cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
@@ -337,12 +331,7 @@ class CacheShard:
         >= ``coalesce_table_slots(n)`` power-of-two slots) — then ``cslot`` holds each
         claimer's slot and ``expand_out`` must run to clean the table again; otherwise
         a temporary table is zeroed here and ``cslot`` is None. CPU shards: a plain
-        lookup, ``first = cslot = None``.
-        ``compact`` (GPU): no scan pass — hits take response offsets from one bump
-        allocation per 1024-key chunk (records in claim order, not row order) and form a
-        compacted segment list the gather copies; ``off`` is valid for claiming rows
-        (duplicates: after ``expand``/``expand_out``) and off[n] is the total. Compacting
-        lookups of one shard must be issued on one stream."""
+        lookup, ``first = cslot = None``."""
         if not self.is_gpu or keys.shape[0] == 0:
             return self.lookup(keys, now, reserve_bytes, total_slot), None, None
         self._check(keys, "keys")
@@ -362,18 +351,11 @@ class CacheShard:
         size = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         now = self.now() if now is None else now
-        seg = (torch.empty(2, n + 1, dtype=torch.int64, device=self.device) if compact else None)
-        nseg = torch.empty(1, dtype=torch.int64, device=self.device) if compact else None
         self._impl.lookup_coalesced(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
                                     loc.data_ptr(), size.data_ptr(), off.data_ptr(), now,
                                     self._s(), int(reserve_bytes), int(total_slot),
                                     cslot.data_ptr() if cslot is not None else 0,
-                                    cslot is not None,
-                                    seg[0].data_ptr() if compact else 0,
-                                    seg[1].data_ptr() if compact else 0,
-                                    nseg.data_ptr() if compact else 0)
-        if compact:
-            return Lookup(loc, size, off, seg[0], seg[1], nseg), first, cslot
+                                    cslot is not None)
         return Lookup(loc, size, off), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
@@ -408,12 +390,8 @@ class CacheShard:
         self._check(out, "out")
         if self.is_gpu:
             cap = out.numel() if out_cap is None else min(int(out_cap), out.numel())
-            if lk.seg_src is not None:  # compacting lookup: copy the hit list only
-                self._impl.gather(lk.seg_src.data_ptr(), lk.seg_dst.data_ptr(), lk.n,
-                                  out.data_ptr(), self._s(), cap, lk.nseg.data_ptr())
-            else:
-                self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
-                                  self._s(), cap)
+            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
+                              self._s(), cap)
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
@@ -445,16 +423,13 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after=None, begin: Optional[str] = None) -> None:
+              index_after=None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
         dedupe, sizing and the log append run at once, the index insert waits for the
         event — so a lookup followed by that event on another stream overlaps the SET's log
-        write (see ``HbmCache::store``).
-        ``begin`` (GPU): queue the first stages only — ``"plan"`` (dedupe, sizes, scan)
-        or ``"append"`` (those plus the log write) — and let ``store_finish`` queue the
-        rest (the index insert, after ``index_after``)."""
+        write (see ``HbmCache::store``)."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -469,18 +444,10 @@ class CacheShard:
             bound = (self.payload_bound(n, values.numel()) if bytes_bound is None
                      else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
-                             fp, ep, n, bound, now, self._s(), _event_handle(index_after),
-                             self._BEGIN[begin])
+                             fp, ep, n, bound, now, self._s(), _event_handle(index_after))
         else:
-            if begin is not None:
-                raise ValueError("begin is a GPU-shard option")
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now)
-
-    def store_finish(self, index_after=None) -> None:
-        """Second half of ``store(begin_only=True)``: the log append and the index insert
-        (which waits for ``index_after``), on the current stream."""
-        self._impl.store_finish(self._s(), _event_handle(index_after))
 
     def set_many(self, keys: Sequence[bytes], values: Sequence[bytes], ttl: int = 0,
                  flags: int = 0) -> None:

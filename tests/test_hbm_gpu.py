@@ -573,45 +573,6 @@ def test_set_index_resets_over_dead_entries_lose_nothing(cuda_dev):
     assert len(hits) > 900
 
 
-@pytest.mark.parametrize("n", [1, 5000, 300000, 2500000])
-def test_compacting_lookup_matches_scanned_lookup(cuda_dev, n):
-    """k_coalesce<COMPACT>: response offsets from one bump allocation per chunk instead of
-    a scan. Every request gets the same record as the scanned coalesced lookup, the total
-    and the hit-list length agree, the hit list is sorted by response offset and tiles
-    [0, total) exactly, and the bump/done words are left zeroed (a second launch agrees)."""
-    from shellac_amd.bench.workload import Workload
-    from shellac_amd.ops.cache import expand
-
-    wl = Workload(20000, cuda_dev)
-    shard = CacheShard(256 << 20, 1 << 14, 1 << 16, cuda_dev)
-    for s0 in range(0, 15000, 5000):  # ids >= 15000 miss
-        shard.store(*_set_args(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
-    keys = wl.digests.index_select(0, wl.sample_ids(n, 3)).contiguous()
-    outs = []
-    for compact in (False, True, True):
-        lk, first, _ = shard.lookup_coalesced(keys, compact=compact)
-        data = shard.gather(lk)
-        torch.cuda.synchronize()
-        if compact:
-            k = int(lk.nseg)
-            dst = lk.seg_dst[: k + 1].cpu()
-            claim = first.cpu() == torch.arange(n, dtype=torch.int32)
-            assert k == int(((lk.size[:n].cpu() > 0) & claim).sum())
-            assert int(dst[k]) == int(lk.off[n])
-            sizes = (lk.size[:n].cpu())[claim & (lk.size[:n].cpu() > 0)]
-            assert int(dst[0]) == 0 and torch.all(dst[1:] >= dst[:-1])
-            assert int(sizes.sum()) == int(dst[k])
-        expand(first, lk.size, lk.off)
-        outs.append((unpack_records(data, lk.off[:n], lk.size[:n]), int(lk.off[n])))
-    assert outs[0] == outs[1] == outs[2]
-    hit = sum(r is not None for r in outs[0][0])
-    assert 0 < hit < n or n == 1
-
-
-def _set_args(b):
-    return b.keys, b.values, b.val_off, b.vlen, b.flags, b.expire
-
-
 def _serve_steps_vs_truth(sc, wl, dev, steps=4, nget=100000):
     """serve() steps of Zipf GETs over a filled cache; per step the number of requests
     that got a value other than the workload's ground truth, and of misses."""
@@ -635,19 +596,16 @@ def _serve_steps_vs_truth(sc, wl, dev, steps=4, nget=100000):
     return out
 
 
-@pytest.mark.parametrize("compact,plan_first", [(False, False), (True, False), (False, True),
-                                                (True, True)])
-def test_serve_schedules_return_the_same_records(cuda_dev, compact, plan_first):
-    """The N=1 step schedules (default; compacting lookup; SET planning first) serve the
-    workload's ground-truth record (value and flags) for every request, step after step,
-    over a cache that holds every key (no misses)."""
+def test_serve_steps_return_ground_truth_records(cuda_dev):
+    """The N=1 serving step (coalesced lookup and gather on the main stream, SET chain on
+    the side stream) serves the workload's ground-truth record (value and flags) for every
+    request, step after step, over a cache that holds every key (no misses)."""
     from shellac_amd.bench.workload import Workload
     from shellac_amd.models.sharded_cache import ShardedCache
 
     wl = Workload(40000, cuda_dev)
     shard = CacheShard(256 << 20, 1 << 15, 1 << 16, cuda_dev)
     sc = ShardedCache(shard)
-    sc.compact, sc.plan_first = compact, plan_first
     for s0 in range(0, 40000, 10000):
         sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
     res = _serve_steps_vs_truth(sc, wl, cuda_dev)
