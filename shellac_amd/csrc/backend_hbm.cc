@@ -579,7 +579,6 @@ void HbmBackend::Dev::loop() {
 
 void HbmBackend::Dev::launch(Flight& f) {
   TraceRange tr("hbm_backend.launch");
-  const HbmBackendConfig& cfg = be->cfg_;
   f.gets.clear();
   f.sets.clear();
   f.dels.clear();

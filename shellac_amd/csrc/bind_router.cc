@@ -81,6 +81,9 @@ void bind_router(py::module_& m) {
       }, py::arg("data"), py::arg("recv"), py::arg("recv_bytes"), py::arg("shard"),
          py::arg("replica").none(true), py::arg("now"), py::arg("out_size"), py::arg("out_off"),
          py::arg("stream"))
+      .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
+      .def("set_defer_join", &RoutedStep::set_defer_join)
+      .def_property_readonly("sets_pending", &RoutedStep::sets_pending)
       .def_property_readonly("mg", &RoutedStep::mg)
       .def_property_readonly("ms", &RoutedStep::ms)
       .def_property_readonly("n_local", &RoutedStep::n_local);

@@ -94,6 +94,13 @@ class RoutedStep {
   void finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
               HbmCache* replica, uint32_t now, uint64_t* out_size, uint64_t* out_off,
               hipStream_t s);
+  // `s` waits for the main-shard SET chain of the last finish(). With the deferred join
+  // (default) finish() does not wait for it: the chain runs under the next step's plan
+  // and the next owner() joins before it touches the main shard, so the caller must
+  // keep `recv` alive until then and call join_sets() before any other use of the shard.
+  void join_sets(hipStream_t s);
+  void set_defer_join(bool on) { defer_join_ = on; }
+  bool sets_pending() const { return sets_pending_; }
 
   int64_t mg() const { return mg_; }
   int64_t ms() const { return ms_; }
@@ -123,6 +130,12 @@ class RoutedStep {
   // the caller's stream (finish); events fork and join the two
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_fill_ = nullptr, ev_join_ = nullptr, ev_pjoin_ = nullptr;
+  // store stream: the received-SET chain of the main shard (fork_store). Separate from
+  // side_ (the SET planning of plan()), so the next step's planning does not queue
+  // behind a deferred SET chain.
+  hipStream_t store_side_ = nullptr;
+  hipEvent_t ev_sfork_ = nullptr;
+  bool defer_join_ = true, sets_pending_ = false;
   // per-step state
   int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
   uint64_t local_bytes_ = 0;

@@ -616,6 +616,8 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   RT_OK(hipSetDevice(device_));
   RT_OK(hipHostMalloc(&host_, (8 * (size_t)world + 8) * sizeof(int64_t), hipHostMallocDefault));
   RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  RT_OK(hipStreamCreateWithFlags(&store_side_, hipStreamNonBlocking));
+  RT_OK(hipEventCreateWithFlags(&ev_sfork_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_fill_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
@@ -631,7 +633,9 @@ RoutedStep::~RoutedStep() {
   (void)hipEventDestroy(ev_fill_);
   (void)hipEventDestroy(ev_join_);
   (void)hipEventDestroy(ev_pjoin_);
+  (void)hipEventDestroy(ev_sfork_);
   (void)hipStreamDestroy(side_);
+  (void)hipStreamDestroy(store_side_);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
@@ -788,6 +792,9 @@ void RoutedStep::pack(uint8_t* send, hipStream_t s) {
 void RoutedStep::owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint64_t* sizes_out,
                        hipStream_t s) {
   const int W = w_;
+  // the last step's SET chain reads the body arena (rrec_) and writes the main shard:
+  // both are about to be reused
+  join_sets(s);
   uint8_t* body = buf<uint8_t>(kBody, 16 * mg_ + 32 * ms_ + 16);
   uint64_t* roff = buf<uint64_t>(kRSegOff, 2 * W + 1);
   uint64_t* rsrc = buf<uint64_t>(kRSegSrc, 2 * W);
@@ -834,14 +841,21 @@ void RoutedStep::fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* s
   uint32_t* fl = buf<uint32_t>(kFl, ms);
   uint32_t* ex = buf<uint32_t>(kEx, ms);
   uint64_t* roff = buf<uint64_t>(kRoff, ms);
-  RT_OK(hipEventRecord(ev_fork_, s));
-  RT_OK(hipStreamWaitEvent(side_, ev_fork_, 0));
+  RT_OK(hipEventRecord(ev_sfork_, s));
+  RT_OK(hipStreamWaitEvent(store_side_, ev_sfork_, 0));
   hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t),
-                     side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
+                     store_side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
   RT_OK(hipGetLastError());
-  RT_OK(hipEventRecord(ev_fill_, side_));
-  shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, side_);
-  RT_OK(hipEventRecord(ev_join_, side_));
+  RT_OK(hipEventRecord(ev_fill_, store_side_));
+  shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, store_side_);
+  RT_OK(hipEventRecord(ev_join_, store_side_));
+  sets_pending_ = true;
+}
+
+void RoutedStep::join_sets(hipStream_t s) {
+  if (!sets_pending_) return;
+  RT_OK(hipStreamWaitEvent(s, ev_join_, 0));
+  sets_pending_ = false;
 }
 
 void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
@@ -865,10 +879,12 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
     roff = buf<uint64_t>(kRoff, ms);
   }
   if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
+  // k_rs_fill reads rtable_, which the next step's count exchange overwrites: later work
+  // on `s` (and the collectives ordered after it) waits for the fill
+  if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_fill_, 0));
   if (ms > 0 && replica) {
     // the replica's own SET rows (tier 1) go after its gather: they may overwrite
-    // log bytes the gather reads
-    RT_OK(hipStreamWaitEvent(s, ev_fill_, 0));
+    // log bytes the gather reads (the fill they read was waited for above)
     replica->store(rkeys, recv, roff, v1, fl, ex, ms, bound, now, s);
   }
   if (n_ > 0)
@@ -877,7 +893,10 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
                        have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off);
   RT_OK(hipGetLastError());
   if (first_) expand_coalesced(first_, n_, out_size, out_off, s);  // duplicates: claimer's record
-  if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_join_, 0));  // join: later work sees the SETs
+  // join: later work sees the SETs. Deferred (default), the next step's plan (replica
+  // probe, routing: no main-shard access) runs concurrently with the SET chain and its
+  // owner() joins
+  if (!defer_join_) join_sets(s);
 }
 
 }  // namespace shellac

@@ -159,6 +159,11 @@ class ShardedCache:
         self.fused = True
         self._engine = None
         self._xtable = None
+        # the routed step's main-shard SET chain is joined by the NEXT step's owner lookup
+        # (RoutedStep::join_sets), so it runs under that step's planning; its input buffer
+        # stays referenced until then. SHELLAC_DEFER_SET_JOIN=0 joins at the end of serve.
+        self.defer_set_join = os.environ.get("SHELLAC_DEFER_SET_JOIN", "1") != "0"
+        self._held_recv = None
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
         # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
         self.overlap_store = os.environ.get("SHELLAC_OVERLAP_STORE", "1") != "0"
@@ -192,6 +197,16 @@ class ShardedCache:
                       "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0}
 
     # ------------------------------------------------------------------------------
+    def sync_sets(self) -> None:
+        """Order the current stream after the SETs of the last routed ``serve`` (whose
+        main-shard store may still be running on the executor's store stream). Every
+        other ShardedCache method calls it; call it before using ``self.shard`` directly
+        after a routed ``serve`` (a device synchronisation also does)."""
+        e = self._engine
+        if e is not None and e.sets_pending:
+            e.join_sets(torch.cuda.current_stream(self.device).cuda_stream)
+            self._held_recv = None
+
     def _route(self, keys: torch.Tensor):
         return R.route(keys, self.ring_pts, self.ring_own, self.world)
 
@@ -211,6 +226,7 @@ class ShardedCache:
         return (cand == keys).all(dim=1)
 
     def get(self, keys: torch.Tensor, now: Optional[int] = None) -> GetResult:
+        self.sync_sets()
         n = keys.shape[0]
         self.stats["get_requests"] += n
         if not self.routed:
@@ -433,6 +449,7 @@ class ShardedCache:
         e = self._engine
         if e is None:
             e = self._engine = c.RoutedStep(w, me, dev.index)
+            e.set_defer_join(self.defer_set_join)
             # [table (3w) | rtable (3w) | extras (3)]: read back with one copy
             self._xtable = torch.empty(6 * w + 3, dtype=i64, device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
@@ -493,6 +510,9 @@ class ShardedCache:
         vwork.wait()  # stream-ordered: the SET stores below read the value region
         e.finish(data.data_ptr(), recv.data_ptr(), rq + rv, self.shard._impl, rep, now,
                  out[0].data_ptr(), out[1].data_ptr(), st)
+        # the main-shard SET chain reads `recv` until the next step's owner() joins it (the
+        # previous step's buffer is released here: this step's owner() has joined)
+        self._held_recv = recv if e.sets_pending else None
         self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
         self.stats["replica_hits"] += n_local - n_dup
         self.stats["coalesced_gets"] += n_dup
@@ -706,6 +726,7 @@ class ShardedCache:
         return GetResult(data, off, size)
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
+        self.sync_sets()
         n = batch.keys.shape[0]
         self.stats["set_requests"] += n
         if not self.routed:
@@ -771,6 +792,7 @@ class ShardedCache:
                                rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
 
     def delete(self, keys: torch.Tensor, now: Optional[int] = None) -> torch.Tensor:
+        self.sync_sets()
         if not self.routed:
             return self.shard.remove(keys, now)
         if self.replica is not None:  # replicas are dropped everywhere (collective)
@@ -797,6 +819,7 @@ class ShardedCache:
                         now: Optional[int] = None) -> int:
         """Collective. Replace the replica tier with the global top-k keys by request
         frequency (from ``keys`` or the recent GET samples). Returns #objects cached."""
+        self.sync_sets()
         if self.replica is None:
             return 0
         dev, w = self.device, self.world
@@ -869,6 +892,7 @@ class ShardedCache:
         the live objects it holds that the new ring assigns elsewhere to their new
         owners through the routed SET path (warm rebalancing: no refetch from the
         origin). Returns the number of objects this rank migrated."""
+        self.sync_sets()
         moved = 0
         batch = None
         mkeys = None
@@ -894,6 +918,7 @@ class ShardedCache:
         """Collective. Simulate (or react to) the loss of ``rank``'s shard: every rank
         drops it from the ring (its keys remap, like ketama auto-eject) and the lost
         shard's contents are discarded."""
+        self.sync_sets()
         if rank not in self.ring.shards:
             return
         self.set_ring(self.ring.without(rank), migrate=False)
@@ -915,13 +940,16 @@ class ShardedCache:
 
         os.makedirs(directory, exist_ok=True)
         path = os.path.join(directory, f"shard-{self.rank}.snap")
+        self.sync_sets()
         self.shard.save(path)
         return path
 
     def load(self, directory: str) -> None:
         import os
 
+        self.sync_sets()
         self.shard.load(os.path.join(directory, f"shard-{self.rank}.snap"))
 
     def counters(self) -> dict:
+        self.sync_sets()
         return allreduce_stats(self.shard.counters(), self.device, self.group)
