@@ -94,6 +94,9 @@ def parse():
     ap.add_argument("--no-smoke", action="store_true")
     ap.add_argument("--no-uncoalesced", action="store_true",
                     help="skip the secondary uncoalesced-GET measurement")
+    ap.add_argument("--no-wrapped", action="store_true",
+                    help="skip the secondary steady-state measurement (value log wrapped, so "
+                         "every SET batch runs the eviction hand)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -358,10 +361,13 @@ def main():
     before = shard.counters()
     st0 = dict(sc.stats)
     gb0 = sc.gathered_bytes
+    head0 = shard.head()
     elapsed, _, res = timed(args.steps, args.warmup)
     gathered = sc.gathered_bytes - gb0
     last_batch = (args.warmup + args.steps - 1) % P
+    sc.sync_sets()
     after = shard.counters()
+    head1 = shard.head()
     # owner-shard counters cover the GETs that left the replica tier; replica hits
     # are counted by the serving step
     rep_hits = sc.stats["replica_hits"] - st0["replica_hits"]
@@ -409,6 +415,43 @@ def main():
         unco_el, _, _ = timed(args.steps, args.warmup)
         sc.coalesce = True
         unco = (args.batch + args.sets) * world * args.steps / unco_el
+
+    # secondary: steady state of a full cache. The headline steps run before the value log
+    # has wrapped (16 GiB per shard, ~66 MB appended per step); a serving cache is full, and
+    # then every SET batch runs the eviction hand (CLOCK second chances) first. Steps run
+    # until every rank's log has wrapped by a quarter lap, then the same K steps are timed.
+    wrapped = None
+    if not args.no_wrapped and not host_edge and dev.type == "cuda":
+        per_step = max((head1 - head0) / max(args.steps, 1), 1.0)
+        need = torch.tensor([max(0.0, (1.25 * log_bytes - shard.head()) / per_step)],
+                            dtype=torch.float64, device=rdev)
+        if real_world > 1:
+            dist.all_reduce(need, op=dist.ReduceOp.MAX)
+        nfill = int(float(need)) + 2
+        if nfill <= 20000:
+            base = args.warmup + 2 * args.steps
+            for i in range(nfill):
+                step(base + i)
+            sync()
+            sc.sync_sets()
+            w0 = shard.counters()
+            el_w, iv_w, _ = timed(args.steps, base + nfill, events=use_events)
+            sc.sync_sets()
+            w1 = shard.counters()
+            wagg = torch.tensor([w1["get_hits"] - w0["get_hits"], w1["get_ops"] - w0["get_ops"],
+                                 w1["reinsert_bytes"] - w0["reinsert_bytes"]],
+                                dtype=torch.int64, device=rdev)
+            if real_world > 1:
+                dist.all_reduce(wagg)
+            wh, wo, wr = (int(v) for v in wagg.tolist())
+            wrapped = {"ms_per_step": round(el_w / args.steps * 1e3, 4),
+                       "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps
+                                                / el_w, 1),
+                       "fill_steps": nfill,
+                       "owner_hit_ratio": round(wh / max(wo, 1), 4),
+                       "reinserted_bytes_per_step_per_rank": round(wr / world / args.steps)}
+            if iv_w:
+                wrapped["ms_per_step_median_gpu_events"] = round(sorted(iv_w)[len(iv_w) // 2], 4)
 
     t_sm = time.perf_counter()
     sm = {} if (args.no_smoke or dev.type != "cuda" or sim or bounce) else smoke(rank, world, dev)
@@ -460,7 +503,13 @@ def main():
         "get_unique_per_s": round((gops + rep_hits) / elapsed, 1),
         "uncoalesced_ops_per_s": round(unco, 1) if unco else None,
         "batches_cycled": P,
+        # CLOCK second chances per step (objects re-appended ahead of the log overwrite):
+        # 0 until the value log has wrapped
+        "reinserted_bytes_per_step": round((after["reinsert_bytes"] - before["reinsert_bytes"])
+                                           / args.steps),
         "edge": args.edge,
+        # the same step with the value log wrapped (eviction in every SET batch)
+        "log_wrapped": wrapped,
         "smoke": sm,
     }
     if host_edge:

@@ -18,6 +18,8 @@
 // prefix sum, and lookups are coalesced 128-byte reads.
 #pragma once
 
+#include <cstdlib>
+
 #include "digest.h"
 
 namespace shellac {
@@ -82,8 +84,21 @@ inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
   r = r < (1ull << 20) ? (1ull << 20) : (r > (1ull << 30) ? (1ull << 30) : r);
   return (r < log_bytes / 4 ? r : log_bytes / 4) / 16 * 16;
 }
+// Window = k * n + 256 entries, k = 2 by default: a batch can reinsert up to about its
+// own bytes (write amplification <= 2) before referenced items past the window age out.
+// Every window entry costs a scan row and a (skip) row of the combined SET chain, so the
+// window is the fixed cost of a SET batch once the log has wrapped: k = 4 made the
+// steady-state N=1 step 0.91 ms at a 5 GiB log and 0.41 ms at 16 GiB, k = 2 0.51 / 0.37
+// ms with the same hit ratio and reinsertions (profiles/r2_hand_window_ab.log); the
+// evict_sim hit ratios are identical for k = 2, 3, 4; k = 1 does not cover the batch's own
+// bytes and degrades to FIFO. SHELLAC_HAND_WINDOW=k overrides (1..16), both engines alike.
 inline int64_t hand_window(int64_t n) {
-  const int64_t w = 4 * n + 256;
+  static const int64_t k = [] {
+    const char* e = std::getenv("SHELLAC_HAND_WINDOW");
+    const long v = e ? std::atol(e) : 2;
+    return (int64_t)(v < 1 ? 1 : (v > 16 ? 16 : v));
+  }();
+  const int64_t w = k * n + 256;
   return w < (1 << 20) ? w : (1 << 20);
 }
 inline uint64_t ring_entries(uint64_t nbuckets) {
