@@ -1359,14 +1359,20 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
         const uint64_t d0 = pack2(w0.x, w0.y), d1 = pack2(w0.z, w0.w);
         const uint32_t vlen = w1.x;
         const Digest d{d0, d1};
+        // the key's entry (a key has at most one): first bucket first, the second only
+        // when the first does not hold the digest (SETs fill the first bucket first, so one
+        // 128-B line per window entry usually settles it). The item is live iff the key's
+        // entry points at it; a superseded copy finds its key's entry pointing elsewhere.
         const uint64_t bs[2] = {bucket1(d, mask), bucket2(d, mask)};
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
+        bool found = false;
+        for (int q = 0; q < 2 && !found; ++q)
 #pragma unroll
           for (int k = 0; k < (int)kEntriesPerBucket; ++k) {
             const Entry* e = index + bs[q] * kEntriesPerBucket + k;
             const uint64_t el = __hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e->d0 == d0 && e->d1 == d1) found = true;
             if (el == l + 1) {
+              found = true;
               const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
               const uint32_t ex = (uint32_t)(ve >> 32);
               if (((uint32_t)ve & kRefBit) && (ex == 0 || ex > a.now)) h = item_bytes(vlen);
@@ -1420,13 +1426,18 @@ __global__ __launch_bounds__(kBlock) void k_rc_cut(RcArgs a, const uint64_t* __r
   __syncthreads();
   unsigned long long hx = s_pre + inc - h;
   for (int k = 0; k < w; ++k) hx += s_w[k];
+  bool meets = false;
   if (j < a.W) {
     rc_hx[j] = hx;
     const uint64_t loc = rc_loc[j];
     const uint64_t r = hx < a.rmax ? hx : a.rmax;
-    if (loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r)
-      atomicMin(&a.ctl[2], (unsigned long long)j);
+    meets = loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r;
   }
+  // only the first entry meeting the bound matters: one atomic per wave (its lowest
+  // lane), not one per entry — past the cut every entry meets it, and same-address
+  // atomics serialise
+  const unsigned long long mb = __ballot(meets);
+  if (mb && lane == __ffsll((long long)mb) - 1) atomicMin(&a.ctl[2], (unsigned long long)j);
 }
 
 __global__ __launch_bounds__(kBlock) void k_rc_pick(
