@@ -365,4 +365,5 @@ PYBIND11_MODULE(_shellac_core, m) {
   bind_http(m);
   bind_net(m);
   bind_router(m);
+  bind_deflate(m);
 }

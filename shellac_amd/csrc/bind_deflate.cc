@@ -1,0 +1,66 @@
+// pybind11 bindings of the GPU batch gzip engine (deflate.h).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <string_view>
+
+#include "bind_parts.h"
+#include "deflate.h"
+
+namespace py = pybind11;
+using namespace shellac;
+
+namespace {
+// Views of the callers' bytes objects (immutable, and the argument list keeps them alive
+// for the call, so the GIL can be released without copying them).
+std::vector<std::string_view> views(const py::list& in) {
+  std::vector<std::string_view> v;
+  v.reserve(in.size());
+  for (const auto& o : in) {
+    if (!PyBytes_Check(o.ptr())) throw py::type_error("gzip inputs must be bytes");
+    v.emplace_back(PyBytes_AS_STRING(o.ptr()), (size_t)PyBytes_GET_SIZE(o.ptr()));
+  }
+  return v;
+}
+
+py::list to_list(const std::vector<std::string>& out) {
+  py::list l(out.size());
+  for (size_t i = 0; i < out.size(); ++i) l[i] = py::bytes(out[i]);
+  return l;
+}
+}  // namespace
+
+void bind_deflate(py::module_& m) {
+  m.attr("DEFLATE_BLOCK") = kDeflateBlock;
+  py::class_<GzipStats>(m, "GzipStats")
+      .def_readonly("inputs", &GzipStats::inputs)
+      .def_readonly("blocks", &GzipStats::blocks)
+      .def_readonly("in_bytes", &GzipStats::in_bytes)
+      .def_readonly("out_bytes", &GzipStats::out_bytes)
+      .def_readonly("stored_blocks", &GzipStats::stored_blocks)
+      .def_readonly("last_pack_ms", &GzipStats::last_pack_ms)
+      .def_readonly("last_gpu_ms", &GzipStats::last_gpu_ms)
+      .def_readonly("last_assemble_ms", &GzipStats::last_assemble_ms);
+  py::class_<GpuGzip>(m, "GpuGzip")
+      .def(py::init<int>(), py::arg("device") = 0)
+      .def("compress", [](GpuGzip& g, const py::list& in) {
+        auto v = views(in);
+        std::vector<std::string> out;
+        {
+          py::gil_scoped_release nogil;
+          out = g.compress(v);
+        }
+        return to_list(out);
+      })
+      .def("deflate", [](GpuGzip& g, const py::list& in) {
+        auto v = views(in);
+        std::vector<std::string> out;
+        {
+          py::gil_scoped_release nogil;
+          out = g.deflate(v);
+        }
+        return to_list(out);
+      })
+      .def("stats", &GpuGzip::stats)
+      .def_property_readonly("device", &GpuGzip::device);
+}

@@ -1,0 +1,72 @@
+// Batch gzip (RFC 1952 members around RFC 1951 DEFLATE data) on one MI355X.
+//
+// The reference gunzips every origin response and gzips it again at level 6 before
+// caching it (src/python/shellac/server/HttpParser.py:124-127, :343-351); the proxy here
+// passes gzip bodies through and compresses only identity text bodies (--compress), on
+// the CPU. This engine moves that compression to the GPU for whole batches of bodies
+// ("batch gzip on GPU for the miss path").
+//
+// Design (deflate.hip): every input is cut into 32 KiB blocks and every block is one
+// workgroup of ONE wave. The wave keeps the block and a 4096-entry hash head table in
+// LDS and parses greedily: at each position the 64 lanes compare the candidate match
+// 64 bytes at a time (one ballot finds the first mismatch), the positions a match covers
+// are hashed in parallel, and the codes go out through a wave-uniform 64-bit bit buffer
+// as fixed-Huffman symbols (BTYPE 01). Blocks are independent (the window never crosses
+// a block), so a non-final block ends with an empty stored block (the zlib sync-flush
+// marker 00 00 FF FF) and the compressed blocks of one input concatenate byte-wise. A
+// block that would not shrink is emitted as a stored block. CRC-32 and ISIZE are
+// computed on the host (zlib crc32 runs at GB/s; the parse is the expensive part).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace shellac {
+
+constexpr int kDeflateBlock = 32768;                 // input bytes per block (= max window)
+constexpr int kDeflateStride = kDeflateBlock + 64;   // output bytes reserved per block
+
+struct GzipStats {
+  uint64_t inputs = 0, blocks = 0, in_bytes = 0, out_bytes = 0, stored_blocks = 0;
+  // last call, milliseconds: host packing, GPU (copies in + kernel + copies out), assembly
+  double last_pack_ms = 0, last_gpu_ms = 0, last_assemble_ms = 0;
+};
+
+class GpuGzip {
+ public:
+  explicit GpuGzip(int device);
+  ~GpuGzip();
+  GpuGzip(const GpuGzip&) = delete;
+  GpuGzip& operator=(const GpuGzip&) = delete;
+
+  // One gzip member per input, in input order (decompressible by zlib / gzip).
+  std::vector<std::string> compress(const std::vector<std::string_view>& in);
+  // Raw DEFLATE streams only (no gzip header / trailer), for tests and benchmarks.
+  std::vector<std::string> deflate(const std::vector<std::string_view>& in);
+  GzipStats stats() const { return stats_; }
+  int device() const { return device_; }
+
+ private:
+  void run(const std::vector<std::string_view>& in, std::vector<std::string>* out, bool gzip);
+  template <typename T>
+  T* grow(T** p, size_t* cap, size_t count, bool host);
+
+  int device_;
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+  GzipStats stats_;
+  // grow-only staging: pinned host and device copies of the packed input, the block
+  // table (src offset, length | final << 31) and the per-block outputs
+  uint8_t *h_in_ = nullptr, *d_in_ = nullptr, *h_out_ = nullptr, *d_out_ = nullptr;
+  uint64_t *h_tab_ = nullptr, *d_tab_ = nullptr;
+  uint32_t *h_len_ = nullptr, *d_len_ = nullptr;
+  size_t h_in_cap_ = 0, d_in_cap_ = 0, h_out_cap_ = 0, d_out_cap_ = 0, h_tab_cap_ = 0,
+         d_tab_cap_ = 0, h_len_cap_ = 0, d_len_cap_ = 0;
+};
+
+}  // namespace shellac
