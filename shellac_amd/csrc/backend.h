@@ -60,6 +60,18 @@ using GetCallback = std::function<void(bool hit, CacheValue v)>;
 using DelCallback = std::function<void(bool found)>;
 using StatList = std::vector<std::pair<std::string, uint64_t>>;
 
+// Asynchronous body compressor for the proxy's -z path: `done` runs on the compressor's
+// thread (callers post back to their reactor) with ok = false and the original body when
+// compression failed. The GPU implementation is GzipService (deflate.h); the proxy
+// itself only sees this interface, so it builds without the HIP runtime.
+class Compressor {
+ public:
+  using Done = std::function<void(bool ok, std::string out)>;
+  virtual ~Compressor() = default;
+  virtual void submit(std::string body, Done done) = 0;
+  virtual void stats(StatList* out) = 0;
+};
+
 class CacheBackend {
  public:
   virtual ~CacheBackend() = default;

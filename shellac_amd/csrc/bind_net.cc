@@ -11,6 +11,7 @@
 #include <pybind11/numpy.h>
 #include "mcserver.h"
 #include "origin.h"
+#include "deflate.h"
 #include "proxy.h"
 
 namespace py = pybind11;
@@ -245,9 +246,11 @@ void bind_net(py::module_& m) {
                        bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
                        uint64_t stream_high_water, const std::string& health_path,
                        int health_interval_ms, int health_timeout_ms, int health_fails,
-                       std::vector<int> cpus, int spin_us) {
+                       std::vector<int> cpus, int spin_us, int gzip_gpu, int gzip_batch_us) {
              ProxyConfig c;
              c.spin_us = spin_us;
+             c.gzip_gpu = gzip_gpu;
+             c.gzip_batch_us = gzip_batch_us;
              c.upstreams = resolve_list(upstreams, 80);
              c.port = port;
              c.bind = bind;
@@ -272,7 +275,10 @@ void bind_net(py::module_& m) {
              std::shared_ptr<CacheBackend> be;
              if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
              c.cache_enabled = be != nullptr;
-             return new Proxy(c, be);
+             auto* px = new Proxy(c, be);
+             if (c.compress && c.gzip_gpu >= 0)
+               px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us));
+             return px;
            }),
            py::arg("upstreams"), py::arg("backend") = py::none(), py::arg("port") = 8080,
            py::arg("bind") = "0.0.0.0", py::arg("threads") = 1, py::arg("ttl") = 170,
@@ -283,7 +289,8 @@ void bind_net(py::module_& m) {
            py::arg("stream_bytes") = 1 << 20, py::arg("stream_high_water") = 8 << 20,
            py::arg("health_path") = "", py::arg("health_interval_ms") = 1000,
            py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2,
-           py::arg("cpus") = std::vector<int>{}, py::arg("spin_us") = 0)
+           py::arg("cpus") = std::vector<int>{}, py::arg("spin_us") = 0,
+           py::arg("gzip_gpu") = -1, py::arg("gzip_batch_us") = 200)
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

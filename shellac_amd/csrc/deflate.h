@@ -20,10 +20,17 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "backend.h"
+
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 namespace shellac {
@@ -67,6 +74,39 @@ class GpuGzip {
   uint32_t *h_len_ = nullptr, *d_len_ = nullptr;
   size_t h_in_cap_ = 0, d_in_cap_ = 0, h_out_cap_ = 0, d_out_cap_ = 0, h_tab_cap_ = 0,
          d_tab_cap_ = 0, h_len_cap_ = 0, d_len_cap_ = 0;
+};
+
+// Asynchronous front end of GpuGzip for the proxy's miss path: reactor threads submit
+// bodies and get a completion; one service thread per GPU collects the submissions of a
+// short window (`batch_us`, or `max_batch` bodies) into ONE GpuGzip::compress call, then
+// runs each completion (which posts back to its reactor). On a GPU error the completion
+// gets ok = false and the original body back, so the caller can fall back to the CPU.
+class GzipService : public Compressor {
+ public:
+  GzipService(int device, int batch_us = 200, size_t max_batch = 4096);
+  ~GzipService() override;
+  void submit(std::string body, Done done) override;
+  void stats(StatList* out) override;
+  struct Stats {
+    uint64_t batches = 0, bodies = 0, in_bytes = 0, out_bytes = 0, errors = 0;
+  };
+  Stats totals();
+
+ private:
+  void loop();
+  struct Job {
+    std::string body;
+    Done done;
+  };
+  std::unique_ptr<GpuGzip> gz_;
+  int batch_us_;
+  size_t max_batch_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  bool stop_ = false;
+  Stats st_;
+  std::thread th_;
 };
 
 }  // namespace shellac

@@ -383,4 +383,91 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   stats_.in_bytes += total;
 }
 
+GzipService::GzipService(int device, int batch_us, size_t max_batch)
+    : gz_(new GpuGzip(device)), batch_us_(batch_us), max_batch_(std::max<size_t>(1, max_batch)) {
+  th_ = std::thread([this] { loop(); });
+}
+
+GzipService::~GzipService() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+void GzipService::submit(std::string body, Done done) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(Job{std::move(body), std::move(done)});
+  }
+  cv_.notify_one();
+}
+
+GzipService::Stats GzipService::totals() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+void GzipService::stats(StatList* out) {
+  const Stats t = totals();
+  out->emplace_back("batches", t.batches);
+  out->emplace_back("bodies", t.bodies);
+  out->emplace_back("in_bytes", t.in_bytes);
+  out->emplace_back("out_bytes", t.out_bytes);
+  out->emplace_back("errors", t.errors);
+}
+
+void GzipService::loop() {
+  std::vector<Job> batch;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty() && stop_) return;
+      // collect for up to batch_us after the first submission (or until max_batch)
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(batch_us_);
+      cv_.wait_until(lk, until, [&] { return stop_ || q_.size() >= max_batch_; });
+      const size_t take = std::min(q_.size(), max_batch_);
+      for (size_t i = 0; i < take; ++i) {
+        batch.push_back(std::move(q_.front()));
+        q_.pop_front();
+      }
+    }
+    std::vector<std::string_view> v;
+    v.reserve(batch.size());
+    uint64_t inb = 0;
+    for (const auto& j : batch) {
+      v.emplace_back(j.body);
+      inb += j.body.size();
+    }
+    std::vector<std::string> out;
+    bool ok = true;
+    try {
+      out = gz_->compress(v);
+    } catch (const std::exception&) {
+      ok = false;
+    }
+    uint64_t outb = 0;
+    for (size_t i = 0; i < batch.size(); ++i) {
+      if (ok) {
+        outb += out[i].size();
+        batch[i].done(true, std::move(out[i]));
+      } else {
+        batch[i].done(false, std::move(batch[i].body));
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.batches++;
+      st_.bodies += batch.size();
+      st_.in_bytes += inb;
+      st_.out_bytes += outb;
+      st_.errors += ok ? 0 : 1;
+    }
+    batch.clear();
+  }
+}
+
 }  // namespace shellac

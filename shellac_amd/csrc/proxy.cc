@@ -138,7 +138,7 @@ class Reactor : public Executor {
   std::atomic<uint64_t> requests{0}, hits{0}, misses{0}, upstream_reqs{0}, responses{0},
       bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
       cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0},
-      streamed{0}, stream_pauses{0};
+      streamed{0}, stream_pauses{0}, gzip_gpu_bodies{0};
   // event-loop health: the longest iteration (events handled between two epoll_waits)
   // and how many took over 10 ms — a reactor that stalls stops accepting connections
   std::atomic<uint64_t> loop_max_us{0}, loop_slow{0}, client_resets{0};
@@ -163,6 +163,7 @@ class Reactor : public Executor {
   void give_parser(std::unique_ptr<HttpParser> p);
   std::vector<std::unique_ptr<HttpParser>> parser_pool_;
   void on_upstream_response(Upstream* u);
+  void finish_response(HttpParser& r, const Pend& p);
   void rewrite_response_headers(HttpParser& r);
   void pause_input(Conn* c, bool paused);
   void rearm(Conn* c);
@@ -915,15 +916,50 @@ void Reactor::on_upstream_response(Upstream* u) {
   }
   rewrite_response_headers(r);
   const std::string* ce = r.header("content-encoding");
+  bool deferred = false;
   if (cfg_.compress && !ce && p.client_gzip && r.body().size() >= 256) {
     const std::string* ct = r.header("content-type");
     if (ct && (contains_ci(ct, "text/") || contains_ci(ct, "json") || contains_ci(ct, "javascript") ||
                contains_ci(ct, "xml"))) {
-      r.mutable_body() = gzip_compress(r.body(), 6);
-      r.set_header("content-encoding", "gzip");
-      r.set_header("vary", "Accept-Encoding");
+      if (px_->gzip_) {
+        // GPU: the body joins the current batch window; the response completes (cache
+        // store, client slot, collapsed waiters) on this reactor when the batch returns.
+        // Keep-alive bookkeeping of the upstream below does not wait for it.
+        std::shared_ptr<HttpParser> rs(std::move(rp));
+        auto ps = std::make_shared<Pend>(std::move(p));
+        std::string body = std::move(rs->mutable_body());
+        px_->gzip_->submit(std::move(body), [this, rs, ps](bool ok, std::string out) {
+          post([this, rs, ps, ok, out = std::move(out)]() mutable {
+            rs->mutable_body() = std::move(out);
+            if (ok) {
+              rs->set_header("content-encoding", "gzip");
+              rs->set_header("vary", "Accept-Encoding");
+              gzip_gpu_bodies++;
+            }
+            finish_response(*rs, *ps);
+          });
+        });
+        deferred = true;
+      } else {
+        r.mutable_body() = gzip_compress(r.body(), 6);
+        r.set_header("content-encoding", "gzip");
+        r.set_header("vary", "Accept-Encoding");
+      }
     }
   }
+  if (!deferred) finish_response(r, p);
+  if (!ka) {
+    server_nka_[u->server] = 1;
+    close_upstream(u);  // remaining pipelined requests are retried elsewhere
+    return;
+  }
+  server_nka_[u->server] = 0;
+  u->ka_timeout = kap.first;
+  u->ka_max = kap.second;
+}
+
+// Cache store, client slot and collapsed waiters of a complete upstream response.
+void Reactor::finish_response(HttpParser& r, const Pend& p) {
   Bytes obj;
   if (p.head) {
     const std::string* cl = r.header("content-length");
@@ -945,14 +981,6 @@ void Reactor::on_upstream_response(Upstream* u) {
     }
   }
   if (p.lookup) release_waiters(p.key, cached ? obj : nullptr);
-  if (!ka) {
-    server_nka_[u->server] = 1;
-    close_upstream(u);  // remaining pipelined requests are retried elsewhere
-    return;
-  }
-  server_nka_[u->server] = 0;
-  u->ka_timeout = kap.first;
-  u->ka_max = kap.second;
 }
 
 void Reactor::rewrite_response_headers(HttpParser& r) {
@@ -1258,6 +1286,15 @@ std::string Proxy::stats_json() {
     << "}"
     << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
     << total << "}";
+  if (gzip_) {
+    uint64_t gb = 0;
+    for (auto& r : reactors_) gb += r->gzip_gpu_bodies;
+    StatList gs;
+    gzip_->stats(&gs);
+    o << ",\"gzip_gpu\":{\"completed\":" << gb;
+    for (const auto& kv : gs) o << ",\"" << kv.first << "\":" << kv.second;
+    o << "}";
+  }
   o << ",\"health_checks\":" << health_checks_.load()
     << ",\"health_transitions\":" << health_transitions_.load() << ",\"upstreams_up\":[";
   const double tn = now_s();

@@ -43,6 +43,11 @@ struct ProxyConfig {
   int spin_us = 0;
   uint32_t ttl = 170;                 // -t (Server.py:514)
   bool compress = false;              // -z: gzip uncompressed text before caching
+  // >= 0: that GPU does the -z compression, batched across reactors (deflate.h
+  // GzipService, one window of gzip_batch_us; the binding installs it with
+  // Proxy::set_compressor); the response completes when it returns
+  int gzip_gpu = -1;
+  int gzip_batch_us = 200;
   bool cache_enabled = true;
   std::string policy = "rfc";         // "rfc" | "reference" (cache every response)
   bool kill_switch = true;            // GET /kill stops the proxy (Server.py:329-331)
@@ -88,6 +93,8 @@ class Proxy {
   std::string stats_json();
   const ProxyConfig& config() const { return cfg_; }
   CacheBackend* backend() { return backend_.get(); }
+  // -z compression off the reactor threads (before start(); null = zlib inline)
+  void set_compressor(std::shared_ptr<Compressor> c) { gzip_ = std::move(c); }
 
   // upstream health (shared by all reactors): passive (failed connects) and active
   bool upstream_up(int idx, double now) const;
@@ -101,6 +108,9 @@ class Proxy {
   std::shared_ptr<CacheBackend> backend_;
   std::vector<std::unique_ptr<Reactor>> reactors_;
   std::vector<std::thread> threads_;
+  // declared after reactors_: released before them (a GzipService joins its thread
+  // then), so a late completion still posts into a live reactor
+  std::shared_ptr<Compressor> gzip_;
   std::atomic<bool> running_{false};
   uint16_t port_ = 0;
   std::unique_ptr<std::atomic<double>[]> up_down_until_;

@@ -123,7 +123,8 @@ class Server:
                  stream_bytes: int = 1 << 20, stream_high_water: int = 8 << 20,
                  health_path: str = "", health_interval_ms: int = 1000,
                  health_timeout_ms: int = 500, health_fails: int = 2,
-                 cpus: Sequence[int] = (), spin_us: int = 0, **backend_opts):
+                 cpus: Sequence[int] = (), spin_us: int = 0, gzip_gpu: int = -1,
+                 gzip_batch_us: int = 200, **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
         self._backend = backend
@@ -137,7 +138,8 @@ class Server:
             decode_gzip=decode_gzip, stream_bytes=stream_bytes,
             stream_high_water=stream_high_water, health_path=health_path,
             health_interval_ms=health_interval_ms, health_timeout_ms=health_timeout_ms,
-            health_fails=health_fails, cpus=[int(c) for c in cpus], spin_us=int(spin_us))
+            health_fails=health_fails, cpus=[int(c) for c in cpus], spin_us=int(spin_us),
+            gzip_gpu=int(gzip_gpu), gzip_batch_us=int(gzip_batch_us))
         self._started = False
 
     @property
@@ -190,6 +192,11 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("-p", "--port", type=int, default=8080, help="Port to listen for connections on.")
     p.add_argument("-t", "--ttl", type=int, default=170, help="Lifetime of cached objects.")
     p.add_argument("-z", "--compress", action="store_true", help="Compress cached objects.")
+    p.add_argument("--gzip-gpu", type=int, default=-1, metavar="GPU",
+                   help="with -z: compress on this GPU, batched across reactor threads "
+                        "(ops/gzip.py; default: zlib on the reactor threads)")
+    p.add_argument("--gzip-batch-us", type=int, default=200,
+                   help="collection window of one GPU gzip batch")
     # beyond the reference
     p.add_argument("--cache", choices=["memcached", "dram", "hbm", "none"], default=None,
                    help="cache backend (default: memcached if -c is given, else dram)")
@@ -262,6 +269,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  stream_bytes=args.stream_bytes, health_path=args.health_check,
                  health_interval_ms=args.health_interval_ms, health_fails=args.health_fails,
                  cpus=parse_cpus(args.cpus), spin_us=args.spin_us,
+                 gzip_gpu=args.gzip_gpu, gzip_batch_us=args.gzip_batch_us,
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,

@@ -71,3 +71,35 @@ def test_large_batch_many_blocks(gz):
     bodies = [_html(rng, rng.randrange(1, 200000)) for _ in range(300)]
     out = gz.compress(bodies)
     assert all(zlib.decompress(o, 31) == b for b, o in zip(bodies, out))
+
+
+def test_proxy_compresses_misses_on_the_gpu(cuda_dev):
+    """proxy -z --gzip-gpu 0: identity text responses of the miss path are gzipped by the
+    GPU service in batches across reactor threads; pipelined order, cache fills and hits
+    behave as with zlib on the reactor."""
+    import json
+
+    from shellac_amd.server.proxy import Server
+    from shellac_amd.utils.httpclient import HttpClient
+    from shellac_amd.utils.origin import Origin
+
+    o = Origin(body_bytes=6000).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend_kind="dram", dram_mb=64,
+                    compress=True, gzip_gpu=cuda_dev.index or 0, threads=2).start() as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/zgpu/{i}.html" for i in range(24)]  # (the origin itself gzips /gz*)
+            rs = c.pipeline(paths, headers={"Accept-Encoding": "gzip"})
+            for p, r in zip(paths, rs):
+                assert r.headers().get("content-encoding") == "gzip", p
+                assert r.body().read().startswith(f"<html>{p} #1 ".encode()), p
+            rs = c.pipeline(paths[:5], headers={"Accept-Encoding": "gzip"})  # cache hits
+            for p, r in zip(paths, rs):
+                assert r.body().read().startswith(f"<html>{p} #1 ".encode()), p
+            st = px.stats()
+            assert st["gzip_gpu"]["completed"] == len(paths) == st["gzip_gpu"]["bodies"] and st["gzip_gpu"]["errors"] == 0
+            assert st["gzip_gpu"]["out_bytes"] < st["gzip_gpu"]["in_bytes"]
+            assert all(o.hits[p] == 1 for p in paths)
+            json.dumps(st)
+    finally:
+        o.stop()

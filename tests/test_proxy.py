@@ -432,3 +432,18 @@ def test_active_health_checks_take_sick_upstream_out_of_rotation():
     finally:
         a.stop()
         b.stop()
+
+
+def test_compress_identity_text_on_cpu(origin):
+    """-z: an identity text body is gzipped (zlib on the reactor) before it is cached and
+    served to clients that accept gzip; a client without Accept-Encoding gets identity."""
+    with make_proxy([origin.port], compress=True) as px:
+        c = HttpClient(port=px.port)
+        r = c.get("/zpage.html", headers={"Accept-Encoding": "gzip"})
+        assert r.headers().get("content-encoding") == "gzip"
+        assert b"<html>/zpage.html #1 " in r.body().read()
+        r = c.get("/zpage.html", headers={"Accept-Encoding": "gzip"})  # cache hit
+        assert b"<html>/zpage.html #1 " in r.body().read()
+        r = c.get("/plain.html")
+        assert r.headers().get("content-encoding") is None
+        assert "gzip_gpu" not in px.stats()
