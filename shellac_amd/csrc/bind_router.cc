@@ -82,6 +82,11 @@ void bind_router(py::module_& m) {
          py::arg("replica").none(true), py::arg("now"), py::arg("out_size"), py::arg("out_off"),
          py::arg("stream"))
       .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
+      .def("gather_local", [](RoutedStep& r, uintptr_t data, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        r.gather_local(P<uint8_t>(data), S(s));
+      })
+      .def("join_local", [](RoutedStep& r, uintptr_t s) { r.join_local(S(s)); })
       .def("set_defer_join", &RoutedStep::set_defer_join)
       .def_property_readonly("sets_pending", &RoutedStep::sets_pending)
       .def_property_readonly("mg", &RoutedStep::mg)

@@ -99,6 +99,12 @@ class RoutedStep {
   // and the next owner() joins before it touches the main shard, so the caller must
   // keep `recv` alive until then and call join_sets() before any other use of the shard.
   void join_sets(hipStream_t s);
+  // Early local gather (after read_counts): the replica hits' records go into
+  // data[0, local_bytes) on a third stream while the request exchange, owner lookup and
+  // host sync 2 proceed; finish() (or join_local) makes `s` wait for it. `data` must
+  // stay allocated until then.
+  void gather_local(uint8_t* data, hipStream_t s);
+  void join_local(hipStream_t s);
   void set_defer_join(bool on) { defer_join_ = on; }
   bool sets_pending() const { return sets_pending_; }
 
@@ -135,6 +141,10 @@ class RoutedStep {
   // behind a deferred SET chain.
   hipStream_t store_side_ = nullptr;
   hipEvent_t ev_sfork_ = nullptr;
+  hipStream_t local_side_ = nullptr;  // early replica gather (gather_local)
+  hipEvent_t ev_lfork_ = nullptr, ev_ljoin_ = nullptr;
+  bool local_pending_ = false, local_done_ = false;
+  HbmCache* replica_ = nullptr;
   bool defer_join_ = true, sets_pending_ = false;
   // per-step state
   int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;

@@ -618,6 +618,9 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   RT_OK(hipStreamCreateWithFlags(&store_side_, hipStreamNonBlocking));
   RT_OK(hipEventCreateWithFlags(&ev_sfork_, hipEventDisableTiming));
+  RT_OK(hipStreamCreateWithFlags(&local_side_, hipStreamNonBlocking));
+  RT_OK(hipEventCreateWithFlags(&ev_lfork_, hipEventDisableTiming));
+  RT_OK(hipEventCreateWithFlags(&ev_ljoin_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_fill_, hipEventDisableTiming));
   RT_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
@@ -634,8 +637,11 @@ RoutedStep::~RoutedStep() {
   (void)hipEventDestroy(ev_join_);
   (void)hipEventDestroy(ev_pjoin_);
   (void)hipEventDestroy(ev_sfork_);
+  (void)hipEventDestroy(ev_lfork_);
+  (void)hipEventDestroy(ev_ljoin_);
   (void)hipStreamDestroy(side_);
   (void)hipStreamDestroy(store_side_);
+  (void)hipStreamDestroy(local_side_);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
@@ -677,6 +683,8 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   n_ = n;
   values_ = svalues;
   have_replica_ = replica != nullptr;
+  replica_ = replica;
+  local_done_ = false;
   table_ = table;
   int64_t* extras = table + 6 * W;  // [table | rtable | extras]: one D2H in read_counts
   first_ = nullptr;
@@ -852,6 +860,22 @@ void RoutedStep::fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* s
   sets_pending_ = true;
 }
 
+void RoutedStep::gather_local(uint8_t* data, hipStream_t s) {
+  if (!(have_replica_ && replica_ && n_local_ > 0 && local_bytes_ > 0)) return;
+  RT_OK(hipEventRecord(ev_lfork_, s));
+  RT_OK(hipStreamWaitEvent(local_side_, ev_lfork_, 0));
+  replica_->gather(rl_loc_, rl_off_, n_, data, local_side_);
+  RT_OK(hipEventRecord(ev_ljoin_, local_side_));
+  local_pending_ = true;
+  local_done_ = true;
+}
+
+void RoutedStep::join_local(hipStream_t s) {
+  if (!local_pending_) return;
+  RT_OK(hipStreamWaitEvent(s, ev_ljoin_, 0));
+  local_pending_ = false;
+}
+
 void RoutedStep::join_sets(hipStream_t s) {
   if (!sets_pending_) return;
   RT_OK(hipStreamWaitEvent(s, ev_join_, 0));
@@ -878,7 +902,8 @@ void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, 
     ex = buf<uint32_t>(kEx, ms);
     roff = buf<uint64_t>(kRoff, ms);
   }
-  if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
+  if (local_done_) join_local(s);  // gathered early (gather_local) on the local stream
+  else if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
   // k_rs_fill reads rtable_, which the next step's count exchange overwrites: later work
   // on `s` (and the collectives ordered after it) waits for the fill
   if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_fill_, 0));
