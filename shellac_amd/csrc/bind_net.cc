@@ -317,8 +317,9 @@ void bind_net(py::module_& m) {
 
   py::class_<NativeOrigin>(m, "NativeOrigin")
       .def(py::init([](uint16_t port, int threads, int body_bytes, int gzip_level,
-                       const std::string& host, bool random_body) {
+                       const std::string& host, bool random_body, bool text_body) {
              OriginConfig c;
+             c.text_body = text_body;
              c.host = host;
              c.port = port;
              c.threads = threads;
@@ -329,7 +330,7 @@ void bind_net(py::module_& m) {
            }),
            py::arg("port") = 0, py::arg("threads") = 2, py::arg("body_bytes") = 1024,
            py::arg("gzip_level") = 1, py::arg("host") = "127.0.0.1",
-           py::arg("random_body") = false)
+           py::arg("random_body") = false, py::arg("text_body") = false)
       .def("start", &NativeOrigin::start)
       .def("stop", &NativeOrigin::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &NativeOrigin::port)

@@ -83,7 +83,9 @@ class GpuGzip {
 // gets ok = false and the original body back, so the caller can fall back to the CPU.
 class GzipService : public Compressor {
  public:
-  GzipService(int device, int batch_us = 200, size_t max_batch = 4096);
+  // `workers` threads, each with its own engine and stream, take batches in turn, so one
+  // batch's host packing and assembly overlap another's GPU work
+  GzipService(int device, int batch_us = 200, size_t max_batch = 4096, int workers = 2);
   ~GzipService() override;
   void submit(std::string body, Done done) override;
   void stats(StatList* out) override;
@@ -93,12 +95,12 @@ class GzipService : public Compressor {
   Stats totals();
 
  private:
-  void loop();
+  void loop(GpuGzip* gz);
   struct Job {
     std::string body;
     Done done;
   };
-  std::unique_ptr<GpuGzip> gz_;
+  std::vector<std::unique_ptr<GpuGzip>> gz_;
   int batch_us_;
   size_t max_batch_;
   std::mutex mu_;
@@ -106,7 +108,7 @@ class GzipService : public Compressor {
   std::deque<Job> q_;
   bool stop_ = false;
   Stats st_;
-  std::thread th_;
+  std::vector<std::thread> th_;
 };
 
 }  // namespace shellac

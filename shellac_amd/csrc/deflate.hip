@@ -383,9 +383,13 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   stats_.in_bytes += total;
 }
 
-GzipService::GzipService(int device, int batch_us, size_t max_batch)
-    : gz_(new GpuGzip(device)), batch_us_(batch_us), max_batch_(std::max<size_t>(1, max_batch)) {
-  th_ = std::thread([this] { loop(); });
+GzipService::GzipService(int device, int batch_us, size_t max_batch, int workers)
+    : batch_us_(batch_us), max_batch_(std::max<size_t>(1, max_batch)) {
+  for (int i = 0; i < std::max(1, workers); ++i) gz_.emplace_back(new GpuGzip(device));
+  for (auto& g : gz_) {
+    GpuGzip* e = g.get();
+    th_.emplace_back([this, e] { loop(e); });
+  }
 }
 
 GzipService::~GzipService() {
@@ -394,7 +398,8 @@ GzipService::~GzipService() {
     stop_ = true;
   }
   cv_.notify_all();
-  if (th_.joinable()) th_.join();
+  for (auto& t : th_)
+    if (t.joinable()) t.join();
 }
 
 void GzipService::submit(std::string body, Done done) {
@@ -419,7 +424,7 @@ void GzipService::stats(StatList* out) {
   out->emplace_back("errors", t.errors);
 }
 
-void GzipService::loop() {
+void GzipService::loop(GpuGzip* gz) {
   std::vector<Job> batch;
   for (;;) {
     {
@@ -435,6 +440,7 @@ void GzipService::loop() {
         q_.pop_front();
       }
     }
+    if (batch.empty()) continue;  // another worker took this window's bodies
     std::vector<std::string_view> v;
     v.reserve(batch.size());
     uint64_t inb = 0;
@@ -445,7 +451,7 @@ void GzipService::loop() {
     std::vector<std::string> out;
     bool ok = true;
     try {
-      out = gz_->compress(v);
+      out = gz->compress(v);
     } catch (const std::exception&) {
       ok = false;
     }

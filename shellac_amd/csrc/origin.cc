@@ -167,6 +167,24 @@ void NativeOrigin::loop(int lfd) {
           x ^= x << 17;
           std::memcpy(&body[k], &x, std::min<size_t>(8, body.size() - k));
         }
+      } else if (cfg_.text_body) {
+        static const char* kWords[] = {"<div class=\"item\">", "</div>", "<span>", "</span>",
+                                       "<a href=\"/static/obj/", "\">", "</a>", "<li>", "</li>",
+                                       "cache", "proxy", "memory", "the", "of", "and", "GPU",
+                                       "request", "\n", "  ", "<p>", "</p>", "object"};
+        constexpr int kNw = (int)(sizeof(kWords) / sizeof(kWords[0]));
+        uint64_t x = 0xcbf29ce484222325ull;
+        for (unsigned char ch : path) x = (x ^ ch) * 0x100000001b3ull;
+        body = "<html>" + path + " #1 ";
+        while ((int)body.size() < cfg_.body_bytes) {
+          x ^= x << 13;
+          x ^= x >> 7;
+          x ^= x << 17;
+          body += kWords[x % kNw];
+          if ((x >> 20) % 7 == 0) body += std::to_string((x >> 32) % 10000000);
+          body += ' ';
+        }
+        body.resize((size_t)cfg_.body_bytes);
       } else {
         body = "<html>" + path + " #1 " + filler + "</html>\n";
       }

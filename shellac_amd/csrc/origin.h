@@ -21,6 +21,9 @@ struct OriginConfig {
   // incompressible bodies: body_bytes of pseudo-random bytes seeded by the path (the same
   // object always has the same body), so cached objects are body_bytes on the wire
   bool random_body = false;
+  // compressible text bodies: body_bytes of HTML-like markup built from a small word list
+  // by a generator seeded with the path (zlib -6 reaches ~0.3 on it, like real pages)
+  bool text_body = false;
 };
 
 class NativeOrigin {

@@ -123,12 +123,14 @@ class NativeOrigin:
     miss-path RPS measures the proxy, not Python's ``http.server``."""
 
     def __init__(self, port: int = 0, body_bytes: int = 1024, threads: int = 2,
-                 gzip_level: int = 1, random_body: bool = False):
+                 gzip_level: int = 1, random_body: bool = False, text_body: bool = False):
         from .._native import core
 
-        # random_body: incompressible per-path bodies of exactly body_bytes
+        # random_body: incompressible per-path bodies of exactly body_bytes;
+        # text_body: compressible HTML-like bodies of exactly body_bytes
         self._o = core().NativeOrigin(port=port, threads=threads, body_bytes=body_bytes,
-                                      gzip_level=gzip_level, random_body=random_body)
+                                      gzip_level=gzip_level, random_body=random_body,
+                                      text_body=text_body)
         self.port = self._o.port
 
     @property
@@ -153,13 +155,14 @@ def serve_native_origin(argv=None) -> int:
     ap.add_argument("--body", type=int, default=4096)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--random-body", action="store_true")
+    ap.add_argument("--text-body", action="store_true")
     ap.add_argument("--gzip-level", type=int, default=1)
     ap.add_argument("--cpus", default="", help="run on these CPUs only ('0-3,8')")
     a = ap.parse_args(argv)
     from .cpus import parse_cpus, pin_process
     pin_process(parse_cpus(a.cpus))
     o = NativeOrigin(body_bytes=a.body, threads=a.threads, gzip_level=a.gzip_level,
-                     random_body=a.random_body).start()
+                     random_body=a.random_body, text_body=a.text_body).start()
     print(f"port {o.port}", flush=True)
     try:
         sys.stdin.read()
