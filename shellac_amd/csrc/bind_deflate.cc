@@ -6,6 +6,7 @@
 
 #include "bind_parts.h"
 #include "deflate.h"
+#include "huffman.h"
 
 namespace py = pybind11;
 using namespace shellac;
@@ -32,6 +33,16 @@ py::list to_list(const std::vector<std::string>& out) {
 
 void bind_deflate(py::module_& m) {
   m.attr("DEFLATE_BLOCK") = kDeflateBlock;
+  // host-side DEFLATE planning, exposed for CPU tests (huffman.h)
+  m.def("huffman_lengths", [](const std::vector<uint32_t>& freq, int max_len) {
+    std::vector<uint8_t> len(freq.size());
+    huffman_lengths(freq.data(), (int)freq.size(), max_len, len.data());
+    return std::vector<int>(len.begin(), len.end());
+  });
+  m.def("deflate_tokens_cpu", [](const std::vector<uint32_t>& tokens, const py::bytes& data,
+                                 bool fin) {
+    return py::bytes(deflate_tokens_cpu(tokens, std::string(data), fin));
+  });
   py::class_<GzipStats>(m, "GzipStats")
       .def_readonly("inputs", &GzipStats::inputs)
       .def_readonly("blocks", &GzipStats::blocks)

@@ -6,16 +6,21 @@
 // the CPU. This engine moves that compression to the GPU for whole batches of bodies
 // ("batch gzip on GPU for the miss path").
 //
-// Design (deflate.hip): every input is cut into 32 KiB blocks and every block is one
-// workgroup of ONE wave. The wave keeps the block and a 4096-entry hash head table in
-// LDS and parses greedily: at each position the 64 lanes compare the candidate match
-// 64 bytes at a time (one ballot finds the first mismatch), the positions a match covers
-// are hashed in parallel, and the codes go out through a wave-uniform 64-bit bit buffer
-// as fixed-Huffman symbols (BTYPE 01). Blocks are independent (the window never crosses
-// a block), so a non-final block ends with an empty stored block (the zlib sync-flush
-// marker 00 00 FF FF) and the compressed blocks of one input concatenate byte-wise. A
-// block that would not shrink is emitted as a stored block. CRC-32 and ISIZE are
-// computed on the host (zlib crc32 runs at GB/s; the parse is the expensive part).
+// Design (deflate.hip, two passes around a host planning step): every input is cut into
+// 32 KiB blocks and every block is one workgroup of ONE wave.
+//  1. k_lz77: the wave keeps the block and a 4096-entry hash head table in LDS and parses
+//     greedily: at each position the 64 lanes compare the candidate match 64 bytes at a
+//     time (one ballot finds the first mismatch) and hash the positions a match covers
+//     in parallel. It writes the block's tokens, its literal/length + distance symbol
+//     histogram and its CRC-32 register (lane slices combined by GF(2) multiplies).
+//  2. host (huffman.cc, a few threads): per block, the cheapest of stored / fixed
+//     Huffman / dynamic Huffman by exact bit count, length-limited canonical codes and
+//     the dynamic header.
+//  3. k_emit: the codes in LDS; each chunk of 64 tokens is placed by a wave prefix sum of
+//     their bit lengths and OR-ed into an LDS bit buffer, written out whole.
+// Blocks are independent (the window never crosses a block), so a non-final block ends
+// with an empty stored block (the zlib sync-flush marker 00 00 FF FF) and the blocks of
+// one input concatenate byte-wise. The host folds the blocks' CRC registers per input.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -72,6 +77,10 @@ class GpuGzip {
   uint8_t *h_in_ = nullptr, *d_in_ = nullptr, *h_out_ = nullptr, *d_out_ = nullptr;
   uint64_t *h_tab_ = nullptr, *d_tab_ = nullptr;
   uint32_t *h_len_ = nullptr, *d_len_ = nullptr;
+  // two-pass encoding: tokens (device), pass-1 results, per-block plans
+  uint32_t *d_tok_ = nullptr, *h_res_ = nullptr, *d_res_ = nullptr, *h_plan_ = nullptr,
+           *d_plan_ = nullptr;
+  size_t d_tok_cap_ = 0, h_res_cap_ = 0, d_res_cap_ = 0, h_plan_cap_ = 0, d_plan_cap_ = 0;
   size_t h_in_cap_ = 0, d_in_cap_ = 0, h_out_cap_ = 0, d_out_cap_ = 0, h_tab_cap_ = 0,
          d_tab_cap_ = 0, h_len_cap_ = 0, d_len_cap_ = 0;
 };

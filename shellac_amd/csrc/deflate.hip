@@ -4,11 +4,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <stdexcept>
 
 #include "common.h"
 #include "deflate.h"
+#include "huffman.h"
 
 #define GZ_OK(expr)                                                                       \
   do {                                                                                    \
@@ -23,79 +25,11 @@ namespace {
 constexpr int kHashBits = 12;
 constexpr int kHashSize = 1 << kHashBits;
 constexpr int kMaxMatch = 258;
+// plan record per block: mode, header bits, total bytes, codes, header bytes (<= 640)
+constexpr int kPlanWords = 3 + kHistSyms + 160;
 
 __device__ __forceinline__ uint32_t rev(uint32_t code, int len) {
   return __builtin_bitreverse32(code) >> (32 - len);
-}
-
-// Wave-uniform LSB-first bit writer into a 4-byte aligned global buffer. Every lane holds
-// the same state; lane 0 stores.
-struct Bits {
-  uint64_t acc = 0;
-  int nb = 0;
-  uint32_t words = 0;
-  uint32_t* out;
-  uint32_t cap_words;
-  bool over = false;
-  __device__ void put(uint32_t v, int n) {  // n <= 32, nb < 32 on entry
-    acc |= (uint64_t)v << nb;
-    nb += n;
-    if (nb >= 32) {
-      if (words < cap_words) {
-        if (__lane_id() == 0) out[words] = (uint32_t)acc;
-      } else {
-        over = true;
-      }
-      ++words;
-      acc >>= 32;
-      nb -= 32;
-    }
-  }
-};
-
-__device__ __forceinline__ void put_literal(Bits& b, uint32_t lit) {
-  if (lit < 144) b.put(rev(0x30 + lit, 8), 8);
-  else b.put(rev(0x190 + (lit - 144), 9), 9);
-}
-
-// Length (3..258) and distance (1..32768) codes of RFC 1951 §3.2.5 by arithmetic: the
-// code tables are "4 codes per extra bit" (lengths) and "2 codes per extra bit"
-// (distances) above a few exact codes, so the code index, base and extra-bit count follow
-// from the position of the top set bit — no table walk per match.
-__device__ __forceinline__ void put_match(Bits& b, int len, int dist) {
-  int i, le, lbase;
-  if (len < 11) {
-    i = len - 3; le = 0; lbase = len;
-  } else if (len == 258) {
-    i = 28; le = 0; lbase = 258;
-  } else {
-    const int L = len - 3;
-    le = 29 - __clz(L);  // floor(log2 L) - 2
-    const int q = (L >> le) & 3;
-    i = 4 * le + 4 + q;
-    lbase = 3 + ((4 + q) << le);
-  }
-  const int sym = 257 + i;
-  uint32_t code, clen;
-  if (sym < 280) {
-    code = rev(sym - 256, 7);
-    clen = 7;
-  } else {
-    code = rev(0xC0 + (sym - 280), 8);
-    clen = 8;
-  }
-  b.put(code | ((uint32_t)(len - lbase) << clen), clen + le);
-  const int D = dist - 1;
-  int j, de, dbase;
-  if (D < 4) {
-    j = D; de = 0; dbase = dist;
-  } else {
-    de = 30 - __clz(D);  // floor(log2 D) - 1
-    const int q = (D >> de) & 1;
-    j = 2 * de + 2 + q;
-    dbase = 1 + ((2 + q) << de);
-  }
-  b.put(rev(j, 5) | ((uint32_t)(dist - dbase) << 5), 5 + de);
 }
 
 // x^(8n) mod P and (a * b) mod P over GF(2) for the reflected CRC-32 polynomial: the
@@ -129,21 +63,50 @@ __device__ __forceinline__ uint32_t hash4(const uint8_t* s, int p) {
   return (w * 2654435761u) >> (32 - kHashBits);
 }
 
-// One wave per block. tab[b] = src offset | (len | final << 31) << 40 ... kept as two
-// words for clarity: tab[2b] = src offset, tab[2b+1] = len | final << 32.
-__global__ __launch_bounds__(64) void k_deflate(const uint8_t* __restrict__ src,
-                                                const uint64_t* __restrict__ tab, int64_t nblk,
-                                                uint8_t* __restrict__ dst,
-                                                uint32_t* __restrict__ out_len,
-                                                uint32_t* __restrict__ out_crc) {
+// Symbol of a match length (257..285) / distance (0..29) and its extra bits, by the
+// position of the top set bit (RFC 1951 §3.2.5) — no table walk.
+__device__ __forceinline__ void len_sym(int len, int* sym, int* nb, uint32_t* val) {
+  if (len < 11) {
+    *sym = 254 + len; *nb = 0; *val = 0;
+  } else if (len == 258) {
+    *sym = 285; *nb = 0; *val = 0;
+  } else {
+    const int L = len - 3;
+    const int e = 29 - __clz(L);  // floor(log2 L) - 2
+    const int q = (L >> e) & 3;
+    *sym = 257 + 4 * e + 4 + q; *nb = e; *val = (uint32_t)(len - 3 - ((4 + q) << e));
+  }
+}
+__device__ __forceinline__ void dist_sym(int dist, int* sym, int* nb, uint32_t* val) {
+  const int D = dist - 1;
+  if (D < 4) {
+    *sym = D; *nb = 0; *val = 0;
+  } else {
+    const int e = 30 - __clz(D);  // floor(log2 D) - 1
+    const int q = (D >> e) & 1;
+    *sym = 2 * e + 2 + q; *nb = e; *val = (uint32_t)(D - ((2 + q) << e));
+  }
+}
+
+// Pass 1: one wave per block. The block and a 4096-entry hash head table live in LDS;
+// the wave parses greedily (the 64 lanes compare a candidate 64 bytes per ballot and hash
+// the positions a match covers in parallel) and writes tokens (huffman.h) plus the
+// block's literal/length and distance histogram, and the block's CRC register.
+// tab[2b] = src offset, tab[2b+1] = len | final << 32.
+__global__ __launch_bounds__(64) void k_lz77(const uint8_t* __restrict__ src,
+                                             const uint64_t* __restrict__ tab, int64_t nblk,
+                                             uint32_t* __restrict__ tok,
+                                             uint32_t* __restrict__ hist,
+                                             uint32_t* __restrict__ ntok,
+                                             uint32_t* __restrict__ out_crc) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kDeflateBlock + 16];
   __shared__ uint32_t s_head[kHashSize];
+  __shared__ uint32_t s_hist[kHistSyms];
   const int64_t b = blockIdx.x;
   if (b >= nblk) return;
   const int lane = threadIdx.x;
   const uint64_t off = tab[2 * b];
   const int n = (int)(tab[2 * b + 1] & 0xFFFFFFFFull);
-  const bool fin = (tab[2 * b + 1] >> 32) != 0;
   // blocks start 16-B aligned in the packed input (the host pads every input)
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* in4 = reinterpret_cast<const u32x4*>(src + off);
@@ -151,6 +114,7 @@ __global__ __launch_bounds__(64) void k_deflate(const uint8_t* __restrict__ src,
   const int n16 = (n + 15) / 16;
   for (int i = lane; i < n16; i += 64) s4[i] = in4[i];
   for (int i = n + lane; i < n16 * 16 + 16; i += 64) s_in[i] = 0;  // zero tail (hash reads)
+  for (int i = lane; i < kHistSyms; i += 64) s_hist[i] = 0;
   // CRC table in the head table's space (it is cleared after the CRC pass)
   for (int i = lane; i < 256; i += 64) {
     uint32_t c = (uint32_t)i;
@@ -174,15 +138,10 @@ __global__ __launch_bounds__(64) void k_deflate(const uint8_t* __restrict__ src,
   for (int i = lane; i < kHashSize; i += 64) s_head[i] = 0;
   __syncthreads();
 
-  uint8_t* out = dst + b * (int64_t)kDeflateStride;
-  Bits bw;
-  bw.out = reinterpret_cast<uint32_t*>(out);
-  // a compressed block larger than its stored form (5 + n bytes) is abandoned
-  bw.cap_words = (uint32_t)((n + 5) / 4);
-  bw.put(fin ? 1u : 0u, 1);
-  bw.put(1u, 2);  // BTYPE 01: fixed Huffman
+  uint32_t* t = tok + b * (int64_t)kDeflateBlock;
+  int nt = 0;
   int pos = 0;
-  while (pos < n && !bw.over) {
+  while (pos < n) {
     int len = 0, dist = 0;
     if (pos + 3 < n) {
       const uint32_t h = hash4(s_in, pos);
@@ -210,7 +169,15 @@ __global__ __launch_bounds__(64) void k_deflate(const uint8_t* __restrict__ src,
       }
     }
     if (len >= 3) {
-      put_match(bw, len, dist);
+      if (lane == 0) {
+        int ls, lb, ds, db;
+        uint32_t lv, dv;
+        len_sym(len, &ls, &lb, &lv);
+        dist_sym(dist, &ds, &db, &dv);
+        t[nt] = kTokMatch | ((uint32_t)len << 16) | (uint32_t)(dist - 1);
+        s_hist[ls]++;
+        s_hist[kLitLenSyms + ds]++;
+      }
       // hash the positions the match covers (latest position wins)
       for (int q = 1 + lane; q < len; q += 64) {
         const int p = pos + q;
@@ -218,34 +185,125 @@ __global__ __launch_bounds__(64) void k_deflate(const uint8_t* __restrict__ src,
       }
       pos += len;
     } else {
-      put_literal(bw, s_in[pos]);
+      if (lane == 0) {
+        const uint32_t lit = s_in[pos];
+        t[nt] = lit;
+        s_hist[lit]++;
+      }
       pos += 1;
     }
+    ++nt;
     __builtin_amdgcn_wave_barrier();  // head-table updates precede the next lookup
   }
-  if (!bw.over) {
-    bw.put(0u, 7);  // end of block (256)
-    if (!fin) bw.put(0u, 3);  // sync flush: empty stored block header (BFINAL 0, BTYPE 00)
-    // tail bytes of the bit buffer, then (non-final) LEN = 0, NLEN = 0xFFFF
-    const int tail = (bw.nb + 7) / 8;
-    const uint32_t total = bw.words * 4 + tail + (fin ? 0 : 4);
-    if (total <= (uint32_t)n + 5) {
-      if (lane < tail) out[bw.words * 4 + lane] = (uint8_t)(bw.acc >> (8 * lane));
-      if (!fin && lane < 4) out[bw.words * 4 + tail + lane] = lane < 2 ? 0x00 : 0xFF;
-      if (lane == 0) out_len[b] = total;
-      return;
+  __syncthreads();
+  for (int i = lane; i < kHistSyms; i += 64) hist[b * (int64_t)kHistSyms + i] = s_hist[i];
+  if (lane == 0) ntok[b] = (uint32_t)nt;
+}
+
+// OR `len` (<= 28) bits of v into the LDS bit buffer at bit `pos`.
+__device__ __forceinline__ void or_bits(uint32_t* w, uint32_t pos, uint32_t v, int len) {
+  if (len == 0) return;
+  const uint32_t k = pos >> 5, sh = pos & 31;
+  atomicOr(&w[k], v << sh);
+  if (sh + len > 32) atomicOr(&w[k + 1], v >> (32 - sh));
+}
+
+// Pass 2: one wave per block encodes its tokens with the host's plan (stored / fixed /
+// dynamic codes, huffman.cc). The codes sit in LDS; each chunk of 64 tokens is placed by
+// a wave prefix sum of the tokens' bit lengths and OR-ed into an LDS bit buffer, which is
+// then written out whole. A plan record: [mode, header bits, total bytes, codes (316),
+// header bytes].
+__global__ __launch_bounds__(64) void k_emit(const uint8_t* __restrict__ src,
+                                             const uint64_t* __restrict__ tab, int64_t nblk,
+                                             const uint32_t* __restrict__ tok,
+                                             const uint32_t* __restrict__ ntok,
+                                             const uint32_t* __restrict__ plans,
+                                             uint8_t* __restrict__ dst,
+                                             uint32_t* __restrict__ out_len) {
+  __shared__ uint32_t s_code[kHistSyms];
+  __shared__ uint32_t s_out[kDeflateStride / 4];
+  const int64_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const int lane = threadIdx.x;
+  const uint64_t off = tab[2 * b];
+  const int n = (int)(tab[2 * b + 1] & 0xFFFFFFFFull);
+  const bool fin = (tab[2 * b + 1] >> 32) != 0;
+  const uint32_t* pl = plans + b * (int64_t)kPlanWords;
+  const uint32_t mode = pl[0], hbits = pl[1], total = pl[2];
+  uint8_t* out = dst + b * (int64_t)kDeflateStride;
+  if (mode == 0) {  // stored: header byte (BFINAL, BTYPE 00, padding), LEN, NLEN, raw bytes
+    if (lane == 0) {
+      out[0] = fin ? 1 : 0;
+      out[1] = (uint8_t)(n & 0xFF);
+      out[2] = (uint8_t)(n >> 8);
+      out[3] = (uint8_t)(~n & 0xFF);
+      out[4] = (uint8_t)((~n >> 8) & 0xFF);
+      out_len[b] = (uint32_t)n + 5 | 0x80000000u;  // top bit: stored
     }
+    for (int i = lane; i < n; i += 64) out[5 + i] = src[off + i];
+    return;
   }
-  // stored block: header byte (BFINAL, BTYPE 00, padding), LEN, NLEN, the raw bytes
+  for (int i = lane; i < kHistSyms; i += 64) s_code[i] = pl[3 + i];
+  const int words = (int)((total + 3) / 4) + 1;
+  for (int i = lane; i < words; i += 64) s_out[i] = 0;
+  __syncthreads();
+  const uint8_t* hdr = reinterpret_cast<const uint8_t*>(pl + 3 + kHistSyms);
+  uint8_t* s_out8 = reinterpret_cast<uint8_t*>(s_out);
+  for (int i = lane; i < (int)((hbits + 7) / 8); i += 64) s_out8[i] = hdr[i];
+  __syncthreads();
+  uint32_t base = hbits;
+  const uint32_t* t = tok + b * (int64_t)kDeflateBlock;
+  const int nt = (int)ntok[b];
+  for (int c0 = 0; c0 < nt; c0 += 64) {
+    const int i = c0 + lane;
+    uint32_t av = 0, bv = 0;
+    int al = 0, bl = 0;
+    if (i < nt) {
+      const uint32_t x = t[i];
+      if (x & kTokMatch) {
+        int ls, lb, ds, db;
+        uint32_t lv, dv;
+        len_sym((int)((x >> 16) & 0x1FF), &ls, &lb, &lv);
+        dist_sym((int)(x & 0xFFFF) + 1, &ds, &db, &dv);
+        const uint32_t lc = s_code[ls], dc = s_code[kLitLenSyms + ds];
+        al = (int)(lc >> 16) + lb;
+        av = (lc & 0xFFFF) | (lv << (lc >> 16));
+        bl = (int)(dc >> 16) + db;
+        bv = (dc & 0xFFFF) | (dv << (dc >> 16));
+      } else {
+        const uint32_t lc = s_code[x & 0xFF];
+        al = (int)(lc >> 16);
+        av = lc & 0xFFFF;
+      }
+    }
+    // inclusive scan of the chunk's bit lengths
+    uint32_t inc = (uint32_t)(al + bl);
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= d) inc += o;
+    }
+    const uint32_t p0 = base + inc - (uint32_t)(al + bl);
+    or_bits(s_out, p0, av, al);
+    or_bits(s_out, p0 + al, bv, bl);
+    base += __shfl(inc, 63);
+  }
+  __syncthreads();
   if (lane == 0) {
-    out[0] = fin ? 1 : 0;
-    out[1] = (uint8_t)(n & 0xFF);
-    out[2] = (uint8_t)(n >> 8);
-    out[3] = (uint8_t)(~n & 0xFF);
-    out[4] = (uint8_t)((~n >> 8) & 0xFF);
-    out_len[b] = (uint32_t)n + 5 | 0x80000000u;  // top bit: stored
+    const uint32_t eob = s_code[256];
+    or_bits(s_out, base, eob & 0xFFFF, (int)(eob >> 16));
+    base += eob >> 16;
+    uint32_t bytes = (base + 7) / 8;
+    if (!fin) {  // sync flush: empty stored block (3 zero bits), pad, LEN 0, NLEN 0xFFFF
+      bytes = (base + 3 + 7) / 8;
+      s_out8[bytes + 2] = 0xFF;
+      s_out8[bytes + 3] = 0xFF;
+      bytes += 4;
+    }
+    out_len[b] = bytes;
   }
-  for (int i = lane; i < n; i += 64) out[5 + i] = s_in[i];
+  __syncthreads();
+  uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+  for (int i = lane; i < words; i += 64) o32[i] = s_out[i];
 }
 
 }  // namespace
@@ -258,9 +316,11 @@ GpuGzip::GpuGzip(int device) : device_(device) {
 GpuGzip::~GpuGzip() {
   (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(stream_);
-  for (void* p : {(void*)h_in_, (void*)h_out_, (void*)h_tab_, (void*)h_len_})
+  for (void* p : {(void*)h_in_, (void*)h_out_, (void*)h_tab_, (void*)h_len_, (void*)h_res_,
+                  (void*)h_plan_})
     if (p) (void)hipHostFree(p);
-  for (void* p : {(void*)d_in_, (void*)d_out_, (void*)d_tab_, (void*)d_len_})
+  for (void* p : {(void*)d_in_, (void*)d_out_, (void*)d_tab_, (void*)d_len_, (void*)d_res_,
+                  (void*)d_plan_, (void*)d_tok_})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(stream_);
 }
@@ -313,9 +373,21 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   uint8_t* din = grow(&d_in_, &d_in_cap_, packed + 16, false);
   uint64_t* htab = grow(&h_tab_, &h_tab_cap_, 2 * nblk, true);
   uint64_t* dtab = grow(&d_tab_, &d_tab_cap_, 2 * nblk, false);
-  // [compressed length per block | CRC register per block]: one D2H
-  uint32_t* hlen = grow(&h_len_, &h_len_cap_, 2 * nblk, true);
-  uint32_t* dlen = grow(&d_len_, &d_len_cap_, 2 * nblk, false);
+  // pass-1 results [histograms (316 per block) | token counts | CRC registers] and pass-2
+  // lengths: one D2H each
+  const size_t nres = nblk * (size_t)kHistSyms + 2 * nblk;
+  uint32_t* hres = grow(&h_res_, &h_res_cap_, nres, true);
+  uint32_t* dres = grow(&d_res_, &d_res_cap_, nres, false);
+  uint32_t* hlen = grow(&h_len_, &h_len_cap_, nblk, true);
+  uint32_t* dlen = grow(&d_len_, &d_len_cap_, nblk, false);
+  uint32_t* dtok = grow(&d_tok_, &d_tok_cap_, nblk * (size_t)kDeflateBlock, false);
+  uint32_t* hplan = grow(&h_plan_, &h_plan_cap_, nblk * (size_t)kPlanWords, true);
+  uint32_t* dplan = grow(&d_plan_, &d_plan_cap_, nblk * (size_t)kPlanWords, false);
+  uint32_t* dhist = dres;
+  uint32_t* dntok = dres + nblk * (size_t)kHistSyms;
+  uint32_t* dcrc = dntok + nblk;
+  const uint32_t* hhist = hres;
+  const uint32_t* hcrc = hres + nblk * (size_t)kHistSyms + nblk;
   uint8_t* dout = grow(&d_out_, &d_out_cap_, nblk * (size_t)kDeflateStride, false);
   uint8_t* hout = grow(&h_out_, &h_out_cap_, nblk * (size_t)kDeflateStride, true);
   using clk = std::chrono::steady_clock;
@@ -337,10 +409,42 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   const auto t1 = clk::now();
   GZ_OK(hipMemcpyAsync(din, hin, packed + 16, hipMemcpyHostToDevice, stream_));
   GZ_OK(hipMemcpyAsync(dtab, htab, 2 * nblk * sizeof(uint64_t), hipMemcpyHostToDevice, stream_));
-  hipLaunchKernelGGL(k_deflate, dim3((unsigned)nblk), dim3(64), 0, stream_, din, dtab,
-                     (int64_t)nblk, dout, dlen, dlen + nblk);
+  hipLaunchKernelGGL(k_lz77, dim3((unsigned)nblk), dim3(64), 0, stream_, din, dtab,
+                     (int64_t)nblk, dtok, dhist, dntok, dcrc);
   GZ_OK(hipGetLastError());
-  GZ_OK(hipMemcpyAsync(hlen, dlen, 2 * nblk * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  GZ_OK(hipMemcpyAsync(hres, dres, nres * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  GZ_OK(hipStreamSynchronize(stream_));
+  // plan every block (stored / fixed / dynamic codes and header) on a few host threads
+  {
+    const size_t nth = std::min<size_t>(std::max<size_t>(1, nblk / 64),
+                                        std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)));
+    auto work = [&](size_t lo, size_t hi) {
+      BlockPlan bp;
+      for (size_t bi = lo; bi < hi; ++bi) {
+        const uint64_t meta = htab[2 * bi + 1];
+        plan_block(hhist + bi * kHistSyms, (uint32_t)(meta & 0xFFFFFFFFu), (meta >> 32) != 0, &bp);
+        uint32_t* rec = hplan + bi * (size_t)kPlanWords;
+        rec[0] = (uint32_t)bp.mode;
+        rec[1] = bp.header_bits;
+        rec[2] = (uint32_t)bp.total_bytes;
+        std::memcpy(rec + 3, bp.codes, sizeof(bp.codes));
+        SH_CHECK(bp.header.size() <= 4 * (size_t)(kPlanWords - 3 - kHistSyms), "gzip header too long");
+        std::memset(rec + 3 + kHistSyms, 0, 4 * (size_t)(kPlanWords - 3 - kHistSyms));
+        std::memcpy(rec + 3 + kHistSyms, bp.header.data(), bp.header.size());
+      }
+    };
+    std::vector<std::thread> ths;
+    const size_t per = (nblk + nth - 1) / nth;
+    for (size_t ti = 1; ti < nth; ++ti)
+      ths.emplace_back(work, std::min(nblk, ti * per), std::min(nblk, (ti + 1) * per));
+    work(0, std::min(nblk, per));
+    for (auto& th : ths) th.join();
+  }
+  GZ_OK(hipMemcpyAsync(dplan, hplan, nblk * (size_t)kPlanWords * 4, hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(k_emit, dim3((unsigned)nblk), dim3(64), 0, stream_, din, dtab,
+                     (int64_t)nblk, dtok, dntok, dplan, dout, dlen);
+  GZ_OK(hipGetLastError());
+  GZ_OK(hipMemcpyAsync(hlen, dlen, nblk * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   GZ_OK(hipMemcpyAsync(hout, dout, nblk * (size_t)kDeflateStride, hipMemcpyDeviceToHost, stream_));
   GZ_OK(hipStreamSynchronize(stream_));
   const auto t2 = clk::now();
@@ -362,7 +466,7 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
       stats_.stored_blocks += l >> 31;
       r.append(reinterpret_cast<const char*>(hout + k * (size_t)kDeflateStride), l & 0x7FFFFFFFu);
       const uint64_t blen = std::min<uint64_t>(kDeflateBlock, s.size() - j * kDeflateBlock);
-      reg = crc_mulmod(crc_x8n(blen), reg) ^ hlen[nblk + k];
+      reg = crc_mulmod(crc_x8n(blen), reg) ^ hcrc[k];
     }
     if (gzip) {
       const uint32_t crc = ~reg;
