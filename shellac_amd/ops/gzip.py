@@ -1,5 +1,6 @@
 """Batch gzip on the GPU (csrc/deflate.hip): one wave per 32 KiB block, greedy LZ77 over
-an LDS hash table, fixed-Huffman DEFLATE; members decompress with zlib / gzip.
+an LDS hash table, per-block stored / fixed / dynamic Huffman codes planned on the host
+(csrc/huffman.cc); members decompress with zlib / gzip.
 
 The reference gunzips and re-gzips every cached origin response at level 6 on the CPU
 (src/python/shellac/server/HttpParser.py:124-127, :343-351). Here whole batches of bodies

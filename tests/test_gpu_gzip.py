@@ -52,8 +52,8 @@ def test_raw_deflate_and_ratio(gz):
         assert zlib.decompress(o, -15) == b
     ratio = sum(map(len, out)) / sum(map(len, bodies))
     z1 = sum(len(zlib.compress(b, 1)) for b in bodies) / sum(map(len, bodies))
-    # greedy single-candidate LZ77 + fixed Huffman: within 2x of zlib level 1 on text
-    assert ratio < 0.5 and ratio < 2 * z1, (ratio, z1)
+    # greedy single-candidate LZ77 + per-block dynamic Huffman codes: about zlib level 1
+    assert ratio < 0.5 and ratio < 1.1 * z1, (ratio, z1)
 
 
 def test_incompressible_falls_back_to_stored(gz):
