@@ -5,6 +5,7 @@
 #include <string_view>
 
 #include "bind_parts.h"
+#include "common.h"
 #include "deflate.h"
 #include "huffman.h"
 
@@ -38,6 +39,14 @@ void bind_deflate(py::module_& m) {
     std::vector<uint8_t> len(freq.size());
     huffman_lengths(freq.data(), (int)freq.size(), max_len, len.data());
     return std::vector<int>(len.begin(), len.end());
+  });
+  m.def("plan_block", [](const std::vector<uint32_t>& hist, uint32_t n, bool fin) {
+    SH_CHECK(hist.size() == (size_t)kHistSyms, "histogram of 316 symbols expected");
+    BlockPlan p;
+    plan_block(hist.data(), n, fin, &p);
+    return py::make_tuple(p.mode, py::bytes(std::string(p.header.begin(), p.header.end())),
+                          p.header_bits, std::vector<uint32_t>(p.codes, p.codes + kHistSyms),
+                          p.total_bytes);
   });
   m.def("deflate_tokens_cpu", [](const std::vector<uint32_t>& tokens, const py::bytes& data,
                                  bool fin) {

@@ -219,13 +219,15 @@ void plan_block(const uint32_t* hist_in, uint32_t n, bool fin, BlockPlan* out) {
   if (fb <= db) {
     out->mode = 1;
     out->total_bytes = fb;
-    uint8_t fl[kLitLenSyms], fd[kDistSyms];
-    for (int s = 0; s < kLitLenSyms; ++s) fl[s] = (uint8_t)fixed_len(s);
-    std::fill(fd, fd + kDistSyms, 5);
-    uint32_t c[kLitLenSyms];
-    canonical(fl, kLitLenSyms, c);
+    // the fixed code is defined over 288 literal/length and 32 distance symbols: the
+    // canonical assignment must count the unused 286-287 (8-bit) and 30-31 codes too
+    uint8_t fl[288], fd[32];
+    for (int s = 0; s < 288; ++s) fl[s] = (uint8_t)fixed_len(s);
+    std::fill(fd, fd + 32, 5);
+    uint32_t c[288];
+    canonical(fl, 288, c);
     for (int s = 0; s < kLitLenSyms; ++s) out->codes[s] = c[s] | ((uint32_t)fl[s] << 16);
-    canonical(fd, kDistSyms, c);
+    canonical(fd, 32, c);
     for (int j = 0; j < kDistSyms; ++j) out->codes[kLitLenSyms + j] = c[j] | (5u << 16);
     bw.put(fin ? 1 : 0, 1);
     bw.put(1, 2);

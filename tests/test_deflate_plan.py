@@ -81,6 +81,16 @@ def test_token_streams_decompress_with_zlib(core, kind):
         assert len(out) < len(zlib.compress(data, 1))
 
 
+def test_fixed_codes_for_high_literals(core):
+    """Tiny blocks take the fixed code; literals >= 144 use its 9-bit codes, whose
+    canonical assignment counts the unused literal/length symbols 286-287."""
+    rng = random.Random(11)
+    for _ in range(300):
+        data = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 6)))
+        out = core.deflate_tokens_cpu(greedy_tokens(data), data, True)
+        assert zlib.decompress(out, -15) == data, data
+
+
 def test_non_final_blocks_concatenate(core):
     rng = random.Random(4)
     parts = [_text(rng, 12000), os.urandom(3000), _text(rng, 9000)]
