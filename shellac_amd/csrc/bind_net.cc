@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include <condition_variable>
+#include <cstdlib>
 
 #include "backend.h"
 #include "bind_parts.h"
@@ -276,8 +277,13 @@ void bind_net(py::module_& m) {
              if (!backend.is_none()) be = backend.cast<BackendHandle&>().be;
              c.cache_enabled = be != nullptr;
              auto* px = new Proxy(c, be);
-             if (c.compress && c.gzip_gpu >= 0)
-               px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us));
+             if (c.compress && c.gzip_gpu >= 0) {
+               // service workers (each its own engine and stream); SHELLAC_GZIP_WORKERS
+               const char* w = std::getenv("SHELLAC_GZIP_WORKERS");
+               const int workers = w ? std::max(1, std::atoi(w)) : 4;
+               px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us,
+                                                                4096, workers));
+             }
              return px;
            }),
            py::arg("upstreams"), py::arg("backend") = py::none(), py::arg("port") = 8080,
