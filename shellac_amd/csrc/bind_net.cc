@@ -278,9 +278,12 @@ void bind_net(py::module_& m) {
              c.cache_enabled = be != nullptr;
              auto* px = new Proxy(c, be);
              if (c.compress && c.gzip_gpu >= 0) {
-               // service workers (each its own engine and stream); SHELLAC_GZIP_WORKERS
+               // service workers (each its own engine and stream); SHELLAC_GZIP_WORKERS.
+               // 2: with 4 the bodies split into twice as many smaller batches and the
+               // per-batch host work grew (49.8K vs 70.6K misses/s,
+               // profiles/r2_http_compress_workers_ab.log)
                const char* w = std::getenv("SHELLAC_GZIP_WORKERS");
-               const int workers = w ? std::max(1, std::atoi(w)) : 4;
+               const int workers = w ? std::max(1, std::atoi(w)) : 2;
                px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us,
                                                                 4096, workers));
              }
