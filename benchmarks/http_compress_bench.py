@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--origin-threads", type=int, default=3)
     ap.add_argument("--conc", type=int, default=256)
     ap.add_argument("--modes", nargs="+", default=["none", "cpu", "gpu"])
+    ap.add_argument("--gzip-batch-us", type=int, default=200, help="GPU service batch window")
     ap.add_argument("--timeout", type=float, default=300.0)
     a = ap.parse_args()
     origin, oport = start_text_origin(a.body, a.origin_threads)
@@ -53,7 +54,8 @@ def main():
             prefix = f"/m{i}/"  # fresh objects per mode: every first-pass request misses
             with Server([("127.0.0.1", oport)], port=0, backend=backend, threads=a.threads,
                         client_max_reqs=1 << 30, compress=mode != "none",
-                        gzip_gpu=0 if mode == "gpu" else -1).start() as px:
+                        gzip_gpu=0 if mode == "gpu" else -1,
+                        gzip_batch_us=a.gzip_batch_us).start() as px:
                 c0 = hb.thread_cpu()
                 t0 = time.time()
                 miss = hb.load(px.port, a.objects, a.conc, a.client_threads, a.objects, 0.0,
@@ -64,6 +66,7 @@ def main():
                 hit = hb.load(px.port, a.objects, a.conc, a.client_threads, a.objects, 0.0,
                               prefix, 2, a.timeout)
                 res = {"mode": mode, "body_bytes": a.body, "objects": a.objects,
+                       "gzip_batch_us": a.gzip_batch_us if mode == "gpu" else None,
                        "miss_rps": round(miss["rps"]),
                        "miss_p50_ms": round(miss["latency_ms"]["p50"], 3),
                        "miss_p99_ms": round(miss["latency_ms"]["p99"], 3),
