@@ -1359,10 +1359,12 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
         const uint64_t d0 = pack2(w0.x, w0.y), d1 = pack2(w0.z, w0.w);
         const uint32_t vlen = w1.x;
         const Digest d{d0, d1};
-        // the key's entry (a key has at most one): first bucket first, the second only
-        // when the first does not hold the digest (SETs fill the first bucket first, so one
-        // 128-B line per window entry usually settles it). The item is live iff the key's
-        // entry points at it; a superseded copy finds its key's entry pointing elsewhere.
+        // the entry pointing at this item: first bucket first, the second only when the
+        // first has none (SETs fill the first bucket first, so one 128-B line per window
+        // entry usually settles it). A digest match alone does not settle it: a dead entry
+        // keeps its digest, so a key can match in one bucket while its live entry is in the
+        // other (stopping there dropped live, referenced items: test_serve_steps_return_
+        // ground_truth_records)
         const uint64_t bs[2] = {bucket1(d, mask), bucket2(d, mask)};
         bool found = false;
         for (int q = 0; q < 2 && !found; ++q)
@@ -1370,7 +1372,6 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
           for (int k = 0; k < (int)kEntriesPerBucket; ++k) {
             const Entry* e = index + bs[q] * kEntriesPerBucket + k;
             const uint64_t el = __hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e->d0 == d0 && e->d1 == d1) found = true;
             if (el == l + 1) {
               found = true;
               const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
