@@ -247,7 +247,8 @@ void bind_net(py::module_& m) {
                        bool decode_gzip, int upstream_retry_s, uint64_t stream_bytes,
                        uint64_t stream_high_water, const std::string& health_path,
                        int health_interval_ms, int health_timeout_ms, int health_fails,
-                       std::vector<int> cpus, int spin_us, int gzip_gpu, int gzip_batch_us) {
+                       std::vector<int> cpus, int spin_us, int gzip_gpu, int gzip_batch_us,
+                       uint64_t max_inflate_bytes, int gzip_workers) {
              ProxyConfig c;
              c.spin_us = spin_us;
              c.gzip_gpu = gzip_gpu;
@@ -265,6 +266,7 @@ void bind_net(py::module_& m) {
              c.client_max_reqs = client_max_reqs;
              c.balance = balance;
              c.decode_gzip = decode_gzip;
+             c.max_inflate_bytes = max_inflate_bytes;
              c.upstream_retry_s = upstream_retry_s;
              c.stream_bytes = stream_bytes;
              c.stream_high_water = stream_high_water;
@@ -278,14 +280,11 @@ void bind_net(py::module_& m) {
              c.cache_enabled = be != nullptr;
              auto* px = new Proxy(c, be);
              if (c.compress && c.gzip_gpu >= 0) {
-               // service workers (each its own engine and stream); SHELLAC_GZIP_WORKERS.
-               // 2: with 4 the bodies split into twice as many smaller batches and the
-               // per-batch host work grew (49.8K vs 70.6K misses/s,
-               // profiles/r2_http_compress_workers_ab.log)
-               const char* w = std::getenv("SHELLAC_GZIP_WORKERS");
-               const int workers = w ? std::max(1, std::atoi(w)) : 2;
+               // service workers (each its own engine and stream), default 2: with 4 the
+               // bodies split into twice as many smaller batches and the per-batch host
+               // work grew (49.8K vs 70.6K misses/s, profiles/r2_http_compress_workers_ab.log)
                px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us,
-                                                                4096, workers));
+                                                                4096, std::max(1, gzip_workers)));
              }
              return px;
            }),
@@ -299,7 +298,8 @@ void bind_net(py::module_& m) {
            py::arg("health_path") = "", py::arg("health_interval_ms") = 1000,
            py::arg("health_timeout_ms") = 500, py::arg("health_fails") = 2,
            py::arg("cpus") = std::vector<int>{}, py::arg("spin_us") = 0,
-           py::arg("gzip_gpu") = -1, py::arg("gzip_batch_us") = 200)
+           py::arg("gzip_gpu") = -1, py::arg("gzip_batch_us") = 200,
+           py::arg("max_inflate_bytes") = 64ull << 20, py::arg("gzip_workers") = 2)
       .def("start", &Proxy::start)
       .def("wait", &Proxy::wait, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Proxy::stop)

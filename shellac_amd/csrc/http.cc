@@ -45,7 +45,7 @@ std::string gzip_compress(const std::string& in, int level) {
   return out;
 }
 
-bool gzip_decompress(const std::string& in, std::string* out) {
+bool gzip_decompress(const std::string& in, std::string* out, uint64_t max_out) {
   z_stream zs;
   std::memset(&zs, 0, sizeof zs);
   if (inflateInit2(&zs, 31) != Z_OK) return false;
@@ -59,6 +59,10 @@ bool gzip_decompress(const std::string& in, std::string* out) {
     rc = inflate(&zs, Z_NO_FLUSH);
     if (rc != Z_OK && rc != Z_STREAM_END) break;
     out->append(buf, sizeof buf - zs.avail_out);
+    if (out->size() > max_out) {  // decompression bomb: give up, never allocate past the cap
+      rc = Z_MEM_ERROR;
+      break;
+    }
   }
   inflateEnd(&zs);
   return rc == Z_STREAM_END;
@@ -76,6 +80,7 @@ HttpParser::~HttpParser() {
 void HttpParser::reset() {
   const bool dg = decode_gzip_, eb = eof_body_;
   const size_t mh = max_header_bytes_;
+  const uint64_t md = max_decoded_bytes_;
   if (zs_) {
     inflateEnd(zs_);
     delete zs_;
@@ -86,6 +91,7 @@ void HttpParser::reset() {
   eof_body_ = eb;
   no_body_ = false;
   max_header_bytes_ = mh;
+  max_decoded_bytes_ = md;
   header_bytes_ = 0;
   line_.clear();
   err_.clear();
@@ -218,24 +224,75 @@ bool HttpParser::on_header_line(const std::string& line) {
   return true;
 }
 
+// Comma-separated list elements of every `name` header, trimmed and lower-cased
+// (empty elements dropped, RFC 7230 §7).
+static std::vector<std::string> header_list(const std::vector<Header>& hs, const char* name) {
+  std::vector<std::string> out;
+  for (const auto& h : hs) {
+    if (h.first != name) continue;
+    size_t i = 0;
+    const std::string& v = h.second;
+    while (i <= v.size()) {
+      size_t j = v.find(',', i);
+      if (j == std::string::npos) j = v.size();
+      std::string t = to_lower(trim(v.substr(i, j - i)));
+      if (!t.empty()) out.push_back(std::move(t));
+      i = j + 1;
+    }
+  }
+  return out;
+}
+
 bool HttpParser::on_headers_done() {
-  const std::string* te = header("transfer-encoding");
-  chunked_ = te && to_lower(*te).find("chunked") != std::string::npos;
+  // Message framing is where a reverse proxy must be strict (RFC 7230 §3.3.3): a
+  // request the proxy and the origin could frame differently is a smuggling vector,
+  // so anything ambiguous is an error (the proxy answers 400 / treats the upstream
+  // as failed) instead of a best guess.
+  chunked_ = false;
+  bool te_eof = false;  // response: a final coding other than chunked = read to EOF
+  const bool has_te = header("transfer-encoding") != nullptr;
+  if (has_te) {
+    const std::vector<std::string> te = header_list(headers_, "transfer-encoding");
+    if (te.empty()) { fail("empty transfer-encoding"); return false; }
+    for (size_t i = 0; i < te.size(); ++i) {
+      if (te[i] == "chunked" && i + 1 != te.size()) { fail("chunked is not the final coding"); return false; }
+      // gzip / deflate / compress transfer-codings are not decoded by this proxy
+      if (te[i] != "chunked") { fail("unsupported transfer-coding: " + te[i]); return false; }
+    }
+    chunked_ = te.back() == "chunked";
+    if (!chunked_) {
+      if (is_request_) { fail("request transfer-encoding without final chunked"); return false; }
+      te_eof = true;
+    }
+  }
   const std::string* ce = header("content-encoding");
-  gzip_ = ce && to_lower(*ce) == "gzip";
-  const std::string* cl = header("content-length");
+  gzip_ = ce && to_lower(trim(*ce)) == "gzip";
   content_length_ = -1;
-  if (cl) {
-    char* endp = nullptr;
-    long long v = std::strtoll(cl->c_str(), &endp, 10);
-    if (endp == cl->c_str() || v < 0) { fail("bad content-length"); return false; }
-    content_length_ = v;
+  if (header("content-length")) {
+    // digits only; repeated values (separate headers or a list) must all agree
+    for (const std::string& v : header_list(headers_, "content-length")) {
+      if (v.size() > 18 || v.find_first_not_of("0123456789") != std::string::npos) {
+        fail("bad content-length");
+        return false;
+      }
+      const int64_t n = (int64_t)std::strtoll(v.c_str(), nullptr, 10);
+      if (content_length_ >= 0 && n != content_length_) { fail("conflicting content-length"); return false; }
+      content_length_ = n;
+    }
+    if (content_length_ < 0) { fail("bad content-length"); return false; }
+    if (has_te) {
+      if (is_request_) { fail("both content-length and transfer-encoding"); return false; }
+      content_length_ = -1;  // response: transfer-encoding wins (RFC 7230 §3.3.3 rule 3)
+    }
   }
   const bool bodyless_resp =
       !is_request_ && (no_body_ || (status_ >= 100 && status_ < 200) || status_ == 204 ||
                        status_ == 304);
   if (bodyless_resp) {
     state_ = kDone;
+  } else if (te_eof) {
+    if (!eof_body_) { fail("close-delimited body without eof framing"); return false; }
+    state_ = kBodyEof;
   } else if (chunked_) {
     state_ = kChunkSize;
   } else if (content_length_ > 0) {
@@ -266,19 +323,28 @@ void HttpParser::append_body(const char* p, size_t n) {
   zs_->next_in = reinterpret_cast<Bytef*>(const_cast<char*>(p));
   zs_->avail_in = (uInt)n;
   char buf[16384];
-  while (zs_->avail_in > 0) {
+  // until the input is consumed AND inflate stopped filling whole buffers (highly
+  // compressible input leaves output pending after its last input byte)
+  for (;;) {
     zs_->next_out = reinterpret_cast<Bytef*>(buf);
     zs_->avail_out = sizeof buf;
     const int rc = inflate(zs_, Z_NO_FLUSH);
     body_.append(buf, sizeof buf - zs_->avail_out);
+    if (body_.size() > max_decoded_bytes_) { fail("decoded gzip body too large"); return; }
     if (rc == Z_STREAM_END) break;
     if (rc != Z_OK && rc != Z_BUF_ERROR) { fail("bad gzip body"); return; }
+    if (zs_->avail_in == 0 && zs_->avail_out != 0) break;
     if (rc == Z_BUF_ERROR && zs_->avail_out != 0) break;
   }
 }
 
+void HttpParser::complete_body() {
+  flush_body();
+  if (state_ != kError) state_ = kDone;
+}
+
 void HttpParser::flush_body() {
-  if (!zs_) return;
+  if (!zs_ || state_ == kError) return;
   char buf[16384];
   int rc;
   do {
@@ -286,9 +352,10 @@ void HttpParser::flush_body() {
     zs_->avail_in = 0;
     zs_->next_out = reinterpret_cast<Bytef*>(buf);
     zs_->avail_out = sizeof buf;
-    rc = inflate(zs_, Z_FINISH);
+    rc = inflate(zs_, Z_SYNC_FLUSH);
     body_.append(buf, sizeof buf - zs_->avail_out);
-  } while (rc == Z_OK && zs_->avail_out == 0);
+    if (body_.size() > max_decoded_bytes_) { fail("decoded gzip body too large"); return; }
+  } while ((rc == Z_OK || rc == Z_BUF_ERROR) && zs_->avail_out == 0);
 }
 
 size_t HttpParser::parse(const char* data, size_t len) {
@@ -329,10 +396,7 @@ size_t HttpParser::parse(const char* data, size_t len) {
           if (!line.empty()) { fail("missing CRLF after chunk"); break; }
           state_ = kChunkSize;
         } else {  // trailers: lines until an empty one
-          if (line.empty()) {
-            flush_body();
-            state_ = kDone;
-          }
+          if (line.empty()) complete_body();
         }
         break;
       }
@@ -343,10 +407,10 @@ size_t HttpParser::parse(const char* data, size_t len) {
         p += n;
         consumed += n;
         remaining_ -= n;
+        if (state_ == kError) break;
         if (remaining_ == 0) {
           if (state_ == kBodyLength) {
-            flush_body();
-            state_ = kDone;
+            complete_body();
           } else {
             state_ = kChunkCrlf;
           }
@@ -367,10 +431,7 @@ size_t HttpParser::parse(const char* data, size_t len) {
 }
 
 bool HttpParser::finish() {
-  if (state_ == kBodyEof) {
-    flush_body();
-    state_ = kDone;
-  }
+  if (state_ == kBodyEof) complete_body();
   return state_ == kDone;
 }
 

@@ -57,6 +57,8 @@ class HttpParser {
   void set_eof_body(bool v) { eof_body_ = v; }          // read unframed responses to EOF
   void set_no_body(bool v) { no_body_ = v; }            // response to HEAD
   void set_max_header_bytes(size_t v) { max_header_bytes_ = v; }
+  // decode_gzip: an inflated body larger than this is an error (decompression bombs)
+  void set_max_decoded_bytes(uint64_t v) { max_decoded_bytes_ = v; }
 
   // state
   bool headers_complete() const { return state_ > kHeaders; }
@@ -102,6 +104,7 @@ class HttpParser {
   bool on_headers_done();
   void append_body(const char* p, size_t n);
   void flush_body();
+  void complete_body();  // flush_body, then kDone unless that failed
   void fail(const std::string& m);
   bool take_line(const char*& p, const char* end, std::string* line, size_t* consumed);
 
@@ -109,6 +112,7 @@ class HttpParser {
   bool decode_gzip_;
   bool eof_body_ = false, no_body_ = false;
   size_t max_header_bytes_ = 64 * 1024;
+  uint64_t max_decoded_bytes_ = 64ull << 20;
   size_t header_bytes_ = 0;
   std::string line_;  // partial line carried across calls
   std::string err_;
@@ -125,9 +129,10 @@ class HttpParser {
 
 // "content-type" -> "Content-Type" (HttpParser.py:134).
 std::string canonical_header(const std::string& lower);
-// gzip (wbits 31) compress at `level`; inflate a complete gzip stream.
+// gzip (wbits 31) compress at `level`.
 std::string gzip_compress(const std::string& in, int level = 6);
-bool gzip_decompress(const std::string& in, std::string* out);
+// Inflate a complete gzip stream; false on a corrupt stream or more than `max_out` bytes.
+bool gzip_decompress(const std::string& in, std::string* out, uint64_t max_out = 64ull << 20);
 std::string to_lower(std::string s);
 
 }  // namespace shellac

@@ -57,6 +57,108 @@ long cc_max_age(const std::string* cc) {
   return best;
 }
 
+// ---- content negotiation + Vary (policy "rfc") ----------------------------------------
+// The proxy forces `Accept-Encoding: gzip` upstream (Server.py:358), so one URL is cached
+// once, usually gzip-coded; a client that did not ask for gzip gets the identity variant
+// decoded from it on the way out (deliver()). Responses that Vary on request headers
+// other than Accept-Encoding are stored per variant: a marker under the URL key names the
+// headers, and the object lives under URL + the request's values of those headers.
+const std::string kVaryMarker = "\x01SHELLAC-VARY\n";  // objects always start with "HTTP/"
+
+bool is_vary_marker(std::string_view v) {
+  return v.size() >= kVaryMarker.size() && v.compare(0, kVaryMarker.size(), kVaryMarker) == 0;
+}
+
+std::vector<std::string> split_names(const std::string& list) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= list.size()) {
+    size_t j = list.find(',', i);
+    if (j == std::string::npos) j = list.size();
+    size_t a = i, b = j;
+    while (a < b && (list[a] == ' ' || list[a] == '\t')) ++a;
+    while (b > a && (list[b - 1] == ' ' || list[b - 1] == '\t')) --b;
+    if (b > a) out.push_back(to_lower(list.substr(a, b - a)));
+    i = j + 1;
+  }
+  return out;
+}
+
+// Request headers a response varies on, sorted, without accept-encoding (negotiated by
+// the proxy itself); {"*"} = varies on something outside the request (never cached).
+std::vector<std::string> vary_names(const HttpParser& r) {
+  std::vector<std::string> names;
+  for (const auto& h : r.headers()) {
+    if (h.first != "vary") continue;
+    for (auto& n : split_names(h.second)) {
+      if (n == "*") return {"*"};
+      if (n != "accept-encoding" && std::find(names.begin(), names.end(), n) == names.end())
+        names.push_back(std::move(n));
+    }
+  }
+  std::sort(names.begin(), names.end());
+  return names;
+}
+
+std::vector<std::string> marker_names(std::string_view v) {
+  return split_names(std::string(v.substr(kVaryMarker.size())));
+}
+
+// Secondary key of one variant: URL key + the request's values of the varied headers.
+std::string vary_key(const std::string& base, const std::vector<std::string>& names,
+                     const std::vector<Header>& req) {
+  std::string k = base;
+  k += '\x1f';
+  for (const auto& n : names) {
+    k += n;
+    k += '=';
+    bool first = true;
+    for (const auto& h : req)
+      if (h.first == n) {
+        if (!first) k += ',';
+        k += h.second;
+        first = false;
+      }
+    k += '\x1e';
+  }
+  return k;
+}
+
+// Does the serialized response's head carry Content-Encoding: gzip?
+bool object_is_gzip(std::string_view ov) {
+  const size_t eoh = ov.find("\r\n\r\n");
+  if (eoh == std::string_view::npos) return false;
+  size_t pos = ov.find("\r\n");
+  while (pos != std::string_view::npos && pos < eoh) {
+    const size_t ls = pos + 2;
+    const size_t le = ov.find("\r\n", ls);
+    const std::string_view line = ov.substr(ls, le - ls);
+    static constexpr std::string_view kCe = "content-encoding:";
+    if (line.size() > kCe.size()) {
+      bool match = true;
+      for (size_t i = 0; i < kCe.size() && match; ++i)
+        match = (char)std::tolower((unsigned char)line[i]) == kCe[i];
+      if (match) return to_lower(std::string(line.substr(kCe.size()))).find("gzip") != std::string::npos;
+    }
+    pos = le;
+  }
+  return false;
+}
+
+// Identity variant of a gzip-coded cached response (body inflated, capped at `cap` bytes;
+// Content-Encoding dropped, Content-Length recomputed, Vary kept). nullptr on a corrupt
+// or oversized body.
+Bytes identity_variant(const Bytes& obj, uint64_t cap) {
+  HttpParser r(false);
+  r.parse(obj->data(), obj->size());
+  if (!r.message_complete() && !r.finish()) return nullptr;
+  std::string body;
+  if (!gzip_decompress(r.body(), &body, cap)) return nullptr;
+  r.remove_header("content-encoding");
+  r.mutable_body() = std::move(body);
+  return std::make_shared<const std::string>(r.serialize());
+}
+
 }  // namespace
 
 struct Slot {
@@ -71,8 +173,12 @@ struct Slot {
   // for re-serializing a request it does not forward. Returned to the reactor's pool.
   std::unique_ptr<HttpParser> req;
   std::string key;
+  std::string base_key;  // URL (+Host) key; `key` becomes a variant key after a Vary marker
   Digest d{};
   bool lookup = false, head = false, client_gzip = false;
+  bool vary_probe = false;  // `key` is a variant key (second lookup after a marker)
+  // request headers, kept for the miss path when a response may Vary (policy rfc)
+  std::shared_ptr<const std::vector<Header>> req_headers;
   int attempts = 0;
   double t0 = 0;
 };
@@ -106,6 +212,8 @@ struct Pend {
   std::string key;
   Digest d;
   bool lookup, head, client_gzip;
+  std::string base_key;
+  std::shared_ptr<const std::vector<Header>> req_headers;
 };
 
 struct Upstream : Conn {
@@ -138,7 +246,8 @@ class Reactor : public Executor {
   std::atomic<uint64_t> requests{0}, hits{0}, misses{0}, upstream_reqs{0}, responses{0},
       bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
       cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0},
-      streamed{0}, stream_pauses{0}, gzip_gpu_bodies{0};
+      streamed{0}, stream_pauses{0}, gzip_gpu_bodies{0}, identity_decoded{0}, vary_stored{0},
+      vary_hits{0};
   // event-loop health: the longest iteration (events handled between two epoll_waits)
   // and how many took over 10 ms — a reactor that stalls stops accepting connections
   std::atomic<uint64_t> loop_max_us{0}, loop_slow{0}, client_resets{0};
@@ -175,6 +284,7 @@ class Reactor : public Executor {
   void flush_client(Client* c);
   void flush_upstream(Upstream* u);
   void complete_slot(Client* c, Slot* s, Bytes data);
+  void deliver(Client* c, Slot* s, Bytes obj);
   void fail_pend(Pend& p, int code, const char* reason);
   void release_waiters(const std::string& key, Bytes obj);
   void close_client(Client* c);
@@ -471,6 +581,7 @@ void Reactor::on_request(Client* c) {
   s->client_gzip = contains_ci(q.header("accept-encoding"), "gzip");
   const std::string* host = q.header("host");
   s->key = cfg_.key_host && host ? *host + url : url;  // reference key: URL (Server.py:327)
+  s->base_key = s->key;
   s->d = digest_bytes(reinterpret_cast<const uint8_t*>(s->key.data()), s->key.size());
   s->lookup = px_->cfg_.cache_enabled &&
               (cfg_.policy == "reference" || method == "GET") && !q.header("authorization");
@@ -492,9 +603,24 @@ void Reactor::on_cache(uint64_t cid, uint64_t seq, bool hit, CacheValue v) {
   if (!c) return;
   Slot* s = find_slot(c, seq);
   if (!s || s->ready) return;
+  if (hit && v.data && is_vary_marker(v.data->view())) {
+    // the URL's responses Vary: look the variant of this request up under its own key
+    // (a marker found by a variant lookup, or without the request, counts as a miss)
+    if (cfg_.policy == "rfc" && !s->vary_probe && s->req) {
+      s->key = vary_key(s->base_key, marker_names(v.data->view()), s->req->headers());
+      s->d = digest_bytes(reinterpret_cast<const uint8_t*>(s->key.data()), s->key.size());
+      s->vary_probe = true;
+      px_->backend_->get(s->key, s->d, this, [this, cid, seq](bool h2, CacheValue v2) {
+        on_cache(cid, seq, h2, std::move(v2));
+      });
+      return;
+    }
+    hit = false;
+  }
   if (hit && v.data) {
     hits++;
-    complete_slot(c, s, v.data);
+    if (s->vary_probe) vary_hits++;
+    deliver(c, s, v.data);
     return;
   }
   misses++;
@@ -532,6 +658,23 @@ static Bytes with_connection_close(const Bytes& obj) {
   out += "Connection: close\r\n\r\n";
   out.append(ov.substr(eoh + 4));
   return std::make_shared<const std::string>(std::move(out));
+}
+
+// A cached (or just fetched) object to one client: under policy rfc a gzip-coded object
+// goes to a client without `Accept-Encoding: gzip` as its identity variant.
+void Reactor::deliver(Client* c, Slot* s, Bytes obj) {
+  if (obj && !s->client_gzip && !s->head && cfg_.policy == "rfc" && object_is_gzip(obj->view())) {
+    Bytes id = identity_variant(obj, cfg_.max_inflate_bytes);
+    if (!id) {
+      errors++;
+      complete_slot(c, s, std::make_shared<const std::string>(simple_response(
+                              502, "Bad Gateway", cfg_.server_name, "undecodable gzip object\n")));
+      return;
+    }
+    identity_decoded++;
+    obj = std::move(id);
+  }
+  complete_slot(c, s, std::move(obj));
 }
 
 void Reactor::complete_slot(Client* c, Slot* s, Bytes data) {
@@ -724,6 +867,8 @@ void Reactor::give_parser(std::unique_ptr<HttpParser> p) {
 void Reactor::forward(Client* c, Slot* s) {
   s->attempts++;
   if (s->fwd.empty() && s->req) {
+    if (s->lookup && cfg_.policy == "rfc")  // a Vary'd response is keyed by these
+      s->req_headers = std::make_shared<const std::vector<Header>>(s->req->headers());
     s->fwd = upstream_request(*s->req);
     give_parser(std::move(s->req));
   }
@@ -734,7 +879,8 @@ void Reactor::forward(Client* c, Slot* s) {
     return;
   }
   u->out.write(s->fwd);
-  u->pend.push_back(Pend{c->id, s->seq, s->key, s->d, s->lookup, s->head, s->client_gzip});
+  u->pend.push_back(Pend{c->id, s->seq, s->key, s->d, s->lookup, s->head, s->client_gzip,
+                        s->base_key, s->req_headers});
   u->count++;
   upstream_reqs++;
   flush_upstream(u);
@@ -778,7 +924,7 @@ void Reactor::release_waiters(const std::string& key, Bytes obj) {
     if (!s || s->ready) continue;
     if (obj) {
       hits++;
-      complete_slot(c, s, obj);
+      deliver(c, s, obj);
     } else {
       forward(c, s);  // uncacheable ("hit-for-pass"): each waiter fetches its own copy
     }
@@ -834,6 +980,7 @@ void Reactor::on_upstream(Upstream* u, uint32_t ev) {
         }
         if (!u->resp) {
           u->resp = std::make_unique<HttpParser>(cfg_.decode_gzip);
+          u->resp->set_max_decoded_bytes(cfg_.max_inflate_bytes);
           u->resp->set_no_body(u->pend.front().head);
           u->resp->set_eof_body(true);
         }
@@ -917,7 +1064,10 @@ void Reactor::on_upstream_response(Upstream* u) {
   rewrite_response_headers(r);
   const std::string* ce = r.header("content-encoding");
   bool deferred = false;
-  if (cfg_.compress && !ce && p.client_gzip && r.body().size() >= 256) {
+  // -z: under rfc the stored variant is gzip whichever client leads the fetch (a client
+  // without gzip gets the identity variant from deliver()); the reference policy keeps
+  // compressing only for gzip clients
+  if (cfg_.compress && !ce && (p.client_gzip || cfg_.policy == "rfc") && r.body().size() >= 256) {
     const std::string* ct = r.header("content-type");
     if (ct && (contains_ci(ct, "text/") || contains_ci(ct, "json") || contains_ci(ct, "javascript") ||
                contains_ci(ct, "xml"))) {
@@ -961,6 +1111,16 @@ void Reactor::on_upstream_response(Upstream* u) {
 // Cache store, client slot and collapsed waiters of a complete upstream response.
 void Reactor::finish_response(HttpParser& r, const Pend& p) {
   Bytes obj;
+  const bool rfc = cfg_.policy == "rfc";
+  std::vector<std::string> vnames;
+  if (rfc && !p.head) {
+    vnames = vary_names(r);
+    // one cache entry serves both codings: say so to downstream caches
+    if (r.header("content-encoding") && !contains_ci(r.header("vary"), "accept-encoding")) {
+      const std::string* v = r.header("vary");
+      r.set_header("vary", v ? *v + ", Accept-Encoding" : std::string("Accept-Encoding"));
+    }
+  }
   if (p.head) {
     const std::string* cl = r.header("content-length");
     const uint64_t len = cl ? std::strtoull(cl->c_str(), nullptr, 10) : 0;
@@ -969,18 +1129,37 @@ void Reactor::finish_response(HttpParser& r, const Pend& p) {
     obj = std::make_shared<const std::string>(r.serialize());
   }
   uint32_t ttl = cfg_.ttl;
-  bool cached = false;
+  bool cached = false, waiters_share = true;
   if (p.lookup && !p.head && cacheable_response(r, &ttl)) {
-    cached = true;
-    px_->backend_->set(p.key, p.d, obj, 0, ttl);  // Server.py:432 mc.set(key, obj, time=ttl)
-    cache_sets++;
+    if (vnames.empty()) {
+      cached = true;
+      px_->backend_->set(p.key, p.d, obj, 0, ttl);  // Server.py:432 mc.set(key, obj, time=ttl)
+      cache_sets++;
+    } else if (vnames[0] != "*" && p.req_headers) {
+      // Vary: marker under the URL key, the object under this request's variant key
+      const std::string vk = vary_key(p.base_key, vnames, *p.req_headers);
+      std::string marker = kVaryMarker;
+      for (size_t i = 0; i < vnames.size(); ++i) marker += (i ? "," : "") + vnames[i];
+      const Digest bd = digest_bytes(reinterpret_cast<const uint8_t*>(p.base_key.data()),
+                                     p.base_key.size());
+      const Digest vd = digest_bytes(reinterpret_cast<const uint8_t*>(vk.data()), vk.size());
+      px_->backend_->set(p.base_key, bd, std::make_shared<const std::string>(std::move(marker)), 0,
+                         ttl);
+      px_->backend_->set(vk, vd, obj, 0, ttl);
+      cache_sets++;
+      vary_stored++;
+      cached = true;
+      // requests collapsed onto the URL key may carry other header values: they fetch
+      // their own variant; those collapsed onto this variant key share it
+      waiters_share = p.key == vk;
+    }  // Vary: * (or no request headers kept): not cacheable
   }
   if (Client* c = find_client(p.client_id)) {
     if (Slot* s = find_slot(c, p.seq)) {
-      if (!s->ready) complete_slot(c, s, obj);
+      if (!s->ready) deliver(c, s, obj);
     }
   }
-  if (p.lookup) release_waiters(p.key, cached ? obj : nullptr);
+  if (p.lookup) release_waiters(p.key, cached && waiters_share ? obj : nullptr);
 }
 
 void Reactor::rewrite_response_headers(HttpParser& r) {
@@ -1244,7 +1423,7 @@ void Proxy::stop() {
 std::string Proxy::stats_json() {
   uint64_t req = 0, hit = 0, miss = 0, ur = 0, resp = 0, bo = 0, err = 0, cl = 0, up = 0, acc = 0,
            gcc = 0, sets = 0, bad = 0, uf = 0, rt = 0, col = 0, stm = 0, stp = 0, lmax = 0,
-           lslow = 0;
+           lslow = 0, idd = 0, vst = 0, vh = 0;
   uint64_t pmax[5] = {}, crst = 0;
   uint64_t h[kHistBuckets] = {};
   for (auto& r : reactors_) {
@@ -1256,6 +1435,9 @@ std::string Proxy::stats_json() {
     lmax = std::max<uint64_t>(lmax, r->loop_max_us);
     lslow += r->loop_slow;
     crst += r->client_resets;
+    idd += r->identity_decoded;
+    vst += r->vary_stored;
+    vh += r->vary_hits;
     for (int k = 0; k < 5; ++k) pmax[k] = std::max<uint64_t>(pmax[k], r->phase_max_us[k]);
     for (int b = 0; b < kHistBuckets; ++b) h[b] += r->hist[b];
   }
@@ -1279,7 +1461,8 @@ std::string Proxy::stats_json() {
     << ",\"upstream_failures\":" << uf << ",\"retries\":" << rt << ",\"collapsed\":" << col
     << ",\"streamed\":" << stm << ",\"stream_pauses\":" << stp << ",\"clients\":" << cl
     << ",\"upstream_conns\":" << up << ",\"accepts\":" << acc << ",\"gc_closed\":" << gcc
-    << ",\"client_resets\":" << crst
+    << ",\"client_resets\":" << crst << ",\"identity_decoded\":" << idd
+    << ",\"vary_stored\":" << vst << ",\"vary_hits\":" << vh
     << ",\"loop_max_us\":" << lmax << ",\"loop_slow\":" << lslow
     << ",\"loop_phase_max_us\":{\"accept\":" << pmax[0] << ",\"client\":" << pmax[1]
     << ",\"upstream\":" << pmax[2] << ",\"posted\":" << pmax[3] << ",\"timer\":" << pmax[4]

@@ -52,7 +52,9 @@ struct ProxyConfig {
   std::string policy = "rfc";         // "rfc" | "reference" (cache every response)
   bool kill_switch = true;            // GET /kill stops the proxy (Server.py:329-331)
   bool kill_loopback_only = true;
-  bool key_host = false;              // cache key = Host + URL (ref: URL only)
+  // cache key = Host + URL (ref: URL only). The Python/CLI layer defaults it on for
+  // policy rfc (vhosts must not share entries) and off for policy reference.
+  bool key_host = false;
   int client_timeout = 30;            // CLIENT_TIMEOUT (Server.py:23)
   int client_max_reqs = 1000;         // CLIENT_MAX_REQS (Server.py:24)
   std::string balance = "random";     // random (ref :123) | roundrobin | leastconn
@@ -68,6 +70,9 @@ struct ProxyConfig {
   int health_fails = 2;
   int health_passes = 1;
   bool decode_gzip = false;           // inflate + re-deflate every miss like the reference
+  // cap on any inflate the proxy runs (--decode-gzip bodies, identity variants for
+  // clients without gzip): a larger body is a decompression bomb and fails (502)
+  uint64_t max_inflate_bytes = 64ull << 20;
   // Responses whose body exceeds this are streamed to the client as they arrive and not
   // cached (the reference buffers every object whole, Server.py:408-421).
   uint64_t stream_bytes = 1 << 20;

@@ -117,20 +117,24 @@ class Server:
     def __init__(self, servers: Sequence[ServerSpec], caches: Sequence[ServerSpec] = (),
                  port: int = 8080, ttl: int = 170, compress: bool = False, cache: bool = False,
                  *, backend=None, backend_kind: Optional[str] = None, threads: int = 1,
-                 policy: str = "rfc", kill_switch: bool = True, key_host: bool = False,
+                 policy: str = "rfc", kill_switch: bool = True, key_host: Optional[bool] = None,
                  client_timeout: int = 30, client_max_reqs: int = 1000,
                  balance: str = "random", bind: str = "0.0.0.0", decode_gzip: bool = False,
                  stream_bytes: int = 1 << 20, stream_high_water: int = 8 << 20,
                  health_path: str = "", health_interval_ms: int = 1000,
                  health_timeout_ms: int = 500, health_fails: int = 2,
                  cpus: Sequence[int] = (), spin_us: int = 0, gzip_gpu: int = -1,
-                 gzip_batch_us: int = 200, **backend_opts):
+                 gzip_batch_us: int = 200, gzip_workers: int = 2,
+                 max_inflate_bytes: int = 64 << 20, **backend_opts):
         if not servers:
             raise ValueError("No upstream web servers specified.")
         self._backend = backend
         if self._backend is None and (cache or backend_kind):
             kind = backend_kind or ("memcached" if caches else "dram")
             self._backend = make_backend(kind, caches=caches, **backend_opts)
+        if key_host is None:
+            # rfc: virtual hosts never share an entry; reference: URL-only keys (Server.py:327)
+            key_host = policy == "rfc"
         self._proxy = core().Proxy(
             _csv(servers, 80), self._backend, port=port, bind=bind, threads=threads, ttl=ttl,
             compress=compress, policy=policy, kill_switch=kill_switch, key_host=key_host,
@@ -139,7 +143,8 @@ class Server:
             stream_high_water=stream_high_water, health_path=health_path,
             health_interval_ms=health_interval_ms, health_timeout_ms=health_timeout_ms,
             health_fails=health_fails, cpus=[int(c) for c in cpus], spin_us=int(spin_us),
-            gzip_gpu=int(gzip_gpu), gzip_batch_us=int(gzip_batch_us))
+            gzip_gpu=int(gzip_gpu), gzip_batch_us=int(gzip_batch_us),
+            max_inflate_bytes=int(max_inflate_bytes), gzip_workers=int(gzip_workers))
         self._started = False
 
     @property
@@ -225,7 +230,13 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--balance", choices=["random", "roundrobin", "leastconn"], default="random")
     p.add_argument("--client-timeout", type=int, default=30)
     p.add_argument("--client-max-reqs", type=int, default=1000)
-    p.add_argument("--key-host", action="store_true", help="include Host in the cache key")
+    p.add_argument("--key-host", dest="key_host", action="store_true", default=None,
+                   help="include Host in the cache key (default: on with --policy rfc)")
+    p.add_argument("--no-key-host", dest="key_host", action="store_false",
+                   help="URL-only cache keys (the reference's, Server.py:327)")
+    p.add_argument("--max-inflate-mb", type=int, default=64,
+                   help="cap on any body the proxy inflates (identity variants for clients "
+                        "without gzip, --decode-gzip); larger bodies answer 502")
     p.add_argument("--health-check", default="", metavar="PATH",
                    help="actively probe every upstream with GET PATH (the reference's TODO "
                         "'check that servers are responsive', Server.py:532)")
@@ -270,6 +281,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  health_interval_ms=args.health_interval_ms, health_fails=args.health_fails,
                  cpus=parse_cpus(args.cpus), spin_us=args.spin_us,
                  gzip_gpu=args.gzip_gpu, gzip_batch_us=args.gzip_batch_us,
+                 max_inflate_bytes=args.max_inflate_mb << 20,
                  **({"fault": args.fault} if args.fault else {}),
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,

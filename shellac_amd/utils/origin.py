@@ -42,6 +42,23 @@ class Origin:
                     if not head:
                         self.wfile.write(body)
                     return
+                if path == "/badcl":  # malformed framing: the proxy must not pass it on
+                    self.send_response(200)
+                    self.send_header("Content-Length", "5x")
+                    self.end_headers()
+                    if not head:
+                        self.wfile.write(b"hello")
+                    return
+                if path.startswith("/bomb"):  # 64 MiB of zeros, ~64 KB gzipped
+                    z = outer.bomb()
+                    self.send_response(200)
+                    self.send_header("Content-Type", "text/html")
+                    self.send_header("Content-Encoding", "gzip")
+                    self.send_header("Content-Length", str(len(z)))
+                    self.end_headers()
+                    if not head:
+                        self.wfile.write(z)
+                    return
                 if path.startswith("/status/"):
                     code = int(path.split("/")[2])
                     body = f"status {code}\n".encode()
@@ -52,6 +69,11 @@ class Origin:
                         nb = int(path.rsplit("/", 1)[1])
                     body = (f"<html>{path} #{n} ".encode() + b"x" * nb + b"</html>\n")
                 headers = {"Content-Type": "text/html"}
+                if path.startswith("/vary/ua"):  # one variant per User-Agent
+                    headers["Vary"] = "User-Agent, Accept-Encoding"
+                    body = body.replace(b"</html>", f"ua={self.headers.get('User-Agent')}</html>".encode())
+                if path.startswith("/vary/star"):
+                    headers["Vary"] = "*"
                 if path.startswith("/nocache"):
                     headers["Cache-Control"] = "no-store"
                 if path.startswith("/cookie"):
@@ -106,6 +128,13 @@ class Origin:
         self._srv = S(("127.0.0.1", port), H)
         self.port = self._srv.server_address[1]
         self._th = threading.Thread(target=self._srv.serve_forever, daemon=True)
+
+    _bomb = None
+
+    def bomb(self) -> bytes:
+        if Origin._bomb is None:
+            Origin._bomb = gzip.compress(bytes(64 << 20), 9)
+        return Origin._bomb
 
     def start(self) -> "Origin":
         self._th.start()

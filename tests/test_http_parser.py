@@ -233,6 +233,56 @@ def test_malformed_raises():
         HttpParser().parse(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n")
 
 
+@pytest.mark.parametrize("head", [
+    b"POST / HTTP/1.1\r\nContent-Length: 12abc\r\n\r\n",           # trailing garbage
+    b"POST / HTTP/1.1\r\nContent-Length: -1\r\n\r\n",
+    b"POST / HTTP/1.1\r\nContent-Length: 3\r\nContent-Length: 4\r\n\r\n",  # conflicting
+    b"POST / HTTP/1.1\r\nContent-Length: 3, 4\r\n\r\n",
+    b"POST / HTTP/1.1\r\nTransfer-Encoding: gzip\r\n\r\n",       # no final chunked
+    b"POST / HTTP/1.1\r\nTransfer-Encoding: chunked, gzip\r\n\r\n",
+    b"POST / HTTP/1.1\r\nTransfer-Encoding: xchunked\r\n\r\n",   # not a substring match
+    b"POST / HTTP/1.1\r\nTransfer-Encoding: chunked\r\nContent-Length: 4\r\n\r\n",  # both
+])
+def test_ambiguous_request_framing_is_an_error(head):
+    """RFC 7230 §3.3.3: a request the proxy and the origin could frame differently is
+    rejected (the proxy answers 400), never guessed at."""
+    with pytest.raises(ValueError):
+        HttpParser().parse(head + b"abcd")
+
+
+def test_strict_framing_accepts_valid_forms():
+    # identical repeated Content-Length values and a chunked final coding are fine
+    p = parse_all(b"POST /a HTTP/1.1\r\nContent-Length: 3\r\nContent-Length: 3\r\n\r\nabc")[0]
+    assert p.body().read() == b"abc"
+    p = parse_all(b"POST /b HTTP/1.1\r\nTransfer-Encoding: Chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n")[0]
+    assert p.body().read() == b"abc"
+    # a response with both: transfer-encoding wins (RFC 7230 §3.3.3 rule 3)
+    p = HttpParser()
+    p.parse(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\nContent-Length: 99\r\n\r\n"
+            b"2\r\nhi\r\n0\r\n\r\n")
+    assert p.message_complete() and p.body().read() == b"hi"
+
+
+def test_gzip_body_with_pending_output_fully_inflated():
+    # 1 MiB of one byte gzips to ~1 KB: after the last input byte most of the output is
+    # still inside zlib and must be drained, not dropped
+    body = b"a" * (1 << 20)
+    z = gz(body)
+    p = HttpParser(decode_gzip=True)
+    p.parse(b"HTTP/1.1 200 OK\r\nContent-Encoding: gzip\r\nContent-Length: %d\r\n\r\n" % len(z) + z)
+    assert p.message_complete() and p.body().read() == body
+
+
+def test_decoded_gzip_body_is_capped():
+    """--decode-gzip inflates every gzip body: a decompression bomb fails the parse
+    instead of allocating the whole output."""
+    bomb = gz(bytes(80 << 20))  # 80 MiB of zeros, ~80 KB compressed
+    p = HttpParser(decode_gzip=True)
+    with pytest.raises(ValueError, match="too large"):
+        p.parse(b"HTTP/1.1 200 OK\r\nContent-Encoding: gzip\r\nContent-Length: %d\r\n\r\n"
+                % len(bomb) + bomb)
+
+
 # ---- StreamBufTests.py port -------------------------------------------------------
 def test_streambuf_reference_behaviour():
     s = StreamBuf()

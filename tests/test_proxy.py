@@ -59,14 +59,131 @@ def test_pipelined_order_mixed_hits_and_misses(origin):
         assert origin.hits["/a"] == 1 and origin.hits["/b"] == 1
 
 
-def test_gzip_passthrough_and_accept_encoding_forced(origin):
+def _raw_get(port, path, headers=b""):
+    """One request on a fresh connection; returns (head, raw body bytes) undecoded."""
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(b"GET " + path.encode() + b" HTTP/1.1\r\nHost: localhost\r\n" + headers +
+              b"Connection: close\r\n\r\n")
+    data = b""
+    while True:
+        d = s.recv(1 << 16)
+        if not d:
+            break
+        data += d
+    s.close()
+    head, _, body = data.partition(b"\r\n\r\n")
+    return head.decode("latin-1").lower(), body
+
+
+@pytest.mark.parametrize("first_gzip", [False, True])
+def test_content_negotiation_one_cached_gzip_variant(origin, first_gzip):
+    """The proxy forces Accept-Encoding: gzip upstream (Server.py:358) and caches the gzip
+    object once per URL; under --policy rfc a client that did not send Accept-Encoding:
+    gzip gets identity bytes, a gzip client gets gzip, from the same cache entry (either
+    client may lead the fetch)."""
+    import gzip as _gz
+
+    with make_proxy([origin.port]) as px:
+        order = [True, False] if first_gzip else [False, True]
+        for accepts in order + order:
+            head, body = _raw_get(px.port, "/gzpage", b"Accept-Encoding: gzip\r\n" if accepts else b"")
+            if accepts:
+                assert "content-encoding: gzip" in head
+                body = _gz.decompress(body)
+            else:
+                assert "content-encoding" not in head
+                assert f"content-length: {len(body)}" in head
+            assert body.startswith(b"<html>/gzpage #1 ")
+            assert "vary: accept-encoding" in head
+        assert origin.hits["/gzpage"] == 1
+        assert px.stats()["identity_decoded"] == 2
+
+
+def test_reference_policy_serves_the_forced_gzip_variant(origin):
+    """--policy reference keeps the reference's behaviour: the cached (gzip) object goes
+    to every client, whatever it accepts."""
+    with make_proxy([origin.port], policy="reference") as px:
+        for _ in range(2):
+            head, body = _raw_get(px.port, "/gzref")
+            assert "content-encoding: gzip" in head
+        assert origin.hits["/gzref"] == 1
+
+
+def test_compress_z_stores_gzip_and_negotiates(origin):
+    """-z under rfc: the stored variant is gzip whichever client leads the fetch; a
+    client without gzip gets identity from it."""
+    import gzip as _gz
+
+    with make_proxy([origin.port], compress=True) as px:
+        head, body = _raw_get(px.port, "/zneg.html")           # leader: no gzip
+        assert "content-encoding" not in head and body.startswith(b"<html>/zneg.html #1 ")
+        head, body = _raw_get(px.port, "/zneg.html", b"Accept-Encoding: gzip\r\n")
+        assert "content-encoding: gzip" in head
+        assert _gz.decompress(body).startswith(b"<html>/zneg.html #1 ")
+        assert origin.hits["/zneg.html"] == 1
+
+
+def test_vary_on_request_header_keys_variants(origin):
+    """A response that Varies on User-Agent is cached per User-Agent value (a marker under
+    the URL key names the headers); Vary: * is never cached."""
+    with make_proxy([origin.port]) as px:
+        a = HttpClient(port=px.port)
+        assert b"ua=alpha" in a.get("/vary/ua/1", headers={"User-Agent": "alpha"}).body().read()
+        assert b"ua=beta" in a.get("/vary/ua/1", headers={"User-Agent": "beta"}).body().read()
+        assert b"ua=alpha" in a.get("/vary/ua/1", headers={"User-Agent": "alpha"}).body().read()
+        assert b"ua=beta" in a.get("/vary/ua/1", headers={"User-Agent": "beta"}).body().read()
+        assert origin.hits["/vary/ua/1"] == 2
+        st = px.stats()
+        assert st["vary_stored"] == 2 and st["vary_hits"] == 2
+        a.get("/vary/star")
+        a.get("/vary/star")
+        assert origin.hits["/vary/star"] == 2
+
+
+def test_host_is_part_of_the_key_under_rfc(origin):
     with make_proxy([origin.port]) as px:
         c = HttpClient(port=px.port)
-        r = c.get("/gzpage")  # origin gzips because the proxy forces Accept-Encoding: gzip
-        assert r.headers().get("content-encoding") == "gzip"
-        assert b"/gzpage #1" in r.body().read()  # client parser inflates
-        r = c.get("/gzpage")
-        assert b"/gzpage #1" in r.body().read()
+        c.get("/vh", host="a.example")
+        c.get("/vh", host="b.example")
+        c.get("/vh", host="a.example")
+        assert origin.hits["/vh"] == 2
+    with make_proxy([origin.port], policy="reference") as px:  # URL-only, like Server.py:327
+        c = HttpClient(port=px.port)
+        c.get("/vh2", host="a.example")
+        c.get("/vh2", host="b.example")
+        assert origin.hits["/vh2"] == 1
+
+
+@pytest.mark.parametrize("req", [
+    b"POST /x HTTP/1.1\r\nHost: a\r\nContent-Length: 12abc\r\n\r\nhello",
+    b"POST /x HTTP/1.1\r\nHost: a\r\nContent-Length: 5\r\nContent-Length: 6\r\n\r\nhello",
+    b"POST /x HTTP/1.1\r\nHost: a\r\nTransfer-Encoding: gzip\r\n\r\nhello",
+    b"POST /x HTTP/1.1\r\nHost: a\r\nTransfer-Encoding: chunked\r\nContent-Length: 5\r\n\r\n"
+    b"5\r\nhello\r\n0\r\n\r\n",
+])
+def test_ambiguous_framing_gets_400(origin, req):
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        c.send(req)
+        assert c.read_response().status() == 400
+        assert c.closed_by_peer()
+        assert origin.hits["POST /x"] == 0
+
+
+def test_bad_upstream_framing_and_inflate_cap(origin):
+    """An upstream answer with malformed framing is a bad gateway (not relayed); a gzip
+    object whose identity variant would exceed --max-inflate is a 502 for a client without
+    gzip, while gzip clients still get it; --decode-gzip bodies are capped the same way."""
+    with make_proxy([origin.port], max_inflate_bytes=1 << 20) as px:
+        c = HttpClient(port=px.port)
+        assert c.get("/badcl").status() == 502
+        head, body = _raw_get(px.port, "/bomb", b"Accept-Encoding: gzip\r\n")
+        assert head.startswith("http/1.1 200") and len(body) < (1 << 20)
+        head, _ = _raw_get(px.port, "/bomb")
+        assert head.startswith("http/1.1 502")
+    with make_proxy([origin.port], decode_gzip=True, max_inflate_bytes=1 << 20) as px:
+        head, _ = _raw_get(px.port, "/bomb2", b"Accept-Encoding: gzip\r\n")
+        assert head.startswith("http/1.1 502")
 
 
 def test_chunked_upstream_dechunked(origin):
@@ -387,11 +504,12 @@ def test_native_origin_behind_proxy():
         assert b"<html>/y #1 " in rs[1].body().read()
         with make_proxy([o.port]) as px:
             c = HttpClient(port=px.port)
-            r = c.get("/gz/obj1.html")
+            r = c.get("/gz/obj1.html", headers={"Accept-Encoding": "gzip"})
             assert r.headers().get("content-encoding") == "gzip"
             assert b"/gz/obj1.html #1" in r.body().read()
             before = o.requests
-            r = c.get("/gz/obj1.html")  # hit: the origin sees nothing
+            r = c.get("/gz/obj1.html")  # hit (identity variant): the origin sees nothing
+            assert r.headers().get("content-encoding") is None
             assert b"/gz/obj1.html #1" in r.body().read()
             assert o.requests == before
             assert px.stats()["cache_hits"] == 1
