@@ -211,7 +211,8 @@ struct HbmBackend::Dev {
   // stats
   std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
       filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
-      key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, dropped{0},
+      key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, arena_misses{0},
+      dropped{0},
       migrated{0}, migrate_ns{0};
 
   void loop();
@@ -220,6 +221,7 @@ struct HbmBackend::Dev {
   bool try_reap(Flight& f, bool block);
   void deliver_gets(Flight& f);
   void deliver_dels(Flight& f);
+  void overflow_misses(Flight& f);
   void fail_flight(Flight& f);
   void fail_requests(std::vector<Req>& reqs);
   void eject(const char* why);
@@ -684,18 +686,31 @@ bool HbmBackend::Dev::try_reap(Flight& f, bool block) {
                                  : cache->host_slot(f.slot);
     if (total == HbmCache::kSlotPending) return false;
     if (total == HbmCache::kSlotFailed) throw Error("edge GET reported a failed look-back");
-    if (total > f.arena->cap) {  // rare: the records outgrew the arena; gather again
-      regathers++;
-      HB_OK(hipEventSynchronize(f.ev));
-      f.arena = pool->take(total + (64u << 10));
-      cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
-                       f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
-      HB_OK(hipEventRecord(f.ev, stream));
-      const uint64_t t2 = cache->wait_host_slot(f.slot, be->cfg_.batch_timeout_ms);
-      SH_CHECK(t2 == total, "regather size changed");
-    }
     if (f.rows) avg_row_bytes = 0.9 * avg_row_bytes + 0.1 * ((double)total / (double)f.rows);
-    deliver_gets(f);
+    if (total > f.arena->cap) {
+      // Rare: the records outgrew the arena (the kernel wrote none of them). A second
+      // lookup sees exactly the first one's state only when nothing has run since: no
+      // SET/DELETE in this flight and no later flight queued on the stream. Otherwise the
+      // GETs answer "miss" (always a valid cache answer: the proxy goes to the origin);
+      // reading a newer state would reorder them after later SETs.
+      if (f.sets.empty() && f.dels.empty() && inflight == 1) {
+        regathers++;
+        HB_OK(hipEventSynchronize(f.ev));
+        f.arena = pool->take(total + (64u << 10));
+        cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
+                         f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
+        HB_OK(hipEventRecord(f.ev, stream));
+        const uint64_t t2 = cache->wait_host_slot(f.slot, be->cfg_.batch_timeout_ms);
+        if (t2 == HbmCache::kSlotPending || t2 == HbmCache::kSlotFailed)
+          throw Error("edge GET regather failed");
+        if (t2 > f.arena->cap) overflow_misses(f);  // cannot happen: state unchanged
+        else deliver_gets(f);
+      } else {
+        overflow_misses(f);
+      }
+    } else {
+      deliver_gets(f);
+    }
     f.got = true;
   }
   if (block) {
@@ -769,6 +784,14 @@ void HbmBackend::Dev::deliver_gets(Flight& f) {
       cb(hit, std::move(v));
   }
   pg.flush();
+}
+
+// Every GET of flight f answers "miss" (its records did not fit the arena).
+void HbmBackend::Dev::overflow_misses(Flight& f) {
+  arena_misses += f.gets.size();
+  std::vector<Req> gets;
+  for (uint32_t i : f.gets) gets.push_back(std::move(f.reqs[i]));
+  fail_requests(gets);
 }
 
 void HbmBackend::Dev::deliver_dels(Flight& f) {
@@ -1099,6 +1122,7 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_ejections", sum(&Dev::ejections));
   out->emplace_back("hbm_restores", sum(&Dev::restores));
   out->emplace_back("hbm_regathers", sum(&Dev::regathers));
+  out->emplace_back("hbm_arena_misses", sum(&Dev::arena_misses));
   out->emplace_back("hbm_migrated", sum(&Dev::migrated));
   out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));

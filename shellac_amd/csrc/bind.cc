@@ -290,12 +290,13 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("store", [](HostCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
-                       uint32_t now) {
+                       uint32_t now, uint64_t bytes_bound) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
-                now);
-      })
+                now, bytes_bound);
+      }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"), py::arg("flags"),
+         py::arg("expire"), py::arg("n"), py::arg("now"), py::arg("bytes_bound") = 0)
       .def("remove", [](HostCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now) {
         py::gil_scoped_release nogil;
         c.remove(P<const Digest>(keys), n, P<uint8_t>(found), now);

@@ -141,7 +141,7 @@ bool HostCache::insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uin
 
 void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                       const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                      int64_t n, uint32_t now) {
+                      int64_t n, uint32_t now, uint64_t bytes_bound) {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<Row> rows;
   std::vector<uint8_t> stage;
@@ -149,8 +149,14 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
     uint64_t bytes = 0;  // the batch's bytes (dedupe losers included), as the device
     for (int64_t i = 0; i < n; ++i)
       if (vlen[i] != kSkipVlen && vlen[i] <= max_item_) bytes += item_bytes(vlen[i]);
+    // the reinsertions share the half-log bound with the batch, capped exactly as
+    // HbmCache::store caps them (same bound in, same decisions out)
+    uint64_t bound = bytes_bound ? std::max(bytes_bound, bytes) : bytes;
+    if (bound > log_bytes_ / 2) bound = bytes;  // (the device refuses such a bound)
+    SH_CHECK(bound <= log_bytes_ / 2, "SET batch larger than half the log; split the batch");
+    const uint64_t rmax = std::min<uint64_t>(rmax_, log_bytes_ / 2 - bound) / 16 * 16;
     // the device's combined batch: reinsertions (in log order) ahead of the batch
-    reclaim_locked(n, bytes, now, &rows, &stage);
+    if (rmax) reclaim_locked(n, bytes, rmax, now, &rows, &stage);
   }
   rows.reserve(rows.size() + (size_t)n);
   for (int64_t i = 0; i < n; ++i)
@@ -159,7 +165,8 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
   store_rows_locked(rows, now);
 }
 
-void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vector<Row>* out,
+void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_t now,
+                               std::vector<Row>* out,
                                std::vector<uint8_t>* stage) {
   const int64_t w = hand_window(n);
   const uint64_t rcap = ring_.size(), rmask = rcap - 1;
@@ -176,7 +183,7 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vec
     std::memcpy(&h, log_ + l % log_bytes_, sizeof h);
     if (h.magic != kItemMagic) continue;
     // stop at the first item the overwrite (batch + reinsertions so far) does not reach
-    if (l + log_bytes_ >= head_ + bytes + std::min(hx, rmax_)) {
+    if (l + log_bytes_ >= head_ + bytes + std::min(hx, rmax)) {
       consumed = j;
       break;
     }
@@ -195,10 +202,10 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vec
   out->clear();
   uint64_t staged = 0;
   for (const Hot& t : hot)
-    if ((uint64_t)t.j < consumed && t.hx + t.h <= rmax_) staged = t.hx + t.h;
+    if ((uint64_t)t.j < consumed && t.hx + t.h <= rmax) staged = t.hx + t.h;
   stage->assign(staged + 16, 0);
   for (const Hot& t : hot) {
-    if ((uint64_t)t.j >= consumed || t.hx + t.h > rmax_) continue;
+    if ((uint64_t)t.j >= consumed || t.hx + t.h > rmax) continue;
     const uint8_t* rec = log_ + t.loc % log_bytes_;
     std::memcpy(stage->data() + t.hx, rec, t.h);
     ItemHeader h;

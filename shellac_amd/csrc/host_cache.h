@@ -28,7 +28,7 @@ class HostCache {
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out) const;
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
-             uint32_t now);
+             uint32_t now, uint64_t bytes_bound = 0);  // 0: the batch's exact bytes
   void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now);
   void sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes);
   void flush();
@@ -66,8 +66,8 @@ class HostCache {
   // CLOCK hand step ahead of a batch of `bytes` log bytes over `n` rows (the device
   // algorithm, sequentially): appends the reinsertion rows to `out`, their records
   // staged in `stage`.
-  void reclaim_locked(int64_t n, uint64_t bytes, uint32_t now, std::vector<Row>* out,
-                      std::vector<uint8_t>* stage);
+  void reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_t now,
+                      std::vector<Row>* out, std::vector<uint8_t>* stage);
 
   uint64_t log_bytes_, nbuckets_, mask_;
   uint32_t max_item_;

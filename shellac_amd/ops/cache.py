@@ -440,14 +440,15 @@ class CacheShard:
         now = self.now() if now is None else now
         fp = 0 if flags is None else flags.data_ptr()
         ep = 0 if expire is None else expire.data_ptr()
+        # the same bound on both twins: the CLOCK hand's reinsertion cap follows from it
+        bound = (self.payload_bound(n, values.numel()) if bytes_bound is None
+                 else int(bytes_bound))
         if self.is_gpu:
-            bound = (self.payload_bound(n, values.numel()) if bytes_bound is None
-                     else int(bytes_bound))
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(), _event_handle(index_after))
         else:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
-                             fp, ep, n, now)
+                             fp, ep, n, now, bound)
 
     def set_many(self, keys: Sequence[bytes], values: Sequence[bytes], ttl: int = 0,
                  flags: int = 0) -> None:

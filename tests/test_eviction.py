@@ -81,3 +81,32 @@ def test_clock_reinserted_values_intact_gpu(cuda_dev):
     assert [r[0] if r else None for r in recs] == hv
     assert all(r[1] == 77 for r in recs)
     assert s.counters()["reinserted"] >= 16
+
+
+def _big_batch_run(dev):
+    """SET batches between a quarter and a half of the log, with read (hot) objects the
+    hand must carry: the reinsertion budget is capped by what the batch leaves of the
+    half-log bound, identically on both twins (the host twin used the full
+    budget and refused such batches)."""
+    s = CacheShard(1 << 20, 1 << 12, 1 << 14, dev)
+    hot = [b"/bb/hot/%d" % i for i in range(100)]
+    s.set_many(hot, [b"h" * 1500] * 100)
+    hits = []
+    for lap in range(8):
+        got = s.get_many(hot)
+        hits.append(sum(g is not None for g in got))
+        ks = [b"/bb/fill/%d/%d" % (lap, i) for i in range(190)]   # ~380 KB per batch
+        s.set_many(ks, [b"f" * 1950] * 190)
+    c = s.counters()
+    return hits, c["reinserted"], s.head()
+
+
+def test_clock_batch_over_quarter_log_host():
+    hits, reins, head = _big_batch_run("cpu")
+    assert reins > 0 and head > 2 * (1 << 20)
+    assert hits[0] == 100
+
+
+@pytest.mark.gpu
+def test_clock_batch_over_quarter_log_gpu_matches_host(cuda_dev):
+    assert _big_batch_run(cuda_dev) == _big_batch_run("cpu")
