@@ -38,58 +38,71 @@ void bind_router(py::module_& m) {
       .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot, uintptr_t dir) {
         r.set_hot(P<const Digest>(hot), nhot, P<const int64_t>(dir));
       }, py::arg("hot"), py::arg("nhot"), py::arg("dir") = 0)
+      .def_property_readonly("row_words", &RoutedStep::row_words)
+      .def("caps", &RoutedStep::caps)
+      .def("reset_caps", &RoutedStep::reset_caps)
+      .def("set_cap_override", &RoutedStep::set_cap_override)
       .def("plan", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
                       uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,
-                      uintptr_t table, uintptr_t s, bool coalesce) {
+                      uintptr_t G, uintptr_t row, uintptr_t s, bool coalesce) {
         py::gil_scoped_release nogil;
         r.plan(P<const Digest>(keys), n, replica, now, P<const Digest>(skeys),
                P<const uint32_t>(svlen), P<const uint32_t>(sflags), P<const uint32_t>(sexpire),
                P<const uint64_t>(sval_off), P<const uint8_t>(svalues), ns, fanout,
-               P<int64_t>(table), S(s), coalesce);
+               P<uint8_t>(G), P<int64_t>(row), S(s), coalesce);
       }, py::arg("keys"), py::arg("n"), py::arg("replica").none(true), py::arg("now"),
          py::arg("skeys"), py::arg("svlen"), py::arg("sflags"), py::arg("sexpire"),
          py::arg("sval_off"), py::arg("svalues"), py::arg("ns"), py::arg("fanout"),
-         py::arg("table"), py::arg("stream"), py::arg("coalesce") = false)
-      .def("read_counts", [](RoutedStep& r, uintptr_t rtable, uintptr_t s) {
+         py::arg("G"), py::arg("row"), py::arg("stream"), py::arg("coalesce") = false)
+      .def("publish", [](RoutedStep& r, uintptr_t mat, uintptr_t s) {
         py::gil_scoped_release nogil;
-        return r.read_counts(P<const int64_t>(rtable), S(s));
+        r.publish(P<const int64_t>(mat), S(s));
       })
-      .def("pack", [](RoutedStep& r, uintptr_t send, uintptr_t s) {
+      .def("calibrate_local", [](RoutedStep& r) {
         py::gil_scoped_release nogil;
-        r.pack(P<uint8_t>(send), S(s));
+        r.calibrate_local();
       })
-      .def("owner", [](RoutedStep& r, uintptr_t recv, HbmCache* shard, uint32_t now,
-                       uintptr_t sizes_out, uintptr_t s) {
+      .def("owner_probe", [](RoutedStep& r, uintptr_t G, HbmCache* shard, uint32_t now,
+                             uintptr_t s) {
         py::gil_scoped_release nogil;
-        r.owner(P<const uint8_t>(recv), shard, now, P<uint64_t>(sizes_out), S(s));
+        r.owner_probe(P<const uint8_t>(G), shard, now, S(s));
       })
-      .def("reply_sizes", [](RoutedStep& r, uintptr_t sizes_in, uintptr_t s) {
-        py::gil_scoped_release nogil;
-        return r.reply_sizes(P<const uint64_t>(sizes_in), S(s));
+      .def("owner_demand", [](RoutedStep& r, uintptr_t out, uintptr_t s) {
+        r.owner_demand(P<int64_t>(out), S(s));
       })
-      .def("gather_replies", [](RoutedStep& r, HbmCache* shard, uintptr_t reply, uintptr_t s) {
+      .def("calibrate_reply", [](RoutedStep& r, uintptr_t dmat) {
         py::gil_scoped_release nogil;
-        r.gather_replies(shard, P<uint8_t>(reply), S(s));
+        r.calibrate_reply(P<const int64_t>(dmat));
       })
-      .def("finish", [](RoutedStep& r, uintptr_t data, uintptr_t recv, int64_t recv_bytes,
-                        HbmCache* shard, HbmCache* replica, uint32_t now, uintptr_t out_size,
-                        uintptr_t out_off, uintptr_t s) {
+      .def("owner_reply", [](RoutedStep& r, HbmCache* shard, uintptr_t R, uintptr_t data,
+                             uintptr_t s) {
         py::gil_scoped_release nogil;
-        r.finish(P<uint8_t>(data), P<const uint8_t>(recv), recv_bytes, shard, replica, now,
-                 P<uint64_t>(out_size), P<uint64_t>(out_off), S(s));
-      }, py::arg("data"), py::arg("recv"), py::arg("recv_bytes"), py::arg("shard"),
-         py::arg("replica").none(true), py::arg("now"), py::arg("out_size"), py::arg("out_off"),
-         py::arg("stream"))
-      .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
+        r.owner_reply(shard, P<uint8_t>(R), P<uint8_t>(data), S(s));
+      })
       .def("gather_local", [](RoutedStep& r, uintptr_t data, uintptr_t s) {
         py::gil_scoped_release nogil;
         r.gather_local(P<uint8_t>(data), S(s));
       })
-      .def("join_local", [](RoutedStep& r, uintptr_t s) { r.join_local(S(s)); })
-      .def("set_defer_join", &RoutedStep::set_defer_join)
-      .def_property_readonly("sets_pending", &RoutedStep::sets_pending)
-      .def_property_readonly("mg", &RoutedStep::mg)
-      .def_property_readonly("ms", &RoutedStep::ms)
-      .def_property_readonly("n_local", &RoutedStep::n_local);
+      .def("set_splits", [](RoutedStep& r) {
+        py::gil_scoped_release nogil;
+        return r.set_splits();
+      })
+      .def("pack_sets", [](RoutedStep& r, uintptr_t Sb, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        r.pack_sets(P<uint8_t>(Sb), S(s));
+      })
+      .def("store_sets", [](RoutedStep& r, uintptr_t Sb, uintptr_t Rs, HbmCache* shard,
+                            HbmCache* replica, uint32_t now, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        r.store_sets(P<const uint8_t>(Sb), P<const uint8_t>(Rs), shard, replica, now, S(s));
+      }, py::arg("S"), py::arg("Rs"), py::arg("shard"), py::arg("replica").none(true),
+         py::arg("now"), py::arg("stream"))
+      .def("assemble", [](RoutedStep& r, uintptr_t data, uintptr_t out_size, uintptr_t out_off,
+                          uintptr_t s) {
+        py::gil_scoped_release nogil;
+        r.assemble(P<const uint8_t>(data), P<uint64_t>(out_size), P<uint64_t>(out_off), S(s));
+      })
+      .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
+      .def_property_readonly("sets_pending", &RoutedStep::sets_pending);
 }

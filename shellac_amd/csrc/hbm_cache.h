@@ -69,6 +69,12 @@ class HbmCache {
                         uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
                         uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
                         uint32_t* cslot = nullptr, bool table_clean = false);
+  // Slotted lookup (the routed step's owner side): nslots x slot_rows rows, slot k's
+  // rows [k * slot_rows, k * slot_rows + slot_cnt[k]) are requests, the rest padding
+  // (size 0, not probed, not counted). off = exclusive scan over all rows.
+  void lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_rows,
+                    const int64_t* slot_cnt, uint64_t* loc, uint64_t* size, uint64_t* off,
+                    uint32_t now, hipStream_t s);
   uint64_t host_slot(int i) const;
   // Spin until the lookup that was given `total_slot` i has written it (no stream or
   // event synchronisation: the kernel's system-scope store is the signal). Throws after
@@ -221,6 +227,12 @@ size_t device_scan_tmp_bytes(int64_t n);
 // from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
              uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
+// Sized variant: segment i holds seg_len[i] bytes at dst + dst_off[i] (dst_off ascending,
+// gaps allowed and left untouched, dst_off[n] = the extent); a segment that does not end
+// within `cap` is dropped (the others still land). Offsets / lengths multiples of 16.
+void segcopy_sized(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
+                   const uint64_t* seg_len, int64_t n, uint8_t* dst, hipStream_t s,
+                   uint64_t cap = ~0ull);
 
 // GET coalescing: first[i] = the row that serves row i (one row per distinct digest
 // serves all its duplicates). `table` is scratch of coalesce_table_slots(n) u32 words.

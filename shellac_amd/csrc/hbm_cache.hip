@@ -57,58 +57,20 @@ namespace shellac {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTileChunks = 4096;          // 16-B chunks per segcopy tile (64 KiB)
 constexpr int kTileSegCap = 1024;          // segments staged in LDS per tile
 constexpr int kMaxGrid = 2048;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// SHELLAC_COALESCE_LOCAL=1: the coalescing lookup collapses duplicates inside each
-// 1024-key chunk only (no global table atomics); an A/B knob, see docs/PERF.md.
-int coalesce_local_only() {
-  static const int v = [] {
-    const char* e = getenv("SHELLAC_COALESCE_LOCAL");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
-// Grid caps for k_probe / k_coalesce (tuning knobs: SHELLAC_PROBE_GRID,
-// SHELLAC_COALESCE_GRID; 0 = the defaults below).
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
-int probe_grid_cap() {
-  static const int v = env_int("SHELLAC_PROBE_GRID", 0);
-  return v > 0 ? v : kMaxGrid;
-}
-int coalesce_grid_cap() {
-  static const int v = env_int("SHELLAC_COALESCE_GRID", 0);
-  return v > 0 ? std::min(v, kMaxGrid) : kMaxGrid;
-}
-
-// Smallest segcopy tile in 16-B chunks (16 KiB); SHELLAC_SEGCOPY_MIN_TILE overrides it
-// for tuning sweeps (benchmarks/kernel_bench.py).
-// Variant (loads in flight per lane, target waves/SIMD); SHELLAC_SEGCOPY_VARIANT selects
-// one for tuning (launch_segcopy lists them); default 1 = 4 loads / 8 waves with
-// nontemporal stores (A/B in scripts/nt_ab.sh: -3.5% gather time vs 6 = plain stores).
-int segcopy_variant() {
-  static const int v = [] {
-    const char* e = getenv("SHELLAC_SEGCOPY_VARIANT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-int min_tile_chunks() {
-  static const int v = [] {
-    const char* e = getenv("SHELLAC_SEGCOPY_MIN_TILE");
-    int t = e ? atoi(e) : 1024;
-    t = (t + kBlock - 1) / kBlock * kBlock;
-    return t < kBlock ? kBlock : (t > kTileChunks ? kTileChunks : t);
-  }();
-  return v;
-}
+// Tuned constants (round-2 sweeps, profiles/r1_probe_grid_sweep.log,
+// r1_segcopy_store_ab.log, r1_overlap_sweep.log; the A/B knobs are gone):
+//  * k_probe / k_coalesce grids cap at kMaxGrid workgroups (halving the grid nearly
+//    doubled a 1M-key probe: it is bound by random lines in flight);
+//  * segcopy: 4 x 16-B loads in flight per lane, 8 waves/SIMD, nontemporal stores
+//    (-3.5 % gather time against plain stores), a 16 KiB minimum tile, and 48/64 of the
+//    co-resident slots so a concurrent SET chain gets CUs (a gather at 3/4 of the slots is
+//    as fast as at all of them: memory-bound).
+constexpr int kSegMinTile = 1024;  // 16-B chunks
+constexpr int kSegOcc64 = 48;
 
 struct DeviceGuard {
   int prev = -1;
@@ -423,7 +385,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                   uint64_t* __restrict__ out_size,
                                                   CacheCounters* __restrict__ ctr,
                                                   uint64_t* __restrict__ part,
-                                                  const uint32_t* __restrict__ first) {
+                                                  const uint32_t* __restrict__ first,
+                                                  int64_t slot_rows,
+                                                  const int64_t* __restrict__ slot_cnt) {
   const int l8 = threadIdx.x & 7;
   // `reserve`: bytes about to be appended before this lookup's gather runs; objects
   // that those appends will overwrite are already treated as evicted
@@ -445,7 +409,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     const int cnt = (int)min((int64_t)kProbeTile, i1 - t0);
     for (int k = threadIdx.x; k < cnt; k += kBlock) {
       s_k[k] = keys[t0 + k];
-      s_go[k] = !first || first[t0 + k] == (uint32_t)(t0 + k);  // duplicates skip
+      const int64_t i = t0 + k;
+      // duplicates skip; in a slotted batch (slot_cnt) rows past their slot's count are
+      // padding and skip too (answered as misses, not counted)
+      s_go[k] = (!first || first[i] == (uint32_t)i) &&
+                (!slot_cnt || i % slot_rows < slot_cnt[i / slot_rows]);
     }
     __syncthreads();
     for (int q0 = threadIdx.x >> 3; q0 < cnt; q0 += kG * kCoProbe) {
@@ -817,6 +785,10 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
 }
 
 // Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w.
+// Mode 2 (sized gather): as mode 0, but segment j holds only seg_len[j] bytes (passed in
+// the `head_ptr` slot) and is copied only when it ends within `cap`; the bytes between a
+// segment's end and the next segment's start are left untouched (gaps, headers written
+// by someone else), and segments past `cap` are dropped instead of the whole copy.
 // Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
 // src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w, where
 // the batch is at most cap/2 so the modulo is one compare against the wrap point.
@@ -834,14 +806,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
     const uint64_t* __restrict__ head_ptr, uint64_t cap, int min_tile) {
-  __shared__ uint64_t s_off[kTileSegCap + 1];
-  __shared__ uint64_t s_src[kTileSegCap];
+  // mode 2 stages a length per segment too: fewer segments per pass keep 8 waves/SIMD
+  constexpr int TSC = MODE == 2 ? 768 : kTileSegCap;
+  __shared__ uint64_t s_off[TSC + 1];
+  __shared__ uint64_t s_src[TSC];
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
   const uint64_t total = dst_off[n];
   if (MODE == 0 && total > cap) return;  // MODE 0: `cap` = destination capacity
+  const uint64_t* __restrict__ seg_len = MODE == 2 ? head_ptr : nullptr;
+  __shared__ uint32_t s_len[MODE == 2 ? TSC : 1];  // records < 4 GiB
   const int64_t nchunks = (int64_t)(total >> 4);
   const uint64_t base = MODE == 1 ? *head_ptr % cap : 0;
+  (void)s_len;
   int64_t span = (nchunks + gridDim.x - 1) / gridDim.x;
   span = (span + kBlock - 1) & ~(int64_t)(kBlock - 1);
   if (span < min_tile) span = min_tile;
@@ -850,11 +827,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   if (r0 >= r1) return;
   block_find2(dst_off, n + 1, (uint64_t)r0 << 4, ((uint64_t)r1 << 4) - 1, s_lo, s_hi, s_cnt);
   const int64_t ja = s_lo[0], jb = s_lo[1];
-  for (int64_t j0 = ja; j0 <= jb; j0 += kTileSegCap) {
-    const int cnt = (int)min((int64_t)kTileSegCap, jb - j0 + 1);
+  for (int64_t j0 = ja; j0 <= jb; j0 += TSC) {
+    const int cnt = (int)min((int64_t)TSC, jb - j0 + 1);
     __syncthreads();  // previous pass done with s_off / s_src (and s_lo read above)
     for (int k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
     for (int k = threadIdx.x; k < cnt; k += kBlock) s_src[k] = src_off[j0 + k];
+    if (MODE == 2)
+      for (int k = threadIdx.x; k < cnt; k += kBlock) {
+        const uint64_t st = dst_off[j0 + k], ln = seg_len[j0 + k];
+        s_len[k] = st + ln <= cap ? (uint32_t)ln : 0u;  // past the capacity: dropped
+      }
     __syncthreads();
     const int64_t c0 = max(r0, (int64_t)(s_off[0] >> 4));
     const int64_t c1 = min(r1, (int64_t)(s_off[cnt] >> 4));
@@ -885,7 +867,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const uint64_t seg_start = s_off[jl];
         const uint64_t seg_src = s_src[jl];
         const uint64_t w = x - seg_start;
-        if (MODE == 0) {
+        if (MODE == 2) {
+          if (x < seg_start || w >= s_len[jl]) continue;  // gap / dropped: untouched
+          sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
+        } else if (MODE == 0) {
           // integer address math: src may be null with absolute addresses in src_off
           sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
         } else {
@@ -910,7 +895,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
-        if (c >= c1) continue;
+        if (c >= c1 || (MODE == 2 && !sp[u])) continue;
         const uint64_t d = MODE == 1 ? dofs[MODE == 1 ? u : 0] : (uint64_t)c << 4;
         if (NTSTORE)
           __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + d));
@@ -936,40 +921,14 @@ int resident_grid(K kernel, int* cache) {
   return cache[dev];
 }
 
-// Share of the co-resident slots a segcopy grid takes, in 1/64ths (64 = all of them).
-// Below 64 the byte mover leaves room for latency-bound kernels queued concurrently
-// on another stream (the SET chain during a GET gather); SHELLAC_SEGCOPY_OCC overrides.
-int segcopy_occ64() {
-  static const int v = [] {
-    const char* e = getenv("SHELLAC_SEGCOPY_OCC");
-    // 48/64: a gather at 3/4 of the slots is as fast as at all of them (memory-bound),
-    // and the rest lets a concurrent SET chain through (scripts/overlap_sweep.sh)
-    const int o = e ? atoi(e) : 48;
-    return o < 8 ? 8 : (o > 64 ? 64 : o);
-  }();
-  return v;
-}
-
-template <int MODE, int U, int WAVES, bool NT = false, typename... Args>
-void launch_segcopy_v(hipStream_t s, Args... args) {
-  static int grid[64];
-  const auto kern = k_segcopy<MODE, U, WAVES, NT>;
-  const int g = std::max(1, resident_grid(kern, grid) * segcopy_occ64() / 64);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., min_tile_chunks());
-}
-
+// The byte mover's launch: 4 loads in flight per lane, 8 waves/SIMD, nontemporal stores,
+// kSegOcc64/64 of the co-resident slots (see the tuned constants above).
 template <int MODE, typename... Args>
 void launch_segcopy(hipStream_t s, Args... args) {
-  switch (segcopy_variant()) {
-    case 0: launch_segcopy_v<MODE, 8, 4>(s, args...); break;
-    case 2: launch_segcopy_v<MODE, 6, 6>(s, args...); break;
-    case 3: launch_segcopy_v<MODE, 2, 8>(s, args...); break;
-    case 4: launch_segcopy_v<MODE, 8, 6>(s, args...); break;
-    case 5: launch_segcopy_v<MODE, 16, 4>(s, args...); break;
-    case 6: launch_segcopy_v<MODE, 4, 8, false>(s, args...); break;
-    case 7: launch_segcopy_v<MODE, 8, 5, true>(s, args...); break;
-    default: launch_segcopy_v<MODE, 4, 8, true>(s, args...);
-  }
+  static int grid[64];
+  const auto kern = k_segcopy<MODE, 4, 8, true>;
+  const int g = std::max(1, resident_grid(kern, grid) * kSegOcc64 / 64);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., kSegMinTile);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1811,6 +1770,14 @@ void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_of
   HIP_OK(hipGetLastError());
 }
 
+void segcopy_sized(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
+                   const uint64_t* seg_len, int64_t n, uint8_t* dst, hipStream_t s, uint64_t cap) {
+  if (n <= 0) return;
+  launch_segcopy<2>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr,
+                    seg_len, cap);
+  HIP_OK(hipGetLastError());
+}
+
 int64_t coalesce_table_slots(int64_t n) {
   int64_t t = 1024;
   while (t < 2 * n) t <<= 1;
@@ -2067,11 +2034,31 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
     if (ht) *ht = 0;
     return;
   }
-  const int grid = grid_for(n * 8, kBlock, std::min(kMaxGrid, probe_grid_cap()));
+  const int grid = grid_for(n * 8, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
-                     cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first);
+                     cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first,
+                     (int64_t)1, (const int64_t*)nullptr);
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht);
+}
+
+void HbmCache::lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_rows,
+                            const int64_t* slot_cnt, uint64_t* loc, uint64_t* size, uint64_t* off,
+                            uint32_t now, hipStream_t s) {
+  TraceRange tr("hbm.lookup_slots");
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  const int64_t n = nslots * slot_rows;
+  if (n <= 0) {
+    HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
+    return;
+  }
+  const int grid = grid_for(n * 8, kBlock, kMaxGrid);
+  hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
+                     cur_head(), (uint64_t)0, cfg_.log_bytes, now, loc, size, ctr_, part_,
+                     (const uint32_t*)nullptr, slot_rows, slot_cnt);
+  HIP_OK(hipGetLastError());
+  launch_offsets(size, n, part_, grid, off, s, nullptr);
 }
 
 void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
@@ -2096,7 +2083,7 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
   // contiguous whole chunks per workgroup, at most kMaxGrid partial sums
   const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
-  const int64_t per = (chunks + coalesce_grid_cap() - 1) / coalesce_grid_cap();
+  const int64_t per = (chunks + kMaxGrid - 1) / kMaxGrid;
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
   // (fusing the offsets scan into this kernel — by decoupled look-back, or by one bump
@@ -2105,7 +2092,7 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
-                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, coalesce_local_only());
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, 0);
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht, plen);
 }

@@ -91,14 +91,10 @@ inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
 // steady-state N=1 step 0.91 ms at a 5 GiB log and 0.41 ms at 16 GiB, k = 2 0.51 / 0.37
 // ms with the same hit ratio and reinsertions (profiles/r2_hand_window_ab.log); the
 // evict_sim hit ratios are identical for k = 2, 3, 4; k = 1 does not cover the batch's own
-// bytes and degrades to FIFO. SHELLAC_HAND_WINDOW=k overrides (1..16), both engines alike.
+// bytes and degrades to FIFO.
+constexpr int64_t kHandWindowK = 2;
 inline int64_t hand_window(int64_t n) {
-  static const int64_t k = [] {
-    const char* e = std::getenv("SHELLAC_HAND_WINDOW");
-    const long v = e ? std::atol(e) : 2;
-    return (int64_t)(v < 1 ? 1 : (v > 16 ? 16 : v));
-  }();
-  const int64_t w = k * n + 256;
+  const int64_t w = kHandWindowK * n + 256;
   return w < (1 << 20) ? w : (1 << 20);
 }
 inline uint64_t ring_entries(uint64_t nbuckets) {

@@ -42,23 +42,44 @@ int64_t scan_parts_words(int64_t n);
 
 class HbmCache;
 
-// The routed serving step of one rank as a native executor: ShardedCache keeps only
-// the five collectives (torch.distributed -> RCCL) and hands every buffer in between
-// to this object, which keeps its scratch in a grow-only device arena (no allocator
-// traffic per step) and reads the two host-visible results (per-peer counts, reply
-// byte splits) through pinned memory with one stream sync each.
+// The routed serving step of one rank as a native executor, device-driven: no host sync
+// between plan and finish. ShardedCache issues the collectives (torch.distributed ->
+// RCCL) and hands every buffer in between to this object, which keeps its scratch in a
+// grow-only device arena.
 //
-// Call order per step (stream-ordered on `s`):
-//   plan -> [a2a table -> rtable] -> read_counts -> pack(send)
-//   -> [a2a send request region -> recv request region]
-//   -> [async a2a send value region -> recv value region]   (SET payloads, off the
-//       critical path: only finish() reads them)
-//   -> owner(recv, sizes_out) -> [a2a sizes_out -> sizes_in] -> reply_sizes(sizes_in)
-//   -> gather_replies(reply) -> [async a2a reply -> data] -> [wait value region]
-//   -> finish(data, recv, ...) -> [wait reply a2a before reading data]
-// send / recv = [request region: per peer G_p | R_p][value region: per peer V_p].
+// Fixed-capacity exchange. The GET requests and the replies travel in per-peer slots of
+// a capacity every rank agrees on (capG rows, capD reply bytes), so the all-to-alls need
+// no split sizes from the device: counts and per-row (size, offset) ride in-band. The
+// capacities come from the demand the ranks observed in earlier steps (one all-gathered
+// row per rank per step), the same numbers on every rank, with slack; a row that does
+// not fit its slot is answered as a miss (always a valid cache answer) and counted, and
+// the next steps' capacities grow. The first step after a reset calibrates the
+// capacities with two host reads (the only synchronising step).
+// SETs travel with exact split sizes: the host reads them from the all-gathered row in
+// the middle of the step (the GPU is still busy with the GET exchange queued before), so
+// no stall either. Self traffic never enters a collective: a rank probes its own slot in
+// place and gathers its own replies straight into the response buffer.
+//
+// Slot layouts (o(q) = q < rank ? q : q - 1 orders the other ranks):
+//   G    = [recv: W-1 slots | self slot | send: W-1 slots], capG x 16-B digests each;
+//          the owner probes G[0, W capG) (sources in o-order, self last) in place.
+//   R    = [W-1 reply slots] (send), slot o(q) for requester q.
+//   data = [local region capL | W-1 reply slots (recv, o-order) | self reply slot]:
+//          the response buffer. A reply slot = [capG x u64 (size << 32 | offset)][capD].
+//   all-gathered row (K = 4W + 8 int64): [GET rows to p (W) | SET rows to p (W) |
+//          SET bytes to p (W) | reply bytes produced for q, previous step (W) |
+//          n_local, local_bytes, n_dup, reply rows dropped (previous step), 0 x 4].
+// Per step (stream-ordered on `s`):
+//   plan(G) -> [all_gather row -> mat] -> publish(mat)
+//   -> [a2a G send -> G recv, capG*16 per other rank]
+//   -> owner_probe(G) -> (calibration only: owner_demand, all_gather, calibrate_reply)
+//   -> owner_reply(R, data) -> [async a2a R -> data, slot bytes per other rank]
+//   -> gather_local(data) -> set_splits() (host waits for publish) -> pack_sets(S)
+//   -> [a2a S -> Rs, exact sizes] -> store_sets(S, Rs)
+//   -> on a side stream after the reply a2a: assemble(data, out) -> wait() before reading.
 class RoutedStep {
  public:
+  static constexpr int kExtras = 8;
   RoutedStep(int world, int rank, int device);
   ~RoutedStep();
   RoutedStep(const RoutedStep&) = delete;
@@ -67,50 +88,59 @@ class RoutedStep {
   void set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts);
   // Sorted hot set (by signed lo) + optional 65537-entry directory (see is_hot).
   void set_hot(const Digest* hot, int64_t nhot, const int64_t* dir = nullptr);
+  int64_t row_words() const { return 4 * (int64_t)w_ + kExtras; }
 
-  // GET routing (replica probe first when `replica`), SET routing + hot fan-out (on a
-  // side stream, concurrently), per-peer table[w][3] = {GET rows, SET rows, SET value
-  // bytes} into `table`, which must hold 6w + 3 words: [table | rtable | extras].
-  // `coalesce`: duplicate GET digests of the batch are not routed; each is answered
-  // from the row that claimed its digest (coalesce_keys / expand_coalesced).
+  // ---- capacities (identical on every rank: derived from all-gathered rows) ----
+  // {capG rows, capD reply bytes, capL local bytes, calibrating (0/1)} for a GET batch
+  // of n rows. While calibrating capG = n (every row fits), capD and capL are set by
+  // calibrate_local / calibrate_reply during the step.
+  std::vector<int64_t> caps(int64_t n) const;
+  void reset_caps();  // next step calibrates (new ring, new hot set)
+  // Tests: fixed capacities (every rank the same), overriding the policy; 0s clear it.
+  void set_cap_override(int64_t capG, int64_t capD, int64_t capL) {
+    ovr_ = {capG, capD, capL};
+  }
+
+  // GET routing (coalescing + replica probe first), the digests of peer p's rows written
+  // into its slot of G (rows past capG: overflow, answered as misses), SET routing + hot
+  // fan-out on a side stream; this rank's all-gather row -> `row`.
   void plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
             const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
             const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues, int64_t ns,
-            bool fanout, int64_t* table, hipStream_t s, bool coalesce = false);
-  // Host sync 1 (one D2H; rtable must be table + 3w). Returns
-  // [table (3w) | rtable (3w) | n_local | local_bytes | coalesced duplicates] (n_local
-  // includes the duplicates).
-  std::vector<int64_t> read_counts(const int64_t* rtable, hipStream_t s);
-  // send: request region (sum 16 G_p + 32 R_p) then value region (sum V_p).
-  void pack(uint8_t* send, hipStream_t s);
-  // Owner side: de-interleave the received requests, probe `shard`; sizes_out[mg+1].
-  void owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint64_t* sizes_out,
-             hipStream_t s);
-  // Host sync 2. Returns [reply bytes per source (w) | bytes per owner (w)].
-  std::vector<int64_t> reply_sizes(const uint64_t* sizes_in, hipStream_t s);
-  void gather_replies(HbmCache* shard, uint8_t* reply, hipStream_t s);
-  // Local replica gather into data[0, local_bytes), received SET stores (main shard
-  // tier 0, replica tier 1), response (size, off) in request order.
-  void finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
-              HbmCache* replica, uint32_t now, uint64_t* out_size, uint64_t* out_off,
-              hipStream_t s);
-  // `s` waits for the main-shard SET chain of the last finish(). With the deferred join
-  // (default) finish() does not wait for it: the chain runs under the next step's plan
-  // and the next owner() joins before it touches the main shard, so the caller must
-  // keep `recv` alive until then and call join_sets() before any other use of the shard.
-  void join_sets(hipStream_t s);
-  // Early local gather (after read_counts): the replica hits' records go into
-  // data[0, local_bytes) on a third stream while the request exchange, owner lookup and
-  // host sync 2 proceed; finish() (or join_local) makes `s` wait for it. `data` must
-  // stay allocated until then.
+            bool fanout, uint8_t* G, int64_t* row, hipStream_t s, bool coalesce);
+  // After the all-gather: per-source row counts of this rank's owner slots, and the
+  // matrix copied to pinned host memory (read by set_splits without stalling the GPU).
+  void publish(const int64_t* mat, hipStream_t s);
+  // Calibration: wait for the published matrix, fix capL from this step's local bytes.
+  void calibrate_local();
+  // Owner side: probe the W slots of G in place (padding rows skipped).
+  void owner_probe(const uint8_t* G, HbmCache* shard, uint32_t now, hipStream_t s);
+  // Reply bytes this shard's probe found per requester -> `out` (W words, device).
+  void owner_demand(int64_t* out, hipStream_t s);
+  // Calibration: capD from the all-gathered demand (W x W, device; host read).
+  void calibrate_reply(const int64_t* dmat);
+  // Reply slots: headers (size, offset per row; 0 = miss / dropped) and the records —
+  // other requesters' into R, this rank's own straight into data's self slot.
+  void owner_reply(HbmCache* shard, uint8_t* R, uint8_t* data, hipStream_t s);
+  // The local replica hits' records into data[0, capL).
   void gather_local(uint8_t* data, hipStream_t s);
-  void join_local(hipStream_t s);
-  void set_defer_join(bool on) { defer_join_ = on; }
+  // Host: wait for the published matrix; returns [send bytes to p (W) | recv bytes from
+  // q (W) | n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped]
+  // (self entries included: the SET buffer is [others in rank order | self]).
+  std::vector<int64_t> set_splits();
+  // SET send buffer: per destination [records 32 B x rows | values], others in rank
+  // order then self.
+  void pack_sets(uint8_t* S, hipStream_t s);
+  // Received SETs (others from Rs, own from S's tail) into the main shard (tier 0, on
+  // the store stream: joined by the next owner_probe) and the replica (tier 1, on `s`).
+  void store_sets(const uint8_t* S, const uint8_t* Rs, HbmCache* shard, HbmCache* replica,
+                  uint32_t now, hipStream_t s);
+  // Per-request (size, off) into `data`, in request order (duplicates: their claimer's
+  // record); run on a stream that has waited for the reply all-to-all.
+  void assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off, hipStream_t s);
+  // `s` waits for the main-shard SET chain of the last store_sets.
+  void join_sets(hipStream_t s);
   bool sets_pending() const { return sets_pending_; }
-
-  int64_t mg() const { return mg_; }
-  int64_t ms() const { return ms_; }
-  int64_t n_local() const { return n_local_; }
   int rank() const { return rank_; }
 
  private:
@@ -120,8 +150,7 @@ class RoutedStep {
   };
   template <typename T>
   T* buf(int slot, size_t count);
-  void fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* shard, uint32_t now,
-                  hipStream_t s);
+  void note_matrix();
 
   int w_, rank_, device_;
   const uint32_t* pts_ = nullptr;
@@ -131,37 +160,36 @@ class RoutedStep {
   int64_t nhot_ = 0;
   const int64_t* hot_dir_ = nullptr;
   std::vector<Buf> bufs_;
-  int64_t* host_ = nullptr;  // pinned
-  // side stream: the main-shard SET chain runs there while the replica gather runs on
-  // the caller's stream (finish); events fork and join the two
-  hipStream_t side_ = nullptr;
-  hipEvent_t ev_fork_ = nullptr, ev_fill_ = nullptr, ev_join_ = nullptr, ev_pjoin_ = nullptr;
-  // store stream: the received-SET chain of the main shard (fork_store). Separate from
-  // side_ (the SET planning of plan()), so the next step's planning does not queue
-  // behind a deferred SET chain.
-  hipStream_t store_side_ = nullptr;
-  hipEvent_t ev_sfork_ = nullptr;
-  hipStream_t local_side_ = nullptr;  // early replica gather (gather_local)
-  hipEvent_t ev_lfork_ = nullptr, ev_ljoin_ = nullptr;
-  bool local_pending_ = false, local_done_ = false;
-  HbmCache* replica_ = nullptr;
-  bool defer_join_ = true, sets_pending_ = false;
+  int64_t* host_mat_ = nullptr;   // pinned: the published all-gather matrix
+  int64_t* host_dmat_ = nullptr;  // pinned: calibration demand matrix
+  uint64_t* host_tab_ = nullptr;  // pinned: per-step SET tables (uploaded)
+  hipStream_t side_ = nullptr, store_side_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_pjoin_ = nullptr, ev_pub_ = nullptr, ev_sfork_ = nullptr,
+             ev_join_ = nullptr, ev_asm_[2] = {nullptr, nullptr};
+  bool asm_pending_[2] = {false, false};
+  bool sets_pending_ = false;
+  // capacities and their history (max over the window of the all-gathered demand)
+  int64_t capG_ = 0, capD_ = 0, capL_ = 0;
+  std::vector<int64_t> ovr_ = {0, 0, 0};
+  bool calibrating_ = true;
+  std::vector<int64_t> hist_g_, hist_d_, hist_l_;
   // per-step state
-  int64_t n_ = 0, ns_ = 0, mg_ = 0, ms_ = 0, n_local_ = 0, n_remote_ = 0;
-  uint64_t local_bytes_ = 0;
-  bool have_replica_ = false;
+  int par_ = 0;  // step parity: the buffers the deferred assemble reads
+  int64_t n_ = 0, ns_ = 0, ns_rows_ = 0, ms_ = 0;
+  bool have_replica_ = false, published_ = false;
+  HbmCache* replica_ = nullptr;
   const uint8_t* values_ = nullptr;
-  // device pointers live for one step (arena slots or caller tensors)
-  int64_t* table_ = nullptr;
-  const int64_t* rtable_ = nullptr;
   uint64_t *rl_loc_ = nullptr, *rl_size_ = nullptr, *rl_off_ = nullptr;
-  Digest* gk_ = nullptr;
-  int64_t *perm_g_ = nullptr, *cnt_g_ = nullptr, *cnt_s_ = nullptr, *srec_ = nullptr;
+  uint32_t* first_ = nullptr;
+  int64_t* route_ = nullptr;
+  int64_t *srec_ = nullptr, *cnt_s_ = nullptr;
   uint64_t *sval_ = nullptr, *svoff_ = nullptr;
-  uint32_t* first_ = nullptr;  // coalescing: claiming row of each GET row (null = off)
-  const int64_t* rrec_ = nullptr;
-  uint64_t *lk_loc_ = nullptr, *lk_off_ = nullptr, *gscan_ = nullptr;
-  const uint64_t* sizes_in_ = nullptr;
+  int64_t* own_cnt_ = nullptr;
+  uint64_t *lk_loc_ = nullptr, *lk_size_ = nullptr, *lk_off_ = nullptr;
+  int64_t* rb_ = nullptr;       // reply bytes per requester (W) + dropped rows (1)
+  std::vector<int64_t> mat_;    // host copy of this step's matrix (after set_splits)
+  std::vector<int64_t> sset_;   // per destination SET bytes (send), rank order
+  std::vector<int64_t> rset_;   // per source SET bytes (recv), rank order
 };
 
 }  // namespace shellac

@@ -80,14 +80,15 @@ __global__ __launch_bounds__(kB) void k_gr_hist(const int32_t* __restrict__ dest
 
 // One workgroup: exclusive scan of table[0..T) in place; counts[d] = bucket totals.
 // Optionally (xtable != nullptr, routed GET plan) also writes the GET column of the
-// exchange table, xtable[d * 3] = counts[d] for d < nb - 1, and
+// exchange row, xtable[d * xstride] = counts[d] for d < nb - 1, and
 // extras = {counts[nb - 1] (local replica hits), *rl_off_n (their response bytes)}.
 __global__ __launch_bounds__(1024) void k_gr_scan(uint64_t* __restrict__ table, int64_t T,
                                                   int32_t nb, int32_t G,
                                                   int64_t* __restrict__ counts,
                                                   int64_t* __restrict__ xtable = nullptr,
                                                   const uint64_t* __restrict__ rl_off_n = nullptr,
-                                                  int64_t* __restrict__ extras = nullptr) {
+                                                  int64_t* __restrict__ extras = nullptr,
+                                                  int xstride = 3) {
   __shared__ unsigned long long s_w[16];
   __shared__ unsigned long long s_total;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(1024) void k_gr_scan(uint64_t* __restrict__ table, 
     const uint64_t s1 = d + 1 < nb ? table[(int64_t)(d + 1) * G] : s_total;
     counts[d] = (int64_t)(s1 - s0);
     if (xtable) {
-      if (d < nb - 1) xtable[(int64_t)d * 3] = (int64_t)(s1 - s0);
+      if (d < nb - 1) xtable[(int64_t)d * xstride] = (int64_t)(s1 - s0);
       else {
         extras[0] = (int64_t)(s1 - s0);
         extras[1] = rl_off_n ? (int64_t)*rl_off_n : 0;
@@ -284,13 +285,14 @@ __device__ unsigned long long block_scan_inplace(uint64_t* __restrict__ t, int64
   return total;
 }
 
-// Scans both SET tables, then writes the SET columns of the per-peer exchange table:
-// table[p * 3 + 1] = SET rows, table[p * 3 + 2] = SET value bytes (k_gr_scan writes
-// column 0 on the other stream).
+// Scans both SET tables, then writes the SET blocks of this rank's exchange row:
+// rows_col[p] = SET rows to peer p, bytes_col[p] = their value bytes (k_gr_scan writes
+// the GET block on the other stream).
 __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
                                                   uint64_t* __restrict__ tbytes, int32_t nb,
                                                   int32_t G, int64_t* __restrict__ cnt_s,
-                                                  int64_t* __restrict__ table) {
+                                                  int64_t* __restrict__ rows_col,
+                                                  int64_t* __restrict__ bytes_col) {
   __shared__ unsigned long long s_w[17];
   const int64_t T = (int64_t)nb * G;
   const unsigned long long tc = block_scan_inplace(tcnt, T, s_w);
@@ -303,8 +305,8 @@ __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
     const int64_t c = (int64_t)(c1 - tcnt[(int64_t)d * G]);
     cnt_s[d] = c;
     if (d < w) {
-      table[d * 3 + 1] = c;
-      table[d * 3 + 2] = (int64_t)(b1 - tbytes[(int64_t)d * G]);
+      rows_col[d] = c;
+      bytes_col[d] = (int64_t)(b1 - tbytes[(int64_t)d * G]);
     }
   }
 }
@@ -348,111 +350,6 @@ __global__ __launch_bounds__(kB) void k_ps_scatter(
       sval[pos] = src;
       svoff[pos] = vglob;
     }
-  }
-}
-
-// Request buffer: a request region [G_0 | R_0 | G_1 | R_1 | ...] (digests and SET
-// records, exchanged synchronously) followed by a value region [V_0 | V_1 | ...] (SET
-// payloads, exchanged asynchronously so they stay off the critical path to the owner
-// lookup). Destination offsets follow from the exchange table, so no scan:
-// segments G_p = 2p, R_p = 2p + 1, value row i = 2w + i; seg_off[2w + ns] = total bytes.
-__global__ __launch_bounds__(kB) void k_send_segs(const int64_t* __restrict__ table,
-                                                  const uint64_t* __restrict__ svoff,
-                                                  const uint64_t* __restrict__ sval,
-                                                  uint64_t gk_base, uint64_t srec_base, int32_t w,
-                                                  int64_t ns, uint64_t* __restrict__ seg_off,
-                                                  uint64_t* __restrict__ seg_src) {
-  extern __shared__ int64_t s_pre[];  // S[w+1] SET rows, Gp[w+1] GET rows, P[w+1] request starts
-  int64_t* S = s_pre;
-  int64_t* Gp = S + (w + 1);
-  int64_t* P = Gp + (w + 1);
-  __shared__ int64_t s_vtot;
-  if (threadIdx.x == 0) {
-    S[0] = Gp[0] = P[0] = 0;
-    int64_t vt = 0;
-    for (int p = 0; p < w; ++p) {
-      const int64_t g = table[p * 3], sr = table[p * 3 + 1];
-      S[p + 1] = S[p] + sr;
-      Gp[p + 1] = Gp[p] + g;
-      P[p + 1] = P[p] + 16 * g + 32 * sr;
-      vt += table[p * 3 + 2];
-    }
-    s_vtot = vt;
-  }
-  __syncthreads();
-  const uint64_t req = (uint64_t)P[w];
-  const int64_t total = ns + w;
-  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i <= total;
-       i += (int64_t)gridDim.x * kB) {
-    if (i == total) {
-      seg_off[2 * w + ns] = req + (uint64_t)s_vtot;
-    } else if (i < ns) {
-      seg_off[2 * w + i] = req + svoff[i];  // svoff: global byte offset in peer order
-      seg_src[2 * w + i] = sval[i];
-    } else {
-      const int p = (int)(i - ns);
-      const int64_t g = Gp[p + 1] - Gp[p];
-      seg_off[2 * p] = (uint64_t)P[p];
-      seg_src[2 * p] = gk_base + 16 * (uint64_t)Gp[p];
-      seg_off[2 * p + 1] = (uint64_t)(P[p] + 16 * g);
-      seg_src[2 * p + 1] = srec_base + 32 * (uint64_t)S[p];
-    }
-  }
-}
-
-// De-interleave the received request region into [all G | all R]: 2w segments + end.
-__global__ void k_recv_segs(const int64_t* __restrict__ rtable, uint64_t recv_base, int32_t w,
-                            uint64_t* __restrict__ seg_off, uint64_t* __restrict__ seg_src) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t q0 = 0, g0 = 0, r0 = 0, gtot = 0;
-  for (int q = 0; q < w; ++q) gtot += 16 * (uint64_t)rtable[q * 3];
-  for (int q = 0; q < w; ++q) {
-    const uint64_t a = (uint64_t)rtable[q * 3], b = (uint64_t)rtable[q * 3 + 1];
-    seg_off[q] = g0;
-    seg_src[q] = recv_base + q0;
-    seg_off[w + q] = gtot + r0;
-    seg_src[w + q] = recv_base + q0 + 16 * a;
-    g0 += 16 * a;
-    r0 += 32 * b;
-    q0 += 16 * a + 32 * b;  // the value region follows all request chunks
-  }
-  seg_off[2 * w] = gtot + r0;
-}
-
-__global__ __launch_bounds__(kB) void k_rs_fill(
-    const int64_t* __restrict__ rrec, int64_t ms, const int64_t* __restrict__ rtable, int32_t w,
-    Digest* __restrict__ keys, uint32_t* __restrict__ vlen0, uint32_t* __restrict__ vlen1,
-    uint32_t* __restrict__ flags, uint32_t* __restrict__ expire, uint64_t* __restrict__ roff) {
-  extern __shared__ int64_t s_q[];  // first[w+1], vstart[w]
-  int64_t* first = s_q;
-  int64_t* vstart = s_q + (w + 1);
-  if (threadIdx.x == 0) {
-    int64_t v0 = 0;  // value region starts after every source's request chunk
-    for (int q = 0; q < w; ++q) v0 += 16 * rtable[q * 3] + 32 * rtable[q * 3 + 1];
-    first[0] = 0;
-    for (int q = 0; q < w; ++q) {
-      vstart[q] = v0;
-      first[q + 1] = first[q] + rtable[q * 3 + 1];
-      v0 += rtable[q * 3 + 2];
-    }
-  }
-  __syncthreads();
-  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < ms; r += (int64_t)gridDim.x * kB) {
-    int lo = 0, hi = w;  // source q with first[q] <= r < first[q+1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (first[mid] <= r) lo = mid; else hi = mid;
-    }
-    const int64_t* rec = rrec + r * 4;
-    keys[r] = Digest{(uint64_t)rec[0], (uint64_t)rec[1]};
-    const uint32_t vl = (uint32_t)rec[2];
-    const uint64_t hi32 = (uint64_t)rec[3] >> 32;
-    const uint32_t tier = (uint32_t)(hi32 >> 31);
-    vlen0[r] = tier == 0 ? vl : kSkipVlen;
-    vlen1[r] = tier == 1 ? vl : kSkipVlen;
-    flags[r] = (uint32_t)((uint64_t)rec[2] >> 32);
-    expire[r] = (uint32_t)rec[3];
-    roff[r] = (uint64_t)vstart[lo] + (hi32 & 0x7FFFFFFFull);
   }
 }
 
@@ -515,47 +412,6 @@ __global__ __launch_bounds__(kB) void k_scan_apply(const uint64_t* __restrict__ 
   if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
 }
 
-__global__ void k_reply_bytes(const uint64_t* __restrict__ lk_off,
-                              const int64_t* __restrict__ rtable,
-                              const uint64_t* __restrict__ gscan,
-                              const int64_t* __restrict__ table, int32_t w,
-                              int64_t* __restrict__ bytes) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int64_t R = 0, G = 0;
-  for (int q = 0; q < w; ++q) {
-    const int64_t a = rtable[q * 3], g = table[q * 3];
-    bytes[q] = (int64_t)(lk_off[R + a] - lk_off[R]);
-    bytes[w + q] = (int64_t)(gscan[G + g] - gscan[G]);
-    R += a;
-    G += g;
-  }
-}
-
-__global__ __launch_bounds__(kB) void k_assemble(const int64_t* __restrict__ perm, int64_t n,
-                                                 int64_t n_remote,
-                                                 const uint64_t* __restrict__ sizes_back,
-                                                 const uint64_t* __restrict__ gscan,
-                                                 const uint64_t* __restrict__ rl_size,
-                                                 const uint64_t* __restrict__ rl_off,
-                                                 uint64_t local_bytes, uint64_t* __restrict__ size,
-                                                 uint64_t* __restrict__ off) {
-  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
-    if (rl_size && rl_size[i] > 0) {
-      size[i] = rl_size[i];
-      off[i] = rl_off[i];
-      continue;
-    }
-    const int64_t p = perm[i];
-    if (p < n_remote) {
-      size[i] = sizes_back[p];
-      off[i] = gscan[p] + local_bytes;
-    } else {
-      size[i] = 0;
-      off[i] = local_bytes;
-    }
-  }
-}
-
 }  // namespace
 
 int64_t group_ws_words(int64_t n, int32_t nb) { return (int64_t)nb * group_grid(n) + 8; }
@@ -596,52 +452,232 @@ int64_t scan_parts_words(int64_t n) { return (n + kScanItems - 1) / kScanItems +
 
 }  // namespace shellac
 
+
 // =====================================================================================
-// RoutedStep
+// RoutedStep: the device-driven routed step (see router.h for the layouts)
 // =====================================================================================
 namespace shellac {
 
 namespace {
+
 enum Slot {
-  kRlLoc, kRlSize, kRlOff, kDestG, kGk, kPermG, kCntG, kWsG, kOwnerS, kVpad, kTcnt,
-  kTbytes, kSrec, kSval, kSvoff, kCntS, kSegOff, kSegSrc, kBody, kRSegOff, kRSegSrc,
-  kLkLoc, kLkOff, kGscan, kParts, kNbytes, kRkeys, kV0, kV1, kFl, kEx, kRoff, kCoTab, kFirst,
-  kNumSlots
+  kRlLoc, kRlSize0, kRlSize1, kRlOff0, kRlOff1, kDestG, kRoute0, kRoute1, kCntG, kWsG,
+  kCoTab, kFirst0, kFirst1, kOwnerS, kVpad, kTcnt, kTbytes, kSrec, kSval, kSvoff, kCntS,
+  kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSegLen, kRb, kTab, kSegOff, kSegSrc,
+  kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
 };
+
+// Slot of G a requester writes peer p's rows into: self = W-1, others W + o(p).
+__device__ __forceinline__ int64_t g_slot(int p, int me, int W) {
+  return p == me ? (int64_t)(W - 1) : (int64_t)W + (p < me ? p : p - 1);
+}
+
+// Counting-sort scatter of the GET rows into the request slots of G: peer p's rows go to
+// its slot at their rank j within p's bucket (j >= capG: overflow, not written).
+// route[i] = p << 32 | j for a row sent to p, -1 for a row answered locally (replica
+// hit or coalesced duplicate).
+__global__ __launch_bounds__(kB) void k_gr_scatter_slots(
+    const int32_t* __restrict__ dest, int64_t n, int32_t nb, int64_t plen,
+    const uint64_t* __restrict__ table, const Digest* __restrict__ keys, int64_t capG,
+    int32_t me, uint8_t* __restrict__ G, int64_t* __restrict__ route) {
+  extern __shared__ uint32_t s_cur[];
+  const int W = nb - 1;
+  for (int d = threadIdx.x; d < nb; d += kB) s_cur[d] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(n, i0 + plen);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += kB) {
+    const int d = dest[i];
+    const int64_t pos =
+        (int64_t)table[(int64_t)d * gridDim.x + blockIdx.x] + atomicAdd(&s_cur[d], 1u);
+    if (d == W) {
+      route[i] = -1;
+      continue;
+    }
+    const int64_t j = pos - (int64_t)table[(int64_t)d * gridDim.x];
+    route[i] = ((int64_t)d << 32) | j;
+    if (j < capG)
+      reinterpret_cast<Digest*>(G)[g_slot(d, me, W) * capG + j] = keys[i];
+  }
+}
+
+// Rows each owner slot holds this step: slot s < W-1 is source o^-1(s), slot W-1 is self.
+__global__ void k_derive(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
+                         int64_t capG, int64_t* __restrict__ own_cnt) {
+  for (int s = threadIdx.x; s < W; s += blockDim.x) {
+    const int q = s == W - 1 ? me : (s < me ? s : s + 1);
+    own_cnt[s] = min(mat[(int64_t)q * K + me], capG);
+  }
+}
+
+// Reply bytes the owner probe found per requester (before any drop): out[q].
+__global__ void k_demand(const uint64_t* __restrict__ lk_off, int32_t W, int32_t me, int64_t capG,
+                         int64_t* __restrict__ out) {
+  for (int s = threadIdx.x; s < W; s += blockDim.x) {
+    const int q = s == W - 1 ? me : (s < me ? s : s + 1);
+    out[q] = (int64_t)(lk_off[(int64_t)(s + 1) * capG] - lk_off[(int64_t)s * capG]);
+  }
+}
+
+// Owner: the reply slot of every probed row. Row r of owner slot s (j = r - s capG) gets
+// header (size << 32 | offset in the slot's data) if its record fits the slot's capD
+// bytes, 0 otherwise (miss or dropped); its destination for the sized gather (others:
+// relative to R, self: relative to data's self slot) and its length.
+__global__ __launch_bounds__(kB) void k_reply_prep(
+    const uint64_t* __restrict__ lk_size, const uint64_t* __restrict__ lk_off,
+    const int64_t* __restrict__ own_cnt, int32_t W, int64_t capG, int64_t capD, int64_t slotR,
+    uint8_t* __restrict__ R, uint8_t* __restrict__ self_slot, uint64_t* __restrict__ dstA,
+    uint64_t* __restrict__ dstB, uint64_t* __restrict__ seg_len,
+    unsigned long long* __restrict__ dropped) {
+  const int64_t rows = (int64_t)W * capG;
+  const uint64_t hdr = (uint64_t)capG * 8;
+  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r <= rows;
+       r += (int64_t)gridDim.x * kB) {
+    if (r == rows) {  // sentinels: the extent of each gather
+      dstA[(int64_t)(W - 1) * capG] = (uint64_t)(W - 1) * (uint64_t)slotR;
+      dstB[capG] = (uint64_t)slotR;
+      continue;
+    }
+    const int64_t s = r / capG, j = r - s * capG;
+    const uint64_t sz = lk_size[r];
+    const uint64_t off_in = lk_off[r] - lk_off[s * capG];
+    const bool keep = sz > 0 && off_in + sz <= (uint64_t)capD;
+    const uint64_t at = hdr + min(off_in, (uint64_t)capD);
+    seg_len[r] = keep ? sz : 0;
+    uint8_t* slot = s == W - 1 ? self_slot : R + s * slotR;
+    if (j < own_cnt[s]) {
+      reinterpret_cast<uint64_t*>(slot)[j] = keep ? (sz << 32 | off_in) : 0ull;
+      if (sz > 0 && !keep) atomicAdd(dropped, 1ull);
+    }
+    if (s == W - 1) dstB[j] = at;
+    else dstA[r] = (uint64_t)s * (uint64_t)slotR + at;
+  }
+}
+
+// Requester: (size, off) of every request row in `data` (0, 0 = miss; duplicates are
+// filled in from their claimer by expand_coalesced afterwards).
+__global__ __launch_bounds__(kB) void k_assemble_slots(
+    const int64_t* __restrict__ route, int64_t n, int32_t W, int32_t me, int64_t capG,
+    int64_t capL, int64_t slotR, const uint8_t* __restrict__ data,
+    const uint64_t* __restrict__ rl_size, const uint64_t* __restrict__ rl_off,
+    uint64_t* __restrict__ out_size, uint64_t* __restrict__ out_off) {
+  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
+    const int64_t r = route[i];
+    uint64_t sz = 0, off = 0;
+    if (r < 0) {
+      if (rl_size && rl_size[i] > 0 && rl_off[i] + rl_size[i] <= (uint64_t)capL) {
+        sz = rl_size[i];
+        off = rl_off[i];
+      }
+    } else {
+      const int p = (int)(r >> 32);
+      const int64_t j = r & 0xFFFFFFFFll;
+      if (j < capG) {
+        const int rs = p == me ? W - 1 : (p < me ? p : p - 1);
+        const uint64_t base = (uint64_t)capL + (uint64_t)rs * (uint64_t)slotR;
+        const uint64_t h = reinterpret_cast<const uint64_t*>(data + base)[j];
+        sz = h >> 32;
+        if (sz) off = base + (uint64_t)capG * 8 + (h & 0xFFFFFFFFull);
+      }
+    }
+    out_size[i] = sz;
+    out_off[i] = off;
+  }
+}
+
+// SET send buffer segments: per destination d (send order: others by rank, self last)
+// one segment of its records and one per value row. tab (rank order, per d):
+// [Sstart (W+1) | Bstart (W) | Psend (W) | segbase (W)].
+__global__ __launch_bounds__(kB) void k_set_segs(const uint64_t* __restrict__ tab, int32_t W,
+                                                 int64_t rows, const uint64_t* __restrict__ sval,
+                                                 const uint64_t* __restrict__ svoff,
+                                                 uint64_t srec_base, uint64_t total,
+                                                 uint64_t* __restrict__ seg_off,
+                                                 uint64_t* __restrict__ seg_src) {
+  const uint64_t* Sst = tab;
+  const uint64_t* Bst = tab + W + 1;
+  const uint64_t* Ps = Bst + W;
+  const uint64_t* sb = Ps + W;
+  for (int64_t t = (int64_t)blockIdx.x * kB + threadIdx.x; t <= rows + W;
+       t += (int64_t)gridDim.x * kB) {
+    if (t == rows + W) {
+      seg_off[rows + W] = total;
+    } else if (t >= rows) {  // destination d's record block
+      const int d = (int)(t - rows);
+      seg_off[sb[d]] = Ps[d];
+      seg_src[sb[d]] = srec_base + 32 * Sst[d];
+    } else {  // value row t (grouped by destination in rank order)
+      int lo = 0, hi = W;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (Sst[mid] <= (uint64_t)t) lo = mid; else hi = mid;
+      }
+      const uint64_t nrec = Sst[lo + 1] - Sst[lo];
+      const int64_t k = (int64_t)sb[lo] + 1 + (t - (int64_t)Sst[lo]);
+      seg_off[k] = Ps[lo] + 32 * nrec + (svoff[t] - Bst[lo]);
+      seg_src[k] = sval[t];
+    }
+  }
+}
+
+// Received SET rows (sources: others by rank, self last) -> store arguments. tab per
+// source k: [first row (W+1) | record block address (W) | value block address (W)].
+__global__ __launch_bounds__(kB) void k_rs_fill_slots(
+    const uint64_t* __restrict__ tab, int32_t W, int64_t ms, Digest* __restrict__ keys,
+    uint32_t* __restrict__ vlen0, uint32_t* __restrict__ vlen1, uint32_t* __restrict__ flags,
+    uint32_t* __restrict__ expire, uint64_t* __restrict__ roff) {
+  const uint64_t* first = tab;
+  const uint64_t* rec = tab + W + 1;
+  const uint64_t* val = rec + W;
+  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < ms; r += (int64_t)gridDim.x * kB) {
+    int lo = 0, hi = W;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (first[mid] <= (uint64_t)r) lo = mid; else hi = mid;
+    }
+    const int64_t* rr = reinterpret_cast<const int64_t*>(rec[lo] + 32 * (r - (int64_t)first[lo]));
+    keys[r] = Digest{(uint64_t)rr[0], (uint64_t)rr[1]};
+    const uint32_t vl = (uint32_t)rr[2];
+    const uint64_t hi32 = (uint64_t)rr[3] >> 32;
+    const uint32_t tier = (uint32_t)(hi32 >> 31);
+    vlen0[r] = tier == 0 ? vl : kSkipVlen;
+    vlen1[r] = tier == 1 ? vl : kSkipVlen;
+    flags[r] = (uint32_t)((uint64_t)rr[2] >> 32);
+    expire[r] = (uint32_t)rr[3];
+    roff[r] = val[lo] + (hi32 & 0x7FFFFFFFull);  // absolute: the store's values base is 0
+  }
+}
+
+int64_t align_up64(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
 }  // namespace
 
 RoutedStep::RoutedStep(int world, int rank, int device)
     : w_(world), rank_(rank), device_(device), bufs_(kNumSlots) {
   SH_CHECK(world >= 1 && world < kMaxBuckets, "bad world size");
   RT_OK(hipSetDevice(device_));
-  RT_OK(hipHostMalloc(&host_, (8 * (size_t)world + 8) * sizeof(int64_t), hipHostMallocDefault));
+  const size_t K = (size_t)row_words();
+  RT_OK(hipHostMalloc(&host_mat_, K * (size_t)world * sizeof(int64_t), hipHostMallocDefault));
+  RT_OK(hipHostMalloc(&host_dmat_, (size_t)world * (size_t)world * sizeof(int64_t),
+                      hipHostMallocDefault));
+  RT_OK(hipHostMalloc(&host_tab_, (8 * (size_t)world + 8) * sizeof(uint64_t), hipHostMallocDefault));
   RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   RT_OK(hipStreamCreateWithFlags(&store_side_, hipStreamNonBlocking));
-  RT_OK(hipEventCreateWithFlags(&ev_sfork_, hipEventDisableTiming));
-  RT_OK(hipStreamCreateWithFlags(&local_side_, hipStreamNonBlocking));
-  RT_OK(hipEventCreateWithFlags(&ev_lfork_, hipEventDisableTiming));
-  RT_OK(hipEventCreateWithFlags(&ev_ljoin_, hipEventDisableTiming));
-  RT_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-  RT_OK(hipEventCreateWithFlags(&ev_fill_, hipEventDisableTiming));
-  RT_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-  RT_OK(hipEventCreateWithFlags(&ev_pjoin_, hipEventDisableTiming));
+  for (hipEvent_t* e : {&ev_fork_, &ev_pjoin_, &ev_pub_, &ev_sfork_, &ev_join_, &ev_asm_[0],
+                        &ev_asm_[1]})
+    RT_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
 RoutedStep::~RoutedStep() {
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
   for (auto& b : bufs_) (void)hipFree(b.p);
-  (void)hipHostFree(host_);
-  (void)hipEventDestroy(ev_fork_);
-  (void)hipEventDestroy(ev_fill_);
-  (void)hipEventDestroy(ev_join_);
-  (void)hipEventDestroy(ev_pjoin_);
-  (void)hipEventDestroy(ev_sfork_);
-  (void)hipEventDestroy(ev_lfork_);
-  (void)hipEventDestroy(ev_ljoin_);
+  (void)hipHostFree(host_mat_);
+  (void)hipHostFree(host_dmat_);
+  (void)hipHostFree(host_tab_);
+  for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1]})
+    (void)hipEventDestroy(e);
   (void)hipStreamDestroy(side_);
   (void)hipStreamDestroy(store_side_);
-  (void)hipStreamDestroy(local_side_);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
@@ -673,44 +709,109 @@ T* RoutedStep::buf(int slot, size_t count) {
   return static_cast<T*>(b.p);
 }
 
+// ---- capacities ---------------------------------------------------------------------
+// Slack over the largest demand of the last kHist steps: 10 % (+256 rows) for the GET
+// slots, 5 % (+256 KiB) for the reply data — per-peer demand of a step varies by ~1 %
+// (Zipf batches of 1M rows), so an overflow needs a shift in the workload, which the
+// next steps absorb; the local region is per rank and costs no link bytes (10 % + 1 MiB).
+namespace {
+constexpr size_t kHist = 16;
+void push_hist(std::vector<int64_t>* h, int64_t v) {
+  h->push_back(v);
+  if (h->size() > kHist) h->erase(h->begin());
+}
+int64_t hist_max(const std::vector<int64_t>& h) {
+  int64_t m = 0;
+  for (int64_t v : h) m = std::max(m, v);
+  return m;
+}
+}  // namespace
+
+std::vector<int64_t> RoutedStep::caps(int64_t n) const {
+  if (ovr_[0] > 0 && !calibrating_)
+    return {align_up64(ovr_[0], 2), align_up64(ovr_[1], 16), align_up64(ovr_[2], 16), 0};
+  if (calibrating_) return {std::max<int64_t>(align_up64(n, 64), 64), capD_, capL_, 1};
+  const int64_t g = align_up64(hist_max(hist_g_) * 11 / 10 + 256, 64);
+  const int64_t d = align_up64(hist_max(hist_d_) * 21 / 20 + (256 << 10), 4096);
+  const int64_t l = align_up64(hist_max(hist_l_) * 11 / 10 + (1 << 20), 4096);
+  return {g, d, l, 0};
+}
+
+void RoutedStep::reset_caps() {
+  hist_g_.clear();
+  hist_d_.clear();
+  hist_l_.clear();
+  calibrating_ = true;
+  capD_ = capL_ = 0;
+}
+
+void RoutedStep::note_matrix() {
+  const int W = w_;
+  const int64_t K = row_words();
+  int64_t mg = 0, md = 0;
+  for (int r = 0; r < W; ++r)
+    for (int p = 0; p < W; ++p) {
+      mg = std::max(mg, mat_[r * K + p]);
+      md = std::max(md, mat_[r * K + 3 * W + p]);
+    }
+  push_hist(&hist_g_, mg);
+  // the reply column is the previous step's demand (none before the first step)
+  if (!calibrating_) push_hist(&hist_d_, md);
+  push_hist(&hist_l_, mat_[rank_ * K + 4 * W + 1]);
+  calibrating_ = false;
+}
+
+// ---- plan ---------------------------------------------------------------------------
 void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
                       const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
                       const uint32_t* sexpire, const uint64_t* sval_off, const uint8_t* svalues,
-                      int64_t ns, bool fanout, int64_t* table, hipStream_t s, bool coalesce) {
+                      int64_t ns, bool fanout, uint8_t* G, int64_t* row, hipStream_t s,
+                      bool coalesce) {
   SH_CHECK(pts_ && own_ && npts_ > 0, "RoutedStep: ring not set");
+  SH_CHECK(n < (1ll << 31), "RoutedStep: GET batch too large");
   const int W = w_;
   const int nb = W + 1;
+  const std::vector<int64_t> c = caps(n);
+  capG_ = c[0];
+  if (!calibrating_) {
+    capD_ = c[1];
+    capL_ = c[2];
+  }
+  par_ ^= 1;
+  const int P = par_;
   n_ = n;
+  ns_ = ns;
   values_ = svalues;
   have_replica_ = replica != nullptr;
   replica_ = replica;
-  local_done_ = false;
-  table_ = table;
-  int64_t* extras = table + 6 * W;  // [table | rtable | extras]: one D2H in read_counts
+  published_ = false;
+  // the deferred assemble of the step two back reads this parity's buffers
+  if (asm_pending_[P]) {
+    RT_OK(hipStreamWaitEvent(s, ev_asm_[P], 0));
+    asm_pending_[P] = false;
+  }
+  // every buffer first (buf() may reallocate, which synchronises the device)
   first_ = nullptr;
   uint32_t* co_tab = nullptr;
   int64_t co_slots = 0;
   if (coalesce && n > 0) {
     co_slots = coalesce_table_slots(n);
     co_tab = buf<uint32_t>(kCoTab, co_slots);
-    first_ = buf<uint32_t>(kFirst, n);
+    first_ = buf<uint32_t>(P ? kFirst1 : kFirst0, n);
   }
-  // every buffer first (buf() may reallocate, which synchronises the device)
-  uint64_t* rl_size = nullptr;
+  rl_size_ = rl_off_ = nullptr;
   if (replica) {
     rl_loc_ = buf<uint64_t>(kRlLoc, n);
-    rl_size = rl_size_ = buf<uint64_t>(kRlSize, n + 1);
-    rl_off_ = buf<uint64_t>(kRlOff, n + 1);
+    rl_size_ = buf<uint64_t>(P ? kRlSize1 : kRlSize0, n + 1);
+    rl_off_ = buf<uint64_t>(P ? kRlOff1 : kRlOff0, n + 1);
   }
   int32_t* dest_g = buf<int32_t>(kDestG, n);
-  gk_ = buf<Digest>(kGk, n);
-  perm_g_ = buf<int64_t>(kPermG, n);
-  cnt_g_ = buf<int64_t>(kCntG, nb);
+  route_ = buf<int64_t>(P ? kRoute1 : kRoute0, n);
+  int64_t* cnt_g = buf<int64_t>(kCntG, nb);
   const int64_t ng = std::max<int64_t>(n, 1);
   const int Gg = group_grid(ng);
   const int64_t plen_g = (ng + Gg - 1) / Gg;
   uint64_t* ws_g = buf<uint64_t>(kWsG, group_ws_words(ng, nb));
-  // SET rows fan out up to W ways: smaller ranges per workgroup than the GET sort
   const int64_t nsx = std::max<int64_t>(ns, 1);
   const int Gs = group_grid(nsx, 256);
   const int64_t plen_s = (nsx + Gs - 1) / Gs;
@@ -723,6 +824,13 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   sval_ = buf<uint64_t>(kSval, mcap);
   svoff_ = buf<uint64_t>(kSvoff, mcap);
   cnt_s_ = buf<int64_t>(kCntS, nb);
+  rb_ = buf<int64_t>(kRb, W + 1);
+  if (hist_g_.empty() && calibrating_) RT_OK(hipMemsetAsync(rb_, 0, (W + 1) * sizeof(int64_t), s));
+
+  // the previous step's reply demand and dropped rows ride in this row
+  RT_OK(hipMemsetAsync(row + 4 * W, 0, kExtras * sizeof(int64_t), s));
+  RT_OK(hipMemcpyAsync(row + 3 * W, rb_, W * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+  RT_OK(hipMemcpyAsync(row + 4 * W + 3, rb_ + W, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
 
   // SET planning on the side stream (owner + hot fan-out, counting sort with value-byte
   // ranges), concurrently with the replica probe and GET sort on `s`
@@ -733,7 +841,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
                      fanout ? nhot_ : 0, fanout ? hot_dir_ : nullptr, nb, plen_s, W, owner_s,
                      vpad, tcnt, tbytes);
   hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, side_, tcnt, tbytes, nb, Gs, cnt_s_,
-                     table);
+                     row + W, row + 2 * W);
   if (ns > 0)
     hipLaunchKernelGGL(k_ps_scatter, dim3(Gs), dim3(kB), nb * sizeof(unsigned long long), side_,
                        ns, nb, plen_s, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
@@ -741,187 +849,246 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   RT_OK(hipGetLastError());
   RT_OK(hipEventRecord(ev_pjoin_, side_));
 
-  // GET rows: coalesce duplicates (they stay local and are filled in by finish), owner
-  // (or bucket W = local replica hit / duplicate), counting sort by owner
-  RT_OK(hipMemsetAsync(extras + 2, 0, sizeof(int64_t), s));
-  if (first_ && replica)  // one pass: each digest's claiming row probes the replica
+  // GET rows: coalesce duplicates (answered from their claimer), replica probe, owner
+  // (or bucket W = answered here), counting sort straight into the request slots
+  if (first_ && replica)
     replica->lookup_coalesced(keys, n, co_tab, co_slots, first_, rl_loc_, rl_size_, rl_off_, now,
                               s);
   else if (first_)
     coalesce_keys(keys, n, co_tab, co_slots, first_, s);
   else if (replica)
     replica->lookup(keys, n, rl_loc_, rl_size_, rl_off_, now, s);
-  hipLaunchKernelGGL(k_route_hist, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, keys, n, rl_size,
+  int64_t* extras = row + 4 * W;
+  hipLaunchKernelGGL(k_route_hist, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, keys, n, rl_size_,
                      pts_, own_, npts_, W, plen_g, dest_g, ws_g, first_,
                      reinterpret_cast<unsigned long long*>(extras + 2));
-  hipLaunchKernelGGL(k_gr_scan, dim3(1), dim3(1024), 0, s, ws_g, (int64_t)nb * Gg, nb, Gg, cnt_g_,
-                     table, replica ? rl_off_ + n : nullptr, extras);
+  hipLaunchKernelGGL(k_gr_scan, dim3(1), dim3(1024), 0, s, ws_g, (int64_t)nb * Gg, nb, Gg, cnt_g,
+                     row, replica ? rl_off_ + n : nullptr, extras, 1);
   if (n > 0)
-    hipLaunchKernelGGL(k_gr_scatter, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, dest_g, n, nb,
-                       plen_g, ws_g, (const uint32_t*)keys, 4, (uint32_t*)gk_, perm_g_);
+    hipLaunchKernelGGL(k_gr_scatter_slots, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, dest_g, n,
+                       nb, plen_g, ws_g, keys, capG_, rank_, G, route_);
   RT_OK(hipGetLastError());
-  RT_OK(hipStreamWaitEvent(s, ev_pjoin_, 0));  // join: the table is complete
+  RT_OK(hipStreamWaitEvent(s, ev_pjoin_, 0));  // join: the row is complete
 }
 
-std::vector<int64_t> RoutedStep::read_counts(const int64_t* rtable, hipStream_t s) {
+void RoutedStep::publish(const int64_t* mat, hipStream_t s) {
   const int W = w_;
-  rtable_ = rtable;
-  SH_CHECK(rtable == table_ + 3 * W, "RoutedStep: rtable must follow table (one D2H)");
-  RT_OK(hipMemcpyAsync(host_, table_, (6 * W + 3) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  RT_OK(hipStreamSynchronize(s));
-  std::vector<int64_t> out(host_, host_ + 6 * W + 3);
-  n_local_ = out[6 * W];
-  local_bytes_ = (uint64_t)out[6 * W + 1];
-  n_remote_ = n_ - n_local_;
-  ns_ = mg_ = ms_ = 0;
+  const int64_t K = row_words();
+  own_cnt_ = buf<int64_t>(kOwnCnt, W);
+  hipLaunchKernelGGL(k_derive, dim3(1), dim3(64), 0, s, mat, K, W, rank_, capG_, own_cnt_);
+  RT_OK(hipGetLastError());
+  RT_OK(hipMemcpyAsync(host_mat_, mat, (size_t)W * K * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  RT_OK(hipEventRecord(ev_pub_, s));
+  published_ = true;
+}
+
+void RoutedStep::calibrate_local() {
+  SH_CHECK(published_, "RoutedStep: publish before calibrate_local");
+  RT_OK(hipEventSynchronize(ev_pub_));
+  const int64_t lb = host_mat_[rank_ * row_words() + 4 * w_ + 1];
+  capL_ = align_up64(lb * 11 / 10 + (1 << 20), 4096);
+}
+
+// ---- owner --------------------------------------------------------------------------
+void RoutedStep::owner_probe(const uint8_t* G, HbmCache* shard, uint32_t now, hipStream_t s) {
+  const int W = w_;
+  // the last step's SET chain writes the main shard: the probe comes after it
+  join_sets(s);
+  const int64_t rows = (int64_t)W * capG_;
+  lk_loc_ = buf<uint64_t>(kLkLoc, rows);
+  lk_size_ = buf<uint64_t>(kLkSize, rows + 1);
+  lk_off_ = buf<uint64_t>(kLkOff, rows + 1);
+  shard->lookup_slots(reinterpret_cast<const Digest*>(G), W, capG_, own_cnt_, lk_loc_, lk_size_,
+                      lk_off_, now, s);
+}
+
+void RoutedStep::owner_demand(int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_demand, dim3(1), dim3(64), 0, s, lk_off_, w_, rank_, capG_, out);
+  RT_OK(hipGetLastError());
+}
+
+void RoutedStep::calibrate_reply(const int64_t* dmat) {
+  const int W = w_;
+  RT_OK(hipMemcpy(host_dmat_, dmat, (size_t)W * W * sizeof(int64_t), hipMemcpyDeviceToHost));
+  int64_t m = 0;
+  for (int i = 0; i < W * W; ++i) m = std::max(m, host_dmat_[i]);
+  push_hist(&hist_d_, m);
+  capD_ = align_up64(m * 21 / 20 + (256 << 10), 4096);
+}
+
+void RoutedStep::owner_reply(HbmCache* shard, uint8_t* R, uint8_t* data, hipStream_t s) {
+  const int W = w_;
+  const int64_t rows = (int64_t)W * capG_;
+  const int64_t slotR = capG_ * 8 + capD_;
+  SH_CHECK(capD_ > 0 && capD_ % 16 == 0, "RoutedStep: reply capacity not set");
+  uint64_t* dstA = buf<uint64_t>(kDstA, (size_t)(W - 1) * capG_ + 1);
+  uint64_t* dstB = buf<uint64_t>(kDstB, capG_ + 1);
+  uint64_t* seg_len = buf<uint64_t>(kSegLen, rows);
+  uint8_t* self_slot = data + capL_ + (int64_t)(W - 1) * slotR;
+  hipLaunchKernelGGL(k_demand, dim3(1), dim3(64), 0, s, lk_off_, W, rank_, capG_, rb_);
+  RT_OK(hipMemsetAsync(rb_ + W, 0, sizeof(int64_t), s));
+  hipLaunchKernelGGL(k_reply_prep, dim3(grid1(rows + 1)), dim3(kB), 0, s, lk_size_, lk_off_,
+                     own_cnt_, W, capG_, capD_, slotR, R, self_slot, dstA, dstB, seg_len,
+                     reinterpret_cast<unsigned long long*>(rb_ + W));
+  RT_OK(hipGetLastError());
+  const uint8_t* log = shard->log_ptr();
+  if (W > 1)
+    segcopy_sized(log, lk_loc_, dstA, seg_len, (int64_t)(W - 1) * capG_, R, s);
+  segcopy_sized(log, lk_loc_ + (int64_t)(W - 1) * capG_, dstB, seg_len + (int64_t)(W - 1) * capG_,
+                capG_, self_slot, s);
+}
+
+void RoutedStep::gather_local(uint8_t* data, hipStream_t s) {
+  if (!have_replica_ || !replica_ || n_ <= 0) return;
+  segcopy_sized(replica_->log_ptr(), rl_loc_, rl_off_, rl_size_, n_, data, s, (uint64_t)capL_);
+}
+
+// ---- SETs ---------------------------------------------------------------------------
+std::vector<int64_t> RoutedStep::set_splits() {
+  SH_CHECK(published_, "RoutedStep: publish before set_splits");
+  const int W = w_, me = rank_;
+  const int64_t K = row_words();
+  RT_OK(hipEventSynchronize(ev_pub_));
+  mat_.assign(host_mat_, host_mat_ + (size_t)W * K);
+  // overflow: GET rows this rank could not send (its slots were full)
+  int64_t over = 0, off_rank = 0;
   for (int p = 0; p < W; ++p) {
-    ns_ += out[3 * p + 1];
-    mg_ += out[3 * W + 3 * p];
-    ms_ += out[3 * W + 3 * p + 1];
+    over += std::max<int64_t>(0, mat_[me * K + p] - capG_);
+    if (p != me) off_rank += mat_[me * K + p];
+  }
+  note_matrix();
+  sset_.assign(W, 0);
+  rset_.assign(W, 0);
+  ns_rows_ = ms_ = 0;
+  for (int p = 0; p < W; ++p) {
+    sset_[p] = 32 * mat_[me * K + W + p] + mat_[me * K + 2 * W + p];
+    rset_[p] = 32 * mat_[p * K + W + me] + mat_[p * K + 2 * W + me];
+    ns_rows_ += mat_[me * K + W + p];
+    ms_ += mat_[p * K + W + me];
     // value offsets travel as 31-bit fields in the SET records
-    SH_CHECK(out[3 * p + 2] < (1ll << 31) && out[3 * W + 3 * p + 2] < (1ll << 31),
+    SH_CHECK(mat_[me * K + 2 * W + p] < (1ll << 31) && mat_[p * K + 2 * W + me] < (1ll << 31),
              "SET values for one peer exceed 2 GiB per step; split the batch");
   }
+  std::vector<int64_t> out(2 * W + 5);
+  for (int p = 0; p < W; ++p) {
+    out[p] = sset_[p];
+    out[W + p] = rset_[p];
+  }
+  out[2 * W] = mat_[me * K + 4 * W];      // n_local (replica hits + duplicates)
+  out[2 * W + 1] = mat_[me * K + 4 * W + 2];  // duplicates
+  out[2 * W + 2] = off_rank;
+  out[2 * W + 3] = over;
+  out[2 * W + 4] = mat_[me * K + 4 * W + 3];  // reply rows this shard dropped (last step)
   return out;
 }
 
-void RoutedStep::pack(uint8_t* send, hipStream_t s) {
-  const int W = w_;
-  const int64_t nseg = 2 * (int64_t)W + ns_;
+void RoutedStep::pack_sets(uint8_t* S, hipStream_t s) {
+  const int W = w_, me = rank_;
+  const int64_t K = row_words();
+  // tab: [Sstart (W+1) | Bstart (W) | Psend (W) | segbase (W)] in rank order; send order
+  // is the other ranks by rank, then self
+  uint64_t* t = host_tab_;
+  uint64_t* Sst = t;
+  uint64_t* Bst = t + W + 1;
+  uint64_t* Ps = Bst + W;
+  uint64_t* sb = Ps + W;
+  Sst[0] = 0;
+  uint64_t b = 0;
+  for (int p = 0; p < W; ++p) {
+    Sst[p + 1] = Sst[p] + (uint64_t)mat_[me * K + W + p];
+    Bst[p] = b;
+    b += (uint64_t)mat_[me * K + 2 * W + p];
+  }
+  uint64_t pos = 0, seg = 0;
+  for (int k = 0; k < W; ++k) {
+    const int d = k == W - 1 ? me : (k < me ? k : k + 1);
+    Ps[d] = pos;
+    sb[d] = seg;
+    pos += (uint64_t)sset_[d];
+    seg += 1 + (uint64_t)mat_[me * K + W + d];
+  }
+  const size_t words = 5 * (size_t)W + 1;
+  uint64_t* dtab = buf<uint64_t>(kTab, 8 * (size_t)W + 8);
+  const int64_t nseg = W + ns_rows_;
   uint64_t* seg_off = buf<uint64_t>(kSegOff, nseg + 1);
   uint64_t* seg_src = buf<uint64_t>(kSegSrc, nseg);
-  hipLaunchKernelGGL(k_send_segs, dim3(grid1(ns_ + W + 1)), dim3(kB), 3 * (W + 1) * sizeof(int64_t),
-                     s, table_, svoff_, sval_, (uint64_t)(uintptr_t)gk_,
-                     (uint64_t)(uintptr_t)srec_, W, ns_, seg_off, seg_src);
+  RT_OK(hipMemcpyAsync(dtab, t, words * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_set_segs, dim3(grid1(ns_rows_ + W + 1)), dim3(kB), 0, s, dtab, W, ns_rows_,
+                     sval_, svoff_, (uint64_t)(uintptr_t)srec_, pos, seg_off, seg_src);
   RT_OK(hipGetLastError());
-  segcopy(nullptr, seg_src, seg_off, nseg, send, s);
+  segcopy(nullptr, seg_src, seg_off, nseg, S, s);
 }
 
-void RoutedStep::owner(const uint8_t* recv, HbmCache* shard, uint32_t now, uint64_t* sizes_out,
-                       hipStream_t s) {
-  const int W = w_;
-  // the last step's SET chain reads the body arena (rrec_) and writes the main shard:
-  // both are about to be reused
-  join_sets(s);
-  uint8_t* body = buf<uint8_t>(kBody, 16 * mg_ + 32 * ms_ + 16);
-  uint64_t* roff = buf<uint64_t>(kRSegOff, 2 * W + 1);
-  uint64_t* rsrc = buf<uint64_t>(kRSegSrc, 2 * W);
-  hipLaunchKernelGGL(k_recv_segs, dim3(1), dim3(64), 0, s, rtable_, (uint64_t)(uintptr_t)recv, W,
-                     roff, rsrc);
-  RT_OK(hipGetLastError());
-  segcopy(nullptr, rsrc, roff, 2 * W, body, s);
-  rrec_ = reinterpret_cast<const int64_t*>(body + 16 * mg_);
-  lk_loc_ = buf<uint64_t>(kLkLoc, mg_);
-  lk_off_ = buf<uint64_t>(kLkOff, mg_ + 1);
-  shard->lookup(reinterpret_cast<const Digest*>(body), mg_, lk_loc_, sizes_out, lk_off_, now, s);
-}
-
-std::vector<int64_t> RoutedStep::reply_sizes(const uint64_t* sizes_in, hipStream_t s) {
-  const int W = w_;
-  sizes_in_ = sizes_in;
-  gscan_ = buf<uint64_t>(kGscan, n_remote_ + 1);
-  scan_u64(sizes_in, n_remote_, buf<uint64_t>(kParts, scan_parts_words(n_remote_)), gscan_, s);
-  int64_t* nb = buf<int64_t>(kNbytes, 2 * W);
-  hipLaunchKernelGGL(k_reply_bytes, dim3(1), dim3(64), 0, s, lk_off_, rtable_, gscan_, table_, W,
-                     nb);
-  RT_OK(hipGetLastError());
-  RT_OK(hipMemcpyAsync(host_ + 6 * W + 2, nb, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  RT_OK(hipStreamSynchronize(s));
-  return std::vector<int64_t>(host_ + 6 * W + 2, host_ + 8 * W + 2);
-}
-
-void RoutedStep::gather_replies(HbmCache* shard, uint8_t* reply, hipStream_t s) {
-  if (mg_ > 0) shard->gather(lk_loc_, lk_off_, mg_, reply, s);
-}
-
-// Received-SET unpacking and the main-shard SET chain on the side stream, after the work
-// queued on `s` so far (the reply gather). Queuing it before host sync 2 instead (with the
-// owner lookup reserving its log bytes), to fill the GPU's idle time there, was measured
-// slower: simulated 8 ranks 0.83 / 0.82 vs 0.83 / 0.79 ms per step, 2 ranks 0.80 / 0.84 vs
-// 0.77 / 0.79 — the SET chain then competes with the owner probe and reply gather.
-void RoutedStep::fork_store(const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
-                            uint32_t now, hipStream_t s) {
+void RoutedStep::store_sets(const uint8_t* S, const uint8_t* Rs, HbmCache* shard,
+                            HbmCache* replica, uint32_t now, hipStream_t s) {
+  const int W = w_, me = rank_;
+  const int64_t K = row_words();
   const int64_t ms = ms_;
-  const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
+  if (ms <= 0) return;
+  // per source k (others by rank, self last): first row, record block, value block
+  uint64_t* t = host_tab_ + 5 * (size_t)W + 1;
+  uint64_t* first = t;
+  uint64_t* rec = t + W + 1;
+  uint64_t* val = rec + W;
+  uint64_t row0 = 0, rpos = 0, recv_bytes = 0;
+  uint64_t self_pos = 0;  // the self block sits after the others in S
+  for (int p = 0; p < W; ++p)
+    if (p != me) self_pos += (uint64_t)sset_[p];
+  for (int k = 0; k < W; ++k) {
+    const int q = k == W - 1 ? me : (k < me ? k : k + 1);
+    const uint64_t rows = (uint64_t)mat_[q * K + W + me];
+    first[k] = row0;
+    const uint64_t base = q == me ? (uint64_t)(uintptr_t)S + self_pos : (uint64_t)(uintptr_t)Rs + rpos;
+    rec[k] = base;
+    val[k] = base + 32 * rows;
+    row0 += rows;
+    recv_bytes += (uint64_t)mat_[q * K + 2 * W + me];
+    if (q != me) rpos += (uint64_t)rset_[q];
+  }
+  first[W] = row0;
+  uint64_t* dtab = buf<uint64_t>(kTab, 8 * (size_t)W + 8) + 5 * (size_t)W + 1;
   Digest* rkeys = buf<Digest>(kRkeys, ms);
   uint32_t* v0 = buf<uint32_t>(kV0, ms);
   uint32_t* v1 = buf<uint32_t>(kV1, ms);
   uint32_t* fl = buf<uint32_t>(kFl, ms);
   uint32_t* ex = buf<uint32_t>(kEx, ms);
   uint64_t* roff = buf<uint64_t>(kRoff, ms);
+  RT_OK(hipMemcpyAsync(dtab, t, (3 * (size_t)W + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_rs_fill_slots, dim3(grid1(ms)), dim3(kB), 0, s, dtab, W, ms, rkeys, v0, v1,
+                     fl, ex, roff);
+  RT_OK(hipGetLastError());
+  const uint64_t bound = 48 * (uint64_t)ms + recv_bytes;
+  // main shard (tier 0) on the store stream, after the reply gather queued on `s` (the
+  // SETs may overwrite log bytes it reads); the next owner_probe joins it
   RT_OK(hipEventRecord(ev_sfork_, s));
   RT_OK(hipStreamWaitEvent(store_side_, ev_sfork_, 0));
-  hipLaunchKernelGGL(k_rs_fill, dim3(grid1(ms)), dim3(kB), (2 * w_ + 1) * sizeof(int64_t),
-                     store_side_, rrec_, ms, rtable_, w_, rkeys, v0, v1, fl, ex, roff);
-  RT_OK(hipGetLastError());
-  RT_OK(hipEventRecord(ev_fill_, store_side_));
-  shard->store(rkeys, recv, roff, v0, fl, ex, ms, bound, now, store_side_);
+  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, store_side_);
   RT_OK(hipEventRecord(ev_join_, store_side_));
   sets_pending_ = true;
+  // replica (tier 1) on `s`, after this step's local gather (same stream)
+  if (replica) replica->store(rkeys, nullptr, roff, v1, fl, ex, ms, bound, now, s);
 }
 
-void RoutedStep::gather_local(uint8_t* data, hipStream_t s) {
-  if (!(have_replica_ && replica_ && n_local_ > 0 && local_bytes_ > 0)) return;
-  RT_OK(hipEventRecord(ev_lfork_, s));
-  RT_OK(hipStreamWaitEvent(local_side_, ev_lfork_, 0));
-  replica_->gather(rl_loc_, rl_off_, n_, data, local_side_);
-  RT_OK(hipEventRecord(ev_ljoin_, local_side_));
-  local_pending_ = true;
-  local_done_ = true;
-}
-
-void RoutedStep::join_local(hipStream_t s) {
-  if (!local_pending_) return;
-  RT_OK(hipStreamWaitEvent(s, ev_ljoin_, 0));
-  local_pending_ = false;
+// ---- assemble -------------------------------------------------------------------------
+void RoutedStep::assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off,
+                          hipStream_t s) {
+  const int P = par_;
+  if (n_ > 0) {
+    const int64_t slotR = capG_ * 8 + capD_;
+    hipLaunchKernelGGL(k_assemble_slots, dim3(grid1(n_)), dim3(kB), 0, s, route_, n_, w_, rank_,
+                       capG_, capL_, slotR, data, have_replica_ ? rl_size_ : nullptr,
+                       have_replica_ ? rl_off_ : nullptr, out_size, out_off);
+    RT_OK(hipGetLastError());
+    if (first_) expand_coalesced(first_, n_, out_size, out_off, s);  // duplicates
+  }
+  RT_OK(hipEventRecord(ev_asm_[P], s));
+  asm_pending_[P] = true;
 }
 
 void RoutedStep::join_sets(hipStream_t s) {
   if (!sets_pending_) return;
   RT_OK(hipStreamWaitEvent(s, ev_join_, 0));
   sets_pending_ = false;
-}
-
-void RoutedStep::finish(uint8_t* data, const uint8_t* recv, int64_t recv_bytes, HbmCache* shard,
-                        HbmCache* replica, uint32_t now, uint64_t* out_size, uint64_t* out_off,
-                        hipStream_t s) {
-  const int64_t ms = ms_;
-  uint32_t *v1 = nullptr, *fl = nullptr, *ex = nullptr;
-  Digest* rkeys = nullptr;
-  uint64_t* roff = nullptr;
-  const uint64_t bound = 48 * (uint64_t)ms + (uint64_t)recv_bytes;
-  if (ms > 0) {
-    // fork: received-SET unpacking and the main-shard SET chain (latency-bound small
-    // grids) go to the side stream, concurrently with the bandwidth-bound replica
-    // gather below. They touch different shards; everything the caller queued before
-    // (reply gather from the main shard, the wait for the SET payloads) comes first.
-    fork_store(recv, recv_bytes, shard, now, s);
-    rkeys = buf<Digest>(kRkeys, ms);  // filled by k_rs_fill on the side stream (ev_fill_)
-    v1 = buf<uint32_t>(kV1, ms);
-    fl = buf<uint32_t>(kFl, ms);
-    ex = buf<uint32_t>(kEx, ms);
-    roff = buf<uint64_t>(kRoff, ms);
-  }
-  if (local_done_) join_local(s);  // gathered early (gather_local) on the local stream
-  else if (have_replica_ && replica && n_local_ > 0) replica->gather(rl_loc_, rl_off_, n_, data, s);
-  // k_rs_fill reads rtable_, which the next step's count exchange overwrites: later work
-  // on `s` (and the collectives ordered after it) waits for the fill
-  if (ms > 0) RT_OK(hipStreamWaitEvent(s, ev_fill_, 0));
-  if (ms > 0 && replica) {
-    // the replica's own SET rows (tier 1) go after its gather: they may overwrite
-    // log bytes the gather reads (the fill they read was waited for above)
-    replica->store(rkeys, recv, roff, v1, fl, ex, ms, bound, now, s);
-  }
-  if (n_ > 0)
-    hipLaunchKernelGGL(k_assemble, dim3(grid1(n_)), dim3(kB), 0, s, perm_g_, n_, n_remote_,
-                       sizes_in_, gscan_, have_replica_ ? rl_size_ : nullptr,
-                       have_replica_ ? rl_off_ : nullptr, local_bytes_, out_size, out_off);
-  RT_OK(hipGetLastError());
-  if (first_) expand_coalesced(first_, n_, out_size, out_off, s);  // duplicates: claimer's record
-  // join: later work sees the SETs. Deferred (default), the next step's plan (replica
-  // probe, routing: no main-shard access) runs concurrently with the SET chain and its
-  // owner() joins
-  if (!defer_join_) join_sets(s);
 }
 
 }  // namespace shellac

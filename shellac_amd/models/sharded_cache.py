@@ -36,8 +36,9 @@ import torch.distributed as dist
 
 from ..ops import routing as R
 from ..ops.cache import CacheShard, StreamEvent, coalesce, expand, expand_out
-from ..parallel.exchange import (all_gather, all_reduce, all_to_all_rows, all_to_all_single,
-                                 allreduce_stats, dist_info, exchange_counts, segment_sums)
+from ..parallel.exchange import (all_gather, all_gather_rows, all_reduce, all_to_all_rows,
+                                 all_to_all_single, allreduce_stats, dist_info, exchange_counts,
+                                 segment_sums)
 from ..parallel.ring import ShardRing
 from .._native import core as _core
 
@@ -58,9 +59,10 @@ class GetResult:
     _pending: Optional[object] = None  # value all-to-all still in flight (routed serve)
 
     def wait(self) -> "GetResult":
-        """Order the current stream after the value transfer. A routed ``serve`` returns
-        while its value all-to-all is still running so the next step's routing overlaps
-        it; call this before reading ``data`` (``off`` / ``size`` are ready)."""
+        """Order the current stream after the reply transfer. A routed ``serve`` returns
+        while its reply all-to-all (and the per-request assembly that reads its in-band
+        headers) is still running, so the next step's routing overlaps it; call this
+        before reading ``data``, ``off`` or ``size``."""
         if self._pending is not None:
             self._pending.wait()
             self._pending = None
@@ -78,6 +80,18 @@ class SetBatch:
     vlen: torch.Tensor      # int32 [n]
     flags: Optional[torch.Tensor] = None   # int32 [n]
     expire: Optional[torch.Tensor] = None  # int32 [n]
+
+
+class _StreamDone:
+    """A routed step's reply transfer + assembly, finished on a side stream: wait() makes
+    the current stream wait for it (no host synchronisation)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream(self.event.device).wait_event(self.event)
+        return True
 
 
 def records_to_set_batch(keys: torch.Tensor, res: GetResult) -> SetBatch:
@@ -158,27 +172,23 @@ class ShardedCache:
         # the framework-op version (_serve_routed) is the CPU path and the test oracle
         self.fused = True
         self._engine = None
-        self._xtable = None
-        # the routed step's main-shard SET chain is joined by the NEXT step's owner lookup
-        # (RoutedStep::join_sets), so it runs under that step's planning; its input buffer
-        # stays referenced until then. SHELLAC_DEFER_SET_JOIN=0 joins at the end of serve.
-        self.defer_set_join = os.environ.get("SHELLAC_DEFER_SET_JOIN", "1") != "0"
-        self._held_recv = None
-        # SHELLAC_EARLY_LOCAL=1: gather the local replica hits right after host sync 1, on
-        # a third stream, into a response buffer sized from earlier steps' remote bytes
-        # (grown, local part copied over, when a step outgrows it). Measured slightly
-        # slower in the simulated step (sim2 0.770/0.775 -> 0.785/0.787 ms, sim8
-        # 0.810/0.792 -> 0.816/0.796; profiles/r2_early_local_ab.log): the early gather
-        # competes with the request packing and the owner probe. Off by default; the
-        # default gathers them in finish(), under the reply exchange.
-        self.early_local = os.environ.get("SHELLAC_EARLY_LOCAL", "0") == "1"
-        self._remote_cap = 0
+        self._row = self._mat = None
+        # the routed step's main-shard SET chain is joined by the NEXT step's owner probe
+        # (RoutedStep::join_sets), so it runs under that step's planning; its buffers stay
+        # referenced until then
+        self._held = None
+        self._asm = None      # side stream of the routed step's reply assembly
+        # buffers the reply all-to-all (on the communicator's own stream) still reads or
+        # writes after serve returns: released two steps later, once the current stream
+        # has waited for that step's assembly (so the allocator never hands them out while
+        # the transfer runs)
+        self._inflight = []
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
         # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
-        self.overlap_store = os.environ.get("SHELLAC_OVERLAP_STORE", "1") != "0"
+        self.overlap_store = True
         # GET coalescing: the duplicate keys of a batch share one probe and one record
-        # (ops.cache.coalesce); SHELLAC_COALESCE=0 probes and copies every request
-        self.coalesce = os.environ.get("SHELLAC_COALESCE", "1") != "0"
+        # (ops.cache.coalesce); False probes and copies every request (bench --no-coalesce)
+        self.coalesce = True
         # (Two other N=1 schedules were measured slower and removed: a compacting lookup
         # with bump-allocated response offsets, and the SET planning kernels ahead of the
         # lookup; profiles/r2_step_schedule_ab.md.)
@@ -192,7 +202,7 @@ class ShardedCache:
         # release / no system fence (both streams are on one GPU; nothing on the host reads
         # what these events order). One box, two rounds: 0.309 / 0.308 ms per step with
         # "device" vs 0.315 / 0.311 with "system" (profiles/r2_event_fence_ab.log)
-        self.event_fence = os.environ.get("SHELLAC_EVENT_FENCE", "device")
+        self.event_fence = "device"
         self._events = {}
         self._side = None
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
@@ -203,7 +213,8 @@ class ShardedCache:
         self.host_edge = False
         self.gathered_bytes = 0  # response bytes the serving steps produced
         self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
-                      "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0}
+                      "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0,
+                      "slot_overflow_rows": 0, "reply_dropped_rows": 0}
 
     # ------------------------------------------------------------------------------
     def sync_sets(self) -> None:
@@ -214,7 +225,13 @@ class ShardedCache:
         e = self._engine
         if e is not None and e.sets_pending:
             e.join_sets(torch.cuda.current_stream(self.device).cuda_stream)
-            self._held_recv = None
+            self._held = None
+
+    def _reset_exchange(self) -> None:
+        """The traffic matrix changes (new ring, new hot set): the routed step's next
+        serve recalibrates its slot capacities (collective: every rank calls it)."""
+        if self._engine is not None:
+            self._engine.reset_caps()
 
     def _route(self, keys: torch.Tensor):
         return R.route(keys, self.ring_pts, self.ring_own, self.world)
@@ -437,17 +454,20 @@ class ShardedCache:
 
     def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
                             now: Optional[int] = None) -> GetResult:
-        """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep):
-        every step between the collectives is a fused kernel sequence over a grow-only
-        device arena; Python issues the all-to-alls and nothing else. Same results as
-        the framework-op version (tests/test_hbm_gpu.py); the wire layout differs in
-        one respect: SET payloads leave the synchronous request exchange and travel in
-        their own asynchronous all-to-all on the data communicator, so the owner lookup
-        and the second host sync do not wait for them (xGMI is point-to-point: at N=2
-        one link carries every byte, so what sits on the critical path matters)."""
+        """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep), with
+        no host synchronisation between planning and the result (after one calibrating
+        step): GET requests and replies travel in fixed-capacity per-peer slots whose
+        counts and (size, offset) headers ride in-band, so the all-to-alls need no split
+        sizes from the device; capacities every rank agrees on come from the demand the
+        ranks all-gathered in earlier steps, and a row that does not fit is a counted
+        miss. SETs travel with exact sizes the host reads mid-step, while the GPU is busy
+        with the GET exchange queued before. Same results as the framework-op version
+        (tests); the reply transfer and the per-request assembly finish on a side stream
+        (``GetResult.wait()``), under the next step's planning."""
         c = _core()
         dev, w, me = self.device, self.world, self.rank
-        st = torch.cuda.current_stream(dev).cuda_stream
+        cur = torch.cuda.current_stream(dev)
+        st = cur.cuda_stream
         i64, u8 = torch.int64, torch.uint8
         n = keys.shape[0]
         ns_in = batch.keys.shape[0]
@@ -458,9 +478,10 @@ class ShardedCache:
         e = self._engine
         if e is None:
             e = self._engine = c.RoutedStep(w, me, dev.index)
-            e.set_defer_join(self.defer_set_join)
-            # [table (3w) | rtable (3w) | extras (3)]: read back with one copy
-            self._xtable = torch.empty(6 * w + 3, dtype=i64, device=dev)
+            k = e.row_words
+            self._row = torch.zeros(k, dtype=i64, device=dev)
+            self._mat = torch.zeros(w * k, dtype=i64, device=dev)
+            self._asm = torch.cuda.Stream(device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
         if fanout and self._hot_dir is None:
@@ -468,80 +489,89 @@ class ShardedCache:
         e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0,
                   self._hot_dir.data_ptr() if fanout else 0)
         rep = self.replica._impl if self.replica is not None else None
-        table, rtable = self._xtable[: 3 * w], self._xtable[3 * w: 6 * w]
+        while len(self._inflight) >= 2:
+            ev, _bufs = self._inflight.pop(0)
+            cur.wait_event(ev)  # long complete: frees the buffers for reuse on this stream
+        cap_g, cap_d, cap_l, cal = e.caps(n)
         ph = _Phases("serve.")
         ph.next("plan")
+        # G = [recv: w-1 slots | self slot | send: w-1 slots] of cap_g digests
+        gslot = 16 * cap_g
+        G = torch.empty((2 * w - 1) * gslot, dtype=u8, device=dev)
         e.plan(keys.data_ptr(), n, rep, now, batch.keys.data_ptr(), batch.vlen.data_ptr(),
                batch.flags.data_ptr() if batch.flags is not None else 0,
                batch.expire.data_ptr() if batch.expire is not None else 0,
                batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
-               table.data_ptr(), st, self.coalesce)
-        ph.next("count_exchange")
-        all_to_all_single(rtable, table, group=self.group)
-        h = e.read_counts(rtable.data_ptr(), st)                          # sync 1
-        g_rows = h[0: 3 * w: 3]
-        rg_rows = h[3 * w: 6 * w: 3]
-        # request region (GET digests + SET records) and value region (SET payloads)
-        send_q = [16 * h[3 * p] + 32 * h[3 * p + 1] for p in range(w)]
-        recv_q = [16 * h[3 * w + 3 * p] + 32 * h[3 * w + 3 * p + 1] for p in range(w)]
-        send_v = [h[3 * p + 2] for p in range(w)]
-        recv_v = [h[3 * w + 3 * p + 2] for p in range(w)]
-        sq, rq, sv, rv = sum(send_q), sum(recv_q), sum(send_v), sum(recv_v)
-        # n_local counts replica hits and coalesced duplicates (neither leaves the GPU)
-        n_local, local_bytes, n_dup = h[6 * w], h[6 * w + 1], h[6 * w + 2]
-        ph.next("pack_requests")
-        send = torch.empty(sq + sv + 16, dtype=u8, device=dev)
-        e.pack(send.data_ptr(), st)
-        data = None
-        if self.early_local and rep is not None and local_bytes > 0:
-            data = torch.empty(local_bytes + self._remote_cap + 16, dtype=u8, device=dev)
-            e.gather_local(data.data_ptr(), st)
-        recv = torch.empty(rq + rv + 16, dtype=u8, device=dev)
+               G.data_ptr(), self._row.data_ptr(), st, self.coalesce)
+        ph.next("row_allgather")
+        all_gather_rows(self._mat, self._row, self.group, peer_blocks=4)
+        e.publish(self._mat.data_ptr(), st)
+        if cal:
+            e.calibrate_local()                                   # calibration: host read
         ph.next("request_a2a")
-        all_to_all_single(recv[:rq], send[:sq], output_split_sizes=recv_q,
-                          input_split_sizes=send_q, group=self.group)
-        # SET payloads travel on the data communicator while the owner probes and the
-        # reply sizes are exchanged; only the SET stores in finish() wait for them
-        vwork = all_to_all_single(recv[rq: rq + rv], send[sq: sq + sv], output_split_sizes=recv_v,
-                                  input_split_sizes=send_v, group=self.data_group, async_op=True)
-        ph.next("owner_lookup")
-        mg = e.mg
-        sizes_out = torch.empty(mg + 1, dtype=i64, device=dev)
-        e.owner(recv.data_ptr(), self.shard._impl, now, sizes_out.data_ptr(), st)
-        sizes_in = all_to_all_rows(sizes_out[:mg], rg_rows, g_rows, self.group)
-        ph.next("reply_sizes")
-        nb = e.reply_sizes(sizes_in.data_ptr(), st)                        # sync 2
-        rep_b, got_b = nb[:w], nb[w:]
-        ph.next("reply_a2a+set_store")
-        reply = torch.empty(max(sum(rep_b), 16), dtype=u8, device=dev)
-        e.gather_replies(self.shard._impl, reply.data_ptr(), st)
-        need = local_bytes + sum(got_b) + 16
-        if data is None:
-            data = torch.empty(need, dtype=u8, device=dev)
-        elif data.numel() < need:
-            # outgrown: the local part moves over once its early gather is done
-            nd = torch.empty(need, dtype=u8, device=dev)
-            e.join_local(st)
-            nd[:local_bytes].copy_(data[:local_bytes])
-            data = nd
-        if self.early_local:
-            self._remote_cap = max(self._remote_cap, int(sum(got_b) * 1.25) // 16 * 16)
-        work = all_to_all_single(data[local_bytes: local_bytes + sum(got_b)], reply[: sum(rep_b)],
-                                 output_split_sizes=got_b, input_split_sizes=rep_b,
-                                 group=self.data_group, async_op=True)
+        if w > 1:
+            sp = [0 if p == me else gslot for p in range(w)]
+            all_to_all_single(G[: (w - 1) * gslot], G[w * gslot:], output_split_sizes=sp,
+                              input_split_sizes=sp, group=self.group)
+        ph.next("owner")
+        e.owner_probe(G.data_ptr(), self.shard._impl, now, st)
+        if cal:
+            dem = torch.empty(w, dtype=i64, device=dev)
+            e.owner_demand(dem.data_ptr(), st)
+            dmat = torch.empty(w * w, dtype=i64, device=dev)
+            all_gather_rows(dmat, dem, self.group, peer_blocks=1)
+            e.calibrate_reply(dmat.data_ptr())                    # calibration: host read
+            cap_g, cap_d, cap_l, _ = e.caps(n)
+        slot_r = 8 * cap_g + cap_d
+        # the response buffer: [local capL | w-1 reply slots (recv) | self reply slot]
+        R = torch.empty(max((w - 1) * slot_r, 16), dtype=u8, device=dev)
+        data = torch.empty(cap_l + w * slot_r + 16, dtype=u8, device=dev)
+        e.owner_reply(self.shard._impl, R.data_ptr(), data.data_ptr(), st)
+        work = None
+        if w > 1:
+            sp = [0 if p == me else slot_r for p in range(w)]
+            work = all_to_all_single(data[cap_l: cap_l + (w - 1) * slot_r], R[: (w - 1) * slot_r],
+                                     output_split_sizes=sp, input_split_sizes=sp,
+                                     group=self.data_group, async_op=True)
+        e.gather_local(data.data_ptr(), st)
+        local_done = torch.cuda.Event()
+        local_done.record(cur)
+        ph.next("set_exchange")
+        h = e.set_splits()           # waits for the published rows: the GPU is still busy
+        send, recv = h[:w], h[w:2 * w]
+        n_local, n_dup, off_rank, over, dropped = h[2 * w: 2 * w + 5]
+        so, ro = sum(send) - send[me], sum(recv) - recv[me]
+        S = torch.empty(sum(send) + 16, dtype=u8, device=dev)
+        e.pack_sets(S.data_ptr(), st)
+        Rs = torch.empty(ro + 16, dtype=u8, device=dev)
+        if w > 1:
+            all_to_all_single(Rs[:ro], S[:so],
+                              output_split_sizes=[0 if q == me else recv[q] for q in range(w)],
+                              input_split_sizes=[0 if p == me else send[p] for p in range(w)],
+                              group=self.group)
+        e.store_sets(S.data_ptr(), Rs.data_ptr(), self.shard._impl, rep, now, st)
+        # the main-shard SET chain reads S / Rs until the next step's owner probe joins it
+        self._held = (S, Rs) if e.sets_pending else None
+        ph.next("assemble")
         out = torch.empty((2, n), dtype=i64, device=dev)
-        vwork.wait()  # stream-ordered: the SET stores below read the value region
-        e.finish(data.data_ptr(), recv.data_ptr(), rq + rv, self.shard._impl, rep, now,
-                 out[0].data_ptr(), out[1].data_ptr(), st)
-        # the main-shard SET chain reads `recv` until the next step's owner() joins it (the
-        # previous step's buffer is released here: this step's owner() has joined)
-        self._held_recv = recv if e.sets_pending else None
-        self.stats["remote_gets"] += (n - n_local) - int(g_rows[me])
+        side = self._asm
+        side.wait_event(local_done)
+        with torch.cuda.stream(side):
+            if work is not None:
+                work.wait()          # the side stream waits for the reply all-to-all
+            e.assemble(data.data_ptr(), out[0].data_ptr(), out[1].data_ptr(), side.cuda_stream)
+        data.record_stream(side)
+        out.record_stream(side)
+        done = torch.cuda.Event()
+        done.record(side)
+        self._inflight.append((done, (R, data)))
+        self.stats["remote_gets"] += off_rank
         self.stats["replica_hits"] += n_local - n_dup
         self.stats["coalesced_gets"] += n_dup
+        self.stats["slot_overflow_rows"] += over
+        self.stats["reply_dropped_rows"] += dropped
         ph.end()
-        # the value transfer completes in the background: GetResult.wait() before reading
-        return GetResult(data, out[1], out[0], _pending=work)
+        return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
 
     def _set_rows(self, batch: SetBatch):
         """Routing of a SET batch: (dest int32 [m], records int64 [m, 4], val_off [m]).
@@ -876,10 +906,12 @@ class ShardedCache:
         if hot.shape[0] == 0:
             self.replica.flush()
             self._hot = None
+            self._reset_exchange()
             return 0
         order = torch.argsort(hot[:, 0])
         self._hot = hot.index_select(0, order).contiguous()
         self._hot_dir = None
+        self._reset_exchange()
         saved = self.replica
         self.replica = None                               # fetch through the owners only
         try:
@@ -931,6 +963,7 @@ class ShardedCache:
             batch = records_to_set_batch(mkeys, GetResult(data, lk.off[:moved], lk.size[:moved]))
         self.ring = ring
         self.ring_pts, self.ring_own = ring.tensors(self.device)
+        self._reset_exchange()
         if batch is not None:
             self.set(batch, now)                  # lands on the new owners
             if moved:
@@ -950,6 +983,7 @@ class ShardedCache:
         if self.replica is not None:
             self.replica.flush()
             self._hot = None
+            self._reset_exchange()
 
     def restore_shard(self, rank: int, now: Optional[int] = None) -> int:
         """Collective. Re-admit ``rank``; objects written while it was out migrate

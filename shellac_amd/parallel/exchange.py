@@ -88,6 +88,38 @@ def _default_group():
     return distributed_c10d._get_default_group()
 
 
+def _mirror_row(row: torch.Tensor, world: int, me: int, q: int, peer_blocks: int) -> torch.Tensor:
+    """Rank q's row under MirrorComm's symmetric traffic: what q sends to x is what I send
+    to x with the roles of me and q exchanged (q -> me equals me -> q)."""
+    r = row.clone()
+    if q != me:
+        for b in range(peer_blocks):
+            r[b * world + me], r[b * world + q] = row[b * world + q], row[b * world + me]
+    return r
+
+
+def all_gather_rows(out: torch.Tensor, row: torch.Tensor, group=None, peer_blocks: int = 0) -> None:
+    """out[q * K : (q + 1) * K] = rank q's ``row`` (K words) for every rank q, stream-ordered
+    (the current stream waits for it). ``peer_blocks``: the row starts with that many
+    blocks of one entry per peer (used only to mirror rows under ``MirrorComm``)."""
+    rank, world = dist_info(group)
+    if isinstance(group, MirrorComm):
+        k = row.numel()
+        for q in range(world):
+            out[q * k:(q + 1) * k].copy_(_mirror_row(row, world, rank, q, peer_blocks))
+        return
+    if isinstance(group, BounceComm):
+        host = [torch.empty(row.shape, dtype=row.dtype) for _ in range(world)]
+        dist.all_gather(host, row.cpu(), group=group.pg)
+        out.copy_(torch.cat(host))
+        return
+    pg = group if group is not None else _default_group()
+    if hasattr(pg, "_allgather_base"):
+        pg._allgather_base(out, row).wait()  # the C++ collective (no Python-wrapper overhead)
+    else:
+        dist.all_gather_into_tensor(out, row, group=group)
+
+
 def all_gather(tensors: list, t: torch.Tensor, group=None) -> None:
     if isinstance(group, MirrorComm):
         for x in tensors:

@@ -306,6 +306,46 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
     assert 0 < s2["replica_hits"] < s1["replica_hits"]
 
 
+def test_routed_step_slot_overflow_is_a_counted_miss(cuda_dev):
+    """Fixed-capacity exchange: GET rows past a peer slot's capacity and replies past its
+    data capacity come back as misses (never wrong data) and are counted; with the
+    capacities the executor learns from the observed demand, the next steps are exact."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+    from shellac_amd.parallel.exchange import MirrorComm
+
+    wl = Workload(30000, cuda_dev)
+    sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(3),
+                      replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev))
+    sc.set(wl.set_batch(torch.arange(0, 30000, device=cuda_dev)))
+    ids = wl.sample_ids(6000, 3)
+    keys = wl.digests.index_select(0, ids).contiguous()
+    expect = [wl.expected_value(i) for i in ids.tolist()]
+
+    def step(k):
+        r = sc.serve(keys, wl.set_batch(wl.uniform_ids(256, 20 + k))).wait()
+        return [None if x is None else x[0] for x in unpack_records(r.data, r.off, r.size)]
+
+    got = step(0)  # calibrating step: exact capacities
+    assert got == expect
+    assert sc.stats["slot_overflow_rows"] == 0
+    e = sc._engine
+    for cap_g, cap_d in ((64, 1 << 20), (1 << 14, 64 << 10)):  # full GET slots, full replies
+        e.set_cap_override(cap_g, cap_d, 8 << 20)
+        before = dict(sc.stats)
+        got = step(1)
+        wrong = [i for i, (g, w) in enumerate(zip(got, expect)) if g is not None and g != w]
+        misses = sum(g is None for g in got)
+        assert not wrong and misses > 0
+        if cap_g == 64:
+            assert sc.stats["slot_overflow_rows"] > before["slot_overflow_rows"]
+    e.set_cap_override(0, 0, 0)
+    step(2)  # the dropped replies of the last forced step are reported one step later
+    assert sc.stats["reply_dropped_rows"] > 0
+    for k in range(3, 5):
+        assert step(k) == expect  # learned capacities: exact again
+
+
 @pytest.mark.parametrize("n,nb", [(1, 2), (777, 3), (100003, 9), (300000, 65)])
 def test_group_rows_counting_sort(cuda_dev, n, nb):
     """csrc/router.hip counting sort: bucket counts, a permutation, rows moved with it,
