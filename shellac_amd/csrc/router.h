@@ -91,9 +91,10 @@ class RoutedStep {
   int64_t row_words() const { return 4 * (int64_t)w_ + kExtras; }
 
   // ---- capacities (identical on every rank: derived from all-gathered rows) ----
-  // {capG rows, capD reply bytes, capL local bytes, calibrating (0/1)} for a GET batch
-  // of n rows. While calibrating capG = n (every row fits), capD and capL are set by
-  // calibrate_local / calibrate_reply during the step.
+  // {capG rows, capD reply bytes, capL local bytes, calibrating, calibrating local} for
+  // a GET batch of n rows. While calibrating capG = n (every row fits), capD is set by
+  // calibrate_reply during the step; capL (per GET row from this rank's history) by
+  // calibrate_local when there is no history yet.
   std::vector<int64_t> caps(int64_t n) const;
   void reset_caps();  // next step calibrates (new ring, new hot set)
   // Tests: fixed capacities (every rank the same), overriding the policy; 0s clear it.
@@ -172,7 +173,8 @@ class RoutedStep {
   int64_t capG_ = 0, capD_ = 0, capL_ = 0;
   std::vector<int64_t> ovr_ = {0, 0, 0};
   bool calibrating_ = true;
-  std::vector<int64_t> hist_g_, hist_d_, hist_l_;
+  std::vector<int64_t> hist_g_, hist_d_;
+  std::vector<double> hist_lr_;  // local bytes per GET row
   // per-step state
   int par_ = 0;  // step parity: the buffers the deferred assemble reads
   int64_t n_ = 0, ns_ = 0, ns_rows_ = 0, ms_ = 0;

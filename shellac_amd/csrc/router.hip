@@ -728,19 +728,24 @@ int64_t hist_max(const std::vector<int64_t>& h) {
 }  // namespace
 
 std::vector<int64_t> RoutedStep::caps(int64_t n) const {
+  // the local region is this rank's own: sized per GET row from its history (no
+  // agreement needed), calibrated by a host read when there is none yet
+  const bool cal_l = hist_lr_.empty() && n > 0;
+  double lr = 0;
+  for (double v : hist_lr_) lr = std::max(lr, v);
+  const int64_t l = cal_l ? capL_ : align_up64((int64_t)(lr * 1.15 * (double)n) + (1 << 20), 4096);
   if (ovr_[0] > 0 && !calibrating_)
-    return {align_up64(ovr_[0], 2), align_up64(ovr_[1], 16), align_up64(ovr_[2], 16), 0};
-  if (calibrating_) return {std::max<int64_t>(align_up64(n, 64), 64), capD_, capL_, 1};
+    return {align_up64(ovr_[0], 2), align_up64(ovr_[1], 16), align_up64(ovr_[2], 16), 0, 0};
+  if (calibrating_) return {std::max<int64_t>(align_up64(n, 64), 64), capD_, l, 1, cal_l};
   const int64_t g = align_up64(hist_max(hist_g_) * 11 / 10 + 256, 64);
   const int64_t d = align_up64(hist_max(hist_d_) * 21 / 20 + (256 << 10), 4096);
-  const int64_t l = align_up64(hist_max(hist_l_) * 11 / 10 + (1 << 20), 4096);
-  return {g, d, l, 0};
+  return {g, d, l, 0, cal_l};
 }
 
 void RoutedStep::reset_caps() {
   hist_g_.clear();
   hist_d_.clear();
-  hist_l_.clear();
+  hist_lr_.clear();
   calibrating_ = true;
   capD_ = capL_ = 0;
 }
@@ -757,7 +762,10 @@ void RoutedStep::note_matrix() {
   push_hist(&hist_g_, mg);
   // the reply column is the previous step's demand (none before the first step)
   if (!calibrating_) push_hist(&hist_d_, md);
-  push_hist(&hist_l_, mat_[rank_ * K + 4 * W + 1]);
+  if (n_ > 0) {
+    hist_lr_.push_back((double)mat_[rank_ * K + 4 * W + 1] / (double)n_);
+    if (hist_lr_.size() > kHist) hist_lr_.erase(hist_lr_.begin());
+  }
   calibrating_ = false;
 }
 
@@ -773,10 +781,8 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   const int nb = W + 1;
   const std::vector<int64_t> c = caps(n);
   capG_ = c[0];
-  if (!calibrating_) {
-    capD_ = c[1];
-    capL_ = c[2];
-  }
+  if (!calibrating_) capD_ = c[1];
+  if (!c[4]) capL_ = c[2];
   par_ ^= 1;
   const int P = par_;
   n_ = n;
@@ -886,7 +892,7 @@ void RoutedStep::calibrate_local() {
   SH_CHECK(published_, "RoutedStep: publish before calibrate_local");
   RT_OK(hipEventSynchronize(ev_pub_));
   const int64_t lb = host_mat_[rank_ * row_words() + 4 * w_ + 1];
-  capL_ = align_up64(lb * 11 / 10 + (1 << 20), 4096);
+  capL_ = align_up64(lb * 23 / 20 + (1 << 20), 4096);
 }
 
 // ---- owner --------------------------------------------------------------------------

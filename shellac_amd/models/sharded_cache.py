@@ -233,6 +233,15 @@ class ShardedCache:
         if self._engine is not None:
             self._engine.reset_caps()
 
+    def recalibrate(self) -> None:
+        """Collective. The routed step sizes its per-peer exchange slots from the demand
+        of earlier steps; after a change of batch shape (say, a much larger GET batch)
+        the first steps would answer the rows that do not fit as misses until the
+        capacities catch up. Calling this on every rank makes the next serve measure the
+        new demand exactly (one step with two host reads) instead."""
+        self.sync_sets()
+        self._reset_exchange()
+
     def _route(self, keys: torch.Tensor):
         return R.route(keys, self.ring_pts, self.ring_own, self.world)
 
@@ -492,7 +501,7 @@ class ShardedCache:
         while len(self._inflight) >= 2:
             ev, _bufs = self._inflight.pop(0)
             cur.wait_event(ev)  # long complete: frees the buffers for reuse on this stream
-        cap_g, cap_d, cap_l, cal = e.caps(n)
+        cap_g, cap_d, cap_l, cal, cal_l = e.caps(n)
         ph = _Phases("serve.")
         ph.next("plan")
         # G = [recv: w-1 slots | self slot | send: w-1 slots] of cap_g digests
@@ -506,7 +515,7 @@ class ShardedCache:
         ph.next("row_allgather")
         all_gather_rows(self._mat, self._row, self.group, peer_blocks=4)
         e.publish(self._mat.data_ptr(), st)
-        if cal:
+        if cal_l:
             e.calibrate_local()                                   # calibration: host read
         ph.next("request_a2a")
         if w > 1:
@@ -521,7 +530,8 @@ class ShardedCache:
             dmat = torch.empty(w * w, dtype=i64, device=dev)
             all_gather_rows(dmat, dem, self.group, peer_blocks=1)
             e.calibrate_reply(dmat.data_ptr())                    # calibration: host read
-            cap_g, cap_d, cap_l, _ = e.caps(n)
+        if cal or cal_l:
+            cap_g, cap_d, cap_l = e.caps(n)[:3]
         slot_r = 8 * cap_g + cap_d
         # the response buffer: [local capL | w-1 reply slots (recv) | self reply slot]
         R = torch.empty(max((w - 1) * slot_r, 16), dtype=u8, device=dev)
