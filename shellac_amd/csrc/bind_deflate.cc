@@ -58,6 +58,7 @@ void bind_deflate(py::module_& m) {
       .def_readonly("in_bytes", &GzipStats::in_bytes)
       .def_readonly("out_bytes", &GzipStats::out_bytes)
       .def_readonly("stored_blocks", &GzipStats::stored_blocks)
+      .def_readonly("inflated", &GzipStats::inflated)
       .def_readonly("last_pack_ms", &GzipStats::last_pack_ms)
       .def_readonly("last_gpu_ms", &GzipStats::last_gpu_ms)
       .def_readonly("last_assemble_ms", &GzipStats::last_assemble_ms);
@@ -81,6 +82,19 @@ void bind_deflate(py::module_& m) {
         }
         return to_list(out);
       })
+      .def("inflate", [](GpuGzip& g, const py::list& in, uint64_t max_out) {
+        auto v = views(in);
+        std::vector<std::string> out;
+        std::vector<uint8_t> ok;
+        {
+          py::gil_scoped_release nogil;
+          out = g.inflate(v, &ok, max_out);
+        }
+        py::list l(out.size());
+        for (size_t i = 0; i < out.size(); ++i)
+          l[i] = ok[i] ? py::object(py::bytes(out[i])) : py::object(py::none());
+        return l;
+      }, py::arg("members"), py::arg("max_out") = 64ull << 20)
       .def("stats", &GpuGzip::stats)
       .def_property_readonly("device", &GpuGzip::device);
 }

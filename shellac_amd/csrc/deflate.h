@@ -44,7 +44,7 @@ constexpr int kDeflateBlock = 32768;                 // input bytes per block (=
 constexpr int kDeflateStride = kDeflateBlock + 64;   // output bytes reserved per block
 
 struct GzipStats {
-  uint64_t inputs = 0, blocks = 0, in_bytes = 0, out_bytes = 0, stored_blocks = 0;
+  uint64_t inputs = 0, blocks = 0, in_bytes = 0, out_bytes = 0, stored_blocks = 0, inflated = 0;
   // last call, milliseconds: host packing, GPU (copies in + kernel + copies out), assembly
   double last_pack_ms = 0, last_gpu_ms = 0, last_assemble_ms = 0;
 };
@@ -60,6 +60,12 @@ class GpuGzip {
   std::vector<std::string> compress(const std::vector<std::string_view>& in);
   // Raw DEFLATE streams only (no gzip header / trailer), for tests and benchmarks.
   std::vector<std::string> deflate(const std::vector<std::string_view>& in);
+  // Batch gunzip: one member per input. ok[i] = 1 when member i decoded on the GPU to
+  // exactly its ISIZE bytes with a matching CRC-32 (else out[i] is empty: a corrupt
+  // member, framing the GPU path does not take, or ISIZE > max_out — the caller may fall
+  // back to zlib, which also reports the error).
+  std::vector<std::string> inflate(const std::vector<std::string_view>& in,
+                                   std::vector<uint8_t>* ok, uint64_t max_out);
   GzipStats stats() const { return stats_; }
   int device() const { return device_; }
 
@@ -78,9 +84,8 @@ class GpuGzip {
   uint64_t *h_tab_ = nullptr, *d_tab_ = nullptr;
   uint32_t *h_len_ = nullptr, *d_len_ = nullptr;
   // two-pass encoding: tokens (device), pass-1 results, per-block plans
-  uint32_t *d_tok_ = nullptr, *h_res_ = nullptr, *d_res_ = nullptr, *h_plan_ = nullptr,
-           *d_plan_ = nullptr;
-  size_t d_tok_cap_ = 0, h_res_cap_ = 0, d_res_cap_ = 0, h_plan_cap_ = 0, d_plan_cap_ = 0;
+  uint32_t *d_tok_ = nullptr, *d_res_ = nullptr, *d_plan_ = nullptr, *d_slot_ = nullptr;
+  size_t d_tok_cap_ = 0, d_res_cap_ = 0, d_plan_cap_ = 0, d_slot_cap_ = 0;
   size_t h_in_cap_ = 0, d_in_cap_ = 0, h_out_cap_ = 0, d_out_cap_ = 0, h_tab_cap_ = 0,
          d_tab_cap_ = 0, h_len_cap_ = 0, d_len_cap_ = 0;
 };

@@ -25,8 +25,6 @@ namespace {
 constexpr int kHashBits = 12;
 constexpr int kHashSize = 1 << kHashBits;
 constexpr int kMaxMatch = 258;
-// plan record per block: mode, header bits, total bytes, codes, header bytes (<= 640)
-constexpr int kPlanWords = 3 + kHistSyms + 160;
 
 __device__ __forceinline__ uint32_t rev(uint32_t code, int len) {
   return __builtin_bitreverse32(code) >> (32 - len);
@@ -88,19 +86,74 @@ __device__ __forceinline__ void dist_sym(int dist, int* sym, int* nb, uint32_t* 
   }
 }
 
-// Pass 1: one wave per block. The block and a 4096-entry hash head table live in LDS;
-// the wave parses greedily (the 64 lanes compare a candidate 64 bytes per ballot and hash
-// the positions a match covers in parallel) and writes tokens (huffman.h) plus the
-// block's literal/length and distance histogram, and the block's CRC register.
+// Pass 1: one wave per block; the block, a 4096-entry hash head table and a per-position
+// hash chain live in LDS.
+//  a. CRC register of the block (lane slices combined by GF(2) multiplies).
+//  b. Hash chains, 64 positions per step: every lane hashes its position, finds the lanes
+//     of the step with the same hash by 13 ballots (bitwise match), and links to the
+//     latest earlier one, or to the head table's entry as of the step; the last lane of
+//     each hash then updates the head. prev[p] = the previous position with p's hash.
+//  c. Parse, one 1/64 segment of the block per lane: at each position the lane walks up
+//     to kChain candidates of the chain, compares 4 bytes at a time (aligned LDS words
+//     combined by alignbyte), keeps the longest match, and defers to the next position
+//     when that one matches longer (lazy matching, as zlib's levels 4-9). A match never
+//     crosses the lane's segment end, so the segments' token lists concatenate.
+//  d. The lanes' token lists are compacted into the block's token array (scan of the
+//     counts); the literal/length + distance histogram is counted in LDS on the way.
 // tab[2b] = src offset, tab[2b+1] = len | final << 32.
+constexpr int kChain = 12;        // chain candidates examined per position
+constexpr int kNiceLen = 96;      // stop searching at a match this long
+constexpr int kLazyLen = 24;      // below this, try the next position (lazy matching)
+constexpr int kSegs = 64;         // parse segments per block (one per lane)
+
+__device__ __forceinline__ uint32_t lds_word_at(const uint32_t* w, uint32_t x) {
+  // bytes x..x+3 from aligned words (LDS has no unaligned dword reads)
+  const uint32_t lo = w[x >> 2], hi = w[(x >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, x & 3);
+}
+
+// Longest match at p among the chain candidates (length capped at maxl); returns the
+// length, *dist the distance.
+__device__ __forceinline__ int best_match(const uint8_t* s_in, const uint32_t* s_w,
+                                          const uint16_t* s_prev, int p, int maxl, int* dist) {
+  int bl = 0, bd = 0;
+  int c = s_prev[p];
+  for (int depth = 0; c && depth < kChain; ++depth) {
+    const int q = c - 1;
+    // quick reject: the byte that would extend the best match so far must match
+    if (bl < maxl && s_in[q + bl] == s_in[p + bl]) {
+      int len = 0;
+      while (len < maxl) {
+        const uint32_t x = lds_word_at(s_w, (uint32_t)(q + len)) ^ lds_word_at(s_w, (uint32_t)(p + len));
+        if (x) {
+          len += (int)(__builtin_ctz(x) >> 3);
+          break;
+        }
+        len += 4;
+      }
+      len = min(len, maxl);
+      if (len > bl) {
+        bl = len;
+        bd = p - q;
+        if (bl >= kNiceLen || bl >= maxl) break;
+      }
+    }
+    c = s_prev[q];
+  }
+  *dist = bd;
+  return bl;
+}
+
 __global__ __launch_bounds__(64) void k_lz77(const uint8_t* __restrict__ src,
                                              const uint64_t* __restrict__ tab, int64_t nblk,
                                              uint32_t* __restrict__ tok,
+                                             uint32_t* __restrict__ stage,
                                              uint32_t* __restrict__ hist,
                                              uint32_t* __restrict__ ntok,
                                              uint32_t* __restrict__ out_crc) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kDeflateBlock + 16];
-  __shared__ uint32_t s_head[kHashSize];
+  __shared__ uint16_t s_prev[kDeflateBlock];
+  __shared__ uint16_t s_head[kHashSize];
   __shared__ uint32_t s_hist[kHistSyms];
   const int64_t b = blockIdx.x;
   if (b >= nblk) return;
@@ -113,23 +166,22 @@ __global__ __launch_bounds__(64) void k_lz77(const uint8_t* __restrict__ src,
   u32x4* s4 = reinterpret_cast<u32x4*>(s_in);
   const int n16 = (n + 15) / 16;
   for (int i = lane; i < n16; i += 64) s4[i] = in4[i];
-  for (int i = n + lane; i < n16 * 16 + 16; i += 64) s_in[i] = 0;  // zero tail (hash reads)
+  for (int i = n + lane; i < n16 * 16 + 16; i += 64) s_in[i] = 0;  // zero tail (word reads)
   for (int i = lane; i < kHistSyms; i += 64) s_hist[i] = 0;
-  // CRC table in the head table's space (it is cleared after the CRC pass)
+  // CRC table in the chain array's space (rebuilt below)
+  uint32_t* s_crc = reinterpret_cast<uint32_t*>(s_prev);
   for (int i = lane; i < 256; i += 64) {
     uint32_t c = (uint32_t)i;
     for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
-    s_head[i] = c;
+    s_crc[i] = c;
   }
   __syncthreads();
   {
-    // CRC register of the block from a zero register (the host folds blocks together):
-    // lane i takes slice [i*S, min(n, (i+1)*S)), then shifts its register past the
-    // bytes after its slice and the wave XORs the registers
+    // CRC register of the block from a zero register (the host folds blocks together)
     const int S = (n + 63) / 64;
     const int a0 = min(n, lane * S), a1 = min(n, a0 + S);
     uint32_t r = 0;
-    for (int p = a0; p < a1; ++p) r = s_head[(r ^ s_in[p]) & 0xFF] ^ (r >> 8);
+    for (int p = a0; p < a1; ++p) r = s_crc[(r ^ s_in[p]) & 0xFF] ^ (r >> 8);
     r = crc_mulmod(crc_x8n((uint64_t)(n - a1)), r);
     for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
     if (lane == 0) out_crc[b] = r;
@@ -137,67 +189,135 @@ __global__ __launch_bounds__(64) void k_lz77(const uint8_t* __restrict__ src,
   __syncthreads();
   for (int i = lane; i < kHashSize; i += 64) s_head[i] = 0;
   __syncthreads();
-
-  uint32_t* t = tok + b * (int64_t)kDeflateBlock;
-  int nt = 0;
-  int pos = 0;
-  while (pos < n) {
-    int len = 0, dist = 0;
-    if (pos + 3 < n) {
-      const uint32_t h = hash4(s_in, pos);
-      const uint32_t c = s_head[h];
-      // one wave per workgroup: its LDS operations complete in issue order, so a wave
-      // barrier (no s_barrier, only no code motion across it) orders the read before
-      // lane 0 replaces the head
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) s_head[h] = (uint32_t)pos + 1;
-      if (c) {
-        const int cand = (int)c - 1;
-        const int maxl = min(kMaxMatch, n - pos);
-        for (int base = 0; base < maxl; base += 64) {
-          const int k = base + lane;
-          const bool eq = k < maxl && s_in[cand + k] == s_in[pos + k];
-          const unsigned long long miss = __ballot(!eq);
-          if (miss) {
-            len = base + __ffsll((long long)miss) - 1;
-            break;
-          }
-          len = base + 64;
-        }
-        len = min(len, maxl);
-        dist = pos - cand;
-      }
+  // b. hash chains
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int p = c0 + lane;
+    const bool valid = p + 3 < n;
+    const uint32_t h = valid ? hash4(s_in, p) : 0u;
+    const uint32_t key = valid ? (h | (1u << kHashBits)) : 0u;  // bit 12: has a hash
+    unsigned long long same = ~0ull;
+#pragma unroll
+    for (int k = 0; k <= kHashBits; ++k) {
+      const unsigned long long bal = __ballot((key >> k) & 1u);
+      same &= ((key >> k) & 1u) ? bal : ~bal;
     }
-    if (len >= 3) {
-      if (lane == 0) {
-        int ls, lb, ds, db;
-        uint32_t lv, dv;
-        len_sym(len, &ls, &lb, &lv);
-        dist_sym(dist, &ds, &db, &dv);
-        t[nt] = kTokMatch | ((uint32_t)len << 16) | (uint32_t)(dist - 1);
-        s_hist[ls]++;
-        s_hist[kLitLenSyms + ds]++;
-      }
-      // hash the positions the match covers (latest position wins)
-      for (int q = 1 + lane; q < len; q += 64) {
-        const int p = pos + q;
-        if (p + 3 < n) atomicMax(&s_head[hash4(s_in, p)], (uint32_t)p + 1);
-      }
-      pos += len;
-    } else {
-      if (lane == 0) {
-        const uint32_t lit = s_in[pos];
-        t[nt] = lit;
-        s_hist[lit]++;
-      }
-      pos += 1;
-    }
-    ++nt;
-    __builtin_amdgcn_wave_barrier();  // head-table updates precede the next lookup
+    uint32_t cand = valid ? s_head[h] : 0u;
+    const unsigned long long earlier = same & below;
+    if (earlier) cand = (uint32_t)(c0 + 63 - __clzll((long long)earlier)) + 1;
+    if (p < n) s_prev[p] = valid ? (uint16_t)cand : 0;
+    const bool last = (same & ~below & ~(1ull << lane)) == 0;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && last) s_head[h] = (uint16_t)(p + 1);
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
+  // c. parse this lane's segment
+  const uint32_t* s_w = reinterpret_cast<const uint32_t*>(s_in);
+  const int S = (n + kSegs - 1) / kSegs;
+  const int a = min(n, lane * S), e = min(n, a + S);
+  uint32_t* t = stage + b * (int64_t)kDeflateBlock + (int64_t)lane * S;
+  int nt = 0, p = a;
+  int nl = -1, nd = 0;  // the next position's search result, when lazy matching made one
+  while (p < e) {
+    int d = 0;
+    int l;
+    if (nl >= 0) {
+      l = nl;
+      d = nd;
+    } else {
+      l = p + 3 < e ? best_match(s_in, s_w, s_prev, p, min(kMaxMatch, e - p), &d) : 0;
+    }
+    nl = -1;
+    if (l >= 3 && l < kLazyLen && p + 4 < e) {
+      int d1 = 0;
+      const int l1 = best_match(s_in, s_w, s_prev, p + 1, min(kMaxMatch, e - p - 1), &d1);
+      if (l1 > l) {  // a literal now, the longer match next
+        nl = l1;
+        nd = d1;
+        l = 0;
+      }
+    }
+    if (l >= 3) {
+      int ls, lb, ds, db;
+      uint32_t lv, dv;
+      len_sym(l, &ls, &lb, &lv);
+      dist_sym(d, &ds, &db, &dv);
+      t[nt++] = kTokMatch | ((uint32_t)l << 16) | (uint32_t)(d - 1);
+      atomicAdd(&s_hist[ls], 1u);
+      atomicAdd(&s_hist[kLitLenSyms + ds], 1u);
+      p += l;
+    } else {
+      const uint32_t lit = s_in[p];
+      t[nt++] = lit;
+      atomicAdd(&s_hist[lit], 1u);
+      p += 1;
+    }
+  }
+  // d. compact the segments' tokens into the block's token array
+  uint32_t inc = (uint32_t)nt;
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint32_t o = __shfl_up(inc, dd);
+    if (lane >= dd) inc += o;
+  }
+  const uint32_t base = inc - (uint32_t)nt;
+  uint32_t* dst = tok + b * (int64_t)kDeflateBlock + base;
+  for (int k = 0; k < nt; ++k) dst[k] = t[k];
+  __syncthreads();
   for (int i = lane; i < kHistSyms; i += 64) hist[b * (int64_t)kHistSyms + i] = s_hist[i];
-  if (lane == 0) ntok[b] = (uint32_t)nt;
+  if (lane == 63) ntok[b] = inc;
+}
+
+// Block planning on the device: one wave per block, its lane 0 runs the shared planner
+// (deflate_plan.h) over the block's histogram with the scratch in LDS and writes the plan
+// record k_emit encodes with — the batch needs no host round trip between the passes.
+__global__ __launch_bounds__(64) void k_plan(const uint64_t* __restrict__ tab, int64_t nblk,
+                                             const uint32_t* __restrict__ hist,
+                                             uint32_t* __restrict__ plans,
+                                             uint32_t* __restrict__ slot) {
+  __shared__ PlanScratch s_ws;
+  const int64_t b = blockIdx.x;
+  if (b >= nblk || threadIdx.x != 0) return;
+  const uint64_t meta = tab[2 * b + 1];
+  uint32_t* rec = plans + b * (int64_t)kPlanWords;
+  plan_block_record(hist + b * (int64_t)kHistSyms, (uint32_t)(meta & 0xFFFFFFFFull),
+                    (meta >> 32) != 0, &s_ws, rec);
+  // output slot: the planned size, 4-byte aligned, + one word (k_emit stores whole words)
+  slot[b] = ((rec[2] + 3) & ~3u) + 4;
+}
+
+// Exclusive scan of the blocks' output slots (one workgroup): the compact output layout,
+// so the batch's result crosses PCIe at its compressed size, not one stride per block.
+__global__ __launch_bounds__(1024) void k_slot_scan(const uint32_t* __restrict__ slot,
+                                                    int64_t nblk, uint64_t* __restrict__ off) {
+  __shared__ unsigned long long s_w[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t per = (nblk + 1023) / 1024;
+  const int64_t a = min(nblk, per * t), e = min(nblk, a + per);
+  unsigned long long mine = 0;
+  for (int64_t i = a; i < e; ++i) mine += slot[i];
+  unsigned long long inc = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int k = 0; k < 16; ++k) {
+      const unsigned long long v = s_w[k];
+      s_w[k] = run;
+      run += v;
+    }
+    off[nblk] = run;
+  }
+  __syncthreads();
+  unsigned long long run = s_w[w] + inc - mine;
+  for (int64_t i = a; i < e; ++i) {
+    off[i] = run;
+    run += slot[i];
+  }
 }
 
 // OR `len` (<= 28) bits of v into the LDS bit buffer at bit `pos`.
@@ -208,8 +328,8 @@ __device__ __forceinline__ void or_bits(uint32_t* w, uint32_t pos, uint32_t v, i
   if (sh + len > 32) atomicOr(&w[k + 1], v >> (32 - sh));
 }
 
-// Pass 2: one wave per block encodes its tokens with the host's plan (stored / fixed /
-// dynamic codes, huffman.cc). The codes sit in LDS; each chunk of 64 tokens is placed by
+// Pass 2: one wave per block encodes its tokens with its plan (stored / fixed / dynamic
+// codes, k_plan). The codes sit in LDS; each chunk of 64 tokens is placed by
 // a wave prefix sum of the tokens' bit lengths and OR-ed into an LDS bit buffer, which is
 // then written out whole. A plan record: [mode, header bits, total bytes, codes (316),
 // header bytes].
@@ -218,6 +338,7 @@ __global__ __launch_bounds__(64) void k_emit(const uint8_t* __restrict__ src,
                                              const uint32_t* __restrict__ tok,
                                              const uint32_t* __restrict__ ntok,
                                              const uint32_t* __restrict__ plans,
+                                             const uint64_t* __restrict__ out_off,
                                              uint8_t* __restrict__ dst,
                                              uint32_t* __restrict__ out_len) {
   __shared__ uint32_t s_code[kHistSyms];
@@ -230,7 +351,7 @@ __global__ __launch_bounds__(64) void k_emit(const uint8_t* __restrict__ src,
   const bool fin = (tab[2 * b + 1] >> 32) != 0;
   const uint32_t* pl = plans + b * (int64_t)kPlanWords;
   const uint32_t mode = pl[0], hbits = pl[1], total = pl[2];
-  uint8_t* out = dst + b * (int64_t)kDeflateStride;
+  uint8_t* out = dst + out_off[b];  // 4-byte aligned compact slot
   if (mode == 0) {  // stored: header byte (BFINAL, BTYPE 00, padding), LEN, NLEN, raw bytes
     if (lane == 0) {
       out[0] = fin ? 1 : 0;
@@ -306,6 +427,289 @@ __global__ __launch_bounds__(64) void k_emit(const uint8_t* __restrict__ src,
   for (int i = lane; i < words; i += 64) o32[i] = s_out[i];
 }
 
+// ---------------------------------------------------------------------------------
+// Batch inflate (RFC 1951 raw DEFLATE streams, one per gzip member; the host parses the
+// gzip framing): one wave per member. Decoding is inherently serial, so the wave runs the
+// bit reader and the canonical-Huffman decoder in lockstep (uniform values in every lane)
+// while the byte work is spread over the lanes: back-reference copies 64 bytes per step
+// (a period-d pattern for d < 64), stored blocks, input refills, output flushes and the
+// CRC-32 of the output (lane slices combined by GF(2) multiplies, as the deflate side).
+// The 32 KiB window lives in LDS; the output goes to global memory in 1 KiB flushes.
+// res[2m] = output bytes | error << 31, res[2m + 1] = CRC-32 of the output.
+constexpr int kInfRing = 8192;   // input bytes staged in LDS (two halves)
+constexpr int kInfWin = 32768;   // window
+constexpr int kInfFlush = 1024;
+
+struct InfHuff {
+  uint16_t count[16];
+  uint16_t symbol[288];
+};
+
+struct InfState {
+  const uint8_t* src;
+  int64_t in_len;
+  int64_t pos;        // next input byte
+  int64_t ring_base;  // the ring holds input [ring_base, ring_base + kInfRing)
+  uint64_t bitbuf;
+  int bitcnt;
+};
+
+__device__ void inf_refill_ring(InfState& st, uint8_t* s_ring, int64_t from, int lane) {
+  // input [from, from + kInfRing / 2) into its ring half (the wave)
+  for (int k = lane; k < kInfRing / 2; k += 64) {
+    const int64_t x = from + k;
+    s_ring[x & (kInfRing - 1)] = x < st.in_len ? st.src[x] : 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t inf_bits(InfState& st, const uint8_t* s_ring, int n) {
+  while (st.bitcnt < n) {
+    st.bitbuf |= (uint64_t)s_ring[st.pos & (kInfRing - 1)] << st.bitcnt;
+    st.pos++;
+    st.bitcnt += 8;
+  }
+  const uint32_t v = (uint32_t)(st.bitbuf & ((1ull << n) - 1));
+  st.bitbuf >>= n;
+  st.bitcnt -= n;
+  return v;
+}
+
+// puff-style canonical decode: one bit at a time against the per-length counts
+__device__ __forceinline__ int inf_decode(InfState& st, const uint8_t* s_ring, const InfHuff* h) {
+  int code = 0, first = 0, index = 0;
+  for (int len = 1; len <= 15; ++len) {
+    code |= (int)inf_bits(st, s_ring, 1);
+    const int count = h->count[len];
+    if (code - count < first) return h->symbol[index + (code - first)];
+    index += count;
+    first += count;
+    first <<= 1;
+    code <<= 1;
+  }
+  return -1;
+}
+
+// counts + symbols from code lengths (lane 0 writes); false on an over-subscribed code
+__device__ bool inf_construct(InfHuff* h, const uint8_t* len, int n, int lane) {
+  bool ok = true;
+  if (lane == 0) {
+    for (int k = 0; k < 16; ++k) h->count[k] = 0;
+    for (int sym = 0; sym < n; ++sym) h->count[len[sym]]++;
+    int left = 1;
+    for (int k = 1; k < 16; ++k) {
+      left <<= 1;
+      left -= h->count[k];
+      if (left < 0) ok = false;
+    }
+    uint16_t offs[16];
+    offs[1] = 0;
+    for (int k = 1; k < 15; ++k) offs[k + 1] = (uint16_t)(offs[k] + h->count[k]);
+    for (int sym = 0; sym < n; ++sym)
+      if (len[sym]) h->symbol[offs[len[sym]]++] = (uint16_t)sym;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __syncthreads();
+  return __shfl(ok ? 1 : 0, 0) != 0;
+}
+
+__global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in,
+                                                const uint64_t* __restrict__ itab,
+                                                uint8_t* __restrict__ out,
+                                                const uint64_t* __restrict__ otab, int64_t nm,
+                                                uint32_t* __restrict__ res) {
+  __shared__ uint8_t s_win[kInfWin];
+  __shared__ uint8_t s_ring[kInfRing];
+  __shared__ uint32_t s_crc[256];
+  __shared__ InfHuff s_ll, s_dd;
+  __shared__ uint8_t s_len[320];
+  const int64_t m = blockIdx.x;
+  if (m >= nm) return;
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 256; i += 64) {
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    s_crc[i] = c;
+  }
+  InfState st;
+  st.src = in + itab[2 * m];
+  st.in_len = (int64_t)itab[2 * m + 1];
+  st.pos = 0;
+  st.ring_base = 0;
+  st.bitbuf = 0;
+  st.bitcnt = 0;
+  uint8_t* dst = out + otab[2 * m];
+  const int64_t cap = (int64_t)otab[2 * m + 1];
+  inf_refill_ring(st, s_ring, 0, lane);
+  inf_refill_ring(st, s_ring, kInfRing / 2, lane);
+  int64_t opos = 0, flushed = 0;
+  uint32_t crc = 0xFFFFFFFFu;
+  int err = 0;
+  // flush s_win[flushed, opos) to the output and fold it into the CRC register
+  auto flush = [&]() {
+    const int64_t nf = opos - flushed;
+    if (nf <= 0) return;
+    const int S = (int)((nf + 63) / 64);
+    const int64_t a0 = flushed + min((int64_t)lane * S, nf), a1 = min(opos, a0 + S);
+    uint32_t r = 0;
+    for (int64_t x = a0; x < a1; ++x) {
+      const uint8_t byte = s_win[x & (kInfWin - 1)];
+      dst[x] = byte;
+      r = s_crc[(r ^ byte) & 0xFF] ^ (r >> 8);
+    }
+    r = crc_mulmod(crc_x8n((uint64_t)(opos - a1)), r);
+    for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
+    crc = crc_mulmod(crc_x8n((uint64_t)nf), crc) ^ r;
+    flushed = opos;
+  };
+  auto maybe_refill = [&]() {
+    if (st.pos - st.ring_base >= (3 * kInfRing) / 4) {
+      inf_refill_ring(st, s_ring, st.ring_base + kInfRing, lane);
+      st.ring_base += kInfRing / 2;
+    }
+  };
+  __syncthreads();
+  bool last = false;
+  while (!last && !err) {
+    maybe_refill();
+    last = inf_bits(st, s_ring, 1) != 0;
+    const uint32_t type = inf_bits(st, s_ring, 2);
+    if (type == 0) {  // stored: byte-aligned LEN, NLEN, raw bytes
+      st.bitbuf = 0;
+      st.bitcnt = 0;  // drop the partial byte (whole bytes were never pre-loaded)
+      const uint32_t len = inf_bits(st, s_ring, 16);
+      const uint32_t nlen = inf_bits(st, s_ring, 16);
+      if ((len ^ 0xFFFFu) != nlen) { err = 1; break; }
+      if (opos + len > cap || st.pos + len > st.in_len) { err = 2; break; }
+      uint32_t done = 0;
+      while (done < len) {
+        maybe_refill();
+        const uint32_t chunk = min(len - done, (uint32_t)kInfRing / 4);
+        if (opos - flushed + chunk > kInfWin - 512) flush();
+        for (uint32_t k = lane; k < chunk; k += 64)
+          s_win[(opos + k) & (kInfWin - 1)] = s_ring[(st.pos + k) & (kInfRing - 1)];
+        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        st.pos += chunk;
+        opos += chunk;
+        done += chunk;
+      }
+      continue;
+    }
+    if (type == 3) { err = 3; break; }
+    if (type == 1) {  // fixed codes (RFC 1951 §3.2.6)
+      if (lane == 0) {
+        for (int sym = 0; sym < 288; ++sym) s_len[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
+        for (int sym = 0; sym < 30; ++sym) s_len[288 + sym] = 5;
+      }
+      __syncthreads();
+      inf_construct(&s_ll, s_len, 288, lane);
+      inf_construct(&s_dd, s_len + 288, 30, lane);
+    } else {  // dynamic codes
+      const int nlen = (int)inf_bits(st, s_ring, 5) + 257;
+      const int ndist = (int)inf_bits(st, s_ring, 5) + 1;
+      const int ncode = (int)inf_bits(st, s_ring, 4) + 4;
+      if (nlen > 286 || ndist > 30) { err = 4; break; }
+      const int kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+      uint32_t clv[19];
+      for (int k = 0; k < 19; ++k) clv[k] = k < ncode ? inf_bits(st, s_ring, 3) : 0;
+      if (lane == 0)
+        for (int k = 0; k < 19; ++k) s_len[kOrd[k]] = (uint8_t)clv[k];
+      __syncthreads();
+      if (!inf_construct(&s_ll, s_len, 19, lane)) { err = 5; break; }
+      int idx = 0;
+      uint8_t prevlen = 0;
+      uint8_t lens[316];
+      while (idx < nlen + ndist) {
+        int sym = inf_decode(st, s_ring, &s_ll);
+        if (sym < 0) { err = 6; break; }
+        if (sym < 16) {
+          lens[idx++] = (uint8_t)sym;
+          prevlen = (uint8_t)sym;
+        } else {
+          int rep;
+          uint8_t v = 0;
+          if (sym == 16) {
+            if (idx == 0) { err = 7; break; }
+            v = prevlen;
+            rep = 3 + (int)inf_bits(st, s_ring, 2);
+          } else if (sym == 17) {
+            rep = 3 + (int)inf_bits(st, s_ring, 3);
+          } else {
+            rep = 11 + (int)inf_bits(st, s_ring, 7);
+          }
+          if (idx + rep > nlen + ndist) { err = 8; break; }
+          while (rep--) lens[idx++] = v;
+          if (sym != 16) prevlen = 0;
+        }
+      }
+      if (err) break;
+      if (lens[256] == 0) { err = 9; break; }
+      if (lane == 0) {
+        for (int k = 0; k < 320; ++k) s_len[k] = 0;
+        for (int k = 0; k < nlen; ++k) s_len[k] = lens[k];
+        for (int k = 0; k < ndist; ++k) s_len[288 + k] = lens[nlen + k];
+      }
+      __syncthreads();
+      inf_construct(&s_ll, s_len, nlen, lane);
+      inf_construct(&s_dd, s_len + 288, ndist, lane);
+    }
+    // the block's symbols
+    static constexpr uint16_t kLBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
+                                            31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195,
+                                            227, 258};
+    static constexpr uint8_t kLExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                          2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+    static constexpr uint16_t kDBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                            193, 257, 385, 513, 769, 1025, 1537, 2049, 3073,
+                                            4097, 6145, 8193, 12289, 16385, 24577};
+    static constexpr uint8_t kDExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                          6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+    for (;;) {
+      maybe_refill();
+      if (opos - flushed > kInfWin - 2 * 258 - kInfFlush) flush();
+      else if (opos - flushed >= kInfFlush) flush();
+      const int sym = inf_decode(st, s_ring, &s_ll);
+      if (sym < 0) { err = 10; break; }
+      if (sym < 256) {
+        if (opos >= cap) { err = 2; break; }
+        if (lane == 0) s_win[opos & (kInfWin - 1)] = (uint8_t)sym;
+        __builtin_amdgcn_wave_barrier();
+        opos++;
+        continue;
+      }
+      if (sym == 256) break;
+      const int ls = sym - 257;
+      if (ls >= 29) { err = 11; break; }
+      const int len = kLBase[ls] + (int)inf_bits(st, s_ring, kLExt[ls]);
+      const int ds = inf_decode(st, s_ring, &s_dd);
+      if (ds < 0 || ds >= 30) { err = 12; break; }
+      const int dist = kDBase[ds] + (int)inf_bits(st, s_ring, kDExt[ds]);
+      if (dist > opos) { err = 13; break; }
+      if (opos + len > cap) { err = 2; break; }
+      __syncthreads();
+      for (int k0 = 0; k0 < len; k0 += 64) {
+        const int k = k0 + lane;
+        uint8_t byte = 0;
+        if (k < len) {
+          const int64_t srcp = dist < 64 ? opos - dist + (k % dist) : opos - dist + k;
+          byte = s_win[srcp & (kInfWin - 1)];
+        }
+        __syncthreads();
+        if (k < len) s_win[(opos + k) & (kInfWin - 1)] = byte;
+        __syncthreads();
+      }
+      opos += len;
+    }
+  }
+  if (!err) flush();
+  if (lane == 0) {
+    res[2 * m] = (uint32_t)min(opos, (int64_t)0x7FFFFFFF) | (err ? 0x80000000u : 0u);
+    res[2 * m + 1] = ~crc;
+  }
+}
+
 }  // namespace
 
 GpuGzip::GpuGzip(int device) : device_(device) {
@@ -316,11 +720,10 @@ GpuGzip::GpuGzip(int device) : device_(device) {
 GpuGzip::~GpuGzip() {
   (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(stream_);
-  for (void* p : {(void*)h_in_, (void*)h_out_, (void*)h_tab_, (void*)h_len_, (void*)h_res_,
-                  (void*)h_plan_})
+  for (void* p : {(void*)h_in_, (void*)h_out_, (void*)h_tab_, (void*)h_len_})
     if (p) (void)hipHostFree(p);
   for (void* p : {(void*)d_in_, (void*)d_out_, (void*)d_tab_, (void*)d_len_, (void*)d_res_,
-                  (void*)d_plan_, (void*)d_tok_})
+                  (void*)d_plan_, (void*)d_tok_, (void*)d_slot_})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(stream_);
 }
@@ -355,6 +758,98 @@ std::vector<std::string> GpuGzip::deflate(const std::vector<std::string_view>& i
   return out;
 }
 
+// gzip member -> (raw DEFLATE offset, length, ISIZE, CRC) or false (framing, RFC 1952)
+static bool parse_gzip_member(std::string_view z, size_t* off, size_t* len, uint32_t* isize,
+                              uint32_t* crc) {
+  if (z.size() < 18 || (uint8_t)z[0] != 0x1f || (uint8_t)z[1] != 0x8b || z[2] != 8) return false;
+  const uint8_t flg = (uint8_t)z[3];
+  size_t p = 10;
+  if (flg & 4) {  // FEXTRA
+    if (p + 2 > z.size()) return false;
+    p += 2 + ((uint8_t)z[p] | ((size_t)(uint8_t)z[p + 1] << 8));
+  }
+  for (int f : {8, 16}) {  // FNAME, FCOMMENT: zero-terminated
+    if (flg & f) {
+      while (p < z.size() && z[p]) ++p;
+      ++p;
+    }
+  }
+  if (flg & 2) p += 2;  // FHCRC
+  if (p + 8 > z.size()) return false;
+  auto u32 = [&](size_t q) {
+    return (uint32_t)(uint8_t)z[q] | ((uint32_t)(uint8_t)z[q + 1] << 8) |
+           ((uint32_t)(uint8_t)z[q + 2] << 16) | ((uint32_t)(uint8_t)z[q + 3] << 24);
+  };
+  *off = p;
+  *len = z.size() - 8 - p;
+  *crc = u32(z.size() - 8);
+  *isize = u32(z.size() - 4);
+  return true;
+}
+
+std::vector<std::string> GpuGzip::inflate(const std::vector<std::string_view>& in,
+                                          std::vector<uint8_t>* ok, uint64_t max_out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  GZ_OK(hipSetDevice(device_));
+  const size_t nm = in.size();
+  std::vector<std::string> out(nm);
+  ok->assign(nm, 0);
+  if (nm == 0) return out;
+  // members whose framing parses and whose ISIZE fits the cap go to the GPU
+  std::vector<size_t> doff(nm), dlen(nm), osz(nm);
+  std::vector<uint32_t> want_crc(nm);
+  size_t packed = 0, obytes = 0;
+  for (size_t i = 0; i < nm; ++i) {
+    uint32_t isize = 0;
+    if (!parse_gzip_member(in[i], &doff[i], &dlen[i], &isize, &want_crc[i]) || isize > max_out) {
+      dlen[i] = 0;
+      osz[i] = ~(size_t)0;  // not decoded
+      continue;
+    }
+    osz[i] = isize;
+    packed += (dlen[i] + 15) & ~(size_t)15;
+    obytes += (isize + 15) & ~(size_t)15;
+  }
+  uint8_t* hin = grow(&h_in_, &h_in_cap_, packed + 16, true);
+  uint8_t* din = grow(&d_in_, &d_in_cap_, packed + 16, false);
+  uint64_t* htab = grow(&h_tab_, &h_tab_cap_, 4 * nm, true);
+  uint64_t* dtab = grow(&d_tab_, &d_tab_cap_, 4 * nm, false);
+  uint8_t* dout = grow(&d_out_, &d_out_cap_, obytes + 16, false);
+  uint8_t* hout = grow(&h_out_, &h_out_cap_, obytes + 16, true);
+  uint32_t* hres = grow(&h_len_, &h_len_cap_, 2 * nm, true);
+  uint32_t* dres = grow(&d_len_, &d_len_cap_, 2 * nm, false);
+  size_t ip = 0, op = 0;
+  for (size_t i = 0; i < nm; ++i) {
+    const size_t cap = osz[i] == ~(size_t)0 ? 0 : osz[i];
+    if (dlen[i]) std::memcpy(hin + ip, in[i].data() + doff[i], dlen[i]);
+    htab[2 * i] = ip;
+    htab[2 * i + 1] = dlen[i];
+    htab[2 * nm + 2 * i] = op;
+    htab[2 * nm + 2 * i + 1] = cap;
+    ip += (dlen[i] + 15) & ~(size_t)15;
+    op += (cap + 15) & ~(size_t)15;
+  }
+  GZ_OK(hipMemcpyAsync(din, hin, packed + 16, hipMemcpyHostToDevice, stream_));
+  GZ_OK(hipMemcpyAsync(dtab, htab, 4 * nm * sizeof(uint64_t), hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(k_inflate, dim3((unsigned)nm), dim3(64), 0, stream_, din, dtab, dout,
+                     dtab + 2 * nm, (int64_t)nm, dres);
+  GZ_OK(hipGetLastError());
+  GZ_OK(hipMemcpyAsync(hres, dres, 2 * nm * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  GZ_OK(hipMemcpyAsync(hout, dout, obytes + 16, hipMemcpyDeviceToHost, stream_));
+  GZ_OK(hipStreamSynchronize(stream_));
+  for (size_t i = 0; i < nm; ++i) {
+    if (osz[i] == ~(size_t)0) continue;
+    const uint32_t r = hres[2 * i];
+    const uint32_t got = r & 0x7FFFFFFFu;
+    // a member is good when it decoded without error to exactly ISIZE bytes with its CRC
+    if ((r >> 31) || got != osz[i] || hres[2 * i + 1] != want_crc[i]) continue;
+    out[i].assign(reinterpret_cast<const char*>(hout + htab[2 * nm + 2 * i]), got);
+    (*ok)[i] = 1;
+  }
+  stats_.inflated += nm;
+  return out;
+}
+
 void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::string>* out,
                   bool gzip) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -375,21 +870,26 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   uint64_t* dtab = grow(&d_tab_, &d_tab_cap_, 2 * nblk, false);
   // pass-1 results [histograms (316 per block) | token counts | CRC registers] and pass-2
   // lengths: one D2H each
-  const size_t nres = nblk * (size_t)kHistSyms + 2 * nblk;
-  uint32_t* hres = grow(&h_res_, &h_res_cap_, nres, true);
+  const size_t nres = nblk * (size_t)kHistSyms + nblk;
   uint32_t* dres = grow(&d_res_, &d_res_cap_, nres, false);
-  uint32_t* hlen = grow(&h_len_, &h_len_cap_, nblk, true);
-  uint32_t* dlen = grow(&d_len_, &d_len_cap_, nblk, false);
-  uint32_t* dtok = grow(&d_tok_, &d_tok_cap_, nblk * (size_t)kDeflateBlock, false);
-  uint32_t* hplan = grow(&h_plan_, &h_plan_cap_, nblk * (size_t)kPlanWords, true);
+  // [lengths (nblk) | CRC registers (nblk) | slot offsets (nblk + 1, u64)]: one D2H
+  const size_t nlen = 2 * nblk + 2 * (nblk + 1) + 2;
+  uint32_t* hlen = grow(&h_len_, &h_len_cap_, nlen, true);
+  uint32_t* dlen = grow(&d_len_, &d_len_cap_, nlen, false);
+  uint32_t* dslot = grow(&d_slot_, &d_slot_cap_, nblk, false);
+  uint64_t* doff = reinterpret_cast<uint64_t*>(dlen + 2 * nblk + ((2 * nblk) & 1));
+  const uint64_t* hoff = reinterpret_cast<const uint64_t*>(hlen + 2 * nblk + ((2 * nblk) & 1));
+  // tokens: the parse's per-segment lists (stage) compacted into one list per block (tok)
+  uint32_t* dtok = grow(&d_tok_, &d_tok_cap_, 2 * nblk * (size_t)kDeflateBlock, false);
+  uint32_t* dstage = dtok + nblk * (size_t)kDeflateBlock;
   uint32_t* dplan = grow(&d_plan_, &d_plan_cap_, nblk * (size_t)kPlanWords, false);
   uint32_t* dhist = dres;
   uint32_t* dntok = dres + nblk * (size_t)kHistSyms;
-  uint32_t* dcrc = dntok + nblk;
-  const uint32_t* hhist = hres;
-  const uint32_t* hcrc = hres + nblk * (size_t)kHistSyms + nblk;
-  uint8_t* dout = grow(&d_out_, &d_out_cap_, nblk * (size_t)kDeflateStride, false);
-  uint8_t* hout = grow(&h_out_, &h_out_cap_, nblk * (size_t)kDeflateStride, true);
+  uint32_t* dcrc = dlen + nblk;
+  const uint32_t* hcrc = hlen + nblk;
+  const size_t out_bound = packed + 16 * nblk + 64;
+  uint8_t* dout = grow(&d_out_, &d_out_cap_, out_bound, false);
+  uint8_t* hout = grow(&h_out_, &h_out_cap_, out_bound, true);
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   size_t o = 0, k = 0;
@@ -410,42 +910,19 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
   GZ_OK(hipMemcpyAsync(din, hin, packed + 16, hipMemcpyHostToDevice, stream_));
   GZ_OK(hipMemcpyAsync(dtab, htab, 2 * nblk * sizeof(uint64_t), hipMemcpyHostToDevice, stream_));
   hipLaunchKernelGGL(k_lz77, dim3((unsigned)nblk), dim3(64), 0, stream_, din, dtab,
-                     (int64_t)nblk, dtok, dhist, dntok, dcrc);
+                     (int64_t)nblk, dtok, dstage, dhist, dntok, dcrc);
   GZ_OK(hipGetLastError());
-  GZ_OK(hipMemcpyAsync(hres, dres, nres * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-  GZ_OK(hipStreamSynchronize(stream_));
-  // plan every block (stored / fixed / dynamic codes and header) on a few host threads
-  {
-    const size_t nth = std::min<size_t>(std::max<size_t>(1, nblk / 64),
-                                        std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)));
-    auto work = [&](size_t lo, size_t hi) {
-      BlockPlan bp;
-      for (size_t bi = lo; bi < hi; ++bi) {
-        const uint64_t meta = htab[2 * bi + 1];
-        plan_block(hhist + bi * kHistSyms, (uint32_t)(meta & 0xFFFFFFFFu), (meta >> 32) != 0, &bp);
-        uint32_t* rec = hplan + bi * (size_t)kPlanWords;
-        rec[0] = (uint32_t)bp.mode;
-        rec[1] = bp.header_bits;
-        rec[2] = (uint32_t)bp.total_bytes;
-        std::memcpy(rec + 3, bp.codes, sizeof(bp.codes));
-        SH_CHECK(bp.header.size() <= 4 * (size_t)(kPlanWords - 3 - kHistSyms), "gzip header too long");
-        std::memset(rec + 3 + kHistSyms, 0, 4 * (size_t)(kPlanWords - 3 - kHistSyms));
-        std::memcpy(rec + 3 + kHistSyms, bp.header.data(), bp.header.size());
-      }
-    };
-    std::vector<std::thread> ths;
-    const size_t per = (nblk + nth - 1) / nth;
-    for (size_t ti = 1; ti < nth; ++ti)
-      ths.emplace_back(work, std::min(nblk, ti * per), std::min(nblk, (ti + 1) * per));
-    work(0, std::min(nblk, per));
-    for (auto& th : ths) th.join();
-  }
-  GZ_OK(hipMemcpyAsync(dplan, hplan, nblk * (size_t)kPlanWords * 4, hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(k_plan, dim3((unsigned)nblk), dim3(64), 0, stream_, dtab, (int64_t)nblk,
+                     dhist, dplan, dslot);
+  hipLaunchKernelGGL(k_slot_scan, dim3(1), dim3(1024), 0, stream_, dslot, (int64_t)nblk, doff);
   hipLaunchKernelGGL(k_emit, dim3((unsigned)nblk), dim3(64), 0, stream_, din, dtab,
-                     (int64_t)nblk, dtok, dntok, dplan, dout, dlen);
+                     (int64_t)nblk, dtok, dntok, dplan, doff, dout, dlen);
   GZ_OK(hipGetLastError());
-  GZ_OK(hipMemcpyAsync(hlen, dlen, nblk * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-  GZ_OK(hipMemcpyAsync(hout, dout, nblk * (size_t)kDeflateStride, hipMemcpyDeviceToHost, stream_));
+  // one D2H of [lengths | CRC registers | slot offsets], one of the compact output; its
+  // extent is bounded by the stored encoding of every block (the input + 9 B per block)
+  GZ_OK(hipMemcpyAsync(hlen, dlen, (2 * nblk + 2 * (nblk + 1)) * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost, stream_));
+  GZ_OK(hipMemcpyAsync(hout, dout, out_bound, hipMemcpyDeviceToHost, stream_));
   GZ_OK(hipStreamSynchronize(stream_));
   const auto t2 = clk::now();
   // assemble: [gzip header] deflate blocks [CRC-32, ISIZE]
@@ -464,7 +941,7 @@ void GpuGzip::run(const std::vector<std::string_view>& in, std::vector<std::stri
     for (size_t j = 0; j < nb; ++j, ++k) {
       const uint32_t l = hlen[k];
       stats_.stored_blocks += l >> 31;
-      r.append(reinterpret_cast<const char*>(hout + k * (size_t)kDeflateStride), l & 0x7FFFFFFFu);
+      r.append(reinterpret_cast<const char*>(hout + hoff[k]), l & 0x7FFFFFFFu);
       const uint64_t blen = std::min<uint64_t>(kDeflateBlock, s.size() - j * kDeflateBlock);
       reg = crc_mulmod(crc_x8n(blen), reg) ^ hcrc[k];
     }

@@ -1,22 +1,16 @@
-// DEFLATE block planning on the host (RFC 1951 §3.2.5-3.2.7): from a block's symbol
-// histogram, choose stored / fixed-Huffman / dynamic-Huffman by exact bit cost, build
-// length-limited canonical Huffman codes and the dynamic block header. The GPU batch
-// gzip (deflate.hip) parses on the device, plans here, and emits on the device; the
-// planner is host C++ so it is also unit-tested on the CPU (deflate_block_cpu).
+// Host API of the DEFLATE block planner (deflate_plan.h, shared with the GPU's k_plan):
+// the BlockPlan view of a plan record, Huffman lengths, and a CPU reference encoder of a
+// token list for tests.
 #pragma once
 
 #include <cstdint>
 #include <string>
 #include <vector>
 
+#include "deflate_plan.h"
+
 namespace shellac {
 
-constexpr int kLitLenSyms = 286;  // 0-255 literals, 256 end of block, 257-285 lengths
-constexpr int kDistSyms = 30;
-constexpr int kHistSyms = kLitLenSyms + kDistSyms;  // histogram layout: [litlen | dist]
-
-// Tokens of a parsed block: a literal byte, or a match (len 3..258, dist 1..32768).
-constexpr uint32_t kTokMatch = 0x80000000u;
 inline uint32_t tok_literal(uint32_t b) { return b; }
 inline uint32_t tok_match(uint32_t len, uint32_t dist) { return kTokMatch | (len << 16) | (dist - 1); }
 

@@ -103,3 +103,40 @@ def test_proxy_compresses_misses_on_the_gpu(cuda_dev):
             json.dumps(st)
     finally:
         o.stop()
+
+
+def test_gpu_inflate_matches_zlib(gz):
+    """Batched GPU gunzip (one wave per member) against zlib-made members of every block
+    type: stored (incompressible), fixed (tiny) and dynamic Huffman, multi-block, empty,
+    long runs (distance 1 back-references), plus the GPU's own members; a corrupt member
+    is rejected (None), never returned wrong."""
+    rng = random.Random(11)
+    bodies = [b"", b"a", b"hello world", b"x" * 100000, os.urandom(70000),
+              _html(rng, 4096), _html(rng, 200000), bytes(range(256)) * 500,
+              b"ab" * 40000 + os.urandom(300)]
+    members = [gzip.compress(b, lvl) for b in bodies for lvl in (1, 6, 9)]
+    members += gz.compress(bodies)
+    want = [b for b in bodies for _ in (1, 6, 9)] + bodies
+    got = gz.inflate(members)
+    assert [g for g in got] == want
+    bad = bytearray(members[15])
+    bad[len(bad) // 2] ^= 0x40
+    assert gz.inflate([bytes(bad)])[0] is None
+    big = gzip.compress(b"\0" * (1 << 20))
+    assert gz.inflate([big], 1000)[0] is None          # ISIZE over the cap: not decoded
+    from shellac_amd.ops.gzip import gunzip_batch
+
+    assert gunzip_batch([big, members[0]], max_out=2 << 20) == [b"\0" * (1 << 20), bodies[0]]
+
+
+def test_gpu_ratio_close_to_zlib6(gz):
+    """The lazy chained parse with per-block dynamic codes lands within 10 % of zlib -6's
+    size on HTML-like text (verdict target: the miss path at a zlib-like ratio)."""
+    rng = random.Random(3)
+    bodies = [_html(rng, 8192) for _ in range(64)] + [_html(rng, 65536) for _ in range(8)]
+    out = gz.compress(bodies)
+    for b, o in zip(bodies, out):
+        assert zlib.decompress(o, 31) == b
+    ratio = sum(map(len, out)) / sum(map(len, bodies))
+    z6 = sum(len(gzip.compress(b, 6)) for b in bodies) / sum(map(len, bodies))
+    assert ratio <= 1.10 * z6, (ratio, z6)
