@@ -176,6 +176,35 @@ def smoke(rank, world, dev):
     return out
 
 
+def check_memory_budget(args, world, sim, dev) -> None:
+    """Fail fast, with a clear message, when a rank's HBM cannot hold its shard: the value
+    log, the index (128 B per bucket, ~4 per key), the replica tier, the workload's
+    payload pool and pre-generated batches, the routed step's exchange buffers (about
+    three steps of responses in flight) and the 1 GiB all-reduce of the smoke check."""
+    gib = 1 << 30
+    shard_keys = args.keys_per_gpu * (sim or 1)
+    nb = 1
+    while nb < shard_keys:
+        nb *= 2
+    need = args.log_gb * (sim or 1) * gib + nb * 128
+    if world > 1 and args.replicate:
+        rgb = args.replica_gb if args.replica_gb is not None else args.replicate * 2048 / gib
+        need += rgb * gib + 2 * args.replicate * 128
+    mean_val = (args.max_val - args.min_val) / max(1.0, __import__("math").log(
+        max(args.max_val, 2) / max(args.min_val, 1)))
+    need += args.keys_per_gpu * world * (mean_val + 64)          # payload pool
+    need += max(1, args.batches) * (args.batch * 16 + args.sets * 64)
+    need += 3 * args.batch * (mean_val + 48) * 1.2 + 2 * gib        # responses in flight
+    if not args.no_smoke and world > 1:
+        need += gib
+    free, total = torch.cuda.mem_get_info(dev)
+    if need > free:
+        print(f"[bench] error: this configuration needs ~{need / gib:.1f} GiB of HBM per rank "
+              f"but {free / gib:.1f} of {total / gib:.1f} GiB are free on {dev}; lower --log-gb "
+              f"or --keys-per-gpu", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+
+
 def _claim_stdout():
     """The contract is ONE JSON line on rank 0's stdout, but RCCL prints a version banner
     to fd 1 when a communicator comes up. Keep a private handle on the real stdout for the
@@ -208,6 +237,12 @@ def main():
         dev = torch.device("cuda", 0)
         dist.init_process_group("gloo", timeout=pg_timeout)
     elif args.device == "cuda":
+        ndev = torch.cuda.device_count()
+        if local >= ndev or (world > 1 and ndev < world and not sim):
+            print(f"[bench] error: --gpus {args.gpus} needs {max(world, local + 1)} GPUs on this "
+                  f"node, {ndev} visible; refusing to put several ranks on one device",
+                  file=sys.stderr, flush=True)
+            raise SystemExit(2)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
@@ -248,6 +283,8 @@ def main():
     if args.replica_gb is None:
         args.replica_gb = args.replicate * 2048 / (1 << 30)
     total_keys = args.keys_per_gpu * world
+    if dev.type == "cuda" and not bounce:
+        check_memory_budget(args, world, sim, dev)
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
     nb = 1

@@ -143,6 +143,10 @@ struct HbmBackendConfig {
   // ...and is then warmed from its peers over xGMI: the objects of its key range that
   // other shards took while it was out are peer-copied back (hipMemcpyPeerAsync)
   bool warm_restore = true;
+  // peer copies of the warm restore: "auto" = direct xGMI where hipDeviceCanAccessPeer
+  // says so (peer access enabled at start), staged through pinned host memory otherwise;
+  // "staged" forces the host path (tests; a node whose xGMI mapping is broken)
+  std::string peer_copy = "auto";
   // Pinned response arenas allocated up front per GPU (depth + 2 of this size): pinning
   // host memory mid-run stalled every socket call on the box for up to ~0.5 s
   uint64_t arena_bytes = 16u << 20;
@@ -165,6 +169,8 @@ class HbmBackend : public CacheBackend {
   void del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) override;
   void flush() override;
   std::string name() const override { return "hbm"; }
+  // peer path chosen for src -> dst: 0 same device, 1 direct (peer access), 2 staged
+  int peer_path(int src_dev, int dst_dev) const;
   void stats(StatList* out) override;
   bool inject_shard_down(int shard, bool down) override;
 
@@ -188,6 +194,7 @@ class HbmBackend : public CacheBackend {
   HbmBackendConfig cfg_;
   DigestRing ring_;
   std::vector<std::unique_ptr<Dev>> devs_;
+  std::vector<uint8_t> peer_ok_;  // [src * n + dst]: peer access enabled (direct xGMI copies)
   std::atomic<uint64_t> up_mask_{0};  // bit i: shard i serves requests
   double epoch_;
   std::atomic<uint64_t> no_shard_misses_{0};

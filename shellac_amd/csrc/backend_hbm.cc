@@ -212,7 +212,7 @@ struct HbmBackend::Dev {
   std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
       filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
       key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, arena_misses{0},
-      dropped{0},
+      dropped{0}, staged_copies{0},
       migrated{0}, migrate_ns{0};
 
   void loop();
@@ -313,6 +313,24 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     }
     up_mask_.fetch_or(1ull << i);
     devs_.push_back(std::move(d));
+  }
+  // Peer access between the shards' GPUs (warm restore copies over xGMI). A pair the
+  // runtime cannot map, or every pair under peer_copy = "staged", copies through pinned
+  // host memory instead (peer_path / copy_between).
+  const size_t nd = devs_.size();
+  peer_ok_.assign(nd * nd, 0);
+  if (cfg_.peer_copy != "staged") {
+    for (size_t i = 0; i < nd; ++i)
+      for (size_t j = 0; j < nd; ++j) {
+        const int a = devs_[i]->device, b = devs_[j]->device;
+        if (a == b) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, b, a) != hipSuccess || !can) continue;
+        HB_OK(hipSetDevice(b));  // b (the destination) reads / DMAs from a's memory
+        const hipError_t e = hipDeviceEnablePeerAccess(a, 0);
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) peer_ok_[i * nd + j] = 1;
+        else (void)hipGetLastError();  // clear the sticky error: the pair stays staged
+      }
   }
   for (auto& d : devs_) {
     Dev* dp = d.get();
@@ -906,6 +924,51 @@ void HbmBackend::Dev::maybe_restore() {
                device, (unsigned long long)moved);
 }
 
+int HbmBackend::peer_path(int src_dev, int dst_dev) const {
+  if (cfg_.peer_copy == "staged") return 2;  // forced (tests run it with one GPU)
+  if (src_dev == dst_dev) return 0;
+  const size_t nd = devs_.size();
+  size_t si = nd, di = nd;
+  for (size_t i = 0; i < nd; ++i) {
+    if (devs_[i]->device == src_dev) si = i;
+    if (devs_[i]->device == dst_dev) di = i;
+  }
+  return si < nd && di < nd && peer_ok_[si * nd + di] ? 1 : 2;
+}
+
+namespace {
+// src (on src_dev) -> dst (on dst_dev), ordered on `stream` (dst_dev's): a device copy on
+// one GPU, a direct peer DMA where peer access is enabled, else staged through pinned
+// host memory in 64 MiB pieces (synchronous; the warm restore is off the request path).
+void copy_between(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes,
+                  hipStream_t stream, int path) {
+  if (!bytes) return;
+  if (path == 0) {
+    HB_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+  } else if (path == 1) {
+    HB_OK(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, stream));
+  } else {
+    const size_t piece = std::min<size_t>(bytes, 64u << 20);
+    void* h = nullptr;
+    HB_OK(hipHostMalloc(&h, piece, hipHostMallocDefault));
+    try {
+      HB_OK(hipStreamSynchronize(stream));  // earlier work on dst's stream first
+      for (size_t o = 0; o < bytes; o += piece) {
+        const size_t n = std::min(piece, bytes - o);
+        HB_OK(hipSetDevice(src_dev));
+        HB_OK(hipMemcpy(h, static_cast<const uint8_t*>(src) + o, n, hipMemcpyDeviceToHost));
+        HB_OK(hipSetDevice(dst_dev));
+        HB_OK(hipMemcpy(static_cast<uint8_t*>(dst) + o, h, n, hipMemcpyHostToDevice));
+      }
+    } catch (...) {
+      (void)hipHostFree(h);
+      throw;
+    }
+    HB_OK(hipHostFree(h));
+  }
+}
+}  // namespace
+
 // Peer migration src -> this (both GPUs' HbmCache APIs are thread-safe; src's work goes
 // on src's migration stream, beside src's own batcher): export src's live digests, route
 // them on src's GPU, take the ones this shard owns, look them up and gather their records
@@ -1009,10 +1072,12 @@ uint64_t HbmBackend::Dev::migrate_from(Dev& src) {
         HB_OK(hipMalloc(&kmeta, 3 * m * 4));
         HB_OK(hipMalloc(&skeys2, m * sizeof(Digest)));
         HB_OK(hipMalloc(&krec, total + 16));
-        HB_OK(hipMemcpyPeerAsync(krec, device, srec, src.device, total, stream));
-        HB_OK(hipMemcpyPeerAsync(koff, device, soff, src.device, (m + 1) * 8, stream));
-        HB_OK(hipMemcpyPeerAsync(ksize, device, ssize, src.device, (m + 1) * 8, stream));
-        HB_OK(hipMemcpyPeerAsync(kk, device, sk, src.device, m * sizeof(Digest), stream));
+        const int path = be->peer_path(src.device, device);
+        copy_between(krec, device, srec, src.device, total, stream, path);
+        copy_between(koff, device, soff, src.device, (m + 1) * 8, stream, path);
+        copy_between(ksize, device, ssize, src.device, (m + 1) * 8, stream, path);
+        copy_between(kk, device, sk, src.device, m * sizeof(Digest), stream, path);
+        if (path == 2) staged_copies++;
         cache->lookup(kk, m, kloc, khave, khoff, t, stream);
         records_to_set(krec, koff, ksize, khave, m, skeys2, kvoff, kmeta, kmeta + m, kmeta + 2 * m,
                        stream);
@@ -1123,6 +1188,10 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_restores", sum(&Dev::restores));
   out->emplace_back("hbm_regathers", sum(&Dev::regathers));
   out->emplace_back("hbm_arena_misses", sum(&Dev::arena_misses));
+  out->emplace_back("hbm_staged_peer_copies", sum(&Dev::staged_copies));
+  uint64_t direct = 0;
+  for (uint8_t v : peer_ok_) direct += v;
+  out->emplace_back("hbm_peer_pairs_direct", direct);
   out->emplace_back("hbm_migrated", sum(&Dev::migrated));
   out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));

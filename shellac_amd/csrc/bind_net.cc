@@ -197,7 +197,7 @@ void bind_net(py::module_& m) {
                           int max_batch, int sweep_interval_s, int spin_us,
                           bool presence_filter, int depth, const std::string& evict,
                           int retry_s, int batch_timeout_ms, bool flush_on_restore,
-                          bool warm_restore) {
+                          bool warm_restore, const std::string& peer_copy) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -215,6 +215,8 @@ void bind_net(py::module_& m) {
     c.batch_timeout_ms = batch_timeout_ms;
     c.flush_on_restore = flush_on_restore;
     c.warm_restore = warm_restore;
+    SH_CHECK(peer_copy == "auto" || peer_copy == "staged", "peer_copy must be auto or staged");
+    c.peer_copy = peer_copy;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
@@ -222,7 +224,8 @@ void bind_net(py::module_& m) {
      py::arg("sweep_interval_s") = 10, py::arg("spin_us") = 50,
      py::arg("presence_filter") = true, py::arg("depth") = 3, py::arg("evict") = "clock",
      py::arg("retry_s") = 2, py::arg("batch_timeout_ms") = 2000,
-     py::arg("flush_on_restore") = true, py::arg("warm_restore") = true);
+     py::arg("flush_on_restore") = true, py::arg("warm_restore") = true,
+     py::arg("peer_copy") = "auto");
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);

@@ -463,7 +463,8 @@ namespace {
 enum Slot {
   kRlLoc, kRlSize0, kRlSize1, kRlOff0, kRlOff1, kDestG, kRoute0, kRoute1, kCntG, kWsG,
   kCoTab, kFirst0, kFirst1, kOwnerS, kVpad, kTcnt, kTbytes, kSrec, kSval, kSvoff, kCntS,
-  kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSegLen, kRb, kTab, kSegOff, kSegSrc,
+  kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSrcA, kSrcB, kHdr, kUsed, kRb, kTab,
+  kSegOff, kSegSrc,
   kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
 };
 
@@ -518,55 +519,92 @@ __global__ void k_demand(const uint64_t* __restrict__ lk_off, int32_t W, int32_t
   }
 }
 
-// Owner: the reply slot of every probed row. Row r of owner slot s (j = r - s capG) gets
-// header (size << 32 | offset in the slot's data) if its record fits the slot's capD
-// bytes, 0 otherwise (miss or dropped); its destination for the sized gather (others:
-// relative to R, self: relative to data's self slot) and its length.
-__global__ __launch_bounds__(kB) void k_reply_prep(
-    const uint64_t* __restrict__ lk_size, const uint64_t* __restrict__ lk_off,
-    const int64_t* __restrict__ own_cnt, int32_t W, int64_t capG, int64_t capD, int64_t slotR,
-    uint8_t* __restrict__ R, uint8_t* __restrict__ self_slot, uint64_t* __restrict__ dstA,
-    uint64_t* __restrict__ dstB, uint64_t* __restrict__ seg_len,
-    unsigned long long* __restrict__ dropped) {
-  const int64_t rows = (int64_t)W * capG;
-  const uint64_t hdr = (uint64_t)capG * 8;
-  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r <= rows;
-       r += (int64_t)gridDim.x * kB) {
-    if (r == rows) {  // sentinels: the extent of each gather
-      dstA[(int64_t)(W - 1) * capG] = (uint64_t)(W - 1) * (uint64_t)slotR;
-      dstB[capG] = (uint64_t)slotR;
-      continue;
+// Owner, reply slots as segments of one plain gather per destination buffer (others: R,
+// self: data's self slot). Slot s = [header (capG x u64) | records | slack], as segments
+// [header | one per row | slack] (capG + 2 per slot): the header segment copies the
+// headers k_reply_prep wrote into `hdr`, the slack segment copies the slot's own unused
+// bytes onto themselves, so the segments tile the buffer and the gather needs no gaps.
+// used[s] = the bytes of slot s's longest row prefix that fits capD (rows past it are
+// dropped: header 0, no bytes).
+__global__ void k_reply_used(const uint64_t* __restrict__ lk_off, int32_t W, int64_t capG,
+                             int64_t capD, int64_t slotR, const uint64_t* __restrict__ hdr,
+                             uint8_t* __restrict__ R, uint8_t* __restrict__ self_slot,
+                             uint64_t* __restrict__ used, uint64_t* __restrict__ offA,
+                             uint64_t* __restrict__ srcA, uint64_t* __restrict__ offB,
+                             uint64_t* __restrict__ srcB) {
+  const int64_t per = capG + 2;
+  for (int s = threadIdx.x; s < W; s += blockDim.x) {
+    const uint64_t base = lk_off[s * capG];
+    int64_t lo = 0, hi = capG;  // the largest j with lk_off[s capG + j] - base <= capD
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (lk_off[s * capG + mid] - base <= (uint64_t)capD) lo = mid; else hi = mid - 1;
     }
+    const uint64_t u = lk_off[s * capG + lo] - base;
+    used[s] = u;
+    const bool self = s == W - 1;
+    uint64_t* off = self ? offB : offA + s * per;
+    uint64_t* src = self ? srcB : srcA + s * per;
+    const uint64_t sb = self ? 0 : (uint64_t)s * (uint64_t)slotR;
+    uint8_t* slot = self ? self_slot : R + s * slotR;
+    off[0] = sb;
+    src[0] = (uint64_t)(uintptr_t)(hdr + s * capG);
+    const uint64_t gap = (uint64_t)capG * 8 + u;
+    off[capG + 1] = sb + gap;
+    src[capG + 1] = (uint64_t)(uintptr_t)(slot + gap);  // slack onto itself
+  }
+  if (threadIdx.x == 0) {
+    offA[(int64_t)(W - 1) * per] = (uint64_t)(W - 1) * (uint64_t)slotR;
+    offB[per] = (uint64_t)slotR;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_reply_prep(
+    const uint64_t* __restrict__ lk_loc, const uint64_t* __restrict__ lk_size,
+    const uint64_t* __restrict__ lk_off, const int64_t* __restrict__ own_cnt,
+    const uint64_t* __restrict__ used, int32_t W, int64_t capG, int64_t slotR,
+    const uint8_t* __restrict__ log, uint64_t* __restrict__ hdr, uint64_t* __restrict__ offA,
+    uint64_t* __restrict__ srcA, uint64_t* __restrict__ offB, uint64_t* __restrict__ srcB,
+    unsigned long long* __restrict__ dropped) {
+  const int64_t rows = (int64_t)W * capG, per = capG + 2;
+  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * kB) {
     const int64_t s = r / capG, j = r - s * capG;
     const uint64_t sz = lk_size[r];
     const uint64_t off_in = lk_off[r] - lk_off[s * capG];
-    const bool keep = sz > 0 && off_in + sz <= (uint64_t)capD;
-    const uint64_t at = hdr + min(off_in, (uint64_t)capD);
-    seg_len[r] = keep ? sz : 0;
-    uint8_t* slot = s == W - 1 ? self_slot : R + s * slotR;
-    if (j < own_cnt[s]) {
-      reinterpret_cast<uint64_t*>(slot)[j] = keep ? (sz << 32 | off_in) : 0ull;
-      if (sz > 0 && !keep) atomicAdd(dropped, 1ull);
-    }
-    if (s == W - 1) dstB[j] = at;
-    else dstA[r] = (uint64_t)s * (uint64_t)slotR + at;
+    const bool keep = sz > 0 && off_in + sz <= used[s];
+    const bool self = s == W - 1;
+    const uint64_t sb = self ? 0 : (uint64_t)s * (uint64_t)slotR;
+    uint64_t* off = self ? offB : offA + s * per;
+    uint64_t* src = self ? srcB : srcA + s * per;
+    // zero-length rows (misses, padding, dropped) sit where the next kept row starts
+    off[1 + j] = sb + (uint64_t)capG * 8 + min(off_in, used[s]);
+    src[1 + j] = keep ? (uint64_t)(uintptr_t)(log + lk_loc[r]) : 0ull;
+    hdr[r] = keep ? (sz << 32 | off_in) : 0ull;
+    if (j < own_cnt[s] && sz > 0 && !keep) atomicAdd(dropped, 1ull);
   }
 }
 
 // Requester: (size, off) of every request row in `data` (0, 0 = miss; duplicates are
 // filled in from their claimer by expand_coalesced afterwards).
+// A coalesced duplicate (first[i] != i) takes its claiming row's record: each row
+// evaluates its claimer directly, so no second expansion pass is needed. The local
+// region holds the replica hits only if their total fit capL (one plain gather).
 __global__ __launch_bounds__(kB) void k_assemble_slots(
-    const int64_t* __restrict__ route, int64_t n, int32_t W, int32_t me, int64_t capG,
-    int64_t capL, int64_t slotR, const uint8_t* __restrict__ data,
-    const uint64_t* __restrict__ rl_size, const uint64_t* __restrict__ rl_off,
-    uint64_t* __restrict__ out_size, uint64_t* __restrict__ out_off) {
+    const int64_t* __restrict__ route, const uint32_t* __restrict__ first, int64_t n,
+    int32_t W, int32_t me, int64_t capG, int64_t capL, int64_t slotR,
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ rl_size,
+    const uint64_t* __restrict__ rl_off, uint64_t* __restrict__ out_size,
+    uint64_t* __restrict__ out_off) {
+  const bool local_ok = rl_size && rl_off[n] <= (uint64_t)capL;
   for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
-    const int64_t r = route[i];
+    const int64_t c = first ? (int64_t)first[i] : i;
+    const int64_t r = route[c];
     uint64_t sz = 0, off = 0;
     if (r < 0) {
-      if (rl_size && rl_size[i] > 0 && rl_off[i] + rl_size[i] <= (uint64_t)capL) {
-        sz = rl_size[i];
-        off = rl_off[i];
+      if (local_ok && rl_size[c] > 0) {
+        sz = rl_size[c];
+        off = rl_off[c];
       }
     } else {
       const int p = (int)(r >> 32);
@@ -926,27 +964,32 @@ void RoutedStep::owner_reply(HbmCache* shard, uint8_t* R, uint8_t* data, hipStre
   const int W = w_;
   const int64_t rows = (int64_t)W * capG_;
   const int64_t slotR = capG_ * 8 + capD_;
+  const int64_t per = capG_ + 2;
   SH_CHECK(capD_ > 0 && capD_ % 16 == 0, "RoutedStep: reply capacity not set");
-  uint64_t* dstA = buf<uint64_t>(kDstA, (size_t)(W - 1) * capG_ + 1);
-  uint64_t* dstB = buf<uint64_t>(kDstB, capG_ + 1);
-  uint64_t* seg_len = buf<uint64_t>(kSegLen, rows);
+  uint64_t* hdr = buf<uint64_t>(kHdr, rows);
+  uint64_t* used = buf<uint64_t>(kUsed, W);
+  uint64_t* offA = buf<uint64_t>(kDstA, (size_t)(W - 1) * per + 1);
+  uint64_t* srcA = buf<uint64_t>(kSrcA, (size_t)(W - 1) * per + 1);
+  uint64_t* offB = buf<uint64_t>(kDstB, per + 1);
+  uint64_t* srcB = buf<uint64_t>(kSrcB, per);
   uint8_t* self_slot = data + capL_ + (int64_t)(W - 1) * slotR;
   hipLaunchKernelGGL(k_demand, dim3(1), dim3(64), 0, s, lk_off_, W, rank_, capG_, rb_);
   RT_OK(hipMemsetAsync(rb_ + W, 0, sizeof(int64_t), s));
-  hipLaunchKernelGGL(k_reply_prep, dim3(grid1(rows + 1)), dim3(kB), 0, s, lk_size_, lk_off_,
-                     own_cnt_, W, capG_, capD_, slotR, R, self_slot, dstA, dstB, seg_len,
-                     reinterpret_cast<unsigned long long*>(rb_ + W));
+  hipLaunchKernelGGL(k_reply_used, dim3(1), dim3(64), 0, s, lk_off_, W, capG_, capD_, slotR, hdr,
+                     R, self_slot, used, offA, srcA, offB, srcB);
+  hipLaunchKernelGGL(k_reply_prep, dim3(grid1(rows)), dim3(kB), 0, s, lk_loc_, lk_size_, lk_off_,
+                     own_cnt_, used, W, capG_, slotR, shard->log_ptr(), hdr, offA, srcA, offB,
+                     srcB, reinterpret_cast<unsigned long long*>(rb_ + W));
   RT_OK(hipGetLastError());
-  const uint8_t* log = shard->log_ptr();
-  if (W > 1)
-    segcopy_sized(log, lk_loc_, dstA, seg_len, (int64_t)(W - 1) * capG_, R, s);
-  segcopy_sized(log, lk_loc_ + (int64_t)(W - 1) * capG_, dstB, seg_len + (int64_t)(W - 1) * capG_,
-                capG_, self_slot, s);
+  if (W > 1) segcopy(nullptr, srcA, offA, (int64_t)(W - 1) * per, R, s);
+  segcopy(nullptr, srcB, offB, per, self_slot, s);
 }
 
 void RoutedStep::gather_local(uint8_t* data, hipStream_t s) {
+  // all-or-nothing: nothing lands when the total outgrew capL (assemble then answers the
+  // replica hits as misses; the next steps' capL grows from the observed bytes)
   if (!have_replica_ || !replica_ || n_ <= 0) return;
-  segcopy_sized(replica_->log_ptr(), rl_loc_, rl_off_, rl_size_, n_, data, s, (uint64_t)capL_);
+  replica_->gather(rl_loc_, rl_off_, n_, data, s, (uint64_t)capL_);
 }
 
 // ---- SETs ---------------------------------------------------------------------------
@@ -1081,11 +1124,10 @@ void RoutedStep::assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out
   const int P = par_;
   if (n_ > 0) {
     const int64_t slotR = capG_ * 8 + capD_;
-    hipLaunchKernelGGL(k_assemble_slots, dim3(grid1(n_)), dim3(kB), 0, s, route_, n_, w_, rank_,
-                       capG_, capL_, slotR, data, have_replica_ ? rl_size_ : nullptr,
+    hipLaunchKernelGGL(k_assemble_slots, dim3(grid1(n_)), dim3(kB), 0, s, route_, first_, n_, w_,
+                       rank_, capG_, capL_, slotR, data, have_replica_ ? rl_size_ : nullptr,
                        have_replica_ ? rl_off_ : nullptr, out_size, out_off);
     RT_OK(hipGetLastError());
-    if (first_) expand_coalesced(first_, n_, out_size, out_off, s);  // duplicates
   }
   RT_OK(hipEventRecord(ev_asm_[P], s));
   asm_pending_[P] = true;

@@ -88,14 +88,25 @@ def _default_group():
     return distributed_c10d._get_default_group()
 
 
-def _mirror_row(row: torch.Tensor, world: int, me: int, q: int, peer_blocks: int) -> torch.Tensor:
-    """Rank q's row under MirrorComm's symmetric traffic: what q sends to x is what I send
-    to x with the roles of me and q exchanged (q -> me equals me -> q)."""
-    r = row.clone()
-    if q != me:
-        for b in range(peer_blocks):
-            r[b * world + me], r[b * world + q] = row[b * world + q], row[b * world + me]
-    return r
+_MIRROR_IDX: dict = {}
+
+
+def _mirror_index(k: int, world: int, me: int, peer_blocks: int, device) -> torch.Tensor:
+    """Gather index of every rank's row under MirrorComm's symmetric traffic: what rank q
+    sends to x is what I send to x with the roles of me and q exchanged (q -> me equals
+    me -> q); one index_select builds the whole matrix."""
+    key = (k, world, me, peer_blocks, str(device))
+    idx = _MIRROR_IDX.get(key)
+    if idx is None:
+        rows = []
+        for q in range(world):
+            r = list(range(k))
+            if q != me:
+                for b in range(peer_blocks):
+                    r[b * world + me], r[b * world + q] = r[b * world + q], r[b * world + me]
+            rows += r
+        idx = _MIRROR_IDX[key] = torch.tensor(rows, dtype=torch.int64, device=device)
+    return idx
 
 
 def all_gather_rows(out: torch.Tensor, row: torch.Tensor, group=None, peer_blocks: int = 0) -> None:
@@ -104,9 +115,8 @@ def all_gather_rows(out: torch.Tensor, row: torch.Tensor, group=None, peer_block
     blocks of one entry per peer (used only to mirror rows under ``MirrorComm``)."""
     rank, world = dist_info(group)
     if isinstance(group, MirrorComm):
-        k = row.numel()
-        for q in range(world):
-            out[q * k:(q + 1) * k].copy_(_mirror_row(row, world, rank, q, peer_blocks))
+        torch.index_select(row, 0, _mirror_index(row.numel(), world, rank, peer_blocks,
+                                                 row.device), out=out)
         return
     if isinstance(group, BounceComm):
         host = [torch.empty(row.shape, dtype=row.dtype) for _ in range(world)]

@@ -70,3 +70,15 @@ def test_bench_rank_count_mismatch_exits_nonzero():
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert "refusing" in p.stderr
+
+
+def test_bench_more_gpus_than_devices_exits_nonzero():
+    """--gpus N on a node with fewer devices: a clear message and no number, instead of
+    several ranks silently sharing a device (here: no GPU at all)."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "GPUs on this node" in p.stderr

@@ -230,14 +230,15 @@ def test_gpu_shard_ejection_drill_and_restore():
         o.stop()
 
 
-def test_gpu_shard_warm_restore_pulls_its_keys_back_from_peers():
+@pytest.mark.parametrize("peer_copy", ["auto", "staged"])
+def test_gpu_shard_warm_restore_pulls_its_keys_back_from_peers(peer_copy):
     """Two shards (both on GPU 0 here; on a node they are two GPUs and the copy goes
     over xGMI). While shard 0 is ejected its key range is served by shard 1; when it
     returns it flushes, then pulls those objects back peer-to-peer, so they keep hitting
     (shard 1 drops them). Objects shard 1 owned all along are untouched."""
     from shellac_amd import core
 
-    be = core().hbm_backend([0, 0], 64 << 20, 1 << 14, 1 << 16, 0)
+    be = core().hbm_backend([0, 0], 64 << 20, 1 << 14, 1 << 16, 0, peer_copy=peer_copy)
     before = [b"/wr/before/%d" % i for i in range(300)]
     for i, k in enumerate(before):
         be.set(k, b"b%d" % i * 20, 1, 0)
@@ -261,6 +262,8 @@ def test_gpu_shard_warm_restore_pulls_its_keys_back_from_peers():
         sum(g is None for g in got)
     st = be.stats()
     assert 100 < st["hbm_migrated"] < 300, st["hbm_migrated"]
+    # "staged": the records went through pinned host memory (a pair without peer access)
+    assert (st["hbm_staged_peer_copies"] > 0) == (peer_copy == "staged")
     # before the drill: shard 1's objects hit, shard 0's were flushed on restore
     hits = sum(be.get(k) == (b"b%d" % i * 20, 1) for i, k in enumerate(before))
     assert 80 < hits < 220, hits
