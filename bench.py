@@ -97,6 +97,10 @@ def parse():
     ap.add_argument("--no-wrapped", action="store_true",
                     help="skip the secondary steady-state measurement (value log wrapped, so "
                          "every SET batch runs the eviction hand)")
+    ap.add_argument("--pressured-gb", type=float, default=5.0,
+                    help="secondary steady state under capacity pressure: a shard with this "
+                         "many GiB of log (the 4M keys' ~4 GiB barely fit), wrapped, so the "
+                         "CLOCK hand re-appends read objects every step (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -197,6 +201,8 @@ def check_memory_budget(args, world, sim, dev) -> None:
     need += 3 * args.batch * (mean_val + 48) * 1.2 + 2 * gib        # responses in flight
     if not args.no_smoke and world > 1:
         need += gib
+    if args.pressured_gb > 0 and not sim:
+        need += args.pressured_gb * gib + nb * 128
     free, total = torch.cuda.mem_get_info(dev)
     if need > free:
         print(f"[bench] error: this configuration needs ~{need / gib:.1f} GiB of HBM per rank "
@@ -365,9 +371,10 @@ def main():
     use_events = dev.type == "cuda"
     rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
 
-    def timed(steps, first, events=False):
+    def timed(steps, first, events=False, cache=None):
         """Run `steps` steps bracketed by barrier + device sync; returns (max-over-ranks
         wall seconds, per-step GPU-event intervals in ms if `events`, last result)."""
+        cache = sc if cache is None else cache
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if events else []
         cur = torch.cuda.current_stream(dev) if events else None
         if real_world > 1:
@@ -378,7 +385,7 @@ def main():
         for i in range(steps):
             if events:
                 evs[i].record(cur)
-            res = step(first + i)
+            res = cache.serve(gets[(first + i) % P], sets[(first + i) % P])
         if events:
             evs[steps].record(cur)
         sync()
@@ -457,38 +464,63 @@ def main():
     # has wrapped (16 GiB per shard, ~66 MB appended per step); a serving cache is full, and
     # then every SET batch runs the eviction hand (CLOCK second chances) first. Steps run
     # until every rank's log has wrapped by a quarter lap, then the same K steps are timed.
-    wrapped = None
-    if not args.no_wrapped and not host_edge and dev.type == "cuda":
+    def steady_state(sc_, shard_, log_bytes_, base):
         per_step = max((head1 - head0) / max(args.steps, 1), 1.0)
-        need = torch.tensor([max(0.0, (1.25 * log_bytes - shard.head()) / per_step)],
+        need = torch.tensor([max(0.0, (1.25 * log_bytes_ - shard_.head()) / per_step)],
                             dtype=torch.float64, device=rdev)
         if real_world > 1:
             dist.all_reduce(need, op=dist.ReduceOp.MAX)
         nfill = int(float(need)) + 2
-        if nfill <= 20000:
-            base = args.warmup + 2 * args.steps
-            for i in range(nfill):
-                step(base + i)
-            sync()
-            sc.sync_sets()
-            w0 = shard.counters()
-            el_w, iv_w, _ = timed(args.steps, base + nfill, events=use_events)
-            sc.sync_sets()
-            w1 = shard.counters()
-            wagg = torch.tensor([w1["get_hits"] - w0["get_hits"], w1["get_ops"] - w0["get_ops"],
-                                 w1["reinsert_bytes"] - w0["reinsert_bytes"]],
-                                dtype=torch.int64, device=rdev)
-            if real_world > 1:
-                dist.all_reduce(wagg)
-            wh, wo, wr = (int(v) for v in wagg.tolist())
-            wrapped = {"ms_per_step": round(el_w / args.steps * 1e3, 4),
-                       "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps
-                                                / el_w, 1),
-                       "fill_steps": nfill,
-                       "owner_hit_ratio": round(wh / max(wo, 1), 4),
-                       "reinserted_bytes_per_step_per_rank": round(wr / world / args.steps)}
-            if iv_w:
-                wrapped["ms_per_step_median_gpu_events"] = round(sorted(iv_w)[len(iv_w) // 2], 4)
+        if nfill > 20000:
+            return None
+        for i in range(nfill):
+            sc_.serve(gets[(base + i) % P], sets[(base + i) % P])
+        sync()
+        sc_.sync_sets()
+        w0 = shard_.counters()
+        el_w, iv_w, _ = timed(args.steps, base + nfill, events=use_events, cache=sc_)
+        sc_.sync_sets()
+        w1 = shard_.counters()
+        wagg = torch.tensor([w1["get_hits"] - w0["get_hits"], w1["get_ops"] - w0["get_ops"],
+                             w1["reinsert_bytes"] - w0["reinsert_bytes"]],
+                            dtype=torch.int64, device=rdev)
+        if real_world > 1:
+            dist.all_reduce(wagg)
+        wh, wo, wr = (int(v) for v in wagg.tolist())
+        res = {"ms_per_step": round(el_w / args.steps * 1e3, 4),
+               "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps / el_w, 1),
+               "log_gib_per_shard": round(log_bytes_ / (1 << 30), 2),
+               "fill_steps": nfill,
+               "owner_hit_ratio": round(wh / max(wo, 1), 4),
+               "reinserted_bytes_per_step_per_rank": round(wr / world / args.steps)}
+        if iv_w:
+            res["ms_per_step_median_gpu_events"] = round(sorted(iv_w)[len(iv_w) // 2], 4)
+        return res
+
+    steady_ok = not host_edge and dev.type == "cuda"
+    wrapped = None
+    if not args.no_wrapped and steady_ok:
+        wrapped = steady_state(sc, shard, log_bytes, args.warmup + 2 * args.steps)
+    # secondary: the same under capacity pressure — a shard whose log barely holds the key
+    # space, so objects the steps read are re-appended (reinsertions > 0) every step
+    pressured = None
+    if args.pressured_gb > 0 and steady_ok and not sim:
+        p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
+        p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
+        p_sc = ShardedCache(p_shard, group=group, replica=replica, data_group=data_group,
+                            routed=True if routed1 else None)
+        p_sc.coalesce = sc.coalesce
+        if replica is not None:
+            p_sc._hot, p_sc._hot_dir = sc._hot, None
+        for s0 in range(lo, hi, chunk):
+            p_sc.set(wl.set_batch(torch.arange(s0, min(s0 + chunk, hi), device=dev)))
+        p_shard.reserve(max(args.sets * 2, chunk))
+        sync()
+        if real_world > 1:
+            dist.barrier()
+        pressured = steady_state(p_sc, p_shard, p_log, 3 * args.warmup + 2 * args.steps)
+        p_sc.sync_sets()
+        del p_sc, p_shard
 
     t_sm = time.perf_counter()
     sm = {} if (args.no_smoke or dev.type != "cuda" or sim or bounce) else smoke(rank, world, dev)
@@ -547,6 +579,8 @@ def main():
         "edge": args.edge,
         # the same step with the value log wrapped (eviction in every SET batch)
         "log_wrapped": wrapped,
+        # the same under capacity pressure (a log the key space barely fits: reinsertions)
+        "log_pressured": pressured,
         "smoke": sm,
     }
     if host_edge:

@@ -173,6 +173,11 @@ def main():
     ap.add_argument("--misc-cpus", type=int, default=0,
                     help="cores for the GPU batcher, the proxy's other threads and the origin "
                          "(default 1: the origin idles once the cache is filled)")
+    ap.add_argument("--batcher-core", choices=["auto", "off"], default="auto",
+                    help="auto (pinned GPU backends): the GPU batcher on a core of its own, "
+                         "next to the misc core")
+    ap.add_argument("--no-edge-server", action="store_true",
+                    help="HBM: a kernel launch per GET batch instead of the resident server")
     ap.add_argument("--layouts", nargs="+", default=None,
                     help="RxC pairs (reactor threads x load-generator threads), each measured "
                          "with its own proxy over the same filled cache (default: "
@@ -190,6 +195,12 @@ def main():
     pin = a.pin == "auto" and len(allowed) >= 4
     nmisc = a.misc_cpus or 1
     misc_cpus = allowed[-nmisc:] if pin else []
+    # the GPU batcher spins on its queue and on the GPU: a core of its own, not the
+    # origin's / the proxy's other threads'
+    batcher_cpus = []
+    if pin and gpu and a.batcher_core == "auto":
+        batcher_cpus = [allowed[-nmisc - 1]]
+        nmisc += 1
     # busy-polling only on dedicated (pinned) cores
     if a.rx_spin_us is None:
         a.rx_spin_us = 200 if pin else 0
@@ -216,7 +227,8 @@ def main():
     else:
         backend = make_backend("hbm", gpus=[0], hbm_gb=hbm_gb, batch_us=a.batch_us,
                                l1_mb=a.l1_mb if a.backend == "tiered" else 0,
-                               depth=a.hbm_depth, evict=a.evict)
+                               depth=a.hbm_depth, evict=a.evict,
+                               edge_server=not a.no_edge_server, batcher_cpus=batcher_cpus)
     prefix = "/o/"  # no /gz prefix: the origin sends the incompressible body as is
     out = {"backend": a.backend, "proxy_threads": layouts[0][0], "objects": a.objects,
            "body_bytes": a.body, "zipf": a.zipf, "working_set_MB": a.objects * item / 1e6,
@@ -225,7 +237,8 @@ def main():
            "hbm_gb": hbm_gb if a.backend in ("hbm", "tiered") else None,
            "cpu_count": os.cpu_count(), "cpu_budget": budget,
            "processes": "origin | proxy | load generator",
-           "cpus": {"proxy_other": misc_cpus, "origin": or_cpus},
+           "cpus": {"proxy_other": misc_cpus, "origin": or_cpus, "gpu_batcher": batcher_cpus},
+           "edge_server": gpu and not a.no_edge_server,
            "spin_us": {"reactors": a.rx_spin_us, "load_generator": a.lg_spin_us}}
     px = None
     try:

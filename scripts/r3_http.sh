@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 3 HTTP matrix (8M x 4 KiB incompressible, Zipf 0.99, c=10 and c=1000): DRAM-only,
+# HBM-only and tiered, the GPU batcher on a core of its own (8 reactors x 6 load-generator
+# workers), HBM-only also without the resident edge server (a launch per GET batch).
+set -o pipefail
+OUT=gpurun_out/${1:-r3_http}
+mkdir -p "$OUT"
+run() { # name args...
+  local name=$1; shift
+  timeout -k 10 560 python benchmarks/http_bench.py "$@" --out "$OUT/$name.json" \
+    > "$OUT/$name.log" 2>&1 || { echo "$name failed"; tail -5 "$OUT/$name.log"; return 1; }
+  grep "\[http\]" "$OUT/$name.log" | sed "s|^|$name |" | cut -c1-260
+}
+shift
+for spec in "$@"; do
+  case $spec in
+    dram)   run dram_8M   --backend dram   --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
+    hbm)    run hbm_8M    --backend hbm    --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
+    hbm_nosrv) run hbm_8M_nosrv --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-edge-server || exit 1;;
+    tiered) run tiered_8M --backend tiered --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
+  esac
+done

@@ -69,6 +69,13 @@ class Compressor {
   using Done = std::function<void(bool ok, std::string out)>;
   virtual ~Compressor() = default;
   virtual void submit(std::string body, Done done) = 0;
+  // gunzip one member off the caller's thread (output capped at max_out bytes); engines
+  // without it return false from can_inflate() and the caller decodes inline
+  virtual bool can_inflate() const { return false; }
+  virtual void submit_inflate(std::string member, uint64_t max_out, Done done) {
+    (void)max_out;
+    done(false, std::move(member));
+  }
   virtual void stats(StatList* out) = 0;
 };
 
@@ -150,6 +157,12 @@ struct HbmBackendConfig {
   // Pinned response arenas allocated up front per GPU (depth + 2 of this size): pinning
   // host memory mid-run stalled every socket call on the box for up to ~0.5 s
   uint64_t arena_bytes = 16u << 20;
+  // GET batches of at most HbmCache::kServeKeys distinct keys go to the GPU's persistent
+  // edge server (HbmCache::serve_get: no launch per batch) unless a SET / DELETE of one
+  // of their keys is still in flight; off: every batch is a launch on the stream
+  bool edge_server = true;
+  // CPUs the batcher threads run on (thread i on batcher_cpus[i % size]; empty: unpinned)
+  std::vector<int> batcher_cpus;
 };
 
 // One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are

@@ -167,9 +167,12 @@ struct Flight {
   size_t rows = 0;                         // distinct GET digests
   Mapped keys, offs, set_keys, set_vals, set_voff, set_meta, del_keys, del_found;
   std::shared_ptr<ArenaPool::Arena> arena;
+  std::vector<uint64_t> wkeys;  // SET / DELETE digests (lo words) counted in Dev::pend_w
+  bool flush = false;           // a flush runs on the stream right before this flight
   hipEvent_t ev = nullptr;
   int slot = -1;
   bool active = false, got = false;
+  bool served = false;  // GETs answered by the persistent edge server (no stream launch)
   uint32_t tnow = 0;
   double t0 = 0;
 };
@@ -207,12 +210,17 @@ struct HbmBackend::Dev {
   int npts = 0;
   // co-table for host GET coalescing (batcher thread only)
   std::vector<int32_t> co_tab;
+  // digests (lo word) with a SET / DELETE in a flight not yet reaped, and flushes in
+  // flight: a GET of such a key takes the stream path, ordered after them
+  std::unordered_map<uint64_t, uint32_t> pend_w;
+  uint32_t pend_flush = 0;
+  void track_writes(const Flight& f, int dir);
   double avg_row_bytes = 4096;
   // stats
   std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
       filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
       key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, arena_misses{0},
-      dropped{0}, staged_copies{0},
+      dropped{0}, staged_copies{0}, served_batches{0}, ordered_gets{0},
       migrated{0}, migrate_ns{0};
 
   void loop();
@@ -487,6 +495,12 @@ void HbmBackend::Dev::loop() {
   (void)hipSetDevice(device);
   const std::string nm = "shellac-hbm" + std::to_string(device);
   pthread_setname_np(pthread_self(), nm.c_str());
+  if (!cfg.batcher_cpus.empty()) {  // a core of its own: it spins on the queue and the GPU
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cfg.batcher_cpus[(size_t)index % cfg.batcher_cpus.size()], &set);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+  }
   std::vector<Req> batch;
   for (;;) {
     bool worked = false;
@@ -509,6 +523,7 @@ void HbmBackend::Dev::loop() {
         eject("stall");
       }
       if (freed) {
+        track_writes(f, -1);
         head = (head + 1) % flights.size();
         --inflight;
         worked = true;
@@ -534,7 +549,9 @@ void HbmBackend::Dev::loop() {
           f.reqs.swap(batch);
           try {
             if (do_flush) cache->flush(stream);
+            f.flush = do_flush;
             launch(f);
+            track_writes(f, +1);
             ++inflight;
           } catch (const std::exception& e) {
             std::fprintf(stderr, "[shellac hbm] gpu %d launch failed: %s\n", device, e.what());
@@ -608,6 +625,7 @@ void HbmBackend::Dev::launch(Flight& f) {
   f.t0 = wall_s();
   f.got = f.gets.empty();
   f.active = true;
+  f.served = false;
   // ---- GET: coalesce equal digests on the host (a hot object under concurrent clients
   // is one GPU row and one arena record, shared by its requests), then one edge-GET
   // launch: keys and offsets in mapped memory, records straight into a pinned arena
@@ -641,8 +659,19 @@ void HbmBackend::Dev::launch(Flight& f) {
     // arena sized from the running average record size (regathered if it falls short)
     const size_t want = (size_t)(avg_row_bytes * 1.5 * (double)f.rows) + (64u << 10);
     f.arena = pool->take(want);
-    cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
-                     f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
+    // small batches go to the resident edge server unless they must stay ordered after a
+    // SET / DELETE / flush still in flight (read-your-writes for memcached clients)
+    bool ordered = pend_flush > 0 || f.flush;
+    for (size_t u = 0; !ordered && !pend_w.empty() && u < f.rows; ++u)
+      ordered = pend_w.count(hk[u].lo) != 0;
+    if (ordered) ordered_gets++;
+    f.served = be->cfg_.edge_server && !ordered && f.rows <= (size_t)HbmCache::kServeKeys &&
+               cache->serve_get(hk, (int64_t)f.rows, f.arena->d, f.arena->cap,
+                                f.offs.dev<uint64_t>(), f.tnow, f.slot);
+    if (f.served) served_batches++;
+    else
+      cache->small_get(f.keys.dev<Digest>(), (int64_t)f.rows, f.arena->d, f.arena->cap,
+                       f.offs.dev<uint64_t>(), f.tnow, stream, f.slot);
   }
   // ---- SET: [klen | key | payload] values packed into mapped staging the SET kernels
   // read directly (no copies), exact log-bytes bound
@@ -702,7 +731,10 @@ bool HbmBackend::Dev::try_reap(Flight& f, bool block) {
   if (!f.got && f.active) {
     const uint64_t total = block ? cache->wait_host_slot(f.slot, be->cfg_.batch_timeout_ms)
                                  : cache->host_slot(f.slot);
-    if (total == HbmCache::kSlotPending) return false;
+    if (total == HbmCache::kSlotPending) {
+      if (f.served) cache->serve_kick();  // relaunch the server if it exited meanwhile
+      return false;
+    }
     if (total == HbmCache::kSlotFailed) throw Error("edge GET reported a failed look-back");
     if (f.rows) avg_row_bytes = 0.9 * avg_row_bytes + 0.1 * ((double)total / (double)f.rows);
     if (total > f.arena->cap) {
@@ -746,6 +778,27 @@ bool HbmBackend::Dev::try_reap(Flight& f, bool block) {
   f.reqs.clear();
   f.arena.reset();  // hits hold their own references
   return true;
+}
+
+// dir = +1 when flight f launches, -1 when it is freed: its SET / DELETE digests and
+// its flush count as in flight until then.
+void HbmBackend::Dev::track_writes(const Flight& f, int dir) {
+  Flight& m = const_cast<Flight&>(f);
+  if (dir > 0) {
+    m.wkeys.clear();
+    for (uint32_t i : f.sets) m.wkeys.push_back(f.reqs[i].d.lo);
+    for (uint32_t i : f.dels) m.wkeys.push_back(f.reqs[i].d.lo);
+    for (uint64_t k : m.wkeys) ++pend_w[k];
+    if (f.flush) ++pend_flush;
+    return;
+  }
+  for (uint64_t k : m.wkeys) {
+    auto it = pend_w.find(k);
+    if (it != pend_w.end() && --it->second == 0) pend_w.erase(it);
+  }
+  m.wkeys.clear();
+  if (m.flush && pend_flush) --pend_flush;
+  m.flush = false;
 }
 
 // Group completions per executor: one post_batch (one lock, one wake-up) per reactor.
@@ -897,6 +950,8 @@ void HbmBackend::Dev::maybe_restore() {
   failed = false;
   inflight = 0;
   head = 0;
+  pend_w.clear();
+  pend_flush = 0;
   for (auto& f : flights) {
     f->active = false;
     f->reqs.clear();
@@ -1188,6 +1243,11 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_restores", sum(&Dev::restores));
   out->emplace_back("hbm_regathers", sum(&Dev::regathers));
   out->emplace_back("hbm_arena_misses", sum(&Dev::arena_misses));
+  out->emplace_back("hbm_served_batches", sum(&Dev::served_batches));
+  out->emplace_back("hbm_ordered_get_batches", sum(&Dev::ordered_gets));
+  uint64_t sl = 0;
+  for (auto& d : devs_) sl += d->cache->serve_launches();
+  out->emplace_back("hbm_server_launches", sl);
   out->emplace_back("hbm_staged_peer_copies", sum(&Dev::staged_copies));
   uint64_t direct = 0;
   for (uint8_t v : peer_ok_) direct += v;

@@ -50,6 +50,7 @@ PYBIND11_MODULE(_shellac_core, m) {
   m.attr("BUCKET_BYTES") = (int)kBucketBytes;
   m.attr("ITEM_HEADER_BYTES") = (int)kItemHeaderBytes;
   m.attr("SMALL_GET_MAX") = (int64_t)HbmCache::kSmallGetMax;
+  m.attr("SERVE_KEYS") = (int64_t)HbmCache::kServeKeys;
   m.attr("ITEM_MAGIC") = kItemMagic;
   m.attr("MISS_LOC") = py::int_(kMissLoc);
 
@@ -111,6 +112,29 @@ PYBIND11_MODULE(_shellac_core, m) {
                     S(s), done_slot);
       }, py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
          py::arg("now"), py::arg("stream"), py::arg("done_slot") = -1)
+      .def("serve_get", [](HbmCache& c, uintptr_t host_keys, int64_t n, uintptr_t out,
+                           uint64_t out_cap, uintptr_t off, uint32_t now, int done_slot) {
+        py::gil_scoped_release nogil;
+        return c.serve_get(P<const Digest>(host_keys), n, P<uint8_t>(out), out_cap,
+                           P<uint64_t>(off), now, done_slot);
+      }, py::arg("host_keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
+         py::arg("now"), py::arg("done_slot"))
+      .def("serve_wait", [](HbmCache& c, int slot, int64_t timeout_ms) {
+        py::gil_scoped_release nogil;
+        return c.serve_wait(slot, timeout_ms);
+      }, py::arg("slot"), py::arg("timeout_ms") = 10000)
+      .def("serve_kick", [](HbmCache& c) {
+        py::gil_scoped_release nogil;
+        c.serve_kick();
+      })
+      .def("serve_stop", [](HbmCache& c) {
+        py::gil_scoped_release nogil;
+        c.serve_stop();
+      })
+      .def("serve_trace", &HbmCache::serve_trace)
+      .def_property_readonly("wall_khz", &HbmCache::wall_khz)
+      .def_property_readonly("serve_launches", &HbmCache::serve_launches)
+      .def_property_readonly("serve_jobs", &HbmCache::serve_jobs)
       .def("host_slot", &HbmCache::host_slot)
       .def("wait_host_slot", [](const HbmCache& c, int i, int64_t timeout_ms) {
         py::gil_scoped_release nogil;

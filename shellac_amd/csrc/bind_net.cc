@@ -197,7 +197,8 @@ void bind_net(py::module_& m) {
                           int max_batch, int sweep_interval_s, int spin_us,
                           bool presence_filter, int depth, const std::string& evict,
                           int retry_s, int batch_timeout_ms, bool flush_on_restore,
-                          bool warm_restore, const std::string& peer_copy) {
+                          bool warm_restore, const std::string& peer_copy, bool edge_server,
+                          std::vector<int> batcher_cpus) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -217,6 +218,8 @@ void bind_net(py::module_& m) {
     c.warm_restore = warm_restore;
     SH_CHECK(peer_copy == "auto" || peer_copy == "staged", "peer_copy must be auto or staged");
     c.peer_copy = peer_copy;
+    c.edge_server = edge_server;
+    c.batcher_cpus = std::move(batcher_cpus);
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
@@ -225,7 +228,8 @@ void bind_net(py::module_& m) {
      py::arg("presence_filter") = true, py::arg("depth") = 3, py::arg("evict") = "clock",
      py::arg("retry_s") = 2, py::arg("batch_timeout_ms") = 2000,
      py::arg("flush_on_restore") = true, py::arg("warm_restore") = true,
-     py::arg("peer_copy") = "auto");
+     py::arg("peer_copy") = "auto", py::arg("edge_server") = true,
+     py::arg("batcher_cpus") = std::vector<int>{});
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);

@@ -95,6 +95,9 @@ class GpuGzip {
 // short window (`batch_us`, or `max_batch` bodies) into ONE GpuGzip::compress call, then
 // runs each completion (which posts back to its reactor). On a GPU error the completion
 // gets ok = false and the original body back, so the caller can fall back to the CPU.
+// Inflate jobs (identity variants of gzip objects for clients without gzip) batch the
+// same way into GpuGzip::inflate; a member the GPU path does not decode is inflated with
+// zlib on the service thread, never on a reactor.
 class GzipService : public Compressor {
  public:
   // `workers` threads, each with its own engine and stream, take batches in turn, so one
@@ -102,9 +105,12 @@ class GzipService : public Compressor {
   GzipService(int device, int batch_us = 200, size_t max_batch = 4096, int workers = 2);
   ~GzipService() override;
   void submit(std::string body, Done done) override;
+  bool can_inflate() const override { return true; }
+  void submit_inflate(std::string member, uint64_t max_out, Done done) override;
   void stats(StatList* out) override;
   struct Stats {
     uint64_t batches = 0, bodies = 0, in_bytes = 0, out_bytes = 0, errors = 0;
+    uint64_t inflate_batches = 0, inflated_gpu = 0, inflated_cpu = 0, inflate_errors = 0;
   };
   Stats totals();
 
@@ -113,7 +119,10 @@ class GzipService : public Compressor {
   struct Job {
     std::string body;
     Done done;
+    bool inflate = false;
+    uint64_t max_out = 0;
   };
+  void run_inflate(GpuGzip* gz, std::vector<Job>& batch);
   std::vector<std::unique_ptr<GpuGzip>> gz_;
   int batch_us_;
   size_t max_batch_;

@@ -10,6 +10,7 @@
 
 #include "common.h"
 #include "deflate.h"
+#include "http.h"
 #include "huffman.h"
 
 #define GZ_OK(expr)                                                                       \
@@ -986,9 +987,53 @@ GzipService::~GzipService() {
 void GzipService::submit(std::string body, Done done) {
   {
     std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back(Job{std::move(body), std::move(done)});
+    q_.push_back(Job{std::move(body), std::move(done), false, 0});
   }
   cv_.notify_one();
+}
+
+void GzipService::submit_inflate(std::string member, uint64_t max_out, Done done) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(Job{std::move(member), std::move(done), true, max_out});
+  }
+  cv_.notify_one();
+}
+
+// One GpuGzip::inflate call for the batch; members it does not decode (or whose output
+// exceeds their own cap) go through zlib here, on the service thread.
+void GzipService::run_inflate(GpuGzip* gz, std::vector<Job>& batch) {
+  std::vector<std::string_view> v;
+  uint64_t cap = 0;
+  for (const auto& j : batch) {
+    v.emplace_back(j.body);
+    cap = std::max(cap, j.max_out);
+  }
+  std::vector<std::string> out;
+  std::vector<uint8_t> okv;
+  try {
+    out = gz->inflate(v, &okv, cap);
+  } catch (const std::exception&) {
+    out.assign(batch.size(), std::string());
+    okv.assign(batch.size(), 0);
+  }
+  uint64_t gpu = 0, cpu = 0, bad = 0;
+  for (size_t i = 0; i < batch.size(); ++i) {
+    if (okv[i] && out[i].size() <= batch[i].max_out) {
+      ++gpu;
+      batch[i].done(true, std::move(out[i]));
+      continue;
+    }
+    std::string o;
+    const bool ok = gzip_decompress(batch[i].body, &o, batch[i].max_out);
+    ok ? ++cpu : ++bad;
+    batch[i].done(ok, ok ? std::move(o) : std::string());
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.inflate_batches++;
+  st_.inflated_gpu += gpu;
+  st_.inflated_cpu += cpu;
+  st_.inflate_errors += bad;
 }
 
 GzipService::Stats GzipService::totals() {
@@ -1003,6 +1048,10 @@ void GzipService::stats(StatList* out) {
   out->emplace_back("in_bytes", t.in_bytes);
   out->emplace_back("out_bytes", t.out_bytes);
   out->emplace_back("errors", t.errors);
+  out->emplace_back("inflate_batches", t.inflate_batches);
+  out->emplace_back("inflated_gpu", t.inflated_gpu);
+  out->emplace_back("inflated_cpu", t.inflated_cpu);
+  out->emplace_back("inflate_errors", t.inflate_errors);
 }
 
 void GzipService::loop(GpuGzip* gz) {
@@ -1015,13 +1064,19 @@ void GzipService::loop(GpuGzip* gz) {
       // collect for up to batch_us after the first submission (or until max_batch)
       const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(batch_us_);
       cv_.wait_until(lk, until, [&] { return stop_ || q_.size() >= max_batch_; });
-      const size_t take = std::min(q_.size(), max_batch_);
-      for (size_t i = 0; i < take; ++i) {
+      // one kind per batch: the compress or inflate jobs at the front of the queue
+      while (!q_.empty() && batch.size() < max_batch_ &&
+             (batch.empty() || q_.front().inflate == batch.front().inflate)) {
         batch.push_back(std::move(q_.front()));
         q_.pop_front();
       }
     }
     if (batch.empty()) continue;  // another worker took this window's bodies
+    if (batch.front().inflate) {
+      run_inflate(gz, batch);
+      batch.clear();
+      continue;
+    }
     std::vector<std::string_view> v;
     v.reserve(batch.size());
     uint64_t inb = 0;

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "layout.h"
 
@@ -97,6 +98,33 @@ class HbmCache {
   void small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t out_cap, uint64_t* off,
                  uint32_t now, hipStream_t s, int done_slot = -1);
   static constexpr int64_t kSmallGetMax = 1 << 17;
+  // Persistent edge-GET server: the same contract as small_get for batches of at most
+  // kServeKeys rows, answered by one resident workgroup that polls a ring of jobs in
+  // pinned host memory — no kernel launch and no stream per batch. The keys are copied
+  // into the ring (host pointer); out / off are device views of mapped memory as for
+  // small_get, and the total (or kSlotFailed) lands in host slot `done_slot`.
+  // Returns false (nothing queued) when the ring is full or n is out of range; the
+  // caller then uses small_get. Each call must eventually be followed by serve_kick()
+  // calls while its slot is pending (the server exits when idle or at the end of its
+  // lifetime, and serve_kick restarts it if jobs are outstanding). Records a SET
+  // overwrites while the server copies them come back with a zeroed magic word (the
+  // caller treats them as misses). Not ordered against anything on any stream: the
+  // caller keeps GETs of keys with SETs / DELETEs in flight on the stream path.
+  static constexpr int kServeKeys = 29;   // a job (5 + 2 per key 16-B granules) is one wave's load
+  static constexpr int kServeRing = 16;
+  bool serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
+                 uint64_t* off, uint32_t now, int done_slot);
+  void serve_kick();
+  // wait_host_slot for a serve_get job: spins, relaunching the server when it exited
+  uint64_t serve_wait(int done_slot, int64_t timeout_ms = 10000);
+  void serve_stop();  // ask the server to exit and wait for it (outstanding jobs stay queued)
+  uint64_t serve_launches() const { return srv_launches_; }
+  uint64_t serve_jobs() const { return srv_ticket_; }
+  // Phase stamps of the last (up to 64) server jobs, wall-clock ticks of the device:
+  // rows of {ticket, poll issued, job seen, probed, copied, done, n, total bytes}; and the
+  // tick rate (kHz).
+  std::vector<uint64_t> serve_trace() const;
+  uint64_t wall_khz() const { return srv_khz_; }
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
   // caller can queue the gather before it knows the total and retry if it did not fit.
@@ -188,12 +216,25 @@ class HbmCache {
   uint64_t* head_ = nullptr;         // device: logical write head, 2 ping-pong slots
   int hsel_ = 0;                     // slot holding the current head
   uint64_t* cur_head() const { return head_ + hsel_; }
+  // furthest log byte any queued SET append will write (monotone; set before the append)
+  uint64_t* claim_ptr() const { return head_ + 4; }
   uint64_t* next_head() const { return head_ + (hsel_ ^ 1); }
   CacheCounters* ctr_ = nullptr;     // device counters (64 shards)
   unsigned long long* scratch_ = nullptr;  // device scratch for reductions
   uint64_t* part_ = nullptr;         // per-workgroup sums: GET sizes, SET sizes, SET counts
   uint64_t* host_buf_ = nullptr;     // pinned scratch for small D2H reads
   uint64_t* host_slots_ = nullptr;   // pinned coherent slots the GPU writes totals into
+  // persistent edge-GET server (serve_get): job ring + control words in pinned coherent
+  // memory, its own CU-masked stream (a queue of its own: nothing queues behind it)
+  void* srv_ring_ = nullptr;
+  uint64_t* srv_ctl_ = nullptr;      // [0] consumed tickets, [8] exited epoch, [16] stop
+  hipStream_t srv_stream_ = nullptr;
+  uint64_t srv_ticket_ = 0, srv_epoch_ = 0, srv_launches_ = 0;
+  uint64_t srv_idle_ticks_ = 0, srv_life_ticks_ = 0, srv_khz_ = 0;
+  uint64_t* srv_trace_ = nullptr;    // pinned: per-job phase stamps (serve_trace)
+  bool srv_running_ = false;
+  std::mutex srv_mu_;
+  void serve_launch_locked();
   unsigned int* done_ctr_ = nullptr; // device: edge-GET workgroups finished + fail flag (self-resetting)
   unsigned long long* lb_state_ = nullptr;  // device: edge-GET look-back words (self-resetting)
   // SET workspace

@@ -238,7 +238,9 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ off,
                                                     uint64_t* __restrict__ host_total,
                                                     const uint64_t* __restrict__ part_cnt,
-                                                    uint64_t* __restrict__ cnt) {
+                                                    uint64_t* __restrict__ cnt,
+                                                    const uint64_t* __restrict__ claim_head,
+                                                    unsigned long long* __restrict__ claim) {
   __shared__ unsigned long long s_w[2][kBlock / 64];
   __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -325,6 +327,9 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
     if (cnt) cnt[n] = totc;
     if (host_total)
       __hip_atomic_store(host_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // a SET batch's sizes: claim the log bytes its append will write before the append
+    // kernel starts (the edge server re-checks its copies against this word)
+    if (claim) atomicMax(claim, (unsigned long long)(*claim_head + tot));
   }
 }
 
@@ -1056,6 +1061,269 @@ __global__ __launch_bounds__(kBlock) void k_edge_get(
 }
 
 // ---------------------------------------------------------------------------------
+// Persistent edge-GET server (HbmCache::serve_get). One 512-thread workgroup stays
+// resident and polls a ring of jobs in pinned, coherent host memory, so a micro-batch
+// costs no kernel launch (profiles/r2_edge_get_latency.log: a launch + completion round
+// trip is 14-19 us of the proxy's 25-33 us batch).
+// Transport: a job is 64 granules of 16 B, each {payload word, tag = ticket + 1}: five
+// header granules (arena, capacity, offsets array, n | now, host slot) and two per key.
+// Wave 0 polls the whole job with one 16-B load per lane — one PCIe round trip — and
+// takes it when every granule it covers carries the ticket's tag (the host writes each
+// granule with one 16-B store, so a granule is never torn): no separate read of the job
+// after its sequence word.
+// Coherence: other CUs' SET kernels write the index and the log and release them (kernel
+// end, or k_set_small's agent release before its index insert); the server reads both
+// with nontemporal loads, which bypass the CU's L1 (L2-served), so no acquire fence per
+// job. A SET chain still running may overwrite a record while it is being copied: every
+// SET batch first raises the claim word (the furthest log byte its append writes;
+// k_offsets / k_set_small, before the append), the probe treats anything the claim
+// reaches as evicted, and after every copy load of a round has returned the claim is read
+// again: a record it now reaches is stored with a zeroed magic word (a miss at the
+// batcher's header check) — a seqlock. An index entry a concurrent insert has
+// half-written can pair a digest with another key's record: the header check rejects it.
+// Exit: when the host sets the stop word, after `idle` ticks without a job, or after
+// `life` ticks of running (so a device-wide synchronisation elsewhere never waits on it
+// for long); it records the tickets it consumed and its epoch, and serve_kick relaunches
+// it when jobs are outstanding. Per job, lane 0 records five wall-clock stamps (poll
+// issue, job seen, probed, copied, done) for serve_trace().
+// ---------------------------------------------------------------------------------
+constexpr int kSrvBlock = 512;
+constexpr int kSrvGroups = kSrvBlock / 8;
+constexpr int kSrvUnroll = 16;  // 16-B chunks in flight per lane: 128 KiB per round
+constexpr int kSrvGranules = 64;
+constexpr int kSrvHdr = 5;
+static_assert(kSrvHdr + 2 * HbmCache::kServeKeys <= kSrvGranules, "a job is one wave's load");
+
+struct SrvGranule {
+  uint64_t v, tag;
+};
+struct SrvJob {  // one ring slot (1 KiB), host-written
+  SrvGranule g[kSrvGranules];
+};
+constexpr int kCtlConsumed = 0, kCtlExited = 8, kCtlStop = 16;  // words, each on its own line
+// The server exits after this long without a job (the next job relaunches it) and after
+// this long in all (a device-wide synchronisation elsewhere waits at most that long).
+constexpr uint64_t kSrvIdleUs = 500, kSrvLifeUs = 2000;
+constexpr int kSrvTrace = 64;  // jobs whose phase stamps are kept (ring)
+
+__device__ __forceinline__ uint64_t sys_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t agent_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane l8's 16-B quarter of a bucket, read past the CU's L1 (nontemporal: L2-served)
+__device__ __forceinline__ uint4 nt_bucket_quarter(const Entry* index, uint64_t b, int l8) {
+  const u32x4 v = __builtin_nontemporal_load(
+      reinterpret_cast<const u32x4*>(index + b * kEntriesPerBucket) + l8);
+  return uint4{v.x, v.y, v.z, v.w};
+}
+// newest log head any kernel has published or claimed (head slots 0/1, claim word 4)
+__device__ __forceinline__ uint64_t newest_head(const uint64_t* heads) {
+  return max(max(agent_load(heads), agent_load(heads + 1)), agent_load(heads + 4));
+}
+
+__global__ __launch_bounds__(kSrvBlock) void k_edge_server(
+    const SrvJob* __restrict__ ring, uint64_t* __restrict__ ctl, uint64_t* __restrict__ slots,
+    Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ heads, uint64_t cap,
+    const uint8_t* __restrict__ log, CacheCounters* __restrict__ ctr,
+    uint64_t* __restrict__ trace, uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks) {
+  constexpr int K = HbmCache::kServeKeys;
+  __shared__ Digest s_key[K];
+  __shared__ uint64_t s_loc[K];      // physical record offset
+  __shared__ uint64_t s_lg[K];       // logical record start + 1 (0: miss)
+  __shared__ uint64_t s_off[K + 1];
+  __shared__ uint64_t s_job[kSrvHdr];  // out, out_cap, off, n | now << 32, slot
+  __shared__ uint64_t s_head;
+  __shared__ int s_cmd;
+  __shared__ unsigned long long s_cnt[3][kSrvBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = tid >> 3, l8 = tid & 7;
+  uint64_t ticket = sys_load(ctl + kCtlConsumed);
+  const uint64_t t_start = (uint64_t)wall_clock64();
+  uint64_t t_last = t_start, t_poll = 0, t_seen = 0;
+  for (;;) {
+    // ---- wait for the next job: wave 0 reads all of it per poll (one 16-B granule a lane)
+    if (w == 0) {
+      const SrvGranule* jg = ring[ticket % HbmCache::kServeRing].g;
+      const uint64_t want = ticket + 1;
+      int cmd = 1;
+      for (;;) {
+        t_poll = (uint64_t)wall_clock64();
+        const u32x4 gv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(jg + lane));
+        const uint64_t v = pack2(gv.x, gv.y), tag = pack2(gv.z, gv.w);
+        const uint64_t nn = __shfl(v, 3) & 0xffffffffu;     // n, from granule 3
+        const bool hdr_ok = __shfl((int)(tag == want), 3) != 0;
+        const bool mine = lane < kSrvHdr + 2 * (int)(hdr_ok ? min(nn, (uint64_t)K) : 0);
+        if (hdr_ok && __ballot(mine && tag != want) == 0ull) {
+          if (lane < kSrvHdr) s_job[lane] = v;
+          const int kk = (lane - kSrvHdr) >> 1;
+          if (lane >= kSrvHdr && mine) {
+            if (((lane - kSrvHdr) & 1) == 0) s_key[kk].lo = v;
+            else s_key[kk].hi = v;
+          }
+          if (lane == 0) s_head = newest_head(heads);
+          cmd = 0;
+          break;
+        }
+        const uint64_t t = (uint64_t)wall_clock64();
+        const bool quit = lane == 0 && (sys_load(ctl + kCtlStop) || t - t_last > idle_ticks ||
+                                        t - t_start > life_ticks);
+        if (__shfl((int)quit, 0)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      t_seen = (uint64_t)wall_clock64();
+      if (lane == 0) s_cmd = cmd;
+    }
+    __syncthreads();
+    if (s_cmd) break;
+    const int n = (int)(s_job[3] & 0xffffffffu);
+    const uint32_t now = (uint32_t)(s_job[3] >> 32);
+    uint8_t* const out = reinterpret_cast<uint8_t*>(s_job[0]);
+    const uint64_t out_cap = s_job[1];
+    uint64_t* const off_out = reinterpret_cast<uint64_t*>(s_job[2]);
+    const uint64_t head = s_head;
+    // ---- probe: one 8-lane group per key, nontemporal (L2-served) bucket reads
+    unsigned long long ops = 0, hits = 0, bytes = 0;
+    for (int k = g; k - g < n; k += kSrvGroups) {
+      uint64_t hl = 0;
+      uint32_t hv = 0;
+      if (k < n) {
+        const Digest d = s_key[k];
+        int he = 0;
+        uint64_t hb = bucket1(d, mask);
+        group_match(nt_bucket_quarter(index, hb, l8), d, l8, head, cap, now, &hl, &hv, &he);
+        if (hl == 0) {
+          hb = bucket2(d, mask);
+          group_match(nt_bucket_quarter(index, hb, l8), d, l8, head, cap, now, &hl, &hv, &he);
+        }
+        if (hl && l8 == 0) mark_ref(index, hb, he, hv);
+        hv = entry_vlen(hv);
+        if (l8 == 0) {
+          s_lg[k] = hl;
+          s_loc[k] = hl ? (hl - 1) % cap : 0;
+          s_off[k] = hl ? item_bytes(hv) : 0;
+          ++ops;
+          hits += hl ? 1 : 0;
+          bytes += hl ? hv : 0;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- exclusive scan of the sizes (wave 0, two keys per lane: K <= 128)
+    if (w == 0) {
+      const uint64_t a = lane < n ? s_off[lane] : 0;
+      const uint64_t b = lane + 64 < n ? s_off[lane + 64] : 0;
+      uint64_t ia = a, ib = b;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint64_t oa = __shfl_up(ia, dd), ob = __shfl_up(ib, dd);
+        if (lane >= dd) {
+          ia += oa;
+          ib += ob;
+        }
+      }
+      const uint64_t ta = __shfl(ia, 63), tb = __shfl(ib, 63);
+      if (lane < n) s_off[lane] = ia - a;
+      if (lane + 64 < n) s_off[lane + 64] = ta + ib - b;
+      if (lane == 0) s_off[n] = ta + tb;
+    }
+    __syncthreads();
+    const uint64_t t_probed = (uint64_t)wall_clock64();
+    const uint64_t total = s_off[n];
+    for (int k = tid; k <= n; k += kSrvBlock) off_out[k] = s_off[k];
+    // ---- stream the records in rounds of kSrvUnroll chunks per lane: loads, then (all
+    //      loads of the round returned) the claim check, then the stores. Nothing when
+    //      the records outgrow the arena (the caller regathers).
+    const int64_t nch = total <= out_cap ? (int64_t)(total >> 4) : 0;
+    for (int64_t c0 = 0; c0 < nch; c0 += (int64_t)kSrvBlock * kSrvUnroll) {
+      u32x4 v[kSrvUnroll];
+      int rec[kSrvUnroll];
+#pragma unroll
+      for (int u = 0; u < kSrvUnroll; ++u) {
+        const int64_t c = c0 + (int64_t)u * kSrvBlock + tid;
+        rec[u] = -1;
+        if (c < nch) {
+          const uint64_t x = (uint64_t)c << 4;
+          int lo = 0, hi = n - 1;  // the record holding byte x: last k with s_off[k] <= x
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= x) lo = mid;
+            else hi = mid - 1;
+          }
+          v[u] = __builtin_nontemporal_load(
+              reinterpret_cast<const u32x4*>(log + s_loc[lo] + (x - s_off[lo])));
+          rec[u] = lo;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) s_head = newest_head(heads);
+      __syncthreads();
+      const uint64_t c2 = s_head;
+#pragma unroll
+      for (int u = 0; u < kSrvUnroll; ++u) {
+        if (rec[u] < 0) continue;
+        const uint64_t x = (uint64_t)(c0 + (int64_t)u * kSrvBlock + tid) << 4;
+        // a record the claim now reaches may be torn: zero its magic word (miss)
+        if (x - s_off[rec[u]] == 16 && !(c2 <= (s_lg[rec[u]] - 1) + cap))
+          v[u] = u32x4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(out + x) = v[u];
+      }
+    }
+    // ---- completion: every wave drains its stores, then one system-scope publish
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint64_t t_copied = (uint64_t)wall_clock64();
+    if (tid == 0) {
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(slots + s_job[4], total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(ctl + kCtlConsumed, ticket + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      t_last = (uint64_t)wall_clock64();
+      uint64_t* tr = trace + (ticket % kSrvTrace) * 8;
+      tr[0] = ticket;
+      tr[1] = t_poll;
+      tr[2] = t_seen;
+      tr[3] = t_probed;
+      tr[4] = t_copied;
+      tr[5] = t_last;
+      tr[6] = (uint64_t)n;
+      tr[7] = total;
+    }
+    // ---- counters (off the latency path)
+    ops = wave_sum(ops);
+    hits = wave_sum(hits);
+    bytes = wave_sum(bytes);
+    if (lane == 0) {
+      s_cnt[0][w] = ops;
+      s_cnt[1][w] = hits;
+      s_cnt[2][w] = bytes;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+      for (int k = 0; k < kSrvBlock / 64; ++k) {
+        t0 += s_cnt[0][k];
+        t1 += s_cnt[1][k];
+        t2 += s_cnt[2][k];
+      }
+      CacheCounters* c_ = ctr + (ticket & (kCtrShards - 1));
+      if (t0) atomicAdd(&c_->get_ops, t0);
+      if (t1) atomicAdd(&c_->get_hits, t1);
+      if (t2) atomicAdd(&c_->get_bytes, t2);
+    }
+    ++ticket;
+    __syncthreads();  // LDS is reused by the next job
+  }
+  if (tid == 0) {
+    __hip_atomic_store(ctl + kCtlConsumed, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ctl + kCtlExited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // SET
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys,
@@ -1119,6 +1387,95 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
 // Keep this kernel at <= 64 VGPRs (8 waves/SIMD): beside the gather, which holds 3/4 of
 // every SIMD's slots, a 72-VGPR build fits one wave per SIMD instead of two and ran 4x
 // slower (126 vs 31 us per 64K-row batch).
+// One SET row's index insert by its 4-lane group (uniform arguments across the group;
+// `active` false: nothing to insert). Lane 0 writes the claimed entry id to *claim_out
+// when the CAS succeeds (the caller pre-sets ~0u); counts evictions / bytes / rows that
+// lost their bucket pair past the retry budget. k_set_small's copy of k_set_index's
+// loop body (k_set_index keeps its own: sharing this function cost it 12 B/lane of
+// scratch at its 64-VGPR budget).
+__device__ __forceinline__ void index_insert(
+    bool active, const Digest& d, uint64_t myloc, uint32_t myvlen, uint32_t myexp,
+    uint32_t* __restrict__ claim_out,
+    Entry* __restrict__ index, uint64_t mask, uint64_t base, uint64_t head_new, uint64_t cap,
+    uint32_t now, unsigned long long& evicted, unsigned long long& bytes,
+    unsigned long long& lost) {
+  const int l4 = threadIdx.x & 3;
+  const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
+  if (!active) return;  // uniform across the 4-lane group
+  const uint64_t b1 = bucket1(d, mask), b2 = bucket2(d, mask);
+  const uint64_t* q1 = reinterpret_cast<const uint64_t*>(index + b1 * kEntriesPerBucket + l4);
+  const uint64_t* q2 = reinterpret_cast<const uint64_t*>(index + b2 * kEntriesPerBucket + l4);
+  for (int attempt = 0; attempt < 16; ++attempt) {
+    // agent-scope loads: a retry must see other workgroups' CAS results, not stale L1
+    uint64_t w1[4], w2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w1[k] = __hip_atomic_load(q1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w2[k] = __hip_atomic_load(q2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // words: d0, d1, loc, vlen | expire << 32. A digest match whose loc belongs to
+    // this batch, (base, head_new], is another row's claim whose digest words have not
+    // landed yet (dedupe leaves one row per key, so it is never this key's entry):
+    // taking it as our own would CAS that row's claim away and lose its SET.
+    const uint64_t span = head_new - base;  // locs of this batch: (base, head_new]
+    const bool in1 = w1[2] - base - 1 < span;
+    const bool in2 = w2[2] - base - 1 < span;
+    const bool m1 = w1[0] == d.lo && w1[1] == d.hi && !in1;
+    const bool m2 = w2[0] == d.lo && w2[1] == d.hi && !in2;
+    const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
+    const bool v2 = entry_live(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
+    const uint32_t mmask = (uint32_t)((__ballot(m1) >> gbase) & 0xfull) |
+                           ((uint32_t)((__ballot(m2) >> gbase) & 0xfull) << 4);
+    const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
+                           ((uint32_t)((__ballot(v2) >> gbase) & 0xfull) << 4);
+    int target;
+    bool evict = false;
+    if (mmask) {
+      target = __ffs(mmask) - 1;
+    } else {
+      const uint32_t dead = ~lmask & 0xffu;
+      if (dead) {
+        const int live1 = __popc(lmask & 0xfu), live2 = __popc(lmask & 0xf0u);
+        const uint32_t pref = __popc(dead & 0x0fu) >= 2
+                                  ? (dead & 0x0fu)
+                                  : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
+        target = __ffs(pref ? pref : dead) - 1;
+      } else {
+        uint64_t oldest = ~0ull;
+        target = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint64_t le = e < 4 ? __shfl(w1[2], gbase + e) : __shfl(w2[2], gbase + e - 4);
+          if (le < oldest) { oldest = le; target = e; }
+        }
+        evict = true;
+      }
+    }
+    const uint64_t e1 = __shfl(w1[2], gbase + (target & 3));
+    const uint64_t e2 = __shfl(w2[2], gbase + (target & 3));
+    const uint64_t expected = target < 4 ? e1 : e2;
+    Entry* const slot = index + (target < 4 ? b1 : b2) * kEntriesPerBucket + (target & 3);
+    int ok = 0;
+    if (l4 == 0) {
+      const unsigned long long prev = atomicCAS(
+          reinterpret_cast<unsigned long long*>(&slot->loc), (unsigned long long)expected,
+          (unsigned long long)myloc);
+      if (prev == expected) {
+        slot->d0 = d.lo;
+        slot->d1 = d.hi;
+        *reinterpret_cast<uint64_t*>(&slot->vlen) = pack2(myvlen, myexp);
+        *claim_out = (uint32_t)(slot - index);
+        ok = 1;
+        evicted += evict ? 1 : 0;
+        bytes += myvlen;
+      }
+    }
+    ok = __shfl(ok, gbase);
+    if (ok) break;
+    if (attempt == 15 && l4 == 0) ++lost;  // bucket pair contended past the retry budget
+  }
+}
+
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_set_index(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ size,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ vlen,
@@ -1257,6 +1614,176 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     e->d1 = d.hi;
     *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vlen[i], expire ? expire[i] : 0u);
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Small SET batches (the proxy's fills, memcached sets): the whole chain above in ONE
+// workgroup and one launch instead of six — dedupe in an LDS hash table (last writer of
+// a digest wins, as k_set_dedupe), sizes and both scans in LDS, the log claim, the append
+// (records synthesised like k_segcopy<1>), then, behind an agent-scope release, the
+// index insert (index_insert, exactly k_set_index's policy), the fix-up, the CLOCK ring
+// entries and the head publication. Rows: kSmallSetRows at most, one per thread.
+// ---------------------------------------------------------------------------------
+constexpr int kSmallSetRows = kBlock;
+
+__global__ __launch_bounds__(kBlock) void k_set_small(
+    const Digest* __restrict__ keys, const uint8_t* __restrict__ values,
+    const uint64_t* __restrict__ val_off, const uint32_t* __restrict__ vlen,
+    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire, int n,
+    uint32_t max_item, Entry* __restrict__ index, uint64_t mask,
+    const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next,
+    unsigned long long* __restrict__ claim_word, uint64_t cap, uint32_t now,
+    uint8_t* __restrict__ log, uint64_t* __restrict__ ring, uint64_t rmask,
+    const uint64_t* __restrict__ ring_tail, uint64_t* __restrict__ ring_tail_next,
+    uint64_t* __restrict__ head_host, CacheCounters* __restrict__ ctr) {
+  constexpr int kT = 2 * kSmallSetRows;  // dedupe table slots
+  __shared__ unsigned long long s_tk[kT];
+  __shared__ int s_tw[kT];
+  __shared__ uint64_t s_off[kSmallSetRows + 1];
+  __shared__ uint64_t s_src[kSmallSetRows];
+  __shared__ uint32_t s_cnt[kSmallSetRows + 1];
+  __shared__ uint32_t s_claim[kSmallSetRows];
+  __shared__ unsigned long long s_w[2][kBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int k = tid; k < kT; k += kBlock) {
+    s_tk[k] = 0ull;
+    s_tw[k] = -1;
+  }
+  __syncthreads();
+  // ---- dedupe: last writer of a digest (lo word, as k_set_dedupe) wins
+  const bool row = tid < n;
+  const uint32_t vl = row ? vlen[tid] : kSkipVlen;
+  const bool skip = vl == kSkipVlen;
+  Digest d{0, 0};
+  int slot = -1;
+  if (row && !skip) {
+    d = keys[tid];
+    const unsigned long long key = d.lo ? d.lo : 1ull;
+    uint32_t t = (uint32_t)fmix64(key) & (kT - 1);
+    for (int probe = 0; probe < kT; ++probe) {
+      const unsigned long long prev = atomicCAS(&s_tk[t], 0ull, key);
+      if (prev == 0ull || prev == key) {
+        atomicMax(&s_tw[t], tid);
+        slot = (int)t;
+        break;
+      }
+      t = (t + 1) & (kT - 1);
+    }
+  }
+  __syncthreads();
+  const bool win = slot >= 0 && s_tw[slot] == tid && vl <= max_item;
+  const uint64_t sz = win ? item_bytes(vl) : 0;
+  // ---- exclusive scans of the sizes and of the stored-row count (CLOCK ring ordinals)
+  uint64_t inc = sz;
+  uint64_t incc = win ? 1 : 0;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint64_t o = __shfl_up(inc, dd), oc = __shfl_up(incc, dd);
+    if (lane >= dd) {
+      inc += o;
+      incc += oc;
+    }
+  }
+  if (lane == 63) {
+    s_w[0][w] = inc;
+    s_w[1][w] = incc;
+  }
+  __syncthreads();
+  uint64_t pre = 0, prec = 0, tot = 0, totc = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; ++k) {
+    if (k < w) {
+      pre += s_w[0][k];
+      prec += s_w[1][k];
+    }
+    tot += s_w[0][k];
+    totc += s_w[1][k];
+  }
+  const uint64_t my_off = pre + inc - sz;
+  s_off[tid] = my_off;
+  s_cnt[tid] = (uint32_t)(prec + incc - (win ? 1 : 0));
+  s_src[tid] = row && win ? (uint64_t)(uintptr_t)values + val_off[tid] : 0;
+  if (tid == 0) {
+    s_off[kSmallSetRows] = tot;
+    s_cnt[kSmallSetRows] = (uint32_t)totc;
+  }
+  const uint64_t base = *head_ptr;
+  const uint64_t head_new = base + tot;
+  // ---- claim the bytes the append writes (the edge server re-checks against it)
+  if (tid == 0 && tot) {
+    atomicMax(claim_word, (unsigned long long)head_new);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // ---- append: 16-B chunks of the batch's records, header words synthesised
+  const int64_t nch = (int64_t)(tot >> 4);
+  const uint64_t pbase = base % cap;
+  for (int64_t c = tid; c < nch; c += kBlock) {
+    const uint64_t x = (uint64_t)c << 4;
+    int lo = 0, hi = n - 1;  // last row with s_off <= x: the record holding byte x
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= x) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint64_t wofs = x - s_off[lo];
+    const uint64_t p = pbase + s_off[lo];
+    uint8_t* dst = log + (p >= cap ? p - cap : p) + wofs;
+    u32x4 v;
+    if (wofs == 0) {
+      const Digest k = keys[lo];
+      v = u32x4{(uint32_t)k.lo, (uint32_t)(k.lo >> 32), (uint32_t)k.hi, (uint32_t)(k.hi >> 32)};
+    } else if (wofs == 16) {
+      v = u32x4{vlen[lo], flags ? flags[lo] : 0u, expire ? expire[lo] : 0u, kItemMagic};
+    } else {
+      v = *reinterpret_cast<const u32x4*>((uintptr_t)s_src[lo] + (wofs - kItemHeaderBytes));
+    }
+    *reinterpret_cast<u32x4*>(dst) = v;
+  }
+  // ---- release the records before any index entry can point at them
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // ---- index insert, 4 lanes per row
+  unsigned long long evicted = 0, bytes = 0, lost = 0;
+  for (int i0 = 0; i0 < n; i0 += kBlock / 4) {
+    const int i = i0 + (tid >> 2);
+    const bool act = i < n && s_off[i + 1] != s_off[i];
+    if ((tid & 3) == 0 && i < n) s_claim[i] = ~0u;
+    index_insert(act, act ? keys[i] : Digest{0, 0}, base + s_off[i] + 1, act ? vlen[i] : 0u,
+                 act && expire ? expire[i] : 0u, s_claim + (i < n ? i : 0), index, mask, base,
+                 head_new, cap, now, evicted, bytes, lost);
+  }
+  // ---- fix-up (entries a later row of this batch re-claimed), CLOCK ring, head
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (row && win) {
+    const uint32_t c = s_claim[tid];
+    const uint64_t myloc = base + my_off + 1;
+    if (c != ~0u) {
+      Entry* const e = index + c;
+      if (__hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == myloc) {
+        e->d0 = d.lo;
+        e->d1 = d.hi;
+        *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vl, expire ? expire[tid] : 0u);
+      }
+    }
+  }
+  const uint64_t rtail = ring ? *ring_tail : 0;
+  if (ring && row && win) ring[(rtail + s_cnt[tid]) & rmask] = base + my_off;
+  if (tid == 0) {
+    *head_next = head_new;
+    if (ring) *ring_tail_next = rtail + s_cnt[kSmallSetRows];
+    __hip_atomic_store(head_host, head_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  block_count(ctr, (unsigned long long)(row && !skip ? 1 : 0), &CacheCounters::set_ops,
+              (unsigned long long)(row && !skip && !win ? 1 : 0), &CacheCounters::set_dropped);
+  block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes, lost,
+              &CacheCounters::set_dropped);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1746,12 +2273,14 @@ size_t device_scan_tmp_bytes(int64_t n) {
 void launch_offsets(const uint64_t* size, int64_t n, const uint64_t* part, int grid,
                     uint64_t* off, hipStream_t s, uint64_t* host_total = nullptr,
                     int64_t plen_override = 0, const uint64_t* part_cnt = nullptr,
-                    uint64_t* cnt = nullptr) {
+                    uint64_t* cnt = nullptr, const uint64_t* claim_head = nullptr,
+                    uint64_t* claim = nullptr) {
   const int64_t plen = plen_override > 0 ? plen_override : part_len(n, grid);
   const int q = (int)std::max<int64_t>(1, 2048 / std::max<int64_t>(plen, 1));
   const int g2 = (grid + q - 1) / q;
   hipLaunchKernelGGL(k_offsets, dim3(g2), dim3(kBlock), 0, s, size, n, part, grid, plen, q, off,
-                     host_total, part_cnt, cnt);
+                     host_total, part_cnt, cnt, claim_head,
+                     reinterpret_cast<unsigned long long*>(claim));
   HIP_OK(hipGetLastError());
 }
 
@@ -1891,6 +2420,22 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(host_slots_, 0, kHostSlots * sizeof(uint64_t));
+  HIP_OK(hipHostMalloc(&srv_ring_, kServeRing * sizeof(SrvJob),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(srv_ring_, 0, kServeRing * sizeof(SrvJob));
+  HIP_OK(hipHostMalloc(&srv_ctl_, 32 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+  memset(srv_ctl_, 0, 32 * sizeof(uint64_t));
+  HIP_OK(hipHostMalloc(&srv_trace_, kSrvTrace * 8 * sizeof(uint64_t),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(srv_trace_, 0, kSrvTrace * 8 * sizeof(uint64_t));
+  {
+    int khz = 0;
+    HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device));
+    if (khz <= 0) khz = 100000;
+    srv_khz_ = (uint64_t)khz;
+    srv_idle_ticks_ = (uint64_t)khz * kSrvIdleUs / 1000;
+    srv_life_ticks_ = (uint64_t)khz * kSrvLifeUs / 1000;
+  }
   HIP_OK(hipMemset(index_, 0, cfg_.nbuckets * kBucketBytes));
   HIP_OK(hipMemset(head_, 0, 64));
   HIP_OK(hipMemset(ctr_, 0, kCtrShards * sizeof(CacheCounters)));
@@ -1910,7 +2455,15 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
 
 HbmCache::~HbmCache() {
   DeviceGuard g(cfg_.device);
+  try {
+    serve_stop();
+  } catch (...) {
+  }
   (void)hipDeviceSynchronize();
+  if (srv_stream_) (void)hipStreamDestroy(srv_stream_);
+  (void)hipHostFree(srv_ring_);
+  (void)hipHostFree(srv_ctl_);
+  (void)hipHostFree(srv_trace_);
   (void)hipFree(log_);
   (void)hipFree(index_);
   (void)hipFree(head_);
@@ -2136,6 +2689,102 @@ void HbmCache::small_get(const Digest* keys, int64_t n, uint8_t* out, uint64_t o
   HIP_OK(hipGetLastError());
 }
 
+void HbmCache::serve_launch_locked() {
+  DeviceGuard g(cfg_.device);
+  if (!srv_stream_) {
+    // A CU mask gives the stream a hardware queue of its own (masked queues are never
+    // shared), so no other stream's work waits behind the resident server; the mask
+    // itself only keeps the server on the first 64 CUs.
+    const uint32_t mask[2] = {0xffffffffu, 0xffffffffu};
+    HIP_OK(hipExtStreamCreateWithCUMask(&srv_stream_, 2, mask));
+  }
+  __atomic_store_n(srv_ctl_ + kCtlStop, 0ull, __ATOMIC_RELEASE);
+  ++srv_epoch_;
+  SrvJob* ring = nullptr;
+  uint64_t *ctl = nullptr, *slots = nullptr, *trace = nullptr;
+  HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring), srv_ring_, 0));
+  HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctl), srv_ctl_, 0));
+  HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&slots), host_slots_, 0));
+  HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&trace), srv_trace_, 0));
+  hipLaunchKernelGGL(k_edge_server, dim3(1), dim3(kSrvBlock), 0, srv_stream_, ring, ctl, slots,
+                     index_, cfg_.nbuckets - 1, (const uint64_t*)head_, cfg_.log_bytes, log_,
+                     ctr_, trace, srv_epoch_, srv_idle_ticks_, srv_life_ticks_);
+  HIP_OK(hipGetLastError());
+  srv_running_ = true;
+  ++srv_launches_;
+}
+
+bool HbmCache::serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
+                         uint64_t* off, uint32_t now, int done_slot) {
+  if (n < 1 || n > kServeKeys || done_slot < 0 || done_slot >= kHostSlots) return false;
+  TraceRange tr("hbm.serve_get");
+  std::lock_guard<std::mutex> lk(srv_mu_);
+  const uint64_t consumed = __atomic_load_n(srv_ctl_ + kCtlConsumed, __ATOMIC_ACQUIRE);
+  if (srv_ticket_ - consumed >= (uint64_t)kServeRing) return false;  // ring full
+  __atomic_store_n(host_slots_ + done_slot, kSlotPending, __ATOMIC_RELEASE);
+  // every 16-B granule is {value, tag}: the value first, then the tag with a release
+  // store, so a granule read whole by the device never pairs a new tag with an old value
+  SrvGranule* jg = static_cast<SrvJob*>(srv_ring_)[srv_ticket_ % kServeRing].g;
+  const uint64_t tag = srv_ticket_ + 1;
+  auto put = [&](int i, uint64_t v) {
+    jg[i].v = v;
+    __atomic_store_n(&jg[i].tag, tag, __ATOMIC_RELEASE);
+  };
+  for (int64_t k = 0; k < n; ++k) {
+    put(kSrvHdr + 2 * (int)k, host_keys[k].lo);
+    put(kSrvHdr + 2 * (int)k + 1, host_keys[k].hi);
+  }
+  put(0, (uint64_t)(uintptr_t)out);
+  put(1, out_cap);
+  put(2, (uint64_t)(uintptr_t)off);
+  put(4, (uint64_t)done_slot);
+  put(3, (uint64_t)(uint32_t)n | ((uint64_t)now << 32));
+  ++srv_ticket_;
+  if (!srv_running_ ||
+      __atomic_load_n(srv_ctl_ + kCtlExited, __ATOMIC_ACQUIRE) == srv_epoch_)
+    serve_launch_locked();
+  return true;
+}
+
+void HbmCache::serve_kick() {
+  std::lock_guard<std::mutex> lk(srv_mu_);
+  if (srv_running_ && __atomic_load_n(srv_ctl_ + kCtlExited, __ATOMIC_ACQUIRE) != srv_epoch_)
+    return;  // running (or launched and about to start)
+  srv_running_ = false;
+  if (__atomic_load_n(srv_ctl_ + kCtlConsumed, __ATOMIC_ACQUIRE) < srv_ticket_)
+    serve_launch_locked();
+}
+
+std::vector<uint64_t> HbmCache::serve_trace() const {
+  std::vector<uint64_t> out(srv_trace_, srv_trace_ + kSrvTrace * 8);
+  return out;
+}
+
+uint64_t HbmCache::serve_wait(int i, int64_t timeout_ms) {
+  SH_CHECK(i >= 0 && i < kHostSlots, "host slot out of range");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    const uint64_t v = __atomic_load_n(host_slots_ + i, __ATOMIC_ACQUIRE);
+    if (v != kSlotPending) return v;
+    if ((spin & 255) == 255) {
+      serve_kick();
+      const auto el = std::chrono::steady_clock::now() - t0;
+      SH_CHECK(std::chrono::duration_cast<std::chrono::milliseconds>(el).count() < timeout_ms,
+               "timed out waiting for the edge server");
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+void HbmCache::serve_stop() {
+  std::lock_guard<std::mutex> lk(srv_mu_);
+  if (!srv_running_) return;
+  DeviceGuard g(cfg_.device);
+  __atomic_store_n(srv_ctl_ + kCtlStop, 1ull, __ATOMIC_RELEASE);
+  HIP_OK(hipStreamSynchronize(srv_stream_));
+  srv_running_ = false;
+}
+
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
                       hipStream_t s, uint64_t out_cap) {
   TraceRange tr("hbm.gather");
@@ -2177,6 +2826,15 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
                  index_after);
+  } else if (n <= kSmallSetRows && !index_after) {
+    // one launch for the whole chain (the proxy's small SET batches)
+    hipLaunchKernelGGL(k_set_small, dim3(1), dim3(kBlock), 0, s, keys, values, val_off, vlen,
+                       flags, expire, (int)n, cfg_.max_item, index_, cfg_.nbuckets - 1,
+                       cur_head(), next_head(),
+                       reinterpret_cast<unsigned long long*>(claim_ptr()), cfg_.log_bytes, now,
+                       log_, ring_, ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(),
+                       next_ring_tail(), host_slots_ + kHeadSlot, ctr_);
+    HIP_OK(hipGetLastError());
   } else {
     ensure_set_ws(n, s);
     store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
@@ -2211,7 +2869,7 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
                      cfg_.max_item, set_size_, ctr_, part_ + kMaxGrid, part_cnt);
   HIP_OK(hipGetLastError());
   launch_offsets(set_size_, n, part_ + kMaxGrid, sgrid, set_off_, s, nullptr, 0, part_cnt,
-                 ring_ ? set_cnt_ : nullptr);
+                 ring_ ? set_cnt_ : nullptr, cur_head(), claim_ptr());
 }
 
 void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
@@ -2374,6 +3032,7 @@ void HbmCache::save(const std::string& path, const uint64_t user[4], hipStream_t
 }
 
 void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
+  serve_stop();  // the snapshot rewrites the index and the log underneath it
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   FILE* f = std::fopen(path.c_str(), "rb");
@@ -2402,6 +3061,7 @@ void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
   std::fclose(f);
   SH_CHECK(ok, "snapshot truncated: " + path);
   HIP_OK(hipMemcpy(cur_head(), &h.head, 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(claim_ptr(), &h.head, 8, hipMemcpyHostToDevice));
   // the CLOCK ring is not part of a snapshot: the first lap after a restore is FIFO
   HIP_OK(hipMemset(head_ + 2, 0, 2 * sizeof(uint64_t)));
   if (rc_ctl_) {

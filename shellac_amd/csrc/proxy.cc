@@ -246,7 +246,8 @@ class Reactor : public Executor {
   std::atomic<uint64_t> requests{0}, hits{0}, misses{0}, upstream_reqs{0}, responses{0},
       bytes_out{0}, errors{0}, clients{0}, upstreams{0}, accepts{0}, gc_closed{0},
       cache_sets{0}, bad_requests{0}, upstream_failures{0}, retries{0}, collapsed{0},
-      streamed{0}, stream_pauses{0}, gzip_gpu_bodies{0}, identity_decoded{0}, vary_stored{0},
+      streamed{0}, stream_pauses{0}, gzip_gpu_bodies{0}, gzip_gpu_inflated{0}, identity_decoded{0},
+      vary_stored{0},
       vary_hits{0};
   // event-loop health: the longest iteration (events handled between two epoll_waits)
   // and how many took over 10 ms — a reactor that stalls stops accepting connections
@@ -664,6 +665,38 @@ static Bytes with_connection_close(const Bytes& obj) {
 // goes to a client without `Accept-Encoding: gzip` as its identity variant.
 void Reactor::deliver(Client* c, Slot* s, Bytes obj) {
   if (obj && !s->client_gzip && !s->head && cfg_.policy == "rfc" && object_is_gzip(obj->view())) {
+    if (px_->gzip_ && px_->gzip_->can_inflate()) {
+      // the GPU gzip service inflates it in a batch (zlib on its thread as the fallback);
+      // the slot completes on this reactor when it returns, if the client is still there
+      auto rp = std::make_shared<HttpParser>(false);
+      rp->parse(obj->data(), obj->size());
+      if (rp->message_complete() || rp->finish()) {
+        std::string member = std::move(rp->mutable_body());
+        const uint64_t cid = c->id, seq = s->seq;
+        px_->gzip_->submit_inflate(
+            std::move(member), cfg_.max_inflate_bytes,
+            [this, rp, cid, seq](bool ok, std::string out) {
+              post([this, rp, cid, seq, ok, out = std::move(out)]() mutable {
+                Client* c2 = find_client(cid);
+                Slot* s2 = c2 ? find_slot(c2, seq) : nullptr;
+                if (!s2 || s2->ready) return;
+                if (!ok) {
+                  errors++;
+                  complete_slot(c2, s2, std::make_shared<const std::string>(simple_response(
+                                            502, "Bad Gateway", cfg_.server_name,
+                                            "undecodable gzip object\n")));
+                  return;
+                }
+                rp->remove_header("content-encoding");
+                rp->mutable_body() = std::move(out);
+                identity_decoded++;
+                gzip_gpu_inflated++;
+                complete_slot(c2, s2, std::make_shared<const std::string>(rp->serialize()));
+              });
+            });
+        return;
+      }
+    }
     Bytes id = identity_variant(obj, cfg_.max_inflate_bytes);
     if (!id) {
       errors++;
@@ -1470,11 +1503,14 @@ std::string Proxy::stats_json() {
     << ",\"latency_us\":{\"p50\":" << pct(0.5) << ",\"p99\":" << pct(0.99) << ",\"samples\":"
     << total << "}";
   if (gzip_) {
-    uint64_t gb = 0;
-    for (auto& r : reactors_) gb += r->gzip_gpu_bodies;
+    uint64_t gb = 0, gi = 0;
+    for (auto& r : reactors_) {
+      gb += r->gzip_gpu_bodies;
+      gi += r->gzip_gpu_inflated;
+    }
     StatList gs;
     gzip_->stats(&gs);
-    o << ",\"gzip_gpu\":{\"completed\":" << gb;
+    o << ",\"gzip_gpu\":{\"completed\":" << gb << ",\"identity_served\":" << gi;
     for (const auto& kv : gs) o << ",\"" << kv.first << "\":" << kv.second;
     o << "}";
   }

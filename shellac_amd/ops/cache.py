@@ -379,6 +379,26 @@ class CacheShard:
                              self.now() if now is None else now, self._s(), int(done_slot))
         return out, off
 
+    def serve_get(self, keys: torch.Tensor, out_cap: int = 16 << 20,
+                  now: Optional[int] = None, done_slot: int = 5, timeout_ms: int = 10000):
+        """The same edge GET answered by the resident edge-server kernel (no launch):
+        ``keys`` are host digests; returns (out bytes, off[n+1]) once the server has
+        published the job's total into ``done_slot``. None when the job could not be
+        queued (ring full, n > SERVE_KEYS). Records a concurrent SET overwrote while
+        they were copied come back with a zeroed magic word (treat as misses)."""
+        assert self.is_gpu
+        keys = keys.to("cpu").contiguous()
+        n = keys.shape[0]
+        out = torch.zeros(max(int(out_cap), 16), dtype=torch.uint8, device=self.device)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)  # the server is on no stream: buffers first
+        if not self._impl.serve_get(keys.data_ptr(), n, out.data_ptr(), int(out_cap),
+                                    off.data_ptr(), self.now() if now is None else now,
+                                    int(done_slot)):
+            return None
+        self._impl.serve_wait(int(done_slot), int(timeout_ms))
+        return out, off
+
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
                total: Optional[int] = None, out_cap: Optional[int] = None) -> torch.Tensor:
         """Copy hits into ``out`` (allocated from off[n] if not given: one sync).

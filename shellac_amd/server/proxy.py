@@ -53,7 +53,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  retry_s: int = 2, l1_mb: int = 0, promote_ttl: int = 60,
                  fault: Optional[str] = None,
                  sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
-                 depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000):
+                 depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000,
+                 edge_server: bool = True, batcher_cpus: Sequence[int] = ()):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -67,6 +68,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
     ``depth`` is how many batches each GPU keeps in flight; ``evict`` is the log policy
     (``clock``: read objects get a second chance, memcached-LRU-like; ``fifo``); a GPU
     whose batch fails or stalls past ``batch_timeout_ms`` is ejected for ``retry_s``.
+    ``edge_server`` sends small GET batches to each GPU's resident edge-server kernel
+    (no launch per batch); ``batcher_cpus`` pins the GPU batcher threads.
     ``fault="gpu_down=K"`` ejects GPU shard K as a drill.
     """
     c = core()
@@ -79,13 +82,15 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              max_item=max_item, batch_us=batch_us, retry_s=retry_s, l1_mb=l1_mb,
                              promote_ttl=promote_ttl, sweep_s=sweep_s, hbm_filter=hbm_filter,
                              spin_us=spin_us, depth=depth, evict=evict,
-                             batch_timeout_ms=batch_timeout_ms)
+                             batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
+                             batcher_cpus=batcher_cpus)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
                           batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s,
                           hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
-                          batch_timeout_ms=batch_timeout_ms)
+                          batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
+                          batcher_cpus=batcher_cpus)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -101,7 +106,9 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
             nb *= 2
         return c.hbm_backend(devs, log_bytes, nb, max_item, batch_us, sweep_interval_s=sweep_s,
                              spin_us=spin_us, presence_filter=hbm_filter, depth=depth,
-                             evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms)
+                             evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms,
+                             edge_server=edge_server,
+                             batcher_cpus=[int(x) for x in batcher_cpus])
     raise ValueError(f"unknown cache backend {kind!r}")
 
 
@@ -253,6 +260,11 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--evict", choices=["clock", "fifo"], default="clock",
                    help="HBM log eviction: clock (read objects get a second chance, "
                         "memcached-LRU-like; default) or fifo")
+    p.add_argument("--no-edge-server", action="store_true",
+                   help="--cache hbm: launch a kernel per GET batch instead of feeding the "
+                        "resident edge-server kernel")
+    p.add_argument("--batcher-cpus", default="",
+                   help="--cache hbm: pin the GPU batcher threads to these CPUs")
     p.add_argument("--stream-bytes", type=int, default=1 << 20,
                    help="stream responses larger than this to the client without caching them")
     p.add_argument("--decode-gzip", action="store_true",
@@ -286,7 +298,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  **({"dram_mb": args.dram_mb} if kind == "dram" else {}),
                  **({"gpus": gpus, "hbm_gb": args.hbm_gb, "batch_us": args.batch_us,
                      "hbm_filter": not args.no_hbm_filter, "spin_us": args.hbm_spin_us,
-                     "depth": args.hbm_depth, "evict": args.evict}
+                     "depth": args.hbm_depth, "evict": args.evict,
+                     "edge_server": not args.no_edge_server,
+                     "batcher_cpus": parse_cpus(args.batcher_cpus)}
                     if kind == "hbm" else {}),
                  **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))
     print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)

@@ -105,6 +105,38 @@ def test_proxy_compresses_misses_on_the_gpu(cuda_dev):
         o.stop()
 
 
+def test_proxy_identity_variants_inflate_on_the_gpu(cuda_dev):
+    """Under --policy rfc a client without Accept-Encoding: gzip gets the identity variant
+    of a gzip-coded cached object; with --gzip-gpu the proxy's GPU service inflates those
+    in batches (zlib on the service thread only for members the GPU path rejects), and the
+    bytes match what the gzip client's response decodes to."""
+    from shellac_amd.server.proxy import Server
+    from shellac_amd.utils.httpclient import HttpClient
+    from shellac_amd.utils.origin import Origin
+
+    o = Origin(body_bytes=9000).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend_kind="dram", dram_mb=64,
+                    compress=True, gzip_gpu=cuda_dev.index or 0, threads=2).start() as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/zid/{i}.html" for i in range(16)] + [f"/gz/zid{i}" for i in range(4)]
+            gz_bodies = [r.body().read() for r in
+                         c.pipeline(paths, headers={"Accept-Encoding": "gzip"})]
+            rs = c.pipeline(paths)  # no Accept-Encoding: identity variants, from the cache
+            for p, r, want in zip(paths, rs, gz_bodies):
+                assert r.status() == 200, p
+                assert "content-encoding" not in r.headers(), p
+                assert r.body().read() == want, p
+            st = px.stats()
+            assert st["identity_decoded"] == len(paths)
+            assert st["gzip_gpu"]["identity_served"] == len(paths)
+            assert st["gzip_gpu"]["inflated_gpu"] + st["gzip_gpu"]["inflated_cpu"] == len(paths)
+            assert st["gzip_gpu"]["inflated_gpu"] >= 16 and st["gzip_gpu"]["inflate_errors"] == 0
+            assert all(o.hits[p] == 1 for p in paths)
+    finally:
+        o.stop()
+
+
 def test_gpu_inflate_matches_zlib(gz):
     """Batched GPU gunzip (one wave per member) against zlib-made members of every block
     type: stored (incompressible), fixed (tiny) and dynamic Huffman, multi-block, empty,

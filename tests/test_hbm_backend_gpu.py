@@ -40,6 +40,34 @@ def test_hbm_backend_roundtrip(hbm):
     assert st["hbm_gpus"] == 1 and st["hbm_batches"] >= 1
 
 
+@pytest.mark.parametrize("edge_server", [True, False])
+def test_hbm_backend_edge_server_paths(edge_server):
+    """Small GET batches go to the resident edge-server kernel (no launch per batch) and
+    return the same objects as the launched path; overwrites and deletes are seen by the
+    next GET once they completed, and batches with a write of one of their keys still in
+    flight fall back to the ordered stream path."""
+    be = make_backend("hbm", gpus=[0], hbm_gb=0.25, edge_server=edge_server)
+    keys = [b"/es/%d" % i for i in range(64)]
+    for i, k in enumerate(keys):
+        be.set(k, b"v%d-" % i * 100, i, 0)
+    assert _wait_get(be, keys[-1]) is not None
+    for rep in range(3):
+        for i, k in enumerate(keys):
+            assert be.get(k) == (b"v%d-" % i * 100, i)
+    be.set(keys[0], b"new" * 50, 7, 0)
+    deadline = time.time() + 3
+    while be.get(keys[0]) != (b"new" * 50, 7) and time.time() < deadline:
+        time.sleep(0.001)
+    assert be.get(keys[0]) == (b"new" * 50, 7)
+    assert be.delete(keys[1]) is True
+    assert be.get(keys[1]) is None
+    st = be.stats()
+    if edge_server:
+        assert st["hbm_served_batches"] > 0 and st["hbm_server_launches"] >= 1
+    else:
+        assert st["hbm_served_batches"] == 0 and st["hbm_server_launches"] == 0
+
+
 def test_hbm_cache_node_over_memcached_protocol(hbm):
     with CacheNode(backend=hbm, port=0, threads=2) as node:
         c = MemcacheClient(port=node.port)

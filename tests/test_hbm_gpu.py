@@ -101,6 +101,39 @@ def test_ttl_delete_sweep(cuda_dev):
     assert g.sweep(now=54) == h.sweep(now=54)
 
 
+@pytest.mark.parametrize("evict", ["clock", "fifo"])
+def test_small_set_kernel_matches_host_engine(cuda_dev, evict):
+    """SET batches of <= 256 rows run as one fused kernel (k_set_small); batches above
+    run the launched chain. Over a log that wraps many times — duplicates, skip rows,
+    values above max_item, TTLs, CLOCK reinsertions fed by the ring entries the fused
+    kernel appends — both engines end with the same head, records and counters."""
+    from shellac_amd.models.sharded_cache import SKIP_VLEN
+
+    g = CacheShard(1 << 21, 1 << 10, 1 << 11, cuda_dev, evict=evict)
+    h = CacheShard(1 << 21, 1 << 10, 1 << 11, "cpu", evict=evict)
+    rng = np.random.default_rng(7)
+    allkeys = [f"/ss/{i}".encode() for i in range(3000)]
+    for b in range(60):
+        n = int(rng.choice([1, 5, 64, 255, 256, 257, 600]))
+        ks = [allkeys[j] for j in rng.integers(0, 3000, size=n)]
+        vs = [rng.integers(0, 256, size=int(rng.integers(0, 2600)), dtype=np.uint8).tobytes()
+              for _ in ks]  # some above max_item (2 KiB): dropped
+        d, v, vo, vl = _batch(ks, vs, cuda_dev)
+        vl[::9] = SKIP_VLEN
+        ex = torch.tensor([0 if i % 4 else 30 + i % 5 for i in range(n)], dtype=torch.int32)
+        for s, dv in ((g, cuda_dev), (h, "cpu")):
+            s.store(d.to(dv), v.to(dv), vo.to(dv), vl.to(dv), expire=ex.to(dv), now=20 + b // 8)
+        if b % 5 == 4:  # reads set CLOCK bits: later hands reinsert those items
+            _get_both(g, h, allkeys[:1500:3], 20 + b // 8)
+    assert g.head() == h.head() and g.head() > (4 << 20)  # the log wrapped twice
+    for now in (25, 40):
+        rg, rh, sg, sh = _get_both(g, h, allkeys, now)
+        assert torch.equal(sg, sh) and rg == rh
+    cg, ch = g.counters(), h.counters()
+    for k in ("set_ops", "set_bytes", "set_dropped", "set_evicted", "reinserted"):
+        assert cg[k] == ch[k], k
+
+
 def test_bucket_overflow_eviction_invariants(cuda_dev):
     g = CacheShard(1 << 20, 2, 64, cuda_dev)  # 8 slots total
     keys = [f"/o/{i}".encode() for i in range(20)]
@@ -453,6 +486,66 @@ def test_small_get_completion_slot(cuda_dev, n):
             assert (g is None) == (i >= 2500)
             if g is not None:
                 assert g[0] == vals[i]
+
+
+@pytest.mark.parametrize("n", [1, 7, 16, 29])
+def test_serve_get_matches_small_get(cuda_dev, n):
+    """The resident edge server answers a job with exactly the launched edge GET's bytes
+    and offsets (misses and duplicates included, records over several copy rounds), reports the full
+    size without writing when the buffer is too small, and rejects batches above
+    SERVE_KEYS so the caller falls back to a launch."""
+    from shellac_amd._native import core
+
+    shard = CacheShard(64 << 20, 1 << 14, 1 << 14, cuda_dev)
+    keys = [f"/srv/{i}".encode() for i in range(3000)]
+    vals = [bytes([i % 251]) * (i * 13 % 3000) for i in range(3000)]
+    shard.set_many(keys[:2000], vals[:2000])
+    torch.cuda.synchronize()
+    for rep in range(3):  # jobs back to back on the same resident kernel
+        req = digest_strings([keys[(i * 7 + rep) % 3000] for i in range(n)], "cpu")
+        out, off = shard.small_get(req.to(cuda_dev), out_cap=8 << 20)
+        torch.cuda.synchronize()
+        got = shard.serve_get(req, out_cap=8 << 20)
+        assert got is not None
+        out2, off2 = got
+        assert torch.equal(off2.cpu(), off.cpu())
+        total = int(off[-1])
+        assert torch.equal(out2[:total].cpu(), out[:total].cpu())
+    if total > 64:
+        out3, off3 = shard.serve_get(req, out_cap=total - 16)
+        assert int(off3[-1]) == total and int(out3.count_nonzero()) == 0
+    big = digest_strings(keys[:int(core().SERVE_KEYS) + 1], "cpu")
+    assert shard.serve_get(big) is None
+
+
+def test_serve_get_relaunches_and_sees_new_sets(cuda_dev):
+    """The server exits when idle and the next job relaunches it; a SET chain that ran
+    while it was resident (other CUs, no stream order with it) is visible to its next job
+    (the per-job acquire), and keys the SET's log append overwrote miss."""
+    import time
+
+    shard = CacheShard(1 << 20, 1 << 12, 1 << 14, cuda_dev, evict="fifo")  # wraps quickly
+    first = [f"/srv2/a{i}".encode() for i in range(29)]
+    shard.set_many(first, [b"a" * 3000] * 29)
+    torch.cuda.synchronize()
+    req = digest_strings(first, "cpu")
+    out, off = shard.serve_get(req)
+    assert all(r is not None for r in unpack_records(out, off[:-1], off[1:] - off[:-1]))
+    l0 = shard._impl.serve_launches
+    time.sleep(0.05)  # past the idle timeout
+    out, off = shard.serve_get(req)
+    assert shard._impl.serve_launches == l0 + 1
+    # overwrite the whole log with new keys while the server may still be resident
+    newer = [f"/srv2/b{i}".encode() for i in range(400)]
+    for k in range(0, 400, 100):  # each SET batch within half the log
+        shard.set_many(newer[k:k + 100], [b"b" * 3000] * 100)
+    torch.cuda.synchronize()
+    out, off = shard.serve_get(req)
+    assert all(r is None for r in unpack_records(out, off[:-1], off[1:] - off[:-1]))
+    tail = digest_strings(newer[-29:], "cpu")
+    out, off = shard.serve_get(tail)
+    got = unpack_records(out, off[:-1], off[1:] - off[:-1])
+    assert all(r is not None and r[0] == b"b" * 3000 for r in got)
 
 
 def test_store_graph_matches_store(cuda_dev):
