@@ -205,6 +205,7 @@ struct HbmBackend::Dev {
   // warm restore over xGMI: a stream for peer work on this GPU and the digest ring on
   // the device (route_keys)
   hipStream_t mstream = nullptr;
+  hipStream_t sstream = nullptr;  // stats reads (non-blocking: never waits on other streams)
   uint32_t* d_pts = nullptr;
   int32_t* d_own = nullptr;
   int npts = 0;
@@ -255,6 +256,7 @@ struct HbmBackend::Dev {
     cache.reset();
     if (stream) (void)hipStreamDestroy(stream);
     if (mstream) (void)hipStreamDestroy(mstream);
+    if (sstream) (void)hipStreamDestroy(sstream);
     (void)hipFree(d_pts);
     (void)hipFree(d_own);
   }
@@ -283,6 +285,7 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     d->cache = std::make_unique<HbmCache>(sc);
     HB_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HB_OK(hipStreamCreateWithFlags(&d->mstream, hipStreamNonBlocking));
+    HB_OK(hipStreamCreateWithFlags(&d->sstream, hipStreamNonBlocking));
     {
       const auto& pts = ring_.points();
       std::vector<uint32_t> hp(pts.size());
@@ -1209,8 +1212,9 @@ void HbmBackend::stats(StatList* out) {
   };
   for (auto& d : devs_) {
     (void)hipSetDevice(d->device);
-    // a separate stream: the batcher's may be busy; counters are advisory
-    const CacheCounters c = d->cache->counters(nullptr);
+    // a stream of its own, non-blocking: the batcher's may be busy, and the legacy null
+    // stream would also wait for the resident edge server; counters are advisory
+    const CacheCounters c = d->cache->counters(d->sstream);
     t.get_ops += c.get_ops; t.get_hits += c.get_hits; t.set_ops += c.set_ops;
     t.set_bytes += c.set_bytes; t.set_evicted += c.set_evicted; t.del_ops += c.del_ops;
     t.reinserted += c.reinserted; t.reinsert_bytes += c.reinsert_bytes;

@@ -121,7 +121,7 @@ class HbmCache {
   uint64_t serve_launches() const { return srv_launches_; }
   uint64_t serve_jobs() const { return srv_ticket_; }
   // Phase stamps of the last (up to 64) server jobs, wall-clock ticks of the device:
-  // rows of {ticket, poll issued, job seen, probed, copied, done, n, total bytes}; and the
+  // rows of {ticket, poll issued, job seen, probed, copied, publish, n, total bytes}; and the
   // tick rate (kHz).
   std::vector<uint64_t> serve_trace() const;
   uint64_t wall_khz() const { return srv_khz_; }

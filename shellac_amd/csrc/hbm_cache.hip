@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_get(
 // `life` ticks of running (so a device-wide synchronisation elsewhere never waits on it
 // for long); it records the tickets it consumed and its epoch, and serve_kick relaunches
 // it when jobs are outstanding. Per job, lane 0 records five wall-clock stamps (poll
-// issue, job seen, probed, copied, done) for serve_trace().
+// issue, job seen, probed, copied, publish) for serve_trace().
 // ---------------------------------------------------------------------------------
 constexpr int kSrvBlock = 512;
 constexpr int kSrvGroups = kSrvBlock / 8;
@@ -1103,9 +1103,20 @@ struct SrvJob {  // one ring slot (1 KiB), host-written
 constexpr int kCtlConsumed = 0, kCtlExited = 8, kCtlStop = 16;  // words, each on its own line
 // The server exits after this long without a job (the next job relaunches it) and after
 // this long in all (a device-wide synchronisation elsewhere waits at most that long).
-constexpr uint64_t kSrvIdleUs = 500, kSrvLifeUs = 2000;
+constexpr uint64_t kSrvIdleUs = 1000, kSrvLifeUs = 10000;
 constexpr int kSrvTrace = 64;  // jobs whose phase stamps are kept (ring)
 
+// 16-B system-coherent load (sc0 sc1: past every GPU cache) of host memory the host
+// rewrites: a plain or nontemporal load of it can be served stale from a cache, and a
+// poll that misses a job then waits for the server's idle exit (measured: ~0.5 ms a job)
+__device__ __forceinline__ u32x4 sys_load16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v)
+               : "v"(p)
+               : "memory");
+  return v;
+}
 __device__ __forceinline__ uint64_t sys_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1149,7 +1160,7 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
       int cmd = 1;
       for (;;) {
         t_poll = (uint64_t)wall_clock64();
-        const u32x4 gv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(jg + lane));
+        const u32x4 gv = sys_load16(jg + lane);
         const uint64_t v = pack2(gv.x, gv.y), tag = pack2(gv.z, gv.w);
         const uint64_t nn = __shfl(v, 3) & 0xffffffffu;     // n, from granule 3
         const bool hdr_ok = __shfl((int)(tag == want), 3) != 0;
@@ -1275,21 +1286,22 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     __syncthreads();
     const uint64_t t_copied = (uint64_t)wall_clock64();
     if (tid == 0) {
-      __threadfence_system();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(slots + s_job[4], total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(ctl + kCtlConsumed, ticket + 1, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      t_last = (uint64_t)wall_clock64();
+      // the job's phase stamps first, so they are in place when the host sees the slot
       uint64_t* tr = trace + (ticket % kSrvTrace) * 8;
       tr[0] = ticket;
       tr[1] = t_poll;
       tr[2] = t_seen;
       tr[3] = t_probed;
       tr[4] = t_copied;
-      tr[5] = t_last;
+      tr[5] = (uint64_t)wall_clock64();
       tr[6] = (uint64_t)n;
       tr[7] = total;
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(slots + s_job[4], total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(ctl + kCtlConsumed, ticket + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      t_last = (uint64_t)wall_clock64();
     }
     // ---- counters (off the latency path)
     ops = wave_sum(ops);
