@@ -115,6 +115,11 @@ class HbmCache {
   bool serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
                  uint64_t* off, uint32_t now, int done_slot);
   void serve_kick();
+  // no server job outstanding (the resident workgroup takes jobs one at a time: a caller
+  // with several batches in flight sends the others down the launched path)
+  bool serve_idle() const {
+    return __atomic_load_n(srv_ctl_, __ATOMIC_ACQUIRE) >= srv_ticket_;
+  }
   // wait_host_slot for a serve_get job: spins, relaunching the server when it exited
   uint64_t serve_wait(int done_slot, int64_t timeout_ms = 10000);
   void serve_stop();  // ask the server to exit and wait for it (outstanding jobs stay queued)

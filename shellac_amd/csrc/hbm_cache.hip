@@ -1637,6 +1637,7 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
 // entries and the head publication. Rows: kSmallSetRows at most, one per thread.
 // ---------------------------------------------------------------------------------
 constexpr int kSmallSetRows = kBlock;
+constexpr int kSetSmallU = 16;  // 16-B chunks in flight per lane in the append
 
 __global__ __launch_bounds__(kBlock) void k_set_small(
     const Digest* __restrict__ keys, const uint8_t* __restrict__ values,
@@ -1655,6 +1656,9 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
   __shared__ uint64_t s_src[kSmallSetRows];
   __shared__ uint32_t s_cnt[kSmallSetRows + 1];
   __shared__ uint32_t s_claim[kSmallSetRows];
+  __shared__ Digest s_key[kSmallSetRows];
+  __shared__ uint32_t s_vl[kSmallSetRows];
+  __shared__ uint32_t s_ex[kSmallSetRows];
   __shared__ unsigned long long s_w[2][kBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int k = tid; k < kT; k += kBlock) {
@@ -1668,8 +1672,11 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
   const bool skip = vl == kSkipVlen;
   Digest d{0, 0};
   int slot = -1;
+  s_vl[tid] = vl;
+  s_ex[tid] = row && expire ? expire[tid] : 0u;
   if (row && !skip) {
     d = keys[tid];
+    s_key[tid] = d;
     const unsigned long long key = d.lo ? d.lo : 1ull;
     uint32_t t = (uint32_t)fmix64(key) & (kT - 1);
     for (int probe = 0; probe < kT; ++probe) {
@@ -1727,30 +1734,44 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  // ---- append: 16-B chunks of the batch's records, header words synthesised
+  // ---- append: 16-B chunks of the batch's records, header words synthesised. The values
+  //      are often in mapped host memory (the proxy's zero-copy staging): kSetSmallU loads
+  //      in flight per lane, issued before their stores, so one workgroup is not bound by
+  //      one PCIe round trip per chunk.
   const int64_t nch = (int64_t)(tot >> 4);
   const uint64_t pbase = base % cap;
-  for (int64_t c = tid; c < nch; c += kBlock) {
-    const uint64_t x = (uint64_t)c << 4;
-    int lo = 0, hi = n - 1;  // last row with s_off <= x: the record holding byte x
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= x) lo = mid;
-      else hi = mid - 1;
+  for (int64_t c0 = 0; c0 < nch; c0 += (int64_t)kBlock * kSetSmallU) {
+    u32x4 v[kSetSmallU];
+    uint8_t* dst[kSetSmallU];
+#pragma unroll
+    for (int u = 0; u < kSetSmallU; ++u) {
+      const int64_t c = c0 + (int64_t)u * kBlock + tid;
+      dst[u] = nullptr;
+      if (c >= nch) continue;
+      const uint64_t x = (uint64_t)c << 4;
+      int lo = 0, hi = n - 1;  // last row with s_off <= x: the record holding byte x
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= x) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t wofs = x - s_off[lo];
+      const uint64_t p = pbase + s_off[lo];
+      dst[u] = log + (p >= cap ? p - cap : p) + wofs;
+      if (wofs == 0) {
+        const Digest k = s_key[lo];
+        v[u] = u32x4{(uint32_t)k.lo, (uint32_t)(k.lo >> 32), (uint32_t)k.hi,
+                     (uint32_t)(k.hi >> 32)};
+      } else if (wofs == 16) {
+        v[u] = u32x4{s_vl[lo], flags ? flags[lo] : 0u, s_ex[lo], kItemMagic};
+      } else {
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+            (uintptr_t)s_src[lo] + (wofs - kItemHeaderBytes)));
+      }
     }
-    const uint64_t wofs = x - s_off[lo];
-    const uint64_t p = pbase + s_off[lo];
-    uint8_t* dst = log + (p >= cap ? p - cap : p) + wofs;
-    u32x4 v;
-    if (wofs == 0) {
-      const Digest k = keys[lo];
-      v = u32x4{(uint32_t)k.lo, (uint32_t)(k.lo >> 32), (uint32_t)k.hi, (uint32_t)(k.hi >> 32)};
-    } else if (wofs == 16) {
-      v = u32x4{vlen[lo], flags ? flags[lo] : 0u, expire ? expire[lo] : 0u, kItemMagic};
-    } else {
-      v = *reinterpret_cast<const u32x4*>((uintptr_t)s_src[lo] + (wofs - kItemHeaderBytes));
-    }
-    *reinterpret_cast<u32x4*>(dst) = v;
+#pragma unroll
+    for (int u = 0; u < kSetSmallU; ++u)
+      if (dst[u]) *reinterpret_cast<u32x4*>(dst[u]) = v[u];
   }
   // ---- release the records before any index entry can point at them
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1766,9 +1787,9 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
     const int i = i0 + (tid >> 2);
     const bool act = i < n && s_off[i + 1] != s_off[i];
     if ((tid & 3) == 0 && i < n) s_claim[i] = ~0u;
-    index_insert(act, act ? keys[i] : Digest{0, 0}, base + s_off[i] + 1, act ? vlen[i] : 0u,
-                 act && expire ? expire[i] : 0u, s_claim + (i < n ? i : 0), index, mask, base,
-                 head_new, cap, now, evicted, bytes, lost);
+    index_insert(act, act ? s_key[i] : Digest{0, 0}, base + s_off[i] + 1, act ? s_vl[i] : 0u,
+                 act ? s_ex[i] : 0u, s_claim + (i < n ? i : 0), index, mask, base, head_new,
+                 cap, now, evicted, bytes, lost);
   }
   // ---- fix-up (entries a later row of this batch re-claimed), CLOCK ring, head
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1781,7 +1802,7 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
       if (__hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == myloc) {
         e->d0 = d.lo;
         e->d1 = d.hi;
-        *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vl, expire ? expire[tid] : 0u);
+        *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vl, s_ex[tid]);
       }
     }
   }

@@ -41,6 +41,27 @@ __device__ __forceinline__ int ring_owner_of(const Digest& k, const uint32_t* __
   return own[lo == npts ? 0 : lo];
 }
 
+// The ring (points + owners) staged in LDS for a kernel's binary searches: a search over
+// global memory is ~11 dependent L2 round trips per key (k_route_hist took 27 us for 1M
+// keys, most of it waiting). Rings of up to kRingLds points (25 shards x 160) fit;
+// bigger ones are searched in place. Every thread of the workgroup must call it.
+constexpr int kRingLds = 4096;
+struct RingView {
+  const uint32_t* pts;
+  const int32_t* own;
+};
+__device__ __forceinline__ RingView stage_ring(const uint32_t* __restrict__ pts,
+                                               const int32_t* __restrict__ own, int npts,
+                                               uint32_t* s_pts, int32_t* s_own) {
+  if (npts > kRingLds) return RingView{pts, own};
+  for (int k = threadIdx.x; k < npts; k += blockDim.x) {
+    s_pts[k] = pts[k];
+    s_own[k] = own[k];
+  }
+  __syncthreads();
+  return RingView{s_pts, s_own};
+}
+
 // Membership in the hot set, sorted by the signed low word (torch's sort of column 0).
 // `dir` (optional, 65537 entries) narrows the search to the keys sharing the top 16
 // bits of the order-preserving unsigned image of lo, ~nhot/65536 of them.
@@ -193,14 +214,17 @@ __global__ __launch_bounds__(kB) void k_route_hist(const Digest* __restrict__ ke
                                                    unsigned long long* __restrict__ ndup) {
   extern __shared__ uint32_t s_c[];
   __shared__ unsigned int s_dup;
+  __shared__ uint32_t s_pts[kRingLds];
+  __shared__ int32_t s_own[kRingLds];
   const int nb = w + 1;
   for (int d = threadIdx.x; d < nb; d += kB) s_c[d] = 0;
   if (threadIdx.x == 0) s_dup = 0;
+  const RingView rv = stage_ring(pts, own, npts, s_pts, s_own);  // (barrier inside)
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(n, i0 + plen);
   for (int64_t i = i0 + threadIdx.x; i < i1; i += kB) {
     const bool dup = first && first[i] != (uint32_t)i;
-    const int d = (dup || (rsize && rsize[i] > 0)) ? w : ring_owner_of(keys[i], pts, own, npts);
+    const int d = (dup || (rsize && rsize[i] > 0)) ? w : ring_owner_of(keys[i], rv.pts, rv.own, npts);
     dest[i] = d;
     atomicAdd(&s_c[d], 1u);
     if (dup) atomicAdd(&s_dup, 1u);
@@ -222,12 +246,15 @@ __global__ __launch_bounds__(kB) void k_ps_dest_hist(
     int32_t nb, int64_t plen, int32_t w, int32_t* __restrict__ owner,
     uint32_t* __restrict__ vpad, uint64_t* __restrict__ tcnt, uint64_t* __restrict__ tbytes) {
   extern __shared__ unsigned long long s_cb[];
+  __shared__ uint32_t s_pts[kRingLds];
+  __shared__ int32_t s_own[kRingLds];
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
+  const RingView rv = stage_ring(pts, own, npts, s_pts, s_own);
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
   for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
     const Digest k = keys[j];
-    const int o = ring_owner_of(k, pts, own, npts);
+    const int o = ring_owner_of(k, rv.pts, rv.own, npts);
     const bool h = nhot > 0 && is_hot(k, hot, nhot, hot_dir);
     owner[j] = h ? (o | (1 << 30)) : o;  // bit 30: fan out to every rank
     const uint32_t vl = vlen[j];
