@@ -16,6 +16,7 @@ for spec in "$@"; do
   case $spec in
     dram)   run dram_8M   --backend dram   --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
     hbm)    run hbm_8M    --backend hbm    --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
+    hbm_b1) run hbm_8M_backlog1 --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --serve-backlog 1 || exit 1;;
     hbm_nosrv) run hbm_8M_nosrv --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-edge-server || exit 1;;
     tiered) run tiered_8M --backend tiered --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
   esac

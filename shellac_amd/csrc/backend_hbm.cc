@@ -265,6 +265,7 @@ struct HbmBackend::Dev {
 // Host slots the edge GET signals completion through: one per flight.
 constexpr int kFlightSlot0 = 8;
 
+
 HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     : cfg_(cfg), ring_((int)cfg.devices.size()), epoch_(wall_s()) {
   SH_CHECK(!cfg_.devices.empty() && cfg_.devices.size() <= 64, "HbmBackend needs 1..64 devices");
@@ -668,11 +669,12 @@ void HbmBackend::Dev::launch(Flight& f) {
     for (size_t u = 0; !ordered && !pend_w.empty() && u < f.rows; ++u)
       ordered = pend_w.count(hk[u].lo) != 0;
     if (ordered) ordered_gets++;
-    // ... and only while the server has no job: it takes one job at a time, so under
-    // load (several batches in flight) the launched path's many workgroups win
-    // (profiles/r3_http: c=1000 with every small batch served 0.95M RPS, launched 1.13M)
+    // ... and only while fewer than serve_backlog jobs are ahead of it: the server takes
+    // one job at a time, so under load (several batches in flight) the launched path's
+    // many workgroups win (profiles/r3_http: c=1000 with every small batch served 0.95M
+    // RPS, launched only 1.13M)
     f.served = be->cfg_.edge_server && !ordered && f.rows <= (size_t)HbmCache::kServeKeys &&
-               cache->serve_idle() &&
+               cache->serve_backlog() < (uint64_t)be->cfg_.serve_backlog &&
                cache->serve_get(hk, (int64_t)f.rows, f.arena->d, f.arena->cap,
                                 f.offs.dev<uint64_t>(), f.tnow, f.slot);
     if (f.served) served_batches++;

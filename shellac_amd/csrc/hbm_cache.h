@@ -115,10 +115,11 @@ class HbmCache {
   bool serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
                  uint64_t* off, uint32_t now, int done_slot);
   void serve_kick();
-  // no server job outstanding (the resident workgroup takes jobs one at a time: a caller
-  // with several batches in flight sends the others down the launched path)
-  bool serve_idle() const {
-    return __atomic_load_n(srv_ctl_, __ATOMIC_ACQUIRE) >= srv_ticket_;
+  // server jobs queued or running (the resident workgroup takes them one at a time: a
+  // caller with several batches in flight sends the rest down the launched path)
+  uint64_t serve_backlog() const {
+    const uint64_t c = __atomic_load_n(srv_ctl_, __ATOMIC_ACQUIRE);
+    return srv_ticket_ > c ? srv_ticket_ - c : 0;
   }
   // wait_host_slot for a serve_get job: spins, relaunching the server when it exited
   uint64_t serve_wait(int done_slot, int64_t timeout_ms = 10000);
@@ -271,6 +272,8 @@ size_t device_scan_tmp_bytes(int64_t n);
 
 // Load-balanced segmented copy: segment i copies (dst_off[i+1]-dst_off[i]) bytes
 // from src + src_off[i] to dst + dst_off[i]. All offsets/lengths multiples of 16.
+// src_off[i] == kSegSkip: segment i is a gap (nothing read or written).
+constexpr uint64_t kSegSkip = ~0ull;
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
              uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
 // Sized variant: segment i holds seg_len[i] bytes at dst + dst_off[i] (dst_off ascending,

@@ -789,7 +789,8 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
   }
 }
 
-// Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w.
+// Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w;
+// a segment whose src_off is kSegSkip is a gap (its bytes are left as they are).
 // Mode 2 (sized gather): as mode 0, but segment j holds only seg_len[j] bytes (passed in
 // the `head_ptr` slot) and is copied only when it ends within `cap`; the bytes between a
 // segment's end and the next segment's start are left untouched (gaps, headers written
@@ -876,6 +877,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
           if (x < seg_start || w >= s_len[jl]) continue;  // gap / dropped: untouched
           sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
         } else if (MODE == 0) {
+          // a kSegSkip source leaves the segment's bytes untouched (no load, no store)
+          if (seg_src == kSegSkip) continue;
           // integer address math: src may be null with absolute addresses in src_off
           sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
         } else {
@@ -900,7 +903,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
-        if (c >= c1 || (MODE == 2 && !sp[u])) continue;
+        if (c >= c1 || (MODE != 1 && !sp[u])) continue;
         const uint64_t d = MODE == 1 ? dofs[MODE == 1 ? u : 0] : (uint64_t)c << 4;
         if (NTSTORE)
           __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + d));
@@ -1172,7 +1175,6 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
             if (((lane - kSrvHdr) & 1) == 0) s_key[kk].lo = v;
             else s_key[kk].hi = v;
           }
-          if (lane == 0) s_head = newest_head(heads);
           cmd = 0;
           break;
         }
@@ -1192,8 +1194,8 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     uint8_t* const out = reinterpret_cast<uint8_t*>(s_job[0]);
     const uint64_t out_cap = s_job[1];
     uint64_t* const off_out = reinterpret_cast<uint64_t*>(s_job[2]);
-    const uint64_t head = s_head;
-    // ---- probe: one 8-lane group per key, nontemporal (L2-served) bucket reads
+    // ---- probe: one 8-lane group per key, nontemporal (L2-served) bucket reads, issued
+    //      together with the (L2-hot) head words the liveness test needs
     unsigned long long ops = 0, hits = 0, bytes = 0;
     for (int k = g; k - g < n; k += kSrvGroups) {
       uint64_t hl = 0;
@@ -1202,7 +1204,10 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
         const Digest d = s_key[k];
         int he = 0;
         uint64_t hb = bucket1(d, mask);
-        group_match(nt_bucket_quarter(index, hb, l8), d, l8, head, cap, now, &hl, &hv, &he);
+        const uint4 q1 = nt_bucket_quarter(index, hb, l8);
+        // each lane judges its own entry: lanes may see different (all valid) heads
+        const uint64_t head = newest_head(heads);
+        group_match(q1, d, l8, head, cap, now, &hl, &hv, &he);
         if (hl == 0) {
           hb = bucket2(d, mask);
           group_match(nt_bucket_quarter(index, hb, l8), d, l8, head, cap, now, &hl, &hv, &he);

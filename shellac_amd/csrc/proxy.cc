@@ -307,6 +307,10 @@ class Reactor : public Executor {
   std::vector<Conn*> graveyard_;
   std::mutex post_mu_;
   std::vector<std::function<void()>> posted_;
+  // the loop is busy-polling (epoll_wait(0), posted work drained every pass): posters
+  // skip the eventfd write — a syscall on their side and a read on this one, per
+  // completion (the HBM batcher posts one per GPU batch)
+  std::atomic<bool> spinning_{false};
   std::mt19937 rng_;
   std::vector<char> buf_;
   // collapsed forwarding: key -> requests waiting on the in-flight miss of the
@@ -356,7 +360,8 @@ void Reactor::post(std::function<void()> fn) {
     was_empty = posted_.empty();
     posted_.push_back(std::move(fn));
   }
-  if (was_empty) wake();  // a non-empty queue already has a wake-up pending
+  // a non-empty queue already has a wake-up pending; a spinning loop needs none
+  if (was_empty && !spinning_.load(std::memory_order_seq_cst)) wake();
 }
 
 void Reactor::post_batch(std::vector<std::function<void()>>& fns) {
@@ -372,7 +377,7 @@ void Reactor::post_batch(std::vector<std::function<void()>>& fns) {
     }
   }
   fns.clear();
-  if (was_empty) wake();
+  if (was_empty && !spinning_.load(std::memory_order_seq_cst)) wake();
 }
 
 void Reactor::drain_posted() {
@@ -410,7 +415,18 @@ void Reactor::loop() {
   double last_work = now_s();
   while (px_->running_) {
     const bool spin = spin_s > 0 && now_s() - last_work < spin_s;
-    const int n = epoll_wait(epfd_, evs, 256, spin ? 0 : 100);
+    int timeout_ms = 0;
+    if (spin) {
+      spinning_.store(true, std::memory_order_seq_cst);
+    } else {
+      // leaving the spin: a poster that still saw spinning_ did not write the eventfd,
+      // so look at the queue after clearing the flag (both seq_cst: one of the two sides
+      // sees the other) and block only when it is empty
+      spinning_.store(false, std::memory_order_seq_cst);
+      std::lock_guard<std::mutex> lk(post_mu_);
+      timeout_ms = posted_.empty() ? 100 : 0;
+    }
+    const int n = epoll_wait(epfd_, evs, 256, timeout_ms);
     const double t_it = n > 0 ? now_s() : 0;
     if (n > 0 && spin_s > 0) last_work = t_it;
     for (int i = 0; i < n; ++i) {

@@ -549,13 +549,12 @@ __global__ void k_demand(const uint64_t* __restrict__ lk_off, int32_t W, int32_t
 // Owner, reply slots as segments of one plain gather per destination buffer (others: R,
 // self: data's self slot). Slot s = [header (capG x u64) | records | slack], as segments
 // [header | one per row | slack] (capG + 2 per slot): the header segment copies the
-// headers k_reply_prep wrote into `hdr`, the slack segment copies the slot's own unused
-// bytes onto themselves, so the segments tile the buffer and the gather needs no gaps.
+// headers k_reply_prep wrote into `hdr`, the slack segment is a kSegSkip gap (the slot's
+// unused tail: neither read nor written), so the segments tile the buffer.
 // used[s] = the bytes of slot s's longest row prefix that fits capD (rows past it are
 // dropped: header 0, no bytes).
 __global__ void k_reply_used(const uint64_t* __restrict__ lk_off, int32_t W, int64_t capG,
                              int64_t capD, int64_t slotR, const uint64_t* __restrict__ hdr,
-                             uint8_t* __restrict__ R, uint8_t* __restrict__ self_slot,
                              uint64_t* __restrict__ used, uint64_t* __restrict__ offA,
                              uint64_t* __restrict__ srcA, uint64_t* __restrict__ offB,
                              uint64_t* __restrict__ srcB) {
@@ -573,12 +572,11 @@ __global__ void k_reply_used(const uint64_t* __restrict__ lk_off, int32_t W, int
     uint64_t* off = self ? offB : offA + s * per;
     uint64_t* src = self ? srcB : srcA + s * per;
     const uint64_t sb = self ? 0 : (uint64_t)s * (uint64_t)slotR;
-    uint8_t* slot = self ? self_slot : R + s * slotR;
     off[0] = sb;
     src[0] = (uint64_t)(uintptr_t)(hdr + s * capG);
     const uint64_t gap = (uint64_t)capG * 8 + u;
     off[capG + 1] = sb + gap;
-    src[capG + 1] = (uint64_t)(uintptr_t)(slot + gap);  // slack onto itself
+    src[capG + 1] = kSegSkip;  // the slot's unused tail: a gap (was copied onto itself)
   }
   if (threadIdx.x == 0) {
     offA[(int64_t)(W - 1) * per] = (uint64_t)(W - 1) * (uint64_t)slotR;
@@ -1003,7 +1001,7 @@ void RoutedStep::owner_reply(HbmCache* shard, uint8_t* R, uint8_t* data, hipStre
   hipLaunchKernelGGL(k_demand, dim3(1), dim3(64), 0, s, lk_off_, W, rank_, capG_, rb_);
   RT_OK(hipMemsetAsync(rb_ + W, 0, sizeof(int64_t), s));
   hipLaunchKernelGGL(k_reply_used, dim3(1), dim3(64), 0, s, lk_off_, W, capG_, capD_, slotR, hdr,
-                     R, self_slot, used, offA, srcA, offB, srcB);
+                     used, offA, srcA, offB, srcB);
   hipLaunchKernelGGL(k_reply_prep, dim3(grid1(rows)), dim3(kB), 0, s, lk_loc_, lk_size_, lk_off_,
                      own_cnt_, used, W, capG_, slotR, shard->log_ptr(), hdr, offA, srcA, offB,
                      srcB, reinterpret_cast<unsigned long long*>(rb_ + W));

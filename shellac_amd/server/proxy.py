@@ -54,7 +54,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  fault: Optional[str] = None,
                  sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
                  depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000,
-                 edge_server: bool = True, batcher_cpus: Sequence[int] = ()):
+                 edge_server: bool = True, batcher_cpus: Sequence[int] = (),
+                 serve_backlog: int = 2):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -83,14 +84,14 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              promote_ttl=promote_ttl, sweep_s=sweep_s, hbm_filter=hbm_filter,
                              spin_us=spin_us, depth=depth, evict=evict,
                              batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
-                             batcher_cpus=batcher_cpus)
+                             batcher_cpus=batcher_cpus, serve_backlog=serve_backlog)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
                           batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s,
                           hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
                           batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
-                          batcher_cpus=batcher_cpus)
+                          batcher_cpus=batcher_cpus, serve_backlog=serve_backlog)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -108,7 +109,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              spin_us=spin_us, presence_filter=hbm_filter, depth=depth,
                              evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms,
                              edge_server=edge_server,
-                             batcher_cpus=[int(x) for x in batcher_cpus])
+                             batcher_cpus=[int(x) for x in batcher_cpus],
+                             serve_backlog=int(serve_backlog))
     raise ValueError(f"unknown cache backend {kind!r}")
 
 
