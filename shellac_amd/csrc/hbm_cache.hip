@@ -1091,7 +1091,10 @@ __global__ __launch_bounds__(kBlock) void k_edge_get(
 // issue, job seen, probed, copied, publish) for serve_trace().
 // ---------------------------------------------------------------------------------
 constexpr int kSrvBlock = 512;
-constexpr int kSrvGroups = kSrvBlock / 8;
+constexpr int kSrvPollWave = kSrvBlock / 64 - 1;  // the last wave polls; the others work
+constexpr int kSrvWorkers = kSrvPollWave * 64;
+constexpr int kSrvGroups = kSrvWorkers / 8;
+static_assert(HbmCache::kServeKeys <= kSrvGroups, "one probe pass per job");
 constexpr int kSrvUnroll = 16;  // 16-B chunks in flight per lane: 128 KiB per round
 constexpr int kSrvGranules = 64;
 constexpr int kSrvHdr = 5;
@@ -1109,10 +1112,13 @@ constexpr int kCtlConsumed = 0, kCtlExited = 8, kCtlStop = 16;  // words, each o
 constexpr uint64_t kSrvIdleUs = 1000, kSrvLifeUs = 10000;
 constexpr int kSrvTrace = 64;  // jobs whose phase stamps are kept (ring)
 
-// 16-B system-coherent load (sc0 sc1: past every GPU cache) of host memory the host
-// rewrites: a plain or nontemporal load of it can be served stale from a cache, and a
-// poll that misses a job then waits for the server's idle exit (measured: ~0.5 ms a job)
-__device__ __forceinline__ u32x4 sys_load16(const void* p) {
+// Lane `lane`'s 16-B granule of ring slot `t`: a system-coherent load (sc0 sc1: past every
+// GPU cache) of host memory the host rewrites — a plain or nontemporal load of it can be
+// served stale from a cache, and a poll that misses a job then waits for the server's
+// idle exit (measured: ~0.5 ms a job). Waits for its own return. (A buffer-load builtin
+// with the same cache policy measured 2.5 us per round trip against 1.4 for this.)
+__device__ __forceinline__ u32x4 poll_slot(const SrvJob* ring, uint64_t t, int lane) {
+  const void* p = &ring[t % HbmCache::kServeRing].g[lane];
   u32x4 v;
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
                : "=v"(v)
@@ -1149,21 +1155,35 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
   __shared__ uint64_t s_off[K + 1];
   __shared__ uint64_t s_job[kSrvHdr];  // out, out_cap, off, n | now << 32, slot
   __shared__ uint64_t s_head;
+  __shared__ uint64_t s_t[3];          // poll issued, job seen (poller); last publish (tid 0)
   __shared__ int s_cmd;
   __shared__ unsigned long long s_cnt[3][kSrvBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = tid >> 3, l8 = tid & 7;
+  const bool worker = w != kSrvPollWave;
   uint64_t ticket = sys_load(ctl + kCtlConsumed);
   const uint64_t t_start = (uint64_t)wall_clock64();
-  uint64_t t_last = t_start, t_poll = 0, t_seen = 0;
+  if (tid == 0) s_t[2] = t_start;
+  u32x4 pre = u32x4{0u, 0u, 0u, 0u};
+  bool have_pre = false;
+  __syncthreads();
   for (;;) {
-    // ---- wait for the next job: wave 0 reads all of it per poll (one 16-B granule a lane)
-    if (w == 0) {
-      const SrvGranule* jg = ring[ticket % HbmCache::kServeRing].g;
+    // ---- wait for the next job. The poller wave reads all of it per poll (one 16-B
+    //      granule a lane); while the workers probe a job it reads the next slot ahead:
+    //      when the host has queued that job meanwhile (back-to-back batches) it is there
+    //      when this one is done, and the round trip hid under the probe.
+    if (!worker) {
       const uint64_t want = ticket + 1;
       int cmd = 1;
+      uint64_t t_poll = 0;
       for (;;) {
+        u32x4 gv;
         t_poll = (uint64_t)wall_clock64();
-        const u32x4 gv = sys_load16(jg + lane);
+        if (have_pre) {
+          gv = pre;
+          have_pre = false;
+        } else {
+          gv = poll_slot(ring, ticket, lane);
+        }
         const uint64_t v = pack2(gv.x, gv.y), tag = pack2(gv.z, gv.w);
         const uint64_t nn = __shfl(v, 3) & 0xffffffffu;     // n, from granule 3
         const bool hdr_ok = __shfl((int)(tag == want), 3) != 0;
@@ -1179,13 +1199,16 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
           break;
         }
         const uint64_t t = (uint64_t)wall_clock64();
-        const bool quit = lane == 0 && (sys_load(ctl + kCtlStop) || t - t_last > idle_ticks ||
+        const bool quit = lane == 0 && (sys_load(ctl + kCtlStop) || t - s_t[2] > idle_ticks ||
                                         t - t_start > life_ticks);
         if (__shfl((int)quit, 0)) break;
         __builtin_amdgcn_s_sleep(2);
       }
-      t_seen = (uint64_t)wall_clock64();
-      if (lane == 0) s_cmd = cmd;
+      if (lane == 0) {
+        s_cmd = cmd;
+        s_t[0] = t_poll;
+        s_t[1] = (uint64_t)wall_clock64();
+      }
     }
     __syncthreads();
     if (s_cmd) break;
@@ -1194,10 +1217,14 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     uint8_t* const out = reinterpret_cast<uint8_t*>(s_job[0]);
     const uint64_t out_cap = s_job[1];
     uint64_t* const off_out = reinterpret_cast<uint64_t*>(s_job[2]);
-    // ---- probe: one 8-lane group per key, nontemporal (L2-served) bucket reads, issued
-    //      together with the (L2-hot) head words the liveness test needs
+    // ---- probe: one 8-lane group of the workers per key, nontemporal (L2-served) bucket
+    //      reads, issued together with the (L2-hot) head words the liveness test needs
     unsigned long long ops = 0, hits = 0, bytes = 0;
-    for (int k = g; k - g < n; k += kSrvGroups) {
+    if (!worker) {  // read ahead (consumed when this job is done)
+      pre = poll_slot(ring, ticket + 1, lane);
+      have_pre = true;
+    }
+    for (int k = g; worker && k - g < n; k += kSrvGroups) {
       uint64_t hl = 0;
       uint32_t hv = 0;
       if (k < n) {
@@ -1246,19 +1273,20 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     __syncthreads();
     const uint64_t t_probed = (uint64_t)wall_clock64();
     const uint64_t total = s_off[n];
-    for (int k = tid; k <= n; k += kSrvBlock) off_out[k] = s_off[k];
-    // ---- stream the records in rounds of kSrvUnroll chunks per lane: loads, then (all
-    //      loads of the round returned) the claim check, then the stores. Nothing when
-    //      the records outgrow the arena (the caller regathers).
+    if (worker)
+      for (int k = tid; k <= n; k += kSrvWorkers) off_out[k] = s_off[k];
+    // ---- stream the records in rounds of kSrvUnroll chunks per worker lane: loads, then
+    //      (all loads of the round returned) the claim check, then the stores. Nothing
+    //      when the records outgrow the arena (the caller regathers).
     const int64_t nch = total <= out_cap ? (int64_t)(total >> 4) : 0;
-    for (int64_t c0 = 0; c0 < nch; c0 += (int64_t)kSrvBlock * kSrvUnroll) {
+    for (int64_t c0 = 0; c0 < nch; c0 += (int64_t)kSrvWorkers * kSrvUnroll) {
       u32x4 v[kSrvUnroll];
       int rec[kSrvUnroll];
 #pragma unroll
       for (int u = 0; u < kSrvUnroll; ++u) {
-        const int64_t c = c0 + (int64_t)u * kSrvBlock + tid;
+        const int64_t c = c0 + (int64_t)u * kSrvWorkers + tid;
         rec[u] = -1;
-        if (c < nch) {
+        if (worker && c < nch) {
           const uint64_t x = (uint64_t)c << 4;
           int lo = 0, hi = n - 1;  // the record holding byte x: last k with s_off[k] <= x
           while (lo < hi) {
@@ -1271,7 +1299,7 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
           rec[u] = lo;
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (worker) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) s_head = newest_head(heads);
       __syncthreads();
@@ -1279,23 +1307,24 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
 #pragma unroll
       for (int u = 0; u < kSrvUnroll; ++u) {
         if (rec[u] < 0) continue;
-        const uint64_t x = (uint64_t)(c0 + (int64_t)u * kSrvBlock + tid) << 4;
+        const uint64_t x = (uint64_t)(c0 + (int64_t)u * kSrvWorkers + tid) << 4;
         // a record the claim now reaches may be torn: zero its magic word (miss)
         if (x - s_off[rec[u]] == 16 && !(c2 <= (s_lg[rec[u]] - 1) + cap))
           v[u] = u32x4{0u, 0u, 0u, 0u};
         *reinterpret_cast<u32x4*>(out + x) = v[u];
       }
     }
-    // ---- completion: every wave drains its stores, then one system-scope publish
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- completion: every worker wave drains its stores, then one system-scope publish
+    //      (the poller's outstanding read-ahead is not waited for)
+    if (worker) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint64_t t_copied = (uint64_t)wall_clock64();
     if (tid == 0) {
       // the job's phase stamps first, so they are in place when the host sees the slot
       uint64_t* tr = trace + (ticket % kSrvTrace) * 8;
       tr[0] = ticket;
-      tr[1] = t_poll;
-      tr[2] = t_seen;
+      tr[1] = s_t[0];
+      tr[2] = s_t[1];
       tr[3] = t_probed;
       tr[4] = t_copied;
       tr[5] = (uint64_t)wall_clock64();
@@ -1306,7 +1335,7 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
       __hip_atomic_store(slots + s_job[4], total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(ctl + kCtlConsumed, ticket + 1, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-      t_last = (uint64_t)wall_clock64();
+      s_t[2] = (uint64_t)wall_clock64();
     }
     // ---- counters (off the latency path)
     ops = wave_sum(ops);
