@@ -9,7 +9,7 @@ export SHELLAC_TRACE=1
 for args in "--simulate-world 2" "--simulate-world 8" "--routed"; do
   name=$(echo "x$args" | tr -d ' -')
   timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/$name" -o bench -- \
-    python3 $R/bench.py --steps 10 --warmup 3 --no-smoke --no-uncoalesced --no-wrapped $args \
+    python3 $R/bench.py --steps 10 --warmup 3 --no-smoke --no-uncoalesced --no-wrapped --pressured-gb 0 $args \
     > "$OUT/$name.log" 2>&1 || { echo "trace $args failed"; tail -20 "$OUT/$name.log"; exit 1; }
   f=$(find "$OUT/$name" -name '*kernel_trace.csv' | head -1)
   d=$(dirname "$f")

@@ -92,12 +92,12 @@ void bind_router(py::module_& m) {
         py::gil_scoped_release nogil;
         r.pack_sets(P<uint8_t>(Sb), S(s));
       })
-      .def("store_sets", [](RoutedStep& r, uintptr_t Sb, uintptr_t Rs, HbmCache* shard,
-                            HbmCache* replica, uint32_t now, uintptr_t s) {
+      .def("store_sets", [](RoutedStep& r, uintptr_t Rs, HbmCache* shard, HbmCache* replica,
+                            uint32_t now, uintptr_t s, uintptr_t sset) {
         py::gil_scoped_release nogil;
-        r.store_sets(P<const uint8_t>(Sb), P<const uint8_t>(Rs), shard, replica, now, S(s));
-      }, py::arg("S"), py::arg("Rs"), py::arg("shard"), py::arg("replica").none(true),
-         py::arg("now"), py::arg("stream"))
+        r.store_sets(P<const uint8_t>(Rs), shard, replica, now, S(s), S(sset));
+      }, py::arg("Rs"), py::arg("shard"), py::arg("replica").none(true), py::arg("now"),
+         py::arg("stream"), py::arg("set_stream"))
       .def("assemble", [](RoutedStep& r, uintptr_t data, uintptr_t out_size, uintptr_t out_off,
                           uintptr_t s) {
         py::gil_scoped_release nogil;

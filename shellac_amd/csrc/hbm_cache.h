@@ -73,9 +73,11 @@ class HbmCache {
   // Slotted lookup (the routed step's owner side): nslots x slot_rows rows, slot k's
   // rows [k * slot_rows, k * slot_rows + slot_cnt[k]) are requests, the rest padding
   // (size 0, not probed, not counted). off = exclusive scan over all rows.
+  // `reserve_dev` (optional, device word): a reserve the stream computes before the
+  // probe runs (the routed step's received SET bytes), as lookup's `reserve`.
   void lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_rows,
                     const int64_t* slot_cnt, uint64_t* loc, uint64_t* size, uint64_t* off,
-                    uint32_t now, hipStream_t s);
+                    uint32_t now, hipStream_t s, const uint64_t* reserve_dev = nullptr);
   uint64_t host_slot(int i) const;
   // Spin until the lookup that was given `total_slot` i has written it (no stream or
   // event synchronisation: the kernel's system-scope store is the signal). Throws after

@@ -392,11 +392,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                   uint64_t* __restrict__ part,
                                                   const uint32_t* __restrict__ first,
                                                   int64_t slot_rows,
-                                                  const int64_t* __restrict__ slot_cnt) {
+                                                  const int64_t* __restrict__ slot_cnt,
+                                                  const uint64_t* __restrict__ reserve_dev) {
   const int l8 = threadIdx.x & 7;
-  // `reserve`: bytes about to be appended before this lookup's gather runs; objects
-  // that those appends will overwrite are already treated as evicted
-  const uint64_t head = *head_ptr + reserve;
+  // `reserve` (+ *reserve_dev, a device-computed bound): bytes about to be appended
+  // before this lookup's gather runs; objects that those appends will overwrite are
+  // already treated as evicted
+  const uint64_t head = *head_ptr + reserve + (reserve_dev ? *reserve_dev : 0ull);
   unsigned long long hits = 0, bytes = 0, ops = 0, psum = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;
   // contiguous key range per workgroup (k_offsets scans it from the partial sums)
@@ -2657,14 +2659,14 @@ void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* si
   const int grid = grid_for(n * 8, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, first,
-                     (int64_t)1, (const int64_t*)nullptr);
+                     (int64_t)1, (const int64_t*)nullptr, (const uint64_t*)nullptr);
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, ht);
 }
 
 void HbmCache::lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_rows,
                             const int64_t* slot_cnt, uint64_t* loc, uint64_t* size, uint64_t* off,
-                            uint32_t now, hipStream_t s) {
+                            uint32_t now, hipStream_t s, const uint64_t* reserve_dev) {
   TraceRange tr("hbm.lookup_slots");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
@@ -2676,7 +2678,7 @@ void HbmCache::lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_row
   const int grid = grid_for(n * 8, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_probe, dim3(grid), dim3(kBlock), 0, s, keys, n, index_, cfg_.nbuckets - 1,
                      cur_head(), (uint64_t)0, cfg_.log_bytes, now, loc, size, ctr_, part_,
-                     (const uint32_t*)nullptr, slot_rows, slot_cnt);
+                     (const uint32_t*)nullptr, slot_rows, slot_cnt, reserve_dev);
   HIP_OK(hipGetLastError());
   launch_offsets(size, n, part_, grid, off, s, nullptr);
 }

@@ -72,10 +72,12 @@ class HbmCache;
 // Per step (stream-ordered on `s`):
 //   plan(G) -> [all_gather row -> mat] -> publish(mat)
 //   -> [a2a G send -> G recv, capG*16 per other rank]
-//   -> owner_probe(G) -> (calibration only: owner_demand, all_gather, calibrate_reply)
+//   -> owner_probe(G) (reserves this step's SET bytes) -> [SET stream forks here]
+//   -> (calibration only: owner_demand, all_gather, calibrate_reply)
 //   -> owner_reply(R, data) -> [async a2a R -> data, slot bytes per other rank]
-//   -> gather_local(data) -> set_splits() (host waits for publish) -> pack_sets(S)
-//   -> [a2a S -> Rs, exact sizes] -> store_sets(S, Rs)
+//   -> gather_local(data) -> set_splits() (host waits for publish)
+//   -> on the SET stream: pack_sets(S) -> [a2a S -> Rs, exact sizes] -> store_sets(Rs),
+//      i.e. the main-shard SET chain beside the reply gather
 //   -> on a side stream after the reply a2a: assemble(data, out) -> wait() before reading.
 class RoutedStep {
  public:
@@ -129,13 +131,15 @@ class RoutedStep {
   // q (W) | n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped]
   // (self entries included: the SET buffer is [others in rank order | self]).
   std::vector<int64_t> set_splits();
-  // SET send buffer: per destination [records 32 B x rows | values], others in rank
-  // order then self.
-  void pack_sets(uint8_t* S, hipStream_t s);
-  // Received SETs (others from Rs, own from S's tail) into the main shard (tier 0, on
-  // the store stream: joined by the next owner_probe) and the replica (tier 1, on `s`).
-  void store_sets(const uint8_t* S, const uint8_t* Rs, HbmCache* shard, HbmCache* replica,
-                  uint32_t now, hipStream_t s);
+  // SET send buffer: per other rank (rank order) [records 32 B x rows | values]; the
+  // self block is never packed. Run on the SET stream (forked from `s` after the probe).
+  void pack_sets(uint8_t* S, hipStream_t sset);
+  // Received SETs (others from Rs, own straight from the planner's buffers and the
+  // caller's batch) into the main shard (tier 0) on the SET stream `sset`, beside the
+  // reply gather (the probe reserved their bytes; joined by the next owner_probe), and
+  // the replica (tier 1) on `s` after the local gather.
+  void store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replica, uint32_t now,
+                  hipStream_t s, hipStream_t sset);
   // Per-request (size, off) into `data`, in request order (duplicates: their claimer's
   // record); run on a stream that has waited for the reply all-to-all.
   void assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off, hipStream_t s);
@@ -164,7 +168,7 @@ class RoutedStep {
   int64_t* host_mat_ = nullptr;   // pinned: the published all-gather matrix
   int64_t* host_dmat_ = nullptr;  // pinned: calibration demand matrix
   uint64_t* host_tab_ = nullptr;  // pinned: per-step SET tables (uploaded)
-  hipStream_t side_ = nullptr, store_side_ = nullptr;
+  hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_pjoin_ = nullptr, ev_pub_ = nullptr, ev_sfork_ = nullptr,
              ev_join_ = nullptr, ev_asm_[2] = {nullptr, nullptr};
   bool asm_pending_[2] = {false, false};
@@ -187,6 +191,8 @@ class RoutedStep {
   int64_t *srec_ = nullptr, *cnt_s_ = nullptr;
   uint64_t *sval_ = nullptr, *svoff_ = nullptr;
   int64_t* own_cnt_ = nullptr;
+  const int64_t* mat_dev_ = nullptr;  // the all-gathered matrix (device), from publish
+  int64_t self_row0_ = 0;             // first row of the self block in srec_ / sval_
   uint64_t *lk_loc_ = nullptr, *lk_size_ = nullptr, *lk_off_ = nullptr;
   int64_t* rb_ = nullptr;       // reply bytes per requester (W) + dropped rows (1)
   std::vector<int64_t> mat_;    // host copy of this step's matrix (after set_splits)

@@ -492,7 +492,7 @@ enum Slot {
   kCoTab, kFirst0, kFirst1, kOwnerS, kVpad, kTcnt, kTbytes, kSrec, kSval, kSvoff, kCntS,
   kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSrcA, kSrcB, kHdr, kUsed, kRb, kTab,
   kSegOff, kSegSrc,
-  kRkeys, kV0, kV1, kFl, kEx, kRoff, kNumSlots
+  kRkeys, kV0, kV1, kFl, kEx, kRoff, kReserve, kSrec1, kSval1, kSvoff1, kNumSlots
 };
 
 // Slot of G a requester writes peer p's rows into: self = W-1, others W + o(p).
@@ -535,6 +535,20 @@ __global__ void k_derive(const int64_t* __restrict__ mat, int64_t K, int32_t W, 
     const int q = s == W - 1 ? me : (s < me ? s : s + 1);
     own_cnt[s] = min(mat[(int64_t)q * K + me], capG);
   }
+}
+
+// Log bytes this step's received SETs may append to the main shard (records, padded
+// values, the CLOCK hand's reinsertion budget): the owner probe treats what they will
+// overwrite as evicted, so the SET chain can run beside the reply gather.
+__global__ void k_owner_reserve(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
+                                uint64_t rmax, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  uint64_t rows = 0, bytes = 0;
+  for (int q = 0; q < W; ++q) {
+    rows += (uint64_t)mat[(int64_t)q * K + W + me];
+    bytes += (uint64_t)mat[(int64_t)q * K + 2 * W + me];
+  }
+  *out = 48 * rows + bytes + rmax;
 }
 
 // Reply bytes the owner probe found per requester (before any drop): out[q].
@@ -684,10 +698,13 @@ __global__ __launch_bounds__(kB) void k_set_segs(const uint64_t* __restrict__ ta
 
 // Received SET rows (sources: others by rank, self last) -> store arguments. tab per
 // source k: [first row (W+1) | record block address (W) | value block address (W)].
+// The self block (k = W - 1) is not packed: its records are the planner's own (srec) and
+// its values stay where the caller's batch holds them (self_sval: absolute addresses).
 __global__ __launch_bounds__(kB) void k_rs_fill_slots(
     const uint64_t* __restrict__ tab, int32_t W, int64_t ms, Digest* __restrict__ keys,
     uint32_t* __restrict__ vlen0, uint32_t* __restrict__ vlen1, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ expire, uint64_t* __restrict__ roff) {
+    uint32_t* __restrict__ expire, uint64_t* __restrict__ roff,
+    const uint64_t* __restrict__ self_sval) {
   const uint64_t* first = tab;
   const uint64_t* rec = tab + W + 1;
   const uint64_t* val = rec + W;
@@ -706,7 +723,8 @@ __global__ __launch_bounds__(kB) void k_rs_fill_slots(
     vlen1[r] = tier == 1 ? vl : kSkipVlen;
     flags[r] = (uint32_t)((uint64_t)rr[2] >> 32);
     expire[r] = (uint32_t)rr[3];
-    roff[r] = val[lo] + (hi32 & 0x7FFFFFFFull);  // absolute: the store's values base is 0
+    // absolute: the store's values base is 0
+    roff[r] = lo == W - 1 ? self_sval[r - (int64_t)first[lo]] : val[lo] + (hi32 & 0x7FFFFFFFull);
   }
 }
 
@@ -722,9 +740,11 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   RT_OK(hipHostMalloc(&host_mat_, K * (size_t)world * sizeof(int64_t), hipHostMallocDefault));
   RT_OK(hipHostMalloc(&host_dmat_, (size_t)world * (size_t)world * sizeof(int64_t),
                       hipHostMallocDefault));
-  RT_OK(hipHostMalloc(&host_tab_, (8 * (size_t)world + 8) * sizeof(uint64_t), hipHostMallocDefault));
+  // two parities: a step's H2D copies of its tables may still be queued on the SET
+  // stream when the next step's host code fills the other half
+  RT_OK(hipHostMalloc(&host_tab_, 2 * (8 * (size_t)world + 8) * sizeof(uint64_t),
+                      hipHostMallocDefault));
   RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-  RT_OK(hipStreamCreateWithFlags(&store_side_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_fork_, &ev_pjoin_, &ev_pub_, &ev_sfork_, &ev_join_, &ev_asm_[0],
                         &ev_asm_[1]})
     RT_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -740,7 +760,6 @@ RoutedStep::~RoutedStep() {
   for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1]})
     (void)hipEventDestroy(e);
   (void)hipStreamDestroy(side_);
-  (void)hipStreamDestroy(store_side_);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
@@ -889,9 +908,10 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   uint32_t* vpad = buf<uint32_t>(kVpad, ns);
   uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * Gs);
   uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * Gs);
-  srec_ = buf<int64_t>(kSrec, 4 * (size_t)mcap);
-  sval_ = buf<uint64_t>(kSval, mcap);
-  svoff_ = buf<uint64_t>(kSvoff, mcap);
+  // by parity: the previous step's SET packing (on the SET stream) may still read them
+  srec_ = buf<int64_t>(P ? kSrec1 : kSrec, 4 * (size_t)mcap);
+  sval_ = buf<uint64_t>(P ? kSval1 : kSval, mcap);
+  svoff_ = buf<uint64_t>(P ? kSvoff1 : kSvoff, mcap);
   cnt_s_ = buf<int64_t>(kCntS, nb);
   rb_ = buf<int64_t>(kRb, W + 1);
   if (hist_g_.empty() && calibrating_) RT_OK(hipMemsetAsync(rb_, 0, (W + 1) * sizeof(int64_t), s));
@@ -944,6 +964,7 @@ void RoutedStep::publish(const int64_t* mat, hipStream_t s) {
   const int W = w_;
   const int64_t K = row_words();
   own_cnt_ = buf<int64_t>(kOwnCnt, W);
+  mat_dev_ = mat;
   hipLaunchKernelGGL(k_derive, dim3(1), dim3(64), 0, s, mat, K, W, rank_, capG_, own_cnt_);
   RT_OK(hipGetLastError());
   RT_OK(hipMemcpyAsync(host_mat_, mat, (size_t)W * K * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -967,8 +988,14 @@ void RoutedStep::owner_probe(const uint8_t* G, HbmCache* shard, uint32_t now, hi
   lk_loc_ = buf<uint64_t>(kLkLoc, rows);
   lk_size_ = buf<uint64_t>(kLkSize, rows + 1);
   lk_off_ = buf<uint64_t>(kLkOff, rows + 1);
+  // this step's SETs are appended beside the reply gather (store_sets): reserve their
+  // bytes, computed on the device from the all-gathered matrix (no host read)
+  uint64_t* reserve = buf<uint64_t>(kReserve, 1);
+  hipLaunchKernelGGL(k_owner_reserve, dim3(1), dim3(64), 0, s, mat_dev_, row_words(), W, rank_,
+                     (uint64_t)shard->reinsert_max(), reserve);
+  RT_OK(hipGetLastError());
   shard->lookup_slots(reinterpret_cast<const Digest*>(G), W, capG_, own_cnt_, lk_loc_, lk_size_,
-                      lk_off_, now, s);
+                      lk_off_, now, s, reserve);
 }
 
 void RoutedStep::owner_demand(int64_t* out, hipStream_t s) {
@@ -1061,7 +1088,7 @@ void RoutedStep::pack_sets(uint8_t* S, hipStream_t s) {
   const int64_t K = row_words();
   // tab: [Sstart (W+1) | Bstart (W) | Psend (W) | segbase (W)] in rank order; send order
   // is the other ranks by rank, then self
-  uint64_t* t = host_tab_;
+  uint64_t* t = host_tab_ + (size_t)par_ * (8 * (size_t)W + 8);
   uint64_t* Sst = t;
   uint64_t* Bst = t + W + 1;
   uint64_t* Ps = Bst + W;
@@ -1081,6 +1108,11 @@ void RoutedStep::pack_sets(uint8_t* S, hipStream_t s) {
     pos += (uint64_t)sset_[d];
     seg += 1 + (uint64_t)mat_[me * K + W + d];
   }
+  self_row0_ = (int64_t)Sst[me];
+  // the self block (last in send order) is not copied: store_sets reads its records and
+  // values where the planner left them, so S holds the other ranks' blocks only
+  const int64_t nseg_out = (int64_t)sb[me];
+  if (nseg_out == 0) return;
   const size_t words = 5 * (size_t)W + 1;
   uint64_t* dtab = buf<uint64_t>(kTab, 8 * (size_t)W + 8);
   const int64_t nseg = W + ns_rows_;
@@ -1090,29 +1122,29 @@ void RoutedStep::pack_sets(uint8_t* S, hipStream_t s) {
   hipLaunchKernelGGL(k_set_segs, dim3(grid1(ns_rows_ + W + 1)), dim3(kB), 0, s, dtab, W, ns_rows_,
                      sval_, svoff_, (uint64_t)(uintptr_t)srec_, pos, seg_off, seg_src);
   RT_OK(hipGetLastError());
-  segcopy(nullptr, seg_src, seg_off, nseg, S, s);
+  // seg_off[sb[me]] = Ps[me]: the end of the other ranks' blocks
+  segcopy(nullptr, seg_src, seg_off, nseg_out, S, s);
 }
 
-void RoutedStep::store_sets(const uint8_t* S, const uint8_t* Rs, HbmCache* shard,
-                            HbmCache* replica, uint32_t now, hipStream_t s) {
+void RoutedStep::store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replica, uint32_t now,
+                            hipStream_t s, hipStream_t sset) {
   const int W = w_, me = rank_;
   const int64_t K = row_words();
   const int64_t ms = ms_;
   if (ms <= 0) return;
   // per source k (others by rank, self last): first row, record block, value block
-  uint64_t* t = host_tab_ + 5 * (size_t)W + 1;
+  uint64_t* t = host_tab_ + (size_t)par_ * (8 * (size_t)W + 8) + 5 * (size_t)W + 1;
   uint64_t* first = t;
   uint64_t* rec = t + W + 1;
   uint64_t* val = rec + W;
   uint64_t row0 = 0, rpos = 0, recv_bytes = 0;
-  uint64_t self_pos = 0;  // the self block sits after the others in S
-  for (int p = 0; p < W; ++p)
-    if (p != me) self_pos += (uint64_t)sset_[p];
   for (int k = 0; k < W; ++k) {
     const int q = k == W - 1 ? me : (k < me ? k : k + 1);
     const uint64_t rows = (uint64_t)mat_[q * K + W + me];
     first[k] = row0;
-    const uint64_t base = q == me ? (uint64_t)(uintptr_t)S + self_pos : (uint64_t)(uintptr_t)Rs + rpos;
+    // self: the planner's records (values by absolute address, self_sval below)
+    const uint64_t base =
+        q == me ? (uint64_t)(uintptr_t)(srec_ + 4 * self_row0_) : (uint64_t)(uintptr_t)Rs + rpos;
     rec[k] = base;
     val[k] = base + 32 * rows;
     row0 += rows;
@@ -1127,20 +1159,25 @@ void RoutedStep::store_sets(const uint8_t* S, const uint8_t* Rs, HbmCache* shard
   uint32_t* fl = buf<uint32_t>(kFl, ms);
   uint32_t* ex = buf<uint32_t>(kEx, ms);
   uint64_t* roff = buf<uint64_t>(kRoff, ms);
-  RT_OK(hipMemcpyAsync(dtab, t, (3 * (size_t)W + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_rs_fill_slots, dim3(grid1(ms)), dim3(kB), 0, s, dtab, W, ms, rkeys, v0, v1,
-                     fl, ex, roff);
+  RT_OK(hipMemcpyAsync(dtab, t, (3 * (size_t)W + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                       sset));
+  hipLaunchKernelGGL(k_rs_fill_slots, dim3(grid1(ms)), dim3(kB), 0, sset, dtab, W, ms, rkeys, v0,
+                     v1, fl, ex, roff, sval_ + self_row0_);
   RT_OK(hipGetLastError());
+  RT_OK(hipEventRecord(ev_sfork_, sset));  // the store arguments are ready
   const uint64_t bound = 48 * (uint64_t)ms + recv_bytes;
-  // main shard (tier 0) on the store stream, after the reply gather queued on `s` (the
-  // SETs may overwrite log bytes it reads); the next owner_probe joins it
-  RT_OK(hipEventRecord(ev_sfork_, s));
-  RT_OK(hipStreamWaitEvent(store_side_, ev_sfork_, 0));
-  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, store_side_);
-  RT_OK(hipEventRecord(ev_join_, store_side_));
+  // Main shard (tier 0) on the SET stream, which forked from `s` after this step's owner
+  // probe: the probe reserved these bytes (k_owner_reserve), so the append never touches
+  // a record the reply gather reads and runs beside it; the previous step's gather is
+  // done (it precedes the probe on `s`). The next owner_probe joins the chain.
+  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, sset);
+  RT_OK(hipEventRecord(ev_join_, sset));
   sets_pending_ = true;
-  // replica (tier 1) on `s`, after this step's local gather (same stream)
-  if (replica) replica->store(rkeys, nullptr, roff, v1, fl, ex, ms, bound, now, s);
+  // replica (tier 1) on `s`, after this step's local gather (same stream) and the fill
+  if (replica) {
+    RT_OK(hipStreamWaitEvent(s, ev_sfork_, 0));
+    replica->store(rkeys, nullptr, roff, v1, fl, ex, ms, bound, now, s);
+  }
 }
 
 // ---- assemble -------------------------------------------------------------------------

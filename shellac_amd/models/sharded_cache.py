@@ -491,6 +491,7 @@ class ShardedCache:
             self._row = torch.zeros(k, dtype=i64, device=dev)
             self._mat = torch.zeros(w * k, dtype=i64, device=dev)
             self._asm = torch.cuda.Stream(device=dev)
+            self._sset = torch.cuda.Stream(device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
         if fanout and self._hot_dir is None:
@@ -524,6 +525,10 @@ class ShardedCache:
                               input_split_sizes=sp, group=self.group)
         ph.next("owner")
         e.owner_probe(G.data_ptr(), self.shard._impl, now, st)
+        # the SET stream forks here: the probe reserved this step's SET bytes, so the SET
+        # exchange and the main-shard SET chain run beside the reply gather
+        sset = self._sset
+        self._xwait(sset, cur, "routed_probe")
         if cal:
             dem = torch.empty(w, dtype=i64, device=dev)
             e.owner_demand(dem.data_ptr(), st)
@@ -551,17 +556,20 @@ class ShardedCache:
         send, recv = h[:w], h[w:2 * w]
         n_local, n_dup, off_rank, over, dropped = h[2 * w: 2 * w + 5]
         so, ro = sum(send) - send[me], sum(recv) - recv[me]
-        S = torch.empty(sum(send) + 16, dtype=u8, device=dev)
-        e.pack_sets(S.data_ptr(), st)
+        # S: the other ranks' blocks only (own SETs are stored from the batch in place)
+        S = torch.empty(so + 16, dtype=u8, device=dev)
         Rs = torch.empty(ro + 16, dtype=u8, device=dev)
+        e.pack_sets(S.data_ptr(), sset.cuda_stream)
         if w > 1:
-            all_to_all_single(Rs[:ro], S[:so],
-                              output_split_sizes=[0 if q == me else recv[q] for q in range(w)],
-                              input_split_sizes=[0 if p == me else send[p] for p in range(w)],
-                              group=self.group)
-        e.store_sets(S.data_ptr(), Rs.data_ptr(), self.shard._impl, rep, now, st)
-        # the main-shard SET chain reads S / Rs until the next step's owner probe joins it
-        self._held = (S, Rs) if e.sets_pending else None
+            with torch.cuda.stream(sset):
+                all_to_all_single(Rs[:ro], S[:so],
+                                  output_split_sizes=[0 if q == me else recv[q] for q in range(w)],
+                                  input_split_sizes=[0 if p == me else send[p] for p in range(w)],
+                                  group=self.group)
+        e.store_sets(Rs.data_ptr(), self.shard._impl, rep, now, st, sset.cuda_stream)
+        # the main-shard SET chain reads S / Rs and the batch until the next step's owner
+        # probe joins it
+        self._held = (S, Rs, batch) if e.sets_pending else None
         ph.next("assemble")
         out = torch.empty((2, n), dtype=i64, device=dev)
         side = self._asm
