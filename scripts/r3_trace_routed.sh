@@ -6,8 +6,10 @@ OUT=$R/gpurun_out/${1:-r3_trace}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 export SHELLAC_TRACE=1
-for args in "--simulate-world 2" "--simulate-world 8" "--routed"; do
+IFS=";" read -ra CASES <<< "${TRACE_CASES:---simulate-world 2;--simulate-world 8;--routed}"
+for args in "${CASES[@]}"; do
   name=$(echo "x$args" | tr -d ' -')
+  [ -n "$args" ] || name=xn1
   timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/$name" -o bench -- \
     python3 $R/bench.py --steps 10 --warmup 3 --no-smoke --no-uncoalesced --no-wrapped --pressured-gb 0 $args \
     > "$OUT/$name.log" 2>&1 || { echo "trace $args failed"; tail -20 "$OUT/$name.log"; exit 1; }

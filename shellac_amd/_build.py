@@ -99,7 +99,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
         cmd = [f"{ROCM}/bin/hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs,
-               "-o", TARGET + ".tmp", f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-lz",
+               "-o", TARGET + ".tmp", f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-lz", "-ldl",
                "-lpthread",
                f"-Wl,-rpath,{ROCM}/lib"]
         p = subprocess.run(cmd, capture_output=True, text=True)

@@ -6,6 +6,7 @@
 #include "bind_parts.h"
 #include "hbm_cache.h"
 #include "router.h"
+#include "step_comm.h"
 
 namespace py = pybind11;
 using namespace shellac;
@@ -14,6 +15,39 @@ namespace {
 template <typename T>
 T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Collectives of RoutedStep::step implemented by a Python object (tests: several ranks
+// sharing one GPU, exchanging through gloo): obj.native_all_gather(out, in, words,
+// peer_blocks, stream) and obj.native_all_to_all(rbuf, roff, rbytes, sbuf, soff,
+// sbytes, stream), raw device pointers and the HIP stream as ints.
+class PyStepComm final : public StepComm {
+ public:
+  PyStepComm(py::object obj, int world, int rank) : obj_(std::move(obj)), w_(world), r_(rank) {}
+  ~PyStepComm() override {
+    py::gil_scoped_acquire g;
+    obj_ = py::object();
+  }
+  int world() const override { return w_; }
+  int rank() const override { return r_; }
+  void all_gather(int64_t* out, const int64_t* in, int64_t words, int peer_blocks, hipStream_t s,
+                  int) override {
+    py::gil_scoped_acquire g;
+    obj_.attr("native_all_gather")((uintptr_t)out, (uintptr_t)in, words, peer_blocks,
+                                   (uintptr_t)s);
+  }
+  void all_to_all(uint8_t* rbuf, const std::vector<int64_t>& roff,
+                  const std::vector<int64_t>& rbytes, const uint8_t* sbuf,
+                  const std::vector<int64_t>& soff, const std::vector<int64_t>& sbytes,
+                  hipStream_t s, int) override {
+    py::gil_scoped_acquire g;
+    obj_.attr("native_all_to_all")((uintptr_t)rbuf, roff, rbytes, (uintptr_t)sbuf, soff, sbytes,
+                                   (uintptr_t)s);
+  }
+
+ private:
+  py::object obj_;
+  int w_, r_;
+};
 }  // namespace
 
 void bind_router(py::module_& m) {
@@ -28,6 +62,43 @@ void bind_router(py::module_& m) {
                          uintptr_t owner, int32_t npts, int32_t w, uintptr_t dest, uintptr_t s) {
     route_gets(P<const Digest>(keys), n, P<const uint64_t>(rsize), P<const uint32_t>(pts),
                P<const int32_t>(owner), npts, w, P<int32_t>(dest), S(s));
+  });
+
+  py::class_<StepComm, std::shared_ptr<StepComm>>(m, "StepComm")
+      .def_property_readonly("world", &StepComm::world)
+      .def_property_readonly("rank", &StepComm::rank);
+  m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
+  m.def("make_rccl_comm", [](int world, int rank, int device, const std::vector<py::bytes>& ids) {
+    std::vector<std::string> v;
+    for (const auto& b : ids) v.emplace_back(b);
+    py::gil_scoped_release nogil;  // collective: blocks until every rank has joined
+    return std::shared_ptr<StepComm>(make_rccl_comm(world, rank, device, v));
+  });
+  m.def("make_mirror_comm", [](int world, int rank) {
+    return std::shared_ptr<StepComm>(make_mirror_comm(world, rank));
+  });
+  m.def("make_python_comm", [](py::object obj, int world, int rank) {
+    return std::shared_ptr<StepComm>(std::make_shared<PyStepComm>(std::move(obj), world, rank));
+  });
+  // synchronous staging copies for the Python-callback comm (after the stream drained)
+  m.def("stream_copy_to_host", [](uintptr_t src, int64_t n, uintptr_t s) {
+    std::string out((size_t)std::max<int64_t>(n, 0), '\0');
+    {
+      py::gil_scoped_release nogil;
+      if (hipStreamSynchronize(S(s)) != hipSuccess ||
+          (n > 0 && hipMemcpy(out.data(), P<const void>(src), (size_t)n, hipMemcpyDeviceToHost) !=
+                        hipSuccess))
+        throw Error("stream_copy_to_host failed");
+    }
+    return py::bytes(out);
+  });
+  m.def("stream_copy_from_host", [](uintptr_t dst, py::bytes data, uintptr_t s) {
+    std::string v(data);
+    py::gil_scoped_release nogil;
+    if (hipStreamSynchronize(S(s)) != hipSuccess ||
+        (!v.empty() && hipMemcpy(P<void>(dst), v.data(), v.size(), hipMemcpyHostToDevice) !=
+                           hipSuccess))
+      throw Error("stream_copy_from_host failed");
   });
 
   py::class_<RoutedStep>(m, "RoutedStep")
@@ -104,5 +175,23 @@ void bind_router(py::module_& m) {
         r.assemble(P<const uint8_t>(data), P<uint64_t>(out_size), P<uint64_t>(out_off), S(s));
       })
       .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
+      .def("set_comm", &RoutedStep::set_comm)
+      .def_property_readonly("has_comm", &RoutedStep::has_comm)
+      .def("step", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
+                      uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
+                      uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,
+                      bool coalesce, HbmCache* shard, uintptr_t data, uintptr_t out_size,
+                      uintptr_t out_off, uintptr_t s, uintptr_t sset, uintptr_t sasm) {
+        py::gil_scoped_release nogil;
+        return r.step(P<const Digest>(keys), n, replica, now, P<const Digest>(skeys),
+                      P<const uint32_t>(svlen), P<const uint32_t>(sflags),
+                      P<const uint32_t>(sexpire), P<const uint64_t>(sval_off),
+                      P<const uint8_t>(svalues), ns, fanout, coalesce, shard, P<uint8_t>(data),
+                      P<uint64_t>(out_size), P<uint64_t>(out_off), S(s), S(sset), S(sasm));
+      }, py::arg("keys"), py::arg("n"), py::arg("replica").none(true), py::arg("now"),
+         py::arg("skeys"), py::arg("svlen"), py::arg("sflags"), py::arg("sexpire"),
+         py::arg("sval_off"), py::arg("svalues"), py::arg("ns"), py::arg("fanout"),
+         py::arg("coalesce"), py::arg("shard"), py::arg("data"), py::arg("out_size"),
+         py::arg("out_off"), py::arg("stream"), py::arg("set_stream"), py::arg("asm_stream"))
       .def_property_readonly("sets_pending", &RoutedStep::sets_pending);
 }

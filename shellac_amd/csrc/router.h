@@ -16,6 +16,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "layout.h"
@@ -41,6 +42,7 @@ void scan_u64(const uint64_t* in, int64_t n, uint64_t* parts, uint64_t* out, hip
 int64_t scan_parts_words(int64_t n);
 
 class HbmCache;
+class StepComm;
 
 // The routed serving step of one rank as a native executor, device-driven: no host sync
 // between plan and finish. ShardedCache issues the collectives (torch.distributed ->
@@ -145,6 +147,25 @@ class RoutedStep {
   void assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off, hipStream_t s);
   // `s` waits for the main-shard SET chain of the last store_sets.
   void join_sets(hipStream_t s);
+
+  // ---- native step -------------------------------------------------------------------
+  // The communicator step() issues its collectives on (RCCL, mirror or callbacks).
+  void set_comm(std::shared_ptr<StepComm> c);
+  bool has_comm() const { return comm_ != nullptr; }
+  // The whole step in one call, every collective issued from here (no Python between
+  // them): plan -> all-gather -> publish -> request a2a -> owner probe -> reply (its
+  // transfer on the executor's comm stream) -> local gather -> SET exchange on `sset`
+  // -> assemble on `sasm`. Not for a calibrating step (caps(n)[3] or [4]: the
+  // multi-call path). `data` holds caps(n)[2] + W (8 capG + capD) + 16 bytes; out_size /
+  // out_off n words each, valid once `sasm` has passed this step. Returns
+  // [n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped].
+  std::vector<int64_t> step(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
+                            const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
+                            const uint32_t* sexpire, const uint64_t* sval_off,
+                            const uint8_t* svalues, int64_t ns, bool fanout, bool coalesce,
+                            HbmCache* shard, uint8_t* data, uint64_t* out_size,
+                            uint64_t* out_off, hipStream_t s, hipStream_t sset,
+                            hipStream_t sasm);
   bool sets_pending() const { return sets_pending_; }
   int rank() const { return rank_; }
 
@@ -169,6 +190,12 @@ class RoutedStep {
   int64_t* host_dmat_ = nullptr;  // pinned: calibration demand matrix
   uint64_t* host_tab_ = nullptr;  // pinned: per-step SET tables (uploaded)
   hipStream_t side_ = nullptr;
+  hipStream_t comm_stream_ = nullptr;  // step(): the reply transfer
+  std::shared_ptr<StepComm> comm_;
+  hipEvent_t ev_probe_ = nullptr, ev_local_ = nullptr, ev_rfork_ = nullptr,
+             ev_reply_[2] = {nullptr, nullptr};
+  bool reply_pending_[2] = {false, false};
+  bool row_init_ = false;
   hipEvent_t ev_fork_ = nullptr, ev_pjoin_ = nullptr, ev_pub_ = nullptr, ev_sfork_ = nullptr,
              ev_join_ = nullptr, ev_asm_[2] = {nullptr, nullptr};
   bool asm_pending_[2] = {false, false};

@@ -7,6 +7,8 @@
 #include <string>
 
 #include "hbm_cache.h"
+#include "step_comm.h"
+#include "trace.h"
 
 #define RT_OK(expr)                                                                     \
   do {                                                                                  \
@@ -492,7 +494,9 @@ enum Slot {
   kCoTab, kFirst0, kFirst1, kOwnerS, kVpad, kTcnt, kTbytes, kSrec, kSval, kSvoff, kCntS,
   kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSrcA, kSrcB, kHdr, kUsed, kRb, kTab,
   kSegOff, kSegSrc,
-  kRkeys, kV0, kV1, kFl, kEx, kRoff, kReserve, kSrec1, kSval1, kSvoff1, kNumSlots
+  kRkeys, kV0, kV1, kFl, kEx, kRoff, kReserve, kSrec1, kSval1, kSvoff1,
+  // RoutedStep::step's own exchange buffers (the multi-call path gets them from Python)
+  kRowB, kMatB, kGB, kR0, kR1, kS0, kS1, kRs0, kRs1, kNumSlots
 };
 
 // Slot of G a requester writes peer p's rows into: self = W-1, others W + o(p).
@@ -528,20 +532,17 @@ __global__ __launch_bounds__(kB) void k_gr_scatter_slots(
   }
 }
 
-// Rows each owner slot holds this step: slot s < W-1 is source o^-1(s), slot W-1 is self.
-__global__ void k_derive(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
-                         int64_t capG, int64_t* __restrict__ own_cnt) {
+// Log bytes this step's received SETs may append to the main shard (records, padded
+// values, the CLOCK hand's reinsertion budget): the owner probe treats what they will
+// overwrite as evicted, so the SET chain can run beside the reply gather.
+// One launch with k_derive's work: the rows each owner slot holds (own_cnt).
+__global__ void k_owner_prep(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
+                             int64_t capG, uint64_t rmax, int64_t* __restrict__ own_cnt,
+                             uint64_t* __restrict__ out) {
   for (int s = threadIdx.x; s < W; s += blockDim.x) {
     const int q = s == W - 1 ? me : (s < me ? s : s + 1);
     own_cnt[s] = min(mat[(int64_t)q * K + me], capG);
   }
-}
-
-// Log bytes this step's received SETs may append to the main shard (records, padded
-// values, the CLOCK hand's reinsertion budget): the owner probe treats what they will
-// overwrite as evicted, so the SET chain can run beside the reply gather.
-__global__ void k_owner_reserve(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
-                                uint64_t rmax, uint64_t* __restrict__ out) {
   if (threadIdx.x != 0) return;
   uint64_t rows = 0, bytes = 0;
   for (int q = 0; q < W; ++q) {
@@ -567,14 +568,20 @@ __global__ void k_demand(const uint64_t* __restrict__ lk_off, int32_t W, int32_t
 // unused tail: neither read nor written), so the segments tile the buffer.
 // used[s] = the bytes of slot s's longest row prefix that fits capD (rows past it are
 // dropped: header 0, no bytes).
-__global__ void k_reply_used(const uint64_t* __restrict__ lk_off, int32_t W, int64_t capG,
-                             int64_t capD, int64_t slotR, const uint64_t* __restrict__ hdr,
-                             uint64_t* __restrict__ used, uint64_t* __restrict__ offA,
-                             uint64_t* __restrict__ srcA, uint64_t* __restrict__ offB,
-                             uint64_t* __restrict__ srcB) {
+// Also k_demand's work (rb[q] = reply bytes for requester q) and rb[W] = 0 (the dropped
+// rows counter k_reply_prep adds to): one launch instead of three.
+__global__ void k_reply_used(const uint64_t* __restrict__ lk_off, int32_t W, int32_t me,
+                             int64_t capG, int64_t capD, int64_t slotR,
+                             const uint64_t* __restrict__ hdr, uint64_t* __restrict__ used,
+                             uint64_t* __restrict__ offA, uint64_t* __restrict__ srcA,
+                             uint64_t* __restrict__ offB, uint64_t* __restrict__ srcB,
+                             int64_t* __restrict__ rb) {
   const int64_t per = capG + 2;
+  if (threadIdx.x == 0) rb[W] = 0;
   for (int s = threadIdx.x; s < W; s += blockDim.x) {
     const uint64_t base = lk_off[s * capG];
+    const int q = s == W - 1 ? me : (s < me ? s : s + 1);
+    rb[q] = (int64_t)(lk_off[(int64_t)(s + 1) * capG] - base);
     int64_t lo = 0, hi = capG;  // the largest j with lk_off[s capG + j] - base <= capD
     while (lo < hi) {
       const int64_t mid = (lo + hi + 1) >> 1;
@@ -745,8 +752,10 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   RT_OK(hipHostMalloc(&host_tab_, 2 * (8 * (size_t)world + 8) * sizeof(uint64_t),
                       hipHostMallocDefault));
   RT_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  RT_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_fork_, &ev_pjoin_, &ev_pub_, &ev_sfork_, &ev_join_, &ev_asm_[0],
-                        &ev_asm_[1]})
+                        &ev_asm_[1], &ev_probe_, &ev_local_, &ev_rfork_, &ev_reply_[0],
+                        &ev_reply_[1]})
     RT_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
@@ -757,8 +766,10 @@ RoutedStep::~RoutedStep() {
   (void)hipHostFree(host_mat_);
   (void)hipHostFree(host_dmat_);
   (void)hipHostFree(host_tab_);
-  for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1]})
+  for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1],
+                       ev_probe_, ev_local_, ev_rfork_, ev_reply_[0], ev_reply_[1]})
     (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(comm_stream_);
   (void)hipStreamDestroy(side_);
 }
 
@@ -963,10 +974,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
 void RoutedStep::publish(const int64_t* mat, hipStream_t s) {
   const int W = w_;
   const int64_t K = row_words();
-  own_cnt_ = buf<int64_t>(kOwnCnt, W);
-  mat_dev_ = mat;
-  hipLaunchKernelGGL(k_derive, dim3(1), dim3(64), 0, s, mat, K, W, rank_, capG_, own_cnt_);
-  RT_OK(hipGetLastError());
+  mat_dev_ = mat;  // owner_probe derives the owner slot counts from it
   RT_OK(hipMemcpyAsync(host_mat_, mat, (size_t)W * K * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   RT_OK(hipEventRecord(ev_pub_, s));
   published_ = true;
@@ -991,8 +999,9 @@ void RoutedStep::owner_probe(const uint8_t* G, HbmCache* shard, uint32_t now, hi
   // this step's SETs are appended beside the reply gather (store_sets): reserve their
   // bytes, computed on the device from the all-gathered matrix (no host read)
   uint64_t* reserve = buf<uint64_t>(kReserve, 1);
-  hipLaunchKernelGGL(k_owner_reserve, dim3(1), dim3(64), 0, s, mat_dev_, row_words(), W, rank_,
-                     (uint64_t)shard->reinsert_max(), reserve);
+  own_cnt_ = buf<int64_t>(kOwnCnt, W);
+  hipLaunchKernelGGL(k_owner_prep, dim3(1), dim3(64), 0, s, mat_dev_, row_words(), W, rank_, capG_,
+                     (uint64_t)shard->reinsert_max(), own_cnt_, reserve);
   RT_OK(hipGetLastError());
   shard->lookup_slots(reinterpret_cast<const Digest*>(G), W, capG_, own_cnt_, lk_loc_, lk_size_,
                       lk_off_, now, s, reserve);
@@ -1025,10 +1034,8 @@ void RoutedStep::owner_reply(HbmCache* shard, uint8_t* R, uint8_t* data, hipStre
   uint64_t* offB = buf<uint64_t>(kDstB, per + 1);
   uint64_t* srcB = buf<uint64_t>(kSrcB, per);
   uint8_t* self_slot = data + capL_ + (int64_t)(W - 1) * slotR;
-  hipLaunchKernelGGL(k_demand, dim3(1), dim3(64), 0, s, lk_off_, W, rank_, capG_, rb_);
-  RT_OK(hipMemsetAsync(rb_ + W, 0, sizeof(int64_t), s));
-  hipLaunchKernelGGL(k_reply_used, dim3(1), dim3(64), 0, s, lk_off_, W, capG_, capD_, slotR, hdr,
-                     used, offA, srcA, offB, srcB);
+  hipLaunchKernelGGL(k_reply_used, dim3(1), dim3(64), 0, s, lk_off_, W, rank_, capG_, capD_, slotR,
+                     hdr, used, offA, srcA, offB, srcB, rb_);
   hipLaunchKernelGGL(k_reply_prep, dim3(grid1(rows)), dim3(kB), 0, s, lk_loc_, lk_size_, lk_off_,
                      own_cnt_, used, W, capG_, slotR, shard->log_ptr(), hdr, offA, srcA, offB,
                      srcB, reinterpret_cast<unsigned long long*>(rb_ + W));
@@ -1193,6 +1200,135 @@ void RoutedStep::assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out
   }
   RT_OK(hipEventRecord(ev_asm_[P], s));
   asm_pending_[P] = true;
+}
+
+// ---- the whole step, natively ----------------------------------------------------------
+void RoutedStep::set_comm(std::shared_ptr<StepComm> c) {
+  SH_CHECK(!c || (c->world() == w_ && c->rank() == rank_), "RoutedStep: comm of another job");
+  comm_ = std::move(c);
+}
+
+std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* replica,
+                                      uint32_t now, const Digest* skeys, const uint32_t* svlen,
+                                      const uint32_t* sflags, const uint32_t* sexpire,
+                                      const uint64_t* sval_off, const uint8_t* svalues, int64_t ns,
+                                      bool fanout, bool coalesce, HbmCache* shard, uint8_t* data,
+                                      uint64_t* out_size, uint64_t* out_off, hipStream_t s,
+                                      hipStream_t sset, hipStream_t sasm) {
+  SH_CHECK(comm_, "RoutedStep::step: no communicator (set_comm)");
+  const int W = w_, me = rank_;
+  const int64_t K = row_words();
+  {
+    const std::vector<int64_t> c = caps(n);
+    SH_CHECK(!c[3] && !c[4], "RoutedStep::step: a calibrating step takes the multi-call path");
+  }
+  // o(p): the position of peer p among the other ranks
+  auto o = [me](int p) { return p < me ? p : p - 1; };
+  int64_t* row = buf<int64_t>(kRowB, K);
+  int64_t* mat = buf<int64_t>(kMatB, (size_t)K * W);
+  if (!row_init_) {
+    RT_OK(hipMemsetAsync(row, 0, K * sizeof(int64_t), s));
+    row_init_ = true;
+  }
+  {
+    const int64_t gslot = 16 * caps(n)[0];
+    uint8_t* G = buf<uint8_t>(kGB, (size_t)(2 * W - 1) * gslot);
+    {
+      TraceRange t("serve.plan");
+      plan(keys, n, replica, now, skeys, svlen, sflags, sexpire, sval_off, svalues, ns, fanout, G,
+           row, s, coalesce);
+    }
+    {
+      TraceRange t("serve.row_allgather");
+      comm_->all_gather(mat, row, K, 4, s, StepComm::kCtrl);
+      publish(mat, s);
+    }
+    if (W > 1) {
+      TraceRange t("serve.request_a2a");
+      // G = [recv: W-1 slots | self | send: W-1 slots], others in o-order on both sides
+      std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, gslot);
+      for (int p = 0; p < W; ++p)
+        if (p != me) {
+          off_r[p] = o(p) * gslot;
+          off_s[p] = (int64_t)W * gslot + o(p) * gslot;
+        }
+      sz[me] = 0;
+      comm_->all_to_all(G, off_r, sz, G, off_s, sz, s, StepComm::kCtrl);
+    }
+    TraceRange t("serve.owner");
+    owner_probe(G, shard, now, s);
+  }
+  const int P = par_;
+  // the SET stream forks here: the probe reserved this step's SET bytes
+  RT_OK(hipEventRecord(ev_probe_, s));
+  RT_OK(hipStreamWaitEvent(sset, ev_probe_, 0));
+  const int64_t slotR = capG_ * 8 + capD_;
+  uint8_t* R = buf<uint8_t>(P ? kR1 : kR0, (size_t)std::max<int64_t>((W - 1) * slotR, 16));
+  // the reply transfer of two steps back read this parity's R
+  if (reply_pending_[P]) {
+    RT_OK(hipStreamWaitEvent(s, ev_reply_[P], 0));
+    reply_pending_[P] = false;
+  }
+  {
+    TraceRange t("serve.reply");
+    owner_reply(shard, R, data, s);
+    if (W > 1) {
+      // the reply transfer on its own stream and channel: the local gather, the SET
+      // exchange and the next step's planning run beside it
+      RT_OK(hipEventRecord(ev_rfork_, s));
+      RT_OK(hipStreamWaitEvent(comm_stream_, ev_rfork_, 0));
+      std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, slotR);
+      for (int p = 0; p < W; ++p)
+        if (p != me) {
+          off_s[p] = o(p) * slotR;
+          off_r[p] = capL_ + o(p) * slotR;
+        }
+      sz[me] = 0;
+      comm_->all_to_all(data, off_r, sz, R, off_s, sz, comm_stream_, StepComm::kData);
+      RT_OK(hipEventRecord(ev_reply_[P], comm_stream_));
+      reply_pending_[P] = true;
+    }
+    gather_local(data, s);
+    RT_OK(hipEventRecord(ev_local_, s));
+  }
+  std::vector<int64_t> stats;
+  {
+    TraceRange t("serve.set_exchange");
+    const std::vector<int64_t> h = set_splits();  // host: waits for the published matrix
+    stats.assign(h.begin() + 2 * W, h.end());
+    int64_t so = 0, ro = 0;
+    for (int p = 0; p < W; ++p)
+      if (p != me) {
+        so += sset_[p];
+        ro += rset_[p];
+      }
+    uint8_t* S = buf<uint8_t>(P ? kS1 : kS0, (size_t)so + 16);
+    uint8_t* Rs = buf<uint8_t>(P ? kRs1 : kRs0, (size_t)ro + 16);
+    pack_sets(S, sset);
+    if (W > 1 && (so > 0 || ro > 0)) {
+      // send blocks at Ps[p] (pack_sets' table), receive blocks in rank order
+      const uint64_t* Ps = host_tab_ + (size_t)P * (8 * (size_t)W + 8) + 2 * (size_t)W + 1;
+      std::vector<int64_t> off_s(W, 0), off_r(W, 0), sb(W, 0), rb(W, 0);
+      int64_t pos = 0;
+      for (int p = 0; p < W; ++p) {
+        if (p == me) continue;
+        off_s[p] = (int64_t)Ps[p];
+        sb[p] = sset_[p];
+        off_r[p] = pos;
+        rb[p] = rset_[p];
+        pos += rset_[p];
+      }
+      comm_->all_to_all(Rs, off_r, rb, S, off_s, sb, sset, StepComm::kSet);
+    }
+    store_sets(Rs, shard, replica, now, s, sset);
+  }
+  {
+    TraceRange t("serve.assemble");
+    RT_OK(hipStreamWaitEvent(sasm, ev_local_, 0));
+    if (W > 1) RT_OK(hipStreamWaitEvent(sasm, ev_reply_[P], 0));
+    assemble(data, out_size, out_off, sasm);
+  }
+  return stats;
 }
 
 void RoutedStep::join_sets(hipStream_t s) {

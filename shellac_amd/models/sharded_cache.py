@@ -38,7 +38,7 @@ from ..ops import routing as R
 from ..ops.cache import CacheShard, StreamEvent, coalesce, expand, expand_out
 from ..parallel.exchange import (all_gather, all_gather_rows, all_reduce, all_to_all_rows,
                                  all_to_all_single, allreduce_stats, dist_info, exchange_counts,
-                                 segment_sums)
+                                 segment_sums, step_comm)
 from ..parallel.ring import ShardRing
 from .._native import core as _core
 
@@ -172,6 +172,9 @@ class ShardedCache:
         # the framework-op version (_serve_routed) is the CPU path and the test oracle
         self.fused = True
         self._engine = None
+        # the native step's communicator (RCCL / mirror / gloo callbacks); False: none,
+        # every step takes the multi-call path (collectives from Python)
+        self._ncomm = None
         self._row = self._mat = None
         # the routed step's main-shard SET chain is joined by the NEXT step's owner probe
         # (RoutedStep::join_sets), so it runs under that step's planning; its buffers stay
@@ -503,6 +506,13 @@ class ShardedCache:
             ev, _bufs = self._inflight.pop(0)
             cur.wait_event(ev)  # long complete: frees the buffers for reuse on this stream
         cap_g, cap_d, cap_l, cal, cal_l = e.caps(n)
+        if self._ncomm is None:
+            self._ncomm = step_comm(self.group, dev) or False
+            if self._ncomm is not False:
+                e.set_comm(self._ncomm)
+        if self._ncomm is not False and not (cal or cal_l):
+            return self._serve_native(e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l,
+                                      fanout, rep)
         ph = _Phases("serve.")
         ph.next("plan")
         # G = [recv: w-1 slots | self slot | send: w-1 slots] of cap_g digests
@@ -589,6 +599,40 @@ class ShardedCache:
         self.stats["slot_overflow_rows"] += over
         self.stats["reply_dropped_rows"] += dropped
         ph.end()
+        return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
+
+    def _serve_native(self, e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l, fanout, rep):
+        """The routed step as one native call (``RoutedStep.step``): every kernel launch
+        and collective of the step is issued from C++, none from Python; only the response
+        buffers are torch tensors (the caller keeps them). Calibrating steps take the
+        multi-call path in ``_serve_routed_fused``."""
+        dev, w = self.device, self.world
+        cur = torch.cuda.current_stream(dev)
+        slot_r = 8 * cap_g + cap_d
+        data = torch.empty(cap_l + w * slot_r + 16, dtype=torch.uint8, device=dev)
+        out = torch.empty((2, n), dtype=torch.int64, device=dev)
+        side = self._asm
+        h = e.step(keys.data_ptr(), n, rep, now, batch.keys.data_ptr(), batch.vlen.data_ptr(),
+                   batch.flags.data_ptr() if batch.flags is not None else 0,
+                   batch.expire.data_ptr() if batch.expire is not None else 0,
+                   batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
+                   self.coalesce, self.shard._impl, data.data_ptr(), out[0].data_ptr(),
+                   out[1].data_ptr(), cur.cuda_stream, self._sset.cuda_stream, side.cuda_stream)
+        # the reply transfer (the executor's comm stream) and the assembly (side) write and
+        # read these; side waited for the transfer, so its event covers both
+        data.record_stream(side)
+        out.record_stream(side)
+        done = torch.cuda.Event()
+        done.record(side)
+        self._inflight.append((done, (data,)))
+        # the main-shard SET chain reads the batch until the next step's probe joins it
+        self._held = (batch,) if e.sets_pending else None
+        n_local, n_dup, off_rank, over, dropped = h
+        self.stats["remote_gets"] += off_rank
+        self.stats["replica_hits"] += n_local - n_dup
+        self.stats["coalesced_gets"] += n_dup
+        self.stats["slot_overflow_rows"] += over
+        self.stats["reply_dropped_rows"] += dropped
         return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
 
     def _set_rows(self, batch: SetBatch):

@@ -196,3 +196,101 @@ def segment_sums(off: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
     ends = torch.cumsum(counts, 0)
     starts = ends - counts
     return off.index_select(0, ends) - off.index_select(0, starts)
+
+
+# ---- communicators of the native routed step (csrc/step_comm.h) ----------------------------
+_RCCL_COMMS: dict = {}
+_RCCL_SEQ = [0]
+
+
+class _BounceNative:
+    """``BounceComm`` for the native executor: the step's collectives call back into
+    Python with raw device pointers; bytes are staged through host memory and exchanged
+    over gloo (tests only: several ranks sharing one GPU)."""
+
+    def __init__(self, comm: BounceComm):
+        self.comm = comm
+
+    def native_all_gather(self, out: int, inp: int, words: int, peer_blocks: int,
+                          stream: int) -> None:
+        from .._native import core
+
+        c = core()
+        row = torch.frombuffer(bytearray(c.stream_copy_to_host(inp, 8 * words, stream)),
+                               dtype=torch.int64)
+        host = [torch.empty(words, dtype=torch.int64) for _ in range(self.comm.world)]
+        dist.all_gather(host, row, group=self.comm.pg)
+        c.stream_copy_from_host(out, torch.cat(host).numpy().tobytes(), stream)
+
+    def native_all_to_all(self, rbuf: int, roff, rbytes, sbuf: int, soff, sbytes,
+                          stream: int) -> None:
+        from .._native import core
+
+        c = core()
+        me, w = self.comm.rank, self.comm.world
+        sb = [0 if p == me else int(sbytes[p]) for p in range(w)]
+        rb = [0 if q == me else int(rbytes[q]) for q in range(w)]
+        blob = b"".join(c.stream_copy_to_host(sbuf + int(soff[p]), sb[p], stream)
+                        for p in range(w) if sb[p])
+        send = (torch.frombuffer(bytearray(blob), dtype=torch.uint8) if blob
+                else torch.empty(0, dtype=torch.uint8))
+        recv = torch.empty(sum(rb), dtype=torch.uint8)
+        dist.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb,
+                               group=self.comm.pg)
+        pos = 0
+        for q in range(w):
+            if rb[q]:
+                c.stream_copy_from_host(rbuf + int(roff[q]), recv[pos:pos + rb[q]].numpy().tobytes(),
+                                        stream)
+                pos += rb[q]
+
+
+def _rccl_comm(world: int, rank: int, device: int):
+    """RCCL communicators of our own (one per channel of the routed step), shared by every
+    executor of this process. Collective on first use: rank 0 makes the unique ids and
+    publishes them in the torch.distributed store, every rank joins."""
+    from .._native import core
+
+    key = (world, rank, device)
+    comm = _RCCL_COMMS.get(key)
+    if comm is None:
+        c = core()
+        store = _default_store()
+        name = f"shellac_amd/rccl_ids/{_RCCL_SEQ[0]}"
+        _RCCL_SEQ[0] += 1
+        nch = 3
+        if rank == 0:
+            ids = [c.rccl_unique_id() for _ in range(nch)]
+            store.set(name, b"".join(ids))
+        blob = bytes(store.get(name))
+        ids = [blob[i * 128:(i + 1) * 128] for i in range(nch)]
+        comm = _RCCL_COMMS[key] = c.make_rccl_comm(world, rank, device, ids)
+    return comm
+
+
+def _default_store():
+    from torch.distributed import distributed_c10d
+
+    return distributed_c10d._get_default_store()
+
+
+def step_comm(group, device: torch.device):
+    """The communicator the native routed step (``RoutedStep.step``) issues its collectives
+    on, or None when only the multi-call path can serve this group (a custom torch group,
+    a non-RCCL backend, a CPU shard)."""
+    from .._native import core
+
+    if device.type != "cuda":
+        return None
+    c = core()
+    if isinstance(group, MirrorComm):
+        return c.make_mirror_comm(group.world, group.rank)
+    if isinstance(group, BounceComm):
+        return c.make_python_comm(_BounceNative(group), group.world, group.rank)
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    if group is not None and group is not _default_group():
+        return None
+    if dist.get_backend() != "nccl":
+        return None
+    return _rccl_comm(dist.get_world_size(), dist.get_rank(), device.index)
