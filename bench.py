@@ -251,6 +251,11 @@ def main():
             raise SystemExit(2)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+        # the serving step's streams take their hardware queues before the process
+        # group's communicators make streams of their own
+        from shellac_amd.ops.cache import reserve_step_streams
+
+        reserve_step_streams(dev)
         if world > 1:
             dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         elif routed1:
@@ -361,9 +366,15 @@ def main():
                          pin(b.expire)) for b in sets]
         sc.host_edge = True
 
+    # the request batches are complete from here on (the routed step may plan a batch
+    # beside the previous step's reply gather)
+    ready = torch.cuda.Event() if dev.type == "cuda" else None
+    if ready is not None:
+        ready.record()
+
     def step(i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
-        return sc.serve(gets[i % P], sets[i % P])
+        return sc.serve(gets[i % P], sets[i % P], inputs_ready=ready)
 
     # Per-step GPU timing events are recorded in a separate pass after the timed one: an
     # event record is a marker packet on the stream, and one between every two steps cost
@@ -385,7 +396,7 @@ def main():
         for i in range(steps):
             if events:
                 evs[i].record(cur)
-            res = cache.serve(gets[(first + i) % P], sets[(first + i) % P])
+            res = cache.serve(gets[(first + i) % P], sets[(first + i) % P], inputs_ready=ready)
         if events:
             evs[steps].record(cur)
         sync()
@@ -474,7 +485,7 @@ def main():
         if nfill > 20000:
             return None
         for i in range(nfill):
-            sc_.serve(gets[(base + i) % P], sets[(base + i) % P])
+            sc_.serve(gets[(base + i) % P], sets[(base + i) % P], inputs_ready=ready)
         sync()
         sc_.sync_sets()
         w0 = shard_.counters()

@@ -17,10 +17,11 @@ def short(n):
 plans=sorted(int(r['Start_Timestamp']) for r in m if r['Function']=='serve.plan')
 print(len(plans),'plan markers')
 st=plans[-nsteps-1:]
-ks=sorted((int(r['Start_Timestamp']),int(r['End_Timestamp']),short(r['Kernel_Name'])) for r in k)
+ks=sorted((int(r['Start_Timestamp']),int(r['End_Timestamp']),short(r['Kernel_Name']),
+           r.get('Queue_Id',''),r.get('Stream_Id','')) for r in k)
 tot=defaultdict(lambda:[0,0])
 t0,t1=st[0],st[-1]
-for s,e,n in ks:
+for s,e,n,_,_ in ks:
     if t0<=s<t1: tot[n][0]+=1; tot[n][1]+=e-s
 busy=sum(v[1] for v in tot.values())
 print(f"wall/step {(t1-t0)/1e3/nsteps:.1f} us, busy {busy/1e3/nsteps:.1f} us")
@@ -36,6 +37,6 @@ for p,v in sorted(ph.items(),key=lambda x:-x[1]): print(f"{v/1e3/nsteps:8.1f} us
 print("--- last step timeline")
 a,b=st[-2],st[-1]
 prev=a
-for s,e,n in ks:
+for s,e,n,q,sid in ks:
     if a<=s<b:
-        print(f"{(s-a)/1e3:8.1f} {(e-s)/1e3:7.1f} gap {(s-prev)/1e3:6.1f} {n}"); prev=max(prev,e)
+        print(f"{(s-a)/1e3:8.1f} {(e-s)/1e3:7.1f} gap {(s-prev)/1e3:6.1f} q{q:>3} s{sid:>3} {n}"); prev=max(prev,e)

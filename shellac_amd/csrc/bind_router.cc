@@ -101,14 +101,20 @@ void bind_router(py::module_& m) {
       throw Error("stream_copy_from_host failed");
   });
 
+  m.def("step_streams", [](int device) {
+    const StepStreams& ss = step_streams(device);
+    return std::vector<uintptr_t>{(uintptr_t)ss.plan, (uintptr_t)ss.set, (uintptr_t)ss.asm_};
+  });
+
   py::class_<RoutedStep>(m, "RoutedStep")
       .def(py::init<int, int, int>(), py::arg("world"), py::arg("rank"), py::arg("device"))
       .def("set_ring", [](RoutedStep& r, uintptr_t pts, uintptr_t owner, int32_t npts) {
         r.set_ring(P<const uint32_t>(pts), P<const int32_t>(owner), npts);
       })
-      .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot, uintptr_t dir) {
-        r.set_hot(P<const Digest>(hot), nhot, P<const int64_t>(dir));
-      }, py::arg("hot"), py::arg("nhot"), py::arg("dir") = 0)
+      .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot, uintptr_t dir, bool changed) {
+        py::gil_scoped_release nogil;
+        r.set_hot(P<const Digest>(hot), nhot, P<const int64_t>(dir), changed);
+      }, py::arg("hot"), py::arg("nhot"), py::arg("dir") = 0, py::arg("changed") = false)
       .def_property_readonly("row_words", &RoutedStep::row_words)
       .def("caps", &RoutedStep::caps)
       .def("reset_caps", &RoutedStep::reset_caps)
@@ -181,17 +187,20 @@ void bind_router(py::module_& m) {
                       uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,
                       bool coalesce, HbmCache* shard, uintptr_t data, uintptr_t out_size,
-                      uintptr_t out_off, uintptr_t s, uintptr_t sset, uintptr_t sasm) {
+                      uintptr_t out_off, uintptr_t s, uintptr_t sset, uintptr_t sasm,
+                      uintptr_t ready) {
         py::gil_scoped_release nogil;
         return r.step(P<const Digest>(keys), n, replica, now, P<const Digest>(skeys),
                       P<const uint32_t>(svlen), P<const uint32_t>(sflags),
                       P<const uint32_t>(sexpire), P<const uint64_t>(sval_off),
                       P<const uint8_t>(svalues), ns, fanout, coalesce, shard, P<uint8_t>(data),
-                      P<uint64_t>(out_size), P<uint64_t>(out_off), S(s), S(sset), S(sasm));
+                      P<uint64_t>(out_size), P<uint64_t>(out_off), S(s), S(sset), S(sasm),
+                      reinterpret_cast<hipEvent_t>(ready));
       }, py::arg("keys"), py::arg("n"), py::arg("replica").none(true), py::arg("now"),
          py::arg("skeys"), py::arg("svlen"), py::arg("sflags"), py::arg("sexpire"),
          py::arg("sval_off"), py::arg("svalues"), py::arg("ns"), py::arg("fanout"),
          py::arg("coalesce"), py::arg("shard"), py::arg("data"), py::arg("out_size"),
-         py::arg("out_off"), py::arg("stream"), py::arg("set_stream"), py::arg("asm_stream"))
+         py::arg("out_off"), py::arg("stream"), py::arg("set_stream"), py::arg("asm_stream"),
+         py::arg("inputs_ready") = 0)
       .def_property_readonly("sets_pending", &RoutedStep::sets_pending);
 }

@@ -44,6 +44,12 @@ int64_t scan_parts_words(int64_t n);
 class HbmCache;
 class StepComm;
 
+// The native step's streams, one set per device for the whole process (never destroyed).
+struct StepStreams {
+  hipStream_t plan = nullptr, set = nullptr, asm_ = nullptr;
+};
+const StepStreams& step_streams(int device);
+
 // The routed serving step of one rank as a native executor, device-driven: no host sync
 // between plan and finish. ShardedCache issues the collectives (torch.distributed ->
 // RCCL) and hands every buffer in between to this object, which keeps its scratch in a
@@ -81,6 +87,7 @@ class StepComm;
 //   -> on the SET stream: pack_sets(S) -> [a2a S -> Rs, exact sizes] -> store_sets(Rs),
 //      i.e. the main-shard SET chain beside the reply gather
 //   -> on a side stream after the reply a2a: assemble(data, out) -> wait() before reading.
+//   (step(): the reply transfer and the assembly share the caller's `sasm` stream.)
 class RoutedStep {
  public:
   static constexpr int kExtras = 8;
@@ -90,8 +97,11 @@ class RoutedStep {
   RoutedStep& operator=(const RoutedStep&) = delete;
 
   void set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts);
-  // Sorted hot set (by signed lo) + optional 65537-entry directory (see is_hot).
-  void set_hot(const Digest* hot, int64_t nhot, const int64_t* dir = nullptr);
+  // Hot set (sorted by signed lo; the directory is kept for the framework-op path). The
+  // SET planner probes a hash set built from it on the first call and whenever
+  // `changed` (or the pointer / size) says the set is new.
+  void set_hot(const Digest* hot, int64_t nhot, const int64_t* dir = nullptr,
+               bool changed = false);
   int64_t row_words() const { return 4 * (int64_t)w_ + kExtras; }
 
   // ---- capacities (identical on every rank: derived from all-gathered rows) ----
@@ -141,7 +151,7 @@ class RoutedStep {
   // reply gather (the probe reserved their bytes; joined by the next owner_probe), and
   // the replica (tier 1) on `s` after the local gather.
   void store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replica, uint32_t now,
-                  hipStream_t s, hipStream_t sset);
+                  hipStream_t s, hipStream_t sset, bool replica_on_sset = false);
   // Per-request (size, off) into `data`, in request order (duplicates: their claimer's
   // record); run on a stream that has waited for the reply all-to-all.
   void assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off, hipStream_t s);
@@ -157,7 +167,11 @@ class RoutedStep {
   // transfer on the executor's comm stream) -> local gather -> SET exchange on `sset`
   // -> assemble on `sasm`. Not for a calibrating step (caps(n)[3] or [4]: the
   // multi-call path). `data` holds caps(n)[2] + W (8 capG + capD) + 16 bytes; out_size /
-  // out_off n words each, valid once `sasm` has passed this step. Returns
+  // out_off n words each, valid once `sasm` has passed this step. `sset` / `sasm` 0: the
+  // process-wide step streams (step_streams). `inputs_ready`
+  // (optional): an event after which the GET keys and the SET batch are complete; then
+  // the plan runs on a stream of its own beside the previous step's reply gather instead
+  // of after everything queued on `s`. Returns
   // [n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped].
   std::vector<int64_t> step(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
                             const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
@@ -165,7 +179,7 @@ class RoutedStep {
                             const uint8_t* svalues, int64_t ns, bool fanout, bool coalesce,
                             HbmCache* shard, uint8_t* data, uint64_t* out_size,
                             uint64_t* out_off, hipStream_t s, hipStream_t sset,
-                            hipStream_t sasm);
+                            hipStream_t sasm, hipEvent_t inputs_ready = nullptr);
   bool sets_pending() const { return sets_pending_; }
   int rank() const { return rank_; }
 
@@ -185,12 +199,20 @@ class RoutedStep {
   const Digest* hot_ = nullptr;
   int64_t nhot_ = 0;
   const int64_t* hot_dir_ = nullptr;
+  Digest* hot_tab_ = nullptr;  // hash set of the hot digests (built by set_hot)
+  uint64_t hot_mask_ = 0;
+  const Digest* hot_built_ = nullptr;
+  int64_t nhot_built_ = 0;
   std::vector<Buf> bufs_;
   int64_t* host_mat_ = nullptr;   // pinned: the published all-gather matrix
   int64_t* host_dmat_ = nullptr;  // pinned: calibration demand matrix
   uint64_t* host_tab_ = nullptr;  // pinned: per-step SET tables (uploaded)
-  hipStream_t side_ = nullptr;
-  hipStream_t comm_stream_ = nullptr;  // step(): the reply transfer
+  hipStream_t side_ = nullptr;  // (streams: the process-wide pool, step_streams)
+  hipStream_t plan_stream_ = nullptr;  // step(): the pipelined plan
+  hipStream_t set_stream_ = nullptr;   // step() without `sset`: the SET side
+  hipStream_t asm_stream_ = nullptr;   // step() without `sasm`: reply transfer + assembly
+  hipEvent_t ev_pfork_ = nullptr, ev_plan_ = nullptr, ev_rep_ = nullptr, ev_start_ = nullptr;
+  bool pfork_valid_ = false, rep_pending_ = false, in_step_ = false;
   std::shared_ptr<StepComm> comm_;
   hipEvent_t ev_probe_ = nullptr, ev_local_ = nullptr, ev_rfork_ = nullptr,
              ev_reply_[2] = {nullptr, nullptr};

@@ -145,6 +145,15 @@ class _Phases:
             self.open = False
 
 
+def _event_handle(ev) -> int:
+    """hipEvent_t of a recorded torch.cuda.Event / StreamEvent (0: none)."""
+    if ev is None:
+        return 0
+    if isinstance(ev, StreamEvent):
+        return int(ev.handle)
+    return int(ev.cuda_event)
+
+
 class ShardedCache:
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
@@ -334,8 +343,14 @@ class ShardedCache:
         self.stats["replica_hits"] += n_local
         return GetResult(data, off, size)
 
-    def serve(self, keys: torch.Tensor, batch: SetBatch, now: Optional[int] = None) -> GetResult:
+    def serve(self, keys: torch.Tensor, batch: SetBatch, now: Optional[int] = None,
+              inputs_ready=None) -> GetResult:
         """One serving step: a GET batch and a SET batch, GETs ordered before SETs.
+
+        ``inputs_ready`` (optional ``torch.cuda.Event``, routed GPU step): an event after
+        which ``keys`` and ``batch`` are complete. The step's planning then starts as soon
+        as the previous step's owner side allows, beside its reply gather, instead of after
+        everything the caller queued on the current stream before this call.
 
         With one rank the GET's extent read (the only host sync) is hidden behind
         the SET kernels: the lookup reserves the SET's log bytes (objects the SET may
@@ -346,7 +361,7 @@ class ShardedCache:
         the whole step instead of 10 and 3 for get() followed by set()."""
         if self.routed:
             if self.fused and self.device.type == "cuda":
-                return self._serve_routed_fused(keys, batch, now)
+                return self._serve_routed_fused(keys, batch, now, inputs_ready)
             return self._serve_routed(keys, batch, now)
         n = keys.shape[0]
         self.stats["get_requests"] += n
@@ -465,7 +480,7 @@ class ShardedCache:
         return self._side
 
     def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
-                            now: Optional[int] = None) -> GetResult:
+                            now: Optional[int] = None, inputs_ready=None) -> GetResult:
         """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep), with
         no host synchronisation between planning and the result (after one calibrating
         step): GET requests and replies travel in fixed-capacity per-peer slots whose
@@ -493,14 +508,20 @@ class ShardedCache:
             k = e.row_words
             self._row = torch.zeros(k, dtype=i64, device=dev)
             self._mat = torch.zeros(w * k, dtype=i64, device=dev)
-            self._asm = torch.cuda.Stream(device=dev)
-            self._sset = torch.cuda.Stream(device=dev)
+            # the executor's process-wide streams (plan, SET side, reply + assembly): the
+            # multi-call path uses the same ones, so a process keeps to four streams, one
+            # hardware queue each (4 per process, taken round robin)
+            ss = [int(x) for x in c.step_streams(dev.index)]
+            self._sset = torch.cuda.ExternalStream(ss[1], device=dev)
+            self._asm = torch.cuda.ExternalStream(ss[2], device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
         fanout = self.replica is not None and self._hot is not None
+        changed = False
         if fanout and self._hot_dir is None:
             self._hot_dir = _hot_directory(self._hot)
+            changed = True  # a new hot set: the executor rebuilds its hash set
         e.set_hot(self._hot.data_ptr() if fanout else 0, self._hot.shape[0] if fanout else 0,
-                  self._hot_dir.data_ptr() if fanout else 0)
+                  self._hot_dir.data_ptr() if fanout else 0, changed)
         rep = self.replica._impl if self.replica is not None else None
         while len(self._inflight) >= 2:
             ev, _bufs = self._inflight.pop(0)
@@ -512,7 +533,7 @@ class ShardedCache:
                 e.set_comm(self._ncomm)
         if self._ncomm is not False and not (cal or cal_l):
             return self._serve_native(e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l,
-                                      fanout, rep)
+                                      fanout, rep, inputs_ready)
         ph = _Phases("serve.")
         ph.next("plan")
         # G = [recv: w-1 slots | self slot | send: w-1 slots] of cap_g digests
@@ -601,7 +622,8 @@ class ShardedCache:
         ph.end()
         return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
 
-    def _serve_native(self, e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l, fanout, rep):
+    def _serve_native(self, e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l, fanout, rep,
+                      inputs_ready=None):
         """The routed step as one native call (``RoutedStep.step``): every kernel launch
         and collective of the step is issued from C++, none from Python; only the response
         buffers are torch tensors (the caller keeps them). Calibrating steps take the
@@ -611,21 +633,25 @@ class ShardedCache:
         slot_r = 8 * cap_g + cap_d
         data = torch.empty(cap_l + w * slot_r + 16, dtype=torch.uint8, device=dev)
         out = torch.empty((2, n), dtype=torch.int64, device=dev)
+        # the reply transfer and the assembly run on the executor's assembly stream (one
+        # per device for the process, never destroyed, so tensors recorded on it are safe)
         side = self._asm
         h = e.step(keys.data_ptr(), n, rep, now, batch.keys.data_ptr(), batch.vlen.data_ptr(),
                    batch.flags.data_ptr() if batch.flags is not None else 0,
                    batch.expire.data_ptr() if batch.expire is not None else 0,
                    batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
                    self.coalesce, self.shard._impl, data.data_ptr(), out[0].data_ptr(),
-                   out[1].data_ptr(), cur.cuda_stream, self._sset.cuda_stream, side.cuda_stream)
-        # the reply transfer (the executor's comm stream) and the assembly (side) write and
-        # read these; side waited for the transfer, so its event covers both
+                   out[1].data_ptr(), cur.cuda_stream, 0, 0,
+                   _event_handle(inputs_ready))
+        # the reply transfer and the assembly (both on `side`) and the local gather (SET
+        # stream, awaited by the assembly) write and read these
         data.record_stream(side)
         out.record_stream(side)
         done = torch.cuda.Event()
         done.record(side)
         self._inflight.append((done, (data,)))
-        # the main-shard SET chain reads the batch until the next step's probe joins it
+        # the main-shard SET chain (the executor's SET stream, a hardware queue of its own)
+        # reads the batch until the next step's probe joins it
         self._held = (batch,) if e.sets_pending else None
         n_local, n_dup, off_rank, over, dropped = h
         self.stats["remote_gets"] += off_rank

@@ -230,6 +230,18 @@ class Lookup:
         return self.size[: self.n] > 0
 
 
+def reserve_step_streams(device) -> None:
+    """Create the routed serving step's streams (plan, SET side, reply + assembly) for
+    ``device`` now. A process gets four hardware queues, handed out round robin as
+    streams are first used; the step keeps four streams busy at once (with the caller's),
+    so it needs them created before anything else makes streams (torch.distributed's
+    communicators, other libraries). Idempotent; bench.py calls it right after choosing the
+    device, and every GPU ``CacheShard`` does."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        core().step_streams(dev.index if dev.index is not None else torch.cuda.current_device())
+
+
 class CacheShard:
     """One cache shard: an HBM arena on ``cuda:i`` or a DRAM arena on ``cpu``.
 
@@ -258,6 +270,7 @@ class CacheShard:
         if self.device.type == "cuda":
             idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
             self.device = torch.device("cuda", idx)
+            reserve_step_streams(self.device)
             self._impl = c.HbmCache(self.log_bytes, self.nbuckets, self.max_item, idx, ev,
                                     int(reinsert_max))
             self.is_gpu = True

@@ -313,7 +313,10 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
 
     wl = Workload(40000, cuda_dev)
     outs = []
-    for fused, co in ((False, False), (True, False), (True, True)):
+    # (fused, coalesce, inputs-ready event): steps after the first (calibrating) one run
+    # the native executor (RoutedStep::step); with the event its plan is pipelined
+    for fused, co, ready in ((False, False, False), (True, False, False), (True, True, False),
+                             (True, True, True)):
         sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(world),
                           replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev))
         sc.fused = fused
@@ -322,15 +325,23 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
             sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
         sc.refresh_replica(2000, keys=wl.digests.index_select(0, wl.sample_ids(50000, 1)))
         keys = wl.digests.index_select(0, wl.sample_ids(8192, 2)).contiguous()
-        got = []
-        for step in range(3):
-            r = sc.serve(keys, wl.set_batch(wl.uniform_ids(1024, 10 + step))).wait()
+        batches = [wl.set_batch(wl.uniform_ids(1024, 10 + step)) for step in range(4)]
+        ev = None
+        if ready:
+            ev = torch.cuda.Event()
+            ev.record()
+        got, pend = [], []
+        for step in range(4):
+            pend.append(sc.serve(keys, batches[step], inputs_ready=ev))
+        for r in pend:  # results stay valid while later steps run
+            r.wait()
             got.append([None if x is None else x[0]
                         for x in unpack_records(r.data, r.off, r.size)])
         outs.append((got, dict(sc.stats)))
-    (g0, s0), (g1, s1), (g2, s2) = outs
+    (g0, s0), (g1, s1), (g2, s2), (g3, s3) = outs
     assert g0 == g1
     assert s0 == s1
+    assert g3 == g2 and s3 == s2
     assert sum(v is not None for v in g1[0]) == 8192     # every GET hits
     assert s1["replica_hits"] > 0
     # coalesced: the same values; duplicates neither probed nor sent
@@ -437,6 +448,20 @@ def test_fused_routed_step_edge_cases(cuda_dev):
                           for x in unpack_records(r.data, r.off, r.size)]))
         results.append((got, dict(sc.stats)))
     assert results[0] == results[1]
+    # the same steps through the native executor (RoutedStep::step) every time: fixed
+    # capacities large enough for every shape, so no step calibrates
+    sc = ShardedCache(CacheShard(512 << 20, 1 << 15, 1 << 16, cuda_dev), group=MirrorComm(3),
+                      replica=CacheShard(128 << 20, 1 << 12, 1 << 16, cuda_dev))
+    sc.set(wl.set_batch(torch.arange(0, 20000, device=cuda_dev)))
+    sc.refresh_replica(500, keys=hot)
+    sc.serve(hot, empty_sb).wait()  # builds the executor
+    sc._engine.set_cap_override(4096, 32 << 20, 16 << 20)
+    got = []
+    for keys, batch in ((empty_keys, sb), (hot, empty_sb), (hot, sb),
+                        (wl.digests[:4000].contiguous(), empty_sb)):
+        r = sc.serve(keys, batch).wait()
+        got.append(([None if x is None else x[0] for x in unpack_records(r.data, r.off, r.size)]))
+    assert got == results[0][0]
     assert all(v is not None for v in results[1][0][1])  # hot keys all served
 
 
