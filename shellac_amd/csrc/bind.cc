@@ -60,6 +60,10 @@ PYBIND11_MODULE(_shellac_core, m) {
     return py::make_tuple(d.lo, d.hi);
   }, "128-bit digest (lo, hi) of a byte string");
   m.def("item_bytes", [](uint32_t vlen) { return item_bytes(vlen); });
+  m.def("bucket_pair", [](uint64_t lo, uint64_t hi, uint64_t nbuckets) {
+    const Digest d{lo, hi};
+    return std::vector<uint64_t>{bucket1(d, nbuckets - 1), bucket2(d, nbuckets - 1)};
+  });
 
   // ---------------- device (HIP) ----------------
   py::class_<HbmCache::StoreGraph>(m, "StoreGraph")
@@ -181,6 +185,8 @@ PYBIND11_MODULE(_shellac_core, m) {
         return py::make_tuple(live, bytes);
       })
       .def("flush", [](HbmCache& c, uintptr_t s) { c.flush(S(s)); })
+      .def("debug_bucket", &HbmCache::debug_bucket)
+      .def("debug_set_entry", &HbmCache::debug_set_entry)
       .def("export_keys", [](HbmCache& c, uintptr_t out, uint64_t cap, uint32_t now, uintptr_t s) {
         py::gil_scoped_release nogil;
         return c.export_keys(P<Digest>(out), cap, now, S(s));
@@ -331,6 +337,8 @@ PYBIND11_MODULE(_shellac_core, m) {
         return py::make_tuple(live, bytes);
       })
       .def("flush", &HostCache::flush)
+      .def("debug_bucket", &HostCache::debug_bucket)
+      .def("debug_set_entry", &HostCache::debug_set_entry)
       .def("export_keys", [](HostCache& c, uintptr_t out, uint64_t cap, uint32_t now) {
         return c.export_keys(P<Digest>(out), cap, now);
       })

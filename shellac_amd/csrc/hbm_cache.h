@@ -184,6 +184,12 @@ class HbmCache {
   void load(const std::string& path, uint64_t user[4], hipStream_t s);
   // Drop everything (memcached FLUSH).
   void flush(hipStream_t s);
+  // Tests: read / overwrite one index bucket (4 entries of {d0, d1, loc, vlen | expire
+  // << 32}), synchronously. Builds index states no API call produces in a fixed order
+  // (e.g. a dead same-digest entry in a key's first bucket beside its live one).
+  std::vector<uint64_t> debug_bucket(uint64_t b);
+  void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
+                       uint32_t vlen, uint32_t expire);
   CacheCounters counters(hipStream_t s);
   uint64_t head(hipStream_t s);
 

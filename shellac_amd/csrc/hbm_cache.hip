@@ -3143,6 +3143,30 @@ void HbmCache::load(const std::string& path, uint64_t user[4], hipStream_t s) {
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
 
+std::vector<uint64_t> HbmCache::debug_bucket(uint64_t b) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  SH_CHECK(b < cfg_.nbuckets, "bucket out of range");
+  HIP_OK(hipDeviceSynchronize());
+  Entry e[kEntriesPerBucket];
+  HIP_OK(hipMemcpy(e, index_ + b * kEntriesPerBucket, sizeof e, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> out;
+  for (const Entry& x : e)
+    for (uint64_t w : {x.d0, x.d1, x.loc, (uint64_t)x.vlen | ((uint64_t)x.expire << 32)})
+      out.push_back(w);
+  return out;
+}
+
+void HbmCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
+                               uint32_t vlen, uint32_t expire) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  SH_CHECK(b < cfg_.nbuckets && slot >= 0 && slot < (int)kEntriesPerBucket, "entry out of range");
+  HIP_OK(hipDeviceSynchronize());
+  const Entry e{d0, d1, loc, vlen, expire};
+  HIP_OK(hipMemcpy(index_ + b * kEntriesPerBucket + slot, &e, sizeof e, hipMemcpyHostToDevice));
+}
+
 void HbmCache::flush(hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);

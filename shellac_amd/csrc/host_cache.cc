@@ -374,6 +374,25 @@ void HostCache::load(const std::string& path, uint64_t user[4]) {
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
 
+std::vector<uint64_t> HostCache::debug_bucket(uint64_t b) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SH_CHECK(b < nbuckets_, "bucket out of range");
+  std::vector<uint64_t> out;
+  for (uint32_t k = 0; k < kEntriesPerBucket; ++k) {
+    const Entry& x = index_[b * kEntriesPerBucket + k];
+    for (uint64_t w : {x.d0, x.d1, x.loc, (uint64_t)x.vlen | ((uint64_t)x.expire << 32)})
+      out.push_back(w);
+  }
+  return out;
+}
+
+void HostCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
+                                uint32_t vlen, uint32_t expire) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SH_CHECK(b < nbuckets_ && slot >= 0 && slot < (int)kEntriesPerBucket, "entry out of range");
+  index_[b * kEntriesPerBucket + slot] = Entry{d0, d1, loc, vlen, expire};
+}
+
 void HostCache::flush() {
   std::lock_guard<std::mutex> lk(mu_);
   std::memset(index_, 0, nbuckets_ * kBucketBytes);

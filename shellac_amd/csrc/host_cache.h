@@ -32,6 +32,10 @@ class HostCache {
   void remove(const Digest* keys, int64_t n, uint8_t* found, uint32_t now);
   void sweep(uint32_t now, uint64_t* live_entries, uint64_t* live_bytes);
   void flush();
+  // Tests: see HbmCache::debug_bucket / debug_set_entry.
+  std::vector<uint64_t> debug_bucket(uint64_t b);
+  void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
+                       uint32_t vlen, uint32_t expire);
   uint64_t export_keys(Digest* out, uint64_t out_cap, uint32_t now);
   void save(const std::string& path, const uint64_t user[4]);
   void load(const std::string& path, uint64_t user[4]);

@@ -110,3 +110,51 @@ def test_clock_batch_over_quarter_log_host():
 @pytest.mark.gpu
 def test_clock_batch_over_quarter_log_gpu_matches_host(cuda_dev):
     assert _big_batch_run(cuda_dev) == _big_batch_run("cpu")
+
+
+def _dead_twin_survives_the_hand(dev):
+    """A key whose first bucket holds a DEAD entry with its digest (an expired or overwritten
+    older copy) while its live, referenced entry sits in its second bucket: when the CLOCK
+    hand reaches the item it must find the live entry (the one pointing at the item), not
+    stop at the digest match, and re-append the item (k_rc_scan / HostCache reclaim; the
+    bug this guards against let the hand overwrite live referenced items)."""
+    from shellac_amd._native import core
+
+    nb = 1 << 12
+    s = CacheShard(1 << 20, nb, 1 << 14, dev, evict="clock")
+    s.set_many([b"/pre/%d" % i for i in range(3)], [b"p" * 1000] * 3)  # /pre/0 at offset 0
+    key, val = b"/twin", b"t" * 1000
+    s.set_many([key], [val])
+    lo, hi = (int(x) & (2 ** 64 - 1) for x in digest_strings([key], "cpu")[0])
+    b1, b2 = core().bucket_pair(lo, hi, nb)
+    e1, e2 = s._impl.debug_bucket(b1), s._impl.debug_bucket(b2)
+    i = next(k for k in range(4) if e1[4 * k] == lo and e1[4 * k + 1] == hi and e1[4 * k + 2])
+    j = next(k for k in range(4) if e2[4 * k + 2] == 0)
+    loc, vx = e1[4 * i + 2], e1[4 * i + 3]
+    # the live entry moves to the second bucket; the first keeps a dead twin (expired at
+    # t=1, pointing at another item)
+    s._impl.debug_set_entry(b2, j, lo, hi, loc, vx & 0xFFFFFFFF, vx >> 32)
+    s._impl.debug_set_entry(b1, i, lo, hi, 1, 1000, 1)
+    assert s.get_many([key])[0] == val  # served from the second bucket, reference bit set
+    # ~1.2 MiB of unread objects, none of them hashed into /twin's first bucket (an insert
+    # there would reuse the dead twin's slot): the log wraps past /twin's item
+    cand = [b"/cold/%d" % k for k in range(1400)]
+    dg = digest_strings(cand, "cpu")
+    cold = [c for c, d in zip(cand, dg.tolist())
+            if b1 not in core().bucket_pair(d[0] & (2 ** 64 - 1), d[1] & (2 ** 64 - 1), nb)]
+    assert len(cold) >= 1200
+    for b in range(60):
+        s.set_many(cold[20 * b: 20 * b + 20], [b"c" * 1000] * 20)
+    assert s._impl.debug_bucket(b1)[4 * i: 4 * i + 2] == [lo, hi]  # the twin is still there
+    assert s.head() > (1 << 20) + 4096
+    assert s.get_many([key])[0] == val
+    assert s.counters()["reinsert_bytes"] > 0
+
+
+def test_clock_hand_skips_dead_same_digest_entry_host():
+    _dead_twin_survives_the_hand("cpu")
+
+
+@pytest.mark.gpu
+def test_clock_hand_skips_dead_same_digest_entry_gpu(cuda_dev):
+    _dead_twin_survives_the_hand(cuda_dev)
