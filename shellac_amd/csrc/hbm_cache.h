@@ -147,9 +147,17 @@ class HbmCache {
   // and log append: it reads the index and the current head slot, which only the index
   // insert changes, and a `reserve` covering this SET keeps its gather off the bytes
   // the append overwrites.
+  // `allow_reclaim` false: no CLOCK hand this batch (the append stays within
+  // `bytes_bound`; a caller that reserved only that much for it, see would_reclaim).
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
-             uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
+             uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
+             bool allow_reclaim = true);
+  // Whether a SET of `bytes_bound` bytes issued now would run the CLOCK hand (the log is
+  // within a few batches of wrapping); the answer can only turn true later.
+  bool would_reclaim(uint64_t bytes_bound) const {
+    return cfg_.evict == kEvictClock && rmax_ && should_reclaim(bytes_bound);
+  }
   // SET through captured hipGraphs, for callers with fixed batch sizes and fixed
   // staging buffers (the proxy's micro-batches, padded to a size class with
   // vlen = kSkipVlen rows). The five SET kernels become one graph launch. A graph bakes

@@ -2864,7 +2864,7 @@ void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
-                     hipEvent_t index_after) {
+                     hipEvent_t index_after, bool allow_reclaim) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
@@ -2873,7 +2873,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   DeviceGuard g(cfg_.device);
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
-  if (rmax && should_reclaim(bytes_bound)) {
+  if (allow_reclaim && rmax && should_reclaim(bytes_bound)) {
     const int64_t w = hand_window(n);
     ensure_rc_ws(w);
     if (w + n > cb_cap_) {

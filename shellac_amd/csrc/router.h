@@ -151,7 +151,8 @@ class RoutedStep {
   // reply gather (the probe reserved their bytes; joined by the next owner_probe), and
   // the replica (tier 1) on `s` after the local gather.
   void store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replica, uint32_t now,
-                  hipStream_t s, hipStream_t sset, bool replica_on_sset = false);
+                  hipStream_t s, hipStream_t sset, bool replica_on_sset = false,
+                  hipEvent_t index_after = nullptr, bool allow_reclaim = true);
   // Per-request (size, off) into `data`, in request order (duplicates: their claimer's
   // record); run on a stream that has waited for the reply all-to-all.
   void assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out_off, hipStream_t s);
@@ -213,6 +214,12 @@ class RoutedStep {
   hipStream_t asm_stream_ = nullptr;   // step() without `sasm`: reply transfer + assembly
   hipEvent_t ev_pfork_ = nullptr, ev_plan_ = nullptr, ev_rep_ = nullptr, ev_start_ = nullptr;
   bool pfork_valid_ = false, rep_pending_ = false, in_step_ = false;
+  // look-ahead reserve (step()): bytes this / the previous probe reserved for the next
+  // step's SETs; recent main-shard SET payload bounds; gather-done events per parity
+  uint64_t ahead_ = 0, ahead_prev_ = 0;
+  std::vector<int64_t> pay_hist_;
+  hipEvent_t ev_gdone_[2] = {nullptr, nullptr};
+  bool gdone_valid_[2] = {false, false};
   std::shared_ptr<StepComm> comm_;
   hipEvent_t ev_probe_ = nullptr, ev_local_ = nullptr, ev_rfork_ = nullptr,
              ev_reply_[2] = {nullptr, nullptr};

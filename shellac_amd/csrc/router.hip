@@ -555,8 +555,8 @@ __global__ __launch_bounds__(kB) void k_gr_scatter_slots(
 // overwrite as evicted, so the SET chain can run beside the reply gather.
 // One launch with k_derive's work: the rows each owner slot holds (own_cnt).
 __global__ void k_owner_prep(const int64_t* __restrict__ mat, int64_t K, int32_t W, int32_t me,
-                             int64_t capG, uint64_t rmax, int64_t* __restrict__ own_cnt,
-                             uint64_t* __restrict__ out) {
+                             int64_t capG, uint64_t rmax, uint64_t ahead,
+                             int64_t* __restrict__ own_cnt, uint64_t* __restrict__ out) {
   for (int s = threadIdx.x; s < W; s += blockDim.x) {
     const int q = s == W - 1 ? me : (s < me ? s : s + 1);
     own_cnt[s] = min(mat[(int64_t)q * K + me], capG);
@@ -567,7 +567,9 @@ __global__ void k_owner_prep(const int64_t* __restrict__ mat, int64_t K, int32_t
     rows += (uint64_t)mat[(int64_t)q * K + W + me];
     bytes += (uint64_t)mat[(int64_t)q * K + 2 * W + me];
   }
-  *out = 48 * rows + bytes + rmax;
+  // `ahead`: the next step's SET bytes too (look-ahead, RoutedStep::step): its append may
+  // then run before the next probe, beside this step's owner phase
+  *out = 48 * rows + bytes + rmax + ahead;
 }
 
 // Reply bytes the owner probe found per requester (before any drop): out[q].
@@ -800,7 +802,8 @@ RoutedStep::RoutedStep(int world, int rank, int device)
                       hipHostMallocDefault));
   for (hipEvent_t* e : {&ev_fork_, &ev_pjoin_, &ev_pub_, &ev_sfork_, &ev_join_, &ev_asm_[0],
                         &ev_asm_[1], &ev_probe_, &ev_local_, &ev_rfork_, &ev_reply_[0],
-                        &ev_reply_[1], &ev_pfork_, &ev_plan_, &ev_rep_, &ev_start_})
+                        &ev_reply_[1], &ev_pfork_, &ev_plan_, &ev_rep_, &ev_start_,
+                        &ev_gdone_[0], &ev_gdone_[1]})
     RT_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
@@ -814,7 +817,7 @@ RoutedStep::~RoutedStep() {
   (void)hipHostFree(host_tab_);
   for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1],
                        ev_probe_, ev_local_, ev_rfork_, ev_reply_[0], ev_reply_[1], ev_pfork_,
-                       ev_plan_, ev_rep_, ev_start_})
+                       ev_plan_, ev_rep_, ev_start_, ev_gdone_[0], ev_gdone_[1]})
     (void)hipEventDestroy(e);
 
 }
@@ -937,7 +940,10 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
                       bool coalesce) {
   SH_CHECK(pts_ && own_ && npts_ > 0, "RoutedStep: ring not set");
   SH_CHECK(n < (1ll << 31), "RoutedStep: GET batch too large");
-  if (!in_step_) pfork_valid_ = false;  // a multi-call step: the next step() plans on `s`
+  if (!in_step_) {  // a multi-call step: the next step() plans on `s`, no look-ahead
+    pfork_valid_ = false;
+    gdone_valid_[0] = gdone_valid_[1] = false;
+  }
   const int W = w_;
   const int nb = W + 1;
   const std::vector<int64_t> c = caps(n);
@@ -1077,8 +1083,17 @@ void RoutedStep::owner_probe(const uint8_t* G, HbmCache* shard, uint32_t now, hi
   // bytes, computed on the device from the all-gathered matrix (no host read)
   uint64_t* reserve = buf<uint64_t>(kReserve, 1);
   own_cnt_ = buf<int64_t>(kOwnCnt, W);
+  // look-ahead (native step only): 5/4 of the largest recent SET payload plus the CLOCK
+  // reinsertion budget, the most the next step's main-shard SET chain can append
+  // (only while the log is far from wrapping: a SET that runs early never runs the CLOCK
+  // hand, so no reinsertion budget needs reserving; near the wrap every SET waits for its
+  // own probe and no look-ahead is reserved, which would cost hit ratio)
+  const uint64_t rmax = (uint64_t)shard->reinsert_max();
+  ahead_prev_ = ahead_;
+  const uint64_t est = pay_hist_.empty() ? 0 : (uint64_t)hist_max(pay_hist_) * 5 / 4;
+  ahead_ = in_step_ && est && !shard->would_reclaim(est) ? est : 0;
   hipLaunchKernelGGL(k_owner_prep, dim3(1), dim3(64), 0, s, mat_dev_, row_words(), W, rank_, capG_,
-                     (uint64_t)shard->reinsert_max(), own_cnt_, reserve);
+                     rmax, ahead_, own_cnt_, reserve);
   RT_OK(hipGetLastError());
   shard->lookup_slots(reinterpret_cast<const Digest*>(G), W, capG_, own_cnt_, lk_loc_, lk_size_,
                       lk_off_, now, s, reserve);
@@ -1214,7 +1229,8 @@ void RoutedStep::pack_sets(uint8_t* S, hipStream_t s) {
 }
 
 void RoutedStep::store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replica, uint32_t now,
-                            hipStream_t s, hipStream_t sset, bool replica_on_sset) {
+                            hipStream_t s, hipStream_t sset, bool replica_on_sset,
+                            hipEvent_t index_after, bool allow_reclaim) {
   const int W = w_, me = rank_;
   const int64_t K = row_words();
   const int64_t ms = ms_;
@@ -1264,7 +1280,7 @@ void RoutedStep::store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replic
   // probe: the probe reserved these bytes (k_owner_reserve), so the append never touches
   // a record the reply gather reads and runs beside it; the previous step's gather is
   // done (it precedes the probe on `s`). The next owner_probe joins the chain.
-  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, sset);
+  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, sset, index_after, allow_reclaim);
   RT_OK(hipEventRecord(ev_join_, sset));
   sets_pending_ = true;
   // replica (tier 1) on `s`, after this step's local gather (same stream) and the fill
@@ -1360,10 +1376,8 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
       plan(keys, n, replica, now, skeys, svlen, sflags, sexpire, sval_off, svalues, ns, fanout, G,
            row, ps, coalesce);
       in_step_ = false;
-      if (ps != s) {
-        RT_OK(hipEventRecord(ev_plan_, ps));
-        RT_OK(hipStreamWaitEvent(s, ev_plan_, 0));
-      }
+      RT_OK(hipEventRecord(ev_plan_, ps));  // the SET stream starts from the plan's output
+      if (ps != s) RT_OK(hipStreamWaitEvent(s, ev_plan_, 0));
     }
     {
       TraceRange t("serve.row_allgather");
@@ -1383,12 +1397,16 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
       comm_->all_to_all(G, off_r, sz, G, off_s, sz, s, StepComm::kCtrl);
     }
     TraceRange t("serve.owner");
+    in_step_ = true;  // owner_probe reserves the look-ahead
     owner_probe(G, shard, now, s);
+    in_step_ = false;
   }
   const int P = par_;
-  // the SET stream forks here: the probe reserved this step's SET bytes
+  // The SET stream starts once the plan is done (the local gather reads its replica
+  // locations; packing its SET rows); its main-shard append waits below for what the
+  // reserves require, its index insert for this probe
   RT_OK(hipEventRecord(ev_probe_, s));
-  RT_OK(hipStreamWaitEvent(sset, ev_probe_, 0));
+  RT_OK(hipStreamWaitEvent(sset, ev_plan_, 0));
   // the local (replica) gather on the SET stream, beside the reply gather: the replica
   // store follows it there, so the next step's replica probe need not wait for the reply
   gather_local(data, sset);
@@ -1405,6 +1423,8 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
     owner_reply(shard, R, data, s);
     // the reply slots (others' in R, the own one in `data`) are written
     RT_OK(hipEventRecord(ev_rfork_, s));
+    RT_OK(hipEventRecord(ev_gdone_[P], s));  // this step's log reads are done
+    gdone_valid_[P] = true;
     if (W > 1) {
       // the reply transfer on its own stream and channel: the SET exchange and the next
       // step's planning run beside it
@@ -1435,6 +1455,18 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
       }
     uint8_t* S = buf<uint8_t>(P ? kS1 : kS0, (size_t)so + 16);
     uint8_t* Rs = buf<uint8_t>(P ? kRs1 : kRs0, (size_t)ro + 16);
+    // Where the main-shard append may start. This step's probe reserved its bytes (the
+    // reply gather never reads them); if the previous probe reserved them too
+    // (look-ahead: this step's bytes within its margin), the append needs only the
+    // previous step's reply gather done and runs beside this owner phase, with the index
+    // insert alone waiting for the probe. Otherwise everything waits for the probe.
+    int64_t pay = 0;
+    for (int q = 0; q < W; ++q)
+      pay += 48 * mat_[(int64_t)q * row_words() + W + me] + mat_[(int64_t)q * row_words() + 2 * W + me];
+    const bool early = gdone_valid_[P ^ 1] && ahead_prev_ >= (uint64_t)pay &&
+                       !shard->would_reclaim((uint64_t)pay);
+    RT_OK(hipStreamWaitEvent(sset, early ? ev_gdone_[P ^ 1] : ev_probe_, 0));
+    push_hist(&pay_hist_, pay);
     pack_sets(S, sset);
     if (W > 1 && (so > 0 || ro > 0)) {
       // send blocks at Ps[p] (pack_sets' table), receive blocks in rank order
@@ -1451,7 +1483,8 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
       }
       comm_->all_to_all(Rs, off_r, rb, S, off_s, sb, sset, StepComm::kSet);
     }
-    store_sets(Rs, shard, replica, now, s, sset, /*replica_on_sset=*/true);
+    store_sets(Rs, shard, replica, now, s, sset, /*replica_on_sset=*/true,
+               early ? ev_probe_ : nullptr, /*allow_reclaim=*/!early);
   }
   {
     TraceRange t("serve.assemble");
