@@ -1468,8 +1468,10 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
     RT_OK(hipStreamWaitEvent(sset, early ? ev_gdone_[P ^ 1] : ev_probe_, 0));
     push_hist(&pay_hist_, pay);
     pack_sets(S, sset);
-    if (W > 1 && (so > 0 || ro > 0)) {
-      // send blocks at Ps[p] (pack_sets' table), receive blocks in rank order
+    if (W > 1) {
+      // Every rank takes part even with nothing to move: a collective-based comm (the
+      // gloo callbacks) needs all ranks; RCCL's grouped send/recv skips empty pairs.
+      // Send blocks at Ps[p] (pack_sets' table), receive blocks in rank order.
       const uint64_t* Ps = host_tab_ + (size_t)P * (8 * (size_t)W + 8) + 2 * (size_t)W + 1;
       std::vector<int64_t> off_s(W, 0), off_r(W, 0), sb(W, 0), rb(W, 0);
       int64_t pos = 0;

@@ -32,13 +32,16 @@ def _run_world(target, world, *args, timeout=240):
         while len(results) < world:
             try:
                 results.append(q.get(timeout=1))
+                if results[-1][1] != "ok":
+                    break  # a failed rank: its peers may wait in a collective forever
             except queue.Empty:
                 dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
                 assert not dead, f"rank exited with {dead} before reporting"
                 assert time.time() - t0 < timeout, "distributed test timed out"
     finally:
+        failed = any(r[1] != "ok" for r in results)
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=2 if failed else 30)
             if p.is_alive():
                 p.kill()
     fails = [r for r in results if r[1] != "ok"]

@@ -17,6 +17,12 @@ pytestmark = pytest.mark.gpu
 def _routed_worker(rank, world, port, q, backend="bounce"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        stack_dir = os.environ.get("SHELLAC_TEST_STACKS")
+        if stack_dir:  # a hung rank leaves its Python stack here (diagnostics)
+            import faulthandler
+
+            faulthandler.dump_traceback_later(
+                60, exit=False, file=open(os.path.join(stack_dir, f"rank{rank}.stack"), "w"))
         from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
         from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
         from shellac_amd.parallel.exchange import BounceComm
@@ -79,6 +85,22 @@ def _routed_worker(rank, world, port, q, backend="bounce"):
         bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
                enumerate(zip(got, want)) if g != w]
         assert not bad, f"rank {rank} step 3: {len(bad)} wrong GETs, first {bad[:6]}"
+        # steps 4-9: the same shapes, the last rank updating 8 keys per step; from the third
+        # native step on, SET appends start early under the previous probe's look-ahead
+        # reserve. Every step's GETs see exactly the SETs of the steps before it.
+        cur = dict(v1)
+        cur.update(new)
+        for t in range(6):
+            upd_t = keys[120 + 8 * t: 128 + 8 * t]
+            vals_t = {k: b"v3-%d-" % t + k for k in upd_t}
+            mine_upd = upd_t if rank == world - 1 else []
+            res = sc.serve(digest_strings(req, dev), batch(mine_upd, [vals_t[k] for k in mine_upd]))
+            got = values(res)
+            want = [cur[k] for k in req[:-3]] + [None] * 3
+            bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
+                   enumerate(zip(got, want)) if g != w]
+            assert not bad, f"rank {rank} step {4 + t}: {len(bad)} wrong GETs, first {bad[:6]}"
+            cur.update(vals_t)
         st = sc.stats
         assert st["coalesced_gets"] > 0
         # world 1: every key is local (no remote GETs, the replica is never consulted)
@@ -95,7 +117,7 @@ def _routed_worker(rank, world, port, q, backend="bounce"):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_fused_routed_step_multiprocess(world):
-    _run_world(_routed_worker, world, timeout=180)
+    _run_world(_routed_worker, world, timeout=120)
 
 
 def test_routed_step_over_rccl_one_rank():
