@@ -166,8 +166,8 @@ class RoutedStep {
   // The whole step in one call, every collective issued from here (no Python between
   // them): plan -> all-gather -> publish -> request a2a -> owner probe -> reply (its
   // transfer on the executor's comm stream) -> local gather -> SET exchange on `sset`
-  // -> assemble on `sasm`. Not for a calibrating step (caps(n)[3] or [4]: the
-  // multi-call path). `data` holds caps(n)[2] + W (8 capG + capD) + 16 bytes; out_size /
+  // -> assemble on `sasm`. Not for a calibrating step (caps(n)[3]: the multi-call path;
+  // every rank agrees on it). `data` holds caps(n)[2] + W (8 capG + capD) + 16 bytes; out_size /
   // out_off n words each, valid once `sasm` has passed this step. `sset` / `sasm` 0: the
   // process-wide step streams (step_streams). `inputs_ready`
   // (optional): an event after which the GET keys and the SET batch are complete; then

@@ -1340,7 +1340,9 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
   const int64_t K = row_words();
   {
     const std::vector<int64_t> c = caps(n);
-    SH_CHECK(!c[3] && !c[4], "RoutedStep::step: a calibrating step takes the multi-call path");
+    // (a rank without a local-region history yet, c[4], still steps natively so that every
+    // rank takes the same path: its replica hits that outgrow the old capL are misses)
+    SH_CHECK(!c[3], "RoutedStep::step: a calibrating step takes the multi-call path");
   }
   // o(p): the position of peer p among the other ranks
   auto o = [me](int p) { return p < me ? p : p - 1; };

@@ -531,7 +531,9 @@ class ShardedCache:
             self._ncomm = step_comm(self.group, dev) or False
             if self._ncomm is not False:
                 e.set_comm(self._ncomm)
-        if self._ncomm is not False and not (cal or cal_l):
+        # the path must be the same on every rank: `cal` is (every rank derives it from the
+        # same all-gathered rows), `cal_l` is per rank (its own local-region history)
+        if self._ncomm is not False and not cal:
             return self._serve_native(e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l,
                                       fanout, rep, inputs_ready)
         ph = _Phases("serve.")
