@@ -1276,11 +1276,12 @@ void RoutedStep::store_sets(const uint8_t* Rs, HbmCache* shard, HbmCache* replic
     RT_OK(hipEventRecord(ev_rep_, sset));
     rep_pending_ = true;
   }
-  // Main shard (tier 0) on the SET stream, which forked from `s` after this step's owner
-  // probe: the probe reserved these bytes (k_owner_reserve), so the append never touches
-  // a record the reply gather reads and runs beside it; the previous step's gather is
-  // done (it precedes the probe on `s`). The next owner_probe joins the chain.
-  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, sset, index_after, allow_reclaim);
+  // Main shard (tier 0) on the SET stream, after this step's owner probe (or, early
+  // under a look-ahead reserve, after the previous step's reply gather with
+  // `index_after` = this probe): the probes reserved these bytes (k_owner_prep), so the
+  // append never touches a record a reply gather reads. The next owner_probe joins it.
+  shard->store(rkeys, nullptr, roff, v0, fl, ex, ms, bound, now, sset, index_after,
+               allow_reclaim);
   RT_OK(hipEventRecord(ev_join_, sset));
   sets_pending_ = true;
   // replica (tier 1) on `s`, after this step's local gather (same stream) and the fill
