@@ -183,6 +183,7 @@ void bind_router(py::module_& m) {
       .def("join_sets", [](RoutedStep& r, uintptr_t s) { r.join_sets(S(s)); })
       .def("set_comm", &RoutedStep::set_comm)
       .def_property_readonly("has_comm", &RoutedStep::has_comm)
+      .def_property_readonly("early_sets", &RoutedStep::early_sets)
       .def("step", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
                       uintptr_t skeys, uintptr_t svlen, uintptr_t sflags, uintptr_t sexpire,
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,

@@ -163,6 +163,8 @@ class RoutedStep {
   // The communicator step() issues its collectives on (RCCL, mirror or callbacks).
   void set_comm(std::shared_ptr<StepComm> c);
   bool has_comm() const { return comm_ != nullptr; }
+  // Steps whose main-shard SET append started early under a look-ahead reserve.
+  int64_t early_sets() const { return early_sets_; }
   // The whole step in one call, every collective issued from here (no Python between
   // them): plan -> all-gather -> publish -> request a2a -> owner probe -> reply (its
   // transfer on the executor's comm stream) -> local gather -> SET exchange on `sset`
@@ -217,6 +219,7 @@ class RoutedStep {
   // look-ahead reserve (step()): bytes this / the previous probe reserved for the next
   // step's SETs; recent main-shard SET payload bounds; gather-done events per parity
   uint64_t ahead_ = 0, ahead_prev_ = 0;
+  int64_t early_sets_ = 0;
   std::vector<int64_t> pay_hist_;
   hipEvent_t ev_gdone_[2] = {nullptr, nullptr};
   bool gdone_valid_[2] = {false, false};

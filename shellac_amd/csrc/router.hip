@@ -1469,6 +1469,7 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
     const bool early = gdone_valid_[P ^ 1] && ahead_prev_ >= (uint64_t)pay &&
                        !shard->would_reclaim((uint64_t)pay);
     RT_OK(hipStreamWaitEvent(sset, early ? ev_gdone_[P ^ 1] : ev_probe_, 0));
+    early_sets_ += early ? 1 : 0;
     push_hist(&pay_hist_, pay);
     pack_sets(S, sset);
     if (W > 1) {

@@ -337,11 +337,13 @@ def test_fused_routed_step_matches_framework_ops(cuda_dev, world):
             r.wait()
             got.append([None if x is None else x[0]
                         for x in unpack_records(r.data, r.off, r.size)])
-        outs.append((got, dict(sc.stats)))
-    (g0, s0), (g1, s1), (g2, s2), (g3, s3) = outs
+        outs.append((got, dict(sc.stats), sc._engine.early_sets if sc._engine else 0))
+    (g0, s0, e0), (g1, s1, e1), (g2, s2, e2), (g3, s3, e3) = outs
     assert g0 == g1
     assert s0 == s1
     assert g3 == g2 and s3 == s2
+    # the native steps after the first two ran their SET appends early (look-ahead)
+    assert e1 >= 1 and e2 >= 1 and e3 >= 1
     assert sum(v is not None for v in g1[0]) == 8192     # every GET hits
     assert s1["replica_hits"] > 0
     # coalesced: the same values; duplicates neither probed nor sent
