@@ -1428,13 +1428,99 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
 // insert is latency-bound, and beside the bandwidth-bound gather it only gets the slots
 // the gather leaves (a 16-lanes-per-key version took 130-140 us there, this one 39 us).
 // Policy: replace the key's own entry, else a dead slot (first bucket while it keeps
-// >= 2 free, else the emptier bucket), else evict the oldest; the entry is claimed by a
+// >= 2 free, else the emptier bucket), else move one entry of the pair to its other
+// bucket (relocate_one), else evict the oldest; the entry is claimed by a
 // CAS on its loc word, the digest / vlen words follow and k_set_fixup repairs entries
 // a later insert of the same batch re-claimed. Workgroup 0 publishes the new log head
 // into the other ping-pong head slot; every row resets its dedupe-table slot.
 // Keep this kernel at <= 64 VGPRs (8 waves/SIMD): beside the gather, which holds 3/4 of
 // every SIMD's slots, a 72-VGPR build fits one wave per SIMD instead of two and ran 4x
 // slower (126 vs 31 us per 64K-row batch).
+// Relocation: when all 8 slots of a new key's bucket pair are live, one of them whose own
+// other bucket has a dead slot moves there (one cuckoo step) and the key takes its place;
+// only when none can move is the oldest evicted. Without it, inserts racing for a pair's
+// last free slots evicted a live key now and then at 30 % slot load (1 key in 40K, in
+// about 1 run in 4; a sequential insert of the same keys evicts none).
+// Called by the whole 4-lane group, in the all-live case (lane l4 holds entry l4 of each
+// bucket in w1 / w2). The lane holding the chosen entry copies it into the dead slot —
+// digest and vlen words while that slot is still dead, then a CAS of its loc — so the
+// copy is never half-written while live, and from then on the key has two entries with
+// the same record. Returns, uniform in the group: the entry's index 0-7 (the caller then
+// CASes it from the entry's loc to its own) and the copy's slot, or -1 when no entry can
+// move, -2 when the copy's CAS lost (re-read and try again). If the caller's
+// CAS then fails (the moved key was updated in the meantime, or evicted), it must drop
+// the copy (undo_relocation) so no stale duplicate stays behind.
+// (Entry words by value: an array argument would put the caller's registers in scratch.)
+// claim[i] of a row k_set_index left to k_set_fixup (no index slot id reaches it)
+constexpr uint32_t kClaimDeferred = 0xfffffffeu;
+
+struct Reloc {
+  uint64_t alt;  // the copy's slot
+  int target;    // 0-7, -1 none can move, -2 the copy's CAS lost
+};
+__device__ __forceinline__ Reloc relocate_one(uint64_t p0, uint64_t p1, uint64_t p2, uint64_t p3,
+                                         uint64_t r0, uint64_t r1, uint64_t r2, uint64_t r3,
+                                         uint64_t b1, uint64_t b2, Entry* __restrict__ index,
+                                         uint64_t mask, uint64_t base, uint64_t span,
+                                         uint64_t head_new, uint64_t cap, uint32_t now) {
+  const int l4 = threadIdx.x & 3;
+  const int gbase = threadIdx.x & 60;
+  int pick = -1;  // this lane's candidate: 0 (its b1 entry) or 1 (its b2 entry)
+  uint64_t a_slot = 0, a_loc = 0;
+#pragma unroll 1
+  for (int h = 0; h < 2 && pick < 0; ++h) {
+    const uint64_t wd0 = h ? r0 : p0, wd1 = h ? r1 : p1, wloc = h ? r2 : p2;
+    const uint64_t own = h ? b2 : b1;
+    if (wloc - base - 1 < span) continue;  // another row's claim of this batch: not final
+    const Digest de{wd0, wd1};
+    const uint64_t x1 = bucket1(de, mask), x2 = bucket2(de, mask);
+    const uint64_t ob = x1 == own ? x2 : (x2 == own ? x1 : own);
+    if (ob == own) continue;
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(index + ob * kEntriesPerBucket);
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t l = __hip_atomic_load(q + 4 * k + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t x = __hip_atomic_load(q + 4 * k + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!entry_live(l, (uint32_t)(x >> 32), head_new, cap, now)) {
+        pick = h;
+        a_slot = ob * kEntriesPerBucket + k;
+        a_loc = l;
+        break;
+      }
+    }
+  }
+  const uint32_t m0 = (uint32_t)((__ballot(pick == 0) >> gbase) & 0xfull);
+  const uint32_t m1 = (uint32_t)((__ballot(pick == 1) >> gbase) & 0xfull);
+  if (!(m0 | m1)) return Reloc{~0ull, -1};
+  const int lane = m0 ? __ffs(m0) - 1 : __ffs(m1) - 1;
+  const int target = (m0 ? 0 : 4) + lane;
+  int ok = 0;
+  if (l4 == lane) {
+    Entry* const a = index + a_slot;
+    a->d0 = m0 ? p0 : r0;
+    a->d1 = m0 ? p1 : r1;
+    *reinterpret_cast<uint64_t*>(&a->vlen) = m0 ? p3 : r3;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the words before the live loc
+    ok = atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)a_loc,
+                   (unsigned long long)(m0 ? p2 : r2)) == a_loc;
+  }
+  ok = __shfl(ok, gbase + lane);
+  return Reloc{__shfl(a_slot, gbase + lane), ok ? target : -2};
+}
+
+// The caller's CAS of the moved key's old slot failed: drop the copy relocate_one made
+// (loc first, then the digest words, so the key's digest never stays behind in a dead
+// slot that a later insert of the same key could match beside its live entry).
+__device__ __forceinline__ void undo_relocation(Entry* __restrict__ index, uint64_t alt,
+                                             uint64_t loc) {
+  Entry* const a = index + alt;
+  if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)loc, 0ull) ==
+      loc) {
+    a->d0 = 0;
+    a->d1 = 0;
+  }
+}
+
 // One SET row's index insert by its 4-lane group (uniform arguments across the group;
 // `active` false: nothing to insert). Lane 0 writes the claimed entry id to *claim_out
 // when the CAS succeeds (the caller pre-sets ~0u); counts evictions / bytes / rows that
@@ -1478,6 +1564,7 @@ __device__ __forceinline__ void index_insert(
                            ((uint32_t)((__ballot(v2) >> gbase) & 0xfull) << 4);
     int target;
     bool evict = false;
+    uint64_t alt = ~0ull;  // relocation copy (all-live pair), dropped if our CAS fails
     if (mmask) {
       target = __ffs(mmask) - 1;
     } else {
@@ -1489,15 +1576,25 @@ __device__ __forceinline__ void index_insert(
                                   : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
         target = __ffs(pref ? pref : dead) - 1;
       } else {
-        uint64_t oldest = ~0ull;
-        target = 0;
+        const Reloc r = relocate_one(w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3],
+                                     b1, b2, index, mask, base, span, head_new, cap, now);
+        target = r.target;
+        alt = r.alt;
+        if (target == -1) {
+          uint64_t oldest = ~0ull;
+          target = 0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint64_t le = e < 4 ? __shfl(w1[2], gbase + e) : __shfl(w2[2], gbase + e - 4);
-          if (le < oldest) { oldest = le; target = e; }
+          for (int e = 0; e < 8; ++e) {
+            const uint64_t le = e < 4 ? __shfl(w1[2], gbase + e) : __shfl(w2[2], gbase + e - 4);
+            if (le < oldest) { oldest = le; target = e; }
+          }
+          evict = true;
         }
-        evict = true;
       }
+    }
+    if (target < 0) {  // the relocation's copy lost its slot: re-read
+      if (attempt == 15 && l4 == 0) ++lost;
+      continue;
     }
     const uint64_t e1 = __shfl(w1[2], gbase + (target & 3));
     const uint64_t e2 = __shfl(w2[2], gbase + (target & 3));
@@ -1516,6 +1613,8 @@ __device__ __forceinline__ void index_insert(
         ok = 1;
         evicted += evict ? 1 : 0;
         bytes += myvlen;
+      } else if (alt != ~0ull) {
+        undo_relocation(index, alt, expected);
       }
     }
     ok = __shfl(ok, gbase);
@@ -1577,7 +1676,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
                              ((uint32_t)((__ballot(v2) >> gbase) & 0xfull) << 4);
       int target;
-      bool evict = false;
       if (mmask) {
         target = __ffs(mmask) - 1;
       } else {
@@ -1589,14 +1687,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                                     : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
           target = __ffs(pref ? pref : dead) - 1;
         } else {
-          uint64_t oldest = ~0ull;
-          target = 0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint64_t le = e < 4 ? __shfl(w1[2], gbase + e) : __shfl(w2[2], gbase + e - 4);
-            if (le < oldest) { oldest = le; target = e; }
-          }
-          evict = true;
+          // all 8 live: k_set_fixup moves one of them or evicts (relocate_one's policy,
+          // one lane per row there: here it cost 40 B/lane of scratch at 64 VGPRs)
+          if (l4 == 0) claim[i] = kClaimDeferred;
+          break;
         }
       }
       const uint64_t e1 = __shfl(w1[2], gbase + (target & 3));
@@ -1614,7 +1708,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
           *reinterpret_cast<uint64_t*>(&slot->vlen) = pack2(myvlen, myexp);
           claim[i] = (uint32_t)(slot - index);
           ok = 1;
-          evicted += evict ? 1 : 0;
           bytes += myvlen;
         }
       }
@@ -1627,16 +1720,103 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
               &CacheCounters::set_dropped);
 }
 
+// One row k_set_index deferred (its pair all live), by one thread inside k_set_fixup:
+// relocate_one's policy lane-serial — move the first entry (bucket 1, then bucket 2; not
+// another claim of this batch) whose other bucket has a dead slot, copying it there
+// before its slot is taken, else evict the oldest. Other deferred rows are the only
+// concurrent writers that can touch these non-batch entries, hence the CAS retries.
+__device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword,
+                                Entry* __restrict__ index, uint64_t mask, uint64_t base,
+                                uint64_t span, uint64_t head_new, uint64_t cap, uint32_t now,
+                                uint32_t* __restrict__ claim_out, unsigned long long& evicted,
+                                unsigned long long& lost) {
+  const uint64_t bb[2] = {bucket1(d, mask), bucket2(d, mask)};
+  for (int attempt = 0; attempt < 16; ++attempt) {
+    Entry* target = nullptr;
+    Entry* copy = nullptr;
+    Entry* victim = nullptr;  // the eviction fallback: the oldest entry not of this batch
+    uint64_t expected = 0, oldest = ~0ull;
+    bool evict = false;
+    for (int e = 0; e < 8 && !target; ++e) {  // a slot that died or freed up meanwhile
+      Entry* const x = index + bb[e >> 2] * kEntriesPerBucket + (e & 3);
+      const uint64_t l = agent_load(&x->loc);
+      const uint64_t w = agent_load(reinterpret_cast<const uint64_t*>(&x->vlen));
+      if (!entry_live(l, (uint32_t)(w >> 32), head_new, cap, now)) {
+        target = x;
+        expected = l;
+      } else if (l - base - 1 >= span && l < oldest) {
+        oldest = l;
+        victim = x;
+      }
+    }
+    if (!target) {
+      for (int e = 0; e < 8 && !target; ++e) {
+        Entry* const x = index + bb[e >> 2] * kEntriesPerBucket + (e & 3);
+        const uint64_t l = agent_load(&x->loc);
+        if (l - base - 1 < span) continue;  // another claim of this batch
+        const Digest de{agent_load(&x->d0), agent_load(&x->d1)};
+        const uint64_t w = agent_load(reinterpret_cast<const uint64_t*>(&x->vlen));
+        const uint64_t x1 = bucket1(de, mask), x2 = bucket2(de, mask);
+        const uint64_t own = bb[e >> 2];
+        const uint64_t ob = x1 == own ? x2 : (x2 == own ? x1 : own);
+        if (ob == own) continue;
+        for (int k = 0; k < 4; ++k) {
+          Entry* const a = index + ob * kEntriesPerBucket + k;
+          const uint64_t al = agent_load(&a->loc);
+          const uint64_t aw = agent_load(reinterpret_cast<const uint64_t*>(&a->vlen));
+          if (entry_live(al, (uint32_t)(aw >> 32), head_new, cap, now)) continue;
+          a->d0 = de.lo;
+          a->d1 = de.hi;
+          *reinterpret_cast<uint64_t*>(&a->vlen) = w;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the words before the live loc
+          if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)al,
+                        (unsigned long long)l) == al) {
+            target = x;
+            expected = l;
+            copy = a;
+          }
+          break;  // copied, or lost the slot: take the next candidate
+        }
+      }
+      if (!target && victim) {
+        target = victim;
+        expected = oldest;
+        evict = true;
+      }
+    }
+    if (!target) continue;
+    if (atomicCAS(reinterpret_cast<unsigned long long*>(&target->loc),
+                  (unsigned long long)expected, (unsigned long long)myloc) == expected) {
+      target->d0 = d.lo;
+      target->d1 = d.hi;
+      *reinterpret_cast<uint64_t*>(&target->vlen) = myword;
+      *claim_out = (uint32_t)(target - index);
+      evicted += evict ? 1 : 0;
+      return;
+    }
+    if (copy &&  // the moved key changed meanwhile: drop the copy (loc, then digest)
+        atomicCAS(reinterpret_cast<unsigned long long*>(&copy->loc), (unsigned long long)expected,
+                  0ull) == expected) {
+      copy->d0 = 0;
+      copy->d1 = 0;
+    }
+  }
+  ++lost;
+}
+
 // After k_set_index (kernel boundary: every CAS and word write is visible): each entry
 // whose loc is still the one a row of this batch claimed gets that row's digest and
 // vlen|expire words again, so no entry pairs one key's digest with another key's loc.
+// Rows k_set_index deferred (kClaimDeferred: all 8 slots of the pair live) are inserted
+// here first, by deferred_insert.
 __global__ __launch_bounds__(kBlock) void k_set_fixup(
     const Digest* __restrict__ keys, int64_t n, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ expire,
-    const uint64_t* __restrict__ head_ptr, const uint32_t* __restrict__ claim,
+    const uint64_t* __restrict__ head_ptr, uint32_t* __restrict__ claim,
     Entry* __restrict__ index, const uint64_t* __restrict__ size, uint64_t* __restrict__ ring,
     uint64_t rmask, const uint64_t* __restrict__ ring_tail, uint64_t* __restrict__ ring_tail_next,
-    const uint64_t* __restrict__ cnt_off, uint64_t* __restrict__ head_host) {
+    const uint64_t* __restrict__ cnt_off, uint64_t* __restrict__ head_host, uint64_t mask,
+    uint64_t cap, uint32_t now, CacheCounters* __restrict__ ctr) {
   const uint64_t base = *head_ptr;
   // item-start ring (CLOCK hand input): every stored row takes the next ring entry in row
   // order = log order (cnt_off: exclusive count of stored rows); the new head goes to the
@@ -1651,9 +1831,16 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kBlock)
       if (size[i]) ring[(rtail + cnt_off[i]) & rmask] = base + off[i] + 0;
+  unsigned long long evicted = 0, lost = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
-    const uint32_t c = claim[i];
+    uint32_t c = claim[i];
+    if (c == kClaimDeferred) {
+      claim[i] = ~0u;
+      deferred_insert(keys[i], base + off[i] + 1, pack2(vlen[i], expire ? expire[i] : 0u), index,
+                      mask, base, off[n], base + off[n], cap, now, claim + i, evicted, lost);
+      continue;  // its words are final (deferred rows are not re-claimed by the batch)
+    }
     if (c == ~0u) continue;
     Entry* const e = index + c;
     if (e->loc != base + off[i] + 1) continue;  // evicted again within the batch
@@ -1662,6 +1849,7 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     e->d1 = d.hi;
     *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vlen[i], expire ? expire[i] : 0u);
   }
+  block_count(ctr, evicted, &CacheCounters::set_evicted, lost, &CacheCounters::set_dropped);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2954,7 +3142,7 @@ void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      set_off_, vlen, expire, cur_head(), set_claim_, index_, set_size_, ring_,
                      ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(), next_ring_tail(), set_cnt_,
-                     host_slots_ + kHeadSlot);
+                     host_slots_ + kHeadSlot, cfg_.nbuckets - 1, cfg_.log_bytes, now, ctr_);
   HIP_OK(hipGetLastError());
 }
 

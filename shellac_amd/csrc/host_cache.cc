@@ -123,10 +123,29 @@ bool HostCache::insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uin
                                 : (live2 < live1 ? (dead & 0xf0u) : (dead & 0x0fu));
       target = __builtin_ctz(pref ? pref : dead);
     } else {
-      uint64_t oldest = ~0ull;
-      for (int e = 0; e < 8; ++e)
-        if (slots[e]->loc < oldest) { oldest = slots[e]->loc; target = e; }
-      evict = true;
+      // all 8 live: move one entry to a dead slot of its own other bucket (one cuckoo
+      // step, as k_set_index's relocate_one), else evict the oldest
+      for (int e = 0; e < 8 && target < 0; ++e) {
+        const Digest de{slots[e]->d0, slots[e]->d1};
+        const uint64_t own = e < 4 ? b1 : b2;
+        const uint64_t x1 = bucket1(de, mask_), x2 = bucket2(de, mask_);
+        const uint64_t ob = x1 == own ? x2 : (x2 == own ? x1 : own);
+        if (ob == own) continue;
+        for (int k = 0; k < 4; ++k) {
+          Entry* a = index_ + ob * kEntriesPerBucket + k;
+          if (!entry_live(a->loc, a->expire, head_, log_bytes_, now)) {
+            *a = *slots[e];
+            target = e;
+            break;
+          }
+        }
+      }
+      if (target < 0) {
+        uint64_t oldest = ~0ull;
+        for (int e = 0; e < 8; ++e)
+          if (slots[e]->loc < oldest) { oldest = slots[e]->loc; target = e; }
+        evict = true;
+      }
     }
   }
   Entry* s = slots[target];
