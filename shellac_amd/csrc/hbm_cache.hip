@@ -273,14 +273,30 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
   // store instruction touch 64 different lines: 27 us per 1M items beside the SET append,
   // now 20 us. The step did not move, 0.319-0.321 vs 0.320-0.323 ms over three rounds
   // (profiles/r2_offsets_ab.log): the gather then starts earlier into the SET append.)
+  // Up to kOffRegs x 64 items per wave (the lookup's 1M rows: 512) are loaded once, all
+  // in flight together, and scanned from registers: the two dependent passes of 64 items
+  // per step were latency-bound, 20-28 us per 1M rows between the lookup and the gather.
   const int64_t len = i1 > i0 ? i1 - i0 : 0;
   const int64_t per = ((len + kBlock / 64 - 1) / (kBlock / 64) + 63) / 64 * 64;
   const int64_t a = min(i1, i0 + per * w), b = min(i1, a + per);
+  constexpr int kOffRegs = 8;
+  const bool in_regs = per <= 64 * kOffRegs;  // uniform across the launch
+  uint64_t rv[kOffRegs];
   unsigned long long ws = 0, wc = 0;
-  for (int64_t i = a + lane; i < b; i += 64) {
-    const uint64_t v = size[i];
-    ws += v;
-    wc += v ? 1 : 0;
+  if (in_regs) {
+#pragma unroll
+    for (int u = 0; u < kOffRegs; ++u) {
+      const int64_t i = a + u * 64 + lane;
+      rv[u] = i < b ? size[i] : 0;
+      ws += rv[u];
+      wc += rv[u] ? 1 : 0;
+    }
+  } else {
+    for (int64_t i = a + lane; i < b; i += 64) {
+      const uint64_t v = size[i];
+      ws += v;
+      wc += v ? 1 : 0;
+    }
   }
   ws = wave_sum(ws);
   wc = wave_sum(wc);
@@ -295,7 +311,31 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
     run += s_w[0][k];
     runc += s_w[1][k];
   }
-  for (int64_t t = a; t < b; t += 64) {
+  if (in_regs) {
+#pragma unroll
+    for (int u = 0; u < kOffRegs; ++u) {
+      const int64_t i = a + u * 64 + lane;
+      const uint64_t v = rv[u];
+      const unsigned long long c = v ? 1 : 0;
+      unsigned long long inc = v, incc = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(inc, d);
+        const unsigned long long oc = __shfl_up(incc, d);
+        if (lane >= d) {
+          inc += o;
+          incc += oc;
+        }
+      }
+      if (i < b) {
+        off[i] = run + inc - v;
+        if (cnt) cnt[i] = runc + incc - c;
+      }
+      run += __shfl(inc, 63);
+      runc += __shfl(incc, 63);
+    }
+  }
+  for (int64_t t = a; !in_regs && t < b; t += 64) {
     const int64_t i = t + lane;
     const uint64_t v = i < b ? size[i] : 0;
     const unsigned long long c = v ? 1 : 0;
