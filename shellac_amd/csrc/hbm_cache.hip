@@ -1360,6 +1360,20 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     //      (the poller's outstanding read-ahead is not waited for)
     if (worker) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // A job of several rounds: a record's chunks after its header round were loaded after
+    // the only check that covered its magic word. Every load has returned now: read the
+    // claim once more and turn every record it reaches into a miss (magic word zeroed)
+    // before the publish. (One round: the round's own check covered every chunk.)
+    if (nch > (int64_t)kSrvWorkers * kSrvUnroll) {
+      if (tid == 0) s_head = newest_head(heads);
+      __syncthreads();
+      const uint64_t c3 = s_head;
+      for (int k = tid; worker && k < n; k += kSrvWorkers)
+        if (s_lg[k] && !(c3 <= (s_lg[k] - 1) + cap))
+          *reinterpret_cast<uint32_t*>(out + s_off[k] + 28) = 0u;
+      if (worker) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     const uint64_t t_copied = (uint64_t)wall_clock64();
     if (tid == 0) {
       // the job's phase stamps first, so they are in place when the host sees the slot
@@ -1482,10 +1496,10 @@ __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict_
 // last free slots evicted a live key now and then at 30 % slot load (1 key in 40K, in
 // about 1 run in 4; a sequential insert of the same keys evicts none).
 // Called by the whole 4-lane group, in the all-live case (lane l4 holds entry l4 of each
-// bucket in w1 / w2). The lane holding the chosen entry copies it into the dead slot —
-// digest and vlen words while that slot is still dead, then a CAS of its loc — so the
-// copy is never half-written while live, and from then on the key has two entries with
-// the same record. Returns, uniform in the group: the entry's index 0-7 (the caller then
+// bucket in w1 / w2). The lane holding the chosen entry copies it into the dead slot
+// (copy_entry: lock the slot's loc, write the words, publish the loc) — so the copy is
+// never half-written while live, no two copies interleave their words in one slot, and
+// from then on the key has two entries with the same record. Returns, uniform in the group: the entry's index 0-7 (the caller then
 // CASes it from the entry's loc to its own) and the copy's slot, or -1 when no entry can
 // move, -2 when the copy's CAS lost (re-read and try again). If the caller's
 // CAS then fails (the moved key was updated in the meantime, or evicted), it must drop
@@ -1498,6 +1512,36 @@ struct Reloc {
   uint64_t alt;  // the copy's slot
   int target;    // 0-7, -1 none can move, -2 the copy's CAS lost
 };
+
+// Copy an entry {d0, d1, loc, vlen|expire} into the free slot `a` whose loc was `expect`:
+// lock the slot first (CAS expect -> kLockedLoc: from then on no other inserter claims,
+// matches or copies into it), write the digest and vlen words, then publish the real loc
+// behind an agent-scope release. Two inserters that picked the same free slot can no
+// longer interleave their digest words: only the one whose lock CAS won writes any.
+// Returns whether the copy is in place.
+__device__ __forceinline__ bool copy_entry(Entry* __restrict__ a, uint64_t expect, uint64_t d0,
+                                           uint64_t d1, uint64_t loc, uint64_t word) {
+  if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)expect,
+                (unsigned long long)kLockedLoc) != expect)
+    return false;
+  a->d0 = d0;
+  a->d1 = d1;
+  *reinterpret_cast<uint64_t*>(&a->vlen) = word;
+  __hip_atomic_store(&a->loc, loc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Drop a copy (its loc still `loc`): lock it, clear the digest words, then free it, so
+// the moved key's digest never lingers in a free slot beside its live entry and no new
+// claimer's words can be overwritten by the clearing.
+__device__ __forceinline__ void drop_entry(Entry* __restrict__ a, uint64_t loc) {
+  if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)loc,
+                (unsigned long long)kLockedLoc) != loc)
+    return;
+  a->d0 = 0;
+  a->d1 = 0;
+  __hip_atomic_store(&a->loc, (uint64_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ Reloc relocate_one(uint64_t p0, uint64_t p1, uint64_t p2, uint64_t p3,
                                          uint64_t r0, uint64_t r1, uint64_t r2, uint64_t r3,
                                          uint64_t b1, uint64_t b2, Entry* __restrict__ index,
@@ -1512,6 +1556,7 @@ __device__ __forceinline__ Reloc relocate_one(uint64_t p0, uint64_t p1, uint64_t
     const uint64_t wd0 = h ? r0 : p0, wd1 = h ? r1 : p1, wloc = h ? r2 : p2;
     const uint64_t own = h ? b2 : b1;
     if (wloc - base - 1 < span) continue;  // another row's claim of this batch: not final
+    if (wloc == kLockedLoc) continue;      // another inserter's copy in flight
     const Digest de{wd0, wd1};
     const uint64_t x1 = bucket1(de, mask), x2 = bucket2(de, mask);
     const uint64_t ob = x1 == own ? x2 : (x2 == own ? x1 : own);
@@ -1521,7 +1566,7 @@ __device__ __forceinline__ Reloc relocate_one(uint64_t p0, uint64_t p1, uint64_t
     for (int k = 0; k < 4; ++k) {
       const uint64_t l = __hip_atomic_load(q + 4 * k + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t x = __hip_atomic_load(q + 4 * k + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!entry_live(l, (uint32_t)(x >> 32), head_new, cap, now)) {
+      if (entry_free(l, (uint32_t)(x >> 32), head_new, cap, now)) {
         pick = h;
         a_slot = ob * kEntriesPerBucket + k;
         a_loc = l;
@@ -1535,30 +1580,16 @@ __device__ __forceinline__ Reloc relocate_one(uint64_t p0, uint64_t p1, uint64_t
   const int lane = m0 ? __ffs(m0) - 1 : __ffs(m1) - 1;
   const int target = (m0 ? 0 : 4) + lane;
   int ok = 0;
-  if (l4 == lane) {
-    Entry* const a = index + a_slot;
-    a->d0 = m0 ? p0 : r0;
-    a->d1 = m0 ? p1 : r1;
-    *reinterpret_cast<uint64_t*>(&a->vlen) = m0 ? p3 : r3;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the words before the live loc
-    ok = atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)a_loc,
-                   (unsigned long long)(m0 ? p2 : r2)) == a_loc;
-  }
+  if (l4 == lane) ok = copy_entry(index + a_slot, a_loc, m0 ? p0 : r0, m0 ? p1 : r1,
+                                  m0 ? p2 : r2, m0 ? p3 : r3);
   ok = __shfl(ok, gbase + lane);
   return Reloc{__shfl(a_slot, gbase + lane), ok ? target : -2};
 }
 
-// The caller's CAS of the moved key's old slot failed: drop the copy relocate_one made
-// (loc first, then the digest words, so the key's digest never stays behind in a dead
-// slot that a later insert of the same key could match beside its live entry).
+// The caller's CAS of the moved key's old slot failed: drop the copy relocate_one made.
 __device__ __forceinline__ void undo_relocation(Entry* __restrict__ index, uint64_t alt,
                                              uint64_t loc) {
-  Entry* const a = index + alt;
-  if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)loc, 0ull) ==
-      loc) {
-    a->d0 = 0;
-    a->d1 = 0;
-  }
+  drop_entry(index + alt, loc);
 }
 
 // One SET row's index insert by its 4-lane group (uniform arguments across the group;
@@ -1592,12 +1623,12 @@ __device__ __forceinline__ void index_insert(
     // landed yet (dedupe leaves one row per key, so it is never this key's entry):
     // taking it as our own would CAS that row's claim away and lose its SET.
     const uint64_t span = head_new - base;  // locs of this batch: (base, head_new]
-    const bool in1 = w1[2] - base - 1 < span;
-    const bool in2 = w2[2] - base - 1 < span;
+    const bool in1 = w1[2] - base - 1 < span || w1[2] == kLockedLoc;
+    const bool in2 = w2[2] - base - 1 < span || w2[2] == kLockedLoc;
     const bool m1 = w1[0] == d.lo && w1[1] == d.hi && !in1;
     const bool m2 = w2[0] == d.lo && w2[1] == d.hi && !in2;
-    const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
-    const bool v2 = entry_live(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
+    const bool v1 = !entry_free(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
+    const bool v2 = !entry_free(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
     const uint32_t mmask = (uint32_t)((__ballot(m1) >> gbase) & 0xfull) |
                            ((uint32_t)((__ballot(m2) >> gbase) & 0xfull) << 4);
     const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
@@ -1705,12 +1736,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       // landed yet (dedupe leaves one row per key, so it is never this key's entry):
       // taking it as our own would CAS that row's claim away and lose its SET.
       const uint64_t span = head_new - base;  // locs of this batch: (base, head_new]
-      const bool in1 = w1[2] - base - 1 < span;
-      const bool in2 = w2[2] - base - 1 < span;
+      const bool in1 = w1[2] - base - 1 < span || w1[2] == kLockedLoc;
+      const bool in2 = w2[2] - base - 1 < span || w2[2] == kLockedLoc;
       const bool m1 = w1[0] == d.lo && w1[1] == d.hi && !in1;
       const bool m2 = w2[0] == d.lo && w2[1] == d.hi && !in2;
-      const bool v1 = entry_live(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
-      const bool v2 = entry_live(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
+      const bool v1 = !entry_free(w1[2], (uint32_t)(w1[3] >> 32), head_new, cap, now);
+      const bool v2 = !entry_free(w2[2], (uint32_t)(w2[3] >> 32), head_new, cap, now);
       const uint32_t mmask = (uint32_t)((__ballot(m1) >> gbase) & 0xfull) |
                              ((uint32_t)((__ballot(m2) >> gbase) & 0xfull) << 4);
       const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
@@ -1769,7 +1800,7 @@ __device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword
                                 Entry* __restrict__ index, uint64_t mask, uint64_t base,
                                 uint64_t span, uint64_t head_new, uint64_t cap, uint32_t now,
                                 uint32_t* __restrict__ claim_out, unsigned long long& evicted,
-                                unsigned long long& lost) {
+                                unsigned long long& bytes, unsigned long long& lost) {
   const uint64_t bb[2] = {bucket1(d, mask), bucket2(d, mask)};
   for (int attempt = 0; attempt < 16; ++attempt) {
     Entry* target = nullptr;
@@ -1781,6 +1812,7 @@ __device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword
       Entry* const x = index + bb[e >> 2] * kEntriesPerBucket + (e & 3);
       const uint64_t l = agent_load(&x->loc);
       const uint64_t w = agent_load(reinterpret_cast<const uint64_t*>(&x->vlen));
+      if (l == kLockedLoc) continue;  // another inserter's copy in flight
       if (!entry_live(l, (uint32_t)(w >> 32), head_new, cap, now)) {
         target = x;
         expected = l;
@@ -1793,9 +1825,13 @@ __device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword
       for (int e = 0; e < 8 && !target; ++e) {
         Entry* const x = index + bb[e >> 2] * kEntriesPerBucket + (e & 3);
         const uint64_t l = agent_load(&x->loc);
-        if (l - base - 1 < span) continue;  // another claim of this batch
+        if (l - base - 1 < span || l == kLockedLoc) continue;  // a claim of this batch / a copy
         const Digest de{agent_load(&x->d0), agent_load(&x->d1)};
         const uint64_t w = agent_load(reinterpret_cast<const uint64_t*>(&x->vlen));
+        // the words belong to loc l only if l is still there (a concurrent insert may have
+        // replaced the entry between the loads): re-check after reading them
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (agent_load(&x->loc) != l) continue;
         const uint64_t x1 = bucket1(de, mask), x2 = bucket2(de, mask);
         const uint64_t own = bb[e >> 2];
         const uint64_t ob = x1 == own ? x2 : (x2 == own ? x1 : own);
@@ -1804,13 +1840,8 @@ __device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword
           Entry* const a = index + ob * kEntriesPerBucket + k;
           const uint64_t al = agent_load(&a->loc);
           const uint64_t aw = agent_load(reinterpret_cast<const uint64_t*>(&a->vlen));
-          if (entry_live(al, (uint32_t)(aw >> 32), head_new, cap, now)) continue;
-          a->d0 = de.lo;
-          a->d1 = de.hi;
-          *reinterpret_cast<uint64_t*>(&a->vlen) = w;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the words before the live loc
-          if (atomicCAS(reinterpret_cast<unsigned long long*>(&a->loc), (unsigned long long)al,
-                        (unsigned long long)l) == al) {
+          if (!entry_free(al, (uint32_t)(aw >> 32), head_new, cap, now)) continue;
+          if (copy_entry(a, al, de.lo, de.hi, l, w)) {
             target = x;
             expected = l;
             copy = a;
@@ -1825,21 +1856,15 @@ __device__ void deferred_insert(const Digest& d, uint64_t myloc, uint64_t myword
       }
     }
     if (!target) continue;
-    if (atomicCAS(reinterpret_cast<unsigned long long*>(&target->loc),
-                  (unsigned long long)expected, (unsigned long long)myloc) == expected) {
-      target->d0 = d.lo;
-      target->d1 = d.hi;
-      *reinterpret_cast<uint64_t*>(&target->vlen) = myword;
+    // the row's own entry goes in through the same lock: a concurrent copy can never
+    // land its words in the slot between this CAS and the words below
+    if (copy_entry(target, expected, d.lo, d.hi, myloc, myword)) {
       *claim_out = (uint32_t)(target - index);
       evicted += evict ? 1 : 0;
+      bytes += (uint32_t)myword;
       return;
     }
-    if (copy &&  // the moved key changed meanwhile: drop the copy (loc, then digest)
-        atomicCAS(reinterpret_cast<unsigned long long*>(&copy->loc), (unsigned long long)expected,
-                  0ull) == expected) {
-      copy->d0 = 0;
-      copy->d1 = 0;
-    }
+    if (copy) drop_entry(copy, expected);  // the moved key changed meanwhile: drop the copy
   }
   ++lost;
 }
@@ -1871,14 +1896,15 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kBlock)
       if (size[i]) ring[(rtail + cnt_off[i]) & rmask] = base + off[i] + 0;
-  unsigned long long evicted = 0, lost = 0;
+  unsigned long long evicted = 0, lost = 0, bytes = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
     uint32_t c = claim[i];
     if (c == kClaimDeferred) {
       claim[i] = ~0u;
       deferred_insert(keys[i], base + off[i] + 1, pack2(vlen[i], expire ? expire[i] : 0u), index,
-                      mask, base, off[n], base + off[n], cap, now, claim + i, evicted, lost);
+                      mask, base, off[n], base + off[n], cap, now, claim + i, evicted, bytes,
+                      lost);
       continue;  // its words are final (deferred rows are not re-claimed by the batch)
     }
     if (c == ~0u) continue;
@@ -1889,7 +1915,8 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
     e->d1 = d.hi;
     *reinterpret_cast<uint64_t*>(&e->vlen) = pack2(vlen[i], expire ? expire[i] : 0u);
   }
-  block_count(ctr, evicted, &CacheCounters::set_evicted, lost, &CacheCounters::set_dropped);
+  block_count(ctr, evicted, &CacheCounters::set_evicted, lost, &CacheCounters::set_dropped, bytes,
+              &CacheCounters::set_bytes);
 }
 
 // ---------------------------------------------------------------------------------

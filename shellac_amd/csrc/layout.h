@@ -69,9 +69,20 @@ SH_HD uint64_t bucket2(const Digest& d, uint64_t mask) {
   return b2 == b1 ? (b1 ^ 1) & mask : b2;
 }
 
+// An entry's loc while one inserter rewrites its digest / vlen words (a relocation copy
+// being written, or one being dropped): neither live (probes and matches skip it) nor free
+// (no other inserter may claim it). Only the thread that stored it moves the slot on.
+constexpr uint64_t kLockedLoc = ~0ull - 1;
+
 SH_HD bool entry_live(uint64_t loc, uint32_t expire, uint64_t head, uint64_t capacity,
                       uint32_t now) {
-  return loc != 0 && head <= (loc - 1) + capacity && (expire == 0 || expire > now);
+  return loc != 0 && loc != kLockedLoc && head <= (loc - 1) + capacity &&
+         (expire == 0 || expire > now);
+}
+// A slot an inserter may claim: neither live nor locked.
+SH_HD bool entry_free(uint64_t loc, uint32_t expire, uint64_t head, uint64_t capacity,
+                      uint32_t now) {
+  return loc != kLockedLoc && !entry_live(loc, expire, head, capacity, now);
 }
 
 // CLOCK eviction geometry shared by the HBM and host engines, so both make identical

@@ -105,21 +105,29 @@ std::vector<std::string> marker_names(std::string_view v) {
 }
 
 // Secondary key of one variant: URL key + the request's values of the varied headers.
+// Repeated headers combine in order with "," (RFC 7230 §3.2.2: `X: a` + `X: b` is the
+// same field value as `X: a,b`, so they select the same variant), and each combined value
+// is length-prefixed, so no value bytes (separators included) can forge another key.
+// Names are tokens from the response's Vary header (no separator bytes).
 std::string vary_key(const std::string& base, const std::vector<std::string>& names,
                      const std::vector<Header>& req) {
   std::string k = base;
   k += '\x1f';
+  std::string v;
   for (const auto& n : names) {
-    k += n;
-    k += '=';
+    v.clear();
     bool first = true;
     for (const auto& h : req)
       if (h.first == n) {
-        if (!first) k += ',';
-        k += h.second;
+        if (!first) v += ',';
+        v += h.second;
         first = false;
       }
-    k += '\x1e';
+    k += n;
+    k += '=';
+    k += std::to_string(v.size());
+    k += ':';
+    k += v;
   }
   return k;
 }

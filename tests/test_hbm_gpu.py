@@ -575,6 +575,63 @@ def test_serve_get_relaunches_and_sees_new_sets(cuda_dev):
     assert all(r is not None and r[0] == b"b" * 3000 for r in got)
 
 
+def test_serve_get_multi_round_jobs_beside_wrapping_sets(cuda_dev):
+    """Edge-server jobs whose records span several copy rounds (29 x 8 KiB = 232 KiB, a
+    round is 112 KiB) answered while SET chains on another stream keep wrapping the log over
+    them: every record that comes back with a valid magic word names its own key and holds
+    its own bytes; torn ones are misses (magic zeroed). The server re-reads the claim after
+    the last round before it publishes."""
+    from shellac_amd.ops.cache import ITEM_MAGIC
+
+    log = 1 << 20
+    shard = CacheShard(log, 1 << 12, 1 << 14, cuda_dev, evict="fifo")
+    K, V = 29, 8192
+    ka = [f"/tear/a{i}".encode() for i in range(K)]
+    da = digest_strings(ka, cuda_dev)
+    va, vao, val = pack_values([bytes([i + 1]) * V for i in range(K)], cuda_dev)
+    # filler batches: 32 x 8 KiB = 256 KiB of 0xEE bytes each, 4 per log lap
+    fills = []
+    for b in range(4):
+        kb = [f"/tear/b{b}/{i}".encode() for i in range(32)]
+        fills.append((digest_strings(kb, cuda_dev),) + pack_values([b"\xee" * V] * 32, cuda_dev))
+    shard.store(da, va, vao, val)
+    torch.cuda.synchronize()
+    dh = da.cpu().contiguous()
+    out = torch.zeros(1 << 20, dtype=torch.uint8, device=cuda_dev)
+    off = torch.zeros(K + 1, dtype=torch.int64, device=cuda_dev)
+    side = torch.cuda.Stream(device=cuda_dev)
+    hits = torn = 0
+    for rnd in range(6):
+        with torch.cuda.stream(side):  # queued, not waited for: runs beside the jobs
+            for rep in range(40):
+                shard.store(da, va, vao, val)
+                for f in fills[: 1 + rep % 4]:
+                    shard.store(*f)
+        for job in range(150):
+            assert shard._impl.serve_get(dh.data_ptr(), K, out.data_ptr(), out.numel(),
+                                         off.data_ptr(), shard.now(), 5)
+            shard._impl.serve_wait(5, 10000)
+            o = out.cpu().numpy()
+            offs = off.cpu().numpy()
+            if int(offs[K]) > out.numel():
+                continue
+            for i in range(K):
+                if offs[i + 1] == offs[i]:
+                    continue
+                base = int(offs[i])
+                hdr = o[base: base + 32].view(np.uint32)
+                if int(hdr[7]) != ITEM_MAGIC:
+                    torn += 1
+                    continue
+                words = o[base: base + 16].view(np.int64)
+                assert words[0] == int(dh[i, 0]) and words[1] == int(dh[i, 1])
+                body = o[base + 32: base + 32 + V]
+                assert int(hdr[4]) == V and bool((body == i + 1).all()), (rnd, job, i)
+                hits += 1
+        side.synchronize()
+    assert hits > 0
+
+
 def test_store_graph_matches_store(cuda_dev):
     """A SET replayed from a captured hipGraph (fixed size class, skip-row padding, one
     executable per head-slot parity) leaves the shard exactly as the launched SET
