@@ -84,6 +84,9 @@ def parse():
                          "RCCL communicator (every collective call of the N-GPU step; all keys "
                          "are local, so no interconnect traffic) — a rehearsal, not a scaling "
                          "number")
+    ap.add_argument("--comm-mode", choices=["single", "channels"], default="single",
+                    help="routed step: every collective on one communicator and one stream in "
+                         "a fixed order (single), or one communicator per channel (channels)")
     ap.add_argument("--evict", choices=["clock", "fifo"], default="clock",
                     help="value-log eviction policy of the shards")
     ap.add_argument("--batches", type=int, default=16,
@@ -318,7 +321,7 @@ def main():
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
     sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group,
-                      routed=True if routed1 else None)
+                      routed=True if routed1 else None, comm_mode=args.comm_mode)
     sc.coalesce = not args.no_coalesce
 
     # populate: every rank SETs its slice of the key space through the routed path
@@ -423,6 +426,19 @@ def main():
     sc.sync_sets()
     after = shard.counters()
     head1 = shard.head()
+    diag = None
+    if sc._engine is not None:
+        # the routed step's SET exchange: early appends (look-ahead), carried rows
+        e = sc._engine
+        carried, cbytes, clost = e.carry_stats()
+        diag = {"early_set_steps": int(e.early_sets), "set_rows_carried": carried,
+                "set_bytes_carried": cbytes, "set_rows_lost": clost,
+                "set_slot_caps": [int(x) for x in e.set_caps()],
+                "log_head_gib": round(head1 / (1 << 30), 3),
+                "reinserted_steps": after["reinserted"] - before["reinserted"]}
+        if replica is not None:
+            diag["replica_head_gib"] = round(replica.head() / (1 << 30), 3)
+            diag["replica_log_gib"] = round(args.replica_gb, 3)
     # owner-shard counters cover the GETs that left the replica tier; replica hits
     # are counted by the serving step
     rep_hits = sc.stats["replica_hits"] - st0["replica_hits"]
@@ -519,7 +535,7 @@ def main():
         p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
         p_sc = ShardedCache(p_shard, group=group, replica=replica, data_group=data_group,
-                            routed=True if routed1 else None)
+                            routed=True if routed1 else None, comm_mode=args.comm_mode)
         p_sc.coalesce = sc.coalesce
         if replica is not None:
             p_sc._hot, p_sc._hot_dir = sc._hot, None
@@ -588,6 +604,7 @@ def main():
         "reinserted_bytes_per_step": round((after["reinsert_bytes"] - before["reinsert_bytes"])
                                            / args.steps),
         "edge": args.edge,
+        "routed_diag": diag,
         # the same step with the value log wrapped (eviction in every SET batch)
         "log_wrapped": wrapped,
         # the same under capacity pressure (a log the key space barely fits: reinsertions)

@@ -91,19 +91,28 @@ class Workload:
         g = torch.Generator(device=self.device).manual_seed(seed)
         return torch.randint(0, self.total_keys, (n,), generator=g, device=self.device)
 
-    def set_batch(self, ids: torch.Tensor, ttl_expire: int = 0):
+    def _offsets(self, ids: torch.Tensor, version: int) -> torch.Tensor:
+        off = self.val_off.index_select(0, ids)
+        if version:
+            # another payload of the same size (an updated object): shifted in the pool
+            span = self.pool_bytes - self.max_val - 16
+            off = torch.remainder(off + version * 1048573 * 16, span) & ~15
+        return off
+
+    def set_batch(self, ids: torch.Tensor, ttl_expire: int = 0, version: int = 0):
+        """SETs of objects `ids`; `version` > 0 gives them other payload bytes (updates)."""
         from ..models.sharded_cache import SetBatch
 
         n = ids.numel()
         return SetBatch(
             keys=self.digests.index_select(0, ids).contiguous(),
             values=self.pool,
-            val_off=self.val_off.index_select(0, ids).contiguous(),
+            val_off=self._offsets(ids, version).contiguous(),
             vlen=self.vlen.index_select(0, ids).contiguous(),
             flags=(ids % 65536).to(torch.int32).contiguous(),
             expire=torch.full((n,), ttl_expire, dtype=torch.int32, device=self.device),
         )
 
-    def expected_value(self, i: int) -> bytes:
-        o = int(self.val_off[i])
+    def expected_value(self, i: int, version: int = 0) -> bytes:
+        o = int(self._offsets(torch.tensor([i], device=self.device), version)[0])
         return self.pool[o : o + int(self.vlen[i])].cpu().numpy().tobytes()

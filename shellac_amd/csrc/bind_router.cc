@@ -117,6 +117,19 @@ void bind_router(py::module_& m) {
       }, py::arg("hot"), py::arg("nhot"), py::arg("dir") = 0, py::arg("changed") = false)
       .def_property_readonly("row_words", &RoutedStep::row_words)
       .def("caps", &RoutedStep::caps)
+      .def("prepare", &RoutedStep::prepare)
+      .def("set_caps", &RoutedStep::set_caps)
+      .def("set_set_cap_override", &RoutedStep::set_set_cap_override)
+      .def("carry_stats", [](RoutedStep& r) {
+        py::gil_scoped_release nogil;
+        return r.carry_stats();
+      })
+      .def("take_stats", &RoutedStep::take_stats)
+      .def("harvest_all", [](RoutedStep& r) {
+        py::gil_scoped_release nogil;
+        r.harvest_all();
+      })
+      .def_property("single_comm", &RoutedStep::single_comm, &RoutedStep::set_single_comm)
       .def("reset_caps", &RoutedStep::reset_caps)
       .def("set_cap_override", &RoutedStep::set_cap_override)
       .def("plan", [](RoutedStep& r, uintptr_t keys, int64_t n, HbmCache* replica, uint32_t now,
@@ -189,19 +202,19 @@ void bind_router(py::module_& m) {
                       uintptr_t sval_off, uintptr_t svalues, int64_t ns, bool fanout,
                       bool coalesce, HbmCache* shard, uintptr_t data, uintptr_t out_size,
                       uintptr_t out_off, uintptr_t s, uintptr_t sset, uintptr_t sasm,
-                      uintptr_t ready) {
+                      uintptr_t ready, int64_t svalues_bytes) {
         py::gil_scoped_release nogil;
         return r.step(P<const Digest>(keys), n, replica, now, P<const Digest>(skeys),
                       P<const uint32_t>(svlen), P<const uint32_t>(sflags),
                       P<const uint32_t>(sexpire), P<const uint64_t>(sval_off),
                       P<const uint8_t>(svalues), ns, fanout, coalesce, shard, P<uint8_t>(data),
                       P<uint64_t>(out_size), P<uint64_t>(out_off), S(s), S(sset), S(sasm),
-                      reinterpret_cast<hipEvent_t>(ready));
+                      reinterpret_cast<hipEvent_t>(ready), svalues_bytes);
       }, py::arg("keys"), py::arg("n"), py::arg("replica").none(true), py::arg("now"),
          py::arg("skeys"), py::arg("svlen"), py::arg("sflags"), py::arg("sexpire"),
          py::arg("sval_off"), py::arg("svalues"), py::arg("ns"), py::arg("fanout"),
          py::arg("coalesce"), py::arg("shard"), py::arg("data"), py::arg("out_size"),
          py::arg("out_off"), py::arg("stream"), py::arg("set_stream"), py::arg("asm_stream"),
-         py::arg("inputs_ready") = 0)
+         py::arg("inputs_ready") = 0, py::arg("svalues_bytes") = 0)
       .def_property_readonly("sets_pending", &RoutedStep::sets_pending);
 }

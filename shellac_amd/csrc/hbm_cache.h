@@ -292,6 +292,10 @@ size_t device_scan_tmp_bytes(int64_t n);
 constexpr uint64_t kSegSkip = ~0ull;
 void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off, int64_t n,
              uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
+// Device-count variant (absolute source addresses in src_off): the number of segments is
+// *n_dev, read by the kernel, so a segment list the GPU built needs no host read.
+void segcopy_dev(const uint64_t* src_off, const uint64_t* dst_off, const int64_t* n_dev,
+                 uint8_t* dst, hipStream_t s, uint64_t dst_cap = ~0ull);
 // Sized variant: segment i holds seg_len[i] bytes at dst + dst_off[i] (dst_off ascending,
 // gaps allowed and left untouched, dst_off[n] = the extent); a segment that does not end
 // within `cap` is dropped (the others still land). Offsets / lengths multiples of 16.

@@ -837,6 +837,8 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
 // the `head_ptr` slot) and is copied only when it ends within `cap`; the bytes between a
 // segment's end and the next segment's start are left untouched (gaps, headers written
 // by someone else), and segments past `cap` are dropped instead of the whole copy.
+// Mode 3: mode 0 with the segment count read from the device word `head_ptr` points at
+// (a plan whose segment list the GPU built: no host read of its length).
 // Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
 // src + src_off[j] + (w - 32); destination = log + (base + dst_off[j]) % cap + w, where
 // the batch is at most cap/2 so the modulo is one compare against the wrap point.
@@ -860,8 +862,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   __shared__ uint64_t s_src[TSC];
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
+  if (MODE == 3) n = *reinterpret_cast<const int64_t*>(head_ptr);  // count on the device
   const uint64_t total = dst_off[n];
-  if (MODE == 0 && total > cap) return;  // MODE 0: `cap` = destination capacity
+  if ((MODE == 0 || MODE == 3) && total > cap) return;  // MODE 0/3: destination capacity
   const uint64_t* __restrict__ seg_len = MODE == 2 ? head_ptr : nullptr;
   __shared__ uint32_t s_len[MODE == 2 ? TSC : 1];  // records < 4 GiB
   const int64_t nchunks = (int64_t)(total >> 4);
@@ -918,7 +921,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         if (MODE == 2) {
           if (x < seg_start || w >= s_len[jl]) continue;  // gap / dropped: untouched
           sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
-        } else if (MODE == 0) {
+        } else if (MODE == 0 || MODE == 3) {
           // a kSegSkip source leaves the segment's bytes untouched (no load, no store)
           if (seg_src == kSegSkip) continue;
           // integer address math: src may be null with absolute addresses in src_off
@@ -2620,6 +2623,13 @@ void segcopy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_of
   if (n <= 0) return;
   launch_segcopy<0>(s, src, src_off, dst_off, n, dst, nullptr, nullptr, nullptr, nullptr, nullptr,
                     dst_cap);
+  HIP_OK(hipGetLastError());
+}
+
+void segcopy_dev(const uint64_t* src_off, const uint64_t* dst_off, const int64_t* n_dev,
+                 uint8_t* dst, hipStream_t s, uint64_t dst_cap) {
+  launch_segcopy<3>(s, nullptr, src_off, dst_off, (int64_t)0, dst, nullptr, nullptr, nullptr,
+                    nullptr, reinterpret_cast<const uint64_t*>(n_dev), dst_cap);
   HIP_OK(hipGetLastError());
 }
 

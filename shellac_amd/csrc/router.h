@@ -16,6 +16,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <deque>
 #include <memory>
 #include <vector>
 
@@ -63,9 +64,16 @@ const StepStreams& step_streams(int device);
 // not fit its slot is answered as a miss (always a valid cache answer) and counted, and
 // the next steps' capacities grow. The first step after a reset calibrates the
 // capacities with two host reads (the only synchronising step).
-// SETs travel with exact split sizes: the host reads them from the all-gathered row in
-// the middle of the step (the GPU is still busy with the GET exchange queued before), so
-// no stall either. Self traffic never enters a collective: a rank probes its own slot in
+// SETs travel the same way in step(): per-peer slots of capS records + capSB value bytes
+// with the row / byte count in a 16-B slot header, packed from a segment list the GPU builds
+// (k_set_fit, k_set_pack_segs, segcopy_dev). A SET row that does not fit its slot is never
+// dropped: it is carried (key, metadata, value bytes) into the next step's plan, ahead of
+// that step's own rows, and stored one step later. The host reads nothing in the middle of
+// a step: the capacities of step i come from the matrices of steps <= i - 2 (the host waits
+// for a matrix two steps old, complete long before), every rank the same.
+// (The multi-call path of calibrating steps still exchanges SETs with exact sizes read by
+// the host: set_splits / pack_sets / store_sets.)
+// Self traffic never enters a collective: a rank probes its own slot in
 // place and gathers its own replies straight into the response buffer.
 //
 // Slot layouts (o(q) = q < rank ? q : q - 1 orders the other ranks):
@@ -87,7 +95,15 @@ const StepStreams& step_streams(int device);
 //   -> on the SET stream: pack_sets(S) -> [a2a S -> Rs, exact sizes] -> store_sets(Rs),
 //      i.e. the main-shard SET chain beside the reply gather
 //   -> on a side stream after the reply a2a: assemble(data, out) -> wait() before reading.
-//   (step(): the reply transfer and the assembly share the caller's `sasm` stream.)
+//   (step(): the reply transfer and the assembly share the caller's `sasm` stream; the SET
+//   exchange uses fixed slots: pack_fixed(S) -> [a2a S -> Rs, slotS per peer] ->
+//   store_fixed(Rs), no host read.)
+// Communicator modes (step()): `single` (default) issues every collective of a step on ONE
+// communicator and ONE stream (the assembly stream) in a fixed order — all-gather, request
+// a2a, reply a2a, SET a2a — with events carrying the data dependencies to and from the
+// compute streams: every rank sees the same FIFO of collectives, so no two collectives can
+// wait on each other. `channels` keeps one communicator per channel on the stream that
+// produces its data (the three may run concurrently; see docs/ARCHITECTURE.md).
 class RoutedStep {
  public:
   static constexpr int kExtras = 8;
@@ -110,11 +126,34 @@ class RoutedStep {
   // calibrate_reply during the step; capL (per GET row from this rank's history) by
   // calibrate_local when there is no history yet.
   std::vector<int64_t> caps(int64_t n) const;
+  // Before a step: take in the matrices of the steps two back (their history), then caps(n).
+  // Call this (not caps) to size a step's buffers: step() does the same harvest first.
+  std::vector<int64_t> prepare(int64_t n);
   void reset_caps();  // next step calibrates (new ring, new hot set)
   // Tests: fixed capacities (every rank the same), overriding the policy; 0s clear it.
   void set_cap_override(int64_t capG, int64_t capD, int64_t capL) {
     ovr_ = {capG, capD, capL};
   }
+  // SET slot capacities of step(): {capS rows, capSB value bytes per peer slot, capSelf
+  // rows, capSelfB bytes stored from this rank's own rows}; from the history like caps().
+  std::vector<int64_t> set_caps() const;
+  // Tests: fixed SET capacities (every rank the same); 0s clear it.
+  void set_set_cap_override(int64_t capS, int64_t capSB, int64_t capSelf, int64_t capSelfB) {
+    ovr_s_ = {capS, capSB, capSelf, capSelfB};
+  }
+  // {SET rows carried into a later step, their bytes, rows lost (carry buffer full)} since
+  // construction (host read: waits for the device).
+  std::vector<int64_t> carry_stats();
+  // Lagged per-step statistics [n_local, n_dup, GET rows sent off-rank, rows over capG,
+  // reply rows dropped], summed over the steps harvested since the last call.
+  std::vector<int64_t> take_stats();
+  // Host: wait for every published step's matrix and add its statistics (not its history:
+  // the capacities stay on the two-step lag every rank follows).
+  void harvest_all();
+  // step(): one communicator and one stream for every collective (default) or one
+  // communicator per channel.
+  void set_single_comm(bool single) { single_ = single; }
+  bool single_comm() const { return single_; }
 
   // GET routing (coalescing + replica probe first), the digests of peer p's rows written
   // into its slot of G (rows past capG: overflow, answered as misses), SET routing + hot
@@ -176,13 +215,16 @@ class RoutedStep {
   // the plan runs on a stream of its own beside the previous step's reply gather instead
   // of after everything queued on `s`. Returns
   // [n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped].
+  // `svalues_bytes`: the size of the SET batch's value buffer (sizes the carry buffer).
+  // Returns take_stats() (the statistics of earlier steps, two steps behind).
   std::vector<int64_t> step(const Digest* keys, int64_t n, HbmCache* replica, uint32_t now,
                             const Digest* skeys, const uint32_t* svlen, const uint32_t* sflags,
                             const uint32_t* sexpire, const uint64_t* sval_off,
                             const uint8_t* svalues, int64_t ns, bool fanout, bool coalesce,
                             HbmCache* shard, uint8_t* data, uint64_t* out_size,
                             uint64_t* out_off, hipStream_t s, hipStream_t sset,
-                            hipStream_t sasm, hipEvent_t inputs_ready = nullptr);
+                            hipStream_t sasm, hipEvent_t inputs_ready = nullptr,
+                            int64_t svalues_bytes = 0);
   bool sets_pending() const { return sets_pending_; }
   int rank() const { return rank_; }
 
@@ -193,7 +235,24 @@ class RoutedStep {
   };
   template <typename T>
   T* buf(int slot, size_t count);
-  void note_matrix();
+  // history (hist = true) and statistics of one all-gathered matrix
+  std::vector<int64_t> note_matrix(const int64_t* m, int64_t n, int64_t capG, bool hist);
+  void harvest(int64_t upto, bool hist);
+  void add_stats(const std::vector<int64_t>& st);
+  // fixed-slot SET exchange of step()
+  void ensure_carry(int64_t rows, uint64_t bytes);
+  void pack_fixed(uint8_t* S, int64_t slotS, const std::vector<int64_t>& sc, hipStream_t ps);
+  void store_fixed(const uint8_t* Rs, int64_t slotS, const std::vector<int64_t>& sc,
+                   HbmCache* shard, HbmCache* replica, uint32_t now, hipStream_t sset,
+                   hipEvent_t index_after, bool allow_reclaim);
+  // a collective on `home` (channels) or on the comm stream with event hops (single)
+  template <typename F>
+  void collective(hipStream_t home, hipStream_t comm_stream, int ch, F issue);
+  // deferred frees: a block another step's queued work may still read is freed once events
+  // recorded on every stream the executor uses have passed (no device synchronisation)
+  void retire(void* p);
+  void reap(bool all);
+  void note_stream(hipStream_t s);
 
   int w_, rank_, device_;
   const uint32_t* pts_ = nullptr;
@@ -255,6 +314,49 @@ class RoutedStep {
   uint64_t *lk_loc_ = nullptr, *lk_size_ = nullptr, *lk_off_ = nullptr;
   int64_t* rb_ = nullptr;       // reply bytes per requester (W) + dropped rows (1)
   std::vector<int64_t> mat_;    // host copy of this step's matrix (after set_splits)
+  // ---- lagged matrices (step()): pinned ring, harvested two steps later ----
+  static constexpr int kPend = 4;
+  struct Pend {
+    int64_t step, n, capG;
+    int slot;
+    bool hist_done, stats_done;
+  };
+  std::deque<Pend> pend_;
+  int64_t* host_ring_ = nullptr;
+  hipEvent_t ev_ring_[kPend] = {};
+  int ring_next_ = 0;
+  int64_t step_id_ = 0;
+  std::vector<int64_t> stat_acc_ = std::vector<int64_t>(5, 0);
+  // ---- fixed-slot SETs and the carry (two parities) ----
+  std::vector<int64_t> hist_s_, hist_sb_, hist_self_, hist_selfb_;
+  std::vector<int64_t> ovr_s_ = {0, 0, 0, 0};
+  Digest* ck_[2] = {nullptr, nullptr};
+  uint32_t *cvl_[2] = {nullptr, nullptr}, *cfl_[2] = {nullptr, nullptr},
+           *cex_[2] = {nullptr, nullptr};
+  uint64_t* cval_[2] = {nullptr, nullptr};
+  int32_t* cdst_[2] = {nullptr, nullptr};
+  uint8_t* cbytes_[2] = {nullptr, nullptr};
+  int64_t ccap_p_[2] = {0, 0};     // carry rows per parity
+  uint64_t cbcap_p_[2] = {0, 0};   // carry value bytes per parity
+  unsigned long long* cctr_ = nullptr;  // [parity][rows, bytes] + totals[rows, bytes, lost]
+  bool carry_written_[2] = {false, false};
+  hipEvent_t ev_carry_[2] = {nullptr, nullptr};
+  int64_t gt_ = 0;       // SET plan workgroups (carry + batch) of this step
+  int64_t nrouted_max_ = 0;
+  uint64_t* set_meta_[2] = {nullptr, nullptr};  // per parity: headers, fit, segment bases
+  hipEvent_t ev_sdone_[2] = {nullptr, nullptr};  // the SET side of a parity is done
+  bool sdone_valid_[2] = {false, false};
+  int64_t sv_bytes_ = 0;
+  bool single_ = true;
+  hipEvent_t ev_c1_ = nullptr, ev_c2_ = nullptr, ev_pack_ = nullptr;
+  hipEvent_t ev_hot_ = nullptr;
+  bool hot_pending_ = false;
+  struct Dead {
+    void* p;
+    std::vector<hipEvent_t> ev;
+  };
+  std::vector<Dead> dead_;
+  std::vector<hipStream_t> seen_streams_;
   std::vector<int64_t> sset_;   // per destination SET bytes (send), rank order
   std::vector<int64_t> rset_;   // per source SET bytes (recv), rank order
 };

@@ -22,6 +22,7 @@ namespace shellac {
 
 namespace {
 
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 constexpr int kB = 256;
 constexpr int64_t kGroupRows = 2048;  // rows per workgroup in the counting sort
 constexpr int kMaxBuckets = 4097;
@@ -254,14 +255,58 @@ __global__ __launch_bounds__(kB) void k_route_hist(const Digest* __restrict__ ke
   if (threadIdx.x == 0 && ndup && s_dup) atomicAdd(ndup, (unsigned long long)s_dup);
 }
 
+// The SET planner's input rows: workgroups [0, Gc) take the rows the previous step carried
+// over (count on the device, clamped to the carry capacity, split evenly over the Gc
+// workgroups), workgroups [Gc, Gc + Gs) the batch, plen rows each, so a carried row always
+// sorts before the batch's rows of its destination (the batch's newer SETs win the
+// owner's dedupe). A carried row keeps its destination and tier (cdest = rank | tier << 29):
+// it is not routed again. Per-row outputs (owner, vpad): carried row j at j, batch row j at
+// ccap + j.
+struct SetRows {
+  const Digest* keys;
+  const uint32_t* vlen;
+  const uint32_t* flags;
+  const uint32_t* expire;
+  const uint64_t* val_off;
+  uint64_t values_base;
+  int64_t n;
+  const Digest* ckeys;
+  const uint32_t* cvlen;
+  const uint32_t* cflags;
+  const uint32_t* cexpire;
+  const uint64_t* cval;  // absolute value addresses
+  const int32_t* cdest;
+  const unsigned long long* cn;
+  int64_t ccap;
+  int32_t Gc;
+};
+constexpr int kTierBit = 29;  // forced destination's tier (carried rows)
+constexpr int kFanBit = 30;   // fan out to every rank (hot key)
+
+__device__ __forceinline__ void set_range(const SetRows& r, int64_t plen, bool* carry,
+                                          int64_t* i0, int64_t* i1, int64_t* v0) {
+  const int b = blockIdx.x;
+  *carry = b < r.Gc;
+  if (*carry) {
+    const int64_t nc = min((int64_t)*r.cn, r.ccap);
+    const int64_t pc = (nc + r.Gc - 1) / r.Gc;
+    *i0 = min(nc, (int64_t)b * pc);
+    *i1 = min(nc, *i0 + pc);
+    *v0 = 0;
+  } else {
+    *i0 = (int64_t)(b - r.Gc) * plen;
+    *i1 = min(r.n, *i0 + plen);
+    *v0 = r.ccap;
+  }
+}
+
 // SET planning, fused: input row j goes to its owner and (fan-out) to every rank when
 // its key is hot (tier 0 = owner copy, tier 1 = replica copy). Each workgroup handles
 // a contiguous range: owner / padded length per row, and the rows AND value bytes per
 // destination in one packed 64-bit LDS counter (rows | bytes << 32) so k_ps_scatter
 // can hand out row slots and byte ranges in the same order.
 __global__ __launch_bounds__(kB) void k_ps_dest_hist(
-    const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen, int64_t ns,
-    const uint32_t* __restrict__ pts, const int32_t* __restrict__ own, int npts,
+    SetRows sr, const uint32_t* __restrict__ pts, const int32_t* __restrict__ own, int npts,
     const Digest* __restrict__ hot_tab, uint64_t hot_mask,
     int32_t nb, int64_t plen, int32_t w, int32_t* __restrict__ owner,
     uint32_t* __restrict__ vpad, uint64_t* __restrict__ tcnt, uint64_t* __restrict__ tbytes) {
@@ -271,20 +316,31 @@ __global__ __launch_bounds__(kB) void k_ps_dest_hist(
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   const RingView rv = stage_ring(pts, own, npts, s_pts, s_own);
   __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
+  bool carry;
+  int64_t i0, i1, v0;
+  set_range(sr, plen, &carry, &i0, &i1, &v0);
   for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
-    const Digest k = keys[j];
-    const int o = ring_owner_of(k, rv.pts, rv.own, npts);
-    const bool h = hot_tab != nullptr && hot_hash_has(k, hot_tab, hot_mask);
-    owner[j] = h ? (o | (1 << 30)) : o;  // bit 30: fan out to every rank
-    const uint32_t vl = vlen[j];
+    int ow;
+    uint32_t vl;
+    bool h = false;
+    if (carry) {
+      ow = sr.cdest[j];
+      vl = sr.cvlen[j];
+    } else {
+      const Digest k = sr.keys[j];
+      const int o = ring_owner_of(k, rv.pts, rv.own, npts);
+      h = hot_tab != nullptr && hot_hash_has(k, hot_tab, hot_mask);
+      ow = h ? (o | (1 << kFanBit)) : o;
+      vl = sr.vlen[j];
+    }
+    owner[v0 + j] = ow;
     const uint32_t vp = vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
-    vpad[j] = vp;
+    vpad[v0 + j] = vp;
     const unsigned long long inc = 1ull | ((unsigned long long)vp << 32);
     if (h) {
       for (int r = 0; r < w; ++r) atomicAdd(&s_cb[r], inc);
     } else {
-      atomicAdd(&s_cb[o], inc);
+      atomicAdd(&s_cb[ow & ((1 << kTierBit) - 1)], inc);
     }
   }
   __syncthreads();
@@ -361,34 +417,42 @@ __global__ __launch_bounds__(1024) void k_ps_scan(uint64_t* __restrict__ tcnt,
 // rec = {lo, hi, vlen | flags << 32, expire | (voff | tier << 31) << 32} where voff is
 // the value's offset inside the destination peer's value block.
 __global__ __launch_bounds__(kB) void k_ps_scatter(
-    int64_t ns, int32_t nb, int64_t plen, const uint64_t* __restrict__ tcnt,
-    const uint64_t* __restrict__ tbytes, const Digest* __restrict__ keys,
-    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ expire, const uint64_t* __restrict__ val_off,
-    uint64_t values_base, const int32_t* __restrict__ owner, const uint32_t* __restrict__ vpad,
-    int32_t w, int64_t* __restrict__ srec, uint64_t* __restrict__ sval,
-    uint64_t* __restrict__ svoff) {
+    SetRows sr, int32_t nb, int64_t plen, const uint64_t* __restrict__ tcnt,
+    const uint64_t* __restrict__ tbytes, const int32_t* __restrict__ owner,
+    const uint32_t* __restrict__ vpad, int32_t w, int64_t* __restrict__ srec,
+    uint64_t* __restrict__ sval, uint64_t* __restrict__ svoff) {
   extern __shared__ unsigned long long s_cb[];
   for (int d = threadIdx.x; d < nb; d += kB) s_cb[d] = 0;
   __syncthreads();
   const int G = gridDim.x;
-  const int64_t i0 = (int64_t)blockIdx.x * plen, i1 = min(ns, i0 + plen);
+  bool carry;
+  int64_t i0, i1, v0;
+  set_range(sr, plen, &carry, &i0, &i1, &v0);
   for (int64_t j = i0 + threadIdx.x; j < i1; j += kB) {
-    const int ow = owner[j];
-    const bool fan = (ow >> 30) != 0;
-    const int o = ow & ((1 << 30) - 1);
-    const uint64_t pad = vpad[j];
-    const Digest k = keys[j];
-    const uint64_t r2 = (uint64_t)vlen[j] | ((uint64_t)(flags ? flags[j] : 0u) << 32);
-    const uint64_t ex = expire ? expire[j] : 0u;
-    const uint64_t src = values_base + val_off[j];
+    const int ow = owner[v0 + j];
+    const bool fan = (ow >> kFanBit) & 1;
+    const int o = ow & ((1 << kTierBit) - 1);
+    const uint64_t pad = vpad[v0 + j];
+    Digest k;
+    uint64_t r2, ex, src;
+    if (carry) {
+      k = sr.ckeys[j];
+      r2 = (uint64_t)sr.cvlen[j] | ((uint64_t)sr.cflags[j] << 32);
+      ex = sr.cexpire[j];
+      src = sr.cval[j];
+    } else {
+      k = sr.keys[j];
+      r2 = (uint64_t)sr.vlen[j] | ((uint64_t)(sr.flags ? sr.flags[j] : 0u) << 32);
+      ex = sr.expire ? sr.expire[j] : 0u;
+      src = sr.values_base + sr.val_off[j];
+    }
     const int r0 = fan ? 0 : o, r1 = fan ? w : o + 1;
     for (int d = r0; d < r1; ++d) {
       const unsigned long long old = atomicAdd(&s_cb[d], 1ull | (pad << 32));
       const int64_t pos = (int64_t)tcnt[(int64_t)d * G + blockIdx.x] + (int64_t)(old & 0xFFFFFFFFull);
       const uint64_t vglob = tbytes[(int64_t)d * G + blockIdx.x] + (old >> 32);
       const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
-      const uint64_t tier = d != o ? 1ull : 0ull;
+      const uint64_t tier = fan ? (d != o ? 1ull : 0ull) : (uint64_t)((ow >> kTierBit) & 1);
       int64_t* rec = srec + pos * 4;
       rec[0] = (int64_t)k.lo;
       rec[1] = (int64_t)k.hi;
@@ -511,7 +575,7 @@ enum Slot {
   kRlLoc, kRlSize0, kRlSize1, kRlOff0, kRlOff1, kDestG, kRoute0, kRoute1, kCntG, kWsG,
   kCoTab, kFirst0, kFirst1, kOwnerS, kVpad, kTcnt, kTbytes, kSrec, kSval, kSvoff, kCntS,
   kOwnCnt, kLkLoc, kLkSize, kLkOff, kDstA, kDstB, kSrcA, kSrcB, kHdr, kUsed, kRb, kTab,
-  kSegOff, kSegSrc,
+  kSegOff, kSegSrc, kTcnt1, kTbytes1, kCntS1, kSegOffF, kSegSrcF,
   kRkeys, kV0, kV1, kFl, kEx, kRoff, kReserve, kSrec1, kSval1, kSvoff1,
   // RoutedStep::step's own exchange buffers (the multi-call path gets them from Python)
   kRowB, kMatB, kGB, kR0, kR1, kS0, kS1, kRs0, kRs1, kNumSlots
@@ -757,6 +821,234 @@ __global__ __launch_bounds__(kB) void k_rs_fill_slots(
 
 int64_t align_up64(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
+// ---- fixed-slot SET exchange (RoutedStep::step) -----------------------------------------
+// set_meta_ words (W ranks): [slot headers {rows, bytes} x W (16-B aligned) | fit (W) |
+// fit bytes (W) | segment base (W) | nseg, self block start, routed rows, 0...].
+struct SetMeta {
+  int W;
+  __device__ __forceinline__ uint64_t* hdr(uint64_t* m) const { return m; }
+  __device__ __forceinline__ uint64_t* fit(uint64_t* m) const { return m + 2 * W; }
+  __device__ __forceinline__ uint64_t* fitb(uint64_t* m) const { return m + 3 * W; }
+  __device__ __forceinline__ uint64_t* segbase(uint64_t* m) const { return m + 4 * W; }
+  __device__ __forceinline__ uint64_t* tail(uint64_t* m) const { return m + 5 * W; }
+};
+int64_t set_meta_words(int W) { return 5 * (int64_t)W + 8; }
+
+__device__ __forceinline__ uint32_t rec_vpad(const int64_t* rec) {
+  const uint32_t vl = (uint32_t)rec[2];
+  return vl == kSkipVlen ? 0u : (uint32_t)align16(vl);
+}
+
+// One workgroup. Per destination d (rank order): the rows that fit its slot (a prefix of
+// its block: row j fits while j < capR and its value ends within capB; value offsets grow
+// with j), their bytes, the slot header {rows, bytes} (others), and the segment bases of
+// the send buffer's segment list (per other rank: header, records, gap, one per row, tail).
+__global__ __launch_bounds__(256) void k_set_fit(const uint64_t* __restrict__ tcnt,
+                                                 const uint64_t* __restrict__ tbytes, int64_t G,
+                                                 const int64_t* __restrict__ cnt_s,
+                                                 const int64_t* __restrict__ srec,
+                                                 const uint64_t* __restrict__ svoff, int32_t W,
+                                                 int32_t me, int64_t capS, int64_t capSB,
+                                                 int64_t capSelf, int64_t capSelfB,
+                                                 uint64_t* __restrict__ meta) {
+  const SetMeta sm{W};
+  for (int d = threadIdx.x; d < W; d += blockDim.x) {
+    const uint64_t sst = tcnt[(int64_t)d * G], bst = tbytes[(int64_t)d * G];
+    const int64_t cnt = cnt_s[d];
+    const int64_t capR = d == me ? capSelf : capS;
+    const uint64_t capB = (uint64_t)(d == me ? capSelfB : capSB);
+    auto end_of = [&](int64_t j) {
+      return svoff[sst + j] - bst + rec_vpad(srec + 4 * (sst + j));
+    };
+    int64_t lo = 0, hi = min(cnt, capR);  // largest f in [lo, hi] whose row f-1 fits
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (end_of(mid - 1) <= capB) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t fb = lo ? end_of(lo - 1) : 0;
+    sm.fit(meta)[d] = (uint64_t)lo;
+    sm.fitb(meta)[d] = fb;
+    if (d != me) {
+      const int k = d < me ? d : d - 1;
+      sm.hdr(meta)[2 * k] = (uint64_t)lo;
+      sm.hdr(meta)[2 * k + 1] = fb;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t sb = 0, rows = 0;
+    for (int d = 0; d < W; ++d) {
+      rows += (uint64_t)cnt_s[d];
+      if (d == me) continue;
+      sm.segbase(meta)[d] = sb;
+      sb += 4 + (uint64_t)cnt_s[d];
+    }
+    sm.tail(meta)[0] = sb;                           // segments of the send buffer
+    sm.tail(meta)[1] = tcnt[(int64_t)me * G];        // first row of the self block
+    sm.tail(meta)[2] = rows;                         // routed rows (all destinations)
+  }
+}
+
+// The carry of one row that did not fit (its block's slot, or the self capacity): key,
+// metadata, destination + tier and a copy of its value bytes (the caller's batch may be
+// gone next step) into the carry buffers of this step's parity. ctr = {rows, bytes} of
+// this parity; tot = {rows, bytes, lost} since construction.
+struct CarryOut {
+  Digest* keys;
+  uint32_t* vlen;
+  uint32_t* flags;
+  uint32_t* expire;
+  uint64_t* val;
+  int32_t* dest;
+  uint8_t* bytes;
+  int64_t cap;
+  uint64_t bcap;
+  unsigned long long* ctr;
+  unsigned long long* tot;
+};
+__device__ void carry_row(const CarryOut& co, const int64_t* __restrict__ rec, uint64_t src,
+                          int d, int me) {
+  const uint32_t vl = (uint32_t)rec[2];
+  const uint64_t r3 = (uint64_t)rec[3];
+  const uint32_t vp = rec_vpad(rec);
+  const unsigned long long slot = atomicAdd(co.ctr, 1ull);
+  if (slot >= (unsigned long long)co.cap) {
+    atomicAdd(co.tot + 2, 1ull);
+    return;
+  }
+  const unsigned long long at = vp ? atomicAdd(co.ctr + 1, (unsigned long long)vp) : 0ull;
+  co.keys[slot] = Digest{(uint64_t)rec[0], (uint64_t)rec[1]};
+  co.flags[slot] = (uint32_t)((uint64_t)rec[2] >> 32);
+  co.expire[slot] = (uint32_t)r3;
+  if (at + vp > co.bcap) {  // no room for the value: a skip row (counted as lost)
+    co.vlen[slot] = kSkipVlen;
+    co.dest[slot] = me;
+    co.val[slot] = 0;
+    atomicAdd(co.tot + 2, 1ull);
+    return;
+  }
+  co.vlen[slot] = vl;
+  co.dest[slot] = d | (int)((r3 >> 63) << kTierBit);
+  co.val[slot] = (uint64_t)(uintptr_t)(co.bytes + at);
+  const u32x4v* s4 = reinterpret_cast<const u32x4v*>((uintptr_t)src);
+  u32x4v* d4 = reinterpret_cast<u32x4v*>(co.bytes + at);
+  for (uint32_t c = 0; c < vp / 16; ++c) d4[c] = s4[c];
+  atomicAdd(co.tot, 1ull);
+  atomicAdd(co.tot + 1, (unsigned long long)vp);
+}
+
+// The send buffer's segment list (slots in o-order = rank order without this rank; slot =
+// [header 16 B | capS records | capSB value bytes]), and the carry of every routed row that
+// does not fit. Threads: one per routed row, then one per destination (its fixed
+// segments), then one for the end offset.
+constexpr int kSegLds = 1024;
+__global__ __launch_bounds__(kB) void k_set_pack_segs(
+    const uint64_t* __restrict__ meta_c, const uint64_t* __restrict__ tcnt,
+    const uint64_t* __restrict__ tbytes, int64_t G, const int64_t* __restrict__ cnt_s,
+    const int64_t* __restrict__ srec, const uint64_t* __restrict__ sval,
+    const uint64_t* __restrict__ svoff, int32_t W, int32_t me, int64_t capS, int64_t slotS,
+    int64_t tmax, uint64_t* __restrict__ seg_off, uint64_t* __restrict__ seg_src,
+    CarryOut co) {
+  __shared__ uint64_t s_sst[kSegLds + 1];
+  uint64_t* meta = const_cast<uint64_t*>(meta_c);
+  const SetMeta sm{W};
+  const bool lds = W <= kSegLds;
+  if (lds) {
+    for (int d = threadIdx.x; d < W; d += kB) s_sst[d] = tcnt[(int64_t)d * G];
+    if (threadIdx.x == 0) s_sst[W] = sm.tail(meta)[2];
+    __syncthreads();
+  }
+  const int64_t total = (int64_t)sm.tail(meta)[2];
+  const uint64_t val0 = 16 + 32 * (uint64_t)capS;
+  for (int64_t t = (int64_t)blockIdx.x * kB + threadIdx.x; t < tmax; t += (int64_t)gridDim.x * kB) {
+    if (t < total) {
+      int lo = 0, hi = W;  // the block holding row t: last d with sst[d] <= t
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t v = lds ? s_sst[mid] : tcnt[(int64_t)mid * G];
+        if (v <= (uint64_t)t) lo = mid; else hi = mid;
+      }
+      const int d = lo;
+      const uint64_t sst = lds ? s_sst[d] : tcnt[(int64_t)d * G];
+      const int64_t j = t - (int64_t)sst;
+      const bool keep = (uint64_t)j < sm.fit(meta)[d];
+      if (d != me) {
+        const int k = d < me ? d : d - 1;
+        const uint64_t vo = svoff[t] - tbytes[(int64_t)d * G];
+        const int64_t q = (int64_t)sm.segbase(meta)[d] + 3 + j;
+        seg_off[q] = (uint64_t)k * slotS + val0 + min(vo, sm.fitb(meta)[d]);
+        seg_src[q] = keep ? sval[t] : 0ull;
+      }
+      if (!keep) carry_row(co, srec + 4 * t, sval[t], d, me);
+    } else if (t < total + W) {
+      const int d = (int)(t - total);
+      if (d == me) continue;
+      const int k = d < me ? d : d - 1;
+      const uint64_t base = (uint64_t)k * slotS, f = sm.fit(meta)[d];
+      const int64_t q = (int64_t)sm.segbase(meta)[d];
+      seg_off[q] = base;
+      seg_src[q] = (uint64_t)(uintptr_t)(sm.hdr(meta) + 2 * k);
+      seg_off[q + 1] = base + 16;
+      seg_src[q + 1] = (uint64_t)(uintptr_t)(srec + 4 * (int64_t)tcnt[(int64_t)d * G]);
+      seg_off[q + 2] = base + 16 + 32 * f;
+      seg_src[q + 2] = kSegSkip;
+      seg_off[q + 3 + cnt_s[d]] = base + val0 + sm.fitb(meta)[d];
+      seg_src[q + 3 + cnt_s[d]] = kSegSkip;
+    } else if (t == total + W) {
+      seg_off[sm.tail(meta)[0]] = (uint64_t)(W - 1) * slotS;
+    }
+  }
+}
+
+// Received SET rows in fixed positions: [source slots (o-order) x capS | capSelf own rows].
+// Row j of slot k is a SET when j < the slot header's row count; an own row when it is
+// within the self block's fit. Every other row is a skip row (kSkipVlen in both tiers).
+__global__ __launch_bounds__(kB) void k_rs_fill_fixed(
+    const uint8_t* __restrict__ Rs, int64_t slotS, int64_t capS, int32_t W,
+    const uint64_t* __restrict__ meta_c, int32_t me, const int64_t* __restrict__ srec,
+    const uint64_t* __restrict__ sval, int64_t nrows, Digest* __restrict__ keys,
+    uint32_t* __restrict__ vlen0, uint32_t* __restrict__ vlen1, uint32_t* __restrict__ flags,
+    uint32_t* __restrict__ expire, uint64_t* __restrict__ roff) {
+  uint64_t* meta = const_cast<uint64_t*>(meta_c);
+  const SetMeta sm{W};
+  const int64_t others = (int64_t)(W - 1) * capS;
+  for (int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * kB) {
+    const int64_t* rr = nullptr;
+    uint64_t vbase = 0, vabs = 0;
+    if (r < others) {
+      const int64_t k = r / capS, j = r - k * capS;
+      const uint8_t* slot = Rs + k * slotS;
+      if ((uint64_t)j < reinterpret_cast<const uint64_t*>(slot)[0]) {
+        rr = reinterpret_cast<const int64_t*>(slot + 16 + 32 * j);
+        vbase = (uint64_t)(uintptr_t)(slot + 16 + 32 * capS);
+      }
+    } else {
+      const int64_t j = r - others;
+      if ((uint64_t)j < sm.fit(meta)[me]) {
+        const int64_t t = (int64_t)sm.tail(meta)[1] + j;
+        rr = srec + 4 * t;
+        vabs = sval[t];
+      }
+    }
+    if (!rr) {
+      keys[r] = Digest{0, 0};
+      vlen0[r] = vlen1[r] = kSkipVlen;
+      flags[r] = expire[r] = 0;
+      roff[r] = 0;
+      continue;
+    }
+    keys[r] = Digest{(uint64_t)rr[0], (uint64_t)rr[1]};
+    const uint32_t vl = (uint32_t)rr[2];
+    const uint64_t hi32 = (uint64_t)rr[3] >> 32;
+    const uint32_t tier = (uint32_t)(hi32 >> 31);
+    vlen0[r] = tier == 0 ? vl : kSkipVlen;
+    vlen1[r] = tier == 1 ? vl : kSkipVlen;
+    flags[r] = (uint32_t)((uint64_t)rr[2] >> 32);
+    expire[r] = (uint32_t)rr[3];
+    roff[r] = rr == nullptr ? 0 : (vabs ? vabs : vbase + (hi32 & 0x7FFFFFFFull));
+  }
+}
+
 }  // namespace
 
 const StepStreams& step_streams(int device) {
@@ -794,6 +1086,8 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   (void)step_streams(device_);  // the process's first streams take the hardware queues
   const size_t K = (size_t)row_words();
   RT_OK(hipHostMalloc(&host_mat_, K * (size_t)world * sizeof(int64_t), hipHostMallocDefault));
+  RT_OK(hipHostMalloc(&host_ring_, kPend * K * (size_t)world * sizeof(int64_t),
+                      hipHostMallocDefault));
   RT_OK(hipHostMalloc(&host_dmat_, (size_t)world * (size_t)world * sizeof(int64_t),
                       hipHostMallocDefault));
   // two parities: a step's H2D copies of its tables may still be queued on the SET
@@ -803,29 +1097,87 @@ RoutedStep::RoutedStep(int world, int rank, int device)
   for (hipEvent_t* e : {&ev_fork_, &ev_pjoin_, &ev_pub_, &ev_sfork_, &ev_join_, &ev_asm_[0],
                         &ev_asm_[1], &ev_probe_, &ev_local_, &ev_rfork_, &ev_reply_[0],
                         &ev_reply_[1], &ev_pfork_, &ev_plan_, &ev_rep_, &ev_start_,
-                        &ev_gdone_[0], &ev_gdone_[1]})
+                        &ev_gdone_[0], &ev_gdone_[1], &ev_carry_[0], &ev_carry_[1], &ev_c1_,
+                        &ev_c2_, &ev_pack_, &ev_hot_, &ev_sdone_[0], &ev_sdone_[1]})
     RT_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t& e : ev_ring_) RT_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // carry counters ([parity][rows, bytes], totals [rows, bytes, lost]) and the SET slot
+  // metadata: zeroed once here (construction, not the serving path)
+  RT_OK(hipMalloc(&cctr_, 8 * sizeof(unsigned long long)));
+  RT_OK(hipMemset(cctr_, 0, 8 * sizeof(unsigned long long)));
+  for (uint64_t*& m : set_meta_) {
+    RT_OK(hipMalloc(&m, set_meta_words(world) * sizeof(uint64_t)));
+    RT_OK(hipMemset(m, 0, set_meta_words(world) * sizeof(uint64_t)));
+  }
+  RT_OK(hipDeviceSynchronize());
 }
 
 RoutedStep::~RoutedStep() {
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
+  reap(true);
   for (auto& b : bufs_) (void)hipFree(b.p);
   if (hot_tab_) (void)hipFree(hot_tab_);
+  for (int p = 0; p < 2; ++p)
+    for (void* q : {(void*)ck_[p], (void*)cvl_[p], (void*)cfl_[p], (void*)cex_[p],
+                    (void*)cval_[p], (void*)cdst_[p], (void*)cbytes_[p]})
+      if (q) (void)hipFree(q);
+  (void)hipFree(cctr_);
+  for (uint64_t* m : set_meta_) (void)hipFree(m);
   (void)hipHostFree(host_mat_);
+  (void)hipHostFree(host_ring_);
   (void)hipHostFree(host_dmat_);
   (void)hipHostFree(host_tab_);
   for (hipEvent_t e : {ev_fork_, ev_pjoin_, ev_pub_, ev_sfork_, ev_join_, ev_asm_[0], ev_asm_[1],
                        ev_probe_, ev_local_, ev_rfork_, ev_reply_[0], ev_reply_[1], ev_pfork_,
-                       ev_plan_, ev_rep_, ev_start_, ev_gdone_[0], ev_gdone_[1]})
+                       ev_plan_, ev_rep_, ev_start_, ev_gdone_[0], ev_gdone_[1], ev_carry_[0],
+                       ev_carry_[1], ev_c1_, ev_c2_, ev_pack_, ev_hot_, ev_sdone_[0], ev_sdone_[1]})
     (void)hipEventDestroy(e);
-
+  for (hipEvent_t e : ev_ring_) (void)hipEventDestroy(e);
 }
 
 void RoutedStep::set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts) {
   pts_ = pts;
   own_ = owner;
   npts_ = npts;
+}
+
+// ---- deferred frees -------------------------------------------------------------------
+void RoutedStep::note_stream(hipStream_t s) {
+  if (std::find(seen_streams_.begin(), seen_streams_.end(), s) == seen_streams_.end())
+    seen_streams_.push_back(s);
+}
+
+void RoutedStep::retire(void* p) {
+  if (!p) return;
+  const StepStreams& ss = step_streams(device_);
+  Dead d{p, {}};
+  std::vector<hipStream_t> all = seen_streams_;
+  for (hipStream_t x : {ss.plan, ss.set, ss.asm_})
+    if (std::find(all.begin(), all.end(), x) == all.end()) all.push_back(x);
+  for (hipStream_t x : all) {
+    hipEvent_t e;
+    RT_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    RT_OK(hipEventRecord(e, x));
+    d.ev.push_back(e);
+  }
+  dead_.push_back(std::move(d));
+}
+
+void RoutedStep::reap(bool all) {
+  for (size_t i = 0; i < dead_.size();) {
+    bool done = true;
+    for (hipEvent_t e : dead_[i].ev)
+      if (all) (void)hipEventSynchronize(e);
+      else if (hipEventQuery(e) != hipSuccess) done = false;
+    if (!done) {
+      ++i;
+      continue;
+    }
+    for (hipEvent_t e : dead_[i].ev) (void)hipEventDestroy(e);
+    (void)hipFree(dead_[i].p);
+    dead_.erase(dead_.begin() + (long)i);
+  }
 }
 
 void RoutedStep::set_hot(const Digest* hot, int64_t nhot, const int64_t* dir, bool changed) {
@@ -836,21 +1188,22 @@ void RoutedStep::set_hot(const Digest* hot, int64_t nhot, const int64_t* dir, bo
   // called every step: build once per hot set (`changed`: new contents, maybe at the
   // same address)
   if (!changed && hot == hot_built_ && nhot == nhot_built_) return;
-  // a new hot set (replica refresh, rare): rebuild the hash set; in-flight steps may
-  // still probe the old table, so drain the device first
+  // a new hot set (replica refresh): a new hash set, built on the plan stream (the next
+  // plan waits for it); the old one is freed once the steps queued before have passed
+  // (no device synchronisation: in-flight collectives on other ranks are never waited for)
   RT_OK(hipSetDevice(device_));
-  RT_OK(hipDeviceSynchronize());
   uint64_t slots = 1024;
   while (slots < 2 * (uint64_t)nhot) slots *= 2;
-  if (hot_tab_) RT_OK(hipFree(hot_tab_));
+  retire(hot_tab_);
   RT_OK(hipMalloc(&hot_tab_, slots * sizeof(Digest)));
-  RT_OK(hipMemset(hot_tab_, 0, slots * sizeof(Digest)));
+  hipStream_t bs = step_streams(device_).plan;
+  RT_OK(hipMemsetAsync(hot_tab_, 0, slots * sizeof(Digest), bs));
   hot_mask_ = slots - 1;
   const int g = (int)std::min<int64_t>((nhot + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_hot_hash_build, dim3(g), dim3(256), 0, nullptr, hot, nhot, hot_tab_,
-                     hot_mask_);
+  hipLaunchKernelGGL(k_hot_hash_build, dim3(g), dim3(256), 0, bs, hot, nhot, hot_tab_, hot_mask_);
   RT_OK(hipGetLastError());
-  RT_OK(hipDeviceSynchronize());
+  RT_OK(hipEventRecord(ev_hot_, bs));
+  hot_pending_ = true;
   hot_built_ = hot;
   nhot_built_ = nhot;
 }
@@ -860,11 +1213,8 @@ T* RoutedStep::buf(int slot, size_t count) {
   Buf& b = bufs_[slot];
   const size_t need = std::max<size_t>(count, 1) * sizeof(T);
   if (b.cap < need) {
-    // grow-only; the old block may still be read by queued work on this device
-    if (b.p) {
-      RT_OK(hipDeviceSynchronize());
-      RT_OK(hipFree(b.p));
-    }
+    // grow-only; the old block may still be read by queued work: freed once it has passed
+    retire(b.p);
     const size_t cap = (need + need / 4 + 255) & ~(size_t)255;
     RT_OK(hipMalloc(&b.p, cap));
     b.cap = cap;
@@ -877,6 +1227,8 @@ T* RoutedStep::buf(int slot, size_t count) {
 // slots, 5 % (+256 KiB) for the reply data — per-peer demand of a step varies by ~1 %
 // (Zipf batches of 1M rows), so an overflow needs a shift in the workload, which the
 // next steps absorb; the local region is per rank and costs no link bytes (10 % + 1 MiB).
+// The SET slots take the same slack (rows, value bytes); a SET that does not fit is
+// carried into the next step, never lost.
 namespace {
 constexpr size_t kHist = 16;
 void push_hist(std::vector<int64_t>* h, int64_t v) {
@@ -905,31 +1257,128 @@ std::vector<int64_t> RoutedStep::caps(int64_t n) const {
   return {g, d, l, 0, cal_l};
 }
 
+std::vector<int64_t> RoutedStep::set_caps() const {
+  if (ovr_s_[0] > 0)
+    return {align_up64(ovr_s_[0], 2), align_up64(ovr_s_[1], 16), align_up64(ovr_s_[2], 2),
+            align_up64(ovr_s_[3], 16)};
+  return {align_up64(hist_max(hist_s_) * 11 / 10 + 256, 64),
+          align_up64(hist_max(hist_sb_) * 21 / 20 + (256 << 10), 4096),
+          align_up64(hist_max(hist_self_) * 11 / 10 + 256, 64),
+          align_up64(hist_max(hist_selfb_) * 21 / 20 + (256 << 10), 4096)};
+}
+
 void RoutedStep::reset_caps() {
-  hist_g_.clear();
-  hist_d_.clear();
+  // pending matrices still count in the statistics, not in the new history
+  for (Pend& p : pend_) {
+    RT_OK(hipEventSynchronize(ev_ring_[p.slot]));
+    if (!p.stats_done)
+      add_stats(note_matrix(host_ring_ + (size_t)p.slot * row_words() * w_, p.n, p.capG, false));
+  }
+  pend_.clear();
+  for (auto* h : {&hist_g_, &hist_d_, &hist_s_, &hist_sb_, &hist_self_, &hist_selfb_}) h->clear();
   hist_lr_.clear();
   calibrating_ = true;
   capD_ = capL_ = 0;
 }
 
-void RoutedStep::note_matrix() {
-  const int W = w_;
+// History (hist) and this rank's statistics of one all-gathered matrix:
+// [n_local, n_dup, GET rows sent off-rank, rows over capG, reply rows dropped].
+std::vector<int64_t> RoutedStep::note_matrix(const int64_t* m, int64_t n, int64_t capG, bool hist) {
+  const int W = w_, me = rank_;
   const int64_t K = row_words();
-  int64_t mg = 0, md = 0;
-  for (int r = 0; r < W; ++r)
-    for (int p = 0; p < W; ++p) {
-      mg = std::max(mg, mat_[r * K + p]);
-      md = std::max(md, mat_[r * K + 3 * W + p]);
+  if (hist) {
+    int64_t mg = 0, md = 0, ms = 0, mb = 0, mself = 0, mselfb = 0;
+    for (int r = 0; r < W; ++r)
+      for (int p = 0; p < W; ++p) {
+        mg = std::max(mg, m[r * K + p]);
+        md = std::max(md, m[r * K + 3 * W + p]);
+        if (p == r) {
+          mself = std::max(mself, m[r * K + W + p]);
+          mselfb = std::max(mselfb, m[r * K + 2 * W + p]);
+        } else {
+          ms = std::max(ms, m[r * K + W + p]);
+          mb = std::max(mb, m[r * K + 2 * W + p]);
+        }
+      }
+    push_hist(&hist_g_, mg);
+    // the reply column is the previous step's demand (none before the first step)
+    if (!calibrating_) push_hist(&hist_d_, md);
+    push_hist(&hist_s_, ms);
+    push_hist(&hist_sb_, mb);
+    push_hist(&hist_self_, mself);
+    push_hist(&hist_selfb_, mselfb);
+    if (n > 0) {
+      hist_lr_.push_back((double)m[me * K + 4 * W + 1] / (double)n);
+      if (hist_lr_.size() > kHist) hist_lr_.erase(hist_lr_.begin());
     }
-  push_hist(&hist_g_, mg);
-  // the reply column is the previous step's demand (none before the first step)
-  if (!calibrating_) push_hist(&hist_d_, md);
-  if (n_ > 0) {
-    hist_lr_.push_back((double)mat_[rank_ * K + 4 * W + 1] / (double)n_);
-    if (hist_lr_.size() > kHist) hist_lr_.erase(hist_lr_.begin());
+    calibrating_ = false;
   }
-  calibrating_ = false;
+  int64_t over = 0, off_rank = 0;
+  for (int p = 0; p < W; ++p) {
+    over += std::max<int64_t>(0, m[me * K + p] - capG);
+    if (p != me) off_rank += m[me * K + p];
+  }
+  return {m[me * K + 4 * W], m[me * K + 4 * W + 2], off_rank, over, m[me * K + 4 * W + 3]};
+}
+
+void RoutedStep::add_stats(const std::vector<int64_t>& st) {
+  for (size_t i = 0; i < stat_acc_.size() && i < st.size(); ++i) stat_acc_[i] += st[i];
+}
+
+// Matrices published by step(), oldest first: statistics once, history (hist) for the
+// steps up to `upto`, in step order; an entry leaves once its history is in. The host
+// waits for a matrix only when its step is that old (two steps: long complete).
+void RoutedStep::harvest(int64_t upto, bool hist) {
+  for (Pend& p : pend_) {
+    if (p.step > upto) break;
+    if (p.stats_done && (!hist || p.hist_done)) continue;
+    RT_OK(hipEventSynchronize(ev_ring_[p.slot]));
+    const int64_t* m = host_ring_ + (size_t)p.slot * row_words() * w_;
+    const std::vector<int64_t> st = note_matrix(m, p.n, p.capG, hist && !p.hist_done);
+    if (!p.stats_done) add_stats(st);
+    p.stats_done = true;
+    if (hist) p.hist_done = true;
+  }
+  while (!pend_.empty() && pend_.front().hist_done) pend_.pop_front();
+}
+
+void RoutedStep::harvest_all() { harvest(INT64_MAX, false); }
+
+std::vector<int64_t> RoutedStep::take_stats() {
+  std::vector<int64_t> out = stat_acc_;
+  std::fill(stat_acc_.begin(), stat_acc_.end(), 0);
+  return out;
+}
+
+std::vector<int64_t> RoutedStep::carry_stats() {
+  unsigned long long h[3] = {0, 0, 0};
+  RT_OK(hipSetDevice(device_));
+  RT_OK(hipDeviceSynchronize());
+  RT_OK(hipMemcpy(h, cctr_ + 4, sizeof(h), hipMemcpyDeviceToHost));
+  return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2]};
+}
+
+void RoutedStep::ensure_carry(int64_t rows, uint64_t bytes) {
+  // parity P only (this step's pack writes it); the other parity holds what the previous
+  // step carried and this step's plan reads it
+  const int P = par_;
+  rows = std::max<int64_t>(rows, 1024);
+  bytes = std::max<uint64_t>(align_up64((int64_t)bytes, 16), 1 << 20);
+  if (ck_[P] && ccap_p_[P] >= rows && cbcap_p_[P] >= bytes) return;
+  for (void* q : {(void*)ck_[P], (void*)cvl_[P], (void*)cfl_[P], (void*)cex_[P], (void*)cval_[P],
+                  (void*)cdst_[P], (void*)cbytes_[P]})
+    retire(q);
+  const int64_t r = rows + rows / 4;
+  const uint64_t b = (bytes + bytes / 4 + 255) & ~(uint64_t)255;
+  RT_OK(hipMalloc(&ck_[P], r * sizeof(Digest)));
+  RT_OK(hipMalloc(&cvl_[P], r * sizeof(uint32_t)));
+  RT_OK(hipMalloc(&cfl_[P], r * sizeof(uint32_t)));
+  RT_OK(hipMalloc(&cex_[P], r * sizeof(uint32_t)));
+  RT_OK(hipMalloc(&cval_[P], r * sizeof(uint64_t)));
+  RT_OK(hipMalloc(&cdst_[P], r * sizeof(int32_t)));
+  RT_OK(hipMalloc(&cbytes_[P], b));
+  ccap_p_[P] = r;
+  cbcap_p_[P] = b;
 }
 
 // ---- plan ---------------------------------------------------------------------------
@@ -963,7 +1412,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
     RT_OK(hipStreamWaitEvent(s, ev_asm_[P], 0));
     asm_pending_[P] = false;
   }
-  // every buffer first (buf() may reallocate, which synchronises the device)
+  // every buffer first
   first_ = nullptr;
   uint32_t* co_tab = nullptr;
   int64_t co_slots = 0;
@@ -985,19 +1434,31 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   const int Gg = group_grid(ng);
   const int64_t plen_g = (ng + Gg - 1) / Gg;
   uint64_t* ws_g = buf<uint64_t>(kWsG, group_ws_words(ng, nb));
+  // the SET rows the previous step carried over (step() writes them; none otherwise):
+  // Gc workgroups of them ahead of the batch's Gs
+  const int Pc = P ^ 1;
+  const bool have_carry = carry_written_[Pc] && ck_[Pc] != nullptr;
+  const int64_t ccap = have_carry ? ccap_p_[Pc] : 0;
   const int64_t nsx = std::max<int64_t>(ns, 1);
   const int Gs = group_grid(nsx, 256);
   const int64_t plen_s = (nsx + Gs - 1) / Gs;
-  const int64_t mcap = fanout ? ns * W : ns;  // upper bound of routed SET rows
-  int32_t* owner_s = buf<int32_t>(kOwnerS, ns);
-  uint32_t* vpad = buf<uint32_t>(kVpad, ns);
-  uint64_t* tcnt = buf<uint64_t>(kTcnt, (size_t)nb * Gs);
-  uint64_t* tbytes = buf<uint64_t>(kTbytes, (size_t)nb * Gs);
+  // (a carry is rare and small: a few workgroups share it, whatever its capacity)
+  const int Gc = have_carry ? 16 : 0;
+  const int Gt = Gs + Gc;
+  // upper bound of routed SET rows (a carried row goes to its one destination)
+  const int64_t mcap = (fanout ? ns * W : ns) + ccap;
+  gt_ = Gt;
+  nrouted_max_ = mcap;
+  int32_t* owner_s = buf<int32_t>(kOwnerS, (size_t)(ccap + ns));
+  uint32_t* vpad = buf<uint32_t>(kVpad, (size_t)(ccap + ns));
+  // by parity: the previous step's fixed-slot pack (SET stream) may still read them
+  uint64_t* tcnt = buf<uint64_t>(P ? kTcnt1 : kTcnt, (size_t)nb * Gt);
+  uint64_t* tbytes = buf<uint64_t>(P ? kTbytes1 : kTbytes, (size_t)nb * Gt);
   // by parity: the previous step's SET packing (on the SET stream) may still read them
   srec_ = buf<int64_t>(P ? kSrec1 : kSrec, 4 * (size_t)mcap);
   sval_ = buf<uint64_t>(P ? kSval1 : kSval, mcap);
   svoff_ = buf<uint64_t>(P ? kSvoff1 : kSvoff, mcap);
-  cnt_s_ = buf<int64_t>(kCntS, nb);
+  cnt_s_ = buf<int64_t>(P ? kCntS1 : kCntS, nb);
   rb_ = buf<int64_t>(kRb, W + 1);
   if (hist_g_.empty() && calibrating_) RT_OK(hipMemsetAsync(rb_, 0, (W + 1) * sizeof(int64_t), s));
 
@@ -1019,17 +1480,25 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
     RT_OK(hipEventRecord(ev_fork_, s));
     RT_OK(hipStreamWaitEvent(ss, ev_fork_, 0));
   }
-  hipLaunchKernelGGL(k_ps_dest_hist, dim3(Gs), dim3(kB), nb * sizeof(unsigned long long), ss,
-                     skeys, svlen, ns, pts_, own_, npts_,
-                     fanout && nhot_ > 0 ? hot_tab_ : nullptr, hot_mask_, nb, plen_s, W, owner_s,
-                     vpad, tcnt, tbytes);
-  hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, ss, tcnt, tbytes, nb, Gs, cnt_s_,
+  if (hot_pending_) {  // a new hot hash set is being built on the plan stream
+    RT_OK(hipStreamWaitEvent(ss, ev_hot_, 0));
+    hot_pending_ = false;
+  }
+  // this step's carry counters (its pack adds to them); the step two back's plan has read them
+  RT_OK(hipMemsetAsync(cctr_ + 2 * P, 0, 2 * sizeof(unsigned long long), ss));
+  const SetRows sr{skeys, svlen, sflags, sexpire, sval_off, (uint64_t)(uintptr_t)svalues, ns,
+                   ck_[Pc], cvl_[Pc], cfl_[Pc], cex_[Pc], cval_[Pc], cdst_[Pc], cctr_ + 2 * Pc,
+                   ccap, Gc};
+  hipLaunchKernelGGL(k_ps_dest_hist, dim3(Gt), dim3(kB), nb * sizeof(unsigned long long), ss, sr,
+                     pts_, own_, npts_, fanout && nhot_ > 0 ? hot_tab_ : nullptr, hot_mask_, nb,
+                     plen_s, W, owner_s, vpad, tcnt, tbytes);
+  hipLaunchKernelGGL(k_ps_scan, dim3(1), dim3(1024), 0, ss, tcnt, tbytes, nb, Gt, cnt_s_,
                      row + W, row + 2 * W);
-  if (ns > 0)
-    hipLaunchKernelGGL(k_ps_scatter, dim3(Gs), dim3(kB), nb * sizeof(unsigned long long), ss,
-                       ns, nb, plen_s, tcnt, tbytes, skeys, svlen, sflags, sexpire, sval_off,
-                       (uint64_t)(uintptr_t)svalues, owner_s, vpad, W, srec_, sval_, svoff_);
+  if (ns > 0 || Gc > 0)
+    hipLaunchKernelGGL(k_ps_scatter, dim3(Gt), dim3(kB), nb * sizeof(unsigned long long), ss, sr,
+                       nb, plen_s, tcnt, tbytes, owner_s, vpad, W, srec_, sval_, svoff_);
   RT_OK(hipGetLastError());
+  carry_written_[Pc] = false;  // consumed (its value bytes stay put until this step's SETs)
   if (ss != s) RT_OK(hipEventRecord(ev_pjoin_, ss));
 
   // GET rows: coalesce duplicates (answered from their claimer), replica probe, owner
@@ -1151,15 +1620,13 @@ std::vector<int64_t> RoutedStep::set_splits() {
   SH_CHECK(published_, "RoutedStep: publish before set_splits");
   const int W = w_, me = rank_;
   const int64_t K = row_words();
+  // the matrices of earlier native steps first (history in step order)
+  harvest(INT64_MAX, true);
   RT_OK(hipEventSynchronize(ev_pub_));
   mat_.assign(host_mat_, host_mat_ + (size_t)W * K);
   // overflow: GET rows this rank could not send (its slots were full)
-  int64_t over = 0, off_rank = 0;
-  for (int p = 0; p < W; ++p) {
-    over += std::max<int64_t>(0, mat_[me * K + p] - capG_);
-    if (p != me) off_rank += mat_[me * K + p];
-  }
-  note_matrix();
+  const std::vector<int64_t> st = note_matrix(mat_.data(), n_, capG_, true);
+  const int64_t off_rank = st[2], over = st[3];
   sset_.assign(W, 0);
   rset_.assign(W, 0);
   ns_rows_ = ms_ = 0;
@@ -1306,10 +1773,94 @@ void RoutedStep::assemble(const uint8_t* data, uint64_t* out_size, uint64_t* out
   asm_pending_[P] = true;
 }
 
+// ---- fixed-slot SETs (step()) -------------------------------------------------------------
+// Send buffer S = [W-1 slots, o-order], slot = [16-B header {rows, bytes} | capS records |
+// capSB value bytes]: k_set_fit finds each destination's fitting prefix, k_set_pack_segs
+// writes the segment list (and carries every row past the prefix), segcopy_dev moves the
+// bytes; all on the SET stream, sized from the device (no host read).
+void RoutedStep::pack_fixed(uint8_t* S, int64_t slotS, const std::vector<int64_t>& sc,
+                            hipStream_t ps) {
+  const int W = w_, me = rank_, P = par_;
+  const uint64_t* tcnt = buf<uint64_t>(P ? kTcnt1 : kTcnt, 1);
+  const uint64_t* tbytes = buf<uint64_t>(P ? kTbytes1 : kTbytes, 1);
+  const int64_t nseg_max = 4 * (int64_t)W + nrouted_max_;
+  uint64_t* seg_off = buf<uint64_t>(kSegOffF, nseg_max + 1);
+  uint64_t* seg_src = buf<uint64_t>(kSegSrcF, nseg_max + 1);
+  uint64_t* meta = set_meta_[P];
+  hipLaunchKernelGGL(k_set_fit, dim3(1), dim3(256), 0, ps, tcnt, tbytes, gt_, cnt_s_, srec_,
+                     svoff_, W, me, sc[0], sc[1], sc[2], sc[3], meta);
+  const CarryOut co{ck_[P],  cvl_[P],     cfl_[P],      cex_[P],      cval_[P],    cdst_[P],
+                    cbytes_[P], ccap_p_[P], cbcap_p_[P], cctr_ + 2 * P, cctr_ + 4};
+  const int64_t tmax = nrouted_max_ + W + 1;
+  hipLaunchKernelGGL(k_set_pack_segs, dim3(grid1(tmax)), dim3(kB), 0, ps, meta, tcnt, tbytes,
+                     gt_, cnt_s_, srec_, sval_, svoff_, W, me, sc[0], slotS, tmax, seg_off,
+                     seg_src, co);
+  RT_OK(hipGetLastError());
+  if (W > 1) segcopy_dev(seg_src, seg_off, reinterpret_cast<const int64_t*>(meta + 5 * W), S, ps);
+  RT_OK(hipEventRecord(ev_pack_, ps));  // the SET exchange sends S
+  carry_written_[P] = true;  // the next plan (same stream) reads the carry
+}
+
+// Received SETs in fixed rows [others' slots x capS | capSelf own rows] -> the replica
+// (tier 1) and the main shard (tier 0), both on the SET stream.
+void RoutedStep::store_fixed(const uint8_t* Rs, int64_t slotS, const std::vector<int64_t>& sc,
+                             HbmCache* shard, HbmCache* replica, uint32_t now, hipStream_t sset,
+                             hipEvent_t index_after, bool allow_reclaim) {
+  const int W = w_;
+  const int64_t nrows = (int64_t)(W - 1) * sc[0] + sc[2];
+  if (nrows <= 0) return;
+  Digest* rkeys = buf<Digest>(kRkeys, nrows);
+  uint32_t* v0 = buf<uint32_t>(kV0, nrows);
+  uint32_t* v1 = buf<uint32_t>(kV1, nrows);
+  uint32_t* fl = buf<uint32_t>(kFl, nrows);
+  uint32_t* ex = buf<uint32_t>(kEx, nrows);
+  uint64_t* roff = buf<uint64_t>(kRoff, nrows);
+  hipLaunchKernelGGL(k_rs_fill_fixed, dim3(grid1(nrows)), dim3(kB), 0, sset, Rs, slotS, sc[0], W,
+                     set_meta_[par_], rank_, srec_, sval_, nrows, rkeys, v0, v1, fl, ex, roff);
+  RT_OK(hipGetLastError());
+  RT_OK(hipEventRecord(ev_sfork_, sset));
+  const uint64_t bound = 48 * (uint64_t)nrows + (uint64_t)(W - 1) * sc[1] + (uint64_t)sc[3];
+  if (replica) {
+    // the local gather already ran on this stream (it reads the replica log these rows
+    // may overwrite); the next step's plan (replica probe) waits for ev_rep_
+    replica->store(rkeys, nullptr, roff, v1, fl, ex, nrows, bound, now, sset);
+    RT_OK(hipEventRecord(ev_rep_, sset));
+    rep_pending_ = true;
+  }
+  shard->store(rkeys, nullptr, roff, v0, fl, ex, nrows, bound, now, sset, index_after,
+               allow_reclaim);
+  RT_OK(hipEventRecord(ev_join_, sset));
+  sets_pending_ = true;
+}
+
 // ---- the whole step, natively ----------------------------------------------------------
 void RoutedStep::set_comm(std::shared_ptr<StepComm> c) {
   SH_CHECK(!c || (c->world() == w_ && c->rank() == rank_), "RoutedStep: comm of another job");
   comm_ = std::move(c);
+}
+
+template <typename F>
+void RoutedStep::collective(hipStream_t home, hipStream_t comm_stream, int ch, F issue) {
+  if (!single_) {
+    issue(home, ch);
+    return;
+  }
+  // single: every collective on the comm stream and the control communicator, in issue
+  // order; events carry the data dependencies in and out
+  if (home != comm_stream) {
+    RT_OK(hipEventRecord(ev_c1_, home));
+    RT_OK(hipStreamWaitEvent(comm_stream, ev_c1_, 0));
+  }
+  issue(comm_stream, (int)StepComm::kCtrl);
+  if (home != comm_stream) {
+    RT_OK(hipEventRecord(ev_c2_, comm_stream));
+    RT_OK(hipStreamWaitEvent(home, ev_c2_, 0));
+  }
+}
+
+std::vector<int64_t> RoutedStep::prepare(int64_t n) {
+  harvest(step_id_ - 2, true);
+  return caps(n);
 }
 
 std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* replica,
@@ -1319,11 +1870,12 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
                                       bool fanout, bool coalesce, HbmCache* shard, uint8_t* data,
                                       uint64_t* out_size, uint64_t* out_off, hipStream_t s,
                                       hipStream_t sset, hipStream_t sasm,
-                                      hipEvent_t inputs_ready) {
+                                      hipEvent_t inputs_ready, int64_t svalues_bytes) {
   SH_CHECK(comm_, "RoutedStep::step: no communicator (set_comm)");
   const int W = w_, me = rank_;
   // the reply transfer and the assembly share one stream: the caller's `sasm` (torch owns
-  // it, so tensors recorded on it never outlive it), else the executor's own
+  // it, so tensors recorded on it never outlive it), else the executor's own; in single
+  // mode it carries every collective of the step
   hipStream_t cs = sasm;
   // The step's streams come from a per-device pool created once per process and never
   // destroyed (like torch's stream pool): tensors the caller recorded on them can never
@@ -1338,6 +1890,12 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
   }
   if (!sasm) cs = asm_stream_;
   if (!sset) sset = set_stream_;
+  note_stream(s);
+  note_stream(cs);
+  note_stream(sset);
+  reap(false);
+  // capacities of this step: the matrices of the steps up to two back (every rank the same)
+  harvest(step_id_ - 2, true);
   const int64_t K = row_words();
   {
     const std::vector<int64_t> c = caps(n);
@@ -1345,10 +1903,14 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
     // rank takes the same path: its replica hits that outgrow the old capL are misses)
     SH_CHECK(!c[3], "RoutedStep::step: a calibrating step takes the multi-call path");
   }
+  const std::vector<int64_t> sc = set_caps();
+  sv_bytes_ = svalues_bytes;
   // o(p): the position of peer p among the other ranks
   auto o = [me](int p) { return p < me ? p : p - 1; };
   int64_t* row = buf<int64_t>(kRowB, K);
   int64_t* mat = buf<int64_t>(kMatB, (size_t)K * W);
+  int64_t slotS = 0;
+  uint8_t* Sbuf = nullptr;
   if (!row_init_) {
     RT_OK(hipMemsetAsync(row, 0, K * sizeof(int64_t), s));
     row_init_ = true;
@@ -1381,23 +1943,46 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
       in_step_ = false;
       RT_OK(hipEventRecord(ev_plan_, ps));  // the SET stream starts from the plan's output
       if (ps != s) RT_OK(hipStreamWaitEvent(s, ev_plan_, 0));
+      // The SET send buffer, packed right behind the plan on its stream (beside this step's
+      // GET exchange), once the SET side of the step two back (same parity: its send
+      // buffer, slot metadata and carry bytes) is done. This step's carry holds twice
+      // the batch's routed rows and a bounded copy of the values (a row finding no room is
+      // counted as lost).
+      const int P = par_;
+      if (sdone_valid_[P]) RT_OK(hipStreamWaitEvent(ps, ev_sdone_[P], 0));
+      ensure_carry(2 * (fanout ? ns * W : ns),
+                   std::max<uint64_t>(2 * (uint64_t)std::max<int64_t>(svalues_bytes, 0), 64ull << 20));
+      slotS = 16 + 32 * sc[0] + sc[1];
+      Sbuf = buf<uint8_t>(P ? kS1 : kS0, (size_t)std::max<int64_t>((W - 1) * slotS, 16));
+      pack_fixed(Sbuf, slotS, sc, ps);
     }
     {
       TraceRange t("serve.row_allgather");
-      comm_->all_gather(mat, row, K, 4, s, StepComm::kCtrl);
-      publish(mat, s);
-    }
-    if (W > 1) {
-      TraceRange t("serve.request_a2a");
-      // G = [recv: W-1 slots | self | send: W-1 slots], others in o-order on both sides
-      std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, gslot);
-      for (int p = 0; p < W; ++p)
-        if (p != me) {
-          off_r[p] = o(p) * gslot;
-          off_s[p] = (int64_t)W * gslot + o(p) * gslot;
+      // the all-gather, the matrix into the pinned ring (read two steps later) and the
+      // request exchange, one collective hop in single mode
+      const int slot = ring_next_;
+      for (const Pend& q : pend_) SH_CHECK(q.slot != slot, "RoutedStep: matrix ring overrun");
+      ring_next_ = (ring_next_ + 1) % kPend;
+      collective(s, cs, StepComm::kCtrl, [&](hipStream_t st, int ch) {
+        comm_->all_gather(mat, row, K, 4, st, ch);
+        RT_OK(hipMemcpyAsync(host_ring_ + (size_t)slot * K * W, mat, (size_t)W * K * sizeof(int64_t),
+                             hipMemcpyDeviceToHost, st));
+        RT_OK(hipEventRecord(ev_ring_[slot], st));
+        if (W > 1) {
+          // G = [recv: W-1 slots | self | send: W-1 slots], others in o-order on both sides
+          std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, gslot);
+          for (int p = 0; p < W; ++p)
+            if (p != me) {
+              off_r[p] = o(p) * gslot;
+              off_s[p] = (int64_t)W * gslot + o(p) * gslot;
+            }
+          sz[me] = 0;
+          comm_->all_to_all(G, off_r, sz, G, off_s, sz, st, ch);
         }
-      sz[me] = 0;
-      comm_->all_to_all(G, off_r, sz, G, off_s, sz, s, StepComm::kCtrl);
+      });
+      pend_.push_back(Pend{step_id_, n, capG_, slot, false, false});
+      mat_dev_ = mat;  // owner_probe derives the owner slot counts from it
+      published_ = false;
     }
     TraceRange t("serve.owner");
     in_step_ = true;  // owner_probe reserves the look-ahead
@@ -1428,79 +2013,66 @@ std::vector<int64_t> RoutedStep::step(const Digest* keys, int64_t n, HbmCache* r
     RT_OK(hipEventRecord(ev_rfork_, s));
     RT_OK(hipEventRecord(ev_gdone_[P], s));  // this step's log reads are done
     gdone_valid_[P] = true;
+    RT_OK(hipStreamWaitEvent(cs, ev_rfork_, 0));
     if (W > 1) {
-      // the reply transfer on its own stream and channel: the SET exchange and the next
-      // step's planning run beside it
-      RT_OK(hipStreamWaitEvent(cs, ev_rfork_, 0));
-      std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, slotR);
-      for (int p = 0; p < W; ++p)
-        if (p != me) {
-          off_s[p] = o(p) * slotR;
-          off_r[p] = capL_ + o(p) * slotR;
-        }
-      sz[me] = 0;
-      comm_->all_to_all(data, off_r, sz, R, off_s, sz, cs, StepComm::kData);
+      // the reply transfer on the comm stream: the SET exchange and the next step's
+      // planning run beside it
+      collective(cs, cs, StepComm::kData, [&](hipStream_t st, int ch) {
+        std::vector<int64_t> off_r(W, 0), off_s(W, 0), sz(W, slotR);
+        for (int p = 0; p < W; ++p)
+          if (p != me) {
+            off_s[p] = o(p) * slotR;
+            off_r[p] = capL_ + o(p) * slotR;
+          }
+        sz[me] = 0;
+        comm_->all_to_all(data, off_r, sz, R, off_s, sz, st, ch);
+      });
       RT_OK(hipEventRecord(ev_reply_[P], cs));
       reply_pending_[P] = true;
     }
     pfork_valid_ = true;
   }
-  std::vector<int64_t> stats;
+  {
+    TraceRange t("serve.assemble");
+    // behind this step's reply transfer on the same stream (and the local gather)
+    RT_OK(hipStreamWaitEvent(cs, ev_local_, 0));
+    assemble(data, out_size, out_off, cs);
+  }
   {
     TraceRange t("serve.set_exchange");
-    const std::vector<int64_t> h = set_splits();  // host: waits for the published matrix
-    stats.assign(h.begin() + 2 * W, h.end());
-    int64_t so = 0, ro = 0;
-    for (int p = 0; p < W; ++p)
-      if (p != me) {
-        so += sset_[p];
-        ro += rset_[p];
-      }
-    uint8_t* S = buf<uint8_t>(P ? kS1 : kS0, (size_t)so + 16);
-    uint8_t* Rs = buf<uint8_t>(P ? kRs1 : kRs0, (size_t)ro + 16);
+    uint8_t* Rs = buf<uint8_t>(P ? kRs1 : kRs0, (size_t)std::max<int64_t>((W - 1) * slotS, 16));
     // Where the main-shard append may start. This step's probe reserved its bytes (the
     // reply gather never reads them); if the previous probe reserved them too
     // (look-ahead: this step's bytes within its margin), the append needs only the
     // previous step's reply gather done and runs beside this owner phase, with the index
-    // insert alone waiting for the probe. Otherwise everything waits for the probe.
-    int64_t pay = 0;
-    for (int q = 0; q < W; ++q)
-      pay += 48 * mat_[(int64_t)q * row_words() + W + me] + mat_[(int64_t)q * row_words() + 2 * W + me];
+    // insert alone waiting for the probe. Otherwise everything waits for the probe. The
+    // payload bound comes from the slot capacities (no host read of the matrix).
+    const int64_t nrows = (int64_t)(W - 1) * sc[0] + sc[2];
+    const int64_t pay = 48 * nrows + (int64_t)(W - 1) * sc[1] + sc[3];
     const bool early = gdone_valid_[P ^ 1] && ahead_prev_ >= (uint64_t)pay &&
                        !shard->would_reclaim((uint64_t)pay);
-    RT_OK(hipStreamWaitEvent(sset, early ? ev_gdone_[P ^ 1] : ev_probe_, 0));
     early_sets_ += early ? 1 : 0;
     push_hist(&pay_hist_, pay);
-    pack_sets(S, sset);
+    RT_OK(hipStreamWaitEvent(sset, ev_pack_, 0));
     if (W > 1) {
-      // Every rank takes part even with nothing to move: a collective-based comm (the
-      // gloo callbacks) needs all ranks; RCCL's grouped send/recv skips empty pairs.
-      // Send blocks at Ps[p] (pack_sets' table), receive blocks in rank order.
-      const uint64_t* Ps = host_tab_ + (size_t)P * (8 * (size_t)W + 8) + 2 * (size_t)W + 1;
-      std::vector<int64_t> off_s(W, 0), off_r(W, 0), sb(W, 0), rb(W, 0);
-      int64_t pos = 0;
-      for (int p = 0; p < W; ++p) {
-        if (p == me) continue;
-        off_s[p] = (int64_t)Ps[p];
-        sb[p] = sset_[p];
-        off_r[p] = pos;
-        rb[p] = rset_[p];
-        pos += rset_[p];
-      }
-      comm_->all_to_all(Rs, off_r, rb, S, off_s, sb, sset, StepComm::kSet);
+      // every rank sends every other rank one full slot (fixed size: no split sizes)
+      collective(sset, cs, StepComm::kSet, [&](hipStream_t st, int ch) {
+        std::vector<int64_t> off_s(W, 0), off_r(W, 0), sz(W, slotS);
+        for (int p = 0; p < W; ++p)
+          if (p != me) off_s[p] = off_r[p] = o(p) * slotS;
+        sz[me] = 0;
+        comm_->all_to_all(Rs, off_r, sz, Sbuf, off_s, sz, st, ch);
+      });
     }
-    store_sets(Rs, shard, replica, now, s, sset, /*replica_on_sset=*/true,
-               early ? ev_probe_ : nullptr, /*allow_reclaim=*/!early);
+    // the transfer needs only the packed slots; the stores wait for what the reserves need
+    RT_OK(hipStreamWaitEvent(sset, early ? ev_gdone_[P ^ 1] : ev_probe_, 0));
+    store_fixed(Rs, slotS, sc, shard, replica, now, sset, early ? ev_probe_ : nullptr,
+                /*allow_reclaim=*/!early);
+    RT_OK(hipEventRecord(ev_sdone_[P], sset));  // the SET side of this parity is done
+    sdone_valid_[P] = true;
   }
-  {
-    TraceRange t("serve.assemble");
-    // on the comm stream, behind this step's reply transfer (a stream of its own would be
-    // a fifth concurrent one)
-    RT_OK(hipStreamWaitEvent(cs, ev_local_, 0));
-    RT_OK(hipStreamWaitEvent(cs, ev_rfork_, 0));  // the own reply slot
-    assemble(data, out_size, out_off, cs);
-  }
-  return stats;
+  ++step_id_;
+  return take_stats();
 }
 
 void RoutedStep::join_sets(hipStream_t s) {

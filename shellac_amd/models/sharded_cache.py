@@ -157,9 +157,16 @@ def _event_handle(ev) -> int:
 class ShardedCache:
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
-                 sample_batches: int = 8, data_group=None, routed: Optional[bool] = None):
+                 sample_batches: int = 8, data_group=None, routed: Optional[bool] = None,
+                 comm_mode: str = "single"):
         self.shard = shard
         self.group = group
+        # native routed step: "single" = every collective of a step on one communicator and
+        # one stream in a fixed order (default: cannot deadlock); "channels" = one
+        # communicator per channel (control, reply, SET) on the stream producing its data
+        if comm_mode not in ("single", "channels"):
+            raise ValueError(f"comm_mode must be 'single' or 'channels', not {comm_mode!r}")
+        self.comm_mode = comm_mode
         # Optional second communicator for the value all-to-all: its stream runs the
         # previous step's value transfer while this step's small exchanges proceed.
         self.data_group = data_group if data_group is not None else group
@@ -224,11 +231,23 @@ class ShardedCache:
         # tier does (bench.py --edge host)
         self.host_edge = False
         self.gathered_bytes = 0  # response bytes the serving steps produced
-        self.stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
+        self._stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0,
                       "slot_overflow_rows": 0, "reply_dropped_rows": 0}
 
     # ------------------------------------------------------------------------------
+    @property
+    def stats(self) -> dict:
+        """Serving counters. The native routed step learns its own per-step numbers two
+        steps late (it never waits for a step's matrix); reading them here collects every
+        step issued so far (the host waits for the latest step's all-gather, not for the
+        step)."""
+        e = self._engine
+        if e is not None:
+            e.harvest_all()
+            self._add_step_stats(e.take_stats())
+        return self._stats
+
     def sync_sets(self) -> None:
         """Order the current stream after the SETs of the last routed ``serve`` (whose
         main-shard store may still be running on the executor's store stream). Every
@@ -238,6 +257,18 @@ class ShardedCache:
         if e is not None and e.sets_pending:
             e.join_sets(torch.cuda.current_stream(self.device).cuda_stream)
             self._held = None
+        if e is not None:
+            # the native step's statistics run two steps behind: collect the rest
+            e.harvest_all()
+            self._add_step_stats(e.take_stats())
+
+    def _add_step_stats(self, h) -> None:
+        n_local, n_dup, off_rank, over, dropped = h
+        self._stats["remote_gets"] += off_rank
+        self._stats["replica_hits"] += n_local - n_dup
+        self._stats["coalesced_gets"] += n_dup
+        self._stats["slot_overflow_rows"] += over
+        self._stats["reply_dropped_rows"] += dropped
 
     def _reset_exchange(self) -> None:
         """The traffic matrix changes (new ring, new hot set): the routed step's next
@@ -275,7 +306,7 @@ class ShardedCache:
     def get(self, keys: torch.Tensor, now: Optional[int] = None) -> GetResult:
         self.sync_sets()
         n = keys.shape[0]
-        self.stats["get_requests"] += n
+        self._stats["get_requests"] += n
         if not self.routed:
             if self.coalesce:
                 lk, first, _ = self.shard.lookup_coalesced(keys, now)
@@ -339,8 +370,8 @@ class ShardedCache:
             off = torch.where(local, rl.off[:n], roff)
         else:
             size, off = rsize, roff
-        self.stats["remote_gets"] += n_remote - int(send_rows[self.rank])
-        self.stats["replica_hits"] += n_local
+        self._stats["remote_gets"] += n_remote - int(send_rows[self.rank])
+        self._stats["replica_hits"] += n_local
         return GetResult(data, off, size)
 
     def serve(self, keys: torch.Tensor, batch: SetBatch, now: Optional[int] = None,
@@ -364,8 +395,8 @@ class ShardedCache:
                 return self._serve_routed_fused(keys, batch, now, inputs_ready)
             return self._serve_routed(keys, batch, now)
         n = keys.shape[0]
-        self.stats["get_requests"] += n
-        self.stats["set_requests"] += batch.keys.shape[0]
+        self._stats["get_requests"] += n
+        self._stats["set_requests"] += batch.keys.shape[0]
         sh = self.shard
         bound = sh.set_bound(batch.keys.shape[0], batch.values.numel())
         if not sh.is_gpu:
@@ -498,13 +529,14 @@ class ShardedCache:
         i64, u8 = torch.int64, torch.uint8
         n = keys.shape[0]
         ns_in = batch.keys.shape[0]
-        self.stats["get_requests"] += n
-        self.stats["set_requests"] += ns_in
+        self._stats["get_requests"] += n
+        self._stats["set_requests"] += ns_in
         self._sample(keys)
         now = self.shard.now() if now is None else now
         e = self._engine
         if e is None:
             e = self._engine = c.RoutedStep(w, me, dev.index)
+            e.single_comm = self.comm_mode == "single"
             k = e.row_words
             self._row = torch.zeros(k, dtype=i64, device=dev)
             self._mat = torch.zeros(w * k, dtype=i64, device=dev)
@@ -526,7 +558,7 @@ class ShardedCache:
         while len(self._inflight) >= 2:
             ev, _bufs = self._inflight.pop(0)
             cur.wait_event(ev)  # long complete: frees the buffers for reuse on this stream
-        cap_g, cap_d, cap_l, cal, cal_l = e.caps(n)
+        cap_g, cap_d, cap_l, cal, cal_l = e.prepare(n)
         if self._ncomm is None:
             self._ncomm = step_comm(self.group, dev) or False
             if self._ncomm is not False:
@@ -616,11 +648,8 @@ class ShardedCache:
         done = torch.cuda.Event()
         done.record(side)
         self._inflight.append((done, (R, data)))
-        self.stats["remote_gets"] += off_rank
-        self.stats["replica_hits"] += n_local - n_dup
-        self.stats["coalesced_gets"] += n_dup
-        self.stats["slot_overflow_rows"] += over
-        self.stats["reply_dropped_rows"] += dropped
+        self._add_step_stats((n_local, n_dup, off_rank, over, dropped))
+        self._add_step_stats(e.take_stats())  # earlier native steps' (lagged)
         ph.end()
         return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
 
@@ -644,7 +673,7 @@ class ShardedCache:
                    batch.val_off.data_ptr(), batch.values.data_ptr(), ns_in, fanout,
                    self.coalesce, self.shard._impl, data.data_ptr(), out[0].data_ptr(),
                    out[1].data_ptr(), cur.cuda_stream, 0, 0,
-                   _event_handle(inputs_ready))
+                   _event_handle(inputs_ready), batch.values.numel())
         # the reply transfer and the assembly (both on `side`) and the local gather (SET
         # stream, awaited by the assembly) write and read these
         data.record_stream(side)
@@ -655,12 +684,8 @@ class ShardedCache:
         # the main-shard SET chain (the executor's SET stream, a hardware queue of its own)
         # reads the batch until the next step's probe joins it
         self._held = (batch,) if e.sets_pending else None
-        n_local, n_dup, off_rank, over, dropped = h
-        self.stats["remote_gets"] += off_rank
-        self.stats["replica_hits"] += n_local - n_dup
-        self.stats["coalesced_gets"] += n_dup
-        self.stats["slot_overflow_rows"] += over
-        self.stats["reply_dropped_rows"] += dropped
+        # statistics of the steps two back (the host never waits for this step's matrix)
+        self._add_step_stats(h)
         return GetResult(data, out[1], out[0], _pending=_StreamDone(done))
 
     def _set_rows(self, batch: SetBatch):
@@ -707,8 +732,8 @@ class ShardedCache:
         """
         dev, w, me = self.device, self.world, self.rank
         n = keys.shape[0]
-        self.stats["get_requests"] += n
-        self.stats["set_requests"] += batch.keys.shape[0]
+        self._stats["get_requests"] += n
+        self._stats["set_requests"] += batch.keys.shape[0]
         self._sample(keys)
         i64 = torch.int64
         ph = _Phases("serve.")
@@ -863,15 +888,15 @@ class ShardedCache:
             off = torch.where(local, rl.off[:n], roff_g)
         else:
             size, off = rsize, roff_g
-        self.stats["remote_gets"] += n_remote - int(g_rows[me])
-        self.stats["replica_hits"] += n_local
+        self._stats["remote_gets"] += n_remote - int(g_rows[me])
+        self._stats["replica_hits"] += n_local
         ph.end()
         return GetResult(data, off, size)
 
     def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
         self.sync_sets()
         n = batch.keys.shape[0]
-        self.stats["set_requests"] += n
+        self._stats["set_requests"] += n
         if not self.routed:
             self.shard.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                              batch.expire, now)
@@ -1026,7 +1051,7 @@ class ShardedCache:
             self.replica.store(sb.keys[a:b], sb.values, sb.val_off[a:b], sb.vlen[a:b],
                                sb.flags[a:b], sb.expire[a:b], now,
                                bytes_bound=int(sizes[i]) + 48 * (b - a))
-        self.stats["replica_refreshes"] += 1
+        self._stats["replica_refreshes"] += 1
         return int((sb.vlen != SKIP_VLEN).sum())
 
     # ------------------------------------------------------------------------------

@@ -392,6 +392,47 @@ def test_routed_step_slot_overflow_is_a_counted_miss(cuda_dev):
         assert step(k) == expect  # learned capacities: exact again
 
 
+@pytest.mark.parametrize("comm_mode", ["single", "channels"])
+def test_routed_step_set_overflow_is_carried_not_lost(cuda_dev, comm_mode):
+    """Fixed-capacity SET slots: rows past a slot's capacity (records or value bytes, to a
+    peer or to this rank's own store) are carried into the next step, never dropped. With
+    forced tiny SET slots the carry is exercised, and once the capacities are learned again
+    every SET of the forced steps is stored within two steps (ground truth for each key)."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+    from shellac_amd.parallel.exchange import MirrorComm
+
+    wl = Workload(30000, cuda_dev)
+    sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(3),
+                      replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev), comm_mode=comm_mode)
+    sc.set(wl.set_batch(torch.arange(0, 30000, device=cuda_dev)))
+    gets = wl.digests.index_select(0, wl.sample_ids(4000, 3)).contiguous()
+    empty = wl.set_batch(torch.zeros(0, dtype=torch.int64, device=cuda_dev))
+    sc.serve(gets, empty).wait()  # calibrating step
+    sc.serve(gets, empty).wait()
+    e = sc._engine
+    e.set_set_cap_override(64, 96 << 10, 64, 96 << 10)
+    # new values for 1500 keys over two forced steps (different bytes from the fill: the
+    # workload's version 1)
+    ids = [torch.arange(1000 + 1500 * k, 1000 + 1500 * k + 750, device=cuda_dev) for k in (0, 1)]
+    for k in (0, 1):
+        b = wl.set_batch(ids[k], version=1)
+        sc.serve(gets, b).wait()
+    carried, cbytes, lost = e.carry_stats()
+    assert carried > 0 and cbytes > 0 and lost == 0
+    e.set_set_cap_override(0, 0, 0, 0)
+    for _ in range(2):
+        sc.serve(gets, empty).wait()
+    sc.sync_sets()
+    allids = torch.cat(ids)
+    r = sc.get(wl.digests.index_select(0, allids).contiguous())
+    got = [None if x is None else x[0] for x in unpack_records(r.data, r.off, r.size)]
+    want = [wl.expected_value(i, version=1) for i in allids.tolist()]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, (len(bad), bad[:5])
+    assert e.carry_stats()[2] == 0
+
+
 @pytest.mark.parametrize("n,nb", [(1, 2), (777, 3), (100003, 9), (300000, 65)])
 def test_group_rows_counting_sort(cuda_dev, n, nb):
     """csrc/router.hip counting sort: bucket counts, a permutation, rows moved with it,

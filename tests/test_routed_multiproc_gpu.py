@@ -101,6 +101,27 @@ def _routed_worker(rank, world, port, q, backend="bounce"):
                    enumerate(zip(got, want)) if g != w]
             assert not bad, f"rank {rank} step {4 + t}: {len(bad)} wrong GETs, first {bad[:6]}"
             cur.update(vals_t)
+        # forced SET overflow: tiny SET slots (the same on every rank) for one step, in which
+        # every rank updates 100 keys; the rows that do not fit are carried, and once the
+        # capacities are learned again every update is visible within two steps
+        e = sc._engine
+        e.set_set_cap_override(16, 8 << 10, 16, 8 << 10)
+        upd_f = keys[rank * 100: rank * 100 + 100]
+        vals_f = {k: b"vf-%d-" % rank + k for k in upd_f}
+        sc.serve(digest_strings(req, dev), batch(upd_f, [vals_f[k] for k in upd_f])).wait()
+        e.set_set_cap_override(0, 0, 0, 0)
+        for _ in range(2):
+            sc.serve(digest_strings(req, dev), batch([], [])).wait()
+        for r in range(world):
+            cur.update({k: b"vf-%d-" % r + k for k in keys[r * 100: r * 100 + 100]})
+        res = sc.serve(digest_strings(req, dev), batch([], []))
+        got = values(res)
+        want = [cur[k] for k in req[:-3]] + [None] * 3
+        bad = [(i, req[i], (g or b"")[:12], (w or b"")[:12]) for i, (g, w) in
+               enumerate(zip(got, want)) if g != w]
+        assert not bad, f"rank {rank} after forced SET overflow: {len(bad)} wrong, {bad[:6]}"
+        carried, _, lost = e.carry_stats()
+        assert carried > 0 and lost == 0, (carried, lost)
         st = sc.stats
         assert st["coalesced_gets"] > 0
         # world 1: every key is local (no remote GETs, the replica is never consulted)
