@@ -65,7 +65,9 @@ def parse():
                          "replicated hot set")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="profiling only: run rank 0 of an N-rank job on one GPU with mirrored "
-                         "all-to-alls (no interconnect); prints a *_simulated metric")
+                         "all-to-alls (no interconnect); every key is mapped onto one rank 0 "
+                         "owns, so its shard holds 1/N of the key space in one --log-gb log "
+                         "like a real rank; prints a *_simulated metric")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = functional rehearsal of the distributed path over gloo "
                          "(DRAM shards); never a performance number")
@@ -84,7 +86,7 @@ def parse():
                          "RCCL communicator (every collective call of the N-GPU step; all keys "
                          "are local, so no interconnect traffic) — a rehearsal, not a scaling "
                          "number")
-    ap.add_argument("--comm-mode", choices=["single", "channels"], default="single",
+    ap.add_argument("--comm-mode", choices=["single", "channels"], default="channels",
                     help="routed step: every collective on one communicator and one stream in "
                          "a fixed order (single), or one communicator per channel (channels)")
     ap.add_argument("--evict", choices=["clock", "fifo"], default="clock",
@@ -98,12 +100,16 @@ def parse():
     ap.add_argument("--no-uncoalesced", action="store_true",
                     help="skip the secondary uncoalesced-GET measurement")
     ap.add_argument("--no-wrapped", action="store_true",
-                    help="skip the secondary steady-state measurement (value log wrapped, so "
-                         "every SET batch runs the eviction hand)")
+                    help="skip the steady-state measurement (value log wrapped, so every SET "
+                         "batch runs the eviction hand); the headline is then the fresh cache")
     ap.add_argument("--pressured-gb", type=float, default=5.0,
                     help="secondary steady state under capacity pressure: a shard with this "
                          "many GiB of log (the 4M keys' ~4 GiB barely fit), wrapped, so the "
                          "CLOCK hand re-appends read objects every step (0 = skip)")
+    ap.add_argument("--headline", choices=["wrapped", "fresh"], default="wrapped",
+                    help="which cache state the headline K steps run in: the steady state of a "
+                         "full cache (value log wrapped, eviction in every SET batch; default) "
+                         "or the fresh cache before the first wrap (also reported as log_fresh)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -189,11 +195,11 @@ def check_memory_budget(args, world, sim, dev) -> None:
     payload pool and pre-generated batches, the routed step's exchange buffers (about
     three steps of responses in flight) and the 1 GiB all-reduce of the smoke check."""
     gib = 1 << 30
-    shard_keys = args.keys_per_gpu * (sim or 1)
+    shard_keys = args.keys_per_gpu
     nb = 1
     while nb < shard_keys:
         nb *= 2
-    need = args.log_gb * (sim or 1) * gib + nb * 128
+    need = args.log_gb * gib + nb * 128
     if world > 1 and args.replicate:
         rgb = args.replica_gb if args.replica_gb is not None else args.replicate * 2048 / gib
         need += rgb * gib + 2 * args.replicate * 128
@@ -206,12 +212,44 @@ def check_memory_budget(args, world, sim, dev) -> None:
         need += gib
     if args.pressured_gb > 0 and not sim:
         need += args.pressured_gb * gib + nb * 128
+    if sim:  # the probe digests of the key space and their sorted index
+        need += args.keys_per_gpu * sim * 48
     free, total = torch.cuda.mem_get_info(dev)
     if need > free:
         print(f"[bench] error: this configuration needs ~{need / gib:.1f} GiB of HBM per rank "
               f"but {free / gib:.1f} of {total / gib:.1f} GiB are free on {dev}; lower --log-gb "
               f"or --keys-per-gpu", file=sys.stderr, flush=True)
         raise SystemExit(2)
+
+
+def simulated_world_map(wl, sim: int, dev) -> dict:
+    """--simulate-world N: rank 0 of N ranks on one GPU, all-to-alls mirrored (what rank 0
+    sends to p comes back as what p sends to rank 0). Requests keep the whole key space
+    (popularity, routing by the real ring, coalescing, the replica tier), but every key i is
+    mapped onto a key f(i) that rank 0 owns — the j-th key (by id) rank p owns onto the j-th
+    key rank 0 owns — and owners probe and store f(i). Rank 0's shard then holds only its
+    1/N of the key space in one log, as a real rank's does, while receiving N-1 mirrored
+    request slots of the real shape. Returns {mine: ids rank 0 owns, f: id -> owner key id,
+    pdig: digests of f, probe_of: request digests -> probe digests}."""
+    from shellac_amd.ops import routing as R
+    from shellac_amd.parallel.ring import ShardRing
+
+    pts, own = ShardRing(list(range(sim)), 160).tensors(dev)
+    owners = R.route(wl.digests, pts, own, sim)[0].long()
+    ids = torch.arange(wl.total_keys, device=dev)
+    mine = ids[owners == 0].contiguous()
+    f = ids.clone()
+    for p in range(1, sim):
+        ip = ids[owners == p]
+        f[ip] = mine[torch.arange(ip.numel(), device=dev) % mine.numel()]
+    pdig = wl.digests.index_select(0, f).contiguous()
+    lo_sorted, order = torch.sort(wl.digests[:, 0].contiguous())
+
+    def probe_of(keys):
+        at = torch.searchsorted(lo_sorted, keys[:, 0].contiguous()).clamp_(max=lo_sorted.numel() - 1)
+        return pdig.index_select(0, order.index_select(0, at)).contiguous()
+
+    return {"mine": mine, "f": f, "pdig": pdig, "probe_of": probe_of}
 
 
 def _claim_stdout():
@@ -301,13 +339,12 @@ def main():
         check_memory_budget(args, world, sim, dev)
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
+    sim_map = simulated_world_map(wl, sim, dev) if sim else None
     nb = 1
-    shard_keys = total_keys if sim else args.keys_per_gpu
+    shard_keys = int(sim_map["mine"].numel()) if sim else args.keys_per_gpu
     while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
-    # the simulated rank's one shard stands in for all N owners: give it N logs' worth
-    # (8 x 16 GiB still fits one MI355X's 288 GB) so the key space does not wrap it
-    log_bytes = int(args.log_gb * (sim or 1) * (1 << 30)) // 16 * 16
+    log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
     shard = CacheShard(log_bytes, nb, max_item=1 << 20, device=dev, evict=args.evict)
     replica = None
     if world > 1 and args.replicate > 0:
@@ -323,14 +360,16 @@ def main():
     sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group,
                       routed=True if routed1 else None, comm_mode=args.comm_mode)
     sc.coalesce = not args.no_coalesce
+    if sim:
+        sc.probe_of = sim_map["probe_of"]
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
     lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
-    if sim:  # the mirrored owners all live in this one shard
-        lo, hi = 0, total_keys
-    for s in range(lo, hi, chunk):
-        ids = torch.arange(s, min(s + chunk, hi), device=dev)
+    fill_ids = sim_map["mine"] if sim else None  # the simulated rank fills what it owns
+    for s in range(0, shard_keys, chunk) if sim else range(lo, hi, chunk):
+        ids = (fill_ids[s: s + chunk] if sim else
+               torch.arange(s, min(s + chunk, hi), device=dev))
         sc.set(wl.set_batch(ids))
     sync()
     if real_world > 1:
@@ -345,6 +384,14 @@ def main():
             for i in range(P)]
     pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
     sets = [wl.set_batch(pick(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
+    gprobe = [None] * P
+    if sim:  # what the (mirrored) owners probe and store: keys the simulated rank owns
+        pd = sim_map["pdig"]
+        gprobe = [pd.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
+                  for i in range(P)]
+        for i in range(P):
+            sets[i].probe_keys = pd.index_select(
+                0, pick(args.sets, 5000 + 97 * rank + i)).contiguous()
     if replica is not None:
         # hot-object replica tier from an observed request stream (periodic in a server);
         # the observed batches are independent samples, not the timed ones
@@ -375,9 +422,12 @@ def main():
     if ready is not None:
         ready.record()
 
-    def step(i):
+    def serve_i(cache, i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
-        return sc.serve(gets[i % P], sets[i % P], inputs_ready=ready)
+        return cache.serve(gets[i % P], sets[i % P], inputs_ready=ready, probe_keys=gprobe[i % P])
+
+    def step(i):
+        return serve_i(sc, i)
 
     # Per-step GPU timing events are recorded in a separate pass after the timed one: an
     # event record is a marker packet on the stream, and one between every two steps cost
@@ -399,7 +449,7 @@ def main():
         for i in range(steps):
             if events:
                 evs[i].record(cur)
-            res = cache.serve(gets[(first + i) % P], sets[(first + i) % P], inputs_ready=ready)
+            res = serve_i(cache, first + i)
         if events:
             evs[steps].record(cur)
         sync()
@@ -413,53 +463,56 @@ def main():
         iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if events else []
         return float(t), iv, res
 
-    for i in range(args.warmup):
-        step(i)
-    sync()
-    before = shard.counters()
-    st0 = dict(sc.stats)
-    gb0 = sc.gathered_bytes
-    head0 = shard.head()
-    elapsed, _, res = timed(args.steps, args.warmup)
-    gathered = sc.gathered_bytes - gb0
-    last_batch = (args.warmup + args.steps - 1) % P
-    sc.sync_sets()
-    after = shard.counters()
-    head1 = shard.head()
-    diag = None
-    if sc._engine is not None:
-        # the routed step's SET exchange: early appends (look-ahead), carried rows
-        e = sc._engine
-        carried, cbytes, clost = e.carry_stats()
-        diag = {"early_set_steps": int(e.early_sets), "set_rows_carried": carried,
-                "set_bytes_carried": cbytes, "set_rows_lost": clost,
-                "set_slot_caps": [int(x) for x in e.set_caps()],
-                "log_head_gib": round(head1 / (1 << 30), 3),
-                "reinserted_steps": after["reinserted"] - before["reinserted"]}
-        if replica is not None:
-            diag["replica_head_gib"] = round(replica.head() / (1 << 30), 3)
-            diag["replica_log_gib"] = round(args.replica_gb, 3)
-    # owner-shard counters cover the GETs that left the replica tier; replica hits
-    # are counted by the serving step
-    rep_hits = sc.stats["replica_hits"] - st0["replica_hits"]
-    agg = torch.tensor([after["get_hits"] - before["get_hits"], after["get_ops"] - before["get_ops"],
-                        after["get_bytes"] - before["get_bytes"], rep_hits,
-                        sc.stats["get_requests"] - st0["get_requests"]], dtype=torch.int64,
-                       device=rdev)
-    if real_world > 1:
-        dist.all_reduce(agg)
-    hits, gops, gbytes, rep_hits, greq = (int(v) for v in agg.tolist())
+    def window(cache, shard_, first):
+        """The headline protocol on `cache`: K steps from batch `first`, bracketed by a
+        barrier and device syncs (timed), and the counters of exactly those steps."""
+        cache.sync_sets()
+        c0 = shard_.counters()
+        st0 = dict(cache.stats)
+        gb0 = cache.gathered_bytes
+        h0 = shard_.head()
+        el, _, res = timed(args.steps, first, cache=cache)
+        gathered = cache.gathered_bytes - gb0
+        cache.sync_sets()
+        c1 = shard_.counters()
+        st1 = cache.stats
+        # owner-shard counters cover the GETs that left the replica tier; replica hits
+        # are counted by the serving step
+        agg = torch.tensor([c1["get_hits"] - c0["get_hits"], c1["get_ops"] - c0["get_ops"],
+                            c1["get_bytes"] - c0["get_bytes"],
+                            st1["replica_hits"] - st0["replica_hits"],
+                            st1["get_requests"] - st0["get_requests"],
+                            c1["reinsert_bytes"] - c0["reinsert_bytes"]],
+                           dtype=torch.int64, device=rdev)
+        if real_world > 1:
+            dist.all_reduce(agg)
+        hits, gops, gbytes, rep, greq, rbytes = (int(v) for v in agg.tolist())
+        return {"el": el, "res": res, "last": (first + args.steps - 1) % P, "hits": hits,
+                "gops": gops, "gbytes": gbytes, "rep": rep, "greq": greq, "rbytes": rbytes,
+                "head0": h0, "head1": shard_.head(), "gathered": gathered, "c0": c0, "c1": c1}
 
-    if args.check:
-        # verify the last GET batch against the workload's ground truth
+    def check(w):
+        """Verify the window's last GET batch against the workload's ground truth (before
+        any later step can reuse its response buffer)."""
         from shellac_amd.ops.cache import unpack_records
 
+        res, last_batch = w["res"], w["last"]
         k = 200
         ids = wl.sample_ids(args.batch, 1000 + 97 * rank + last_batch)[:k]
         res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
-        bad = sum(1 for i, r in zip(ids.tolist(), recs) if r is not None and r[0] != wl.expected_value(i))
-        log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
+        if sim:
+            # the owner holds key f(i) for request i: several requests alias one owner key
+            # (and a SET of any of them updates it), so values are informational here
+            fmap = sim_map["f"]
+            bad = sum(1 for i, r in zip(ids.tolist(), recs)
+                      if r is not None and r[0] != wl.expected_value(int(fmap[i])))
+            log(rank, f"[bench] check (simulated world, aliased values): {bad} of {k} sampled "
+                      f"GETs differ from the owner key's first value")
+        else:
+            bad = sum(1 for i, r in zip(ids.tolist(), recs)
+                      if r is not None and r[0] != wl.expected_value(i))
+            log(rank, f"[bench] check: {bad} mismatches in {k} sampled GETs")
         # every hit of the whole last batch: its record's header names the requested digest
         words = res.data[: res.data.numel() // 8 * 8].view(torch.int64)
         wd = words.device  # pinned host memory under --edge host
@@ -467,16 +520,74 @@ def main():
         hit = (res.size > 0).to(wd)
         at = torch.where(hit, torch.div(res.off.to(wd), 8, rounding_mode="floor"),
                          torch.zeros_like(res.off, device=wd))
-        wrong = hit & ((words.index_select(0, at) != keys_last[:, 0]) |
-                       (words.index_select(0, at + 1) != keys_last[:, 1]))
+        w0, w1 = words.index_select(0, at), words.index_select(0, at + 1)
+        wrong = hit & ((w0 != keys_last[:, 0]) | (w1 != keys_last[:, 1]))
+        if sim:  # an owner's record names the probe digest (a replica's the request's)
+            pk = gprobe[last_batch].to(wd)
+            wrong &= (w0 != pk[:, 0]) | (w1 != pk[:, 1])
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
                   f"another key")
 
-    # secondary (outside the headline timed region): the same steps again with a GPU timing
-    # event between every two (per-step GPU time, median over the batches)
-    intervals = []
-    if use_events:
-        intervals = timed(args.steps, args.warmup + args.steps, events=True)[1]
+    def median(iv):
+        return round(sorted(iv)[len(iv) // 2], 4) if iv else None
+
+    def summary(w, iv=None, log_bytes_=log_bytes, fill=None):
+        out_ = {"ms_per_step": round(w["el"] / args.steps * 1e3, 4),
+                "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps / w["el"], 1),
+                "log_gib_per_shard": round(log_bytes_ / (1 << 30), 2),
+                "log_head_laps": round(w["head1"] / log_bytes_, 3),
+                "owner_hit_ratio": round(w["hits"] / max(w["gops"], 1), 4),
+                "reinserted_bytes_per_step_per_rank": round(w["rbytes"] / world / args.steps)}
+        if fill is not None:
+            out_["fill_steps"] = fill
+        if iv:
+            out_["ms_per_step_median_gpu_events"] = median(iv)
+        return out_
+
+    # The log fills at ~66 MB per step and rank; a serving cache is full, and then every
+    # SET batch runs the eviction hand (CLOCK second chances) first. Steps run until every
+    # rank's log has wrapped by a quarter lap (untimed).
+    def fill_to_wrap(cache, shard_, log_bytes_, base, per_step):
+        need = torch.tensor([max(0.0, (1.25 * log_bytes_ - shard_.head()) / per_step)],
+                            dtype=torch.float64, device=rdev)
+        if real_world > 1:
+            dist.all_reduce(need, op=dist.ReduceOp.MAX)
+        nfill = int(float(need)) + 2
+        if nfill > 20000:
+            return None
+        for i in range(nfill):
+            serve_i(cache, base + i)
+        sync()
+        return nfill
+
+    steady_ok = not host_edge and dev.type == "cuda" and not args.no_wrapped
+    headline_wrapped = steady_ok and args.headline == "wrapped"
+    for i in range(args.warmup):
+        step(i)
+    sync()
+    # the log not yet wrapped (the first K steps after the warmup)
+    fresh = window(sc, shard, args.warmup)
+    if args.check and not headline_wrapped:
+        check(fresh)
+    diag = None
+    if sc._engine is not None:
+        # the routed step's SET exchange: early appends (look-ahead), carried rows
+        e = sc._engine
+        carried, cbytes, clost = e.carry_stats()
+        cg = e.prepare(args.batch)
+        scp = [int(x) for x in e.set_caps()]
+        # bytes per step on each link (one per peer, each direction): request slot, reply
+        # slot (headers + data), SET slot: fixed sizes, whatever the step carries
+        per_peer = 16 * cg[0] + 8 * cg[0] + cg[1] + 16 + 32 * scp[0] + scp[1]
+        diag = {"early_set_steps": int(e.early_sets), "set_rows_carried": carried,
+                "set_bytes_carried": cbytes, "set_rows_lost": clost, "set_slot_caps": scp,
+                "get_slot_caps": [int(cg[0]), int(cg[1])],
+                "link_bytes_per_peer_per_step": int(per_peer) if world > 1 else 0,
+                "link_ms_per_step_at_55GBps": round(per_peer / 55e9 * 1e3, 3) if world > 1 else 0}
+        if replica is not None:
+            diag["replica_head_gib"] = round(replica.head() / (1 << 30), 3)
+            diag["replica_log_gib"] = round(args.replica_gb, 3)
+    fresh_iv = timed(args.steps, args.warmup + args.steps, events=True)[1] if use_events else []
     # secondary: the same steps with every GET probed and copied (no in-batch request
     # collapsing)
     unco = None
@@ -486,48 +597,24 @@ def main():
         unco_el, _, _ = timed(args.steps, args.warmup)
         sc.coalesce = True
         unco = (args.batch + args.sets) * world * args.steps / unco_el
+    per_step = max((fresh["head1"] - fresh["head0"]) / max(args.steps, 1), 1.0)
 
-    # secondary: steady state of a full cache. The headline steps run before the value log
-    # has wrapped (16 GiB per shard, ~66 MB appended per step); a serving cache is full, and
-    # then every SET batch runs the eviction hand (CLOCK second chances) first. Steps run
-    # until every rank's log has wrapped by a quarter lap, then the same K steps are timed.
-    def steady_state(sc_, shard_, log_bytes_, base):
-        per_step = max((head1 - head0) / max(args.steps, 1), 1.0)
-        need = torch.tensor([max(0.0, (1.25 * log_bytes_ - shard_.head()) / per_step)],
-                            dtype=torch.float64, device=rdev)
-        if real_world > 1:
-            dist.all_reduce(need, op=dist.ReduceOp.MAX)
-        nfill = int(float(need)) + 2
-        if nfill > 20000:
-            return None
-        for i in range(nfill):
-            sc_.serve(gets[(base + i) % P], sets[(base + i) % P], inputs_ready=ready)
-        sync()
-        sc_.sync_sets()
-        w0 = shard_.counters()
-        el_w, iv_w, _ = timed(args.steps, base + nfill, events=use_events, cache=sc_)
-        sc_.sync_sets()
-        w1 = shard_.counters()
-        wagg = torch.tensor([w1["get_hits"] - w0["get_hits"], w1["get_ops"] - w0["get_ops"],
-                             w1["reinsert_bytes"] - w0["reinsert_bytes"]],
-                            dtype=torch.int64, device=rdev)
-        if real_world > 1:
-            dist.all_reduce(wagg)
-        wh, wo, wr = (int(v) for v in wagg.tolist())
-        res = {"ms_per_step": round(el_w / args.steps * 1e3, 4),
-               "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps / el_w, 1),
-               "log_gib_per_shard": round(log_bytes_ / (1 << 30), 2),
-               "fill_steps": nfill,
-               "owner_hit_ratio": round(wh / max(wo, 1), 4),
-               "reinserted_bytes_per_step_per_rank": round(wr / world / args.steps)}
-        if iv_w:
-            res["ms_per_step_median_gpu_events"] = round(sorted(iv_w)[len(iv_w) // 2], 4)
-        return res
-
-    steady_ok = not host_edge and dev.type == "cuda"
-    wrapped = None
-    if not args.no_wrapped and steady_ok:
-        wrapped = steady_state(sc, shard, log_bytes, args.warmup + 2 * args.steps)
+    # the headline: steady state of the full cache (value log wrapped)
+    wrapped = wrapped_iv = nfill = None
+    if steady_ok:
+        base = args.warmup + 3 * args.steps
+        nfill = fill_to_wrap(sc, shard, log_bytes, base, per_step)
+        if nfill is not None:
+            wrapped = window(sc, shard, base + nfill)
+            if args.check and headline_wrapped:
+                check(wrapped)
+            if use_events:
+                wrapped_iv = timed(args.steps, base + nfill + args.steps, events=True)[1]
+    if headline_wrapped and wrapped is None:
+        raise SystemExit("[bench] the value log could not be wrapped for the headline; "
+                         "pass --headline fresh")
+    hw = wrapped if headline_wrapped else fresh
+    hw_iv = wrapped_iv if headline_wrapped else fresh_iv
     # secondary: the same under capacity pressure — a shard whose log barely holds the key
     # space, so objects the steps read are re-appended (reinsertions > 0) every step
     pressured = None
@@ -545,7 +632,13 @@ def main():
         sync()
         if real_world > 1:
             dist.barrier()
-        pressured = steady_state(p_sc, p_shard, p_log, 3 * args.warmup + 2 * args.steps)
+        pbase = 3 * args.warmup + 2 * args.steps
+        pfill = fill_to_wrap(p_sc, p_shard, p_log, pbase, per_step)
+        if pfill is not None:
+            pw = window(p_sc, p_shard, pbase + pfill)
+            piv = timed(args.steps, pbase + pfill + args.steps, events=True,
+                        cache=p_sc)[1] if use_events else []
+            pressured = summary(pw, piv, p_log, pfill)
         p_sc.sync_sets()
         del p_sc, p_shard
 
@@ -555,9 +648,15 @@ def main():
         # BASELINE.json's headline: wall clock of the platform smoke checks
         sm["smoke_wallclock_s"] = round(time.perf_counter() - t_sm, 3)
 
+    elapsed, gathered = hw["el"], hw["gathered"]
+    hits, gops, gbytes, rep_hits, greq = hw["hits"], hw["gops"], hw["gbytes"], hw["rep"], hw["greq"]
     ops_per_step = (args.batch + args.sets) * world
     ms = elapsed / args.steps * 1e3
     value = ops_per_step * args.steps / elapsed
+    if world == 1 and not routed1:
+        parallelism = "shard1 (one GPU, no routing)"
+    else:
+        parallelism = f"shard{world} (all-to-all routed, {args.comm_mode} communicator mode)"
     out = {
         "metric": "cache_ops_per_s",
         "value": round(value, 1),
@@ -576,7 +675,7 @@ def main():
                      "+ 2-choice index",
             "global_batch": ops_per_step,
             "seq_len": None,
-            "parallelism": f"shard{world} (all-to-all routed)",
+            "parallelism": parallelism,
             "get_per_rank": args.batch,
             "set_per_rank": args.sets,
             "keys_total": total_keys,
@@ -586,6 +685,12 @@ def main():
             "set_dist": args.set_dist,
             "replicated_hot_objects": args.replicate if world > 1 else 0,
         },
+        # which cache state the headline steps ran in: "log_wrapped" = the steady state of a
+        # full cache (every SET batch runs the CLOCK hand), "log_fresh" = before the first wrap
+        "headline_phase": "log_wrapped" if headline_wrapped else "log_fresh",
+        "warmup_detail": (f"{args.warmup} warmup steps, {args.steps} pre-wrap steps (log_fresh), "
+                          f"{2 * args.steps} more, {nfill} fill steps to wrap the log; then the "
+                          f"{args.steps} timed steps") if headline_wrapped else None,
         "get_coalescing": sc.coalesce,
         # owner-shard probes (+ replica hits) per GET request: < 1 when duplicate
         # requests of a batch share one probe and one response record
@@ -601,12 +706,13 @@ def main():
         "batches_cycled": P,
         # CLOCK second chances per step (objects re-appended ahead of the log overwrite):
         # 0 until the value log has wrapped
-        "reinserted_bytes_per_step": round((after["reinsert_bytes"] - before["reinsert_bytes"])
-                                           / args.steps),
+        "reinserted_bytes_per_step": round(hw["rbytes"] / args.steps),
         "edge": args.edge,
         "routed_diag": diag,
-        # the same step with the value log wrapped (eviction in every SET batch)
-        "log_wrapped": wrapped,
+        # the step before the value log first wraps (no eviction work)
+        "log_fresh": summary(fresh, fresh_iv),
+        # the step with the value log wrapped (eviction in every SET batch)
+        "log_wrapped": summary(wrapped, wrapped_iv, fill=nfill) if wrapped else None,
         # the same under capacity pressure (a log the key space barely fits: reinsertions)
         "log_pressured": pressured,
         "smoke": sm,
@@ -620,9 +726,8 @@ def main():
         out["host_read_GBps"] = round(
             (args.batch * 16 + args.sets * (16 + 8 + 12) + int(wl.vlen.float().mean()) * args.sets)
             * args.steps / elapsed / 1e9, 2)
-    if intervals:
-        srt = sorted(intervals)
-        out["ms_per_step_median_gpu_events"] = round(srt[len(srt) // 2], 4)
+    if hw_iv:
+        out["ms_per_step_median_gpu_events"] = median(hw_iv)
     if dev.type != "cuda":
         out["data"] = "cpu rehearsal over gloo: functional only, not a performance number"
     if bounce:
@@ -636,7 +741,8 @@ def main():
     if sim:
         out["metric"] = "cache_ops_per_s_simulated"
         out["data"] = (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
-                       "locally (no interconnect); profiling only, not a scaling result")
+                       "locally (no interconnect), keys mapped onto the simulated rank's 1/N "
+                       "of the key space; profiling only, not a scaling result")
         out["n_gpus"] = 1
         out["simulated_world"] = sim
     if rank == 0:

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 3 HTTP matrix (8M x 4 KiB incompressible, Zipf 0.99, c=10 and c=1000): DRAM-only,
+# HTTP matrix (8M x 4 KiB incompressible, Zipf 0.99, c=10 and c=1000): DRAM-only,
 # HBM-only and tiered, the GPU batcher on a core of its own (8 reactors x 6 load-generator
 # workers), HBM-only also without the resident edge server (a launch per GET batch).
 set -o pipefail
-OUT=gpurun_out/${1:-r3_http}
+OUT=gpurun_out/${1:-http_matrix}
 mkdir -p "$OUT"
 run() { # name args...
   local name=$1; shift

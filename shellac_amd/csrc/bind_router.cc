@@ -111,6 +111,9 @@ void bind_router(py::module_& m) {
       .def("set_ring", [](RoutedStep& r, uintptr_t pts, uintptr_t owner, int32_t npts) {
         r.set_ring(P<const uint32_t>(pts), P<const int32_t>(owner), npts);
       })
+      .def("set_probe_keys", [](RoutedStep& r, uintptr_t pkeys, uintptr_t spkeys) {
+        r.set_probe_keys(P<const Digest>(pkeys), P<const Digest>(spkeys));
+      })
       .def("set_hot", [](RoutedStep& r, uintptr_t hot, int64_t nhot, uintptr_t dir, bool changed) {
         py::gil_scoped_release nogil;
         r.set_hot(P<const Digest>(hot), nhot, P<const int64_t>(dir), changed);

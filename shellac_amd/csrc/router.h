@@ -113,6 +113,13 @@ class RoutedStep {
   RoutedStep& operator=(const RoutedStep&) = delete;
 
   void set_ring(const uint32_t* pts, const int32_t* owner, int32_t npts);
+  // Simulated world (bench.py --simulate-world): the digests the owner probes / stores for
+  // the next plan's GET rows and SET rows (routing, replica probes and replica copies keep
+  // the request digests). Null: the request digests themselves.
+  void set_probe_keys(const Digest* pkeys, const Digest* spkeys) {
+    pkeys_ = pkeys;
+    spkeys_ = spkeys;
+  }
   // Hot set (sorted by signed lo; the directory is kept for the framework-op path). The
   // SET planner probes a hash set built from it on the first call and whenever
   // `changed` (or the pointer / size) says the set is new.
@@ -258,6 +265,8 @@ class RoutedStep {
   const uint32_t* pts_ = nullptr;
   const int32_t* own_ = nullptr;
   int32_t npts_ = 0;
+  const Digest* pkeys_ = nullptr;
+  const Digest* spkeys_ = nullptr;
   const Digest* hot_ = nullptr;
   int64_t nhot_ = 0;
   const int64_t* hot_dir_ = nullptr;

@@ -270,6 +270,7 @@ struct SetRows {
   const uint64_t* val_off;
   uint64_t values_base;
   int64_t n;
+  const Digest* pkeys;  // owner copies' digests (simulated world), else null
   const Digest* ckeys;
   const uint32_t* cvlen;
   const uint32_t* cflags;
@@ -454,8 +455,9 @@ __global__ __launch_bounds__(kB) void k_ps_scatter(
       const uint64_t voff = vglob - tbytes[(int64_t)d * G];  // within the peer's value block
       const uint64_t tier = fan ? (d != o ? 1ull : 0ull) : (uint64_t)((ow >> kTierBit) & 1);
       int64_t* rec = srec + pos * 4;
-      rec[0] = (int64_t)k.lo;
-      rec[1] = (int64_t)k.hi;
+      const Digest kk = (!carry && tier == 0 && sr.pkeys) ? sr.pkeys[j] : k;
+      rec[0] = (int64_t)kk.lo;
+      rec[1] = (int64_t)kk.hi;
       rec[2] = (int64_t)r2;
       rec[3] = (int64_t)(ex | ((voff | (tier << 31)) << 32));
       sval[pos] = src;
@@ -594,6 +596,8 @@ __global__ __launch_bounds__(kB) void k_gr_scatter_slots(
     const int32_t* __restrict__ dest, int64_t n, int32_t nb, int64_t plen,
     const uint64_t* __restrict__ table, const Digest* __restrict__ keys, int64_t capG,
     int32_t me, uint8_t* __restrict__ G, int64_t* __restrict__ route) {
+  // (keys: what the owner probes — the request digests, or their probe digests in a
+  // simulated world, RoutedStep::set_probe_keys)
   extern __shared__ uint32_t s_cur[];
   const int W = nb - 1;
   for (int d = threadIdx.x; d < nb; d += kB) s_cur[d] = 0;
@@ -1487,7 +1491,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
   // this step's carry counters (its pack adds to them); the step two back's plan has read them
   RT_OK(hipMemsetAsync(cctr_ + 2 * P, 0, 2 * sizeof(unsigned long long), ss));
   const SetRows sr{skeys, svlen, sflags, sexpire, sval_off, (uint64_t)(uintptr_t)svalues, ns,
-                   ck_[Pc], cvl_[Pc], cfl_[Pc], cex_[Pc], cval_[Pc], cdst_[Pc], cctr_ + 2 * Pc,
+                   spkeys_, ck_[Pc], cvl_[Pc], cfl_[Pc], cex_[Pc], cval_[Pc], cdst_[Pc], cctr_ + 2 * Pc,
                    ccap, Gc};
   hipLaunchKernelGGL(k_ps_dest_hist, dim3(Gt), dim3(kB), nb * sizeof(unsigned long long), ss, sr,
                      pts_, own_, npts_, fanout && nhot_ > 0 ? hot_tab_ : nullptr, hot_mask_, nb,
@@ -1518,7 +1522,7 @@ void RoutedStep::plan(const Digest* keys, int64_t n, HbmCache* replica, uint32_t
                      row, replica ? rl_off_ + n : nullptr, extras, 1);
   if (n > 0)
     hipLaunchKernelGGL(k_gr_scatter_slots, dim3(Gg), dim3(kB), nb * sizeof(uint32_t), s, dest_g, n,
-                       nb, plen_g, ws_g, keys, capG_, rank_, G, route_);
+                       nb, plen_g, ws_g, pkeys_ ? pkeys_ : keys, capG_, rank_, G, route_);
   RT_OK(hipGetLastError());
   if (ss != s) RT_OK(hipStreamWaitEvent(s, ev_pjoin_, 0));  // join: the row is complete
 }

@@ -80,6 +80,8 @@ class SetBatch:
     vlen: torch.Tensor      # int32 [n]
     flags: Optional[torch.Tensor] = None   # int32 [n]
     expire: Optional[torch.Tensor] = None  # int32 [n]
+    # simulated world only (bench.py --simulate-world): the digests the owner stores
+    probe_keys: Optional[torch.Tensor] = None  # int64 [n, 2]
 
 
 class _StreamDone:
@@ -158,7 +160,7 @@ class ShardedCache:
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
                  sample_batches: int = 8, data_group=None, routed: Optional[bool] = None,
-                 comm_mode: str = "single"):
+                 comm_mode: str = "channels"):
         self.shard = shard
         self.group = group
         # native routed step: "single" = every collective of a step on one communicator and
@@ -203,6 +205,8 @@ class ShardedCache:
         # the transfer runs)
         self._inflight = []
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
+        # simulated world: request digests -> the digests their owners hold (see serve)
+        self.probe_of = None
         # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
         self.overlap_store = True
         # GET coalescing: the duplicate keys of a batch share one probe and one record
@@ -303,7 +307,10 @@ class ShardedCache:
         cand = h.index_select(0, idx)
         return (cand == keys).all(dim=1)
 
-    def get(self, keys: torch.Tensor, now: Optional[int] = None) -> GetResult:
+    def get(self, keys: torch.Tensor, now: Optional[int] = None,
+            probe_keys: Optional[torch.Tensor] = None) -> GetResult:
+        """GET a batch (collective when routed). ``probe_keys`` (simulated world only): the
+        digests the owners probe for each request."""
         self.sync_sets()
         n = keys.shape[0]
         self._stats["get_requests"] += n
@@ -325,7 +332,7 @@ class ShardedCache:
             dest = torch.where(local, torch.full_like(dest, w), dest)
         counts = torch.bincount(dest.long(), minlength=w + 1)
         perm = R.scatter_positions(dest, counts)         # local hits sort to the tail
-        send_keys = R.permute(keys, perm)
+        send_keys = R.permute(keys if probe_keys is None else probe_keys, perm)
         recv_counts = exchange_counts(counts[:w].contiguous(), self.group)
         local_total = rl.off[n:n + 1] if rl is not None else torch.zeros(1, dtype=torch.int64,
                                                                            device=self.device)
@@ -375,7 +382,7 @@ class ShardedCache:
         return GetResult(data, off, size)
 
     def serve(self, keys: torch.Tensor, batch: SetBatch, now: Optional[int] = None,
-              inputs_ready=None) -> GetResult:
+              inputs_ready=None, probe_keys: Optional[torch.Tensor] = None) -> GetResult:
         """One serving step: a GET batch and a SET batch, GETs ordered before SETs.
 
         ``inputs_ready`` (optional ``torch.cuda.Event``, routed GPU step): an event after
@@ -384,6 +391,10 @@ class ShardedCache:
         everything the caller queued on the current stream before this call.
 
         With one rank the GET's extent read (the only host sync) is hidden behind
+        ``probe_keys`` / ``batch.probe_keys`` (simulated world, routed GPU step only): the
+        digests owners probe and store (bench.py --simulate-world maps every key onto one
+        the simulated rank owns, so its shard holds 1/N of the key space like a real one).
+
         the SET kernels: the lookup reserves the SET's log bytes (objects the SET may
         overwrite count as misses) and its kernel writes the total into a pinned host
         slot; the SET is queued, and only then does the host spin on that slot to size
@@ -392,7 +403,7 @@ class ShardedCache:
         the whole step instead of 10 and 3 for get() followed by set()."""
         if self.routed:
             if self.fused and self.device.type == "cuda":
-                return self._serve_routed_fused(keys, batch, now, inputs_ready)
+                return self._serve_routed_fused(keys, batch, now, inputs_ready, probe_keys)
             return self._serve_routed(keys, batch, now)
         n = keys.shape[0]
         self._stats["get_requests"] += n
@@ -511,7 +522,8 @@ class ShardedCache:
         return self._side
 
     def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
-                            now: Optional[int] = None, inputs_ready=None) -> GetResult:
+                            now: Optional[int] = None, inputs_ready=None,
+                            probe_keys: Optional[torch.Tensor] = None) -> GetResult:
         """``_serve_routed`` run by the native executor (csrc/router.hip, RoutedStep), with
         no host synchronisation between planning and the result (after one calibrating
         step): GET requests and replies travel in fixed-capacity per-peer slots whose
@@ -547,6 +559,8 @@ class ShardedCache:
             self._sset = torch.cuda.ExternalStream(ss[1], device=dev)
             self._asm = torch.cuda.ExternalStream(ss[2], device=dev)
         e.set_ring(self.ring_pts.data_ptr(), self.ring_own.data_ptr(), self.ring_pts.numel())
+        e.set_probe_keys(probe_keys.data_ptr() if probe_keys is not None else 0,
+                         batch.probe_keys.data_ptr() if batch.probe_keys is not None else 0)
         fanout = self.replica is not None and self._hot is not None
         changed = False
         if fanout and self._hot_dir is None:
@@ -983,13 +997,10 @@ class ShardedCache:
         return back.index_select(0, perm).bool()
 
     # ------------------------------------------------------------------------------
-    def refresh_replica(self, top_k: int, keys: Optional[torch.Tensor] = None,
-                        now: Optional[int] = None) -> int:
-        """Collective. Replace the replica tier with the global top-k keys by request
-        frequency (from ``keys`` or the recent GET samples). Returns #objects cached."""
-        self.sync_sets()
-        if self.replica is None:
-            return 0
+    def _hot_candidates(self, top_k: int, keys: Optional[torch.Tensor]) -> torch.Tensor:
+        """Collective: the global top-k digests by request count (from ``keys`` or the
+        recent GET samples), the same on every rank, most requested first (ties in digest
+        order: a stable sort of the all-gathered counts, identical everywhere)."""
         dev, w = self.device, self.world
         if keys is None:
             keys = torch.cat(self._samples) if self._samples else torch.zeros((0, 2), dtype=torch.int64,
@@ -1016,31 +1027,36 @@ class ShardedCache:
         valid = tot > 0
         tot = torch.where(valid, tot, torch.full_like(tot, -1))
         kk = min(top_k, u.shape[0])
-        hot = u.index_select(0, torch.topk(tot, kk).indices)
-        hot = hot[(hot != 0).any(dim=1)].contiguous()      # drop padding rows (identical everywhere)
-        if hot.shape[0] == 0:
-            self.replica.flush()
-            self._hot = None
-            self._reset_exchange()
-            return 0
-        order = torch.argsort(hot[:, 0])
-        self._hot = hot.index_select(0, order).contiguous()
-        self._hot_dir = None
-        self._reset_exchange()
+        order = torch.sort(-tot, stable=True).indices[:kk]
+        hot = u.index_select(0, order)
+        return hot[(hot != 0).any(dim=1)].contiguous()     # drop padding rows (identical everywhere)
+
+    @staticmethod
+    def _member(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+        """Rows of ``a`` that are rows of ``b`` (both [n, 2] digests; b sorted by lo)."""
+        if a.shape[0] == 0 or b.shape[0] == 0:
+            return torch.zeros(a.shape[0], dtype=torch.bool, device=a.device)
+        at = torch.searchsorted(b[:, 0].contiguous(), a[:, 0].contiguous())
+        at = torch.clamp(at, max=b.shape[0] - 1)
+        return (b.index_select(0, at) == a).all(dim=1)
+
+    def _fetch_into_replica(self, keys: torch.Tensor, now: Optional[int]) -> tuple:
+        """Collective. GET ``keys`` through their owners (never the replica) and store the
+        records in this rank's replica (keys this rank owns stay out: an owner serves its
+        own keys from its main shard). Returns (objects stored, record bytes fetched)."""
+        if keys.shape[0] == 0:
+            return 0, 0
         saved = self.replica
         self.replica = None                               # fetch through the owners only
         try:
-            res = self.get(hot, now)
+            res = self.get(keys, now, probe_keys=self.probe_of(keys) if self.probe_of else None)
         finally:
             self.replica = saved
-        self.replica.flush()
-        sb = records_to_set_batch(hot, res)
-        # an owner serves its own keys from its main shard (write-through updates only
-        # non-owner replicas), so owned keys stay out of the local replica
-        owner, _ = self._route(hot)
+        sb = records_to_set_batch(keys, res)
+        owner, _ = self._route(keys)
         sb.vlen = torch.where(owner == self.rank, torch.full_like(sb.vlen, SKIP_VLEN), sb.vlen)
         # store in chunks with exact byte bounds (the records buffer can be GBs)
-        k = hot.shape[0]
+        k = keys.shape[0]
         chunk = 1 << 17
         cuts = list(range(0, k, chunk)) + [k]
         # records of a chunk are scattered in the response buffer: bound by their sizes
@@ -1051,39 +1067,140 @@ class ShardedCache:
             self.replica.store(sb.keys[a:b], sb.values, sb.val_off[a:b], sb.vlen[a:b],
                                sb.flags[a:b], sb.expire[a:b], now,
                                bytes_bound=int(sizes[i]) + 48 * (b - a))
+        return int((sb.vlen != SKIP_VLEN).sum()), int(sum(sizes))
+
+    def refresh_replica(self, top_k: int, keys: Optional[torch.Tensor] = None,
+                        now: Optional[int] = None, budget_bytes: Optional[int] = None,
+                        chunk_keys: int = 1 << 16) -> int:
+        """Collective. Move the replica tier towards the global top-k keys by request
+        frequency (from ``keys`` or the recent GET samples), incrementally: keys that left
+        the top-k are deleted from the replica and stop being written through; keys that
+        entered it are fetched from their owners, most popular first, until
+        ``budget_bytes`` of records have moved (None: all of them) — the rest stay
+        un-replicated (served by their owners) and are candidates again at the next
+        refresh (fetched ``chunk_keys`` at a time: the budget's granularity). Nothing is
+        flushed: the replica keeps serving the keys that stay hot. The hot set changes
+        identically on every rank. Returns #objects this call stored."""
+        self.sync_sets()
+        if self.replica is None:
+            return 0
+        dev = self.device
+        ranked = self._hot_candidates(top_k, keys)          # most requested first
+        target = ranked.index_select(0, torch.argsort(ranked[:, 0])).contiguous()
+        old = self._hot if self._hot is not None else torch.zeros((0, 2), dtype=torch.int64,
+                                                                    device=dev)
+        if target.shape[0] == 0 and old.shape[0] == 0:
+            return 0
+        stay = self._member(old, target)
+        dropped = old[~stay].contiguous()
+        kept = old[stay]
+        # newly hot keys, most requested first, fetched in chunks under the byte budget
+        added = ranked[~self._member(ranked, old)]
+        stored = fetched = 0
+        took = []
+        chunk = max(1, int(chunk_keys))
+        for a in range(0, added.shape[0], chunk):
+            if budget_bytes is not None and fetched >= budget_bytes:
+                break
+            part = added[a: a + chunk].contiguous()
+            n_st, nb = self._fetch_into_replica(part, now)
+            stored += n_st
+            fetched += nb
+            took.append(part)
+        if dropped.shape[0]:
+            self.replica.remove(dropped, now)             # no longer written through
+        new = torch.cat([kept] + took) if (took or kept.shape[0]) else kept
+        if new.shape[0] == 0:
+            self._hot = None
+        else:
+            self._hot = new.index_select(0, torch.argsort(new[:, 0])).contiguous()
+        self._hot_dir = None
+        changed = dropped.shape[0] + sum(t.shape[0] for t in took)
+        # a large change of the hot set changes the traffic matrix: measure it afresh (the
+        # fixed-capacity exchange otherwise adapts within a few steps)
+        if changed * 4 > max(old.shape[0], 1):
+            self._reset_exchange()
         self._stats["replica_refreshes"] += 1
-        return int((sb.vlen != SKIP_VLEN).sum())
+        self._stats["replica_added"] = self._stats.get("replica_added", 0) + sum(
+            t.shape[0] for t in took)
+        self._stats["replica_dropped"] = self._stats.get("replica_dropped", 0) + int(dropped.shape[0])
+        self._stats["replica_fetched_bytes"] = self._stats.get("replica_fetched_bytes", 0) + fetched
+        return stored
 
     # ------------------------------------------------------------------------------
     # membership changes: rebalancing, failure, warm recovery, snapshots
     # ------------------------------------------------------------------------------
-    def set_ring(self, ring: ShardRing, migrate: bool = True, now: Optional[int] = None) -> int:
+    def set_ring(self, ring: ShardRing, migrate: bool = True, now: Optional[int] = None,
+                 chunk_keys: int = 1 << 18, incremental: bool = False) -> int:
         """Collective. Switch every rank to ``ring``. With ``migrate`` each rank ships
         the live objects it holds that the new ring assigns elsewhere to their new
         owners through the routed SET path (warm rebalancing: no refetch from the
-        origin). Returns the number of objects this rank migrated."""
+        origin), ``chunk_keys`` objects at a time (bounded memory). ``incremental``: only
+        switch the ring and queue the migration; ``migrate_step`` then moves it a byte
+        budget at a time between serving steps (meanwhile a moved key's GET misses at its
+        new owner until its object arrives — a cache miss, never a wrong answer). Returns
+        the number of objects this rank has to migrate."""
         self.sync_sets()
-        moved = 0
-        batch = None
         mkeys = None
         if migrate and self.world > 1:
             keys = self.shard.export_keys(now)
             pts, own = ring.tensors(self.device)
             dest, _ = R.route(keys, pts, own, self.world)
-            sel = dest != self.rank
-            mkeys = keys[sel].contiguous()
-            moved = int(mkeys.shape[0])
-            lk = self.shard.lookup(mkeys, now)
-            data = self.shard.gather(lk)
-            batch = records_to_set_batch(mkeys, GetResult(data, lk.off[:moved], lk.size[:moved]))
+            mkeys = keys[dest != self.rank].contiguous()
         self.ring = ring
         self.ring_pts, self.ring_own = ring.tensors(self.device)
         self._reset_exchange()
-        if batch is not None:
-            self.set(batch, now)                  # lands on the new owners
-            if moved:
-                self.shard.remove(mkeys, now)     # this rank no longer owns them
+        self._migrating = mkeys if mkeys is not None else None
+        self._migrate_chunk = chunk_keys
+        moved = int(mkeys.shape[0]) if mkeys is not None else 0
+        if migrate and self.world > 1 and not incremental:
+            while self.migrate_step(None, now):
+                pass
         return moved
+
+    def migrate_step(self, budget_bytes: Optional[int] = None, now: Optional[int] = None) -> bool:
+        """Collective. Move queued migration objects (``set_ring``) to their new owners:
+        chunks of ``chunk_keys`` until ``budget_bytes`` of records have moved on this rank
+        (None: one chunk). Returns whether any rank has objects left (the same on every
+        rank)."""
+        self.sync_sets()
+        moved_bytes = 0
+        while True:
+            q = getattr(self, "_migrating", None)
+            left = torch.tensor([0 if q is None else int(q.shape[0])], dtype=torch.int64,
+                                device=self.device)
+            all_reduce(left, op=dist.ReduceOp.MAX, group=self.group)
+            if int(left) == 0:
+                self._migrating = None
+                return False
+            part = (q[: self._migrate_chunk] if q is not None
+                    else torch.zeros((0, 2), dtype=torch.int64, device=self.device)).contiguous()
+            batch = None
+            if part.shape[0]:
+                lk = self.shard.lookup(part, now)
+                data = self.shard.gather(lk)
+                n = part.shape[0]
+                batch = records_to_set_batch(part, GetResult(data, lk.off[:n], lk.size[:n]))
+                moved_bytes += int(lk.off[n])
+            else:
+                empty = torch.zeros(0, dtype=torch.int64, device=self.device)
+                batch = SetBatch(part, torch.zeros(16, dtype=torch.uint8, device=self.device),
+                                 empty, empty.to(torch.int32))
+            self.set(batch, now)                  # lands on the new owners (collective)
+            if part.shape[0]:
+                self.shard.remove(part, now)      # this rank no longer owns them
+                self._migrating = q[part.shape[0]:] if q.shape[0] > part.shape[0] else None
+            # stop once any rank has used its budget (the decision is collective)
+            q = getattr(self, "_migrating", None)
+            st = torch.tensor([0 if q is None else int(q.shape[0]),
+                               int(budget_bytes is None or moved_bytes >= budget_bytes)],
+                              dtype=torch.int64, device=self.device)
+            all_reduce(st, op=dist.ReduceOp.MAX, group=self.group)
+            if int(st[0]) == 0:
+                self._migrating = None
+                return False
+            if int(st[1]):
+                return True
 
     def fail_shard(self, rank: int) -> None:
         """Collective. Simulate (or react to) the loss of ``rank``'s shard: every rank

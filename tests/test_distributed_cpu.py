@@ -286,3 +286,117 @@ def _serve_worker(rank, world, port, q):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_fused_serve_step_gloo(world):
     _run_world(_serve_worker, world)
+
+
+def _drift_worker(rank, world, port, q):
+    """Incremental replica maintenance: the hot set drifts; a refresh drops the keys that
+    cooled (deleted from the replica, no longer written through: an update of one at its
+    owner is never shadowed by a stale copy) and fetches newly hot ones under a byte budget
+    (the rest follow at the next refresh), without flushing the replica."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+
+        sc = ShardedCache(CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu"),
+                          replica=CacheShard(1 << 21, 1 << 10, 1 << 14, "cpu"))
+        keys = [f"/d{i}".encode() for i in range(600)]
+
+        def put(ks, tag, who=0):
+            mine = ks if rank == who else []
+            v, vo, vl = pack_values([tag + k for k in mine])
+            sc.set(SetBatch(digest_strings(mine), v, vo, vl))
+
+        def read(ks):
+            res = sc.get(digest_strings(ks))
+            return [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+
+        put(keys, b"a-" + b"x" * 200)
+        a = keys[:40]
+        b = keys[30:70]       # 10 stay hot, 30 cool down, 30 heat up
+        sc.refresh_replica(40, keys=digest_strings(a * 5))
+        assert sc._hot.shape[0] == 40
+        r0 = sc.stats["replica_refreshes"]
+        # the drift: b is hot now; a budget of ~10 records per call on every rank
+        budget = 10 * 260
+        sc.refresh_replica(40, keys=digest_strings(b * 5), budget_bytes=budget, chunk_keys=8)
+        hot = {tuple(x) for x in sc._hot.tolist()}
+        want_b = {tuple(x) for x in digest_strings(b).tolist()}
+        gone = {tuple(x) for x in digest_strings(keys[:30]).tolist()}
+        assert not (hot & gone), "cooled keys stay out of the hot set"
+        assert 10 < len(hot & want_b) < 40, len(hot & want_b)   # the budget held some back
+        # a cooled key updated at its owner: nobody may see the stale replica copy
+        put(keys[:5], b"c-", who=world - 1)
+        assert read(keys[:5]) == [b"c-" + k for k in keys[:5]]
+        # the next refreshes bring the rest of b in
+        sc.refresh_replica(40, keys=digest_strings(b * 5), budget_bytes=budget, chunk_keys=8)
+        sc.refresh_replica(40, keys=digest_strings(b * 5))
+        hot = {tuple(x) for x in sc._hot.tolist()}
+        assert hot == want_b
+        assert sc.stats["replica_refreshes"] == r0 + 3
+        before = sc.stats["replica_hits"]
+        got = read(b)
+        assert got == [b"a-" + b"x" * 200 + k for k in b]
+        owned = sum(sc.ring.owner_of_key(k) == rank for k in b)
+        assert sc.stats["replica_hits"] - before == 40 - owned
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_incremental_replica_refresh_gloo(world):
+    _run_world(_drift_worker, world)
+
+
+def _migrate_worker(rank, world, port, q):
+    """A ring change migrated incrementally (a byte budget per call between steps): every
+    GET in the meantime returns the right value or a miss, never a wrong one, and once the
+    migration is done every key hits on its new owner."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+        from shellac_amd.parallel.ring import ShardRing
+
+        sc = ShardedCache(CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu"))
+        keys = [f"/g{i}".encode() for i in range(900)]
+        mine = keys[rank::world]
+        v, vo, vl = pack_values([b"m-" + k for k in mine])
+        sc.set(SetBatch(digest_strings(mine), v, vo, vl))
+
+        def read(ks):
+            res = sc.get(digest_strings(ks))
+            return [r[0] if r else None for r in unpack_records(res.data, res.off, res.size)]
+
+        new = ShardRing(list(range(world)), 97)   # another continuum: many keys move
+        n = sc.set_ring(new, incremental=True, chunk_keys=16)
+        calls = 0
+        while True:
+            got = read(keys)
+            assert all(g is None or g == b"m-" + k for g, k in zip(got, keys))
+            calls += 1
+            if not sc.migrate_step(budget_bytes=16 * 40):
+                break
+        assert calls > 2 or n == 0
+        assert read(keys) == [b"m-" + k for k in keys]
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_incremental_ring_migration_gloo(world):
+    _run_world(_migrate_worker, world)
