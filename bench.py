@@ -110,6 +110,16 @@ def parse():
                     help="which cache state the headline K steps run in: the steady state of a "
                          "full cache (value log wrapped, eviction in every SET batch; default) "
                          "or the fresh cache before the first wrap (also reported as log_fresh)")
+    ap.add_argument("--drift-epochs", type=int, default=4,
+                    help="hot_drift block (N>1 / simulated, replica on): epochs of drifted "
+                         "popularity, each --drift-steps steps then an incremental replica "
+                         "refresh (0 = skip)")
+    ap.add_argument("--drift-steps", type=int, default=400)
+    ap.add_argument("--drift-swap", type=float, default=0.05,
+                    help="share of the replicated top ranks whose objects trade places with "
+                         "tail objects every epoch (content cooling, new content heating up)")
+    ap.add_argument("--drift-budget-mb", type=float, default=512.0,
+                    help="replica refresh byte budget per epoch and rank (MiB)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -560,6 +570,76 @@ def main():
         sync()
         return nfill
 
+    def hot_drift():
+        E, K = args.drift_epochs, args.drift_steps
+        R_ = args.replicate
+        swap = max(1, int(R_ * args.drift_swap))
+        order = wl.rank_to_id
+        budget = int(args.drift_budget_mb * (1 << 20))
+        PB = 4
+        # the refresh ranks keys by their requests over the whole epoch: 1/8 of every batch
+        # (a 2M-key hot set cannot be ranked from a few batches: its tail is seen ~once)
+        sc.sample_rows, sc.sample_batches, sc._samples = args.batch // 8, K, []
+        epochs = []
+        t_steps = t_ref = 0.0
+        for e in range(1, E + 1):
+            order = wl.drifted(order, R_, swap, 4242 + e)   # the same drift on every rank
+            ids_e = [wl.sample_ids(args.batch, 7000 + 97 * rank + 13 * e + i, rank_to_id=order)
+                     for i in range(PB)]
+            g = [wl.digests.index_select(0, x).contiguous() for x in ids_e]
+            gp = ([sim_map["pdig"].index_select(0, x).contiguous() for x in ids_e] if sim
+                  else [None] * PB)
+            del ids_e
+            ev = torch.cuda.Event()
+            ev.record()
+            sc.sync_sets()
+            c0, st0 = shard.counters(), dict(sc.stats)
+            cal0 = int(getattr(sc, "_calibrations", 0))
+            if real_world > 1:
+                dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            for i in range(K):
+                sc.serve(g[i % PB], sets[i % P], inputs_ready=ev, probe_keys=gp[i % PB])
+            sync()
+            t1 = time.perf_counter()
+            sc.sync_sets()
+            c1, st1 = shard.counters(), sc.stats
+            rep = st1["replica_hits"] - st0["replica_hits"]
+            ops = c1["get_ops"] - c0["get_ops"]
+            t2 = time.perf_counter()
+            sc.refresh_replica(args.replicate, budget_bytes=budget)
+            sync()
+            t3 = time.perf_counter()
+            # how much of this epoch's true top-R (ground truth) the refreshed hot set holds
+            truth = wl.digests.index_select(0, order[:R_])
+            hotset = sc._hot if sc._hot is not None else truth[:0]
+            prec = float(ShardedCache._member(truth, hotset).float().mean()) if R_ else 0.0
+            agg = torch.tensor([t1 - t0, t3 - t2, rep, ops], dtype=torch.float64, device=rdev)
+            if real_world > 1:
+                dist.all_reduce(agg, op=dist.ReduceOp.MAX)  # (times: the slowest rank)
+            ts, tr, rep, ops = agg.tolist()
+            t_steps += ts
+            t_ref += tr
+            epochs.append({"ms_per_step": round(ts / K * 1e3, 4), "refresh_ms": round(tr * 1e3, 1),
+                           "replica_hit_fraction": round(rep / max(rep + ops, 1), 4),
+                           "hot_set_size_after_refresh": int(hotset.shape[0]),
+                           "top_covered_after_refresh": round(prec, 4),
+                           "slot_overflow_rows": st1["slot_overflow_rows"] - st0["slot_overflow_rows"],
+                           "calibrating_steps": int(getattr(sc, "_calibrations", 0)) - cal0,
+                           "replica_log_laps": round(replica.head() / (args.replica_gb * (1 << 30)), 3),
+                           "reinsert_mib": round((c1["reinsert_bytes"] - c0["reinsert_bytes"]) / (1 << 20), 1)})
+            del g, gp
+        st = sc.stats
+        return {"epochs": E, "steps_per_epoch": K, "hot_objects_replaced_per_epoch": swap,
+                "refresh_budget_mib": args.drift_budget_mb,
+                "ms_per_step": round(t_steps / (E * K) * 1e3, 4),
+                "ms_per_step_with_refresh": round((t_steps + t_ref) / (E * K) * 1e3, 4),
+                "per_epoch": epochs,
+                "replica_added": st.get("replica_added", 0),
+                "replica_dropped": st.get("replica_dropped", 0),
+                "replica_fetched_gib": round(st.get("replica_fetched_bytes", 0) / (1 << 30), 3)}
+
     steady_ok = not host_edge and dev.type == "cuda" and not args.no_wrapped
     headline_wrapped = steady_ok and args.headline == "wrapped"
     for i in range(args.warmup):
@@ -642,6 +722,13 @@ def main():
         p_sc.sync_sets()
         del p_sc, p_shard
 
+    # secondary: a drifting hot set (hot objects replaced every epoch) with the replica tier
+    # maintained incrementally between epochs (refresh under a byte budget, no flush)
+    drift = None
+    if (args.drift_epochs > 0 and replica is not None and dev.type == "cuda" and not bounce
+            and sc._hot is not None):
+        drift = hot_drift()
+
     t_sm = time.perf_counter()
     sm = {} if (args.no_smoke or dev.type != "cuda" or sim or bounce) else smoke(rank, world, dev)
     if sm:
@@ -715,6 +802,8 @@ def main():
         "log_wrapped": summary(wrapped, wrapped_iv, fill=nfill) if wrapped else None,
         # the same under capacity pressure (a log the key space barely fits: reinsertions)
         "log_pressured": pressured,
+        # a drifting hot set with the replica maintained between epochs (N>1 / simulated)
+        "hot_drift": drift,
         "smoke": sm,
     }
     if host_edge:

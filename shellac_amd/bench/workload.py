@@ -78,12 +78,25 @@ class Workload:
         self.val_off = ((torch.arange(self.total_keys, dtype=torch.int64) * 2654435761) % span
                         & ~15).to(dev)
 
-    def sample_ids(self, n: int, seed: int) -> torch.Tensor:
-        """Zipf(s)-popular object ids (GET traffic)."""
+    def sample_ids(self, n: int, seed: int, rank_to_id: torch.Tensor = None) -> torch.Tensor:
+        """Zipf(s)-popular object ids (GET traffic); ``rank_to_id``: another popularity
+        order (a drifted hot set, see ``drifted``)."""
         g = torch.Generator(device=self.device).manual_seed(seed)
         r = torch.rand(n, generator=g, dtype=torch.float64, device=self.device)
         idx = torch.searchsorted(self.cdf, r).clamp_(max=self.total_keys - 1)
-        return self.rank_to_id.index_select(0, idx)
+        return (self.rank_to_id if rank_to_id is None else rank_to_id).index_select(0, idx)
+
+    def drifted(self, rank_to_id: torch.Tensor, top: int, m: int, seed: int) -> torch.Tensor:
+        """A drifted popularity order: `m` objects of the top `top` ranks (at random ranks)
+        trade places with `m` objects of the tail — content going cold while new content
+        becomes popular, the rest of the order unchanged."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        top = min(top, self.total_keys // 2)
+        a = torch.randperm(top, generator=g)[:m].to(self.device)
+        b = (top + torch.randperm(self.total_keys - top, generator=g)[:m]).to(self.device)
+        out = rank_to_id.clone()
+        out[a], out[b] = rank_to_id[b], rank_to_id[a]
+        return out
 
     def uniform_ids(self, n: int, seed: int) -> torch.Tensor:
         """Uniform object ids (cache-fill / refresh SET traffic: in a TTL cache every

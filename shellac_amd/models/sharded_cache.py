@@ -36,7 +36,7 @@ import torch.distributed as dist
 
 from ..ops import routing as R
 from ..ops.cache import CacheShard, StreamEvent, coalesce, expand, expand_out
-from ..parallel.exchange import (all_gather, all_gather_rows, all_reduce, all_to_all_rows,
+from ..parallel.exchange import (MirrorComm, all_gather, all_gather_rows, all_reduce, all_to_all_rows,
                                  all_to_all_single, allreduce_stats, dist_info, exchange_counts,
                                  segment_sums, step_comm)
 from ..parallel.ring import ShardRing
@@ -207,6 +207,10 @@ class ShardedCache:
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
         # simulated world: request digests -> the digests their owners hold (see serve)
         self.probe_of = None
+        # replica refresh: scores of the hot keys (aligned with _hot) and their decay per
+        # refresh (_hot_candidates)
+        self._hot_score = None
+        self.hot_decay = 0.5
         # run SET chains on a side stream, concurrently with GET gathers (GPU shards)
         self.overlap_store = True
         # GET coalescing: the duplicate keys of a batch share one probe and one record
@@ -582,6 +586,7 @@ class ShardedCache:
         if self._ncomm is not False and not cal:
             return self._serve_native(e, keys, batch, now, n, ns_in, cap_g, cap_d, cap_l,
                                       fanout, rep, inputs_ready)
+        self._calibrations = getattr(self, "_calibrations", 0) + 1  # (the multi-call path)
         ph = _Phases("serve.")
         ph.next("plan")
         # G = [recv: w-1 slots | self slot | send: w-1 slots] of cap_g digests
@@ -997,17 +1002,29 @@ class ShardedCache:
         return back.index_select(0, perm).bool()
 
     # ------------------------------------------------------------------------------
-    def _hot_candidates(self, top_k: int, keys: Optional[torch.Tensor]) -> torch.Tensor:
+    def _hot_candidates(self, top_k: int, keys: Optional[torch.Tensor],
+                        old: Optional[torch.Tensor] = None,
+                        old_score: Optional[torch.Tensor] = None):
         """Collective: the global top-k digests by request count (from ``keys`` or the
         recent GET samples), the same on every rank, most requested first (ties in digest
-        order: a stable sort of the all-gathered counts, identical everywhere)."""
+        order: stable sorts of all-gathered / all-reduced counts, identical everywhere),
+        and their scores. With the current hot set ``old`` (sorted by lo) and its scores
+        from the last refresh, an old key scores decay * its old score + its requests now
+        + 1 (hysteresis): the tail of a large hot set is seen a few times per sample at
+        most, so a key only displaces a hot one when it is seen more often — the hot set
+        follows a drift instead of churning on sampling noise."""
         dev, w = self.device, self.world
         if keys is None:
             keys = torch.cat(self._samples) if self._samples else torch.zeros((0, 2), dtype=torch.int64,
                                                                              device=dev)
+        # count by the low digest word (a 1-D sort; two keys sharing it are vanishingly rare)
         if keys.shape[0]:
-            uniq, cnt = torch.unique(keys, dim=0, return_counts=True)
+            ulo, inv, cnt = torch.unique(keys[:, 0].contiguous(), return_inverse=True,
+                                         return_counts=True)
+            uniq = torch.empty((ulo.numel(), 2), dtype=torch.int64, device=dev)
+            uniq[inv] = keys
         else:
+            ulo = torch.zeros(0, dtype=torch.int64, device=dev)
             uniq = torch.zeros((0, 2), dtype=torch.int64, device=dev)
             cnt = torch.zeros(0, dtype=torch.int64, device=dev)
         k = min(top_k, uniq.shape[0])
@@ -1022,14 +1039,35 @@ class ShardedCache:
         all_gather(all_n, ccnt, group=self.group)
         allc = torch.cat(all_c)
         alln = torch.cat(all_n)
-        u, inv = torch.unique(allc, dim=0, return_inverse=True)
+        # merge by the low word (a 1-D sort), in digest order: identical on every rank
+        ulo2, inv = torch.unique(allc[:, 0].contiguous(), return_inverse=True)
+        u = torch.empty((ulo2.numel(), 2), dtype=torch.int64, device=dev)
+        u[inv] = allc
         tot = torch.zeros(u.shape[0], dtype=torch.int64, device=dev).scatter_add_(0, inv, alln)
-        valid = tot > 0
-        tot = torch.where(valid, tot, torch.full_like(tot, -1))
-        kk = min(top_k, u.shape[0])
-        order = torch.sort(-tot, stable=True).indices[:kk]
-        hot = u.index_select(0, order)
-        return hot[(hot != 0).any(dim=1)].contiguous()     # drop padding rows (identical everywhere)
+        # a key enters the hot set only once seen twice (a mirrored world counts every
+        # sighting once per simulated rank)
+        min_count = 2 * (w if isinstance(self.group, MirrorComm) else 1)
+        keep = ((u != 0).any(dim=1)) & (tot >= min_count)  # (drops the padding rows too)
+        u, score = u[keep], tot[keep].to(torch.float64)
+        if old is not None and old.shape[0]:
+            # the old keys' requests in this sample, summed over the ranks
+            oc = torch.zeros(old.shape[0], dtype=torch.int64, device=dev)
+            if ulo.numel():
+                at = torch.clamp(torch.searchsorted(ulo, old[:, 0].contiguous()), max=ulo.numel() - 1)
+                oc = torch.where(ulo.index_select(0, at) == old[:, 0], cnt.index_select(0, at), oc)
+            all_reduce(oc, group=self.group)
+            prev = old_score if old_score is not None else torch.zeros(old.shape[0], dtype=torch.float64,
+                                                                       device=dev)
+            osc = prev * self.hot_decay + oc.to(torch.float64) + 1.0
+            fresh = ~self._member(u, old)
+            u = torch.cat([old, u[fresh]])
+            score = torch.cat([osc, score[fresh]])
+        # (with an old hot set every old key stays in the ranking: the caller picks the
+        # top-k among the keys it could put in place)
+        order = torch.sort(-score, stable=True).indices
+        if old is None or old.shape[0] == 0:
+            order = order[:top_k]
+        return u.index_select(0, order).contiguous(), score.index_select(0, order).contiguous()
 
     @staticmethod
     def _member(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -1085,17 +1123,15 @@ class ShardedCache:
         if self.replica is None:
             return 0
         dev = self.device
-        ranked = self._hot_candidates(top_k, keys)          # most requested first
-        target = ranked.index_select(0, torch.argsort(ranked[:, 0])).contiguous()
         old = self._hot if self._hot is not None else torch.zeros((0, 2), dtype=torch.int64,
                                                                     device=dev)
-        if target.shape[0] == 0 and old.shape[0] == 0:
+        ranked, rscore = self._hot_candidates(top_k, keys, old, self._hot_score)  # hottest first
+        if ranked.shape[0] == 0 and old.shape[0] == 0:
             return 0
-        stay = self._member(old, target)
-        dropped = old[~stay].contiguous()
-        kept = old[stay]
-        # newly hot keys, most requested first, fetched in chunks under the byte budget
-        added = ranked[~self._member(ranked, old)]
+        # newly hot keys (in the top k, not in place yet), most requested first, fetched in
+        # chunks under the byte budget
+        top = ranked[:top_k]
+        added = top[~self._member(top, old)]
         stored = fetched = 0
         took = []
         chunk = max(1, int(chunk_keys))
@@ -1107,13 +1143,24 @@ class ShardedCache:
             stored += n_st
             fetched += nb
             took.append(part)
+        # the new hot set: the top-k of the ranking among the keys that are in place (old
+        # ones and the ones fetched now); an old key leaves only for a fetched hotter one
+        avail = torch.cat([old] + took) if took else old
+        avail = avail.index_select(0, torch.argsort(avail[:, 0])).contiguous()
+        new = ranked[self._member(ranked, avail)][:top_k] if avail.shape[0] else avail
+        nsorted = new.index_select(0, torch.argsort(new[:, 0])).contiguous()
+        dropped = old[~self._member(old, nsorted)].contiguous()
         if dropped.shape[0]:
             self.replica.remove(dropped, now)             # no longer written through
-        new = torch.cat([kept] + took) if (took or kept.shape[0]) else kept
         if new.shape[0] == 0:
-            self._hot = None
+            self._hot = self._hot_score = None
         else:
-            self._hot = new.index_select(0, torch.argsort(new[:, 0])).contiguous()
+            self._hot = nsorted
+            # the scores of the hot keys, aligned with self._hot (the next refresh decays them)
+            by_lo = torch.argsort(ranked[:, 0])
+            rlo = ranked[:, 0].index_select(0, by_lo).contiguous()
+            at = torch.clamp(torch.searchsorted(rlo, nsorted[:, 0].contiguous()), max=rlo.numel() - 1)
+            self._hot_score = rscore.index_select(0, by_lo.index_select(0, at)).contiguous()
         self._hot_dir = None
         changed = dropped.shape[0] + sum(t.shape[0] for t in took)
         # a large change of the hot set changes the traffic matrix: measure it afresh (the
@@ -1214,7 +1261,7 @@ class ShardedCache:
             self.shard.flush()
         if self.replica is not None:
             self.replica.flush()
-            self._hot = None
+            self._hot = self._hot_score = None
             self._reset_exchange()
 
     def restore_shard(self, rank: int, now: Optional[int] = None) -> int:
