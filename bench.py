@@ -118,8 +118,12 @@ def parse():
     ap.add_argument("--drift-swap", type=float, default=0.05,
                     help="share of the replicated top ranks whose objects trade places with "
                          "tail objects every epoch (content cooling, new content heating up)")
+    ap.add_argument("--drift-sample", type=int, default=16 << 20,
+                    help="observed requests per rank the replica refresh ranks keys by")
     ap.add_argument("--drift-budget-mb", type=float, default=512.0,
                     help="replica refresh byte budget per epoch and rank (MiB)")
+    ap.add_argument("--gather-after-append", action="store_true",
+                    help="one GPU: the GET gather waits for the SET batch's log append")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -370,6 +374,7 @@ def main():
     sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group,
                       routed=True if routed1 else None, comm_mode=args.comm_mode)
     sc.coalesce = not args.no_coalesce
+    sc.gather_after_append = args.gather_after_append
     if sim:
         sc.probe_of = sim_map["probe_of"]
 
@@ -577,9 +582,10 @@ def main():
         order = wl.rank_to_id
         budget = int(args.drift_budget_mb * (1 << 20))
         PB = 4
-        # the refresh ranks keys by their requests over the whole epoch: 1/8 of every batch
-        # (a 2M-key hot set cannot be ranked from a few batches: its tail is seen ~once)
-        sc.sample_rows, sc.sample_batches, sc._samples = args.batch // 8, K, []
+        # The refresh ranks keys by the requests of the epoch: the steps cycle a few batches,
+        # so the traffic the epoch stands for is sampled afresh from its popularity order
+        # (--drift-sample requests per rank; a 2M-key hot set cannot be ranked from a few
+        # batches: its tail is seen about once)
         epochs = []
         t_steps = t_ref = 0.0
         for e in range(1, E + 1):
@@ -607,8 +613,12 @@ def main():
             c1, st1 = shard.counters(), sc.stats
             rep = st1["replica_hits"] - st0["replica_hits"]
             ops = c1["get_ops"] - c0["get_ops"]
+            seen = wl.digests.index_select(0, wl.sample_ids(args.drift_sample, 9100 + 97 * rank + e,
+                                                            rank_to_id=order))
+            sync()
             t2 = time.perf_counter()
-            sc.refresh_replica(args.replicate, budget_bytes=budget)
+            sc.refresh_replica(args.replicate, keys=seen, budget_bytes=budget)
+            del seen
             sync()
             t3 = time.perf_counter()
             # how much of this epoch's true top-R (ground truth) the refreshed hot set holds

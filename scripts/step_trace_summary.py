@@ -3,10 +3,13 @@
 step (scripts/trace_bench.sh): kernels and ROCTX phases between consecutive
 `serve.plan` markers, plus the timeline of the last step.
 
-usage: step_trace_summary.py TRACE_DIR [STEPS]"""
+usage: step_trace_summary.py TRACE_DIR [STEPS] [STEP_MARKER]
+STEP_MARKER: the ROCTX range that starts a step (default serve.plan, the routed step;
+hbm.lookup_coalesced for the one-GPU step)."""
 import csv,sys,re
 from collections import defaultdict
 d=sys.argv[1]; nsteps=int(sys.argv[2]) if len(sys.argv)>2 else 10
+marker=sys.argv[3] if len(sys.argv)>3 else 'serve.plan'
 m=list(csv.DictReader(open(d+'/bench_marker_api_trace.csv')))
 k=list(csv.DictReader(open(d+'/bench_kernel_trace.csv')))
 def short(n):
@@ -14,7 +17,7 @@ def short(n):
     mm=re.match(r"([\w:]+(<[^()]*?>)?)",n); b=mm.group(1) if mm else n
     if b.startswith("at::") or b.startswith("rocprim"): b=b.split("<")[0]
     return b.replace("shellac::","")[:60]
-plans=sorted(int(r['Start_Timestamp']) for r in m if r['Function']=='serve.plan')
+plans=sorted(int(r['Start_Timestamp']) for r in m if r['Function']==marker)
 print(len(plans),'plan markers')
 st=plans[-nsteps-1:]
 ks=sorted((int(r['Start_Timestamp']),int(r['End_Timestamp']),short(r['Kernel_Name']),

@@ -145,12 +145,16 @@ PYBIND11_MODULE(_shellac_core, m) {
         return c.wait_host_slot(i, timeout_ms);
       }, py::arg("slot"), py::arg("timeout_ms") = 10000)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
-                        uintptr_t s, uint64_t out_cap) {
+                        uintptr_t s, uint64_t out_cap, uintptr_t first, uintptr_t size,
+                        uintptr_t out_size, uintptr_t out_off, uintptr_t table, uintptr_t cslot) {
         py::gil_scoped_release nogil;
         c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s),
-                 out_cap);
+                 out_cap, P<const uint32_t>(first), P<const uint64_t>(size), P<uint64_t>(out_size),
+                 P<uint64_t>(out_off), P<uint32_t>(table), P<const uint32_t>(cslot));
       }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
-         py::arg("out_cap") = ~0ull)
+         py::arg("out_cap") = ~0ull, py::arg("first") = 0, py::arg("size") = 0,
+         py::arg("out_size") = 0, py::arg("out_off") = 0, py::arg("table") = 0,
+         py::arg("cslot") = 0)
       .def("store_graph", [](HbmCache& c, HbmCache::StoreGraph& g, uintptr_t keys,
                              uintptr_t values, uintptr_t val_off, uintptr_t vlen, uintptr_t flags,
                              uintptr_t expire, int64_t n, uint64_t bytes_bound, uint32_t now,
@@ -163,14 +167,18 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
-                       uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after) {
+                       uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after,
+                       uintptr_t append_after, uintptr_t append_done) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
-                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after));
+                bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), true,
+                reinterpret_cast<hipEvent_t>(append_after),
+                reinterpret_cast<hipEvent_t>(append_done));
       }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
          py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
-         py::arg("stream"), py::arg("index_after") = 0)
+         py::arg("stream"), py::arg("index_after") = 0, py::arg("append_after") = 0,
+         py::arg("append_done") = 0)
       .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
                         uintptr_t s) {
         py::gil_scoped_release nogil;

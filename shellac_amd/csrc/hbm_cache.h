@@ -136,8 +136,14 @@ class HbmCache {
   // GET phase 2: copy each hit's [ItemHeader | value | pad] to out + off[i]. `out` may be
   // pinned host memory (zero-copy); nothing is written when off[n] > out_cap, so the
   // caller can queue the gather before it knows the total and retry if it did not fit.
+  // `first` (a coalesced lookup): the gather's workgroups also write every request's
+  // (size, off) from its claimer into out_size / out_off and clear the claimers' slots of
+  // the coalescing table (expand_coalesced_out's work, no launch of its own).
   void gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out, hipStream_t s,
-              uint64_t out_cap = ~0ull);
+              uint64_t out_cap = ~0ull, const uint32_t* first = nullptr,
+              const uint64_t* size = nullptr, uint64_t* out_size = nullptr,
+              uint64_t* out_off = nullptr, uint32_t* table = nullptr,
+              const uint32_t* cslot = nullptr);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).
@@ -149,10 +155,15 @@ class HbmCache {
   // the append overwrites.
   // `allow_reclaim` false: no CLOCK hand this batch (the append stays within
   // `bytes_bound`; a caller that reserved only that much for it, see would_reclaim).
+  // `append_after`: the log append (and what follows) waits for this event; the CLOCK
+  // hand, the dedupe and the sizing (reads only) run at once — beside a gather that
+  // still reads the region the append will overwrite. `append_done`: recorded right after
+  // the log append (a caller can keep its gather from contending with it).
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
              uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-             bool allow_reclaim = true);
+             bool allow_reclaim = true, hipEvent_t append_after = nullptr,
+             hipEvent_t append_done = nullptr);
   // Whether a SET of `bytes_bound` bytes issued now would run the CLOCK hand (the log is
   // within a few batches of wrapping); the answer can only turn true later.
   bool would_reclaim(uint64_t bytes_bound) const {
@@ -273,7 +284,8 @@ class HbmCache {
   std::mutex mu_;
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                    int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr);
+                    int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
+                    hipEvent_t append_after = nullptr, hipEvent_t append_done = nullptr);
   void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after);

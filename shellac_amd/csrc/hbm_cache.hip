@@ -831,6 +831,30 @@ __device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, in
   }
 }
 
+// A coalesced GET's per-request answers, done by the gather's workgroups after their
+// copies (a grid-stride tail, n = 0: none): row i takes its claimer's (size, off), and
+// every claimer clears its slot of the coalescing table (k_expand_out's work, without a
+// launch or a stream of its own).
+struct ExpandTail {
+  const uint32_t* first = nullptr;
+  int64_t n = 0;
+  const uint64_t* size = nullptr;
+  const uint64_t* off = nullptr;
+  uint64_t* out_size = nullptr;
+  uint64_t* out_off = nullptr;
+  uint32_t* tab = nullptr;
+  const uint32_t* cslot = nullptr;
+};
+__device__ __forceinline__ void expand_tail(const ExpandTail& ex) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < ex.n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t f = ex.first[i];
+    ex.out_size[i] = ex.size[f];
+    ex.out_off[i] = ex.off[f];
+    if (f == (uint32_t)i && ex.tab) ex.tab[ex.cslot[i]] = 0u;
+  }
+}
+
 // Mode 0 (gather/pack): chunk at byte x of segment j comes from src + src_off[j] + w;
 // a segment whose src_off is kSegSkip is a gap (its bytes are left as they are).
 // Mode 2 (sized gather): as mode 0, but segment j holds only seg_len[j] bytes (passed in
@@ -855,7 +879,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // MODE 1 extras
     const Digest* __restrict__ keys, const uint32_t* __restrict__ vlen,
     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ expire,
-    const uint64_t* __restrict__ head_ptr, uint64_t cap, int min_tile) {
+    const uint64_t* __restrict__ head_ptr, uint64_t cap, int min_tile, ExpandTail ex) {
+  // the copy (a uniform early exit per workgroup skips to the expand tail)
+  do {
   // mode 2 stages a length per segment too: fewer segments per pass keep 8 waves/SIMD
   constexpr int TSC = MODE == 2 ? 768 : kTileSegCap;
   __shared__ uint64_t s_off[TSC + 1];
@@ -864,7 +890,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   __shared__ int s_cnt[kBlock / 64];
   if (MODE == 3) n = *reinterpret_cast<const int64_t*>(head_ptr);  // count on the device
   const uint64_t total = dst_off[n];
-  if ((MODE == 0 || MODE == 3) && total > cap) return;  // MODE 0/3: destination capacity
+  if ((MODE == 0 || MODE == 3) && total > cap) break;  // MODE 0/3: destination capacity
   const uint64_t* __restrict__ seg_len = MODE == 2 ? head_ptr : nullptr;
   __shared__ uint32_t s_len[MODE == 2 ? TSC : 1];  // records < 4 GiB
   const int64_t nchunks = (int64_t)(total >> 4);
@@ -875,7 +901,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   if (span < min_tile) span = min_tile;
   const int64_t r0 = (int64_t)blockIdx.x * span;
   const int64_t r1 = min(r0 + span, nchunks);
-  if (r0 >= r1) return;
+  if (r0 >= r1) break;
   block_find2(dst_off, n + 1, (uint64_t)r0 << 4, ((uint64_t)r1 << 4) - 1, s_lo, s_hi, s_cnt);
   const int64_t ja = s_lo[0], jb = s_lo[1];
   for (int64_t j0 = ja; j0 <= jb; j0 += TSC) {
@@ -957,6 +983,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
       }
     }
   }
+  } while (false);
+  if (ex.n) expand_tail(ex);
 }
 
 // Co-resident workgroups of a kernel on the current device (occupancy x CUs), cached.
@@ -977,11 +1005,15 @@ int resident_grid(K kernel, int* cache) {
 // The byte mover's launch: 4 loads in flight per lane, 8 waves/SIMD, nontemporal stores,
 // kSegOcc64/64 of the co-resident slots (see the tuned constants above).
 template <int MODE, typename... Args>
-void launch_segcopy(hipStream_t s, Args... args) {
+void launch_segcopy_ex(hipStream_t s, const ExpandTail& ex, Args... args) {
   static int grid[64];
   const auto kern = k_segcopy<MODE, 4, 8, true>;
   const int g = std::max(1, resident_grid(kern, grid) * kSegOcc64 / 64);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., kSegMinTile);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., kSegMinTile, ex);
+}
+template <int MODE, typename... Args>
+void launch_segcopy(hipStream_t s, Args... args) {
+  launch_segcopy_ex<MODE>(s, ExpandTail{}, args...);
 }
 
 // ---------------------------------------------------------------------------------
@@ -3120,16 +3152,24 @@ void HbmCache::serve_stop() {
 }
 
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
-                      hipStream_t s, uint64_t out_cap) {
+                      hipStream_t s, uint64_t out_cap, const uint32_t* first,
+                      const uint64_t* size, uint64_t* out_size, uint64_t* out_off,
+                      uint32_t* table, const uint32_t* cslot) {
   TraceRange tr("hbm.gather");
   DeviceGuard g(cfg_.device);
-  segcopy(log_, loc, off, n, out, s, out_cap);
+  if (n <= 0) return;
+  ExpandTail ex;
+  if (first) ex = ExpandTail{first, n, size, off, out_size, out_off, table, cslot};
+  launch_segcopy_ex<0>(s, ex, log_, loc, off, n, out, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       out_cap);
+  HIP_OK(hipGetLastError());
 }
 
 void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
-                     hipEvent_t index_after, bool allow_reclaim) {
+                     hipEvent_t index_after, bool allow_reclaim, hipEvent_t append_after,
+                     hipEvent_t append_done) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
@@ -3159,8 +3199,8 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
-                 index_after);
-  } else if (n <= kSmallSetRows && !index_after) {
+                 index_after, append_after, append_done);
+  } else if (n <= kSmallSetRows && !index_after && !append_after && !append_done) {
     // one launch for the whole chain (the proxy's small SET batches)
     hipLaunchKernelGGL(k_set_small, dim3(1), dim3(kBlock), 0, s, keys, values, val_off, vlen,
                        flags, expire, (int)n, cfg_.max_item, index_, cfg_.nbuckets - 1,
@@ -3171,7 +3211,8 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     HIP_OK(hipGetLastError());
   } else {
     ensure_set_ws(n, s);
-    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after);
+    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, append_after,
+                 append_done);
   }
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
@@ -3184,11 +3225,14 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
 // `index_after`, is the only part a concurrent lookup can observe.
 void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                            int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after) {
+                            int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
+                            hipEvent_t append_after, hipEvent_t append_done) {
   store_plan_locked(keys, vlen, n, s);
+  if (append_after) HIP_OK(hipStreamWaitEvent(s, append_after, 0));
   launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());
+  if (append_done) HIP_OK(hipEventRecord(append_done, s));
   store_index_locked(keys, vlen, expire, n, now, s, index_after);
 }
 

@@ -230,6 +230,8 @@ class ShardedCache:
         # what these events order). One box, two rounds: 0.309 / 0.308 ms per step with
         # "device" vs 0.315 / 0.311 with "system" (profiles/r2_event_fence_ab.log)
         self.event_fence = "device"
+        # one GPU: the gather waits for the SET batch's log append (see serve)
+        self.gather_after_append = False
         self._events = {}
         self._side = None
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
@@ -422,12 +424,15 @@ class ShardedCache:
             return GetResult(data, lk.off[:n], lk.size[:n])
         side = self._side_stream() if self.overlap_store else None
         if side is not None:
-            # The SET chain runs on a side stream from the start of the step: its dedupe,
-            # sizing and log append (bytes the lookup reserves, so the gather never reads
-            # them) overlap the coalescing and the probe; only its index insert waits for
-            # the probe (event), then runs under the bandwidth-bound gather.
+            # The SET chain runs on a side stream from the start of the step: its CLOCK hand
+            # (a full cache), dedupe and sizing run at once — beside the previous step's
+            # gather, which may still read the log region this append overwrites — its log
+            # append (bytes the lookup reserves, so this step's gather never reads them) once
+            # that gather is done, overlapping the coalescing and the probe; only its index
+            # insert waits for the probe (event), then runs under the bandwidth-bound gather.
             main = torch.cuda.current_stream(self.device)
-            self._xwait(side, main, "start")  # the previous step's gather is done with the log
+            start = self._event("start")
+            start.record(main)                # the previous step's gather is done with the log
             now = sh.now() if now is None else now
         if self.coalesce:
             table = self._coalesce_table(n) if side is not None else None
@@ -449,13 +454,19 @@ class ShardedCache:
             out_off = torch.empty(n, dtype=torch.int64, device=self.device)
         ev = self._event("probe")
         ev.record(main)
+        appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                     batch.expire, now, index_after=ev)
-            if first is not None:
-                # per-request (size, off) and the table clean-up, under the gather
-                expand_out(first, lk.size, lk.off, out_size, out_off, table, cslot)
-        data = self._gather_unsynced(lk)
+                     batch.expire, now, index_after=ev, append_after=start, append_done=appended)
+        if appended is not None:
+            # the gather runs after the log append, not beside it: the two byte movers
+            # contending for HBM are slower together than one after the other
+            appended.wait(main) if isinstance(appended, StreamEvent) else main.wait_event(appended)
+        # per-request (size, off) and the table clean-up: the gather's workgroups do them
+        # after their copies (no launch, and nothing on the side stream for the next
+        # step's lookup to wait for but the SET chain)
+        data = self._gather_unsynced(
+            lk, None if first is None else (first, out_size, out_off, table, cslot))
         self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
         if first is not None:
             return GetResult(data, out_off, out_size)
@@ -488,7 +499,7 @@ class ShardedCache:
             t = self._co_table = torch.zeros(slots, dtype=torch.int32, device=self.device)
         return t
 
-    def _gather_unsynced(self, lk) -> torch.Tensor:
+    def _gather_unsynced(self, lk, expand=None) -> torch.Tensor:
         """Gather a lookup given ``total_slot=0`` without stalling the GPU: the gather
         is queued at once into a buffer sized from earlier steps (the kernel writes
         nothing if the total exceeds it) and the host reads the kernel-written total
@@ -497,13 +508,14 @@ class ShardedCache:
         cap = self._gather_cap
         if cap:
             data = self._out_buffer(cap)
-            sh.gather(lk, data, out_cap=cap)
+            sh.gather(lk, data, out_cap=cap, expand=expand)
         total = sh.host_total(0)
         self.gathered_bytes += total
         if cap and total <= cap:
             return data
         self._gather_cap = max(int(total * 1.25), 1 << 20) // 16 * 16
-        return sh.gather(lk, self._out_buffer(max(total, 16)))
+        # (the expand tail ran with the first gather too: it is idempotent)
+        return sh.gather(lk, self._out_buffer(max(total, 16)), expand=expand)
 
     def _out_buffer(self, nbytes: int) -> torch.Tensor:
         if self.host_edge:

@@ -413,18 +413,27 @@ class CacheShard:
         return out, off
 
     def gather(self, lk: Lookup, out: Optional[torch.Tensor] = None,
-               total: Optional[int] = None, out_cap: Optional[int] = None) -> torch.Tensor:
+               total: Optional[int] = None, out_cap: Optional[int] = None,
+               expand=None) -> torch.Tensor:
         """Copy hits into ``out`` (allocated from off[n] if not given: one sync).
         ``out_cap`` (GPU): the kernel writes nothing when off[n] exceeds it, so a gather
-        can be queued before the total is known."""
+        can be queued before the total is known. ``expand`` (GPU, a coalesced lookup):
+        (first, out_size, out_off, table, cslot) — the gather also writes every request's
+        (size, off) from its claimer and clears the coalescing table (``expand_out``)."""
         if out is None:
             total = int(lk.off[lk.n].item()) if total is None else total
             out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
         self._check(out, "out")
         if self.is_gpu:
             cap = out.numel() if out_cap is None else min(int(out_cap), out.numel())
+            ex = [0] * 6
+            if expand is not None:
+                first, osz, ooff, table, cslot = expand
+                ex = [first.data_ptr(), lk.size.data_ptr(), osz.data_ptr(), ooff.data_ptr(),
+                      table.data_ptr() if table is not None else 0,
+                      cslot.data_ptr() if cslot is not None else 0]
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
-                              self._s(), cap)
+                              self._s(), cap, *ex)
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
@@ -456,13 +465,16 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after=None) -> None:
+              index_after=None, append_after=None, append_done=None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
         dedupe, sizing and the log append run at once, the index insert waits for the
         event — so a lookup followed by that event on another stream overlaps the SET's log
-        write (see ``HbmCache::store``)."""
+        write (see ``HbmCache::store``). ``append_after`` (GPU, an event): the log append
+        waits for it, the CLOCK hand and the SET planning do not (a gather still reading the
+        region the append overwrites may run meanwhile). ``append_done`` (GPU, an event):
+        recorded right after the log append."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -478,7 +490,8 @@ class CacheShard:
                  else int(bytes_bound))
         if self.is_gpu:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
-                             fp, ep, n, bound, now, self._s(), _event_handle(index_after))
+                             fp, ep, n, bound, now, self._s(), _event_handle(index_after),
+                             _event_handle(append_after), _event_handle(append_done))
         else:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now, bound)
