@@ -97,6 +97,15 @@ class CacheBackend {
     (void)down;
     return false;
   }
+  // Reactor-direct submission (HbmBackend's edge server): a reactor thread attaches once
+  // with itself as `ex`; its GETs may then be held by the tier and sent to the GPU from
+  // the reactor's own loop by direct_service(), which also answers finished ones inline —
+  // no batcher-thread hop either way. direct_service() returns true while jobs are
+  // outstanding (the loop keeps polling instead of blocking); direct_detach() drains them
+  // before the thread exits. Wrappers forward; other tiers ignore them.
+  virtual void direct_attach(Executor* ex) { (void)ex; }
+  virtual bool direct_service() { return false; }
+  virtual void direct_detach() {}
 };
 
 // 32-bit-point ring over digests, identical to shellac_amd.parallel.ring.ShardRing.
@@ -167,6 +176,14 @@ struct HbmBackendConfig {
   int serve_backlog = 2;
   // CPUs the batcher threads run on (thread i on batcher_cpus[i % size]; empty: unpinned)
   std::vector<int> batcher_cpus;
+  // Reactor-direct GETs (CacheBackend::direct_attach): an attached reactor writes its own
+  // edge-server jobs (at most kServeKeys distinct keys, while fewer than direct_backlog
+  // jobs are queued on the server) and polls their completion words in its loop; larger
+  // or write-ordered batches still go through the batcher. Needs edge_server.
+  bool direct = true;
+  int direct_backlog = 4;
+  uint64_t direct_arena_bytes = 1u << 20;  // pinned arenas reserved per GPU for them
+  int direct_arenas = 32;
 };
 
 // One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are
@@ -190,6 +207,9 @@ class HbmBackend : public CacheBackend {
   int peer_path(int src_dev, int dst_dev) const;
   void stats(StatList* out) override;
   bool inject_shard_down(int shard, bool down) override;
+  void direct_attach(Executor* ex) override;
+  bool direct_service() override;
+  void direct_detach() override;
 
   struct Req {
     int kind;  // 0 get, 1 set, 2 del
@@ -202,15 +222,36 @@ class HbmBackend : public CacheBackend {
     DelCallback dcb;
   };
   struct Dev;
+  struct Direct;
+  // reactor contexts (host slots kDirectSlot0 + kDirectJobs * context + job)
+  static constexpr int kDirectJobs = 2, kDirectSlot0 = 32, kDirectMax = 15;
 
  private:
   int route(const Digest& d) const;
   void enqueue(int dev, Req r);
+  void enqueue_many(int dev, std::vector<Req>& rs);
   uint32_t now() const;
+  // SETs / DELETEs accepted and not yet finished on the GPU, counted per digest hash: a
+  // reactor-direct GET of such a key goes through the batcher (ordered after them)
+  static constexpr size_t kWpend = 1 << 16;
+  void write_begin(uint64_t lo) {
+    wpend_[lo & (kWpend - 1)].fetch_add(1, std::memory_order_acq_rel);
+  }
+  void write_end(uint64_t lo) {
+    wpend_[lo & (kWpend - 1)].fetch_sub(1, std::memory_order_acq_rel);
+  }
+  bool writes_pending(uint64_t lo) const {
+    return wpend_[lo & (kWpend - 1)].load(std::memory_order_acquire) != 0;
+  }
+  void direct_submit(Direct& dc, size_t k);
+  void direct_reap(Direct& dc, size_t k, int j);
 
   HbmBackendConfig cfg_;
   DigestRing ring_;
   std::vector<std::unique_ptr<Dev>> devs_;
+  std::unique_ptr<std::atomic<uint32_t>[]> wpend_;
+  std::mutex direct_mu_;
+  std::vector<std::unique_ptr<Direct>> direct_;
   std::vector<uint8_t> peer_ok_;  // [src * n + dst]: peer access enabled (direct xGMI copies)
   std::atomic<uint64_t> up_mask_{0};  // bit i: shard i serves requests
   double epoch_;
@@ -234,6 +275,18 @@ class TieredBackend : public CacheBackend {
   std::string name() const override { return l1_->name() + "+" + l2_->name(); }
   void stats(StatList* out) override;
   bool inject_shard_down(int shard, bool down) override;
+  void direct_attach(Executor* ex) override {
+    l1_->direct_attach(ex);
+    l2_->direct_attach(ex);
+  }
+  bool direct_service() override {
+    const bool a = l1_->direct_service();
+    return l2_->direct_service() || a;
+  }
+  void direct_detach() override {
+    l1_->direct_detach();
+    l2_->direct_detach();
+  }
 
  private:
   std::shared_ptr<CacheBackend> l1_, l2_;
@@ -268,6 +321,9 @@ class FaultBackend : public CacheBackend {
   std::string name() const override { return "fault(" + inner_->name() + ")"; }
   void stats(StatList* out) override;
   bool inject_shard_down(int shard, bool down) override;
+  void direct_attach(Executor* ex) override { inner_->direct_attach(ex); }
+  bool direct_service() override { return inner_->direct_service(); }
+  void direct_detach() override { inner_->direct_detach(); }
   void set_spec(const FaultSpec& spec);
   FaultSpec spec() const;
 

@@ -134,6 +134,27 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
       delete p;
     });
   }
+  // take() without allocating or trimming (no HIP call: safe on a reactor thread); null
+  // when no idle arena fits
+  std::shared_ptr<Arena> try_take(size_t min_cap) {
+    Arena a{};
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      int best = -1;
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].cap >= min_cap && (best < 0 || free_[i].cap < free_[(size_t)best].cap))
+          best = (int)i;
+      if (best < 0) return nullptr;
+      a = free_[(size_t)best];
+      free_.erase(free_.begin() + best);
+      free_bytes_ -= a.cap;
+    }
+    auto pool = shared_from_this();
+    return std::shared_ptr<Arena>(new Arena(a), [pool](Arena* p) {
+      pool->give_back(*p);
+      delete p;
+    });
+  }
   // n arenas of cap bytes into the free list (at start-up, before any traffic)
   void reserve(size_t n, size_t cap) {
     std::vector<std::shared_ptr<Arena>> held;
@@ -192,6 +213,7 @@ struct HbmBackend::Dev {
   std::atomic<size_t> qn{0};
   std::atomic<bool> spinning{false};
   bool stop = false, flush_req = false;
+  bool kick = false;  // the shard's state changed (drill set / lifted): wake an idle batcher
   std::atomic<bool> ctl_pending{false};  // flush / filter rebuild requested (no requests needed)
   std::thread th;
   // health
@@ -217,12 +239,19 @@ struct HbmBackend::Dev {
   uint32_t pend_flush = 0;
   void track_writes(const Flight& f, int dir);
   double avg_row_bytes = 4096;
+  // flushes requested and not yet finished on the GPU (any thread reads it: a
+  // reactor-direct GET waits for them by going through the batcher)
+  std::atomic<uint32_t> flush_pend{0};
+  void flush_done() { flush_pend.fetch_sub(1, std::memory_order_acq_rel); }
+  // offsets arrays of the reactor-direct jobs on this GPU (mapped; 32 words per job)
+  Mapped direct_offs;
   // stats
   std::atomic<uint64_t> batches{0}, batched_reqs{0}, max_batch{0}, batch_ns{0}, coalesced{0},
       filt_skips{0}, filt_rebuilds{0}, sweeps{0}, live_objects{0}, live_bytes{0},
       key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, arena_misses{0},
       dropped{0}, staged_copies{0}, served_batches{0}, ordered_gets{0},
-      migrated{0}, migrate_ns{0};
+      migrated{0}, migrate_ns{0}, direct_jobs{0}, direct_reqs{0}, direct_fallbacks{0},
+      direct_overflows{0}, direct_timeouts{0};
 
   void loop();
   bool take_batch(std::vector<Req>* out, bool* do_flush, bool* rebuilding);
@@ -232,7 +261,8 @@ struct HbmBackend::Dev {
   void deliver_dels(Flight& f);
   void overflow_misses(Flight& f);
   void fail_flight(Flight& f);
-  void fail_requests(std::vector<Req>& reqs);
+  // `unlaunched`: the requests never reached the GPU (their SETs / DELETEs end here)
+  void fail_requests(std::vector<Req>& reqs, bool unlaunched);
   void eject(const char* why);
   void maybe_restore();
   uint64_t migrate_from(Dev& src);
@@ -253,6 +283,7 @@ struct HbmBackend::Dev {
       f->arena.reset();
       if (f->ev) (void)hipEventDestroy(f->ev);
     }
+    direct_offs.release();
     cache.reset();
     if (stream) (void)hipStreamDestroy(stream);
     if (mstream) (void)hipStreamDestroy(mstream);
@@ -265,12 +296,77 @@ struct HbmBackend::Dev {
 // Host slots the edge GET signals completion through: one per flight.
 constexpr int kFlightSlot0 = 8;
 
+// A reactor's direct-submission context (one per attached reactor thread, used only by
+// that thread): per GPU, the GETs it accepted this loop iteration and up to kDirectJobs
+// edge-server jobs in flight, each answered from its own host slot and pinned arena.
+struct HbmBackend::Direct {
+  static constexpr int kOffWords = 32;  // >= kServeKeys + 1
+  struct Job {
+    int slot = -1;
+    bool busy = false, answered = false;
+    std::vector<Req> reqs;
+    std::vector<uint32_t> urow;
+    Digest keys[HbmCache::kServeKeys];
+    size_t rows = 0;
+    uint64_t* offs_h = nullptr;
+    uint64_t* offs_d = nullptr;
+    std::shared_ptr<ArenaPool::Arena> arena;
+    uint32_t tnow = 0;
+    double t0 = 0;
+  };
+  struct PerDev {
+    std::vector<Req> pending;
+    Job jobs[kDirectJobs];
+    double avg_row_bytes = 4096;
+  };
+  int idx = 0;
+  Executor* ex = nullptr;  // the attached reactor (null: context free)
+  bool poisoned = false;   // a job never completed: the context is not reused
+  std::vector<PerDev> dev;
+};
+
+namespace {
+// The calling thread's direct context (set by direct_attach on a reactor thread).
+struct DirectTls {
+  HbmBackend* be = nullptr;
+  HbmBackend::Direct* ctx = nullptr;
+};
+thread_local DirectTls tl_direct;
+
+// Record [ItemHeader | u16 klen | key | payload] at base + o (sz bytes, 0 = miss) checked
+// against the request's digest and key; a hit is a ByteRef slice that keeps `owner` alive.
+bool read_hit(const uint8_t* base, uint64_t o, uint64_t sz, const Digest& d,
+              const std::string& key, uint32_t tnow, const std::shared_ptr<const void>& owner,
+              CacheValue* v, bool* mismatch) {
+  if (!sz) return false;
+  ItemHeader h;
+  std::memcpy(&h, base + o, sizeof h);
+  if (h.magic != kItemMagic || h.d0 != d.lo || h.d1 != d.hi) return false;
+  size_t po = 0;
+  const char* val = reinterpret_cast<const char*>(base + o + kItemHeaderBytes);
+  if (!keyed_match(val, h.vlen, key, &po)) {
+    *mismatch = true;  // digest collision
+    return false;
+  }
+  v->flags = h.flags;
+  v->ttl_left = h.expire ? (int64_t)h.expire - (int64_t)tnow : 0;
+  v->data = ByteRef(owner, val + po, h.vlen - po);
+  return true;
+}
+}  // namespace
+
 
 HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     : cfg_(cfg), ring_((int)cfg.devices.size()), epoch_(wall_s()) {
   SH_CHECK(!cfg_.devices.empty() && cfg_.devices.size() <= 64, "HbmBackend needs 1..64 devices");
-  SH_CHECK(cfg_.depth >= 1 && kFlightSlot0 + cfg_.depth <= HbmCache::kHeadSlot,
+  SH_CHECK(cfg_.depth >= 1 && kFlightSlot0 + cfg_.depth <= kDirectSlot0,
            "pipeline depth out of range");
+  static_assert(kDirectSlot0 + kDirectJobs * kDirectMax <= HbmCache::kHeadSlot,
+                "direct host slots overlap the head slot");
+  static_assert(Direct::kOffWords >= HbmCache::kServeKeys + 1, "direct offsets too short");
+  SH_CHECK(cfg_.direct_backlog >= 1, "direct_backlog must be >= 1");
+  wpend_.reset(new std::atomic<uint32_t>[kWpend]);
+  for (size_t i = 0; i < kWpend; ++i) wpend_[i].store(0, std::memory_order_relaxed);
   for (size_t i = 0; i < cfg_.devices.size(); ++i) {
     auto d = std::make_unique<Dev>();
     d->be = this;
@@ -306,6 +402,12 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     }
     d->pool = std::make_shared<ArenaPool>(d->device);
     if (cfg_.arena_bytes) d->pool->reserve((size_t)cfg_.depth + 2, (size_t)cfg_.arena_bytes);
+    if (cfg_.direct && cfg_.edge_server) {
+      // reactors never allocate pinned memory: their arenas and offsets exist up front
+      if (cfg_.direct_arenas > 0 && cfg_.direct_arena_bytes)
+        d->pool->reserve((size_t)cfg_.direct_arenas, (size_t)cfg_.direct_arena_bytes);
+      d->direct_offs.ensure((size_t)kDirectMax * kDirectJobs * Direct::kOffWords * 8);
+    }
     for (int k = 0; k < cfg_.depth; ++k) {
       auto f = std::make_unique<Flight>();
       HB_OK(hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
@@ -325,6 +427,22 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     }
     up_mask_.fetch_or(1ull << i);
     devs_.push_back(std::move(d));
+  }
+  if (cfg_.direct && cfg_.edge_server) {
+    for (int c = 0; c < kDirectMax; ++c) {
+      auto dc = std::make_unique<Direct>();
+      dc->idx = c;
+      dc->dev.resize(devs_.size());
+      for (size_t k = 0; k < devs_.size(); ++k)
+        for (int j = 0; j < kDirectJobs; ++j) {
+          Direct::Job& jb = dc->dev[k].jobs[j];
+          const size_t w = ((size_t)c * kDirectJobs + (size_t)j) * Direct::kOffWords;
+          jb.slot = kDirectSlot0 + c * kDirectJobs + j;
+          jb.offs_h = devs_[k]->direct_offs.host<uint64_t>() + w;
+          jb.offs_d = devs_[k]->direct_offs.dev<uint64_t>() + w;
+        }
+      direct_.push_back(std::move(dc));
+    }
   }
   // Peer access between the shards' GPUs (warm restore copies over xGMI). A pair the
   // runtime cannot map, or every pair under peer_copy = "staged", copies through pinned
@@ -384,6 +502,18 @@ void HbmBackend::enqueue(int k, Req r) {
   if (!dv.spinning.load(std::memory_order_acquire)) dv.cv.notify_one();
 }
 
+void HbmBackend::enqueue_many(int k, std::vector<Req>& rs) {
+  if (rs.empty()) return;
+  Dev& dv = *devs_[k];
+  {
+    std::lock_guard<std::mutex> lk(dv.mu);
+    for (auto& r : rs) dv.q.push_back(std::move(r));  // GETs only: no filter update
+    dv.qn.store(dv.q.size(), std::memory_order_release);
+  }
+  rs.clear();
+  if (!dv.spinning.load(std::memory_order_acquire)) dv.cv.notify_one();
+}
+
 void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
   const int k = route(d);
   if (k < 0) {  // every shard ejected: the request falls through to the origin
@@ -403,6 +533,15 @@ void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetC
   r.key = key;
   r.ex = ex;
   r.gcb = std::move(done);
+  // Reactor-direct: the calling reactor sends it to the edge server itself at the end of
+  // its loop iteration (direct_service), unless a write or flush of this shard it must
+  // stay ordered after has not finished on the GPU yet
+  Direct* dc = tl_direct.be == this ? tl_direct.ctx : nullptr;
+  if (dc && ex == dc->ex && dv.flush_pend.load(std::memory_order_acquire) == 0 &&
+      !writes_pending(d.lo)) {
+    dc->dev[(size_t)k].pending.push_back(std::move(r));
+    return;
+  }
   enqueue(k, std::move(r));
 }
 
@@ -418,6 +557,7 @@ void HbmBackend::set(const std::string& key, const Digest& d, Bytes value, uint3
   r.value = std::move(value);
   r.flags = flags;
   r.ttl = ttl_s;
+  write_begin(d.lo);  // ends when its flight is reaped (or the request is failed)
   enqueue(k, std::move(r));
 }
 
@@ -433,6 +573,7 @@ void HbmBackend::del(const std::string& key, const Digest& d, Executor* ex, DelC
   r.key = key;
   r.ex = ex;
   r.dcb = std::move(done);
+  write_begin(d.lo);
   enqueue(k, std::move(r));
 }
 
@@ -440,6 +581,7 @@ void HbmBackend::flush() {
   for (auto& d : devs_) {
     {
       std::lock_guard<std::mutex> lk(d->mu);
+      if (!d->flush_req) d->flush_pend.fetch_add(1, std::memory_order_acq_rel);
       d->flush_req = true;
       d->ctl_pending.store(true, std::memory_order_release);
     }
@@ -455,8 +597,191 @@ bool HbmBackend::inject_shard_down(int shard, bool down) {
     dv.set_up(false);
     dv.ejections++;
   }
+  {
+    std::lock_guard<std::mutex> lk(dv.mu);
+    dv.kick = true;
+  }
   dv.cv.notify_one();  // the batcher restores the shard (flushing it) when forced_down clears
   return true;
+}
+
+// ---------------------------------------------------------------------------------
+// reactor-direct submission: the reactor is its own batcher for
+// small GET batches — it writes the edge-server job, polls the job's host slot in its
+// loop and answers the requests inline. Replaces the reference's blocking mc.get inside
+// the reactor (src/python/shellac/server/Server.py:335) without blocking.
+// ---------------------------------------------------------------------------------
+void HbmBackend::direct_attach(Executor* ex) {
+  if (!ex || direct_.empty() || tl_direct.be == this) return;
+  std::lock_guard<std::mutex> lk(direct_mu_);
+  for (auto& dc : direct_)
+    if (!dc->ex && !dc->poisoned) {
+      dc->ex = ex;
+      tl_direct = DirectTls{this, dc.get()};
+      return;
+    }
+  // more reactors than contexts: the rest use the batcher
+}
+
+void HbmBackend::direct_submit(Direct& dc, size_t k) {
+  Dev& dv = *devs_[k];
+  Direct::PerDev& pd = dc.dev[k];
+  std::vector<Req>& P = pd.pending;
+  int free_job = -1;
+  for (int j = 0; j < kDirectJobs && free_job < 0; ++j)
+    if (!pd.jobs[j].busy) free_job = j;
+  // distinct digests (at most kServeKeys: a bigger batch is the batcher's)
+  size_t rows = 0;
+  Digest keys[HbmCache::kServeKeys];
+  std::vector<uint32_t> urow(P.size());
+  bool small = true;
+  for (size_t i = 0; i < P.size() && small; ++i) {
+    size_t u = 0;
+    while (u < rows && !(keys[u].lo == P[i].d.lo && keys[u].hi == P[i].d.hi)) ++u;
+    if (u == rows) {
+      if (rows == (size_t)HbmCache::kServeKeys) {
+        small = false;
+        break;
+      }
+      keys[rows++] = P[i].d;
+    }
+    urow[i] = (uint32_t)u;
+  }
+  // both jobs busy with a small batch pending: it goes out when one finishes (a few us)
+  if (small && free_job < 0) return;
+  bool ok = small && dv.up() && dv.flush_pend.load(std::memory_order_acquire) == 0 &&
+            dv.cache->serve_backlog() < (uint64_t)cfg_.direct_backlog;
+  Direct::Job* jb = ok ? &pd.jobs[free_job] : nullptr;
+  if (ok) {
+    jb->arena = dv.pool->try_take((size_t)(pd.avg_row_bytes * 1.5 * (double)rows) + (64u << 10));
+    ok = jb->arena != nullptr;
+  }
+  if (ok) {
+    jb->tnow = now();
+    std::copy(keys, keys + rows, jb->keys);
+    ok = dv.cache->serve_get(jb->keys, (int64_t)rows, jb->arena->d, jb->arena->cap, jb->offs_d,
+                             jb->tnow, jb->slot);
+    if (!ok) jb->arena.reset();
+  }
+  if (!ok) {
+    dv.direct_fallbacks.fetch_add(P.size(), std::memory_order_relaxed);
+    enqueue_many((int)k, P);
+    return;
+  }
+  jb->rows = rows;
+  jb->urow.swap(urow);
+  jb->reqs.swap(P);
+  P.clear();
+  jb->busy = true;
+  jb->answered = false;
+  jb->t0 = wall_s();
+  dv.direct_jobs.fetch_add(1, std::memory_order_relaxed);
+  dv.direct_reqs.fetch_add(jb->reqs.size(), std::memory_order_relaxed);
+  dv.coalesced.fetch_add(jb->reqs.size() - rows, std::memory_order_relaxed);
+}
+
+void HbmBackend::direct_reap(Direct& dc, size_t k, int j) {
+  Dev& dv = *devs_[k];
+  Direct::PerDev& pd = dc.dev[k];
+  Direct::Job& jb = pd.jobs[j];
+  const uint64_t total = dv.cache->host_slot(jb.slot);
+  if (total == HbmCache::kSlotPending) {
+    const double el = wall_s() - jb.t0;
+    // the server may have exited (idle / lifetime) just before taking the job
+    if (el > 20e-6) dv.cache->serve_kick();
+    if (!jb.answered && el * 1e3 > cfg_.batch_timeout_ms) {
+      // stalled: answer misses now; the job (arena, slot) stays reserved until it ends
+      dv.direct_timeouts.fetch_add(1, std::memory_order_relaxed);
+      std::vector<Req> rs;
+      rs.swap(jb.reqs);
+      jb.answered = true;
+      for (auto& r : rs)
+        if (r.gcb) r.gcb(false, CacheValue{});
+    }
+    return;
+  }
+  std::vector<Req> rs;
+  rs.swap(jb.reqs);
+  std::shared_ptr<ArenaPool::Arena> arena = std::move(jb.arena);
+  const bool answered = jb.answered;
+  jb.busy = false;
+  jb.answered = false;
+  if (answered) return;
+  if (total == HbmCache::kSlotFailed) {
+    for (auto& r : rs) r.gcb(false, CacheValue{});
+    return;
+  }
+  if (jb.rows) pd.avg_row_bytes = 0.9 * pd.avg_row_bytes + 0.1 * ((double)total / (double)jb.rows);
+  if (total > arena->cap) {  // the records did not fit (none written): the batcher regathers
+    dv.direct_overflows.fetch_add(1, std::memory_order_relaxed);
+    enqueue_many((int)k, rs);
+    return;
+  }
+  // answers first, callbacks after: a callback may issue GETs of its own (into pending)
+  std::shared_ptr<const void> owner = arena;
+  struct Ans {
+    bool hit;
+    CacheValue v;
+  };
+  std::vector<Ans> ans(rs.size());
+  for (size_t i = 0; i < rs.size(); ++i) {
+    const uint32_t u = jb.urow[i];
+    const uint64_t o = jb.offs_h[u], sz = jb.offs_h[u + 1] - o;
+    bool mismatch = false;
+    ans[i].hit = read_hit(arena->h, o, sz, jb.keys[u], rs[i].key, jb.tnow, owner, &ans[i].v,
+                          &mismatch);
+    if (mismatch) dv.key_mismatch.fetch_add(1, std::memory_order_relaxed);
+  }
+  for (size_t i = 0; i < rs.size(); ++i) {
+    Req& r = rs[i];
+    if (r.ex == dc.ex) r.gcb(ans[i].hit, std::move(ans[i].v));
+    else if (r.ex) {
+      auto cb = std::move(r.gcb);
+      r.ex->post([cb = std::move(cb), a = std::move(ans[i])]() mutable { cb(a.hit, std::move(a.v)); });
+    } else {
+      r.gcb(ans[i].hit, std::move(ans[i].v));
+    }
+  }
+}
+
+bool HbmBackend::direct_service() {
+  Direct* dc = tl_direct.be == this ? tl_direct.ctx : nullptr;
+  if (!dc) return false;
+  bool busy = false;
+  for (size_t k = 0; k < devs_.size(); ++k) {
+    Direct::PerDev& pd = dc->dev[k];
+    for (int j = 0; j < kDirectJobs; ++j)
+      if (pd.jobs[j].busy) direct_reap(*dc, k, j);
+    if (!pd.pending.empty()) direct_submit(*dc, k);
+    for (int j = 0; j < kDirectJobs; ++j) busy |= pd.jobs[j].busy;
+    busy |= !pd.pending.empty();
+  }
+  return busy;
+}
+
+void HbmBackend::direct_detach() {
+  Direct* dc = tl_direct.be == this ? tl_direct.ctx : nullptr;
+  if (!dc) return;
+  for (size_t k = 0; k < devs_.size(); ++k) enqueue_many((int)k, dc->dev[k].pending);
+  const double until = wall_s() + cfg_.batch_timeout_ms * 1e-3 + 1.0;
+  for (;;) {
+    bool busy = false;
+    for (size_t k = 0; k < devs_.size(); ++k)
+      for (int j = 0; j < kDirectJobs; ++j)
+        if (dc->dev[k].jobs[j].busy) {
+          direct_reap(*dc, k, j);
+          busy |= dc->dev[k].jobs[j].busy;
+        }
+    if (!busy) break;
+    if (wall_s() > until) {
+      dc->poisoned = true;  // a job never finished: its arena / slot stay reserved
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  tl_direct = DirectTls{};
+  std::lock_guard<std::mutex> lk(direct_mu_);
+  dc->ex = nullptr;
 }
 
 // ---------------------------------------------------------------------------------
@@ -541,13 +866,20 @@ void HbmBackend::Dev::loop() {
       if (take_batch(&batch, &do_flush, &rebuilding)) {
         worked = true;
         if (!up() || failed) {
-          fail_requests(batch);
+          fail_requests(batch, true);
+          if (do_flush) flush_done();
         } else if (batch.empty()) {
           try {
-            if (do_flush) cache->flush(stream);
+            // finished before anything else may read the shard: edge-server GETs are not
+            // ordered after the stream
+            if (do_flush) {
+              cache->flush(stream);
+              HB_OK(hipStreamSynchronize(stream));
+            }
           } catch (const std::exception& e) {
             std::fprintf(stderr, "[shellac hbm] gpu %d flush failed: %s\n", device, e.what());
           }
+          if (do_flush) flush_done();
         } else {
           Flight& f = *flights[(head + inflight) % flights.size()];
           f.reqs.swap(batch);
@@ -559,7 +891,9 @@ void HbmBackend::Dev::loop() {
             ++inflight;
           } catch (const std::exception& e) {
             std::fprintf(stderr, "[shellac hbm] gpu %d launch failed: %s\n", device, e.what());
-            fail_requests(f.reqs);
+            fail_requests(f.reqs, true);
+            if (do_flush) flush_done();
+            f.flush = false;
             f.reqs.clear();
             f.active = false;
             eject("launch error");
@@ -599,8 +933,11 @@ void HbmBackend::Dev::loop() {
     }
     std::unique_lock<std::mutex> lk(mu);
     if (stop && q.empty()) return;
-    if (!q.empty() || flush_req || filt_want_rebuild) continue;
-    const auto wake = [&] { return stop || !q.empty() || flush_req || filt_want_rebuild; };
+    if (!q.empty() || flush_req || filt_want_rebuild || kick) {
+      kick = false;
+      continue;
+    }
+    const auto wake = [&] { return stop || !q.empty() || flush_req || filt_want_rebuild || kick; };
     const int wait_s = !up() ? 1 : cfg.sweep_interval_s;
     if (wait_s > 0) {
       if (!cv.wait_for(lk, std::chrono::seconds(wait_s), wake) && up() && cfg.sweep_interval_s > 0) {
@@ -804,9 +1141,13 @@ void HbmBackend::Dev::track_writes(const Flight& f, int dir) {
   for (uint64_t k : m.wkeys) {
     auto it = pend_w.find(k);
     if (it != pend_w.end() && --it->second == 0) pend_w.erase(it);
+    be->write_end(k);
   }
   m.wkeys.clear();
-  if (m.flush && pend_flush) --pend_flush;
+  if (m.flush) {
+    if (pend_flush) --pend_flush;
+    flush_done();
+  }
   m.flush = false;
 }
 
@@ -840,23 +1181,9 @@ void HbmBackend::Dev::deliver_gets(Flight& f) {
     const uint32_t u = f.urow[j];
     const uint64_t o = off[u], sz = off[u + 1] - o;
     CacheValue v;
-    bool hit = false;
-    if (sz) {
-      ItemHeader h;
-      std::memcpy(&h, base + o, sizeof h);
-      size_t po = 0;
-      const char* val = reinterpret_cast<const char*>(base + o + kItemHeaderBytes);
-      if (h.magic == kItemMagic && h.d0 == hk[u].lo && h.d1 == hk[u].hi) {
-        if (keyed_match(val, h.vlen, r.key, &po)) {
-          hit = true;
-          v.flags = h.flags;
-          v.ttl_left = h.expire ? (int64_t)h.expire - (int64_t)f.tnow : 0;
-          v.data = ByteRef(owner, val + po, h.vlen - po);
-        } else {
-          key_mismatch.fetch_add(1, std::memory_order_relaxed);  // digest collision
-        }
-      }
-    }
+    bool mismatch = false;
+    const bool hit = read_hit(base, o, sz, hk[u], r.key, f.tnow, owner, &v, &mismatch);
+    if (mismatch) key_mismatch.fetch_add(1, std::memory_order_relaxed);
     auto cb = std::move(r.gcb);
     if (r.ex)
       pg.at(r.ex).push_back([cb = std::move(cb), hit, v = std::move(v)]() { cb(hit, v); });
@@ -871,7 +1198,7 @@ void HbmBackend::Dev::overflow_misses(Flight& f) {
   arena_misses += f.gets.size();
   std::vector<Req> gets;
   for (uint32_t i : f.gets) gets.push_back(std::move(f.reqs[i]));
-  fail_requests(gets);
+  fail_requests(gets, false);
 }
 
 void HbmBackend::Dev::deliver_dels(Flight& f) {
@@ -890,9 +1217,10 @@ void HbmBackend::Dev::deliver_dels(Flight& f) {
   pg.flush();
 }
 
-void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs) {
+void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs, bool unlaunched) {
   PostGroups pg;
   for (auto& r : reqs) {
+    if (unlaunched && r.kind != 0) be->write_end(r.d.lo);
     if (r.kind == 0 && r.gcb) {
       auto cb = std::move(r.gcb);
       if (r.ex) pg.at(r.ex).push_back([cb = std::move(cb)]() { cb(false, CacheValue{}); });
@@ -912,11 +1240,11 @@ void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs) {
 // flight itself stays reserved until the GPU finishes with its buffers.
 void HbmBackend::Dev::fail_flight(Flight& f) {
   failures++;
-  if (!f.got) fail_requests(f.reqs);
+  if (!f.got) fail_requests(f.reqs, false);
   else {
     std::vector<Req> rest;
     for (uint32_t i : f.dels) rest.push_back(std::move(f.reqs[i]));
-    fail_requests(rest);
+    fail_requests(rest, false);
   }
   f.got = true;
   f.gets.clear();
@@ -939,7 +1267,7 @@ void HbmBackend::Dev::eject(const char* why) {
     pending.swap(q);
     qn.store(0, std::memory_order_release);
   }
-  fail_requests(pending);
+  fail_requests(pending, true);
 }
 
 // Bring an ejected shard back: the fault drill was lifted, or retry_s passed and every
@@ -957,6 +1285,8 @@ void HbmBackend::Dev::maybe_restore() {
     return;
   }
   failed = false;
+  for (size_t i = 0; i < inflight; ++i)  // every flight has finished: its writes end
+    track_writes(*flights[(head + i) % flights.size()], -1);
   inflight = 0;
   head = 0;
   pend_w.clear();
@@ -1255,6 +1585,11 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_arena_misses", sum(&Dev::arena_misses));
   out->emplace_back("hbm_served_batches", sum(&Dev::served_batches));
   out->emplace_back("hbm_ordered_get_batches", sum(&Dev::ordered_gets));
+  out->emplace_back("hbm_direct_jobs", sum(&Dev::direct_jobs));
+  out->emplace_back("hbm_direct_requests", sum(&Dev::direct_reqs));
+  out->emplace_back("hbm_direct_fallback_requests", sum(&Dev::direct_fallbacks));
+  out->emplace_back("hbm_direct_overflows", sum(&Dev::direct_overflows));
+  out->emplace_back("hbm_direct_timeouts", sum(&Dev::direct_timeouts));
   uint64_t sl = 0;
   for (auto& d : devs_) sl += d->cache->serve_launches();
   out->emplace_back("hbm_server_launches", sl);

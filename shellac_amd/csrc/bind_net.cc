@@ -198,7 +198,8 @@ void bind_net(py::module_& m) {
                           bool presence_filter, int depth, const std::string& evict,
                           int retry_s, int batch_timeout_ms, bool flush_on_restore,
                           bool warm_restore, const std::string& peer_copy, bool edge_server,
-                          std::vector<int> batcher_cpus, int serve_backlog) {
+                          std::vector<int> batcher_cpus, int serve_backlog, bool direct,
+                          int direct_backlog) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -222,6 +223,9 @@ void bind_net(py::module_& m) {
     c.batcher_cpus = std::move(batcher_cpus);
     SH_CHECK(serve_backlog >= 1, "serve_backlog must be >= 1");
     c.serve_backlog = serve_backlog;
+    SH_CHECK(direct_backlog >= 1, "direct_backlog must be >= 1");
+    c.direct = direct;
+    c.direct_backlog = direct_backlog;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
@@ -231,7 +235,8 @@ void bind_net(py::module_& m) {
      py::arg("retry_s") = 2, py::arg("batch_timeout_ms") = 2000,
      py::arg("flush_on_restore") = true, py::arg("warm_restore") = true,
      py::arg("peer_copy") = "auto", py::arg("edge_server") = true,
-     py::arg("batcher_cpus") = std::vector<int>{}, py::arg("serve_backlog") = 2);
+     py::arg("batcher_cpus") = std::vector<int>{}, py::arg("serve_backlog") = 2,
+     py::arg("direct") = true, py::arg("direct_backlog") = 4);
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);

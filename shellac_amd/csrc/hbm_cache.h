@@ -119,15 +119,16 @@ class HbmCache {
   void serve_kick();
   // server jobs queued or running (the resident workgroup takes them one at a time: a
   // caller with several batches in flight sends the rest down the launched path)
-  uint64_t serve_backlog() const {
+  uint64_t serve_backlog() const {  // any thread (the batcher, reactors submitting directly)
     const uint64_t c = __atomic_load_n(srv_ctl_, __ATOMIC_ACQUIRE);
-    return srv_ticket_ > c ? srv_ticket_ - c : 0;
+    const uint64_t t = __atomic_load_n(&srv_ticket_, __ATOMIC_RELAXED);
+    return t > c ? t - c : 0;
   }
   // wait_host_slot for a serve_get job: spins, relaunching the server when it exited
   uint64_t serve_wait(int done_slot, int64_t timeout_ms = 10000);
   void serve_stop();  // ask the server to exit and wait for it (outstanding jobs stay queued)
   uint64_t serve_launches() const { return srv_launches_; }
-  uint64_t serve_jobs() const { return srv_ticket_; }
+  uint64_t serve_jobs() const { return __atomic_load_n(&srv_ticket_, __ATOMIC_RELAXED); }
   // Phase stamps of the last (up to 64) server jobs, wall-clock ticks of the device:
   // rows of {ticket, poll issued, job seen, probed, copied, publish, n, total bytes}; and the
   // tick rate (kHz).

@@ -3105,7 +3105,7 @@ bool HbmCache::serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint6
   put(2, (uint64_t)(uintptr_t)off);
   put(4, (uint64_t)done_slot);
   put(3, (uint64_t)(uint32_t)n | ((uint64_t)now << 32));
-  ++srv_ticket_;
+  __atomic_store_n(&srv_ticket_, srv_ticket_ + 1, __ATOMIC_RELAXED);  // serve_backlog reads it
   if (!srv_running_ ||
       __atomic_load_n(srv_ctl_ + kCtlExited, __ATOMIC_ACQUIRE) == srv_epoch_)
     serve_launch_locked();

@@ -421,6 +421,11 @@ void Reactor::loop() {
   epoll_event evs[256];
   const double spin_s = cfg_.spin_us * 1e-6;
   double last_work = now_s();
+  // the cache tier may take this thread's GETs directly (HbmBackend: the reactor writes
+  // the edge-server job and polls its completion below, no batcher thread either way)
+  CacheBackend* const be = px_->backend_.get();
+  if (be) be->direct_attach(this);
+  bool direct_busy = false;
   while (px_->running_) {
     const bool spin = spin_s > 0 && now_s() - last_work < spin_s;
     int timeout_ms = 0;
@@ -432,7 +437,7 @@ void Reactor::loop() {
       // sees the other) and block only when it is empty
       spinning_.store(false, std::memory_order_seq_cst);
       std::lock_guard<std::mutex> lk(post_mu_);
-      timeout_ms = posted_.empty() ? 100 : 0;
+      timeout_ms = posted_.empty() && !direct_busy ? 100 : 0;
     }
     const int n = epoll_wait(epfd_, evs, 256, timeout_ms);
     const double t_it = n > 0 ? now_s() : 0;
@@ -467,6 +472,11 @@ void Reactor::loop() {
     {
       const double t0 = now_s();
       drain_posted();
+      // GETs this iteration accepted go to the GPU now; finished ones are answered here
+      if (be) {
+        direct_busy = be->direct_service();
+        if (direct_busy && spin_s > 0) last_work = t0;
+      }
       phase_done(3, t0);
     }
     for (Conn* c : graveyard_) delete c;
@@ -477,6 +487,7 @@ void Reactor::loop() {
       if (us > 10000) loop_slow.fetch_add(1, std::memory_order_relaxed);
     }
   }
+  if (be) be->direct_detach();  // answers (or hands to the batcher) what it still holds
 }
 
 void Reactor::accept_all() {

@@ -55,7 +55,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
                  depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000,
                  edge_server: bool = True, batcher_cpus: Sequence[int] = (),
-                 serve_backlog: int = 2):
+                 serve_backlog: int = 2, direct: bool = True):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -70,7 +70,9 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
     (``clock``: read objects get a second chance, memcached-LRU-like; ``fifo``); a GPU
     whose batch fails or stalls past ``batch_timeout_ms`` is ejected for ``retry_s``.
     ``edge_server`` sends small GET batches to each GPU's resident edge-server kernel
-    (no launch per batch); ``batcher_cpus`` pins the GPU batcher threads.
+    (no launch per batch); ``batcher_cpus`` pins the GPU batcher threads. ``direct``
+    lets each proxy reactor write its own small GET batches to the edge server and poll
+    their completion in its loop (no batcher-thread hop; larger batches still batch).
     ``fault="gpu_down=K"`` ejects GPU shard K as a drill.
     """
     c = core()
@@ -84,14 +86,16 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              promote_ttl=promote_ttl, sweep_s=sweep_s, hbm_filter=hbm_filter,
                              spin_us=spin_us, depth=depth, evict=evict,
                              batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
-                             batcher_cpus=batcher_cpus, serve_backlog=serve_backlog)
+                             batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
+                             direct=direct)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
                           batch_us=batch_us, retry_s=retry_s, sweep_s=sweep_s,
                           hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
                           batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
-                          batcher_cpus=batcher_cpus, serve_backlog=serve_backlog)
+                          batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
+                          direct=direct)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -110,7 +114,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms,
                              edge_server=edge_server,
                              batcher_cpus=[int(x) for x in batcher_cpus],
-                             serve_backlog=int(serve_backlog))
+                             serve_backlog=int(serve_backlog), direct=bool(direct))
     raise ValueError(f"unknown cache backend {kind!r}")
 
 
@@ -265,6 +269,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-edge-server", action="store_true",
                    help="--cache hbm: launch a kernel per GET batch instead of feeding the "
                         "resident edge-server kernel")
+    p.add_argument("--no-hbm-direct", action="store_true",
+                   help="--cache hbm: every GET goes through the GPU batcher thread (default: "
+                        "reactors send small GET batches to the edge server themselves)")
     p.add_argument("--batcher-cpus", default="",
                    help="--cache hbm: pin the GPU batcher threads to these CPUs")
     p.add_argument("--stream-bytes", type=int, default=1 << 20,
@@ -302,6 +309,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                      "hbm_filter": not args.no_hbm_filter, "spin_us": args.hbm_spin_us,
                      "depth": args.hbm_depth, "evict": args.evict,
                      "edge_server": not args.no_edge_server,
+                     "direct": not args.no_hbm_direct,
                      "batcher_cpus": parse_cpus(args.batcher_cpus)}
                     if kind == "hbm" else {}),
                  **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))

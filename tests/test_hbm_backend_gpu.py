@@ -102,6 +102,38 @@ def test_proxy_with_hbm_backend(hbm):
         o.stop()
 
 
+@pytest.mark.parametrize("direct", [True, False])
+def test_proxy_reactor_direct_gets(direct):
+    """Reactor-direct submission: each proxy reactor writes its own edge-server jobs and
+    answers them from its loop. Bodies match the batcher path; a GET right after the miss
+    that stored its key is ordered after that SET (it hits); pipelines with more distinct
+    keys than one server job still go through the batcher."""
+    be = make_backend("hbm", gpus=[0], hbm_gb=0.25, direct=direct)
+    o = Origin(body_bytes=2500).start()
+    try:
+        with Server([("127.0.0.1", o.port)], port=0, backend=be, threads=2) as px:
+            c = HttpClient(port=px.port)
+            paths = [f"/rd/{i}" for i in range(60)]
+            first = []
+            for p in paths:
+                first.append(c.get(p).body().read())
+                assert c.get(p).body().read() == first[-1]  # read-your-write: a hit
+            assert all(o.hits[p] == 1 for p in paths)
+            for _ in range(3):
+                assert [c.get(p).body().read() for p in paths] == first
+            rs = c.pipeline(paths[:40] * 2)
+            assert [r.body().read() for r in rs] == first[:40] * 2
+            assert all(o.hits[p] == 1 for p in paths)
+            st = be.stats()
+            if direct:
+                assert st["hbm_direct_jobs"] > 0 and st["hbm_direct_requests"] >= 180
+                assert st["hbm_direct_timeouts"] == 0 and st["hbm_key_mismatch"] == 0
+            else:
+                assert st["hbm_direct_jobs"] == 0 and st["hbm_direct_requests"] == 0
+    finally:
+        o.stop()
+
+
 def test_proxy_with_tiered_dram_hbm():
     be = make_backend("hbm", gpus=[0], hbm_gb=1.0, batch_us=20, l1_mb=16)
     o = Origin(body_bytes=1000).start()

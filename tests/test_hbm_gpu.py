@@ -433,6 +433,46 @@ def test_routed_step_set_overflow_is_carried_not_lost(cuda_dev, comm_mode):
     assert e.carry_stats()[2] == 0
 
 
+def test_routed_comm_modes_give_identical_results(cuda_dev):
+    """`comm_mode="single"` (every collective of a step on one stream, in issue order) and
+    the default `"channels"` (three communicator channels on their own streams) are the
+    same step: from identical caches, the same GET / SET batches give byte-identical
+    answers every step (hot-replica fan-out included), and the caches end identical."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+    from shellac_amd.parallel.exchange import MirrorComm
+
+    wl = Workload(40000, cuda_dev)
+    caches = {}
+    for mode in ("channels", "single"):
+        sc = ShardedCache(CacheShard(256 << 20, 1 << 16, 1 << 16, cuda_dev), group=MirrorComm(3),
+                          replica=CacheShard(64 << 20, 1 << 12, 1 << 16, cuda_dev),
+                          comm_mode=mode)
+        sc.set(wl.set_batch(torch.arange(0, 40000, device=cuda_dev)))
+        sc.sync_sets()
+        caches[mode] = sc
+    outs = {m: [] for m in caches}
+    for k in range(6):
+        gets = wl.digests.index_select(0, wl.sample_ids(5000, 10 + k)).contiguous()
+        sets = wl.set_batch(wl.uniform_ids(600, 30 + k), version=1 + k % 2)
+        for m, sc in caches.items():
+            r = sc.serve(gets, sets).wait()
+            outs[m].append(unpack_records(r.data, r.off, r.size))
+        if k == 2:  # from here on the hottest keys are also answered from the replica tier
+            for sc in caches.values():
+                sc.refresh_replica(256, gets)
+    for k in range(6):
+        assert outs["channels"][k] == outs["single"][k], k
+        assert sum(x is not None for x in outs["channels"][k]) > 4000
+    allk = wl.digests[:40000].contiguous()
+    final = {}
+    for m, sc in caches.items():
+        sc.sync_sets()
+        r = sc.get(allk)
+        final[m] = unpack_records(r.data, r.off, r.size)
+    assert final["channels"] == final["single"]
+
+
 @pytest.mark.parametrize("n,nb", [(1, 2), (777, 3), (100003, 9), (300000, 65)])
 def test_group_rows_counting_sort(cuda_dev, n, nb):
     """csrc/router.hip counting sort: bucket counts, a permutation, rows moved with it,
