@@ -180,6 +180,8 @@ def main():
                     help="HBM: a kernel launch per GET batch instead of the resident server")
     ap.add_argument("--no-direct", action="store_true",
                     help="HBM: every GET through the batcher thread (no reactor-direct jobs)")
+    ap.add_argument("--serve-blocks", type=int, default=8,
+                    help="HBM: resident edge-server blocks per GPU (jobs served side by side)")
     ap.add_argument("--serve-backlog", type=int, default=2,
                     help="HBM: server jobs that may be ahead of a batch sent to the server")
     ap.add_argument("--layouts", nargs="+", default=None,
@@ -233,7 +235,8 @@ def main():
                                l1_mb=a.l1_mb if a.backend == "tiered" else 0,
                                depth=a.hbm_depth, evict=a.evict,
                                edge_server=not a.no_edge_server, batcher_cpus=batcher_cpus,
-                               serve_backlog=a.serve_backlog, direct=not a.no_direct)
+                               serve_backlog=a.serve_backlog, direct=not a.no_direct,
+                               serve_blocks=a.serve_blocks)
     prefix = "/o/"  # no /gz prefix: the origin sends the incompressible body as is
     out = {"backend": a.backend, "proxy_threads": layouts[0][0], "objects": a.objects,
            "body_bytes": a.body, "zipf": a.zipf, "working_set_MB": a.objects * item / 1e6,
@@ -243,7 +246,7 @@ def main():
            "cpu_count": os.cpu_count(), "cpu_budget": budget,
            "processes": "origin | proxy | load generator",
            "cpus": {"proxy_other": misc_cpus, "origin": or_cpus, "gpu_batcher": batcher_cpus},
-           "edge_server": gpu and not a.no_edge_server, "serve_backlog": a.serve_backlog,
+           "edge_server": gpu and not a.no_edge_server, "serve_backlog": a.serve_backlog, "serve_blocks": a.serve_blocks,
            "reactor_direct": gpu and not a.no_edge_server and not a.no_direct,
            "spin_us": {"reactors": a.rx_spin_us, "load_generator": a.lg_spin_us}}
     px = None

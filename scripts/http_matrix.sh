@@ -1,7 +1,8 @@
 #!/bin/bash
 # HTTP matrix (8M x 4 KiB incompressible, Zipf 0.99, c=10 and c=1000): DRAM-only,
 # HBM-only and tiered, the GPU batcher on a core of its own (8 reactors x 6 load-generator
-# workers), HBM-only also without reactor-direct jobs (every GET through the batcher thread)
+# workers), HBM-only also without reactor-direct jobs (every GET through the batcher thread),
+# with 1 or 4 edge-server blocks instead of 8 (hbm_blk1, hbm_blk4)
 # and without the resident edge server (a launch per GET batch).
 set -o pipefail
 OUT=gpurun_out/${1:-http_matrix}
@@ -18,6 +19,8 @@ for spec in "$@"; do
     dram)   run dram_8M   --backend dram   --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
     hbm)    run hbm_8M    --backend hbm    --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
     hbm_b1) run hbm_8M_backlog1 --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --serve-backlog 1 || exit 1;;
+    hbm_blk1) run hbm_8M_blk1 --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --serve-blocks 1 || exit 1;;
+    hbm_blk4) run hbm_8M_blk4 --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --serve-blocks 4 || exit 1;;
     hbm_nodirect) run hbm_8M_nodirect --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-direct || exit 1;;
     hbm_nosrv) run hbm_8M_nosrv --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-edge-server || exit 1;;
     tiered) run tiered_8M --backend tiered --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;

@@ -174,6 +174,9 @@ struct HbmBackendConfig {
   // one job (~4-9 us) rather than take a launch (~15 us) — c=10 284K vs 252K RPS at 1
   // (profiles/r3_http)
   int serve_backlog = 2;
+  // resident edge-server blocks per GPU (ShardConfig::serve_blocks): jobs of different
+  // submitters are served side by side; serve_backlog counts jobs per block
+  int serve_blocks = 8;
   // CPUs the batcher threads run on (thread i on batcher_cpus[i % size]; empty: unpinned)
   std::vector<int> batcher_cpus;
   // Reactor-direct GETs (CacheBackend::direct_attach): an attached reactor writes its own

@@ -218,6 +218,9 @@ struct HbmBackend::Dev {
   std::thread th;
   // health
   std::atomic<bool> forced_down{false};
+  // back in the ring and still pulling its objects from peers: GETs neither skip on the
+  // presence filter nor bypass the batcher (they queue behind the migration)
+  std::atomic<bool> restoring{false};
   bool failed = false;
   double retry_at = 0;
   // presence filter (this shard's digests)
@@ -251,7 +254,7 @@ struct HbmBackend::Dev {
       key_mismatch{0}, failures{0}, ejections{0}, restores{0}, regathers{0}, arena_misses{0},
       dropped{0}, staged_copies{0}, served_batches{0}, ordered_gets{0},
       migrated{0}, migrate_ns{0}, direct_jobs{0}, direct_reqs{0}, direct_fallbacks{0},
-      direct_overflows{0}, direct_timeouts{0};
+      direct_overflows{0}, direct_timeouts{0}, direct_ns{0};
 
   void loop();
   bool take_batch(std::vector<Req>* out, bool* do_flush, bool* rebuilding);
@@ -379,6 +382,7 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
     sc.max_item = cfg_.max_item + (uint32_t)keyed_size(kMaxKeyedKey, 0);
     sc.device = d->device;
     sc.evict = cfg_.evict;
+    sc.serve_blocks = cfg_.serve_blocks;
     d->cache = std::make_unique<HbmCache>(sc);
     HB_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HB_OK(hipStreamCreateWithFlags(&d->mstream, hipStreamNonBlocking));
@@ -522,7 +526,8 @@ void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetC
     return;
   }
   Dev& dv = *devs_[k];
-  if (cfg_.presence_filter && !std::atomic_load(&dv.filt)->maybe(d)) {
+  const bool restoring = dv.restoring.load(std::memory_order_acquire);
+  if (cfg_.presence_filter && !restoring && !std::atomic_load(&dv.filt)->maybe(d)) {
     dv.filt_skips.fetch_add(1, std::memory_order_relaxed);  // never stored: no GPU batch
     done(false, CacheValue{});
     return;
@@ -537,7 +542,7 @@ void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetC
   // its loop iteration (direct_service), unless a write or flush of this shard it must
   // stay ordered after has not finished on the GPU yet
   Direct* dc = tl_direct.be == this ? tl_direct.ctx : nullptr;
-  if (dc && ex == dc->ex && dv.flush_pend.load(std::memory_order_acquire) == 0 &&
+  if (dc && ex == dc->ex && !restoring && dv.flush_pend.load(std::memory_order_acquire) == 0 &&
       !writes_pending(d.lo)) {
     dc->dev[(size_t)k].pending.push_back(std::move(r));
     return;
@@ -650,7 +655,8 @@ void HbmBackend::direct_submit(Direct& dc, size_t k) {
   // both jobs busy with a small batch pending: it goes out when one finishes (a few us)
   if (small && free_job < 0) return;
   bool ok = small && dv.up() && dv.flush_pend.load(std::memory_order_acquire) == 0 &&
-            dv.cache->serve_backlog() < (uint64_t)cfg_.direct_backlog;
+            dv.cache->serve_backlog() <
+                (uint64_t)cfg_.direct_backlog * (uint64_t)dv.cache->serve_blocks();
   Direct::Job* jb = ok ? &pd.jobs[free_job] : nullptr;
   if (ok) {
     jb->arena = dv.pool->try_take((size_t)(pd.avg_row_bytes * 1.5 * (double)rows) + (64u << 10));
@@ -700,6 +706,7 @@ void HbmBackend::direct_reap(Direct& dc, size_t k, int j) {
     }
     return;
   }
+  dv.direct_ns.fetch_add((uint64_t)((wall_s() - jb.t0) * 1e9), std::memory_order_relaxed);
   std::vector<Req> rs;
   rs.swap(jb.reqs);
   std::shared_ptr<ArenaPool::Arena> arena = std::move(jb.arena);
@@ -1011,7 +1018,8 @@ void HbmBackend::Dev::launch(Flight& f) {
     // many workgroups win (profiles/r3_http: c=1000 with every small batch served 0.95M
     // RPS, launched only 1.13M)
     f.served = be->cfg_.edge_server && !ordered && f.rows <= (size_t)HbmCache::kServeKeys &&
-               cache->serve_backlog() < (uint64_t)be->cfg_.serve_backlog &&
+               cache->serve_backlog() <
+                   (uint64_t)be->cfg_.serve_backlog * (uint64_t)cache->serve_blocks() &&
                cache->serve_get(hk, (int64_t)f.rows, f.arena->d, f.arena->cap,
                                 f.offs.dev<uint64_t>(), f.tnow, f.slot);
     if (f.served) served_batches++;
@@ -1301,6 +1309,7 @@ void HbmBackend::Dev::maybe_restore() {
   // took while it was out are copied back GPU-to-GPU, inserted only where this shard has
   // nothing yet — so a SET that reaches it from now on is never overwritten by an older
   // migrated copy (requests queued meanwhile run after the migration, on this thread).
+  restoring.store(true, std::memory_order_release);
   set_up(true);
   uint64_t moved = 0;
   if (be->cfg_.warm_restore && be->cfg_.flush_on_restore) {
@@ -1314,6 +1323,7 @@ void HbmBackend::Dev::maybe_restore() {
       }
     }
   }
+  restoring.store(false, std::memory_order_release);
   std::fprintf(stderr, "[shellac hbm] gpu %d back in service (%llu objects warmed from peers)\n",
                device, (unsigned long long)moved);
 }
@@ -1590,6 +1600,8 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_direct_fallback_requests", sum(&Dev::direct_fallbacks));
   out->emplace_back("hbm_direct_overflows", sum(&Dev::direct_overflows));
   out->emplace_back("hbm_direct_timeouts", sum(&Dev::direct_timeouts));
+  // submit -> completion seen by the reactor, summed over jobs
+  out->emplace_back("hbm_direct_job_ns_total", sum(&Dev::direct_ns));
   uint64_t sl = 0;
   for (auto& d : devs_) sl += d->cache->serve_launches();
   out->emplace_back("hbm_server_launches", sl);

@@ -74,7 +74,7 @@ PYBIND11_MODULE(_shellac_core, m) {
 
   py::class_<HbmCache>(m, "HbmCache")
       .def(py::init([](uint64_t log_bytes, uint64_t nbuckets, uint32_t max_item, int device,
-                       int evict, uint64_t reinsert_max) {
+                       int evict, uint64_t reinsert_max, int serve_blocks) {
              ShardConfig c;
              c.log_bytes = log_bytes;
              c.nbuckets = nbuckets;
@@ -82,10 +82,13 @@ PYBIND11_MODULE(_shellac_core, m) {
              c.device = device;
              c.evict = evict;
              c.reinsert_max = reinsert_max;
+             c.serve_blocks = serve_blocks;
              return new HbmCache(c);
            }),
            py::arg("log_bytes"), py::arg("nbuckets"), py::arg("max_item"), py::arg("device"),
-           py::arg("evict") = (int)kEvictClock, py::arg("reinsert_max") = 0)
+           py::arg("evict") = (int)kEvictClock, py::arg("reinsert_max") = 0,
+           py::arg("serve_blocks") = 8)
+      .def_property_readonly("serve_blocks", &HbmCache::serve_blocks)
       .def_property_readonly("reinsert_max", &HbmCache::reinsert_max)
       .def("lookup", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t loc, uintptr_t size,
                         uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve, int slot,

@@ -199,7 +199,7 @@ void bind_net(py::module_& m) {
                           int retry_s, int batch_timeout_ms, bool flush_on_restore,
                           bool warm_restore, const std::string& peer_copy, bool edge_server,
                           std::vector<int> batcher_cpus, int serve_backlog, bool direct,
-                          int direct_backlog) {
+                          int direct_backlog, int serve_blocks) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -226,6 +226,8 @@ void bind_net(py::module_& m) {
     SH_CHECK(direct_backlog >= 1, "direct_backlog must be >= 1");
     c.direct = direct;
     c.direct_backlog = direct_backlog;
+    SH_CHECK(serve_blocks >= 1 && serve_blocks <= 8, "serve_blocks must be in 1..8");
+    c.serve_blocks = serve_blocks;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
@@ -236,7 +238,7 @@ void bind_net(py::module_& m) {
      py::arg("flush_on_restore") = true, py::arg("warm_restore") = true,
      py::arg("peer_copy") = "auto", py::arg("edge_server") = true,
      py::arg("batcher_cpus") = std::vector<int>{}, py::arg("serve_backlog") = 2,
-     py::arg("direct") = true, py::arg("direct_backlog") = 4);
+     py::arg("direct") = true, py::arg("direct_backlog") = 4, py::arg("serve_blocks") = 8);
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);

@@ -36,6 +36,7 @@ struct ShardConfig {
   // capacity pressure). kEvictFifo: plain circular log.
   int evict = kEvictClock;
   uint64_t reinsert_max = 0;  // reinsertion budget per SET batch (bytes); 0 = auto
+  int serve_blocks = 8;       // resident edge-server blocks (serve_get jobs side by side)
 };
 
 class HbmCache {
@@ -120,10 +121,15 @@ class HbmCache {
   // server jobs queued or running (the resident workgroup takes them one at a time: a
   // caller with several batches in flight sends the rest down the launched path)
   uint64_t serve_backlog() const {  // any thread (the batcher, reactors submitting directly)
-    const uint64_t c = __atomic_load_n(srv_ctl_, __ATOMIC_ACQUIRE);
+    uint64_t c = 0;
+    for (int b = 0; b < srv_blocks_; ++b)
+      c += __atomic_load_n(srv_ctl_ + kSrvCtlConsumed + 8 * b, __ATOMIC_ACQUIRE);
     const uint64_t t = __atomic_load_n(&srv_ticket_, __ATOMIC_RELAXED);
     return t > c ? t - c : 0;
   }
+  static constexpr int kServeBlocksMax = 8;
+  static constexpr int kSrvCtlConsumed = 24;  // control word of block 0's consumed count
+  int serve_blocks() const { return srv_blocks_; }
   // wait_host_slot for a serve_get job: spins, relaunching the server when it exited
   uint64_t serve_wait(int done_slot, int64_t timeout_ms = 10000);
   void serve_stop();  // ask the server to exit and wait for it (outstanding jobs stay queued)
@@ -261,7 +267,9 @@ class HbmCache {
   // persistent edge-GET server (serve_get): job ring + control words in pinned coherent
   // memory, its own CU-masked stream (a queue of its own: nothing queues behind it)
   void* srv_ring_ = nullptr;
-  uint64_t* srv_ctl_ = nullptr;      // [0] consumed tickets, [8] exited epoch, [16] stop
+  uint64_t* srv_ctl_ = nullptr;      // [8] exited epoch, [16] stop, [24 + 8 b] block b's consumed
+  uint64_t* srv_sync_ = nullptr;     // device: the server blocks' shared idle clock, exit count
+  int srv_blocks_ = 1;
   hipStream_t srv_stream_ = nullptr;
   uint64_t srv_ticket_ = 0, srv_epoch_ = 0, srv_launches_ = 0;
   uint64_t srv_idle_ticks_ = 0, srv_life_ticks_ = 0, srv_khz_ = 0;

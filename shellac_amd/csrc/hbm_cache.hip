@@ -1183,7 +1183,10 @@ struct SrvGranule {
 struct SrvJob {  // one ring slot (1 KiB), host-written
   SrvGranule g[kSrvGranules];
 };
-constexpr int kCtlConsumed = 0, kCtlExited = 8, kCtlStop = 16;  // words, each on its own line
+// control words, each on its own line: the exited epoch, the stop word, then each server
+// block's consumed count (block b at kCtlConsumed + 8 b)
+constexpr int kCtlExited = 8, kCtlStop = 16, kCtlConsumed = HbmCache::kSrvCtlConsumed;
+constexpr int kCtlWords = kCtlConsumed + 8 * HbmCache::kServeBlocksMax;
 // The server exits after this long without a job (the next job relaunches it) and after
 // this long in all (a device-wide synchronisation elsewhere waits at most that long).
 constexpr uint64_t kSrvIdleUs = 1000, kSrvLifeUs = 10000;
@@ -1220,12 +1223,24 @@ __device__ __forceinline__ uint64_t newest_head(const uint64_t* heads) {
   return max(max(agent_load(heads), agent_load(heads + 1)), agent_load(heads + 4));
 }
 
+// Several server blocks (HbmCache::serve_blocks): block b serves the tickets T with
+// T % nblk == b from a ring of its own, so jobs of different submitters (the batcher,
+// each reactor) are served side by side. The blocks leave together: a block stranded
+// alone would keep the others' jobs waiting for the relaunch until it idles. `sync`
+// (device memory, zeroed at launch): [0] the last job's publish tick of any block (idle
+// means all idle), [1] blocks that have exited (the last one out writes the exited
+// epoch), [2] set by the first block that decides to leave (lifetime, idle, stop): every
+// block checks it before each poll.
 __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     const SrvJob* __restrict__ ring, uint64_t* __restrict__ ctl, uint64_t* __restrict__ slots,
     Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ heads, uint64_t cap,
     const uint8_t* __restrict__ log, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ trace, uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks) {
+    uint64_t* __restrict__ trace, uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
+    uint64_t* __restrict__ sync, int nblk) {
   constexpr int K = HbmCache::kServeKeys;
+  const int blk = blockIdx.x;
+  ring += (size_t)blk * HbmCache::kServeRing;
+  uint64_t* const consumed = ctl + kCtlConsumed + 8 * blk;
   __shared__ Digest s_key[K];
   __shared__ uint64_t s_loc[K];      // physical record offset
   __shared__ uint64_t s_lg[K];       // logical record start + 1 (0: miss)
@@ -1237,7 +1252,7 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
   __shared__ unsigned long long s_cnt[3][kSrvBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = tid >> 3, l8 = tid & 7;
   const bool worker = w != kSrvPollWave;
-  uint64_t ticket = sys_load(ctl + kCtlConsumed);
+  uint64_t ticket = sys_load(consumed);  // this block's tickets: T = ticket * nblk + blk
   const uint64_t t_start = (uint64_t)wall_clock64();
   if (tid == 0) s_t[2] = t_start;
   u32x4 pre = u32x4{0u, 0u, 0u, 0u};
@@ -1253,6 +1268,9 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
       int cmd = 1;
       uint64_t t_poll = 0;
       for (;;) {
+        // another block is leaving: leave too (its jobs and ours wait for the relaunch, so
+        // every block goes at once, at most one job apart)
+        if (nblk > 1 && __shfl((int)(lane == 0 && agent_load(sync + 2) != 0), 0)) break;
         u32x4 gv;
         t_poll = (uint64_t)wall_clock64();
         if (have_pre) {
@@ -1276,9 +1294,15 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
           break;
         }
         const uint64_t t = (uint64_t)wall_clock64();
-        const bool quit = lane == 0 && (sys_load(ctl + kCtlStop) || t - s_t[2] > idle_ticks ||
-                                        t - t_start > life_ticks);
-        if (__shfl((int)quit, 0)) break;
+        // (another block's publish may be newer than t: compare, do not subtract)
+        const bool quit =
+            lane == 0 && (sys_load(ctl + kCtlStop) ||
+                          t > max(s_t[2], agent_load(sync)) + idle_ticks || t - t_start > life_ticks);
+        if (__shfl((int)quit, 0)) {
+          if (lane == 0 && nblk > 1)
+            __hip_atomic_store(sync + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
       }
       if (lane == 0) {
@@ -1410,10 +1434,11 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
       __syncthreads();
     }
     const uint64_t t_copied = (uint64_t)wall_clock64();
+    const uint64_t gticket = ticket * (uint64_t)nblk + (uint64_t)blk;
     if (tid == 0) {
       // the job's phase stamps first, so they are in place when the host sees the slot
-      uint64_t* tr = trace + (ticket % kSrvTrace) * 8;
-      tr[0] = ticket;
+      uint64_t* tr = trace + (gticket % kSrvTrace) * 8;
+      tr[0] = gticket;
       tr[1] = s_t[0];
       tr[2] = s_t[1];
       tr[3] = t_probed;
@@ -1424,9 +1449,10 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
       __threadfence_system();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(slots + s_job[4], total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(ctl + kCtlConsumed, ticket + 1, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(consumed, ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       s_t[2] = (uint64_t)wall_clock64();
+      if (nblk > 1)
+        __hip_atomic_fetch_max(sync, s_t[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- counters (off the latency path)
     ops = wave_sum(ops);
@@ -1446,7 +1472,7 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
         t1 += s_cnt[1][k];
         t2 += s_cnt[2][k];
       }
-      CacheCounters* c_ = ctr + (ticket & (kCtrShards - 1));
+      CacheCounters* c_ = ctr + (gticket & (kCtrShards - 1));
       if (t0) atomicAdd(&c_->get_ops, t0);
       if (t1) atomicAdd(&c_->get_hits, t1);
       if (t2) atomicAdd(&c_->get_bytes, t2);
@@ -1455,8 +1481,11 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
     __syncthreads();  // LDS is reused by the next job
   }
   if (tid == 0) {
-    __hip_atomic_store(ctl + kCtlConsumed, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ctl + kCtlExited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(consumed, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t out = __hip_atomic_fetch_add(sync + 1, 1ull, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (out + 1 == (uint64_t)nblk)  // the last block out: every ticket it could take is done
+      __hip_atomic_store(ctl + kCtlExited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -2786,11 +2815,16 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipHostMalloc(&host_slots_, kHostSlots * sizeof(uint64_t),
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(host_slots_, 0, kHostSlots * sizeof(uint64_t));
-  HIP_OK(hipHostMalloc(&srv_ring_, kServeRing * sizeof(SrvJob),
+  SH_CHECK(cfg_.serve_blocks >= 1 && cfg_.serve_blocks <= kServeBlocksMax,
+           "serve_blocks out of range");
+  srv_blocks_ = cfg_.serve_blocks;
+  HIP_OK(hipHostMalloc(&srv_ring_, (size_t)kServeRing * srv_blocks_ * sizeof(SrvJob),
                        hipHostMallocMapped | hipHostMallocCoherent));
-  memset(srv_ring_, 0, kServeRing * sizeof(SrvJob));
-  HIP_OK(hipHostMalloc(&srv_ctl_, 32 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
-  memset(srv_ctl_, 0, 32 * sizeof(uint64_t));
+  memset(srv_ring_, 0, (size_t)kServeRing * srv_blocks_ * sizeof(SrvJob));
+  HIP_OK(hipHostMalloc(&srv_ctl_, kCtlWords * sizeof(uint64_t),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(srv_ctl_, 0, kCtlWords * sizeof(uint64_t));
+  HIP_OK(hipMalloc(&srv_sync_, 64));
   HIP_OK(hipHostMalloc(&srv_trace_, kSrvTrace * 8 * sizeof(uint64_t),
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(srv_trace_, 0, kSrvTrace * 8 * sizeof(uint64_t));
@@ -2830,6 +2864,7 @@ HbmCache::~HbmCache() {
   (void)hipHostFree(srv_ring_);
   (void)hipHostFree(srv_ctl_);
   (void)hipHostFree(srv_trace_);
+  (void)hipFree(srv_sync_);
   (void)hipFree(log_);
   (void)hipFree(index_);
   (void)hipFree(head_);
@@ -3072,9 +3107,11 @@ void HbmCache::serve_launch_locked() {
   HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctl), srv_ctl_, 0));
   HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&slots), host_slots_, 0));
   HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&trace), srv_trace_, 0));
-  hipLaunchKernelGGL(k_edge_server, dim3(1), dim3(kSrvBlock), 0, srv_stream_, ring, ctl, slots,
-                     index_, cfg_.nbuckets - 1, (const uint64_t*)head_, cfg_.log_bytes, log_,
-                     ctr_, trace, srv_epoch_, srv_idle_ticks_, srv_life_ticks_);
+  HIP_OK(hipMemsetAsync(srv_sync_, 0, 64, srv_stream_));
+  hipLaunchKernelGGL(k_edge_server, dim3(srv_blocks_), dim3(kSrvBlock), 0, srv_stream_, ring, ctl,
+                     slots, index_, cfg_.nbuckets - 1, (const uint64_t*)head_, cfg_.log_bytes,
+                     log_, ctr_, trace, srv_epoch_, srv_idle_ticks_, srv_life_ticks_, srv_sync_,
+                     srv_blocks_);
   HIP_OK(hipGetLastError());
   srv_running_ = true;
   ++srv_launches_;
@@ -3085,13 +3122,15 @@ bool HbmCache::serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint6
   if (n < 1 || n > kServeKeys || done_slot < 0 || done_slot >= kHostSlots) return false;
   TraceRange tr("hbm.serve_get");
   std::lock_guard<std::mutex> lk(srv_mu_);
-  const uint64_t consumed = __atomic_load_n(srv_ctl_ + kCtlConsumed, __ATOMIC_ACQUIRE);
-  if (srv_ticket_ - consumed >= (uint64_t)kServeRing) return false;  // ring full
+  // ticket T goes to server block T % blocks, as that block's ticket T / blocks
+  const uint64_t blk = srv_ticket_ % (uint64_t)srv_blocks_, t = srv_ticket_ / (uint64_t)srv_blocks_;
+  const uint64_t consumed = __atomic_load_n(srv_ctl_ + kCtlConsumed + 8 * blk, __ATOMIC_ACQUIRE);
+  if (t - consumed >= (uint64_t)kServeRing) return false;  // that block's ring is full
   __atomic_store_n(host_slots_ + done_slot, kSlotPending, __ATOMIC_RELEASE);
   // every 16-B granule is {value, tag}: the value first, then the tag with a release
   // store, so a granule read whole by the device never pairs a new tag with an old value
-  SrvGranule* jg = static_cast<SrvJob*>(srv_ring_)[srv_ticket_ % kServeRing].g;
-  const uint64_t tag = srv_ticket_ + 1;
+  SrvGranule* jg = static_cast<SrvJob*>(srv_ring_)[blk * kServeRing + t % kServeRing].g;
+  const uint64_t tag = t + 1;
   auto put = [&](int i, uint64_t v) {
     jg[i].v = v;
     __atomic_store_n(&jg[i].tag, tag, __ATOMIC_RELEASE);
@@ -3117,8 +3156,7 @@ void HbmCache::serve_kick() {
   if (srv_running_ && __atomic_load_n(srv_ctl_ + kCtlExited, __ATOMIC_ACQUIRE) != srv_epoch_)
     return;  // running (or launched and about to start)
   srv_running_ = false;
-  if (__atomic_load_n(srv_ctl_ + kCtlConsumed, __ATOMIC_ACQUIRE) < srv_ticket_)
-    serve_launch_locked();
+  if (serve_backlog() > 0) serve_launch_locked();
 }
 
 std::vector<uint64_t> HbmCache::serve_trace() const {

@@ -253,13 +253,14 @@ class CacheShard:
         re-appended instead of overwritten — memcached-LRU-like hit ratios) or "fifo"
         (plain circular log).
       reinsert_max: CLOCK reinsertion budget per SET batch in bytes (0 = auto).
+      serve_blocks: resident edge-server blocks (GPU; ``serve_get`` jobs side by side).
     """
 
     EVICT = {"fifo": 0, "clock": 1}
 
     def __init__(self, log_bytes: int, nbuckets: int, max_item: int = 1 << 20,
                  device: str | torch.device = "cpu", evict: str = "clock",
-                 reinsert_max: int = 0):
+                 reinsert_max: int = 0, serve_blocks: int = 8):
         self.device = torch.device(device)
         self.log_bytes = int(log_bytes)
         self.nbuckets = int(nbuckets)
@@ -272,7 +273,7 @@ class CacheShard:
             self.device = torch.device("cuda", idx)
             reserve_step_streams(self.device)
             self._impl = c.HbmCache(self.log_bytes, self.nbuckets, self.max_item, idx, ev,
-                                    int(reinsert_max))
+                                    int(reinsert_max), int(serve_blocks))
             self.is_gpu = True
         elif self.device.type == "cpu":
             self._impl = c.HostCache(self.log_bytes, self.nbuckets, self.max_item, ev,

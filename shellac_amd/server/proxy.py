@@ -55,7 +55,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
                  depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000,
                  edge_server: bool = True, batcher_cpus: Sequence[int] = (),
-                 serve_backlog: int = 2, direct: bool = True):
+                 serve_backlog: int = 2, direct: bool = True, serve_blocks: int = 8):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -87,7 +87,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              spin_us=spin_us, depth=depth, evict=evict,
                              batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
                              batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
-                             direct=direct)
+                             direct=direct, serve_blocks=serve_blocks)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
@@ -95,7 +95,7 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                           hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
                           batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
                           batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
-                          direct=direct)
+                          direct=direct, serve_blocks=serve_blocks)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -114,7 +114,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              evict=evict, retry_s=retry_s, batch_timeout_ms=batch_timeout_ms,
                              edge_server=edge_server,
                              batcher_cpus=[int(x) for x in batcher_cpus],
-                             serve_backlog=int(serve_backlog), direct=bool(direct))
+                             serve_backlog=int(serve_backlog), direct=bool(direct),
+                             serve_blocks=int(serve_blocks))
     raise ValueError(f"unknown cache backend {kind!r}")
 
 

@@ -626,6 +626,50 @@ def test_serve_get_matches_small_get(cuda_dev, n):
     assert shard.serve_get(big) is None
 
 
+@pytest.mark.parametrize("blocks", [1, 4, 8])
+def test_serve_blocks_answer_concurrent_submitters(cuda_dev, blocks):
+    """Several resident server blocks: ticket T goes to block T % blocks. Eight host
+    threads (the proxy's reactors) submit small jobs with slots of their own, interleaved;
+    every job is answered with its own keys' records, whichever block took it."""
+    import threading
+
+    shard = CacheShard(64 << 20, 1 << 14, 1 << 14, cuda_dev, serve_blocks=blocks)
+    assert shard._impl.serve_blocks == blocks
+    keys = [f"/blk/{i}".encode() for i in range(2000)]
+    vals = [bytes([i % 251 + 1]) * (64 + i * 7 % 4000) for i in range(2000)]
+    shard.set_many(keys, vals)
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(t):
+        out = torch.zeros(1 << 18, dtype=torch.uint8, device=cuda_dev)
+        off = torch.zeros(32, dtype=torch.int64, device=cuda_dev)
+        slot = 20 + t
+        try:
+            for j in range(150):
+                n = 1 + (t + j) % 5
+                ids = [(t * 331 + j * 17 + k * 101) % 2000 for k in range(n)]
+                dh = digest_strings([keys[i] for i in ids], "cpu").contiguous()
+                while not shard._impl.serve_get(dh.data_ptr(), n, out.data_ptr(), out.numel(),
+                                                off.data_ptr(), shard.now(), slot):
+                    pass  # this block's ring is full: retry
+                total = shard._impl.serve_wait(slot, 10000)
+                o, f = out[:total].cpu(), off[:n + 1].cpu()
+                got = unpack_records(o, f[:-1], f[1:] - f[:-1])
+                if [g[0] if g else None for g in got] != [vals[i] for i in ids]:
+                    errors.append((t, j))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    assert shard._impl.serve_jobs == 8 * 150
+
+
 def test_serve_get_relaunches_and_sees_new_sets(cuda_dev):
     """The server exits when idle and the next job relaunches it; a SET chain that ran
     while it was resident (other CUs, no stream order with it) is visible to its next job
