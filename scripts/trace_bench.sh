@@ -11,5 +11,5 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export SHELLAC_TRACE=1
 EXTRA=""
 if [ "${HIP_TRACE:-0}" = 1 ]; then EXTRA="--hip-trace"; fi
-rocprofv3 --marker-trace --kernel-trace $EXTRA --stats --output-format csv -d "$OUT" -o bench -- \
+timeout -k 10 ${TRACE_LIMIT:-300} rocprofv3 --marker-trace --kernel-trace $EXTRA --stats --output-format csv -d "$OUT" -o bench -- \
   python3 bench.py --steps 10 --warmup 2 --no-smoke "$@"
