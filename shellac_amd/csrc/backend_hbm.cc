@@ -19,6 +19,7 @@
 #include <pthread.h>
 
 #include <chrono>
+#include <unordered_set>
 #include <cstdio>
 
 #include "backend.h"
@@ -239,6 +240,7 @@ struct HbmBackend::Dev {
   // digests (lo word) with a SET / DELETE in a flight not yet reaped, and flushes in
   // flight: a GET of such a key takes the stream path, ordered after them
   std::unordered_map<uint64_t, uint32_t> pend_w;
+  std::unordered_set<uint64_t> take_wset;  // take_batch scratch: write digests so far
   uint32_t pend_flush = 0;
   void track_writes(const Flight& f, int dir);
   double avg_row_bytes = 4096;
@@ -813,12 +815,30 @@ bool HbmBackend::Dev::take_batch(std::vector<Req>* out, bool* do_flush, bool* re
     filt_want_rebuild = false;
     *rebuilding = true;
   }
-  if ((int)q.size() <= cfg.max_batch) {
+  // A flight runs its GETs before its SETs / DELETEs, so a GET queued behind a write of
+  // the same key ends the batch: it goes into the next flight, which is ordered after this
+  // one (read-your-writes for a client that re-reads right after a fill; seen as a second
+  // origin fetch in test_proxy_reactor_direct_gets when the reactor's GET reached the queue
+  // before the batcher took the SET)
+  size_t take = std::min(q.size(), (size_t)std::max(cfg.max_batch, 1));
+  {
+    std::unordered_set<uint64_t>& w = take_wset;
+    w.clear();
+    for (size_t i = 0; i < take; ++i) {
+      const Req& r = q[i];
+      if (r.kind != 0) {
+        w.insert(r.d.lo);
+      } else if (!w.empty() && w.count(r.d.lo)) {
+        take = i;
+        break;
+      }
+    }
+  }
+  if (take == q.size()) {
     out->swap(q);
   } else {
-    out->assign(std::make_move_iterator(q.begin()),
-                std::make_move_iterator(q.begin() + cfg.max_batch));
-    q.erase(q.begin(), q.begin() + cfg.max_batch);
+    out->assign(std::make_move_iterator(q.begin()), std::make_move_iterator(q.begin() + take));
+    q.erase(q.begin(), q.begin() + take);
   }
   qn.store(q.size(), std::memory_order_release);
   *do_flush = flush_req;
