@@ -240,12 +240,13 @@ class HbmCache {
   // CLOCK state
   uint64_t* ring_ = nullptr;           // item-start ring (logical locs, kRingSkip holes)
   uint64_t ring_cap_ = 0;
-  unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, consumed
+  unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut
   uint8_t* rc_scratch_ = nullptr;      // staged reinsertions (rmax_ + 64 bytes)
   uint64_t rmax_ = 0;
   int64_t rc_cap_ = 0;
-  uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_hx_ = nullptr, *rc_part_ = nullptr;
-  uint64_t *rc_src_ = nullptr, *rc_len_ = nullptr, *cb_voff_ = nullptr;
+  uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr;
+  uint64_t *cb_voff_ = nullptr;
+  int64_t rc_adv_w_ = 0;  // > 0: the next SET plan's dedupe advances the hand (window w)
   Digest* cb_keys_ = nullptr;
   uint32_t *cb_vlen_ = nullptr, *cb_flags_ = nullptr, *cb_expire_ = nullptr;
   int64_t cb_cap_ = 0;

@@ -1492,27 +1492,6 @@ __global__ __launch_bounds__(kSrvBlock) void k_edge_server(
 // ---------------------------------------------------------------------------------
 // SET
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vlen, int64_t n,
-                                                       unsigned long long* __restrict__ tk,
-                                                       int* __restrict__ tw, uint32_t tmask,
-                                                       uint32_t* __restrict__ slot_of) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock) {
-    if (vlen[i] == kSkipVlen) { slot_of[i] = 0; continue; }
-    const unsigned long long key = keys[i].lo ? keys[i].lo : 1ull;
-    uint32_t s = (uint32_t)fmix64(key) & tmask;
-    for (uint32_t probe = 0; probe <= tmask; ++probe) {
-      const unsigned long long prev = atomicCAS(&tk[s], 0ull, key);
-      if (prev == 0ull || prev == key) {
-        atomicMax(&tw[s], (int)i);
-        slot_of[i] = s;
-        break;
-      }
-      s = (s + 1) & tmask;
-    }
-  }
-}
 
 __global__ __launch_bounds__(kBlock) void k_set_size(const uint32_t* __restrict__ vlen, int64_t n,
                                                      const int* __restrict__ tw,
@@ -2186,17 +2165,30 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 // B + R bytes, R = reinserted bytes of entries [0, c) — does not reach:
 //     loc_c >= head - cap + R_c + B        (entries [0, c) consumed)
 // R is capped by the reinsertion budget `rmax` (hot items past it just age out).
-// Kernels: k_rc_scan (per-entry loc/hot size + block partials), k_rc_cut (exclusive scan
-// of hot bytes, first entry meeting the bound), k_rc_pick (reinsert rows + the batch's
-// own rows into one combined SET batch), k_rc_copy (stage the reinserted records in a
-// scratch buffer: their old bytes lie in the region the combined batch overwrites).
+// Kernels (two launches: the hand is a dependent chain on the SET stream, and a launch
+// queued while the GET lookup holds every CU waits for its workgroups to retire):
+//   k_rc_scan  per window entry: its loc and hot size (h, 0 when not referenced), a block
+//              partial of h, the batch's bytes B; hot entries' rows of the combined batch
+//              are written from the header it read (no second header read), the others as
+//              skip rows, and the batch's own rows are copied behind the window.
+//   k_rc_emit  the exclusive scan of h (block partials of the previous launch + a block
+//              scan) gives each entry its reinsertion offset hx and its cut test
+//                  meets_j = loc_j + cap >= head + B + min(hx_j, rmax)
+//              which is monotone over valid entries (a valid entry's loc grows at least by
+//              the hot bytes of the entries before it), so an entry is consumed iff it does
+//              not meet the bound: the pick needs no grid-wide cut. Picked records are staged
+//              in the scratch buffer (their old bytes lie in the region the combined batch
+//              overwrites) by the workgroup's waves; the first meeting entry is min-reduced
+//              (an atomic, no fence: k_set_dedupe, the next launch on the stream, advances
+//              the hand and resets the control words — a last-workgroup hand-off here needs
+//              an agent-scope release per workgroup, an L2 write-back beside the gather).
 // The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
 // win over a reinsertion of the same key). Host twin: HostCache::reclaim.
 struct RcArgs {
   const uint64_t* ring;
   uint64_t rmask;
   const uint64_t* ring_tail;
-  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first unconsumed, [3] consumed
+  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first meeting entry
   int64_t W;
   const uint64_t* head_ptr;
   uint64_t cap;
@@ -2204,35 +2196,56 @@ struct RcArgs {
   uint64_t rmax;
 };
 
-__global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __restrict__ log,
+// The combined SET batch (rows [0, W) reinsertions, [W, W + n) the batch).
+struct RcBatch {
+  Digest* keys;
+  uint64_t* voff;
+  uint32_t* vlen;
+  uint32_t* flags;
+  uint32_t* expire;
+};
+
+__global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const uint8_t* __restrict__ log,
                                                     const Entry* __restrict__ index, uint64_t mask,
+                                                    const Digest* __restrict__ keys,
+                                                    const uint8_t* __restrict__ values,
+                                                    const uint64_t* __restrict__ val_off,
                                                     const uint32_t* __restrict__ vlen_new,
+                                                    const uint32_t* __restrict__ flags,
+                                                    const uint32_t* __restrict__ expire,
                                                     int64_t n_new, uint32_t max_item,
                                                     uint64_t* __restrict__ rc_loc,
                                                     uint64_t* __restrict__ rc_h,
                                                     uint64_t* __restrict__ part_h) {
   const uint64_t hand = a.ctl[0], rtail = *a.ring_tail, head = *a.head_ptr;
-  // the batch's bytes (upper bound: dedupe losers included)
+  // the batch's own rows behind the window, and its bytes (upper bound: dedupe losers
+  // included)
   unsigned long long best = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_new;
        i += (int64_t)gridDim.x * kBlock) {
     const uint32_t v = vlen_new[i];
     if (v != kSkipVlen && v <= max_item) best += item_bytes(v);
+    const int64_t r = a.W + i;
+    cb.keys[r] = keys[i];
+    cb.voff[r] = (uint64_t)(uintptr_t)values + val_off[i];
+    cb.vlen[r] = v;
+    cb.flags[r] = flags ? flags[i] : 0u;
+    cb.expire[r] = expire ? expire[i] : 0u;
   }
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t avail = rtail - hand;
   uint64_t loc = kRingSkip, h = 0;
+  uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
   if (j < a.W && (uint64_t)j < avail) {
     const uint64_t idx = hand + (uint64_t)j;
     const uint64_t l = rtail - idx <= a.rmask + 1 ? a.ring[idx & a.rmask] : kRingSkip;
     if (l != kRingSkip && head <= l + a.cap) {  // intact (not overwritten yet)
       const uint4* hp = reinterpret_cast<const uint4*>(log + l % a.cap);
-      const uint4 w0 = hp[0], w1 = hp[1];
+      w0 = hp[0];
+      w1 = hp[1];
       if (w1.w == kItemMagic) {
         loc = l;
-        const uint64_t d0 = pack2(w0.x, w0.y), d1 = pack2(w0.z, w0.w);
-        const uint32_t vlen = w1.x;
-        const Digest d{d0, d1};
+        const Digest d{pack2(w0.x, w0.y), pack2(w0.z, w0.w)};
         // the entry pointing at this item: first bucket first, the second only when the
         // first has none (SETs fill the first bucket first, so one 128-B line per window
         // entry usually settles it). A digest match alone does not settle it: a dead entry
@@ -2250,7 +2263,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
               found = true;
               const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
               const uint32_t ex = (uint32_t)(ve >> 32);
-              if (((uint32_t)ve & kRefBit) && (ex == 0 || ex > a.now)) h = item_bytes(vlen);
+              if (((uint32_t)ve & kRefBit) && (ex == 0 || ex > a.now)) h = item_bytes(w1.x);
             }
           }
       }
@@ -2259,6 +2272,13 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
   if (j < a.W) {
     rc_loc[j] = loc;
     rc_h[j] = h;
+    // a hot entry's row from the header just read (k_rc_emit fills in its value pointer
+    // or turns it into a skip row); every other entry is a skip row already
+    cb.keys[j] = h ? Digest{pack2(w0.x, w0.y), pack2(w0.z, w0.w)} : Digest{0, 0};
+    cb.voff[j] = 0;
+    cb.vlen[j] = h ? w1.x : kSkipVlen;
+    cb.flags[j] = h ? w1.y : 0u;
+    cb.expire[j] = h ? w1.z : 0u;
   }
   block_partial(h, part_h);
   // batch bytes: one atomic per block
@@ -2274,17 +2294,23 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, const uint8_t* __r
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rc_cut(RcArgs a, const uint64_t* __restrict__ rc_loc,
-                                                   const uint64_t* __restrict__ rc_h,
-                                                   const uint64_t* __restrict__ part_h,
-                                                   uint64_t* __restrict__ rc_hx) {
+__global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
+                                                    const uint8_t* __restrict__ log,
+                                                    const uint64_t* __restrict__ rc_loc,
+                                                    const uint64_t* __restrict__ rc_h,
+                                                    const uint64_t* __restrict__ part_h,
+                                                    uint8_t* __restrict__ scratch,
+                                                    CacheCounters* __restrict__ ctr) {
   __shared__ unsigned long long s_w[kBlock / 64];
   __shared__ unsigned long long s_pre;
+  __shared__ uint64_t s_src[kBlock], s_dst[kBlock], s_len[kBlock];
+  __shared__ int s_n;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long pre = 0;
   for (unsigned b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += part_h[b];
   pre = wave_sum(pre);
   if (lane == 0) s_w[w] = pre;
+  if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   if (threadIdx.x == 0) s_pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
   __syncthreads();
@@ -2302,98 +2328,85 @@ __global__ __launch_bounds__(kBlock) void k_rc_cut(RcArgs a, const uint64_t* __r
   unsigned long long hx = s_pre + inc - h;
   for (int k = 0; k < w; ++k) hx += s_w[k];
   bool meets = false;
+  unsigned long long nre = 0, bre = 0;
   if (j < a.W) {
-    rc_hx[j] = hx;
     const uint64_t loc = rc_loc[j];
     const uint64_t r = hx < a.rmax ? hx : a.rmax;
     meets = loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r;
+    if (h) {
+      if (!meets && hx + h <= a.rmax) {
+        cb.voff[j] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
+        const int k = atomicAdd(&s_n, 1);
+        s_src[k] = loc % a.cap;
+        s_dst[k] = hx;
+        s_len[k] = h;
+        ++nre;
+        bre += cb.vlen[j];
+      } else {
+        cb.vlen[j] = kSkipVlen;  // consumed past the budget, or not consumed: ages out
+      }
+    }
   }
-  // only the first entry meeting the bound matters: one atomic per wave (its lowest
-  // lane), not one per entry — past the cut every entry meets it, and same-address
-  // atomics serialise
+  // only the first entry meeting the bound matters: one atomic per wave (its lowest lane)
   const unsigned long long mb = __ballot(meets);
   if (mb && lane == __ffsll((long long)mb) - 1) atomicMin(&a.ctl[2], (unsigned long long)j);
-}
-
-__global__ __launch_bounds__(kBlock) void k_rc_pick(
-    RcArgs a, const uint8_t* __restrict__ log, const uint64_t* __restrict__ rc_loc,
-    const uint64_t* __restrict__ rc_h, const uint64_t* __restrict__ rc_hx,
-    const uint8_t* __restrict__ scratch, const Digest* __restrict__ keys,
-    const uint8_t* __restrict__ values, const uint64_t* __restrict__ val_off,
-    const uint32_t* __restrict__ vlen, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ expire, int64_t n_new, Digest* __restrict__ cb_keys,
-    uint64_t* __restrict__ cb_voff, uint32_t* __restrict__ cb_vlen,
-    uint32_t* __restrict__ cb_flags, uint32_t* __restrict__ cb_expire,
-    uint64_t* __restrict__ rc_src, uint64_t* __restrict__ rc_len, CacheCounters* __restrict__ ctr) {
-  const uint64_t avail = *a.ring_tail - a.ctl[0];
-  const uint64_t weff = (uint64_t)a.W < avail ? (uint64_t)a.W : avail;
-  const unsigned long long cut = a.ctl[2];
-  const uint64_t consumed = cut != ~0ull ? cut : weff;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl[3] = consumed;
-  unsigned long long nre = 0, bre = 0;
-  const int64_t rows = a.W + n_new;
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < rows;
-       r += (int64_t)gridDim.x * kBlock) {
-    if (r < a.W) {
-      const uint64_t h = rc_h[r], hx = rc_hx[r];
-      if ((uint64_t)r < consumed && h && hx + h <= a.rmax) {
-        const uint64_t phys = rc_loc[r] % a.cap;
-        const uint4* hp = reinterpret_cast<const uint4*>(log + phys);
-        const uint4 w0 = hp[0], w1 = hp[1];
-        cb_keys[r] = Digest{pack2(w0.x, w0.y), pack2(w0.z, w0.w)};
-        cb_voff[r] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
-        cb_vlen[r] = w1.x;
-        cb_flags[r] = w1.y;
-        cb_expire[r] = w1.z;
-        rc_src[r] = phys;
-        rc_len[r] = h;
-        ++nre;
-        bre += w1.x;
-      } else {
-        cb_keys[r] = Digest{0, 0};
-        cb_voff[r] = 0;
-        cb_vlen[r] = kSkipVlen;
-        cb_flags[r] = 0;
-        cb_expire[r] = 0;
-        rc_len[r] = 0;
-      }
-    } else {
-      const int64_t i = r - a.W;
-      cb_keys[r] = keys[i];
-      cb_voff[r] = (uint64_t)(uintptr_t)values + val_off[i];
-      cb_vlen[r] = vlen[i];
-      cb_flags[r] = flags ? flags[i] : 0u;
-      cb_expire[r] = expire ? expire[i] : 0u;
-    }
+  __syncthreads();
+  // stage the picked records, one wave per record
+  const int np = s_n;
+  for (int k = w; k < np; k += kBlock / 64) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(log + s_src[k]);
+    u32x4* dst = reinterpret_cast<u32x4*>(scratch + s_dst[k]);
+    for (uint64_t c = lane; c < (s_len[k] >> 4); c += 64) dst[c] = __builtin_nontemporal_load(src + c);
   }
   block_count(ctr, nre, &CacheCounters::reinserted, bre, &CacheCounters::reinsert_bytes);
 }
 
-// One wave per reinserted record: copy [header | value | pad] into the scratch buffer at
-// the record's hot-byte prefix. The last kernel of the hand step: advances the hand and
-// resets the per-step control words.
-__global__ __launch_bounds__(kBlock) void k_rc_copy(RcArgs a, const uint8_t* __restrict__ log,
-                                                    const uint64_t* __restrict__ rc_src,
-                                                    const uint64_t* __restrict__ rc_len,
-                                                    const uint64_t* __restrict__ rc_hx,
-                                                    uint8_t* __restrict__ scratch) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    uint64_t hand = a.ctl[0] + a.ctl[3];
-    const uint64_t rtail = *a.ring_tail;
-    if (rtail - hand > a.rmask + 1) hand = rtail - (a.rmask + 1);  // ring lapped the hand
-    a.ctl[0] = hand;
-    a.ctl[1] = 0;
-    a.ctl[2] = ~0ull;
-    a.ctl[3] = 0;
-  }
-  const int lane = threadIdx.x & 63;
-  const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; r < a.W; r += nwaves) {
-    const uint64_t len = rc_len[r];
-    if (!len) continue;
-    const u32x4* src = reinterpret_cast<const u32x4*>(log + rc_src[r]);
-    u32x4* dst = reinterpret_cast<u32x4*>(scratch + rc_hx[r]);
-    for (uint64_t c = lane; c < (len >> 4); c += 64) dst[c] = __builtin_nontemporal_load(src + c);
+// The hand's advance past the consumed entries (k_set_dedupe's block 0, the launch after
+// k_rc_emit): consumed = the first entry meeting the bound (none: the whole window).
+struct RcAdvance {
+  unsigned long long* ctl = nullptr;  // null: this SET batch ran no hand
+  const uint64_t* ring_tail = nullptr;
+  uint64_t rmask = 0;
+  int64_t W = 0;
+};
+
+__device__ __forceinline__ void rc_advance(const RcAdvance& r) {
+  const uint64_t rtail = *r.ring_tail;
+  const uint64_t hand0 = r.ctl[0];
+  const uint64_t avail = rtail - hand0;
+  const uint64_t weff = (uint64_t)r.W < avail ? (uint64_t)r.W : avail;
+  const unsigned long long cut = r.ctl[2];
+  uint64_t hand = hand0 + (cut != ~0ull && cut < weff ? cut : weff);
+  if (rtail - hand > r.rmask + 1) hand = rtail - (r.rmask + 1);  // ring lapped the hand
+  r.ctl[0] = hand;
+  r.ctl[1] = 0;
+  r.ctl[2] = ~0ull;
+  r.ctl[3] = 0;
+}
+
+// SET dedupe (last writer of a digest wins). `adv`: the CLOCK hand step before this batch
+// (k_rc_emit) left its cut in the control words; block 0 advances the hand.
+__global__ __launch_bounds__(kBlock) void k_set_dedupe(const Digest* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vlen, int64_t n,
+                                                       unsigned long long* __restrict__ tk,
+                                                       int* __restrict__ tw, uint32_t tmask,
+                                                       uint32_t* __restrict__ slot_of,
+                                                       RcAdvance adv) {
+  if (adv.ctl && blockIdx.x == 0 && threadIdx.x == 0) rc_advance(adv);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (vlen[i] == kSkipVlen) { slot_of[i] = 0; continue; }
+    const unsigned long long key = keys[i].lo ? keys[i].lo : 1ull;
+    uint32_t s = (uint32_t)fmix64(key) & tmask;
+    for (uint32_t probe = 0; probe <= tmask; ++probe) {
+      const unsigned long long prev = atomicCAS(&tk[s], 0ull, key);
+      if (prev == 0ull || prev == key) {
+        atomicMax(&tw[s], (int)i);
+        slot_of[i] = s;
+        break;
+      }
+      s = (s + 1) & tmask;
+    }
   }
 }
 
@@ -2881,8 +2894,8 @@ HbmCache::~HbmCache() {
   (void)hipFree(set_size_);
   (void)hipFree(set_off_); (void)hipFree(set_claim_); (void)hipFree(set_cnt_);
   (void)hipFree(ring_); (void)hipFree(rc_ctl_); (void)hipFree(rc_scratch_);
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_hx_, (void*)rc_part_, (void*)rc_src_,
-                  (void*)rc_len_, (void*)cb_voff_, (void*)cb_keys_, (void*)cb_vlen_,
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_, (void*)cb_voff_,
+                  (void*)cb_keys_, (void*)cb_vlen_,
                   (void*)cb_flags_, (void*)cb_expire_})
     (void)hipFree(p);
 }
@@ -2899,15 +2912,10 @@ void HbmCache::ensure_rc_ws(int64_t w) {
   int64_t cap = rc_cap_ ? rc_cap_ : 4096;
   while (cap < w) cap *= 2;
   HIP_OK(hipDeviceSynchronize());
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_hx_, (void*)rc_part_, (void*)rc_src_,
-                  (void*)rc_len_})
-    (void)hipFree(p);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) (void)hipFree(p);
   HIP_OK(hipMalloc(&rc_loc_, cap * 8));
   HIP_OK(hipMalloc(&rc_h_, cap * 8));
-  HIP_OK(hipMalloc(&rc_hx_, cap * 8));
   HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
-  HIP_OK(hipMalloc(&rc_src_, cap * 8));
-  HIP_OK(hipMalloc(&rc_len_, cap * 8));
   rc_cap_ = cap;
 }
 
@@ -2926,15 +2934,13 @@ void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const u
                               int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s) {
   RcArgs a{ring_, ring_cap_ - 1, cur_ring_tail(), rc_ctl_, w, cur_head(), cfg_.log_bytes, now, rmax};
   const int g = (int)((w + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, log_, index_, cfg_.nbuckets - 1,
-                     vlen, n, cfg_.max_item, rc_loc_, rc_h_, rc_part_);
-  hipLaunchKernelGGL(k_rc_cut, dim3(g), dim3(kBlock), 0, s, a, rc_loc_, rc_h_, rc_part_, rc_hx_);
-  hipLaunchKernelGGL(k_rc_pick, dim3(grid_for(w + n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, a,
-                     log_, rc_loc_, rc_h_, rc_hx_, rc_scratch_, keys, values, val_off, vlen, flags,
-                     expire, n, cb_keys_, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, rc_src_,
-                     rc_len_, ctr_);
-  hipLaunchKernelGGL(k_rc_copy, dim3(grid_for(w * 64, kBlock, kMaxGrid)), dim3(kBlock), 0, s, a,
-                     log_, rc_src_, rc_len_, rc_hx_, rc_scratch_);
+  const RcBatch cb{cb_keys_, cb_voff_, cb_vlen_, cb_flags_, cb_expire_};
+  hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, cb, log_, index_, cfg_.nbuckets - 1,
+                     keys, values, val_off, vlen, flags, expire, n, cfg_.max_item, rc_loc_, rc_h_,
+                     rc_part_);
+  hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, log_, rc_loc_, rc_h_, rc_part_,
+                     rc_scratch_, ctr_);
+  rc_adv_w_ = w;  // the combined batch's dedupe advances the hand
   HIP_OK(hipGetLastError());
 }
 
@@ -3277,8 +3283,13 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,
                                  hipStream_t s) {
   const int grid = grid_for(n, kBlock, kMaxGrid);
+  RcAdvance adv;
+  if (rc_adv_w_ > 0) {
+    adv = RcAdvance{rc_ctl_, cur_ring_tail(), ring_cap_ - 1, rc_adv_w_};
+    rc_adv_w_ = 0;
+  }
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
-                     (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_);
+                     (unsigned long long*)dd_keys_, dd_win_, dd_mask_, dd_slot_, adv);
   const int sgrid = grid_for(n, kBlock, kMaxGrid);
   uint64_t* part_cnt = ring_ ? part_ + 2 * kMaxGrid : nullptr;
   hipLaunchKernelGGL(k_set_size, dim3(sgrid), dim3(kBlock), 0, s, vlen, n, dd_win_, dd_slot_,
