@@ -86,6 +86,11 @@ def parse():
                          "RCCL communicator (every collective call of the N-GPU step; all keys "
                          "are local, so no interconnect traffic) — a rehearsal, not a scaling "
                          "number")
+    ap.add_argument("--route", choices=["host", "device"], default="host",
+                    help="N>1 ranks: 'host' — requests reach the GPU that owns their key (ketama "
+                         "on the host proxy, as the HTTP path's HbmBackend routes; GPUs exchange "
+                         "no values); 'device' — GPU-resident request batches routed between GPUs "
+                         "by the all-to-all step (RCCL over xGMI)")
     ap.add_argument("--comm-mode", choices=["single", "channels"], default="channels",
                     help="routed step: every collective on one communicator and one stream in "
                          "a fixed order (single), or one communicator per channel (channels)")
@@ -334,6 +339,10 @@ def main():
         group = MirrorComm(sim)
         world = sim
     real_world = 1 if sim else world
+    # N real ranks behind host proxies: each GPU serves the requests for the keys it owns
+    host_route = real_world > 1 and not bounce and args.route == "host"
+    if host_route:
+        args.replicate = 0  # nothing is remote: no replica tier
     if routed1:
         args.replicate = 0  # one rank owns every key: the replica tier is never consulted
     if bounce:
@@ -342,10 +351,10 @@ def main():
         group = BounceComm()
 
     if args.replicate is None:
-        # xGMI is point-to-point: N ranks talk over N-1 links each, so at small N the
-        # links bound the step and a bigger replica (fewer remote GETs, more SET fan-out)
-        # pays; at N=8 the step is compute-bound and the smaller replica is cheaper
-        args.replicate = (4 << 20) if world <= 4 else (2 << 20)
+        # device-routed step: the per-N table (profiles/r4_sweep2, docs/PERF.md) — every
+        # N is link-bound, and 1M replicated objects give the lowest max(compute, link) at
+        # N=2 and N=8 and are within 1 % of it at N=4
+        args.replicate = 1 << 20
     if args.replica_gb is None:
         args.replica_gb = args.replicate * 2048 / (1 << 30)
     total_keys = args.keys_per_gpu * world
@@ -354,8 +363,17 @@ def main():
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
     sim_map = simulated_world_map(wl, sim, dev) if sim else None
+    owner_of = mine = None
+    if host_route:
+        from shellac_amd.ops import routing as R
+        from shellac_amd.parallel.ring import ShardRing
+
+        pts, own = ShardRing(list(range(world)), 160).tensors(dev)
+        owner_of = R.route(wl.digests, pts, own, world)[0].long()
+        mine = torch.nonzero(owner_of == rank).flatten().contiguous()
     nb = 1
-    shard_keys = int(sim_map["mine"].numel()) if sim else args.keys_per_gpu
+    shard_keys = (int(sim_map["mine"].numel()) if sim else
+                  int(mine.numel()) if host_route else args.keys_per_gpu)
     while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
     log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
@@ -368,11 +386,12 @@ def main():
         replica = CacheShard(int(args.replica_gb * (1 << 30)) // 16 * 16, max(rnb, 1024),
                              max_item=1 << 20, device=dev)
     data_group = None
-    if (real_world > 1 or routed1) and not bounce:
+    if (real_world > 1 or routed1) and not bounce and not host_route:
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
-    sc = ShardedCache(shard, group=group, replica=replica, data_group=data_group,
-                      routed=True if routed1 else None, comm_mode=args.comm_mode)
+    sc = ShardedCache(shard, group=None if host_route else group, replica=replica,
+                      data_group=data_group, routed=True if routed1 else None,
+                      comm_mode=args.comm_mode)
     sc.coalesce = not args.no_coalesce
     sc.gather_after_append = args.gather_after_append
     if sim:
@@ -381,9 +400,10 @@ def main():
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
     lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
-    fill_ids = sim_map["mine"] if sim else None  # the simulated rank fills what it owns
-    for s in range(0, shard_keys, chunk) if sim else range(lo, hi, chunk):
-        ids = (fill_ids[s: s + chunk] if sim else
+    # (the simulated rank and a host-routed rank fill what they own)
+    fill_ids = sim_map["mine"] if sim else mine
+    for s in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
+        ids = (fill_ids[s: s + chunk] if fill_ids is not None else
                torch.arange(s, min(s + chunk, hi), device=dev))
         sc.set(wl.set_batch(ids))
     sync()
@@ -395,10 +415,27 @@ def main():
     # distinct pairs by default, so the GET digests alone (16 x 16 MiB) outgrow the 256 MB
     # MALL and each step reads its batch from HBM rather than from the last-level cache
     P = max(1, args.batches)
-    gets = [wl.digests.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
-            for i in range(P)]
     pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
-    sets = [wl.set_batch(pick(args.sets, 5000 + 97 * rank + i)) for i in range(P)]
+    if host_route:
+        # the global request stream restricted to this rank's keys: what the host proxies'
+        # ketama routing hands this GPU
+        def owned(fn, n, seed):
+            out, got, k = [], 0, 0
+            while got < n:
+                c = fn(n * world + 4096, seed * 7919 + k)
+                c = c[owner_of.index_select(0, c) == rank]
+                out.append(c)
+                got += c.numel()
+                k += 1
+            return torch.cat(out)[:n].contiguous()
+
+        get_ids = [owned(wl.sample_ids, args.batch, 1000 + 97 * rank + i) for i in range(P)]
+        set_ids = [owned(pick, args.sets, 5000 + 97 * rank + i) for i in range(P)]
+    else:
+        get_ids = [wl.sample_ids(args.batch, 1000 + 97 * rank + i) for i in range(P)]
+        set_ids = [pick(args.sets, 5000 + 97 * rank + i) for i in range(P)]
+    gets = [wl.digests.index_select(0, g).contiguous() for g in get_ids]
+    sets = [wl.set_batch(x) for x in set_ids]
     gprobe = [None] * P
     if sim:  # what the (mirrored) owners probe and store: keys the simulated rank owns
         pd = sim_map["pdig"]
@@ -513,7 +550,7 @@ def main():
 
         res, last_batch = w["res"], w["last"]
         k = 200
-        ids = wl.sample_ids(args.batch, 1000 + 97 * rank + last_batch)[:k]
+        ids = get_ids[last_batch][:k]
         res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
         if sim:
@@ -711,13 +748,15 @@ def main():
     if args.pressured_gb > 0 and steady_ok and not sim:
         p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
-        p_sc = ShardedCache(p_shard, group=group, replica=replica, data_group=data_group,
-                            routed=True if routed1 else None, comm_mode=args.comm_mode)
+        p_sc = ShardedCache(p_shard, group=None if host_route else group, replica=replica,
+                            data_group=data_group, routed=True if routed1 else None,
+                            comm_mode=args.comm_mode)
         p_sc.coalesce = sc.coalesce
         if replica is not None:
             p_sc._hot, p_sc._hot_dir = sc._hot, None
-        for s0 in range(lo, hi, chunk):
-            p_sc.set(wl.set_batch(torch.arange(s0, min(s0 + chunk, hi), device=dev)))
+        for s0 in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
+            p_sc.set(wl.set_batch(fill_ids[s0: s0 + chunk] if fill_ids is not None else
+                                  torch.arange(s0, min(s0 + chunk, hi), device=dev)))
         p_shard.reserve(max(args.sets * 2, chunk))
         sync()
         if real_world > 1:
@@ -752,6 +791,9 @@ def main():
     value = ops_per_step * args.steps / elapsed
     if world == 1 and not routed1:
         parallelism = "shard1 (one GPU, no routing)"
+    elif host_route:
+        parallelism = (f"shard{world} (host-routed: ketama on the host proxies sends each "
+                       f"request to the GPU owning its key; no GPU-to-GPU value traffic)")
     else:
         parallelism = f"shard{world} (all-to-all routed, {args.comm_mode} communicator mode)"
     out = {
@@ -781,6 +823,8 @@ def main():
             "log_gib_per_shard": args.log_gb,
             "set_dist": args.set_dist,
             "replicated_hot_objects": args.replicate if world > 1 else 0,
+            "routing": ("none" if world == 1 and not sim and not routed1 else
+                        "host" if host_route else "device (all-to-all)"),
         },
         # which cache state the headline steps ran in: "log_wrapped" = the steady state of a
         # full cache (every SET batch runs the CLOCK hand), "log_fresh" = before the first wrap

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -19,13 +21,16 @@ def _free_port():
     return p
 
 
-def test_bench_cpu_rehearsal_world2():
+@pytest.mark.parametrize("route", ["host", "device"])
+def test_bench_cpu_rehearsal_world2(route):
+    """host: each rank serves the requests for the keys it owns (the default); device: the
+    all-to-all routed step over gloo."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--device", "cpu", "--batch", "4096", "--sets", "512", "--keys-per-gpu", "32768",
            "--log-gb", "0.125", "--replicate", "4096", "--replica-gb", "0.03",
-           "--sample-batches", "2", "--check"]
+           "--sample-batches", "2", "--check", "--route", route]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp")
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -37,6 +42,8 @@ def test_bench_cpu_rehearsal_world2():
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
     assert out["config"]["global_batch"] == 2 * (4096 + 512)
     assert out["get_hit_ratio"] == 1.0
+    assert out["config"]["routing"] == ("host" if route == "host" else "device (all-to-all)")
+    assert out["config"]["replicated_hot_objects"] == (0 if route == "host" else 4096)
     assert "0 mismatches" in p.stderr
     assert "check: 0 of 4096 hit records name another key" in p.stderr
 
