@@ -127,6 +127,9 @@ def parse():
                     help="observed requests per rank the replica refresh ranks keys by")
     ap.add_argument("--drift-budget-mb", type=float, default=512.0,
                     help="replica refresh byte budget per epoch and rank (MiB)")
+    ap.add_argument("--event-fence", choices=["device", "none", "system"], default=None,
+                    help="one-GPU step: fence scope of the events ordering its two streams "
+                         "(ShardedCache.event_fence; default: the cache's)")
     ap.add_argument("--gather-after-append", action="store_true",
                     help="one GPU: the GET gather waits for the SET batch's log append")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
@@ -394,6 +397,8 @@ def main():
                       comm_mode=args.comm_mode)
     sc.coalesce = not args.no_coalesce
     sc.gather_after_append = args.gather_after_append
+    if args.event_fence:
+        sc.event_fence = args.event_fence
     if sim:
         sc.probe_of = sim_map["probe_of"]
 

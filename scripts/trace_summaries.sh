@@ -1,8 +1,9 @@
 #!/bin/bash
 # Step timelines and host-wait audits on the box, summarised there (the raw rocprofv3 CSVs of
 # a HIP-API trace outgrow what gpurun copies back): `bash scripts/trace_summaries.sh OUT`.
-# Runs scripts/trace_bench.sh for the N=1 step (wrapped headline), the one-rank RCCL routed
-# step and the simulated 8-rank step (the latter two with HIP_TRACE=1), writes
+# `bash scripts/trace_summaries.sh OUT ["n1 n1fresh routed sim8"]` (N1_HIP=1: HIP API trace
+# for the one-GPU runs too). Runs scripts/trace_bench.sh for the N=1 step (wrapped headline
+# or fresh), the one-rank RCCL routed step and the simulated 8-rank step, writes
 # step_trace_summary.py / host_wait_audit.py output under gpurun_out/OUT/, then deletes the
 # raw traces.
 set -o pipefail
@@ -18,12 +19,22 @@ run() {  # name marker hip_trace bench-args...
   python3 scripts/step_trace_summary.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_summary.txt"
   if [ "$hip" = 1 ]; then
     python3 scripts/host_wait_audit.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_hostwait.txt"
+    python3 scripts/launch_lag.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_launch_lag.txt"
   fi
   rm -rf "gpurun_out/$OUT/raw_$name"
   echo "== $name"; head -3 "$R/${name}_summary.txt"
   [ "$hip" = 1 ] && head -12 "$R/${name}_hostwait.txt"
   return 0
 }
-run n1 hbm.lookup_coalesced 0 --no-uncoalesced --pressured-gb 0 \
-  && run routed serve.plan 1 --routed --no-uncoalesced --no-wrapped \
-  && run sim8 serve.plan 1 --simulate-world 8 --no-uncoalesced --no-wrapped
+WHICH=${2:-"n1 routed sim8"}
+ok=0
+for w in $WHICH; do
+  case $w in
+    n1) run n1 hbm.lookup_coalesced ${N1_HIP:-0} --no-uncoalesced --pressured-gb 0 || ok=1 ;;
+    n1fresh) run n1fresh hbm.lookup_coalesced ${N1_HIP:-0} --no-uncoalesced --pressured-gb 0 --no-wrapped || ok=1 ;;
+    routed) run routed serve.plan 1 --routed --no-uncoalesced --no-wrapped || ok=1 ;;
+    sim8) run sim8 serve.plan 1 --simulate-world 8 --no-uncoalesced --no-wrapped || ok=1 ;;
+  esac
+  [ $ok -ne 0 ] && exit 1
+done
+exit 0

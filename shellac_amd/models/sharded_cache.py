@@ -225,11 +225,14 @@ class ShardedCache:
         # which cost ~30 us per step in k_offsets. Not adopted.)
         # fence scope of the events that order the main and side streams of a step:
         # "system" = torch's events (a system-scope release: L2 write-back + invalidate
-        # at every record); "device" (default) / "none" = StreamEvent with a device-scope
+        # at every record); "device" / "none" (default) = StreamEvent with a device-scope
         # release / no system fence (both streams are on one GPU; nothing on the host reads
-        # what these events order). One box, two rounds: 0.309 / 0.308 ms per step with
-        # "device" vs 0.315 / 0.311 with "system" (profiles/r2_event_fence_ab.log)
-        self.event_fence = "device"
+        # what these events order, and every kernel dispatch carries its own release). One
+        # box, two rounds: 0.309 / 0.308 ms per step with "device" vs 0.315 / 0.311 with
+        # "system" (profiles/r2_event_fence_ab.log); round 4, one box, two rounds each:
+        # wrapped 0.3362 / 0.3363 "device" vs 0.3313 / 0.3304 "none", fresh 0.3008 / 0.3004
+        # vs 0.2953 / 0.2952 (profiles/r4h_fence)
+        self.event_fence = "none"
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
         self._events = {}
