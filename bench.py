@@ -86,11 +86,13 @@ def parse():
                          "RCCL communicator (every collective call of the N-GPU step; all keys "
                          "are local, so no interconnect traffic) — a rehearsal, not a scaling "
                          "number")
-    ap.add_argument("--route", choices=["host", "device"], default="host",
+    ap.add_argument("--route", choices=["host", "device"], default=None,
                     help="N>1 ranks: 'host' — requests reach the GPU that owns their key (ketama "
                          "on the host proxy, as the HTTP path's HbmBackend routes; GPUs exchange "
                          "no values); 'device' — GPU-resident request batches routed between GPUs "
-                         "by the all-to-all step (RCCL over xGMI)")
+                         "by the all-to-all step (RCCL over xGMI). Default: host with real ranks, "
+                         "device with --simulate-world (--simulate-world N --route host: rank "
+                         "0's owner share of the stream on its 1/N of the key space)")
     ap.add_argument("--comm-mode", choices=["single", "channels"], default="channels",
                     help="routed step: every collective on one communicator and one stream in "
                          "a fixed order (single), or one communicator per channel (channels)")
@@ -343,9 +345,12 @@ def main():
         world = sim
     real_world = 1 if sim else world
     # N real ranks behind host proxies: each GPU serves the requests for the keys it owns
-    host_route = real_world > 1 and not bounce and args.route == "host"
+    host_route = ((real_world > 1 and not bounce and (args.route or "host") == "host") or
+                  (sim and args.route == "host"))
+    msim = 0 if host_route else sim  # the mirrored (device-routed) simulation
     if host_route:
         args.replicate = 0  # nothing is remote: no replica tier
+        group = None
     if routed1:
         args.replicate = 0  # one rank owns every key: the replica tier is never consulted
     if bounce:
@@ -362,10 +367,10 @@ def main():
         args.replica_gb = args.replicate * 2048 / (1 << 30)
     total_keys = args.keys_per_gpu * world
     if dev.type == "cuda" and not bounce:
-        check_memory_budget(args, world, sim, dev)
+        check_memory_budget(args, world, msim, dev)
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
-    sim_map = simulated_world_map(wl, sim, dev) if sim else None
+    sim_map = simulated_world_map(wl, sim, dev) if msim else None
     owner_of = mine = None
     if host_route:
         from shellac_amd.ops import routing as R
@@ -375,7 +380,7 @@ def main():
         owner_of = R.route(wl.digests, pts, own, world)[0].long()
         mine = torch.nonzero(owner_of == rank).flatten().contiguous()
     nb = 1
-    shard_keys = (int(sim_map["mine"].numel()) if sim else
+    shard_keys = (int(sim_map["mine"].numel()) if msim else
                   int(mine.numel()) if host_route else args.keys_per_gpu)
     while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
@@ -399,14 +404,14 @@ def main():
     sc.gather_after_append = args.gather_after_append
     if args.event_fence:
         sc.event_fence = args.event_fence
-    if sim:
+    if msim:
         sc.probe_of = sim_map["probe_of"]
 
     # populate: every rank SETs its slice of the key space through the routed path
     chunk = 1 << 18
     lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
     # (the simulated rank and a host-routed rank fill what they own)
-    fill_ids = sim_map["mine"] if sim else mine
+    fill_ids = sim_map["mine"] if msim else mine
     for s in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
         ids = (fill_ids[s: s + chunk] if fill_ids is not None else
                torch.arange(s, min(s + chunk, hi), device=dev))
@@ -442,7 +447,7 @@ def main():
     gets = [wl.digests.index_select(0, g).contiguous() for g in get_ids]
     sets = [wl.set_batch(x) for x in set_ids]
     gprobe = [None] * P
-    if sim:  # what the (mirrored) owners probe and store: keys the simulated rank owns
+    if msim:  # what the (mirrored) owners probe and store: keys the simulated rank owns
         pd = sim_map["pdig"]
         gprobe = [pd.index_select(0, wl.sample_ids(args.batch, 1000 + 97 * rank + i)).contiguous()
                   for i in range(P)]
@@ -558,7 +563,7 @@ def main():
         ids = get_ids[last_batch][:k]
         res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
-        if sim:
+        if msim:
             # the owner holds key f(i) for request i: several requests alias one owner key
             # (and a SET of any of them updates it), so values are informational here
             fmap = sim_map["f"]
@@ -579,7 +584,7 @@ def main():
                          torch.zeros_like(res.off, device=wd))
         w0, w1 = words.index_select(0, at), words.index_select(0, at + 1)
         wrong = hit & ((w0 != keys_last[:, 0]) | (w1 != keys_last[:, 1]))
-        if sim:  # an owner's record names the probe digest (a replica's the request's)
+        if msim:  # an owner's record names the probe digest (a replica's the request's)
             pk = gprobe[last_batch].to(wd)
             wrong &= (w0 != pk[:, 0]) | (w1 != pk[:, 1])
         log(rank, f"[bench] check: {int(wrong.sum())} of {int(hit.sum())} hit records name "
@@ -635,7 +640,7 @@ def main():
             ids_e = [wl.sample_ids(args.batch, 7000 + 97 * rank + 13 * e + i, rank_to_id=order)
                      for i in range(PB)]
             g = [wl.digests.index_select(0, x).contiguous() for x in ids_e]
-            gp = ([sim_map["pdig"].index_select(0, x).contiguous() for x in ids_e] if sim
+            gp = ([sim_map["pdig"].index_select(0, x).contiguous() for x in ids_e] if msim
                   else [None] * PB)
             del ids_e
             ev = torch.cuda.Event()
@@ -750,7 +755,7 @@ def main():
     # secondary: the same under capacity pressure — a shard whose log barely holds the key
     # space, so objects the steps read are re-appended (reinsertions > 0) every step
     pressured = None
-    if args.pressured_gb > 0 and steady_ok and not sim:
+    if args.pressured_gb > 0 and steady_ok and not msim:
         p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
         p_sc = ShardedCache(p_shard, group=None if host_route else group, replica=replica,
@@ -888,9 +893,12 @@ def main():
         out["data"] += "; routed one-rank rehearsal: not the N=1 headline"
     if sim:
         out["metric"] = "cache_ops_per_s_simulated"
-        out["data"] = (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
-                       "locally (no interconnect), keys mapped onto the simulated rank's 1/N "
-                       "of the key space; profiling only, not a scaling result")
+        out["data"] = ((f"single-GPU simulation of rank 0 of {sim} host-routed ranks: its owner "
+                        "share of the Zipf stream on its 1/N of the key space; profiling only, "
+                        "not a scaling result") if host_route else
+                       (f"single-GPU simulation of rank 0 of {sim} ranks: all-to-alls mirrored "
+                        "locally (no interconnect), keys mapped onto the simulated rank's 1/N "
+                        "of the key space; profiling only, not a scaling result"))
         out["n_gpus"] = 1
         out["simulated_world"] = sim
     if rank == 0:

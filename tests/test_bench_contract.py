@@ -89,3 +89,19 @@ def test_bench_more_gpus_than_devices_exits_nonzero():
     assert p.returncode == 2, p.stderr[-2000:]
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert "GPUs on this node" in p.stderr
+
+
+def test_bench_simulated_host_routed_world_cpu():
+    """--simulate-world 4 --route host: rank 0's owner share of the Zipf stream over its
+    1/4 of a 4x key space (one process, no mirrored collectives)."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2",
+                        "--warmup", "1", "--device", "cpu", "--batch", "2048", "--sets", "256",
+                        "--keys-per-gpu", "8192", "--log-gb", "0.125", "--batches", "2",
+                        "--no-uncoalesced", "--simulate-world", "4", "--route", "host",
+                        "--check"], capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["config"]["routing"] == "host" and out["simulated_world"] == 4
+    assert out["config"]["keys_total"] == 4 * 8192
+    assert out["get_hit_ratio"] == 1.0
+    assert "0 mismatches" in p.stderr
