@@ -762,6 +762,8 @@ def main():
                             data_group=data_group, routed=True if routed1 else None,
                             comm_mode=args.comm_mode)
         p_sc.coalesce = sc.coalesce
+        p_sc.event_fence = sc.event_fence
+        p_sc.gather_after_append = sc.gather_after_append
         if replica is not None:
             p_sc._hot, p_sc._hot_dir = sc._hot, None
         for s0 in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
