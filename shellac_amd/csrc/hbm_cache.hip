@@ -2252,20 +2252,23 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
         // keeps its digest, so a key can match in one bucket while its live entry is in the
         // other (stopping there dropped live, referenced items: test_serve_steps_return_
         // ground_truth_records)
+        // Each entry's {loc, vlen, expire} half is one 16-B load, and a bucket's four are
+        // issued together (no insert runs beside the hand: the SET chain is on this stream;
+        // a concurrent lookup only sets reference bits, read either way)
         const uint64_t bs[2] = {bucket1(d, mask), bucket2(d, mask)};
         bool found = false;
-        for (int q = 0; q < 2 && !found; ++q)
+        for (int q = 0; q < 2 && !found; ++q) {
+          uint4 hv[kEntriesPerBucket];
 #pragma unroll
-          for (int k = 0; k < (int)kEntriesPerBucket; ++k) {
-            const Entry* e = index + bs[q] * kEntriesPerBucket + k;
-            const uint64_t el = __hip_atomic_load(&e->loc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (el == l + 1) {
+          for (int k = 0; k < (int)kEntriesPerBucket; ++k)
+            hv[k] = reinterpret_cast<const uint4*>(index + bs[q] * kEntriesPerBucket + k)[1];
+#pragma unroll
+          for (int k = 0; k < (int)kEntriesPerBucket; ++k)
+            if (pack2(hv[k].x, hv[k].y) == l + 1) {
               found = true;
-              const uint64_t ve = *reinterpret_cast<const uint64_t*>(&e->vlen);
-              const uint32_t ex = (uint32_t)(ve >> 32);
-              if (((uint32_t)ve & kRefBit) && (ex == 0 || ex > a.now)) h = item_bytes(w1.x);
+              if ((hv[k].z & kRefBit) && (hv[k].w == 0 || hv[k].w > a.now)) h = item_bytes(w1.x);
             }
-          }
+        }
       }
     }
   }
