@@ -644,6 +644,10 @@ def test_serve_blocks_answer_concurrent_submitters(cuda_dev, blocks):
     def worker(t):
         out = torch.zeros(1 << 18, dtype=torch.uint8, device=cuda_dev)
         off = torch.zeros(32, dtype=torch.int64, device=cuda_dev)
+        # the server is on no stream: the zero fills must land before it writes a job's
+        # answer (a fill still queued behind the first job overwrote it: job 0 came back
+        # empty now and then)
+        torch.cuda.synchronize(cuda_dev)
         slot = 20 + t
         try:
             for j in range(150):
@@ -724,6 +728,7 @@ def test_serve_get_multi_round_jobs_beside_wrapping_sets(cuda_dev):
     dh = da.cpu().contiguous()
     out = torch.zeros(1 << 20, dtype=torch.uint8, device=cuda_dev)
     off = torch.zeros(K + 1, dtype=torch.int64, device=cuda_dev)
+    torch.cuda.synchronize(cuda_dev)  # the zero fills before the (stream-less) server writes
     side = torch.cuda.Stream(device=cuda_dev)
     hits = torn = 0
     for rnd in range(6):
