@@ -61,8 +61,10 @@ class GetResult:
     def wait(self) -> "GetResult":
         """Order the current stream after the reply transfer. A routed ``serve`` returns
         while its reply all-to-all (and the per-request assembly that reads its in-band
-        headers) is still running, so the next step's routing overlaps it; call this
-        before reading ``data``, ``off`` or ``size``."""
+        headers) is still running, so the next step's routing overlaps it; a host-edge
+        ``serve`` returns while the DMA copy of its response into host memory runs (then
+        this blocks the host until it is done); call this before reading ``data``, ``off``
+        or ``size``."""
         if self._pending is not None:
             self._pending.wait()
             self._pending = None
@@ -70,6 +72,17 @@ class GetResult:
 
     def hit_mask(self) -> torch.Tensor:
         return self.size > 0
+
+
+class _HostCopy:
+    """A response still being copied to host memory (host edge): wait() blocks the host
+    until the copy is done."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        self.event.synchronize()
 
 
 @dataclass
@@ -243,6 +256,13 @@ class ShardedCache:
         # responses are gathered straight into pinned host memory, as the proxy's HBM
         # tier does (bench.py --edge host)
         self.host_edge = False
+        # host edge: the gather writes the response into HBM and a DMA engine copies it to
+        # the pinned host buffer (56 GB/s D2H, scripts/pcie_d2h_micro.py) instead of the
+        # gather kernel storing over PCIe itself (~38 GB/s)
+        self.host_edge_dma = True
+        self._dma = [None, None]       # per turn: (staging buffer, copy-done event)
+        self._copy_stream = None
+        self._last_pending = None
         self.gathered_bytes = 0  # response bytes the serving steps produced
         self._stats = {"get_requests": 0, "set_requests": 0, "remote_gets": 0,
                       "replica_hits": 0, "replica_refreshes": 0, "coalesced_gets": 0,
@@ -426,6 +446,13 @@ class ShardedCache:
             data = sh.gather(lk)
             return GetResult(data, lk.off[:n], lk.size[:n])
         side = self._side_stream() if self.overlap_store else None
+        stage = self.host_edge and self.host_edge_dma and keys.device.type == "cpu"
+        if stage:
+            # host edge: the GET digests into HBM by DMA on this stream (the lookup reads
+            # them from HBM instead of across PCIe); the SET batch likewise on the SET
+            # stream, below
+            t = self._stage_turn = 1 - getattr(self, "_stage_turn", 1)
+            keys = self._staged(t, "keys", keys)
         if side is not None:
             # The SET chain runs on a side stream from the start of the step: its CLOCK hand
             # (a full cache), dedupe and sizing run at once — beside the previous step's
@@ -449,7 +476,7 @@ class ShardedCache:
                      batch.expire, now)
             data = self._gather_unsynced(lk)
             expand(first, lk.size, lk.off)
-            return GetResult(data, lk.off[:n], lk.size[:n])
+            return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
         # Safe by construction: the lookup reserved the SET's log bytes, so the gather
         # never reads a region the SET writes, and the gather does not read the index.
         if first is not None:
@@ -459,6 +486,10 @@ class ShardedCache:
         ev.record(main)
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
+            if stage:
+                batch = SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
+                    (batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                     batch.expire))))
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now, index_after=ev, append_after=start, append_done=appended)
         if appended is not None:
@@ -472,8 +503,8 @@ class ShardedCache:
             lk, None if first is None else (first, out_size, out_off, table, cslot))
         self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
         if first is not None:
-            return GetResult(data, out_off, out_size)
-        return GetResult(data, lk.off[:n], lk.size[:n])
+            return GetResult(data, out_off, out_size, self._take_pending())
+        return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
 
     def _event(self, name: str):
         e = self._events.get(name)
@@ -502,11 +533,32 @@ class ShardedCache:
             t = self._co_table = torch.zeros(slots, dtype=torch.int32, device=self.device)
         return t
 
+    def _staged(self, turn: int, name: str, x: Optional[torch.Tensor]):
+        """``x`` (pinned host) copied into a persistent HBM buffer of this turn by DMA on the
+        current stream (which runs everything that reads the buffer, so the copy of turn t
+        two steps later is ordered after those reads)."""
+        if x is None:
+            return None
+        bufs = self._stage_bufs = getattr(self, "_stage_bufs", None) or [{}, {}]
+        b = bufs[turn].get(name)
+        if b is None or b.numel() < x.numel() or b.dtype != x.dtype:
+            b = bufs[turn][name] = torch.empty(max(x.numel(), 1), dtype=x.dtype,
+                                               device=self.device)
+        d = b[: x.numel()].view(x.shape)
+        d.copy_(x, non_blocking=True)
+        return d
+
+    def _take_pending(self):
+        p, self._last_pending = self._last_pending, None
+        return p
+
     def _gather_unsynced(self, lk, expand=None) -> torch.Tensor:
         """Gather a lookup given ``total_slot=0`` without stalling the GPU: the gather
         is queued at once into a buffer sized from earlier steps (the kernel writes
         nothing if the total exceeds it) and the host reads the kernel-written total
         while the gather runs; only an outgrown buffer costs a second gather."""
+        if self.host_edge and self.host_edge_dma and self.device.type == "cuda":
+            return self._gather_dma(lk, expand)
         sh = self.shard
         cap = self._gather_cap
         if cap:
@@ -519,6 +571,49 @@ class ShardedCache:
         self._gather_cap = max(int(total * 1.25), 1 << 20) // 16 * 16
         # (the expand tail ran with the first gather too: it is idempotent)
         return sh.gather(lk, self._out_buffer(max(total, 16)), expand=expand)
+
+    def _gather_dma(self, lk, expand=None) -> torch.Tensor:
+        """Host edge: gather into an HBM staging buffer, then copy [0, total) to the pinned
+        host buffer on a copy stream (a DMA engine; the next step's kernels run beside it).
+        Two turns: the gather of step k+2 waits for the copy of step k out of its staging
+        buffer. The result's ``wait()`` blocks the host until its copy is done."""
+        sh = self.shard
+        main = torch.cuda.current_stream(self.device)
+        k = self._host_turn = 1 - getattr(self, "_host_turn", 1)
+        cap = self._gather_cap or (64 << 20)
+        stg, done = self._dma[k] if self._dma[k] is not None else (None, None)
+        if done is not None:
+            main.wait_event(done)  # that turn's copy has read its staging buffer
+        if stg is None or stg.numel() < cap:
+            stg = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        sh.gather(lk, stg, out_cap=cap, expand=expand)
+        total = sh.host_total(0)
+        self.gathered_bytes += total
+        if total > cap:
+            self._gather_cap = max(int(total * 1.25), 1 << 20) // 16 * 16
+            stg = torch.empty(self._gather_cap, dtype=torch.uint8, device=self.device)
+            sh.gather(lk, stg, out_cap=self._gather_cap, expand=expand)
+        elif not self._gather_cap:
+            self._gather_cap = cap
+        n = max(total, 16)
+        bufs = getattr(self, "_host_out", None) or [None, None]
+        self._host_out = bufs
+        if bufs[k] is None or bufs[k].numel() < n:
+            bufs[k] = torch.empty(max(n, self._gather_cap), dtype=torch.uint8, pin_memory=True)
+        host = bufs[k][:n]
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(device=self.device)
+        cs = self._copy_stream
+        gathered = torch.cuda.Event()
+        gathered.record(main)
+        cs.wait_event(gathered)
+        with torch.cuda.stream(cs):
+            host.copy_(stg[:n], non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(cs)
+        self._dma[k] = (stg, done)
+        self._last_pending = _HostCopy(done)
+        return host
 
     def _out_buffer(self, nbytes: int) -> torch.Tensor:
         if self.host_edge:

@@ -987,3 +987,44 @@ def test_serve_event_fences_return_the_same_records(cuda_dev, fence):
     assert all(v is not None and v[0] == pool[voff[i]: voff[i] + vlen[i]].tobytes()
                for v, i in zip(v2, ids))
     assert int(sc._co_table.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("dma", [True, False])
+def test_host_edge_serve_matches_device_edge(cuda_dev, dma):
+    """Host edge (digests, SET payloads and responses in pinned host memory): the response
+    lands in host memory — by a DMA copy of an HBM staging buffer (host_edge_dma, the
+    default) or by the gather's own stores — and every step returns the same records as
+    the device edge on the same inputs, across the two buffer turns."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+
+    wl = Workload(20000, cuda_dev, min_val=64, max_val=2048, pool_bytes=4 << 20)
+    gets = [wl.digests.index_select(0, wl.sample_ids(3000 + 11 * i, 21 + i)).contiguous()
+            for i in range(4)]
+    sets = [wl.set_batch(wl.uniform_ids(500, 70 + i)) for i in range(4)]
+    runs = []
+    for host in (False, True):
+        sc = ShardedCache(CacheShard(32 << 20, 1 << 14, 1 << 16, cuda_dev))
+        sc.overlap_store = True
+        sc.host_edge, sc.host_edge_dma = host, dma
+        for s0 in range(0, 20000, 4000):
+            sc.set(wl.set_batch(torch.arange(s0, s0 + 4000, device=cuda_dev)))
+        out = []
+        for step in range(6):
+            g, b = gets[step % 4], sets[step % 4]
+            if host:
+                def pin(t):
+                    return None if t is None else t.cpu().pin_memory()
+
+                g = pin(g)
+                b = SetBatch(pin(b.keys), pin(b.values), pin(b.val_off), pin(b.vlen),
+                             pin(b.flags), pin(b.expire))
+            r = sc.serve(g, b).wait()
+            assert r.data.device.type == ("cpu" if host else "cuda")
+            out.append((r.size.cpu().clone(), unpack_records(r.data, r.off, r.size)))
+        torch.cuda.synchronize(cuda_dev)
+        runs.append(out)
+    for (s0, d0), (s1, d1) in zip(*runs):
+        assert torch.equal(s0, s1)
+        assert d0 == d1
+    assert sum(int((s > 0).sum()) for s, _ in runs[1]) > 0
