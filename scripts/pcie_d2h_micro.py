@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""PCIe device-to-host rates on one MI355X: a DMA copy (hipMemcpyAsync of a device buffer
-into pinned host memory, torch's non_blocking copy_) against kernel stores into pinned host
-memory (the bench's --edge host gather writes its response that way), for the response
-sizes of the N=1 step (~300 MB). Also the host-to-device DMA rate. Prints GB/s."""
+"""PCIe DMA rates on one MI355X: hipMemcpyAsync (torch's non_blocking copy_) of an HBM
+buffer into pinned host memory and back, for the response sizes of the N=1 step (64 and
+320 MiB). Prints GB/s. The gather kernel's own stores into pinned memory ran at ~38 GB/s
+(bench.py --edge host, round 3); profiles/r4s_edge_host compares the two in the step."""
 import time
 
 import torch
@@ -26,19 +26,7 @@ def main():
         h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         print(f"{mb} MiB: DMA D2H {rate(lambda: h.copy_(d, non_blocking=True), n):.1f} GB/s, "
               f"DMA H2D {rate(lambda: d.copy_(h, non_blocking=True), n):.1f} GB/s", flush=True)
-        # kernel stores into pinned host memory: a device-side elementwise op whose output
-        # is the mapped host buffer
-        hv = h.view(torch.int64)
-        dv = d.view(torch.int64)
-        mapped = torch.from_numpy(hv.numpy())  # the same pinned pages
-        try:
-            from shellac_amd import core
-            _ = core
-        except Exception:
-            pass
-        print(f"{mb} MiB: kernel stores via the bench's gather: see profiles (38.5 GB/s)",
-              flush=True)
-        del d, h, hv, dv, mapped
+        del d, h
 
 
 if __name__ == "__main__":
