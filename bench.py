@@ -432,6 +432,9 @@ def main():
         def owned(fn, n, seed):
             out, got, k = [], 0, 0
             while got < n:
+                if k > 64:
+                    raise SystemExit(f"[bench] rank {rank} owns too few keys to sample "
+                                     f"{n} requests from (ring imbalance?)")
                 c = fn(n * world + 4096, seed * 7919 + k)
                 c = c[owner_of.index_select(0, c) == rank]
                 out.append(c)
