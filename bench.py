@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import faulthandler
 import json
 import os
 import socket
@@ -290,6 +291,9 @@ def main():
     args = parse()
     maybe_launch(args)
     json_out = _claim_stdout()
+    if os.environ.get("SHELLAC_BENCH_STACKS"):
+        # debugging a hung rank: every rank prints all its threads' stacks every N seconds
+        faulthandler.dump_traceback_later(float(os.environ["SHELLAC_BENCH_STACKS"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -345,15 +349,21 @@ def main():
         world = sim
     real_world = 1 if sim else world
     # N real ranks behind host proxies: each GPU serves the requests for the keys it owns
-    host_route = ((real_world > 1 and not bounce and (args.route or "host") == "host") or
-                  (sim and args.route == "host"))
+    # (a bounce rehearsal keeps the device-routed step unless --route host is given: then
+    # every rank is a host-routed GPU server sharing cuda:0, its barriers and reductions
+    # over gloo — the real N>1 default's flow, rehearsed on one GPU)
+    host_route = ((real_world > 1 and (args.route or ("device" if bounce else "host")) == "host")
+                  or (sim and args.route == "host"))
     msim = 0 if host_route else sim  # the mirrored (device-routed) simulation
     if host_route:
+        from shellac_amd.parallel.exchange import LocalComm
+
         args.replicate = 0  # nothing is remote: no replica tier
-        group = None
+        # the rank's cache never routes (group=None would mean the world group here)
+        group = LocalComm()
     if routed1:
         args.replicate = 0  # one rank owns every key: the replica tier is never consulted
-    if bounce:
+    if bounce and not host_route:
         from shellac_amd.parallel.exchange import BounceComm
 
         group = BounceComm()
@@ -397,9 +407,11 @@ def main():
     if (real_world > 1 or routed1) and not bounce and not host_route:
         # second communicator: the value all-to-all of step i overlaps step i+1's exchanges
         data_group = dist.new_group(ranks=list(range(real_world)))
-    sc = ShardedCache(shard, group=None if host_route else group, replica=replica,
+    sc = ShardedCache(shard, group=group, replica=replica,
                       data_group=data_group, routed=True if routed1 else None,
                       comm_mode=args.comm_mode)
+    if host_route and (sc.world, sc.routed) != (1, False):
+        raise SystemExit("[bench] a host-routed rank's cache must serve only its own keys")
     sc.coalesce = not args.no_coalesce
     sc.gather_after_append = args.gather_after_append
     if args.event_fence:
@@ -761,7 +773,7 @@ def main():
     if args.pressured_gb > 0 and steady_ok and not msim:
         p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
-        p_sc = ShardedCache(p_shard, group=None if host_route else group, replica=replica,
+        p_sc = ShardedCache(p_shard, group=group, replica=replica,
                             data_group=data_group, routed=True if routed1 else None,
                             comm_mode=args.comm_mode)
         p_sc.coalesce = sc.coalesce

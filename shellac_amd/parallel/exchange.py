@@ -42,13 +42,23 @@ class BounceComm:
         self.rank, self.world = dist.get_rank(pg), dist.get_world_size(pg)
 
 
+class LocalComm:
+    """The group of a rank that serves only the keys it owns: a host-routed process of an
+    N-GPU job (ketama runs on the host proxies), or any process that has a
+    default process group for other work. World 1, every collective an identity; without
+    it ``group=None`` would mean the default (world) group once torch.distributed is up,
+    and the cache would route its batches over it."""
+
+    rank, world = 0, 1
+
+
 class _Done:
     def wait(self):
         return True
 
 
 def dist_info(group=None) -> tuple[int, int]:
-    if isinstance(group, (MirrorComm, BounceComm)):
+    if isinstance(group, (MirrorComm, BounceComm, LocalComm)):
         return group.rank, group.world
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(group), dist.get_world_size(group)
@@ -58,7 +68,7 @@ def dist_info(group=None) -> tuple[int, int]:
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, output_split_sizes=None,
                       input_split_sizes=None, group=None, async_op: bool = False):
     """torch.distributed.all_to_all_single (RCCL on ROCm) or the mirror stand-in."""
-    if isinstance(group, MirrorComm):
+    if isinstance(group, (MirrorComm, LocalComm)):
         if out.numel() != inp.numel():
             raise ValueError("mirror all_to_all needs symmetric splits")
         out.copy_(inp.view(out.shape) if out.shape != inp.shape else inp)
@@ -114,6 +124,9 @@ def all_gather_rows(out: torch.Tensor, row: torch.Tensor, group=None, peer_block
     (the current stream waits for it). ``peer_blocks``: the row starts with that many
     blocks of one entry per peer (used only to mirror rows under ``MirrorComm``)."""
     rank, world = dist_info(group)
+    if isinstance(group, LocalComm):
+        out.copy_(row)
+        return
     if isinstance(group, MirrorComm):
         torch.index_select(row, 0, _mirror_index(row.numel(), world, rank, peer_blocks,
                                                  row.device), out=out)
@@ -131,7 +144,7 @@ def all_gather_rows(out: torch.Tensor, row: torch.Tensor, group=None, peer_block
 
 
 def all_gather(tensors: list, t: torch.Tensor, group=None) -> None:
-    if isinstance(group, MirrorComm):
+    if isinstance(group, (MirrorComm, LocalComm)):
         for x in tensors:
             x.copy_(t)
         return
@@ -146,6 +159,8 @@ def all_gather(tensors: list, t: torch.Tensor, group=None) -> None:
 
 def all_reduce(t: torch.Tensor, op=None, group=None) -> None:
     op = dist.ReduceOp.SUM if op is None else op
+    if isinstance(group, LocalComm):
+        return
     if isinstance(group, MirrorComm):
         if op == dist.ReduceOp.SUM:
             t.mul_(group.world)
@@ -161,7 +176,7 @@ def all_reduce(t: torch.Tensor, op=None, group=None) -> None:
 def barrier(group=None) -> None:
     if isinstance(group, BounceComm):
         dist.barrier(group=group.pg)
-    elif not isinstance(group, MirrorComm):
+    elif not isinstance(group, (MirrorComm, LocalComm)):
         dist.barrier(group=group)
 
 
@@ -280,7 +295,7 @@ def step_comm(group, device: torch.device):
     a non-RCCL backend, a CPU shard)."""
     from .._native import core
 
-    if device.type != "cuda":
+    if device.type != "cuda" or isinstance(group, LocalComm):
         return None
     c = core()
     if isinstance(group, MirrorComm):

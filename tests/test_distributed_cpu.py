@@ -401,3 +401,46 @@ def _migrate_worker(rank, world, port, q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_incremental_ring_migration_gloo(world):
     _run_world(_migrate_worker, world)
+
+
+def _local_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from shellac_amd.models.sharded_cache import SetBatch, ShardedCache
+        from shellac_amd.ops.cache import CacheShard, digest_strings, pack_values, unpack_records
+        from shellac_amd.parallel.exchange import LocalComm
+
+        # a host-routed rank: its cache serves the keys the host sent it and never takes
+        # part in a collective, so ranks may make different numbers of calls
+        sc = ShardedCache(CacheShard(1 << 22, 1 << 12, 1 << 14, "cpu"), group=LocalComm())
+        assert (sc.world, sc.routed) == (1, False)
+        n_batches = 1 + 2 * rank
+        for b in range(n_batches):
+            keys = [f"/r{rank}/{b}/{i}".encode() for i in range(50)]
+            v, vo, vl = pack_values([k * 2 for k in keys])
+            sc.set(SetBatch(digest_strings(keys), v, vo, vl))
+        mine = [f"/r{rank}/{b}/{i}".encode() for b in range(n_batches) for i in range(50)]
+        other = [f"/r{(rank + 1) % world}/0/{i}".encode() for i in range(50)]
+        res = sc.get(digest_strings(mine + other))
+        recs = unpack_records(res.data, res.off, res.size)
+        assert [r[0] for r in recs[: len(mine)]] == [k * 2 for k in mine]
+        assert all(r is None for r in recs[len(mine):])  # another rank's keys stay there
+        assert sc.counters()["get_ops"] == len(mine) + len(other)  # this shard only
+        dist.barrier()
+        q.put((rank, "ok", None))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_local_group_never_routes_gloo():
+    """A host-routed rank (bench.py --route host) holds a default process group for the
+    barriers and reductions around its steps; its cache must not route over it. With
+    group=None it would (the default group), and ranks that made different numbers of
+    SET calls deadlocked in the first count exchange (seen on a 2-rank GPU rehearsal)."""
+    _run_world(_local_worker, 2, timeout=120)
