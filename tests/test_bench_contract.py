@@ -105,3 +105,24 @@ def test_bench_simulated_host_routed_world_cpu():
     assert out["config"]["keys_total"] == 4 * 8192
     assert out["get_hit_ratio"] == 1.0
     assert "0 mismatches" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_host_routed_ranks_on_one_gpu():
+    """The N>1 default's flow (host-routed ranks, barriers and reductions between steps,
+    per-rank shard populate of different sizes) with two processes sharing the box's GPU
+    over gloo: one JSON line, --check clean. (The flow once deadlocked in populate: each
+    rank's cache routed over the default group.)"""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--bounce", "--route", "host", "--check", "--steps", "3", "--warmup",
+                        "1", "--no-uncoalesced"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp",
+                       env={**os.environ, "SHELLAC_BENCH_STACKS": "60"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["config"]["routing"] == "host" and out["n_gpus"] == 2
+    assert out["get_hit_ratio"] == 1.0
+    assert "check: 0 mismatches in 200 sampled GETs" in p.stderr
+    assert " 0 of " in p.stderr and "hit records name another key" in p.stderr
