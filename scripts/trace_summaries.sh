@@ -1,7 +1,7 @@
 #!/bin/bash
 # Step timelines and host-wait audits on the box, summarised there (the raw rocprofv3 CSVs of
 # a HIP-API trace outgrow what gpurun copies back): `bash scripts/trace_summaries.sh OUT`.
-# `bash scripts/trace_summaries.sh OUT ["n1 n1fresh routed sim8"]` (N1_HIP=1: HIP API trace
+# `bash scripts/trace_summaries.sh OUT ["n1 n1fresh pressured routed sim8"]` (N1_HIP=1: HIP API trace
 # for the one-GPU runs too). Runs scripts/trace_bench.sh for the N=1 step (wrapped headline
 # or fresh), the one-rank RCCL routed step and the simulated 8-rank step, writes
 # step_trace_summary.py / host_wait_audit.py output under gpurun_out/OUT/, then deletes the
@@ -31,6 +31,7 @@ ok=0
 for w in $WHICH; do
   case $w in
     n1) run n1 hbm.lookup_coalesced ${N1_HIP:-0} --no-uncoalesced --pressured-gb 0 || ok=1 ;;
+    pressured) run pressured hbm.lookup_coalesced ${N1_HIP:-0} --no-uncoalesced --pressured-gb 0 --log-gb 5 || ok=1 ;;
     n1fresh) run n1fresh hbm.lookup_coalesced ${N1_HIP:-0} --no-uncoalesced --pressured-gb 0 --no-wrapped || ok=1 ;;
     routed) run routed serve.plan 1 --routed --no-uncoalesced --no-wrapped || ok=1 ;;
     sim8) run sim8 serve.plan 1 --simulate-world 8 --no-uncoalesced --no-wrapped || ok=1 ;;
