@@ -499,15 +499,8 @@ def main():
     if ready is not None:
         ready.record()
 
-    prio = (torch.cuda.Stream(device=dev, priority=int(os.environ["SHELLAC_MAIN_PRIO"]))
-            if os.environ.get("SHELLAC_MAIN_PRIO") and dev.type == "cuda" else None)
-
     def serve_i(cache, i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
-        if prio is not None:
-            with torch.cuda.stream(prio):
-                return cache.serve(gets[i % P], sets[i % P], inputs_ready=ready,
-                                   probe_keys=gprobe[i % P])
         return cache.serve(gets[i % P], sets[i % P], inputs_ready=ready, probe_keys=gprobe[i % P])
 
     def step(i):
