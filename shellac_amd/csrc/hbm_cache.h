@@ -170,7 +170,7 @@ class HbmCache {
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
              uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
              bool allow_reclaim = true, hipEvent_t append_after = nullptr,
-             hipEvent_t append_done = nullptr);
+             hipEvent_t append_done = nullptr, int phase = 0);
   // Whether a SET of `bytes_bound` bytes issued now would run the CLOCK hand (the log is
   // within a few batches of wrapping); the answer can only turn true later.
   bool would_reclaim(uint64_t bytes_bound) const {
@@ -246,7 +246,10 @@ class HbmCache {
   int64_t rc_cap_ = 0;
   uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr;
   uint64_t *cb_voff_ = nullptr;
-  int64_t rc_adv_w_ = 0;  // > 0: the next SET plan's dedupe advances the hand (window w)
+  int64_t rc_adv_w_ = 0;
+  // store(phase=1) queued the CLOCK hand of a batch of hand_n_ rows with a window of hand_w_
+  // (0: none); store(phase=2) runs that combined batch's chain
+  int64_t hand_w_ = 0, hand_n_ = 0;  // > 0: the next SET plan's dedupe advances the hand (window w)
   Digest* cb_keys_ = nullptr;
   uint32_t *cb_vlen_ = nullptr, *cb_flags_ = nullptr, *cb_expire_ = nullptr;
   int64_t cb_cap_ = 0;

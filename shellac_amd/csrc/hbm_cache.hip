@@ -3256,15 +3256,29 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
                      hipEvent_t index_after, bool allow_reclaim, hipEvent_t append_after,
-                     hipEvent_t append_done) {
+                     hipEvent_t append_done, int phase) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
            "SET batch larger than half the log; split the batch");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
+  // phase 2: the rest of a batch whose CLOCK hand a phase-1 call queued
+  if (phase == 2 && hand_w_ > 0) {
+    SH_CHECK(hand_n_ == n, "store phase 2 of a different batch than phase 1");
+    const int64_t w = hand_w_;
+    hand_w_ = 0;
+    store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
+                 index_after, append_after, append_done);
+    hsel_ ^= 1;
+    return;
+  }
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
+  if (phase == 1 && !(allow_reclaim && rmax && should_reclaim(bytes_bound))) {
+    hand_w_ = 0;  // no hand for this batch: phase 2 runs the plain chain
+    return;
+  }
   if (allow_reclaim && rmax && should_reclaim(bytes_bound)) {
     const int64_t w = hand_window(n);
     ensure_rc_ws(w);
@@ -3284,6 +3298,11 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     }
     ensure_set_ws(w + n, s);
     reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
+    if (phase == 1) {  // the chain follows in phase 2
+      hand_w_ = w;
+      hand_n_ = n;
+      return;
+    }
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
                  index_after, append_after, append_done);

@@ -248,6 +248,10 @@ class ShardedCache:
         self.event_fence = "none"
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
+        # one GPU: the SET batch's CLOCK hand is queued before the lookup, which waits for
+        # it (see serve); False queues the whole SET chain after the lookup
+        self.hand_first = os.environ.get("SHELLAC_HAND_FIRST", "1") == "1"
+        self._side_pending = False
         self._events = {}
         self._side = None
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
@@ -286,6 +290,10 @@ class ShardedCache:
         main-shard store may still be running on the executor's store stream). Every
         other ShardedCache method calls it; call it before using ``self.shard`` directly
         after a routed ``serve`` (a device synchronisation also does)."""
+        if self._side_pending:
+            # the last one-GPU serve's SET chain (hand_first leaves it for the next step)
+            self._xwait(torch.cuda.current_stream(self.device), self._side, "end")
+            self._side_pending = False
         e = self._engine
         if e is not None and e.sets_pending:
             e.join_sets(torch.cuda.current_stream(self.device).cuda_stream)
@@ -447,6 +455,7 @@ class ShardedCache:
             return GetResult(data, lk.off[:n], lk.size[:n])
         side = self._side_stream() if self.overlap_store else None
         stage = self.host_edge and self.host_edge_dma and keys.device.type == "cpu"
+        stage_set = stage
         if stage:
             # host edge: the GET digests into HBM by DMA on this stream (the lookup reads
             # them from HBM instead of across PCIe); the SET batch likewise on the SET
@@ -461,9 +470,25 @@ class ShardedCache:
             # that gather is done, overlapping the coalescing and the probe; only its index
             # insert waits for the probe (event), then runs under the bandwidth-bound gather.
             main = torch.cuda.current_stream(self.device)
+            now = sh.now() if now is None else now
+            if self.hand_first:
+                # The CLOCK hand first (a full cache), and the lookup after it: queued beside
+                # the lookup, the hand's workgroups waited for the lookup's to retire, and the
+                # log append behind it then ran beside the gather (the pressured step). This
+                # wait also joins the previous step's SET chain (the hand follows it on the
+                # SET stream), which the end of the previous serve left pending.
+                with torch.cuda.stream(side):
+                    if stage:
+                        batch = SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
+                            (batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                             batch.expire))))
+                        stage_set = False
+                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                             batch.expire, now, phase=1)
+                self._xwait(main, side, "hand")
+                self._side_pending = False
             start = self._event("start")
             start.record(main)                # the previous step's gather is done with the log
-            now = sh.now() if now is None else now
         if self.coalesce:
             table = self._coalesce_table(n) if side is not None else None
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
@@ -486,12 +511,13 @@ class ShardedCache:
         ev.record(main)
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
-            if stage:
+            if stage and stage_set:
                 batch = SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
                     (batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire))))
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                     batch.expire, now, index_after=ev, append_after=start, append_done=appended)
+                     batch.expire, now, index_after=ev, append_after=start, append_done=appended,
+                     phase=2 if self.hand_first else 0)
         if appended is not None:
             # the gather runs after the log append, not beside it: the two byte movers
             # contending for HBM are slower together than one after the other
@@ -501,7 +527,11 @@ class ShardedCache:
         # step's lookup to wait for but the SET chain)
         data = self._gather_unsynced(
             lk, None if first is None else (first, out_size, out_off, table, cslot))
-        self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
+        if self.hand_first:
+            # joined by the next serve's hand wait, or by sync_sets (every other method)
+            self._side_pending = True
+        else:
+            self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
         if first is not None:
             return GetResult(data, out_off, out_size, self._take_pending())
         return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
