@@ -921,7 +921,19 @@ def test_set_index_resets_over_dead_entries_lose_nothing(cuda_dev):
     assert len(hits) > 900
 
 
-def _serve_steps_vs_truth(sc, wl, dev, steps=4, nget=100000):
+def _compact(b):
+    """The SetBatch with its values gathered into a buffer of their own (its bytes, not
+    the workload's whole pool, bound the log bytes the SET may append)."""
+    import dataclasses
+
+    vl = b.vlen.long()
+    off = torch.cumsum(vl, 0) - vl
+    src = torch.repeat_interleave(b.val_off - off, vl) + torch.arange(int(vl.sum()),
+                                                                      device=vl.device)
+    return dataclasses.replace(b, values=b.values[src].contiguous(), val_off=off.contiguous())
+
+
+def _serve_steps_vs_truth(sc, wl, dev, steps=4, nget=100000, compact=False):
     """serve() steps of Zipf GETs over a filled cache; per step the number of requests
     that got a value other than the workload's ground truth, and of misses."""
     pool = wl.pool.cpu().numpy()  # ground truth on the host once (not one copy per request)
@@ -934,7 +946,8 @@ def _serve_steps_vs_truth(sc, wl, dev, steps=4, nget=100000):
     for step in range(steps):
         ids = wl.sample_ids(nget, 11 + step)
         keys = wl.digests.index_select(0, ids).contiguous()
-        r = sc.serve(keys, wl.set_batch(wl.uniform_ids(4096, 21 + step)))
+        b = wl.set_batch(wl.uniform_ids(4096, 21 + step))
+        r = sc.serve(keys, _compact(b) if compact else b)
         torch.cuda.synchronize()
         recs = unpack_records(r.data, r.off, r.size)
         wrong = [(k, i) for k, (i, x) in enumerate(zip(ids.tolist(), recs))
@@ -958,6 +971,40 @@ def test_serve_steps_return_ground_truth_records(cuda_dev):
         sc.set(wl.set_batch(torch.arange(s0, s0 + 10000, device=cuda_dev)))
     res = _serve_steps_vs_truth(sc, wl, cuda_dev)
     assert all(w == 0 and m == 0 for w, m, _, _ in res), res
+
+
+@pytest.mark.parametrize("hand_first", [True, False])
+def test_serve_wrapped_log_ground_truth_both_hand_schedules(cuda_dev, hand_first):
+    """A log the key space overfills, so every serve step runs the CLOCK hand: with the
+    hand queued before the lookup (hand_first, the default) and after it, every request that
+    hits gets its ground-truth record, the hand reinserts, and a later get() (which joins
+    the pending SET chain) agrees with the last serve."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    wl = Workload(100000, cuda_dev)  # ~100 MB of records into a 96 MiB log
+    shard = CacheShard(96 << 20, 1 << 16, 1 << 13, cuda_dev)
+    sc = ShardedCache(shard)
+    sc.hand_first = hand_first
+    for s0 in range(0, 100000, 5000):
+        sc.set(_compact(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
+    c0 = sc.counters()
+    res = _serve_steps_vs_truth(sc, wl, cuda_dev, steps=6, nget=50000, compact=True)
+    assert all(w == 0 for w, _, _, _ in res), res
+    assert sum(m for _, m, _, _ in res) < 6 * 50000 // 2, res
+    assert sc.counters()["reinserted"] > c0["reinserted"]
+    ids = wl.sample_ids(20000, 99)
+    keys = wl.digests.index_select(0, ids).contiguous()
+    r = sc.serve(keys, _compact(wl.set_batch(wl.uniform_ids(4096, 98))))
+    g = sc.get(keys)  # no device sync in between: get() joins the serve's SET chain
+    torch.cuda.synchronize()
+    a = unpack_records(r.data, r.off, r.size)
+    b = unpack_records(g.data, g.off, g.size)
+    pool, voff, vlen = wl.pool.cpu().numpy(), wl.val_off.cpu().tolist(), wl.vlen.cpu().tolist()
+    for i, x, y in zip(ids.tolist(), a, b):
+        t = pool[voff[i]: voff[i] + vlen[i]].tobytes()
+        assert x is None or x[0] == t
+        assert y is None or y[0] == t
 
 
 @pytest.mark.parametrize("fence", ["system", "device", "none"])
