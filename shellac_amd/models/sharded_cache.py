@@ -463,12 +463,11 @@ class ShardedCache:
             t = self._stage_turn = 1 - getattr(self, "_stage_turn", 1)
             keys = self._staged(t, "keys", keys)
         if side is not None:
-            # The SET chain runs on a side stream from the start of the step: its CLOCK hand
-            # (a full cache), dedupe and sizing run at once — beside the previous step's
-            # gather, which may still read the log region this append overwrites — its log
-            # append (bytes the lookup reserves, so this step's gather never reads them) once
-            # that gather is done, overlapping the coalescing and the probe; only its index
-            # insert waits for the probe (event), then runs under the bandwidth-bound gather.
+            # The SET chain runs on a side stream: its CLOCK hand (a full cache) first, which
+            # the lookup waits for (hand_first), then dedupe and sizing beside the lookup, its
+            # log append (bytes the lookup reserves, so this step's gather never reads them)
+            # once the previous step's gather is done with the region it overwrites; only its
+            # index insert waits for the probe (event), then runs under the gather.
             main = torch.cuda.current_stream(self.device)
             now = sh.now() if now is None else now
             if self.hand_first:
@@ -489,13 +488,23 @@ class ShardedCache:
                 self._side_pending = False
             start = self._event("start")
             start.record(main)                # the previous step's gather is done with the log
-        if self.coalesce:
-            table = self._coalesce_table(n) if side is not None else None
-            lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
-                                                   table=table)
-        else:
-            lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound, total_slot=0),
-                                       None, None, None)
+        try:
+            if self.coalesce:
+                table = self._coalesce_table(n) if side is not None else None
+                lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound,
+                                                       total_slot=0, table=table)
+            else:
+                lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound,
+                                                     total_slot=0), None, None, None)
+        except BaseException:
+            if side is not None and self.hand_first:
+                # a queued hand's batch still runs its chain (the native store pairs phase 1
+                # with the next phase 2)
+                with torch.cuda.stream(side):
+                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                             batch.expire, now, phase=2)
+                self._side_pending = True
+            raise
         if side is None:
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now)
