@@ -135,6 +135,10 @@ def parse():
                          "(ShardedCache.event_fence; default: the cache's)")
     ap.add_argument("--gather-after-append", action="store_true",
                     help="one GPU: the GET gather waits for the SET batch's log append")
+    ap.add_argument("--hand", choices=["early", "inline"], default="early",
+                    help="one GPU, full cache: the CLOCK hand detached on a stream of its own, "
+                         "beside the previous step's SET chain, its reinsertions indexed as "
+                         "moves (early), or at the head of the SET chain (inline)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
 
@@ -409,7 +413,7 @@ def main():
         data_group = dist.new_group(ranks=list(range(real_world)))
     sc = ShardedCache(shard, group=group, replica=replica,
                       data_group=data_group, routed=True if routed1 else None,
-                      comm_mode=args.comm_mode)
+                      comm_mode=args.comm_mode, hand=args.hand)
     if host_route and (sc.world, sc.routed) != (1, False):
         raise SystemExit("[bench] a host-routed rank's cache must serve only its own keys")
     sc.coalesce = not args.no_coalesce
@@ -775,7 +779,7 @@ def main():
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
         p_sc = ShardedCache(p_shard, group=group, replica=replica,
                             data_group=data_group, routed=True if routed1 else None,
-                            comm_mode=args.comm_mode)
+                            comm_mode=args.comm_mode, hand=args.hand)
         p_sc.coalesce = sc.coalesce
         p_sc.event_fence = sc.event_fence
         p_sc.gather_after_append = sc.gather_after_append

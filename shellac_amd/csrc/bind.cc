@@ -38,6 +38,7 @@ py::dict counters_dict(const CacheCounters& c) {
   d["get_coalesced"] = c.get_coalesced;
   d["reinserted"] = c.reinserted;
   d["reinsert_bytes"] = c.reinsert_bytes;
+  d["reinsert_lost"] = c.reinsert_lost;
   return d;
 }
 
@@ -171,17 +172,19 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("store", [](HbmCache& c, uintptr_t keys, uintptr_t values, uintptr_t val_off,
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after,
-                       uintptr_t append_after, uintptr_t append_done, int phase) {
+                       uintptr_t append_after, uintptr_t append_done, int phase,
+                       uintptr_t plan_done) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
                 bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), true,
                 reinterpret_cast<hipEvent_t>(append_after),
-                reinterpret_cast<hipEvent_t>(append_done), phase);
+                reinterpret_cast<hipEvent_t>(append_done), phase,
+                reinterpret_cast<hipEvent_t>(plan_done));
       }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
          py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
          py::arg("stream"), py::arg("index_after") = 0, py::arg("append_after") = 0,
-         py::arg("append_done") = 0, py::arg("phase") = 0)
+         py::arg("append_done") = 0, py::arg("phase") = 0, py::arg("plan_done") = 0)
       .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
                         uintptr_t s) {
         py::gil_scoped_release nogil;

@@ -166,11 +166,22 @@ class HbmCache {
   // hand, the dedupe and the sizing (reads only) run at once — beside a gather that
   // still reads the region the append will overwrite. `append_done`: recorded right after
   // the log append (a caller can keep its gather from contending with it).
+  // `phase` 1 queues only the batch's CLOCK hand, 2 the rest of its chain (0: both).
+  // A phase-1 hand is *detached*: it may run as soon as the previous batch's planning is
+  // done (`plan_done` of that batch's phase 2), beside that batch's log append and index
+  // insert. It reads the head the previous append will reach (the claim word) and the ring
+  // tail of the batch before (the last one whose ring entries are written), and its
+  // reinsertions are indexed as *moves*: a reinsertion row's insert CASes the entry from
+  // the item's old location to the new one, and is dropped when the entry has moved on
+  // (a SET or DELETE of the key landed after the hand read the index) — so an early hand
+  // can never resurrect a superseded or deleted value. Two hand buffers alternate, so the
+  // hand of batch k+1 never writes what batch k's append still reads.
+  // `plan_done`: recorded after the batch's planning kernels (dedupe, sizes, offsets).
   void store(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
              const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire, int64_t n,
              uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
              bool allow_reclaim = true, hipEvent_t append_after = nullptr,
-             hipEvent_t append_done = nullptr, int phase = 0);
+             hipEvent_t append_done = nullptr, int phase = 0, hipEvent_t plan_done = nullptr);
   // Whether a SET of `bytes_bound` bytes issued now would run the CLOCK hand (the log is
   // within a few batches of wrapping); the answer can only turn true later.
   bool would_reclaim(uint64_t bytes_bound) const {
@@ -230,29 +241,49 @@ class HbmCache {
 
  private:
   void ensure_set_ws(int64_t n, hipStream_t s);
-  void ensure_rc_ws(int64_t w);
+  void ensure_rc_ws(int64_t w, hipStream_t s);
+  void ensure_cb(int b, int64_t rows, hipStream_t s);
   bool should_reclaim(uint64_t bytes_bound) const;
   void reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                       const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                      int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s);
+                      int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s,
+                      bool detached);
   uint64_t* cur_ring_tail() const { return head_ + 2 + hsel_; }
   uint64_t* next_ring_tail() const { return head_ + 2 + (hsel_ ^ 1); }
+  // Deferred frees (no device-wide synchronisation on the serving path): a grown buffer's
+  // old block is kept until the cache is destroyed or a synchronising maintenance call
+  // (flush, sweep) runs; `note_stream` remembers the streams SET work was queued on.
+  void retire(void* p);
+  void free_retired();
+  void note_stream(hipStream_t s);
+  std::vector<void*> retired_;
+  std::vector<hipStream_t> set_streams_;
   // CLOCK state
   uint64_t* ring_ = nullptr;           // item-start ring (logical locs, kRingSkip holes)
   uint64_t ring_cap_ = 0;
-  unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut
-  uint8_t* rc_scratch_ = nullptr;      // staged reinsertions (rmax_ + 64 bytes)
+  unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, entries scanned
   uint64_t rmax_ = 0;
   int64_t rc_cap_ = 0;
   uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr;
-  uint64_t *cb_voff_ = nullptr;
   int64_t rc_adv_w_ = 0;
   // store(phase=1) queued the CLOCK hand of a batch of hand_n_ rows with a window of hand_w_
-  // (0: none); store(phase=2) runs that combined batch's chain
+  // (0: none) into hand buffer hand_b_; store(phase=2) runs that combined batch's chain
   int64_t hand_w_ = 0, hand_n_ = 0;  // > 0: the next SET plan's dedupe advances the hand (window w)
-  Digest* cb_keys_ = nullptr;
-  uint32_t *cb_vlen_ = nullptr, *cb_flags_ = nullptr, *cb_expire_ = nullptr;
-  int64_t cb_cap_ = 0;
+  int hand_b_ = 0;
+  // The combined SET batch (reinsertion rows, then the batch's own rows) and the staged
+  // reinsertion records, two buffers taken in turn (a detached hand fills one while the
+  // previous batch's chain still reads the other). `from`: a reinsertion row's old entry
+  // loc (a move), 0 for the batch's rows.
+  struct HandBuf {
+    Digest* keys = nullptr;
+    uint64_t* voff = nullptr;
+    uint64_t* from = nullptr;
+    uint32_t *vlen = nullptr, *flags = nullptr, *expire = nullptr;
+    int64_t cap = 0;
+    uint8_t* scratch = nullptr;  // staged reinsertions (rmax_ + 64 bytes)
+  };
+  HandBuf hb_[2];
+  int hb_next_ = 0;
 
   ShardConfig cfg_;
   uint8_t* log_ = nullptr;
@@ -298,10 +329,12 @@ class HbmCache {
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                     int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
-                    hipEvent_t append_after = nullptr, hipEvent_t append_done = nullptr);
+                    hipEvent_t append_after = nullptr, hipEvent_t append_done = nullptr,
+                    const uint64_t* from = nullptr, hipEvent_t plan_done = nullptr);
   void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
-                          int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after);
+                          int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
+                          const uint64_t* from = nullptr);
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------

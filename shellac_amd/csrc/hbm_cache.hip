@@ -1743,13 +1743,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     const uint32_t* __restrict__ expire, Entry* __restrict__ index, uint64_t mask,
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
-    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim) {
+    int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim,
+    const uint64_t* __restrict__ from) {
   const int l4 = threadIdx.x & 3;
   const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
   const uint64_t head_new = base + off[n];
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
-  unsigned long long evicted = 0, bytes = 0, lost = 0;
+  unsigned long long evicted = 0, bytes = 0, lost = 0, moved_away = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
   for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
     if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
@@ -1763,6 +1764,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     const uint64_t myloc = base + off[i] + 1;
     const uint32_t myvlen = vlen[i];
     const uint32_t myexp = expire ? expire[i] : 0u;
+    // a CLOCK reinsertion (detached hand): a move of the entry that still points at the
+    // item's old location, or nothing (uniform in the group)
+    const uint64_t fr = from ? from[i] : 0ull;
     const uint64_t b1 = bucket1(d, mask), b2 = bucket2(d, mask);
     const uint64_t* q1 = reinterpret_cast<const uint64_t*>(index + b1 * kEntriesPerBucket + l4);
     const uint64_t* q2 = reinterpret_cast<const uint64_t*>(index + b2 * kEntriesPerBucket + l4);
@@ -1790,7 +1794,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       const uint32_t lmask = (uint32_t)((__ballot(v1) >> gbase) & 0xfull) |
                              ((uint32_t)((__ballot(v2) >> gbase) & 0xfull) << 4);
       int target;
-      if (mmask) {
+      if (fr) {
+        // the move's source entry: the one whose loc is still the old item's (a SET, DELETE
+        // or eviction since the hand read the index replaced it: the reinsertion is dropped)
+        const uint32_t fmask = (uint32_t)((__ballot(w1[2] == fr) >> gbase) & 0xfull) |
+                               ((uint32_t)((__ballot(w2[2] == fr) >> gbase) & 0xfull) << 4);
+        if (!fmask) {
+          if (l4 == 0) ++moved_away;
+          break;
+        }
+        target = __ffs(fmask) - 1;
+      } else if (mmask) {
         target = __ffs(mmask) - 1;
       } else {
         const uint32_t dead = ~lmask & 0xffu;
@@ -1827,11 +1841,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       }
       ok = __shfl(ok, gbase);
       if (ok) break;
+      if (fr) {  // the entry moved on between the read and the CAS: drop the reinsertion
+        if (l4 == 0) ++moved_away;
+        break;
+      }
       if (attempt == 15 && l4 == 0) ++lost;  // bucket pair contended past the retry budget
     }
   }
   block_count(ctr, evicted, &CacheCounters::set_evicted, bytes, &CacheCounters::set_bytes, lost,
               &CacheCounters::set_dropped);
+  if (from) block_count(ctr, moved_away, &CacheCounters::reinsert_lost);
 }
 
 // One row k_set_index deferred (its pair all live), by one thread inside k_set_fixup:
@@ -2187,22 +2206,24 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 struct RcArgs {
   const uint64_t* ring;
   uint64_t rmask;
-  const uint64_t* ring_tail;
-  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first meeting entry
+  const uint64_t* ring_tail;  // the last batch whose ring entries are written (see store)
+  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first meeting entry, [3] scanned
   int64_t W;
-  const uint64_t* head_ptr;
+  const uint64_t* head_ptr;  // the claim word: the head the queued appends will reach
   uint64_t cap;
   uint32_t now;
   uint64_t rmax;
 };
 
-// The combined SET batch (rows [0, W) reinsertions, [W, W + n) the batch).
+// The combined SET batch (rows [0, W) reinsertions, [W, W + n) the batch). `from`: a
+// picked reinsertion's old entry loc (its index insert is a move from it), 0 otherwise.
 struct RcBatch {
   Digest* keys;
   uint64_t* voff;
   uint32_t* vlen;
   uint32_t* flags;
   uint32_t* expire;
+  uint64_t* from;
 };
 
 __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const uint8_t* __restrict__ log,
@@ -2231,9 +2252,13 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
     cb.vlen[r] = v;
     cb.flags[r] = flags ? flags[i] : 0u;
     cb.expire[r] = expire ? expire[i] : 0u;
+    cb.from[r] = 0;
   }
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t avail = rtail - hand;
+  // the entries this hand examines (a detached hand sees the ring tail of the batch before
+  // the previous one): the advance consumes at most these
+  if (j == 0) a.ctl[3] = (uint64_t)a.W < avail ? (uint64_t)a.W : avail;
   uint64_t loc = kRingSkip, h = 0;
   uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
   if (j < a.W && (uint64_t)j < avail) {
@@ -2282,6 +2307,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
     cb.vlen[j] = h ? w1.x : kSkipVlen;
     cb.flags[j] = h ? w1.y : 0u;
     cb.expire[j] = h ? w1.z : 0u;
+    cb.from[j] = 0;
   }
   block_partial(h, part_h);
   // batch bytes: one atomic per block
@@ -2339,6 +2365,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
     if (h) {
       if (!meets && hx + h <= a.rmax) {
         cb.voff[j] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
+        cb.from[j] = loc + 1;  // indexed as a move from the entry that points here
         const int k = atomicAdd(&s_n, 1);
         s_src[k] = loc % a.cap;
         s_dst[k] = hx;
@@ -2416,8 +2443,7 @@ struct RcAdvance {
 __device__ __forceinline__ void rc_advance(const RcAdvance& r) {
   const uint64_t rtail = *r.ring_tail;
   const uint64_t hand0 = r.ctl[0];
-  const uint64_t avail = rtail - hand0;
-  const uint64_t weff = (uint64_t)r.W < avail ? (uint64_t)r.W : avail;
+  const uint64_t weff = r.ctl[3];  // the entries the hand examined (k_rc_scan)
   const unsigned long long cut = r.ctl[2];
   uint64_t hand = hand0 + (cut != ~0ull && cut < weff ? cut : weff);
   if (rtail - hand > r.rmask + 1) hand = rtail - (r.rmask + 1);  // ring lapped the hand
@@ -2904,7 +2930,7 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipMalloc(&rc_ctl_, 8 * sizeof(unsigned long long)));
     HIP_OK(hipMemset(rc_ctl_, 0, 8 * sizeof(unsigned long long)));
     HIP_OK(hipMemset(rc_ctl_ + 2, 0xff, sizeof(unsigned long long)));  // no cut yet
-    HIP_OK(hipMalloc(&rc_scratch_, rmax_ + 64));
+    for (HandBuf& b : hb_) HIP_OK(hipMalloc(&b.scratch, rmax_ + 64));
   }
   HIP_OK(hipDeviceSynchronize());
 }
@@ -2936,30 +2962,66 @@ HbmCache::~HbmCache() {
   (void)hipFree(dd_slot_);
   (void)hipFree(set_size_);
   (void)hipFree(set_off_); (void)hipFree(set_claim_); (void)hipFree(set_cnt_);
-  (void)hipFree(ring_); (void)hipFree(rc_ctl_); (void)hipFree(rc_scratch_);
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_, (void*)cb_voff_,
-                  (void*)cb_keys_, (void*)cb_vlen_,
-                  (void*)cb_flags_, (void*)cb_expire_})
-    (void)hipFree(p);
+  (void)hipFree(ring_); (void)hipFree(rc_ctl_);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) (void)hipFree(p);
+  for (HandBuf& b : hb_)
+    for (void* p : {(void*)b.keys, (void*)b.voff, (void*)b.from, (void*)b.vlen, (void*)b.flags,
+                    (void*)b.expire, (void*)b.scratch})
+      (void)hipFree(p);
+  free_retired();
+}
+
+void HbmCache::retire(void* p) {
+  if (p) retired_.push_back(p);
+}
+
+void HbmCache::free_retired() {
+  for (void* p : retired_) (void)hipFree(p);
+  retired_.clear();
+}
+
+void HbmCache::note_stream(hipStream_t s) {
+  if (std::find(set_streams_.begin(), set_streams_.end(), s) == set_streams_.end())
+    set_streams_.push_back(s);
 }
 
 uint64_t HbmCache::hbm_bytes() const {
   return cfg_.log_bytes + item_bytes(cfg_.max_item) + 64 + cfg_.nbuckets * kBucketBytes +
-         ring_cap_ * sizeof(uint64_t) + (rc_scratch_ ? rmax_ + 64 : 0);
+         ring_cap_ * sizeof(uint64_t) + (hb_[0].scratch ? 2 * (rmax_ + 64) : 0);
 }
 
-// Hand-step workspace for windows of w ring entries, and the combined SET batch (w
-// reinsertion rows + the batch's own rows).
-void HbmCache::ensure_rc_ws(int64_t w) {
+// Hand-step workspace for windows of w ring entries. Buffers grow without a device
+// synchronisation: the old blocks are retired (freed with the cache), since queued work on
+// any stream may still read them.
+void HbmCache::ensure_rc_ws(int64_t w, hipStream_t s) {
+  (void)s;
   if (w <= rc_cap_) return;
   int64_t cap = rc_cap_ ? rc_cap_ : 4096;
   while (cap < w) cap *= 2;
-  HIP_OK(hipDeviceSynchronize());
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) (void)hipFree(p);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) retire(p);
   HIP_OK(hipMalloc(&rc_loc_, cap * 8));
   HIP_OK(hipMalloc(&rc_h_, cap * 8));
   HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
   rc_cap_ = cap;
+}
+
+// Hand buffer b for a combined batch of `rows` rows (w reinsertion rows + the batch's own).
+void HbmCache::ensure_cb(int b, int64_t rows, hipStream_t s) {
+  (void)s;
+  HandBuf& h = hb_[b];
+  if (rows <= h.cap) return;
+  int64_t cap = h.cap ? h.cap : 4096;
+  while (cap < rows) cap *= 2;
+  for (void* p : {(void*)h.keys, (void*)h.voff, (void*)h.from, (void*)h.vlen, (void*)h.flags,
+                  (void*)h.expire})
+    retire(p);
+  HIP_OK(hipMalloc(&h.keys, cap * sizeof(Digest)));
+  HIP_OK(hipMalloc(&h.voff, cap * 8));
+  HIP_OK(hipMalloc(&h.from, cap * 8));
+  HIP_OK(hipMalloc(&h.vlen, cap * 4));
+  HIP_OK(hipMalloc(&h.flags, cap * 4));
+  HIP_OK(hipMalloc(&h.expire, cap * 4));
+  h.cap = cap;
 }
 
 bool HbmCache::should_reclaim(uint64_t bytes_bound) const {
@@ -2974,39 +3036,43 @@ bool HbmCache::should_reclaim(uint64_t bytes_bound) const {
 
 void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                               const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
-                              int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s) {
-  RcArgs a{ring_, ring_cap_ - 1, cur_ring_tail(), rc_ctl_, w, cur_head(), cfg_.log_bytes, now, rmax};
+                              int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s,
+                              bool detached) {
+  // The head: the claim word, i.e. the head every queued append will have reached (equal to
+  // the head slot once they have run). The ring tail: a detached hand may run before the
+  // previous batch's fixup writes its ring entries and tail, so it reads the tail of the
+  // batch before that one (the other ping-pong slot), whose entries are written.
+  RcArgs a{ring_, ring_cap_ - 1, detached ? next_ring_tail() : cur_ring_tail(), rc_ctl_, w,
+           claim_ptr(), cfg_.log_bytes, now, rmax};
   const int g = (int)((w + kBlock - 1) / kBlock);
-  const RcBatch cb{cb_keys_, cb_voff_, cb_vlen_, cb_flags_, cb_expire_};
+  const HandBuf& hb = hb_[hand_b_];
+  const RcBatch cb{hb.keys, hb.voff, hb.vlen, hb.flags, hb.expire, hb.from};
   hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, cb, log_, index_, cfg_.nbuckets - 1,
                      keys, values, val_off, vlen, flags, expire, n, cfg_.max_item, rc_loc_, rc_h_,
                      rc_part_);
   hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, log_, rc_loc_, rc_h_, rc_part_,
-                     rc_scratch_, ctr_);
+                     hb.scratch, ctr_);
   rc_adv_w_ = w;  // the combined batch's dedupe advances the hand
   HIP_OK(hipGetLastError());
 }
 
 void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
-  (void)s;
   if (n <= set_cap_) return;
   int64_t cap = set_cap_ ? set_cap_ : 1024;
   while (cap < n) cap *= 2;
-  HIP_OK(hipDeviceSynchronize());
-  (void)hipFree(dd_keys_); (void)hipFree(dd_win_); (void)hipFree(dd_slot_);
-  (void)hipFree(set_size_); (void)hipFree(set_off_); (void)hipFree(set_claim_);
-  (void)hipFree(set_cnt_);
+  // the old workspace may still be read by queued SET chains on other streams: retired,
+  // not freed (no device synchronisation on the serving path)
+  for (void* p : {(void*)dd_keys_, (void*)dd_win_, (void*)dd_slot_, (void*)set_size_,
+                  (void*)set_off_, (void*)set_claim_, (void*)set_cnt_})
+    retire(p);
   const uint64_t tslots = (uint64_t)cap * 2;
   HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
-  // the table is cleared once here; k_set_index resets every slot a batch used
-  HIP_OK(hipMemset(dd_keys_, 0, tslots * sizeof(uint64_t)));
-  HIP_OK(hipMemset(dd_win_, 0xff, tslots * sizeof(int)));
-  // hipMemset is asynchronous for device memory and runs on the null stream, which a
-  // non-blocking stream (the routed step's side stream) does not wait for: without this
-  // sync the first SET batch's dedupe could read the table before it is cleared and drop
-  // its rows (seen as set_dropped on one rank of a 3-process test, ~1 run in 6)
-  HIP_OK(hipDeviceSynchronize());
+  // the table is cleared once here, on the stream of the SET that first uses it (ordered
+  // before its dedupe; the null stream is not: a non-blocking stream does not wait for it,
+  // which once dropped the first batch's rows); k_set_index resets every slot a batch used
+  HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
+  HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
   HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
@@ -3021,6 +3087,9 @@ void HbmCache::reserve(int64_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, nullptr);
+  // (a maintenance call, not on the serving path: the null-stream clears land before any
+  // stream's next SET)
+  HIP_OK(hipDeviceSynchronize());
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
@@ -3256,20 +3325,22 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                      const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
                      hipEvent_t index_after, bool allow_reclaim, hipEvent_t append_after,
-                     hipEvent_t append_done, int phase) {
+                     hipEvent_t append_done, int phase, hipEvent_t plan_done) {
   TraceRange tr("hbm.store");
   if (n <= 0) return;
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
            "SET batch larger than half the log; split the batch");
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
+  note_stream(s);
   // phase 2: the rest of a batch whose CLOCK hand a phase-1 call queued
   if (phase == 2 && hand_w_ > 0) {
     SH_CHECK(hand_n_ == n, "store phase 2 of a different batch than phase 1");
     const int64_t w = hand_w_;
     hand_w_ = 0;
-    store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
-                 index_after, append_after, append_done);
+    const HandBuf& hb = hb_[hand_b_];
+    store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
+                 index_after, append_after, append_done, hb.from, plan_done);
     hsel_ ^= 1;
     return;
   }
@@ -3281,32 +3352,25 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   }
   if (allow_reclaim && rmax && should_reclaim(bytes_bound)) {
     const int64_t w = hand_window(n);
-    ensure_rc_ws(w);
-    if (w + n > cb_cap_) {
-      int64_t cap = cb_cap_ ? cb_cap_ : 4096;
-      while (cap < w + n) cap *= 2;
-      HIP_OK(hipDeviceSynchronize());
-      for (void* p : {(void*)cb_voff_, (void*)cb_keys_, (void*)cb_vlen_, (void*)cb_flags_,
-                      (void*)cb_expire_})
-        (void)hipFree(p);
-      HIP_OK(hipMalloc(&cb_keys_, cap * sizeof(Digest)));
-      HIP_OK(hipMalloc(&cb_voff_, cap * 8));
-      HIP_OK(hipMalloc(&cb_vlen_, cap * 4));
-      HIP_OK(hipMalloc(&cb_flags_, cap * 4));
-      HIP_OK(hipMalloc(&cb_expire_, cap * 4));
-      cb_cap_ = cap;
-    }
+    ensure_rc_ws(w, s);
+    // the hand buffers alternate: a detached hand of the next batch fills the other one
+    // while this batch's chain still reads this one
+    hand_b_ = hb_next_;
+    hb_next_ ^= 1;
+    ensure_cb(hand_b_, w + n, s);
     ensure_set_ws(w + n, s);
-    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s);
+    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, phase == 1);
     if (phase == 1) {  // the chain follows in phase 2
       hand_w_ = w;
       hand_n_ = n;
       return;
     }
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
-    store_locked(cb_keys_, nullptr, cb_voff_, cb_vlen_, cb_flags_, cb_expire_, w + n, now, s,
-                 index_after, append_after, append_done);
-  } else if (n <= kSmallSetRows && !index_after && !append_after && !append_done) {
+    const HandBuf& hb = hb_[hand_b_];
+    store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
+                 index_after, append_after, append_done, hb.from, plan_done);
+  } else if (n <= kSmallSetRows && !index_after && !append_after && !append_done &&
+             !plan_done) {
     // one launch for the whole chain (the proxy's small SET batches)
     hipLaunchKernelGGL(k_set_small, dim3(1), dim3(kBlock), 0, s, keys, values, val_off, vlen,
                        flags, expire, (int)n, cfg_.max_item, index_, cfg_.nbuckets - 1,
@@ -3318,7 +3382,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   } else {
     ensure_set_ws(n, s);
     store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, append_after,
-                 append_done);
+                 append_done, nullptr, plan_done);
   }
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
@@ -3332,14 +3396,16 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
 void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                             int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
-                            hipEvent_t append_after, hipEvent_t append_done) {
+                            hipEvent_t append_after, hipEvent_t append_done,
+                            const uint64_t* from, hipEvent_t plan_done) {
   store_plan_locked(keys, vlen, n, s);
+  if (plan_done) HIP_OK(hipEventRecord(plan_done, s));
   if (append_after) HIP_OK(hipStreamWaitEvent(s, append_after, 0));
   launch_segcopy<1>(s, values, val_off, set_off_, n, log_, keys, vlen, flags, expire, cur_head(),
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());
   if (append_done) HIP_OK(hipEventRecord(append_done, s));
-  store_index_locked(keys, vlen, expire, n, now, s, index_after);
+  store_index_locked(keys, vlen, expire, n, now, s, index_after, from);
 }
 
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,
@@ -3363,14 +3429,14 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
 
 void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
                                   const uint32_t* expire, int64_t n, uint32_t now, hipStream_t s,
-                                  hipEvent_t index_after) {
+                                  hipEvent_t index_after, const uint64_t* from) {
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
   const int igrid = grid_for(n * 4, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                      vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                      cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
-                     set_claim_);
+                     set_claim_, from);
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      set_off_, vlen, expire, cur_head(), set_claim_, index_, set_size_, ring_,
                      ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(), next_ring_tail(), set_cnt_,

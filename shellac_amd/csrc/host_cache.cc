@@ -230,7 +230,7 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
     ItemHeader h;
     std::memcpy(&h, rec, sizeof h);
     out->push_back(Row{Digest{h.d0, h.d1}, stage->data() + t.hx + kItemHeaderBytes, h.vlen,
-                       h.flags, h.expire});
+                       h.flags, h.expire, t.loc + 1});
     ctr_.reinserted++;
     ctr_.reinsert_bytes += h.vlen;
   }
@@ -284,8 +284,28 @@ void HostCache::store_rows_locked(const std::vector<Row>& rows, uint32_t now) {
   acc = 0;
   for (int64_t i = 0; i < n; ++i) {
     if (!sz[i]) continue;
-    insert_locked(rows[i].key, base + acc + 1, rows[i].vlen, rows[i].expire, now);
-    ctr_.set_bytes += rows[i].vlen;
+    const Row& r = rows[i];
+    if (r.from) {
+      // a reinsertion is a move of the entry that still points at the old item (the
+      // device's detached hand may run before a SET / DELETE of the key lands; here the
+      // hand ran after every earlier batch, so the entry is always still there)
+      Entry* src = nullptr;
+      for (uint64_t b : {bucket1(r.key, mask_), bucket2(r.key, mask_)})
+        for (uint32_t k = 0; k < kEntriesPerBucket && !src; ++k)
+          if (index_[b * kEntriesPerBucket + k].loc == r.from) src = &index_[b * kEntriesPerBucket + k];
+      if (src) {
+        src->loc = base + acc + 1;
+        src->vlen = r.vlen;
+        src->expire = r.expire;
+        ctr_.set_bytes += r.vlen;
+      } else {
+        ctr_.reinsert_lost++;
+      }
+      acc += sz[i];
+      continue;
+    }
+    insert_locked(r.key, base + acc + 1, r.vlen, r.expire, now);
+    ctr_.set_bytes += r.vlen;
     acc += sz[i];
   }
 }

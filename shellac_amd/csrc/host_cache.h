@@ -61,6 +61,7 @@ class HostCache {
     Digest key;
     const uint8_t* val;
     uint32_t vlen, flags, expire;
+    uint64_t from = 0;  // a CLOCK reinsertion: a move of the entry at this loc (see HbmCache)
   };
   bool insert_locked(const Digest& d, uint64_t loc1, uint32_t vlen, uint32_t expire, uint32_t now);
   // mark: a GET (sets the CLOCK reference bit of the entry it finds)

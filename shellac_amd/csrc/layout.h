@@ -132,7 +132,10 @@ struct CacheCounters {
   unsigned long long get_coalesced; // duplicate GET rows served by a batch-mate's probe
   unsigned long long reinserted;    // referenced items the CLOCK hand gave a second life
   unsigned long long reinsert_bytes;
-  unsigned long long reserved[3];
+  // reinsertions indexed as moves whose entry had moved on (a SET or DELETE of the key
+  // landed after the hand read the index): their log bytes are dead on arrival
+  unsigned long long reinsert_lost;
+  unsigned long long reserved[2];
 };
 static_assert(sizeof(CacheCounters) == 128, "CacheCounters layout");
 

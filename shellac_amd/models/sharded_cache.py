@@ -170,10 +170,12 @@ def _event_handle(ev) -> int:
 
 
 class ShardedCache:
+    HANDS = ("early", "inline")
+
     def __init__(self, shard: CacheShard, group=None, points_per_shard: int = 160,
                  replica: Optional[CacheShard] = None, sample_rows: int = 65536,
                  sample_batches: int = 8, data_group=None, routed: Optional[bool] = None,
-                 comm_mode: str = "channels"):
+                 comm_mode: str = "channels", hand: str = "early"):
         self.shard = shard
         self.group = group
         # native routed step: "single" = every collective of a step on one communicator and
@@ -218,6 +220,10 @@ class ShardedCache:
         # the transfer runs)
         self._inflight = []
         self._hot_dir = None  # 65537-entry directory into self._hot (built lazily)
+        # incremental migration (set_ring): keys SET / DELETEd since the ring switch
+        self._migrating = None
+        self._touched = None
+        self._touched_all = None
         # simulated world: request digests -> the digests their owners hold (see serve)
         self.probe_of = None
         # replica refresh: scores of the hot keys (aligned with _hot) and their decay per
@@ -248,10 +254,18 @@ class ShardedCache:
         self.event_fence = "none"
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
-        # one GPU: the SET batch's CLOCK hand is queued before the lookup, which waits for
-        # it (see serve); False queues the whole SET chain after the lookup
-        self.hand_first = os.environ.get("SHELLAC_HAND_FIRST", "1") == "1"
+        # one GPU, a full cache: where the SET batch's CLOCK hand runs (see serve).
+        # "early": detached, on a stream of its own, as soon as the previous step's SET
+        # planning is done — beside that step's log append, index insert and gather; its
+        # reinsertions are indexed as moves (HbmCache::store). "inline": at the head of the
+        # SET chain on the side stream, after the lookup is queued.
+        if hand not in self.HANDS:
+            raise ValueError(f"hand must be one of {self.HANDS}, not {hand!r}")
+        self.hand = hand
         self._side_pending = False
+        self._planned = False    # the last serve's plan_done event can order the next hand
+        self._held_set = None    # the SET batch the side chain still reads (until joined)
+        self._hand_s = None
         self._events = {}
         self._side = None
         self._gather_cap = 0     # response buffer bytes for the unsynced gather
@@ -291,9 +305,13 @@ class ShardedCache:
         other ShardedCache method calls it; call it before using ``self.shard`` directly
         after a routed ``serve`` (a device synchronisation also does)."""
         if self._side_pending:
-            # the last one-GPU serve's SET chain (hand_first leaves it for the next step)
+            # the last one-GPU serve's SET chain (serve leaves it for the next step)
             self._xwait(torch.cuda.current_stream(self.device), self._side, "end")
             self._side_pending = False
+            self._held_set = None
+        # whatever runs next on the caller's stream (a set, a delete, ...) is not covered by
+        # the last serve's plan event: the next early hand follows the caller's stream
+        self._planned = False
         e = self._engine
         if e is not None and e.sets_pending:
             e.join_sets(torch.cuda.current_stream(self.device).cuda_stream)
@@ -438,6 +456,7 @@ class ShardedCache:
         the gather (no event, no copy).
         With several ranks see ``_serve_routed``: 4-5 collectives and 2 host syncs for
         the whole step instead of 10 and 3 for get() followed by set()."""
+        self._touch(batch.keys)
         if self.routed:
             if self.fused and self.device.type == "cuda":
                 return self._serve_routed_fused(keys, batch, now, inputs_ready, probe_keys)
@@ -455,62 +474,84 @@ class ShardedCache:
             return GetResult(data, lk.off[:n], lk.size[:n])
         side = self._side_stream() if self.overlap_store else None
         stage = self.host_edge and self.host_edge_dma and keys.device.type == "cpu"
-        stage_set = stage
         if stage:
             # host edge: the GET digests into HBM by DMA on this stream (the lookup reads
-            # them from HBM instead of across PCIe); the SET batch likewise on the SET
-            # stream, below
+            # them from HBM instead of across PCIe); the SET batch likewise on the stream
+            # that first reads it, below
             t = self._stage_turn = 1 - getattr(self, "_stage_turn", 1)
             keys = self._staged(t, "keys", keys)
-        if side is not None:
-            # The SET chain runs on a side stream: its CLOCK hand (a full cache) first, which
-            # the lookup waits for (hand_first), then dedupe and sizing beside the lookup, its
-            # log append (bytes the lookup reserves, so this step's gather never reads them)
-            # once the previous step's gather is done with the region it overwrites; only its
-            # index insert waits for the probe (event), then runs under the gather.
-            main = torch.cuda.current_stream(self.device)
-            now = sh.now() if now is None else now
-            if self.hand_first:
-                # The CLOCK hand first (a full cache), and the lookup after it: queued beside
-                # the lookup, the hand's workgroups waited for the lookup's to retire, and the
-                # log append behind it then ran beside the gather (the pressured step). This
-                # wait also joins the previous step's SET chain (the hand follows it on the
-                # SET stream), which the end of the previous serve left pending.
-                with torch.cuda.stream(side):
-                    if stage:
-                        batch = SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
-                            (batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                             batch.expire))))
-                        stage_set = False
-                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                             batch.expire, now, phase=1)
-                self._xwait(main, side, "hand")
-                self._side_pending = False
-            start = self._event("start")
-            start.record(main)                # the previous step's gather is done with the log
-        try:
-            if self.coalesce:
-                table = self._coalesce_table(n) if side is not None else None
-                lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound,
-                                                       total_slot=0, table=table)
-            else:
-                lk, first, cslot, table = (sh.lookup(keys, now, reserve_bytes=bound,
-                                                     total_slot=0), None, None, None)
-        except BaseException:
-            if side is not None and self.hand_first:
-                # a queued hand's batch still runs its chain (the native store pairs phase 1
-                # with the next phase 2)
-                with torch.cuda.stream(side):
-                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                             batch.expire, now, phase=2)
-                self._side_pending = True
-            raise
+
+        def staged_batch(b):
+            if not stage:
+                return b
+            return SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
+                (b.keys, b.values, b.val_off, b.vlen, b.flags, b.expire))))
+
         if side is None:
+            lk, first, cslot, _ = self._lookup_step(keys, now, bound, None)
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now)
             data = self._gather_unsynced(lk)
             expand(first, lk.size, lk.off)
             return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
+        # The SET chain runs beside the GET path. Streams: the caller's (main: lookup,
+        # gather), the SET stream (side: dedupe, sizing, log append, index insert) and, with
+        # hand="early", a hand stream (the CLOCK hand of a full cache). Ordering:
+        #  * everything that reads the request batches waits for `ready` (inputs_ready, or
+        #    the caller's stream as of this call);
+        #  * the lookup waits for the previous step's SET chain (a step's GETs see the
+        #    previous step's SETs, never this step's);
+        #  * the log append waits for the previous step's gather (it overwrites the oldest
+        #    region, which that gather may still read; the lookup reserved the SET's bytes,
+        #    so this step's gather never reads them); the index insert waits for the lookup;
+        #  * the early hand waits for the previous step's SET planning only (it reads the
+        #    hand position, the claimed head and the ring the planning leaves) and runs beside
+        #    that step's append, index insert and gather; its reinsertions are moves, so a
+        #    SET that lands after it read the index makes them no-ops, never stale values.
+        main = torch.cuda.current_stream(self.device)
+        now = sh.now() if now is None else now
+        if inputs_ready is None:
+            ready = self._event("inputs")
+            ready.record(main)
+        else:
+            ready = inputs_ready
+        early = self.hand == "early"
+        hand_done = None
+        if early:
+            hs = self._hand_stream()
+            self._wait(hs, ready)
+            if self._planned:
+                self._wait(hs, self._event("planned"))
+            else:
+                # no serve plan to follow (first step, or other work since): the caller's
+                # stream as of now, which has joined every earlier SET chain
+                self._xwait(hs, main, "mainpos")
+            with torch.cuda.stream(hs):
+                batch = staged_batch(batch)
+                sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                         batch.expire, now, phase=1)
+            hand_done = self._event("hand")
+            hand_done.record(hs)
+        if self._side_pending:
+            self._xwait(main, side, "end")   # the previous step's SET chain
+            self._side_pending = False
+        start = self._event("start")
+        start.record(main)                   # ... and its gather: the append may overwrite
+        try:
+            lk, first, cslot, table = self._lookup_step(keys, now, bound, side)
+        except BaseException:
+            if early:
+                # the queued hand's batch still runs its chain (the native store pairs phase 1
+                # with the next phase 2), after the previous gather like any append
+                with torch.cuda.stream(side):
+                    self._wait(side, hand_done)
+                    sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+                             batch.expire, now, append_after=start, phase=2,
+                             plan_done=self._event("planned"))
+                self._side_pending = True
+                self._held_set = batch
+                self._planned = True
+            raise
         # Safe by construction: the lookup reserved the SET's log bytes, so the gather
         # never reads a region the SET writes, and the gather does not read the index.
         if first is not None:
@@ -520,30 +561,58 @@ class ShardedCache:
         ev.record(main)
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
-            if stage and stage_set:
-                batch = SetBatch(*(self._staged(t, f"s{i}", x) for i, x in enumerate(
-                    (batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                     batch.expire))))
+            if early:
+                self._wait(side, hand_done)  # (the hand followed `ready`)
+            else:
+                self._wait(side, ready)
+                batch = staged_batch(batch)
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now, index_after=ev, append_after=start, append_done=appended,
-                     phase=2 if self.hand_first else 0)
+                     phase=2 if early else 0, plan_done=self._event("planned") if early else None)
+        self._planned = early
         if appended is not None:
             # the gather runs after the log append, not beside it: the two byte movers
             # contending for HBM are slower together than one after the other
-            appended.wait(main) if isinstance(appended, StreamEvent) else main.wait_event(appended)
+            self._wait(main, appended)
         # per-request (size, off) and the table clean-up: the gather's workgroups do them
         # after their copies (no launch, and nothing on the side stream for the next
         # step's lookup to wait for but the SET chain)
         data = self._gather_unsynced(
             lk, None if first is None else (first, out_size, out_off, table, cslot))
-        if self.hand_first:
-            # joined by the next serve's hand wait, or by sync_sets (every other method)
-            self._side_pending = True
-        else:
-            self._xwait(main, side, "end")  # the next step's lookup sees this step's SETs
+        # joined by the next serve's lookup, or by sync_sets (every other method); the
+        # chain reads the batch until then
+        self._side_pending = True
+        self._held_set = batch
         if first is not None:
             return GetResult(data, out_off, out_size, self._take_pending())
         return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
+
+    def _lookup_step(self, keys, now, bound, side):
+        """The step's GET lookup (coalesced unless ``coalesce`` is off): (lookup, first,
+        cslot, table)."""
+        sh = self.shard
+        if self.coalesce:
+            table = self._coalesce_table(keys.shape[0]) if side is not None else None
+            lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
+                                                   table=table)
+            return lk, first, cslot, table
+        return sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None, None
+
+    @staticmethod
+    def _wait(stream, ev) -> None:
+        """``stream`` waits for a recorded event (a StreamEvent or a torch.cuda.Event)."""
+        if isinstance(ev, StreamEvent):
+            ev.wait(stream)
+        else:
+            stream.wait_event(ev)
+
+    def _hand_stream(self):
+        """The early CLOCK hand's stream: the executor's plan stream, a hardware queue of its
+        own (reserve_step_streams), unused by the one-GPU step otherwise."""
+        if self._hand_s is None:
+            ss = [int(x) for x in _core().step_streams(self.device.index)]
+            self._hand_s = torch.cuda.ExternalStream(ss[0], device=self.device)
+        return self._hand_s
 
     def _event(self, name: str):
         e = self._events.get(name)
@@ -667,11 +736,14 @@ class ShardedCache:
         return torch.empty(nbytes, dtype=torch.uint8, device=self.device)
 
     def _side_stream(self):
+        """The one-GPU step's SET stream: the executor's SET stream, a hardware queue of its
+        own (reserve_step_streams), so nothing queues behind the caller's gather."""
         if self.device.type != "cuda":
             return None
         if self._side is None:
             # (a high-priority side stream measured the same: 0.3156 vs 0.3161 ms/step)
-            self._side = torch.cuda.Stream(device=self.device)
+            ss = [int(x) for x in _core().step_streams(self.device.index)]
+            self._side = torch.cuda.ExternalStream(ss[1], device=self.device)
         return self._side
 
     def _serve_routed_fused(self, keys: torch.Tensor, batch: SetBatch,
@@ -1061,8 +1133,13 @@ class ShardedCache:
         ph.end()
         return GetResult(data, off, size)
 
-    def set(self, batch: SetBatch, now: Optional[int] = None) -> None:
+    def set(self, batch: SetBatch, now: Optional[int] = None, if_absent: bool = False) -> None:
+        """SET a batch (collective when routed). ``if_absent``: an owner stores a row only
+        when it holds no live object of the key (a migration's delivery, which must never
+        overwrite a newer value the owner received directly)."""
         self.sync_sets()
+        if not if_absent:  # (a migration's own delivery is not a newer write)
+            self._touch(batch.keys)
         n = batch.keys.shape[0]
         self._stats["set_requests"] += n
         if not self.routed:
@@ -1121,7 +1198,13 @@ class ShardedCache:
         roff = R.exclusive_scan((rvlen.to(torch.int64) + 15) & ~15)[:-1].contiguous()
         tier = rmeta[:, 3]
         skip = torch.full_like(rvlen, SKIP_VLEN)
-        self.shard.store(rkeys, rvals, roff, torch.where(tier == 0, rvlen, skip).contiguous(),
+        main_vlen = torch.where(tier == 0, rvlen, skip)
+        if if_absent and rkeys.shape[0]:
+            # insert-if-absent (as HbmBackend's warm restore): keys this owner already holds
+            # keep their (newer) value
+            have = self.shard.lookup(rkeys.contiguous(), now).size[: rkeys.shape[0]] > 0
+            main_vlen = torch.where(have, skip, main_vlen)
+        self.shard.store(rkeys, rvals, roff, main_vlen.contiguous(),
                          rmeta[:, 1].contiguous(), rmeta[:, 2].contiguous(), now)
         if self.replica is not None and self._hot is not None:  # tier-1 rows only exist then
             self.replica.store(rkeys, rvals, roff, torch.where(tier == 1, rvlen, skip).contiguous(),
@@ -1129,6 +1212,7 @@ class ShardedCache:
 
     def delete(self, keys: torch.Tensor, now: Optional[int] = None) -> torch.Tensor:
         self.sync_sets()
+        self._touch(keys)
         if not self.routed:
             return self.shard.remove(keys, now)
         if self.replica is not None:  # replicas are dropped everywhere (collective)
@@ -1348,26 +1432,73 @@ class ShardedCache:
         self._reset_exchange()
         self._migrating = mkeys if mkeys is not None else None
         self._migrate_chunk = chunk_keys
+        # until the migration is done, every key a SET or DELETE names (on any rank, through
+        # any path) is remembered: its migrated copy is older than what the new owner got
+        self._touched = [] if migrate and self.world > 1 else None
+        self._touched_all = None
         moved = int(mkeys.shape[0]) if mkeys is not None else 0
         if migrate and self.world > 1 and not incremental:
             while self.migrate_step(None, now):
                 pass
         return moved
 
+    def _touch(self, keys: torch.Tensor) -> None:
+        """During an incremental migration: remember keys a SET / DELETE names."""
+        t = getattr(self, "_touched", None)
+        if t is not None and keys.shape[0]:
+            t.append(keys.to(self.device).contiguous().clone())
+
+    def _gather_touched(self) -> None:
+        """Collective: merge every rank's keys SET or DELETEd since the ring switch into
+        ``_touched_all`` (sorted by lo, the same on every rank), and drop them from this
+        rank's migration queue (their old copies here are stale: the new owner has a newer
+        value, or the key is gone)."""
+        dev = self.device
+        mine = (torch.cat(self._touched) if self._touched else
+                torch.zeros((0, 2), dtype=torch.int64, device=dev))
+        self._touched = []
+        cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=dev)
+        all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
+        m = int(cnt)
+        if m == 0:
+            return
+        pad = torch.zeros((m, 2), dtype=torch.int64, device=dev)
+        pad[: mine.shape[0]] = mine
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        all_gather(parts, pad, group=self.group)
+        allk = torch.cat(parts + ([self._touched_all] if self._touched_all is not None else []))
+        allk = allk[(allk != 0).any(dim=1)]
+        ulo, inv = torch.unique(allk[:, 0].contiguous(), return_inverse=True)
+        u = torch.empty((ulo.numel(), 2), dtype=torch.int64, device=dev)
+        u[inv] = allk
+        self._touched_all = u  # torch.unique sorts by lo
+        q = getattr(self, "_migrating", None)
+        if q is not None and q.shape[0]:
+            stale = self._member(q, u)
+            if bool(stale.any()):
+                self.shard.remove(q[stale].contiguous(), None)
+                q = q[~stale].contiguous()
+                self._migrating = q if q.shape[0] else None
+
     def migrate_step(self, budget_bytes: Optional[int] = None, now: Optional[int] = None) -> bool:
         """Collective. Move queued migration objects (``set_ring``) to their new owners:
         chunks of ``chunk_keys`` until ``budget_bytes`` of records have moved on this rank
         (None: one chunk). Returns whether any rank has objects left (the same on every
-        rank)."""
+        rank). A key SET or DELETEd anywhere since the ring switch is not migrated (its
+        copy here is older than what its new owner holds, or it was deleted), and a
+        delivered object is stored only where the new owner holds nothing of the key."""
         self.sync_sets()
         moved_bytes = 0
         while True:
+            if getattr(self, "_touched", None) is not None:
+                self._gather_touched()
             q = getattr(self, "_migrating", None)
             left = torch.tensor([0 if q is None else int(q.shape[0])], dtype=torch.int64,
                                 device=self.device)
             all_reduce(left, op=dist.ReduceOp.MAX, group=self.group)
             if int(left) == 0:
                 self._migrating = None
+                self._touched = self._touched_all = None
                 return False
             part = (q[: self._migrate_chunk] if q is not None
                     else torch.zeros((0, 2), dtype=torch.int64, device=self.device)).contiguous()
@@ -1382,7 +1513,8 @@ class ShardedCache:
                 empty = torch.zeros(0, dtype=torch.int64, device=self.device)
                 batch = SetBatch(part, torch.zeros(16, dtype=torch.uint8, device=self.device),
                                  empty, empty.to(torch.int32))
-            self.set(batch, now)                  # lands on the new owners (collective)
+            # lands on the new owners (collective), where they hold nothing of the key yet
+            self.set(batch, now, if_absent=True)
             if part.shape[0]:
                 self.shard.remove(part, now)      # this rank no longer owns them
                 self._migrating = q[part.shape[0]:] if q.shape[0] > part.shape[0] else None
@@ -1394,6 +1526,7 @@ class ShardedCache:
             all_reduce(st, op=dist.ReduceOp.MAX, group=self.group)
             if int(st[0]) == 0:
                 self._migrating = None
+                self._touched = self._touched_all = None
                 return False
             if int(st[1]):
                 return True

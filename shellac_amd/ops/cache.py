@@ -466,7 +466,8 @@ class CacheShard:
               vlen: torch.Tensor, flags: Optional[torch.Tensor] = None,
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
-              index_after=None, append_after=None, append_done=None, phase: int = 0) -> None:
+              index_after=None, append_after=None, append_done=None, phase: int = 0,
+              plan_done=None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
@@ -476,7 +477,12 @@ class CacheShard:
         waits for it, the CLOCK hand and the SET planning do not (a gather still reading the
         region the append overwrites may run meanwhile). ``append_done`` (GPU, an event):
         recorded right after the log append. ``phase`` (GPU): 1 queues only the batch's
-        CLOCK hand (a full cache), 2 the rest of the chain for the same batch; 0 both."""
+        CLOCK hand (a full cache), 2 the rest of the chain for the same batch; 0 both. A
+        phase-1 hand is *detached*: it may run as soon as the previous batch's planning is
+        done (``plan_done`` of that batch's phase 2), beside that batch's append and index
+        insert — its reinsertions are indexed as moves, dropped when the key's entry has
+        moved on (``HbmCache::store``). ``plan_done`` (GPU, an event): recorded after the
+        batch's planning kernels."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -493,7 +499,8 @@ class CacheShard:
         if self.is_gpu:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(), _event_handle(index_after),
-                             _event_handle(append_after), _event_handle(append_done), phase)
+                             _event_handle(append_after), _event_handle(append_done), phase,
+                             _event_handle(plan_done))
         elif phase != 1:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now, bound)

@@ -379,15 +379,28 @@ def _migrate_worker(rank, world, port, q):
 
         new = ShardRing(list(range(world)), 97)   # another continuum: many keys move
         n = sc.set_ring(new, incremental=True, chunk_keys=16)
+        # the value every key must end with: writes and deletes land on the new owners
+        # between migrate_step calls (every rank issues a slice of them), and no migrated
+        # (older) copy may overwrite a newer value or bring a deleted key back
+        want = {k: b"m-" + k for k in keys}
         calls = 0
         while True:
             got = read(keys)
-            assert all(g is None or g == b"m-" + k for g, k in zip(got, keys))
+            assert all(g is None or g == want[k] for g, k in zip(got, keys)), calls
             calls += 1
+            upd = keys[(37 * calls) % 900::53][:6]
+            dele = keys[(11 * calls + 5) % 900::71][:4]
+            v, vo, vl = pack_values([b"u%d-" % calls + k for k in upd[rank::world]])
+            sc.set(SetBatch(digest_strings(upd[rank::world]), v, vo, vl))
+            sc.delete(digest_strings(dele[rank::world]))
+            for k in upd:
+                want[k] = b"u%d-" % calls + k
+            for k in dele:
+                want[k] = None
             if not sc.migrate_step(budget_bytes=16 * 40):
                 break
         assert calls > 2 or n == 0
-        assert read(keys) == [b"m-" + k for k in keys]
+        assert read(keys) == [want[k] for k in keys]
         q.put((rank, "ok", 0))
     except BaseException:
         import traceback

@@ -1,5 +1,8 @@
 """HIP kernels vs the host (DRAM) engine / plain PyTorch references. GPU only."""
+import dataclasses
+
 import numpy as np
+
 import pytest
 import torch
 
@@ -973,19 +976,18 @@ def test_serve_steps_return_ground_truth_records(cuda_dev):
     assert all(w == 0 and m == 0 for w, m, _, _ in res), res
 
 
-@pytest.mark.parametrize("hand_first", [True, False])
-def test_serve_wrapped_log_ground_truth_both_hand_schedules(cuda_dev, hand_first):
+@pytest.mark.parametrize("hand", ["early", "inline"])
+def test_serve_wrapped_log_ground_truth_both_hand_schedules(cuda_dev, hand):
     """A log the key space overfills, so every serve step runs the CLOCK hand: with the
-    hand queued before the lookup (hand_first, the default) and after it, every request that
-    hits gets its ground-truth record, the hand reinserts, and a later get() (which joins
-    the pending SET chain) agrees with the last serve."""
+    hand detached on its own stream (early, the default) and at the head of the SET chain
+    (inline), every request that hits gets its ground-truth record, the hand reinserts,
+    and a later get() (which joins the pending SET chain) agrees with the last serve."""
     from shellac_amd.bench.workload import Workload
     from shellac_amd.models.sharded_cache import ShardedCache
 
     wl = Workload(100000, cuda_dev)  # ~100 MB of records into a 96 MiB log
     shard = CacheShard(96 << 20, 1 << 16, 1 << 13, cuda_dev)
-    sc = ShardedCache(shard)
-    sc.hand_first = hand_first
+    sc = ShardedCache(shard, hand=hand)
     for s0 in range(0, 100000, 5000):
         sc.set(_compact(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
     c0 = sc.counters()
@@ -1005,6 +1007,111 @@ def test_serve_wrapped_log_ground_truth_both_hand_schedules(cuda_dev, hand_first
         t = pool[voff[i]: voff[i] + vlen[i]].tobytes()
         assert x is None or x[0] == t
         assert y is None or y[0] == t
+
+
+@pytest.mark.parametrize("hand", ["early", "inline"])
+def test_serve_back_to_back_updates_never_resurrect_stale_values(cuda_dev, hand):
+    """Steps queued back to back (no host sync) over a full cache whose SET batches UPDATE
+    objects (new payload versions) and DELETE some: the early hand of step k+1 runs beside
+    step k's index insert, so it may pick for reinsertion an object step k's SET or DELETE
+    is superseding. Its reinsertion is a move that must then be dropped. Every GET of step
+    k returns the version the SETs of steps < k left, or a miss — never an older version
+    and never a deleted key — and the hand does reinsert."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    N = 60000
+    wl = Workload(N, cuda_dev, min_val=64, max_val=2048)
+    # ~25 MB of records into a 16 MiB log: the populate wraps it, every step runs the hand
+    sc = ShardedCache(CacheShard(16 << 20, 1 << 16, 1 << 13, cuda_dev), hand=hand)
+    for s0 in range(0, N, 5000):
+        sc.set(_compact(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
+    sc.sync_sets()
+    c0 = sc.counters()
+    # hot keys, so the hand finds referenced objects; SETs hit the hot keys too
+    steps, results = 10, []
+    version = [0] * N           # host truth: the version the SETs so far left
+    deleted = set()
+    truth_at = []               # per step: (ids, versions expected, deleted ids) at its GETs
+    batches = []
+    for k in range(steps):
+        ids = wl.sample_ids(20000, 300 + k)
+        up = torch.cat([wl.sample_ids(1500, 500 + k), wl.uniform_ids(1500, 700 + k)])
+        truth_at.append((ids.tolist(), list(version), set(deleted)))
+        b = _compact(wl.set_batch(up, version=k + 1))
+        batches.append(b)
+        r = sc.serve(wl.digests.index_select(0, ids).contiguous(), b)
+        results.append(r)
+        for i in up.tolist():
+            version[i] = k + 1
+            deleted.discard(i)
+        if k % 3 == 2:          # a DELETE between steps (joins the pending chain)
+            dels = wl.sample_ids(300, 900 + k).unique()
+            sc.delete(wl.digests.index_select(0, dels).contiguous())
+            deleted |= set(dels.tolist())
+    torch.cuda.synchronize()
+    pool = wl.pool.cpu().numpy()
+    vlen = wl.vlen.cpu().tolist()
+    offs = {}
+
+    def truth(i, v):
+        if (i, v) not in offs:
+            offs[(i, v)] = int(wl._offsets(torch.tensor([i], device=cuda_dev), v)[0])
+        o = offs[(i, v)]
+        return pool[o: o + vlen[i]].tobytes()
+
+    stale = dead = hits = 0
+    for (ids, ver, gone), r in zip(truth_at, results):
+        for i, x in zip(ids, unpack_records(r.data, r.off, r.size)):
+            if x is None:
+                continue
+            hits += 1
+            if i in gone:
+                dead += 1
+            elif x[0] != truth(i, ver[i]):
+                stale += 1
+    c1 = sc.counters()
+    assert stale == 0 and dead == 0, (stale, dead, hits)
+    assert hits > steps * 20000 // 2
+    assert c1["reinserted"] > c0["reinserted"]
+
+
+def test_serve_waits_for_a_batch_the_caller_is_still_producing(cuda_dev):
+    """The SET batch is finished on the caller's stream right before serve() (behind a slow
+    kernel): the SET chain and the early hand must not read it before then. A later get()
+    returns the new values of every key the batch set."""
+    from shellac_amd.bench.workload import Workload
+    from shellac_amd.models.sharded_cache import ShardedCache
+
+    N = 30000
+    wl = Workload(N, cuda_dev, min_val=64, max_val=1024)
+    sc = ShardedCache(CacheShard(8 << 20, 1 << 15, 1 << 13, cuda_dev))  # ~11 MB of records
+    for s0 in range(0, N, 5000):
+        sc.set(_compact(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
+    keys = wl.digests.index_select(0, wl.sample_ids(8000, 5)).contiguous()
+    for k in range(3):   # the log is overfilled: every step runs the hand
+        sc.serve(keys, _compact(wl.set_batch(wl.uniform_ids(2000, 40 + k))))
+    ids = wl.uniform_ids(2000, 77).unique()
+    real = _compact(wl.set_batch(ids, version=5))
+    # the batch the caller passes: zero keys and values until a slow producer on the
+    # current stream writes them, queued right before serve()
+    b = dataclasses.replace(real, keys=torch.zeros_like(real.keys),
+                            values=torch.zeros_like(real.values))
+    torch.cuda.synchronize()
+    torch.cuda._sleep(20_000_000)      # ~10 ms of GPU time ahead of the copies
+    b.keys.copy_(real.keys)
+    b.values.copy_(real.values)
+    sc.serve(keys, b)
+    del b                              # the cache keeps what its chain still reads
+    g = sc.get(wl.digests.index_select(0, ids).contiguous())
+    torch.cuda.synchronize()
+    pool = wl.pool.cpu().numpy()
+    vlen = wl.vlen.cpu().tolist()
+    offs = wl._offsets(ids, 5).cpu().tolist()
+    recs = unpack_records(g.data, g.off, g.size)
+    got = sum(1 for i, o, x in zip(ids.tolist(), offs, recs)
+              if x is not None and x[0] == pool[o: o + vlen[i]].tobytes())
+    assert got == len(recs), (got, len(recs))
 
 
 @pytest.mark.parametrize("fence", ["system", "device", "none"])
