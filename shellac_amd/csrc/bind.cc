@@ -120,13 +120,17 @@ PYBIND11_MODULE(_shellac_core, m) {
                     S(s), done_slot);
       }, py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
          py::arg("now"), py::arg("stream"), py::arg("done_slot") = -1)
+      // ordered after `stream` (the caller's current stream; 0 = the null stream): the
+      // resident server runs on no stream, so what the caller queued to fill `out` / `off`
+      // (or the keys' SETs) lands before the job is queued
       .def("serve_get", [](HbmCache& c, uintptr_t host_keys, int64_t n, uintptr_t out,
-                           uint64_t out_cap, uintptr_t off, uint32_t now, int done_slot) {
+                           uint64_t out_cap, uintptr_t off, uint32_t now, int done_slot,
+                           uintptr_t stream) {
         py::gil_scoped_release nogil;
-        return c.serve_get(P<const Digest>(host_keys), n, P<uint8_t>(out), out_cap,
-                           P<uint64_t>(off), now, done_slot);
+        return c.serve_get_after(S(stream), P<const Digest>(host_keys), n, P<uint8_t>(out),
+                                 out_cap, P<uint64_t>(off), now, done_slot);
       }, py::arg("host_keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
-         py::arg("now"), py::arg("done_slot"))
+         py::arg("now"), py::arg("done_slot"), py::arg("stream") = 0)
       .def("serve_wait", [](HbmCache& c, int slot, int64_t timeout_ms) {
         py::gil_scoped_release nogil;
         return c.serve_wait(slot, timeout_ms);

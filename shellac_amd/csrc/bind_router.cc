@@ -5,6 +5,7 @@
 
 #include "bind_parts.h"
 #include "hbm_cache.h"
+#include "host_router.h"
 #include "router.h"
 #include "step_comm.h"
 
@@ -100,6 +101,34 @@ void bind_router(py::module_& m) {
                            hipSuccess))
       throw Error("stream_copy_from_host failed");
   });
+
+  // The host request router (host_router.h); host pointers as ints.
+  py::class_<HostRouter>(m, "HostRouter")
+      .def(py::init<int, int>(), py::arg("nshards"), py::arg("points_per_shard") = 160)
+      .def_property_readonly("nshards", &HostRouter::nshards)
+      .def_property_readonly("nhot", &HostRouter::nhot)
+      .def_property_readonly("cumulative", &HostRouter::cumulative)
+      .def("owner", [](const HostRouter& r, uint64_t lo, uint64_t hi) {
+        return r.owner(Digest{lo, hi});
+      })
+      .def("set_hot", [](HostRouter& r, uintptr_t hot, int64_t n, std::vector<double> w) {
+        SH_CHECK((int)w.size() == r.nshards(), "one spray weight per shard");
+        py::gil_scoped_release nogil;
+        r.set_hot(P<const Digest>(hot), n, w.data());
+      })
+      .def("route_gets", [](const HostRouter& r, uintptr_t keys, int64_t n, uint64_t seq0,
+                            uintptr_t dest, uintptr_t counts, int threads) {
+        py::gil_scoped_release nogil;
+        r.route_gets(P<const Digest>(keys), n, seq0, P<int32_t>(dest), P<int64_t>(counts),
+                     threads);
+      }, py::arg("keys"), py::arg("n"), py::arg("seq0"), py::arg("dest"), py::arg("counts"),
+         py::arg("threads") = 1)
+      .def("route_sets", [](const HostRouter& r, uintptr_t keys, int64_t n, uintptr_t dest,
+                            uintptr_t counts, int threads) {
+        py::gil_scoped_release nogil;
+        r.route_sets(P<const Digest>(keys), n, P<int32_t>(dest), P<int64_t>(counts), threads);
+      }, py::arg("keys"), py::arg("n"), py::arg("dest"), py::arg("counts"),
+         py::arg("threads") = 1);
 
   m.def("step_streams", [](int device) {
     const StepStreams& ss = step_streams(device);

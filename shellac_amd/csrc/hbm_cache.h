@@ -117,6 +117,11 @@ class HbmCache {
   static constexpr int kServeRing = 16;
   bool serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
                  uint64_t* off, uint32_t now, int done_slot);
+  // The same, ordered after the work queued so far on stream `after` (the caller's: what
+  // it queued to fill `out` / `off` or the keys' SETs): an event recorded there is
+  // host-polled before the job is queued, so the stream-less server never races it.
+  bool serve_get_after(hipStream_t after, const Digest* host_keys, int64_t n, uint8_t* out,
+                       uint64_t out_cap, uint64_t* off, uint32_t now, int done_slot);
   void serve_kick();
   // server jobs queued or running (the resident workgroup takes them one at a time: a
   // caller with several batches in flight sends the rest down the launched path)
@@ -330,11 +335,12 @@ class HbmCache {
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                     int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
                     hipEvent_t append_after = nullptr, hipEvent_t append_done = nullptr,
-                    const uint64_t* from = nullptr, hipEvent_t plan_done = nullptr);
+                    const uint64_t* from = nullptr, hipEvent_t plan_done = nullptr,
+                    int64_t nmove = 0);
   void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
-                          const uint64_t* from = nullptr);
+                          const uint64_t* from = nullptr, int64_t nmove = 0);
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------

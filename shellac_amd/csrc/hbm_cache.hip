@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
     int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim,
-    const uint64_t* __restrict__ from) {
+    const uint64_t* __restrict__ from, int64_t r0, int64_t r1) {
   const int l4 = threadIdx.x & 3;
   const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
@@ -1752,7 +1752,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   const int64_t ngroups = ((int64_t)gridDim.x * kBlock) >> 2;
   unsigned long long evicted = 0, bytes = 0, lost = 0, moved_away = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *head_next = head_new;
-  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2; i < n; i += ngroups) {
+  for (int64_t i = r0 + (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 2); i < r1; i += ngroups) {
     if (l4 == 0 && vlen[i] != kSkipVlen) {  // leave the dedupe table clean for the next batch
       const uint32_t sl = slot_of[i];
       dd_keys[sl] = 0ull;
@@ -3269,6 +3269,33 @@ bool HbmCache::serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint6
   return true;
 }
 
+bool HbmCache::serve_get_after(hipStream_t after, const Digest* host_keys, int64_t n,
+                               uint8_t* out, uint64_t out_cap, uint64_t* off, uint32_t now,
+                               int done_slot) {
+  if (n < 1 || n > kServeKeys || done_slot < 0 || done_slot >= kHostSlots) return false;
+  {
+    // one event per thread and device (the proxy's reactors and test threads submit
+    // concurrently); polled, not synchronised (no yield on the submission path)
+    DeviceGuard g(cfg_.device);
+    thread_local hipEvent_t ev[64] = {};
+    SH_CHECK(cfg_.device >= 0 && cfg_.device < 64, "device out of range");
+    hipEvent_t& e = ev[cfg_.device];
+    if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(e, after));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      const hipError_t q = hipEventQuery(e);
+      if (q == hipSuccess) break;
+      SH_CHECK(q == hipErrorNotReady, std::string("event query failed: ") + hipGetErrorString(q));
+      if ((spin & 1023) == 1023)
+        SH_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(30),
+                 "timed out waiting for the caller's stream before an edge job");
+      __builtin_ia32_pause();
+    }
+  }
+  return serve_get(host_keys, n, out, out_cap, off, now, done_slot);
+}
+
 void HbmCache::serve_kick() {
   std::lock_guard<std::mutex> lk(srv_mu_);
   if (srv_running_ && __atomic_load_n(srv_ctl_ + kCtlExited, __ATOMIC_ACQUIRE) != srv_epoch_)
@@ -3340,7 +3367,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     hand_w_ = 0;
     const HandBuf& hb = hb_[hand_b_];
     store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
-                 index_after, append_after, append_done, hb.from, plan_done);
+                 index_after, append_after, append_done, hb.from, plan_done, w);
     hsel_ ^= 1;
     return;
   }
@@ -3368,7 +3395,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     const HandBuf& hb = hb_[hand_b_];
     store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
-                 index_after, append_after, append_done, hb.from, plan_done);
+                 index_after, append_after, append_done, hb.from, plan_done, w);
   } else if (n <= kSmallSetRows && !index_after && !append_after && !append_done &&
              !plan_done) {
     // one launch for the whole chain (the proxy's small SET batches)
@@ -3397,7 +3424,7 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
                             const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                             int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
                             hipEvent_t append_after, hipEvent_t append_done,
-                            const uint64_t* from, hipEvent_t plan_done) {
+                            const uint64_t* from, hipEvent_t plan_done, int64_t nmove) {
   store_plan_locked(keys, vlen, n, s);
   if (plan_done) HIP_OK(hipEventRecord(plan_done, s));
   if (append_after) HIP_OK(hipStreamWaitEvent(s, append_after, 0));
@@ -3405,7 +3432,7 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
                     cfg_.log_bytes);
   HIP_OK(hipGetLastError());
   if (append_done) HIP_OK(hipEventRecord(append_done, s));
-  store_index_locked(keys, vlen, expire, n, now, s, index_after, from);
+  store_index_locked(keys, vlen, expire, n, now, s, index_after, from, nmove);
 }
 
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,
@@ -3429,14 +3456,23 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
 
 void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
                                   const uint32_t* expire, int64_t n, uint32_t now, hipStream_t s,
-                                  hipEvent_t index_after, const uint64_t* from) {
+                                  hipEvent_t index_after, const uint64_t* from, int64_t nmove) {
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
-  const int igrid = grid_for(n * 4, kBlock, kMaxGrid);
-  hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
-                     vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
-                     cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_, ctr_,
-                     set_claim_, from);
+  // A combined batch's reinsertions (rows [0, nmove), moves) land in a launch of their own
+  // before the batch's rows: a batch row may claim the slot of an item this batch's append
+  // overwrites as dead, and must not take a reinserted item's entry from under its move
+  // (the host twin runs the rows in this order too).
+  if (!from) nmove = 0;
+  for (int pass = nmove > 0 ? 0 : 1; pass < 2; ++pass) {
+    const int64_t r0 = pass ? nmove : 0, r1 = pass ? n : nmove;
+    if (r1 <= r0) continue;
+    const int igrid = grid_for((r1 - r0) * 4, kBlock, kMaxGrid);
+    hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
+                       vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
+                       cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_,
+                       ctr_, set_claim_, pass ? (const uint64_t*)nullptr : from, r0, r1);
+  }
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      set_off_, vlen, expire, cur_head(), set_claim_, index_, set_size_, ring_,
                      ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(), next_ring_tail(), set_cnt_,

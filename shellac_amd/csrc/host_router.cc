@@ -1,0 +1,174 @@
+// HostRouter (host_router.h): ketama ownership + hot-object spreading for the host-routed
+// multi-GPU topology.
+#include "host_router.h"
+
+#include <algorithm>
+#include <string>
+#include <thread>
+
+namespace shellac {
+
+namespace {
+constexpr uint64_t kWeyl = 0x9E3779B97F4A7C15ull;  // 2^64 / golden ratio
+constexpr int kPrefetch = 16;                       // requests whose hot-table line is in flight
+}  // namespace
+
+HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, -1) {
+  SH_CHECK(nshards >= 1 && nshards <= 32767 && pps >= 1, "bad router geometry");
+  std::vector<std::pair<uint32_t, int>> pts;
+  for (int i = 0; i < nshards; ++i)
+    for (int j = 0; j < pps; ++j) {  // DigestRing's (and ShardRing's) points
+      const std::string s = "shellac-shard-" + std::to_string(i) + "-" + std::to_string(j);
+      const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+      pts.emplace_back((uint32_t)(d.hi >> 32), i);
+    }
+  std::stable_sort(pts.begin(), pts.end(),
+                   [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
+                     return a.first < b.first;
+                   });
+  for (const auto& p : pts) {
+    pts_.push_back(p.first);
+    own_.push_back(p.second);
+  }
+  // span s = [a, a + 65535]: one owner for all of it iff no point lies in [a, a + 65534]
+  for (uint32_t s = 0; s < 65536; ++s) {
+    const uint32_t a = s << 16, b = a + 65535u;
+    const auto it = std::lower_bound(pts_.begin(), pts_.end(), a);
+    if (it == pts_.end() || *it >= b) tab_[s] = (int16_t)search(b);
+  }
+  cw_.assign((size_t)n_, 0.0);
+  for (int r = 0; r < n_; ++r) cw_[(size_t)r] = (double)(r + 1) / n_;
+  cw_.back() = 1.0;
+}
+
+int HostRouter::search(uint32_t p) const {
+  const auto it = std::lower_bound(pts_.begin(), pts_.end(), p);
+  return own_[it == pts_.end() ? 0 : (size_t)(it - pts_.begin())];
+}
+
+void HostRouter::set_hot(const Digest* hot, int64_t n, const double* w) {
+  nhot_ = 0;
+  hot_tab_.clear();
+  hot_bits_.clear();
+  hot_mask_ = bits_mask_ = 0;
+  if (n <= 0) return;
+  uint64_t slots = 1024;
+  while (slots < 2 * (uint64_t)n) slots <<= 1;
+  hot_tab_.assign(slots, Digest{0, 0});
+  hot_mask_ = slots - 1;
+  uint64_t bits = 1 << 12;
+  while (bits < 16 * (uint64_t)n) bits <<= 1;
+  hot_bits_.assign(bits / 64, 0);
+  bits_mask_ = bits - 1;
+  for (int64_t i = 0; i < n; ++i) {
+    const Digest d = hot[i];
+    if (!d.lo && !d.hi) continue;
+    const uint64_t fb = (d.lo >> 20) & bits_mask_;
+    hot_bits_[fb >> 6] |= 1ull << (fb & 63);
+    for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
+      Digest& e = hot_tab_[s];
+      if (e.lo == d.lo && e.hi == d.hi) break;
+      if (!e.lo && !e.hi) {
+        e = d;
+        ++nhot_;
+        break;
+      }
+    }
+  }
+  double tot = 0;
+  for (int r = 0; r < n_; ++r) {
+    SH_CHECK(w[r] >= 0, "spray weights must be non-negative");
+    tot += w[r];
+  }
+  SH_CHECK(tot > 0, "spray weights sum to zero");
+  double acc = 0;
+  for (int r = 0; r < n_; ++r) {
+    acc += w[r];
+    cw_[(size_t)r] = acc / tot;
+  }
+  cw_.back() = 1.0;
+}
+
+int HostRouter::spray(uint64_t j) const {
+  const double u = (double)((j * kWeyl) >> 11) * (1.0 / 9007199254740992.0);  // 2^-53
+  int r = 0;  // #{cw <= u} over the first n - 1 weights, branch-free (the rank is random)
+  for (int k = 0; k < n_ - 1; ++k) r += cw_[(size_t)k] <= u;
+  return r;
+}
+
+template <bool kSets>
+void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0,
+                             int32_t* dest, int64_t* counts) const {
+  if (!nhot_) {
+    for (int64_t i = a; i < b; ++i) {
+      const int o = owner(keys[i]);
+      dest[i] = o;
+      ++counts[o];
+    }
+    return;
+  }
+  // the filter word and the table line of the requests kPrefetch ahead are prefetched,
+  // so a group's cache misses overlap
+  for (int64_t g = a; g < b; g += kPrefetch) {
+    const int64_t e = std::min<int64_t>(b, g + kPrefetch);
+    for (int64_t i = g + kPrefetch; i < std::min<int64_t>(b, e + kPrefetch); ++i) {
+      const uint64_t lo = keys[i].lo;
+      __builtin_prefetch(&hot_bits_[((lo >> 20) & bits_mask_) >> 6]);
+      __builtin_prefetch(&hot_tab_[lo & hot_mask_]);
+    }
+    for (int64_t i = g; i < e; ++i) {
+      const Digest d = keys[i];
+      if (is_hot(d)) {
+        if (kSets) {
+          dest[i] = -1;
+          for (int r = 0; r < n_; ++r) ++counts[r];
+        } else {
+          const int r = spray(seq0 + (uint64_t)i);
+          dest[i] = r;
+          ++counts[r];
+        }
+      } else {
+        const int o = owner(d);
+        dest[i] = o;
+        ++counts[o];
+      }
+    }
+  }
+}
+
+namespace {
+template <typename F>
+void parallel_ranges(int64_t n, int threads, int nshards, int64_t* counts, F&& f) {
+  if (threads <= 1 || n < (1 << 16)) {
+    f(0, n, counts);
+    return;
+  }
+  threads = (int)std::min<int64_t>(threads, n >> 14);
+  std::vector<std::vector<int64_t>> part((size_t)threads, std::vector<int64_t>((size_t)nshards, 0));
+  std::vector<std::thread> th;
+  const int64_t per = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    const int64_t a = std::min(n, t * per), b = std::min(n, a + per);
+    th.emplace_back([&, t, a, b] { f(a, b, part[(size_t)t].data()); });
+  }
+  for (auto& x : th) x.join();
+  for (const auto& p : part)
+    for (int r = 0; r < nshards; ++r) counts[r] += p[(size_t)r];
+}
+}  // namespace
+
+void HostRouter::route_gets(const Digest* keys, int64_t n, uint64_t seq0, int32_t* dest,
+                            int64_t* counts, int threads) const {
+  parallel_ranges(n, threads, n_, counts, [&](int64_t a, int64_t b, int64_t* c) {
+    route_range<false>(keys, a, b, seq0, dest, c);
+  });
+}
+
+void HostRouter::route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_t* counts,
+                            int threads) const {
+  parallel_ranges(n, threads, n_, counts, [&](int64_t a, int64_t b, int64_t* c) {
+    route_range<true>(keys, a, b, 0, dest, c);
+  });
+}
+
+}  // namespace shellac

@@ -1,0 +1,83 @@
+// Host request router of the host-routed multi-GPU topology: ketama ownership plus
+// hot-object spreading.
+//
+// Reference: the cache client picks the memcached node owning a key by ketama
+// (src/python/shellac/server/Server.py:81-83), so a node receives its keys' true share
+// of the traffic, hot keys included (README.md:30 sells ketama for node loss, not for
+// load). Here each GPU of a node is a ketama node (DigestRing points), and the router
+// adds what a Zipf workload needs on top: the hottest objects are replicated on every
+// GPU (SURVEY.md §5.8 hot-object replication), a GET of one goes to a GPU chosen to
+// even out the load, and a SET of one is written through to every GPU.
+//
+// Decisions are a pure function of (digest, position in the stream), identical to the
+// tensor version in shellac_amd/parallel/hotspread.py (tests check both agree):
+//   owner(d)   first ring point >= ring_position(d) (wrapping), DigestRing's rule; a
+//              65536-entry table answers the 2^16-wide spans no point splits (~98 % of
+//              positions at 8 x 160 points), a binary search the rest.
+//   GET i      hot(d) ? spray(seq0 + i) : owner(d), where spray(j) picks rank r with
+//              probability w_r from a Weyl sequence: u = frac(j * 0x9E3779B97F4A7C15 / 2^64)
+//              (top 53 bits), r = #{cumulative weight <= u}.
+//   SET        hot(d) ? every rank (dest -1) : owner(d).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "digest.h"
+
+namespace shellac {
+
+class HostRouter {
+ public:
+  explicit HostRouter(int nshards, int points_per_shard = 160);
+  int nshards() const { return n_; }
+  int owner(const Digest& d) const {
+    const uint32_t p = ring_position(d);
+    const int16_t t = tab_[p >> 16];
+    return t >= 0 ? t : search(p);
+  }
+  // The replicated hot set (n digests, any order) and the spray weights of its GETs
+  // (`w`: nshards non-negative weights, normalised here). n = 0: no spreading.
+  void set_hot(const Digest* hot, int64_t n, const double* w);
+  int64_t nhot() const { return nhot_; }
+  bool is_hot(const Digest& d) const {
+    if (!nhot_) return false;
+    const uint64_t b = (d.lo >> 20) & bits_mask_;
+    if (!((hot_bits_[b >> 6] >> (b & 63)) & 1)) return false;
+    for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
+      const Digest& e = hot_tab_[s];
+      if (e.lo == d.lo && e.hi == d.hi) return true;
+      if (!e.lo && !e.hi) return false;
+    }
+  }
+  // dest[i] for a GET stream whose first request has stream position seq0; counts[r] +=
+  // requests sent to r. `threads` <= 0: one.
+  void route_gets(const Digest* keys, int64_t n, uint64_t seq0, int32_t* dest, int64_t* counts,
+                  int threads) const;
+  // dest[i] = owner, or -1 (a hot object: every rank); counts[r] += rows rank r stores.
+  void route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_t* counts,
+                  int threads) const;
+  // Cumulative spray weights (nshards doubles, the last exactly 1).
+  const std::vector<double>& cumulative() const { return cw_; }
+
+ private:
+  int search(uint32_t p) const;
+  int spray(uint64_t j) const;
+  template <bool kSets>
+  void route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
+                   int64_t* counts) const;
+  int n_;
+  std::vector<uint32_t> pts_;
+  std::vector<int32_t> own_;
+  std::vector<int16_t> tab_;      // 65536: owner of a span no point splits, else -1
+  std::vector<Digest> hot_tab_;   // open addressing on lo (a hash already), {0, 0} = empty
+  uint64_t hot_mask_ = 0;
+  // a one-hash filter in front of it, 16 bits per hot object (~6 % of cold digests pass):
+  // a cold request then costs no table line
+  std::vector<uint64_t> hot_bits_;
+  uint64_t bits_mask_ = 0;
+  int64_t nhot_ = 0;
+  std::vector<double> cw_;
+};
+
+}  // namespace shellac

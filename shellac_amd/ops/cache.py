@@ -399,16 +399,17 @@ class CacheShard:
         ``keys`` are host digests; returns (out bytes, off[n+1]) once the server has
         published the job's total into ``done_slot``. None when the job could not be
         queued (ring full, n > SERVE_KEYS). Records a concurrent SET overwrote while
-        they were copied come back with a zeroed magic word (treat as misses)."""
+        they were copied come back with a zeroed magic word (treat as misses). The job is
+        ordered after the work queued so far on the current stream (the server runs on no
+        stream: the binding polls an event recorded there before it queues the job)."""
         assert self.is_gpu
         keys = keys.to("cpu").contiguous()
         n = keys.shape[0]
         out = torch.zeros(max(int(out_cap), 16), dtype=torch.uint8, device=self.device)
         off = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
-        torch.cuda.synchronize(self.device)  # the server is on no stream: buffers first
         if not self._impl.serve_get(keys.data_ptr(), n, out.data_ptr(), int(out_cap),
                                     off.data_ptr(), self.now() if now is None else now,
-                                    int(done_slot)):
+                                    int(done_slot), self._s()):
             return None
         self._impl.serve_wait(int(done_slot), int(timeout_ms))
         return out, off

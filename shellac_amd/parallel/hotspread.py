@@ -1,0 +1,238 @@
+"""Hot-object spreading for the host-routed multi-GPU topology.
+
+Reference: the cache client sends every request to the memcached node that owns its key
+by ketama (src/python/shellac/server/Server.py:81-83), so a node takes its keys' true
+share of the traffic — a Zipf hot key loads one node (README.md:30 sells ketama for node
+loss, not for load). SURVEY.md §5.8 asks for hot-object replication over xGMI: here the
+hottest objects live on every GPU, a GET of one goes to a GPU chosen to even out the load
+and a SET of one is written through to every GPU.
+
+Routing decisions are a pure function of (digest, stream position), implemented twice
+with identical results (tests check it): ``route_gets`` / ``route_sets`` below in tensor
+ops (the bench prepares its request batches with them on the GPU) and the native
+``HostRouter`` (csrc/host_router.cc, the host proxy's router, whose throughput the bench
+measures):
+
+* ``owner(d)``: the first ``ShardRing`` point at or after ``ring_position(d)``.
+* a GET at stream position j of a hot object goes to the rank a Weyl sequence picks with
+  the spray weights: u = top 53 bits of (j * 0x9E3779B97F4A7C15 mod 2^64) / 2^53, rank =
+  #{cumulative weight <= u}; every other GET to its owner.
+* a SET of a hot object goes to every rank (dest -1), every other SET to its owner.
+
+The spray weights water-fill the ranks: with L_r the share of the traffic rank r gets as
+the owner of non-hot objects and H the hot share, w_r is proportional to max(0, T - L_r)
+for the level T that spends H, so every rank ends near 1/N when H allows it.
+
+Replicas are ordinary objects of each rank's shard (one lookup, one gather per step; the
+CLOCK hand keeps them, they are the most read objects). ``replicate_hot`` fills them from
+their owners with one all-gather of records (RCCL over xGMI on GPUs, gloo on the CPU).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .._native import core
+from ..ops import routing as R
+from .ring import ShardRing
+
+PHI = 0x9E3779B97F4A7C15 - (1 << 64)   # the Weyl constant as an int64 bit pattern
+_M53 = (1 << 53) - 1
+
+
+def cumulative(weights: Sequence[float]) -> list:
+    """Normalised cumulative weights, computed exactly as HostRouter::set_hot does."""
+    tot = 0.0
+    for w in weights:
+        if w < 0:
+            raise ValueError("spray weights must be non-negative")
+        tot += float(w)
+    if tot <= 0:
+        raise ValueError("spray weights sum to zero")
+    out, acc = [], 0.0
+    for w in weights:
+        acc += float(w)
+        out.append(acc / tot)
+    out[-1] = 1.0
+    return out
+
+
+def spray_ranks(pos: torch.Tensor, cw: torch.Tensor) -> torch.Tensor:
+    """Rank of each stream position (int64) under cumulative weights ``cw`` (float64)."""
+    h = pos * PHI                                   # wraps mod 2^64 (two's complement)
+    u = ((h >> 11) & _M53).to(torch.float64) * (1.0 / (1 << 53))
+    r = torch.searchsorted(cw, u, right=True)
+    return r.clamp_(max=cw.numel() - 1).to(torch.int32)
+
+
+def water_fill(owner_share: Sequence[float], hot_share: float) -> list:
+    """Spray weights that bring every rank's share as close to 1/N as ``hot_share`` allows:
+    w_r proportional to max(0, T - L_r), sum = hot_share."""
+    n = len(owner_share)
+    if hot_share <= 0:
+        return [1.0] * n
+    order = sorted(range(n), key=lambda r: owner_share[r])
+    level, spent = 0.0, 0.0
+    for k in range(1, n + 1):
+        # raise the k lowest ranks to the (k+1)-th lowest share or until H is spent
+        lo = [owner_share[order[i]] for i in range(k)]
+        nxt = owner_share[order[k]] if k < n else float("inf")
+        need = sum(nxt - x for x in lo)
+        if need >= hot_share or k == n:
+            level = (hot_share + sum(lo)) / k
+            break
+    w = [max(0.0, level - owner_share[r]) for r in range(n)]
+    return w if sum(w) > 0 else [1.0] * n
+
+
+def member(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Rows of ``a`` that are rows of ``b`` (digests [n, 2]; ``b`` sorted by lo)."""
+    if a.shape[0] == 0 or b is None or b.shape[0] == 0:
+        return torch.zeros(a.shape[0], dtype=torch.bool, device=a.device)
+    at = torch.searchsorted(b[:, 0].contiguous(), a[:, 0].contiguous())
+    at = torch.clamp(at, max=b.shape[0] - 1)
+    return (b.index_select(0, at) == a).all(dim=1)
+
+
+class HotSpread:
+    """The host-routed topology's routing state: the ketama ring over ``world`` GPUs, the
+    replicated hot set and its spray weights, as tensors (device routing) and as the
+    native ``HostRouter`` (host routing)."""
+
+    def __init__(self, world: int, device, points_per_shard: int = 160):
+        self.world = world
+        self.device = torch.device(device)
+        self.ring = ShardRing(list(range(world)), points_per_shard)
+        self.pts, self.own = self.ring.tensors(self.device)
+        self.router = core().HostRouter(world, points_per_shard)
+        self.hot: Optional[torch.Tensor] = None     # [h, 2] sorted by lo
+        self.weights = [1.0] * world
+        self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
+
+    # -- decisions -----------------------------------------------------------------
+    def owners(self, keys: torch.Tensor) -> torch.Tensor:
+        return R.route(keys.contiguous(), self.pts, self.own, self.world)[0]
+
+    def is_hot(self, keys: torch.Tensor) -> torch.Tensor:
+        return member(keys, self.hot)
+
+    def route_gets(self, keys: torch.Tensor, seq0: int = 0) -> torch.Tensor:
+        """dest int32 [n] for a GET stream starting at stream position ``seq0``."""
+        dest = self.owners(keys)
+        if self.hot is None:
+            return dest
+        pos = torch.arange(keys.shape[0], dtype=torch.int64, device=keys.device) + int(seq0)
+        return torch.where(self.is_hot(keys), spray_ranks(pos, self.cw.to(keys.device)), dest)
+
+    def route_sets(self, keys: torch.Tensor) -> torch.Tensor:
+        """dest int32 [n]: the owner, or -1 (a hot object: every rank stores it)."""
+        dest = self.owners(keys)
+        if self.hot is None:
+            return dest
+        return torch.where(self.is_hot(keys), torch.full_like(dest, -1), dest)
+
+    # -- the hot set -----------------------------------------------------------------
+    @staticmethod
+    def top_keys(sample: torch.Tensor, k: int) -> torch.Tensor:
+        """The k digests requested most often in ``sample`` (ties by digest order), sorted
+        by lo: identical on every rank that sees the same sample."""
+        if k <= 0 or sample.shape[0] == 0:
+            return sample[:0]
+        ulo, inv, cnt = torch.unique(sample[:, 0].contiguous(), return_inverse=True,
+                                     return_counts=True)
+        uniq = torch.empty((ulo.numel(), 2), dtype=torch.int64, device=sample.device)
+        uniq[inv] = sample
+        order = torch.sort(-cnt, stable=True).indices[:k]
+        top = uniq.index_select(0, order)
+        return top.index_select(0, torch.argsort(top[:, 0])).contiguous()
+
+    def plan(self, sample: torch.Tensor, k: int) -> dict:
+        """Pick the hot set (top ``k`` of an observed GET sample) and water-fill the spray
+        weights from the same sample. Returns the sample's shares."""
+        hot = self.top_keys(sample, k)
+        n = max(sample.shape[0], 1)
+        hmask = member(sample, hot)
+        own = self.owners(sample).long()
+        owner_share = torch.bincount(own[~hmask], minlength=self.world).double() / n
+        hshare = float(hmask.float().mean()) if sample.shape[0] else 0.0
+        w = water_fill(owner_share.tolist(), hshare)
+        self.set_hot(hot, w)
+        return {"hot_share": hshare, "owner_share": owner_share.tolist(), "weights": w}
+
+    def set_hot(self, hot: Optional[torch.Tensor], weights: Optional[Sequence[float]] = None):
+        if hot is None or hot.shape[0] == 0:
+            self.hot, self.weights = None, [1.0] * self.world
+            self.router.set_hot(0, 0, self.weights)
+        else:
+            self.hot = hot.index_select(0, torch.argsort(hot[:, 0])).contiguous().to(self.device)
+            self.weights = list(weights) if weights is not None else [1.0] * self.world
+            h = self.hot.cpu().contiguous()
+            self.router.set_hot(h.data_ptr(), h.shape[0], self.weights)
+        self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
+
+    # -- the native router ---------------------------------------------------------------
+    def host_route_gets(self, keys_host: torch.Tensor, seq0: int = 0, threads: int = 1):
+        """The native router on host digests: (dest int32 [n], counts int64 [world])."""
+        keys_host = keys_host.contiguous()
+        dest = torch.empty(keys_host.shape[0], dtype=torch.int32)
+        counts = torch.zeros(self.world, dtype=torch.int64)
+        self.router.route_gets(keys_host.data_ptr(), keys_host.shape[0], int(seq0),
+                               dest.data_ptr(), counts.data_ptr(), int(threads))
+        return dest, counts
+
+    def host_route_sets(self, keys_host: torch.Tensor, threads: int = 1):
+        keys_host = keys_host.contiguous()
+        dest = torch.empty(keys_host.shape[0], dtype=torch.int32)
+        counts = torch.zeros(self.world, dtype=torch.int64)
+        self.router.route_sets(keys_host.data_ptr(), keys_host.shape[0], dest.data_ptr(),
+                               counts.data_ptr(), int(threads))
+        return dest, counts
+
+
+def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, world: int,
+                  group=None, now: Optional[int] = None) -> int:
+    """Collective: every rank stores, as ordinary objects of its shard, the hot objects it
+    does not own, fetched from their owners — each owner looks its hot objects up and
+    gathers their records, one all-gather moves them (RCCL over xGMI between GPUs, gloo
+    between CPU ranks). ``cache`` is the rank's local (unrouted) ShardedCache, ``owner``
+    the owner rank of each hot digest. Returns the objects this rank stored."""
+    from ..models.sharded_cache import GetResult, records_to_set_batch
+
+    dev = hot.device
+    mine = hot[owner.to(dev) == rank].contiguous()
+    sh = cache.shard
+    cache.sync_sets()
+    lk = sh.lookup(mine, now)
+    n = mine.shape[0]
+    data = sh.gather(lk)
+    nbytes = int(lk.off[n])
+    meta = torch.tensor([n, nbytes], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    m = torch.stack(metas).cpu()
+    maxn, maxb = int(m[:, 0].max()), int(m[:, 1].max())
+    # fixed-size blocks per rank: [keys | off | size] rows and the record bytes
+    rows = torch.zeros((max(maxn, 1), 4), dtype=torch.int64, device=dev)
+    rows[:n, :2] = mine
+    rows[:n, 2] = lk.off[:n]
+    rows[:n, 3] = lk.size[:n]
+    recs = torch.zeros(max(maxb, 16), dtype=torch.uint8, device=dev)
+    recs[:nbytes] = data[:nbytes]
+    all_rows = [torch.empty_like(rows) for _ in range(world)]
+    all_recs = [torch.empty_like(recs) for _ in range(world)]
+    dist.all_gather(all_rows, rows, group=group)
+    dist.all_gather(all_recs, recs, group=group)
+    stored = 0
+    for p in range(world):
+        cnt = int(m[p, 0])
+        if p == rank or cnt == 0:
+            continue
+        r = all_rows[p][:cnt]
+        res = GetResult(all_recs[p], r[:, 2].contiguous(), r[:, 3].contiguous())
+        sb = records_to_set_batch(r[:, :2].contiguous(), res)
+        cache.set(sb, now)
+        stored += int((r[:, 3] > 0).sum())
+    cache.sync_sets()
+    return stored

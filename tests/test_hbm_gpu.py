@@ -640,17 +640,16 @@ def test_serve_blocks_answer_concurrent_submitters(cuda_dev, blocks):
     assert shard._impl.serve_blocks == blocks
     keys = [f"/blk/{i}".encode() for i in range(2000)]
     vals = [bytes([i % 251 + 1]) * (64 + i * 7 % 4000) for i in range(2000)]
-    shard.set_many(keys, vals)
-    torch.cuda.synchronize()
+    shard.set_many(keys, vals)   # (the jobs are ordered after it on the null stream)
     errors = []
 
     def worker(t):
+        # the zero fills are queued on this thread's current stream and not waited for:
+        # serve_get orders the job after them (a fill landing after the server wrote a
+        # job's answer would wipe it)
         out = torch.zeros(1 << 18, dtype=torch.uint8, device=cuda_dev)
         off = torch.zeros(32, dtype=torch.int64, device=cuda_dev)
-        # the server is on no stream: the zero fills must land before it writes a job's
-        # answer (a fill still queued behind the first job overwrote it: job 0 came back
-        # empty now and then)
-        torch.cuda.synchronize(cuda_dev)
+        stream = torch.cuda.current_stream(cuda_dev).cuda_stream
         slot = 20 + t
         try:
             for j in range(150):
@@ -658,7 +657,7 @@ def test_serve_blocks_answer_concurrent_submitters(cuda_dev, blocks):
                 ids = [(t * 331 + j * 17 + k * 101) % 2000 for k in range(n)]
                 dh = digest_strings([keys[i] for i in ids], "cpu").contiguous()
                 while not shard._impl.serve_get(dh.data_ptr(), n, out.data_ptr(), out.numel(),
-                                                off.data_ptr(), shard.now(), slot):
+                                                off.data_ptr(), shard.now(), slot, stream):
                     pass  # this block's ring is full: retry
                 total = shard._impl.serve_wait(slot, 10000)
                 o, f = out[:total].cpu(), off[:n + 1].cpu()
@@ -675,6 +674,40 @@ def test_serve_blocks_answer_concurrent_submitters(cuda_dev, blocks):
         th.join()
     assert not errors, errors[:5]
     assert shard._impl.serve_jobs == 8 * 150
+
+
+def test_serve_get_orders_after_a_side_stream_fill(cuda_dev):
+    """The response buffers are zero-filled on a side stream that is still busy (a slow
+    kernel ahead of the fill) and the job is submitted at once from that stream: the
+    stream-less server must answer after the fill, so the answer survives."""
+    shard = CacheShard(16 << 20, 1 << 12, 1 << 14, cuda_dev)
+    keys = [f"/ord/{i}".encode() for i in range(29)]
+    vals = [bytes([i + 1]) * (100 + 37 * i) for i in range(29)]
+    shard.set_many(keys, vals)
+    dh = digest_strings(keys, "cpu").contiguous()
+    side = torch.cuda.Stream(device=cuda_dev)
+    side.wait_stream(torch.cuda.current_stream(cuda_dev))
+    for rep in range(3):
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(5_000_000)   # a few ms of work queued ahead of the fills
+            out = torch.full((1 << 16,), 7, dtype=torch.uint8, device=cuda_dev)
+            off = torch.full((30,), -1, dtype=torch.int64, device=cuda_dev)
+            out.zero_()
+            off.zero_()
+            assert shard._impl.serve_get(dh.data_ptr(), 29, out.data_ptr(), out.numel(),
+                                         off.data_ptr(), shard.now(), 6, side.cuda_stream)
+        total = shard._impl.serve_wait(6, 10000)
+        side.synchronize()
+        o, f = out[:total].cpu(), off.cpu()
+        got = unpack_records(o, f[:-1], f[1:] - f[:-1])
+        assert [g[0] if g else None for g in got] == vals, rep
+        # the Python wrapper orders after the current stream the same way
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(2_000_000)
+            r = shard.serve_get(dh)
+        assert r is not None
+        o, f = r[0].cpu(), r[1].cpu()
+        assert [g[0] if g else None for g in unpack_records(o, f[:-1], f[1:] - f[:-1])] == vals
 
 
 def test_serve_get_relaunches_and_sees_new_sets(cuda_dev):
@@ -731,7 +764,7 @@ def test_serve_get_multi_round_jobs_beside_wrapping_sets(cuda_dev):
     dh = da.cpu().contiguous()
     out = torch.zeros(1 << 20, dtype=torch.uint8, device=cuda_dev)
     off = torch.zeros(K + 1, dtype=torch.int64, device=cuda_dev)
-    torch.cuda.synchronize(cuda_dev)  # the zero fills before the (stream-less) server writes
+    cur = torch.cuda.current_stream(cuda_dev).cuda_stream  # serve_get orders after the fills
     side = torch.cuda.Stream(device=cuda_dev)
     hits = torn = 0
     for rnd in range(6):
@@ -742,7 +775,7 @@ def test_serve_get_multi_round_jobs_beside_wrapping_sets(cuda_dev):
                     shard.store(*f)
         for job in range(150):
             assert shard._impl.serve_get(dh.data_ptr(), K, out.data_ptr(), out.numel(),
-                                         off.data_ptr(), shard.now(), 5)
+                                         off.data_ptr(), shard.now(), 5, cur)
             shard._impl.serve_wait(5, 10000)
             o = out.cpu().numpy()
             offs = off.cpu().numpy()
