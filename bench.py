@@ -87,6 +87,19 @@ def parse():
                          "RCCL communicator (every collective call of the N-GPU step; all keys "
                          "are local, so no interconnect traffic) — a rehearsal, not a scaling "
                          "number")
+    ap.add_argument("--spread", type=int, default=None,
+                    help="host-routed N>1: hot objects replicated on every GPU (the top of an "
+                         "observed GET sample), their GETs sprayed over the GPUs to even out "
+                         "the load and their SETs written through to every GPU (0 = off; "
+                         "default 65536)")
+    ap.add_argument("--spread-sample", type=int, default=1 << 22,
+                    help="GET requests of the observed sample that picks the hot set")
+    ap.add_argument("--sim-rank", type=int, default=-1,
+                    help="--simulate-world N --route host: the rank to simulate (default: the "
+                         "most loaded one under the routing in force)")
+    ap.add_argument("--route-threads", type=int, default=0,
+                    help="threads of the measured host router (0: the CPUs this process may "
+                         "use, at most 16, the box's share of one GPU)")
     ap.add_argument("--route", choices=["host", "device"], default=None,
                     help="N>1 ranks: 'host' — requests reach the GPU that owns their key (ketama "
                          "on the host proxy, as the HTTP path's HbmBackend routes; GPUs exchange "
@@ -362,9 +375,13 @@ def main():
     if host_route:
         from shellac_amd.parallel.exchange import LocalComm
 
-        args.replicate = 0  # nothing is remote: no replica tier
+        args.replicate = 0  # no device-routed replica tier (hot objects: --spread)
         # the rank's cache never routes (group=None would mean the world group here)
         group = LocalComm()
+        if args.spread is None:
+            args.spread = 1 << 16
+    else:
+        args.spread = 0
     if routed1:
         args.replicate = 0  # one rank owns every key: the replica tier is never consulted
     if bounce and not host_route:
@@ -385,17 +402,87 @@ def main():
     t_setup = time.perf_counter()
     wl = Workload(total_keys, dev, zipf_s=args.zipf, min_val=args.min_val, max_val=args.max_val)
     sim_map = simulated_world_map(wl, sim, dev) if msim else None
-    owner_of = mine = None
+    owner_of = mine = spread = None
+    me = rank
+    route_info = {}
     if host_route:
-        from shellac_amd.ops import routing as R
-        from shellac_amd.parallel.ring import ShardRing
+        # The host proxies' routing (HostRouter; its tensor twin prepares the batches here):
+        # one global request stream per step, N x --batch GETs and N x --sets SETs drawn
+        # with the same seeds on every rank, of which each rank serves what the router sends
+        # it — its keys' true ketama share, hot objects sprayed when --spread is on
+        from shellac_amd.parallel.hotspread import HotSpread, member, water_fill
 
-        pts, own = ShardRing(list(range(world)), 160).tensors(dev)
-        owner_of = R.route(wl.digests, pts, own, world)[0].long()
-        mine = torch.nonzero(owner_of == rank).flatten().contiguous()
+        spread = HotSpread(world, dev)
+        owner_of = spread.owners(wl.digests).long()
+        # (at most 1/64 of the key space: every GPU holds the replicas on top of its share)
+        args.spread = min(args.spread, total_keys // 64)
+        if args.spread > 0:
+            sample = wl.sample_ids(args.spread_sample, 8800)   # the observed stream
+            u, cnt = torch.unique(sample, return_counts=True)
+            order = torch.sort(-cnt, stable=True).indices[: args.spread]
+            hot_ids = u.index_select(0, order)
+            hmask = torch.zeros(total_keys, dtype=torch.bool, device=dev)
+            hmask[hot_ids] = True
+            hs = hmask.index_select(0, sample)
+            owner_share = (torch.bincount(owner_of.index_select(0, sample[~hs]), minlength=world)
+                           .double() / sample.numel())
+            hot_share = float(hs.float().mean())
+            spread.set_hot(wl.digests.index_select(0, hot_ids),
+                           water_fill(owner_share.tolist(), hot_share))
+            route_info.update(spread_hot_objects=int(hot_ids.numel()),
+                              spread_hot_share_of_gets=round(hot_share, 4),
+                              spread_weights=[round(x, 5) for x in spread.weights])
+            del sample, hs
+        else:
+            hmask = None
+
+        def global_batch(p):
+            """Batch pair p of the global stream, routed: (GET ids, GET dest, SET ids,
+            SET dest) — dest -1 = every rank (a hot object's SET)."""
+            g = wl.sample_ids(world * args.batch, 1000 + 97 * p)
+            gd = spread.route_gets(wl.digests.index_select(0, g), seq0=p * world * args.batch)
+            pick_ = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
+            st = pick_(world * args.sets, 5000 + 97 * p)
+            sd = spread.route_sets(wl.digests.index_select(0, st))
+            return g, gd, st, sd
+
+        # per-rank requests of the first batch pair: the shares, and the rank a simulation runs
+        g0, gd0, st0, sd0 = global_batch(0)
+        load = (torch.bincount(gd0.long(), minlength=world) +
+                torch.bincount(sd0[sd0 >= 0].long(), minlength=world) +
+                int((sd0 < 0).sum())).double()
+        if sim:
+            me = int(torch.argmax(load)) if args.sim_rank < 0 else args.sim_rank
+        route_info.update(rank_requests_share=[round(x, 5) for x in (load / load.sum()).tolist()],
+                          rank_share_max_over_mean=round(float(load.max() / load.mean()), 4))
+        # the native router on the same stream (host memory), timed: what the host proxies
+        # can feed
+        import time as _t
+
+        kh = wl.digests.index_select(0, g0).cpu().contiguous()
+        th = args.route_threads or min(16, len(os.sched_getaffinity(0)))
+        rates = {}
+        for t_ in sorted({1, th}):
+            best = float("inf")
+            for _ in range(3):
+                t0_ = _t.perf_counter()
+                hd, _hc = spread.host_route_gets(kh, seq0=0, threads=t_)
+                best = min(best, _t.perf_counter() - t0_)
+            rates[t_] = kh.shape[0] / best
+        route_info.update(host_route_threads=th,
+                          host_route_req_per_s=round(rates[th], 1),
+                          host_route_req_per_s_one_thread=round(rates[1], 1),
+                          host_route_agrees_with_device=bool(torch.equal(hd, gd0.cpu())))
+        del kh, g0, gd0, st0, sd0
+        mine = torch.nonzero(owner_of == me).flatten().contiguous()
+        if hmask is not None:   # replicas: hot objects this rank does not own
+            rep_ids = torch.nonzero(hmask & (owner_of != me)).flatten().contiguous()
+        else:
+            rep_ids = None
     nb = 1
     shard_keys = (int(sim_map["mine"].numel()) if msim else
-                  int(mine.numel()) if host_route else args.keys_per_gpu)
+                  int(mine.numel()) + (int(rep_ids.numel()) if rep_ids is not None else 0)
+                  if host_route else args.keys_per_gpu)
     while nb < shard_keys:  # ~25% slot load with 4-entry buckets (HBM is plentiful)
         nb *= 2
     log_bytes = int(args.log_gb * (1 << 30)) // 16 * 16
@@ -428,11 +515,27 @@ def main():
     lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
     # (the simulated rank and a host-routed rank fill what they own)
     fill_ids = sim_map["mine"] if msim else mine
-    for s in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
-        ids = (fill_ids[s: s + chunk] if fill_ids is not None else
-               torch.arange(s, min(s + chunk, hi), device=dev))
-        sc.set(wl.set_batch(ids))
-    sync()
+
+    def populate(cache):
+        n_own = int(fill_ids.numel()) if fill_ids is not None else hi - lo
+        for s0 in range(0, n_own, chunk):
+            ids = (fill_ids[s0: s0 + chunk] if fill_ids is not None else
+                   torch.arange(lo + s0, min(lo + s0 + chunk, hi), device=dev))
+            cache.set(wl.set_batch(ids))
+        if host_route and rep_ids is not None and rep_ids.numel():
+            # the hot objects this rank does not own, fetched from their owners
+            if real_world > 1:
+                from shellac_amd.parallel.hotspread import replicate_hot
+
+                hot_d = spread.hot
+                replicate_hot(cache, hot_d, spread.owners(hot_d), rank, world,
+                              group=dist.group.WORLD)
+            else:  # a simulated rank: its peers' copies are the workload's objects
+                for s0 in range(0, int(rep_ids.numel()), chunk):
+                    cache.set(wl.set_batch(rep_ids[s0: s0 + chunk]))
+        sync()
+
+    populate(sc)
     if real_world > 1:
         dist.barrier()
     log(rank, f"[bench] populated {total_keys} keys in {time.perf_counter() - t_setup:.1f}s")
@@ -443,23 +546,19 @@ def main():
     P = max(1, args.batches)
     pick = wl.uniform_ids if args.set_dist == "uniform" else wl.sample_ids
     if host_route:
-        # the global request stream restricted to this rank's keys: what the host proxies'
-        # ketama routing hands this GPU
-        def owned(fn, n, seed):
-            out, got, k = [], 0, 0
-            while got < n:
-                if k > 64:
-                    raise SystemExit(f"[bench] rank {rank} owns too few keys to sample "
-                                     f"{n} requests from (ring imbalance?)")
-                c = fn(n * world + 4096, seed * 7919 + k)
-                c = c[owner_of.index_select(0, c) == rank]
-                out.append(c)
-                got += c.numel()
-                k += 1
-            return torch.cat(out)[:n].contiguous()
-
-        get_ids = [owned(wl.sample_ids, args.batch, 1000 + 97 * rank + i) for i in range(P)]
-        set_ids = [owned(pick, args.sets, 5000 + 97 * rank + i) for i in range(P)]
+        # what the router sends this rank out of each batch pair of the global stream
+        get_ids, set_ids = [], []
+        rank_req = torch.zeros(world, dtype=torch.float64, device=dev)
+        for i in range(P):
+            g, gd, st, sd = global_batch(i)
+            get_ids.append(g[gd == me].contiguous())
+            set_ids.append(st[(sd == me) | (sd < 0)].contiguous())
+            rank_req += (torch.bincount(gd.long(), minlength=world) +
+                         torch.bincount(sd[sd >= 0].long(), minlength=world) +
+                         int((sd < 0).sum())).double()
+            del g, gd, st, sd
+        route_info["rank_requests_per_step"] = [round(x / P) for x in rank_req.tolist()]
+        route_info["rank_share_max_over_mean"] = round(float(rank_req.max() / rank_req.mean()), 4)
     else:
         get_ids = [wl.sample_ids(args.batch, 1000 + 97 * rank + i) for i in range(P)]
         set_ids = [pick(args.sets, 5000 + 97 * rank + i) for i in range(P)]
@@ -516,6 +615,8 @@ def main():
     use_events = dev.type == "cuda"
     rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
 
+    last_rank_ms = []   # each rank's own ms/step of the last timed() (before the barrier)
+
     def timed(steps, first, events=False, cache=None):
         """Run `steps` steps bracketed by barrier + device sync; returns (max-over-ranks
         wall seconds, per-step GPU-event intervals in ms if `events`, last result)."""
@@ -534,6 +635,7 @@ def main():
         if events:
             evs[steps].record(cur)
         sync()
+        own = time.perf_counter() - t0   # this rank's steps, before it waits for the others
         if real_world > 1:
             dist.barrier()
         sync()
@@ -541,6 +643,11 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=rdev)
         if real_world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ot = torch.zeros(max(real_world, 1), dtype=torch.float64, device=rdev)
+        ot[rank if real_world > 1 else 0] = own
+        if real_world > 1:
+            dist.all_reduce(ot)
+        last_rank_ms[:] = [round(x / steps * 1e3, 4) for x in ot.tolist()]
         iv = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if events else []
         return float(t), iv, res
 
@@ -553,6 +660,7 @@ def main():
         gb0 = cache.gathered_bytes
         h0 = shard_.head()
         el, _, res = timed(args.steps, first, cache=cache)
+        rank_ms = list(last_rank_ms)
         gathered = cache.gathered_bytes - gb0
         cache.sync_sets()
         c1 = shard_.counters()
@@ -570,7 +678,8 @@ def main():
         hits, gops, gbytes, rep, greq, rbytes = (int(v) for v in agg.tolist())
         return {"el": el, "res": res, "last": (first + args.steps - 1) % P, "hits": hits,
                 "gops": gops, "gbytes": gbytes, "rep": rep, "greq": greq, "rbytes": rbytes,
-                "head0": h0, "head1": shard_.head(), "gathered": gathered, "c0": c0, "c1": c1}
+                "head0": h0, "head1": shard_.head(), "gathered": gathered, "c0": c0, "c1": c1,
+                "rank_ms": rank_ms}
 
     def check(w):
         """Verify the window's last GET batch against the workload's ground truth (before
@@ -621,6 +730,8 @@ def main():
                 "reinserted_bytes_per_step_per_rank": round(w["rbytes"] / world / args.steps)}
         if fill is not None:
             out_["fill_steps"] = fill
+        if host_route:
+            out_["rank_ms_per_step"] = w["rank_ms"]
         if iv:
             out_["ms_per_step_median_gpu_events"] = median(iv)
         return out_
@@ -785,9 +896,7 @@ def main():
         p_sc.gather_after_append = sc.gather_after_append
         if replica is not None:
             p_sc._hot, p_sc._hot_dir = sc._hot, None
-        for s0 in range(0, shard_keys, chunk) if fill_ids is not None else range(lo, hi, chunk):
-            p_sc.set(wl.set_batch(fill_ids[s0: s0 + chunk] if fill_ids is not None else
-                                  torch.arange(s0, min(s0 + chunk, hi), device=dev)))
+        populate(p_sc)
         p_shard.reserve(max(args.sets * 2, chunk))
         sync()
         if real_world > 1:
@@ -824,7 +933,10 @@ def main():
         parallelism = "shard1 (one GPU, no routing)"
     elif host_route:
         parallelism = (f"shard{world} (host-routed: ketama on the host proxies sends each "
-                       f"request to the GPU owning its key; no GPU-to-GPU value traffic)")
+                       f"request to the GPU owning its key"
+                       + (f", the {args.spread} hottest objects replicated on every GPU and "
+                          f"their GETs sprayed" if args.spread else "") +
+                       "; no GPU-to-GPU value traffic in the step)")
     else:
         parallelism = f"shard{world} (all-to-all routed, {args.comm_mode} communicator mode)"
     out = {
@@ -856,7 +968,13 @@ def main():
             "replicated_hot_objects": args.replicate if world > 1 else 0,
             "routing": ("none" if world == 1 and not sim and not routed1 else
                         "host" if host_route else "device (all-to-all)"),
+            "spread_hot_objects": args.spread if host_route else 0,
         },
+        # host routing (N > 1): each rank's true share of the one global stream (ketama
+        # owners, hot objects sprayed with --spread), the per-rank steps of the headline
+        # window, and the measured rate of the native host router on the box's cores
+        "host_routing": (dict(route_info, simulated_rank=me if sim else None)
+                         if host_route else None),
         # which cache state the headline steps ran in: "log_wrapped" = the steady state of a
         # full cache (every SET batch runs the CLOCK hand), "log_fresh" = before the first wrap
         "headline_phase": "log_wrapped" if headline_wrapped else "log_fresh",

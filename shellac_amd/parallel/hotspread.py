@@ -74,7 +74,7 @@ def water_fill(owner_share: Sequence[float], hot_share: float) -> list:
     if hot_share <= 0:
         return [1.0] * n
     order = sorted(range(n), key=lambda r: owner_share[r])
-    level, spent = 0.0, 0.0
+    level = 0.0
     for k in range(1, n + 1):
         # raise the k lowest ranks to the (k+1)-th lowest share or until H is spent
         lo = [owner_share[order[i]] for i in range(k)]
@@ -201,6 +201,8 @@ def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, worl
     from ..models.sharded_cache import GetResult, records_to_set_batch
 
     dev = hot.device
+    # gloo moves host tensors (a rehearsal of GPU ranks over gloo stages through the host)
+    cdev = (torch.device("cpu") if dist.get_backend(group) == "gloo" else dev)
     mine = hot[owner.to(dev) == rank].contiguous()
     sh = cache.shard
     cache.sync_sets()
@@ -208,17 +210,17 @@ def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, worl
     n = mine.shape[0]
     data = sh.gather(lk)
     nbytes = int(lk.off[n])
-    meta = torch.tensor([n, nbytes], dtype=torch.int64, device=dev)
+    meta = torch.tensor([n, nbytes], dtype=torch.int64, device=cdev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
     m = torch.stack(metas).cpu()
     maxn, maxb = int(m[:, 0].max()), int(m[:, 1].max())
     # fixed-size blocks per rank: [keys | off | size] rows and the record bytes
-    rows = torch.zeros((max(maxn, 1), 4), dtype=torch.int64, device=dev)
+    rows = torch.zeros((max(maxn, 1), 4), dtype=torch.int64, device=cdev)
     rows[:n, :2] = mine
     rows[:n, 2] = lk.off[:n]
     rows[:n, 3] = lk.size[:n]
-    recs = torch.zeros(max(maxb, 16), dtype=torch.uint8, device=dev)
+    recs = torch.zeros(max(maxb, 16), dtype=torch.uint8, device=cdev)
     recs[:nbytes] = data[:nbytes]
     all_rows = [torch.empty_like(rows) for _ in range(world)]
     all_recs = [torch.empty_like(recs) for _ in range(world)]
@@ -229,8 +231,8 @@ def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, worl
         cnt = int(m[p, 0])
         if p == rank or cnt == 0:
             continue
-        r = all_rows[p][:cnt]
-        res = GetResult(all_recs[p], r[:, 2].contiguous(), r[:, 3].contiguous())
+        r = all_rows[p][:cnt].to(dev)
+        res = GetResult(all_recs[p].to(dev), r[:, 2].contiguous(), r[:, 3].contiguous())
         sb = records_to_set_batch(r[:, :2].contiguous(), res)
         cache.set(sb, now)
         stored += int((r[:, 3] > 0).sum())

@@ -45,7 +45,20 @@ def test_bench_cpu_rehearsal_world2(route):
     assert out["config"]["routing"] == ("host" if route == "host" else "device (all-to-all)")
     assert out["config"]["replicated_hot_objects"] == (0 if route == "host" else 4096)
     assert "0 mismatches" in p.stderr
-    assert "check: 0 of 4096 hit records name another key" in p.stderr
+    if route == "host":
+        # each rank serves its true share of the one global stream (unequal batches), hot
+        # objects sprayed: the shares stay within 5 % of the mean, and the native host
+        # router sends every request where the tensor routing did
+        import re
+
+        assert re.search(r"check: 0 of \d+ hit records name another key", p.stderr)
+        hr = out["host_routing"]
+        assert hr["rank_share_max_over_mean"] <= 1.05
+        assert hr["host_route_agrees_with_device"] is True and hr["host_route_req_per_s"] > 0
+        assert hr["spread_hot_objects"] > 0 and len(out["log_fresh"]["rank_ms_per_step"]) == 2
+        assert sum(hr["rank_requests_per_step"]) >= 2 * (4096 + 512)
+    else:
+        assert "check: 0 of 4096 hit records name another key" in p.stderr
 
 
 SMALL = ["--steps", "2", "--warmup", "1", "--device", "cpu", "--batch", "2048", "--sets", "256",

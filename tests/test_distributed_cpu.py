@@ -457,3 +457,79 @@ def test_local_group_never_routes_gloo():
     group=None it would (the default group), and ranks that made different numbers of
     SET calls deadlocked in the first count exchange (seen on a 2-rank GPU rehearsal)."""
     _run_world(_local_worker, 2, timeout=120)
+
+
+def _spread_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import torch
+
+        from shellac_amd.bench.workload import Workload
+        from shellac_amd.models.sharded_cache import ShardedCache
+        from shellac_amd.ops.cache import CacheShard, unpack_records
+        from shellac_amd.parallel.exchange import LocalComm
+        from shellac_amd.parallel.hotspread import HotSpread, replicate_hot, water_fill
+
+        N = 6000 * world
+        wl = Workload(N, "cpu", min_val=16, max_val=512, pool_bytes=1 << 20)
+        hs = HotSpread(world, "cpu")
+        owner = hs.owners(wl.digests).long()
+        # the hot set and spray weights from an observed sample (the same on every rank)
+        sample = wl.sample_ids(50000, 8)
+        u, cnt = torch.unique(sample, return_counts=True)
+        hot_ids = u[torch.sort(-cnt, stable=True).indices[:200]]
+        hmask = torch.zeros(N, dtype=torch.bool)
+        hmask[hot_ids] = True
+        hsamp = hmask[sample]
+        share = torch.bincount(owner[sample[~hsamp]], minlength=world).double() / sample.numel()
+        hs.set_hot(wl.digests[hot_ids], water_fill(share.tolist(), float(hsamp.float().mean())))
+        # a host-routed rank: its own keys, then the hot objects it does not own, fetched
+        # from their owners with one all-gather of records
+        sc = ShardedCache(CacheShard(16 << 20, 1 << 14, 1 << 12, "cpu"), group=LocalComm())
+        sc.set(wl.set_batch(torch.nonzero(owner == rank).flatten()))
+        got = replicate_hot(sc, hs.hot, hs.owners(hs.hot), rank, world)
+        want = int((hmask & (owner != rank)).sum())
+        assert got == want, (got, want)
+        version = torch.zeros(N, dtype=torch.int64)
+        served = torch.zeros(world, dtype=torch.int64)
+        for step in range(3):
+            g = wl.sample_ids(4000 * world, 100 + step)           # one global GET stream
+            gd = hs.route_gets(wl.digests[g], seq0=step * 4000 * world)
+            hd, _ = hs.host_route_gets(wl.digests[g].contiguous(), seq0=step * 4000 * world,
+                                       threads=2)
+            assert torch.equal(gd, hd)
+            st = wl.uniform_ids(300 * world, 200 + step)           # one global SET stream
+            st = torch.cat([st, hot_ids[step::7]])                 # hot objects are updated too
+            sd = hs.route_sets(wl.digests[st])
+            mine_g = g[gd == rank]
+            mine_s = st[(sd == rank) | (sd < 0)]
+            vb = wl.set_batch(mine_s, version=step + 1)
+            r = sc.serve(wl.digests[mine_g].contiguous(), vb)
+            recs = unpack_records(r.data, r.off, r.size)
+            for i, x in zip(mine_g.tolist(), recs):
+                assert x is not None, (step, i)                   # owners and replicas hit
+                assert x[0] == wl.expected_value(i, int(version[i])), (step, i)
+            version[st] = step + 1        # GETs of the next step see this step's SETs
+            served[rank] += mine_g.numel() + mine_s.numel()
+        dist.all_reduce(served)
+        mean = served.double().mean()
+        assert float(served.max() / mean) < 1.08, served.tolist()
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_routed_true_shares_with_hot_spreading_gloo(world):
+    """The host-routed topology end to end on CPU ranks: one global Zipf stream routed by
+    ketama with the hottest objects replicated on every rank (filled from their owners by an
+    all-gather) and their GETs sprayed, their SETs written through everywhere. Every rank
+    serves exactly its share, every GET of it returns the version the SETs of earlier steps
+    left, wherever it was sent, and the ranks' loads stay within a few percent."""
+    _run_world(_spread_worker, world)

@@ -1,0 +1,73 @@
+"""Host-routed topology routing (parallel/hotspread.py, csrc/host_router.cc) on the CPU:
+the native HostRouter and the tensor routing make the same decisions, and spraying the
+hot objects' GETs evens out a Zipf stream's per-rank load."""
+import pytest
+import torch
+
+from shellac_amd.parallel.hotspread import HotSpread, cumulative, spray_ranks, water_fill
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_native_router_matches_tensor_routing(world):
+    g = torch.Generator().manual_seed(world)
+    keys = torch.randint(-2**63, 2**63 - 1, (50000, 2), dtype=torch.int64, generator=g)
+    hs = HotSpread(world, "cpu")
+    stream = keys[torch.randint(0, 3000, (200000,), generator=g)].contiguous()
+    for hot in (None, keys[:300]):
+        w = [1.0 + (r % 3) for r in range(world)]
+        hs.set_hot(hot, w if hot is not None else None)
+        for seq0 in (0, 12345678901):
+            d, c = hs.host_route_gets(stream, seq0=seq0, threads=3)
+            assert torch.equal(d, hs.route_gets(stream, seq0=seq0))
+            assert torch.equal(c, torch.bincount(d.long(), minlength=world))
+        s, c = hs.host_route_sets(stream, threads=2)
+        assert torch.equal(s, hs.route_sets(stream))
+        fan = int((s < 0).sum())
+        assert torch.equal(c, torch.bincount(s[s >= 0].long(), minlength=world) + fan)
+        assert (fan > 0) == (hot is not None and world >= 1)
+    # ownership alone is the ketama ring's (ShardRing, DigestRing)
+    own = hs.owners(stream)
+    for i in range(0, 200000, 20011):
+        lo, hi = int(stream[i, 0]) & (2**64 - 1), int(stream[i, 1]) & (2**64 - 1)
+        assert hs.router.owner(lo, hi) == int(own[i]) == hs.ring.owner_of_digest(lo, hi)
+
+
+def test_spray_follows_the_weights():
+    cw = torch.tensor(cumulative([1.0, 3.0, 0.0, 4.0]), dtype=torch.float64)
+    r = spray_ranks(torch.arange(80000, dtype=torch.int64), cw)
+    share = torch.bincount(r.long(), minlength=4).double() / 80000
+    assert torch.allclose(share, torch.tensor([0.125, 0.375, 0.0, 0.5], dtype=torch.float64),
+                          atol=2e-3)
+
+
+def test_water_fill_levels_the_ranks():
+    own = [0.10, 0.02, 0.20, 0.05]
+    w = water_fill(own, 0.63)
+    tot = sum(w)
+    final = [o + 0.63 * x / tot for o, x in zip(own, w)]
+    assert max(final) - min(final) < 1e-9 and abs(sum(final) - 1.0) < 1e-9
+    # a rank the non-hot traffic already overloads gets no hot traffic
+    w = water_fill([0.6, 0.1, 0.1], 0.2)
+    assert w[0] == 0.0 and abs(w[1] - w[2]) < 1e-12
+
+
+def test_spreading_evens_out_a_zipf_stream():
+    """Zipf(0.99) over 400K keys on 8 ranks: ketama alone leaves the most loaded rank well
+    above the mean (the hot keys' owners); the top 4096 objects sprayed bring it within
+    2 %."""
+    n, world = 400000, 8
+    g = torch.Generator().manual_seed(3)
+    keys = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, generator=g)
+    ranks = torch.arange(1, n + 1, dtype=torch.float64)
+    cdf = torch.cumsum(ranks.pow(-0.99), 0)
+    cdf /= cdf[-1].clone()
+    ids = torch.searchsorted(cdf, torch.rand(2_000_000, generator=g, dtype=torch.float64))
+    stream = keys[ids.clamp_(max=n - 1)]
+    hs = HotSpread(world, "cpu")
+    c0 = torch.bincount(hs.route_gets(stream).long(), minlength=world).double()
+    info = hs.plan(stream[:1_000_000], 4096)
+    c1 = torch.bincount(hs.route_gets(stream[1_000_000:], seq0=1_000_000).long(),
+                        minlength=world).double()
+    assert float(c0.max() / c0.mean()) > 1.1
+    assert float(c1.max() / c1.mean()) < 1.02, (c1 / c1.mean()).tolist()
+    assert info["hot_share"] > 0.3
