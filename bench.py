@@ -94,6 +94,14 @@ def parse():
                          "default 65536)")
     ap.add_argument("--spread-sample", type=int, default=1 << 22,
                     help="GET requests of the observed sample that picks the hot set")
+    ap.add_argument("--spread-policy", choices=["designate", "spray"], default="designate",
+                    help="a hot object's GETs go to one rank designated to even out the load "
+                         "(objects above 1/(4N) of the traffic sprayed), or every hot object's "
+                         "GETs are sprayed over all ranks")
+    ap.add_argument("--ring-points", type=int, default=1024,
+                    help="host routing: ring points per GPU (the per-GPU key-space share, "
+                         "hence the distinct-key work, is within ~5 %% of the mean at 1024 "
+                         "for 8 GPUs, ~12 %% at 160)")
     ap.add_argument("--sim-rank", type=int, default=-1,
                     help="--simulate-world N --route host: the rank to simulate (default: the "
                          "most loaded one under the routing in force)")
@@ -410,29 +418,22 @@ def main():
         # one global request stream per step, N x --batch GETs and N x --sets SETs drawn
         # with the same seeds on every rank, of which each rank serves what the router sends
         # it — its keys' true ketama share, hot objects sprayed when --spread is on
-        from shellac_amd.parallel.hotspread import HotSpread, member, water_fill
+        from shellac_amd.parallel.hotspread import HotSpread, member
 
-        spread = HotSpread(world, dev)
+        spread = HotSpread(world, dev, points_per_shard=args.ring_points)
         owner_of = spread.owners(wl.digests).long()
+        route_info["ring_points_per_gpu"] = args.ring_points
         # (at most 1/64 of the key space: every GPU holds the replicas on top of its share)
         args.spread = min(args.spread, total_keys // 64)
         if args.spread > 0:
-            sample = wl.sample_ids(args.spread_sample, 8800)   # the observed stream
-            u, cnt = torch.unique(sample, return_counts=True)
-            order = torch.sort(-cnt, stable=True).indices[: args.spread]
-            hot_ids = u.index_select(0, order)
-            hmask = torch.zeros(total_keys, dtype=torch.bool, device=dev)
-            hmask[hot_ids] = True
-            hs = hmask.index_select(0, sample)
-            owner_share = (torch.bincount(owner_of.index_select(0, sample[~hs]), minlength=world)
-                           .double() / sample.numel())
-            hot_share = float(hs.float().mean())
-            spread.set_hot(wl.digests.index_select(0, hot_ids),
-                           water_fill(owner_share.tolist(), hot_share))
-            route_info.update(spread_hot_objects=int(hot_ids.numel()),
-                              spread_hot_share_of_gets=round(hot_share, 4),
-                              spread_weights=[round(x, 5) for x in spread.weights])
-            del sample, hs
+            sample = wl.digests.index_select(0, wl.sample_ids(args.spread_sample, 8800))
+            info = spread.plan(sample, args.spread, policy=args.spread_policy)
+            hmask = member(wl.digests, spread.hot)
+            route_info.update(spread_hot_objects=int(spread.hot.shape[0]),
+                              spread_policy=args.spread_policy,
+                              spread_hot_share_of_gets=round(info["hot_share"], 4),
+                              spread_sprayed_objects=info.get("sprayed_objects"))
+            del sample
         else:
             hmask = None
 
@@ -446,15 +447,24 @@ def main():
             sd = spread.route_sets(wl.digests.index_select(0, st))
             return g, gd, st, sd
 
-        # per-rank requests of the first batch pair: the shares, and the rank a simulation runs
+        # per-rank requests and distinct GET keys of the first batch pair: the shares, and
+        # the rank a simulation runs. A step's work is mostly per distinct key (probe, record
+        # copy; duplicates collapse): measured ~0.9 ns per distinct key and ~0.06 per request
+        # (profiles/r5c_hostsim), so the simulated rank is the one with the most of that cost
         g0, gd0, st0, sd0 = global_batch(0)
         load = (torch.bincount(gd0.long(), minlength=world) +
                 torch.bincount(sd0[sd0 >= 0].long(), minlength=world) +
                 int((sd0 < 0).sum())).double()
+        distinct = torch.tensor([float(torch.unique(g0[gd0 == r]).numel()) for r in range(world)],
+                                dtype=torch.float64, device=dev)
+        cost = 0.9 * distinct + 0.06 * load
         if sim:
-            me = int(torch.argmax(load)) if args.sim_rank < 0 else args.sim_rank
+            me = int(torch.argmax(cost)) if args.sim_rank < 0 else args.sim_rank
         route_info.update(rank_requests_share=[round(x, 5) for x in (load / load.sum()).tolist()],
-                          rank_share_max_over_mean=round(float(load.max() / load.mean()), 4))
+                          rank_share_max_over_mean=round(float(load.max() / load.mean()), 4),
+                          rank_distinct_gets=[int(x) for x in distinct.tolist()],
+                          rank_distinct_max_over_mean=round(float(distinct.max() / distinct.mean()), 4),
+                          rank_cost_max_over_mean=round(float(cost.max() / cost.mean()), 4))
         # the native router on the same stream (host memory), timed: what the host proxies
         # can feed
         import time as _t

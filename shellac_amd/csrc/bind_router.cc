@@ -111,11 +111,12 @@ void bind_router(py::module_& m) {
       .def("owner", [](const HostRouter& r, uint64_t lo, uint64_t hi) {
         return r.owner(Digest{lo, hi});
       })
-      .def("set_hot", [](HostRouter& r, uintptr_t hot, int64_t n, std::vector<double> w) {
+      .def("set_hot", [](HostRouter& r, uintptr_t hot, int64_t n, uintptr_t rank,
+                         std::vector<double> w) {
         SH_CHECK((int)w.size() == r.nshards(), "one spray weight per shard");
         py::gil_scoped_release nogil;
-        r.set_hot(P<const Digest>(hot), n, w.data());
-      })
+        r.set_hot(P<const Digest>(hot), n, P<const int32_t>(rank), w.data());
+      }, py::arg("hot"), py::arg("n"), py::arg("rank"), py::arg("weights"))
       .def("route_gets", [](const HostRouter& r, uintptr_t keys, int64_t n, uint64_t seq0,
                             uintptr_t dest, uintptr_t counts, int threads) {
         py::gil_scoped_release nogil;

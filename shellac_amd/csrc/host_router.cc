@@ -46,15 +46,17 @@ int HostRouter::search(uint32_t p) const {
   return own_[it == pts_.end() ? 0 : (size_t)(it - pts_.begin())];
 }
 
-void HostRouter::set_hot(const Digest* hot, int64_t n, const double* w) {
+void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, const double* w) {
   nhot_ = 0;
   hot_tab_.clear();
+  hot_rank_.clear();
   hot_bits_.clear();
   hot_mask_ = bits_mask_ = 0;
   if (n <= 0) return;
   uint64_t slots = 1024;
   while (slots < 2 * (uint64_t)n) slots <<= 1;
   hot_tab_.assign(slots, Digest{0, 0});
+  hot_rank_.assign(slots, kSpray);
   hot_mask_ = slots - 1;
   uint64_t bits = 1 << 12;
   while (bits < 16 * (uint64_t)n) bits <<= 1;
@@ -65,11 +67,17 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const double* w) {
     if (!d.lo && !d.hi) continue;
     const uint64_t fb = (d.lo >> 20) & bits_mask_;
     hot_bits_[fb >> 6] |= 1ull << (fb & 63);
+    const int32_t r = rank ? rank[i] : kSpray;
+    SH_CHECK(r >= kSpray && r < n_, "designated rank out of range");
     for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
       Digest& e = hot_tab_[s];
-      if (e.lo == d.lo && e.hi == d.hi) break;
+      if (e.lo == d.lo && e.hi == d.hi) {
+        hot_rank_[s] = r;
+        break;
+      }
       if (!e.lo && !e.hi) {
         e = d;
+        hot_rank_[s] = r;
         ++nhot_;
         break;
       }
@@ -118,12 +126,13 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     }
     for (int64_t i = g; i < e; ++i) {
       const Digest d = keys[i];
-      if (is_hot(d)) {
+      const int hr = hot_rank(d);
+      if (hr != kNotHot) {
         if (kSets) {
           dest[i] = -1;
           for (int r = 0; r < n_; ++r) ++counts[r];
         } else {
-          const int r = spray(seq0 + (uint64_t)i);
+          const int r = hr >= 0 ? hr : spray(seq0 + (uint64_t)i);
           dest[i] = r;
           ++counts[r];
         }

@@ -14,9 +14,11 @@
 //   owner(d)   first ring point >= ring_position(d) (wrapping), DigestRing's rule; a
 //              65536-entry table answers the 2^16-wide spans no point splits (~98 % of
 //              positions at 8 x 160 points), a binary search the rest.
-//   GET i      hot(d) ? spray(seq0 + i) : owner(d), where spray(j) picks rank r with
-//              probability w_r from a Weyl sequence: u = frac(j * 0x9E3779B97F4A7C15 / 2^64)
-//              (top 53 bits), r = #{cumulative weight <= u}.
+//   GET i      a hot object's GETs go to its designated rank (chosen at the hot set's
+//              refresh to even out the load; every rank holds a replica), or, for the few
+//              objects too hot for one rank, to spray(seq0 + i): rank r with probability w_r
+//              from a Weyl sequence, u = frac(j * 0x9E3779B97F4A7C15 / 2^64) (top 53 bits),
+//              r = #{cumulative weight <= u}. Every other GET to owner(d).
 //   SET        hot(d) ? every rank (dest -1) : owner(d).
 #pragma once
 
@@ -36,20 +38,24 @@ class HostRouter {
     const int16_t t = tab_[p >> 16];
     return t >= 0 ? t : search(p);
   }
-  // The replicated hot set (n digests, any order) and the spray weights of its GETs
-  // (`w`: nshards non-negative weights, normalised here). n = 0: no spreading.
-  void set_hot(const Digest* hot, int64_t n, const double* w);
+  // The replicated hot set (n digests, any order), each object's designated GET rank
+  // (`rank`: n values, -1 = sprayed; null = all sprayed) and the spray weights (`w`:
+  // nshards non-negative weights, normalised here). n = 0: no spreading.
+  void set_hot(const Digest* hot, int64_t n, const int32_t* rank, const double* w);
   int64_t nhot() const { return nhot_; }
-  bool is_hot(const Digest& d) const {
-    if (!nhot_) return false;
+  // kNotHot, kSpray, or the object's designated rank
+  static constexpr int kNotHot = -2, kSpray = -1;
+  int hot_rank(const Digest& d) const {
+    if (!nhot_) return kNotHot;
     const uint64_t b = (d.lo >> 20) & bits_mask_;
-    if (!((hot_bits_[b >> 6] >> (b & 63)) & 1)) return false;
+    if (!((hot_bits_[b >> 6] >> (b & 63)) & 1)) return kNotHot;
     for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
       const Digest& e = hot_tab_[s];
-      if (e.lo == d.lo && e.hi == d.hi) return true;
-      if (!e.lo && !e.hi) return false;
+      if (e.lo == d.lo && e.hi == d.hi) return hot_rank_[s];
+      if (!e.lo && !e.hi) return kNotHot;
     }
   }
+  bool is_hot(const Digest& d) const { return hot_rank(d) != kNotHot; }
   // dest[i] for a GET stream whose first request has stream position seq0; counts[r] +=
   // requests sent to r. `threads` <= 0: one.
   void route_gets(const Digest* keys, int64_t n, uint64_t seq0, int32_t* dest, int64_t* counts,
@@ -71,6 +77,7 @@ class HostRouter {
   std::vector<int32_t> own_;
   std::vector<int16_t> tab_;      // 65536: owner of a span no point splits, else -1
   std::vector<Digest> hot_tab_;   // open addressing on lo (a hash already), {0, 0} = empty
+  std::vector<int32_t> hot_rank_; // per slot: the designated rank, or kSpray
   uint64_t hot_mask_ = 0;
   // a one-hash filter in front of it, 16 bits per hot object (~6 % of cold digests pass):
   // a cold request then costs no table line

@@ -14,14 +14,26 @@ ops (the bench prepares its request batches with them on the GPU) and the native
 measures):
 
 * ``owner(d)``: the first ``ShardRing`` point at or after ``ring_position(d)``.
-* a GET at stream position j of a hot object goes to the rank a Weyl sequence picks with
-  the spray weights: u = top 53 bits of (j * 0x9E3779B97F4A7C15 mod 2^64) / 2^53, rank =
-  #{cumulative weight <= u}; every other GET to its owner.
+* a GET of a hot object goes to its *designated* rank (every rank holds a replica; the
+  designation is made when the hot set is picked, to even out the load), or — for the
+  few objects too hot for one rank — to the rank a Weyl sequence picks at its stream
+  position j with the spray weights: u = top 53 bits of (j * 0x9E3779B97F4A7C15 mod
+  2^64) / 2^53, rank = #{cumulative weight <= u}; every other GET to its owner.
 * a SET of a hot object goes to every rank (dest -1), every other SET to its owner.
 
-The spray weights water-fill the ranks: with L_r the share of the traffic rank r gets as
-the owner of non-hot objects and H the hot share, w_r is proportional to max(0, T - L_r)
-for the level T that spends H, so every rank ends near 1/N when H allows it.
+Why designate instead of spraying every hot object: the serving step collapses duplicate
+requests (GET coalescing), so a rank's work is mostly per *distinct* key (probe, record
+copy) and little per request. Spraying 64K hot objects over 8 GPUs made every GPU probe
+and copy each of them every step — the most loaded simulated rank got slower (0.363 vs
+0.341 ms) although its requests fell from 1.43x to 1.01x the mean (profiles/r5c_hostsim).
+Designation (greedy: hottest first, each to the least loaded rank, starting from the
+ranks' non-hot owner loads) evens out requests without copying any key's work; objects
+above 1/(4N) of the traffic are sprayed, their duplicated work is a handful of keys. The
+per-rank *distinct-key* balance is the ring's key-space balance: more ring points per
+shard (the bench uses 1024: 1.045x, against 1.118x at 160, for 8 shards) even it out.
+
+``water_fill`` (the spray weights' level) is kept for ``policy="spray"``, which sprays
+every hot object.
 
 Replicas are ordinary objects of each rank's shard (one lookup, one gather per step; the
 CLOCK hand keeps them, they are the most read objects). ``replicate_hot`` fills them from
@@ -108,6 +120,7 @@ class HotSpread:
         self.pts, self.own = self.ring.tensors(self.device)
         self.router = core().HostRouter(world, points_per_shard)
         self.hot: Optional[torch.Tensor] = None     # [h, 2] sorted by lo
+        self.hot_rank: Optional[torch.Tensor] = None  # int32 [h]: designated rank, -1 spray
         self.weights = [1.0] * world
         self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
 
@@ -123,8 +136,14 @@ class HotSpread:
         dest = self.owners(keys)
         if self.hot is None:
             return dest
+        h = self.hot
+        at = torch.clamp(torch.searchsorted(h[:, 0].contiguous(), keys[:, 0].contiguous()),
+                         max=h.shape[0] - 1)
+        hot = (h.index_select(0, at) == keys).all(dim=1)
+        hr = self.hot_rank.to(keys.device).index_select(0, at)
         pos = torch.arange(keys.shape[0], dtype=torch.int64, device=keys.device) + int(seq0)
-        return torch.where(self.is_hot(keys), spray_ranks(pos, self.cw.to(keys.device)), dest)
+        sprayed = torch.where(hr >= 0, hr, spray_ranks(pos, self.cw.to(keys.device)))
+        return torch.where(hot, sprayed, dest)
 
     def route_sets(self, keys: torch.Tensor) -> torch.Tensor:
         """dest int32 [n]: the owner, or -1 (a hot object: every rank stores it)."""
@@ -148,28 +167,76 @@ class HotSpread:
         top = uniq.index_select(0, order)
         return top.index_select(0, torch.argsort(top[:, 0])).contiguous()
 
-    def plan(self, sample: torch.Tensor, k: int) -> dict:
-        """Pick the hot set (top ``k`` of an observed GET sample) and water-fill the spray
-        weights from the same sample. Returns the sample's shares."""
-        hot = self.top_keys(sample, k)
+    def plan(self, sample: torch.Tensor, k: int, policy: str = "designate",
+             spray_above: Optional[float] = None) -> dict:
+        """Pick the hot set (top ``k`` of an observed GET sample) and how its GETs are
+        spread, from the same sample. ``policy="designate"``: greedy designation (hottest
+        first, each to the rank with the least load so far, starting from the non-hot owner
+        loads); objects above ``spray_above`` of the traffic (default 1/(4N)) are sprayed
+        evenly. ``policy="spray"``: every hot object sprayed, water-filled weights. Returns
+        the sample's shares and the planned per-rank load."""
         n = max(sample.shape[0], 1)
-        hmask = member(sample, hot)
+        if k <= 0 or sample.shape[0] == 0:
+            self.set_hot(None)
+            return {"hot_share": 0.0}
+        ulo, inv, cnt = torch.unique(sample[:, 0].contiguous(), return_inverse=True,
+                                     return_counts=True)
+        uniq = torch.empty((ulo.numel(), 2), dtype=torch.int64, device=sample.device)
+        uniq[inv] = sample
+        order = torch.sort(-cnt, stable=True).indices[:k]
+        hot, hcnt = uniq.index_select(0, order), cnt.index_select(0, order)
+        hmask = member(sample, hot.index_select(0, torch.argsort(hot[:, 0])))
         own = self.owners(sample).long()
-        owner_share = torch.bincount(own[~hmask], minlength=self.world).double() / n
-        hshare = float(hmask.float().mean()) if sample.shape[0] else 0.0
-        w = water_fill(owner_share.tolist(), hshare)
-        self.set_hot(hot, w)
-        return {"hot_share": hshare, "owner_share": owner_share.tolist(), "weights": w}
+        owner_load = torch.bincount(own[~hmask], minlength=self.world).double()
+        hshare = float(hmask.float().mean())
+        if policy == "spray":
+            w = water_fill((owner_load / n).tolist(), hshare)
+            self.set_hot(hot, None, w)
+            return {"hot_share": hshare, "owner_share": (owner_load / n).tolist(), "weights": w}
+        if policy != "designate":
+            raise ValueError(f"unknown spreading policy {policy!r}")
+        thr = (spray_above if spray_above is not None else 1.0 / (4 * self.world)) * n
+        load = owner_load.tolist()
+        ranks = []
+        import heapq
 
-    def set_hot(self, hot: Optional[torch.Tensor], weights: Optional[Sequence[float]] = None):
+        cl = hcnt.tolist()
+        sprayed = sum(c for c in cl if c > thr)
+        for r in range(self.world):
+            load[r] += sprayed / self.world
+        heap = [(load[r], r) for r in range(self.world)]
+        heapq.heapify(heap)
+        for c in cl:
+            if c > thr:
+                ranks.append(-1)
+                continue
+            lr, r = heapq.heappop(heap)
+            ranks.append(r)
+            heapq.heappush(heap, (lr + c, r))
+        for lr, r in heap:
+            load[r] = lr
+        self.set_hot(hot, torch.tensor(ranks, dtype=torch.int32), [1.0] * self.world)
+        return {"hot_share": hshare, "owner_share": (owner_load / n).tolist(),
+                "sprayed_objects": sum(1 for r in ranks if r < 0),
+                "planned_load": [x / n for x in load]}
+
+    def set_hot(self, hot: Optional[torch.Tensor], ranks: Optional[torch.Tensor] = None,
+                weights: Optional[Sequence[float]] = None):
+        """Install a hot set: digests ``hot`` [h, 2], each one's designated rank (``ranks``
+        int32 [h], -1 = sprayed; None = all sprayed) and the spray weights."""
         if hot is None or hot.shape[0] == 0:
-            self.hot, self.weights = None, [1.0] * self.world
-            self.router.set_hot(0, 0, self.weights)
+            self.hot, self.hot_rank, self.weights = None, None, [1.0] * self.world
+            self.router.set_hot(0, 0, 0, self.weights)
         else:
-            self.hot = hot.index_select(0, torch.argsort(hot[:, 0])).contiguous().to(self.device)
+            order = torch.argsort(hot[:, 0])
+            self.hot = hot.index_select(0, order).contiguous().to(self.device)
+            r = (torch.full((hot.shape[0],), -1, dtype=torch.int32) if ranks is None
+                 else ranks.to(torch.int32).cpu().index_select(0, order.cpu()))
+            self.hot_rank = r.contiguous().to(self.device)
             self.weights = list(weights) if weights is not None else [1.0] * self.world
             h = self.hot.cpu().contiguous()
-            self.router.set_hot(h.data_ptr(), h.shape[0], self.weights)
+            rh = r.contiguous()
+            self.router.set_hot(h.data_ptr(), h.shape[0], rh.data_ptr(), self.weights)
         self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
 
     # -- the native router ---------------------------------------------------------------

@@ -459,7 +459,7 @@ def test_local_group_never_routes_gloo():
     _run_world(_local_worker, 2, timeout=120)
 
 
-def _spread_worker(rank, world, port, q):
+def _spread_worker(rank, world, port, q, rank_policy):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -469,7 +469,7 @@ def _spread_worker(rank, world, port, q):
         from shellac_amd.models.sharded_cache import ShardedCache
         from shellac_amd.ops.cache import CacheShard, unpack_records
         from shellac_amd.parallel.exchange import LocalComm
-        from shellac_amd.parallel.hotspread import HotSpread, replicate_hot, water_fill
+        from shellac_amd.parallel.hotspread import HotSpread, member, replicate_hot, water_fill
 
         N = 6000 * world
         wl = Workload(N, "cpu", min_val=16, max_val=512, pool_bytes=1 << 20)
@@ -483,7 +483,15 @@ def _spread_worker(rank, world, port, q):
         hmask[hot_ids] = True
         hsamp = hmask[sample]
         share = torch.bincount(owner[sample[~hsamp]], minlength=world).double() / sample.numel()
-        hs.set_hot(wl.digests[hot_ids], water_fill(share.tolist(), float(hsamp.float().mean())))
+        if rank_policy == "spray":
+            hs.set_hot(wl.digests[hot_ids], None,
+                       water_fill(share.tolist(), float(hsamp.float().mean())))
+        else:
+            hs.plan(wl.digests[sample], 200)      # (ties at the cut may pick other keys)
+            hot_ids = torch.nonzero(member(wl.digests, hs.hot)).flatten()
+            hmask = torch.zeros(N, dtype=torch.bool)
+            hmask[hot_ids] = True
+            assert hot_ids.numel() == 200 and int((hs.hot_rank >= 0).sum()) > 150
         # a host-routed rank: its own keys, then the hot objects it does not own, fetched
         # from their owners with one all-gather of records
         sc = ShardedCache(CacheShard(16 << 20, 1 << 14, 1 << 12, "cpu"), group=LocalComm())
@@ -525,11 +533,11 @@ def _spread_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_host_routed_true_shares_with_hot_spreading_gloo(world):
+@pytest.mark.parametrize("world,policy", [(2, "designate"), (3, "designate"), (3, "spray")])
+def test_host_routed_true_shares_with_hot_spreading_gloo(world, policy):
     """The host-routed topology end to end on CPU ranks: one global Zipf stream routed by
     ketama with the hottest objects replicated on every rank (filled from their owners by an
     all-gather) and their GETs sprayed, their SETs written through everywhere. Every rank
     serves exactly its share, every GET of it returns the version the SETs of earlier steps
     left, wherever it was sent, and the ranks' loads stay within a few percent."""
-    _run_world(_spread_worker, world)
+    _run_world(_spread_worker, world, policy)

@@ -15,7 +15,10 @@ def test_native_router_matches_tensor_routing(world):
     stream = keys[torch.randint(0, 3000, (200000,), generator=g)].contiguous()
     for hot in (None, keys[:300]):
         w = [1.0 + (r % 3) for r in range(world)]
-        hs.set_hot(hot, w if hot is not None else None)
+        # designated ranks for most hot objects, sprayed (-1) for every fifth
+        ranks = torch.tensor([-1 if i % 5 == 0 else i % world for i in range(300)],
+                             dtype=torch.int32)
+        hs.set_hot(hot, ranks if hot is not None else None, w if hot is not None else None)
         for seq0 in (0, 12345678901):
             d, c = hs.host_route_gets(stream, seq0=seq0, threads=3)
             assert torch.equal(d, hs.route_gets(stream, seq0=seq0))
@@ -51,10 +54,11 @@ def test_water_fill_levels_the_ranks():
     assert w[0] == 0.0 and abs(w[1] - w[2]) < 1e-12
 
 
-def test_spreading_evens_out_a_zipf_stream():
+@pytest.mark.parametrize("policy", ["designate", "spray"])
+def test_spreading_evens_out_a_zipf_stream(policy):
     """Zipf(0.99) over 400K keys on 8 ranks: ketama alone leaves the most loaded rank well
-    above the mean (the hot keys' owners); the top 4096 objects sprayed bring it within
-    2 %."""
+    above the mean (the hot keys' owners); the top 4096 objects designated to ranks (or
+    sprayed) bring it within 2 %."""
     n, world = 400000, 8
     g = torch.Generator().manual_seed(3)
     keys = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, generator=g)
@@ -65,7 +69,7 @@ def test_spreading_evens_out_a_zipf_stream():
     stream = keys[ids.clamp_(max=n - 1)]
     hs = HotSpread(world, "cpu")
     c0 = torch.bincount(hs.route_gets(stream).long(), minlength=world).double()
-    info = hs.plan(stream[:1_000_000], 4096)
+    info = hs.plan(stream[:1_000_000], 4096, policy=policy)
     c1 = torch.bincount(hs.route_gets(stream[1_000_000:], seq0=1_000_000).long(),
                         minlength=world).double()
     assert float(c0.max() / c0.mean()) > 1.1
