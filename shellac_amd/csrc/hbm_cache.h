@@ -271,10 +271,20 @@ class HbmCache {
   int64_t rc_cap_ = 0;
   uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr;
   int64_t rc_adv_w_ = 0;
-  // store(phase=1) queued the CLOCK hand of a batch of hand_n_ rows with a window of hand_w_
-  // (0: none) into hand buffer hand_b_; store(phase=2) runs that combined batch's chain
-  int64_t hand_w_ = 0, hand_n_ = 0;  // > 0: the next SET plan's dedupe advances the hand (window w)
-  int hand_b_ = 0;
+  // store(phase=1) queued a batch's CLOCK hand and planning; store(phase=2) runs the rest
+  // of its chain (append, index insert) from this record
+  struct Pending {
+    bool active = false;
+    int64_t n = 0, rows = 0, nmove = 0;  // caller rows; rows of the (combined) batch; moves
+    int parity = 0;                       // its SET workspace and hand buffer
+    const Digest* keys = nullptr;
+    const uint8_t* values = nullptr;
+    const uint64_t* voff = nullptr;
+    const uint32_t *vlen = nullptr, *flags = nullptr, *expire = nullptr;
+    const uint64_t* from = nullptr;
+  };
+  Pending pend_;
+  int hand_b_ = 0;  // the hand buffer reclaim_locked fills
   // The combined SET batch (reinsertion rows, then the batch's own rows) and the staged
   // reinsertion records, two buffers taken in turn (a detached hand fills one while the
   // previous batch's chain still reads the other). `from`: a reinsertion row's old entry
@@ -288,7 +298,23 @@ class HbmCache {
     uint8_t* scratch = nullptr;  // staged reinsertions (rmax_ + 64 bytes)
   };
   HandBuf hb_[2];
-  int hb_next_ = 0;
+  // SET workspaces, two taken in turn by consecutive batches (ws_next_): a batch's planning
+  // (phase 1) may run while the previous batch's append and index insert still use theirs.
+  // The dd_* / set_* members below point at the one in use (select_ws).
+  struct SetWs {
+    uint64_t* dd_keys = nullptr;
+    int* dd_win = nullptr;
+    uint32_t* dd_slot = nullptr;
+    uint64_t *set_size = nullptr, *set_off = nullptr, *set_cnt = nullptr;
+    uint32_t* set_claim = nullptr;
+  };
+  SetWs ws_[2];
+  int ws_next_ = 0;
+  void select_ws(int p) {
+    const SetWs& w = ws_[p];
+    dd_keys_ = w.dd_keys; dd_win_ = w.dd_win; dd_slot_ = w.dd_slot; set_size_ = w.set_size;
+    set_off_ = w.set_off; set_cnt_ = w.set_cnt; set_claim_ = w.set_claim;
+  }
 
   ShardConfig cfg_;
   uint8_t* log_ = nullptr;
@@ -337,7 +363,10 @@ class HbmCache {
                     hipEvent_t append_after = nullptr, hipEvent_t append_done = nullptr,
                     const uint64_t* from = nullptr, hipEvent_t plan_done = nullptr,
                     int64_t nmove = 0);
-  void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s);
+  void store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n, hipStream_t s,
+                         bool detached = false);
+  void store_tail_locked(uint32_t now, hipStream_t s, hipEvent_t index_after,
+                         hipEvent_t append_after, hipEvent_t append_done);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
                           const uint64_t* from = nullptr, int64_t nmove = 0);

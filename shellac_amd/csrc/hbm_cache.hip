@@ -2957,11 +2957,10 @@ HbmCache::~HbmCache() {
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
-  (void)hipFree(dd_keys_);
-  (void)hipFree(dd_win_);
-  (void)hipFree(dd_slot_);
-  (void)hipFree(set_size_);
-  (void)hipFree(set_off_); (void)hipFree(set_claim_); (void)hipFree(set_cnt_);
+  for (SetWs& w : ws_)
+    for (void* p : {(void*)w.dd_keys, (void*)w.dd_win, (void*)w.dd_slot, (void*)w.set_size,
+                    (void*)w.set_off, (void*)w.set_claim, (void*)w.set_cnt})
+      (void)hipFree(p);
   (void)hipFree(ring_); (void)hipFree(rc_ctl_);
   for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) (void)hipFree(p);
   for (HandBuf& b : hb_)
@@ -3060,24 +3059,28 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   if (n <= set_cap_) return;
   int64_t cap = set_cap_ ? set_cap_ : 1024;
   while (cap < n) cap *= 2;
-  // the old workspace may still be read by queued SET chains on other streams: retired,
-  // not freed (no device synchronisation on the serving path)
-  for (void* p : {(void*)dd_keys_, (void*)dd_win_, (void*)dd_slot_, (void*)set_size_,
-                  (void*)set_off_, (void*)set_claim_, (void*)set_cnt_})
-    retire(p);
   const uint64_t tslots = (uint64_t)cap * 2;
-  HIP_OK(hipMalloc(&dd_keys_, tslots * sizeof(uint64_t)));
-  HIP_OK(hipMalloc(&dd_win_, tslots * sizeof(int)));
-  // the table is cleared once here, on the stream of the SET that first uses it (ordered
-  // before its dedupe; the null stream is not: a non-blocking stream does not wait for it,
-  // which once dropped the first batch's rows); k_set_index resets every slot a batch used
-  HIP_OK(hipMemsetAsync(dd_keys_, 0, tslots * sizeof(uint64_t), s));
-  HIP_OK(hipMemsetAsync(dd_win_, 0xff, tslots * sizeof(int), s));
-  HIP_OK(hipMalloc(&dd_slot_, cap * sizeof(uint32_t)));
-  HIP_OK(hipMalloc(&set_size_, (cap + 1) * sizeof(uint64_t)));
-  HIP_OK(hipMalloc(&set_off_, (cap + 1) * sizeof(uint64_t)));
-  HIP_OK(hipMalloc(&set_claim_, cap * sizeof(uint32_t)));
-  HIP_OK(hipMalloc(&set_cnt_, (cap + 1) * sizeof(uint64_t)));
+  for (SetWs& w : ws_) {
+    // the old workspace may still be read by queued SET chains on other streams: retired,
+    // not freed (no device synchronisation on the serving path)
+    for (void* p : {(void*)w.dd_keys, (void*)w.dd_win, (void*)w.dd_slot, (void*)w.set_size,
+                    (void*)w.set_off, (void*)w.set_claim, (void*)w.set_cnt})
+      retire(p);
+    HIP_OK(hipMalloc(&w.dd_keys, tslots * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&w.dd_win, tslots * sizeof(int)));
+    // the tables are cleared once here, on the stream of the SET that first uses them
+    // (ordered before its dedupe; the null stream is not: a non-blocking stream does not
+    // wait for it, which once dropped the first batch's rows); k_set_index resets every
+    // slot a batch used
+    HIP_OK(hipMemsetAsync(w.dd_keys, 0, tslots * sizeof(uint64_t), s));
+    HIP_OK(hipMemsetAsync(w.dd_win, 0xff, tslots * sizeof(int), s));
+    HIP_OK(hipMalloc(&w.dd_slot, cap * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&w.set_size, (cap + 1) * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&w.set_off, (cap + 1) * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&w.set_claim, cap * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&w.set_cnt, (cap + 1) * sizeof(uint64_t)));
+  }
+  select_ws(0);
   dd_mask_ = (uint32_t)(tslots - 1);
   set_cap_ = cap;
   ++ws_gen_;
@@ -3360,44 +3363,18 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   note_stream(s);
-  // phase 2: the rest of a batch whose CLOCK hand a phase-1 call queued
-  if (phase == 2 && hand_w_ > 0) {
-    SH_CHECK(hand_n_ == n, "store phase 2 of a different batch than phase 1");
-    const int64_t w = hand_w_;
-    hand_w_ = 0;
-    const HandBuf& hb = hb_[hand_b_];
-    store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
-                 index_after, append_after, append_done, hb.from, plan_done, w);
-    hsel_ ^= 1;
+  // phase 2: the rest of the chain of the batch a phase-1 call planned
+  if (phase == 2) {
+    SH_CHECK(pend_.active && pend_.n == n, "store phase 2 without the same batch's phase 1");
+    store_tail_locked(now, s, index_after, append_after, append_done);
     return;
   }
+  SH_CHECK(!pend_.active, "store: a phase-1 batch is still waiting for its phase 2");
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
-  if (phase == 1 && !(allow_reclaim && rmax && should_reclaim(bytes_bound))) {
-    hand_w_ = 0;  // no hand for this batch: phase 2 runs the plain chain
-    return;
-  }
-  if (allow_reclaim && rmax && should_reclaim(bytes_bound)) {
-    const int64_t w = hand_window(n);
-    ensure_rc_ws(w, s);
-    // the hand buffers alternate: a detached hand of the next batch fills the other one
-    // while this batch's chain still reads this one
-    hand_b_ = hb_next_;
-    hb_next_ ^= 1;
-    ensure_cb(hand_b_, w + n, s);
-    ensure_set_ws(w + n, s);
-    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, phase == 1);
-    if (phase == 1) {  // the chain follows in phase 2
-      hand_w_ = w;
-      hand_n_ = n;
-      return;
-    }
-    // combined batch: reinsertions first (log order), then the batch (its SETs win)
-    const HandBuf& hb = hb_[hand_b_];
-    store_locked(hb.keys, nullptr, hb.voff, hb.vlen, hb.flags, hb.expire, w + n, now, s,
-                 index_after, append_after, append_done, hb.from, plan_done, w);
-  } else if (n <= kSmallSetRows && !index_after && !append_after && !append_done &&
-             !plan_done) {
+  const bool hand = allow_reclaim && rmax && should_reclaim(bytes_bound);
+  if (!hand && phase == 0 && n <= kSmallSetRows && !index_after && !append_after &&
+      !append_done && !plan_done) {
     // one launch for the whole chain (the proxy's small SET batches)
     hipLaunchKernelGGL(k_set_small, dim3(1), dim3(kBlock), 0, s, keys, values, val_off, vlen,
                        flags, expire, (int)n, cfg_.max_item, index_, cfg_.nbuckets - 1,
@@ -3406,11 +3383,65 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                        log_, ring_, ring_ ? ring_cap_ - 1 : 0ull, cur_ring_tail(),
                        next_ring_tail(), host_slots_ + kHeadSlot, ctr_);
     HIP_OK(hipGetLastError());
+    hsel_ ^= 1;
+    return;
+  }
+  // consecutive batches take the two SET workspaces and hand buffers in turn
+  Pending p;
+  p.active = true;
+  p.n = n;
+  p.parity = ws_next_;
+  ws_next_ ^= 1;
+  const bool detached = phase == 1;
+  if (hand) {
+    const int64_t w = hand_window(n);
+    ensure_rc_ws(w, s);
+    hand_b_ = p.parity;
+    ensure_cb(hand_b_, w + n, s);
+    ensure_set_ws(w + n, s);
+    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, detached);
+    // combined batch: reinsertions first (log order), then the batch (its SETs win)
+    const HandBuf& hb = hb_[hand_b_];
+    p.rows = w + n;
+    p.nmove = w;
+    p.keys = hb.keys;
+    p.values = nullptr;
+    p.voff = hb.voff;
+    p.vlen = hb.vlen;
+    p.flags = hb.flags;
+    p.expire = hb.expire;
+    p.from = hb.from;
   } else {
     ensure_set_ws(n, s);
-    store_locked(keys, values, val_off, vlen, flags, expire, n, now, s, index_after, append_after,
-                 append_done, nullptr, plan_done);
+    p.rows = n;
+    p.keys = keys;
+    p.values = values;
+    p.voff = val_off;
+    p.vlen = vlen;
+    p.flags = flags;
+    p.expire = expire;
   }
+  select_ws(p.parity);
+  store_plan_locked(p.keys, p.vlen, p.rows, s, detached);
+  if (plan_done) HIP_OK(hipEventRecord(plan_done, s));
+  pend_ = p;
+  if (detached) return;  // the chain follows in phase 2
+  store_tail_locked(now, s, index_after, append_after, append_done);
+}
+
+// The planned batch's log append (after `append_after`) and index insert (after
+// `index_after`); publishes the new head (the ping-pong slot flips).
+void HbmCache::store_tail_locked(uint32_t now, hipStream_t s, hipEvent_t index_after,
+                                 hipEvent_t append_after, hipEvent_t append_done) {
+  const Pending p = pend_;
+  pend_.active = false;
+  select_ws(p.parity);
+  if (append_after) HIP_OK(hipStreamWaitEvent(s, append_after, 0));
+  launch_segcopy<1>(s, p.values, p.voff, set_off_, p.rows, log_, p.keys, p.vlen, p.flags,
+                    p.expire, cur_head(), cfg_.log_bytes);
+  HIP_OK(hipGetLastError());
+  if (append_done) HIP_OK(hipEventRecord(append_done, s));
+  store_index_locked(p.keys, p.vlen, p.expire, p.rows, now, s, index_after, p.from, p.nmove);
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
 
@@ -3435,12 +3466,17 @@ void HbmCache::store_locked(const Digest* keys, const uint8_t* values, const uin
   store_index_locked(keys, vlen, expire, n, now, s, index_after, from, nmove);
 }
 
+// `detached`: the planning of a phase-1 batch, which may run before the previous batch's
+// append and index insert: the ring tail it clamps the hand with is the batch-before's (the
+// last one written), and the claim grows from itself (the head every queued append
+// reaches) rather than from the head slot the previous index insert has not published yet.
 void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64_t n,
-                                 hipStream_t s) {
+                                 hipStream_t s, bool detached) {
   const int grid = grid_for(n, kBlock, kMaxGrid);
   RcAdvance adv;
   if (rc_adv_w_ > 0) {
-    adv = RcAdvance{rc_ctl_, cur_ring_tail(), ring_cap_ - 1, rc_adv_w_};
+    adv = RcAdvance{rc_ctl_, detached ? next_ring_tail() : cur_ring_tail(), ring_cap_ - 1,
+                    rc_adv_w_};
     rc_adv_w_ = 0;
   }
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
@@ -3451,7 +3487,7 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
                      cfg_.max_item, set_size_, ctr_, part_ + kMaxGrid, part_cnt);
   HIP_OK(hipGetLastError());
   launch_offsets(set_size_, n, part_ + kMaxGrid, sgrid, set_off_, s, nullptr, 0, part_cnt,
-                 ring_ ? set_cnt_ : nullptr, cur_head(), claim_ptr());
+                 ring_ ? set_cnt_ : nullptr, detached ? claim_ptr() : cur_head(), claim_ptr());
 }
 
 void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
@@ -3502,6 +3538,7 @@ void HbmCache::store_graph(StoreGraph* g, const Digest* keys, const uint8_t* val
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard dg(cfg_.device);
   ensure_set_ws(n, s);  // before any capture: allocation is not capturable
+  select_ws(0);         // (graphs bake the workspace in: always the first)
   const void* ptrs[6] = {keys, values, val_off, vlen, flags, expire};
   bool same = g->n == n && g->bound == bytes_bound && g->now == now && g->ws_gen == ws_gen_ &&
               g->exec[0] && g->exec[1];

@@ -263,8 +263,10 @@ class ShardedCache:
             raise ValueError(f"hand must be one of {self.HANDS}, not {hand!r}")
         self.hand = hand
         self._side_pending = False
-        self._planned = False    # the last serve's plan_done event can order the next hand
-        self._held_set = None    # the SET batch the side chain still reads (until joined)
+        self._planned = False    # the serve pipeline orders the next hand (see serve)
+        self._ends = [None, None]  # per step parity: recorded after the step's SET chain
+        self._last_end = None
+        self._held_steps = []    # the SET batches the last two steps' chains may still read
         self._hand_s = None
         self._events = {}
         self._side = None
@@ -306,9 +308,9 @@ class ShardedCache:
         after a routed ``serve`` (a device synchronisation also does)."""
         if self._side_pending:
             # the last one-GPU serve's SET chain (serve leaves it for the next step)
-            self._xwait(torch.cuda.current_stream(self.device), self._side, "end")
+            self._wait(torch.cuda.current_stream(self.device), self._last_end)
             self._side_pending = False
-            self._held_set = None
+        self._held_steps = []
         # whatever runs next on the caller's stream (a set, a delete, ...) is not covered by
         # the last serve's plan event: the next early hand follows the caller's stream
         self._planned = False
@@ -516,24 +518,27 @@ class ShardedCache:
         else:
             ready = inputs_ready
         early = self.hand == "early"
-        hand_done = None
+        k = self._nserve = getattr(self, "_nserve", -1) + 1   # this step's event parity
+        planned = self._event("planned") if early else None
         if early:
+            # the hand and the planning of this batch, on the hand stream: after the
+            # previous batch's planning (the stream's order) and the chain of the batch
+            # before that (its SET workspace and hand buffer, which this batch reuses)
             hs = self._hand_stream()
             self._wait(hs, ready)
             if self._planned:
-                self._wait(hs, self._event("planned"))
+                if self._ends[k % 2] is not None:
+                    self._wait(hs, self._ends[k % 2])
             else:
-                # no serve plan to follow (first step, or other work since): the caller's
-                # stream as of now, which has joined every earlier SET chain
+                # no serve pipeline to follow (first step, or other work since): the
+                # caller's stream as of now, which has joined every earlier SET chain
                 self._xwait(hs, main, "mainpos")
             with torch.cuda.stream(hs):
                 batch = staged_batch(batch)
                 sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                         batch.expire, now, phase=1)
-            hand_done = self._event("hand")
-            hand_done.record(hs)
+                         batch.expire, now, phase=1, plan_done=planned)
         if self._side_pending:
-            self._xwait(main, side, "end")   # the previous step's SET chain
+            self._wait(main, self._ends[(k - 1) % 2])   # the previous step's SET chain
             self._side_pending = False
         start = self._event("start")
         start.record(main)                   # ... and its gather: the append may overwrite
@@ -541,16 +546,13 @@ class ShardedCache:
             lk, first, cslot, table = self._lookup_step(keys, now, bound, side)
         except BaseException:
             if early:
-                # the queued hand's batch still runs its chain (the native store pairs phase 1
+                # the planned batch still runs its chain (the native store pairs phase 1
                 # with the next phase 2), after the previous gather like any append
                 with torch.cuda.stream(side):
-                    self._wait(side, hand_done)
+                    self._wait(side, planned)
                     sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
-                             batch.expire, now, append_after=start, phase=2,
-                             plan_done=self._event("planned"))
-                self._side_pending = True
-                self._held_set = batch
-                self._planned = True
+                             batch.expire, now, append_after=start, phase=2)
+                self._end_step(side, k, batch, early)
             raise
         # Safe by construction: the lookup reserved the SET's log bytes, so the gather
         # never reads a region the SET writes, and the gather does not read the index.
@@ -562,14 +564,14 @@ class ShardedCache:
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
             if early:
-                self._wait(side, hand_done)  # (the hand followed `ready`)
+                self._wait(side, planned)    # (the plan followed `ready`)
             else:
                 self._wait(side, ready)
                 batch = staged_batch(batch)
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now, index_after=ev, append_after=start, append_done=appended,
-                     phase=2 if early else 0, plan_done=self._event("planned") if early else None)
-        self._planned = early
+                     phase=2 if early else 0)
+        self._end_step(side, k, batch, early)
         if appended is not None:
             # the gather runs after the log append, not beside it: the two byte movers
             # contending for HBM are slower together than one after the other
@@ -579,13 +581,26 @@ class ShardedCache:
         # step's lookup to wait for but the SET chain)
         data = self._gather_unsynced(
             lk, None if first is None else (first, out_size, out_off, table, cslot))
-        # joined by the next serve's lookup, or by sync_sets (every other method); the
-        # chain reads the batch until then
-        self._side_pending = True
-        self._held_set = batch
         if first is not None:
             return GetResult(data, out_off, out_size, self._take_pending())
         return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
+
+    def _end_step(self, side, k: int, batch, early: bool) -> None:
+        """After a step's SET chain is queued: its end event (the next step's lookup and the
+        step after next's hand wait for it), the batch kept alive until the chain is joined
+        (the next serve's lookup or sync_sets)."""
+        e = self._ends[k % 2]
+        if e is None:
+            e = self._ends[k % 2] = (torch.cuda.Event() if self.event_fence == "system"
+                                     else StreamEvent(self.event_fence))
+        e.record(side)
+        self._last_end = e
+        self._side_pending = True
+        held = self._held_steps
+        held.append(batch)
+        while len(held) > 2:   # the chain of two steps back is joined by now
+            held.pop(0)
+        self._planned = early
 
     def _lookup_step(self, keys, now, bound, side):
         """The step's GET lookup (coalesced unless ``coalesce`` is off): (lookup, first,
