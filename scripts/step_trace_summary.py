@@ -43,3 +43,13 @@ prev=a
 for s,e,n,q,sid in ks:
     if a<=s<b:
         print(f"{(s-a)/1e3:8.1f} {(e-s)/1e3:7.1f} gap {(s-prev)/1e3:6.1f} q{q:>3} s{sid:>3} {n}"); prev=max(prev,e)
+# STEP_TABLE=1: one line per step (wall, then the busiest kernels' time in that step)
+import os
+if os.environ.get("STEP_TABLE"):
+    top=[n for n,_ in sorted(tot.items(),key=lambda x:-x[1][1])[:8]]
+    print("--- per step (us): wall | "+" | ".join(top))
+    for i in range(len(st)-1):
+        a,b=st[i],st[i+1]; row=defaultdict(int)
+        for s,e,n,_,_ in ks:
+            if a<=s<b: row[n]+=e-s
+        print(f"{(b-a)/1e3:7.1f} | "+" | ".join(f"{row[n]/1e3:6.1f}" for n in top))

@@ -16,7 +16,7 @@ run() {  # name marker hip_trace bench-args...
   shift 3
   HIP_TRACE=$hip TRACE_OUT=$OUT/raw_$name bash scripts/trace_bench.sh "$@" > "$R/$name.log" 2>&1 \
     || { echo "trace $name failed"; tail -20 "$R/$name.log"; return 1; }
-  python3 scripts/step_trace_summary.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_summary.txt"
+  python3 scripts/step_trace_summary.py "gpurun_out/$OUT/raw_$name" ${TRACE_STEPS:-8} "$marker" > "$R/${name}_summary.txt"
   if [ "$hip" = 1 ]; then
     python3 scripts/host_wait_audit.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_hostwait.txt"
     python3 scripts/launch_lag.py "gpurun_out/$OUT/raw_$name" 8 "$marker" > "$R/${name}_launch_lag.txt"
