@@ -131,14 +131,19 @@ def parse():
     ap.add_argument("--no-wrapped", action="store_true",
                     help="skip the steady-state measurement (value log wrapped, so every SET "
                          "batch runs the eviction hand); the headline is then the fresh cache")
-    ap.add_argument("--pressured-gb", type=float, default=5.0,
-                    help="secondary steady state under capacity pressure: a shard with this "
-                         "many GiB of log (the 4M keys' ~4 GiB barely fit), wrapped, so the "
-                         "CLOCK hand re-appends read objects every step (0 = skip)")
-    ap.add_argument("--headline", choices=["wrapped", "fresh"], default="wrapped",
-                    help="which cache state the headline K steps run in: the steady state of a "
-                         "full cache (value log wrapped, eviction in every SET batch; default) "
-                         "or the fresh cache before the first wrap (also reported as log_fresh)")
+    ap.add_argument("--pressured-gb", type=float, default=None,
+                    help="the full-cache steady state (the headline): a shard log of this many "
+                         "GiB, wrapped, so the CLOCK hand re-appends read objects every step. "
+                         "Default: sized so the shard's working set (every key it owns, one "
+                         "record each) fills --pressured-fill of it (0 = skip)")
+    ap.add_argument("--pressured-fill", type=float, default=0.8,
+                    help="working set over log capacity of the default pressured shard")
+    ap.add_argument("--headline", choices=["pressured", "wrapped", "fresh"], default="pressured",
+                    help="which cache state the headline K steps run in: a full cache whose "
+                         "working set fills --pressured-fill of the log (default: eviction with "
+                         "CLOCK reinsertions in every SET batch, hit ratio < 1), the 16 GiB log "
+                         "wrapped (eviction hand in every batch, nothing live to evict), or the "
+                         "fresh cache before the first wrap")
     ap.add_argument("--drift-epochs", type=int, default=4,
                     help="hot_drift block (N>1 / simulated, replica on): epochs of drifted "
                          "popularity, each --drift-steps steps then an incremental replica "
@@ -260,8 +265,10 @@ def check_memory_budget(args, world, sim, dev) -> None:
     need += 3 * args.batch * (mean_val + 48) * 1.2 + 2 * gib        # responses in flight
     if not args.no_smoke and world > 1:
         need += gib
-    if args.pressured_gb > 0 and not sim:
-        need += args.pressured_gb * gib + nb * 128
+    if (args.pressured_gb is None or args.pressured_gb > 0) and not sim:
+        pgb = (args.pressured_gb if args.pressured_gb is not None else
+               args.keys_per_gpu * (mean_val + 48) / max(args.pressured_fill, 0.1) / gib)
+        need += pgb * gib + nb * 128
     if sim:  # the probe digests of the key space and their sorted index
         need += args.keys_per_gpu * sim * 48
     free, total = torch.cuda.mem_get_info(dev)
@@ -472,11 +479,12 @@ def main():
         kh = wl.digests.index_select(0, g0).cpu().contiguous()
         th = args.route_threads or min(16, len(os.sched_getaffinity(0)))
         rates = {}
+        hbuf = torch.empty(kh.shape[0], dtype=torch.int32)
         for t_ in sorted({1, th}):
             best = float("inf")
             for _ in range(3):
                 t0_ = _t.perf_counter()
-                hd, _hc = spread.host_route_gets(kh, seq0=0, threads=t_)
+                hd, _hc = spread.host_route_gets(kh, seq0=0, threads=t_, out=hbuf)
                 best = min(best, _t.perf_counter() - t0_)
             rates[t_] = kh.shape[0] / best
         route_info.update(host_route_threads=th,
@@ -669,7 +677,10 @@ def main():
         st0 = dict(cache.stats)
         gb0 = cache.gathered_bytes
         h0 = shard_.head()
-        el, _, res = timed(args.steps, first, cache=cache)
+        # SHELLAC_BENCH_WINDOW_EVENTS=1 (diagnostic): per-step GPU events inside the timed
+        # window itself (they cost a few us per step), reported as window_step_ms
+        wev = bool(os.environ.get("SHELLAC_BENCH_WINDOW_EVENTS")) and use_events
+        el, wiv, res = timed(args.steps, first, events=wev, cache=cache)
         rank_ms = list(last_rank_ms)
         gathered = cache.gathered_bytes - gb0
         cache.sync_sets()
@@ -689,7 +700,7 @@ def main():
         return {"el": el, "res": res, "last": (first + args.steps - 1) % P, "hits": hits,
                 "gops": gops, "gbytes": gbytes, "rep": rep, "greq": greq, "rbytes": rbytes,
                 "head0": h0, "head1": shard_.head(), "gathered": gathered, "c0": c0, "c1": c1,
-                "rank_ms": rank_ms}
+                "rank_ms": rank_ms, "wiv": wiv}
 
     def check(w):
         """Verify the window's last GET batch against the workload's ground truth (before
@@ -736,6 +747,7 @@ def main():
                 "cache_ops_per_s": round((args.batch + args.sets) * world * args.steps / w["el"], 1),
                 "log_gib_per_shard": round(log_bytes_ / (1 << 30), 2),
                 "log_head_laps": round(w["head1"] / log_bytes_, 3),
+                "working_set_over_capacity": round(ws_bytes / log_bytes_, 4),
                 "owner_hit_ratio": round(w["hits"] / max(w["gops"], 1), 4),
                 "reinserted_bytes_per_step_per_rank": round(w["rbytes"] / world / args.steps)}
         if fill is not None:
@@ -744,6 +756,8 @@ def main():
             out_["rank_ms_per_step"] = w["rank_ms"]
         if iv:
             out_["ms_per_step_median_gpu_events"] = median(iv)
+        if w.get("wiv"):
+            out_["window_step_ms"] = [round(x, 4) for x in w["wiv"]]
         return out_
 
     # The log fills at ~66 MB per step and rank; a serving cache is full, and then every
@@ -838,13 +852,25 @@ def main():
                 "replica_fetched_gib": round(st.get("replica_fetched_bytes", 0) / (1 << 30), 3)}
 
     steady_ok = not host_edge and dev.type == "cuda" and not args.no_wrapped
-    headline_wrapped = steady_ok and args.headline == "wrapped"
+    # the shard's working set: one record of every key it holds (its owner share, plus the
+    # replicas of spread hot objects), as the log stores it (header + 16-B aligned value)
+    held = (torch.arange(lo, hi, device=dev) if fill_ids is None else
+            fill_ids if rep_ids is None else torch.cat([fill_ids, rep_ids]))
+    ws_bytes = int((32 + ((wl.vlen.index_select(0, held).long() + 15) & ~15)).sum())
+    del held
+    p_gb = args.pressured_gb
+    if p_gb is None:
+        p_gb = ws_bytes / max(args.pressured_fill, 0.1) / (1 << 30)
+    do_pressured = p_gb > 0 and steady_ok and not msim
+    headline = args.headline if steady_ok else "fresh"
+    if headline == "pressured" and not do_pressured:
+        headline = "wrapped"
     for i in range(args.warmup):
         step(i)
     sync()
     # the log not yet wrapped (the first K steps after the warmup)
     fresh = window(sc, shard, args.warmup)
-    if args.check and not headline_wrapped:
+    if args.check and headline == "fresh":
         check(fresh)
     diag = None
     if sc._engine is not None:
@@ -876,27 +902,27 @@ def main():
         unco = (args.batch + args.sets) * world * args.steps / unco_el
     per_step = max((fresh["head1"] - fresh["head0"]) / max(args.steps, 1), 1.0)
 
-    # the headline: steady state of the full cache (value log wrapped)
+    # the 16 GiB log wrapped: every SET batch runs the eviction hand, but the working set
+    # fills only ~1/4 of the log, so nothing live is evicted or re-appended
     wrapped = wrapped_iv = nfill = None
     if steady_ok:
         base = args.warmup + 3 * args.steps
         nfill = fill_to_wrap(sc, shard, log_bytes, base, per_step)
         if nfill is not None:
             wrapped = window(sc, shard, base + nfill)
-            if args.check and headline_wrapped:
+            if args.check and headline == "wrapped":
                 check(wrapped)
             if use_events:
                 wrapped_iv = timed(args.steps, base + nfill + args.steps, events=True)[1]
-    if headline_wrapped and wrapped is None:
+    if headline == "wrapped" and wrapped is None:
         raise SystemExit("[bench] the value log could not be wrapped for the headline; "
                          "pass --headline fresh")
-    hw = wrapped if headline_wrapped else fresh
-    hw_iv = wrapped_iv if headline_wrapped else fresh_iv
-    # secondary: the same under capacity pressure — a shard whose log barely holds the key
-    # space, so objects the steps read are re-appended (reinsertions > 0) every step
-    pressured = None
-    if args.pressured_gb > 0 and steady_ok and not msim:
-        p_log = int(args.pressured_gb * (1 << 30)) // 16 * 16
+    # the full cache (the headline): a shard whose working set fills --pressured-fill of its
+    # log, wrapped, so the CLOCK hand re-appends the objects the steps read (reinsertions)
+    # and evicts the rest: the state a serving cache runs in (memcached evicts under load)
+    pressured = pw = piv = pfill = None
+    if do_pressured:
+        p_log = int(p_gb * (1 << 30)) // 16 * 16
         p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
         p_sc = ShardedCache(p_shard, group=group, replica=replica,
                             data_group=data_group, routed=True if routed1 else None,
@@ -915,11 +941,25 @@ def main():
         pfill = fill_to_wrap(p_sc, p_shard, p_log, pbase, per_step)
         if pfill is not None:
             pw = window(p_sc, p_shard, pbase + pfill)
+            if args.check and headline == "pressured":
+                check(pw)
             piv = timed(args.steps, pbase + pfill + args.steps, events=True,
                         cache=p_sc)[1] if use_events else []
             pressured = summary(pw, piv, p_log, pfill)
+            # the cost of a step varies with where the hand is in the lap (the objects it
+            # re-appended one lap earlier come round together): one whole lap, timed
+            lap_steps = int(p_log / max(1.0, (pw["head1"] - pw["head0"]) / args.steps)) + 1
+            lap_el = timed(lap_steps, pbase + pfill + 2 * args.steps, cache=p_sc)[0]
+            pressured["lap_steps"] = lap_steps
+            pressured["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
         p_sc.sync_sets()
         del p_sc, p_shard
+    if headline == "pressured" and pw is None:
+        raise SystemExit("[bench] the pressured log could not be wrapped for the headline; "
+                         "pass --headline wrapped")
+    hw, hw_iv, hw_log, hw_fill = {"pressured": (pw, piv, p_gb, pfill),
+                                  "wrapped": (wrapped, wrapped_iv, None, nfill),
+                                  "fresh": (fresh, fresh_iv, None, None)}[headline]
 
     # secondary: a drifting hot set (hot objects replaced every epoch) with the replica tier
     # maintained incrementally between epochs (refresh under a byte budget, no flush)
@@ -973,7 +1013,8 @@ def main():
             "keys_total": total_keys,
             "zipf_s": args.zipf,
             "value_bytes": [args.min_val, args.max_val],
-            "log_gib_per_shard": args.log_gb,
+            # the headline phase's shard log
+            "log_gib_per_shard": round(hw_log, 3) if hw_log else args.log_gb,
             "set_dist": args.set_dist,
             "replicated_hot_objects": args.replicate if world > 1 else 0,
             "routing": ("none" if world == 1 and not sim and not routed1 else
@@ -985,12 +1026,20 @@ def main():
         # window, and the measured rate of the native host router on the box's cores
         "host_routing": (dict(route_info, simulated_rank=me if sim else None)
                          if host_route else None),
-        # which cache state the headline steps ran in: "log_wrapped" = the steady state of a
-        # full cache (every SET batch runs the CLOCK hand), "log_fresh" = before the first wrap
-        "headline_phase": "log_wrapped" if headline_wrapped else "log_fresh",
+        # which cache state the headline steps ran in: "log_pressured" = a full cache (the
+        # working set fills --pressured-fill of the log: CLOCK reinsertions and evictions in
+        # every SET batch), "log_wrapped" = the 16 GiB log wrapped (the hand runs, nothing
+        # live is evicted), "log_fresh" = before the first wrap
+        "headline_phase": "log_" + headline,
+        "working_set_over_capacity": round(ws_bytes / (hw_log * (1 << 30) if hw_log else log_bytes), 4),
         "warmup_detail": (f"{args.warmup} warmup steps, {args.steps} pre-wrap steps (log_fresh), "
+                          f"{2 * args.steps} more, {nfill} fill steps to wrap the 16 GiB log, 2 x "
+                          f"{args.steps} steps there (log_wrapped); a {hw_log:.2f} GiB shard "
+                          f"populated and {hw_fill} fill steps to wrap it; then the {args.steps} "
+                          f"timed steps") if headline == "pressured" else
+                         (f"{args.warmup} warmup steps, {args.steps} pre-wrap steps (log_fresh), "
                           f"{2 * args.steps} more, {nfill} fill steps to wrap the log; then the "
-                          f"{args.steps} timed steps") if headline_wrapped else None,
+                          f"{args.steps} timed steps") if headline == "wrapped" else None,
         "get_coalescing": sc.coalesce,
         # owner-shard probes (+ replica hits) per GET request: < 1 when duplicate
         # requests of a batch share one probe and one response record
@@ -1011,9 +1060,9 @@ def main():
         "routed_diag": diag,
         # the step before the value log first wraps (no eviction work)
         "log_fresh": summary(fresh, fresh_iv),
-        # the step with the value log wrapped (eviction in every SET batch)
+        # the 16 GiB log wrapped (the hand in every SET batch; ~1/4 of it live)
         "log_wrapped": summary(wrapped, wrapped_iv, fill=nfill) if wrapped else None,
-        # the same under capacity pressure (a log the key space barely fits: reinsertions)
+        # the full cache (the default headline): reinsertions and evictions every step
         "log_pressured": pressured,
         # a drifting hot set with the replica maintained between epochs (N>1 / simulated)
         "hot_drift": drift,

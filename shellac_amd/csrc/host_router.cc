@@ -10,10 +10,9 @@ namespace shellac {
 
 namespace {
 constexpr uint64_t kWeyl = 0x9E3779B97F4A7C15ull;  // 2^64 / golden ratio
-constexpr int kPrefetch = 16;                       // requests whose hot-table line is in flight
 }  // namespace
 
-HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, -1) {
+HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, 0) {
   SH_CHECK(nshards >= 1 && nshards <= 32767 && pps >= 1, "bad router geometry");
   std::vector<std::pair<uint32_t, int>> pts;
   for (int i = 0; i < nshards; ++i)
@@ -30,15 +29,28 @@ HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, -1) {
     pts_.push_back(p.first);
     own_.push_back(p.second);
   }
-  // span s = [a, a + 65535]: one owner for all of it iff no point lies in [a, a + 65534]
+  // span s = [a, a + 65535]: one owner for all of it iff no point lies in [a, a + 65534];
+  // otherwise the index of its first point (the owner of any p in it is at or after it)
   for (uint32_t s = 0; s < 65536; ++s) {
     const uint32_t a = s << 16, b = a + 65535u;
     const auto it = std::lower_bound(pts_.begin(), pts_.end(), a);
-    if (it == pts_.end() || *it >= b) tab_[s] = (int16_t)search(b);
+    if (it == pts_.end() || *it >= b)
+      tab_[s] = search(b);
+    else
+      tab_[s] = -(int32_t)(it - pts_.begin()) - 1;
   }
   cw_.assign((size_t)n_, 0.0);
   for (int r = 0; r < n_; ++r) cw_[(size_t)r] = (double)(r + 1) / n_;
   cw_.back() = 1.0;
+}
+
+HostRouter::~HostRouter() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : pool_) t.join();
 }
 
 int HostRouter::search(uint32_t p) const {
@@ -49,14 +61,12 @@ int HostRouter::search(uint32_t p) const {
 void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, const double* w) {
   nhot_ = 0;
   hot_tab_.clear();
-  hot_rank_.clear();
   hot_bits_.clear();
   hot_mask_ = bits_mask_ = 0;
   if (n <= 0) return;
   uint64_t slots = 1024;
   while (slots < 2 * (uint64_t)n) slots <<= 1;
-  hot_tab_.assign(slots, Digest{0, 0});
-  hot_rank_.assign(slots, kSpray);
+  hot_tab_.assign(slots, HotSlot{});
   hot_mask_ = slots - 1;
   uint64_t bits = 1 << 12;
   while (bits < 16 * (uint64_t)n) bits <<= 1;
@@ -70,14 +80,15 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
     const int32_t r = rank ? rank[i] : kSpray;
     SH_CHECK(r >= kSpray && r < n_, "designated rank out of range");
     for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
-      Digest& e = hot_tab_[s];
+      HotSlot& e = hot_tab_[s];
       if (e.lo == d.lo && e.hi == d.hi) {
-        hot_rank_[s] = r;
+        e.rank = r;
         break;
       }
       if (!e.lo && !e.hi) {
-        e = d;
-        hot_rank_[s] = r;
+        e.lo = d.lo;
+        e.hi = d.hi;
+        e.rank = r;
         ++nhot_;
         break;
       }
@@ -115,67 +126,103 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     }
     return;
   }
-  // the filter word and the table line of the requests kPrefetch ahead are prefetched,
-  // so a group's cache misses overlap
-  for (int64_t g = a; g < b; g += kPrefetch) {
-    const int64_t e = std::min<int64_t>(b, g + kPrefetch);
-    for (int64_t i = g + kPrefetch; i < std::min<int64_t>(b, e + kPrefetch); ++i) {
-      const uint64_t lo = keys[i].lo;
-      __builtin_prefetch(&hot_bits_[((lo >> 20) & bits_mask_) >> 6]);
-      __builtin_prefetch(&hot_tab_[lo & hot_mask_]);
-    }
-    for (int64_t i = g; i < e; ++i) {
-      const Digest d = keys[i];
-      const int hr = hot_rank(d);
-      if (hr != kNotHot) {
-        if (kSets) {
-          dest[i] = -1;
-          for (int r = 0; r < n_; ++r) ++counts[r];
-        } else {
-          const int r = hr >= 0 ? hr : spray(seq0 + (uint64_t)i);
-          dest[i] = r;
-          ++counts[r];
+  // locals: the stores through dest / counts cannot make the compiler reload them
+  const uint64_t* const bits = hot_bits_.data();
+  const uint64_t bmask = bits_mask_, hmask = hot_mask_;
+  const HotSlot* const tab = hot_tab_.data();
+  for (int64_t i = a; i < b; ++i) {
+    const Digest d = keys[i];
+    const uint64_t fb = (d.lo >> 20) & bmask;
+    int hr = kNotHot;
+    if ((bits[fb >> 6] >> (fb & 63)) & 1) {
+      for (uint64_t s = d.lo & hmask;; s = (s + 1) & hmask) {
+        const HotSlot& e = tab[s];
+        if (e.lo == d.lo && e.hi == d.hi) {
+          hr = e.rank;
+          break;
         }
-      } else {
-        const int o = owner(d);
-        dest[i] = o;
-        ++counts[o];
+        if (!e.lo && !e.hi) break;
       }
+    }
+    if (hr != kNotHot) {
+      if (kSets) {
+        dest[i] = -1;
+        for (int r = 0; r < n_; ++r) ++counts[r];
+      } else {
+        const int r = hr >= 0 ? hr : spray(seq0 + (uint64_t)i);
+        dest[i] = r;
+        ++counts[r];
+      }
+    } else {
+      const int o = owner(d);
+      dest[i] = o;
+      ++counts[o];
     }
   }
 }
 
-namespace {
-template <typename F>
-void parallel_ranges(int64_t n, int threads, int nshards, int64_t* counts, F&& f) {
+void HostRouter::worker(int id) {
+  uint64_t seen = 0;
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+    if (stop_) return;
+    seen = gen_;
+    if (id >= want_) continue;
+    const std::function<void(int)>* job = job_;
+    lk.unlock();
+    (*job)(id);
+    lk.lock();
+    if (--left_ == 0) done_cv_.notify_one();
+  }
+}
+
+void HostRouter::parallel(int64_t n, int threads, int64_t* counts,
+                          const std::function<void(int64_t, int64_t, int64_t*)>& f) const {
   if (threads <= 1 || n < (1 << 16)) {
     f(0, n, counts);
     return;
   }
   threads = (int)std::min<int64_t>(threads, n >> 14);
-  std::vector<std::vector<int64_t>> part((size_t)threads, std::vector<int64_t>((size_t)nshards, 0));
-  std::vector<std::thread> th;
+  std::lock_guard<std::mutex> call(call_mu_);
+  std::vector<std::vector<int64_t>> part((size_t)threads, std::vector<int64_t>((size_t)n_, 0));
   const int64_t per = (n + threads - 1) / threads;
-  for (int t = 0; t < threads; ++t) {
-    const int64_t a = std::min(n, t * per), b = std::min(n, a + per);
-    th.emplace_back([&, t, a, b] { f(a, b, part[(size_t)t].data()); });
+  const std::function<void(int)> job = [&](int t) {
+    const int64_t lo = std::min(n, t * per), hi = std::min(n, lo + per);
+    f(lo, hi, part[(size_t)t].data());
+  };
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto* self = const_cast<HostRouter*>(this);
+    while ((int)pool_.size() < threads - 1) {
+      const int id = (int)pool_.size();
+      pool_.emplace_back([self, id] { self->worker(id); });
+    }
+    job_ = &job;
+    want_ = left_ = threads - 1;
+    ++gen_;
   }
-  for (auto& x : th) x.join();
+  cv_.notify_all();
+  job(threads - 1);  // the caller's own slice
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+  }
   for (const auto& p : part)
-    for (int r = 0; r < nshards; ++r) counts[r] += p[(size_t)r];
+    for (int r = 0; r < n_; ++r) counts[r] += p[(size_t)r];
 }
-}  // namespace
 
 void HostRouter::route_gets(const Digest* keys, int64_t n, uint64_t seq0, int32_t* dest,
                             int64_t* counts, int threads) const {
-  parallel_ranges(n, threads, n_, counts, [&](int64_t a, int64_t b, int64_t* c) {
+  parallel(n, threads, counts, [&](int64_t a, int64_t b, int64_t* c) {
     route_range<false>(keys, a, b, seq0, dest, c);
   });
 }
 
 void HostRouter::route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_t* counts,
                             int threads) const {
-  parallel_ranges(n, threads, n_, counts, [&](int64_t a, int64_t b, int64_t* c) {
+  parallel(n, threads, counts, [&](int64_t a, int64_t b, int64_t* c) {
     route_range<true>(keys, a, b, 0, dest, c);
   });
 }

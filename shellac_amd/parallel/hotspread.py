@@ -240,10 +240,13 @@ class HotSpread:
         self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
 
     # -- the native router ---------------------------------------------------------------
-    def host_route_gets(self, keys_host: torch.Tensor, seq0: int = 0, threads: int = 1):
-        """The native router on host digests: (dest int32 [n], counts int64 [world])."""
+    def host_route_gets(self, keys_host: torch.Tensor, seq0: int = 0, threads: int = 1,
+                        out: Optional[torch.Tensor] = None):
+        """The native router on host digests: (dest int32 [n], counts int64 [world]).
+        ``out``: a reused int32 destination buffer (a proxy routes into buffers it keeps;
+        fresh pages would add first-touch faults to the routing time)."""
         keys_host = keys_host.contiguous()
-        dest = torch.empty(keys_host.shape[0], dtype=torch.int32)
+        dest = out if out is not None else torch.empty(keys_host.shape[0], dtype=torch.int32)
         counts = torch.zeros(self.world, dtype=torch.int64)
         self.router.route_gets(keys_host.data_ptr(), keys_host.shape[0], int(seq0),
                                dest.data_ptr(), counts.data_ptr(), int(threads))
