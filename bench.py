@@ -5,15 +5,24 @@ Contract (see task README): ``python bench.py --gpus N --steps K --warmup W``;
 for N>1 launched by torch.distributed.run (one rank per GPU, RCCL). Prints ONE
 JSON line on rank 0.
 
-Step = one serving tick of the distributed cache on every rank:
-  * a GET batch of ``--batch`` Zipf(0.99) requests over the whole key space,
-    routed to owner shards (RCCL all-to-all), probed + gathered on the owner's
-    HBM by the HIP kernels, values returned to the requesting rank's HBM;
-  * a SET batch of ``--sets`` requests (same popularity law) routed, shipped
-    (payload all-to-all) and committed (dedupe, scan-allocate, log write, CAS
-    index insert) on the owners.
-Per-GPU work is fixed as N grows (weak scaling): each rank issues the same
-number of requests and owns ``--keys-per-gpu`` objects of the key space.
+Step = one serving tick of the distributed cache on every rank: a GET batch of Zipf(0.99)
+requests and a SET batch, probed / gathered and committed (dedupe, scan-allocate, log write
+with CLOCK reinsertions, CAS index insert) by the HIP kernels on the shard's HBM.
+  * One GPU: ``--batch`` GETs and ``--sets`` SETs over the ``--keys-per-gpu`` key space.
+  * N>1 ranks (default ``--route host``, the HTTP path's topology): every step draws ONE
+    global stream of N x --batch GETs and N x --sets SETs (same seeds on every rank); the
+    host router (ketama, csrc/host_router.cc) sends each request to the GPU owning its key,
+    the ``--spread`` hottest objects replicated on every GPU with their GETs spread to even
+    out the load. Each rank serves its true, unequal share; the timed region ends at the
+    slowest rank. No value crosses xGMI in the step. ``--route device``: the experimental
+    all-to-all step (GPU-resident batches routed between GPUs over RCCL; see docs/PERF.md).
+Per-GPU work is fixed as N grows (weak scaling): the key space is N x --keys-per-gpu.
+
+Headline (``--headline pressured``): the full cache — a shard log sized so its working set
+(every key it holds, one record each) fills --pressured-fill (0.8) of it, wrapped, so every
+SET batch's CLOCK hand re-appends the objects read since it last passed and evicts the rest
+(hit ratio < 1). Secondary: the fresh cache (``log_fresh``) and a 16 GiB log that has
+wrapped with the working set at ~1/4 of it (``log_wrapped``).
 
 Metric: whole-job cache operations per second (GET+SET requests served).
 The reference (kmacrow/Shellac) publishes no numbers, so vs_baseline is null.
@@ -57,8 +66,8 @@ def parse():
     ap.add_argument("--set-dist", choices=["uniform", "zipf"], default="uniform",
                     help="SET popularity: uniform (TTL refresh fills, default) or zipf")
     ap.add_argument("--replicate", type=int, default=None,
-                    help="hot objects replicated on every rank (N>1; 0 = off). Default: 4M "
-                         "up to 4 ranks, 2M at 8 (see docs/PERF.md, link model)")
+                    help="--route device: hot objects replicated on every rank (0 = off; "
+                         "default 1M, the per-N replica table in docs/PERF.md)")
     ap.add_argument("--replica-gb", type=float, default=None,
                     help="replica log GiB (default: 2 KiB per replicated object)")
     ap.add_argument("--sample-batches", type=int, default=32,
@@ -890,6 +899,10 @@ def main():
         if replica is not None:
             diag["replica_head_gib"] = round(replica.head() / (1 << 30), 3)
             diag["replica_log_gib"] = round(args.replica_gb, 3)
+        if args.check and clost:
+            # a SET row that neither fit its slot nor the carry leaves the owner's older
+            # value in place (a stale hit, not a miss): a checked run must not have any
+            raise SystemExit(f"[bench] check: {clost} routed SET rows were lost (carry full)")
     fresh_iv = timed(args.steps, args.warmup + args.steps, events=True)[1] if use_events else []
     # secondary: the same steps with every GET probed and copied (no in-batch request
     # collapsing)
@@ -1068,6 +1081,13 @@ def main():
         "hot_drift": drift,
         "smoke": sm,
     }
+    if host_route and out["host_routing"] and "host_route_req_per_s" in out["host_routing"]:
+        # what the host proxies can feed: one router per GPU share of the host's cores (the
+        # measured rate is this process's, on its share), against the job's request rate
+        hr_ = out["host_routing"]
+        cap_ = hr_["host_route_req_per_s"] * world
+        hr_["host_route_job_capacity_req_per_s"] = round(cap_, 1)
+        hr_["router_feeds_job"] = bool(cap_ >= value)
     if host_edge:
         # responses delivered into pinned host memory (GPU -> host over PCIe) against the
         # PCIe 5.0 x16 roofline (~63 GB/s per direction); the keys and SET payloads

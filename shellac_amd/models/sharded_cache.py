@@ -179,7 +179,7 @@ class ShardedCache:
         self.shard = shard
         self.group = group
         # native routed step: "single" = every collective of a step on one communicator and
-        # one stream in a fixed order (default: cannot deadlock); "channels" = one
+        # one stream in a fixed order (cannot deadlock); "channels" (the default) = one
         # communicator per channel (control, reply, SET) on the stream producing its data
         if comm_mode not in ("single", "channels"):
             raise ValueError(f"comm_mode must be 'single' or 'channels', not {comm_mode!r}")
