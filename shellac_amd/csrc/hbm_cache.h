@@ -269,7 +269,7 @@ class HbmCache {
   unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, entries scanned
   uint64_t rmax_ = 0;
   int64_t rc_cap_ = 0;
-  uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr;
+  uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr, *rc_hx_ = nullptr;
   int64_t rc_adv_w_ = 0;
   // store(phase=1) queued a batch's CLOCK hand and planning; store(phase=2) runs the rest
   // of its chain (append, index insert) from this record

@@ -2252,12 +2252,16 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 //                  meets_j = loc_j + cap >= head + B + min(hx_j, rmax)
 //              which is monotone over valid entries (a valid entry's loc grows at least by
 //              the hot bytes of the entries before it), so an entry is consumed iff it does
-//              not meet the bound: the pick needs no grid-wide cut. Picked records are staged
-//              in the scratch buffer (their old bytes lie in the region the combined batch
-//              overwrites) by the workgroup's waves; the first meeting entry is min-reduced
+//              not meet the bound: the pick needs no grid-wide cut. It writes the staging
+//              copy's plan (offset hx, picked length, log offset per entry); the first
+//              meeting entry is min-reduced
 //              (an atomic, no fence: k_set_dedupe, the next launch on the stream, advances
 //              the hand and resets the control words — a last-workgroup hand-off here needs
 //              an agent-scope release per workgroup, an L2 write-back beside the gather).
+//   k_segcopy<2> stages the picked records in the scratch buffer (their old bytes lie in the
+//              region the combined batch overwrites) on the byte mover's resident grid.
+//              (The emit's own workgroups staging their picks — 512 workgroups, 2 waves per
+//              SIMD — took 100-150 us for ~40 MB in the pressured step, latency-bound.)
 // The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
 // win over a reinsertion of the same key). Host twin: HostCache::reclaim.
 struct RcArgs {
@@ -2381,22 +2385,19 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
 }
 
 __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
-                                                    const uint8_t* __restrict__ log,
-                                                    const uint64_t* __restrict__ rc_loc,
-                                                    const uint64_t* __restrict__ rc_h,
+                                                    uint64_t* __restrict__ rc_loc,
+                                                    uint64_t* __restrict__ rc_h,
                                                     const uint64_t* __restrict__ part_h,
-                                                    uint8_t* __restrict__ scratch,
+                                                    uint64_t* __restrict__ rc_hx,
+                                                    const uint8_t* __restrict__ scratch,
                                                     CacheCounters* __restrict__ ctr) {
   __shared__ unsigned long long s_w[kBlock / 64];
   __shared__ unsigned long long s_pre;
-  __shared__ uint64_t s_src[kBlock], s_dst[kBlock], s_len[kBlock];
-  __shared__ int s_n;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long pre = 0;
   for (unsigned b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += part_h[b];
   pre = wave_sum(pre);
   if (lane == 0) s_w[w] = pre;
-  if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   if (threadIdx.x == 0) s_pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
   __syncthreads();
@@ -2419,72 +2420,28 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
     const uint64_t loc = rc_loc[j];
     const uint64_t r = hx < a.rmax ? hx : a.rmax;
     meets = loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r;
+    bool pick = false;
     if (h) {
       if (!meets && hx + h <= a.rmax) {
+        pick = true;
         cb.voff[j] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
         cb.from[j] = loc + 1;  // indexed as a move from the entry that points here
-        const int k = atomicAdd(&s_n, 1);
-        s_src[k] = loc % a.cap;
-        s_dst[k] = hx;
-        s_len[k] = h;
         ++nre;
         bre += cb.vlen[j];
       } else {
         cb.vlen[j] = kSkipVlen;  // consumed past the budget, or not consumed: ages out
       }
     }
+    // the staging copy's plan (k_segcopy<2>, the next launch): entry j's record goes from
+    // its log offset to scratch + hx, only when picked (a zero length leaves the gap)
+    rc_hx[j] = hx;
+    rc_h[j] = pick ? h : 0;
+    rc_loc[j] = pick ? loc % a.cap : 0;
+    if (j == a.W - 1) rc_hx[a.W] = hx + h;
   }
   // only the first entry meeting the bound matters: one atomic per wave (its lowest lane)
   const unsigned long long mb = __ballot(meets);
   if (mb && lane == __ffsll((long long)mb) - 1) atomicMin(&a.ctl[2], (unsigned long long)j);
-  __syncthreads();
-  // Stage the picked records. Their 16-B chunks are numbered across the workgroup (an
-  // exclusive scan of the chunk counts in LDS) and every thread copies chunks q, q + kBlock,
-  // ... with kStageU loads in flight before its stores. (One wave per record, one chunk
-  // per lane per dependent load/store round, left a ~50-record workgroup latency-bound:
-  // 142 us for the 36 MB a pressured step reinserts.)
-  constexpr int kStageU = 4;
-  __shared__ uint32_t s_cw[kBlock / 64], s_cpre[kBlock];
-  const int np = s_n;
-  const uint32_t nc = threadIdx.x < np ? (uint32_t)(s_len[threadIdx.x] >> 4) : 0u;
-  uint32_t ci = nc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(ci, d);
-    if (lane >= d) ci += o;
-  }
-  if (lane == 63) s_cw[w] = ci;
-  __syncthreads();
-  uint32_t cbase = 0, total = 0;
-#pragma unroll
-  for (int k = 0; k < kBlock / 64; ++k) {
-    if (k < w) cbase += s_cw[k];
-    total += s_cw[k];
-  }
-  s_cpre[threadIdx.x] = cbase + ci - nc;
-  __syncthreads();
-  for (uint32_t q0 = threadIdx.x; q0 < total; q0 += kBlock * kStageU) {
-    u32x4 v[kStageU];
-    u32x4* dp[kStageU];
-#pragma unroll
-    for (int u = 0; u < kStageU; ++u) {
-      const uint32_t q = q0 + (uint32_t)u * kBlock;
-      dp[u] = nullptr;
-      if (q < total) {
-        int lo = 0, hi = np - 1;  // the last record whose first chunk is <= q
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (s_cpre[mid] <= q) lo = mid; else hi = mid - 1;
-        }
-        const uint32_t c = q - s_cpre[lo];
-        v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(log + s_src[lo]) + c);
-        dp[u] = reinterpret_cast<u32x4*>(scratch + s_dst[lo]) + c;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kStageU; ++u)
-      if (dp[u]) *dp[u] = v[u];
-  }
   block_count(ctr, nre, &CacheCounters::reinserted, bre, &CacheCounters::reinsert_bytes);
 }
 
@@ -3019,7 +2976,7 @@ HbmCache::~HbmCache() {
                     (void*)w.set_off, (void*)w.set_claim, (void*)w.set_cnt})
       (void)hipFree(p);
   (void)hipFree(ring_); (void)hipFree(rc_ctl_);
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) (void)hipFree(p);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_, (void*)rc_hx_}) (void)hipFree(p);
   for (HandBuf& b : hb_)
     for (void* p : {(void*)b.keys, (void*)b.voff, (void*)b.from, (void*)b.vlen, (void*)b.flags,
                     (void*)b.expire, (void*)b.scratch})
@@ -3054,10 +3011,11 @@ void HbmCache::ensure_rc_ws(int64_t w, hipStream_t s) {
   if (w <= rc_cap_) return;
   int64_t cap = rc_cap_ ? rc_cap_ : 4096;
   while (cap < w) cap *= 2;
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_}) retire(p);
+  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_, (void*)rc_hx_}) retire(p);
   HIP_OK(hipMalloc(&rc_loc_, cap * 8));
   HIP_OK(hipMalloc(&rc_h_, cap * 8));
   HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
+  HIP_OK(hipMalloc(&rc_hx_, (cap + 1) * 8));
   rc_cap_ = cap;
 }
 
@@ -3106,8 +3064,10 @@ void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const u
   hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, cb, log_, index_, cfg_.nbuckets - 1,
                      keys, values, val_off, vlen, flags, expire, n, cfg_.max_item, rc_loc_, rc_h_,
                      rc_part_);
-  hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, log_, rc_loc_, rc_h_, rc_part_,
-                     hb.scratch, ctr_);
+  hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, rc_loc_, rc_h_, rc_part_,
+                     rc_hx_, hb.scratch, ctr_);
+  launch_segcopy<2>(s, log_, rc_loc_, rc_hx_, w, hb.scratch, nullptr, nullptr, nullptr, nullptr,
+                    rc_h_, rmax);
   rc_adv_w_ = w;  // the combined batch's dedupe advances the hand
   HIP_OK(hipGetLastError());
 }
