@@ -638,7 +638,7 @@ def main():
 
     # Per-step GPU timing events are recorded in a separate pass after the timed one: an
     # event record is a marker packet on the stream, and one between every two steps cost
-    # ~6 us of a 0.32 ms step (profiles/r2_bench_events_ab.log)
+    # ~6 us of a 0.32 ms step (profiles/archive/r2_bench_events_ab.log)
     use_events = dev.type == "cuda"
     rdev = torch.device("cpu") if bounce else dev  # gloo reduces host tensors
 

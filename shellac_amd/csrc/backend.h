@@ -172,7 +172,7 @@ struct HbmBackendConfig {
   bool edge_server = true;
   // server jobs that may be ahead of a batch sent to it: 2 = a batch waits behind at most
   // one job (~4-9 us) rather than take a launch (~15 us) — c=10 284K vs 252K RPS at 1
-  // (profiles/r3_http)
+  // (profiles/archive/r3_http)
   int serve_backlog = 2;
   // resident edge-server blocks per GPU (ShardConfig::serve_blocks): jobs of different
   // submitters are served side by side; serve_backlog counts jobs per block

@@ -1035,7 +1035,7 @@ void HbmBackend::Dev::launch(Flight& f) {
     if (ordered) ordered_gets++;
     // ... and only while fewer than serve_backlog jobs are ahead of it: the server takes
     // one job at a time, so under load (several batches in flight) the launched path's
-    // many workgroups win (profiles/r3_http: c=1000 with every small batch served 0.95M
+    // many workgroups win (profiles/archive/r3_http: c=1000 with every small batch served 0.95M
     // RPS, launched only 1.13M)
     f.served = be->cfg_.edge_server && !ordered && f.rows <= (size_t)HbmCache::kServeKeys &&
                cache->serve_backlog() <

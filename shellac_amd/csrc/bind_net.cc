@@ -298,7 +298,7 @@ void bind_net(py::module_& m) {
              if (c.compress && c.gzip_gpu >= 0) {
                // service workers (each its own engine and stream), default 2: with 4 the
                // bodies split into twice as many smaller batches and the per-batch host
-               // work grew (49.8K vs 70.6K misses/s, profiles/r2_http_compress_workers_ab.log)
+               // work grew (49.8K vs 70.6K misses/s, profiles/archive/r2_http_compress_workers_ab.log)
                px->set_compressor(std::make_shared<GzipService>(c.gzip_gpu, c.gzip_batch_us,
                                                                 4096, std::max(1, gzip_workers)));
              }

@@ -61,7 +61,7 @@ constexpr int kTileSegCap = 1024;          // segments staged in LDS per tile
 constexpr int kMaxGrid = 2048;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Tuned constants (round-2 sweeps, profiles/r1_probe_grid_sweep.log,
+// Tuned constants (round-2 sweeps, profiles/archive/r1_probe_grid_sweep.log,
 // r1_segcopy_store_ab.log, r1_overlap_sweep.log; the A/B knobs are gone):
 //  * k_probe / k_coalesce grids cap at kMaxGrid workgroups (halving the grid nearly
 //    doubled a 1M-key probe: it is bound by random lines in flight);
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_offsets(const uint64_t* __restrict__
   // (from cache) and scans. (Lane-contiguous runs of `per` items made every load and
   // store instruction touch 64 different lines: 27 us per 1M items beside the SET append,
   // now 20 us. The step did not move, 0.319-0.321 vs 0.320-0.323 ms over three rounds
-  // (profiles/r2_offsets_ab.log): the gather then starts earlier into the SET append.)
+  // (profiles/archive/r2_offsets_ab.log): the gather then starts earlier into the SET append.)
   // Up to kOffRegs x 64 items per wave (the lookup's 1M rows: 512) are loaded once, all
   // in flight together, and scanned from registers: the two dependent passes of 64 items
   // per step were latency-bound, 20-28 us per 1M rows between the lookup and the gather.
@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_get(
 // ---------------------------------------------------------------------------------
 // Persistent edge-GET server (HbmCache::serve_get). One 512-thread workgroup stays
 // resident and polls a ring of jobs in pinned, coherent host memory, so a micro-batch
-// costs no kernel launch (profiles/r2_edge_get_latency.log: a launch + completion round
+// costs no kernel launch (profiles/archive/r2_edge_get_latency.log: a launch + completion round
 // trip is 14-19 us of the proxy's 25-33 us batch).
 // Transport: a job is 64 granules of 16 B, each {payload word, tag = ticket + 1}: five
 // header granules (arena, capacity, offsets array, n | now, host slot) and two per key.

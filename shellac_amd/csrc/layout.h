@@ -100,7 +100,7 @@ inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
 // Every window entry costs a scan row and a (skip) row of the combined SET chain, so the
 // window is the fixed cost of a SET batch once the log has wrapped: k = 4 made the
 // steady-state N=1 step 0.91 ms at a 5 GiB log and 0.41 ms at 16 GiB, k = 2 0.51 / 0.37
-// ms with the same hit ratio and reinsertions (profiles/r2_hand_window_ab.log); the
+// ms with the same hit ratio and reinsertions (profiles/archive/r2_hand_window_ab.log); the
 // evict_sim hit ratios are identical for k = 2, 3, 4; k = 1 does not cover the batch's own
 // bytes and degrades to FIFO.
 constexpr int64_t kHandWindowK = 2;

@@ -237,7 +237,7 @@ class ShardedCache:
         self.coalesce = True
         # (Two other N=1 schedules were measured slower and removed: a compacting lookup
         # with bump-allocated response offsets, and the SET planning kernels ahead of the
-        # lookup; profiles/r2_step_schedule_ab.md.)
+        # lookup; profiles/archive/r2_step_schedule_ab.md.)
         # (Queuing the SET index insert after the host read the lookup total, with no
         # event between lookup and gather, needs the total published only once every
         # lookup workgroup has released its outputs: a device-scope fence per workgroup,
@@ -248,7 +248,7 @@ class ShardedCache:
         # release / no system fence (both streams are on one GPU; nothing on the host reads
         # what these events order, and every kernel dispatch carries its own release). One
         # box, two rounds: 0.309 / 0.308 ms per step with "device" vs 0.315 / 0.311 with
-        # "system" (profiles/r2_event_fence_ab.log); round 4, one box, two rounds each:
+        # "system" (profiles/archive/r2_event_fence_ab.log); round 4, one box, two rounds each:
         # wrapped 0.3362 / 0.3363 "device" vs 0.3313 / 0.3304 "none", fresh 0.3008 / 0.3004
         # vs 0.2953 / 0.2952 (profiles/r4h_fence)
         self.event_fence = "none"

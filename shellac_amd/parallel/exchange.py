@@ -81,7 +81,7 @@ def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, output_split_sizes=N
         return _Done() if async_op else None
     # Straight to the process group's C++ collective: torch.distributed's Python wrapper
     # spends ~36 us per call on argument checks and group bookkeeping (cProfile of the
-    # routed step, profiles/r2_routed_host_profile.txt), and a step issues 5 of them.
+    # routed step, profiles/archive/r2_routed_host_profile.txt), and a step issues 5 of them.
     pg = group if group is not None else _default_group()
     opts = dist.AllToAllOptions()
     work = pg.alltoall_base(out, inp, list(output_split_sizes or []),
