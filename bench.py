@@ -962,6 +962,10 @@ def main():
             # the cost of a step varies with where the hand is in the lap (the objects it
             # re-appended one lap earlier come round together): one whole lap, timed
             lap_steps = int(p_log / max(1.0, (pw["head1"] - pw["head0"]) / args.steps)) + 1
+            if real_world > 1:  # one step count on every rank (the longest lap)
+                lt = torch.tensor([lap_steps], dtype=torch.int64, device=rdev)
+                dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+                lap_steps = int(lt)
             lap_el = timed(lap_steps, pbase + pfill + 2 * args.steps, cache=p_sc)[0]
             pressured["lap_steps"] = lap_steps
             pressured["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
