@@ -29,6 +29,7 @@
 #include "backend.h"
 #include "digest.h"
 #include "host_cache.h"
+#include "host_router.h"
 #include "http.h"
 #include "ketama.h"
 #include "loadgen.h"
@@ -163,6 +164,40 @@ void test_ketama() {
     if (owner[i] != 1) moved += o != owner[i];
   }
   CHECK(moved == 0);  // only the ejected node's keys move
+}
+
+// The host router's worker pool: threaded routing equals one thread's, call after call
+// (the pool is reused), for GETs and SETs, with and without a hot set.
+void test_host_router_pool() {
+  HostRouter r(8, 64);
+  std::vector<Digest> keys(200000);
+  uint64_t x = 0x243F6A8885A308D3ull;
+  for (auto& d : keys) {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    d.lo = x;
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    d.hi = x;
+  }
+  std::vector<int32_t> rank(4096);
+  for (int i = 0; i < 4096; ++i) rank[(size_t)i] = i < 3 ? -1 : i % 8;
+  const std::vector<double> w(8, 1.0);
+  for (int hot = 0; hot < 2; ++hot) {
+    r.set_hot(keys.data(), hot ? 4096 : 0, rank.data(), w.data());
+    std::vector<int32_t> d1(keys.size()), dn(keys.size());
+    std::vector<int64_t> c1(8, 0), cn(8, 0);
+    r.route_gets(keys.data(), (int64_t)keys.size(), 77, d1.data(), c1.data(), 1);
+    for (int rep = 0; rep < 3; ++rep) {
+      std::fill(cn.begin(), cn.end(), 0);
+      r.route_gets(keys.data(), (int64_t)keys.size(), 77, dn.data(), cn.data(), 4);
+      CHECK(dn == d1 && cn == c1);
+    }
+    r.route_sets(keys.data(), (int64_t)keys.size(), d1.data(), c1.data(), 1);
+    r.route_sets(keys.data(), (int64_t)keys.size(), dn.data(), cn.data(), 3);
+    CHECK(dn == d1);
+    int64_t hot_rows = 0;
+    for (int32_t v : d1) hot_rows += v < 0;
+    CHECK(hot_rows == (hot ? 4096 : 0));
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -315,6 +350,7 @@ int main(int argc, char** argv) {
       {"http_parser", test_http_parser_splits_and_garbage},
       {"stream_buf", test_stream_buf},
       {"ketama", test_ketama},
+      {"host_router_pool", test_host_router_pool},
       {"proxy_threads_dram", [] { test_proxy_threads_dram(nullptr); }},
       {"proxy_threads_fault", [] { test_proxy_threads_dram("get_miss=0.3,set_drop=0.3,delay_us=200"); }},
       {"proxy_memcached_node", test_proxy_over_memcached_node},
