@@ -1002,7 +1002,8 @@ def main():
         parallelism = (f"shard{world} (host-routed: ketama on the host proxies sends each "
                        f"request to the GPU owning its key"
                        + (f", the {args.spread} hottest objects replicated on every GPU and "
-                          f"their GETs sprayed" if args.spread else "") +
+                          f"their GETs spread over the GPUs ({args.spread_policy})"
+                          if args.spread else "") +
                        "; no GPU-to-GPU value traffic in the step)")
     else:
         parallelism = f"shard{world} (all-to-all routed, {args.comm_mode} communicator mode)"
