@@ -252,7 +252,7 @@ class HbmCache {
   void reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                       const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                       int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s,
-                      bool detached);
+                      bool detached, bool lead);
   uint64_t* cur_ring_tail() const { return head_ + 2 + hsel_; }
   uint64_t* next_ring_tail() const { return head_ + 2 + (hsel_ ^ 1); }
   // Deferred frees (no device-wide synchronisation on the serving path): a grown buffer's

@@ -2249,19 +2249,26 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 //              skip rows, and the batch's own rows are copied behind the window.
 //   k_rc_emit  the exclusive scan of h (block partials of the previous launch + a block
 //              scan) gives each entry its reinsertion offset hx and its cut test
-//                  meets_j = loc_j + cap >= head + B + min(hx_j, rmax)
+//                  meets_j = loc_j + cap >= head + B + min(hx_j, rmax) + lead
 //              which is monotone over valid entries (a valid entry's loc grows at least by
 //              the hot bytes of the entries before it), so an entry is consumed iff it does
-//              not meet the bound: the pick needs no grid-wide cut. It writes the staging
-//              copy's plan (offset hx, picked length, log offset per entry); the first
-//              meeting entry is min-reduced
-//              (an atomic, no fence: k_set_dedupe, the next launch on the stream, advances
-//              the hand and resets the control words — a last-workgroup hand-off here needs
-//              an agent-scope release per workgroup, an L2 write-back beside the gather).
-//   k_segcopy<2> stages the picked records in the scratch buffer (their old bytes lie in the
-//              region the combined batch overwrites) on the byte mover's resident grid.
-//              (The emit's own workgroups staging their picks — 512 workgroups, 2 waves per
-//              SIMD — took 100-150 us for ~40 MB in the pressured step, latency-bound.)
+//              not meet the bound: the pick needs no grid-wide cut. The first meeting entry
+//              is min-reduced (an atomic, no fence: k_set_dedupe, the next launch on the
+//              stream, advances the hand and resets the control words — a last-workgroup
+//              hand-off here needs an agent-scope release per workgroup, an L2 write-back
+//              beside the gather).
+// Lead mode (a log of at least 16 x (batch bound + rmax), HBM serving shards): the hand runs
+// lead = rmax + 1.25 B ahead of the overwrite and decides about entries about two batches
+// before the log overwrites them. A pick then lies beyond everything the batch can
+// overwrite, so the log append copies it straight from its old place — one copy per
+// reinserted byte — and, above all, a referenced object has moved before any lookup's
+// reserve (the next SET's bytes + rmax, treated as misses) reaches its old copy: without the
+// lead every hot object near the tail missed for a step or two per lap (the 5 GiB shard's
+// hit ratio 0.963 -> 0.998, profiles/r5x_hand_lead). On a small log (a batch a sizeable
+// share of it) deciding two batches early costs hit ratio instead, so there the hand has no
+// lead and
+//   k_segcopy<2> stages the picked records in scratch (their old bytes lie in the region
+//              the batch overwrites, which the previous step's gather may still read).
 // The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
 // win over a reinsertion of the same key). Host twin: HostCache::reclaim.
 struct RcArgs {
@@ -2274,6 +2281,9 @@ struct RcArgs {
   uint64_t cap;
   uint32_t now;
   uint64_t rmax;
+  // 1: the hand runs `lead` = rmax + 1.25 B ahead of the overwrite and its picks are
+  // copied straight from the log; 0: no lead, picks staged through scratch (see below)
+  uint64_t lead_mode;
 };
 
 // The combined SET batch (rows [0, W) reinsertions, [W, W + n) the batch). `from`: a
@@ -2385,6 +2395,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
 }
 
 __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
+                                                    const uint8_t* __restrict__ log,
                                                     uint64_t* __restrict__ rc_loc,
                                                     uint64_t* __restrict__ rc_h,
                                                     const uint64_t* __restrict__ part_h,
@@ -2419,25 +2430,33 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
   if (j < a.W) {
     const uint64_t loc = rc_loc[j];
     const uint64_t r = hx < a.rmax ? hx : a.rmax;
-    meets = loc != kRingSkip && loc + a.cap >= *a.head_ptr + a.ctl[1] + r;
+    const uint64_t head = *a.head_ptr, bb = a.ctl[1];
+    const uint64_t lead = a.lead_mode ? a.rmax + bb + (bb >> 2) : 0;
+    meets = loc != kRingSkip && loc + a.cap >= head + bb + r + lead;
     bool pick = false;
     if (h) {
-      if (!meets && hx + h <= a.rmax) {
+      // lead mode: a pick must lie beyond everything the batch can overwrite (its bytes +
+      // the whole budget); an unsafe one (the hand not yet `lead` ahead: the first steps
+      // after the log fills, a batch much larger than the last) ages out
+      if (!meets && hx + h <= a.rmax && (!a.lead_mode || loc + a.cap >= head + bb + a.rmax)) {
         pick = true;
-        cb.voff[j] = (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
+        cb.voff[j] = a.lead_mode ? (uint64_t)(uintptr_t)log + loc % a.cap + kItemHeaderBytes
+                                 : (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
         cb.from[j] = loc + 1;  // indexed as a move from the entry that points here
         ++nre;
         bre += cb.vlen[j];
       } else {
-        cb.vlen[j] = kSkipVlen;  // consumed past the budget, or not consumed: ages out
+        cb.vlen[j] = kSkipVlen;  // consumed past the budget or unsafe, or not consumed
       }
     }
-    // the staging copy's plan (k_segcopy<2>, the next launch): entry j's record goes from
-    // its log offset to scratch + hx, only when picked (a zero length leaves the gap)
-    rc_hx[j] = hx;
-    rc_h[j] = pick ? h : 0;
-    rc_loc[j] = pick ? loc % a.cap : 0;
-    if (j == a.W - 1) rc_hx[a.W] = hx + h;
+    if (!a.lead_mode) {
+      // the staging copy's plan (k_segcopy<2>, the next launch): entry j's record goes
+      // from its log offset to scratch + hx, only when picked (a zero length leaves a gap)
+      rc_hx[j] = hx;
+      rc_h[j] = pick ? h : 0;
+      rc_loc[j] = pick ? loc % a.cap : 0;
+      if (j == a.W - 1) rc_hx[a.W] = hx + h;
+    }
   }
   // only the first entry meeting the bound matters: one atomic per wave (its lowest lane)
   const unsigned long long mb = __ballot(meets);
@@ -3051,23 +3070,24 @@ bool HbmCache::should_reclaim(uint64_t bytes_bound) const {
 void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                               const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                               int64_t n, int64_t w, uint64_t rmax, uint32_t now, hipStream_t s,
-                              bool detached) {
+                              bool detached, bool lead) {
   // The head: the claim word, i.e. the head every queued append will have reached (equal to
   // the head slot once they have run). The ring tail: a detached hand may run before the
   // previous batch's fixup writes its ring entries and tail, so it reads the tail of the
   // batch before that one (the other ping-pong slot), whose entries are written.
   RcArgs a{ring_, ring_cap_ - 1, detached ? next_ring_tail() : cur_ring_tail(), rc_ctl_, w,
-           claim_ptr(), cfg_.log_bytes, now, rmax};
+           claim_ptr(), cfg_.log_bytes, now, rmax, lead ? 1ull : 0ull};
   const int g = (int)((w + kBlock - 1) / kBlock);
   const HandBuf& hb = hb_[hand_b_];
   const RcBatch cb{hb.keys, hb.voff, hb.vlen, hb.flags, hb.expire, hb.from};
   hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, cb, log_, index_, cfg_.nbuckets - 1,
                      keys, values, val_off, vlen, flags, expire, n, cfg_.max_item, rc_loc_, rc_h_,
                      rc_part_);
-  hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, rc_loc_, rc_h_, rc_part_,
-                     rc_hx_, hb.scratch, ctr_);
-  launch_segcopy<2>(s, log_, rc_loc_, rc_hx_, w, hb.scratch, nullptr, nullptr, nullptr, nullptr,
-                    rc_h_, rmax);
+  hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, log_, rc_loc_, rc_h_,
+                     rc_part_, rc_hx_, hb.scratch, ctr_);
+  if (!lead)
+    launch_segcopy<2>(s, log_, rc_loc_, rc_hx_, w, hb.scratch, nullptr, nullptr, nullptr,
+                      nullptr, rc_h_, rmax);
   rc_adv_w_ = w;  // the combined batch's dedupe advances the hand
   HIP_OK(hipGetLastError());
 }
@@ -3416,7 +3436,8 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     hand_b_ = p.parity;
     ensure_cb(hand_b_, w + n, s);
     ensure_set_ws(w + n, s);
-    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, detached);
+    reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, detached,
+                   hand_lead(cfg_.log_bytes, bytes_bound, rmax));
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     const HandBuf& hb = hb_[hand_b_];
     p.rows = w + n;

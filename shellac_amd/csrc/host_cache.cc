@@ -175,7 +175,8 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
     SH_CHECK(bound <= log_bytes_ / 2, "SET batch larger than half the log; split the batch");
     const uint64_t rmax = std::min<uint64_t>(rmax_, log_bytes_ / 2 - bound) / 16 * 16;
     // the device's combined batch: reinsertions (in log order) ahead of the batch
-    if (rmax) reclaim_locked(n, bytes, rmax, now, &rows, &stage);
+    if (rmax)
+      reclaim_locked(n, bytes, rmax, now, &rows, &stage, hand_lead(log_bytes_, bound, rmax));
   }
   rows.reserve(rows.size() + (size_t)n);
   for (int64_t i = 0; i < n; ++i)
@@ -186,7 +187,7 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
 
 void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_t now,
                                std::vector<Row>* out,
-                               std::vector<uint8_t>* stage) {
+                               std::vector<uint8_t>* stage, bool lead_mode) {
   const int64_t w = hand_window(n);
   const uint64_t rcap = ring_.size(), rmask = rcap - 1;
   const uint64_t avail = ring_tail_ - hand_;
@@ -194,6 +195,8 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
   struct Hot { int64_t j; uint64_t loc, h, hx; };
   std::vector<Hot> hot;
   uint64_t hx = 0, consumed = weff;
+  // lead mode: the hand's lead and a pick's safety bound (HbmCache k_rc_emit's rules)
+  const uint64_t lead = lead_mode ? rmax + bytes + (bytes >> 2) : 0;
   for (uint64_t j = 0; j < weff; ++j) {
     const uint64_t idx = hand_ + j;
     const uint64_t l = ring_tail_ - idx <= rcap ? ring_[idx & rmask] : kRingSkip;
@@ -201,8 +204,8 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
     ItemHeader h;
     std::memcpy(&h, log_ + l % log_bytes_, sizeof h);
     if (h.magic != kItemMagic) continue;
-    // stop at the first item the overwrite (batch + reinsertions so far) does not reach
-    if (l + log_bytes_ >= head_ + bytes + std::min(hx, rmax)) {
+    // stop at the first item `lead` past the overwrite (batch + reinsertions so far)
+    if (l + log_bytes_ >= head_ + bytes + std::min(hx, rmax) + lead) {
       consumed = j;
       break;
     }
@@ -220,11 +223,15 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
   }
   out->clear();
   uint64_t staged = 0;
+  auto picked = [&](const Hot& t) {
+    return (uint64_t)t.j < consumed && t.hx + t.h <= rmax &&
+           (!lead_mode || t.loc + log_bytes_ >= head_ + bytes + rmax);
+  };
   for (const Hot& t : hot)
-    if ((uint64_t)t.j < consumed && t.hx + t.h <= rmax) staged = t.hx + t.h;
+    if (picked(t)) staged = t.hx + t.h;
   stage->assign(staged + 16, 0);
   for (const Hot& t : hot) {
-    if ((uint64_t)t.j >= consumed || t.hx + t.h > rmax) continue;
+    if (!picked(t)) continue;
     const uint8_t* rec = log_ + t.loc % log_bytes_;
     std::memcpy(stage->data() + t.hx, rec, t.h);
     ItemHeader h;

@@ -72,7 +72,7 @@ class HostCache {
   // algorithm, sequentially): appends the reinsertion rows to `out`, their records
   // staged in `stage`.
   void reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_t now,
-                      std::vector<Row>* out, std::vector<uint8_t>* stage);
+                      std::vector<Row>* out, std::vector<uint8_t>* stage, bool lead_mode);
 
   uint64_t log_bytes_, nbuckets_, mask_;
   uint32_t max_item_;

@@ -108,6 +108,12 @@ inline int64_t hand_window(int64_t n) {
   const int64_t w = kHandWindowK * n + 256;
   return w < (1 << 20) ? w : (1 << 20);
 }
+// Whether the hand runs ahead of the overwrite (lead mode, HbmCache k_rc_emit): on a log of
+// at least 16 x (the batch's byte bound + the reinsertion budget). Both engines decide the
+// same way from the same bound.
+inline bool hand_lead(uint64_t log_bytes, uint64_t bytes_bound, uint64_t rmax) {
+  return log_bytes >= 16 * (bytes_bound + rmax);
+}
 inline uint64_t ring_entries(uint64_t nbuckets) {
   uint64_t r = 4096;
   while (r < 2 * nbuckets * kEntriesPerBucket) r <<= 1;
