@@ -158,3 +158,32 @@ def test_clock_hand_skips_dead_same_digest_entry_host():
 @pytest.mark.gpu
 def test_clock_hand_skips_dead_same_digest_entry_gpu(cuda_dev):
     _dead_twin_survives_the_hand(cuda_dev)
+
+
+def _lead_trace(dev):
+    """A log 32x the largest SET batch (the HBM shards' shape): the hand runs in lead mode
+    (layout.h hand_lead: decisions ~two batches ahead of the overwrite, picks copied straight
+    from the log). Working set 1.5x the log, 64-request micro-batches."""
+    from shellac_amd._native import core  # noqa: F401  (the native module must load)
+
+    sizes, reqs = evict_sim.make_trace(40000, 400000, 0.99, 64, 4096, seed=11)
+    ws = sum(evict_sim.item_bytes(int(v)) for v in sizes)
+    log = int(ws / 1.5) // 16 * 16
+    rmax = max(1 << 20, min(log // 32, 1 << 30)) // 16 * 16
+    assert log >= 16 * (64 * evict_sim.item_bytes(4096) + rmax)  # lead mode for every batch
+    warm = 100000 // 64 * 64
+    r = evict_sim.cache_hit_ratio(sizes, reqs, log, 64, warm, dev, "clock")
+    return r, evict_sim.lru_hit_ratio(sizes, reqs, log, 64, warm)
+
+
+def test_clock_lead_mode_tracks_lru_host():
+    r, lru = _lead_trace("cpu")
+    assert r["reinserted"] > 0
+    assert r["hit_ratio"] >= lru - 0.02, (r, lru)
+
+
+@pytest.mark.gpu
+def test_clock_lead_mode_gpu_matches_host(cuda_dev):
+    g, _ = _lead_trace(cuda_dev)
+    h, _ = _lead_trace("cpu")
+    assert g == h and g["reinserted"] > 0
