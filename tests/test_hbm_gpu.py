@@ -1042,21 +1042,27 @@ def test_serve_wrapped_log_ground_truth_both_hand_schedules(cuda_dev, hand):
         assert y is None or y[0] == t
 
 
-@pytest.mark.parametrize("hand", ["early", "inline"])
-def test_serve_back_to_back_updates_never_resurrect_stale_values(cuda_dev, hand):
+@pytest.mark.parametrize("hand,lead", [("early", False), ("inline", False), ("early", True)])
+def test_serve_back_to_back_updates_never_resurrect_stale_values(cuda_dev, hand, lead):
     """Steps queued back to back (no host sync) over a full cache whose SET batches UPDATE
     objects (new payload versions) and DELETE some: the early hand of step k+1 runs beside
     step k's index insert, so it may pick for reinsertion an object step k's SET or DELETE
     is superseding. Its reinsertion is a move that must then be dropped. Every GET of step
     k returns the version the SETs of steps < k left, or a miss — never an older version
-    and never a deleted key — and the hand does reinsert."""
+    and never a deleted key — and the hand does reinsert. lead: a log 32x the SET batch, so
+    the hand runs in lead mode (decisions two batches ahead, reinsertions copied straight
+    from the log, layout.h hand_lead)."""
     from shellac_amd.bench.workload import Workload
     from shellac_amd.models.sharded_cache import ShardedCache
 
-    N = 60000
+    N = 300000 if lead else 60000
+    log = (128 << 20) if lead else (16 << 20)
     wl = Workload(N, cuda_dev, min_val=64, max_val=2048)
-    # ~25 MB of records into a 16 MiB log: the populate wraps it, every step runs the hand
-    sc = ShardedCache(CacheShard(16 << 20, 1 << 16, 1 << 13, cuda_dev), hand=hand)
+    # ~25 MB of records into a 16 MiB log (lead: ~185 MB into 128 MiB): the populate wraps
+    # it, every step runs the hand
+    shard = CacheShard(log, 1 << 18 if lead else 1 << 16, 1 << 13, cuda_dev)
+    sc = ShardedCache(shard, hand=hand)
+    rmax = shard._impl.reinsert_max
     for s0 in range(0, N, 5000):
         sc.set(_compact(wl.set_batch(torch.arange(s0, s0 + 5000, device=cuda_dev))))
     sc.sync_sets()
@@ -1072,6 +1078,8 @@ def test_serve_back_to_back_updates_never_resurrect_stale_values(cuda_dev, hand)
         up = torch.cat([wl.sample_ids(1500, 500 + k), wl.uniform_ids(1500, 700 + k)])
         truth_at.append((ids.tolist(), list(version), set(deleted)))
         b = _compact(wl.set_batch(up, version=k + 1))
+        # layout.h hand_lead on this batch's byte bound (CacheShard.store's default)
+        assert (log >= 16 * (shard.payload_bound(b.keys.shape[0], b.values.numel()) + rmax)) == lead
         batches.append(b)
         r = sc.serve(wl.digests.index_select(0, ids).contiguous(), b)
         results.append(r)
