@@ -25,7 +25,9 @@ def test_native_driver_under_sanitizer(preset):
     env = dict(os.environ)
     env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0"
     env["TSAN_OPTIONS"] = "halt_on_error=0:second_deadlock_stack=1"
-    exe = os.path.join(ROOT, "build", preset, "shellac_native_tests")
+    # (the presets build under /tmp/shellac-cmake: generated CMake sources stay out of the
+    # source tree)
+    exe = os.path.join("/tmp/shellac-cmake", preset, "shellac_native_tests")
     p = subprocess.run([exe], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     report = p.stdout[-3000:] + p.stderr[-6000:]
     assert "ALL OK" in p.stdout, report
