@@ -51,6 +51,7 @@ PYBIND11_MODULE(_shellac_core, m) {
   m.attr("BUCKET_BYTES") = (int)kBucketBytes;
   m.attr("ITEM_HEADER_BYTES") = (int)kItemHeaderBytes;
   m.attr("SMALL_GET_MAX") = (int64_t)HbmCache::kSmallGetMax;
+  m.attr("LOOKUP_PREFIX_WORDS") = (int64_t)HbmCache::kLookupPrefixWords;
   m.attr("SERVE_KEYS") = (int64_t)HbmCache::kServeKeys;
   m.attr("ITEM_MAGIC") = kItemMagic;
   m.attr("MISS_LOC") = py::int_(kMissLoc);
@@ -103,15 +104,16 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("lookup_coalesced", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t table,
                                   int64_t slots, uintptr_t first, uintptr_t loc, uintptr_t size,
                                   uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve,
-                                  int slot, uintptr_t cslot, bool table_clean) {
+                                  int slot, uintptr_t cslot, bool table_clean, uintptr_t prefix) {
         py::gil_scoped_release nogil;
-        c.lookup_coalesced(P<const Digest>(keys), n, P<uint32_t>(table), slots, P<uint32_t>(first),
-                           P<uint64_t>(loc), P<uint64_t>(size), P<uint64_t>(off), now, S(s),
-                           reserve, slot, P<uint32_t>(cslot), table_clean);
+        return c.lookup_coalesced(P<const Digest>(keys), n, P<uint32_t>(table), slots,
+                                  P<uint32_t>(first), P<uint64_t>(loc), P<uint64_t>(size),
+                                  P<uint64_t>(off), now, S(s), reserve, slot, P<uint32_t>(cslot),
+                                  table_clean, P<uint64_t>(prefix));
       }, py::arg("keys"), py::arg("n"), py::arg("table"), py::arg("slots"), py::arg("first"),
          py::arg("loc"), py::arg("size"), py::arg("off"), py::arg("now"), py::arg("stream"),
          py::arg("reserve") = 0, py::arg("total_slot") = -1, py::arg("cslot") = 0,
-         py::arg("table_clean") = false)
+         py::arg("table_clean") = false, py::arg("prefix") = 0)
       .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
                            uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s,
                            int done_slot) {
@@ -154,15 +156,17 @@ PYBIND11_MODULE(_shellac_core, m) {
       }, py::arg("slot"), py::arg("timeout_ms") = 10000)
       .def("gather", [](HbmCache& c, uintptr_t loc, uintptr_t off, int64_t n, uintptr_t out,
                         uintptr_t s, uint64_t out_cap, uintptr_t first, uintptr_t size,
-                        uintptr_t out_size, uintptr_t out_off, uintptr_t table, uintptr_t cslot) {
+                        uintptr_t out_size, uintptr_t out_off, uintptr_t table, uintptr_t cslot,
+                        uintptr_t prefix, int shift) {
         py::gil_scoped_release nogil;
         c.gather(P<const uint64_t>(loc), P<const uint64_t>(off), n, P<uint8_t>(out), S(s),
                  out_cap, P<const uint32_t>(first), P<const uint64_t>(size), P<uint64_t>(out_size),
-                 P<uint64_t>(out_off), P<uint32_t>(table), P<const uint32_t>(cslot));
+                 P<uint64_t>(out_off), P<uint32_t>(table), P<const uint32_t>(cslot),
+                 P<const uint64_t>(prefix), shift);
       }, py::arg("loc"), py::arg("off"), py::arg("n"), py::arg("out"), py::arg("stream"),
          py::arg("out_cap") = ~0ull, py::arg("first") = 0, py::arg("size") = 0,
          py::arg("out_size") = 0, py::arg("out_off") = 0, py::arg("table") = 0,
-         py::arg("cslot") = 0)
+         py::arg("cslot") = 0, py::arg("prefix") = 0, py::arg("shift") = 0)
       .def("store_graph", [](HbmCache& c, HbmCache::StoreGraph& g, uintptr_t keys,
                              uintptr_t values, uintptr_t val_off, uintptr_t vlen, uintptr_t flags,
                              uintptr_t expire, int64_t n, uint64_t bytes_bound, uint32_t now,

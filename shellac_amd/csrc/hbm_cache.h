@@ -67,10 +67,16 @@ class HbmCache {
   // `cslot` (optional, u32 [n]): each claiming row's table slot, for
   // expand_coalesced_out to clear; `table_clean`: the caller guarantees a zeroed table
   // (skips the memset).
-  void lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
-                        uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
-                        uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
-                        uint32_t* cslot = nullptr, bool table_clean = false);
+  // `prefix` (optional, kMaxGrid + 1 words): block-local offsets — `off` gets each row's
+  // offset within its lookup workgroup's rows and `prefix` the exclusive prefix of the
+  // workgroup totals (one small scan instead of the n-row one); returns the row shift of a
+  // workgroup (its rows are [b << shift, (b + 1) << shift)), for gather(prefix, shift).
+  // Without `prefix`: `off` is the exclusive scan of `size`; returns -1.
+  int lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table, int64_t table_slots,
+                       uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
+                       uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
+                       uint32_t* cslot = nullptr, bool table_clean = false,
+                       uint64_t* prefix = nullptr);
   // Slotted lookup (the routed step's owner side): nslots x slot_rows rows, slot k's
   // rows [k * slot_rows, k * slot_rows + slot_cnt[k]) are requests, the rest padding
   // (size 0, not probed, not counted). off = exclusive scan over all rows.
@@ -88,6 +94,8 @@ class HbmCache {
   static constexpr int kHeadSlot = kHostSlots - 2;  // the SET chain publishes the head here
   static constexpr uint64_t kSlotPending = ~0ull;
   static constexpr uint64_t kSlotFailed = ~0ull - 1;  // the edge GET could not complete
+  // words of a lookup_coalesced `prefix` (the lookup's workgroups, at most 2048, + 1)
+  static constexpr int64_t kLookupPrefixWords = 2049;
   // Edge GET (the proxy's micro-batches, n <= kSmallGetMax): probe + scan + gather in
   // one launch, every key probed once (decoupled look-back scan across workgroups).
   // keys / out / off may be mapped host memory (no copies); off[0..n] is always written;
@@ -155,7 +163,8 @@ class HbmCache {
               uint64_t out_cap = ~0ull, const uint32_t* first = nullptr,
               const uint64_t* size = nullptr, uint64_t* out_size = nullptr,
               uint64_t* out_off = nullptr, uint32_t* table = nullptr,
-              const uint32_t* cslot = nullptr);
+              const uint32_t* cslot = nullptr, const uint64_t* prefix = nullptr,
+              int shift = 0);
   // SET a batch. values + val_off[i] holds vlen[i] bytes (val_off 16-byte aligned,
   // the buffer readable 16 bytes past every value). Later duplicates of a key in
   // the same batch win. `bytes_bound` must bound sum(item_bytes(vlen)).

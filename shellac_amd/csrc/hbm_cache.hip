@@ -39,6 +39,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "hbm_cache.h"
@@ -552,8 +553,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ part, int local_only) {
+    uint64_t* __restrict__ part, int local_only, uint64_t* __restrict__ woff) {
   __shared__ Digest s_k[kCoKeys];       // the chunk's digests (LDS compares, probe input)
+  // woff (PROBE, optional): each row's exclusive offset within this workgroup's rows (the
+  // gather adds the prefix of the workgroup totals, k_block_prefix): the chunk's sizes are
+  // kept in s_tab (free after the local claims) and scanned at the end of the chunk
+  __shared__ unsigned long long s_wt[kBlock / 64], s_run;
+  if (threadIdx.x == 0) s_run = 0;
   __shared__ uint32_t s_tab[kCoSlots];  // local row + 1
   __shared__ uint32_t s_rep[kCoKeys];   // global claimer of each local claimer
   __shared__ uint32_t s_dup[kCoKeys];   // local duplicates of each local claimer
@@ -699,6 +705,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             ++ops;
             out_loc[base + j] = hl ? (hl - 1) % cap : kMissLoc;
             out_size[base + j] = hl ? item_bytes(hv) : 0;
+            if (woff) s_tab[j] = hl ? (uint32_t)item_bytes(hv) : 0u;
             if (hl) {
               ++hits;
               bytes += hv;
@@ -718,10 +725,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (PROBE && f != (uint32_t)(base + j)) {
         out_loc[base + j] = kMissLoc;
         out_size[base + j] = 0;
+        if (woff) s_tab[j] = 0u;
         ++dups;
       }
     }
     __syncthreads();  // LDS is reused by the next chunk
+    if (PROBE && woff) {
+      // the chunk's exclusive offsets from its sizes (kCoPer consecutive rows per thread)
+      const int t4 = threadIdx.x * kCoPer;
+      uint32_t v[kCoPer];
+      unsigned long long ts = 0;
+#pragma unroll
+      for (int u = 0; u < kCoPer; ++u) {
+        v[u] = t4 + u < cnt ? s_tab[t4 + u] : 0u;
+        ts += v[u];
+      }
+      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      unsigned long long inc = ts;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(inc, d);
+        if (lane >= d) inc += o;
+      }
+      if (lane == 63) s_wt[wv] = inc;
+      __syncthreads();
+      unsigned long long ex = s_run + inc - ts, tot = 0;
+#pragma unroll
+      for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wv) ex += s_wt[k];
+        tot += s_wt[k];
+      }
+#pragma unroll
+      for (int u = 0; u < kCoPer; ++u) {
+        if (t4 + u < cnt) woff[base + t4 + u] = ex;
+        ex += v[u];
+      }
+      __syncthreads();  // s_run and s_wt read by every thread
+      if (threadIdx.x == 0) s_run += tot;
+      // (the next chunk's first barrier orders s_run's update before its scan)
+    }
   }
   if (PROBE) {
     if (blockIdx.x == 0 && threadIdx.x == 0) out_size[n] = 0;
@@ -729,6 +771,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 &CacheCounters::get_bytes);
     block_count(ctr, dups, &CacheCounters::get_coalesced);
     block_partial(psum, part);  // k_offsets scans the partials
+  }
+}
+
+// The exclusive prefix of the coalescing lookup's per-workgroup totals (at most kMaxGrid):
+// prefix[b] = bytes of workgroups < b, prefix[nparts] = the total, also published to the
+// pinned host slot (the unsynced gather's size check). One workgroup; with the lookup's
+// block-local offsets it replaces the 1M-row offsets scan (BlockedOff).
+static_assert(HbmCache::kLookupPrefixWords == kMaxGrid + 1, "prefix words: kMaxGrid + 1");
+__global__ __launch_bounds__(kBlock) void k_block_prefix(const uint64_t* __restrict__ part,
+                                                         int nparts,
+                                                         uint64_t* __restrict__ prefix,
+                                                         uint64_t* __restrict__ host_total) {
+  constexpr int kPer = kMaxGrid / kBlock;
+  __shared__ unsigned long long s_w[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t v[kPer];
+  unsigned long long ts = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x * kPer + u;
+    v[u] = i < nparts ? part[i] : 0;
+    ts += v[u];
+  }
+  unsigned long long inc = ts;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  unsigned long long ex = inc - ts;
+  for (int k = 0; k < w; ++k) ex += s_w[k];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x * kPer + u;
+    if (i < nparts) prefix[i] = ex;
+    ex += v[u];
+  }
+  if (threadIdx.x == kBlock - 1) {
+    prefix[nparts] = ex;
+    if (host_total)
+      __hip_atomic_store(host_total, (uint64_t)ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -791,11 +876,30 @@ __device__ __forceinline__ int64_t seg_search_global(const uint64_t* off, int64_
   return lo;
 }
 
+// Segment offsets of a byte mover: a plain array, or (Blocked) the coalescing lookup's
+// block-local offsets plus the exclusive prefix of its per-workgroup totals — off(j) =
+// prefix[j >> shift] + local[j] for j < n, the total for j >= n (no 1M-row scan between
+// the lookup and the gather: k_block_prefix scans only the workgroup totals).
+struct PlainOff {
+  const uint64_t* __restrict__ p;
+  __device__ __forceinline__ uint64_t operator[](int64_t j) const { return p[j]; }
+};
+struct BlockedOff {
+  const uint64_t* __restrict__ local;
+  const uint64_t* __restrict__ prefix;
+  int64_t n;
+  int shift;
+  __device__ __forceinline__ uint64_t operator[](int64_t j) const {
+    return j < n ? prefix[j >> shift] + local[j] : prefix[((n - 1) >> shift) + 1];
+  }
+};
+
 // Cooperative search: each half of the block (128 lanes) finds, for its own x,
 // the last j in [0, n1) with off[j] <= x by 128-ary narrowing (one load per lane
 // per round, ~3 rounds for 10^6 segments) instead of one lane's ~20 dependent
 // loads. Every thread of the block must call it; results land in s_res[0..1].
-__device__ __forceinline__ void block_find2(const uint64_t* __restrict__ off, int64_t n1,
+template <typename Off>
+__device__ __forceinline__ void block_find2(const Off off, int64_t n1,
                                             uint64_t x0, uint64_t x1, int64_t* s_lo,
                                             int64_t* s_hi, int* s_cnt) {
   const int h = threadIdx.x >> 7, t = threadIdx.x & 127, w = threadIdx.x >> 6;
@@ -841,7 +945,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 // Last j in [lo, hi) with off[j] <= x, given off[lo] <= x (off non-decreasing), by the
 // whole block in 256-ary narrowing rounds (one load per thread per round). Every thread of
 // the block must call it; s_b (2 words) and s_cnt (kBlock / 64) are scratch in LDS.
-__device__ __forceinline__ int64_t block_last_le(const uint64_t* __restrict__ off, int64_t lo,
+template <typename Off>
+__device__ __forceinline__ int64_t block_last_le(const Off off, int64_t lo,
                                                  int64_t hi, uint64_t x, int64_t* s_b,
                                                  int* s_cnt) {
   __syncthreads();  // s_b free
@@ -890,13 +995,15 @@ struct ExpandTail {
   uint64_t* out_off = nullptr;
   uint32_t* tab = nullptr;
   const uint32_t* cslot = nullptr;
+  const uint64_t* prefix = nullptr;  // non-null: `off` holds block-local offsets (BlockedOff)
+  int shift = 0;
 };
 __device__ __forceinline__ void expand_tail(const ExpandTail& ex) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < ex.n;
        i += (int64_t)gridDim.x * kBlock) {
     const uint32_t f = ex.first[i];
     ex.out_size[i] = ex.size[f];
-    ex.out_off[i] = ex.off[f];
+    ex.out_off[i] = ex.prefix ? ex.prefix[f >> ex.shift] + ex.off[f] : ex.off[f];
     if (f == (uint32_t)i && ex.tab) ex.tab[ex.cslot[i]] = 0u;
   }
 }
@@ -907,6 +1014,7 @@ __device__ __forceinline__ void expand_tail(const ExpandTail& ex) {
 // the `head_ptr` slot) and is copied only when it ends within `cap`; the bytes between a
 // segment's end and the next segment's start are left untouched (gaps, headers written
 // by someone else), and segments past `cap` are dropped instead of the whole copy.
+// Mode 4: mode 0 with BlockedOff segment offsets (`dst_off` block-local, ex.prefix/shift).
 // Mode 3: mode 0 with the segment count read from the device word `head_ptr` points at
 // (a plan whose segment list the GPU built: no host read of its length).
 // Mode 1 (SET log write): w < 32 synthesises the ItemHeader, else value bytes from
@@ -935,8 +1043,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
   if (MODE == 3) n = *reinterpret_cast<const int64_t*>(head_ptr);  // count on the device
-  const uint64_t total = dst_off[n];
-  if ((MODE == 0 || MODE == 3) && total > cap) break;  // MODE 0/3: destination capacity
+  using Off = typename std::conditional<MODE == 4, BlockedOff, PlainOff>::type;
+  Off doff;
+  if constexpr (MODE == 4)
+    doff = BlockedOff{dst_off, ex.prefix, n, ex.shift};
+  else
+    doff = PlainOff{dst_off};
+  const uint64_t total = doff[n];
+  if ((MODE == 0 || MODE == 3 || MODE == 4) && total > cap) break;  // destination capacity
   const uint64_t* __restrict__ seg_len = MODE == 2 ? head_ptr : nullptr;
   __shared__ uint32_t s_len[MODE == 2 ? TSC : 1];  // records < 4 GiB
   const int64_t nchunks = (int64_t)(total >> 4);
@@ -948,7 +1062,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   const int64_t r0 = (int64_t)blockIdx.x * span;
   const int64_t r1 = min(r0 + span, nchunks);
   if (r0 >= r1) break;
-  block_find2(dst_off, n + 1, (uint64_t)r0 << 4, ((uint64_t)r1 << 4) - 1, s_lo, s_hi, s_cnt);
+  block_find2(doff, n + 1, (uint64_t)r0 << 4, ((uint64_t)r1 << 4) - 1, s_lo, s_hi, s_cnt);
   // (the pass bounds are uniform: scalar registers, and scalar loads below)
   const int64_t ja = uniform64(s_lo[0]), jb = uniform64(s_lo[1]);
   for (int64_t j0 = ja; j0 <= jb; j0 += TSC) {
@@ -959,12 +1073,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
       // not re-appended), and staging them 1024 at a time made the workgroup whose range
       // spans such a run the append's straggler (250 us instead of 45 for a 105 MiB
       // append, alone).
-      const uint64_t o0 = dst_off[j0];
-      if (dst_off[j0 + 1] == o0) j0 = uniform64(block_last_le(dst_off, j0, jb + 1, o0, s_lo, s_cnt));
+      const uint64_t o0 = doff[j0];
+      if (doff[j0 + 1] == o0) j0 = uniform64(block_last_le(doff, j0, jb + 1, o0, s_lo, s_cnt));
     }
     const int cnt = (int)min((int64_t)TSC, jb - j0 + 1);
     __syncthreads();  // previous pass done with s_off / s_src (and s_lo read above)
-    for (int k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = dst_off[j0 + k];
+    for (int k = threadIdx.x; k <= cnt; k += kBlock) s_off[k] = doff[j0 + k];
     for (int k = threadIdx.x; k < cnt; k += kBlock) s_src[k] = src_off[j0 + k];
     if (MODE == 2)
       for (int k = threadIdx.x; k < cnt; k += kBlock) {
@@ -1004,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         if (MODE == 2) {
           if (x < seg_start || w >= s_len[jl]) continue;  // gap / dropped: untouched
           sp[u] = reinterpret_cast<const u32x4*>((uintptr_t)src + seg_src + w);
-        } else if (MODE == 0 || MODE == 3) {
+        } else if (MODE == 0 || MODE == 3 || MODE == 4) {
           // a kSegSkip source leaves the segment's bytes untouched (no load, no store)
           if (seg_src == kSegSkip) continue;
           // integer address math: src may be null with absolute addresses in src_off
@@ -2834,7 +2948,7 @@ void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
                      (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, cslot,
                      nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
-                     0);
+                     0, nullptr);
   HIP_OK(hipGetLastError());
 }
 
@@ -3173,11 +3287,11 @@ void HbmCache::lookup_slots(const Digest* keys, int64_t nslots, int64_t slot_row
   launch_offsets(size, n, part_, grid, off, s, nullptr);
 }
 
-void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
-                                int64_t table_slots, uint32_t* first, uint64_t* loc,
-                                uint64_t* size, uint64_t* off, uint32_t now, hipStream_t s,
-                                uint64_t reserve, int total_slot, uint32_t* cslot,
-                                bool table_clean) {
+int HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
+                               int64_t table_slots, uint32_t* first, uint64_t* loc,
+                               uint64_t* size, uint64_t* off, uint32_t now, hipStream_t s,
+                               uint64_t reserve, int total_slot, uint32_t* cslot,
+                               bool table_clean, uint64_t* prefix) {
   TraceRange tr("hbm.lookup_coalesced");
   SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
@@ -3189,13 +3303,20 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   if (ht) __atomic_store_n(ht, kSlotPending, __ATOMIC_RELEASE);
   if (n <= 0) {
     HIP_OK(hipMemsetAsync(off, 0, sizeof(uint64_t), s));
+    if (prefix) HIP_OK(hipMemsetAsync(prefix, 0, sizeof(uint64_t), s));
     if (ht) *ht = 0;
-    return;
+    return prefix ? 31 : -1;
   }
   if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
   // contiguous whole chunks per workgroup, at most kMaxGrid partial sums
   const int64_t chunks = (n + kCoKeys - 1) / kCoKeys;
-  const int64_t per = (chunks + kMaxGrid - 1) / kMaxGrid;
+  int64_t per = (chunks + kMaxGrid - 1) / kMaxGrid;
+  if (prefix)  // a power of two: the gather finds a row's workgroup by a shift
+    for (int64_t p2 = 1;; p2 <<= 1)
+      if (p2 >= per) {
+        per = p2;
+        break;
+      }
   const int grid = (int)((chunks + per - 1) / per);
   const int64_t plen = per * kCoKeys;
   // (fusing the offsets scan into this kernel — by decoupled look-back, or by one bump
@@ -3204,9 +3325,17 @@ void HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   hipLaunchKernelGGL(k_coalesce<true>, dim3(grid), dim3(kBlock), 0, s, keys, n, plen, table,
                      (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1,
                      cur_head(),
-                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, 0);
+                     reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, 0, prefix ? off : nullptr);
   HIP_OK(hipGetLastError());
-  launch_offsets(size, n, part_, grid, off, s, ht, plen);
+  if (!prefix) {
+    launch_offsets(size, n, part_, grid, off, s, ht, plen);
+    return -1;
+  }
+  hipLaunchKernelGGL(k_block_prefix, dim3(1), dim3(kBlock), 0, s, part_, grid, prefix, ht);
+  HIP_OK(hipGetLastError());
+  int shift = 0;
+  while ((int64_t)1 << shift < plen) ++shift;
+  return shift;
 }
 
 uint64_t HbmCache::host_slot(int i) const {
@@ -3377,14 +3506,21 @@ void HbmCache::serve_stop() {
 void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8_t* out,
                       hipStream_t s, uint64_t out_cap, const uint32_t* first,
                       const uint64_t* size, uint64_t* out_size, uint64_t* out_off,
-                      uint32_t* table, const uint32_t* cslot) {
+                      uint32_t* table, const uint32_t* cslot, const uint64_t* prefix,
+                      int shift) {
   TraceRange tr("hbm.gather");
   DeviceGuard g(cfg_.device);
   if (n <= 0) return;
   ExpandTail ex;
   if (first) ex = ExpandTail{first, n, size, off, out_size, out_off, table, cslot};
-  launch_segcopy_ex<0>(s, ex, log_, loc, off, n, out, nullptr, nullptr, nullptr, nullptr, nullptr,
-                       out_cap);
+  ex.prefix = prefix;
+  ex.shift = shift;
+  if (prefix)  // block-local offsets (lookup_coalesced with a prefix)
+    launch_segcopy_ex<4>(s, ex, log_, loc, off, n, out, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, out_cap);
+  else
+    launch_segcopy_ex<0>(s, ex, log_, loc, off, n, out, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, out_cap);
   HIP_OK(hipGetLastError());
 }
 

@@ -608,8 +608,10 @@ class ShardedCache:
         sh = self.shard
         if self.coalesce:
             table = self._coalesce_table(keys.shape[0]) if side is not None else None
+            # with the table (the step's path, whose gather carries the expand tail): block-
+            # local offsets, no n-row offsets scan between the lookup and the gather
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
-                                                   table=table)
+                                                   table=table, blocked=table is not None)
             return lk, first, cslot, table
         return sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None, None
 

@@ -221,10 +221,23 @@ class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
     size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
     off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
+    # block-local offsets (lookup_coalesced(blocked=True)): `off[i]` is row i's offset within
+    # its lookup workgroup's rows [b << shift, (b + 1) << shift), `prefix[b]` the bytes of
+    # the workgroups before b (prefix[last + 1] = the total); only gather() (with its expand
+    # tail) reads them: the per-request offsets come from the expand tail
+    prefix: Optional[torch.Tensor] = None
+    shift: int = 0
 
     @property
     def n(self) -> int:
         return self.loc.numel()
+
+    def total(self) -> torch.Tensor:
+        """Total response bytes (a one-element device tensor)."""
+        if self.prefix is None:
+            return self.off[self.n:self.n + 1]
+        nb = ((self.n - 1) >> self.shift) + 1 if self.n else 0
+        return self.prefix[nb:nb + 1]
 
     def hits(self) -> torch.Tensor:
         return self.size[: self.n] > 0
@@ -337,15 +350,17 @@ class CacheShard:
 
     def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
                          reserve_bytes: int = 0, total_slot: int = -1,
-                         table: Optional[torch.Tensor] = None):
+                         table: Optional[torch.Tensor] = None, blocked: bool = False):
         """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
         row that claims a digest probes the index for it). Returns (Lookup, first,
         cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
         after the gather. ``table``: a caller-owned, zeroed coalescing table (int32,
         >= ``coalesce_table_slots(n)`` power-of-two slots) — then ``cslot`` holds each
         claimer's slot and ``expand_out`` must run to clean the table again; otherwise
-        a temporary table is zeroed here and ``cslot`` is None. CPU shards: a plain
-        lookup, ``first = cslot = None``."""
+        a temporary table is zeroed here and ``cslot`` is None. ``blocked`` (GPU): the
+        Lookup holds block-local offsets (``Lookup.prefix``), which only ``gather`` with an
+        ``expand`` tail reads — no n-row offsets scan between the lookup and the gather.
+        CPU shards: a plain lookup, ``first = cslot = None``."""
         if not self.is_gpu or keys.shape[0] == 0:
             return self.lookup(keys, now, reserve_bytes, total_slot), None, None
         self._check(keys, "keys")
@@ -365,12 +380,16 @@ class CacheShard:
         size = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         now = self.now() if now is None else now
-        self._impl.lookup_coalesced(keys.data_ptr(), n, table.data_ptr(), slots, first.data_ptr(),
-                                    loc.data_ptr(), size.data_ptr(), off.data_ptr(), now,
-                                    self._s(), int(reserve_bytes), int(total_slot),
-                                    cslot.data_ptr() if cslot is not None else 0,
-                                    cslot is not None)
-        return Lookup(loc, size, off), first, cslot
+        prefix = (torch.empty(int(c.LOOKUP_PREFIX_WORDS), dtype=torch.int64, device=self.device)
+                  if blocked else None)
+        shift = self._impl.lookup_coalesced(keys.data_ptr(), n, table.data_ptr(), slots,
+                                            first.data_ptr(), loc.data_ptr(), size.data_ptr(),
+                                            off.data_ptr(), now, self._s(), int(reserve_bytes),
+                                            int(total_slot),
+                                            cslot.data_ptr() if cslot is not None else 0,
+                                            cslot is not None,
+                                            prefix.data_ptr() if prefix is not None else 0)
+        return Lookup(loc, size, off, prefix, max(int(shift), 0)), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
         """Total bytes of the last lookup given ``total_slot=slot``: spins on the pinned
@@ -423,7 +442,7 @@ class CacheShard:
         (first, out_size, out_off, table, cslot) — the gather also writes every request's
         (size, off) from its claimer and clears the coalescing table (``expand_out``)."""
         if out is None:
-            total = int(lk.off[lk.n].item()) if total is None else total
+            total = int(lk.total().item()) if total is None else total
             out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
         self._check(out, "out")
         if self.is_gpu:
@@ -434,8 +453,11 @@ class CacheShard:
                 ex = [first.data_ptr(), lk.size.data_ptr(), osz.data_ptr(), ooff.data_ptr(),
                       table.data_ptr() if table is not None else 0,
                       cslot.data_ptr() if cslot is not None else 0]
+            elif lk.prefix is not None:
+                raise ValueError("a blocked lookup's offsets are read only with an expand tail")
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
-                              self._s(), cap, *ex)
+                              self._s(), cap, *ex,
+                              lk.prefix.data_ptr() if lk.prefix is not None else 0, lk.shift)
         else:
             self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr())
         return out
