@@ -12,8 +12,9 @@ namespace {
 constexpr uint64_t kWeyl = 0x9E3779B97F4A7C15ull;  // 2^64 / golden ratio
 }  // namespace
 
-HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, 0) {
-  SH_CHECK(nshards >= 1 && nshards <= 32767 && pps >= 1, "bad router geometry");
+HostRouter::HostRouter(int nshards, int pps)
+    : n_(nshards), span_(65536, 0), hot_tab_(1), hot_bits_(1, 0) {
+  SH_CHECK(nshards >= 1 && nshards <= 1023 && pps >= 1, "bad router geometry");
   std::vector<std::pair<uint32_t, int>> pts;
   for (int i = 0; i < nshards; ++i)
     for (int j = 0; j < pps; ++j) {  // DigestRing's (and ShardRing's) points
@@ -29,15 +30,32 @@ HostRouter::HostRouter(int nshards, int pps) : n_(nshards), tab_(65536, 0) {
     pts_.push_back(p.first);
     own_.push_back(p.second);
   }
-  // span s = [a, a + 65535]: one owner for all of it iff no point lies in [a, a + 65534];
-  // otherwise the index of its first point (the owner of any p in it is at or after it)
+  // span s = [a, a + 65535]: its points q1 < q2 (if any); owner(p), t = p - a:
+  // t <= q1 - a -> own(q1), t <= q2 - a -> own(q2), else the owner after the last of them
+  auto after = [&](uint64_t q) { return q >= 0xFFFFFFFFull ? own_[0] : search((uint32_t)q + 1); };
   for (uint32_t s = 0; s < 65536; ++s) {
-    const uint32_t a = s << 16, b = a + 65535u;
-    const auto it = std::lower_bound(pts_.begin(), pts_.end(), a);
-    if (it == pts_.end() || *it >= b)
-      tab_[s] = search(b);
-    else
-      tab_[s] = -(int32_t)(it - pts_.begin()) - 1;
+    const uint32_t a = s << 16;
+    const uint64_t b = (uint64_t)a + 65535u;
+    const size_t i0 = (size_t)(std::lower_bound(pts_.begin(), pts_.end(), a) - pts_.begin());
+    size_t i1 = i0;
+    while (i1 < pts_.size() && pts_[i1] <= b) ++i1;
+    const size_t k = i1 - i0;
+    uint64_t c1, c2, o1, o2, o3;
+    if (k == 0) {
+      c1 = c2 = 0xFFFF;
+      o1 = o2 = o3 = (uint64_t)after(b);
+    } else if (k == 1) {
+      c1 = c2 = pts_[i0] - a;
+      o1 = (uint64_t)own_[i0];
+      o2 = o3 = (uint64_t)after(pts_[i0]);
+    } else {
+      c1 = pts_[i0] - a;
+      c2 = pts_[i0 + 1] - a;
+      o1 = (uint64_t)own_[i0];
+      o2 = (uint64_t)own_[i0 + 1];
+      o3 = (uint64_t)after(pts_[i0 + 1]);
+    }
+    span_[s] = c1 | c2 << 16 | o1 << 32 | o2 << 42 | o3 << 52 | (k > 2 ? 1ull << 63 : 0ull);
   }
   cw_.assign((size_t)n_, 0.0);
   for (int r = 0; r < n_; ++r) cw_[(size_t)r] = (double)(r + 1) / n_;
@@ -60,37 +78,40 @@ int HostRouter::search(uint32_t p) const {
 
 void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, const double* w) {
   nhot_ = 0;
-  hot_tab_.clear();
-  hot_bits_.clear();
-  hot_mask_ = bits_mask_ = 0;
-  if (n <= 0) return;
-  uint64_t slots = 1024;
-  while (slots < 2 * (uint64_t)n) slots <<= 1;
-  hot_tab_.assign(slots, HotSlot{});
-  hot_mask_ = slots - 1;
-  uint64_t bits = 1 << 12;
-  while (bits < 16 * (uint64_t)n) bits <<= 1;
-  hot_bits_.assign(bits / 64, 0);
-  bits_mask_ = bits - 1;
-  for (int64_t i = 0; i < n; ++i) {
-    const Digest d = hot[i];
-    if (!d.lo && !d.hi) continue;
-    const uint64_t fb = (d.lo >> 20) & bits_mask_;
-    hot_bits_[fb >> 6] |= 1ull << (fb & 63);
-    const int32_t r = rank ? rank[i] : kSpray;
-    SH_CHECK(r >= kSpray && r < n_, "designated rank out of range");
-    for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
-      HotSlot& e = hot_tab_[s];
-      if (e.lo == d.lo && e.hi == d.hi) {
-        e.rank = r;
-        break;
-      }
-      if (!e.lo && !e.hi) {
-        e.lo = d.lo;
-        e.hi = d.hi;
-        e.rank = r;
-        ++nhot_;
-        break;
+  hot_tab_.assign(1, HotSlot{});
+  hot_mask_ = 0;
+  hot_bits_.assign(1, 0);
+  bits_mask_ = 0;
+  if (n > 0) {
+    uint64_t slots = 1024;
+    while (slots < 2 * (uint64_t)n) slots <<= 1;
+    hot_tab_.assign(slots, HotSlot{});
+    hot_mask_ = slots - 1;
+    uint64_t bits = 1 << 12;
+    while (bits < 16 * (uint64_t)n) bits <<= 1;
+    hot_bits_.assign(bits / 64, 0);
+    bits_mask_ = bits - 1;
+    // in the given order (hottest first, HotSpread.plan): the hottest keep their home slot
+    for (int64_t i = 0; i < n; ++i) {
+      const Digest d = hot[i];
+      if (!d.lo && !d.hi) continue;
+      const int32_t r = rank ? rank[i] : kSpray;
+      SH_CHECK(r >= kSpray && r < n_, "designated rank out of range");
+      const uint64_t fb = (d.lo >> 20) & bits_mask_;
+      hot_bits_[fb >> 6] |= 1ull << (fb & 63);
+      const uint64_t tag = (d.hi & ~0xFFFFull) | (uint64_t)(r + 2);
+      for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
+        HotSlot& e = hot_tab_[s];
+        if (e.lo == d.lo && ((e.tag ^ d.hi) >> 16) == 0 && (e.tag & 0xFFFF)) {
+          e.tag = tag;  // a repeated digest: the last rank
+          break;
+        }
+        if (!(e.tag & 0xFFFF)) {
+          e.lo = d.lo;
+          e.tag = tag;
+          ++nhot_;
+          break;
+        }
       }
     }
   }
@@ -106,6 +127,14 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
     cw_[(size_t)r] = acc / tot;
   }
   cw_.back() = 1.0;
+}
+
+uint32_t HostRouter::hot_code_slow(const Digest& d) const {
+  for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
+    const HotSlot& e = hot_tab_[s];
+    if (hot_match(e, d)) return (uint32_t)(e.tag & 0xFFFFu);
+    if (!(e.tag & 0xFFFFu)) return 0;
+  }
 }
 
 int HostRouter::spray(uint64_t j) const {
@@ -126,30 +155,15 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     }
     return;
   }
-  // locals: the stores through dest / counts cannot make the compiler reload them
-  const uint64_t* const bits = hot_bits_.data();
-  const uint64_t bmask = bits_mask_, hmask = hot_mask_;
-  const HotSlot* const tab = hot_tab_.data();
   for (int64_t i = a; i < b; ++i) {
     const Digest d = keys[i];
-    const uint64_t fb = (d.lo >> 20) & bmask;
-    int hr = kNotHot;
-    if ((bits[fb >> 6] >> (fb & 63)) & 1) {
-      for (uint64_t s = d.lo & hmask;; s = (s + 1) & hmask) {
-        const HotSlot& e = tab[s];
-        if (e.lo == d.lo && e.hi == d.hi) {
-          hr = e.rank;
-          break;
-        }
-        if (!e.lo && !e.hi) break;
-      }
-    }
-    if (hr != kNotHot) {
+    const uint32_t c = hot_code(d);
+    if (c) {
       if (kSets) {
         dest[i] = -1;
         for (int r = 0; r < n_; ++r) ++counts[r];
       } else {
-        const int r = hr >= 0 ? hr : spray(seq0 + (uint64_t)i);
+        const int r = c >= 2 ? (int)c - 2 : spray(seq0 + (uint64_t)i);
         dest[i] = r;
         ++counts[r];
       }

@@ -12,9 +12,9 @@
 // Decisions are a pure function of (digest, position in the stream), identical to the
 // tensor version in shellac_amd/parallel/hotspread.py (tests check both agree):
 //   owner(d)   first ring point >= ring_position(d) (wrapping), DigestRing's rule. A
-//              65536-entry table answers a 2^16-wide span no point splits directly and
-//              names the first point of a split span otherwise, from which a short scan
-//              (~1 point) finds the owner: no binary search on the request path.
+//              65536-entry span table answers it with one 8-byte load and two compares: each
+//              2^16-wide span stores the (at most two) points inside it and the owners on
+//              either side of them; the rare span with more points falls back to a search.
 //   GET i      a hot object's GETs go to its designated rank (chosen at the hot set's
 //              refresh to even out the load; every rank holds a replica), or, for the few
 //              objects too hot for one rank, to spray(seq0 + i): rank r with probability w_r
@@ -23,8 +23,15 @@
 //   SET        hot(d) ? every rank (dest -1) : owner(d).
 //
 // Throughput: a batch is split over a persistent worker pool (threads created once, not
-// per call); a request costs a table load (cold) or a filter word and a hot-table slot
-// (hot). Software prefetching of the slots measured no faster (they are cache-resident).
+// per call). A cold request costs one 8-B span-table load and a filter word; a hot one the
+// filter word and (for the hottest objects, inserted first) its home slot. Measured on the
+// host (scripts/router_micro.py): the span table took cold routing from ~150 to ~210 M
+// requests/s per thread; a branch-free variant (owner and hot table both looked up, the
+// result selected by masks) removed the hot/cold mispredictions but its extra loads made
+// the Zipf mix slower (34-40 against 45-50 M/s), so the hot path keeps its branch.
+// The hot table matches a digest on its low word and the top 48 bits of its high word (the
+// low 16 bits hold the rank): a cold digest agreeing on those 112 bits would be treated as
+// hot — consistently for its GETs and SETs, so it would still be served correctly.
 #pragma once
 
 #include <condition_variable>
@@ -47,12 +54,12 @@ class HostRouter {
   int nshards() const { return n_; }
   int owner(const Digest& d) const {
     const uint32_t p = ring_position(d);
-    const int32_t t = tab_[p >> 16];
-    if (t >= 0) return t;
-    size_t i = (size_t)(-(int64_t)t - 1);  // the span's first point; the owner is at or after it
-    const size_t np = pts_.size();
-    while (i < np && pts_[i] < p) ++i;
-    return own_[i == np ? 0 : i];
+    const uint64_t e = span_[p >> 16];
+    if (e >> 63) return search(p);  // a span with more than two points
+    const uint32_t t = p & 0xFFFFu, c1 = e & 0xFFFFu, c2 = (e >> 16) & 0xFFFFu;
+    const int o1 = (int)((e >> 32) & 1023), o2 = (int)((e >> 42) & 1023),
+              o3 = (int)((e >> 52) & 1023);
+    return t <= c1 ? o1 : (t <= c2 ? o2 : o3);
   }
   // The replicated hot set (n digests, any order), each object's designated GET rank
   // (`rank`: n values, -1 = sprayed; null = all sprayed) and the spray weights (`w`:
@@ -62,14 +69,8 @@ class HostRouter {
   // kNotHot, kSpray, or the object's designated rank
   static constexpr int kNotHot = -2, kSpray = -1;
   int hot_rank(const Digest& d) const {
-    if (!nhot_) return kNotHot;
-    const uint64_t b = (d.lo >> 20) & bits_mask_;
-    if (!((hot_bits_[b >> 6] >> (b & 63)) & 1)) return kNotHot;
-    for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
-      const HotSlot& e = hot_tab_[s];
-      if (e.lo == d.lo && e.hi == d.hi) return e.rank;
-      if (!e.lo && !e.hi) return kNotHot;
-    }
+    const uint32_t c = hot_code(d);
+    return c == 0 ? kNotHot : (int)c - 2;
   }
   bool is_hot(const Digest& d) const { return hot_rank(d) != kNotHot; }
   // dest[i] for a GET stream whose first request has stream position seq0; counts[r] +=
@@ -83,11 +84,27 @@ class HostRouter {
   const std::vector<double>& cumulative() const { return cw_; }
 
  private:
-  // one slot of the hot table: the digest and its designated rank in one 32-B line half
-  struct alignas(32) HotSlot {
-    uint64_t lo = 0, hi = 0;
-    int32_t rank = kSpray;
+  // hot table: open addressing on lo (linear probing, at most half full), slots
+  // {lo, (hi & ~0xFFFF) | code}, code = designated rank + 2 (1: sprayed, 0: empty). The hot
+  // set is inserted hottest first, so the objects that carry most requests sit in their
+  // home slot; a one-hash filter (16 bits per object) answers most cold digests.
+  struct HotSlot {
+    uint64_t lo = 0, tag = 0;
   };
+  bool hot_match(const HotSlot& e, const Digest& d) const {
+    return (e.lo == d.lo) & (((e.tag ^ d.hi) >> 16) == 0) & ((e.tag & 0xFFFFu) != 0);
+  }
+  // 0: not hot; 1: sprayed; r + 2: designated rank r. The common cases (a cold digest the
+  // filter rejects, a hot one in its home slot) take no data-dependent branch: a rejected
+  // digest reads slot 0 instead of its home slot (a cached line), and the code is masked.
+  uint32_t hot_code(const Digest& d) const {
+    const uint64_t fb = (d.lo >> 20) & bits_mask_;
+    if (!((hot_bits_[fb >> 6] >> (fb & 63)) & 1)) return 0;
+    const HotSlot& e = hot_tab_[d.lo & hot_mask_];
+    if (hot_match(e, d)) return (uint32_t)(e.tag & 0xFFFFu);
+    return hot_code_slow(d);  // probe further
+  }
+  uint32_t hot_code_slow(const Digest& d) const;
   int search(uint32_t p) const;
   int spray(uint64_t j) const;
   template <bool kSets>
@@ -100,11 +117,11 @@ class HostRouter {
   int n_;
   std::vector<uint32_t> pts_;
   std::vector<int32_t> own_;
-  std::vector<int32_t> tab_;      // 65536: owner of a span no point splits, else -(first point + 1)
-  std::vector<HotSlot> hot_tab_;  // open addressing on lo (a hash already), {0, 0} = empty
+  // per 2^16-wide span: c1 | c2 << 16 | o1 << 32 | o2 << 42 | o3 << 52, bit 63 = more than
+  // two points (owner() searches)
+  std::vector<uint64_t> span_;
+  std::vector<HotSlot> hot_tab_;  // one empty slot when there is no hot set
   uint64_t hot_mask_ = 0;
-  // a one-hash filter in front of it, 16 bits per hot object (~6 % of cold digests pass):
-  // a cold request then costs no table line
   std::vector<uint64_t> hot_bits_;
   uint64_t bits_mask_ = 0;
   int64_t nhot_ = 0;
