@@ -100,7 +100,8 @@ def parse():
                     help="host-routed N>1: hot objects replicated on every GPU (the top of an "
                          "observed GET sample), their GETs sprayed over the GPUs to even out "
                          "the load and their SETs written through to every GPU (0 = off; "
-                         "default 65536)")
+                         "default 1024: the request shares are within 0.3 %% of the mean "
+                         "with 1024 at N = 2-8, as with 65536, and the router stays faster)")
     ap.add_argument("--spread-sample", type=int, default=1 << 22,
                     help="GET requests of the observed sample that picks the hot set")
     ap.add_argument("--spread-policy", choices=["designate", "spray"], default="designate",
@@ -403,7 +404,7 @@ def main():
         # the rank's cache never routes (group=None would mean the world group here)
         group = LocalComm()
         if args.spread is None:
-            args.spread = 1 << 16
+            args.spread = 1 << 10
     else:
         args.spread = 0
     if routed1:

@@ -1,13 +1,13 @@
 #!/bin/bash
 # The most loaded rank of the host-routed N-rank job, simulated on one GPU (its true share of
 # the global Zipf stream on its 1/N of the key space), with hot-object spreading off and on:
-# `bash scripts/host_route_sim.sh OUT "2 4 8" ["0 65536"]`. The driver's defaults otherwise
+# `bash scripts/host_route_sim.sh OUT "2 4 8" ["0 1024"]`. The driver's defaults otherwise
 # (the pressured headline); --check on each. SIM_ARGS: extra bench flags.
 set -o pipefail
 OUT=gpurun_out/${1:-host_route_sim}
 mkdir -p "$OUT"
 for n in ${2:-"2 4 8"}; do
-  for k in ${3:-"0 65536"}; do
+  for k in ${3:-"0 1024"}; do
     tag=sim${n}_spread${k}
     timeout -k 10 400 python -u bench.py --no-uncoalesced --no-smoke --check --simulate-world "$n" \
       --route host --spread "$k" $SIM_ARGS > "$OUT/$tag.json" 2> "$OUT/$tag.err" \

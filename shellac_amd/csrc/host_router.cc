@@ -155,22 +155,46 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     }
     return;
   }
+  // locals: the stores through dest / counts cannot make the compiler reload any of these
+  const uint64_t* const span = span_.data();
+  const uint64_t* const bits = hot_bits_.data();
+  const HotSlot* const tab = hot_tab_.data();
+  const uint64_t bmask = bits_mask_, hmask = hot_mask_;
   for (int64_t i = a; i < b; ++i) {
     const Digest d = keys[i];
-    const uint32_t c = hot_code(d);
-    if (c) {
-      if (kSets) {
+    // owner (owner()'s span rule)
+    const uint32_t p = ring_position(d);
+    const uint64_t se = span[p >> 16];
+    int o;
+    if (__builtin_expect(se >> 63, 0)) {
+      o = search(p);
+    } else {
+      const uint32_t t = p & 0xFFFFu;
+      o = t <= (se & 0xFFFFu) ? (int)((se >> 32) & 1023)
+                              : (t <= ((se >> 16) & 0xFFFFu) ? (int)((se >> 42) & 1023)
+                                                             : (int)((se >> 52) & 1023));
+    }
+    // hot code (hot_code()'s rule)
+    const uint64_t fb = (d.lo >> 20) & bmask;
+    const uint64_t pass = (bits[fb >> 6] >> (fb & 63)) & 1;
+    const HotSlot& e = tab[d.lo & hmask];
+    const uint64_t hit = pass & (uint64_t)hot_match(e, d);
+    const uint32_t c = __builtin_expect(pass & (hit ^ 1), 0)
+                           ? hot_code_slow(d)
+                           : (uint32_t)(e.tag & 0xFFFFu & ((uint64_t)0 - hit));
+    if (kSets) {
+      if (c) {  // (SETs: a hot object's share of a SET stream is small and predictable)
         dest[i] = -1;
         for (int r = 0; r < n_; ++r) ++counts[r];
       } else {
-        const int r = c >= 2 ? (int)c - 2 : spray(seq0 + (uint64_t)i);
-        dest[i] = r;
-        ++counts[r];
+        dest[i] = o;
+        ++counts[o];
       }
     } else {
-      const int o = owner(d);
-      dest[i] = o;
-      ++counts[o];
+      int r = c >= 2 ? (int)c - 2 : o;             // a select, not a branch
+      if (c == 1) r = spray(seq0 + (uint64_t)i);  // the few sprayed objects
+      dest[i] = r;
+      ++counts[r];
     }
   }
 }

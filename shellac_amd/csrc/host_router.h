@@ -23,12 +23,15 @@
 //   SET        hot(d) ? every rank (dest -1) : owner(d).
 //
 // Throughput: a batch is split over a persistent worker pool (threads created once, not
-// per call). A cold request costs one 8-B span-table load and a filter word; a hot one the
-// filter word and (for the hottest objects, inserted first) its home slot. Measured on the
-// host (scripts/router_micro.py): the span table took cold routing from ~150 to ~210 M
-// requests/s per thread; a branch-free variant (owner and hot table both looked up, the
-// result selected by masks) removed the hot/cold mispredictions but its extra loads made
-// the Zipf mix slower (34-40 against 45-50 M/s), so the hot path keeps its branch.
+// per call), and a request is routed without a data-dependent branch in the common cases:
+// its owner (one 8-B span-table load) and its hot-table home slot are both read and the
+// result selected by masks; only a digest that passes the filter but is not in its home
+// slot (a filter false positive, or a hot object displaced by a hotter one: the set is
+// inserted hottest first) and the few sprayed objects branch. Branching on hot vs cold
+// mispredicted on a large share of a Zipf stream's requests (a host micro-benchmark,
+// scripts/router_micro.py: 65 against 173 M requests/s per thread with 256 hot objects).
+// The home-slot read is cheap while the hot set is small (the bench's default 1024
+// objects: a 32 KiB table); with 64K objects it misses the caches for cold requests.
 // The hot table matches a digest on its low word and the top 48 bits of its high word (the
 // low 16 bits hold the rank): a cold digest agreeing on those 112 bits would be treated as
 // hot — consistently for its GETs and SETs, so it would still be served correctly.
@@ -99,10 +102,11 @@ class HostRouter {
   // digest reads slot 0 instead of its home slot (a cached line), and the code is masked.
   uint32_t hot_code(const Digest& d) const {
     const uint64_t fb = (d.lo >> 20) & bits_mask_;
-    if (!((hot_bits_[fb >> 6] >> (fb & 63)) & 1)) return 0;
-    const HotSlot& e = hot_tab_[d.lo & hot_mask_];
-    if (hot_match(e, d)) return (uint32_t)(e.tag & 0xFFFFu);
-    return hot_code_slow(d);  // probe further
+    const uint64_t pass = (hot_bits_[fb >> 6] >> (fb & 63)) & 1;
+    const HotSlot& e = hot_tab_[d.lo & hot_mask_];  // the home slot, read either way
+    const uint64_t hit = pass & (uint64_t)hot_match(e, d);
+    if (__builtin_expect(pass & (hit ^ 1), 0)) return hot_code_slow(d);  // probe further
+    return (uint32_t)(e.tag & 0xFFFFu & ((uint64_t)0 - hit));
   }
   uint32_t hot_code_slow(const Digest& d) const;
   int search(uint32_t p) const;
