@@ -169,10 +169,14 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     if (__builtin_expect(se >> 63, 0)) {
       o = search(p);
     } else {
+      // t <= c1 ? o1 : t <= c2 ? o2 : o3, by masks (g++ turned the ternaries into branches
+      // that mispredict on a random stream)
       const uint32_t t = p & 0xFFFFu;
-      o = t <= (se & 0xFFFFu) ? (int)((se >> 32) & 1023)
-                              : (t <= ((se >> 16) & 0xFFFFu) ? (int)((se >> 42) & 1023)
-                                                             : (int)((se >> 52) & 1023));
+      const uint32_t s1 = 0u - (uint32_t)(t <= (se & 0xFFFFu));
+      const uint32_t s2 = 0u - (uint32_t)(t <= ((se >> 16) & 0xFFFFu));
+      const uint32_t o1 = (se >> 32) & 1023, o2 = (se >> 42) & 1023, o3 = (se >> 52) & 1023;
+      const uint32_t x = o3 ^ ((o2 ^ o3) & s2);
+      o = (int)(x ^ ((o1 ^ x) & s1));
     }
     // hot code (hot_code()'s rule)
     const uint64_t fb = (d.lo >> 20) & bmask;
@@ -191,7 +195,8 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
         ++counts[o];
       }
     } else {
-      int r = c >= 2 ? (int)c - 2 : o;             // a select, not a branch
+      const uint32_t sel = 0u - (uint32_t)(c >= 2);  // a select by mask, not a branch
+      int r = (int)((uint32_t)o ^ (((c - 2) ^ (uint32_t)o) & sel));
       if (c == 1) r = spray(seq0 + (uint64_t)i);  // the few sprayed objects
       dest[i] = r;
       ++counts[r];
