@@ -148,6 +148,9 @@ def parse():
                          "record each) fills --pressured-fill of it (0 = skip)")
     ap.add_argument("--pressured-fill", type=float, default=0.8,
                     help="working set over log capacity of the default pressured shard")
+    ap.add_argument("--overfull-fill", type=float, default=1.25,
+                    help="secondary block log_overfull: a shard log the working set fills "
+                         "this many times over (0 = skip; only with the default pressured log)")
     ap.add_argument("--headline", choices=["pressured", "wrapped", "fresh"], default="pressured",
                     help="which cache state the headline K steps run in: a full cache whose "
                          "working set fills --pressured-fill of the log (default: eviction with "
@@ -630,9 +633,13 @@ def main():
     if ready is not None:
         ready.record()
 
+    set_cycle = [sets]   # the SET batches the steps cycle (a phase may swap in its own)
+
     def serve_i(cache, i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
-        return cache.serve(gets[i % P], sets[i % P], inputs_ready=ready, probe_keys=gprobe[i % P])
+        sl = set_cycle[0]
+        return cache.serve(gets[i % P], sl[i % len(sl)], inputs_ready=ready,
+                           probe_keys=gprobe[i % P])
 
     def step(i):
         return serve_i(sc, i)
@@ -934,44 +941,81 @@ def main():
     # the full cache (the headline): a shard whose working set fills --pressured-fill of its
     # log, wrapped, so the CLOCK hand re-appends the objects the steps read (reinsertions)
     # and evicts the rest: the state a serving cache runs in (memcached evicts under load)
-    pressured = pw = piv = pfill = None
-    if do_pressured:
-        p_log = int(p_gb * (1 << 30)) // 16 * 16
-        p_shard = CacheShard(p_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
-        p_sc = ShardedCache(p_shard, group=group, replica=replica,
+    def full_cache(gb, check_it, min_fill=0, set_list=None):
+        """A shard of `gb` GiB populated with this rank's keys, wrapped (fill steps, at least
+        `min_fill`), then the headline protocol (K timed steps), a GPU-event pass and one
+        whole lap timed: (summary, window, event intervals, fill steps). `set_list`: the
+        SET batches the steps cycle instead of the default ones."""
+        if set_list is not None:
+            set_cycle[0] = set_list
+        f_log = int(gb * (1 << 30)) // 16 * 16
+        f_shard = CacheShard(f_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
+        f_sc = ShardedCache(f_shard, group=group, replica=replica,
                             data_group=data_group, routed=True if routed1 else None,
                             comm_mode=args.comm_mode, hand=args.hand)
-        p_sc.coalesce = sc.coalesce
-        p_sc.event_fence = sc.event_fence
-        p_sc.gather_after_append = sc.gather_after_append
+        f_sc.coalesce = sc.coalesce
+        f_sc.event_fence = sc.event_fence
+        f_sc.gather_after_append = sc.gather_after_append
         if replica is not None:
-            p_sc._hot, p_sc._hot_dir = sc._hot, None
-        populate(p_sc)
-        p_shard.reserve(max(args.sets * 2, chunk))
+            f_sc._hot, f_sc._hot_dir = sc._hot, None
+        populate(f_sc)
+        f_shard.reserve(max(args.sets * 2, chunk))
         sync()
         if real_world > 1:
             dist.barrier()
-        pbase = 3 * args.warmup + 2 * args.steps
-        pfill = fill_to_wrap(p_sc, p_shard, p_log, pbase, per_step)
-        if pfill is not None:
-            pw = window(p_sc, p_shard, pbase + pfill)
-            if args.check and headline == "pressured":
-                check(pw)
-            piv = timed(args.steps, pbase + pfill + args.steps, events=True,
-                        cache=p_sc)[1] if use_events else []
-            pressured = summary(pw, piv, p_log, pfill)
+        fbase = 3 * args.warmup + 2 * args.steps
+        ffill = fill_to_wrap(f_sc, f_shard, f_log, fbase, per_step)
+        if ffill is not None and ffill < min_fill:
+            for i in range(ffill, min_fill):
+                serve_i(f_sc, fbase + i)
+            sync()
+            ffill = min_fill
+        out_ = fw = fiv = None
+        if ffill is not None:
+            fw = window(f_sc, f_shard, fbase + ffill)
+            if check_it:
+                check(fw)
+            fiv = timed(args.steps, fbase + ffill + args.steps, events=True,
+                        cache=f_sc)[1] if use_events else []
+            out_ = summary(fw, fiv, f_log, ffill)
             # the cost of a step varies with where the hand is in the lap (the objects it
             # re-appended one lap earlier come round together): one whole lap, timed
-            lap_steps = int(p_log / max(1.0, (pw["head1"] - pw["head0"]) / args.steps)) + 1
+            lap_steps = int(f_log / max(1.0, (fw["head1"] - fw["head0"]) / args.steps)) + 1
             if real_world > 1:  # one step count on every rank (the longest lap)
                 lt = torch.tensor([lap_steps], dtype=torch.int64, device=rdev)
                 dist.all_reduce(lt, op=dist.ReduceOp.MAX)
                 lap_steps = int(lt)
-            lap_el = timed(lap_steps, pbase + pfill + 2 * args.steps, cache=p_sc)[0]
-            pressured["lap_steps"] = lap_steps
-            pressured["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
-        p_sc.sync_sets()
-        del p_sc, p_shard
+            lap_el = timed(lap_steps, fbase + ffill + 2 * args.steps, cache=f_sc)[0]
+            out_["lap_steps"] = lap_steps
+            out_["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
+        f_sc.sync_sets()
+        set_cycle[0] = sets
+        del f_sc, f_shard
+        return out_, fw, fiv, ffill
+
+    pressured = pw = piv = pfill = None
+    if do_pressured:
+        pressured, pw, piv, pfill = full_cache(p_gb, args.check and headline == "pressured")
+    # secondary: a working set larger than the log (--overfull-fill x the log): the hit ratio
+    # when the cache cannot hold every key
+    overfull = None
+    if do_pressured and args.overfull_fill > 0 and args.pressured_gb is None:
+        # An evicted key comes back only when it is SET again: the default steps cycle 16
+        # SET batches (1M of the 4M keys), so here the SETs walk a permutation of every key
+        # this rank holds (each re-SET once per keys/sets steps, like a cache-aside refill
+        # of the whole key space). The populate itself wraps this log, evicting unread
+        # objects in key order: two passes of the permutation run before the window, so it
+        # sees the steady state, not the populate's transient.
+        own = (torch.arange(lo, hi, device=dev) if fill_ids is None else fill_ids)
+        g = torch.Generator(device="cpu").manual_seed(777 + rank)
+        own = own.index_select(0, torch.randperm(int(own.numel()), generator=g).to(own.device))
+        ov_sets = [wl.set_batch(own[s0: s0 + args.sets].contiguous())
+                   for s0 in range(0, int(own.numel()) - args.sets + 1, args.sets)]
+        overfull = full_cache(ws_bytes / args.overfull_fill / (1 << 30), False,
+                              min_fill=2 * len(ov_sets), set_list=ov_sets)[0]
+        if overfull is not None:
+            overfull["set_batches_cycled"] = len(ov_sets)
+        del own, ov_sets
     if headline == "pressured" and pw is None:
         raise SystemExit("[bench] the pressured log could not be wrapped for the headline; "
                          "pass --headline wrapped")
@@ -1083,6 +1127,8 @@ def main():
         "log_wrapped": summary(wrapped, wrapped_iv, fill=nfill) if wrapped else None,
         # the full cache (the default headline): reinsertions and evictions every step
         "log_pressured": pressured,
+        # the working set --overfull-fill x the log (more keys than the cache holds)
+        "log_overfull": overfull,
         # a drifting hot set with the replica maintained between epochs (N>1 / simulated)
         "hot_drift": drift,
         "smoke": sm,
