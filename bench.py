@@ -500,7 +500,7 @@ def main():
                 hd, _hc = spread.host_route_gets(kh, seq0=0, threads=t_, out=hbuf)
                 best = min(best, _t.perf_counter() - t0_)
             rates[t_] = kh.shape[0] / best
-        route_info.update(host_route_threads=th,
+        route_info.update(host_route_threads=th, host_route_avx512_lanes=bool(spread.router.lanes),
                           host_route_req_per_s=round(rates[th], 1),
                           host_route_req_per_s_one_thread=round(rates[1], 1),
                           host_route_agrees_with_device=bool(torch.equal(hd, gd0.cpu())))

@@ -108,6 +108,7 @@ void bind_router(py::module_& m) {
       .def_property_readonly("nshards", &HostRouter::nshards)
       .def_property_readonly("nhot", &HostRouter::nhot)
       .def_property_readonly("cumulative", &HostRouter::cumulative)
+      .def_property("lanes", &HostRouter::lanes, &HostRouter::set_lanes)
       .def("owner", [](const HostRouter& r, uint64_t lo, uint64_t hi) {
         return r.owner(Digest{lo, hi});
       })

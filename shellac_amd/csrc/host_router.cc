@@ -2,7 +2,10 @@
 // multi-GPU topology.
 #include "host_router.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <thread>
 
@@ -10,10 +13,11 @@ namespace shellac {
 
 namespace {
 constexpr uint64_t kWeyl = 0x9E3779B97F4A7C15ull;  // 2^64 / golden ratio
+const bool kHaveAvx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq");
 }  // namespace
 
 HostRouter::HostRouter(int nshards, int pps)
-    : n_(nshards), span_(65536, 0), hot_tab_(1), hot_bits_(1, 0) {
+    : n_(nshards), span_(65536, 0), hot_tab_(1), hot_bits_(1, 0), lanes_(kHaveAvx512) {
   SH_CHECK(nshards >= 1 && nshards <= 1023 && pps >= 1, "bad router geometry");
   std::vector<std::pair<uint32_t, int>> pts;
   for (int i = 0; i < nshards; ++i)
@@ -60,6 +64,16 @@ HostRouter::HostRouter(int nshards, int pps)
   cw_.assign((size_t)n_, 0.0);
   for (int r = 0; r < n_; ++r) cw_[(size_t)r] = (double)(r + 1) / n_;
   cw_.back() = 1.0;
+  set_thresholds();
+}
+
+void HostRouter::set_lanes(bool on) { lanes_ = on && kHaveAvx512; }
+
+void HostRouter::set_thresholds() {
+  // cw <= x * 2^-53 <=> x >= ceil(cw * 2^53) for an integer x < 2^53 (exact in doubles)
+  spray_t_.assign(cw_.size(), 0);
+  for (size_t k = 0; k < cw_.size(); ++k)
+    spray_t_[k] = (uint64_t)std::ceil(cw_[k] * 9007199254740992.0);
 }
 
 HostRouter::~HostRouter() {
@@ -84,7 +98,7 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
   bits_mask_ = 0;
   if (n > 0) {
     uint64_t slots = 1024;
-    while (slots < 2 * (uint64_t)n) slots <<= 1;
+    while (slots < 4 * (uint64_t)n) slots <<= 1;
     hot_tab_.assign(slots, HotSlot{});
     hot_mask_ = slots - 1;
     uint64_t bits = 1 << 12;
@@ -127,6 +141,7 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
     cw_[(size_t)r] = acc / tot;
   }
   cw_.back() = 1.0;
+  set_thresholds();
 }
 
 uint32_t HostRouter::hot_code_slow(const Digest& d) const {
@@ -144,9 +159,18 @@ int HostRouter::spray(uint64_t j) const {
   return r;
 }
 
+int HostRouter::route_one_get(const Digest& d, uint64_t j) const {
+  const uint32_t c = nhot_ ? hot_code(d) : 0;
+  return c >= 2 ? (int)c - 2 : c == 1 ? spray(j) : owner(d);
+}
+
 template <bool kSets>
 void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0,
                              int32_t* dest, int64_t* counts) const {
+  if (!kSets && lanes_) {
+    route_gets_x8(keys, a, b, seq0, dest, counts);
+    return;
+  }
   if (!nhot_) {
     for (int64_t i = a; i < b; ++i) {
       const int o = owner(keys[i]);
@@ -202,6 +226,120 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
       ++counts[r];
     }
   }
+}
+
+// GETs, eight per iteration in 512-bit lanes: the span entry, the filter word and the
+// home slot are gathered, owner and hot code computed and selected under lane masks, and
+// the eight ranks stored as one 32-byte write. Lanes that need more (a span with more than
+// two points, a filter pass that missed the home slot, a sprayed object) are redone by the
+// scalar rule. The per-rank counts are taken from the written block afterwards (the
+// increments inside the lane loop would serialise on store-to-load forwarding).
+__attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
+    const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
+    int64_t* counts) const {
+  const long long* const span = reinterpret_cast<const long long*>(span_.data());
+  const long long* const bits = reinterpret_cast<const long long*>(hot_bits_.data());
+  const long long* const tab = reinterpret_cast<const long long*>(hot_tab_.data());
+  const __m512i ilo = _mm512_setr_epi64(0, 2, 4, 6, 8, 10, 12, 14);
+  const __m512i ihi = _mm512_setr_epi64(1, 3, 5, 7, 9, 11, 13, 15);
+  const __m512i m16 = _mm512_set1_epi64(0xFFFF), m1023 = _mm512_set1_epi64(1023);
+  const __m512i one = _mm512_set1_epi64(1), two = _mm512_set1_epi64(2);
+  const __m512i zero = _mm512_setzero_si512(), m63 = _mm512_set1_epi64(63);
+  const __m512i lane = _mm512_setr_epi64(0, 1, 2, 3, 4, 5, 6, 7);
+  const __m512i weyl = _mm512_set1_epi64((long long)kWeyl);
+  const __m512i bmask = _mm512_set1_epi64((long long)bits_mask_);
+  const __m512i hmask = _mm512_set1_epi64((long long)hot_mask_);
+  const bool hot = nhot_ != 0;
+  constexpr int64_t kBlock = 2048;  // counted while the block's ranks are in L1
+  uint32_t cnt[4][1024];
+  for (auto& c : cnt) std::fill(c, c + n_, 0u);
+  for (int64_t c0 = a; c0 < b; c0 += kBlock) {
+    const int64_t c1 = std::min(b, c0 + kBlock);
+    int64_t i = c0;
+    for (; i + 8 <= c1; i += 8) {
+      const __m512i k0 = _mm512_loadu_si512(keys + i), k1 = _mm512_loadu_si512(keys + i + 4);
+      const __m512i lo = _mm512_permutex2var_epi64(k0, ilo, k1);
+      const __m512i hi = _mm512_permutex2var_epi64(k0, ihi, k1);
+      // owner: t <= c1 ? o1 : t <= c2 ? o2 : o3 from the span entry
+      const __m512i se = _mm512_i64gather_epi64(_mm512_srli_epi64(hi, 48), span, 8);
+      const __m512i t = _mm512_and_si512(_mm512_srli_epi64(hi, 32), m16);
+      const __mmask8 s1 = _mm512_cmple_epu64_mask(t, _mm512_and_si512(se, m16));
+      const __mmask8 s2 =
+          _mm512_cmple_epu64_mask(t, _mm512_and_si512(_mm512_srli_epi64(se, 16), m16));
+      __m512i o = _mm512_mask_blend_epi64(s2, _mm512_and_si512(_mm512_srli_epi64(se, 52), m1023),
+                                          _mm512_and_si512(_mm512_srli_epi64(se, 42), m1023));
+      o = _mm512_mask_blend_epi64(s1, o, _mm512_and_si512(_mm512_srli_epi64(se, 32), m1023));
+      __mmask8 redo = _mm512_cmplt_epi64_mask(se, zero);  // bit 63: search the points
+      if (hot) {
+        const __m512i fb = _mm512_and_si512(_mm512_srli_epi64(lo, 20), bmask);
+        const __m512i w = _mm512_i64gather_epi64(_mm512_srli_epi64(fb, 6), bits, 8);
+        const __mmask8 pass =
+            _mm512_test_epi64_mask(_mm512_srlv_epi64(w, _mm512_and_si512(fb, m63)), one);
+        if (pass) {
+          // the home slot, then (where another object holds it) the next one: with the
+          // table at most a quarter full a digest that matches neither, and whose second
+          // slot is taken too, is rare (it is redone)
+          __m512i at = _mm512_slli_epi64(_mm512_and_si512(lo, hmask), 1);
+          __m512i elo = _mm512_mask_i64gather_epi64(zero, pass, at, tab, 8);
+          __m512i etag = _mm512_mask_i64gather_epi64(zero, pass, _mm512_add_epi64(at, one), tab, 8);
+          __m512i code = _mm512_and_si512(etag, m16);
+          __mmask8 hit = pass & _mm512_cmpeq_epi64_mask(elo, lo) &
+                         _mm512_cmpeq_epi64_mask(
+                             _mm512_srli_epi64(_mm512_xor_si512(etag, hi), 16), zero) &
+                         _mm512_test_epi64_mask(code, m16);
+          const __mmask8 other = pass & ~hit & _mm512_test_epi64_mask(code, m16);
+          if (other) {
+            at = _mm512_slli_epi64(_mm512_and_si512(_mm512_add_epi64(lo, one), hmask), 1);
+            elo = _mm512_mask_i64gather_epi64(zero, other, at, tab, 8);
+            etag = _mm512_mask_i64gather_epi64(zero, other, _mm512_add_epi64(at, one), tab, 8);
+            const __m512i code1 = _mm512_and_si512(etag, m16);
+            const __mmask8 hit1 = other & _mm512_cmpeq_epi64_mask(elo, lo) &
+                                  _mm512_cmpeq_epi64_mask(
+                                      _mm512_srli_epi64(_mm512_xor_si512(etag, hi), 16), zero) &
+                                  _mm512_test_epi64_mask(code1, m16);
+            code = _mm512_mask_mov_epi64(code, hit1, code1);
+            hit |= hit1;
+            redo |= other & ~hit1 & _mm512_test_epi64_mask(code1, m16);
+          }
+          const __mmask8 des = hit & _mm512_cmpge_epu64_mask(code, two);
+          o = _mm512_mask_sub_epi64(o, des, code, two);
+          const __mmask8 spr = hit & _mm512_cmpeq_epi64_mask(code, one);
+          // (a few ranks: computed for every group, as the sprayed lanes come and go at
+          // random; more: only when a lane needs it)
+          if (n_ <= 16 || spr) {
+            if (n_ <= 64) {  // r = #{thresholds <= the lane's 53-bit Weyl draw}
+              const __m512i j = _mm512_add_epi64(
+                  _mm512_set1_epi64((long long)(seq0 + (uint64_t)i)), lane);
+              const __m512i x = _mm512_srli_epi64(_mm512_mullo_epi64(j, weyl), 11);
+              __m512i r = zero;
+              for (int k = 0; k < n_ - 1; ++k)
+                r = _mm512_mask_add_epi64(
+                    r, _mm512_cmpge_epu64_mask(x, _mm512_set1_epi64((long long)spray_t_[(size_t)k])),
+                    r, one);
+              o = _mm512_mask_mov_epi64(o, spr, r);
+            } else {
+              redo |= spr;
+            }
+          }
+        }
+      }
+      _mm256_storeu_si256(reinterpret_cast<__m256i*>(dest + i), _mm512_cvtepi64_epi32(o));
+      if (__builtin_expect(redo != 0, 0))
+        for (unsigned m = redo; m; m &= m - 1) {
+          const int l = __builtin_ctz(m);
+          dest[i + l] = route_one_get(keys[i + l], seq0 + (uint64_t)(i + l));
+        }
+    }
+    for (; i < c1; ++i) dest[i] = route_one_get(keys[i], seq0 + (uint64_t)i);
+    for (i = c0; i + 4 <= c1; i += 4) {
+      ++cnt[0][dest[i]];
+      ++cnt[1][dest[i + 1]];
+      ++cnt[2][dest[i + 2]];
+      ++cnt[3][dest[i + 3]];
+    }
+    for (; i < c1; ++i) ++cnt[0][dest[i]];
+  }
+  for (int r = 0; r < n_; ++r) counts[r] += (int64_t)cnt[0][r] + cnt[1][r] + cnt[2][r] + cnt[3][r];
 }
 
 void HostRouter::worker(int id) {

@@ -23,15 +23,17 @@
 //   SET        hot(d) ? every rank (dest -1) : owner(d).
 //
 // Throughput: a batch is split over a persistent worker pool (threads created once, not
-// per call), and a request is routed without a data-dependent branch in the common cases:
-// its owner (one 8-B span-table load) and its hot-table home slot are both read and the
-// result selected by masks; only a digest that passes the filter but is not in its home
-// slot (a filter false positive, or a hot object displaced by a hotter one: the set is
-// inserted hottest first) and the few sprayed objects branch. Branching on hot vs cold
-// mispredicted on a large share of a Zipf stream's requests (a host micro-benchmark,
-// scripts/router_micro.py: 65 against 173 M requests/s per thread with 256 hot objects).
-// The home-slot read is cheap while the hot set is small (the bench's default 1024
-// objects: a 32 KiB table); with 64K objects it misses the caches for cold requests.
+// per call). GETs go eight at a time through 512-bit lanes where the CPU has AVX-512
+// (route_gets_x8): the span entry, filter word and hot-table slots are gathered and owner,
+// hot code and spray rank computed and selected under lane masks; a lane needing more (a
+// span with more than two points, a digest past its second probe slot, a spray over more
+// than 64 ranks) is redone by the scalar rule. The scalar rule (SETs, and CPUs without
+// AVX-512) selects by masks too: branching on hot vs cold mispredicted on a large share of
+// a Zipf stream's requests. The hot set must arrive hottest first (HotSpread passes plan's
+// order): inserted in digest order, displaced hot objects sent a quarter of the 8-lane
+// groups down the second probe and 4.6 % of the lanes to the scalar redo. Per thread on a
+// Xeon core (scripts/router_micro.py, 8 GPUs, 1024 hot objects, Zipf 0.99): 45-63 M
+// requests/s scalar, 165-190 M in lanes; 174 and ~260 M without a hot set.
 // The hot table matches a digest on its low word and the top 48 bits of its high word (the
 // low 16 bits hold the rank): a cold digest agreeing on those 112 bits would be treated as
 // hot — consistently for its GETs and SETs, so it would still be served correctly.
@@ -83,11 +85,15 @@ class HostRouter {
   // dest[i] = owner, or -1 (a hot object: every rank); counts[r] += rows rank r stores.
   void route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_t* counts,
                   int threads) const;
+  // The 8-lane AVX-512 GET path (on where the CPU has AVX-512F/DQ; off: the scalar rule).
+  // Both make the same decisions; the switch is for tests and comparisons.
+  bool lanes() const { return lanes_; }
+  void set_lanes(bool on);
   // Cumulative spray weights (nshards doubles, the last exactly 1).
   const std::vector<double>& cumulative() const { return cw_; }
 
  private:
-  // hot table: open addressing on lo (linear probing, at most half full), slots
+  // hot table: open addressing on lo (linear probing, at most a quarter full), slots
   // {lo, (hi & ~0xFFFF) | code}, code = designated rank + 2 (1: sprayed, 0: empty). The hot
   // set is inserted hottest first, so the objects that carry most requests sit in their
   // home slot; a one-hash filter (16 bits per object) answers most cold digests.
@@ -111,6 +117,9 @@ class HostRouter {
   uint32_t hot_code_slow(const Digest& d) const;
   int search(uint32_t p) const;
   int spray(uint64_t j) const;
+  int route_one_get(const Digest& d, uint64_t j) const;  // the scalar GET rule
+  void route_gets_x8(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
+                     int64_t* counts) const;
   template <bool kSets>
   void route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
                    int64_t* counts) const;
@@ -130,6 +139,9 @@ class HostRouter {
   uint64_t bits_mask_ = 0;
   int64_t nhot_ = 0;
   std::vector<double> cw_;
+  bool lanes_;
+  std::vector<uint64_t> spray_t_;  // ceil(cw * 2^53): spray() on integers (the lane path)
+  void set_thresholds();
   // the worker pool (grown on demand; one job at a time: callers serialise on call_mu_)
   mutable std::mutex call_mu_, mu_;
   mutable std::condition_variable cv_, done_cv_;

@@ -234,8 +234,11 @@ class HotSpread:
                  else ranks.to(torch.int32).cpu().index_select(0, order.cpu()))
             self.hot_rank = r.contiguous().to(self.device)
             self.weights = list(weights) if weights is not None else [1.0] * self.world
-            h = self.hot.cpu().contiguous()
-            rh = r.contiguous()
+            # the native router in the given order (plan's: hottest first, so the objects
+            # that carry most requests get their home slots)
+            h = hot.cpu().contiguous()
+            rh = (torch.full((hot.shape[0],), -1, dtype=torch.int32) if ranks is None
+                  else ranks.to(torch.int32).cpu().contiguous())
             self.router.set_hot(h.data_ptr(), h.shape[0], rh.data_ptr(), self.weights)
         self.cw = torch.tensor(cumulative(self.weights), dtype=torch.float64, device=self.device)
 

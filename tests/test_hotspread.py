@@ -7,11 +7,16 @@ import torch
 from shellac_amd.parallel.hotspread import HotSpread, cumulative, spray_ranks, water_fill
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_native_router_matches_tensor_routing(world):
+@pytest.mark.parametrize("lanes", [False, True])
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 20, 70])
+def test_native_router_matches_tensor_routing(world, lanes):
     g = torch.Generator().manual_seed(world)
     keys = torch.randint(-2**63, 2**63 - 1, (50000, 2), dtype=torch.int64, generator=g)
+    # crowded hot-table buckets: 40 hot objects on one home slot (long probe runs: the
+    # lanes' second probe misses and the scalar rule redoes them)
+    keys[260:300, 0] = (keys[260:300, 0] & ~0xFFFF) | 0x1234
     hs = HotSpread(world, "cpu")
+    hs.router.lanes = lanes
     stream = keys[torch.randint(0, 3000, (200000,), generator=g)].contiguous()
     for hot in (None, keys[:300]):
         w = [1.0 + (r % 3) for r in range(world)]
@@ -23,6 +28,9 @@ def test_native_router_matches_tensor_routing(world):
             d, c = hs.host_route_gets(stream, seq0=seq0, threads=3)
             assert torch.equal(d, hs.route_gets(stream, seq0=seq0))
             assert torch.equal(c, torch.bincount(d.long(), minlength=world))
+            # an odd-sized slice (the lanes' scalar tail) at an odd stream position
+            d1, _ = hs.host_route_gets(stream[7:1006], seq0=seq0 + 7)
+            assert torch.equal(d1, d[7:1006])
         s, c = hs.host_route_sets(stream, threads=2)
         assert torch.equal(s, hs.route_sets(stream))
         fan = int((s < 0).sum())
