@@ -59,6 +59,19 @@ def parse():
     ap.add_argument("--batch", type=int, default=1 << 20, help="GET requests per rank per step")
     ap.add_argument("--sets", type=int, default=1 << 16, help="SET requests per rank per step")
     ap.add_argument("--keys-per-gpu", type=int, default=4 << 20)
+    ap.add_argument("--keys-total", type=int, default=None,
+                    help="a fixed total key count (strong scaling of capacity): each of the N "
+                         "ranks gets keys-total / N instead of --keys-per-gpu (with --set-walk "
+                         "and a fixed --pressured-gb: hit ratio against the pooled capacity, "
+                         "scripts/pooled_capacity.sh)")
+    ap.add_argument("--walk-get-batches", type=int, default=256,
+                    help="GET batches of the request stream pre-generated for --set-walk and "
+                         "log_overfull (cycled; more than a log lap of steps, so a key's "
+                         "re-reads are the stream's, not the cycle's)")
+    ap.add_argument("--set-walk", action="store_true",
+                    help="the full-cache blocks' SETs walk a permutation of every key the shard "
+                         "holds (each re-SET once per keys/sets steps) instead of cycling the "
+                         "pre-generated SET batches: an evicted key comes back")
     ap.add_argument("--zipf", type=float, default=0.99)
     ap.add_argument("--min-val", type=int, default=64)
     ap.add_argument("--max-val", type=int, default=4096)
@@ -282,6 +295,9 @@ def check_memory_budget(args, world, sim, dev) -> None:
         pgb = (args.pressured_gb if args.pressured_gb is not None else
                args.keys_per_gpu * (mean_val + 48) / max(args.pressured_fill, 0.1) / gib)
         need += pgb * gib + nb * 128
+    if args.set_walk or (args.overfull_fill > 0 and args.pressured_gb is None):
+        # walk_batches(): fresh GET batches (ids + digests) and SET batches over every key
+        need += args.walk_get_batches * args.batch * 24 + args.keys_per_gpu * 48
     if sim:  # the probe digests of the key space and their sorted index
         need += args.keys_per_gpu * sim * 48
     free, total = torch.cuda.mem_get_info(dev)
@@ -393,6 +409,8 @@ def main():
         group = MirrorComm(sim)
         world = sim
     real_world = 1 if sim else world
+    if args.keys_total:
+        args.keys_per_gpu = max(1, args.keys_total // world)
     # N real ranks behind host proxies: each GPU serves the requests for the keys it owns
     # (a bounce rehearsal keeps the device-routed step unless --route host is given: then
     # every rank is a host-routed GPU server sharing cuda:0, its barriers and reductions
@@ -633,13 +651,15 @@ def main():
     if ready is not None:
         ready.record()
 
-    set_cycle = [sets]   # the SET batches the steps cycle (a phase may swap in its own)
+    # the batches the steps cycle (a phase may swap in its own): GET digests, their ids
+    # (for --check) and the SET batches
+    cyc = {"gets": gets, "get_ids": get_ids, "sets": sets}
 
     def serve_i(cache, i):
         # GET batch then SET batch; with one rank the GET's host sync overlaps the SET
-        sl = set_cycle[0]
-        return cache.serve(gets[i % P], sl[i % len(sl)], inputs_ready=ready,
-                           probe_keys=gprobe[i % P])
+        gl, sl = cyc["gets"], cyc["sets"]
+        return cache.serve(gl[i % len(gl)], sl[i % len(sl)], inputs_ready=ready,
+                           probe_keys=gprobe[i % P] if msim else None)
 
     def step(i):
         return serve_i(sc, i)
@@ -714,7 +734,8 @@ def main():
         if real_world > 1:
             dist.all_reduce(agg)
         hits, gops, gbytes, rep, greq, rbytes = (int(v) for v in agg.tolist())
-        return {"el": el, "res": res, "last": (first + args.steps - 1) % P, "hits": hits,
+        return {"el": el, "res": res, "last": (first + args.steps - 1) % len(cyc["gets"]),
+                "hits": hits,
                 "gops": gops, "gbytes": gbytes, "rep": rep, "greq": greq, "rbytes": rbytes,
                 "head0": h0, "head1": shard_.head(), "gathered": gathered, "c0": c0, "c1": c1,
                 "rank_ms": rank_ms, "wiv": wiv}
@@ -726,7 +747,7 @@ def main():
 
         res, last_batch = w["res"], w["last"]
         k = 200
-        ids = get_ids[last_batch][:k]
+        ids = cyc["get_ids"][last_batch][:k]
         res.wait()
         recs = unpack_records(res.data, res.off[:k], res.size[:k])
         if msim:
@@ -744,7 +765,7 @@ def main():
         # every hit of the whole last batch: its record's header names the requested digest
         words = res.data[: res.data.numel() // 8 * 8].view(torch.int64)
         wd = words.device  # pinned host memory under --edge host
-        keys_last = gets[last_batch].to(wd)
+        keys_last = cyc["gets"][last_batch].to(wd)
         hit = (res.size > 0).to(wd)
         at = torch.where(hit, torch.div(res.off.to(wd), 8, rounding_mode="floor"),
                          torch.zeros_like(res.off, device=wd))
@@ -941,13 +962,13 @@ def main():
     # the full cache (the headline): a shard whose working set fills --pressured-fill of its
     # log, wrapped, so the CLOCK hand re-appends the objects the steps read (reinsertions)
     # and evicts the rest: the state a serving cache runs in (memcached evicts under load)
-    def full_cache(gb, check_it, min_fill=0, set_list=None):
+    def full_cache(gb, check_it, min_fill=0, walk=None):
         """A shard of `gb` GiB populated with this rank's keys, wrapped (fill steps, at least
         `min_fill`), then the headline protocol (K timed steps), a GPU-event pass and one
-        whole lap timed: (summary, window, event intervals, fill steps). `set_list`: the
-        SET batches the steps cycle instead of the default ones."""
-        if set_list is not None:
-            set_cycle[0] = set_list
+        whole lap timed: (summary, window, event intervals, fill steps). `walk`: the
+        (GET digests, GET ids, SET batches) the steps cycle instead of the default ones."""
+        if walk is not None:
+            cyc["gets"], cyc["get_ids"], cyc["sets"] = walk
         f_log = int(gb * (1 << 30)) // 16 * 16
         f_shard = CacheShard(f_log, nb, max_item=1 << 20, device=dev, evict=args.evict)
         f_sc = ShardedCache(f_shard, group=group, replica=replica,
@@ -964,20 +985,58 @@ def main():
         if real_world > 1:
             dist.barrier()
         fbase = 3 * args.warmup + 2 * args.steps
+
+        def debug_hot(when):
+            # SHELLAC_BENCH_DEBUG_HOT=1 (diagnostic): which of the 16 most popular objects
+            # this shard holds (host routing: their owner and GET rank)
+            if not os.environ.get("SHELLAC_BENCH_DEBUG_HOT"):
+                return
+            f_sc.sync_sets()
+            sync()
+            top = wl.rank_to_id[:16]
+            d = wl.digests.index_select(0, top).contiguous()
+            _, _, sz = f_shard.get(d)
+            extra = ""
+            if host_route:
+                extra = (f" owners {owner_of.index_select(0, top).tolist()} GET ranks "
+                         f"{spread.route_gets(d).tolist()}")
+            hand, tail, head, hloc = f_shard._impl.debug_hand()
+            lag = (hloc - (head - f_log)) / 2**20 if hloc != 2**64 - 1 else None
+            log(rank, f"[debug] {when}: top-16 present {(sz > 0).int().tolist()}{extra}; hand "
+                      f"{tail - hand} entries behind the ring tail, its item {lag} MiB past "
+                      f"the overwrite point")
+
+        debug_hot("after populate")
         ffill = fill_to_wrap(f_sc, f_shard, f_log, fbase, per_step)
+        debug_hot("after fill")
         if ffill is not None and ffill < min_fill:
             for i in range(ffill, min_fill):
                 serve_i(f_sc, fbase + i)
+                if i % 64 == 0:
+                    debug_hot(f"fill step {i}")
             sync()
             ffill = min_fill
         out_ = fw = fiv = None
         if ffill is not None:
             fw = window(f_sc, f_shard, fbase + ffill)
+            debug_hot("after window")
             if check_it:
                 check(fw)
             fiv = timed(args.steps, fbase + ffill + args.steps, events=True,
                         cache=f_sc)[1] if use_events else []
             out_ = summary(fw, fiv, f_log, ffill)
+            # what a client sees: the share of GET requests (duplicates included) answered
+            # with a record, over K more steps (untimed: a reduction per step)
+            hit_n = torch.zeros(2, dtype=torch.int64, device=dev)
+            for i in range(args.steps):
+                res = serve_i(f_sc, fbase + ffill + 2 * args.steps + i).wait()
+                hit_n[0] += (res.size > 0).sum().to(dev)
+                hit_n[1] += res.size.numel()
+            if real_world > 1:
+                hr = hit_n.to(rdev)
+                dist.all_reduce(hr)
+                hit_n = hr
+            out_["request_hit_ratio"] = round(float(hit_n[0]) / max(float(hit_n[1]), 1.0), 4)
             # the cost of a step varies with where the hand is in the lap (the objects it
             # re-appended one lap earlier come round together): one whole lap, timed
             lap_steps = int(f_log / max(1.0, (fw["head1"] - fw["head0"]) / args.steps)) + 1
@@ -985,37 +1044,66 @@ def main():
                 lt = torch.tensor([lap_steps], dtype=torch.int64, device=rdev)
                 dist.all_reduce(lt, op=dist.ReduceOp.MAX)
                 lap_steps = int(lt)
-            lap_el = timed(lap_steps, fbase + ffill + 2 * args.steps, cache=f_sc)[0]
+            lap_el = timed(lap_steps, fbase + ffill + 3 * args.steps, cache=f_sc)[0]
             out_["lap_steps"] = lap_steps
             out_["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
         f_sc.sync_sets()
-        set_cycle[0] = sets
+        cyc["gets"], cyc["get_ids"], cyc["sets"] = gets, get_ids, sets
         del f_sc, f_shard
         return out_, fw, fiv, ffill
 
+    def walk_batches():
+        """For a cache that cannot hold every key: (GET digests, GET ids, SET batches) where
+        the SETs walk a random permutation of every key this rank holds (an evicted key comes
+        back when the walk reaches it, like a cache-aside refill of the whole key space) and
+        the GETs are --walk-get-batches fresh batches of the request stream. The 16 default
+        GET batches repeat every 16 steps, so the keys they touch (~1/3 of 16M requests)
+        would be the whole read working set: a log far smaller than the key space would
+        still hold all of it."""
+        own = torch.arange(lo, hi, device=dev) if fill_ids is None else fill_ids
+        g = torch.Generator(device="cpu").manual_seed(777 + rank)
+        own = own.index_select(0, torch.randperm(int(own.numel()), generator=g).to(own.device))
+        ws_ = [wl.set_batch(own[s0: s0 + args.sets].contiguous())
+               for s0 in range(0, max(1, int(own.numel()) - args.sets + 1), args.sets)]
+        del own
+        gi = []
+        for i in range(max(args.walk_get_batches, 1)):
+            if host_route:   # this rank's share of batch P + i of the global stream
+                gg, gd, _, _ = global_batch(P + i)
+                gi.append(gg[gd == me].contiguous())
+                del gg, gd
+            else:
+                gi.append(wl.sample_ids(args.batch, 200000 + 1009 * rank + i))
+        gd_ = [wl.digests.index_select(0, x).contiguous() for x in gi]
+        return gd_, gi, ws_
+
     pressured = pw = piv = pfill = None
     if do_pressured:
-        pressured, pw, piv, pfill = full_cache(p_gb, args.check and headline == "pressured")
+        wb = walk_batches() if args.set_walk else None
+        pressured, pw, piv, pfill = full_cache(
+            p_gb, args.check and headline == "pressured",
+            min_fill=2 * len(wb[2]) if wb else 0, walk=wb)
+        if wb and pressured is not None:
+            pressured["set_batches_cycled"] = len(wb[2])
+            pressured["get_batches_cycled"] = len(wb[0])
+        del wb
     # secondary: a working set larger than the log (--overfull-fill x the log): the hit ratio
     # when the cache cannot hold every key
     overfull = None
     if do_pressured and args.overfull_fill > 0 and args.pressured_gb is None:
-        # An evicted key comes back only when it is SET again: the default steps cycle 16
-        # SET batches (1M of the 4M keys), so here the SETs walk a permutation of every key
-        # this rank holds (each re-SET once per keys/sets steps, like a cache-aside refill
-        # of the whole key space). The populate itself wraps this log, evicting unread
-        # objects in key order: two passes of the permutation run before the window, so it
-        # sees the steady state, not the populate's transient.
-        own = (torch.arange(lo, hi, device=dev) if fill_ids is None else fill_ids)
-        g = torch.Generator(device="cpu").manual_seed(777 + rank)
-        own = own.index_select(0, torch.randperm(int(own.numel()), generator=g).to(own.device))
-        ov_sets = [wl.set_batch(own[s0: s0 + args.sets].contiguous())
-                   for s0 in range(0, int(own.numel()) - args.sets + 1, args.sets)]
+        # An evicted key comes back only when it is SET again (the default steps cycle 16
+        # SET batches, 1M of the 4M keys), and 16 cycled GET batches read only ~1/3 of the
+        # keys: walk_batches() (every key re-SET in turn, 256 fresh GET batches). The
+        # populate itself wraps this log, evicting unread objects in key order: two passes
+        # of the walk run before the window, so it sees the steady state, not the populate's
+        # transient.
+        wb = walk_batches()
         overfull = full_cache(ws_bytes / args.overfull_fill / (1 << 30), False,
-                              min_fill=2 * len(ov_sets), set_list=ov_sets)[0]
+                              min_fill=2 * len(wb[2]), walk=wb)[0]
         if overfull is not None:
-            overfull["set_batches_cycled"] = len(ov_sets)
-        del own, ov_sets
+            overfull["set_batches_cycled"] = len(wb[2])
+            overfull["get_batches_cycled"] = len(wb[0])
+        del wb
     if headline == "pressured" and pw is None:
         raise SystemExit("[bench] the pressured log could not be wrapped for the headline; "
                          "pass --headline wrapped")
