@@ -159,16 +159,18 @@ int HostRouter::spray(uint64_t j) const {
   return r;
 }
 
-int HostRouter::route_one_get(const Digest& d, uint64_t j) const {
+template <bool kSets>
+int HostRouter::route_one(const Digest& d, uint64_t j) const {
   const uint32_t c = nhot_ ? hot_code(d) : 0;
+  if (kSets) return c ? -1 : owner(d);
   return c >= 2 ? (int)c - 2 : c == 1 ? spray(j) : owner(d);
 }
 
 template <bool kSets>
 void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0,
                              int32_t* dest, int64_t* counts) const {
-  if (!kSets && lanes_) {
-    route_gets_x8(keys, a, b, seq0, dest, counts);
+  if (lanes_) {
+    route_x8<kSets>(keys, a, b, seq0, dest, counts);
     return;
   }
   if (!nhot_) {
@@ -228,13 +230,15 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
   }
 }
 
-// GETs, eight per iteration in 512-bit lanes: the span entry, the filter word and the
+// Eight requests per iteration in 512-bit lanes: the span entry, the filter word and the
 // home slot are gathered, owner and hot code computed and selected under lane masks, and
 // the eight ranks stored as one 32-byte write. Lanes that need more (a span with more than
-// two points, a filter pass that missed the home slot, a sprayed object) are redone by the
-// scalar rule. The per-rank counts are taken from the written block afterwards (the
-// increments inside the lane loop would serialise on store-to-load forwarding).
-__attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
+// two points, a filter pass that missed both probe slots, a GET of a sprayed object over
+// more than 64 ranks) are redone by the scalar rule. The per-rank counts are taken from the
+// written block afterwards (the increments inside the lane loop would serialise on
+// store-to-load forwarding). SETs (kSets): a hot object's lane is -1 (every rank).
+template <bool kSets>
+__attribute__((target("avx512f,avx512dq"))) void HostRouter::route_x8(
     const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
     int64_t* counts) const {
   const long long* const span = reinterpret_cast<const long long*>(span_.data());
@@ -253,6 +257,7 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
   constexpr int64_t kBlock = 2048;  // counted while the block's ranks are in L1
   uint32_t cnt[4][1024];
   for (auto& c : cnt) std::fill(c, c + n_, 0u);
+  int64_t fan = 0;
   for (int64_t c0 = a; c0 < b; c0 += kBlock) {
     const int64_t c1 = std::min(b, c0 + kBlock);
     int64_t i = c0;
@@ -301,6 +306,9 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
             hit |= hit1;
             redo |= other & ~hit1 & _mm512_test_epi64_mask(code1, m16);
           }
+          if (kSets) {
+            o = _mm512_mask_mov_epi64(o, hit, _mm512_set1_epi64(-1));
+          } else {
           const __mmask8 des = hit & _mm512_cmpge_epu64_mask(code, two);
           o = _mm512_mask_sub_epi64(o, des, code, two);
           const __mmask8 spr = hit & _mm512_cmpeq_epi64_mask(code, one);
@@ -321,16 +329,24 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
               redo |= spr;
             }
           }
+          }
         }
       }
       _mm256_storeu_si256(reinterpret_cast<__m256i*>(dest + i), _mm512_cvtepi64_epi32(o));
       if (__builtin_expect(redo != 0, 0))
         for (unsigned m = redo; m; m &= m - 1) {
           const int l = __builtin_ctz(m);
-          dest[i + l] = route_one_get(keys[i + l], seq0 + (uint64_t)(i + l));
+          dest[i + l] = route_one<kSets>(keys[i + l], seq0 + (uint64_t)(i + l));
         }
     }
-    for (; i < c1; ++i) dest[i] = route_one_get(keys[i], seq0 + (uint64_t)i);
+    for (; i < c1; ++i) dest[i] = route_one<kSets>(keys[i], seq0 + (uint64_t)i);
+    if (kSets) {  // -1 (a hot object's SET) counts once for every rank
+      for (i = c0; i < c1; ++i) {
+        const int32_t r = dest[i];
+        if (r < 0) ++fan; else ++cnt[i & 3][r];
+      }
+      continue;
+    }
     for (i = c0; i + 4 <= c1; i += 4) {
       ++cnt[0][dest[i]];
       ++cnt[1][dest[i + 1]];
@@ -339,7 +355,8 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_gets_x8(
     }
     for (; i < c1; ++i) ++cnt[0][dest[i]];
   }
-  for (int r = 0; r < n_; ++r) counts[r] += (int64_t)cnt[0][r] + cnt[1][r] + cnt[2][r] + cnt[3][r];
+  for (int r = 0; r < n_; ++r)
+    counts[r] += (int64_t)cnt[0][r] + cnt[1][r] + cnt[2][r] + cnt[3][r] + fan;
 }
 
 void HostRouter::worker(int id) {

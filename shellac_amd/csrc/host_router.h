@@ -23,11 +23,11 @@
 //   SET        hot(d) ? every rank (dest -1) : owner(d).
 //
 // Throughput: a batch is split over a persistent worker pool (threads created once, not
-// per call). GETs go eight at a time through 512-bit lanes where the CPU has AVX-512
-// (route_gets_x8): the span entry, filter word and hot-table slots are gathered and owner,
+// per call). Requests go eight at a time through 512-bit lanes where the CPU has AVX-512
+// (route_x8): the span entry, filter word and hot-table slots are gathered and owner,
 // hot code and spray rank computed and selected under lane masks; a lane needing more (a
 // span with more than two points, a digest past its second probe slot, a spray over more
-// than 64 ranks) is redone by the scalar rule. The scalar rule (SETs, and CPUs without
+// than 64 ranks) is redone by the scalar rule. The scalar rule (CPUs without
 // AVX-512) selects by masks too: branching on hot vs cold mispredicted on a large share of
 // a Zipf stream's requests. The hot set must arrive hottest first (HotSpread passes plan's
 // order): inserted in digest order, displaced hot objects sent a quarter of the 8-lane
@@ -117,9 +117,11 @@ class HostRouter {
   uint32_t hot_code_slow(const Digest& d) const;
   int search(uint32_t p) const;
   int spray(uint64_t j) const;
-  int route_one_get(const Digest& d, uint64_t j) const;  // the scalar GET rule
-  void route_gets_x8(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
-                     int64_t* counts) const;
+  template <bool kSets>
+  int route_one(const Digest& d, uint64_t j) const;  // the scalar rule
+  template <bool kSets>
+  void route_x8(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
+                int64_t* counts) const;
   template <bool kSets>
   void route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
                    int64_t* counts) const;
