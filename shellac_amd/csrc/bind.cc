@@ -208,6 +208,7 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("flush", [](HbmCache& c, uintptr_t s) { c.flush(S(s)); })
       .def("debug_bucket", &HbmCache::debug_bucket)
+      .def("debug_hand", &HbmCache::debug_hand)
       .def("debug_set_entry", &HbmCache::debug_set_entry)
       .def("export_keys", [](HbmCache& c, uintptr_t out, uint64_t cap, uint32_t now, uintptr_t s) {
         py::gil_scoped_release nogil;

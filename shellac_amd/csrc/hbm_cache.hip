@@ -2385,12 +2385,17 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 //              the batch overwrites, which the previous step's gather may still read).
 // The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
 // win over a reinsertion of the same key). Host twin: HostCache::reclaim.
+constexpr unsigned long long kRcCount = 1ull << 43;  // k_rc_scan / k_rc_emit packed counts
+
 struct RcArgs {
   const uint64_t* ring;
   uint64_t rmask;
   const uint64_t* ring_tail;  // the last batch whose ring entries are written (see store)
-  unsigned long long* ctl;  // [0] hand, [1] batch bytes B, [2] first meeting entry, [3] scanned
-  int64_t W;
+  // [0] hand, [1] batch bytes B, [2] first meeting entry, [3] scanned, [4] entries the last
+  // batch consumed (the adaptive window, layout.h hand_window_eff)
+  unsigned long long* ctl;
+  int64_t W;      // the window's rows
+  int64_t n_new;  // the batch's rows (the window's base 2n + 256; reinsertions <= W - n)
   const uint64_t* head_ptr;  // the claim word: the head the queued appends will reach
   uint64_t cap;
   uint32_t now;
@@ -2442,11 +2447,13 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t avail = rtail - hand;
   // the entries this hand examines (a detached hand sees the ring tail of the batch before
-  // the previous one): the advance consumes at most these
-  if (j == 0) a.ctl[3] = (uint64_t)a.W < avail ? (uint64_t)a.W : avail;
+  // the previous one; rows past the effective window are skip rows): the advance consumes
+  // at most these
+  const int64_t weff = hand_window_eff(a.n_new, a.ctl[4]);
+  if (j == 0) a.ctl[3] = (uint64_t)weff < avail ? (uint64_t)weff : avail;
   uint64_t loc = kRingSkip, h = 0;
   uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
-  if (j < a.W && (uint64_t)j < avail) {
+  if (j < weff && (uint64_t)j < avail) {
     const uint64_t idx = hand + (uint64_t)j;
     const uint64_t l = rtail - idx <= a.rmask + 1 ? a.ring[idx & a.rmask] : kRingSkip;
     if (l != kRingSkip && head <= l + a.cap) {  // intact (not overwritten yet)
@@ -2494,7 +2501,8 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
     cb.expire[j] = h ? w1.z : 0u;
     cb.from[j] = 0;
   }
-  block_partial(h, part_h);
+  // hot bytes and (bits 43+) hot entries, scanned together by k_rc_emit
+  block_partial(h ? h + kRcCount : 0ull, part_h);
   // batch bytes: one atomic per block
   __shared__ unsigned long long s_b[kBlock / 64];
   best = wave_sum(best);
@@ -2528,7 +2536,8 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
   __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t h = j < a.W ? rc_h[j] : 0;
-  unsigned long long inc = h;
+  const unsigned long long hp = h ? h + kRcCount : 0ull;  // bytes | hot entries << 43
+  unsigned long long inc = hp;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const unsigned long long o = __shfl_up(inc, d);
@@ -2537,8 +2546,10 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
   __syncthreads();  // s_w reuse
   if (lane == 63) s_w[w] = inc;
   __syncthreads();
-  unsigned long long hx = s_pre + inc - h;
-  for (int k = 0; k < w; ++k) hx += s_w[k];
+  unsigned long long hxp = s_pre + inc - hp;
+  for (int k = 0; k < w; ++k) hxp += s_w[k];
+  // hot bytes and hot entries before entry j
+  const unsigned long long hx = hxp & (kRcCount - 1), hc = hxp / kRcCount;
   bool meets = false;
   unsigned long long nre = 0, bre = 0;
   if (j < a.W) {
@@ -2552,7 +2563,8 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
       // lead mode: a pick must lie beyond everything the batch can overwrite (its bytes +
       // the whole budget); an unsafe one (the hand not yet `lead` ahead: the first steps
       // after the log fills, a batch much larger than the last) ages out
-      if (!meets && hx + h <= a.rmax && (!a.lead_mode || loc + a.cap >= head + bb + a.rmax)) {
+      if (!meets && hx + h <= a.rmax && hc < (unsigned long long)(a.W - a.n_new) &&
+          (!a.lead_mode || loc + a.cap >= head + bb + a.rmax)) {
         pick = true;
         cb.voff[j] = a.lead_mode ? (uint64_t)(uintptr_t)log + loc % a.cap + kItemHeaderBytes
                                  : (uint64_t)(uintptr_t)scratch + hx + kItemHeaderBytes;
@@ -2585,19 +2597,48 @@ struct RcAdvance {
   const uint64_t* ring_tail = nullptr;
   uint64_t rmask = 0;
   int64_t W = 0;
+  const uint64_t* ring = nullptr;
+  const uint64_t* head = nullptr;  // the claim word (the head before this batch's append)
+  uint64_t cap = 0;
 };
+
+// A hand behind the overwrite (batches that skipped it while the log filled, e.g. a
+// populate that queued dozens of stores before the first completed, or a burst it could not
+// keep up with) would spend its windows on items already overwritten while referenced ones
+// reach the overwrite unexamined: it jumps to the first entry the overwrite has not reached.
+// Ring locations grow along the ring; a skip entry ends the search early (conservative).
+// One dependent load when the hand is where it should be; a binary search otherwise.
+// HostCache::reclaim_locked does the same.
+__device__ __forceinline__ uint64_t hand_catch_up(const uint64_t* ring, uint64_t rmask,
+                                                  uint64_t hand, uint64_t rtail, uint64_t head,
+                                                  uint64_t cap) {
+  auto over = [&](uint64_t idx) {
+    const uint64_t l = ring[idx & rmask];
+    return l != kRingSkip && head > l + cap;
+  };
+  if (hand >= rtail || !over(hand)) return hand;
+  uint64_t lo = hand + 1, hi = rtail;  // over(lo - 1); the first entry not over in [lo, hi]
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (over(mid)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
 
 __device__ __forceinline__ void rc_advance(const RcAdvance& r) {
   const uint64_t rtail = *r.ring_tail;
   const uint64_t hand0 = r.ctl[0];
   const uint64_t weff = r.ctl[3];  // the entries the hand examined (k_rc_scan)
   const unsigned long long cut = r.ctl[2];
-  uint64_t hand = hand0 + (cut != ~0ull && cut < weff ? cut : weff);
+  const uint64_t consumed = cut != ~0ull && cut < weff ? cut : weff;
+  uint64_t hand = hand0 + consumed;
   if (rtail - hand > r.rmask + 1) hand = rtail - (r.rmask + 1);  // ring lapped the hand
+  hand = hand_catch_up(r.ring, r.rmask, hand, rtail, *r.head, r.cap);
   r.ctl[0] = hand;
   r.ctl[1] = 0;
   r.ctl[2] = ~0ull;
   r.ctl[3] = 0;
+  r.ctl[4] = consumed;  // the next batch's window (hand_window_eff)
 }
 
 // SET dedupe (last writer of a digest wins). `adv`: the CLOCK hand step before this batch
@@ -3177,6 +3218,8 @@ bool HbmCache::should_reclaim(uint64_t bytes_bound) const {
   // few stores may be queued behind it, so reclaim once the log is within 4 batches of
   // wrapping (the hand step decides exactly on the device; skipping is only an
   // optimisation for a log that has not filled yet)
+  // (a populate queues dozens of large batches before the first completes, so they can all
+  // skip the hand and leave it laps behind the overwrite: rc_advance then jumps it)
   const uint64_t h = __atomic_load_n(host_slots_ + kHeadSlot, __ATOMIC_ACQUIRE);
   return h + 4 * (bytes_bound + rmax_) > cfg_.log_bytes;
 }
@@ -3189,7 +3232,7 @@ void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const u
   // the head slot once they have run). The ring tail: a detached hand may run before the
   // previous batch's fixup writes its ring entries and tail, so it reads the tail of the
   // batch before that one (the other ping-pong slot), whose entries are written.
-  RcArgs a{ring_, ring_cap_ - 1, detached ? next_ring_tail() : cur_ring_tail(), rc_ctl_, w,
+  RcArgs a{ring_, ring_cap_ - 1, detached ? next_ring_tail() : cur_ring_tail(), rc_ctl_, w, n,
            claim_ptr(), cfg_.log_bytes, now, rmax, lead ? 1ull : 0ull};
   const int g = (int)((w + kBlock - 1) / kBlock);
   const HandBuf& hb = hb_[hand_b_];
@@ -3650,7 +3693,7 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
   RcAdvance adv;
   if (rc_adv_w_ > 0) {
     adv = RcAdvance{rc_ctl_, detached ? next_ring_tail() : cur_ring_tail(), ring_cap_ - 1,
-                    rc_adv_w_};
+                    rc_adv_w_, ring_, claim_ptr(), cfg_.log_bytes};
     rc_adv_w_ = 0;
   }
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
@@ -3888,6 +3931,19 @@ std::vector<uint64_t> HbmCache::debug_bucket(uint64_t b) {
     for (uint64_t w : {x.d0, x.d1, x.loc, (uint64_t)x.vlen | ((uint64_t)x.expire << 32)})
       out.push_back(w);
   return out;
+}
+
+std::vector<uint64_t> HbmCache::debug_hand() {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  HIP_OK(hipDeviceSynchronize());
+  uint64_t hand = 0, tail = 0, head = 0, loc = ~0ull;
+  if (rc_ctl_) HIP_OK(hipMemcpy(&hand, rc_ctl_, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&tail, cur_ring_tail(), 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&head, cur_head(), 8, hipMemcpyDeviceToHost));
+  if (ring_ && tail > hand && tail - hand <= ring_cap_)
+    HIP_OK(hipMemcpy(&loc, ring_ + (hand & (ring_cap_ - 1)), 8, hipMemcpyDeviceToHost));
+  return {hand, tail, head, loc};
 }
 
 void HbmCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,

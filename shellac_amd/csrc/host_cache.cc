@@ -191,8 +191,10 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
   const int64_t w = hand_window(n);
   const uint64_t rcap = ring_.size(), rmask = rcap - 1;
   const uint64_t avail = ring_tail_ - hand_;
-  const uint64_t weff = std::min<uint64_t>((uint64_t)w, avail);
-  struct Hot { int64_t j; uint64_t loc, h, hx; };
+  // the adaptive window (layout.h hand_window_eff) and the reinsertion count cap
+  const uint64_t weff = std::min<uint64_t>((uint64_t)hand_window_eff(n, hand_consumed_), avail);
+  const uint64_t cmax = (uint64_t)(w - n);
+  struct Hot { int64_t j; uint64_t loc, h, hx, c; };  // c: hot entries before it
   std::vector<Hot> hot;
   uint64_t hx = 0, consumed = weff;
   // lead mode: the hand's lead and a pick's safety bound (HbmCache k_rc_emit's rules)
@@ -218,13 +220,13 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
         if (e.loc == l + 1 && (e.vlen & kRefBit) && (e.expire == 0 || e.expire > now))
           hb = item_bytes(h.vlen);
       }
-    if (hb) hot.push_back(Hot{(int64_t)j, l, hb, hx});
+    if (hb) hot.push_back(Hot{(int64_t)j, l, hb, hx, (uint64_t)hot.size()});
     hx += hb;
   }
   out->clear();
   uint64_t staged = 0;
   auto picked = [&](const Hot& t) {
-    return (uint64_t)t.j < consumed && t.hx + t.h <= rmax &&
+    return (uint64_t)t.j < consumed && t.hx + t.h <= rmax && t.c < cmax &&
            (!lead_mode || t.loc + log_bytes_ >= head_ + bytes + rmax);
   };
   for (const Hot& t : hot)
@@ -242,7 +244,21 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
     ctr_.reinsert_bytes += h.vlen;
   }
   hand_ += consumed;
+  hand_consumed_ = consumed;
   if (ring_tail_ - hand_ > rcap) hand_ = ring_tail_ - rcap;
+  // behind the overwrite: jump to the first entry it has not reached (rc_advance's rule)
+  auto over = [&](uint64_t idx) {
+    const uint64_t l = ring_[idx & rmask];
+    return l != kRingSkip && head_ > l + log_bytes_;
+  };
+  if (hand_ < ring_tail_ && over(hand_)) {
+    uint64_t lo = hand_ + 1, hi = ring_tail_;
+    while (lo < hi) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if (over(mid)) lo = mid + 1; else hi = mid;
+    }
+    hand_ = lo;
+  }
 }
 
 void HostCache::store_rows_locked(const std::vector<Row>& rows, uint32_t now) {
@@ -415,7 +431,7 @@ void HostCache::load(const std::string& path, uint64_t user[4]) {
   std::fclose(f);
   SH_CHECK(ok, "snapshot truncated: " + path);
   head_ = h.head;
-  ring_tail_ = hand_ = 0;  // the CLOCK ring is not part of a snapshot (first lap FIFO)
+  ring_tail_ = hand_ = hand_consumed_ = 0;  // the CLOCK ring is not part of a snapshot (first lap FIFO)
   if (user)
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }

@@ -87,6 +87,7 @@ class HostCache {
   uint64_t rmax_ = 0;
   std::vector<uint64_t> ring_;  // item starts in log order (kRingSkip holes)
   uint64_t ring_tail_ = 0, hand_ = 0;
+  uint64_t hand_consumed_ = 0;  // entries the hand consumed last batch (adaptive window)
 };
 
 // CPU versions of the device batch helpers (same contracts as hbm_cache.h).

@@ -103,10 +103,27 @@ inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
 // ms with the same hit ratio and reinsertions (profiles/archive/r2_hand_window_ab.log); the
 // evict_sim hit ratios are identical for k = 2, 3, 4; k = 1 does not cover the batch's own
 // bytes and degrades to FIFO.
+// Adaptive window: the hand must pass every item the overwrite reaches, i.e. the items a
+// step appended one lap earlier (its SETs + its reinsertions). When a read-heavy step
+// reinserts more items than its batch holds, 2n + 256 entries fall behind; behind the
+// overwrite the hand can no longer give second chances and every referenced object ages
+// out (the host twin: hit ratio 0.43 instead of 0.77 at 2x the log, hot objects lost). So
+// the window holds up to kHandWindowMaxK * n + 256 rows, of which the hand examines
+//     W_eff = min(W, max(2n + 256, 1.25 x (entries it consumed last batch) + 256))
+// (hand_window_eff; the rest are skip rows without reads), and reinsertions are capped at
+// W - n items per batch, so the items a batch appends stay within the window a lap later.
 constexpr int64_t kHandWindowK = 2;
-inline int64_t hand_window(int64_t n) {
-  const int64_t w = kHandWindowK * n + 256;
+constexpr int64_t kHandWindowMaxK = 3;
+SH_HD int64_t hand_window(int64_t n) {  // the rows of the window (allocation, launch)
+  const int64_t w = kHandWindowMaxK * n + 256;
   return w < (1 << 20) ? w : (1 << 20);
+}
+SH_HD int64_t hand_window_eff(int64_t n, uint64_t consumed_last) {
+  const int64_t w = hand_window(n);
+  int64_t e = kHandWindowK * n + 256;
+  const uint64_t want = consumed_last + consumed_last / 4 + 256;
+  if ((uint64_t)e < want) e = want > (uint64_t)w ? w : (int64_t)want;
+  return e < w ? e : w;
 }
 // Whether the hand runs ahead of the overwrite (lead mode, HbmCache k_rc_emit): on a log of
 // at least 16 x (the batch's byte bound + the reinsertion budget). Both engines decide the

@@ -187,3 +187,65 @@ def test_clock_lead_mode_gpu_matches_host(cuda_dev):
     g, _ = _lead_trace(cuda_dev)
     h, _ = _lead_trace("cpu")
     assert g == h and g["reinserted"] > 0
+
+
+def _read_heavy_trace(dev):
+    """A read-heavy shard (each step's Zipf GETs touch 1/4 of the key space, its SET batch
+    1/250 of it; working set 2x the log): the hand must pass more items per batch than the
+    batch holds (the reinsertions a lap earlier). With a window of 2n + 256 entries it fell
+    behind the overwrite, could give no more second chances, and lost even objects read
+    every step (hit ratio 0.63, all 16 hot objects gone). Hot objects are stored once and
+    never SET again, as a replica of another shard's object is."""
+    from shellac_amd.bench.workload import Workload
+
+    K, G, S, steps = 100000, 25000, 400, 200
+    wl = Workload(K, torch.device("cpu"))
+    ib = 32 + ((wl.vlen.long() + 15) & ~15)
+    log = int(int(ib.sum()) / 2.0) // 16 * 16
+    nb = 1
+    while nb < K:
+        nb *= 2
+    sh = CacheShard(log, nb, max_item=1 << 20, device=torch.device(dev))
+    hot = wl.rank_to_id[:16]
+    ishot = torch.zeros(K, dtype=torch.bool)
+    ishot[hot] = True
+
+    def put(ids, bound=None):
+        # the exact byte bound (the default assumes the whole 64 MB payload pool is stored,
+        # more than half this log)
+        b = wl.set_batch(ids)
+        if bound is None:
+            bound = int((32 + ((wl.vlen[ids].long() + 15) & ~15)).sum())
+        sh.store(*(None if x is None else x.to(dev) for x in
+                   (b.keys, b.values, b.val_off, b.vlen, b.flags, b.expire)), bytes_bound=bound)
+
+    for s0 in range(0, K, 4000):
+        put(torch.arange(s0, min(K, s0 + 4000)))
+    put(hot)
+    hits = []
+    for st in range(steps):
+        ids = wl.sample_ids(G, 1000 + st)
+        u = wl.uniform_ids(S, 5000 + st)
+        u = u[~ishot[u]]
+        bb = int((32 + ((wl.vlen[u].long() + 15) & ~15)).sum())
+        lk = sh.lookup(wl.digests.index_select(0, ids).to(dev),
+                       reserve_bytes=bb + sh._impl.reinsert_max)
+        hits.append(int((lk.size[:G] > 0).sum()))
+        put(u, bb)
+    present = int((sh.lookup(wl.digests.index_select(0, hot).to(dev)).size[:16] > 0).sum())
+    return hits, present, sh.counters(), G
+
+
+def test_clock_read_heavy_keeps_hot_objects_host():
+    hits, present, c, G = _read_heavy_trace("cpu")
+    assert present == 16
+    assert sum(hits[120:]) / (80 * G) > 0.72, sum(hits[120:]) / (80 * G)
+    assert c["reinserted"] > 0
+
+
+@pytest.mark.gpu
+def test_clock_read_heavy_gpu_matches_host(cuda_dev):
+    g = _read_heavy_trace(cuda_dev)
+    h = _read_heavy_trace("cpu")
+    assert g[0] == h[0] and g[1] == h[1] == 16
+    assert g[2]["reinserted"] == h[2]["reinserted"] and g[2]["reinsert_bytes"] == h[2]["reinsert_bytes"]
