@@ -2489,7 +2489,13 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
       }
     }
   }
-  if (j < a.W) {
+  if (j >= weff && j < a.W) {
+    // a row past the effective window: a skip row (the SET chain reads nothing else of a
+    // row whose vlen says skip)
+    rc_loc[j] = kRingSkip;
+    rc_h[j] = 0;
+    cb.vlen[j] = kSkipVlen;
+  } else if (j < a.W) {
     rc_loc[j] = loc;
     rc_h[j] = h;
     // a hot entry's row from the header just read (k_rc_emit fills in its value pointer
@@ -2526,6 +2532,9 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
                                                     CacheCounters* __restrict__ ctr) {
   __shared__ unsigned long long s_w[kBlock / 64];
   __shared__ unsigned long long s_pre;
+  // lead mode: a workgroup wholly past the entries the hand examined (k_rc_scan's count)
+  // has nothing to pick, cut or plan (its rows are skip rows already)
+  if (a.lead_mode && (uint64_t)blockIdx.x * kBlock >= a.ctl[3]) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long pre = 0;
   for (unsigned b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += part_h[b];
