@@ -380,7 +380,8 @@ class HbmCache {
                          hipEvent_t append_after, hipEvent_t append_done);
   void store_index_locked(const Digest* keys, const uint32_t* vlen, const uint32_t* expire,
                           int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after,
-                          const uint64_t* from = nullptr, int64_t nmove = 0);
+                          const uint64_t* from = nullptr, int64_t nmove = 0,
+                          int win_parity = -1);
 };
 
 // ---- Generic device kernels used by the distributed serving path ----------------

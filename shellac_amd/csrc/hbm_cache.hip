@@ -1915,7 +1915,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     const uint64_t* __restrict__ head_ptr, uint64_t* __restrict__ head_next, uint64_t cap,
     uint32_t now, const uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ dd_keys,
     int* __restrict__ dd_win, CacheCounters* __restrict__ ctr, uint32_t* __restrict__ claim,
-    const uint64_t* __restrict__ from, int64_t r0, int64_t r1) {
+    const uint64_t* __restrict__ from, int64_t r0, int64_t r1,
+    const unsigned long long* __restrict__ r1_dev) {
+  // r1_dev: the combined batch's effective hand window (rows past it are skip rows)
+  if (r1_dev && (int64_t)*r1_dev < r1) r1 = (int64_t)*r1_dev;
   const int l4 = threadIdx.x & 3;
   const int gbase = threadIdx.x & 60;  // this group's first lane within the wave
   const uint64_t base = *head_ptr;
@@ -2132,6 +2135,9 @@ __global__ __launch_bounds__(kBlock) void k_set_fixup(
   unsigned long long evicted = 0, lost = 0, bytes = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
+    // a row that stored nothing claimed nothing (and past a hand's effective window
+    // k_set_index did not reset its claim word)
+    if (!size[i]) continue;
     uint32_t c = claim[i];
     if (c == kClaimDeferred) {
       claim[i] = ~0u;
@@ -2392,10 +2398,12 @@ struct RcArgs {
   uint64_t rmask;
   const uint64_t* ring_tail;  // the last batch whose ring entries are written (see store)
   // [0] hand, [1] batch bytes B, [2] first meeting entry, [3] scanned, [4] entries the last
-  // batch consumed (the adaptive window, layout.h hand_window_eff)
+  // batch consumed (the adaptive window, layout.h hand_window_eff), [5 + parity] the effective
+  // window of the batch in hand buffer `parity` (its index pass stops there)
   unsigned long long* ctl;
   int64_t W;      // the window's rows
   int64_t n_new;  // the batch's rows (the window's base 2n + 256; reinsertions <= W - n)
+  int parity;     // the hand buffer's: ctl[5 + parity] = this batch's effective window
   const uint64_t* head_ptr;  // the claim word: the head the queued appends will reach
   uint64_t cap;
   uint32_t now;
@@ -2450,7 +2458,10 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
   // the previous one; rows past the effective window are skip rows): the advance consumes
   // at most these
   const int64_t weff = hand_window_eff(a.n_new, a.ctl[4]);
-  if (j == 0) a.ctl[3] = (uint64_t)weff < avail ? (uint64_t)weff : avail;
+  if (j == 0) {
+    a.ctl[3] = (uint64_t)weff < avail ? (uint64_t)weff : avail;
+    a.ctl[5 + a.parity] = (unsigned long long)weff;
+  }
   uint64_t loc = kRingSkip, h = 0;
   uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
   if (j < weff && (uint64_t)j < avail) {
@@ -2491,9 +2502,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
   }
   if (j >= weff && j < a.W) {
     // a row past the effective window: a skip row (the SET chain reads nothing else of a
-    // row whose vlen says skip)
-    rc_loc[j] = kRingSkip;
-    rc_h[j] = 0;
+    // row whose vlen says skip; k_rc_emit reads no rc_loc / rc_h past the examined entries)
     cb.vlen[j] = kSkipVlen;
   } else if (j < a.W) {
     rc_loc[j] = loc;
@@ -2544,7 +2553,8 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
   if (threadIdx.x == 0) s_pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
   __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t h = j < a.W ? rc_h[j] : 0;
+  const bool examined = j < a.W && (uint64_t)j < a.ctl[3];
+  const uint64_t h = examined ? rc_h[j] : 0;
   const unsigned long long hp = h ? h + kRcCount : 0ull;  // bytes | hot entries << 43
   unsigned long long inc = hp;
 #pragma unroll
@@ -2562,7 +2572,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_emit(RcArgs a, RcBatch cb,
   bool meets = false;
   unsigned long long nre = 0, bre = 0;
   if (j < a.W) {
-    const uint64_t loc = rc_loc[j];
+    const uint64_t loc = examined ? rc_loc[j] : kRingSkip;
     const uint64_t r = hx < a.rmax ? hx : a.rmax;
     const uint64_t head = *a.head_ptr, bb = a.ctl[1];
     const uint64_t lead = a.lead_mode ? a.rmax + bb + (bb >> 2) : 0;
@@ -3242,7 +3252,7 @@ void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const u
   // previous batch's fixup writes its ring entries and tail, so it reads the tail of the
   // batch before that one (the other ping-pong slot), whose entries are written.
   RcArgs a{ring_, ring_cap_ - 1, detached ? next_ring_tail() : cur_ring_tail(), rc_ctl_, w, n,
-           claim_ptr(), cfg_.log_bytes, now, rmax, lead ? 1ull : 0ull};
+           hand_b_, claim_ptr(), cfg_.log_bytes, now, rmax, lead ? 1ull : 0ull};
   const int g = (int)((w + kBlock - 1) / kBlock);
   const HandBuf& hb = hb_[hand_b_];
   const RcBatch cb{hb.keys, hb.voff, hb.vlen, hb.flags, hb.expire, hb.from};
@@ -3667,7 +3677,8 @@ void HbmCache::store_tail_locked(uint32_t now, hipStream_t s, hipEvent_t index_a
                     p.expire, cur_head(), cfg_.log_bytes);
   HIP_OK(hipGetLastError());
   if (append_done) HIP_OK(hipEventRecord(append_done, s));
-  store_index_locked(p.keys, p.vlen, p.expire, p.rows, now, s, index_after, p.from, p.nmove);
+  store_index_locked(p.keys, p.vlen, p.expire, p.rows, now, s, index_after, p.from, p.nmove,
+                     p.nmove ? p.parity : -1);
   hsel_ ^= 1;  // later operations on the stream read the published slot
 }
 
@@ -3718,7 +3729,8 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
 
 void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
                                   const uint32_t* expire, int64_t n, uint32_t now, hipStream_t s,
-                                  hipEvent_t index_after, const uint64_t* from, int64_t nmove) {
+                                  hipEvent_t index_after, const uint64_t* from, int64_t nmove,
+                                  int win_parity) {
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
   // A combined batch's reinsertions (rows [0, nmove), moves) land in a launch of their own
@@ -3733,7 +3745,8 @@ void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
     hipLaunchKernelGGL(k_set_index, dim3(igrid), dim3(kBlock), 0, s, keys, n, set_size_, set_off_,
                        vlen, expire, index_, cfg_.nbuckets - 1, cur_head(), next_head(),
                        cfg_.log_bytes, now, dd_slot_, (unsigned long long*)dd_keys_, dd_win_,
-                       ctr_, set_claim_, pass ? (const uint64_t*)nullptr : from, r0, r1);
+                       ctr_, set_claim_, pass ? (const uint64_t*)nullptr : from, r0, r1,
+                       pass || win_parity < 0 ? nullptr : rc_ctl_ + 5 + win_parity);
   }
   hipLaunchKernelGGL(k_set_fixup, dim3(grid_for(n, kBlock, kMaxGrid)), dim3(kBlock), 0, s, keys, n,
                      set_off_, vlen, expire, cur_head(), set_claim_, index_, set_size_, ring_,
