@@ -5,9 +5,11 @@
 # tracing). `bash scripts/trace_bench.sh [bench args]`
 set -eu
 cd /tmp && export TMPDIR=/tmp
+# (the tree to trace: TRACE_TREE, default the repo root; the output always lands under the
+# repo root's gpurun_out, which gpurun copies back)
 OUT="${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/${TRACE_OUT:-trace}"
 mkdir -p "$OUT"
-cd "${GRAFT_REPO_ROOT:-/root/repo}"
+cd "${TRACE_TREE:-${GRAFT_REPO_ROOT:-/root/repo}}"
 export SHELLAC_TRACE=1
 EXTRA=""
 if [ "${HIP_TRACE:-0}" = 1 ]; then EXTRA="--hip-trace"; fi
