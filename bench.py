@@ -1000,11 +1000,12 @@ def main():
             if host_route:
                 extra = (f" owners {owner_of.index_select(0, top).tolist()} GET ranks "
                          f"{spread.route_gets(d).tolist()}")
-            hand, tail, head, hloc = f_shard._impl.debug_hand()
+            hand, tail, head, hloc, *rest = f_shard._impl.debug_hand()
             lag = (hloc - (head - f_log)) / 2**20 if hloc != 2**64 - 1 else None
             log(rank, f"[debug] {when}: top-16 present {(sz > 0).int().tolist()}{extra}; hand "
                       f"{tail - hand} entries behind the ring tail, its item {lag} MiB past "
-                      f"the overwrite point")
+                      f"the overwrite point; consumed / windows {rest}; reinserted "
+                      f"{f_shard.counters()['reinserted']}")
 
         debug_hot("after populate")
         ffill = fill_to_wrap(f_sc, f_shard, f_log, fbase, per_step)
@@ -1012,7 +1013,7 @@ def main():
         if ffill is not None and ffill < min_fill:
             for i in range(ffill, min_fill):
                 serve_i(f_sc, fbase + i)
-                if i % 64 == 0:
+                if i % 64 == 0 or (os.environ.get("SHELLAC_BENCH_DEBUG_HOT") == "2" and i < 24):
                     debug_hot(f"fill step {i}")
             sync()
             ffill = min_fill

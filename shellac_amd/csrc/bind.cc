@@ -361,6 +361,7 @@ PYBIND11_MODULE(_shellac_core, m) {
       })
       .def("flush", &HostCache::flush)
       .def("debug_bucket", &HostCache::debug_bucket)
+      .def("debug_hand", &HostCache::debug_hand)
       .def("debug_set_entry", &HostCache::debug_set_entry)
       .def("export_keys", [](HostCache& c, uintptr_t out, uint64_t cap, uint32_t now) {
         return c.export_keys(P<Digest>(out), cap, now);

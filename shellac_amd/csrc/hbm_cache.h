@@ -239,7 +239,8 @@ class HbmCache {
   // << 32}), synchronously. Builds index states no API call produces in a fixed order
   // (e.g. a dead same-digest entry in a key's first bucket beside its live one).
   std::vector<uint64_t> debug_bucket(uint64_t b);
-  // {hand (ring index), ring tail, head, the log offset of the hand's item (~0: none)}
+  // {hand (ring index), ring tail, head, the log offset of the hand's item (~0: none), entries
+  // the hand consumed last batch, the effective windows of hand buffers 0 and 1}
   std::vector<uint64_t> debug_hand();
   void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
                        uint32_t vlen, uint32_t expire);

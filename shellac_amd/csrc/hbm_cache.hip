@@ -3965,7 +3965,9 @@ std::vector<uint64_t> HbmCache::debug_hand() {
   HIP_OK(hipMemcpy(&head, cur_head(), 8, hipMemcpyDeviceToHost));
   if (ring_ && tail > hand && tail - hand <= ring_cap_)
     HIP_OK(hipMemcpy(&loc, ring_ + (hand & (ring_cap_ - 1)), 8, hipMemcpyDeviceToHost));
-  return {hand, tail, head, loc};
+  unsigned long long ctl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rc_ctl_) HIP_OK(hipMemcpy(ctl, rc_ctl_, sizeof ctl, hipMemcpyDeviceToHost));
+  return {hand, tail, head, loc, ctl[4], ctl[5], ctl[6]};
 }
 
 void HbmCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,

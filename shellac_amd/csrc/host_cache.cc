@@ -436,6 +436,14 @@ void HostCache::load(const std::string& path, uint64_t user[4]) {
     for (int i = 0; i < 4; ++i) user[i] = h.user[i];
 }
 
+std::vector<uint64_t> HostCache::debug_hand() {
+  std::lock_guard<std::mutex> lk(mu_);
+  const uint64_t rcap = ring_.size();
+  const uint64_t loc = rcap && ring_tail_ > hand_ && ring_tail_ - hand_ <= rcap
+                           ? ring_[hand_ & (rcap - 1)] : ~0ull;
+  return {hand_, ring_tail_, head_, loc};
+}
+
 std::vector<uint64_t> HostCache::debug_bucket(uint64_t b) {
   std::lock_guard<std::mutex> lk(mu_);
   SH_CHECK(b < nbuckets_, "bucket out of range");

@@ -34,6 +34,8 @@ class HostCache {
   void flush();
   // Tests: see HbmCache::debug_bucket / debug_set_entry.
   std::vector<uint64_t> debug_bucket(uint64_t b);
+  // {hand (ring index), ring tail, head, the log offset of the hand's item (~0: none)}
+  std::vector<uint64_t> debug_hand();
   void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
                        uint32_t vlen, uint32_t expire);
   uint64_t export_keys(Digest* out, uint64_t out_cap, uint32_t now);

@@ -144,3 +144,28 @@ def test_bench_host_routed_ranks_on_one_gpu():
     assert out["log_fresh"]["owner_hit_ratio"] == 1.0
     assert "check: 0 mismatches in 200 sampled GETs" in p.stderr
     assert " 0 of " in p.stderr and "hit records name another key" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_pooled_capacity_mode_on_one_gpu():
+    """scripts/pooled_capacity.sh's mode, smaller: a fixed total key space (--keys-total) over a
+    simulated 2-rank host-routed job, a 4 GiB shard log half the rank's working set (large
+    enough for the hand's lead mode, layout.h hand_lead, as the bench's logs), SETs walking
+    every key and fresh GET batches (--set-walk): evictions miss some requests, the replicas
+    of spread hot objects stay (they are read every step), --check clean."""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"),
+                        "--simulate-world", "2", "--route", "host", "--keys-total", str(16 << 20),
+                        "--pressured-gb", "4", "--log-gb", "2", "--set-walk",
+                        "--walk-get-batches", "32", "--overfull-fill", "0", "--check",
+                        "--steps", "3", "--warmup", "1", "--no-uncoalesced", "--no-smoke"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    pr = out["log_pressured"]
+    assert out["config"]["keys_total"] == 16 << 20
+    assert pr["working_set_over_capacity"] > 1.5
+    assert pr["get_batches_cycled"] == 32 and pr["set_batches_cycled"] >= 120
+    # a cache holding half the keys: some misses, but the Zipf head (hot replicas included)
+    # stays resident (0.67 when the CLOCK hand fell behind the overwrite and lost them)
+    assert 0.85 < pr["request_hit_ratio"] < 1.0, pr
+    assert "check: 0 mismatches in 200 sampled GETs" in p.stderr
