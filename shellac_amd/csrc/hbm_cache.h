@@ -279,6 +279,7 @@ class HbmCache {
   uint64_t* ring_ = nullptr;           // item-start ring (logical locs, kRingSkip holes)
   uint64_t ring_cap_ = 0;
   unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, entries scanned
+  bool lead_ = false;  // the hand's mode (layout.h hand_lead, sticky; HostCache keeps the same)
   uint64_t rmax_ = 0;
   int64_t rc_cap_ = 0;
   uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr, *rc_hx_ = nullptr;

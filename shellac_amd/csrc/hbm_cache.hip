@@ -3608,6 +3608,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   // the CLOCK hand's reinsertions share the half-log bound with the batch
   const uint64_t rmax = std::min<uint64_t>(rmax_, cfg_.log_bytes / 2 - bytes_bound) / 16 * 16;
   const bool hand = allow_reclaim && rmax && should_reclaim(bytes_bound);
+  lead_ = hand_lead(cfg_.log_bytes, bytes_bound, rmax, lead_);  // every batch, as HostCache
   if (!hand && phase == 0 && n <= kSmallSetRows && !index_after && !append_after &&
       !append_done && !plan_done) {
     // one launch for the whole chain (the proxy's small SET batches)
@@ -3635,7 +3636,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     ensure_cb(hand_b_, w + n, s);
     ensure_set_ws(w + n, s);
     reclaim_locked(keys, values, val_off, vlen, flags, expire, n, w, rmax, now, s, detached,
-                   hand_lead(cfg_.log_bytes, bytes_bound, rmax));
+                   lead_);
     // combined batch: reinsertions first (log order), then the batch (its SETs win)
     const HandBuf& hb = hb_[hand_b_];
     p.rows = w + n;

@@ -175,8 +175,8 @@ void HostCache::store(const Digest* keys, const uint8_t* values, const uint64_t*
     SH_CHECK(bound <= log_bytes_ / 2, "SET batch larger than half the log; split the batch");
     const uint64_t rmax = std::min<uint64_t>(rmax_, log_bytes_ / 2 - bound) / 16 * 16;
     // the device's combined batch: reinsertions (in log order) ahead of the batch
-    if (rmax)
-      reclaim_locked(n, bytes, rmax, now, &rows, &stage, hand_lead(log_bytes_, bound, rmax));
+    lead_ = hand_lead(log_bytes_, bound, rmax, lead_);  // every batch (sticky), as HbmCache
+    if (rmax) reclaim_locked(n, bytes, rmax, now, &rows, &stage, lead_);
   }
   rows.reserve(rows.size() + (size_t)n);
   for (int64_t i = 0; i < n; ++i)

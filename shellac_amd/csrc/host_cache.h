@@ -90,6 +90,7 @@ class HostCache {
   std::vector<uint64_t> ring_;  // item starts in log order (kRingSkip holes)
   uint64_t ring_tail_ = 0, hand_ = 0;
   uint64_t hand_consumed_ = 0;  // entries the hand consumed last batch (adaptive window)
+  bool lead_ = false;  // the hand's mode (layout.h hand_lead, sticky)
 };
 
 // CPU versions of the device batch helpers (same contracts as hbm_cache.h).

@@ -128,8 +128,13 @@ SH_HD int64_t hand_window_eff(int64_t n, uint64_t consumed_last) {
 // Whether the hand runs ahead of the overwrite (lead mode, HbmCache k_rc_emit): on a log of
 // at least 16 x (the batch's byte bound + the reinsertion budget). Both engines decide the
 // same way from the same bound.
-inline bool hand_lead(uint64_t log_bytes, uint64_t bytes_bound, uint64_t rmax) {
-  return log_bytes >= 16 * (bytes_bound + rmax);
+// The decision is sticky (`prev`: the last batch's): a batch bound that straddles the
+// threshold flipped the mode from batch to batch, and each switch into lead mode drops the
+// referenced items the hand then finds too close to the overwrite to copy (host twin, working
+// set 2x the log: hit ratio 0.40 against 0.86). Lead mode is left below 12x.
+inline bool hand_lead(uint64_t log_bytes, uint64_t bytes_bound, uint64_t rmax,
+                      bool prev = false) {
+  return log_bytes >= (prev ? 12 : 16) * (bytes_bound + rmax);
 }
 inline uint64_t ring_entries(uint64_t nbuckets) {
   uint64_t r = 4096;
