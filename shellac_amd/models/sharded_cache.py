@@ -1160,7 +1160,11 @@ class ShardedCache:
         n = batch.keys.shape[0]
         self._stats["set_requests"] += n
         if not self.routed:
-            self.shard.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
+            vlen = batch.vlen
+            if if_absent and n:
+                have = self.shard.lookup(batch.keys.contiguous(), now).size[:n] > 0
+                vlen = torch.where(have, torch.full_like(vlen, SKIP_VLEN), vlen).contiguous()
+            self.shard.store(batch.keys, batch.values, batch.val_off, vlen, batch.flags,
                              batch.expire, now)
             return
         dev, w = self.device, self.world

@@ -170,15 +170,22 @@ class HotSpread:
     def plan(self, sample: torch.Tensor, k: int, policy: str = "designate",
              spray_above: Optional[float] = None) -> dict:
         """Pick the hot set (top ``k`` of an observed GET sample) and how its GETs are
-        spread, from the same sample. ``policy="designate"``: greedy designation (hottest
-        first, each to the rank with the least load so far, starting from the non-hot owner
-        loads); objects above ``spray_above`` of the traffic (default 1/(4N)) are sprayed
-        evenly. ``policy="spray"``: every hot object sprayed, water-filled weights. Returns
-        the sample's shares and the planned per-rank load."""
+        spread, from the same sample, and install it. ``policy="designate"``: greedy
+        designation (hottest first, each to the rank with the least load so far, starting
+        from the non-hot owner loads); objects above ``spray_above`` of the traffic (default
+        1/(4N)) are sprayed evenly. ``policy="spray"``: every hot object sprayed, water-filled
+        weights. Returns the sample's shares and the planned per-rank load."""
+        hot, ranks, w, info = self.design(sample, k, policy, spray_above)
+        self.set_hot(hot, ranks, w)
+        return info
+
+    def design(self, sample: torch.Tensor, k: int, policy: str = "designate",
+               spray_above: Optional[float] = None):
+        """``plan`` without installing: (hot digests hottest first or None, designated ranks
+        (None: all sprayed), spray weights, info)."""
         n = max(sample.shape[0], 1)
         if k <= 0 or sample.shape[0] == 0:
-            self.set_hot(None)
-            return {"hot_share": 0.0}
+            return None, None, None, {"hot_share": 0.0}
         ulo, inv, cnt = torch.unique(sample[:, 0].contiguous(), return_inverse=True,
                                      return_counts=True)
         uniq = torch.empty((ulo.numel(), 2), dtype=torch.int64, device=sample.device)
@@ -191,8 +198,8 @@ class HotSpread:
         hshare = float(hmask.float().mean())
         if policy == "spray":
             w = water_fill((owner_load / n).tolist(), hshare)
-            self.set_hot(hot, None, w)
-            return {"hot_share": hshare, "owner_share": (owner_load / n).tolist(), "weights": w}
+            return hot, None, w, {"hot_share": hshare, "owner_share": (owner_load / n).tolist(),
+                                  "weights": w}
         if policy != "designate":
             raise ValueError(f"unknown spreading policy {policy!r}")
         thr = (spray_above if spray_above is not None else 1.0 / (4 * self.world)) * n
@@ -215,10 +222,10 @@ class HotSpread:
             heapq.heappush(heap, (lr + c, r))
         for lr, r in heap:
             load[r] = lr
-        self.set_hot(hot, torch.tensor(ranks, dtype=torch.int32), [1.0] * self.world)
-        return {"hot_share": hshare, "owner_share": (owner_load / n).tolist(),
-                "sprayed_objects": sum(1 for r in ranks if r < 0),
-                "planned_load": [x / n for x in load]}
+        return hot, torch.tensor(ranks, dtype=torch.int32), [1.0] * self.world, {
+            "hot_share": hshare, "owner_share": (owner_load / n).tolist(),
+            "sprayed_objects": sum(1 for r in ranks if r < 0),
+            "planned_load": [x / n for x in load]}
 
     def set_hot(self, hot: Optional[torch.Tensor], ranks: Optional[torch.Tensor] = None,
                 weights: Optional[Sequence[float]] = None):
@@ -265,12 +272,14 @@ class HotSpread:
 
 
 def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, world: int,
-                  group=None, now: Optional[int] = None) -> int:
+                  group=None, now: Optional[int] = None, if_absent: bool = False) -> int:
     """Collective: every rank stores, as ordinary objects of its shard, the hot objects it
     does not own, fetched from their owners — each owner looks its hot objects up and
     gathers their records, one all-gather moves them (RCCL over xGMI between GPUs, gloo
     between CPU ranks). ``cache`` is the rank's local (unrouted) ShardedCache, ``owner``
-    the owner rank of each hot digest. Returns the objects this rank stored."""
+    the owner rank of each hot digest. ``if_absent``: a rank keeps a copy it already holds
+    (a write-through SET that landed after the router began writing the object through is
+    newer than the owner's copy read here). Returns the objects this rank stored (fetched)."""
     from ..models.sharded_cache import GetResult, records_to_set_batch
 
     dev = hot.device
@@ -307,7 +316,90 @@ def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, worl
         r = all_rows[p][:cnt].to(dev)
         res = GetResult(all_recs[p].to(dev), r[:, 2].contiguous(), r[:, 3].contiguous())
         sb = records_to_set_batch(r[:, :2].contiguous(), res)
-        cache.set(sb, now)
+        cache.set(sb, now, if_absent=if_absent)
         stored += int((r[:, 3] > 0).sum())
     cache.sync_sets()
     return stored
+
+
+def refresh_hot(cache, spread: HotSpread, sample: torch.Tensor, k: int, rank: int, world: int,
+                group=None, budget_bytes: Optional[int] = None, now: Optional[int] = None,
+                policy: str = "designate") -> dict:
+    """Collective (every rank, the same ``sample`` of the GET stream): move the replicated
+    hot set to the top ``k`` of ``sample`` incrementally — only objects that became hot are
+    fetched, at most ``budget_bytes`` of their records (hottest first; the rest wait for a
+    later refresh), and the replicas of objects that cooled are dropped. Order, so that no GET
+    is ever answered by a stale copy:
+
+    1. the router writes the newly hot objects' SETs through to every rank, their GETs still
+       going to their owners (they are hot, designated to the owner);
+    2. their records are fetched from the owners into the other ranks, insert-if-absent (a
+       SET written through since step 1 is newer than the owner's copy read here);
+    3. the router installs the new hot set and designations (GETs of new objects may now go
+       to any replica; objects that cooled go back to their owners, GETs and SETs);
+    4. replicas of the cooled objects are deleted on the non-owner ranks (no SET reaches them
+       any more: a later promotion must fetch a fresh copy, which insert-if-absent would
+       otherwise refuse).
+
+    ``cache``: this rank's local (unrouted) ShardedCache. Returns counts and fetched bytes."""
+    dev = spread.device
+    old = spread.hot if spread.hot is not None else torch.zeros((0, 2), dtype=torch.int64,
+                                                                  device=dev)
+    old_rank = (spread.hot_rank if spread.hot_rank is not None
+                else torch.zeros(0, dtype=torch.int32, device=dev))
+    new, new_rank, new_w, info = spread.design(sample.to(dev), k, policy)
+    if new is None:
+        new = torch.zeros((0, 2), dtype=torch.int64, device=dev)
+        new_rank = torch.zeros(0, dtype=torch.int32, device=dev)
+    if new_rank is None:
+        new_rank = torch.full((new.shape[0],), -1, dtype=torch.int32, device=dev)
+    new_rank = new_rank.to(dev)
+    old_sorted = old  # (sorted by lo)
+    is_added = ~member(new, old_sorted)
+    added, added_rank = new[is_added], new_rank[is_added]
+    new_sorted = new.index_select(0, torch.argsort(new[:, 0])) if new.shape[0] else new
+    removed = old[~member(old, new_sorted)]
+    owner_added = spread.owners(added).long() if added.shape[0] else torch.zeros(
+        0, dtype=torch.long, device=dev)
+    # the budget, hottest first: record sizes from the owners (an all-reduce of each rank's
+    # sizes of the objects it owns)
+    deferred = 0
+    if budget_bytes is not None and added.shape[0]:
+        sh = cache.shard
+        cache.sync_sets()
+        sz = torch.zeros(added.shape[0], dtype=torch.int64, device=dev)
+        mine = owner_added == rank
+        if bool(mine.any()):
+            lk = sh.lookup(added[mine].contiguous(), now)
+            sz[mine] = lk.size[: int(mine.sum())].to(torch.int64)
+        cdev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+        szc = sz.to(cdev)
+        dist.all_reduce(szc, group=group)
+        # every non-owner rank stores a copy: (world - 1) x the record per object
+        keep = torch.cumsum(szc.to(dev) * (world - 1), 0) <= int(budget_bytes)
+        deferred = int((~keep).sum())
+        added, added_rank, owner_added = added[keep], added_rank[keep], owner_added[keep]
+    kept = new[~is_added]
+    kept_rank = new_rank[~is_added]
+    # 1. write-through for the newly hot objects, their GETs still to their owners
+    spread.set_hot(torch.cat([old, added]),
+                   torch.cat([old_rank.to(dev), owner_added.to(torch.int32)]), spread.weights)
+    # 2. fetch them into the other ranks, insert-if-absent
+    fetched = replicate_hot(cache, added, owner_added, rank, world, group, now, if_absent=True)
+    # 3. the new hot set (objects past the budget stay cold until a later refresh)
+    final = torch.cat([kept, added])
+    final_rank = torch.cat([kept_rank, added_rank])
+    if final.shape[0]:
+        spread.set_hot(final, final_rank, new_w if new_w is not None else spread.weights)
+    else:
+        spread.set_hot(None)
+    # 4. drop the cooled objects' replicas (not on their owners)
+    dropped = 0
+    if removed.shape[0]:
+        gone = removed[spread.owners(removed).long() != rank].contiguous()
+        if gone.shape[0]:
+            dropped = int(cache.delete(gone, now).sum())
+    cache.sync_sets()
+    return {"added": int(added.shape[0]), "deferred": deferred, "removed": int(removed.shape[0]),
+            "replicas_dropped": dropped, "fetched": fetched, "hot": int(final.shape[0]),
+            "hot_share": info.get("hot_share", 0.0)}

@@ -541,3 +541,79 @@ def test_host_routed_true_shares_with_hot_spreading_gloo(world, policy):
     serves exactly its share, every GET of it returns the version the SETs of earlier steps
     left, wherever it was sent, and the ranks' loads stay within a few percent."""
     _run_world(_spread_worker, world, policy)
+
+
+def _spread_refresh_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import torch
+
+        from shellac_amd.bench.workload import Workload
+        from shellac_amd.models.sharded_cache import ShardedCache
+        from shellac_amd.ops.cache import CacheShard, unpack_records
+        from shellac_amd.parallel.exchange import LocalComm
+        from shellac_amd.parallel.hotspread import HotSpread, member, refresh_hot, replicate_hot
+
+        N = 6000 * world
+        wl = Workload(N, "cpu", min_val=16, max_val=512, pool_bytes=1 << 20)
+        hs = HotSpread(world, "cpu")
+        owner = hs.owners(wl.digests).long()
+        sc = ShardedCache(CacheShard(16 << 20, 1 << 14, 1 << 12, "cpu"), group=LocalComm())
+        sc.set(wl.set_batch(torch.nonzero(owner == rank).flatten()))
+        hs.plan(wl.digests[wl.sample_ids(50000, 8)], 200)
+        replicate_hot(sc, hs.hot, hs.owners(hs.hot), rank, world)
+        version = torch.zeros(N, dtype=torch.int64)
+
+        def steps(order, first, count):
+            for step in range(first, first + count):
+                g = wl.sample_ids(4000 * world, 100 + step, rank_to_id=order)
+                gd = hs.route_gets(wl.digests[g], seq0=step * 4000 * world)
+                st = torch.cat([wl.uniform_ids(300 * world, 200 + step),
+                                order[step % 5:400:5]])      # hot (old and new) objects too
+                sd = hs.route_sets(wl.digests[st])
+                mine_g, mine_s = g[gd == rank], st[(sd == rank) | (sd < 0)]
+                r = sc.serve(wl.digests[mine_g].contiguous(),
+                             wl.set_batch(mine_s, version=step + 1))
+                for i, x in zip(mine_g.tolist(), unpack_records(r.data, r.off, r.size)):
+                    assert x is not None, (step, i)
+                    assert x[0] == wl.expected_value(i, int(version[i])), (step, i)
+                version[st] = step + 1
+
+        order0 = wl.rank_to_id
+        steps(order0, 0, 2)
+        old_hot = hs.hot.clone()
+        # the popularity drifts: 120 of the top 200 trade places with tail objects
+        order1 = wl.drifted(order0, 200, 120, 4242)
+        # a budget that admits about half of the newly hot objects' copies
+        info = refresh_hot(sc, hs, wl.digests[wl.sample_ids(50000, 9, rank_to_id=order1)], 200,
+                           rank, world, budget_bytes=60 * 260 * (world - 1))
+        assert info["added"] > 20 and info["deferred"] > 20 and info["removed"] > 20, info
+        # the cooled objects' replicas are gone from the ranks that do not own them
+        cooled = old_hot[~member(old_hot, hs.hot)]
+        not_mine = cooled[hs.owners(cooled).long() != rank]
+        assert int((sc.shard.lookup(not_mine).size[: not_mine.shape[0]] > 0).sum()) == 0
+        steps(order1, 2, 3)
+        # back to the first order: objects demoted above (and SET meanwhile at their owners
+        # only) are promoted again and must be fetched fresh
+        refresh_hot(sc, hs, wl.digests[wl.sample_ids(50000, 10, rank_to_id=order0)], 200,
+                    rank, world)
+        steps(order0, 5, 2)
+        q.put((rank, "ok", 0))
+    except BaseException:
+        import traceback
+
+        q.put((rank, "fail", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_routed_hot_set_refresh_gloo(world):
+    """The host-routed hot set follows a drifting popularity order incrementally
+    (parallel/hotspread.py refresh_hot): only newly hot objects are fetched, within a byte
+    budget (the rest wait), cooled objects' replicas are dropped, and every GET before,
+    after and across two refreshes (one promoting objects demoted earlier, which were SET at
+    their owners meanwhile) returns the version the SETs left."""
+    _run_world(_spread_refresh_worker, world)
