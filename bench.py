@@ -175,6 +175,13 @@ def parse():
                          "popularity, each --drift-steps steps then an incremental replica "
                          "refresh (0 = skip)")
     ap.add_argument("--drift-steps", type=int, default=400)
+    ap.add_argument("--spread-drift-steps", type=int, default=40,
+                    help="spread_drift block (host routing with --spread): steps per epoch of "
+                         "drifted popularity after each incremental hot-set refresh "
+                         "(--drift-epochs epochs; 0 = skip)")
+    ap.add_argument("--spread-drift-swap", type=float, default=0.25,
+                    help="share of the spread hot set whose objects trade places with tail "
+                         "objects every spread_drift epoch")
     ap.add_argument("--drift-swap", type=float, default=0.05,
                     help="share of the replicated top ranks whose objects trade places with "
                          "tail objects every epoch (content cooling, new content heating up)")
@@ -1112,6 +1119,103 @@ def main():
                                   "wrapped": (wrapped, wrapped_iv, None, nfill),
                                   "fresh": (fresh, fresh_iv, None, None)}[headline]
 
+    # secondary (host routing): the spread hot set follows a drifting popularity order, one
+    # incremental refresh per epoch (parallel/hotspread.py refresh_hot: only newly hot objects
+    # fetched, within --drift-budget-mb, cooled replicas dropped), then steps of the drifted
+    # stream routed by the new table
+    def spread_drift():
+        from shellac_amd.parallel.hotspread import refresh_hot
+
+        E, K, PB = args.drift_epochs, args.spread_drift_steps, 4
+        order = wl.rank_to_id
+        swap = max(1, int(args.spread * args.spread_drift_swap))
+        budget = int(args.drift_budget_mb * (1 << 20))
+        fetch = sizes = None
+        if sim:
+            # the simulated rank's peers: their copies are the workload's objects
+            lo_sorted, lo_order = torch.sort(wl.digests[:, 0].contiguous())
+
+            def ids_of(dg):
+                at = torch.searchsorted(lo_sorted, dg[:, 0].contiguous()).clamp_(
+                    max=lo_sorted.numel() - 1)
+                return lo_order.index_select(0, at)
+
+            def fetch(dg, own):
+                ids = ids_of(dg[own.to(dg.device) != me])
+                if ids.numel():
+                    sc.set(wl.set_batch(ids), if_absent=True)
+                return int(ids.numel())
+
+            def sizes(dg):
+                return 32 + ((wl.vlen.index_select(0, ids_of(dg)).long() + 15) & ~15)
+        epochs = []
+        for e in range(1, E + 1):
+            order = wl.drifted(order, args.spread, swap, 5151 + e)   # the same on every rank
+            sample = wl.digests.index_select(0, wl.sample_ids(args.spread_sample, 8800 + e,
+                                                              rank_to_id=order))
+            sc.sync_sets()
+            if real_world > 1:
+                dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            info = refresh_hot(sc, spread, sample, args.spread, me, world, budget_bytes=budget,
+                               fetch=fetch, sizes=sizes)
+            sync()
+            t_ref = time.perf_counter() - t0
+            del sample
+            g_e, s_e = [], []
+            req = torch.zeros(world, dtype=torch.float64, device=dev)
+            for i in range(PB):
+                g = wl.sample_ids(world * args.batch, 7700 + 97 * e + i, rank_to_id=order)
+                gd = spread.route_gets(wl.digests.index_select(0, g), seq0=i * world * args.batch)
+                st = wl.uniform_ids(world * args.sets, 7900 + 97 * e + i)
+                sd = spread.route_sets(wl.digests.index_select(0, st))
+                g_e.append(wl.digests.index_select(0, g[gd == me]).contiguous())
+                s_e.append(wl.set_batch(st[(sd == me) | (sd < 0)].contiguous()))
+                req += (torch.bincount(gd.long(), minlength=world) +
+                        torch.bincount(sd[sd >= 0].long(), minlength=world) +
+                        int((sd < 0).sum())).double()
+                del g, gd, st, sd
+            ev = torch.cuda.Event()
+            ev.record()
+            sc.sync_sets()
+            c0 = shard.counters()
+            if real_world > 1:
+                dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            for i in range(K):
+                sc.serve(g_e[i % PB], s_e[i % PB], inputs_ready=ev)
+            sync()
+            t_steps = time.perf_counter() - t0
+            sc.sync_sets()
+            c1 = shard.counters()
+            hit_n = [0, 0]
+            for i in range(PB):   # what a client sees (untimed)
+                r = sc.serve(g_e[i], s_e[i], inputs_ready=ev).wait()
+                hit_n[0] += int((r.size > 0).sum())
+                hit_n[1] += int(r.size.numel())
+            agg = torch.tensor([t_steps, t_ref], dtype=torch.float64, device=rdev)
+            if real_world > 1:
+                dist.all_reduce(agg, op=dist.ReduceOp.MAX)
+            epochs.append({"ms_per_step": round(float(agg[0]) / K * 1e3, 4),
+                           "refresh_ms": round(float(agg[1]) * 1e3, 1),
+                           "hot_added": info["added"], "hot_deferred": info["deferred"],
+                           "hot_removed": info["removed"],
+                           "replicas_dropped": info["replicas_dropped"],
+                           "rank_share_max_over_mean": round(float(req.max() / req.mean()), 4),
+                           "owner_hit_ratio": round((c1["get_hits"] - c0["get_hits"]) /
+                                                    max(c1["get_ops"] - c0["get_ops"], 1), 4),
+                           "request_hit_ratio": round(hit_n[0] / max(hit_n[1], 1), 4)})
+            del g_e, s_e
+        return {"epochs": E, "steps_per_epoch": K, "hot_objects_replaced_per_epoch": swap,
+                "refresh_budget_mib": args.drift_budget_mb, "per_epoch": epochs}
+
+    sdrift = None
+    if (host_route and args.spread and args.drift_epochs > 0 and args.spread_drift_steps > 0
+            and steady_ok and not bounce):
+        sdrift = spread_drift()
+
     # secondary: a drifting hot set (hot objects replaced every epoch) with the replica tier
     # maintained incrementally between epochs (refresh under a byte budget, no flush)
     drift = None
@@ -1220,6 +1324,8 @@ def main():
         "log_overfull": overfull,
         # a drifting hot set with the replica maintained between epochs (N>1 / simulated)
         "hot_drift": drift,
+        # host routing: the spread hot set refreshed incrementally under drift
+        "spread_drift": sdrift,
         "smoke": sm,
     }
     if host_route and out["host_routing"] and "host_route_req_per_s" in out["host_routing"]:

@@ -324,7 +324,7 @@ def replicate_hot(cache, hot: torch.Tensor, owner: torch.Tensor, rank: int, worl
 
 def refresh_hot(cache, spread: HotSpread, sample: torch.Tensor, k: int, rank: int, world: int,
                 group=None, budget_bytes: Optional[int] = None, now: Optional[int] = None,
-                policy: str = "designate") -> dict:
+                policy: str = "designate", fetch=None, sizes=None) -> dict:
     """Collective (every rank, the same ``sample`` of the GET stream): move the replicated
     hot set to the top ``k`` of ``sample`` incrementally — only objects that became hot are
     fetched, at most ``budget_bytes`` of their records (hottest first; the rest wait for a
@@ -341,7 +341,9 @@ def refresh_hot(cache, spread: HotSpread, sample: torch.Tensor, k: int, rank: in
        any more: a later promotion must fetch a fresh copy, which insert-if-absent would
        otherwise refuse).
 
-    ``cache``: this rank's local (unrouted) ShardedCache. Returns counts and fetched bytes."""
+    ``cache``: this rank's local (unrouted) ShardedCache. ``fetch(digests, owners)`` and
+    ``sizes(digests)`` replace the collectives (a simulated rank, bench.py --simulate-world:
+    its peers' records come from the workload). Returns counts."""
     dev = spread.device
     old = spread.hot if spread.hot is not None else torch.zeros((0, 2), dtype=torch.int64,
                                                                   device=dev)
@@ -365,16 +367,19 @@ def refresh_hot(cache, spread: HotSpread, sample: torch.Tensor, k: int, rank: in
     # sizes of the objects it owns)
     deferred = 0
     if budget_bytes is not None and added.shape[0]:
-        sh = cache.shard
-        cache.sync_sets()
-        sz = torch.zeros(added.shape[0], dtype=torch.int64, device=dev)
-        mine = owner_added == rank
-        if bool(mine.any()):
-            lk = sh.lookup(added[mine].contiguous(), now)
-            sz[mine] = lk.size[: int(mine.sum())].to(torch.int64)
-        cdev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
-        szc = sz.to(cdev)
-        dist.all_reduce(szc, group=group)
+        if sizes is not None:
+            szc = sizes(added).to(torch.int64)
+        else:
+            sh = cache.shard
+            cache.sync_sets()
+            sz = torch.zeros(added.shape[0], dtype=torch.int64, device=dev)
+            mine = owner_added == rank
+            if bool(mine.any()):
+                lk = sh.lookup(added[mine].contiguous(), now)
+                sz[mine] = lk.size[: int(mine.sum())].to(torch.int64)
+            cdev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+            szc = sz.to(cdev)
+            dist.all_reduce(szc, group=group)
         # every non-owner rank stores a copy: (world - 1) x the record per object
         keep = torch.cumsum(szc.to(dev) * (world - 1), 0) <= int(budget_bytes)
         deferred = int((~keep).sum())
@@ -385,7 +390,8 @@ def refresh_hot(cache, spread: HotSpread, sample: torch.Tensor, k: int, rank: in
     spread.set_hot(torch.cat([old, added]),
                    torch.cat([old_rank.to(dev), owner_added.to(torch.int32)]), spread.weights)
     # 2. fetch them into the other ranks, insert-if-absent
-    fetched = replicate_hot(cache, added, owner_added, rank, world, group, now, if_absent=True)
+    fetched = (fetch(added, owner_added) if fetch is not None else
+               replicate_hot(cache, added, owner_added, rank, world, group, now, if_absent=True))
     # 3. the new hot set (objects past the budget stay cold until a later refresh)
     final = torch.cat([kept, added])
     final_rank = torch.cat([kept_rank, added_rank])
