@@ -176,7 +176,7 @@ def parse():
                          "refresh (0 = skip)")
     ap.add_argument("--drift-steps", type=int, default=400)
     ap.add_argument("--spread-drift-steps", type=int, default=40,
-                    help="spread_drift block (host routing with --spread): steps per epoch of "
+                    help="spread_drift block (simulated host-routed world with --spread): steps per epoch of "
                          "drifted popularity after each incremental hot-set refresh "
                          "(--drift-epochs epochs; 0 = skip)")
     ap.add_argument("--spread-drift-swap", type=float, default=0.25,
@@ -1212,8 +1212,10 @@ def main():
                 "refresh_budget_mib": args.drift_budget_mb, "per_epoch": epochs}
 
     sdrift = None
-    if (host_route and args.spread and args.drift_epochs > 0 and args.spread_drift_steps > 0
-            and steady_ok and not bounce):
+    # (simulated worlds only: the real N-rank job's collectives in refresh_hot are covered by
+    # the gloo test, and a secondary block must not put the driver's scaling run at risk)
+    if (host_route and sim and args.spread and args.drift_epochs > 0
+            and args.spread_drift_steps > 0 and steady_ok):
         sdrift = spread_drift()
 
     # secondary: a drifting hot set (hot objects replaced every epoch) with the replica tier
