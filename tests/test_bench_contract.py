@@ -169,3 +169,24 @@ def test_bench_pooled_capacity_mode_on_one_gpu():
     # stays resident (0.67 when the CLOCK hand fell behind the overwrite and lost them)
     assert 0.85 < pr["request_hit_ratio"] < 1.0, pr
     assert "check: 0 mismatches in 200 sampled GETs" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_spread_drift_block_on_one_gpu():
+    """The spread_drift block (simulated host-routed world): each epoch drifts the
+    popularity order, refreshes the spread hot set incrementally (hotspread.refresh_hot) and
+    times steps of the drifted stream; the request shares stay even and every epoch reports
+    what the refresh added and dropped."""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"),
+                        "--simulate-world", "2", "--route", "host", "--keys-per-gpu", str(1 << 20),
+                        "--drift-epochs", "2", "--spread-drift-steps", "4", "--overfull-fill", "0",
+                        "--steps", "3", "--warmup", "1", "--no-uncoalesced", "--no-smoke"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    sd = out["spread_drift"]
+    assert sd is not None and sd["epochs"] == 2 and len(sd["per_epoch"]) == 2
+    for e in sd["per_epoch"]:
+        assert e["hot_added"] > 0 and e["hot_added"] == e["hot_removed"]
+        assert e["rank_share_max_over_mean"] < 1.05
+        assert e["ms_per_step"] > 0 and 0.0 < e["request_hit_ratio"] <= 1.0
