@@ -21,8 +21,15 @@ Per-GPU work is fixed as N grows (weak scaling): the key space is N x --keys-per
 Headline (``--headline pressured``): the full cache — a shard log sized so its working set
 (every key it holds, one record each) fills --pressured-fill (0.8) of it, wrapped, so every
 SET batch's CLOCK hand re-appends the objects read since it last passed and evicts the rest
-(hit ratio < 1). Secondary: the fresh cache (``log_fresh``) and a 16 GiB log that has
-wrapped with the working set at ~1/4 of it (``log_wrapped``).
+(hit ratio < 1). Secondary: the fresh cache (``log_fresh``), a 16 GiB log that has
+wrapped with the working set at ~1/4 of it (``log_wrapped``), and a working set
+--overfull-fill (1.25) times the log (``log_overfull``: its SETs walk every key and its GETs
+come from --walk-get-batches fresh batches, so an evicted key misses until re-SET). The
+full-cache blocks also report ``request_hit_ratio`` (duplicates included, untimed steps).
+Pooled capacity (scripts/pooled_capacity.sh): ``--keys-total`` fixes the key space across N
+and ``--set-walk`` gives the headline block the overfull block's batches. A simulated
+host-routed world also runs ``spread_drift``: the spread hot set refreshed incrementally
+(parallel/hotspread.py refresh_hot) under a drifting popularity order.
 
 Metric: whole-job cache operations per second (GET+SET requests served).
 The reference (kmacrow/Shellac) publishes no numbers, so vs_baseline is null.
