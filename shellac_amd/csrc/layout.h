@@ -109,10 +109,12 @@ inline uint64_t reinsert_budget(uint64_t log_bytes, uint64_t req) {
 // overwrite the hand can no longer give second chances and every referenced object ages
 // out (the host twin: hit ratio 0.43 instead of 0.77 at 2x the log, hot objects lost). So
 // the window holds up to kHandWindowMaxK * n + 256 rows, of which the hand examines
-//     W_eff = min(W, max(2n + 256, 1.25 x (entries it consumed last batch) + 256))
+//     W_eff = min(W, max(1.5n + 256, 1.25 x (entries it consumed last batch) + 256))
+// (a 1.5n base, down from the fixed 2n: the wrapped step -1.5 %, the full cache and the hit
+// ratios unchanged, profiles/r5ar_window_base)
 // (hand_window_eff; the rest are skip rows without reads), and reinsertions are capped at
 // W - n items per batch, so the items a batch appends stay within the window a lap later.
-constexpr int64_t kHandWindowK = 2;
+constexpr int64_t kHandWindowK = 3;     // halves: the base window 1.5 n + 256
 constexpr int64_t kHandWindowMaxK = 3;
 SH_HD int64_t hand_window(int64_t n) {  // the rows of the window (allocation, launch)
   const int64_t w = kHandWindowMaxK * n + 256;
@@ -120,7 +122,7 @@ SH_HD int64_t hand_window(int64_t n) {  // the rows of the window (allocation, l
 }
 SH_HD int64_t hand_window_eff(int64_t n, uint64_t consumed_last) {
   const int64_t w = hand_window(n);
-  int64_t e = kHandWindowK * n + 256;
+  int64_t e = kHandWindowK * n / 2 + 256;
   const uint64_t want = consumed_last + consumed_last / 4 + 256;
   if ((uint64_t)e < want) e = want > (uint64_t)w ? w : (int64_t)want;
   return e < w ? e : w;
