@@ -14,7 +14,7 @@ for n in ${2:-"2 4 8"}; do
       || { echo "$tag failed"; tail -20 "$OUT/$tag.err"; exit 1; }
     python3 -c "
 import json; d=json.load(open('$OUT/$tag.json')); f=d.get('log_fresh') or {}; w=d.get('log_wrapped') or {}; p=d.get('log_pressured') or {}; h=d['host_routing']
-print('$tag rank', h['simulated_rank'], 'share max/mean', h['rank_share_max_over_mean'], d['headline_phase'], d['ms_per_step'], 'lap', p.get('lap_ms_per_step'), 'fresh', f.get('ms_per_step'), 'wrapped', w.get('ms_per_step'), 'hit', d['get_hit_ratio'], 'router', h['host_route_req_per_s'], h['host_route_threads'], 'thr', h['host_route_req_per_s_one_thread'], 'feeds', h.get('router_feeds_job'))"
+print('$tag rank', h['simulated_rank'], 'share max/mean', h['rank_share_max_over_mean'], d['headline_phase'], d['ms_per_step'], 'lap', p.get('lap_ms_per_step'), 'fresh', f.get('ms_per_step'), 'wrapped', w.get('ms_per_step'), 'hit', d['get_hit_ratio'], 'request hit', p.get('request_hit_ratio'), 'router', h['host_route_req_per_s'], h['host_route_threads'], 'thr', h['host_route_req_per_s_one_thread'], 'feeds', h.get('router_feeds_job'))"
     grep "check" "$OUT/$tag.err"
   done
 done
