@@ -295,45 +295,3 @@ def test_clock_lead_mode_is_sticky_host():
     assert present == 16
     assert sum(hits[120:]) / (80 * G) > 0.75, sum(hits[120:]) / (80 * G)
 
-
-@pytest.mark.gpu
-def test_clock_hand_catches_up_after_a_queued_populate_gpu(cuda_dev):
-    """A populate that queues many large stores before the first completes lets them all skip
-    the CLOCK hand (should_reclaim reads the last published head), leaving the hand laps
-    behind the overwrite; it must jump to the overwrite point (hand_catch_up) instead of
-    spending hundreds of batches on overwritten entries while referenced objects age out
-    (profiles/r5aj_capacity). Hot objects stored once after the populate and read every
-    step survive; the hand ends at or past the overwrite point."""
-    from shellac_amd.bench.workload import Workload
-
-    K = 200000
-    wl = Workload(K, torch.device("cpu"))
-    ib = 32 + ((wl.vlen.long() + 15) & ~15)
-    log = int(int(ib.sum()) / 2.0) // 16 * 16
-    nb = 1
-    while nb < K:
-        nb *= 2
-    sh = CacheShard(log, nb, max_item=1 << 20, device=cuda_dev)
-    hot = wl.rank_to_id[:16]
-    ishot = torch.zeros(K, dtype=torch.bool)
-    ishot[hot] = True
-
-    def put(ids):
-        b = wl.set_batch(ids)
-        bound = int((32 + ((wl.vlen[ids].long() + 15) & ~15)).sum())
-        sh.store(*(None if x is None else x.to(cuda_dev) for x in
-                   (b.keys, b.values, b.val_off, b.vlen, b.flags, b.expire)), bytes_bound=bound)
-
-    for s0 in range(0, K, 8000):          # queued back to back: no synchronisation between
-        put(torch.arange(s0, min(K, s0 + 8000)))
-    put(hot)
-    hd = wl.digests.index_select(0, hot).to(cuda_dev)
-    for st in range(60):
-        ids = wl.sample_ids(20000, 1000 + st)
-        sh.lookup(torch.cat([hd, wl.digests.index_select(0, ids).to(cuda_dev)]))
-        u = wl.uniform_ids(800, 5000 + st)
-        put(u[~ishot[u]])
-    torch.cuda.synchronize(cuda_dev)
-    assert int((sh.lookup(hd).size[:16] > 0).sum()) == 16
-    hand, tail, head, loc = sh._impl.debug_hand()[:4]
-    assert loc != 2**64 - 1 and loc + log >= head, (hand, tail, head, loc, log)
