@@ -30,6 +30,7 @@
 
 #include "digest.h"
 #include "host_cache.h"
+#include "host_router.h"
 #include "ketama.h"
 #include "net.h"
 #include "object_cache.h"
@@ -106,6 +107,9 @@ class CacheBackend {
   virtual void direct_attach(Executor* ex) { (void)ex; }
   virtual bool direct_service() { return false; }
   virtual void direct_detach() {}
+  // Hot-object spreading (HbmBackend on several GPUs): re-plan the replicated hot set now;
+  // returns the refresh's counts (empty: the tier has none). Wrappers forward.
+  virtual StatList hot_refresh() { return {}; }
 };
 
 // 32-bit-point ring over digests, identical to shellac_amd.parallel.ring.ShardRing.
@@ -187,6 +191,22 @@ struct HbmBackendConfig {
   int direct_backlog = 4;
   uint64_t direct_arena_bytes = 1u << 20;  // pinned arenas reserved per GPU for them
   int direct_arenas = 32;
+  // Hot-object spreading over the shards (more than one device, and
+  // flush_on_restore: a restored shard must not keep replicas it missed writes for). The
+  // `hot_objects` most requested objects of a sampled GET stream (one GET in `hot_sample`,
+  // a power of two) are replicated on every shard: their SETs / DELETEs are written through
+  // to every shard, their GETs go to a designated shard chosen to even out the load
+  // (objects above `hot_spray_above` of the sampled GETs, default 1/(4N), are sprayed over
+  // all shards). A refresh thread re-plans every `hot_refresh_ms` (0: only on request,
+  // HbmBackend::hot_refresh) once `hot_min_samples` samples are in, and fetches the
+  // records of newly hot objects from their owners over xGMI (at most hot_fill_budget
+  // bytes per refresh, hottest first). 0 objects: plain ketama (every key on its owner).
+  int hot_objects = 1024;
+  int hot_refresh_ms = 1000;
+  int hot_sample = 8;
+  uint64_t hot_min_samples = 512;
+  uint64_t hot_fill_budget = 256ull << 20;
+  double hot_spray_above = 0;  // 0: 1 / (4 * shards)
 };
 
 // One HBM shard per local MI355X. Each GPU has its own batcher thread: requests are
@@ -214,8 +234,9 @@ class HbmBackend : public CacheBackend {
   bool direct_service() override;
   void direct_detach() override;
 
+  struct HotFill;
   struct Req {
-    int kind;  // 0 get, 1 set, 2 del
+    int kind;  // 0 get, 1 set, 2 del, 3 barrier, 4 hot-replica fill
     Digest d;
     std::string key;
     Bytes value;
@@ -223,14 +244,30 @@ class HbmBackend : public CacheBackend {
     Executor* ex = nullptr;
     GetCallback gcb;
     DelCallback dcb;
+    // kinds 3 / 4: runs on the batcher thread once the request's flight has finished on
+    // the GPU (ok) or was failed
+    std::function<void(bool ok)> ccb;
+    std::shared_ptr<HotFill> fill;
   };
   struct Dev;
   struct Direct;
+  // One hot-set refresh now (serialised with the refresh thread's); its counts. A no-op
+  // with spreading off.
+  StatList hot_refresh() override;
+  bool hot_spreading() const { return hot_on_; }
   // reactor contexts (host slots kDirectSlot0 + kDirectJobs * context + job)
   static constexpr int kDirectJobs = 2, kDirectSlot0 = 32, kDirectMax = 15;
 
  private:
-  int route(const Digest& d) const;
+  // owner among the shards up in `up` (-1: none)
+  int owner_of(const Digest& d, uint64_t up) const;
+  // a GET's shard: a hot object's designated / sprayed replica when that shard holds the
+  // replicas (spread_mask_) and is up, else the owner
+  int route_get(const Digest& d);
+  void sample_get(const Digest& d);
+  void enqueue_ctl(int dev, std::function<void(bool)> cb);
+  void hot_loop();
+  StatList hot_refresh_locked();
   void enqueue(int dev, Req r);
   void enqueue_many(int dev, std::vector<Req>& rs);
   uint32_t now() const;
@@ -259,6 +296,36 @@ class HbmBackend : public CacheBackend {
   std::atomic<uint64_t> up_mask_{0};  // bit i: shard i serves requests
   double epoch_;
   std::atomic<uint64_t> no_shard_misses_{0};
+  // ---- hot-object spreading (hot_refresh_locked documents the protocol)
+  std::unique_ptr<HostRouter> router_;  // ketama owners + the published hot table
+  bool hot_on_ = false;
+  // shards holding current replicas of the whole published hot set: a GET may go there
+  std::atomic<uint64_t> spread_mask_{0};
+  static constexpr int kSampleStripes = 16;
+  struct alignas(64) SampleStripe {
+    std::mutex mu;
+    std::vector<Digest> v;
+  };
+  std::unique_ptr<SampleStripe[]> samples_;
+  std::mutex hot_mu_;  // one refresh at a time; guards the refresh state below
+  struct DigestHash {
+    size_t operator()(const Digest& d) const { return (size_t)(d.lo ^ (d.hi * 0x9E3779B97F4A7C15ull)); }
+  };
+  struct DigestEq {
+    bool operator()(const Digest& a, const Digest& b) const { return a.lo == b.lo && a.hi == b.hi; }
+  };
+  std::unordered_map<Digest, uint64_t, DigestHash, DigestEq> hot_counts_;
+  std::vector<Digest> hot_set_;     // the published hot set, hottest first
+  std::vector<int32_t> hot_rank_;   // its designated ranks (-1: sprayed)
+  std::vector<double> hot_weights_;
+  std::thread hot_th_;
+  std::mutex hot_th_mu_;
+  std::condition_variable hot_cv_;
+  bool hot_stop_ = false;
+  std::atomic<uint64_t> hot_refreshes_{0}, hot_added_{0}, hot_removed_{0}, hot_filled_{0},
+      hot_fill_skipped_{0}, hot_fill_failed_{0}, hot_spread_gets_{0}, hot_deferred_{0},
+      hot_fill_bytes_{0}, hot_refresh_us_{0}, hot_samples_{0}, hot_objects_{0},
+      hot_dropped_replicas_{0};
 };
 
 // Two-level cache: a small host-DRAM L1 in front of a big L2 (HBM shards or
@@ -290,6 +357,7 @@ class TieredBackend : public CacheBackend {
     l1_->direct_detach();
     l2_->direct_detach();
   }
+  StatList hot_refresh() override { return l2_->hot_refresh(); }
 
  private:
   std::shared_ptr<CacheBackend> l1_, l2_;
@@ -327,6 +395,7 @@ class FaultBackend : public CacheBackend {
   void direct_attach(Executor* ex) override { inner_->direct_attach(ex); }
   bool direct_service() override { return inner_->direct_service(); }
   void direct_detach() override { inner_->direct_detach(); }
+  StatList hot_refresh() override { return inner_->hot_refresh(); }
   void set_spec(const FaultSpec& spec);
   FaultSpec spec() const;
 

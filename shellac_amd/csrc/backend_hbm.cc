@@ -18,9 +18,10 @@
 // payload that keeps the arena alive until the last client write completes.
 #include <pthread.h>
 
+#include <algorithm>
 #include <chrono>
-#include <unordered_set>
 #include <cstdio>
+#include <unordered_set>
 
 #include "backend.h"
 #include "hbm_cache.h"
@@ -68,6 +69,31 @@ struct Mapped {
   T* host() const { return reinterpret_cast<T*>(h); }
   template <typename T>
   T* dev() const { return reinterpret_cast<T*>(d); }
+};
+
+// Device buffer that grows on demand (the hot-set refresh's staging; the caller has set
+// the device). Growing frees the old block, so only the refresh thread, which owns these,
+// grows them, and never while a fill that reads them is still queued.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <typename T>
+  T* ensure(size_t bytes) {
+    if (bytes > cap) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      const size_t c = std::max<size_t>({bytes, 4096});
+      HB_OK(hipMalloc(&p, c));
+      cap = c;
+    }
+    return static_cast<T*>(p);
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
 };
 
 // Pinned response arenas. A GET batch gathers into one; its hits are ByteRef slices that
@@ -185,6 +211,7 @@ class ArenaPool : public std::enable_shared_from_this<ArenaPool> {
 struct Flight {
   std::vector<HbmBackend::Req> reqs;
   std::vector<uint32_t> gets, sets, dels;  // request indices by kind
+  std::vector<uint32_t> ctls;              // barriers and hot-replica fills
   std::vector<uint32_t> urow;              // GET request -> GPU row (host coalescing)
   size_t rows = 0;                         // distinct GET digests
   Mapped keys, offs, set_keys, set_vals, set_voff, set_meta, del_keys, del_found;
@@ -197,6 +224,28 @@ struct Flight {
   bool served = false;  // GETs answered by the persistent edge server (no stream launch)
   uint32_t tnow = 0;
   double t0 = 0;
+};
+
+// A hot-replica fill queued on a target shard (HbmBackend::hot_refresh_locked): m records
+// gathered on their owners and peer-copied into this shard's staging (krec at koff, digests
+// kk), stored by the target's batcher in stream order. Rows whose digest had a SET or DELETE
+// queued to this shard since the refresh began (Dev::touched) are dropped at launch: the
+// write-through copy is newer than the owner's record read here.
+struct HbmBackend::HotFill {
+  int64_t m = 0;
+  const Digest* kk = nullptr;
+  const uint8_t* krec = nullptr;
+  const uint64_t* koff = nullptr;
+  uint64_t* hsize = nullptr;      // mapped host view of the row sizes (0: no record)
+  const uint64_t* dsize = nullptr;  // its device view
+  Digest* okeys = nullptr;
+  uint64_t* ovoff = nullptr;
+  uint32_t* ometa = nullptr;
+  uint64_t bound = 0;
+  std::vector<uint64_t> lo;  // row digests' low words (the touched check)
+  // under the target Dev's mu
+  bool cancelled = false, launched = false;
+  uint64_t skipped = 0, rows = 0;
 };
 
 struct HbmBackend::Dev {
@@ -237,6 +286,19 @@ struct HbmBackend::Dev {
   int npts = 0;
   // co-table for host GET coalescing (batcher thread only)
   std::vector<int32_t> co_tab;
+  // hot-set refresh: digests (lo) being filled into this shard, and those of them that a
+  // SET / DELETE queued here since (both under mu)
+  std::unordered_set<uint64_t> filling, touched;
+  // refresh staging on this GPU (the refresh thread's): as an owner (snapshot) and as a
+  // target (fill)
+  DevBuf hs_keys, hs_loc, hs_size, hs_off, hs_rec, hf_keys, hf_rec, hf_off, hf_okeys, hf_voff,
+      hf_meta;
+  Mapped hf_size;
+  std::atomic<uint64_t> eject_gen{0};  // bumped when the shard leaves service
+  struct alignas(64) Ctr {
+    std::atomic<uint64_t> v{0};
+  };
+  Ctr routed_gets;  // GETs routed to this shard (per-shard load)
   // digests (lo word) with a SET / DELETE in a flight not yet reaped, and flushes in
   // flight: a GET of such a key takes the stream path, ordered after them
   std::unordered_map<uint64_t, uint32_t> pend_w;
@@ -289,6 +351,10 @@ struct HbmBackend::Dev {
       if (f->ev) (void)hipEventDestroy(f->ev);
     }
     direct_offs.release();
+    for (DevBuf* b : {&hs_keys, &hs_loc, &hs_size, &hs_off, &hs_rec, &hf_keys, &hf_rec, &hf_off,
+                      &hf_okeys, &hf_voff, &hf_meta})
+      b->release();
+    hf_size.release();
     cache.reset();
     if (stream) (void)hipStreamDestroy(stream);
     if (mstream) (void)hipStreamDestroy(mstream);
@@ -468,13 +534,32 @@ HbmBackend::HbmBackend(const HbmBackendConfig& cfg)
         else (void)hipGetLastError();  // clear the sticky error: the pair stays staged
       }
   }
+  if (devs_.size() > 1) {
+    // DigestRing's points (tests check the owners agree), answered from the span table
+    router_ = std::make_unique<HostRouter>((int)devs_.size());
+    if (cfg_.hot_objects > 0 && cfg_.flush_on_restore) {
+      SH_CHECK(cfg_.hot_sample >= 1 && (cfg_.hot_sample & (cfg_.hot_sample - 1)) == 0,
+               "hot_sample must be a power of two");
+      hot_on_ = true;
+      samples_.reset(new SampleStripe[kSampleStripes]);
+      hot_weights_.assign(devs_.size(), 1.0);
+      spread_mask_.store(up_mask_.load());
+    }
+  }
   for (auto& d : devs_) {
     Dev* dp = d.get();
     dp->th = std::thread([dp] { dp->loop(); });
   }
+  if (hot_on_ && cfg_.hot_refresh_ms > 0) hot_th_ = std::thread([this] { hot_loop(); });
 }
 
 HbmBackend::~HbmBackend() {
+  {
+    std::lock_guard<std::mutex> lk(hot_th_mu_);
+    hot_stop_ = true;
+  }
+  hot_cv_.notify_all();
+  if (hot_th_.joinable()) hot_th_.join();  // first: a refresh waits on the batchers
   for (auto& d : devs_) {
     {
       std::lock_guard<std::mutex> lk(d->mu);
@@ -488,10 +573,43 @@ HbmBackend::~HbmBackend() {
 
 uint32_t HbmBackend::now() const { return (uint32_t)(wall_s() - epoch_) + 1; }
 
-int HbmBackend::route(const Digest& d) const {
-  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+int HbmBackend::owner_of(const Digest& d, uint64_t up) const {
   if (devs_.size() == 1) return up & 1 ? 0 : -1;
-  return ring_.owner(d, up);
+  const uint64_t all = devs_.size() >= 64 ? ~0ull : (1ull << devs_.size()) - 1;
+  if ((up & all) == all) return router_->owner(d);  // the span table: one load, two compares
+  return ring_.owner(d, up);  // ketama ejection: the next live point
+}
+
+namespace {
+thread_local uint64_t tl_spray_seq = 0;  // a reactor's stream position (sprayed objects)
+thread_local uint32_t tl_sample_ctr = 0;
+std::atomic<unsigned> g_sample_slot{0};
+thread_local unsigned tl_sample_slot = g_sample_slot.fetch_add(1, std::memory_order_relaxed);
+}  // namespace
+
+int HbmBackend::route_get(const Digest& d) {
+  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+  if (hot_on_) {
+    if (((tl_sample_ctr++) & (uint32_t)(cfg_.hot_sample - 1)) == 0) sample_get(d);
+    int r = -1;
+    {
+      const HostRouter::Read rd(*router_);
+      const int hr = rd.hot_rank(d);
+      if (hr != HostRouter::kNotHot) r = hr >= 0 ? hr : rd.spray(tl_spray_seq++);
+    }
+    if (r >= 0 && ((up & spread_mask_.load(std::memory_order_acquire)) >> r) & 1) {
+      const int o = owner_of(d, up);
+      if (r != o) hot_spread_gets_.fetch_add(1, std::memory_order_relaxed);
+      return r;
+    }
+  }
+  return owner_of(d, up);
+}
+
+void HbmBackend::sample_get(const Digest& d) {
+  SampleStripe& st = samples_[tl_sample_slot % kSampleStripes];
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (st.v.size() < (1u << 16)) st.v.push_back(d);  // bounded while no refresh drains it
 }
 
 void HbmBackend::enqueue(int k, Req r) {
@@ -502,6 +620,9 @@ void HbmBackend::enqueue(int k, Req r) {
       dv.filt->add(r.d);
       if (dv.filt_next) dv.filt_next->add(r.d);
     }
+    // a write of an object being filled into this shard: the fill must not overwrite it
+    if ((r.kind == 1 || r.kind == 2) && !dv.filling.empty() && dv.filling.count(r.d.lo))
+      dv.touched.insert(r.d.lo);
     dv.q.push_back(std::move(r));
     dv.qn.store(dv.q.size(), std::memory_order_release);
   }
@@ -521,13 +642,14 @@ void HbmBackend::enqueue_many(int k, std::vector<Req>& rs) {
 }
 
 void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetCallback done) {
-  const int k = route(d);
+  const int k = route_get(d);
   if (k < 0) {  // every shard ejected: the request falls through to the origin
     no_shard_misses_.fetch_add(1, std::memory_order_relaxed);
     done(false, CacheValue{});
     return;
   }
   Dev& dv = *devs_[k];
+  dv.routed_gets.v.fetch_add(1, std::memory_order_relaxed);
   const bool restoring = dv.restoring.load(std::memory_order_acquire);
   if (cfg_.presence_filter && !restoring && !std::atomic_load(&dv.filt)->maybe(d)) {
     dv.filt_skips.fetch_add(1, std::memory_order_relaxed);  // never stored: no GPU batch
@@ -555,8 +677,6 @@ void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetC
 void HbmBackend::set(const std::string& key, const Digest& d, Bytes value, uint32_t flags,
                      uint32_t ttl_s) {
   if (!value || value->size() > cfg_.max_item || key.size() > kMaxKeyedKey) return;
-  const int k = route(d);
-  if (k < 0) return;
   Req r;
   r.kind = 1;
   r.d = d;
@@ -564,23 +684,82 @@ void HbmBackend::set(const std::string& key, const Digest& d, Bytes value, uint3
   r.value = std::move(value);
   r.flags = flags;
   r.ttl = ttl_s;
-  write_begin(d.lo);  // ends when its flight is reaped (or the request is failed)
-  enqueue(k, std::move(r));
+  if (!hot_on_) {
+    const int k = owner_of(d, up_mask_.load(std::memory_order_acquire));
+    if (k < 0) return;
+    write_begin(d.lo);  // ends when its flight is reaped (or the request is failed)
+    enqueue(k, std::move(r));
+    return;
+  }
+  // held until every copy is queued: a refresh's set_hot returns only after this
+  const HostRouter::Read rd(*router_);
+  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+  const int o = owner_of(d, up);
+  if (o < 0) return;
+  const bool hot = rd.hot_rank(d) != HostRouter::kNotHot;
+  write_begin(d.lo);
+  if (!hot) {
+    enqueue(o, std::move(r));
+    return;
+  }
+  enqueue(o, r);  // write-through: the owner, then every other shard in service
+  for (size_t k = 0; k < devs_.size(); ++k) {
+    if ((int)k == o || !((up >> k) & 1)) continue;
+    write_begin(d.lo);
+    enqueue((int)k, r);
+  }
 }
 
 void HbmBackend::del(const std::string& key, const Digest& d, Executor* ex, DelCallback done) {
-  const int k = route(d);
-  if (k < 0) {
-    if (done) done(false);
-    return;
-  }
   Req r;
   r.kind = 2;
   r.d = d;
   r.key = key;
   r.ex = ex;
-  r.dcb = std::move(done);
-  write_begin(d.lo);
+  std::unique_ptr<HostRouter::Read> rd;  // write-through: held until every copy is queued
+  if (hot_on_) rd = std::make_unique<HostRouter::Read>(*router_);
+  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+  const int k = owner_of(d, up);
+  if (k < 0) {
+    if (done) done(false);
+    return;
+  }
+  std::vector<int> to{k};
+  if (rd && rd->hot_rank(d) != HostRouter::kNotHot)
+    for (size_t j = 0; j < devs_.size(); ++j)
+      if ((int)j != k && ((up >> j) & 1)) to.push_back((int)j);
+  if (to.size() == 1) {
+    r.dcb = std::move(done);
+    write_begin(d.lo);
+    enqueue(k, std::move(r));
+    return;
+  }
+  // one answer: found anywhere, once every copy is gone
+  struct Fan {
+    std::atomic<int> left;
+    std::atomic<bool> found{false};
+    DelCallback cb;
+  };
+  auto fan = std::make_shared<Fan>();
+  fan->left.store((int)to.size());
+  fan->cb = std::move(done);
+  for (int j : to) {
+    Req c = r;
+    c.dcb = [fan](bool f) {
+      if (f) fan->found.store(true, std::memory_order_relaxed);
+      if (fan->left.fetch_sub(1, std::memory_order_acq_rel) == 1 && fan->cb)
+        fan->cb(fan->found.load(std::memory_order_relaxed));
+    };
+    write_begin(d.lo);
+    enqueue(j, std::move(c));
+  }
+}
+
+void HbmBackend::enqueue_ctl(int k, std::function<void(bool)> cb) {
+  Req r;
+  r.kind = 3;
+  r.d = Digest{0, 0};
+  r.ccb = std::move(cb);
   enqueue(k, std::move(r));
 }
 
@@ -601,7 +780,9 @@ bool HbmBackend::inject_shard_down(int shard, bool down) {
   Dev& dv = *devs_[shard];
   dv.forced_down.store(down, std::memory_order_release);
   if (down) {
+    dv.eject_gen.fetch_add(1, std::memory_order_acq_rel);
     dv.set_up(false);
+    spread_mask_.fetch_and(~(1ull << shard), std::memory_order_acq_rel);  // replicas suspect
     dv.ejections++;
   }
   {
@@ -826,9 +1007,12 @@ bool HbmBackend::Dev::take_batch(std::vector<Req>* out, bool* do_flush, bool* re
     w.clear();
     for (size_t i = 0; i < take; ++i) {
       const Req& r = q[i];
-      if (r.kind != 0) {
+      if (r.kind == 1 || r.kind == 2) {
         w.insert(r.d.lo);
-      } else if (!w.empty() && w.count(r.d.lo)) {
+      } else if (r.kind == 4) {  // a fill ends its flight (it runs after the flight's writes)
+        take = i + 1;
+        break;
+      } else if (r.kind == 0 && !w.empty() && w.count(r.d.lo)) {
         take = i;
         break;
       }
@@ -987,8 +1171,11 @@ void HbmBackend::Dev::launch(Flight& f) {
   f.gets.clear();
   f.sets.clear();
   f.dels.clear();
-  for (uint32_t i = 0; i < f.reqs.size(); ++i)
-    (f.reqs[i].kind == 0 ? f.gets : f.reqs[i].kind == 1 ? f.sets : f.dels).push_back(i);
+  f.ctls.clear();
+  for (uint32_t i = 0; i < f.reqs.size(); ++i) {
+    const int kd = f.reqs[i].kind;
+    (kd == 0 ? f.gets : kd == 1 ? f.sets : kd == 2 ? f.dels : f.ctls).push_back(i);
+  }
   f.tnow = be->now();
   f.t0 = wall_s();
   f.got = f.gets.empty();
@@ -1091,6 +1278,27 @@ void HbmBackend::Dev::launch(Flight& f) {
     cache->remove(f.del_keys.dev<Digest>(), (int64_t)nd, f.del_found.dev<uint8_t>(), f.tnow,
                   stream);
   }
+  // ---- hot-replica fills (last in the flight: every write queued before them ran first)
+  for (uint32_t i : f.ctls) {
+    if (f.reqs[i].kind != 4) continue;
+    HotFill& h = *f.reqs[i].fill;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (h.cancelled) continue;  // the refresh gave up on this shard
+      h.launched = true;
+      for (int64_t j = 0; j < h.m; ++j)
+        if (h.hsize[j] && touched.count(h.lo[(size_t)j])) {
+          h.hsize[j] = 0;  // a newer write-through copy is (or will be) here
+          ++h.skipped;
+        } else if (h.hsize[j]) {
+          ++h.rows;
+        }
+    }
+    records_to_set(h.krec, h.koff, h.dsize, nullptr, h.m, h.okeys, h.ovoff, h.ometa,
+                   h.ometa + h.m, h.ometa + 2 * h.m, stream);
+    cache->store(h.okeys, h.krec, h.ovoff, h.ometa, h.ometa + h.m, h.ometa + 2 * h.m, h.m,
+                 h.bound, f.tnow, stream);
+  }
   HB_OK(hipEventRecord(f.ev, stream));
   batches++;
   batched_reqs += f.reqs.size();
@@ -1146,6 +1354,8 @@ bool HbmBackend::Dev::try_reap(Flight& f, bool block) {
   }
   if (f.active) {
     deliver_dels(f);
+    for (uint32_t i : f.ctls)
+      if (f.reqs[i].ccb) f.reqs[i].ccb(true);
     batch_ns += (uint64_t)((wall_s() - f.t0) * 1e9);
   }
   f.active = false;
@@ -1248,8 +1458,11 @@ void HbmBackend::Dev::deliver_dels(Flight& f) {
 void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs, bool unlaunched) {
   PostGroups pg;
   for (auto& r : reqs) {
-    if (unlaunched && r.kind != 0) be->write_end(r.d.lo);
-    if (r.kind == 0 && r.gcb) {
+    if (unlaunched && (r.kind == 1 || r.kind == 2)) be->write_end(r.d.lo);
+    if (r.kind >= 3) {
+      if (r.ccb) r.ccb(false);
+      r.ccb = nullptr;
+    } else if (r.kind == 0 && r.gcb) {
       auto cb = std::move(r.gcb);
       if (r.ex) pg.at(r.ex).push_back([cb = std::move(cb)]() { cb(false, CacheValue{}); });
       else cb(false, CacheValue{});
@@ -1268,15 +1481,18 @@ void HbmBackend::Dev::fail_requests(std::vector<Req>& reqs, bool unlaunched) {
 // flight itself stays reserved until the GPU finishes with its buffers.
 void HbmBackend::Dev::fail_flight(Flight& f) {
   failures++;
-  if (!f.got) fail_requests(f.reqs, false);
-  else {
+  if (!f.got) {
+    fail_requests(f.reqs, false);
+  } else {
     std::vector<Req> rest;
     for (uint32_t i : f.dels) rest.push_back(std::move(f.reqs[i]));
+    for (uint32_t i : f.ctls) rest.push_back(std::move(f.reqs[i]));
     fail_requests(rest, false);
   }
   f.got = true;
   f.gets.clear();
   f.dels.clear();
+  f.ctls.clear();
   f.active = false;
 }
 
@@ -1288,7 +1504,9 @@ void HbmBackend::Dev::eject(const char* why) {
   }
   failed = true;
   retry_at = wall_s() + be->cfg_.retry_s;
+  eject_gen.fetch_add(1, std::memory_order_acq_rel);
   set_up(false);
+  be->spread_mask_.fetch_and(~(1ull << index), std::memory_order_acq_rel);
   std::vector<Req> pending;
   {
     std::lock_guard<std::mutex> lk(mu);
@@ -1442,6 +1660,15 @@ uint64_t HbmBackend::Dev::migrate_from(Dev& src) {
   for (uint64_t i = 0; i < got; ++i)
     if (dest[i] == index) mine.push_back(keys[i]);
   (void)hipFree(s_keys);
+  if (be->hot_on_ && !mine.empty()) {
+    // hot objects stay where they are: the peers hold write-through replicas (they keep
+    // serving the GETs spread to them), and this shard receives the whole hot set from the
+    // next refresh's heal fill before it rejoins the spread mask
+    const HostRouter::Read rd(*be->router_);
+    mine.erase(std::remove_if(mine.begin(), mine.end(),
+                              [&](const Digest& d) { return rd.hot_rank(d) != HostRouter::kNotHot; }),
+               mine.end());
+  }
   if (be->cfg_.presence_filter && !mine.empty()) {  // GETs routed here must not skip them
     std::lock_guard<std::mutex> lk(mu);
     for (const Digest& d : mine) {
@@ -1568,6 +1795,470 @@ void HbmBackend::Dev::finish_filter_rebuild() {
   filt_rebuilds++;
 }
 
+// ---------------------------------------------------------------------------------
+// hot-object spreading: the reference's ketama client
+// sends each key to one node (src/python/shellac/server/Server.py:81-83), so a hot key
+// loads one GPU. The hot set follows a sampled GET stream; its objects are replicated on
+// every shard in service and their GETs spread by the router's designation / spray.
+// ---------------------------------------------------------------------------------
+void HbmBackend::hot_loop() {
+  pthread_setname_np(pthread_self(), "shellac-hot");
+  std::unique_lock<std::mutex> lk(hot_th_mu_);
+  while (!hot_stop_) {
+    hot_cv_.wait_for(lk, std::chrono::milliseconds(cfg_.hot_refresh_ms), [&] { return hot_stop_; });
+    if (hot_stop_) break;
+    lk.unlock();
+    try {
+      hot_refresh();
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "[shellac hbm] hot-set refresh failed: %s\n", e.what());
+    }
+    lk.lock();
+  }
+}
+
+StatList HbmBackend::hot_refresh() {
+  std::lock_guard<std::mutex> lk(hot_mu_);
+  return hot_refresh_locked();
+}
+
+namespace {
+// waits for n completion callbacks (barriers, fills); ok[i] per callback index
+struct Waiter {
+  std::mutex mu;
+  std::condition_variable cv;
+  int left = 0;
+  std::vector<int> ok;  // 1 ok, 0 failed, -1 pending
+  explicit Waiter(int n) : left(n), ok((size_t)n, -1) {}
+  std::function<void(bool)> cb(int i) {
+    return [this, i](bool good) {
+      std::lock_guard<std::mutex> lk(mu);
+      ok[(size_t)i] = good ? 1 : 0;
+      if (--left == 0) cv.notify_all();
+    };
+  }
+  bool wait(int timeout_ms) {
+    std::unique_lock<std::mutex> lk(mu);
+    return cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return left == 0; });
+  }
+  int state(int i) {
+    std::lock_guard<std::mutex> lk(mu);
+    return ok[(size_t)i];
+  }
+};
+}  // namespace
+
+// One refresh. The order keeps every GET answered by a copy no older than the last SET /
+// DELETE that finished before the GET began (HotSpread's refresh_hot, single process):
+//  1. plan the new hot set from the sampled counts (plan_hot: top hot_objects, designated
+//     greedily from the owners' cold loads, the hottest sprayed);
+//  2. every shard in service starts recording writes of the objects about to be filled
+//     (Dev::filling / touched);
+//  3. router table T1 = the current hot set + the new objects designated to their owners:
+//     the new objects' SETs / DELETEs are written through from here on, their GETs still go
+//     to their owners. set_hot returns once nothing routes under the old table, so every
+//     write routed owner-only has been queued;
+//  4. a barrier on each owner: those writes have finished on its GPU;
+//  5. the owners look the objects up and gather their records (one snapshot per owner);
+//  6. per target shard, the records of the objects it does not own go over xGMI into its
+//     staging (copy_between: hipMemcpyPeerAsync, or staged through pinned host memory) and
+//     a fill request is queued behind the shard's writes; the batcher drops the rows with
+//     a write queued since step 2 (that copy is newer) and stores the rest;
+//  7. once every fill has finished, the shards that now hold the whole set join the
+//     spread mask, and T2 = the new hot set with its designations is published;
+//  8. objects that left the set lose their non-owner replicas (deleted: no SET reaches
+//     them any more, and a later promotion must find no stale copy).
+// Shards that are down, or eject mid-refresh, drop out of the spread mask (a restored
+// shard is flushed and rejoins with a full fill at the next refresh).
+StatList HbmBackend::hot_refresh_locked() {
+  StatList out;
+  if (!hot_on_) return out;
+  TraceRange tr("hbm_backend.hot_refresh");
+  const double t_start = wall_s();
+  const int N = (int)devs_.size();
+  // ---- samples -> decayed counts
+  uint64_t nsamp = 0;
+  for (int i = 0; i < kSampleStripes; ++i) {
+    std::vector<Digest> v;
+    {
+      std::lock_guard<std::mutex> lk(samples_[i].mu);
+      v.swap(samples_[i].v);
+    }
+    nsamp += v.size();
+    for (const Digest& d : v) {
+      auto it = hot_counts_.find(d);
+      if (it != hot_counts_.end()) ++it->second;
+      else if (hot_counts_.size() < (1u << 18)) hot_counts_.emplace(d, 1);
+    }
+  }
+  hot_samples_.fetch_add(nsamp, std::memory_order_relaxed);
+  uint64_t total = 0;
+  for (const auto& kv : hot_counts_) total += kv.second;
+  out.emplace_back("samples", total);
+  if (total < cfg_.hot_min_samples) {
+    out.emplace_back("skipped", 1);
+    return out;
+  }
+  const uint64_t up = up_mask_.load(std::memory_order_acquire);
+  std::vector<std::pair<Digest, uint64_t>> counts(hot_counts_.begin(), hot_counts_.end());
+  for (auto it = hot_counts_.begin(); it != hot_counts_.end();) {  // halve: recent traffic rules
+    it->second >>= 1;
+    if (!it->second) it = hot_counts_.erase(it);
+    else ++it;
+  }
+  const double above = cfg_.hot_spray_above > 0 ? cfg_.hot_spray_above : 1.0 / (4.0 * N);
+  HotPlan plan = plan_hot(counts, cfg_.hot_objects, N, up,
+                          [&](const Digest& d) { return owner_of(d, up); }, above);
+  // ---- what changes
+  std::unordered_map<Digest, int32_t, DigestHash, DigestEq> cur;
+  for (size_t i = 0; i < hot_set_.size(); ++i) cur.emplace(hot_set_[i], hot_rank_[i]);
+  std::unordered_set<Digest, DigestHash, DigestEq> added;
+  for (const Digest& d : plan.hot)
+    if (!cur.count(d)) added.insert(d);
+  const uint64_t mask0 = spread_mask_.load(std::memory_order_acquire) & up;
+  const uint64_t heal = up & ~mask0;  // in service, holding no replicas yet (restored, new)
+  std::vector<uint64_t> gen0((size_t)N);
+  for (int r = 0; r < N; ++r) gen0[(size_t)r] = devs_[(size_t)r]->eject_gen.load();
+  // objects to snapshot, hottest first: the new ones, and every planned one for a heal
+  std::vector<Digest> fill_objs;
+  for (const Digest& d : plan.hot)
+    if (heal || added.count(d)) fill_objs.push_back(d);
+  // ---- 2. record writes of those objects on every shard in service
+  for (int r = 0; r < N; ++r) {
+    if (!((up >> r) & 1)) continue;
+    Dev& dv = *devs_[(size_t)r];
+    std::lock_guard<std::mutex> lk(dv.mu);
+    dv.filling.clear();
+    dv.touched.clear();
+    for (const Digest& d : fill_objs) dv.filling.insert(d.lo);
+  }
+  auto stop_recording = [&] {
+    for (auto& dv : devs_) {
+      std::lock_guard<std::mutex> lk(dv->mu);
+      dv->filling.clear();
+      dv->touched.clear();
+    }
+  };
+  // ---- 3. T1: write-through for the new objects, their GETs at their owners
+  {
+    std::vector<Digest> h(hot_set_);
+    std::vector<int32_t> rk(hot_rank_);
+    for (const Digest& d : plan.hot)
+      if (added.count(d)) {
+        h.push_back(d);
+        rk.push_back(owner_of(d, up));
+      }
+    router_->set_hot(h.data(), (int64_t)h.size(), rk.data(), hot_weights_.data());
+  }
+  const uint32_t t = now();
+  const int wait_ms = 2 * cfg_.batch_timeout_ms + 1000;
+  // ---- 4. barrier on every owner (source) of an object to fill
+  // (an object of the current set owned by a shard being healed is read from a shard that
+  // holds its replica: the healed one was flushed, and warm restore leaves hot objects be)
+  int replica_src = -1;
+  for (int r = 0; r < N && replica_src < 0; ++r)
+    if ((mask0 >> r) & 1) replica_src = r;
+  std::vector<std::vector<Digest>> by_owner((size_t)N);
+  for (const Digest& d : fill_objs) {
+    int o = owner_of(d, up);
+    if (o >= 0 && ((heal >> o) & 1) && replica_src >= 0 && cur.count(d)) o = replica_src;
+    if (o >= 0) by_owner[(size_t)o].push_back(d);
+  }
+  uint64_t bad = 0;  // shards that failed a barrier or a fill this refresh
+  {
+    std::vector<int> who;
+    for (int o = 0; o < N; ++o)
+      if (!by_owner[(size_t)o].empty()) who.push_back(o);
+    auto w = std::make_shared<Waiter>((int)who.size());
+    for (size_t i = 0; i < who.size(); ++i) {
+      auto wp = w;
+      auto cb = w->cb((int)i);
+      enqueue_ctl(who[i], [wp, cb](bool ok) { cb(ok); });
+    }
+    w->wait(wait_ms);
+    for (size_t i = 0; i < who.size(); ++i)
+      if (w->state((int)i) != 1) {
+        bad |= 1ull << who[i];
+        by_owner[(size_t)who[i]].clear();  // its objects are not filled this time
+      }
+  }
+  // ---- 5. snapshot on each owner
+  struct Snap {
+    std::vector<Digest> keys;
+    std::vector<uint64_t> size, off;
+    uint64_t total = 0;
+  };
+  std::vector<Snap> snap((size_t)N);
+  for (int o = 0; o < N; ++o) {
+    Snap& sn = snap[(size_t)o];
+    sn.keys = by_owner[(size_t)o];
+    const int64_t m = (int64_t)sn.keys.size();
+    if (!m) continue;
+    Dev& od = *devs_[(size_t)o];
+    try {
+      HB_OK(hipSetDevice(od.device));
+      Digest* sk = od.hs_keys.ensure<Digest>((size_t)m * sizeof(Digest));
+      uint64_t* sloc = od.hs_loc.ensure<uint64_t>((size_t)m * 8);
+      uint64_t* ssz = od.hs_size.ensure<uint64_t>((size_t)(m + 1) * 8);
+      uint64_t* soff = od.hs_off.ensure<uint64_t>((size_t)(m + 1) * 8);
+      HB_OK(hipMemcpyAsync(sk, sn.keys.data(), (size_t)m * sizeof(Digest), hipMemcpyHostToDevice,
+                           od.mstream));
+      od.cache->lookup(sk, m, sloc, ssz, soff, t, od.mstream, od.cache->config().log_bytes / 8);
+      sn.size.assign((size_t)m + 1, 0);
+      sn.off.assign((size_t)m + 1, 0);
+      HB_OK(hipMemcpyAsync(sn.size.data(), ssz, (size_t)m * 8, hipMemcpyDeviceToHost, od.mstream));
+      HB_OK(hipMemcpyAsync(sn.off.data(), soff, (size_t)(m + 1) * 8, hipMemcpyDeviceToHost,
+                           od.mstream));
+      HB_OK(hipStreamSynchronize(od.mstream));
+      sn.total = sn.off[(size_t)m];
+      if (sn.total) {
+        uint8_t* srec = od.hs_rec.ensure<uint8_t>(sn.total + 16);
+        od.cache->gather(sloc, soff, m, srec, od.mstream);
+        HB_OK(hipStreamSynchronize(od.mstream));
+      }
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "[shellac hbm] hot snapshot on gpu %d failed: %s\n", od.device, e.what());
+      bad |= 1ull << o;
+      sn = Snap{};
+    }
+  }
+  // ---- budget: new objects hottest first, (targets) x record bytes each
+  std::unordered_set<Digest, DigestHash, DigestEq> deferred;
+  {
+    std::unordered_map<Digest, uint64_t, DigestHash, DigestEq> rec;
+    for (int o = 0; o < N; ++o)
+      for (size_t i = 0; i < snap[(size_t)o].keys.size(); ++i)
+        rec[snap[(size_t)o].keys[i]] = snap[(size_t)o].size[i];
+    const uint64_t targets = (uint64_t)std::max(1, __builtin_popcountll(up) - 1);
+    uint64_t spent = 0;
+    for (const Digest& d : plan.hot) {
+      if (!added.count(d)) continue;
+      auto it = rec.find(d);
+      const uint64_t b = it == rec.end() ? 0 : it->second * targets;
+      if (spent + b > cfg_.hot_fill_budget) deferred.insert(d);
+      else spent += b;
+    }
+  }
+  // an object is spread after this refresh if it stays (was hot and still is) or was added,
+  // snapshot ok (owner did not fail) and within the budget
+  std::unordered_set<Digest, DigestHash, DigestEq> filled_ok;
+  for (int o = 0; o < N; ++o)
+    for (const Digest& d : snap[(size_t)o].keys) filled_ok.insert(d);
+  // ---- 6. fills, one per target shard
+  std::vector<std::shared_ptr<HotFill>> fills((size_t)N);
+  uint64_t fill_bytes = 0;
+  std::vector<int> tgt;
+  for (int r = 0; r < N; ++r) {
+    if (!((up >> r) & 1) || ((bad >> r) & 1)) continue;
+    const bool full = (heal >> r) & 1;
+    // rows: every snapshot row of the other owners; size 0 where this shard takes no copy
+    int64_t m = 0;
+    uint64_t bytes = 0;
+    for (int o = 0; o < N; ++o)
+      if (o != r && snap[(size_t)o].total) {
+        m += (int64_t)snap[(size_t)o].keys.size();
+        bytes += snap[(size_t)o].total;
+      }
+    if (!m) continue;
+    Dev& td = *devs_[(size_t)r];
+    auto h = std::make_shared<HotFill>();
+    try {
+      HB_OK(hipSetDevice(td.device));
+      Digest* kk = td.hf_keys.ensure<Digest>((size_t)m * sizeof(Digest));
+      uint8_t* krec = td.hf_rec.ensure<uint8_t>(bytes + 16);
+      uint64_t* koff = td.hf_off.ensure<uint64_t>((size_t)(m + 1) * 8);
+      h->okeys = td.hf_okeys.ensure<Digest>((size_t)m * sizeof(Digest));
+      h->ovoff = td.hf_voff.ensure<uint64_t>((size_t)m * 8);
+      h->ometa = td.hf_meta.ensure<uint32_t>((size_t)m * 12);
+      td.hf_size.ensure((size_t)(m + 1) * 8);
+      std::vector<Digest> keys;
+      std::vector<uint64_t> off;
+      keys.reserve((size_t)m);
+      off.reserve((size_t)m + 1);
+      h->hsize = td.hf_size.host<uint64_t>();
+      h->dsize = td.hf_size.dev<uint64_t>();
+      uint64_t base = 0;
+      int64_t row = 0;
+      for (int o = 0; o < N; ++o) {
+        const Snap& sn = snap[(size_t)o];
+        if (o == r || !sn.total) continue;
+        Dev& od = *devs_[(size_t)o];
+        copy_between(krec + base, td.device, od.hs_rec.p, od.device, sn.total, td.mstream,
+                     peer_path(od.device, td.device));
+        if (peer_path(od.device, td.device) == 2) td.staged_copies++;
+        for (size_t i = 0; i < sn.keys.size(); ++i, ++row) {
+          const Digest& d = sn.keys[i];
+          keys.push_back(d);
+          off.push_back(base + sn.off[i]);
+          const bool want = (full || added.count(d)) && !deferred.count(d);
+          h->hsize[row] = want ? sn.size[i] : 0;
+          h->lo.push_back(d.lo);
+          if (want && sn.size[i]) fill_bytes += sn.size[i];
+        }
+        base += sn.total;
+      }
+      off.push_back(base);
+      HB_OK(hipMemcpyAsync(kk, keys.data(), (size_t)m * sizeof(Digest), hipMemcpyHostToDevice,
+                           td.mstream));
+      HB_OK(hipMemcpyAsync(koff, off.data(), (size_t)(m + 1) * 8, hipMemcpyHostToDevice,
+                           td.mstream));
+      HB_OK(hipStreamSynchronize(td.mstream));
+      h->m = m;
+      h->kk = kk;
+      h->krec = krec;
+      h->koff = koff;
+      h->bound = bytes + 48 * (uint64_t)m;
+      if (cfg_.presence_filter) {  // GETs spread here must not skip the replicas
+        std::lock_guard<std::mutex> lk(td.mu);
+        for (int64_t i = 0; i < m; ++i)
+          if (h->hsize[i]) {
+            td.filt->add(keys[(size_t)i]);
+            if (td.filt_next) td.filt_next->add(keys[(size_t)i]);
+          }
+      }
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "[shellac hbm] hot fill staging on gpu %d failed: %s\n", td.device,
+                   e.what());
+      bad |= 1ull << r;
+      continue;
+    }
+    fills[(size_t)r] = h;
+    tgt.push_back(r);
+  }
+  {
+    auto w = std::make_shared<Waiter>((int)tgt.size());
+    for (size_t i = 0; i < tgt.size(); ++i) {
+      Req q;
+      q.kind = 4;
+      q.d = Digest{0, 0};
+      q.fill = fills[(size_t)tgt[i]];
+      auto wp = w;
+      auto cb = w->cb((int)i);
+      q.ccb = [wp, cb](bool ok) { cb(ok); };
+      enqueue(tgt[i], std::move(q));
+    }
+    if (!w->wait(wait_ms)) {
+      // a shard that never got to its fill: cancel it if not launched (else it completes
+      // with its touched check made in time, and only its buffers must outlive it)
+      for (size_t i = 0; i < tgt.size(); ++i) {
+        if (w->state((int)i) != -1) continue;
+        Dev& td = *devs_[(size_t)tgt[i]];
+        std::lock_guard<std::mutex> lk(td.mu);
+        HotFill& h = *fills[(size_t)tgt[i]];
+        if (!h.launched) h.cancelled = true;
+        else {  // still running on the GPU: its staging is abandoned (leaked), not reused
+          td.hf_keys = DevBuf{}; td.hf_rec = DevBuf{}; td.hf_off = DevBuf{};
+          td.hf_okeys = DevBuf{}; td.hf_voff = DevBuf{}; td.hf_meta = DevBuf{};
+          td.hf_size = Mapped{};
+        }
+      }
+    }
+    uint64_t rows = 0, skipped = 0;
+    for (size_t i = 0; i < tgt.size(); ++i) {
+      const int r = tgt[i];
+      if (w->state((int)i) != 1) {
+        bad |= 1ull << r;
+        hot_fill_failed_.fetch_add(1, std::memory_order_relaxed);
+        continue;
+      }
+      Dev& td = *devs_[(size_t)r];
+      std::lock_guard<std::mutex> lk(td.mu);
+      rows += fills[(size_t)r]->rows;
+      skipped += fills[(size_t)r]->skipped;
+    }
+    hot_filled_.fetch_add(rows, std::memory_order_relaxed);
+    hot_fill_skipped_.fetch_add(skipped, std::memory_order_relaxed);
+    out.emplace_back("filled_rows", rows);
+    out.emplace_back("fill_skipped_rows", skipped);
+  }
+  stop_recording();
+  // ---- 7. the spread mask, then T2
+  uint64_t mask = (mask0 | heal) & ~bad;
+  for (int r = 0; r < N; ++r)
+    if (devs_[(size_t)r]->eject_gen.load() != gen0[(size_t)r]) mask &= ~(1ull << r);
+  // owners whose barrier or snapshot failed: their new objects are not filled anywhere
+  std::vector<Digest> final_hot;
+  std::vector<int32_t> final_rank;
+  for (size_t i = 0; i < plan.hot.size(); ++i) {
+    const Digest& d = plan.hot[i];
+    if (added.count(d) && (deferred.count(d) || !filled_ok.count(d))) continue;
+    final_hot.push_back(d);
+    final_rank.push_back(plan.rank[i]);
+  }
+  std::vector<double> wts((size_t)N, 0.0);
+  double wsum = 0;
+  for (int r = 0; r < N; ++r)
+    if ((mask >> r) & 1) wsum += (wts[(size_t)r] = plan.weights[(size_t)r]);
+  if (wsum <= 0) {  // nowhere to spread: no hot set
+    final_hot.clear();
+    final_rank.clear();
+    wts.assign((size_t)N, 1.0);
+  }
+  spread_mask_.store(mask, std::memory_order_release);
+  for (int r = 0; r < N; ++r)  // an ejection that raced the store above
+    if (devs_[(size_t)r]->eject_gen.load() != gen0[(size_t)r] || !devs_[(size_t)r]->up())
+      spread_mask_.fetch_and(~(1ull << r), std::memory_order_acq_rel);
+  router_->set_hot(final_hot.data(), (int64_t)final_hot.size(), final_rank.data(), wts.data());
+  // ---- 8. replicas of objects no longer hot (the old set and this refresh's write-through
+  // set minus the new one) go from every shard but their owner
+  std::unordered_set<Digest, DigestHash, DigestEq> fin(final_hot.begin(), final_hot.end());
+  std::vector<Digest> gone;
+  for (const Digest& d : hot_set_)
+    if (!fin.count(d)) gone.push_back(d);
+  for (const Digest& d : added)
+    if (!fin.count(d)) gone.push_back(d);
+  const uint64_t up2 = up_mask_.load(std::memory_order_acquire);
+  uint64_t dropped = 0;
+  for (const Digest& d : gone) {
+    const int o = owner_of(d, up2);
+    for (int r = 0; r < N; ++r) {
+      if (r == o || !((up2 >> r) & 1)) continue;
+      Req q;
+      q.kind = 2;
+      q.d = d;
+      write_begin(d.lo);
+      enqueue(r, std::move(q));
+      ++dropped;
+    }
+  }
+  hot_set_ = std::move(final_hot);
+  hot_rank_ = std::move(final_rank);
+  hot_weights_ = wts;
+  hot_objects_.store(hot_set_.size(), std::memory_order_relaxed);
+  uint64_t n_added = 0;
+  for (const Digest& d : added) n_added += fin.count(d);
+  hot_added_.fetch_add(n_added, std::memory_order_relaxed);
+  hot_removed_.fetch_add(gone.size(), std::memory_order_relaxed);
+  hot_deferred_.fetch_add(deferred.size(), std::memory_order_relaxed);
+  hot_dropped_replicas_.fetch_add(dropped, std::memory_order_relaxed);
+  hot_fill_bytes_.fetch_add(fill_bytes, std::memory_order_relaxed);
+  hot_refreshes_.fetch_add(1, std::memory_order_relaxed);
+  const uint64_t us = (uint64_t)((wall_s() - t_start) * 1e6);
+  hot_refresh_us_.store(us, std::memory_order_relaxed);
+  out.emplace_back("hot", hot_set_.size());
+  out.emplace_back("added", n_added);
+  out.emplace_back("removed", gone.size());
+  out.emplace_back("deferred", deferred.size());
+  out.emplace_back("replicas_dropped", dropped);
+  out.emplace_back("fill_bytes", fill_bytes);
+  out.emplace_back("spread_mask", spread_mask_.load());
+  out.emplace_back("heal_mask", heal);
+  out.emplace_back("failed_mask", bad);
+  out.emplace_back("hot_share_ppm", (uint64_t)(plan.hot_share * 1e6));
+  double pmax = 0, psum = 0;
+  int pn = 0;
+  for (int r = 0; r < N; ++r)
+    if ((up >> r) & 1) {
+      pmax = std::max(pmax, plan.planned[(size_t)r]);
+      psum += plan.planned[(size_t)r];
+      ++pn;
+    }
+  out.emplace_back("planned_max_over_mean_ppm",
+                   psum > 0 ? (uint64_t)(pmax / (psum / pn) * 1e6) : 0);
+  out.emplace_back("refresh_us", us);
+  return out;
+}
+
 void HbmBackend::stats(StatList* out) {
   CacheCounters t{};
   uint64_t hbm = 0;
@@ -1633,6 +2324,27 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_migrate_ns", sum(&Dev::migrate_ns));
   out->emplace_back("hbm_dropped_sets", sum(&Dev::dropped));
   out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
+  // per-shard GET routing (the load hot-object spreading evens out) and the hot set
+  for (size_t i = 0; i < devs_.size(); ++i)
+    out->emplace_back("hbm_shard_gets_" + std::to_string(i), devs_[i]->routed_gets.v.load());
+  out->emplace_back("hbm_hot_spreading", hot_on_ ? 1 : 0);
+  if (hot_on_) {
+    out->emplace_back("hbm_hot_objects", hot_objects_.load());
+    out->emplace_back("hbm_hot_refreshes", hot_refreshes_.load());
+    out->emplace_back("hbm_hot_added", hot_added_.load());
+    out->emplace_back("hbm_hot_removed", hot_removed_.load());
+    out->emplace_back("hbm_hot_deferred", hot_deferred_.load());
+    out->emplace_back("hbm_hot_filled_rows", hot_filled_.load());
+    out->emplace_back("hbm_hot_fill_skipped_rows", hot_fill_skipped_.load());
+    out->emplace_back("hbm_hot_fill_failures", hot_fill_failed_.load());
+    out->emplace_back("hbm_hot_fill_bytes", hot_fill_bytes_.load());
+    out->emplace_back("hbm_hot_replicas_dropped", hot_dropped_replicas_.load());
+    out->emplace_back("hbm_hot_spread_gets", hot_spread_gets_.load());
+    out->emplace_back("hbm_hot_samples", hot_samples_.load());
+    out->emplace_back("hbm_hot_spread_mask", spread_mask_.load());
+    out->emplace_back("hbm_hot_refresh_us_last", hot_refresh_us_.load());
+    out->emplace_back("hbm_hot_router_tables", router_->publications());
+  }
   uint64_t arena = 0, aallocs = 0, afrees = 0, amax = 0;
   for (auto& d : devs_) {
     amax = std::max<uint64_t>(amax, d->pool->alloc_max_us());

@@ -171,6 +171,40 @@ void bind_net(py::module_& m) {
         h.be->set(k, d, std::make_shared<const std::string>(std::string(value)), flags, ttl);
       }, py::arg("key"), py::arg("value"), py::arg("flags") = 0, py::arg("ttl") = 0)
       .def("delete", [](BackendHandle& h, py::bytes key) { return blocking_del(h.be.get(), key); })
+      .def("get_many", [](BackendHandle& h, std::vector<std::string> keys) {
+        // every GET issued at once (one batch stream, as concurrent clients would), then
+        // waited for: [(value, flags) or None]
+        const size_t n = keys.size();
+        std::vector<CacheValue> vals(n);
+        std::vector<uint8_t> hit(n, 0);
+        std::mutex mu;
+        std::condition_variable cv;
+        size_t left = n;
+        {
+          py::gil_scoped_release nogil;
+          for (size_t i = 0; i < n; ++i) {
+            const Digest d = digest_bytes(reinterpret_cast<const uint8_t*>(keys[i].data()),
+                                          keys[i].size());
+            h.be->get(keys[i], d, &g_inline, [&, i](bool ht, CacheValue v) {
+              std::lock_guard<std::mutex> lk(mu);
+              hit[i] = ht;
+              vals[i] = std::move(v);
+              if (--left == 0) cv.notify_all();
+            });
+          }
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return left == 0; });
+        }
+        py::list out;
+        for (size_t i = 0; i < n; ++i) {
+          if (hit[i] && vals[i].data)
+            out.append(py::make_tuple(py::bytes(vals[i].data->data(), vals[i].data->size()),
+                                      vals[i].flags));
+          else
+            out.append(py::none());
+        }
+        return out;
+      })
       .def("flush", [](BackendHandle& h) { h.be->flush(); })
       .def("stats", [](BackendHandle& h) {
         StatList st;
@@ -199,7 +233,9 @@ void bind_net(py::module_& m) {
                           int retry_s, int batch_timeout_ms, bool flush_on_restore,
                           bool warm_restore, const std::string& peer_copy, bool edge_server,
                           std::vector<int> batcher_cpus, int serve_backlog, bool direct,
-                          int direct_backlog, int serve_blocks) {
+                          int direct_backlog, int serve_blocks, int hot_objects,
+                          int hot_refresh_ms, int hot_sample, uint64_t hot_min_samples,
+                          uint64_t hot_fill_budget, double hot_spray_above) {
     HbmBackendConfig c;
     c.devices = std::move(devices);
     c.log_bytes_per_gpu = log_bytes_per_gpu;
@@ -228,6 +264,13 @@ void bind_net(py::module_& m) {
     c.direct_backlog = direct_backlog;
     SH_CHECK(serve_blocks >= 1 && serve_blocks <= 8, "serve_blocks must be in 1..8");
     c.serve_blocks = serve_blocks;
+    SH_CHECK(hot_objects >= 0 && hot_refresh_ms >= 0, "hot_objects / hot_refresh_ms must be >= 0");
+    c.hot_objects = hot_objects;
+    c.hot_refresh_ms = hot_refresh_ms;
+    c.hot_sample = hot_sample;
+    c.hot_min_samples = hot_min_samples;
+    c.hot_fill_budget = hot_fill_budget;
+    c.hot_spray_above = hot_spray_above;
     py::gil_scoped_release nogil;
     return BackendHandle{std::make_shared<HbmBackend>(c)};
   }, py::arg("devices"), py::arg("log_bytes_per_gpu"), py::arg("nbuckets_per_gpu"),
@@ -238,7 +281,20 @@ void bind_net(py::module_& m) {
      py::arg("flush_on_restore") = true, py::arg("warm_restore") = true,
      py::arg("peer_copy") = "auto", py::arg("edge_server") = true,
      py::arg("batcher_cpus") = std::vector<int>{}, py::arg("serve_backlog") = 2,
-     py::arg("direct") = true, py::arg("direct_backlog") = 4, py::arg("serve_blocks") = 8);
+     py::arg("direct") = true, py::arg("direct_backlog") = 4, py::arg("serve_blocks") = 8,
+     py::arg("hot_objects") = 1024, py::arg("hot_refresh_ms") = 1000, py::arg("hot_sample") = 8,
+     py::arg("hot_min_samples") = 512, py::arg("hot_fill_budget") = 256ull << 20,
+     py::arg("hot_spray_above") = 0.0);
+  m.def("hot_refresh", [](BackendHandle& h) {
+    StatList st;
+    {
+      py::gil_scoped_release nogil;
+      st = h.be->hot_refresh();
+    }
+    py::dict d;
+    for (auto& kv : st) d[py::str(kv.first)] = kv.second;
+    return d;
+  }, py::arg("backend"));
   m.def("inject_shard_down", [](BackendHandle& h, int shard, bool down) {
     return h.be->inject_shard_down(shard, down);
   }, py::arg("backend"), py::arg("shard"), py::arg("down") = true);

@@ -109,6 +109,10 @@ void bind_router(py::module_& m) {
       .def_property_readonly("nhot", &HostRouter::nhot)
       .def_property_readonly("cumulative", &HostRouter::cumulative)
       .def_property("lanes", &HostRouter::lanes, &HostRouter::set_lanes)
+      .def_property_readonly("publications", &HostRouter::publications)
+      .def("hot_rank", [](const HostRouter& r, uint64_t lo, uint64_t hi) {
+        return r.hot_rank(Digest{lo, hi});
+      })
       .def("owner", [](const HostRouter& r, uint64_t lo, uint64_t hi) {
         return r.owner(Digest{lo, hi});
       })
@@ -131,6 +135,27 @@ void bind_router(py::module_& m) {
         r.route_sets(P<const Digest>(keys), n, P<int32_t>(dest), P<int64_t>(counts), threads);
       }, py::arg("keys"), py::arg("n"), py::arg("dest"), py::arg("counts"),
          py::arg("threads") = 1);
+
+  // plan_hot (host_router.h) over (lo, hi, count) rows with the router's owners
+  m.def("plan_hot", [](const HostRouter& router, std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> rows,
+                       int k, uint64_t eligible, double spray_above, uint64_t min_count) {
+    std::vector<std::pair<Digest, uint64_t>> c;
+    c.reserve(rows.size());
+    for (auto& t : rows) c.emplace_back(Digest{std::get<0>(t), std::get<1>(t)}, std::get<2>(t));
+    const HotPlan p = plan_hot(c, k, router.nshards(), eligible,
+                               [&](const Digest& d) { return router.owner(d); }, spray_above,
+                               min_count);
+    py::list hot;
+    for (const Digest& d : p.hot) hot.append(py::make_tuple(d.lo, d.hi));
+    py::dict out;
+    out["hot"] = hot;
+    out["rank"] = p.rank;
+    out["weights"] = p.weights;
+    out["hot_share"] = p.hot_share;
+    out["planned"] = p.planned;
+    return out;
+  }, py::arg("router"), py::arg("rows"), py::arg("k"), py::arg("eligible"),
+     py::arg("spray_above"), py::arg("min_count") = 2);
 
   m.def("step_streams", [](int device) {
     const StepStreams& ss = step_streams(device);

@@ -17,7 +17,11 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supp
 }  // namespace
 
 HostRouter::HostRouter(int nshards, int pps)
-    : n_(nshards), span_(65536, 0), hot_tab_(1), hot_bits_(1, 0), lanes_(kHaveAvx512) {
+    : n_(nshards), span_(65536, 0), lanes_(kHaveAvx512), readers_(new ReadSlot[kReadSlots]) {
+  for (int i = 0; i < kReadSlots; ++i) {
+    readers_[i].c[0].store(0, std::memory_order_relaxed);
+    readers_[i].c[1].store(0, std::memory_order_relaxed);
+  }
   SH_CHECK(nshards >= 1 && nshards <= 1023 && pps >= 1, "bad router geometry");
   std::vector<std::pair<uint32_t, int>> pts;
   for (int i = 0; i < nshards; ++i)
@@ -61,19 +65,21 @@ HostRouter::HostRouter(int nshards, int pps)
     }
     span_[s] = c1 | c2 << 16 | o1 << 32 | o2 << 42 | o3 << 52 | (k > 2 ? 1ull << 63 : 0ull);
   }
-  cw_.assign((size_t)n_, 0.0);
-  for (int r = 0; r < n_; ++r) cw_[(size_t)r] = (double)(r + 1) / n_;
-  cw_.back() = 1.0;
-  set_thresholds();
+  auto* t = new HotTable;
+  t->cw.assign((size_t)n_, 0.0);
+  for (int r = 0; r < n_; ++r) t->cw[(size_t)r] = (double)(r + 1) / n_;
+  t->cw.back() = 1.0;
+  set_thresholds(t);
+  hot_.store(t, std::memory_order_release);
 }
 
 void HostRouter::set_lanes(bool on) { lanes_ = on && kHaveAvx512; }
 
-void HostRouter::set_thresholds() {
+void HostRouter::set_thresholds(HotTable* t) const {
   // cw <= x * 2^-53 <=> x >= ceil(cw * 2^53) for an integer x < 2^53 (exact in doubles)
-  spray_t_.assign(cw_.size(), 0);
-  for (size_t k = 0; k < cw_.size(); ++k)
-    spray_t_[k] = (uint64_t)std::ceil(cw_[k] * 9007199254740992.0);
+  t->spray_t.assign(t->cw.size(), 0);
+  for (size_t k = 0; k < t->cw.size(); ++k)
+    t->spray_t[k] = (uint64_t)std::ceil(t->cw[k] * 9007199254740992.0);
 }
 
 HostRouter::~HostRouter() {
@@ -83,6 +89,7 @@ HostRouter::~HostRouter() {
   }
   cv_.notify_all();
   for (auto& t : pool_) t.join();
+  delete hot_.load(std::memory_order_acquire);
 }
 
 int HostRouter::search(uint32_t p) const {
@@ -90,32 +97,69 @@ int HostRouter::search(uint32_t p) const {
   return own_[it == pts_.end() ? 0 : (size_t)(it - pts_.begin())];
 }
 
+// ---- readers and the grace period -------------------------------------------------
+namespace {
+std::atomic<unsigned> g_next_slot{0};
+int my_read_slot(int slots) {
+  thread_local int s = (int)(g_next_slot.fetch_add(1, std::memory_order_relaxed) % (unsigned)slots);
+  return s;
+}
+}  // namespace
+
+HostRouter::Read::Read(const HostRouter& r) : r_(r), slot_(my_read_slot(kReadSlots)) {
+  // count in first, then read the table: a writer that published after our count sees it
+  // (seq_cst on both sides), one that published before is the table we read
+  phase_ = (int)(r.phase_.load(std::memory_order_seq_cst) & 1);
+  r.readers_[slot_].c[phase_].fetch_add(1, std::memory_order_seq_cst);
+  t_ = r.hot_.load(std::memory_order_seq_cst);
+}
+
+HostRouter::Read::~Read() {
+  r_.readers_[slot_].c[phase_].fetch_sub(1, std::memory_order_release);
+}
+
+void HostRouter::grace_period() {
+  // Two phase flips, each followed by a wait for the old phase's readers (the classic
+  // sleepable-RCU argument: one flip is not enough for a reader that read the phase, then
+  // stalled before counting itself in, across a whole earlier grace period).
+  for (int round = 0; round < 2; ++round) {
+    const uint64_t p = phase_.fetch_add(1, std::memory_order_seq_cst) & 1;
+    for (int spins = 0;; ++spins) {
+      int64_t s = 0;
+      for (int i = 0; i < kReadSlots; ++i) s += readers_[i].c[p].load(std::memory_order_seq_cst);
+      if (s == 0) break;
+      if (spins < 64) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+  }
+}
+
+int64_t HostRouter::nhot() const { return Read(*this).table().nhot; }
+
+std::vector<double> HostRouter::cumulative() const { return Read(*this).table().cw; }
+
 void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, const double* w) {
-  nhot_ = 0;
-  hot_tab_.assign(1, HotSlot{});
-  hot_mask_ = 0;
-  hot_bits_.assign(1, 0);
-  bits_mask_ = 0;
+  std::unique_ptr<HotTable> t(new HotTable);
   if (n > 0) {
     uint64_t slots = 1024;
     while (slots < 4 * (uint64_t)n) slots <<= 1;
-    hot_tab_.assign(slots, HotSlot{});
-    hot_mask_ = slots - 1;
+    t->tab.assign(slots, HotSlot{});
+    t->mask = slots - 1;
     uint64_t bits = 1 << 12;
     while (bits < 16 * (uint64_t)n) bits <<= 1;
-    hot_bits_.assign(bits / 64, 0);
-    bits_mask_ = bits - 1;
+    t->bits.assign(bits / 64, 0);
+    t->bits_mask = bits - 1;
     // in the given order (hottest first, HotSpread.plan): the hottest keep their home slot
     for (int64_t i = 0; i < n; ++i) {
       const Digest d = hot[i];
       if (!d.lo && !d.hi) continue;
       const int32_t r = rank ? rank[i] : kSpray;
       SH_CHECK(r >= kSpray && r < n_, "designated rank out of range");
-      const uint64_t fb = (d.lo >> 20) & bits_mask_;
-      hot_bits_[fb >> 6] |= 1ull << (fb & 63);
+      const uint64_t fb = (d.lo >> 20) & t->bits_mask;
+      t->bits[fb >> 6] |= 1ull << (fb & 63);
       const uint64_t tag = (d.hi & ~0xFFFFull) | (uint64_t)(r + 2);
-      for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
-        HotSlot& e = hot_tab_[s];
+      for (uint64_t s = d.lo & t->mask;; s = (s + 1) & t->mask) {
+        HotSlot& e = t->tab[s];
         if (e.lo == d.lo && ((e.tag ^ d.hi) >> 16) == 0 && (e.tag & 0xFFFF)) {
           e.tag = tag;  // a repeated digest: the last rank
           break;
@@ -123,7 +167,7 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
         if (!(e.tag & 0xFFFF)) {
           e.lo = d.lo;
           e.tag = tag;
-          ++nhot_;
+          ++t->nhot;
           break;
         }
       }
@@ -135,45 +179,51 @@ void HostRouter::set_hot(const Digest* hot, int64_t n, const int32_t* rank, cons
     tot += w[r];
   }
   SH_CHECK(tot > 0, "spray weights sum to zero");
+  t->cw.assign((size_t)n_, 0.0);
   double acc = 0;
   for (int r = 0; r < n_; ++r) {
     acc += w[r];
-    cw_[(size_t)r] = acc / tot;
+    t->cw[(size_t)r] = acc / tot;
   }
-  cw_.back() = 1.0;
-  set_thresholds();
+  t->cw.back() = 1.0;
+  set_thresholds(t.get());
+  std::lock_guard<std::mutex> lk(set_mu_);
+  const HotTable* old = hot_.exchange(t.release(), std::memory_order_seq_cst);
+  grace_period();  // nobody reads `old` any more
+  delete old;
+  pubs_.fetch_add(1, std::memory_order_relaxed);
 }
 
-uint32_t HostRouter::hot_code_slow(const Digest& d) const {
-  for (uint64_t s = d.lo & hot_mask_;; s = (s + 1) & hot_mask_) {
-    const HotSlot& e = hot_tab_[s];
-    if (hot_match(e, d)) return (uint32_t)(e.tag & 0xFFFFu);
+uint32_t HostRouter::HotTable::code_slow(const Digest& d) const {
+  for (uint64_t s = d.lo & mask;; s = (s + 1) & mask) {
+    const HotSlot& e = tab[s];
+    if (match(e, d)) return (uint32_t)(e.tag & 0xFFFFu);
     if (!(e.tag & 0xFFFFu)) return 0;
   }
 }
 
-int HostRouter::spray(uint64_t j) const {
+int HostRouter::HotTable::spray(uint64_t j) const {
   const double u = (double)((j * kWeyl) >> 11) * (1.0 / 9007199254740992.0);  // 2^-53
   int r = 0;  // #{cw <= u} over the first n - 1 weights, branch-free (the rank is random)
-  for (int k = 0; k < n_ - 1; ++k) r += cw_[(size_t)k] <= u;
+  for (size_t k = 0; k + 1 < cw.size(); ++k) r += cw[k] <= u;
   return r;
 }
 
 template <bool kSets>
-int HostRouter::route_one(const Digest& d, uint64_t j) const {
-  const uint32_t c = nhot_ ? hot_code(d) : 0;
+int HostRouter::route_one(const HotTable& t, const Digest& d, uint64_t j) const {
+  const uint32_t c = t.nhot ? t.code(d) : 0;
   if (kSets) return c ? -1 : owner(d);
-  return c >= 2 ? (int)c - 2 : c == 1 ? spray(j) : owner(d);
+  return c >= 2 ? (int)c - 2 : c == 1 ? t.spray(j) : owner(d);
 }
 
 template <bool kSets>
-void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t seq0,
-                             int32_t* dest, int64_t* counts) const {
+void HostRouter::route_range(const HotTable& t, const Digest* keys, int64_t a, int64_t b,
+                             uint64_t seq0, int32_t* dest, int64_t* counts) const {
   if (lanes_) {
-    route_x8<kSets>(keys, a, b, seq0, dest, counts);
+    route_x8<kSets>(t, keys, a, b, seq0, dest, counts);
     return;
   }
-  if (!nhot_) {
+  if (!t.nhot) {
     for (int64_t i = a; i < b; ++i) {
       const int o = owner(keys[i]);
       dest[i] = o;
@@ -183,9 +233,9 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
   }
   // locals: the stores through dest / counts cannot make the compiler reload any of these
   const uint64_t* const span = span_.data();
-  const uint64_t* const bits = hot_bits_.data();
-  const HotSlot* const tab = hot_tab_.data();
-  const uint64_t bmask = bits_mask_, hmask = hot_mask_;
+  const uint64_t* const bits = t.bits.data();
+  const HotSlot* const tab = t.tab.data();
+  const uint64_t bmask = t.bits_mask, hmask = t.mask;
   for (int64_t i = a; i < b; ++i) {
     const Digest d = keys[i];
     // owner (owner()'s span rule)
@@ -197,20 +247,20 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     } else {
       // t <= c1 ? o1 : t <= c2 ? o2 : o3, by masks (g++ turned the ternaries into branches
       // that mispredict on a random stream)
-      const uint32_t t = p & 0xFFFFu;
-      const uint32_t s1 = 0u - (uint32_t)(t <= (se & 0xFFFFu));
-      const uint32_t s2 = 0u - (uint32_t)(t <= ((se >> 16) & 0xFFFFu));
+      const uint32_t tt = p & 0xFFFFu;
+      const uint32_t s1 = 0u - (uint32_t)(tt <= (se & 0xFFFFu));
+      const uint32_t s2 = 0u - (uint32_t)(tt <= ((se >> 16) & 0xFFFFu));
       const uint32_t o1 = (se >> 32) & 1023, o2 = (se >> 42) & 1023, o3 = (se >> 52) & 1023;
       const uint32_t x = o3 ^ ((o2 ^ o3) & s2);
       o = (int)(x ^ ((o1 ^ x) & s1));
     }
-    // hot code (hot_code()'s rule)
+    // hot code (HotTable::code()'s rule)
     const uint64_t fb = (d.lo >> 20) & bmask;
     const uint64_t pass = (bits[fb >> 6] >> (fb & 63)) & 1;
     const HotSlot& e = tab[d.lo & hmask];
-    const uint64_t hit = pass & (uint64_t)hot_match(e, d);
+    const uint64_t hit = pass & (uint64_t)HotTable::match(e, d);
     const uint32_t c = __builtin_expect(pass & (hit ^ 1), 0)
-                           ? hot_code_slow(d)
+                           ? t.code_slow(d)
                            : (uint32_t)(e.tag & 0xFFFFu & ((uint64_t)0 - hit));
     if (kSets) {
       if (c) {  // (SETs: a hot object's share of a SET stream is small and predictable)
@@ -223,7 +273,7 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
     } else {
       const uint32_t sel = 0u - (uint32_t)(c >= 2);  // a select by mask, not a branch
       int r = (int)((uint32_t)o ^ (((c - 2) ^ (uint32_t)o) & sel));
-      if (c == 1) r = spray(seq0 + (uint64_t)i);  // the few sprayed objects
+      if (c == 1) r = t.spray(seq0 + (uint64_t)i);  // the few sprayed objects
       dest[i] = r;
       ++counts[r];
     }
@@ -239,11 +289,11 @@ void HostRouter::route_range(const Digest* keys, int64_t a, int64_t b, uint64_t 
 // store-to-load forwarding). SETs (kSets): a hot object's lane is -1 (every rank).
 template <bool kSets>
 __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_x8(
-    const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
+    const HotTable& ht, const Digest* keys, int64_t a, int64_t b, uint64_t seq0, int32_t* dest,
     int64_t* counts) const {
   const long long* const span = reinterpret_cast<const long long*>(span_.data());
-  const long long* const bits = reinterpret_cast<const long long*>(hot_bits_.data());
-  const long long* const tab = reinterpret_cast<const long long*>(hot_tab_.data());
+  const long long* const bits = reinterpret_cast<const long long*>(ht.bits.data());
+  const long long* const tab = reinterpret_cast<const long long*>(ht.tab.data());
   const __m512i ilo = _mm512_setr_epi64(0, 2, 4, 6, 8, 10, 12, 14);
   const __m512i ihi = _mm512_setr_epi64(1, 3, 5, 7, 9, 11, 13, 15);
   const __m512i m16 = _mm512_set1_epi64(0xFFFF), m1023 = _mm512_set1_epi64(1023);
@@ -251,9 +301,9 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_x8(
   const __m512i zero = _mm512_setzero_si512(), m63 = _mm512_set1_epi64(63);
   const __m512i lane = _mm512_setr_epi64(0, 1, 2, 3, 4, 5, 6, 7);
   const __m512i weyl = _mm512_set1_epi64((long long)kWeyl);
-  const __m512i bmask = _mm512_set1_epi64((long long)bits_mask_);
-  const __m512i hmask = _mm512_set1_epi64((long long)hot_mask_);
-  const bool hot = nhot_ != 0;
+  const __m512i bmask = _mm512_set1_epi64((long long)ht.bits_mask);
+  const __m512i hmask = _mm512_set1_epi64((long long)ht.mask);
+  const bool hot = ht.nhot != 0;
   constexpr int64_t kBlock = 2048;  // counted while the block's ranks are in L1
   uint32_t cnt[4][1024];
   for (auto& c : cnt) std::fill(c, c + n_, 0u);
@@ -322,7 +372,7 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_x8(
               __m512i r = zero;
               for (int k = 0; k < n_ - 1; ++k)
                 r = _mm512_mask_add_epi64(
-                    r, _mm512_cmpge_epu64_mask(x, _mm512_set1_epi64((long long)spray_t_[(size_t)k])),
+                    r, _mm512_cmpge_epu64_mask(x, _mm512_set1_epi64((long long)ht.spray_t[(size_t)k])),
                     r, one);
               o = _mm512_mask_mov_epi64(o, spr, r);
             } else {
@@ -336,10 +386,10 @@ __attribute__((target("avx512f,avx512dq"))) void HostRouter::route_x8(
       if (__builtin_expect(redo != 0, 0))
         for (unsigned m = redo; m; m &= m - 1) {
           const int l = __builtin_ctz(m);
-          dest[i + l] = route_one<kSets>(keys[i + l], seq0 + (uint64_t)(i + l));
+          dest[i + l] = route_one<kSets>(ht, keys[i + l], seq0 + (uint64_t)(i + l));
         }
     }
-    for (; i < c1; ++i) dest[i] = route_one<kSets>(keys[i], seq0 + (uint64_t)i);
+    for (; i < c1; ++i) dest[i] = route_one<kSets>(ht, keys[i], seq0 + (uint64_t)i);
     if (kSets) {  // -1 (a hot object's SET) counts once for every rank
       for (i = c0; i < c1; ++i) {
         const int32_t r = dest[i];
@@ -413,16 +463,86 @@ void HostRouter::parallel(int64_t n, int threads, int64_t* counts,
 
 void HostRouter::route_gets(const Digest* keys, int64_t n, uint64_t seq0, int32_t* dest,
                             int64_t* counts, int threads) const {
+  const Read rd(*this);  // one table for the whole call
   parallel(n, threads, counts, [&](int64_t a, int64_t b, int64_t* c) {
-    route_range<false>(keys, a, b, seq0, dest, c);
+    route_range<false>(rd.table(), keys, a, b, seq0, dest, c);
   });
 }
 
 void HostRouter::route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_t* counts,
                             int threads) const {
+  const Read rd(*this);
   parallel(n, threads, counts, [&](int64_t a, int64_t b, int64_t* c) {
-    route_range<true>(keys, a, b, 0, dest, c);
+    route_range<true>(rd.table(), keys, a, b, 0, dest, c);
   });
+}
+
+HotPlan plan_hot(const std::vector<std::pair<Digest, uint64_t>>& counts, int k, int nshards,
+                 uint64_t eligible, const std::function<int(const Digest&)>& owner,
+                 double spray_above, uint64_t min_count) {
+  HotPlan p;
+  p.weights.assign((size_t)nshards, 0.0);
+  p.planned.assign((size_t)nshards, 0.0);
+  std::vector<int> el;
+  for (int r = 0; r < nshards; ++r)
+    if ((eligible >> r) & 1) {
+      el.push_back(r);
+      p.weights[(size_t)r] = 1.0;
+    }
+  uint64_t total = 0;
+  for (const auto& c : counts) total += c.second;
+  if (k <= 0 || el.empty() || total == 0) {
+    if (el.empty()) p.weights.assign((size_t)nshards, 1.0);
+    return p;
+  }
+  // the top k by count (ties by digest, so every caller with the same counts agrees; the
+  // low word compared as a signed int64, the order HotSpread.design's tensors sort in)
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < counts.size(); ++i)
+    if (counts[i].second >= min_count) idx.push_back(i);
+  auto hotter = [&](size_t a, size_t b) {
+    const auto &x = counts[a], &y = counts[b];
+    if (x.second != y.second) return x.second > y.second;
+    if (x.first.lo != y.first.lo) return (int64_t)x.first.lo < (int64_t)y.first.lo;
+    return (int64_t)x.first.hi < (int64_t)y.first.hi;
+  };
+  if ((int64_t)idx.size() > k) {
+    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), hotter);
+    idx.resize((size_t)k);
+  } else {
+    std::sort(idx.begin(), idx.end(), hotter);
+  }
+  std::vector<uint8_t> is_hot(counts.size(), 0);
+  uint64_t hot_total = 0;
+  for (size_t i : idx) {
+    is_hot[i] = 1;
+    hot_total += counts[i].second;
+  }
+  p.hot_share = (double)hot_total / (double)total;
+  // loads: the non-hot sampled GETs at their owners (an ineligible owner's requests stay
+  // there: that rank is not a target for hot GETs)
+  std::vector<double> load((size_t)nshards, 0.0);
+  for (size_t i = 0; i < counts.size(); ++i)
+    if (!is_hot[i]) load[(size_t)owner(counts[i].first)] += (double)counts[i].second;
+  const double thr = spray_above * (double)total;
+  double sprayed = 0;
+  for (size_t i : idx)
+    if ((double)counts[i].second > thr) sprayed += (double)counts[i].second;
+  for (int r : el) load[(size_t)r] += sprayed / (double)el.size();
+  for (size_t i : idx) {
+    p.hot.push_back(counts[i].first);
+    if ((double)counts[i].second > thr) {
+      p.rank.push_back(-1);
+      continue;
+    }
+    int best = el[0];  // the least loaded eligible rank (lowest index on ties)
+    for (int r : el)
+      if (load[(size_t)r] < load[(size_t)best]) best = r;
+    load[(size_t)best] += (double)counts[i].second;
+    p.rank.push_back(best);
+  }
+  for (int r = 0; r < nshards; ++r) p.planned[(size_t)r] = load[(size_t)r] / (double)total;
+  return p;
 }
 
 }  // namespace shellac

@@ -55,7 +55,8 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                  sweep_s: int = 10, hbm_filter: bool = True, spin_us: int = 50,
                  depth: int = 3, evict: str = "clock", batch_timeout_ms: int = 2000,
                  edge_server: bool = True, batcher_cpus: Sequence[int] = (),
-                 serve_backlog: int = 2, direct: bool = True, serve_blocks: int = 8):
+                 serve_backlog: int = 2, direct: bool = True, serve_blocks: int = 8,
+                 hot_objects: int = 1024, hot_refresh_ms: int = 1000, hot_sample: int = 8):
     """Build a native cache backend.
 
     kind: ``memcached`` (ketama over ``caches``; the reference's configuration),
@@ -73,7 +74,11 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
     (no launch per batch); ``batcher_cpus`` pins the GPU batcher threads. ``direct``
     lets each proxy reactor write its own small GET batches to the edge server and poll
     their completion in its loop (no batcher-thread hop; larger batches still batch).
-    ``fault="gpu_down=K"`` ejects GPU shard K as a drill.
+    ``fault="gpu_down=K"`` ejects GPU shard K as a drill. With several GPUs,
+    ``hot_objects`` (0: off) is the size of the replicated hot set: the most requested
+    objects of a sampled GET stream live on every GPU, their GETs spread over the GPUs and
+    their SETs / DELETEs written through, re-planned every ``hot_refresh_ms`` (0: only on
+    ``hot_refresh(backend)``) from one GET in ``hot_sample``.
     """
     c = core()
     if kind == "none":
@@ -87,7 +92,9 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              spin_us=spin_us, depth=depth, evict=evict,
                              batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
                              batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
-                             direct=direct, serve_blocks=serve_blocks)
+                             direct=direct, serve_blocks=serve_blocks,
+                             hot_objects=hot_objects, hot_refresh_ms=hot_refresh_ms,
+                             hot_sample=hot_sample)
         return c.fault_backend(inner, fault)
     if l1_mb and kind in ("hbm", "memcached"):
         l2 = make_backend(kind, caches=caches, gpus=gpus, hbm_gb=hbm_gb, max_item=max_item,
@@ -95,7 +102,9 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                           hbm_filter=hbm_filter, spin_us=spin_us, depth=depth, evict=evict,
                           batch_timeout_ms=batch_timeout_ms, edge_server=edge_server,
                           batcher_cpus=batcher_cpus, serve_backlog=serve_backlog,
-                          direct=direct, serve_blocks=serve_blocks)
+                          direct=direct, serve_blocks=serve_blocks,
+                          hot_objects=hot_objects, hot_refresh_ms=hot_refresh_ms,
+                             hot_sample=hot_sample)
         return c.tiered_backend(c.dram_backend(int(l1_mb) << 20, max_item), l2, promote_ttl)
     if kind == "memcached":
         if not caches:
@@ -115,8 +124,15 @@ def make_backend(kind: str = "dram", *, caches: Sequence[ServerSpec] = (),
                              edge_server=edge_server,
                              batcher_cpus=[int(x) for x in batcher_cpus],
                              serve_backlog=int(serve_backlog), direct=bool(direct),
-                             serve_blocks=int(serve_blocks))
+                             serve_blocks=int(serve_blocks), hot_objects=int(hot_objects),
+                             hot_refresh_ms=int(hot_refresh_ms), hot_sample=int(hot_sample))
     raise ValueError(f"unknown cache backend {kind!r}")
+
+
+def hot_refresh(backend) -> dict:
+    """Re-plan an HBM tier's replicated hot set now (what its refresh thread does every
+    ``hot_refresh_ms``); returns the refresh's counts ({} when the tier has no hot set)."""
+    return dict(core().hot_refresh(backend))
 
 
 def set_fault(backend, spec: str) -> None:
@@ -275,6 +291,11 @@ def build_arg_parser() -> argparse.ArgumentParser:
                         "reactors send small GET batches to the edge server themselves)")
     p.add_argument("--batcher-cpus", default="",
                    help="--cache hbm: pin the GPU batcher threads to these CPUs")
+    p.add_argument("--hot-objects", type=int, default=1024,
+                   help="--cache hbm on several GPUs: replicate this many of the most requested "
+                        "objects on every GPU and spread their GETs (0: plain ketama)")
+    p.add_argument("--hot-refresh-ms", type=int, default=1000,
+                   help="--cache hbm: how often the replicated hot set follows the traffic")
     p.add_argument("--stream-bytes", type=int, default=1 << 20,
                    help="stream responses larger than this to the client without caching them")
     p.add_argument("--decode-gzip", action="store_true",
@@ -311,7 +332,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                      "depth": args.hbm_depth, "evict": args.evict,
                      "edge_server": not args.no_edge_server,
                      "direct": not args.no_hbm_direct,
-                     "batcher_cpus": parse_cpus(args.batcher_cpus)}
+                     "batcher_cpus": parse_cpus(args.batcher_cpus),
+                     "hot_objects": args.hot_objects, "hot_refresh_ms": args.hot_refresh_ms}
                     if kind == "hbm" else {}),
                  **({"l1_mb": args.l1_mb} if kind in ("hbm", "memcached") else {}))
     print(f"Running Shellac on port {args.port} (cache: {kind})...", flush=True)

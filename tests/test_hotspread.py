@@ -83,3 +83,85 @@ def test_spreading_evens_out_a_zipf_stream(policy):
     assert float(c0.max() / c0.mean()) > 1.1
     assert float(c1.max() / c1.mean()) < 1.02, (c1 / c1.mean()).tolist()
     assert info["hot_share"] > 0.3
+
+
+def test_router_tables_swap_under_concurrent_routing():
+    """set_hot publishes a new immutable table while other threads route (the proxy's
+    reactors route every request while the hot-set refresh thread re-plans): each
+    route_gets call sees exactly one table, never a half-built one, and set_hot returns
+    only after the old table has no readers (it is freed there)."""
+    import threading
+
+    from shellac_amd import core
+
+    world = 4
+    r = core().HostRouter(world)
+    g = torch.Generator().manual_seed(3)
+    hot = torch.randint(-2**63, 2**63 - 1, (512, 2), dtype=torch.int64, generator=g)
+    # the routed batch: the hot objects only, so a call's ranks name its table
+    stream = hot[torch.randint(0, 512, (70000,), generator=g)].contiguous()
+    tables = []
+    for t in range(world):  # table t designates every hot object to rank t
+        ranks = torch.full((512,), t, dtype=torch.int32)
+        tables.append(ranks)
+    w = [1.0] * world
+    stop = threading.Event()
+    bad = []
+
+    def route():
+        dest = torch.empty(stream.shape[0], dtype=torch.int32)
+        counts = torch.zeros(world, dtype=torch.int64)
+        while not stop.is_set():
+            counts.zero_()
+            r.route_gets(stream.data_ptr(), stream.shape[0], 0, dest.data_ptr(),
+                         counts.data_ptr(), 2)
+            u = torch.unique(dest)
+            if u.numel() != 1 or int(counts.max()) != stream.shape[0]:
+                bad.append(u.tolist())
+
+    r.set_hot(hot.data_ptr(), 512, tables[0].data_ptr(), w)  # before any reader starts
+    ths = [threading.Thread(target=route) for _ in range(3)]
+    for th in ths:
+        th.start()
+    try:
+        for i in range(200):
+            ranks = tables[i % world]
+            r.set_hot(hot.data_ptr(), 512, ranks.data_ptr(), w)
+            assert r.nhot == 512
+            # after set_hot returned, every decision uses the new table
+            lo, hi = int(hot[7, 0]) & (2**64 - 1), int(hot[7, 1]) & (2**64 - 1)
+            assert r.hot_rank(lo, hi) == i % world
+    finally:
+        stop.set()
+        for th in ths:
+            th.join()
+    assert not bad, bad[:5]
+    assert r.publications == 201
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_native_hot_plan_matches_hotspread_design(world):
+    """plan_hot (the proxy HBM tier's planner, host_router.cc) makes HotSpread.design's
+    decisions on the same sample: the same hot set in the same order, the same designated
+    ranks (sprayed -1 above 1/(4N)) and the same planned loads."""
+    from shellac_amd import core
+
+    g = torch.Generator().manual_seed(world)
+    keys = torch.randint(-2**63, 2**63 - 1, (3000, 2), dtype=torch.int64, generator=g)
+    p = 1.0 / torch.arange(1, 3001, dtype=torch.float64) ** 0.99
+    sample = keys[torch.multinomial(p, 40000, replacement=True, generator=g)]
+    hs = HotSpread(world, "cpu")
+    hot, ranks, _, info = hs.design(sample, 200)
+    u, cnt = torch.unique(sample, dim=0, return_counts=True)
+    rows = [(int(a) & (2**64 - 1), int(b) & (2**64 - 1), int(c))
+            for (a, b), c in zip(u.tolist(), cnt.tolist())]
+    plan = core().plan_hot(hs.router, rows, 200, (1 << world) - 1, 1.0 / (4 * world), 1)
+    want = [(int(a) & (2**64 - 1), int(b) & (2**64 - 1)) for a, b in hot.tolist()]
+    assert [tuple(x) for x in plan["hot"]] == want
+    assert plan["rank"] == ranks.tolist()
+    assert abs(plan["hot_share"] - info["hot_share"]) < 1e-6  # (the tensor mean is fp32)
+    assert plan["planned"] == pytest.approx(info["planned_load"], abs=1e-12)
+    # only eligible ranks are designation / spray targets
+    el = (1 << world) - 1 - 2
+    plan = core().plan_hot(hs.router, rows, 200, el, 1.0 / (4 * world), 1)
+    assert 1 not in plan["rank"] and plan["weights"][1] == 0.0
