@@ -20,14 +20,20 @@ Per-GPU work is fixed as N grows (weak scaling): the key space is N x --keys-per
 
 Headline (``--headline pressured``): the full cache — a shard log sized so its working set
 (every key it holds, one record each) fills --pressured-fill (0.8) of it, wrapped, so every
-SET batch's CLOCK hand re-appends the objects read since it last passed and evicts the rest
-(hit ratio < 1). Secondary: the fresh cache (``log_fresh``), a 16 GiB log that has
-wrapped with the working set at ~1/4 of it (``log_wrapped``), and a working set
---overfull-fill (1.25) times the log (``log_overfull``: its SETs walk every key and its GETs
-come from --walk-get-batches fresh batches, so an evicted key misses until re-SET). The
-full-cache blocks also report ``request_hit_ratio`` (duplicates included, untimed steps).
-Pooled capacity (scripts/pooled_capacity.sh): ``--keys-total`` fixes the key space across N
-and ``--set-walk`` gives the headline block the overfull block's batches. A simulated
+SET batch's CLOCK hand re-appends the objects read since it last passed and evicts the rest.
+Its request stream is the walk (``walk_batches``): the SETs walk a permutation of every key
+the shard holds and the GETs are --walk-get-batches (256) fresh batches of the Zipf
+stream, more than a log lap of steps, so the keys read over a lap are nearly the whole key
+space (``read_working_set_over_capacity``: their records over the log, ~0.78 at the
+defaults) rather than the ~1/2 of it 16 cycled batches touch. Secondary: the same full
+cache on the 16 cycled GET / SET batches (``log_pressured_cycled``, the round-5 headline),
+the fresh cache (``log_fresh``), a 16 GiB log that has wrapped with the working set at ~1/4
+of it (``log_wrapped``), and a working set --overfull-fill (1.25) times the log
+(``log_overfull``, on the walk too, so an evicted key misses until re-SET). The full-cache
+blocks also report ``request_hit_ratio`` (duplicates included, untimed steps).
+Pooled capacity (scripts/pooled_capacity.sh): ``--keys-total`` fixes the key space across N.
+Host routing (N > 1): ``value`` is bounded by what the host routers can feed — the measured
+native router rate times N — when that is below the job's rate. A simulated
 host-routed world also runs ``spread_drift``: the spread hot set refreshed incrementally
 (parallel/hotspread.py refresh_hot) under a drifting popularity order.
 
@@ -75,10 +81,15 @@ def parse():
                     help="GET batches of the request stream pre-generated for --set-walk and "
                          "log_overfull (cycled; more than a log lap of steps, so a key's "
                          "re-reads are the stream's, not the cycle's)")
-    ap.add_argument("--set-walk", action="store_true",
-                    help="the full-cache blocks' SETs walk a permutation of every key the shard "
-                         "holds (each re-SET once per keys/sets steps) instead of cycling the "
-                         "pre-generated SET batches: an evicted key comes back")
+    ap.add_argument("--set-walk", dest="set_walk", action="store_true", default=True,
+                    help="(default) the headline full-cache block runs on the walk: its SETs walk "
+                         "a permutation of every key the shard holds (each re-SET once per "
+                         "keys/sets steps) and its GETs are --walk-get-batches fresh batches")
+    ap.add_argument("--cycled-headline", dest="set_walk", action="store_false",
+                    help="the headline full-cache block cycles the 16 pre-generated GET / SET "
+                         "batches instead (the round-5 headline: ~1/2 of the keys read)")
+    ap.add_argument("--no-cycled", action="store_true",
+                    help="skip the secondary log_pressured_cycled block")
     ap.add_argument("--zipf", type=float, default=0.99)
     ap.add_argument("--min-val", type=int, default=64)
     ap.add_argument("--max-val", type=int, default=4096)
@@ -207,6 +218,24 @@ def parse():
                          "moves (early), or at the head of the SET chain (inline)")
     ap.add_argument("--check", action="store_true", help="verify a sample of GET values")
     return ap.parse_args()
+
+
+def router_bound(out: dict, router_req_per_s: float, world: int) -> dict:
+    """The host-routed headline bounded by its router: value =
+    min(job rate, N x the measured native router rate); ms_per_step follows the value.
+    Returns the updated fields (``value``, ``ms_per_step``, ``host_routing``)."""
+    hr_ = dict(out["host_routing"])
+    value, ms = out["value"], out["ms_per_step"]
+    cap_ = router_req_per_s * world
+    hr_["host_route_job_capacity_req_per_s"] = round(cap_, 1)
+    hr_["router_feeds_job"] = bool(cap_ >= value)
+    hr_["job_rate_req_per_s"] = value
+    hr_["job_ms_per_step"] = ms
+    if cap_ < value:
+        ms = round(ms * value / cap_, 4)
+        value = round(cap_, 1)
+    hr_["value_bounded_by_router"] = not hr_["router_feeds_job"]
+    return {"value": value, "ms_per_step": ms, "host_routing": hr_}
 
 
 def _free_port() -> int:
@@ -1062,6 +1091,21 @@ def main():
             lap_el = timed(lap_steps, fbase + ffill + 3 * args.steps, cache=f_sc)[0]
             out_["lap_steps"] = lap_steps
             out_["lap_ms_per_step"] = round(lap_el / lap_steps * 1e3, 4)
+            # the read working set: distinct keys the GET batches of one lap of steps read
+            # (the stream's, the batches cycled when a lap is longer), as records over the log
+            nb_ = len(cyc["get_ids"])
+            seen = torch.zeros(int(wl.vlen.numel()), dtype=torch.bool, device=dev)
+            for j in range(min(lap_steps, nb_)):
+                seen[cyc["get_ids"][(fbase + ffill + j) % nb_].to(dev)] = True
+            rid = seen.nonzero().flatten()
+            rbytes = int((32 + ((wl.vlen.index_select(0, rid).long() + 15) & ~15)).sum())
+            rk = torch.tensor([rbytes, int(rid.numel())], dtype=torch.int64, device=rdev)
+            if real_world > 1:
+                dist.all_reduce(rk, op=dist.ReduceOp.MAX)  # (the rank that reads the most)
+            out_["read_working_set_over_capacity"] = round(int(rk[0]) / f_log, 4)
+            out_["read_keys_per_lap"] = int(rk[1])
+            out_["get_batches_per_lap"] = min(lap_steps, nb_)
+            del seen, rid
         f_sc.sync_sets()
         cyc["gets"], cyc["get_ids"], cyc["sets"] = gets, get_ids, sets
         del f_sc, f_shard
@@ -1093,15 +1137,24 @@ def main():
         return gd_, gi, ws_
 
     pressured = pw = piv = pfill = None
+    pressured_cycled = None
+    wb = None  # the walk: built once, shared by the headline and log_overfull
+    if do_pressured and (args.set_walk or (args.overfull_fill > 0 and args.pressured_gb is None)):
+        wb = walk_batches()
     if do_pressured:
-        wb = walk_batches() if args.set_walk else None
+        walk = wb if args.set_walk else None
         pressured, pw, piv, pfill = full_cache(
             p_gb, args.check and headline == "pressured",
-            min_fill=2 * len(wb[2]) if wb else 0, walk=wb)
-        if wb and pressured is not None:
-            pressured["set_batches_cycled"] = len(wb[2])
-            pressured["get_batches_cycled"] = len(wb[0])
-        del wb
+            min_fill=2 * len(walk[2]) if walk else 0, walk=walk)
+        if pressured is not None:
+            pressured["stream"] = "walk" if walk else "cycled"
+            pressured["set_batches_cycled"] = len(walk[2]) if walk else len(cyc["sets"])
+            pressured["get_batches_cycled"] = len(walk[0]) if walk else len(cyc["gets"])
+        if walk is not None and not args.no_cycled:
+            # secondary: the same full cache on the 16 cycled batches (round 5's headline)
+            pressured_cycled = full_cache(p_gb, False)[0]
+            if pressured_cycled is not None:
+                pressured_cycled["stream"] = "cycled"
     # secondary: a working set larger than the log (--overfull-fill x the log): the hit ratio
     # when the cache cannot hold every key
     overfull = None
@@ -1112,13 +1165,12 @@ def main():
         # populate itself wraps this log, evicting unread objects in key order: two passes
         # of the walk run before the window, so it sees the steady state, not the populate's
         # transient.
-        wb = walk_batches()
         overfull = full_cache(ws_bytes / args.overfull_fill / (1 << 30), False,
                               min_fill=2 * len(wb[2]), walk=wb)[0]
         if overfull is not None:
             overfull["set_batches_cycled"] = len(wb[2])
             overfull["get_batches_cycled"] = len(wb[0])
-        del wb
+    del wb
     if headline == "pressured" and pw is None:
         raise SystemExit("[bench] the pressured log could not be wrapped for the headline; "
                          "pass --headline wrapped")
@@ -1329,6 +1381,8 @@ def main():
         "log_wrapped": summary(wrapped, wrapped_iv, fill=nfill) if wrapped else None,
         # the full cache (the default headline): reinsertions and evictions every step
         "log_pressured": pressured,
+        # the same full cache on the 16 cycled GET / SET batches (~1/2 of the keys read)
+        "log_pressured_cycled": pressured_cycled,
         # the working set --overfull-fill x the log (more keys than the cache holds)
         "log_overfull": overfull,
         # a drifting hot set with the replica maintained between epochs (N>1 / simulated)
@@ -1339,11 +1393,10 @@ def main():
     }
     if host_route and out["host_routing"] and "host_route_req_per_s" in out["host_routing"]:
         # what the host proxies can feed: one router per GPU share of the host's cores (the
-        # measured rate is this process's, on its share), against the job's request rate
-        hr_ = out["host_routing"]
-        cap_ = hr_["host_route_req_per_s"] * world
-        hr_["host_route_job_capacity_req_per_s"] = round(cap_, 1)
-        hr_["router_feeds_job"] = bool(cap_ >= value)
+        # measured rate is this process's, on its share), against the job's request rate.
+        # The routing of the timed steps' batches was done beforehand, so the job rate alone
+        # could claim more than the routers deliver: the headline is the smaller of the two.
+        out.update(router_bound(out, route_info["host_route_req_per_s"], world))
     if host_edge:
         # responses delivered into pinned host memory (GPU -> host over PCIe) against the
         # PCIe 5.0 x16 roofline (~63 GB/s per direction); the keys and SET payloads
