@@ -122,9 +122,10 @@ PYBIND11_MODULE(_shellac_core, m) {
                     S(s), done_slot);
       }, py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("out_cap"), py::arg("off"),
          py::arg("now"), py::arg("stream"), py::arg("done_slot") = -1)
-      // ordered after `stream` (the caller's current stream; 0 = the null stream): the
-      // resident server runs on no stream, so what the caller queued to fill `out` / `off`
-      // (or the keys' SETs) lands before the job is queued
+      // ordered after `stream` only (the caller's current stream; 0 = the null stream): the
+      // resident server runs on no stream, so what the caller queued there to fill `out` /
+      // `off` (or SETs queued on that stream) lands before the job is queued; SETs a
+      // ShardedCache queued on its own streams need its sync_sets() first
       .def("serve_get", [](HbmCache& c, uintptr_t host_keys, int64_t n, uintptr_t out,
                            uint64_t out_cap, uintptr_t off, uint32_t now, int done_slot,
                            uintptr_t stream) {
@@ -210,6 +211,9 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("debug_bucket", &HbmCache::debug_bucket)
       .def("debug_hand", &HbmCache::debug_hand)
       .def("debug_set_entry", &HbmCache::debug_set_entry)
+      .def("debug_set_hand", &HbmCache::debug_set_hand, py::arg("hand"), py::arg("catch_up") = true)
+      .def("retired_bytes", &HbmCache::retired_bytes, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("retired_ever", &HbmCache::retired_ever)
       .def("export_keys", [](HbmCache& c, uintptr_t out, uint64_t cap, uint32_t now, uintptr_t s) {
         py::gil_scoped_release nogil;
         return c.export_keys(P<Digest>(out), cap, now, S(s));
@@ -363,6 +367,7 @@ PYBIND11_MODULE(_shellac_core, m) {
       .def("debug_bucket", &HostCache::debug_bucket)
       .def("debug_hand", &HostCache::debug_hand)
       .def("debug_set_entry", &HostCache::debug_set_entry)
+      .def("debug_set_hand", &HostCache::debug_set_hand, py::arg("hand"), py::arg("catch_up") = true)
       .def("export_keys", [](HostCache& c, uintptr_t out, uint64_t cap, uint32_t now) {
         return c.export_keys(P<Digest>(out), cap, now);
       })

@@ -125,9 +125,11 @@ class HbmCache {
   static constexpr int kServeRing = 16;
   bool serve_get(const Digest* host_keys, int64_t n, uint8_t* out, uint64_t out_cap,
                  uint64_t* off, uint32_t now, int done_slot);
-  // The same, ordered after the work queued so far on stream `after` (the caller's: what
-  // it queued to fill `out` / `off` or the keys' SETs): an event recorded there is
-  // host-polled before the job is queued, so the stream-less server never races it.
+  // The same, ordered after the work queued so far on stream `after` only (what the caller
+  // queued there to fill `out` / `off`, or SETs it queued on that stream): an event recorded
+  // there is host-polled before the job is queued, so the stream-less server never races it.
+  // SETs queued on other streams are not covered (ShardedCache queues its SETs on its side
+  // and hand streams: call its sync_sets() first).
   bool serve_get_after(hipStream_t after, const Digest* host_keys, int64_t n, uint8_t* out,
                        uint64_t out_cap, uint64_t* off, uint32_t now, int done_slot);
   void serve_kick();
@@ -244,6 +246,11 @@ class HbmCache {
   std::vector<uint64_t> debug_hand();
   void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
                        uint32_t vlen, uint32_t expire);
+  // Tests: move the CLOCK hand to ring index `hand` (e.g. a lap behind the overwrite), and
+  // whether the hand may jump to the first entry the overwrite has not reached
+  // (hand_catch_up; false isolates it: a hand left behind then spends its windows on
+  // overwritten entries).
+  void debug_set_hand(uint64_t hand, bool catch_up = true);
   CacheCounters counters(hipStream_t s);
   uint64_t head(hipStream_t s);
 
@@ -253,6 +260,10 @@ class HbmCache {
   uint64_t* head_ptr() const { return head_ + hsel_; }
   // Pre-size the SET workspace for batches of n keys (allocates; call outside capture).
   void reserve(int64_t n);
+  // Bytes of grown-out workspaces not freed yet (their chains still running); frees the
+  // ones whose chains have finished first.
+  uint64_t retired_bytes();
+  uint64_t retired_ever() const { return retired_ever_; }  // bytes ever retired (tests)
   uint64_t hbm_bytes() const;
   uint64_t reinsert_max() const { return cfg_.evict == kEvictClock ? rmax_ : 0; }
 
@@ -268,18 +279,34 @@ class HbmCache {
   uint64_t* cur_ring_tail() const { return head_ + 2 + hsel_; }
   uint64_t* next_ring_tail() const { return head_ + 2 + (hsel_ ^ 1); }
   // Deferred frees (no device-wide synchronisation on the serving path): a grown buffer's
-  // old block is kept until the cache is destroyed or a synchronising maintenance call
-  // (flush, sweep) runs; `note_stream` remembers the streams SET work was queued on.
-  void retire(void* p);
-  void free_retired();
+  // old blocks are retired as a group with an event recorded on every stream SET work was
+  // queued on (`note_stream`) and the growing call's; reap_retired frees a group once its
+  // events have completed (every chain that could read the old blocks has finished) — at
+  // the start of every store and in sweep; reserve (which synchronises the device) and the
+  // destructor free every group.
+  struct RetiredGroup {
+    std::vector<void*> ptrs;
+    std::vector<hipEvent_t> ev;
+    uint64_t bytes = 0;
+  };
+  void retire_group(std::initializer_list<void*> ptrs, uint64_t bytes, hipStream_t s);
+  void reap_retired(bool all);
   void note_stream(hipStream_t s);
-  std::vector<void*> retired_;
+  std::vector<RetiredGroup> retired_;
+  uint64_t retired_ever_ = 0;
   std::vector<hipStream_t> set_streams_;
+  // The SET workspace's tables are cleared on the stream of the call that grew them;
+  // a store on another stream waits for that (ws_ready_) once (ws_ordered_).
+  hipEvent_t ws_ready_ = nullptr;
+  hipStream_t ws_grow_stream_ = nullptr;
+  std::vector<hipStream_t> ws_ordered_;
+  void ws_order(hipStream_t s);
   // CLOCK state
   uint64_t* ring_ = nullptr;           // item-start ring (logical locs, kRingSkip holes)
   uint64_t ring_cap_ = 0;
   unsigned long long* rc_ctl_ = nullptr;  // hand, batch bytes, cut, entries scanned
   bool lead_ = false;  // the hand's mode (layout.h hand_lead, sticky; HostCache keeps the same)
+  bool catch_up_ = true;  // debug_set_hand
   uint64_t rmax_ = 0;
   int64_t rc_cap_ = 0;
   uint64_t *rc_loc_ = nullptr, *rc_h_ = nullptr, *rc_part_ = nullptr, *rc_hx_ = nullptr;

@@ -2619,6 +2619,7 @@ struct RcAdvance {
   const uint64_t* ring = nullptr;
   const uint64_t* head = nullptr;  // the claim word (the head before this batch's append)
   uint64_t cap = 0;
+  int catch_up = 1;  // 0: tests only (debug_set_hand), the hand never jumps
 };
 
 // A hand behind the overwrite (batches that skipped it while the log filled, e.g. a
@@ -2652,7 +2653,7 @@ __device__ __forceinline__ void rc_advance(const RcAdvance& r) {
   const uint64_t consumed = cut != ~0ull && cut < weff ? cut : weff;
   uint64_t hand = hand0 + consumed;
   if (rtail - hand > r.rmask + 1) hand = rtail - (r.rmask + 1);  // ring lapped the hand
-  hand = hand_catch_up(r.ring, r.rmask, hand, rtail, *r.head, r.cap);
+  if (r.catch_up) hand = hand_catch_up(r.ring, r.rmask, hand, rtail, *r.head, r.cap);
   r.ctl[0] = hand;
   r.ctl[1] = 0;
   r.ctl[2] = ~0ull;
@@ -3174,16 +3175,58 @@ HbmCache::~HbmCache() {
     for (void* p : {(void*)b.keys, (void*)b.voff, (void*)b.from, (void*)b.vlen, (void*)b.flags,
                     (void*)b.expire, (void*)b.scratch})
       (void)hipFree(p);
-  free_retired();
+  reap_retired(true);
+  if (ws_ready_) (void)hipEventDestroy(ws_ready_);
 }
 
-void HbmCache::retire(void* p) {
-  if (p) retired_.push_back(p);
+void HbmCache::retire_group(std::initializer_list<void*> ptrs, uint64_t bytes, hipStream_t s) {
+  RetiredGroup g;
+  for (void* p : ptrs)
+    if (p) g.ptrs.push_back(p);
+  if (g.ptrs.empty()) return;
+  g.bytes = bytes;
+  retired_ever_ += bytes;
+  std::vector<hipStream_t> all = set_streams_;
+  if (std::find(all.begin(), all.end(), s) == all.end()) all.push_back(s);
+  for (hipStream_t x : all) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(e, x));
+    g.ev.push_back(e);
+  }
+  retired_.push_back(std::move(g));
 }
 
-void HbmCache::free_retired() {
-  for (void* p : retired_) (void)hipFree(p);
-  retired_.clear();
+void HbmCache::reap_retired(bool all) {
+  for (size_t i = 0; i < retired_.size();) {
+    bool done = true;
+    for (hipEvent_t e : retired_[i].ev)
+      if (all) (void)hipEventSynchronize(e);
+      else if (hipEventQuery(e) != hipSuccess) done = false;
+    if (!done) {
+      ++i;
+      continue;
+    }
+    for (hipEvent_t e : retired_[i].ev) (void)hipEventDestroy(e);
+    for (void* p : retired_[i].ptrs) (void)hipFree(p);
+    retired_.erase(retired_.begin() + (long)i);
+  }
+}
+
+uint64_t HbmCache::retired_bytes() {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  reap_retired(false);
+  uint64_t b = 0;
+  for (const RetiredGroup& r : retired_) b += r.bytes;
+  return b;
+}
+
+void HbmCache::ws_order(hipStream_t s) {
+  if (!ws_ready_ || s == ws_grow_stream_) return;
+  if (std::find(ws_ordered_.begin(), ws_ordered_.end(), s) != ws_ordered_.end()) return;
+  HIP_OK(hipStreamWaitEvent(s, ws_ready_, 0));  // the grow's table clears land first
+  ws_ordered_.push_back(s);
 }
 
 void HbmCache::note_stream(hipStream_t s) {
@@ -3200,11 +3243,12 @@ uint64_t HbmCache::hbm_bytes() const {
 // synchronisation: the old blocks are retired (freed with the cache), since queued work on
 // any stream may still read them.
 void HbmCache::ensure_rc_ws(int64_t w, hipStream_t s) {
-  (void)s;
   if (w <= rc_cap_) return;
   int64_t cap = rc_cap_ ? rc_cap_ : 4096;
   while (cap < w) cap *= 2;
-  for (void* p : {(void*)rc_loc_, (void*)rc_h_, (void*)rc_part_, (void*)rc_hx_}) retire(p);
+  const uint64_t oc = (uint64_t)rc_cap_;
+  retire_group({rc_loc_, rc_h_, rc_part_, rc_hx_}, oc * 8 * 2 + (oc / kBlock + 1) * 8 + (oc + 1) * 8,
+               s);
   HIP_OK(hipMalloc(&rc_loc_, cap * 8));
   HIP_OK(hipMalloc(&rc_h_, cap * 8));
   HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
@@ -3214,14 +3258,11 @@ void HbmCache::ensure_rc_ws(int64_t w, hipStream_t s) {
 
 // Hand buffer b for a combined batch of `rows` rows (w reinsertion rows + the batch's own).
 void HbmCache::ensure_cb(int b, int64_t rows, hipStream_t s) {
-  (void)s;
   HandBuf& h = hb_[b];
   if (rows <= h.cap) return;
   int64_t cap = h.cap ? h.cap : 4096;
   while (cap < rows) cap *= 2;
-  for (void* p : {(void*)h.keys, (void*)h.voff, (void*)h.from, (void*)h.vlen, (void*)h.flags,
-                  (void*)h.expire})
-    retire(p);
+  retire_group({h.keys, h.voff, h.from, h.vlen, h.flags, h.expire}, (uint64_t)h.cap * 44, s);
   HIP_OK(hipMalloc(&h.keys, cap * sizeof(Digest)));
   HIP_OK(hipMalloc(&h.voff, cap * 8));
   HIP_OK(hipMalloc(&h.from, cap * 8));
@@ -3273,12 +3314,12 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   int64_t cap = set_cap_ ? set_cap_ : 1024;
   while (cap < n) cap *= 2;
   const uint64_t tslots = (uint64_t)cap * 2;
+  const uint64_t oc = (uint64_t)set_cap_;
   for (SetWs& w : ws_) {
-    // the old workspace may still be read by queued SET chains on other streams: retired,
-    // not freed (no device synchronisation on the serving path)
-    for (void* p : {(void*)w.dd_keys, (void*)w.dd_win, (void*)w.dd_slot, (void*)w.set_size,
-                    (void*)w.set_off, (void*)w.set_claim, (void*)w.set_cnt})
-      retire(p);
+    // the old workspace may still be read by queued SET chains on other streams: retired
+    // until their events say they finished (no device synchronisation on the serving path)
+    retire_group({w.dd_keys, w.dd_win, w.dd_slot, w.set_size, w.set_off, w.set_claim, w.set_cnt},
+                 2 * oc * 12 + oc * 8 + 3 * (oc + 1) * 8, s);
     HIP_OK(hipMalloc(&w.dd_keys, tslots * sizeof(uint64_t)));
     HIP_OK(hipMalloc(&w.dd_win, tslots * sizeof(int)));
     // the tables are cleared once here, on the stream of the SET that first uses them
@@ -3297,6 +3338,12 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
   dd_mask_ = (uint32_t)(tslots - 1);
   set_cap_ = cap;
   ++ws_gen_;
+  // a store on another stream waits for these clears (the dedupe tables were
+  // read uncleared by a store on a stream the grow was not ordered with)
+  if (!ws_ready_) HIP_OK(hipEventCreateWithFlags(&ws_ready_, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(ws_ready_, s));
+  ws_grow_stream_ = s;
+  ws_ordered_.clear();
 }
 
 void HbmCache::reserve(int64_t n) {
@@ -3304,8 +3351,9 @@ void HbmCache::reserve(int64_t n) {
   DeviceGuard g(cfg_.device);
   ensure_set_ws(n, nullptr);
   // (a maintenance call, not on the serving path: the null-stream clears land before any
-  // stream's next SET)
+  // stream's next SET, and every grown-out workspace can go)
   HIP_OK(hipDeviceSynchronize());
+  reap_retired(true);
 }
 
 void HbmCache::lookup(const Digest* keys, int64_t n, uint64_t* loc, uint64_t* size, uint64_t* off,
@@ -3598,6 +3646,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   note_stream(s);
+  if (!retired_.empty()) reap_retired(false);  // grown-out workspaces whose chains finished
   // phase 2: the rest of the chain of the batch a phase-1 call planned
   if (phase == 2) {
     SH_CHECK(pend_.active && pend_.n == n, "store phase 2 without the same batch's phase 1");
@@ -3658,6 +3707,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
     p.flags = flags;
     p.expire = expire;
   }
+  ws_order(s);
   select_ws(p.parity);
   store_plan_locked(p.keys, p.vlen, p.rows, s, detached);
   if (plan_done) HIP_OK(hipEventRecord(plan_done, s));
@@ -3714,7 +3764,7 @@ void HbmCache::store_plan_locked(const Digest* keys, const uint32_t* vlen, int64
   RcAdvance adv;
   if (rc_adv_w_ > 0) {
     adv = RcAdvance{rc_ctl_, detached ? next_ring_tail() : cur_ring_tail(), ring_cap_ - 1,
-                    rc_adv_w_, ring_, claim_ptr(), cfg_.log_bytes};
+                    rc_adv_w_, ring_, claim_ptr(), cfg_.log_bytes, catch_up_ ? 1 : 0};
     rc_adv_w_ = 0;
   }
   hipLaunchKernelGGL(k_set_dedupe, dim3(grid), dim3(kBlock), 0, s, keys, vlen, n,
@@ -3778,6 +3828,7 @@ void HbmCache::store_graph(StoreGraph* g, const Digest* keys, const uint8_t* val
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard dg(cfg_.device);
   ensure_set_ws(n, s);  // before any capture: allocation is not capturable
+  ws_order(s);
   select_ws(0);         // (graphs bake the workspace in: always the first)
   const void* ptrs[6] = {keys, values, val_off, vlen, flags, expire};
   bool same = g->n == n && g->bound == bytes_bound && g->now == now && g->ws_gen == ws_gen_ &&
@@ -3837,6 +3888,7 @@ void HbmCache::sweep(uint32_t now, hipStream_t s, uint64_t* live_entries, uint64
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(host_buf_, out, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  reap_retired(false);  // (the idle-time maintenance call: grown-out workspaces that are done)
   if (live_entries) *live_entries = host_buf_[0];
   if (live_bytes) *live_bytes = host_buf_[1];
 }
@@ -3969,6 +4021,15 @@ std::vector<uint64_t> HbmCache::debug_hand() {
   unsigned long long ctl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rc_ctl_) HIP_OK(hipMemcpy(ctl, rc_ctl_, sizeof ctl, hipMemcpyDeviceToHost));
   return {hand, tail, head, loc, ctl[4], ctl[5], ctl[6]};
+}
+
+void HbmCache::debug_set_hand(uint64_t hand, bool catch_up) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DeviceGuard g(cfg_.device);
+  SH_CHECK(rc_ctl_ != nullptr, "no CLOCK hand (FIFO eviction)");
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(rc_ctl_, &hand, 8, hipMemcpyHostToDevice));
+  catch_up_ = catch_up;
 }
 
 void HbmCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,

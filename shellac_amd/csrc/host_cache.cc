@@ -251,7 +251,7 @@ void HostCache::reclaim_locked(int64_t n, uint64_t bytes, uint64_t rmax, uint32_
     const uint64_t l = ring_[idx & rmask];
     return l != kRingSkip && head_ > l + log_bytes_;
   };
-  if (hand_ < ring_tail_ && over(hand_)) {
+  if (catch_up_ && hand_ < ring_tail_ && over(hand_)) {
     uint64_t lo = hand_ + 1, hi = ring_tail_;
     while (lo < hi) {
       const uint64_t mid = lo + (hi - lo) / 2;
@@ -454,6 +454,12 @@ std::vector<uint64_t> HostCache::debug_bucket(uint64_t b) {
       out.push_back(w);
   }
   return out;
+}
+
+void HostCache::debug_set_hand(uint64_t hand, bool catch_up) {
+  std::lock_guard<std::mutex> lk(mu_);
+  hand_ = hand;
+  catch_up_ = catch_up;
 }
 
 void HostCache::debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,

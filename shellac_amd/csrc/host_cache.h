@@ -38,6 +38,7 @@ class HostCache {
   std::vector<uint64_t> debug_hand();
   void debug_set_entry(uint64_t b, int slot, uint64_t d0, uint64_t d1, uint64_t loc,
                        uint32_t vlen, uint32_t expire);
+  void debug_set_hand(uint64_t hand, bool catch_up = true);  // HbmCache::debug_set_hand
   uint64_t export_keys(Digest* out, uint64_t out_cap, uint32_t now);
   void save(const std::string& path, const uint64_t user[4]);
   void load(const std::string& path, uint64_t user[4]);
@@ -91,6 +92,7 @@ class HostCache {
   uint64_t ring_tail_ = 0, hand_ = 0;
   uint64_t hand_consumed_ = 0;  // entries the hand consumed last batch (adaptive window)
   bool lead_ = false;  // the hand's mode (layout.h hand_lead, sticky)
+  bool catch_up_ = true;  // debug_set_hand
 };
 
 // CPU versions of the device batch helpers (same contracts as hbm_cache.h).

@@ -220,13 +220,23 @@ def _event_handle(ev) -> int:
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
     size: torch.Tensor  # int64 [n+1] response bytes per key (0 = miss); size[n] = 0
-    off: torch.Tensor   # int64 [n+1] exclusive scan of size; off[n] = total bytes
-    # block-local offsets (lookup_coalesced(blocked=True)): `off[i]` is row i's offset within
-    # its lookup workgroup's rows [b << shift, (b + 1) << shift), `prefix[b]` the bytes of
-    # the workgroups before b (prefix[last + 1] = the total); only gather() (with its expand
-    # tail) reads them: the per-request offsets come from the expand tail
+    # the offsets buffer as the lookup wrote it: the exclusive scan of size (off_raw[n] =
+    # total bytes), or, for a blocked lookup (lookup_coalesced(blocked=True)), row i's
+    # offset within its lookup workgroup's rows [b << shift, (b + 1) << shift) with
+    # off_raw[n] unwritten, `prefix[b]` the bytes of the workgroups before b (prefix[last +
+    # 1] = the total). Read it through `off`, which refuses a blocked lookup: only gather()
+    # (with its expand tail, which writes the per-request offsets) reads those.
+    off_raw: torch.Tensor
     prefix: Optional[torch.Tensor] = None
     shift: int = 0
+
+    @property
+    def off(self) -> torch.Tensor:
+        """int64 [n+1]: the exclusive scan of ``size`` (off[n] = total bytes)."""
+        if self.prefix is not None:
+            raise ValueError("a blocked lookup holds workgroup-local offsets: the per-request "
+                             "offsets come from the gather's expand tail")
+        return self.off_raw
 
     @property
     def n(self) -> int:
@@ -235,7 +245,7 @@ class Lookup:
     def total(self) -> torch.Tensor:
         """Total response bytes (a one-element device tensor)."""
         if self.prefix is None:
-            return self.off[self.n:self.n + 1]
+            return self.off_raw[self.n:self.n + 1]
         nb = ((self.n - 1) >> self.shift) + 1 if self.n else 0
         return self.prefix[nb:nb + 1]
 
@@ -455,7 +465,7 @@ class CacheShard:
                       cslot.data_ptr() if cslot is not None else 0]
             elif lk.prefix is not None:
                 raise ValueError("a blocked lookup's offsets are read only with an expand tail")
-            self._impl.gather(lk.loc.data_ptr(), lk.off.data_ptr(), lk.n, out.data_ptr(),
+            self._impl.gather(lk.loc.data_ptr(), lk.off_raw.data_ptr(), lk.n, out.data_ptr(),
                               self._s(), cap, *ex,
                               lk.prefix.data_ptr() if lk.prefix is not None else 0, lk.shift)
         else:

@@ -295,3 +295,53 @@ def test_clock_lead_mode_is_sticky_host():
     assert present == 16
     assert sum(hits[120:]) / (80 * G) > 0.75, sum(hits[120:]) / (80 * G)
 
+
+
+def _catch_up_run(dev, catch_up=True):
+    """A CLOCK hand a lap behind the overwrite (set there with debug_set_hand: the state a
+    burst of queued stores leaves): after one SET batch it must stand
+    on the first ring entry the overwrite has not reached (hand_catch_up), so the objects
+    about to be overwritten next are examined and the referenced ones re-appended. With
+    the jump disabled the hand spends its windows on overwritten entries and the read
+    objects at the overwrite point are lost."""
+    s = CacheShard(1 << 20, 1 << 12, 1 << 14, dev, evict="clock")
+    keys = [b"/cu/%d" % i for i in range(3200)]  # ~3 laps of 1 KB objects, none read
+    for b in range(0, 3200, 20):
+        s.set_many(keys[b:b + 20], [b"x%05d" % b * 166] * 20)
+    hand0, tail, head0 = s._impl.debug_hand()[:3]
+    assert tail - hand0 < 1100  # ~1008 live entries: a lap
+    s._impl.debug_set_hand(hand0 - 1000, catch_up)  # one lap behind the overwrite
+    s.set_many([b"/cu/tiny"], [b"t" * 16])
+    hand, _, head, loc = s._impl.debug_hand()[:4]
+    live = [i for i, g in enumerate(s.get_many(keys)) if g is not None]
+    first = live[0]
+    old = keys[first:first + 40]  # the oldest live objects: the next batches overwrite them
+    assert all(g is not None for g in s.get_many(old))  # read: their reference bits set
+    for b in range(3):
+        s.set_many([b"/cu/new/%d/%d" % (b, i) for i in range(20)], [b"n" * 1000] * 20)
+    got = s.get_many(old)
+    return {"hand0": hand0, "hand": hand, "hand_item_intact": loc + (1 << 20) >= head,
+            "first_live": first, "survived": sum(g is not None for g in got),
+            "values_ok": all(g is None or g == b"x%05d" % ((first + i) // 20 * 20) * 166
+                             for i, g in enumerate(got)),
+            "reinserted": s.counters()["reinserted"], "head": s.head()}
+
+
+def test_clock_hand_catches_up_a_lap_behind_host():
+    r = _catch_up_run("cpu")
+    # the jump lands exactly on the first entry the overwrite has not reached (ring index ==
+    # key index: one entry per SET, no reinsertions during the fill)
+    assert r["hand"] == r["first_live"] == r["hand0"] and r["hand_item_intact"], r
+    assert r["survived"] == 40 and r["values_ok"], r
+    # the same state without the jump: the hand is still behind and the read objects go
+    s = _catch_up_run("cpu", catch_up=False)
+    assert s["hand"] < s["first_live"] and not s["hand_item_intact"], s
+    assert s["survived"] == 0, s
+
+
+@pytest.mark.gpu
+def test_clock_hand_catches_up_gpu_matches_host(cuda_dev):
+    g, h = _catch_up_run(cuda_dev), _catch_up_run("cpu")
+    assert g == h and g["survived"] == 40
+    g, h = _catch_up_run(cuda_dev, False), _catch_up_run("cpu", False)
+    assert g == h and g["survived"] == 0

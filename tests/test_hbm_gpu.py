@@ -1223,3 +1223,35 @@ def test_host_edge_serve_matches_device_edge(cuda_dev, dma):
         assert torch.equal(s0, s1)
         assert d0 == d1
     assert sum(int((s > 0).sum()) for s, _ in runs[1]) > 0
+
+
+@pytest.mark.gpu
+def test_set_workspace_grows_then_frees_retired_blocks(cuda_dev):
+    """SET batches growing 8x (1000 -> 8000 rows, on two streams in turn): every grow
+    retires the old SET workspace with events on the streams that used it, and once those
+    chains have drained the next store frees it — retired bytes back to 0, no keep-forever
+    and no device synchronisation in store. A store on the other
+    stream is ordered after the grow's dedupe-table clears: every value lands."""
+    from shellac_amd.ops.cache import CacheShard
+
+    s = CacheShard(64 << 20, 1 << 15, 1 << 14, cuda_dev)
+    ever0 = s._impl.retired_ever
+    side = torch.cuda.Stream(cuda_dev)
+    n, written = 1000, []
+    for step in range(4):
+        keys = [b"/grow/%d/%d" % (step, i) for i in range(n)]
+        vals = [b"v%d-%d-" % (step, i) * 5 for i in range(n)]
+        if step % 2:
+            with torch.cuda.stream(side):
+                s.set_many(keys, vals)
+        else:
+            s.set_many(keys, vals)
+        written.append((keys, vals))
+        n *= 2
+    torch.cuda.synchronize()
+    assert s._impl.retired_ever > ever0  # the workspace did grow (and retire) 3 times
+    s.set_many([b"/grow/last"], [b"x" * 10])  # a store reaps the groups whose chains drained
+    torch.cuda.synchronize()
+    assert s._impl.retired_bytes() == 0
+    for keys, vals in written:
+        assert s.get_many(keys) == vals
