@@ -188,6 +188,12 @@ def main():
                     help="RxC pairs (reactor threads x load-generator threads), each measured "
                          "with its own proxy over the same filled cache (default: "
                          "--threads x --client-threads)")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="HBM shards (all on GPU 0, a stand-in for that many GPUs: the ketama "
+                         "split and hot-object spreading run as on a node)")
+    ap.add_argument("--hot-objects", type=int, default=1024,
+                    help="with --shards > 1: the replicated hot set (0: plain ketama)")
+    ap.add_argument("--hot-refresh-ms", type=int, default=500)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -205,8 +211,9 @@ def main():
     # origin's / the proxy's other threads'
     batcher_cpus = []
     if pin and gpu and a.batcher_core == "auto":
-        batcher_cpus = [allowed[-nmisc - 1]]
-        nmisc += 1
+        shards = a.shards if a.backend in ("hbm", "tiered") else 1
+        batcher_cpus = allowed[len(allowed) - nmisc - shards: len(allowed) - nmisc]
+        nmisc += shards
     # busy-polling only on dedicated (pinned) cores
     if a.rx_spin_us is None:
         a.rx_spin_us = 200 if pin else 0
@@ -231,7 +238,9 @@ def main():
     elif a.backend == "dram":
         backend = make_backend("dram", dram_mb=a.dram_mb)
     else:
-        backend = make_backend("hbm", gpus=[0], hbm_gb=hbm_gb, batch_us=a.batch_us,
+        backend = make_backend("hbm", gpus=[0] * a.shards, hbm_gb=hbm_gb / a.shards,
+                               batch_us=a.batch_us, hot_objects=a.hot_objects,
+                               hot_refresh_ms=a.hot_refresh_ms,
                                l1_mb=a.l1_mb if a.backend == "tiered" else 0,
                                depth=a.hbm_depth, evict=a.evict,
                                edge_server=not a.no_edge_server, batcher_cpus=batcher_cpus,
@@ -243,6 +252,8 @@ def main():
            "dram_mb": a.dram_mb if a.backend == "dram" else None,
            "l1_mb": a.l1_mb if a.backend == "tiered" else None,
            "hbm_gb": hbm_gb if a.backend in ("hbm", "tiered") else None,
+           "hbm_shards": a.shards if a.backend in ("hbm", "tiered") else None,
+           "hot_objects": a.hot_objects if a.shards > 1 else 0,
            "cpu_count": os.cpu_count(), "cpu_budget": budget,
            "processes": "origin | proxy | load generator",
            "cpus": {"proxy_other": misc_cpus, "origin": or_cpus, "gpu_batcher": batcher_cpus},
@@ -288,6 +299,12 @@ def main():
                 r["hit_ratio"] = hits / max(reqs, 1)
                 r["origin_requests"] = s1["upstream_requests"] - s0["upstream_requests"]
                 r["layout"] = f"{nrx}x{ncl}"
+                sg = [s1.get("cache", {}).get(f"hbm_shard_gets_{i}", 0) -
+                      s0.get("cache", {}).get(f"hbm_shard_gets_{i}", 0) for i in range(a.shards)]
+                if a.shards > 1 and sum(sg):
+                    # per-shard GET share (ketama split, evened out by hot-object spreading)
+                    r["shard_get_share"] = [round(x / sum(sg), 4) for x in sg]
+                    r["shard_get_max_over_mean"] = round(max(sg) / (sum(sg) / len(sg)), 4)
                 out[f"{tag}c{conc}"] = r
                 lm = r["latency_ms"]
                 print(f"[http] {a.backend} {nrx}x{ncl} c={conc}: {r['rps']:.0f} rps "

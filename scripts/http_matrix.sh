@@ -3,7 +3,8 @@
 # HBM-only and tiered, the GPU batcher on a core of its own (8 reactors x 6 load-generator
 # workers), HBM-only also without reactor-direct jobs (every GET through the batcher thread),
 # with 1 or 4 edge-server blocks instead of 8 (hbm_blk1, hbm_blk4)
-# and without the resident edge server (a launch per GET batch).
+# and without the resident edge server (a launch per GET batch); hbm2 / hbm2_nohot: two HBM
+# shards on GPU 0 (a stand-in for two GPUs) with and without hot-object spreading.
 set -o pipefail
 OUT=gpurun_out/${1:-http_matrix}
 mkdir -p "$OUT"
@@ -23,6 +24,8 @@ for spec in "$@"; do
     hbm_blk4) run hbm_8M_blk4 --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --serve-blocks 4 || exit 1;;
     hbm_nodirect) run hbm_8M_nodirect --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-direct || exit 1;;
     hbm_nosrv) run hbm_8M_nosrv --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 --no-edge-server || exit 1;;
+    hbm2)   run hbm2_8M   --backend hbm    --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 7x6 --timeout 400 --shards 2 || exit 1;;
+    hbm2_nohot) run hbm2_8M_nohot --backend hbm --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 7x6 --timeout 400 --shards 2 --hot-objects 0 || exit 1;;
     tiered) run tiered_8M --backend tiered --objects 8000000 --requests 2000000 --conc 10 1000 --layouts 8x6 --timeout 400 || exit 1;;
   esac
 done
