@@ -258,7 +258,9 @@ class HbmCache {
   uint8_t* log_ptr() const { return log_; }
   Entry* index_ptr() const { return index_; }
   uint64_t* head_ptr() const { return head_ + hsel_; }
-  // Pre-size the SET workspace for batches of n keys (allocates; call outside capture).
+  // Pre-size the SET workspace for batches of n keys, and with CLOCK the hand's workspaces
+  // for the combined batch such a SET runs once the log wraps (allocates; synchronises;
+  // call outside capture and before serving).
   void reserve(int64_t n);
   // Bytes of grown-out workspaces not freed yet (their chains still running); frees the
   // ones whose chains have finished first.

@@ -1175,11 +1175,23 @@ int resident_grid(K kernel, int* cache) {
 
 // The byte mover's launch: 4 loads in flight per lane, 8 waves/SIMD, nontemporal stores,
 // kSegOcc64/64 of the co-resident slots (see the tuned constants above).
+// (SHELLAC_SEGOCC_<MODE> = slots / 64 overrides kSegOcc64 for one mode: A/B experiments)
+inline int seg_occ64(int mode) {
+  static int occ[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  if (occ[mode] < 0) {
+    const std::string v = "SHELLAC_SEGOCC_" + std::to_string(mode);
+    const char* e = getenv(v.c_str());
+    const int x = e ? atoi(e) : 0;
+    occ[mode] = x >= 1 && x <= 64 ? x : kSegOcc64;
+  }
+  return occ[mode];
+}
+
 template <int MODE, typename... Args>
 void launch_segcopy_ex(hipStream_t s, const ExpandTail& ex, Args... args) {
   static int grid[64];
   const auto kern = k_segcopy<MODE, 4, 8, true>;
-  const int g = std::max(1, resident_grid(kern, grid) * kSegOcc64 / 64);
+  const int g = std::max(1, resident_grid(kern, grid) * seg_occ64(MODE) / 64);
   hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., kSegMinTile, ex);
 }
 template <int MODE, typename... Args>
@@ -2392,6 +2404,7 @@ __global__ __launch_bounds__(kBlock) void k_set_small(
 // The combined batch then runs the ordinary SET chain (dedupe lets the batch's own SETs
 // win over a reinsertion of the same key). Host twin: HostCache::reclaim.
 constexpr unsigned long long kRcCount = 1ull << 43;  // k_rc_scan / k_rc_emit packed counts
+constexpr int kRcScanK = 1;  // window entries per lane of k_rc_scan (SHELLAC_RCSCAN_K)
 
 struct RcArgs {
   const uint64_t* ring;
@@ -2424,6 +2437,28 @@ struct RcBatch {
   uint64_t* from;
 };
 
+// block_partial into part[at] (several 256-entry sub-blocks per workgroup)
+__device__ __forceinline__ void block_partial_at(unsigned long long v, uint64_t* __restrict__ part,
+                                                 int64_t at) {
+  __shared__ unsigned long long s_p[kBlock / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_p[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += s_p[k];
+    part[at] = t;
+  }
+  __syncthreads();
+}
+
+// K window entries per lane (entries j = (blockIdx.x * K + k) * kBlock + threadIdx.x): the K
+// ring -> header -> index chains are issued phase by phase, so each lane keeps K of them in
+// flight — the window needs 1/K of the workgroups, which matters beside the gather, which
+// holds most of the co-resident slots (the hand scan was latency-bound at 5 %
+// of the HBM roofline). Every entry's decision is the single-entry rule's.
+template <int K>
 __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const uint8_t* __restrict__ log,
                                                     const Entry* __restrict__ index, uint64_t mask,
                                                     const Digest* __restrict__ keys,
@@ -2452,72 +2487,107 @@ __global__ __launch_bounds__(kBlock) void k_rc_scan(RcArgs a, RcBatch cb, const 
     cb.expire[r] = expire ? expire[i] : 0u;
     cb.from[r] = 0;
   }
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t avail = rtail - hand;
   // the entries this hand examines (a detached hand sees the ring tail of the batch before
   // the previous one; rows past the effective window are skip rows): the advance consumes
   // at most these
   const int64_t weff = hand_window_eff(a.n_new, a.ctl[4]);
-  if (j == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.ctl[3] = (uint64_t)weff < avail ? (uint64_t)weff : avail;
     a.ctl[5 + a.parity] = (unsigned long long)weff;
   }
-  uint64_t loc = kRingSkip, h = 0;
-  uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
-  if (j < weff && (uint64_t)j < avail) {
-    const uint64_t idx = hand + (uint64_t)j;
-    const uint64_t l = rtail - idx <= a.rmask + 1 ? a.ring[idx & a.rmask] : kRingSkip;
-    if (l != kRingSkip && head <= l + a.cap) {  // intact (not overwritten yet)
-      const uint4* hp = reinterpret_cast<const uint4*>(log + l % a.cap);
-      w0 = hp[0];
-      w1 = hp[1];
-      if (w1.w == kItemMagic) {
-        loc = l;
-        const Digest d{pack2(w0.x, w0.y), pack2(w0.z, w0.w)};
-        // the entry pointing at this item: first bucket first, the second only when the
-        // first has none (SETs fill the first bucket first, so one 128-B line per window
-        // entry usually settles it). A digest match alone does not settle it: a dead entry
-        // keeps its digest, so a key can match in one bucket while its live entry is in the
-        // other (stopping there dropped live, referenced items: test_serve_steps_return_
-        // ground_truth_records)
-        // Each entry's {loc, vlen, expire} half is one 16-B load, and a bucket's four are
-        // issued together (no insert runs beside the hand: the SET chain is on this stream;
-        // a concurrent lookup only sets reference bits, read either way)
-        const uint64_t bs[2] = {bucket1(d, mask), bucket2(d, mask)};
-        bool found = false;
-        for (int q = 0; q < 2 && !found; ++q) {
-          uint4 hv[kEntriesPerBucket];
+  int64_t j[K];
+  uint64_t l[K], loc[K], h[K];
+  uint4 w0[K], w1[K];
+  // 1. the ring entries
 #pragma unroll
-          for (int k = 0; k < (int)kEntriesPerBucket; ++k)
-            hv[k] = reinterpret_cast<const uint4*>(index + bs[q] * kEntriesPerBucket + k)[1];
-#pragma unroll
-          for (int k = 0; k < (int)kEntriesPerBucket; ++k)
-            if (pack2(hv[k].x, hv[k].y) == l + 1) {
-              found = true;
-              if ((hv[k].z & kRefBit) && (hv[k].w == 0 || hv[k].w > a.now)) h = item_bytes(w1.x);
-            }
-        }
-      }
+  for (int k = 0; k < K; ++k) {
+    j[k] = ((int64_t)blockIdx.x * K + k) * kBlock + threadIdx.x;
+    l[k] = kRingSkip;
+    loc[k] = kRingSkip;
+    h[k] = 0;
+    w0[k] = w1[k] = make_uint4(0, 0, 0, 0);
+    if (j[k] < weff && (uint64_t)j[k] < avail) {
+      const uint64_t idx = hand + (uint64_t)j[k];
+      l[k] = rtail - idx <= a.rmask + 1 ? a.ring[idx & a.rmask] : kRingSkip;
     }
   }
-  if (j >= weff && j < a.W) {
-    // a row past the effective window: a skip row (the SET chain reads nothing else of a
-    // row whose vlen says skip; k_rc_emit reads no rc_loc / rc_h past the examined entries)
-    cb.vlen[j] = kSkipVlen;
-  } else if (j < a.W) {
-    rc_loc[j] = loc;
-    rc_h[j] = h;
-    // a hot entry's row from the header just read (k_rc_emit fills in its value pointer
-    // or turns it into a skip row); every other entry is a skip row already
-    cb.keys[j] = h ? Digest{pack2(w0.x, w0.y), pack2(w0.z, w0.w)} : Digest{0, 0};
-    cb.voff[j] = 0;
-    cb.vlen[j] = h ? w1.x : kSkipVlen;
-    cb.flags[j] = h ? w1.y : 0u;
-    cb.expire[j] = h ? w1.z : 0u;
-    cb.from[j] = 0;
+  // 2. the headers of the intact (not overwritten) items
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (l[k] != kRingSkip && head <= l[k] + a.cap) {
+      const uint4* hp = reinterpret_cast<const uint4*>(log + l[k] % a.cap);
+      w0[k] = hp[0];
+      w1[k] = hp[1];
+    }
+  // 3. the entry pointing at each item: first bucket first, the second only when the first
+  // has none (SETs fill the first bucket first, so one 128-B line per window entry usually
+  // settles it). A digest match alone does not settle it: a dead entry keeps its digest, so
+  // a key can match in one bucket while its live entry is in the other (stopping there
+  // dropped live, referenced items: test_serve_steps_return_ground_truth_records). Each
+  // entry's {loc, vlen, expire} half is one 16-B load, and a bucket's four are issued
+  // together, the K entries' first buckets together (no insert runs beside the hand: the SET
+  // chain is on this stream; a concurrent lookup only sets reference bits, read either way)
+  uint4 hv[K][kEntriesPerBucket];
+  bool found[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    found[k] = false;
+    if (l[k] != kRingSkip && w1[k].w == kItemMagic) {
+      loc[k] = l[k];
+      const Digest d{pack2(w0[k].x, w0[k].y), pack2(w0[k].z, w0[k].w)};
+      const uint64_t b = bucket1(d, mask);
+#pragma unroll
+      for (int e = 0; e < (int)kEntriesPerBucket; ++e)
+        hv[k][e] = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket + e)[1];
+    }
   }
-  // hot bytes and (bits 43+) hot entries, scanned together by k_rc_emit
-  block_partial(h ? h + kRcCount : 0ull, part_h);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (loc[k] == kRingSkip) continue;
+#pragma unroll
+    for (int e = 0; e < (int)kEntriesPerBucket; ++e)
+      if (pack2(hv[k][e].x, hv[k][e].y) == loc[k] + 1) {
+        found[k] = true;
+        if ((hv[k][e].z & kRefBit) && (hv[k][e].w == 0 || hv[k][e].w > a.now))
+          h[k] = item_bytes(w1[k].x);
+      }
+    if (!found[k]) {
+      const Digest d{pack2(w0[k].x, w0[k].y), pack2(w0[k].z, w0[k].w)};
+      const uint64_t b = bucket2(d, mask);
+      uint4 h2[kEntriesPerBucket];
+#pragma unroll
+      for (int e = 0; e < (int)kEntriesPerBucket; ++e)
+        h2[e] = reinterpret_cast<const uint4*>(index + b * kEntriesPerBucket + e)[1];
+#pragma unroll
+      for (int e = 0; e < (int)kEntriesPerBucket; ++e)
+        if (pack2(h2[e].x, h2[e].y) == loc[k] + 1) {
+          if ((h2[e].z & kRefBit) && (h2[e].w == 0 || h2[e].w > a.now)) h[k] = item_bytes(w1[k].x);
+        }
+    }
+  }
+  // 4. the rows
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (j[k] >= weff && j[k] < a.W) {
+      // a row past the effective window: a skip row (the SET chain reads nothing else of a
+      // row whose vlen says skip; k_rc_emit reads no rc_loc / rc_h past the examined entries)
+      cb.vlen[j[k]] = kSkipVlen;
+    } else if (j[k] < a.W) {
+      rc_loc[j[k]] = loc[k];
+      rc_h[j[k]] = h[k];
+      // a hot entry's row from the header just read (k_rc_emit fills in its value pointer
+      // or turns it into a skip row); every other entry is a skip row already
+      cb.keys[j[k]] = h[k] ? Digest{pack2(w0[k].x, w0[k].y), pack2(w0[k].z, w0[k].w)} : Digest{0, 0};
+      cb.voff[j[k]] = 0;
+      cb.vlen[j[k]] = h[k] ? w1[k].x : kSkipVlen;
+      cb.flags[j[k]] = h[k] ? w1[k].y : 0u;
+      cb.expire[j[k]] = h[k] ? w1[k].z : 0u;
+      cb.from[j[k]] = 0;
+    }
+    // hot bytes and (bits 43+) hot entries of each 256-entry sub-block, scanned by k_rc_emit
+    block_partial_at(h[k] ? h[k] + kRcCount : 0ull, part_h, (int64_t)blockIdx.x * K + k);
+  }
   // batch bytes: one atomic per block
   __shared__ unsigned long long s_b[kBlock / 64];
   best = wave_sum(best);
@@ -3247,11 +3317,11 @@ void HbmCache::ensure_rc_ws(int64_t w, hipStream_t s) {
   int64_t cap = rc_cap_ ? rc_cap_ : 4096;
   while (cap < w) cap *= 2;
   const uint64_t oc = (uint64_t)rc_cap_;
-  retire_group({rc_loc_, rc_h_, rc_part_, rc_hx_}, oc * 8 * 2 + (oc / kBlock + 1) * 8 + (oc + 1) * 8,
+  retire_group({rc_loc_, rc_h_, rc_part_, rc_hx_}, oc * 8 * 2 + (oc / kBlock + 5) * 8 + (oc + 1) * 8,
                s);
   HIP_OK(hipMalloc(&rc_loc_, cap * 8));
   HIP_OK(hipMalloc(&rc_h_, cap * 8));
-  HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 1) * 8));
+  HIP_OK(hipMalloc(&rc_part_, (cap / kBlock + 5) * 8));  // + K - 1 sub-blocks of the scan
   HIP_OK(hipMalloc(&rc_hx_, (cap + 1) * 8));
   rc_cap_ = cap;
 }
@@ -3297,9 +3367,26 @@ void HbmCache::reclaim_locked(const Digest* keys, const uint8_t* values, const u
   const int g = (int)((w + kBlock - 1) / kBlock);
   const HandBuf& hb = hb_[hand_b_];
   const RcBatch cb{hb.keys, hb.voff, hb.vlen, hb.flags, hb.expire, hb.from};
-  hipLaunchKernelGGL(k_rc_scan, dim3(g), dim3(kBlock), 0, s, a, cb, log_, index_, cfg_.nbuckets - 1,
-                     keys, values, val_off, vlen, flags, expire, n, cfg_.max_item, rc_loc_, rc_h_,
-                     rc_part_);
+  // window entries per lane of the scan (SHELLAC_RCSCAN_K: A/B experiments); its part_h stays
+  // one word per 256 entries, rc_part_ is sized for g + K of them
+  static const int rk = [] {
+    const char* e = getenv("SHELLAC_RCSCAN_K");
+    const int v = e ? atoi(e) : kRcScanK;
+    return v == 1 || v == 2 || v == 4 ? v : kRcScanK;
+  }();
+  const int gk = (g + rk - 1) / rk;
+  if (rk == 4)
+    hipLaunchKernelGGL(k_rc_scan<4>, dim3(gk), dim3(kBlock), 0, s, a, cb, log_, index_,
+                       cfg_.nbuckets - 1, keys, values, val_off, vlen, flags, expire, n,
+                       cfg_.max_item, rc_loc_, rc_h_, rc_part_);
+  else if (rk == 2)
+    hipLaunchKernelGGL(k_rc_scan<2>, dim3(gk), dim3(kBlock), 0, s, a, cb, log_, index_,
+                       cfg_.nbuckets - 1, keys, values, val_off, vlen, flags, expire, n,
+                       cfg_.max_item, rc_loc_, rc_h_, rc_part_);
+  else
+    hipLaunchKernelGGL(k_rc_scan<1>, dim3(gk), dim3(kBlock), 0, s, a, cb, log_, index_,
+                       cfg_.nbuckets - 1, keys, values, val_off, vlen, flags, expire, n,
+                       cfg_.max_item, rc_loc_, rc_h_, rc_part_);
   hipLaunchKernelGGL(k_rc_emit, dim3(g), dim3(kBlock), 0, s, a, cb, log_, rc_loc_, rc_h_,
                      rc_part_, rc_hx_, hb.scratch, ctr_);
   if (!lead)
@@ -3349,6 +3436,16 @@ void HbmCache::ensure_set_ws(int64_t n, hipStream_t s) {
 void HbmCache::reserve(int64_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
+  if (cfg_.evict == kEvictClock && rmax_ && n > 0) {
+    // a SET batch of n rows runs as a combined batch of hand_window(n) + n rows once the
+    // log wraps: size the hand's workspaces and both hand buffers for it now, so no serving
+    // store allocates in steady state
+    const int64_t w = hand_window(n);
+    ensure_rc_ws(w, nullptr);
+    ensure_cb(0, w + n, nullptr);
+    ensure_cb(1, w + n, nullptr);
+    n = w + n;
+  }
   ensure_set_ws(n, nullptr);
   // (a maintenance call, not on the serving path: the null-stream clears land before any
   // stream's next SET, and every grown-out workspace can go)

@@ -1255,3 +1255,23 @@ def test_set_workspace_grows_then_frees_retired_blocks(cuda_dev):
     assert s._impl.retired_bytes() == 0
     for keys, vals in written:
         assert s.get_many(keys) == vals
+
+
+@pytest.mark.gpu
+def test_reserve_presizes_the_clock_combined_batch(cuda_dev):
+    """reserve(n) sizes the SET workspace, the hand's window workspace and both hand buffers
+    for the combined batch (hand window + n rows) a SET of n runs once the log wraps, so a
+    serving store never allocates in steady state: three laps of 2000-row SETs with the hand
+    active grow (and retire) nothing."""
+    from shellac_amd.ops.cache import CacheShard
+
+    s = CacheShard(4 << 20, 1 << 14, 1 << 14, cuda_dev)
+    s.reserve(2000)
+    ever = s._impl.retired_ever
+    for b in range(24):  # ~600 KB per batch: 3+ laps of the 4 MiB log
+        s.set_many([b"/rsv/%d/%d" % (b, i) for i in range(2000)], [b"r" * 280] * 2000)
+        if b % 4 == 0:
+            s.get_many([b"/rsv/%d/%d" % (b, i) for i in range(0, 2000, 7)])  # referenced
+    torch.cuda.synchronize()
+    assert s.head() > 3 * (4 << 20) and s.counters()["reinserted"] > 0
+    assert s._impl.retired_ever == ever
