@@ -298,7 +298,15 @@ struct HbmBackend::Dev {
   struct alignas(64) Ctr {
     std::atomic<uint64_t> v{0};
   };
-  Ctr routed_gets;  // GETs routed to this shard (per-shard load)
+  // GETs routed to this shard (per-shard load), sharded by the routing thread's slot: the
+  // reactors never share a counter line
+  static constexpr int kCtrShards = 16;
+  Ctr routed_gets[kCtrShards];
+  uint64_t routed_total() const {
+    uint64_t t = 0;
+    for (const Ctr& c : routed_gets) t += c.v.load(std::memory_order_relaxed);
+    return t;
+  }
   // digests (lo word) with a SET / DELETE in a flight not yet reaped, and flushes in
   // flight: a GET of such a key takes the stream path, ordered after them
   std::unordered_map<uint64_t, uint32_t> pend_w;
@@ -649,7 +657,8 @@ void HbmBackend::get(const std::string& key, const Digest& d, Executor* ex, GetC
     return;
   }
   Dev& dv = *devs_[k];
-  dv.routed_gets.v.fetch_add(1, std::memory_order_relaxed);
+  if (devs_.size() > 1)
+    dv.routed_gets[tl_sample_slot % Dev::kCtrShards].v.fetch_add(1, std::memory_order_relaxed);
   const bool restoring = dv.restoring.load(std::memory_order_acquire);
   if (cfg_.presence_filter && !restoring && !std::atomic_load(&dv.filt)->maybe(d)) {
     dv.filt_skips.fetch_add(1, std::memory_order_relaxed);  // never stored: no GPU batch
@@ -1907,11 +1916,15 @@ StatList HbmBackend::hot_refresh_locked() {
     else ++it;
   }
   const double above = cfg_.hot_spray_above > 0 ? cfg_.hot_spray_above : 1.0 / (4.0 * N);
-  HotPlan plan = plan_hot(counts, cfg_.hot_objects, N, up,
-                          [&](const Digest& d) { return owner_of(d, up); }, above);
-  // ---- what changes
   std::unordered_map<Digest, int32_t, DigestHash, DigestEq> cur;
   for (size_t i = 0; i < hot_set_.size(); ++i) cur.emplace(hot_set_[i], hot_rank_[i]);
+  // hysteresis: an object already replicated stays unless a new one is twice as hot (the
+  // set's tail would otherwise churn on sampling noise: a fill and a delete per object)
+  const std::function<bool(const Digest&)> sticky = [&](const Digest& d) { return cur.count(d) > 0; };
+  HotPlan plan = plan_hot(counts, cfg_.hot_objects, N, up,
+                          [&](const Digest& d) { return owner_of(d, up); }, above, 2, &sticky,
+                          2.0);
+  // ---- what changes
   std::unordered_set<Digest, DigestHash, DigestEq> added;
   for (const Digest& d : plan.hot)
     if (!cur.count(d)) added.insert(d);
@@ -2326,7 +2339,7 @@ void HbmBackend::stats(StatList* out) {
   out->emplace_back("hbm_no_shard_misses", no_shard_misses_.load());
   // per-shard GET routing (the load hot-object spreading evens out) and the hot set
   for (size_t i = 0; i < devs_.size(); ++i)
-    out->emplace_back("hbm_shard_gets_" + std::to_string(i), devs_[i]->routed_gets.v.load());
+    out->emplace_back("hbm_shard_gets_" + std::to_string(i), devs_[i]->routed_total());
   out->emplace_back("hbm_hot_spreading", hot_on_ ? 1 : 0);
   if (hot_on_) {
     out->emplace_back("hbm_hot_objects", hot_objects_.load());

@@ -479,7 +479,8 @@ void HostRouter::route_sets(const Digest* keys, int64_t n, int32_t* dest, int64_
 
 HotPlan plan_hot(const std::vector<std::pair<Digest, uint64_t>>& counts, int k, int nshards,
                  uint64_t eligible, const std::function<int(const Digest&)>& owner,
-                 double spray_above, uint64_t min_count) {
+                 double spray_above, uint64_t min_count,
+                 const std::function<bool(const Digest&)>* sticky, double sticky_factor) {
   HotPlan p;
   p.weights.assign((size_t)nshards, 0.0);
   p.planned.assign((size_t)nshards, 0.0);
@@ -498,11 +499,15 @@ HotPlan plan_hot(const std::vector<std::pair<Digest, uint64_t>>& counts, int k, 
   // the top k by count (ties by digest, so every caller with the same counts agrees; the
   // low word compared as a signed int64, the order HotSpread.design's tensors sort in)
   std::vector<size_t> idx;
-  for (size_t i = 0; i < counts.size(); ++i)
+  std::vector<double> rank_w(counts.size());
+  for (size_t i = 0; i < counts.size(); ++i) {
+    rank_w[i] = (double)counts[i].second;
+    if (sticky && sticky_factor != 1.0 && (*sticky)(counts[i].first)) rank_w[i] *= sticky_factor;
     if (counts[i].second >= min_count) idx.push_back(i);
+  }
   auto hotter = [&](size_t a, size_t b) {
     const auto &x = counts[a], &y = counts[b];
-    if (x.second != y.second) return x.second > y.second;
+    if (rank_w[a] != rank_w[b]) return rank_w[a] > rank_w[b];
     if (x.first.lo != y.first.lo) return (int64_t)x.first.lo < (int64_t)y.first.lo;
     return (int64_t)x.first.hi < (int64_t)y.first.hi;
   };

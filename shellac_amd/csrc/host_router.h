@@ -219,8 +219,13 @@ struct HotPlan {
   double hot_share = 0;
   std::vector<double> planned;
 };
+// `sticky` (optional): objects that are hot already rank with their count x sticky_factor
+// (hysteresis: a refresh does not churn the tail of the set on sampling noise; their loads
+// use the true counts).
 HotPlan plan_hot(const std::vector<std::pair<Digest, uint64_t>>& counts, int k, int nshards,
                  uint64_t eligible, const std::function<int(const Digest&)>& owner,
-                 double spray_above, uint64_t min_count = 2);
+                 double spray_above, uint64_t min_count = 2,
+                 const std::function<bool(const Digest&)>* sticky = nullptr,
+                 double sticky_factor = 1.0);
 
 }  // namespace shellac
