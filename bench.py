@@ -18,14 +18,14 @@ with CLOCK reinsertions, CAS index insert) by the HIP kernels on the shard's HBM
     all-to-all step (GPU-resident batches routed between GPUs over RCCL; see docs/PERF.md).
 Per-GPU work is fixed as N grows (weak scaling): the key space is N x --keys-per-gpu.
 
-Headline (``--headline pressured``): the full cache — a shard log sized so its working set
-(every key it holds, one record each) fills --pressured-fill (0.8) of it, wrapped, so every
-SET batch's CLOCK hand re-appends the objects read since it last passed and evicts the rest.
-Its request stream is the walk (``walk_batches``): the SETs walk a permutation of every key
-the shard holds and the GETs are --walk-get-batches (256) fresh batches of the Zipf
-stream, more than a log lap of steps, so the keys read over a lap are nearly the whole key
-space (``read_working_set_over_capacity``: their records over the log, ~0.78 at the
-defaults) rather than the ~1/2 of it 16 cycled batches touch. Secondary: the same full
+Headline (``--headline pressured``): the full cache — a shard log sized to its working set
+(every key it holds, one record each: --pressured-fill 1.0), wrapped, so every SET batch's
+CLOCK hand re-appends the objects read since it last passed and evicts the rest. Its request
+stream is the walk (``walk_batches``): the SETs walk a permutation of every key the shard
+holds and the GETs are --walk-get-batches (256) fresh batches of the Zipf stream, more than
+a log lap of steps, so the keys read over one lap of the log fill 3/4 of it
+(``read_working_set_over_capacity`` 0.750 at the defaults) rather than the 0.40 the 16
+cycled batches touched in round 5's headline. Secondary: the same full
 cache on the 16 cycled GET / SET batches (``log_pressured_cycled``, the round-5 headline),
 the fresh cache (``log_fresh``), a 16 GiB log that has wrapped with the working set at ~1/4
 of it (``log_wrapped``), and a working set --overfull-fill (1.25) times the log
@@ -177,7 +177,7 @@ def parse():
                          "GiB, wrapped, so the CLOCK hand re-appends read objects every step. "
                          "Default: sized so the shard's working set (every key it owns, one "
                          "record each) fills --pressured-fill of it (0 = skip)")
-    ap.add_argument("--pressured-fill", type=float, default=0.8,
+    ap.add_argument("--pressured-fill", type=float, default=1.0,
                     help="working set over log capacity of the default pressured shard")
     ap.add_argument("--overfull-fill", type=float, default=1.25,
                     help="secondary block log_overfull: a shard log the working set fills "
