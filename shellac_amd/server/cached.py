@@ -57,11 +57,16 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--no-hbm-filter", action="store_true",
                    help="send every GET to the GPUs (no host presence filter)")
     p.add_argument("--hbm-spin-us", type=int, default=50)
+    p.add_argument("--hot-objects", type=int, default=1024,
+                   help="--cache hbm on several GPUs: replicate this many of the most requested "
+                        "objects on every GPU and spread their GETs (0: plain ketama)")
+    p.add_argument("--hot-refresh-ms", type=int, default=1000)
     a = p.parse_args(argv)
     opts = ({"dram_mb": a.dram_mb} if a.cache == "dram" else
             {"gpus": [int(x) for x in a.gpus.split(",")] if a.gpus else None, "hbm_gb": a.hbm_gb,
              "batch_us": a.batch_us, "hbm_filter": not a.no_hbm_filter,
-             "spin_us": a.hbm_spin_us})
+             "spin_us": a.hbm_spin_us, "hot_objects": a.hot_objects,
+             "hot_refresh_ms": a.hot_refresh_ms})
     node = CacheNode(port=a.port, bind=a.bind, threads=a.threads, kind=a.cache, **opts).start()
     print(f"shellac-cached on port {node.port} ({a.cache})", flush=True)
     stop = threading.Event()

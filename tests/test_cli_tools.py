@@ -103,3 +103,15 @@ def test_prof_helper(tmp_path, capsys):
     cProfile.runctx("sum(range(1000))", {}, {}, str(out))
     assert prof_main([str(out)]) == 0
     assert "cumulative" in capsys.readouterr().out
+
+
+def test_cli_hot_spreading_flags():
+    """`shellac` / `shellac-cached` take the HBM tier's hot-object spreading knobs (SURVEY.md
+    §5.8): --hot-objects (0 = plain ketama) and --hot-refresh-ms."""
+    from shellac_amd.server.proxy import build_arg_parser
+
+    a = build_arg_parser().parse_args(["-s", "127.0.0.1:80", "--cache", "hbm",
+                                       "--hot-objects", "0", "--hot-refresh-ms", "250"])
+    assert a.hot_objects == 0 and a.hot_refresh_ms == 250
+    a = build_arg_parser().parse_args(["-s", "127.0.0.1:80"])
+    assert a.hot_objects == 1024 and a.hot_refresh_ms == 1000
