@@ -1150,8 +1150,9 @@ def main():
             pressured["stream"] = "walk" if walk else "cycled"
             pressured["set_batches_cycled"] = len(walk[2]) if walk else len(cyc["sets"])
             pressured["get_batches_cycled"] = len(walk[0]) if walk else len(cyc["gets"])
-        if walk is not None and not args.no_cycled:
-            # secondary: the same full cache on the 16 cycled batches (round 5's headline)
+        if walk is not None and not args.no_cycled and world == 1:
+            # secondary (N = 1): the same full cache on the 16 cycled batches (round 5's
+            # headline); skipped with more ranks, where each block repopulates every shard
             pressured_cycled = full_cache(p_gb, False)[0]
             if pressured_cycled is not None:
                 pressured_cycled["stream"] = "cycled"
