@@ -138,13 +138,21 @@ void bind_router(py::module_& m) {
 
   // plan_hot (host_router.h) over (lo, hi, count) rows with the router's owners
   m.def("plan_hot", [](const HostRouter& router, std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> rows,
-                       int k, uint64_t eligible, double spray_above, uint64_t min_count) {
+                       int k, uint64_t eligible, double spray_above, uint64_t min_count,
+                       std::vector<std::pair<uint64_t, uint64_t>> sticky, double sticky_factor) {
     std::vector<std::pair<Digest, uint64_t>> c;
     c.reserve(rows.size());
     for (auto& t : rows) c.emplace_back(Digest{std::get<0>(t), std::get<1>(t)}, std::get<2>(t));
+    std::vector<Digest> st;
+    for (auto& x : sticky) st.push_back(Digest{x.first, x.second});
+    const std::function<bool(const Digest&)> is_sticky = [&](const Digest& d) {
+      for (const Digest& x : st)
+        if (x.lo == d.lo && x.hi == d.hi) return true;
+      return false;
+    };
     const HotPlan p = plan_hot(c, k, router.nshards(), eligible,
                                [&](const Digest& d) { return router.owner(d); }, spray_above,
-                               min_count);
+                               min_count, st.empty() ? nullptr : &is_sticky, sticky_factor);
     py::list hot;
     for (const Digest& d : p.hot) hot.append(py::make_tuple(d.lo, d.hi));
     py::dict out;
@@ -155,7 +163,9 @@ void bind_router(py::module_& m) {
     out["planned"] = p.planned;
     return out;
   }, py::arg("router"), py::arg("rows"), py::arg("k"), py::arg("eligible"),
-     py::arg("spray_above"), py::arg("min_count") = 2);
+     py::arg("spray_above"), py::arg("min_count") = 2,
+     py::arg("sticky") = std::vector<std::pair<uint64_t, uint64_t>>{},
+     py::arg("sticky_factor") = 1.0);
 
   m.def("step_streams", [](int device) {
     const StepStreams& ss = step_streams(device);

@@ -165,3 +165,27 @@ def test_native_hot_plan_matches_hotspread_design(world):
     el = (1 << world) - 1 - 2
     plan = core().plan_hot(hs.router, rows, 200, el, 1.0 / (4 * world), 1)
     assert 1 not in plan["rank"] and plan["weights"][1] == 0.0
+
+
+def test_native_hot_plan_hysteresis_keeps_the_replicated_tail():
+    """The HBM tier re-plans its hot set every refresh from decayed sampled counts; objects
+    already replicated rank at 2x (sticky), so a tail object is replaced only by one at least
+    twice as hot — sampling noise does not churn fills and deletes."""
+    from shellac_amd import core
+
+    r = core().HostRouter(4)
+    rows = [(1000 + i, 7 * i + 1, 100 - i) for i in range(60)]  # counts 100 .. 41
+    top = core().plan_hot(r, rows, 10, 0b1111, 0.25, 1)
+    assert [h[0] for h in top["hot"]] == list(range(1000, 1010))
+    # a tail object of the current set (count 60) against colder newcomers above it
+    cur = [(1040, 7 * 40 + 1)]
+    plan = core().plan_hot(r, rows, 10, 0b1111, 0.25, 1, sticky=cur, sticky_factor=2.0)
+    hot = [h[0] for h in plan["hot"]]
+    assert 1040 in hot and 1009 not in hot  # 60 x 2 = 120 outranks the 91 of the newcomer
+    # ... but not against one more than twice as hot
+    rows2 = rows + [(5000, 3, 130)]
+    plan = core().plan_hot(r, rows2, 10, 0b1111, 0.25, 1, sticky=cur, sticky_factor=2.0)
+    hot = [h[0] for h in plan["hot"]]
+    assert 5000 in hot and 1040 in hot
+    # the designation loads use the true counts (the sticky factor ranks only)
+    assert abs(sum(plan["planned"]) - 1.0) < 1e-9
