@@ -87,9 +87,10 @@ def test_hot_spreading_evens_out_per_shard_gets(nshards):
 
 def test_hot_spreading_never_serves_stale_or_deleted_copies():
     """SETs and DELETEs of hot objects are written through: a GET issued after them sees
-    them on whichever replica it lands. Hot-set refreshes while a writer updates versions
-    never let a reader see a version older than one whose SET had returned before the
-    GET, and objects that cool lose their non-owner replicas (a later promotion refills)."""
+    them on whichever replica it lands. Hot-set refreshes while one writer updates versions
+    and another SETs then DELETEs objects in turn never let a reader see a version older
+    than one whose SET had returned before the GET, nor a version whose DELETE had returned;
+    objects that cool lose their non-owner replicas (a later promotion refills)."""
     be = _backend(4, 64, hot_sample=1)
     _fill(be)
     rng = np.random.default_rng(11)
@@ -127,17 +128,40 @@ def test_hot_spreading_never_serves_stale_or_deleted_copies():
                     committed[i] = v
             v += 1
 
+    # a second writer SETs and then DELETEs 16 more objects in turn (a DELETE returns once
+    # every copy is gone): a GET issued after it must not return the deleted version
+    churn = list(range(24, 32)) + list(range(2024, 2032))
+    last = {i: (0, "set") for i in churn}
+
+    def deleter():
+        v = 10
+        while not stop.is_set():
+            for i in churn:
+                be.set(KEYS[i], _val(i, v), v, 0)
+                with lock:
+                    last[i] = (v, "set")
+                be.delete(KEYS[i])
+                with lock:
+                    last[i] = (v, "del")
+            v += 1
+
     def reader():
         while not stop.is_set():
             with lock:
                 snap = dict(committed)
-            got = be.get_many([KEYS[i] for i in watched])
+                snap_c = dict(last)
+            got = be.get_many([KEYS[i] for i in watched + churn])
             for i, g in zip(watched, got):
                 if g is None or g[1] < snap[i] or g[0] != _val(i, g[1]):
                     errors.append((i, snap[i], g))
+            for i, g in zip(churn, got[len(watched):]):
+                v, kind = snap_c[i]
+                if g is not None and (g[1] < v or (kind == "del" and g[1] == v) or
+                                      g[0] != _val(i, g[1])):
+                    errors.append((i, snap_c[i], g))
 
-    th = [threading.Thread(target=writer), threading.Thread(target=reader),
-          threading.Thread(target=reader)]
+    th = [threading.Thread(target=writer), threading.Thread(target=deleter),
+          threading.Thread(target=reader), threading.Thread(target=reader)]
     for t in th:
         t.start()
     totals = {"added": 0, "removed": 0, "replicas_dropped": 0}
