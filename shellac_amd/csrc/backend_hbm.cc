@@ -1952,8 +1952,9 @@ StatList HbmBackend::hot_refresh_locked() {
       dv->touched.clear();
     }
   };
-  // ---- 3. T1: write-through for the new objects, their GETs at their owners
-  {
+  // ---- 3. T1: write-through for the new objects, their GETs at their owners (nothing new:
+  // the published table already is T1)
+  if (!added.empty()) {
     std::vector<Digest> h(hot_set_);
     std::vector<int32_t> rk(hot_rank_);
     for (const Digest& d : plan.hot)
@@ -2211,7 +2212,13 @@ StatList HbmBackend::hot_refresh_locked() {
   for (int r = 0; r < N; ++r)  // an ejection that raced the store above
     if (devs_[(size_t)r]->eject_gen.load() != gen0[(size_t)r] || !devs_[(size_t)r]->up())
       spread_mask_.fetch_and(~(1ull << r), std::memory_order_acq_rel);
-  router_->set_hot(final_hot.data(), (int64_t)final_hot.size(), final_rank.data(), wts.data());
+  const bool same = added.empty() && final_hot.size() == hot_set_.size() &&
+                    final_rank == std::vector<int32_t>(hot_rank_.begin(), hot_rank_.end()) &&
+                    wts == hot_weights_ &&
+                    std::equal(final_hot.begin(), final_hot.end(), hot_set_.begin(),
+                               [](const Digest& x, const Digest& y) { return x.lo == y.lo && x.hi == y.hi; });
+  if (!same)  // (an unchanged table is not republished)
+    router_->set_hot(final_hot.data(), (int64_t)final_hot.size(), final_rank.data(), wts.data());
   // ---- 8. replicas of objects no longer hot (the old set and this refresh's write-through
   // set minus the new one) go from every shard but their owner
   std::unordered_set<Digest, DigestHash, DigestEq> fin(final_hot.begin(), final_hot.end());
