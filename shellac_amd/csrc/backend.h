@@ -322,8 +322,14 @@ class HbmBackend : public CacheBackend {
   std::mutex hot_th_mu_;
   std::condition_variable hot_cv_;
   bool hot_stop_ = false;
+  // GETs answered by a non-owner replica, sharded by the routing thread's slot (every
+  // reactor counts without sharing a line)
+  struct alignas(64) SpreadCtr {
+    std::atomic<uint64_t> v{0};
+  };
+  SpreadCtr hot_spread_gets_[16];
   std::atomic<uint64_t> hot_refreshes_{0}, hot_added_{0}, hot_removed_{0}, hot_filled_{0},
-      hot_fill_skipped_{0}, hot_fill_failed_{0}, hot_spread_gets_{0}, hot_deferred_{0},
+      hot_fill_skipped_{0}, hot_fill_failed_{0}, hot_deferred_{0},
       hot_fill_bytes_{0}, hot_refresh_us_{0}, hot_samples_{0}, hot_objects_{0},
       hot_dropped_replicas_{0};
 };

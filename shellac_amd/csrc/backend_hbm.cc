@@ -607,7 +607,7 @@ int HbmBackend::route_get(const Digest& d) {
     }
     if (r >= 0 && ((up & spread_mask_.load(std::memory_order_acquire)) >> r) & 1) {
       const int o = owner_of(d, up);
-      if (r != o) hot_spread_gets_.fetch_add(1, std::memory_order_relaxed);
+      if (r != o) hot_spread_gets_[tl_sample_slot % 16].v.fetch_add(1, std::memory_order_relaxed);
       return r;
     }
   }
@@ -2359,7 +2359,9 @@ void HbmBackend::stats(StatList* out) {
     out->emplace_back("hbm_hot_fill_failures", hot_fill_failed_.load());
     out->emplace_back("hbm_hot_fill_bytes", hot_fill_bytes_.load());
     out->emplace_back("hbm_hot_replicas_dropped", hot_dropped_replicas_.load());
-    out->emplace_back("hbm_hot_spread_gets", hot_spread_gets_.load());
+    uint64_t sg = 0;
+    for (const SpreadCtr& c : hot_spread_gets_) sg += c.v.load(std::memory_order_relaxed);
+    out->emplace_back("hbm_hot_spread_gets", sg);
     out->emplace_back("hbm_hot_samples", hot_samples_.load());
     out->emplace_back("hbm_hot_spread_mask", spread_mask_.load());
     out->emplace_back("hbm_hot_refresh_us_last", hot_refresh_us_.load());
