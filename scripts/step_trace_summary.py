@@ -53,3 +53,15 @@ if os.environ.get("STEP_TABLE"):
         for s,e,n,_,_ in ks:
             if a<=s<b: row[n]+=e-s
         print(f"{(b-a)/1e3:7.1f} | "+" | ".join(f"{row[n]/1e3:6.1f}" for n in top))
+# SPAN=n: every kernel of the last n steps on one GPU clock (origin: the first k_coalesce
+# among them), with its queue: the cross-stream hand-offs and in-queue gaps of the chains
+if os.environ.get("SPAN"):
+    nspan=int(os.environ["SPAN"]); a=st[-nspan-1]; b=st[-1]
+    sel=[x for x in ks if a<=x[0]<b]
+    org=next((s for s,e,n,q,sid in sel if n.startswith("k_coalesce")),sel[0][0] if sel else 0)
+    print(f"--- last {nspan} steps on the GPU clock (origin: first k_coalesce)")
+    lastq={}
+    for s,e,n,q,sid in sel:
+        g=(s-lastq[q])/1e3 if q in lastq else float('nan')
+        print(f"{(s-org)/1e3:8.1f} {(e-org)/1e3:8.1f} {(e-s)/1e3:7.1f} qgap {g:6.1f} q{q:>3} {n}")
+        lastq[q]=max(lastq.get(q,0),e)
