@@ -479,7 +479,7 @@ def main():
         group = BounceComm()
 
     if args.replicate is None:
-        # device-routed step: the per-N table (profiles/r4_sweep2, docs/PERF.md) — every
+        # device-routed step: the per-N table (profiles/archive/r4_sweep2, docs/PERF.md) — every
         # N is link-bound, and 1M replicated objects give the lowest max(compute, link) at
         # N=2 and N=8 and are within 1 % of it at N=4
         args.replicate = 1 << 20

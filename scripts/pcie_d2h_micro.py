@@ -2,7 +2,7 @@
 """PCIe DMA rates on one MI355X: hipMemcpyAsync (torch's non_blocking copy_) of an HBM
 buffer into pinned host memory and back, for the response sizes of the N=1 step (64 and
 320 MiB). Prints GB/s. The gather kernel's own stores into pinned memory ran at ~38 GB/s
-(bench.py --edge host, round 3); profiles/r4s_edge_host compares the two in the step."""
+(bench.py --edge host, round 3); profiles/archive/r4s_edge_host compares the two in the step."""
 import time
 
 import torch

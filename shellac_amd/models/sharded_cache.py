@@ -250,7 +250,7 @@ class ShardedCache:
         # box, two rounds: 0.309 / 0.308 ms per step with "device" vs 0.315 / 0.311 with
         # "system" (profiles/archive/r2_event_fence_ab.log); round 4, one box, two rounds each:
         # wrapped 0.3362 / 0.3363 "device" vs 0.3313 / 0.3304 "none", fresh 0.3008 / 0.3004
-        # vs 0.2953 / 0.2952 (profiles/r4h_fence)
+        # vs 0.2953 / 0.2952 (profiles/archive/r4h_fence)
         self.event_fence = "none"
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
