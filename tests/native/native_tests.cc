@@ -200,6 +200,85 @@ void test_host_router_pool() {
   }
 }
 
+// The hot table swapped under routing (the proxy's refresh beside its reactors): readers
+// hold Read guards and route small batches while a writer alternates two hot sets. Every
+// decision is one of the two tables' (never a torn one), and when set_hot returns no reader
+// is still inside a guard on the previous table (the refresh protocol relies on it). Under
+// TSAN this is the race check of the lock-free read side.
+void test_host_router_hot_swap_concurrent() {
+  constexpr int kShards = 8, kReaders = 4;
+  HostRouter r(kShards, 64);
+  std::vector<Digest> keys(4096);
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (auto& d : keys) {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    d.lo = x;
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    d.hi = x;
+  }
+  // table A: keys [0, 1024) on rank i % 8; table B: keys [512, 1512) on rank (i + 3) % 8
+  std::vector<int32_t> ra(1024), rb(1000);
+  for (int i = 0; i < 1024; ++i) ra[(size_t)i] = i % kShards;
+  for (int i = 0; i < 1000; ++i) rb[(size_t)i] = (512 + i + 3) % kShards;
+  const std::vector<double> w(kShards, 1.0);
+  auto want = [&](int table, int k) {  // the rank table A (0) or B (1) gives key k
+    if (table == 0) return k < 1024 ? ra[(size_t)k] : HostRouter::kNotHot;
+    return k >= 512 && k < 1512 ? rb[(size_t)(k - 512)] : HostRouter::kNotHot;
+  };
+  r.set_hot(keys.data(), 1024, ra.data(), w.data());
+  std::atomic<bool> stop{false};
+  std::atomic<int> bad{0};
+  std::atomic<int64_t> held[kReaders];
+  std::atomic<uint64_t> decisions{0};
+  for (auto& h : held) h.store(-1);
+  std::vector<std::thread> th;
+  for (int t = 0; t < kReaders; ++t)
+    th.emplace_back([&, t] {
+      std::vector<int32_t> dest(64);
+      std::vector<int64_t> cnt(kShards);
+      uint64_t n = 0;
+      for (uint32_t it = 0; !stop.load(std::memory_order_acquire); ++it) {
+        const int k = (int)((it * 2654435761u + (uint32_t)t * 977u) % 1600u);
+        {
+          const HostRouter::Read rd(r);
+          const int64_t nh = rd.table().nhot;
+          held[t].store(nh, std::memory_order_release);
+          const int got = rd.hot_rank(keys[(size_t)k]);
+          if (!((nh == 1024 && got == want(0, k)) || (nh == 1000 && got == want(1, k))))
+            bad.fetch_add(1);
+          held[t].store(-1, std::memory_order_release);
+        }
+        if ((it & 63) == 0) {  // a batch through the routing call (its own guard)
+          std::fill(cnt.begin(), cnt.end(), 0);
+          r.route_gets(keys.data() + (k & ~63), 64, 0, dest.data(), cnt.data(), 1);
+          for (int i = 0; i < 64; ++i) {
+            const int kk = (k & ~63) + i;
+            const int own = r.owner(keys[(size_t)kk]);
+            const int a = want(0, kk) == HostRouter::kNotHot ? own : want(0, kk);
+            const int b = want(1, kk) == HostRouter::kNotHot ? own : want(1, kk);
+            if (dest[(size_t)i] != a && dest[(size_t)i] != b) bad.fetch_add(1);
+          }
+        }
+        ++n;
+      }
+      decisions.fetch_add(n);
+    });
+  for (int rep = 0; rep < 200; ++rep) {
+    const bool to_b = rep % 2 == 0;
+    const int64_t old = to_b ? 1024 : 1000;
+    if (to_b)
+      r.set_hot(keys.data() + 512, 1000, rb.data(), w.data());
+    else
+      r.set_hot(keys.data(), 1024, ra.data(), w.data());
+    for (auto& h : held)
+      if (h.load(std::memory_order_acquire) == old) bad.fetch_add(1);  // grace period broken
+  }
+  stop.store(true, std::memory_order_release);
+  for (auto& t : th) t.join();
+  CHECK(bad.load() == 0);
+  CHECK(decisions.load() > 1000);
+}
+
 // ---------------------------------------------------------------------------------
 // Minimal keep-alive origin: one thread per connection, Content-Length bodies.
 class Origin {
@@ -351,6 +430,7 @@ int main(int argc, char** argv) {
       {"stream_buf", test_stream_buf},
       {"ketama", test_ketama},
       {"host_router_pool", test_host_router_pool},
+      {"host_router_hot_swap", test_host_router_hot_swap_concurrent},
       {"proxy_threads_dram", [] { test_proxy_threads_dram(nullptr); }},
       {"proxy_threads_fault", [] { test_proxy_threads_dram("get_miss=0.3,set_drop=0.3,delay_us=200"); }},
       {"proxy_memcached_node", test_proxy_over_memcached_node},

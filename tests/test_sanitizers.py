@@ -2,7 +2,8 @@
 
 Builds the host-only library and tests/native/native_tests.cc with the CMake presets
 (CMakePresets.json) and runs the driver: HostCache against an oracle, HTTP parser
-splits + garbage, StreamBuf, ketama ejection, and the multi-threaded proxy (4 reactor
+splits + garbage, StreamBuf, ketama ejection, the host router (worker pool; hot table
+swapped under concurrent readers), and the multi-threaded proxy (4 reactor
 threads) over DRAM, fault-injected DRAM (timer thread) and a memcached-protocol node
 (IO thread). Any sanitizer report fails the test."""
 import os
