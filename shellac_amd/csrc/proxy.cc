@@ -9,6 +9,7 @@
 #include <sys/uio.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdlib>
 #include <cmath>
@@ -603,9 +604,13 @@ void Reactor::on_request(Client* c) {
   s->seq = c->next_seq++;
   s->t0 = now_s();
   s->close_after = !q.keep_alive() || c->nreq >= cfg_.client_max_reqs;
-  if (url == "/_shellac/stats") {
-    s->out.write(simple_response(200, "OK", cfg_.server_name, px_->stats_json(),
-                                 "application/json", s->close_after));
+  if (url == "/_shellac/stats" || url == "/_shellac/metrics") {
+    // the same counters as JSON, or in the Prometheus text format for a scraper
+    const bool prom = url == "/_shellac/metrics";
+    s->out.write(simple_response(200, "OK", cfg_.server_name,
+                                 prom ? prometheus_text(px_->stats_json()) : px_->stats_json(),
+                                 prom ? "text/plain; version=0.0.4" : "application/json",
+                                 s->close_after));
     s->out.close();
     s->ready = true;
     c->slots.push_back(std::move(s));
@@ -1486,6 +1491,96 @@ void Proxy::wait() {
 void Proxy::stop() {
   running_ = false;
   for (auto& r : reactors_) r->wake();
+}
+
+namespace {
+// A minimal reader of the stats JSON above (objects, arrays, numbers, strings; no escapes
+// beyond \" are ever produced), flattened into Prometheus samples: nested keys join with
+// '_' under the `shellac_` prefix, array elements become an `i` label, and string fields
+// (server, backend) become labels of one `shellac_info` sample.
+struct PromFlat {
+  const std::string& j;
+  size_t p = 0;
+  std::ostringstream out;
+  std::vector<std::pair<std::string, std::string>> info;
+  explicit PromFlat(const std::string& s) : j(s) {}
+  void ws() {
+    while (p < j.size() && (j[p] == ' ' || j[p] == '\n' || j[p] == '\t' || j[p] == '\r')) ++p;
+  }
+  std::string str() {
+    std::string r;
+    ++p;  // opening quote
+    while (p < j.size() && j[p] != '"') {
+      if (j[p] == '\\' && p + 1 < j.size()) ++p;
+      r += j[p++];
+    }
+    ++p;
+    return r;
+  }
+  static std::string clean(const std::string& k) {
+    std::string r;
+    for (char c : k) r += (std::isalnum((unsigned char)c) || c == '_') ? c : '_';
+    return r;
+  }
+  void value(const std::string& name, const std::string& label) {
+    ws();
+    if (p >= j.size()) return;
+    const char c = j[p];
+    if (c == '{') {
+      ++p;
+      for (;;) {
+        ws();
+        if (p < j.size() && j[p] == '}') {
+          ++p;
+          return;
+        }
+        const std::string k = str();
+        ws();
+        ++p;  // ':'
+        value(name.empty() ? clean(k) : name + "_" + clean(k), label);
+        ws();
+        if (p < j.size() && j[p] == ',') ++p;
+      }
+    } else if (c == '[') {
+      ++p;
+      for (int i = 0;; ++i) {
+        ws();
+        if (p < j.size() && j[p] == ']') {
+          ++p;
+          return;
+        }
+        value(name, "i=\"" + std::to_string(i) + "\"");
+        ws();
+        if (p < j.size() && j[p] == ',') ++p;
+      }
+    } else if (c == '"') {
+      info.emplace_back(name, str());
+    } else {
+      const size_t a = p;
+      while (p < j.size() && j[p] != ',' && j[p] != '}' && j[p] != ']' && !std::isspace((unsigned char)j[p])) ++p;
+      out << "shellac_" << name;
+      if (!label.empty()) out << "{" << label << "}";
+      out << " " << j.substr(a, p - a) << "\n";
+    }
+  }
+};
+}  // namespace
+
+std::string prometheus_text(const std::string& stats_json) {
+  PromFlat f(stats_json);
+  f.value("", "");
+  std::ostringstream o;
+  if (!f.info.empty()) {
+    o << "shellac_info{";
+    for (size_t i = 0; i < f.info.size(); ++i) {
+      std::string v;
+      for (char c : f.info[i].second) v += (c == '"' || c == '\\') ? '_' : c;
+      o << (i ? "," : "") << f.info[i].first << "=\"" << v << "\"";
+    }
+    o << "} 1\n";
+  }
+  o << f.out.str();
+  return o.str();
 }
 
 std::string Proxy::stats_json() {

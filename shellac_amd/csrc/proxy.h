@@ -128,4 +128,9 @@ class Proxy {
   double start_time_ = 0;
 };
 
+// The stats JSON (Proxy::stats_json) as Prometheus text-format samples (GET
+// /_shellac/metrics): nested keys joined with '_' under `shellac_`, array elements as an
+// `i` label, string fields as labels of `shellac_info`.
+std::string prometheus_text(const std::string& stats_json);
+
 }  // namespace shellac

@@ -356,6 +356,34 @@ def test_stats_endpoint(origin):
         assert "p99" in st["latency_us"]
 
 
+def test_metrics_endpoint_is_prometheus_text(origin):
+    """GET /_shellac/metrics: the stats endpoint's counters as Prometheus text samples
+    (nested keys joined, arrays as an index label, string fields as labels of
+    shellac_info), every sample line `name[{labels}] number`, the same values as the JSON."""
+    import re
+
+    with make_proxy([origin.port]) as px:
+        c = HttpClient(port=px.port)
+        for i in range(3):
+            c.get("/m%d" % i)
+        st = json.loads(c.get("/_shellac/stats").body().read())
+        r = c.get("/_shellac/metrics")
+        assert r.status() == 200 and "text/plain" in str(r.headers())
+        lines = r.body().read().decode().strip().splitlines()
+    sample = re.compile(r'^shellac_[A-Za-z0-9_]+(\{[A-Za-z_]+="[^"]*"(,[A-Za-z_]+="[^"]*")*\})? -?[0-9.eE+-]+$')
+    assert lines and all(sample.match(ln) for ln in lines), [ln for ln in lines if not sample.match(ln)]
+    vals = {}
+    for ln in lines:
+        name, v = ln.rsplit(" ", 1)
+        vals[name] = float(v)
+    assert any(k.startswith("shellac_info{") and 'backend="dram"' in k for k in vals)
+    assert vals["shellac_cache_hits"] + vals["shellac_cache_misses"] >= 3
+    assert vals["shellac_requests"] >= st["requests"]
+    assert "shellac_latency_us_p99" in vals and 'shellac_upstreams_up{i="0"}' in vals
+    for k, v in st["cache"].items():
+        assert "shellac_cache_" + k in vals
+
+
 def test_kill_switch(origin):
     px = make_proxy([origin.port])
     c = HttpClient(port=px.port)
