@@ -322,6 +322,17 @@ PYBIND11_MODULE(_shellac_core, m) {
     SH_CHECK(hipStreamWaitEvent(S(s), reinterpret_cast<hipEvent_t>(e), 0) == hipSuccess,
              "hipStreamWaitEvent failed");
   });
+  // raw streams a caller owns (tests: a stream destroyed while a cache still remembers it)
+  m.def("stream_create", []() {
+    hipStream_t st = nullptr;
+    SH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess,
+             "hipStreamCreateWithFlags failed");
+    return reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("stream_destroy", [](uintptr_t s) {
+    SH_CHECK(hipStreamSynchronize(S(s)) == hipSuccess && hipStreamDestroy(S(s)) == hipSuccess,
+             "hipStreamDestroy failed");
+  });
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -281,11 +281,13 @@ class HbmCache {
   uint64_t* cur_ring_tail() const { return head_ + 2 + hsel_; }
   uint64_t* next_ring_tail() const { return head_ + 2 + (hsel_ ^ 1); }
   // Deferred frees (no device-wide synchronisation on the serving path): a grown buffer's
-  // old blocks are retired as a group with an event recorded on every stream SET work was
-  // queued on (`note_stream`) and the growing call's; reap_retired frees a group once its
-  // events have completed (every chain that could read the old blocks has finished) — at
-  // the start of every store and in sweep; reserve (which synchronises the device) and the
-  // destructor free every group.
+  // old blocks are retired as a group with one event recorded on the growing call's stream
+  // after it has waited for the last store queued on every other stream SET work used
+  // (`note_stream`; each store records its stream's `last` event when it returns, so no
+  // call ever records on a stream the caller may since have destroyed); reap_retired frees
+  // a group once its event has completed (every chain that could read the old blocks has
+  // finished) — at the start of every store and in sweep; reserve (which synchronises the
+  // device) and the destructor free every group.
   struct RetiredGroup {
     std::vector<void*> ptrs;
     std::vector<hipEvent_t> ev;
@@ -294,9 +296,14 @@ class HbmCache {
   void retire_group(std::initializer_list<void*> ptrs, uint64_t bytes, hipStream_t s);
   void reap_retired(bool all);
   void note_stream(hipStream_t s);
+  void note_store_end(hipStream_t s);
   std::vector<RetiredGroup> retired_;
   uint64_t retired_ever_ = 0;
-  std::vector<hipStream_t> set_streams_;
+  struct SetStream {
+    hipStream_t s = nullptr;
+    hipEvent_t last = nullptr;  // recorded after the last store queued on s
+  };
+  std::vector<SetStream> set_streams_;
   // The SET workspace's tables are cleared on the stream of the call that grew them;
   // a store on another stream waits for that (ws_ready_) once (ws_ordered_).
   hipEvent_t ws_ready_ = nullptr;

@@ -3247,6 +3247,8 @@ HbmCache::~HbmCache() {
       (void)hipFree(p);
   reap_retired(true);
   if (ws_ready_) (void)hipEventDestroy(ws_ready_);
+  for (const SetStream& x : set_streams_)
+    if (x.last) (void)hipEventDestroy(x.last);
 }
 
 void HbmCache::retire_group(std::initializer_list<void*> ptrs, uint64_t bytes, hipStream_t s) {
@@ -3256,14 +3258,14 @@ void HbmCache::retire_group(std::initializer_list<void*> ptrs, uint64_t bytes, h
   if (g.ptrs.empty()) return;
   g.bytes = bytes;
   retired_ever_ += bytes;
-  std::vector<hipStream_t> all = set_streams_;
-  if (std::find(all.begin(), all.end(), s) == all.end()) all.push_back(s);
-  for (hipStream_t x : all) {
-    hipEvent_t e;
-    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_OK(hipEventRecord(e, x));
-    g.ev.push_back(e);
-  }
+  // the growing stream waits for the other SET streams' last stores (their events, not
+  // their streams: a stream a caller has destroyed is never touched), then one event
+  for (const SetStream& x : set_streams_)
+    if (x.s != s && x.last) HIP_OK(hipStreamWaitEvent(s, x.last, 0));
+  hipEvent_t e;
+  HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(e, s));
+  g.ev.push_back(e);
   retired_.push_back(std::move(g));
 }
 
@@ -3300,8 +3302,20 @@ void HbmCache::ws_order(hipStream_t s) {
 }
 
 void HbmCache::note_stream(hipStream_t s) {
-  if (std::find(set_streams_.begin(), set_streams_.end(), s) == set_streams_.end())
-    set_streams_.push_back(s);
+  for (const SetStream& x : set_streams_)
+    if (x.s == s) return;
+  SetStream x;
+  x.s = s;
+  HIP_OK(hipEventCreateWithFlags(&x.last, hipEventDisableTiming));
+  set_streams_.push_back(x);
+}
+
+void HbmCache::note_store_end(hipStream_t s) {
+  for (const SetStream& x : set_streams_)
+    if (x.s == s) {
+      (void)hipEventRecord(x.last, s);
+      return;
+    }
 }
 
 uint64_t HbmCache::hbm_bytes() const {
@@ -3743,6 +3757,11 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard g(cfg_.device);
   note_stream(s);
+  struct EndMark {  // the stream's `last` event, after whatever this call queues
+    HbmCache* c;
+    hipStream_t s;
+    ~EndMark() { c->note_store_end(s); }
+  } end_mark{this, s};
   if (!retired_.empty()) reap_retired(false);  // grown-out workspaces whose chains finished
   // phase 2: the rest of the chain of the batch a phase-1 call planned
   if (phase == 2) {

@@ -1228,7 +1228,7 @@ def test_host_edge_serve_matches_device_edge(cuda_dev, dma):
 @pytest.mark.gpu
 def test_set_workspace_grows_then_frees_retired_blocks(cuda_dev):
     """SET batches growing 8x (1000 -> 8000 rows, on two streams in turn): every grow
-    retires the old SET workspace with events on the streams that used it, and once those
+    retires the old SET workspace behind the last stores of the streams that used it, and once those
     chains have drained the next store frees it — retired bytes back to 0, no keep-forever
     and no device synchronisation in store. A store on the other
     stream is ordered after the grow's dedupe-table clears: every value lands."""
@@ -1253,6 +1253,39 @@ def test_set_workspace_grows_then_frees_retired_blocks(cuda_dev):
     s.set_many([b"/grow/last"], [b"x" * 10])  # a store reaps the groups whose chains drained
     torch.cuda.synchronize()
     assert s._impl.retired_bytes() == 0
+    for keys, vals in written:
+        assert s.get_many(keys) == vals
+
+
+def test_set_workspace_grow_after_a_store_stream_was_destroyed(cuda_dev):
+    """A SET on a caller's raw stream that the caller then destroys, then SET batches that
+    grow the workspace on the current stream: the retire must not touch the dead stream
+    (it waits for that stream's last-store event instead), the retired blocks are freed
+    once drained, and every value lands."""
+    from shellac_amd import core
+    from shellac_amd.ops.cache import CacheShard
+
+    c = core()
+    s = CacheShard(64 << 20, 1 << 15, 1 << 14, cuda_dev)
+    raw = c.stream_create()
+    ext = torch.cuda.ExternalStream(raw, device=cuda_dev)
+    with torch.cuda.stream(ext):
+        s.set_many([b"/dead/%d" % i for i in range(500)], [b"d%d" % i for i in range(500)])
+    c.stream_destroy(raw)
+    del ext
+    ever0 = s._impl.retired_ever
+    written = []
+    for step, n in enumerate((1000, 4000, 16000)):
+        keys = [b"/after/%d/%d" % (step, i) for i in range(n)]
+        vals = [b"a%d-%d" % (step, i) for i in range(n)]
+        s.set_many(keys, vals)
+        written.append((keys, vals))
+    torch.cuda.synchronize()
+    assert s._impl.retired_ever > ever0
+    s.set_many([b"/after/last"], [b"x"])
+    torch.cuda.synchronize()
+    assert s._impl.retired_bytes() == 0
+    assert s.get_many([b"/dead/%d" % i for i in range(500)]) == [b"d%d" % i for i in range(500)]
     for keys, vals in written:
         assert s.get_many(keys) == vals
 
