@@ -3306,7 +3306,8 @@ void HbmCache::note_stream(hipStream_t s) {
     if (x.s == s) return;
   SetStream x;
   x.s = s;
-  HIP_OK(hipEventCreateWithFlags(&x.last, hipEventDisableTiming));
+  // (only orders execution: no system-scope cache flush at every store's end marker)
+  HIP_OK(hipEventCreateWithFlags(&x.last, hipEventDisableTiming | hipEventDisableSystemFence));
   set_streams_.push_back(x);
 }
 
