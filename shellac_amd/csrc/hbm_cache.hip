@@ -3,7 +3,7 @@
 // Kernel map (all wave64, 256-thread workgroups):
 //   k_coalesce     GET request collapsing: each workgroup collapses a 1024-key chunk
 //                  in an LDS table, its local claimers claim a global open-addressing
-//                  table (one CAS; a plain load first for keys repeated in the chunk),
+//                  table (a plain load, then one CAS where the slot is still free),
 //                  and (PROBE) the global claimers are probed by 8-lane groups.
 //   k_probe        8 lanes per key, digests staged in LDS, 3 keys in flight per
 //                  group: the group reads the first bucket (one 128-B line) and only
@@ -534,8 +534,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
 // key alone (measured: 330 us per 1M-key batch). Each workgroup therefore first
 // collapses its own chunk of 1024 keys in an LDS table, and only its local claimers go
 // to the global table: a key's global atomics are bounded by the number of chunks.
-// A local claimer that saw local duplicates (likely hot) reads the global slot before
-// it CASes; a local single goes straight to the CAS (one round trip).
+// Every local claimer reads the global slot before it CASes: the ~780K claims of a 1M
+// Zipf batch are bound by the memory-side atomics' throughput, and a slot another chunk
+// already took costs a load instead of an atomic (round 5 read first only for keys repeated
+// in the chunk; reading first for all took the lookup from 101.7 to 97.1 us).
 // PROBE: the global claimer of a digest also probes the shard's index for it (one lane
 // reads the 128-B bucket), so coalescing and lookup are one pass over the batch, and
 // the workgroup's contiguous row range yields the partial sums k_offsets scans.
@@ -621,10 +623,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const int j = u * kBlock + threadIdx.x;
         act[u] = !local_only && j < cnt && lrep[u] == (uint32_t)j;
         hh[u] = (uint32_t)(dk[u].hi ^ (dk[u].hi >> 29)) & tmask;
-        // likely hot (seen again in this chunk): read before the CAS
-        vv[u] = act[u] && s_dup[j] > 0
-                    ? __hip_atomic_load(tab + hh[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : 0u;
+        // read before the CAS: a slot another chunk's claimer already holds needs no atomic
+        // (the global claims are bound by the memory-side atomics' throughput: ~52 of the
+        // lookup's ~100 us; reading first took the lookup from 101.7 to 97.1 us,
+        // profiles/archive/r6_fused_gather_rejected/README.md)
+        vv[u] = act[u] ? __hip_atomic_load(tab + hh[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kCoPer; ++u)
