@@ -252,6 +252,16 @@ class ShardedCache:
         # wrapped 0.3362 / 0.3363 "device" vs 0.3313 / 0.3304 "none", fresh 0.3008 / 0.3004
         # vs 0.2953 / 0.2952 (profiles/archive/r4h_fence)
         self.event_fence = "none"
+        # the step's cross-stream events ride on the kernels' own completion signals: the
+        # lookup's probe completes `probe` (the index insert's wait), the SET chain's index
+        # fix-up completes the step's end (the next lookup's wait), and the log append waits
+        # for the step's input event instead of a `start` marker behind the previous chain
+        # — no marker packet on the main stream's critical path (each costs ~2.7 us; a stop
+        # event is seen ~2.4 us sooner across streams than a recorded one: profiles/r6_hop).
+        # Needs StreamEvents (event_fence != "system"). SHELLAC_STOP_EVENTS=0: markers.
+        self.stop_events = os.environ.get("SHELLAC_STOP_EVENTS", "1") != "0"
+        # fence scope of the events kernels complete as stop events (A/B: SHELLAC_STOP_FENCE)
+        self.stop_fence = os.environ.get("SHELLAC_STOP_FENCE", "none")
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
         # one GPU, a full cache: where the SET batch's CLOCK hand runs (see serve).
@@ -537,13 +547,22 @@ class ShardedCache:
                 batch = staged_batch(batch)
                 sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                          batch.expire, now, phase=1, plan_done=planned)
+        stop = self.stop_events and self.event_fence != "system"
         if self._side_pending:
             self._wait(main, self._ends[(k - 1) % 2])   # the previous step's SET chain
             self._side_pending = False
-        start = self._event("start")
-        start.record(main)                   # ... and its gather: the append may overwrite
+        if stop and inputs_ready is None:
+            # the append follows the previous step's gather (and everything else queued on
+            # main before this call: `ready` marks it); the previous chain precedes it on
+            # the side stream itself
+            start = ready
+        else:
+            start = self._event("start")
+            start.record(main)               # ... and its gather: the append may overwrite
+        ev = self._event("probe")
         try:
-            lk, first, cslot, table = self._lookup_step(keys, now, bound, side)
+            lk, first, cslot, table = self._lookup_step(keys, now, bound, side,
+                                                        ev if stop else None)
         except BaseException:
             if early:
                 # the planned batch still runs its chain (the native store pairs phase 1
@@ -559,8 +578,8 @@ class ShardedCache:
         if first is not None:
             out_size = torch.empty(n, dtype=torch.int64, device=self.device)
             out_off = torch.empty(n, dtype=torch.int64, device=self.device)
-        ev = self._event("probe")
-        ev.record(main)
+        if not (stop and self._probe_stopped):
+            ev.record(main)
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
             if early:
@@ -568,10 +587,11 @@ class ShardedCache:
             else:
                 self._wait(side, ready)
                 batch = staged_batch(batch)
+            end = self._end_event(k) if stop else None
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now, index_after=ev, append_after=start, append_done=appended,
-                     phase=2 if early else 0)
-        self._end_step(side, k, batch, early)
+                     phase=2 if early else 0, done=end)
+        self._end_step(side, k, batch, early, recorded=end is not None)
         if appended is not None:
             # the gather runs after the log append, not beside it: the two byte movers
             # contending for HBM are slower together than one after the other
@@ -585,15 +605,27 @@ class ShardedCache:
             return GetResult(data, out_off, out_size, self._take_pending())
         return GetResult(data, lk.off[:n], lk.size[:n], self._take_pending())
 
-    def _end_step(self, side, k: int, batch, early: bool) -> None:
-        """After a step's SET chain is queued: its end event (the next step's lookup and the
-        step after next's hand wait for it), the batch kept alive until the chain is joined
-        (the next serve's lookup or sync_sets)."""
+    def _end_event(self, k: int):
+        """The end event of step parity ``k % 2`` (created on first use)."""
         e = self._ends[k % 2]
         if e is None:
             e = self._ends[k % 2] = (torch.cuda.Event() if self.event_fence == "system"
-                                     else StreamEvent(self.event_fence))
-        e.record(side)
+                                     else StreamEvent(self._fence_of("end")))
+        return e
+
+    def _fence_of(self, name: str) -> str:
+        """Fence scope of a StreamEvent: the stop events' own for those a kernel completes."""
+        return (self.stop_fence if self.stop_events and name in ("end", "probe")
+                else self.event_fence)
+
+    def _end_step(self, side, k: int, batch, early: bool, recorded: bool = False) -> None:
+        """After a step's SET chain is queued: its end event (the next step's lookup and the
+        step after next's hand wait for it; ``recorded``: the chain's last kernel already
+        completes it), the batch kept alive until the chain is joined (the next serve's
+        lookup or sync_sets)."""
+        e = self._end_event(k)
+        if not recorded:
+            e.record(side)
         self._last_end = e
         self._side_pending = True
         held = self._held_steps
@@ -602,16 +634,20 @@ class ShardedCache:
             held.pop(0)
         self._planned = early
 
-    def _lookup_step(self, keys, now, bound, side):
+    def _lookup_step(self, keys, now, bound, side, index_done=None):
         """The step's GET lookup (coalesced unless ``coalesce`` is off): (lookup, first,
-        cslot, table)."""
+        cslot, table). ``index_done`` (a StreamEvent): completed by the lookup's probe
+        kernel when the coalescing lookup runs (``_probe_stopped`` says whether it did)."""
         sh = self.shard
+        self._probe_stopped = False
         if self.coalesce:
             table = self._coalesce_table(keys.shape[0]) if side is not None else None
             # with the table (the step's path, whose gather carries the expand tail): block-
             # local offsets, no n-row offsets scan between the lookup and the gather
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
-                                                   table=table, blocked=table is not None)
+                                                   table=table, blocked=table is not None,
+                                                   index_done=index_done)
+            self._probe_stopped = index_done is not None and sh.is_gpu and keys.shape[0] > 0
             return lk, first, cslot, table
         return sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None, None
 
@@ -635,7 +671,7 @@ class ShardedCache:
         e = self._events.get(name)
         if e is None:
             e = self._events[name] = (torch.cuda.Event() if self.event_fence == "system"
-                                      else StreamEvent(self.event_fence))
+                                      else StreamEvent(self._fence_of(name)))
         return e
 
     def _xwait(self, waiter, signaler, name: str) -> None:

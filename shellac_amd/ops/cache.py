@@ -216,6 +216,17 @@ def _event_handle(ev) -> int:
     return ev.cuda_event
 
 
+
+def _stop_handle(ev) -> int:
+    """hipEvent_t a launch completes as its stop event: a ``StreamEvent`` only (a
+    ``torch.cuda.Event`` has no handle before its first record)."""
+    if ev is None:
+        return 0
+    if not isinstance(ev, StreamEvent):
+        raise TypeError("a stop event must be a StreamEvent")
+    return ev.handle
+
+
 @dataclass
 class Lookup:
     loc: torch.Tensor   # int64 [n]  physical log offset (MISS_LOC as -1 on miss)
@@ -360,7 +371,8 @@ class CacheShard:
 
     def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
                          reserve_bytes: int = 0, total_slot: int = -1,
-                         table: Optional[torch.Tensor] = None, blocked: bool = False):
+                         table: Optional[torch.Tensor] = None, blocked: bool = False,
+                         index_done=None):
         """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
         row that claims a digest probes the index for it). Returns (Lookup, first,
         cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
@@ -370,6 +382,8 @@ class CacheShard:
         a temporary table is zeroed here and ``cslot`` is None. ``blocked`` (GPU): the
         Lookup holds block-local offsets (``Lookup.prefix``), which only ``gather`` with an
         ``expand`` tail reads — no n-row offsets scan between the lookup and the gather.
+        ``index_done`` (GPU, a ``StreamEvent``): completes with the kernel that reads the
+        index, as that kernel's own completion signal (a SET's ``index_after``).
         CPU shards: a plain lookup, ``first = cslot = None``."""
         if not self.is_gpu or keys.shape[0] == 0:
             return self.lookup(keys, now, reserve_bytes, total_slot), None, None
@@ -398,7 +412,8 @@ class CacheShard:
                                             int(total_slot),
                                             cslot.data_ptr() if cslot is not None else 0,
                                             cslot is not None,
-                                            prefix.data_ptr() if prefix is not None else 0)
+                                            prefix.data_ptr() if prefix is not None else 0,
+                                            _stop_handle(index_done))
         return Lookup(loc, size, off, prefix, max(int(shift), 0)), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
@@ -500,7 +515,7 @@ class CacheShard:
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
               index_after=None, append_after=None, append_done=None, phase: int = 0,
-              plan_done=None) -> None:
+              plan_done=None, done=None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
@@ -515,7 +530,8 @@ class CacheShard:
         done (``plan_done`` of that batch's phase 2), beside that batch's append and index
         insert — its reinsertions are indexed as moves, dropped when the key's entry has
         moved on (``HbmCache::store``). ``plan_done`` (GPU, an event): recorded after the
-        batch's planning kernels."""
+        batch's planning kernels. ``done`` (GPU, a ``StreamEvent``): completes with everything
+        the call queued, carried by the chain's last kernel as its completion signal."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -533,7 +549,7 @@ class CacheShard:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(), _event_handle(index_after),
                              _event_handle(append_after), _event_handle(append_done), phase,
-                             _event_handle(plan_done))
+                             _event_handle(plan_done), _stop_handle(done))
         elif phase != 1:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now, bound)
