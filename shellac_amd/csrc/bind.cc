@@ -317,6 +317,9 @@ PYBIND11_MODULE(_shellac_core, m) {
              "hipEventElapsedTime failed");
     return ms;
   });
+  m.def("event_query", [](uintptr_t e) {  // true: the work the event marks is complete
+    return hipEventQuery(reinterpret_cast<hipEvent_t>(e)) == hipSuccess;
+  });
   m.def("event_record", [](uintptr_t e, uintptr_t s) {
     SH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(s)) == hipSuccess,
              "hipEventRecord failed");

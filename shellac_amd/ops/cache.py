@@ -194,6 +194,10 @@ class StreamEvent:
         """``stream`` waits for the work this event recorded."""
         core().stream_wait_event(stream.cuda_stream, self.handle)
 
+    def query(self) -> bool:
+        """Whether the work this event marks (or the kernel that completes it) is done."""
+        return bool(core().event_query(self.handle))
+
     def elapsed_time(self, end: "StreamEvent") -> float:
         """Milliseconds from this event to ``end`` (both created with timing=True);
         waits for ``end``."""

@@ -1308,3 +1308,41 @@ def test_reserve_presizes_the_clock_combined_batch(cuda_dev):
     torch.cuda.synchronize()
     assert s.head() > 3 * (4 << 20) and s.counters()["reinserted"] > 0
     assert s._impl.retired_ever == ever
+
+
+@pytest.mark.parametrize("n", [100, 3000])
+def test_stop_events_order_a_second_stream(cuda_dev, n):
+    """``store(done=)`` and ``lookup_coalesced(index_done=)`` complete the caller's event as
+    their last / probing kernel's own completion signal (hipExtLaunchKernel stop event;
+    the small-batch path records it instead): the event is pending while the call's kernels
+    wait behind other work on their stream, and a second stream ordered by it sees the
+    SETs (n = 100: the one-launch small path; n = 3000: the full chain, fix-up last)."""
+    from shellac_amd.ops.cache import StreamEvent
+
+    shard = CacheShard(32 << 20, 1 << 14, 1 << 14, cuda_dev)
+    keys = [f"/stop/{n}/{i}".encode() for i in range(n)]
+    vals = [bytes([i % 251 + 1]) * (40 + (i * 37) % 900) for i in range(n)]
+    d, v, vo, vl = (t.to(cuda_dev) for t in _batch(keys, vals, "cpu"))
+    main = torch.cuda.current_stream(cuda_dev)
+    side = torch.cuda.Stream(device=cuda_dev)
+    side.wait_stream(main)
+    done = StreamEvent("none")
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)   # the store's kernels queue behind ~10 ms of work
+        shard.store(d, v, vo, vl, done=done)
+    assert not done.query()
+    done.wait(main)                     # main: the lookup follows the whole SET chain
+    out, off, size = shard.get(d)
+    got = unpack_records(out, off, size)
+    assert [g[0] if g else None for g in got] == vals
+    assert done.query()
+    # the coalescing lookup's probe completes index_done
+    probed = StreamEvent("none")
+    dup = torch.cat([d, d[: n // 2]])
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)
+        lk, first, _ = shard.lookup_coalesced(dup, index_done=probed)
+    assert not probed.query()
+    side.synchronize()
+    assert probed.query()
+    assert int((lk.size[: dup.shape[0]] > 0).sum()) == n   # one claimer per distinct key
