@@ -262,6 +262,7 @@ class ShardedCache:
         self.stop_events = os.environ.get("SHELLAC_STOP_EVENTS", "1") != "0"
         # fence scope of the events kernels complete as stop events (A/B: SHELLAC_STOP_FENCE)
         self.stop_fence = os.environ.get("SHELLAC_STOP_FENCE", "none")
+        self._probe_stopped = False   # the last step lookup completed its `probe` itself
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
         # one GPU, a full cache: where the SET batch's CLOCK hand runs (see serve).
