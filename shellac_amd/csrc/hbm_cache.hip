@@ -3774,7 +3774,10 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                      hipEvent_t append_done, int phase, hipEvent_t plan_done,
                      hipEvent_t done) {
   TraceRange tr("hbm.store");
-  if (n <= 0) return;
+  if (n <= 0) {
+    if (done) HIP_OK(hipEventRecord(done, s));  // nothing queued to carry it
+    return;
+  }
   SH_CHECK(bytes_bound <= cfg_.log_bytes / 2,
            "SET batch larger than half the log; split the batch");
   std::lock_guard<std::mutex> lk(mu_);

@@ -542,6 +542,8 @@ class CacheShard:
             raise TypeError("vlen must be int32 and val_off int64")
         n = keys.shape[0]
         if n == 0:
+            if done is not None and self.is_gpu:
+                done.record(torch.cuda.current_stream(self.device))   # nothing to carry it
             return
         now = self.now() if now is None else now
         fp = 0 if flags is None else flags.data_ptr()

@@ -1346,3 +1346,11 @@ def test_stop_events_order_a_second_stream(cuda_dev, n):
     side.synchronize()
     assert probed.query()
     assert int((lk.size[: dup.shape[0]] > 0).sum()) == n   # one claimer per distinct key
+    # an empty batch queues no kernel: its done event is recorded on the stream instead
+    empty = StreamEvent("none")
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)
+        shard.store(d[:0], v, vo[:0], vl[:0], done=empty)
+    assert not empty.query()
+    side.synchronize()
+    assert empty.query()
