@@ -1073,9 +1073,20 @@ const StepStreams& step_streams(int device) {
     RT_OK(hipMemsetAsync(scratch, 0, 64, nullptr));
     RT_OK(hipStreamSynchronize(nullptr));
     RT_OK(hipFree(scratch));
-    RT_OK(hipStreamCreateWithFlags(&p.plan, hipStreamNonBlocking));
-    RT_OK(hipStreamCreateWithFlags(&p.set, hipStreamNonBlocking));
-    RT_OK(hipStreamCreateWithFlags(&p.asm_, hipStreamNonBlocking));
+    // SHELLAC_STREAM_PRIO="plan,set,asm" (A/B): per-stream priorities, clamped to the
+    // device's range (on this image least 1, greatest -1); default: all normal
+    int prio[3] = {0, 0, 0};
+    if (const char* e = getenv("SHELLAC_STREAM_PRIO")) {
+      int lo = 0, hi = 0;
+      RT_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      (void)sscanf(e, "%d,%d,%d", &prio[0], &prio[1], &prio[2]);
+      for (int& x : prio) x = std::max(hi, std::min(lo, x));
+      fprintf(stderr, "[shellac] step stream priorities plan %d set %d asm %d (least %d greatest %d)\n",
+              prio[0], prio[1], prio[2], lo, hi);
+    }
+    RT_OK(hipStreamCreateWithPriority(&p.plan, hipStreamNonBlocking, prio[0]));
+    RT_OK(hipStreamCreateWithPriority(&p.set, hipStreamNonBlocking, prio[1]));
+    RT_OK(hipStreamCreateWithPriority(&p.asm_, hipStreamNonBlocking, prio[2]));
     // measured: with the plan stream sharing the assembly's queue the simulated 8-rank step
     // took 0.93 ms (the plan waited behind the mirrored reply copy), sharing the main
     // stream's 0.50 ms at one rank (behind the reply gather)
