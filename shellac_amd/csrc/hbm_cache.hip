@@ -1031,7 +1031,13 @@ __device__ __forceinline__ void expand_tail(const ExpandTail& ex) {
 // the range's first and last byte; their offsets are then staged in LDS kTileSegCap at
 // a time, and every lane walks its chunks (256 x 16 B apart) with a galloping search
 // over the staged offsets, issuing U independent 16-B loads before their stores.
-template <int MODE, int U, int WAVES, bool NTSTORE = false>
+// GLDS: the source loads land in LDS by LDS-DMA (`global_load_lds_dwordx4`, no VGPR
+// destination; a per-wave staging area of U KiB, lane-linear), then each lane reads back
+// its own 16 B for the store; the segment tables then stage 512 segments per pass so a
+// workgroup's LDS stays at ~24 KB (benchmarks/native/gather_glds_micro.hip: the gather's
+// pattern alone, 304 MiB: 133.5 us by LDS-DMA vs 151.6-157.6 us through VGPRs, but no gain
+// once 16 KB more LDS per workgroup lowers the co-resident count).
+template <int MODE, int U, int WAVES, bool NTSTORE = false, bool GLDS = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_segcopy(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint64_t* __restrict__ dst_off, int64_t n, uint8_t* __restrict__ dst,
@@ -1042,8 +1048,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   // the copy (a uniform early exit per workgroup skips to the expand tail)
   do {
   // mode 2 stages a length per segment too: fewer segments per pass keep 8 waves/SIMD
-  constexpr int TSC = MODE == 2 ? 768 : kTileSegCap;
+  constexpr int TSC = MODE == 2 ? 768 : GLDS ? 512 : kTileSegCap;
   __shared__ uint64_t s_off[TSC + 1];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[GLDS ? kBlock / 64 : 1][GLDS ? U : 1]
+                                                         [GLDS ? 1024 : 16];
   __shared__ uint64_t s_src[TSC];
   __shared__ int64_t s_lo[2], s_hi[2];
   __shared__ int s_cnt[kBlock / 64];
@@ -1144,9 +1152,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
           }
         }
       }
+      if constexpr (GLDS) {
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (sp[u]) v[u] = __builtin_nontemporal_load(sp[u]);
+        for (int u = 0; u < U; ++u)
+          if (sp[u])
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)sp[u],
+                (__attribute__((address_space(3))) void*)&s_stage[wv][u][0], 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs have landed in LDS
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (sp[u]) v[u] = *reinterpret_cast<const u32x4*>(&s_stage[wv][u][lane * 16]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (sp[u]) v[u] = __builtin_nontemporal_load(sp[u]);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t c = c0 + (u0 + u) * kBlock + threadIdx.x;
@@ -1192,11 +1214,30 @@ inline int seg_occ64(int mode) {
   return occ[mode];
 }
 
+// SHELLAC_GLDS=1 (A/B): the gather (modes 0 / 4) stages its loads by LDS-DMA, with the
+// workgroup count of the register version (its co-resident count x the mode's slot share)
+inline bool seg_glds() {
+  static const int on = [] {
+    const char* e = getenv("SHELLAC_GLDS");
+    return e && atoi(e) != 0 ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 template <int MODE, typename... Args>
 void launch_segcopy_ex(hipStream_t s, const ExpandTail& ex, Args... args) {
   static int grid[64];
   const auto kern = k_segcopy<MODE, 4, 8, true>;
   const int g = std::max(1, resident_grid(kern, grid) * seg_occ64(MODE) / 64);
+  if constexpr (MODE == 0 || MODE == 4) {
+    if (seg_glds()) {
+      static int ggrid[64];
+      const auto gk = k_segcopy<MODE, 4, 8, true, true>;
+      hipLaunchKernelGGL(gk, dim3(std::min(g, resident_grid(gk, ggrid))), dim3(kBlock), 0, s,
+                         args..., kSegMinTile, ex);
+      return;
+    }
+  }
   hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, args..., kSegMinTile, ex);
 }
 template <int MODE, typename... Args>
