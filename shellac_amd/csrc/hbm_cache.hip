@@ -1185,72 +1185,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   if (ex.n) expand_tail(ex);
 }
 
-// Row-wise gather (A/B: SHELLAC_GATHER_ROWS=1 registers, =2 LDS-DMA): the step's gather
-// with block-local offsets (mode 4's inputs) as one wave per record, the shape
-// benchmarks/native/gather_glds_micro.hip measured 12-15 % faster with LDS-DMA staging at
-// ~16 KB of LDS per workgroup (no segment tables: a wave reads the sizes, locations and
-// offsets of 64 rows at once, one lane each, and copies their non-empty records one after
-// the other, U 16-B loads per lane in flight).
-template <bool GLDS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_gather_rows(
-    const uint8_t* __restrict__ log, const uint64_t* __restrict__ loc,
-    const uint64_t* __restrict__ local, int64_t n, uint8_t* __restrict__ dst, uint64_t cap,
-    ExpandTail ex) {
-  constexpr int U = 4;
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[GLDS ? kBlock / 64 : 1][GLDS ? U : 1]
-                                                         [GLDS ? 1024 : 16];
-  const BlockedOff doff{local, ex.prefix, n, ex.shift};
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (doff[n] <= cap) {
-    const int64_t nchunk = (n + 63) >> 6;
-    for (int64_t ch = (int64_t)blockIdx.x * (kBlock / 64) + wv; ch < nchunk;
-         ch += (int64_t)gridDim.x * (kBlock / 64)) {
-      const int64_t j = (ch << 6) + lane;
-      const uint64_t sz = j < n ? ex.size[j] : 0;
-      const uint64_t so = sz ? loc[j] : 0, dof = sz ? doff[j] : 0;
-      unsigned long long m = __ballot(sz != 0);
-      while (m) {
-        const int r = __ffsll(m) - 1;
-        m &= m - 1;
-        const uint64_t s = uniform64((int64_t)__shfl(so, r));
-        const uint64_t d = uniform64((int64_t)__shfl(dof, r));
-        const uint64_t len = uniform64((int64_t)__shfl(sz, r)) >> 4;
-        for (uint64_t c0 = 0; c0 < len; c0 += 64 * U) {
-          u32x4 v[U];
-          if constexpr (GLDS) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const uint64_t c = c0 + u * 64 + lane;
-              if (c < len)
-                __builtin_amdgcn_global_load_lds(
-                    (__attribute__((address_space(1))) void*)(log + s + c * 16),
-                    (__attribute__((address_space(3))) void*)&s_stage[wv][u][0], 16, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-              if (c0 + u * 64 + lane < len)
-                v[u] = *reinterpret_cast<const u32x4*>(&s_stage[wv][u][lane * 16]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const uint64_t c = c0 + u * 64 + lane;
-              if (c < len)
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(log + s) + c);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint64_t c = c0 + u * 64 + lane;
-            if (c < len) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + d) + c);
-          }
-        }
-      }
-    }
-  }
-  if (ex.n) expand_tail(ex);
-}
-
 // Co-resident workgroups of a kernel on the current device (occupancy x CUs), cached.
 template <typename K>
 int resident_grid(K kernel, int* cache) {
@@ -3865,20 +3799,7 @@ void HbmCache::gather(const uint64_t* loc, const uint64_t* off, int64_t n, uint8
   if (first) ex = ExpandTail{first, n, size, off, out_size, out_off, table, cslot};
   ex.prefix = prefix;
   ex.shift = shift;
-  static const int rows = [] {
-    const char* e = getenv("SHELLAC_GATHER_ROWS");
-    return e ? atoi(e) : 0;
-  }();
-  if (prefix && size && rows) {  // A/B: the row-wise gather (k_gather_rows)
-    static int grid[64], ggrid[64];
-    const int g = std::max(1, resident_grid(k_segcopy<4, 4, 8, true>, grid) * seg_occ64(4) / 64);
-    if (rows == 2)
-      hipLaunchKernelGGL(k_gather_rows<true>, dim3(std::min(g, resident_grid(k_gather_rows<true>, ggrid))),
-                         dim3(kBlock), 0, s, log_, loc, off, n, out, out_cap, ex);
-    else
-      hipLaunchKernelGGL(k_gather_rows<false>, dim3(g), dim3(kBlock), 0, s, log_, loc, off, n, out,
-                         out_cap, ex);
-  } else if (prefix)  // block-local offsets (lookup_coalesced with a prefix)
+  if (prefix)  // block-local offsets (lookup_coalesced with a prefix)
     launch_segcopy_ex<4>(s, ex, log_, loc, off, n, out, nullptr, nullptr, nullptr, nullptr,
                          nullptr, out_cap);
   else
