@@ -105,18 +105,17 @@ PYBIND11_MODULE(_shellac_core, m) {
                                   int64_t slots, uintptr_t first, uintptr_t loc, uintptr_t size,
                                   uintptr_t off, uint32_t now, uintptr_t s, uint64_t reserve,
                                   int slot, uintptr_t cslot, bool table_clean, uintptr_t prefix,
-                                  uintptr_t index_done, uint64_t probe_seq) {
+                                  uintptr_t index_done) {
         py::gil_scoped_release nogil;
         return c.lookup_coalesced(P<const Digest>(keys), n, P<uint32_t>(table), slots,
                                   P<uint32_t>(first), P<uint64_t>(loc), P<uint64_t>(size),
                                   P<uint64_t>(off), now, S(s), reserve, slot, P<uint32_t>(cslot),
                                   table_clean, P<uint64_t>(prefix),
-                                  reinterpret_cast<hipEvent_t>(index_done), probe_seq);
+                                  reinterpret_cast<hipEvent_t>(index_done));
       }, py::arg("keys"), py::arg("n"), py::arg("table"), py::arg("slots"), py::arg("first"),
          py::arg("loc"), py::arg("size"), py::arg("off"), py::arg("now"), py::arg("stream"),
          py::arg("reserve") = 0, py::arg("total_slot") = -1, py::arg("cslot") = 0,
-         py::arg("table_clean") = false, py::arg("prefix") = 0, py::arg("index_done") = 0,
-         py::arg("probe_seq") = 0)
+         py::arg("table_clean") = false, py::arg("prefix") = 0, py::arg("index_done") = 0)
       .def("small_get", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t out,
                            uint64_t out_cap, uintptr_t off, uint32_t now, uintptr_t s,
                            int done_slot) {
@@ -185,20 +184,19 @@ PYBIND11_MODULE(_shellac_core, m) {
                        uintptr_t vlen, uintptr_t flags, uintptr_t expire, int64_t n,
                        uint64_t bytes_bound, uint32_t now, uintptr_t s, uintptr_t index_after,
                        uintptr_t append_after, uintptr_t append_done, int phase,
-                       uintptr_t plan_done, uintptr_t done, uint64_t index_after_seq) {
+                       uintptr_t plan_done, uintptr_t done) {
         py::gil_scoped_release nogil;
         c.store(P<const Digest>(keys), P<const uint8_t>(values), P<const uint64_t>(val_off),
                 P<const uint32_t>(vlen), P<const uint32_t>(flags), P<const uint32_t>(expire), n,
                 bytes_bound, now, S(s), reinterpret_cast<hipEvent_t>(index_after), true,
                 reinterpret_cast<hipEvent_t>(append_after),
                 reinterpret_cast<hipEvent_t>(append_done), phase,
-                reinterpret_cast<hipEvent_t>(plan_done), reinterpret_cast<hipEvent_t>(done),
-                index_after_seq);
+                reinterpret_cast<hipEvent_t>(plan_done), reinterpret_cast<hipEvent_t>(done));
       }, py::arg("keys"), py::arg("values"), py::arg("val_off"), py::arg("vlen"),
          py::arg("flags"), py::arg("expire"), py::arg("n"), py::arg("bytes_bound"), py::arg("now"),
          py::arg("stream"), py::arg("index_after") = 0, py::arg("append_after") = 0,
          py::arg("append_done") = 0, py::arg("phase") = 0, py::arg("plan_done") = 0,
-         py::arg("done") = 0, py::arg("index_after_seq") = 0)
+         py::arg("done") = 0)
       .def("remove", [](HbmCache& c, uintptr_t keys, int64_t n, uintptr_t found, uint32_t now,
                         uintptr_t s) {
         py::gil_scoped_release nogil;

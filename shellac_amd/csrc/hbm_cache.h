@@ -72,9 +72,6 @@ class HbmCache {
   // workgroup totals (one small scan instead of the n-row one); returns the row shift of a
   // workgroup (its rows are [b << shift, (b + 1) << shift)), for gather(prefix, shift).
   // Without `prefix`: `off` is the exclusive scan of `size`; returns -1.
-  // `probe_seq` (> 0): the coalescing kernel's last workgroup also writes it into the cache's
-  // probe word (after every workgroup's index writes are released), for a store's
-  // `index_after_seq` — a wait on the SET stream, no packet on `s` (SHELLAC_WAIT_WORDS).
   // `index_done`: completes with the kernel that reads (and reference-marks) the index, as
   // that kernel's own completion signal (no marker packet between it and the next kernel
   // of `s`): a SET's index insert on another stream may wait for it.
@@ -82,8 +79,7 @@ class HbmCache {
                        uint32_t* first, uint64_t* loc, uint64_t* size, uint64_t* off,
                        uint32_t now, hipStream_t s, uint64_t reserve = 0, int total_slot = -1,
                        uint32_t* cslot = nullptr, bool table_clean = false,
-                       uint64_t* prefix = nullptr, hipEvent_t index_done = nullptr,
-                       uint64_t probe_seq = 0);
+                       uint64_t* prefix = nullptr, hipEvent_t index_done = nullptr);
   // Slotted lookup (the routed step's owner side): nslots x slot_rows rows, slot k's
   // rows [k * slot_rows, k * slot_rows + slot_cnt[k]) are requests, the rest padding
   // (size 0, not probed, not counted). off = exclusive scan over all rows.
@@ -200,8 +196,6 @@ class HbmCache {
   // can never resurrect a superseded or deleted value. Two hand buffers alternate, so the
   // hand of batch k+1 never writes what batch k's append still reads.
   // `plan_done`: recorded after the batch's planning kernels (dedupe, sizes, offsets).
-  // `index_after_seq` (> 0): the index insert also waits (hipStreamWaitValue64) for the probe
-  // word to reach it (lookup_coalesced(probe_seq)).
   // `done`: completes with everything this call queued; carried by the chain's last kernel
   // as its completion signal (profiles/r6_hop: ~2.4 us sooner across queues than a
   // recorded event), or recorded when the call queued no chain.
@@ -210,7 +204,7 @@ class HbmCache {
              uint64_t bytes_bound, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,
              bool allow_reclaim = true, hipEvent_t append_after = nullptr,
              hipEvent_t append_done = nullptr, int phase = 0, hipEvent_t plan_done = nullptr,
-             hipEvent_t done = nullptr, uint64_t index_after_seq = 0);
+             hipEvent_t done = nullptr);
   // Whether a SET of `bytes_bound` bytes issued now would run the CLOCK hand (the log is
   // within a few batches of wrapping); the answer can only turn true later.
   bool would_reclaim(uint64_t bytes_bound) const {
@@ -422,9 +416,6 @@ class HbmCache {
   // store(done): the event the call's last kernel carries as its completion signal (taken
   // by that launch; recorded by a marker if the path queued no such kernel)
   hipEvent_t stop_ev_ = nullptr;
-  uint64_t idx_wait_seq_ = 0;        // store(index_after_seq): taken by the index insert
-  uint64_t* probe_word_ = nullptr;   // signal memory: the last lookup_coalesced(probe_seq)
-  unsigned* probe_ctr_ = nullptr;    // its workgroups' arrival count (reset by the last)
   void store_locked(const Digest* keys, const uint8_t* values, const uint64_t* val_off,
                     const uint32_t* vlen, const uint32_t* flags, const uint32_t* expire,
                     int64_t n, uint32_t now, hipStream_t s, hipEvent_t index_after = nullptr,

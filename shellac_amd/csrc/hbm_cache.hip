@@ -556,8 +556,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     Entry* __restrict__ index, uint64_t mask, const uint64_t* __restrict__ head_ptr,
     uint64_t reserve, uint64_t cap, uint32_t now, uint64_t* __restrict__ out_loc,
     uint64_t* __restrict__ out_size, CacheCounters* __restrict__ ctr,
-    uint64_t* __restrict__ part, int local_only, uint64_t* __restrict__ woff,
-    unsigned* __restrict__ done_ctr, uint64_t* __restrict__ done_word, uint64_t done_val) {
+    uint64_t* __restrict__ part, int local_only, uint64_t* __restrict__ woff) {
   __shared__ Digest s_k[kCoKeys];       // the chunk's digests (LDS compares, probe input)
   // woff (PROBE, optional): each row's exclusive offset within this workgroup's rows (the
   // gather adds the prefix of the workgroup totals, k_block_prefix): the chunk's sizes are
@@ -777,21 +776,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 &CacheCounters::get_bytes);
     block_count(ctr, dups, &CacheCounters::get_coalesced);
     block_partial(psum, part);  // k_offsets scans the partials
-    if (done_word) {
-      // the probe word: the last workgroup to arrive publishes done_val. The SET index
-      // insert waiting for it needs only this kernel's index reads done and its reference
-      // marks performed: the marks are device-scope atomics (performed where every XCD sees
-      // them), and the barrier waits for every wave's outstanding memory operations, so no
-      // per-workgroup cache write-back (a __threadfence here made the step 13 % slower)
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        if (atomicAdd(done_ctr, 1u) == gridDim.x - 1) {
-          __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __threadfence_system();
-          __hip_atomic_store(done_word, done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-    }
   }
 }
 
@@ -3157,7 +3141,7 @@ void coalesce_keys(const Digest* keys, int64_t n, uint32_t* table, int64_t table
   hipLaunchKernelGGL(k_coalesce<false>, dim3((unsigned)chunks), dim3(kBlock), 0, s, keys, n,
                      (int64_t)kCoKeys, table, (uint32_t)(table_slots - 1), first, cslot,
                      nullptr, 0ull, nullptr, 0ull, 0ull, 0u, nullptr, nullptr, nullptr, nullptr,
-                     0, nullptr, nullptr, nullptr, 0ull);
+                     0, nullptr);
   HIP_OK(hipGetLastError());
 }
 
@@ -3245,11 +3229,6 @@ HbmCache::HbmCache(const ShardConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMalloc(&scratch_, 64));
   HIP_OK(hipMalloc(&done_ctr_, 64));
   HIP_OK(hipMemset(done_ctr_, 0, 64));
-  HIP_OK(hipMalloc(&probe_ctr_, 64));
-  HIP_OK(hipMemset(probe_ctr_, 0, 64));
-  HIP_OK(hipExtMallocWithFlags(reinterpret_cast<void**>(&probe_word_), sizeof(uint64_t),
-                               hipMallocSignalMemory));
-  HIP_OK(hipMemset(probe_word_, 0, sizeof(uint64_t)));
   const size_t lb_words = (size_t)(kSmallGetMax / kEdgeKeys + 1);
   HIP_OK(hipMalloc(&lb_state_, lb_words * sizeof(unsigned long long)));
   HIP_OK(hipMemset(lb_state_, 0, lb_words * sizeof(unsigned long long)));
@@ -3318,8 +3297,6 @@ HbmCache::~HbmCache() {
   (void)hipFree(part_);
   (void)hipHostFree(host_buf_);
   (void)hipHostFree(host_slots_);
-  (void)hipFree(probe_ctr_);
-  (void)hipFree(probe_word_);
   for (SetWs& w : ws_)
     for (void* p : {(void*)w.dd_keys, (void*)w.dd_win, (void*)w.dd_slot, (void*)w.set_size,
                     (void*)w.set_off, (void*)w.set_claim, (void*)w.set_cnt})
@@ -3598,8 +3575,7 @@ int HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
                                int64_t table_slots, uint32_t* first, uint64_t* loc,
                                uint64_t* size, uint64_t* off, uint32_t now, hipStream_t s,
                                uint64_t reserve, int total_slot, uint32_t* cslot,
-                               bool table_clean, uint64_t* prefix, hipEvent_t index_done,
-                               uint64_t probe_seq) {
+                               bool table_clean, uint64_t* prefix, hipEvent_t index_done) {
   TraceRange tr("hbm.lookup_coalesced");
   SH_CHECK(total_slot < kHostSlots, "host slot out of range");
   SH_CHECK(n < (1ll << 31), "coalesce: batch too large");
@@ -3614,7 +3590,6 @@ int HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
     if (prefix) HIP_OK(hipMemsetAsync(prefix, 0, sizeof(uint64_t), s));
     if (ht) *ht = 0;
     if (index_done) HIP_OK(hipEventRecord(index_done, s));
-    if (probe_seq) HIP_OK(hipStreamWriteValue64(s, probe_word_, probe_seq, 0));
     return prefix ? 31 : -1;
   }
   if (!table_clean) HIP_OK(hipMemsetAsync(table, 0, (size_t)table_slots * sizeof(uint32_t), s));
@@ -3634,8 +3609,7 @@ int HbmCache::lookup_coalesced(const Digest* keys, int64_t n, uint32_t* table,
   // 0.32 ms per step; see docs/PERF.md)
   launch_stop(&index_done, k_coalesce<true>, dim3(grid), dim3(kBlock), s, keys, n, plen, table,
               (uint32_t)(table_slots - 1), first, cslot, index_, cfg_.nbuckets - 1, cur_head(),
-              reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, 0, prefix ? off : nullptr,
-              probe_seq ? probe_ctr_ : nullptr, probe_seq ? probe_word_ : nullptr, probe_seq);
+              reserve, cfg_.log_bytes, now, loc, size, ctr_, part_, 0, prefix ? off : nullptr);
   HIP_OK(hipGetLastError());
   if (!prefix) {
     launch_offsets(size, n, part_, grid, off, s, ht, plen);
@@ -3839,7 +3813,7 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
                      int64_t n, uint64_t bytes_bound, uint32_t now, hipStream_t s,
                      hipEvent_t index_after, bool allow_reclaim, hipEvent_t append_after,
                      hipEvent_t append_done, int phase, hipEvent_t plan_done,
-                     hipEvent_t done, uint64_t index_after_seq) {
+                     hipEvent_t done) {
   TraceRange tr("hbm.store");
   if (n <= 0) {
     if (done) HIP_OK(hipEventRecord(done, s));  // nothing queued to carry it
@@ -3851,7 +3825,6 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
   DeviceGuard g(cfg_.device);
   note_stream(s);
   stop_ev_ = done;  // the chain's last kernel (the index fix-up) takes it
-  idx_wait_seq_ = index_after_seq;  // the index insert's wait on the probe word
   struct EndMark {  // the stream's `last` event, after whatever this call queues
     HbmCache* c;
     hipStream_t s;
@@ -3860,7 +3833,6 @@ void HbmCache::store(const Digest* keys, const uint8_t* values, const uint64_t* 
         (void)hipEventRecord(c->stop_ev_, s);
         c->stop_ev_ = nullptr;
       }
-      c->idx_wait_seq_ = 0;
       c->note_store_end(s);
     }
   } end_mark{this, s};
@@ -4002,10 +3974,6 @@ void HbmCache::store_index_locked(const Digest* keys, const uint32_t* vlen,
                                   int win_parity) {
   // the index insert is the only SET kernel a concurrent lookup can observe
   if (index_after) HIP_OK(hipStreamWaitEvent(s, index_after, 0));
-  if (idx_wait_seq_) {
-    HIP_OK(hipStreamWaitValue64(s, probe_word_, idx_wait_seq_, hipStreamWaitValueGte, ~0ull));
-    idx_wait_seq_ = 0;
-  }
   // A combined batch's reinsertions (rows [0, nmove), moves) land in a launch of their own
   // before the batch's rows: a batch row may claim the slot of an item this batch's append
   // overwrites as dead, and must not take a reinserted item's entry from under its move

@@ -263,11 +263,6 @@ class ShardedCache:
         # fence scope of the events kernels complete as stop events (A/B: SHELLAC_STOP_FENCE)
         self.stop_fence = os.environ.get("SHELLAC_STOP_FENCE", "none")
         self._probe_stopped = False   # the last step lookup completed its `probe` itself
-        # SHELLAC_WAIT_WORDS=1 (A/B): the lookup's last workgroup writes a sequence number into
-        # the shard's probe word and the index insert waits for it on the SET stream
-        # (hipStreamWaitValue64): no event packet on the main stream between the lookup and
-        # the gather at all
-        self.wait_words = os.environ.get("SHELLAC_WAIT_WORDS", "0") != "0"
         # one GPU: the gather waits for the SET batch's log append (see serve)
         self.gather_after_append = False
         # one GPU, a full cache: where the SET batch's CLOCK hand runs (see serve).
@@ -566,14 +561,9 @@ class ShardedCache:
             start = self._event("start")
             start.record(main)               # ... and its gather: the append may overwrite
         ev = self._event("probe")
-        seq = 0
-        if stop and self.wait_words and self.coalesce and keys.shape[0] > 0:
-            # (counted on the shard: its probe word is the native cache's, whichever
-            # ShardedCache drives it)
-            seq = sh._probe_seq = getattr(sh, "_probe_seq", 0) + 1
         try:
             lk, first, cslot, table = self._lookup_step(keys, now, bound, side,
-                                                        ev if stop and not seq else None, seq)
+                                                        ev if stop else None)
         except BaseException:
             if early:
                 # the planned batch still runs its chain (the native store pairs phase 1
@@ -589,9 +579,7 @@ class ShardedCache:
         if first is not None:
             out_size = torch.empty(n, dtype=torch.int64, device=self.device)
             out_off = torch.empty(n, dtype=torch.int64, device=self.device)
-        if seq:
-            ev = None                        # the index insert waits for the probe word
-        elif not (stop and self._probe_stopped):
+        if not (stop and self._probe_stopped):
             ev.record(main)
         appended = self._event("appended") if self.gather_after_append else None
         with torch.cuda.stream(side):
@@ -603,7 +591,7 @@ class ShardedCache:
             end = self._end_event(k) if stop else None
             sh.store(batch.keys, batch.values, batch.val_off, batch.vlen, batch.flags,
                      batch.expire, now, index_after=ev, append_after=start, append_done=appended,
-                     phase=2 if early else 0, done=end, index_after_seq=seq)
+                     phase=2 if early else 0, done=end)
         self._end_step(side, k, batch, early, recorded=end is not None)
         if appended is not None:
             # the gather runs after the log append, not beside it: the two byte movers
@@ -647,7 +635,7 @@ class ShardedCache:
             held.pop(0)
         self._planned = early
 
-    def _lookup_step(self, keys, now, bound, side, index_done=None, probe_seq: int = 0):
+    def _lookup_step(self, keys, now, bound, side, index_done=None):
         """The step's GET lookup (coalesced unless ``coalesce`` is off): (lookup, first,
         cslot, table). ``index_done`` (a StreamEvent): completed by the lookup's probe
         kernel when the coalescing lookup runs (``_probe_stopped`` says whether it did)."""
@@ -659,7 +647,7 @@ class ShardedCache:
             # local offsets, no n-row offsets scan between the lookup and the gather
             lk, first, cslot = sh.lookup_coalesced(keys, now, reserve_bytes=bound, total_slot=0,
                                                    table=table, blocked=table is not None,
-                                                   index_done=index_done, probe_seq=probe_seq)
+                                                   index_done=index_done)
             self._probe_stopped = index_done is not None and sh.is_gpu and keys.shape[0] > 0
             return lk, first, cslot, table
         return sh.lookup(keys, now, reserve_bytes=bound, total_slot=0), None, None, None

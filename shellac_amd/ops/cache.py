@@ -376,7 +376,7 @@ class CacheShard:
     def lookup_coalesced(self, keys: torch.Tensor, now: Optional[int] = None,
                          reserve_bytes: int = 0, total_slot: int = -1,
                          table: Optional[torch.Tensor] = None, blocked: bool = False,
-                         index_done=None, probe_seq: int = 0):
+                         index_done=None):
         """``coalesce`` + ``lookup(first=...)`` fused into one kernel on GPU shards (the
         row that claims a digest probes the index for it). Returns (Lookup, first,
         cslot); duplicate rows have size 0 until ``expand(first, lk.size, lk.off)`` runs
@@ -388,9 +388,6 @@ class CacheShard:
         ``expand`` tail reads — no n-row offsets scan between the lookup and the gather.
         ``index_done`` (GPU, a ``StreamEvent``): completes with the kernel that reads the
         index, as that kernel's own completion signal (a SET's ``index_after``).
-        ``probe_seq`` (GPU, > 0): the coalescing kernel's last workgroup writes it into the
-        cache's probe word (a SET's ``index_after_seq``; only when this call reaches the
-        GPU: ``keys`` not empty).
         CPU shards: a plain lookup, ``first = cslot = None``."""
         if not self.is_gpu or keys.shape[0] == 0:
             return self.lookup(keys, now, reserve_bytes, total_slot), None, None
@@ -420,7 +417,7 @@ class CacheShard:
                                             cslot.data_ptr() if cslot is not None else 0,
                                             cslot is not None,
                                             prefix.data_ptr() if prefix is not None else 0,
-                                            _stop_handle(index_done), int(probe_seq))
+                                            _stop_handle(index_done))
         return Lookup(loc, size, off, prefix, max(int(shift), 0)), first, cslot
 
     def host_total(self, slot: int, timeout_ms: int = 10000) -> int:
@@ -522,7 +519,7 @@ class CacheShard:
               expire: Optional[torch.Tensor] = None, now: Optional[int] = None,
               bytes_bound: Optional[int] = None,
               index_after=None, append_after=None, append_done=None, phase: int = 0,
-              plan_done=None, done=None, index_after_seq: int = 0) -> None:
+              plan_done=None, done=None) -> None:
         """SET a batch (later duplicates win). ``bytes_bound`` bounds the log bytes the
         batch appends; the default assumes every byte of ``values`` is stored.
         ``index_after`` (GPU, a recorded ``torch.cuda.Event`` or a ``StreamEvent``):
@@ -538,9 +535,7 @@ class CacheShard:
         insert — its reinsertions are indexed as moves, dropped when the key's entry has
         moved on (``HbmCache::store``). ``plan_done`` (GPU, an event): recorded after the
         batch's planning kernels. ``done`` (GPU, a ``StreamEvent``): completes with everything
-        the call queued, carried by the chain's last kernel as its completion signal.
-        ``index_after_seq`` (GPU, > 0): the index insert also waits for the probe word to reach
-        it (``lookup_coalesced(probe_seq=)``)."""
+        the call queued, carried by the chain's last kernel as its completion signal."""
         for t, nm in ((keys, "keys"), (values, "values"), (val_off, "val_off"), (vlen, "vlen")):
             self._check(t, nm)
         if vlen.dtype != torch.int32 or val_off.dtype != torch.int64:
@@ -560,7 +555,7 @@ class CacheShard:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, bound, now, self._s(), _event_handle(index_after),
                              _event_handle(append_after), _event_handle(append_done), phase,
-                             _event_handle(plan_done), _stop_handle(done), int(index_after_seq))
+                             _event_handle(plan_done), _stop_handle(done))
         elif phase != 1:
             self._impl.store(keys.data_ptr(), values.data_ptr(), val_off.data_ptr(), vlen.data_ptr(),
                              fp, ep, n, now, bound)
