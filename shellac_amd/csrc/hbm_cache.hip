@@ -1037,9 +1037,7 @@ __device__ __forceinline__ void expand_tail(const ExpandTail& ex) {
 // workgroup's LDS stays at ~24 KB (benchmarks/native/gather_glds_micro.hip: the gather's
 // pattern alone, 304 MiB: 133.5 us by LDS-DMA vs 151.6-157.6 us through VGPRs, but no gain
 // once 16 KB more LDS per workgroup lowers the co-resident count).
-// SEGCAP (> 0): segments staged per pass instead of the default (a smaller LDS footprint
-// lets more workgroups sit beside the coalescing lookup's 4 x 33 KB per CU).
-template <int MODE, int U, int WAVES, bool NTSTORE = false, bool GLDS = false, int SEGCAP = 0>
+template <int MODE, int U, int WAVES, bool NTSTORE = false, bool GLDS = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_segcopy(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint64_t* __restrict__ dst_off, int64_t n, uint8_t* __restrict__ dst,
@@ -1050,7 +1048,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
   // the copy (a uniform early exit per workgroup skips to the expand tail)
   do {
   // mode 2 stages a length per segment too: fewer segments per pass keep 8 waves/SIMD
-  constexpr int TSC = SEGCAP > 0 ? SEGCAP : MODE == 2 ? 768 : GLDS ? 512 : kTileSegCap;
+  constexpr int TSC = MODE == 2 ? 768 : GLDS ? 512 : kTileSegCap;
   __shared__ uint64_t s_off[TSC + 1];
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[GLDS ? kBlock / 64 : 1][GLDS ? U : 1]
                                                          [GLDS ? 1024 : 16];
@@ -1231,20 +1229,6 @@ void launch_segcopy_ex(hipStream_t s, const ExpandTail& ex, Args... args) {
   static int grid[64];
   const auto kern = k_segcopy<MODE, 4, 8, true>;
   const int g = std::max(1, resident_grid(kern, grid) * seg_occ64(MODE) / 64);
-  if constexpr (MODE == 1) {
-    // SHELLAC_APPEND_SEGCAP=256 (A/B): the SET append with 4 KB of segment tables
-    static const int cap = [] {
-      const char* e = getenv("SHELLAC_APPEND_SEGCAP");
-      return e ? atoi(e) : 0;
-    }();
-    if (cap == 256) {
-      static int agrid[64];
-      const auto ak = k_segcopy<1, 4, 8, true, false, 256>;
-      const int ag = std::max(1, resident_grid(ak, agrid) * seg_occ64(MODE) / 64);
-      hipLaunchKernelGGL(ak, dim3(ag), dim3(kBlock), 0, s, args..., kSegMinTile, ex);
-      return;
-    }
-  }
   if constexpr (MODE == 0 || MODE == 4) {
     if (seg_glds()) {
       static int ggrid[64];
